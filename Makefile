@@ -1,0 +1,35 @@
+# Builds libdeltareplay.so (HIP for gfx950 + host C++) in-tree, and the CPU oracle baseline.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+CSRC := delta_amd/csrc
+LIB := delta_amd/libdeltareplay.so
+HIP_SRCS := $(CSRC)/engine.hip $(CSRC)/k_json.hip $(CSRC)/k_parquet.hip $(CSRC)/k_replay.hip $(CSRC)/k_util.hip
+CXX_SRCS := $(CSRC)/parquet_meta.cpp $(CSRC)/log_segment.cpp $(CSRC)/json_host.cpp $(CSRC)/snappy_host.cpp
+OBJDIR := build/obj
+HIP_OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS))
+CXX_OBJS := $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(CXX_SRCS))
+HDRS := $(wildcard $(CSRC)/*.h) include/deltareplay.h
+HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function -Wno-unused-variable
+CXXFLAGS := -O2 -std=c++17 -fPIC -Wall
+
+all: $(LIB) oracle
+
+$(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/%.o: $(CSRC)/%.cpp $(HDRS)
+	@mkdir -p $(OBJDIR)
+	g++ $(CXXFLAGS) -c $< -o $@
+
+$(LIB): $(HIP_OBJS) $(CXX_OBJS)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf build $(LIB)
+	$(MAKE) -C oracle clean
+
+.PHONY: all clean oracle

@@ -1,0 +1,1160 @@
+// libdeltareplay: host orchestration of the device replay and the C ABI (include/deltareplay.h).
+//
+// One dr_ctx owns a HIP stream and a caching device allocator. dr_stage copies a LogSegment's
+// bytes into HBM and plans the checkpoint page decode; dr_replay_staged runs K1 (JSON), K2
+// (Parquet), canonicalisation, K3 (hash partition) and K4 (per-bucket last-writer-wins) on the
+// device and keeps the reconstructed state resident until dr_state_release.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "common.h"
+#include "json_host.h"
+#include "kernels.h"
+#include "log_segment.h"
+#include "parquet_meta.h"
+
+using namespace dr;
+
+#define HIP_OK(x)                                                                                  \
+  do {                                                                                             \
+    hipError_t e_ = (x);                                                                           \
+    if (e_ != hipSuccess) fail(DR_E_DEVICE, fmt("%s failed: %s", #x, hipGetErrorString(e_)));      \
+  } while (0)
+
+// ---------------------------------------------------------------------------------------------------
+// context + caching allocator
+// ---------------------------------------------------------------------------------------------------
+struct dr_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  bool timing = false;
+  std::vector<std::pair<std::string, hipEvent_t>> marks;
+  std::vector<std::pair<std::string, float>> timings;
+  std::multimap<size_t, void*> free_blocks;
+  std::unordered_map<void*, size_t> sizes;
+  std::mutex mu;
+
+  void* alloc(size_t n) {
+    n = (n + 255) & ~size_t(255);
+    if (n == 0) n = 256;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      auto it = free_blocks.lower_bound(n);
+      if (it != free_blocks.end() && it->first <= 2 * n + (1 << 20)) {
+        void* p = it->second;
+        free_blocks.erase(it);
+        return p;
+      }
+    }
+    void* p = nullptr;
+    if (hipMalloc(&p, n) != hipSuccess) {
+      (void)hipGetLastError();
+      trim();
+      if (hipMalloc(&p, n) != hipSuccess) {
+        (void)hipGetLastError();
+        fail(DR_E_OOM, fmt("device allocation of %zu bytes failed", n));
+      }
+    }
+    std::lock_guard<std::mutex> g(mu);
+    sizes[p] = n;
+    return p;
+  }
+  void release(void* p) {
+    if (!p) return;
+    std::lock_guard<std::mutex> g(mu);
+    free_blocks.emplace(sizes[p], p);
+  }
+  void trim() {
+    std::lock_guard<std::mutex> g(mu);
+    for (auto& kv : free_blocks) {
+      (void)hipFree(kv.second);
+      sizes.erase(kv.second);
+    }
+    free_blocks.clear();
+  }
+  void mark(const char* name) {
+    if (!timing) return;
+    hipEvent_t e;
+    HIP_OK(hipEventCreate(&e));
+    HIP_OK(hipEventRecord(e, stream));
+    marks.emplace_back(name, e);
+  }
+  void collect_timings() {
+    timings.clear();
+    if (marks.empty()) return;
+    HIP_OK(hipEventSynchronize(marks.back().second));
+    for (size_t i = 1; i < marks.size(); ++i) {
+      float ms = 0;
+      HIP_OK(hipEventElapsedTime(&ms, marks[i - 1].second, marks[i].second));
+      timings.emplace_back(marks[i].first, ms);
+    }
+    for (auto& m : marks) (void)hipEventDestroy(m.second);
+    marks.clear();
+  }
+};
+
+// RAII device buffer from the context cache.
+template <typename T>
+struct DBuf {
+  dr_ctx* ctx = nullptr;
+  T* p = nullptr;
+  size_t n = 0;
+  DBuf() = default;
+  DBuf(dr_ctx* c, size_t count) : ctx(c), n(count) { p = static_cast<T*>(c->alloc(std::max<size_t>(count, 1) * sizeof(T))); }
+  DBuf(const DBuf&) = delete;
+  DBuf& operator=(const DBuf&) = delete;
+  DBuf(DBuf&& o) noexcept { *this = std::move(o); }
+  DBuf& operator=(DBuf&& o) noexcept {
+    reset();
+    ctx = o.ctx; p = o.p; n = o.n;
+    o.p = nullptr; o.n = 0;
+    return *this;
+  }
+  ~DBuf() { reset(); }
+  void reset() {
+    if (p && ctx) ctx->release(p);
+    p = nullptr;
+    n = 0;
+  }
+  void zero(hipStream_t s) { if (p) HIP_OK(hipMemsetAsync(p, 0, std::max<size_t>(n, 1) * sizeof(T), s)); }
+};
+
+template <typename T>
+static T d2h_one(const T* p, hipStream_t s) {
+  T v;
+  HIP_OK(hipMemcpyAsync(&v, p, sizeof(T), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return v;
+}
+
+template <typename T>
+static std::vector<T> d2h(const T* p, size_t n, hipStream_t s) {
+  std::vector<T> v(n);
+  if (n) {
+    HIP_OK(hipMemcpyAsync(v.data(), p, n * sizeof(T), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+  }
+  return v;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// staged segment
+// ---------------------------------------------------------------------------------------------------
+struct JsonFileRec { int64_t version; uint64_t off, len; };
+
+struct CkPart {
+  uint64_t off = 0, len = 0;   // within the concatenated checkpoint bytes
+  pq::FileMeta meta;
+  uint64_t row_base = 0;
+};
+
+struct NonFileAction {
+  int kind;                    // dev::K_METADATA / K_TXN / K_PROTOCOL
+  uint64_t order;              // action index (replay order)
+  std::string json;            // {"metaData":{...}} etc.
+  JVal val;                    // inner object
+};
+
+// Hot checkpoint columns decoded on the device.
+enum HotCol { HC_ADD_PATH = 0, HC_ADD_SIZE = 1, HC_RM_PATH = 2, HC_RM_DELTS = 3, HC_N = 4 };
+static const char* kHotPath[HC_N] = {"add.path", "add.size", "remove.path", "remove.deletionTimestamp"};
+
+struct StagedData {
+  dr_ctx* ctx = nullptr;
+  std::vector<uint8_t> h_json, h_pq;
+  DBuf<uint8_t> d_json, d_pq, d_arena;
+  std::vector<JsonFileRec> jfiles;
+  std::vector<CkPart> parts;
+  uint64_t ck_rows = 0;
+  int64_t ck_version = -1;
+  int64_t version = -1;
+  // page plan
+  std::vector<PageDesc> pages;
+  DBuf<PageDesc> d_pages;
+  uint32_t dict_entries = 0;
+  bool has_col[HC_N] = {false, false, false, false};
+  int max_def[HC_N] = {0, 0, 0, 0};
+  int add_def = 1, rm_def = 1;
+  std::vector<NonFileAction> ck_nonfile;  // protocol/metaData/txn rows of the checkpoint
+};
+
+struct dr_staged {
+  std::shared_ptr<StagedData> d;
+};
+
+struct ExportCols {
+  bool built = false;
+  int64_t n = 0;
+  std::vector<int64_t> path_off, size, mtime, delts, stats_off, pv_entry_off, pv_key_off, pv_val_off,
+      tags_entry_off, tags_key_off, tags_val_off;
+  std::vector<uint8_t> path_bytes, delts_valid, efm, stats_bytes, stats_null, pv_null, pv_key_bytes,
+      pv_val_bytes, pv_val_null, tags_null, tags_key_bytes, tags_val_bytes, tags_val_null;
+};
+
+struct dr_state {
+  dr_ctx* ctx = nullptr;
+  std::shared_ptr<StagedData> staged;
+  uint64_t n_actions = 0;
+  // resident action arrays
+  DBuf<uint8_t> kind, flags;
+  DBuf<uint64_t> key, path_ptr, src_off;
+  DBuf<uint32_t> path_len, src_len;
+  DBuf<int64_t> size, delts;
+  DBuf<uint8_t> canon_arena;
+  DBuf<uint32_t> live, tomb;   // survivor action indices (hash order per bucket)
+  uint64_t n_live = 0, n_tomb = 0;
+  dr_counts counts{};
+  std::string nonfile_json;
+  std::vector<NonFileAction> nonfile;  // winners: protocol, metadata, txns
+  ExportCols exp[2];
+};
+
+// ---------------------------------------------------------------------------------------------------
+// checkpoint planning (host)
+// ---------------------------------------------------------------------------------------------------
+static int leaf_def_of(const pq::Leaf& l, int depth) { return l.def_of[size_t(depth)]; }
+
+static std::string render_protocol(const std::vector<pq::Entry>& rd, const std::vector<pq::Entry>& wr, size_t i,
+                                   size_t j) {
+  JVal o;
+  o.t = JVal::OBJ;
+  JVal a; a.t = JVal::NUM; a.s = std::to_string(rd[i].ival);
+  JVal b; b.t = JVal::NUM; b.s = std::to_string(wr[j].ival);
+  o.o.emplace_back("minReaderVersion", a);
+  o.o.emplace_back("minWriterVersion", b);
+  return json_dump(o);
+}
+
+// Decodes protocol / metaData / txn rows of one checkpoint part on the host (run-wise, so the
+// all-null runs of a 10M-row checkpoint cost nothing). Rows are reported in row order.
+static void decode_ck_nonfile(StagedData& s, CkPart& part, uint64_t base_action) {
+  const uint8_t* file = s.h_pq.data() + part.off;
+  const pq::FileMeta& m = part.meta;
+  int64_t rg_base = 0;
+  for (const pq::RowGroup& rg : m.row_groups) {
+    auto col = [&](const std::string& path) -> const pq::ColumnChunk* {
+      for (auto& c : rg.cols) if (c.path == path) return &c;
+      return nullptr;
+    };
+    // Collect entries per column keyed by row.
+    struct Field { std::string name; std::vector<pq::Entry> e; const pq::Leaf* leaf; };
+    auto load = [&](const std::string& path, int thr_depth) -> std::vector<pq::Entry> {
+      const pq::Leaf* l = m.leaf(path);
+      const pq::ColumnChunk* c = col(path);
+      if (!l || !c) return {};
+      return pq::sparse_entries(file, part.len, *c, *l, leaf_def_of(*l, thr_depth),
+                                int64_t(part.row_base) + rg_base);
+    };
+    std::map<int64_t, NonFileAction> rows;  // row -> action
+    // protocol
+    {
+      auto rd = load("protocol.minReaderVersion", 0);
+      auto wr = load("protocol.minWriterVersion", 0);
+      for (size_t i = 0; i < rd.size(); ++i) {
+        NonFileAction a;
+        a.kind = 5;
+        a.order = base_action + uint64_t(rd[i].row);
+        JVal o; o.t = JVal::OBJ;
+        JVal x; x.t = JVal::NUM; x.s = std::to_string(rd[i].has_value ? rd[i].ival : 0);
+        o.o.emplace_back("minReaderVersion", x);
+        int64_t wv = 0;
+        for (auto& w : wr) if (w.row == rd[i].row && w.has_value) wv = w.ival;
+        JVal y; y.t = JVal::NUM; y.s = std::to_string(wv);
+        o.o.emplace_back("minWriterVersion", y);
+        a.val = o;
+        a.json = "{\"protocol\":" + json_dump(o) + "}";
+        rows[rd[i].row] = a;
+      }
+    }
+    // txn
+    {
+      auto app = load("txn.appId", 0);
+      auto ver = load("txn.version", 0);
+      auto lu = load("txn.lastUpdated", 0);
+      for (auto& e : app) {
+        NonFileAction a;
+        a.kind = 4;
+        a.order = base_action + uint64_t(e.row);
+        JVal o; o.t = JVal::OBJ;
+        JVal id; if (e.has_value) { id.t = JVal::STR; id.s = e.sval; }
+        o.o.emplace_back("appId", id);
+        for (auto& v : ver) if (v.row == e.row) { JVal x; x.t = JVal::NUM; x.s = std::to_string(v.has_value ? v.ival : 0); o.o.emplace_back("version", x); }
+        for (auto& v : lu) if (v.row == e.row && v.has_value) { JVal x; x.t = JVal::NUM; x.s = std::to_string(v.ival); o.o.emplace_back("lastUpdated", x); }
+        a.val = o;
+        a.json = "{\"txn\":" + json_dump(o) + "}";
+        rows[e.row] = a;
+      }
+    }
+    // metaData
+    {
+      auto id = load("metaData.id", 0);
+      if (!id.empty()) {
+        auto name = load("metaData.name", 0);
+        auto desc = load("metaData.description", 0);
+        auto prov = load("metaData.format.provider", 0);
+        auto ok = load("metaData.format.options.key_value.key", 2);
+        auto ov = load("metaData.format.options.key_value.value", 2);
+        auto schema = load("metaData.schemaString", 0);
+        auto pcols = load("metaData.partitionColumns.list.element", 1);
+        auto ck = load("metaData.configuration.key_value.key", 1);
+        auto cv = load("metaData.configuration.key_value.value", 1);
+        auto ct = load("metaData.createdTime", 0);
+        auto str_at = [](const std::vector<pq::Entry>& v, int64_t row, JVal* out) {
+          for (auto& e : v) if (e.row == row && e.has_value) { out->t = JVal::STR; out->s = e.sval; return true; }
+          return false;
+        };
+        // map / list entries of one row: entries whose def reaches the key_value (or list) level
+        auto map_of = [](const std::vector<pq::Entry>& ks, const std::vector<pq::Entry>& vs, int64_t row,
+                         int entry_def, JVal* out) {
+          out->t = JVal::OBJ;
+          bool present = false;
+          for (size_t i = 0; i < ks.size(); ++i) {
+            if (ks[i].row != row) continue;
+            present = true;
+            if (ks[i].def < entry_def) continue;
+            JVal v;
+            if (i < vs.size() && vs[i].has_value) { v.t = JVal::STR; v.s = vs[i].sval; }
+            out->o.emplace_back(ks[i].sval, v);
+          }
+          return present;
+        };
+        for (auto& e : id) {
+          int64_t r = e.row;
+          NonFileAction a;
+          a.kind = 3;
+          a.order = base_action + uint64_t(r);
+          JVal o; o.t = JVal::OBJ;
+          JVal v;
+          if (e.has_value) { v.t = JVal::STR; v.s = e.sval; o.o.emplace_back("id", v); }
+          if (str_at(name, r, &v)) o.o.emplace_back("name", v);
+          v = JVal();
+          if (str_at(desc, r, &v)) o.o.emplace_back("description", v);
+          JVal fmtv; fmtv.t = JVal::OBJ;
+          v = JVal();
+          if (str_at(prov, r, &v)) fmtv.o.emplace_back("provider", v);
+          JVal opts;
+          const pq::Leaf* okl = m.leaf("metaData.format.options.key_value.key");
+          map_of(ok, ov, r, okl ? okl->max_def : 0, &opts);
+          fmtv.o.emplace_back("options", opts);
+          o.o.emplace_back("format", fmtv);
+          v = JVal();
+          if (str_at(schema, r, &v)) o.o.emplace_back("schemaString", v);
+          JVal pc; pc.t = JVal::ARR;
+          const pq::Leaf* pcl = m.leaf("metaData.partitionColumns.list.element");
+          for (auto& x : pcols) {
+            if (x.row != r || !pcl || x.def < pcl->max_def - 1) continue;
+            JVal s;
+            if (x.has_value) { s.t = JVal::STR; s.s = x.sval; }
+            pc.a.push_back(s);
+          }
+          o.o.emplace_back("partitionColumns", pc);
+          JVal conf;
+          const pq::Leaf* ckl = m.leaf("metaData.configuration.key_value.key");
+          map_of(ck, cv, r, ckl ? ckl->max_def : 0, &conf);
+          o.o.emplace_back("configuration", conf);
+          for (auto& x : ct) if (x.row == r && x.has_value) { JVal n; n.t = JVal::NUM; n.s = std::to_string(x.ival); o.o.emplace_back("createdTime", n); }
+          a.val = o;
+          a.json = "{\"metaData\":" + json_dump(o) + "}";
+          rows[r] = a;
+        }
+      }
+    }
+    for (auto& kv : rows) s.ck_nonfile.push_back(kv.second);
+    rg_base += rg.num_rows;
+  }
+}
+
+static void plan_checkpoint(StagedData& s) {
+  uint64_t row_base = 0;
+  for (CkPart& part : s.parts) {
+    part.meta = pq::parse_footer(s.h_pq.data() + part.off, part.len);
+    part.row_base = row_base;
+    row_base += uint64_t(part.meta.num_rows);
+  }
+  s.ck_rows = row_base;
+  if (s.parts.empty()) return;
+  const pq::FileMeta& m0 = s.parts[0].meta;
+  for (int c = 0; c < HC_N; ++c) {
+    const pq::Leaf* l = m0.leaf(kHotPath[c]);
+    s.has_col[c] = l != nullptr;
+    if (l) {
+      if (l->max_rep != 0) fail(DR_E_PARQUET, fmt("column %s is repeated", kHotPath[c]));
+      s.max_def[c] = l->max_def;
+      if (c == HC_ADD_PATH) s.add_def = l->def_of[0];
+      if (c == HC_RM_PATH) s.rm_def = l->def_of[0];
+    }
+  }
+  if (!s.has_col[HC_ADD_PATH]) fail(DR_E_PARQUET, "checkpoint has no add.path column");
+  // pages of the hot columns
+  uint64_t arena = 0;
+  uint32_t dict_pool = 0;
+  for (CkPart& part : s.parts) {
+    const uint8_t* file = s.h_pq.data() + part.off;
+    uint64_t rg_row = part.row_base;
+    for (const pq::RowGroup& rg : part.meta.row_groups) {
+      for (int c = 0; c < HC_N; ++c) {
+        if (!s.has_col[c]) continue;
+        const pq::ColumnChunk* cc = nullptr;
+        for (auto& x : rg.cols) if (x.path == kHotPath[c]) cc = &x;
+        if (!cc) continue;
+        if (cc->codec != 0 && cc->codec != 1)
+          fail(DR_E_UNSUPPORTED, fmt("checkpoint codec %d is not supported (column %s)", cc->codec, kHotPath[c]));
+        const pq::Leaf* l = part.meta.leaf(kHotPath[c]);
+        int dict_idx = -1;
+        uint64_t row = rg_row;
+        for (const pq::Page& p : pq::walk_pages(file, part.len, *cc)) {
+          PageDesc d{};
+          d.src = uint64_t(part.off + uint64_t(p.data_off));  // relocated below
+          d.dst = arena;
+          d.csize = uint32_t(p.compressed_size);
+          d.usize = uint32_t(p.uncompressed_size);
+          d.num_values = uint32_t(p.num_values);
+          d.kind = p.page_type == pq::DICTIONARY_PAGE ? PG_DICT : p.page_type == pq::DATA_PAGE_V2 ? PG_DATA_V2 : PG_DATA_V1;
+          d.encoding = p.encoding;
+          d.codec = cc->codec;
+          d.col = c;
+          d.phys = l->type;
+          d.max_def = l->max_def;
+          d.v2_def_len = p.v2_def_len;
+          d.v2_rep_len = p.v2_rep_len;
+          d.v2_compressed = p.v2_compressed;
+          if (d.kind == PG_DICT) {
+            dict_idx = int(s.pages.size());
+            d.dict_base = dict_pool;
+            dict_pool += d.num_values;
+            d.dict = -1;
+          } else {
+            d.dict = dict_idx;
+            d.row_base = row;
+            row += p.num_values;
+            if (d.encoding != 0 && d.encoding != 2 && d.encoding != 8 && !(d.encoding == 3 && l->type == 0))
+              fail(DR_E_UNSUPPORTED, fmt("encoding %d not supported for %s", d.encoding, kHotPath[c]));
+          }
+          arena += (uint64_t(d.usize) + 16 + 15) & ~uint64_t(15);
+          s.pages.push_back(d);
+        }
+        if (row != rg_row + uint64_t(rg.num_rows))
+          fail(DR_E_PARQUET, fmt("column %s: %llu levels for %lld rows", kHotPath[c],
+                                 (unsigned long long)(row - rg_row), (long long)rg.num_rows));
+      }
+      rg_row += uint64_t(rg.num_rows);
+    }
+  }
+  s.dict_entries = dict_pool;
+  s.d_arena = DBuf<uint8_t>(s.ctx, arena + 64);
+  for (PageDesc& d : s.pages) {
+    d.src = reinterpret_cast<uint64_t>(s.d_pq.p) + d.src;
+    d.dst = reinterpret_cast<uint64_t>(s.d_arena.p) + d.dst;
+  }
+  s.d_pages = DBuf<PageDesc>(s.ctx, s.pages.size());
+  if (!s.pages.empty())
+    HIP_OK(hipMemcpyAsync(s.d_pages.p, s.pages.data(), s.pages.size() * sizeof(PageDesc), hipMemcpyHostToDevice,
+                          s.ctx->stream));
+  for (CkPart& part : s.parts) decode_ck_nonfile(s, part, part.row_base);
+}
+
+static std::shared_ptr<StagedData> stage_files(dr_ctx* ctx, const dr_file* files, int32_t nfiles) {
+  auto s = std::make_shared<StagedData>();
+  s->ctx = ctx;
+  std::vector<const dr_file*> js, cks;
+  for (int32_t i = 0; i < nfiles; ++i) (files[i].kind == DR_FILE_CHECKPOINT ? cks : js).push_back(&files[i]);
+  std::stable_sort(cks.begin(), cks.end(), [](const dr_file* a, const dr_file* b) { return a->part < b->part; });
+  // JSON: concatenation, every file newline-terminated
+  for (const dr_file* f : js) {
+    JsonFileRec r{f->version, s->h_json.size(), f->len};
+    s->h_json.insert(s->h_json.end(), f->data, f->data + f->len);
+    if (f->len == 0 || f->data[f->len - 1] != '\n') s->h_json.push_back('\n');
+    r.len = s->h_json.size() - r.off;
+    s->jfiles.push_back(r);
+    s->version = std::max(s->version, f->version);
+  }
+  const uint64_t json_len = s->h_json.size();
+  s->h_json.resize(json_len + 64, 0);
+  for (const dr_file* f : cks) {
+    CkPart p;
+    p.off = s->h_pq.size();
+    p.len = f->len;
+    s->h_pq.insert(s->h_pq.end(), f->data, f->data + f->len);
+    s->h_pq.resize((s->h_pq.size() + 15) & ~size_t(15), 0);
+    s->parts.push_back(p);
+    s->ck_version = f->version;
+    s->version = std::max(s->version, f->version);
+  }
+  s->h_pq.resize(s->h_pq.size() + 64, 0);
+  s->d_json = DBuf<uint8_t>(ctx, s->h_json.size());
+  s->d_pq = DBuf<uint8_t>(ctx, s->h_pq.size());
+  HIP_OK(hipMemcpyAsync(s->d_json.p, s->h_json.data(), s->h_json.size(), hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipMemcpyAsync(s->d_pq.p, s->h_pq.data(), s->h_pq.size(), hipMemcpyHostToDevice, ctx->stream));
+  s->h_json.resize(json_len);
+  plan_checkpoint(*s);
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  return s;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// replay
+// ---------------------------------------------------------------------------------------------------
+static int bucket_bits_for(uint64_t n) {
+  int bits = 0;
+  while ((n >> bits) > 1536 && bits < 22) ++bits;
+  return bits;
+}
+
+static void reduce_nonfile(dr_state& st, std::vector<NonFileAction>& acts, bool validate) {
+  // InMemoryLogReplay.append for the non-path actions: last protocol, last metaData, last txn per
+  // appId (D/actions/InMemoryLogReplay.scala:47-53).
+  std::sort(acts.begin(), acts.end(), [](const NonFileAction& a, const NonFileAction& b) { return a.order < b.order; });
+  const NonFileAction* prot = nullptr;
+  const NonFileAction* meta = nullptr;
+  std::vector<std::string> app_order;
+  std::map<std::string, const NonFileAction*> txns;
+  for (const NonFileAction& a : acts) {
+    if (a.kind == 5) prot = &a;
+    else if (a.kind == 3) meta = &a;
+    else if (a.kind == 4) {
+      const JVal* id = a.val.get("appId");
+      std::string k = id && id->t == JVal::STR ? id->s : std::string();
+      if (!txns.count(k)) app_order.push_back(k);
+      txns[k] = &a;
+    }
+  }
+  st.nonfile.clear();
+  std::string out;
+  if (prot) { st.nonfile.push_back(*prot); out += prot->json + "\n"; }
+  if (meta) { st.nonfile.push_back(*meta); out += meta->json + "\n"; }
+  for (auto& k : app_order) { st.nonfile.push_back(*txns[k]); out += txns[k]->json + "\n"; }
+  st.nonfile_json = out;
+  st.counts.num_protocol = prot ? 1 : 0;
+  st.counts.num_metadata = meta ? 1 : 0;
+  st.counts.num_set_transactions = int64_t(txns.size());
+  if (validate && !prot)  // D/Snapshot.scala:154-162, D/DeltaErrors.scala:553-560
+    fail(DR_E_MISSING_PROTOCOL, fmt("The protocol of your Delta table could not be recovered while Reconstructing "
+                                    "version: %lld. Did you manually delete files in the _delta_log directory?",
+                                    (long long)st.counts.version));
+  if (validate && !meta)
+    fail(DR_E_MISSING_METADATA, fmt("The metadata of your Delta table could not be recovered while Reconstructing "
+                                    "version: %lld. Did you manually delete files in the _delta_log directory?",
+                                    (long long)st.counts.version));
+}
+
+static dr_state* replay(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, int64_t cutoff, uint32_t flags) {
+  StagedData& s = *sp;
+  hipStream_t stream = ctx->stream;
+  auto st = std::make_unique<dr_state>();
+  st->ctx = ctx;
+  st->staged = sp;
+  st->counts.version = s.version;
+  ctx->mark("start");
+  // ---- K1a: newline index ----
+  const uint64_t json_len = s.h_json.size();
+  const uint64_t nbj = json_num_blocks(json_len);
+  DBuf<uint32_t> jcounts(ctx, nbj + 1);
+  DBuf<uint64_t> joff(ctx, nbj + 1);
+  DBuf<uint8_t> scratch(ctx, scan_scratch_bytes(std::max<uint64_t>(nbj, uint64_t(1) << 23)));
+  uint64_t nlines = 0;
+  if (nbj) {
+    launch_json_count(s.d_json.p, json_len, jcounts.p, stream);
+    launch_scan_u32(jcounts.p, joff.p, nbj, scratch.p, stream);
+    nlines = d2h_one(joff.p + nbj, stream);
+  }
+  const uint64_t R = s.ck_rows, N = R + nlines;
+  st->n_actions = N;
+  st->kind = DBuf<uint8_t>(ctx, N);
+  st->flags = DBuf<uint8_t>(ctx, N);
+  st->key = DBuf<uint64_t>(ctx, N);
+  st->path_ptr = DBuf<uint64_t>(ctx, N);
+  st->path_len = DBuf<uint32_t>(ctx, N);
+  st->size = DBuf<int64_t>(ctx, N);
+  st->delts = DBuf<int64_t>(ctx, N);
+  st->src_off = DBuf<uint64_t>(ctx, N);
+  st->src_len = DBuf<uint32_t>(ctx, N);
+  DBuf<uint64_t> counters(ctx, 8);  // 0 special count, 1 special bytes, 2 nonfile count, 3 errors, 4 canon fill
+  counters.zero(stream);
+  DBuf<uint64_t> nl(ctx, nlines);
+  DBuf<uint64_t> nonfile(ctx, nlines);
+  ActionArrays act{st->kind.p, st->flags.p, st->key.p, st->path_ptr.p, st->path_len.p, st->size.p, st->delts.p,
+                   st->src_off.p, st->src_len.p};
+  ctx->mark("json_index");
+  if (nlines) {
+    launch_json_newlines(s.d_json.p, json_len, joff.p, nl.p, stream);
+    ctx->mark("json_newlines");
+    JsonParseArgs ja{s.d_json.p, nl.p, nlines, R, act.kind, act.flags, act.key, act.path_ptr, act.path_len,
+                     act.size, act.delts, act.src_off, act.src_len, counters.p + 0, counters.p + 1, counters.p + 2,
+                     nonfile.p, nlines, counters.p + 3};
+    launch_json_parse(ja, stream);
+    ctx->mark("json_parse");
+  }
+  // ---- K2: checkpoint ----
+  DBuf<uint8_t> cdef[HC_N];
+  DBuf<int64_t> cival[HC_N];
+  DBuf<uint64_t> csptr[HC_N];
+  DBuf<uint32_t> cslen[HC_N];
+  DBuf<uint64_t> dict_ptr;
+  DBuf<uint32_t> dict_len, pq_err;
+  if (R) {
+    ParquetArgs pa{};
+    pa.pages = s.d_pages.p;
+    pa.npages = uint32_t(s.pages.size());
+    pa.ncols = HC_N;
+    for (int c = 0; c < HC_N; ++c) {
+      cdef[c] = DBuf<uint8_t>(ctx, R);
+      cdef[c].zero(stream);
+      if (c == HC_ADD_PATH || c == HC_RM_PATH) {
+        csptr[c] = DBuf<uint64_t>(ctx, R);
+        cslen[c] = DBuf<uint32_t>(ctx, R);
+      } else {
+        cival[c] = DBuf<int64_t>(ctx, R);
+      }
+      pa.cols[c] = FlatColumn{cdef[c].p, cival[c].p, csptr[c].p, cslen[c].p};
+    }
+    dict_ptr = DBuf<uint64_t>(ctx, s.dict_entries);
+    dict_len = DBuf<uint32_t>(ctx, s.dict_entries);
+    pq_err = DBuf<uint32_t>(ctx, 1);
+    pq_err.zero(stream);
+    pa.dict_ptr = dict_ptr.p;
+    pa.dict_len = dict_len.p;
+    pa.error = pq_err.p;
+    launch_pq_inflate(pa, stream);
+    ctx->mark("pq_inflate");
+    launch_pq_dict(pa, stream);
+    launch_pq_data(pa, stream);
+    ctx->mark("pq_decode");
+    CkptAssembleArgs ca{};
+    ca.add_path = pa.cols[HC_ADD_PATH];
+    ca.add_size = pa.cols[HC_ADD_SIZE];
+    ca.rm_path = pa.cols[HC_RM_PATH];
+    ca.rm_delts = pa.cols[HC_RM_DELTS];
+    ca.add_def = s.add_def;
+    ca.rm_def = s.rm_def;
+    ca.add_path_max = s.max_def[HC_ADD_PATH];
+    ca.add_size_max = s.has_col[HC_ADD_SIZE] ? s.max_def[HC_ADD_SIZE] : 255;
+    ca.rm_path_max = s.max_def[HC_RM_PATH];
+    ca.rm_delts_max = s.has_col[HC_RM_DELTS] ? s.max_def[HC_RM_DELTS] : 255;
+    ca.has_rm = s.has_col[HC_RM_PATH] ? 1 : 0;
+    ca.nrows = R;
+    ca.row_base = 0;
+    ca.act = act;
+    ca.special_count = counters.p + 0;
+    ca.special_bytes = counters.p + 1;
+    launch_ckpt_assemble(ca, stream);
+    ctx->mark("ckpt_assemble");
+  }
+  std::vector<uint64_t> cnt = d2h(counters.p, 8, stream);
+  if (R && d2h_one(pq_err.p, stream) != 0)
+    fail(DR_E_PARQUET, fmt("device checkpoint decode failed (code %u)", d2h_one(pq_err.p, stream)));
+  st->counts.malformed_lines = int64_t(cnt[3]);
+  // ---- canonicalisation of special paths ----
+  if (cnt[0]) {
+    const uint64_t cap = cnt[1] * 2 + 64 * cnt[0] + 64;
+    st->canon_arena = DBuf<uint8_t>(ctx, cap);
+    CanonArgs cg{act, N, st->canon_arena.p, cap, counters.p + 4};
+    launch_canon(cg, stream);
+    ctx->mark("canon");
+  }
+  // ---- K3: partition by hash bucket ----
+  const int bits = bucket_bits_for(N);
+  const uint32_t nb = 1u << bits;
+  DBuf<uint32_t> bcount(ctx, nb);
+  DBuf<uint64_t> boff(ctx, nb + 1);
+  bcount.zero(stream);
+  PartitionArgs pa{st->kind.p, st->flags.p, st->key.p, st->delts.p, N, cutoff, bits, bcount.p, boff.p, nullptr, nullptr};
+  launch_bucket_hist(pa, stream);
+  launch_scan_u32(bcount.p, boff.p, nb, scratch.p, stream);
+  bcount.zero(stream);
+  DBuf<uint64_t> rkey(ctx, N);
+  DBuf<uint32_t> rmeta(ctx, N);
+  pa.rec_key = rkey.p;
+  pa.rec_meta = rmeta.p;
+  ctx->mark("partition_hist");
+  launch_bucket_scatter(pa, stream);
+  ctx->mark("partition_scatter");
+  // ---- K4: per-bucket last-writer-wins ----
+  DBuf<uint32_t> olive(ctx, N), otomb(ctx, N), lcount(ctx, nb), tcount(ctx, nb), clist(ctx, nb), olist(ctx, nb);
+  DBuf<unsigned long long> totals(ctx, 8);
+  totals.zero(stream);
+  ReduceArgs ra{rkey.p, rmeta.p, boff.p, nb, bits, st->path_ptr.p, st->path_len.p, st->size.p, 1u,
+                olive.p, otomb.p, lcount.p, tcount.p, totals.p, clist.p, olist.p};
+  launch_bucket_reduce(ra, stream);
+  ctx->mark("reduce");
+  std::vector<unsigned long long> tot = d2h(totals.p, 8, stream);
+  if (tot[3] || tot[4]) {
+    std::vector<uint32_t> redo = d2h(clist.p, size_t(tot[3]), stream);
+    std::vector<uint32_t> ov = d2h(olist.p, size_t(tot[4]), stream);
+    redo.insert(redo.end(), ov.begin(), ov.end());
+    DBuf<uint32_t> dredo(ctx, redo.size());
+    HIP_OK(hipMemcpyAsync(dredo.p, redo.data(), redo.size() * 4, hipMemcpyHostToDevice, stream));
+    launch_bucket_exact(ra, dredo.p, uint32_t(redo.size()), stream);
+    tot = d2h(totals.p, 8, stream);
+    ctx->mark("reduce_exact");
+  }
+  // ---- compaction ----
+  DBuf<uint64_t> loff(ctx, nb + 1), toff(ctx, nb + 1);
+  launch_scan_u32(lcount.p, loff.p, nb, scratch.p, stream);
+  launch_scan_u32(tcount.p, toff.p, nb, scratch.p, stream);
+  st->n_live = tot[0];
+  st->n_tomb = tot[2];
+  st->live = DBuf<uint32_t>(ctx, st->n_live);
+  st->tomb = DBuf<uint32_t>(ctx, st->n_tomb);
+  launch_compact(CompactArgs{olive.p, boff.p, lcount.p, loff.p, nb, st->live.p}, stream);
+  launch_compact(CompactArgs{otomb.p, boff.p, tcount.p, toff.p, nb, st->tomb.p}, stream);
+  const uint64_t n_file_actions = d2h_one(boff.p + nb, stream);
+  ctx->mark("compact");
+  st->counts.num_files = int64_t(tot[0]);
+  st->counts.size_in_bytes = int64_t(tot[1]);
+  st->counts.num_removes = int64_t(tot[2]);
+  st->counts.live_key_sum = tot[5];
+  st->counts.tomb_key_sum = tot[6];
+  st->counts.num_actions = int64_t(N);
+  st->counts.num_file_actions = int64_t(n_file_actions);
+  // ---- non-file actions (host): checkpoint rows first, then JSON lines in order ----
+  std::vector<NonFileAction> nf = s.ck_nonfile;
+  const uint64_t nnf = std::min<uint64_t>(cnt[2], nlines);
+  if (nnf) {
+    std::vector<uint64_t> lines = d2h(nonfile.p, nnf, stream);
+    std::sort(lines.begin(), lines.end());
+    DBuf<uint64_t> dl(ctx, nnf), dof(ctx, nnf);
+    HIP_OK(hipMemcpyAsync(dl.p, lines.data(), nnf * 8, hipMemcpyHostToDevice, stream));
+    for (uint64_t& x : lines) x += R;  // action indices
+    DBuf<uint64_t> didx(ctx, nnf);
+    HIP_OK(hipMemcpyAsync(didx.p, lines.data(), nnf * 8, hipMemcpyHostToDevice, stream));
+    launch_gather_u64_by64(st->src_off.p, didx.p, nnf, dof.p, stream);
+    std::vector<uint64_t> offs = d2h(dof.p, nnf, stream);
+    for (uint64_t k = 0; k < nnf; ++k) {
+      const uint64_t li = lines[k] - R;
+      const uint64_t b = offs[k];
+      uint64_t e = b;
+      while (e < json_len && s.h_json[e] != '\n') ++e;
+      JVal v;
+      std::string perr;
+      if (!json_parse(reinterpret_cast<const char*>(s.h_json.data() + b), e - b, &v, &perr) || v.t != JVal::OBJ)
+        continue;  // malformed non-file line: PERMISSIVE null row
+      // unwrap priority among non-file kinds: metaData > txn > protocol
+      const char* names[3] = {"metaData", "txn", "protocol"};
+      const int kinds[3] = {3, 4, 5};
+      for (int k = 0; k < 3; ++k) {
+        const JVal* x = v.get(names[k]);
+        if (x && x->t != JVal::NUL) {
+          NonFileAction a;
+          a.kind = kinds[k];
+          a.order = R + li;
+          a.val = *x;
+          a.json = std::string("{\"") + names[k] + "\":" + json_dump(*x) + "}";
+          nf.push_back(std::move(a));
+          break;
+        }
+      }
+    }
+  }
+  reduce_nonfile(*st, nf, !(flags & DR_FLAG_NO_VALIDATION));
+  ctx->mark("end");
+  return st.release();
+}
+
+// ---------------------------------------------------------------------------------------------------
+// export (records materialised on the host from the resident state)
+// ---------------------------------------------------------------------------------------------------
+struct RecordFields {
+  std::string path;
+  int64_t size = 0, mtime = 0, delts = 0;
+  bool delts_valid = false, efm = false;
+  bool stats_null = true;
+  std::string stats;
+  bool pv_null = true, tags_null = true;
+  std::vector<std::pair<std::string, std::pair<bool, std::string>>> pv, tags;  // key -> (null?, value)
+};
+
+static void map_from_json(const JVal* v, bool* is_null, std::vector<std::pair<std::string, std::pair<bool, std::string>>>& out) {
+  if (!v || v->t == JVal::NUL) { *is_null = true; return; }
+  *is_null = false;
+  if (v->t != JVal::OBJ) return;
+  std::map<std::string, size_t> seen;
+  for (auto& kv : v->o) {
+    std::pair<bool, std::string> val{kv.second.t == JVal::NUL, kv.second.t == JVal::STR ? kv.second.s : json_dump(kv.second)};
+    auto it = seen.find(kv.first);
+    if (it != seen.end()) { out[it->second].second = val; continue; }
+    seen[kv.first] = out.size();
+    out.emplace_back(kv.first, val);
+  }
+}
+
+static void fields_from_json(const JVal& o, RecordFields& r) {
+  auto i64 = [&](const char* k, int64_t* dst, bool* valid) {
+    const JVal* v = o.get(k);
+    if (v && v->is_int()) { *dst = v->as_int(); if (valid) *valid = true; }
+  };
+  i64("size", &r.size, nullptr);
+  i64("modificationTime", &r.mtime, nullptr);
+  i64("deletionTimestamp", &r.delts, &r.delts_valid);
+  const JVal* e = o.get("extendedFileMetadata");
+  r.efm = e && e->t == JVal::BOOL && e->b;
+  const JVal* st = o.get("stats");
+  if (st && st->t != JVal::NUL) { r.stats_null = false; r.stats = st->t == JVal::STR ? st->s : json_dump(*st); }
+  map_from_json(o.get("partitionValues"), &r.pv_null, r.pv);
+  map_from_json(o.get("tags"), &r.tags_null, r.tags);
+}
+
+// Checkpoint rows of one side (add or remove) decoded on the host for export.
+struct CkRows {
+  std::unordered_map<int64_t, RecordFields> rows;
+};
+
+static void load_ck_side(StagedData& s, bool add, CkRows& out) {
+  const char* pre = add ? "add." : "remove.";
+  for (CkPart& part : s.parts) {
+    const uint8_t* file = s.h_pq.data() + part.off;
+    int64_t rg_base = int64_t(part.row_base);
+    for (const pq::RowGroup& rg : part.meta.row_groups) {
+      auto col = [&](const std::string& name, int depth, std::vector<pq::Entry>* v, const pq::Leaf** lf) {
+        std::string path = std::string(pre) + name;
+        const pq::Leaf* l = part.meta.leaf(path);
+        if (lf) *lf = l;
+        for (auto& c : rg.cols)
+          if (c.path == path && l) { *v = pq::sparse_entries(file, part.len, c, *l, l->def_of[size_t(depth)], rg_base); return; }
+      };
+      std::vector<pq::Entry> size, mtime, delts, efm, stats, pvk, pvv, tk, tv;
+      const pq::Leaf *pvl = nullptr, *tl = nullptr;
+      col("size", 0, &size, nullptr);
+      col("modificationTime", 0, &mtime, nullptr);
+      col("deletionTimestamp", 0, &delts, nullptr);
+      col("extendedFileMetadata", 0, &efm, nullptr);
+      col("stats", 0, &stats, nullptr);
+      col("partitionValues.key_value.key", 0, &pvk, &pvl);
+      col("partitionValues.key_value.value", 0, &pvv, nullptr);
+      col("tags.key_value.key", 0, &tk, &tl);
+      col("tags.key_value.value", 0, &tv, nullptr);
+      for (auto& e : size) if (e.has_value) out.rows[e.row].size = e.ival;
+      for (auto& e : mtime) if (e.has_value) out.rows[e.row].mtime = e.ival;
+      for (auto& e : delts) if (e.has_value) { out.rows[e.row].delts = e.ival; out.rows[e.row].delts_valid = true; }
+      for (auto& e : efm) if (e.has_value) out.rows[e.row].efm = e.ival != 0;
+      for (auto& e : stats) if (e.has_value) { out.rows[e.row].stats = e.sval; out.rows[e.row].stats_null = false; }
+      auto maps = [&](std::vector<pq::Entry>& ks, std::vector<pq::Entry>& vs, const pq::Leaf* l, bool pvmap) {
+        if (!l) return;
+        const int map_def = l->def_of[1];      // partitionValues non-null
+        const int entry_def = l->def_of[2];    // key_value present
+        for (size_t i = 0; i < ks.size(); ++i) {
+          RecordFields& r = out.rows[ks[i].row];
+          bool& isnull = pvmap ? r.pv_null : r.tags_null;
+          if (ks[i].def >= map_def) isnull = false;
+          if (ks[i].def < entry_def) continue;
+          bool vnull = !(i < vs.size() && vs[i].has_value);
+          (pvmap ? r.pv : r.tags).emplace_back(ks[i].sval, std::make_pair(vnull, vnull ? std::string() : vs[i].sval));
+        }
+      };
+      maps(pvk, pvv, pvl, true);
+      maps(tk, tv, tl, false);
+      rg_base += rg.num_rows;
+    }
+  }
+}
+
+static void build_export(dr_state& st, int which) {
+  ExportCols& ex = st.exp[which];
+  if (ex.built) return;
+  hipStream_t stream = st.ctx->stream;
+  StagedData& s = *st.staged;
+  const uint64_t n = which == DR_LIVE ? st.n_live : st.n_tomb;
+  std::vector<uint32_t> idx = d2h(which == DR_LIVE ? st.live.p : st.tomb.p, n, stream);
+  std::vector<uint64_t> pptr(n), soff(n);
+  std::vector<uint32_t> plen(n), slen(n);
+  // gather the per-action fields (small D2H per record batch)
+  {
+    const uint32_t* didx = which == DR_LIVE ? st.live.p : st.tomb.p;
+    DBuf<uint64_t> a(st.ctx, n), b(st.ctx, n);
+    DBuf<uint32_t> c(st.ctx, n), d(st.ctx, n);
+    launch_gather_u64(st.path_ptr.p, didx, n, a.p, stream);
+    launch_gather_u64(st.src_off.p, didx, n, b.p, stream);
+    launch_gather_u32(st.path_len.p, didx, n, c.p, stream);
+    launch_gather_u32(st.src_len.p, didx, n, d.p, stream);
+    pptr = d2h(a.p, n, stream);
+    soff = d2h(b.p, n, stream);
+    plen = d2h(c.p, n, stream);
+    slen = d2h(d.p, n, stream);
+    // canonical path bytes in one transfer
+    std::vector<uint64_t> off(n + 1, 0);
+    for (uint64_t i = 0; i < n; ++i) off[i + 1] = off[i] + plen[i];
+    DBuf<uint64_t> doff(st.ctx, n + 1);
+    DBuf<uint8_t> bytes(st.ctx, off[n] + 1);
+    HIP_OK(hipMemcpyAsync(doff.p, off.data(), (n + 1) * 8, hipMemcpyHostToDevice, stream));
+    launch_gather_bytes(a.p, c.p, doff.p, n, bytes.p, stream);
+    ex.path_bytes = d2h(bytes.p, off[n], stream);
+    ex.path_off.assign(off.begin(), off.end());
+  }
+  CkRows ck;
+  bool ck_loaded = false;
+  ex.n = int64_t(n);
+  ex.stats_off.push_back(0);
+  ex.pv_entry_off.push_back(0);
+  ex.pv_key_off.push_back(0);
+  ex.pv_val_off.push_back(0);
+  ex.tags_entry_off.push_back(0);
+  ex.tags_key_off.push_back(0);
+  ex.tags_val_off.push_back(0);
+  for (uint64_t i = 0; i < n; ++i) {
+    RecordFields r;
+    if (idx[i] >= s.ck_rows) {
+      JVal v;
+      json_parse(reinterpret_cast<const char*>(s.h_json.data() + soff[i]), slen[i], &v);
+      const JVal* o = v.get(which == DR_LIVE ? "add" : "remove");
+      if (o) fields_from_json(*o, r);
+    } else {
+      if (!ck_loaded) { load_ck_side(s, which == DR_LIVE, ck); ck_loaded = true; }
+      auto it = ck.rows.find(int64_t(soff[i]));
+      if (it != ck.rows.end()) r = it->second;
+    }
+    ex.size.push_back(r.size);
+    ex.mtime.push_back(r.mtime);
+    ex.delts.push_back(r.delts);
+    ex.delts_valid.push_back(r.delts_valid);
+    ex.efm.push_back(r.efm);
+    ex.stats_null.push_back(r.stats_null);
+    ex.stats_bytes.insert(ex.stats_bytes.end(), r.stats.begin(), r.stats.end());
+    ex.stats_off.push_back(int64_t(ex.stats_bytes.size()));
+    ex.pv_null.push_back(r.pv_null);
+    for (auto& kv : r.pv) {
+      ex.pv_key_bytes.insert(ex.pv_key_bytes.end(), kv.first.begin(), kv.first.end());
+      ex.pv_key_off.push_back(int64_t(ex.pv_key_bytes.size()));
+      ex.pv_val_null.push_back(kv.second.first);
+      ex.pv_val_bytes.insert(ex.pv_val_bytes.end(), kv.second.second.begin(), kv.second.second.end());
+      ex.pv_val_off.push_back(int64_t(ex.pv_val_bytes.size()));
+    }
+    ex.pv_entry_off.push_back(int64_t(ex.pv_val_null.size()));
+    ex.tags_null.push_back(r.tags_null);
+    for (auto& kv : r.tags) {
+      ex.tags_key_bytes.insert(ex.tags_key_bytes.end(), kv.first.begin(), kv.first.end());
+      ex.tags_key_off.push_back(int64_t(ex.tags_key_bytes.size()));
+      ex.tags_val_null.push_back(kv.second.first);
+      ex.tags_val_bytes.insert(ex.tags_val_bytes.end(), kv.second.second.begin(), kv.second.second.end());
+      ex.tags_val_off.push_back(int64_t(ex.tags_val_bytes.size()));
+    }
+    ex.tags_entry_off.push_back(int64_t(ex.tags_val_null.size()));
+  }
+  ex.built = true;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------------------------------
+namespace {
+template <typename F>
+int guard(dr_ctx* ctx, F&& f) {
+  try {
+    f();
+    if (ctx) ctx->err.clear();
+    return DR_OK;
+  } catch (const Error& e) {
+    if (ctx) ctx->err = e.what();
+    return e.status;
+  } catch (const std::bad_alloc&) {
+    if (ctx) ctx->err = "host allocation failed";
+    return DR_E_OOM;
+  } catch (const std::exception& e) {
+    if (ctx) ctx->err = e.what();
+    return DR_E_INTERNAL;
+  }
+}
+}  // namespace
+
+extern "C" {
+
+int dr_abi_version(void) { return DR_ABI_VERSION; }
+
+int dr_ctx_create(int device, dr_ctx** out) {
+  if (!out) return DR_E_INVALID_ARG;
+  *out = nullptr;
+  auto c = std::make_unique<dr_ctx>();
+  c->device = device;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) {
+    (void)hipGetLastError();
+    return DR_E_DEVICE;
+  }
+  if (hipSetDevice(device) != hipSuccess) return DR_E_DEVICE;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return DR_E_DEVICE;
+  *out = c.release();
+  return DR_OK;
+}
+
+void dr_ctx_destroy(dr_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipStreamSynchronize(ctx->stream);
+  ctx->trim();
+  (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+const char* dr_last_error(const dr_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int dr_log_segment(dr_ctx* ctx, const char* log_path, int64_t version_to_load, char* buf, uint64_t buf_len,
+                   uint64_t* needed, int64_t* version_out) {
+  return guard(ctx, [&] {
+    if (!log_path) fail(DR_E_INVALID_ARG, "null log path");
+    LogSegmentInfo seg = get_log_segment(log_path, version_to_load);
+    std::string s;
+    for (auto& f : seg.checkpoint) s += fmt("%d %lld %d %s\n", f.kind, (long long)f.version, f.part, f.name.c_str());
+    for (auto& f : seg.deltas) s += fmt("%d %lld %d %s\n", f.kind, (long long)f.version, f.part, f.name.c_str());
+    if (needed) *needed = s.size() + 1;
+    if (version_out) *version_out = seg.version;
+    if (buf && buf_len) {
+      size_t n = std::min<size_t>(s.size(), buf_len - 1);
+      memcpy(buf, s.data(), n);
+      buf[n] = 0;
+    }
+  });
+}
+
+int dr_stage(dr_ctx* ctx, const dr_file* files, int32_t nfiles, dr_staged** out) {
+  if (!ctx || !out || (nfiles && !files)) return DR_E_INVALID_ARG;
+  return guard(ctx, [&] {
+    HIP_OK(hipSetDevice(ctx->device));
+    auto s = std::make_unique<dr_staged>();
+    s->d = stage_files(ctx, files, nfiles);
+    *out = s.release();
+  });
+}
+
+int dr_stage_log(dr_ctx* ctx, const char* log_path, int64_t version_to_load, dr_staged** out) {
+  if (!ctx || !out || !log_path) return DR_E_INVALID_ARG;
+  return guard(ctx, [&] {
+    HIP_OK(hipSetDevice(ctx->device));
+    LogSegmentInfo seg = get_log_segment(log_path, version_to_load);
+    std::vector<std::vector<uint8_t>> bytes;
+    std::vector<dr_file> files;
+    for (auto* list : {&seg.checkpoint, &seg.deltas})
+      for (auto& f : *list) bytes.push_back(read_file(std::string(log_path) + "/" + f.name));
+    size_t k = 0;
+    for (auto* list : {&seg.checkpoint, &seg.deltas})
+      for (auto& f : *list) {
+        files.push_back(dr_file{f.version, f.kind, f.part, bytes[k].data(), bytes[k].size()});
+        ++k;
+      }
+    auto s = std::make_unique<dr_staged>();
+    s->d = stage_files(ctx, files.data(), int32_t(files.size()));
+    s->d->version = seg.version;
+    *out = s.release();
+  });
+}
+
+int dr_staged_release(dr_staged* staged) {
+  delete staged;
+  return DR_OK;
+}
+
+int dr_staged_bytes(const dr_staged* staged, uint64_t* json_bytes, uint64_t* checkpoint_bytes) {
+  if (!staged) return DR_E_INVALID_ARG;
+  if (json_bytes) *json_bytes = staged->d->h_json.size();
+  if (checkpoint_bytes) {
+    uint64_t n = 0;
+    for (auto& p : staged->d->parts) n += p.len;
+    *checkpoint_bytes = n;
+  }
+  return DR_OK;
+}
+
+int dr_replay_staged(dr_ctx* ctx, const dr_staged* staged, int64_t cutoff, uint32_t flags, dr_state** out) {
+  if (!ctx || !staged || !out) return DR_E_INVALID_ARG;
+  *out = nullptr;
+  int rc = guard(ctx, [&] {
+    HIP_OK(hipSetDevice(ctx->device));
+    *out = replay(ctx, staged->d, cutoff, flags);
+    ctx->collect_timings();
+  });
+  if (rc != DR_OK) {
+    for (auto& m : ctx->marks) (void)hipEventDestroy(m.second);
+    ctx->marks.clear();
+  }
+  return rc;
+}
+
+int dr_replay(dr_ctx* ctx, const dr_file* files, int32_t nfiles, int64_t cutoff, uint32_t flags, dr_state** out) {
+  dr_staged* s = nullptr;
+  int rc = dr_stage(ctx, files, nfiles, &s);
+  if (rc != DR_OK) return rc;
+  rc = dr_replay_staged(ctx, s, cutoff, flags, out);
+  dr_staged_release(s);
+  return rc;
+}
+
+int dr_state_release(dr_state* state) {
+  if (!state) return DR_OK;
+  (void)hipStreamSynchronize(state->ctx->stream);
+  delete state;
+  return DR_OK;
+}
+
+int dr_state_counts(dr_state* state, dr_counts* out) {
+  if (!state || !out) return DR_E_INVALID_ARG;
+  *out = state->counts;
+  return DR_OK;
+}
+
+int dr_state_nonfile_json(dr_state* state, const char** json, uint64_t* len) {
+  if (!state || !json || !len) return DR_E_INVALID_ARG;
+  *json = state->nonfile_json.c_str();
+  *len = state->nonfile_json.size();
+  return DR_OK;
+}
+
+int dr_state_export(dr_state* state, int32_t which, dr_export* out) {
+  if (!state || !out || (which != DR_LIVE && which != DR_TOMBSTONES)) return DR_E_INVALID_ARG;
+  return guard(state->ctx, [&] {
+    build_export(*state, which);
+    ExportCols& e = state->exp[which];
+    *out = dr_export{};
+    out->n = e.n;
+    out->path_off = e.path_off.data(); out->path_bytes = e.path_bytes.data();
+    out->size = e.size.data(); out->modification_time = e.mtime.data();
+    out->deletion_timestamp = e.delts.data(); out->deletion_timestamp_valid = e.delts_valid.data();
+    out->extended_file_metadata = e.efm.data();
+    out->stats_off = e.stats_off.data(); out->stats_bytes = e.stats_bytes.data(); out->stats_null = e.stats_null.data();
+    out->pv_entry_off = e.pv_entry_off.data(); out->pv_null = e.pv_null.data();
+    out->pv_key_off = e.pv_key_off.data(); out->pv_key_bytes = e.pv_key_bytes.data();
+    out->pv_val_off = e.pv_val_off.data(); out->pv_val_bytes = e.pv_val_bytes.data(); out->pv_val_null = e.pv_val_null.data();
+    out->tags_entry_off = e.tags_entry_off.data(); out->tags_null = e.tags_null.data();
+    out->tags_key_off = e.tags_key_off.data(); out->tags_key_bytes = e.tags_key_bytes.data();
+    out->tags_val_off = e.tags_val_off.data(); out->tags_val_bytes = e.tags_val_bytes.data();
+    out->tags_val_null = e.tags_val_null.data();
+  });
+}
+
+int dr_filter(dr_state* state, const dr_predicate* pred, int64_t** selected, int64_t* nselected) {
+  if (!state || !pred || !selected || !nselected) return DR_E_INVALID_ARG;
+  state->ctx->err = "dr_filter: partition pruning kernel not built yet";
+  return DR_E_UNSUPPORTED;
+}
+
+void dr_free(void* p) { free(p); }
+
+int dr_set_timing(dr_ctx* ctx, int32_t on) {
+  if (!ctx) return DR_E_INVALID_ARG;
+  ctx->timing = on != 0;
+  return DR_OK;
+}
+
+int dr_last_timings(dr_ctx* ctx, char* names, uint64_t names_len, float* ms, int32_t cap, int32_t* n) {
+  if (!ctx || !n) return DR_E_INVALID_ARG;
+  std::string all;
+  int32_t k = 0;
+  for (auto& t : ctx->timings) {
+    if (k < cap && ms) ms[k] = t.second;
+    all += t.first;
+    all.push_back('\0');
+    ++k;
+  }
+  *n = k;
+  if (names && names_len) {
+    size_t c = std::min<size_t>(all.size(), names_len);
+    memcpy(names, all.data(), c);
+  }
+  return DR_OK;
+}
+
+}  // extern "C"

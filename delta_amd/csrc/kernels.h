@@ -1,0 +1,178 @@
+// Kernel argument blocks and launchers (host <-> device contract of libdeltareplay).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace dr {
+
+// Per-action SoA arrays in HBM; action index = checkpoint rows first, then JSON lines (the
+// reference's replay order: D/Snapshot.scala:102-104 sorts by input file name).
+struct ActionArrays {
+  uint8_t* kind;
+  uint8_t* flags;
+  uint64_t* key;        // xxh64(canonical path) | (==0)
+  uint64_t* path_ptr;   // device address of the canonical path bytes
+  uint32_t* path_len;
+  int64_t* size;
+  int64_t* delts;
+  uint64_t* src_off;    // JSON: line offset in the JSON buffer; checkpoint: row index
+  uint32_t* src_len;    // JSON: line length
+};
+
+struct JsonParseArgs {
+  const uint8_t* buf;
+  const uint64_t* nl;
+  uint64_t nlines;
+  uint64_t base;        // action index of the first JSON line
+  uint8_t* kind;
+  uint8_t* flags;
+  uint64_t* key;
+  uint64_t* path_ptr;
+  uint32_t* path_len;
+  int64_t* size;
+  int64_t* delts;
+  uint64_t* src_off;
+  uint32_t* src_len;
+  uint64_t* special_count;
+  uint64_t* special_bytes;
+  uint64_t* nonfile_count;
+  uint64_t* nonfile_idx;
+  uint64_t nonfile_cap;
+  uint64_t* error_count;
+};
+
+uint64_t json_num_blocks(uint64_t len);
+void launch_json_count(const uint8_t* buf, uint64_t len, uint32_t* block_counts, hipStream_t st);
+void launch_json_newlines(const uint8_t* buf, uint64_t len, const uint64_t* block_off, uint64_t* nl,
+                          hipStream_t st);
+void launch_json_parse(const JsonParseArgs& a, hipStream_t st);
+
+// ---- scans ------------------------------------------------------------------------------------
+// Exclusive scan of n u32 counts into u64 offsets; out[n] = total. Scratch: scan_scratch_bytes(n).
+uint64_t scan_scratch_bytes(uint64_t n);
+void launch_scan_u32(const uint32_t* in, uint64_t* out, uint64_t n, void* scratch, hipStream_t st);
+
+// ---- Parquet (K2) -------------------------------------------------------------------------------
+enum PageKind : int32_t { PG_DATA_V1 = 0, PG_DICT = 2, PG_DATA_V2 = 3 };
+
+struct PageDesc {
+  uint64_t src;          // device address of the page body (compressed)
+  uint64_t dst;          // device address of the decompressed body in the arena
+  uint32_t csize, usize;
+  uint32_t num_values;   // levels in the page (= rows for flat columns)
+  int32_t kind;          // PageKind
+  int32_t encoding;
+  int32_t codec;         // 0 uncompressed, 1 snappy
+  int32_t col;           // output column slot
+  int32_t phys;          // physical type
+  int32_t max_def;
+  int32_t dict;          // index (into the page table) of this chunk's dictionary page, -1 none
+  uint64_t row_base;     // first checkpoint row of the page (flat columns)
+  int32_t v2_def_len, v2_rep_len, v2_compressed;
+  uint32_t dict_base;    // dictionary pages: first slot in the dictionary pool
+};
+
+// Decoded flat column (max_rep == 0): one entry per checkpoint row.
+struct FlatColumn {
+  uint8_t* def;          // definition level per row
+  int64_t* ival;         // INT64/INT32/BOOLEAN value (valid where def == max_def)
+  uint64_t* sptr;        // BYTE_ARRAY: device address of the value bytes
+  uint32_t* slen;
+};
+
+struct ParquetArgs {
+  PageDesc* pages;
+  uint32_t npages;
+  FlatColumn cols[8];
+  int32_t ncols;
+  uint64_t* dict_ptr;    // dictionary pool (BYTE_ARRAY: address; INT: value)
+  uint32_t* dict_len;
+  uint32_t* error;       // first error code (0 = ok)
+};
+
+void launch_pq_inflate(const ParquetArgs& a, hipStream_t st);
+void launch_pq_dict(const ParquetArgs& a, hipStream_t st);
+void launch_pq_data(const ParquetArgs& a, hipStream_t st);
+
+// Checkpoint row assembly: flat columns -> action arrays.
+struct CkptAssembleArgs {
+  FlatColumn add_path, add_size, rm_path, rm_delts;
+  int32_t add_def, rm_def;              // def level at which add / remove is non-null
+  int32_t add_path_max, add_size_max, rm_path_max, rm_delts_max;
+  int32_t has_rm;                       // checkpoint has a remove column
+  uint64_t nrows;
+  uint64_t row_base;                    // action index of checkpoint row 0
+  ActionArrays act;
+  uint64_t* special_count;
+  uint64_t* special_bytes;
+};
+void launch_ckpt_assemble(const CkptAssembleArgs& a, hipStream_t st);
+
+// ---- canonicalization of special paths ---------------------------------------------------------
+struct CanonArgs {
+  ActionArrays act;
+  uint64_t n;
+  uint8_t* arena;
+  uint64_t arena_cap;
+  uint64_t* arena_fill;
+};
+void launch_canon(const CanonArgs& a, hipStream_t st);
+
+// ---- K3/K4: partition by hash bucket + per-bucket last-writer-wins ------------------------------
+struct PartitionArgs {
+  const uint8_t* kind;
+  const uint8_t* flags;
+  const uint64_t* key;
+  const int64_t* delts;
+  uint64_t n;
+  int64_t cutoff;          // minFileRetentionTimestamp
+  int32_t bucket_bits;
+  uint32_t* bucket_count;  // [nbuckets] histogram / cursors
+  const uint64_t* bucket_off;  // [nbuckets+1] exclusive offsets
+  uint64_t* rec_key;       // partitioned records
+  uint32_t* rec_meta;      // idx << 2 | class
+};
+void launch_bucket_hist(const PartitionArgs& a, hipStream_t st);
+void launch_bucket_scatter(const PartitionArgs& a, hipStream_t st);
+
+struct ReduceArgs {
+  const uint64_t* rec_key;
+  const uint32_t* rec_meta;
+  const uint64_t* bucket_off;
+  uint32_t nbuckets;
+  int32_t bucket_bits;
+  const uint64_t* path_ptr;
+  const uint32_t* path_len;
+  const int64_t* size;
+  uint32_t verify_bytes;   // 1: byte-verify every multi-member key group
+  uint32_t* out_live;      // per-bucket survivors, written at bucket_off[b]
+  uint32_t* out_tomb;
+  uint32_t* live_count;    // [nbuckets]
+  uint32_t* tomb_count;    // [nbuckets]
+  unsigned long long* totals;  // [0] live files, [1] size sum, [2] tombstones, [3] collisions, [4] overflow buckets
+  uint32_t* collide_list;  // buckets that saw a path-hash collision (resolved by k_bucket_exact)
+  uint32_t* overflow_list; // buckets whose distinct keys overflowed the LDS table
+};
+void launch_bucket_reduce(const ReduceArgs& a, hipStream_t st);
+void launch_bucket_exact(const ReduceArgs& a, const uint32_t* buckets, uint32_t nb, hipStream_t st);
+
+// Compaction of per-bucket survivor lists into dense arrays.
+struct CompactArgs {
+  const uint32_t* src;
+  const uint64_t* bucket_off;
+  const uint32_t* counts;
+  const uint64_t* dst_off;   // exclusive scan of counts
+  uint32_t nbuckets;
+  uint32_t* dst;
+};
+void launch_compact(const CompactArgs& a, hipStream_t st);
+
+}  // namespace dr
+
+namespace dr {
+void launch_gather_u64(const uint64_t* src, const uint32_t* idx, uint64_t n, uint64_t* dst, hipStream_t st);
+void launch_gather_u32(const uint32_t* src, const uint32_t* idx, uint64_t n, uint32_t* dst, hipStream_t st);
+void launch_gather_u64_by64(const uint64_t* src, const uint64_t* idx, uint64_t n, uint64_t* dst, hipStream_t st);
+void launch_gather_bytes(const uint64_t* ptr, const uint32_t* len, const uint64_t* off, uint64_t n, uint8_t* out,
+                         hipStream_t st);
+}  // namespace dr

@@ -1,0 +1,442 @@
+"""Host-side mirror of the reference's DeltaLog / Snapshot API over the MI355X replay engine.
+
+Same names, argument meaning and error behaviour as the reference for this path:
+  DeltaLog.for_table            <- DeltaLog.forTable (D/DeltaLog.scala:390-475)
+  DeltaLog.update / snapshot    <- SnapshotManagement.update (D/SnapshotManagement.scala:244-339)
+  DeltaLog.get_snapshot_at      <- SnapshotManagement.getSnapshotAt (:342-360)
+  DeltaLog.min_file_retention_timestamp <- D/DeltaLog.scala:109-120
+  Snapshot.all_files/tombstones <- D/Snapshot.scala:193-204 (dataChange forced false)
+  Snapshot.num_of_files etc.    <- computedState (D/Snapshot.scala:136-186)
+  Snapshot.files_for_scan       <- PartitionFiltering.filesForScan (D/PartitionFiltering.scala:27-42)
+  InMemoryLogReplay             <- D/actions/InMemoryLogReplay.scala:35-77 (append/checkpoint)
+
+All replay work runs in libdeltareplay on the GPU; this module only does control flow.
+D/ = core/src/main/scala/org/apache/spark/sql/delta/ of the reference checkout.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+import re
+import threading
+import time
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+from . import _native as N
+
+
+class DeltaError(Exception):
+    """Carries the reference's exception class name (`kind`) and the C status."""
+
+    KIND = {3: "FileNotFoundException", 4: "FileNotFoundException", 5: "FileNotFoundException",
+            6: "IllegalStateException", 7: "IllegalArgumentException", 8: "IllegalStateException",
+            9: "IllegalStateException", 10: "IllegalStateException", 11: "IllegalStateException"}
+
+    def __init__(self, status: int, msg: str):
+        super().__init__(msg)
+        self.status = status
+        self.code = N.STATUS.get(status, str(status))
+        self.kind = self.KIND.get(status, "RuntimeException")
+
+
+# ---- clocks (org.apache.spark.util.Clock / ManualClock as used by DeltaRetentionSuite) ---------
+class SystemClock:
+    def get_time_millis(self) -> int:
+        return int(time.time() * 1000)
+
+
+class ManualClock:
+    def __init__(self, t: int = 0):
+        self.t = int(t)
+
+    def get_time_millis(self) -> int:
+        return self.t
+
+    def advance(self, ms: int) -> None:
+        self.t += int(ms)
+
+
+# ---- engine (one dr_ctx per thread and device) --------------------------------------------------
+class Engine:
+    _tls = threading.local()
+
+    def __init__(self, device: int = 0):
+        self.lib = N.lib()
+        self.ctx = C.c_void_p()
+        rc = self.lib.dr_ctx_create(device, C.byref(self.ctx))
+        if rc != N.DR_OK:
+            raise DeltaError(rc, "cannot open HIP device %d (libdeltareplay needs an MI355X GPU)" % device)
+        self.device = device
+
+    @classmethod
+    def get(cls, device: int = 0) -> "Engine":
+        d = getattr(cls._tls, "engines", None)
+        if d is None:
+            d = cls._tls.engines = {}
+        if device not in d:
+            d[device] = Engine(device)
+        return d[device]
+
+    def check(self, rc: int) -> None:
+        if rc != N.DR_OK:
+            raise DeltaError(rc, self.lib.dr_last_error(self.ctx).decode("utf-8", "replace"))
+
+    def set_timing(self, on: bool) -> None:
+        self.check(self.lib.dr_set_timing(self.ctx, 1 if on else 0))
+
+    def last_timings(self) -> Dict[str, float]:
+        names = C.create_string_buffer(8192)
+        ms = (C.c_float * 64)()
+        n = C.c_int32()
+        self.check(self.lib.dr_last_timings(self.ctx, names, 8192, ms, 64, C.byref(n)))
+        parts = names.raw.split(b"\0")
+        out: Dict[str, float] = {}
+        for i in range(min(n.value, 64)):
+            k = parts[i].decode()
+            out[k] = out.get(k, 0.0) + float(ms[i])
+        return out
+
+    # staging / replay -------------------------------------------------------------------------
+    def stage_log(self, log_path: str, version: int = -1) -> "Staged":
+        h = C.c_void_p()
+        self.check(self.lib.dr_stage_log(self.ctx, log_path.encode(), int(version), C.byref(h)))
+        return Staged(self, h)
+
+    def stage_files(self, files: Sequence[Tuple[int, int, int, bytes]]) -> "Staged":
+        arr = (N.dr_file * max(len(files), 1))()
+        keep = []
+        for i, (version, kind, part, data) in enumerate(files):
+            buf = C.create_string_buffer(data, len(data))
+            keep.append(buf)
+            arr[i] = N.dr_file(version, kind, part, C.cast(buf, C.c_void_p), len(data))
+        h = C.c_void_p()
+        self.check(self.lib.dr_stage(self.ctx, arr, len(files), C.byref(h)))
+        return Staged(self, h)
+
+    def log_segment(self, log_path: str, version: int = -1):
+        need = C.c_uint64()
+        ver = C.c_int64()
+        self.check(self.lib.dr_log_segment(self.ctx, log_path.encode(), int(version), None, 0,
+                                           C.byref(need), C.byref(ver)))
+        buf = C.create_string_buffer(need.value + 1)
+        self.check(self.lib.dr_log_segment(self.ctx, log_path.encode(), int(version), buf, need.value + 1,
+                                           C.byref(need), C.byref(ver)))
+        files = []
+        for line in buf.value.decode().splitlines():
+            kind, v, part, name = line.split(" ", 3)
+            files.append((int(kind), int(v), int(part), name))
+        return ver.value, files
+
+
+class Staged:
+    def __init__(self, eng: Engine, handle: C.c_void_p):
+        self.eng, self.h = eng, handle
+
+    def bytes(self) -> Tuple[int, int]:
+        j, c = C.c_uint64(), C.c_uint64()
+        self.eng.check(self.eng.lib.dr_staged_bytes(self.h, C.byref(j), C.byref(c)))
+        return j.value, c.value
+
+    def replay(self, min_file_retention_timestamp: int, validate: bool = True) -> "State":
+        st = C.c_void_p()
+        flags = 0 if validate else N.DR_FLAG_NO_VALIDATION
+        self.eng.check(self.eng.lib.dr_replay_staged(self.eng.ctx, self.h, int(min_file_retention_timestamp),
+                                                     flags, C.byref(st)))
+        return State(self.eng, st)
+
+    def release(self) -> None:
+        if self.h:
+            self.eng.lib.dr_staged_release(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:
+            pass
+
+
+def _arr(ptr, n):
+    return [ptr[i] for i in range(n)]
+
+
+class State:
+    """The reconstructed state resident in HBM (the reference's cached `state` Dataset)."""
+
+    def __init__(self, eng: Engine, handle: C.c_void_p):
+        self.eng, self.h = eng, handle
+        c = N.dr_counts()
+        eng.check(eng.lib.dr_state_counts(handle, C.byref(c)))
+        self.counts = {f: getattr(c, f) for f, _ in N.dr_counts._fields_}
+        p = C.c_char_p()
+        n = C.c_uint64()
+        eng.check(eng.lib.dr_state_nonfile_json(handle, C.byref(p), C.byref(n)))
+        text = C.string_at(p, n.value).decode("utf-8") if n.value else ""
+        self.nonfile = [json.loads(l) for l in text.splitlines() if l.strip()]
+
+    def export(self, which: int) -> List[dict]:
+        e = N.dr_export()
+        self.eng.check(self.eng.lib.dr_state_export(self.h, which, C.byref(e)))
+        n = e.n
+        out = []
+        if n == 0:
+            return out
+
+        def strs(off, data, count):
+            o = _arr(off, count + 1)
+            raw = C.string_at(data, o[-1]) if o[-1] else b""
+            return [raw[o[i]:o[i + 1]].decode("utf-8") for i in range(count)]
+
+        paths = strs(e.path_off, e.path_bytes, n)
+        sizes = _arr(e.size, n)
+        stats = strs(e.stats_off, e.stats_bytes, n)
+        stats_null = _arr(e.stats_null, n)
+
+        def maps(entry_off, map_null, koff, kbytes, voff, vbytes, vnull):
+            eo = _arr(entry_off, n + 1)
+            m = eo[-1]
+            ks = strs(koff, kbytes, m) if m else []
+            vs = strs(voff, vbytes, m) if m else []
+            vn = _arr(vnull, m) if m else []
+            nulls = _arr(map_null, n)
+            res = []
+            for i in range(n):
+                if nulls[i]:
+                    res.append(None)
+                    continue
+                res.append({ks[j]: (None if vn[j] else vs[j]) for j in range(eo[i], eo[i + 1])})
+            return res
+
+        pvs = maps(e.pv_entry_off, e.pv_null, e.pv_key_off, e.pv_key_bytes, e.pv_val_off, e.pv_val_bytes,
+                   e.pv_val_null)
+        tags = maps(e.tags_entry_off, e.tags_null, e.tags_key_off, e.tags_key_bytes, e.tags_val_off,
+                    e.tags_val_bytes, e.tags_val_null)
+        if which == N.DR_LIVE:
+            mt = _arr(e.modification_time, n)
+            for i in range(n):
+                out.append({"path": paths[i], "partitionValues": pvs[i], "size": sizes[i],
+                            "modificationTime": mt[i], "dataChange": False,
+                            "stats": None if stats_null[i] else stats[i], "tags": tags[i]})
+        else:
+            dt = _arr(e.deletion_timestamp, n)
+            dv = _arr(e.deletion_timestamp_valid, n)
+            efm = _arr(e.extended_file_metadata, n)
+            for i in range(n):
+                out.append({"path": paths[i], "deletionTimestamp": dt[i] if dv[i] else None,
+                            "dataChange": False, "extendedFileMetadata": bool(efm[i]),
+                            "partitionValues": pvs[i], "size": sizes[i], "tags": tags[i]})
+        return out
+
+    def filter(self, program) -> List[int]:
+        from .predicates import lower_program
+        pred, keep = lower_program(program)
+        sel = C.POINTER(C.c_int64)()
+        n = C.c_int64()
+        self.eng.check(self.eng.lib.dr_filter(self.h, C.byref(pred), C.byref(sel), C.byref(n)))
+        res = [sel[i] for i in range(n.value)]
+        self.eng.lib.dr_free(C.cast(sel, C.c_void_p))
+        return res
+
+    def release(self) -> None:
+        if self.h:
+            self.eng.lib.dr_state_release(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:
+            pass
+
+
+# ---- retention (DeltaConfigs.TOMBSTONE_RETENTION, D/DeltaConfig.scala:325-331) -----------------
+_UNIT_MS = {"millisecond": 1, "milliseconds": 1, "ms": 1, "second": 1000, "seconds": 1000,
+            "minute": 60_000, "minutes": 60_000, "hour": 3_600_000, "hours": 3_600_000,
+            "day": 86_400_000, "days": 86_400_000, "week": 604_800_000, "weeks": 604_800_000,
+            "microsecond": 0.001, "microseconds": 0.001}
+DEFAULT_TOMBSTONE_RETENTION = "interval 1 week"
+
+
+def interval_millis(s: str) -> int:
+    """CalendarInterval -> ms (DeltaConfigs.getMilliSeconds); months/years are rejected."""
+    t = s.strip().lower()
+    if t.startswith("interval"):
+        t = t[len("interval"):].strip()
+    total = 0.0
+    toks = t.split()
+    if not toks or len(toks) % 2:
+        raise ValueError("invalid interval %r" % s)
+    for i in range(0, len(toks), 2):
+        unit = toks[i + 1]
+        if unit not in _UNIT_MS:
+            raise ValueError("unsupported interval unit %r" % unit)
+        total += float(toks[i]) * _UNIT_MS[unit]
+    return int(total)
+
+
+def tombstone_retention_millis(metadata: Optional[dict]) -> int:
+    conf = (metadata or {}).get("configuration") or {}
+    return interval_millis(conf.get("delta.deletedFileRetentionDuration", DEFAULT_TOMBSTONE_RETENTION))
+
+
+# ---- Snapshot / DeltaLog --------------------------------------------------------------------------
+class Snapshot:
+    def __init__(self, delta_log: "DeltaLog", version: int, state: State, min_file_retention_timestamp: int):
+        self.delta_log = delta_log
+        self.version = version
+        self.state = state
+        self.min_file_retention_timestamp = min_file_retention_timestamp
+        c = state.counts
+        self.num_of_files = c["num_files"]
+        self.size_in_bytes = c["size_in_bytes"]
+        self.num_of_removes = c["num_removes"]
+        self.num_of_metadata = c["num_metadata"]
+        self.num_of_protocol = c["num_protocol"]
+        self.num_of_set_transactions = c["num_set_transactions"]
+        self.protocol = next((a["protocol"] for a in state.nonfile if "protocol" in a), None)
+        self.metadata = next((a["metaData"] for a in state.nonfile if "metaData" in a), None)
+        self.set_transactions = [a["txn"] for a in state.nonfile if "txn" in a]
+        self._all = None
+        self._tomb = None
+
+    @property
+    def all_files(self) -> List[dict]:
+        if self._all is None:
+            self._all = self.state.export(N.DR_LIVE)
+        return self._all
+
+    @property
+    def tombstones(self) -> List[dict]:
+        if self._tomb is None:
+            self._tomb = self.state.export(N.DR_TOMBSTONES)
+        return self._tomb
+
+    @property
+    def transactions(self) -> Dict[str, int]:
+        return {t["appId"]: t["version"] for t in self.set_transactions}
+
+    def partition_schema(self) -> Dict[str, str]:
+        from .predicates import partition_schema
+        return partition_schema(self.metadata)
+
+    def files_for_scan(self, filters: Sequence) -> List[dict]:
+        """PartitionFiltering.filesForScan: metadata-only conjuncts, evaluated on the GPU."""
+        from .predicates import split_metadata_and_data_predicates, build_program
+        parts = (self.metadata or {}).get("partitionColumns") or []
+        meta_preds = []
+        for f in filters:
+            meta_preds.extend(split_metadata_and_data_predicates(f, parts)[0])
+        if not meta_preds:
+            return list(self.all_files)
+        prog = build_program(self.partition_schema(), meta_preds)
+        sel = self.state.filter(prog)
+        files = self.all_files
+        return [files[i] for i in sel]
+
+    def release(self) -> None:
+        self.state.release()
+
+
+class DeltaLog:
+    _cache: Dict[Tuple[str, int], "DeltaLog"] = {}
+    _lock = threading.Lock()
+
+    def __init__(self, data_path: str, clock=None, device: int = 0):
+        self.data_path = os.path.abspath(data_path)
+        self.log_path = os.path.join(self.data_path, "_delta_log")
+        self.clock = clock or SystemClock()
+        self.engine = Engine.get(device)
+        self._snapshot: Optional[Snapshot] = None
+        self._lock = threading.RLock()  # deltaLogLock (D/DeltaLog.scala:84)
+        self._snapshot = self._build(-1)
+
+    @classmethod
+    def for_table(cls, data_path: str, clock=None, device: int = 0) -> "DeltaLog":
+        key = (os.path.abspath(data_path), device)
+        with cls._lock:
+            dl = cls._cache.get(key)
+            if dl is None:
+                dl = DeltaLog(data_path, clock, device)
+                cls._cache[key] = dl
+            return dl
+
+    @classmethod
+    def clear_cache(cls) -> None:
+        with cls._lock:
+            for dl in cls._cache.values():
+                if dl._snapshot is not None:
+                    dl._snapshot.release()
+            cls._cache.clear()
+
+    @property
+    def min_file_retention_timestamp(self) -> int:
+        md = self._snapshot.metadata if self._snapshot is not None else None
+        return self.clock.get_time_millis() - tombstone_retention_millis(md)
+
+    def _build(self, version: int) -> Snapshot:
+        if not os.path.isdir(self.log_path):
+            raise DeltaError(3, "No file found in the directory: %s." % self.log_path)
+        cutoff = self.min_file_retention_timestamp
+        staged = self.engine.stage_log(self.log_path, version)
+        try:
+            ver, _ = self.engine.log_segment(self.log_path, version)
+            state = staged.replay(cutoff)
+        finally:
+            staged.release()
+        return Snapshot(self, ver, state, cutoff)
+
+    @property
+    def snapshot(self) -> Snapshot:
+        return self._snapshot
+
+    def update(self) -> Snapshot:
+        with self._lock:
+            new = self._build(-1)
+            old, self._snapshot = self._snapshot, new
+            if old is not None:
+                old.release()  # replaceSnapshot -> uncache (D/SnapshotManagement.scala:333-339)
+            return new
+
+    def get_snapshot_at(self, version: int) -> Snapshot:
+        with self._lock:
+            if self._snapshot is not None and self._snapshot.version == version:
+                return self._snapshot
+            return self._build(version)
+
+
+class InMemoryLogReplay:
+    """D/actions/InMemoryLogReplay.scala:35-77 over the GPU engine: `append` buffers each
+    version's actions (as their JSON encoding), `checkpoint` replays them on the device and
+    returns protocol, metadata, txns, then the live AddFiles and unexpired tombstones sorted by
+    path (dataChange=false)."""
+
+    def __init__(self, min_file_retention_timestamp: int, device: int = 0):
+        self.min_file_retention_timestamp = int(min_file_retention_timestamp)
+        self.engine = Engine.get(device)
+        self.current_version = -1
+        self._files: List[Tuple[int, int, int, bytes]] = []
+
+    def append(self, version: int, actions: Iterable[dict]) -> None:
+        assert self.current_version == -1 or version == self.current_version + 1, (
+            "Attempted to replay version %d, but state is at %d" % (version, self.current_version))
+        self.current_version = version
+        body = "".join(json.dumps(a, separators=(",", ":")) + "\n" for a in actions)
+        self._files.append((version, N.DR_FILE_JSON, 0, body.encode()))
+
+    def checkpoint(self) -> List[Tuple[str, dict]]:
+        staged = self.engine.stage_files(self._files)
+        try:
+            st = staged.replay(self.min_file_retention_timestamp, validate=False)
+        finally:
+            staged.release()
+        try:
+            out: List[Tuple[str, dict]] = []
+            for a in st.nonfile:
+                (k, v), = a.items()
+                out.append((k, v))
+            files = [("add", f) for f in st.export(N.DR_LIVE)] + [("remove", f) for f in st.export(N.DR_TOMBSTONES)]
+            files.sort(key=lambda kv: kv[1]["path"])
+            return out + files
+        finally:
+            st.release()

@@ -1,0 +1,363 @@
+"""Seeded synthetic `_delta_log` generator for the BASELINE.json configs.
+
+Writes newline-delimited JSON commits in the field order Jackson produces for the reference's
+case classes (D/actions/actions.scala:220-320; D/util/JsonUtils.scala:26-31) and Parquet
+checkpoints with the checkpoint column layout of D/Checkpoints.scala:340-389 (v1 data pages,
+dictionary encoding, SNAPPY) written by pyarrow.
+
+Every table also gets its expected result *by construction* (which file ids are live, which
+tombstones survive the cutoff, the aggregate counts): a size-independent check that does not
+need any replay at all.
+
+File identity: file id `i` has path
+  p0=<date>/p1=<int>[/p2=<word>/p3=<bool>]/part-<5 digits>-<uuid>-c000.snappy.parquet
+(~88 bytes, URI-safe, relative).
+"""
+from __future__ import annotations
+
+import json
+import os
+import uuid as _uuid
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import numpy as np
+
+BASE_SEED = 0xDE17A
+T0 = 1_700_000_000_000  # modificationTime base (ms)
+DAY_MS = 86_400_000
+WORDS = ["w%d" % i for i in range(64)]
+PART_COLS = ["p0", "p1", "p2", "p3"]
+PART_TYPES = {"p0": "date", "p1": "integer", "p2": "string", "p3": "boolean"}
+HIVE_NULL = "__HIVE_DEFAULT_PARTITION__"
+
+
+@dataclass
+class Expected:
+    version: int
+    min_file_retention_timestamp: int
+    num_files: int
+    size_in_bytes: int
+    num_removes: int
+    num_actions: int           # SURVEY §8d unit of work: non-blank JSON lines + checkpoint rows
+    num_file_actions: int
+    live_ids: Optional[np.ndarray] = None
+    tomb_ids: Optional[np.ndarray] = None
+
+
+class FilePool:
+    """Vectorized description of every file id the generator ever mints."""
+
+    def __init__(self, rng: np.random.Generator, n: int, ncols: int):
+        self.ncols = ncols
+        self.p0 = rng.integers(0, 365, n, dtype=np.int32)             # days after 2020-01-01
+        self.p1 = rng.integers(0, 1000, n, dtype=np.int32)
+        self.p2 = rng.integers(0, 64, n, dtype=np.int32)
+        self.p2null = rng.random(n) < 0.01
+        self.p3 = rng.integers(0, 2, n, dtype=np.int8)
+        self.part = rng.integers(0, 100000, n, dtype=np.int32)
+        self.uuid = rng.integers(0, 2 ** 63, (n, 2), dtype=np.int64)
+        self.size = np.exp(rng.uniform(np.log(1024), np.log(256 * 2 ** 20), n)).astype(np.int64)
+        self.nrec = rng.integers(1, 1_000_000, n, dtype=np.int64)
+        self.minv = rng.integers(0, 1000, n, dtype=np.int64)
+        self._dates = [str(np.datetime64("2020-01-01") + np.timedelta64(int(d), "D")) for d in range(365)]
+
+    def grow(self, rng, n):
+        other = FilePool(rng, n, self.ncols)
+        for k in ("p0", "p1", "p2", "p2null", "p3", "part", "uuid", "size", "nrec", "minv"):
+            setattr(self, k, np.concatenate([getattr(self, k), getattr(other, k)]))
+
+    def __len__(self):
+        return len(self.p0)
+
+    # -- per-file strings ------------------------------------------------------------------
+    def pvals(self, i) -> Dict[str, Optional[str]]:
+        d = {"p0": self._dates[self.p0[i]], "p1": str(int(self.p1[i]))}
+        if self.ncols >= 4:
+            d["p2"] = None if self.p2null[i] else WORDS[self.p2[i]]
+            d["p3"] = "true" if self.p3[i] else "false"
+        return d
+
+    def path(self, i) -> str:
+        u = _uuid.UUID(int=(int(self.uuid[i, 0]) << 64) | int(self.uuid[i, 1]))
+        d = "p0=%s/p1=%d" % (self._dates[self.p0[i]], self.p1[i])
+        if self.ncols >= 4:
+            d += "/p2=%s/p3=%s" % (HIVE_NULL if self.p2null[i] else WORDS[self.p2[i]],
+                                   "true" if self.p3[i] else "false")
+        return "%s/part-%05d-%s-c000.snappy.parquet" % (d, self.part[i], u)
+
+    def stats(self, i) -> str:
+        return ('{"numRecords":%d,"minValues":{"id":%d},"maxValues":{"id":%d},"nullCount":{"id":0}}'
+                % (self.nrec[i], self.minv[i], self.minv[i] + self.nrec[i]))
+
+
+def _esc(s: str) -> str:
+    return json.dumps(s)
+
+
+def _pv_json(pv: Dict[str, Optional[str]]) -> str:
+    return "{" + ",".join('"%s":%s' % (k, "null" if v is None else _esc(v)) for k, v in pv.items()) + "}"
+
+
+def add_line(pool: FilePool, i: int, mtime: int) -> str:
+    return ('{"add":{"path":%s,"partitionValues":%s,"size":%d,"modificationTime":%d,'
+            '"dataChange":true,"stats":%s}}' % (_esc(pool.path(i)), _pv_json(pool.pvals(i)),
+                                                pool.size[i], mtime, _esc(pool.stats(i))))
+
+
+def remove_line(pool: FilePool, i: int, del_ts: int) -> str:
+    return ('{"remove":{"path":%s,"deletionTimestamp":%d,"dataChange":true,'
+            '"extendedFileMetadata":true,"partitionValues":%s,"size":%d}}'
+            % (_esc(pool.path(i)), del_ts, _pv_json(pool.pvals(i)), pool.size[i]))
+
+
+def protocol_line() -> str:
+    return '{"protocol":{"minReaderVersion":1,"minWriterVersion":2}}'
+
+
+def schema_string(ncols: int) -> str:
+    fields = [{"name": "id", "type": "long", "nullable": True, "metadata": {}}]
+    for c in PART_COLS[:ncols]:
+        fields.append({"name": c, "type": PART_TYPES[c], "nullable": True, "metadata": {}})
+    return json.dumps({"type": "struct", "fields": fields}, separators=(",", ":"))
+
+
+def metadata_dict(ncols: int) -> dict:
+    return {"id": "00000000-0000-4000-8000-00000000de17", "format": {"provider": "parquet", "options": {}},
+            "schemaString": schema_string(ncols), "partitionColumns": PART_COLS[:ncols],
+            "configuration": {}, "createdTime": T0}
+
+
+def metadata_line(ncols: int) -> str:
+    return json.dumps({"metaData": metadata_dict(ncols)}, separators=(",", ":"))
+
+
+def commit_info_line(version: int, op: str = "WRITE") -> str:
+    return ('{"commitInfo":{"timestamp":%d,"operation":"%s","operationParameters":{"mode":"Append",'
+            '"partitionBy":"[]"},"readVersion":%d,"isBlindAppend":false}}'
+            % (T0 + version * 60000, op, max(version - 1, 0)))
+
+
+def delta_name(v: int) -> str:
+    return "%020d.json" % v
+
+
+# ----------------------------------------------------------------------------------------------
+# Checkpoint writer (pyarrow) -- exact checkpoint layout (D/Checkpoints.scala:354-389)
+# ----------------------------------------------------------------------------------------------
+def _map_type():
+    import pyarrow as pa
+    return pa.map_(pa.string(), pa.string())
+
+
+def write_checkpoint(path: str, pool: FilePool, add_ids: np.ndarray, ncols: int, version: int,
+                     with_parsed: bool = False, row_group_size: int = 1 << 20,
+                     data_page_size: int = 1 << 20) -> int:
+    """Rows: protocol, metaData, then one `add` per id. Returns the row count."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+
+    n = len(add_ids)
+    nrows = n + 2
+    mt = _map_type()
+    # --- add ---
+    paths = [pool.path(i) for i in add_ids]
+    keys, vals, offs = [], [], [0]
+    for i in add_ids:
+        pv = pool.pvals(i)
+        keys.extend(pv.keys())
+        vals.extend(pv.values())
+        offs.append(len(keys))
+    # two leading null rows (protocol, metaData)
+    add_valid = np.concatenate([[False, False], np.ones(n, bool)])
+    pad = [None, None]
+    pv_off = np.array([0, 0] + offs, dtype=np.int32)
+    pv_arr = pa.MapArray.from_arrays(pa.array(pv_off), pa.array(keys, pa.string()),
+                                     pa.array(vals, pa.string()))
+    add_fields = [
+        pa.array(pad + paths, pa.string()),
+        pv_arr,
+        pa.array(np.concatenate([[0, 0], pool.size[add_ids]]), pa.int64()),
+        pa.array(np.concatenate([[0, 0], T0 + version * 60000 + np.arange(n, dtype=np.int64) % 60000]),
+                 pa.int64()),
+        pa.array(np.zeros(nrows, bool)),
+        pa.array([None] * nrows, mt),
+        pa.array(pad + [pool.stats(i) for i in add_ids], pa.string()),
+    ]
+    add_names = ["path", "partitionValues", "size", "modificationTime", "dataChange", "tags", "stats"]
+    add_types = [pa.string(), mt, pa.int64(), pa.int64(), pa.bool_(), mt, pa.string()]
+    if with_parsed and ncols:
+        from datetime import date, timedelta
+        parsed_arrays, parsed_fields = [], []
+        for c in PART_COLS[:ncols]:
+            if c == "p0":
+                arr = pa.array(np.concatenate([[0, 0], pool.p0[add_ids] + 18262]).astype(np.int32), pa.date32())
+            elif c == "p1":
+                arr = pa.array(np.concatenate([[0, 0], pool.p1[add_ids]]).astype(np.int32), pa.int32())
+            elif c == "p2":
+                arr = pa.array(pad + [None if pool.p2null[i] else WORDS[pool.p2[i]] for i in add_ids], pa.string())
+            else:
+                arr = pa.array(np.concatenate([[0, 0], pool.p3[add_ids]]).astype(bool), pa.bool_())
+            parsed_arrays.append(arr)
+            parsed_fields.append(pa.field(c, arr.type))
+        add_fields.append(pa.StructArray.from_arrays(parsed_arrays, fields=parsed_fields))
+        add_names.append("partitionValues_parsed")
+        add_types.append(pa.struct(parsed_fields))
+    add_struct = pa.StructArray.from_arrays(
+        add_fields, fields=[pa.field(nm, t) for nm, t in zip(add_names, add_types)],
+        mask=pa.array(~add_valid))
+    # --- remove (all null) ---
+    rm_type = pa.struct([("path", pa.string()), ("deletionTimestamp", pa.int64()),
+                         ("dataChange", pa.bool_()), ("extendedFileMetadata", pa.bool_()),
+                         ("partitionValues", mt), ("size", pa.int64()), ("tags", mt)])
+    rm_struct = pa.nulls(nrows, rm_type)
+    txn_type = pa.struct([("appId", pa.string()), ("version", pa.int64()), ("lastUpdated", pa.int64())])
+    txn_struct = pa.nulls(nrows, txn_type)
+    # --- metaData / protocol ---
+    md = metadata_dict(ncols)
+    fmt_type = pa.struct([("provider", pa.string()), ("options", mt)])
+    md_type = pa.struct([("id", pa.string()), ("name", pa.string()), ("description", pa.string()),
+                         ("format", fmt_type), ("schemaString", pa.string()),
+                         ("partitionColumns", pa.list_(pa.string())), ("configuration", mt),
+                         ("createdTime", pa.int64())])
+    md_rows = [None, {"id": md["id"], "name": None, "description": None,
+                      "format": {"provider": "parquet", "options": []},
+                      "schemaString": md["schemaString"], "partitionColumns": md["partitionColumns"],
+                      "configuration": [], "createdTime": md["createdTime"]}]
+    md_struct = pa.concat_arrays([pa.array(md_rows, md_type), pa.nulls(n, md_type)])
+    prot_type = pa.struct([("minReaderVersion", pa.int32()), ("minWriterVersion", pa.int32())])
+    prot_struct = pa.concat_arrays([pa.array([{"minReaderVersion": 1, "minWriterVersion": 2}], prot_type),
+                                    pa.nulls(n + 1, prot_type)])
+    table = pa.Table.from_arrays([txn_struct, add_struct, rm_struct, md_struct, prot_struct],
+                                 names=["txn", "add", "remove", "metaData", "protocol"])
+    pq.write_table(table, path, compression="snappy", use_dictionary=True, version="1.0",
+                   data_page_version="1.0", row_group_size=row_group_size,
+                   data_page_size=data_page_size, write_statistics=False)
+    return nrows
+
+
+# ----------------------------------------------------------------------------------------------
+# Config builders
+# ----------------------------------------------------------------------------------------------
+@dataclass
+class ChurnSpec:
+    ckpt_files: int            # live files in the checkpoint (0 = no checkpoint)
+    ckpt_version: int
+    n_deltas: int
+    removes_per_delta: int
+    adds_per_delta: int
+    readd_frac: float          # fraction of adds that re-add earlier-removed paths
+    ncols: int = 2
+    n_at_cutoff: int = 0       # removes placed exactly at the cutoff (must be dropped)
+    init_adds: int = 0         # no-checkpoint mode: adds in v0 (with protocol+metadata)
+
+
+def build_table(table_dir: str, spec: ChurnSpec, seed: int, checkpoint_with_parsed=False,
+                data_page_size: int = 1 << 20, keep_ids: bool = True) -> Expected:
+    rng = np.random.default_rng(seed)
+    log = os.path.join(table_dir, "_delta_log")
+    os.makedirs(log, exist_ok=True)
+    total_new = spec.ckpt_files + spec.init_adds + spec.n_deltas * spec.adds_per_delta
+    pool = FilePool(rng, max(total_new, 1), spec.ncols)
+    # per file id: last action kind (0 none, 1 add, 2 remove), delTs
+    state = np.zeros(len(pool), np.int8)
+    delts = np.zeros(len(pool), np.int64)
+    next_id = 0
+    n_actions = 0
+    n_file_actions = 0
+    window0 = T0 + 30 * DAY_MS           # deletionTimestamp window [window0, window0 + 14 days)
+    cutoff = window0 + 7 * DAY_MS
+    version = 0
+    if spec.ckpt_files:
+        version = spec.ckpt_version
+        ids = np.arange(spec.ckpt_files)
+        next_id = spec.ckpt_files
+        state[ids] = 1
+        nrows = write_checkpoint(os.path.join(log, "%020d.checkpoint.parquet" % version), pool, ids,
+                                 spec.ncols, version, with_parsed=checkpoint_with_parsed,
+                                 data_page_size=data_page_size)
+        n_actions += nrows
+        n_file_actions += spec.ckpt_files
+        with open(os.path.join(log, "_last_checkpoint"), "w") as f:
+            f.write('{"version":%d,"size":%d}\n' % (version, nrows))
+        # a stale earlier commit before the checkpoint, as real logs have (not replayed)
+        with open(os.path.join(log, delta_name(version)), "w") as f:
+            f.write(commit_info_line(version) + "\n")
+    else:
+        lines = [commit_info_line(0), protocol_line(), metadata_line(spec.ncols)]
+        ids = np.arange(spec.init_adds)
+        next_id = spec.init_adds
+        state[ids] = 1
+        lines += [add_line(pool, i, T0 + j) for j, i in enumerate(ids)]
+        with open(os.path.join(log, delta_name(0)), "w") as f:
+            f.write("\n".join(lines) + "\n")
+        n_actions += len(lines)
+        n_file_actions += len(ids)
+    removed_pool: List[int] = []
+    at_cutoff_left = spec.n_at_cutoff
+    for d in range(spec.n_deltas):
+        version += 1
+        live = np.flatnonzero(state == 1)
+        rm_ids = rng.choice(live, size=min(spec.removes_per_delta, len(live)), replace=False)
+        ts = rng.integers(window0, window0 + 14 * DAY_MS, len(rm_ids), dtype=np.int64)
+        if at_cutoff_left:
+            k = min(at_cutoff_left, len(ts))
+            ts[:k] = cutoff
+            at_cutoff_left -= k
+        n_readd = int(spec.adds_per_delta * spec.readd_frac) if removed_pool else 0
+        n_readd = min(n_readd, len(removed_pool))
+        if n_readd:
+            pick = rng.choice(len(removed_pool), size=n_readd, replace=False)
+            readd = np.asarray(removed_pool)[pick]
+            keep = np.ones(len(removed_pool), bool)
+            keep[pick] = False
+            removed_pool = list(np.asarray(removed_pool)[keep])
+        else:
+            readd = np.zeros(0, np.int64)
+        n_new = spec.adds_per_delta - n_readd
+        new = np.arange(next_id, next_id + n_new)
+        next_id += n_new
+        add_ids = np.concatenate([readd, new]).astype(np.int64)
+        lines = [commit_info_line(version, "OPTIMIZE" if spec.removes_per_delta else "WRITE")]
+        lines += [remove_line(pool, i, t) for i, t in zip(rm_ids, ts)]
+        mt0 = T0 + version * 60000
+        lines += [add_line(pool, i, mt0 + j) for j, i in enumerate(add_ids)]
+        with open(os.path.join(log, delta_name(version)), "w") as f:
+            f.write("\n".join(lines) + "\n")
+        state[rm_ids] = 2
+        delts[rm_ids] = ts
+        state[add_ids] = 1
+        removed_pool.extend(int(x) for x in rm_ids)
+        n_actions += len(lines)
+        n_file_actions += len(rm_ids) + len(add_ids)
+    live_ids = np.flatnonzero(state == 1)
+    tomb_ids = np.flatnonzero((state == 2) & (delts > cutoff))
+    return Expected(version=version, min_file_retention_timestamp=cutoff,
+                    num_files=len(live_ids), size_in_bytes=int(pool.size[live_ids].sum()),
+                    num_removes=len(tomb_ids), num_actions=n_actions, num_file_actions=n_file_actions,
+                    live_ids=live_ids if keep_ids else None, tomb_ids=tomb_ids if keep_ids else None)
+
+
+def config_spec(config: int, scale: float = 1.0) -> ChurnSpec:
+    """BASELINE.json configs; `scale` shrinks file counts for tests."""
+    s = lambda x: max(1, int(round(x * scale)))
+    if config == 1:
+        return ChurnSpec(ckpt_files=0, ckpt_version=0, n_deltas=99, removes_per_delta=0,
+                         adds_per_delta=s(100), readd_frac=0.0, ncols=2, init_adds=s(100))
+    if config == 2:
+        return ChurnSpec(ckpt_files=s(1_000_000), ckpt_version=100, n_deltas=10,
+                         removes_per_delta=s(5000), adds_per_delta=s(5000), readd_frac=0.0, ncols=2)
+    if config == 3:
+        return ChurnSpec(ckpt_files=s(10_000_000), ckpt_version=1000, n_deltas=30,
+                         removes_per_delta=s(100_000), adds_per_delta=s(100_000), readd_frac=0.5,
+                         ncols=2, n_at_cutoff=min(1000, s(1000)))
+    if config == 4:
+        return ChurnSpec(ckpt_files=s(100_000_000), ckpt_version=1000, n_deltas=0,
+                         removes_per_delta=0, adds_per_delta=0, readd_frac=0.0, ncols=4)
+    raise ValueError(config)
+
+
+def build_config(config: int, table_dir: str, scale: float = 1.0, seed: Optional[int] = None,
+                 **kw) -> Expected:
+    seed = BASE_SEED + config if seed is None else seed
+    return build_table(table_dir, config_spec(config, scale), seed, **kw)

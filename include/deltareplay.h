@@ -1,0 +1,202 @@
+/*
+ * deltareplay.h -- C ABI of the MI355X-native Delta Lake snapshot state reconstruction.
+ *
+ * The reference has no FFI on this path; the seam is cut where a JNI shim
+ * replaces the body of Snapshot.stateReconstruction / InMemoryLogReplay and
+ * DeltaLog.filterFileList. Every entry point below names the reference interface it replaces
+ * (paths relative to the reference checkout, D/ = core/src/main/scala/org/apache/spark/sql/delta/).
+ *
+ * Conventions: plain pointers and sizes only; every call returns an int status (DR_OK = 0) and
+ * leaves a message in dr_last_error(ctx). One dr_ctx per host thread / HIP stream; calls on
+ * distinct contexts are thread-safe. The library owns every device and host buffer it returns
+ * until the matching *_release call (Snapshot.uncache, D/util/StateCache.scala:104-109).
+ */
+#ifndef DELTAREPLAY_H
+#define DELTAREPLAY_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DR_ABI_VERSION 1
+
+/* Status codes. The JNI shim rethrows the reference's exception class with dr_last_error():
+ *   DR_E_EMPTY_DIR / DR_E_LOG_TRUNCATED / DR_E_MISSING_PART -> FileNotFoundException
+ *     (D/DeltaErrors.scala:451-457,915-917,543-546)
+ *   DR_E_NONCONTIGUOUS / DR_E_MISSING_PROTOCOL / DR_E_MISSING_METADATA -> IllegalStateException
+ *     (D/DeltaErrors.scala:548-551,553-560)
+ *   DR_E_BAD_SEGMENT -> IllegalArgumentException (require(...) in D/SnapshotManagement.scala:124-131) */
+enum dr_status {
+  DR_OK = 0,
+  DR_E_INVALID_ARG = 1,
+  DR_E_IO = 2,
+  DR_E_EMPTY_DIR = 3,
+  DR_E_LOG_TRUNCATED = 4,
+  DR_E_MISSING_PART = 5,
+  DR_E_NONCONTIGUOUS = 6,
+  DR_E_BAD_SEGMENT = 7,
+  DR_E_MISSING_PROTOCOL = 8,
+  DR_E_MISSING_METADATA = 9,
+  DR_E_PARSE = 10,
+  DR_E_PARQUET = 11,
+  DR_E_UNSUPPORTED = 12,
+  DR_E_OOM = 13,
+  DR_E_DEVICE = 14,
+  DR_E_INTERNAL = 15
+};
+
+/* Segment file kinds (D/DeltaLogFileIndex.scala:67-68). */
+enum dr_file_kind { DR_FILE_JSON = 0, DR_FILE_CHECKPOINT = 1 };
+
+/* One LogSegment file (D/SnapshotManagement.scala:394-416). Bytes are borrowed for the call. */
+typedef struct dr_file {
+  int64_t version;     /* commit version, or the checkpoint version for checkpoint parts */
+  int32_t kind;        /* dr_file_kind */
+  int32_t part;        /* 1-based checkpoint part (0 for JSON / single-part) */
+  const uint8_t* data; /* file bytes (host memory) */
+  uint64_t len;
+} dr_file;
+
+/* computedState counters (D/Snapshot.scala:140-151). */
+typedef struct dr_counts {
+  int64_t num_files;              /* count(add) */
+  int64_t size_in_bytes;          /* coalesce(sum(add.size), 0) */
+  int64_t num_removes;            /* count(remove): unexpired tombstones */
+  int64_t num_metadata;
+  int64_t num_protocol;
+  int64_t num_set_transactions;
+  int64_t num_actions;            /* actions replayed (JSON lines + checkpoint rows) */
+  int64_t num_file_actions;       /* add + remove actions replayed */
+  int64_t version;                /* snapshot version */
+  int64_t malformed_lines;        /* JSON lines Spark's PERMISSIVE reader would null out */
+  uint64_t live_key_sum;          /* sum (mod 2^64) of xxh64(path key) over allFiles */
+  uint64_t tomb_key_sum;          /* same over tombstones: order-free checksum for parity */
+} dr_counts;
+
+/* Replay flags. */
+#define DR_FLAG_NO_VALIDATION 0x1u  /* stateReconstructionValidation.enabled=false (D/sources/DeltaSQLConf.scala:86-91) */
+
+/* Export columns of one side of the state (allFiles or tombstones; D/Snapshot.scala:193-204).
+ * Strings: `*_off` has n+1 entries into `*_bytes`. Maps (partitionValues, tags): `*_entry_off`
+ * has n+1 entries into the entry arrays; map_null[i] != 0 means the map itself is null.
+ * All buffers are owned by the state and valid until dr_state_release. */
+typedef struct dr_export {
+  int64_t n;
+  const int64_t* path_off;   const uint8_t* path_bytes;
+  const int64_t* size;
+  const int64_t* modification_time;     /* adds */
+  const int64_t* deletion_timestamp;    /* removes; valid where deletion_timestamp_valid[i] */
+  const uint8_t* deletion_timestamp_valid;
+  const uint8_t* extended_file_metadata;/* removes */
+  const int64_t* stats_off;  const uint8_t* stats_bytes; const uint8_t* stats_null;
+  const int64_t* pv_entry_off; const uint8_t* pv_null;
+  const int64_t* pv_key_off; const uint8_t* pv_key_bytes;
+  const int64_t* pv_val_off; const uint8_t* pv_val_bytes; const uint8_t* pv_val_null;
+  const int64_t* tags_entry_off; const uint8_t* tags_null;
+  const int64_t* tags_key_off; const uint8_t* tags_key_bytes;
+  const int64_t* tags_val_off; const uint8_t* tags_val_bytes; const uint8_t* tags_val_null;
+} dr_export;
+
+enum dr_which { DR_LIVE = 0, DR_TOMBSTONES = 1 };
+
+typedef struct dr_ctx dr_ctx;
+typedef struct dr_state dr_state;
+typedef struct dr_staged dr_staged;
+
+/* ---- context ------------------------------------------------------------------------------ */
+/* Creates a context bound to HIP device `device` with its own stream. */
+int dr_ctx_create(int device, dr_ctx** out);
+void dr_ctx_destroy(dr_ctx* ctx);
+const char* dr_last_error(const dr_ctx* ctx);
+int dr_abi_version(void);
+
+/* ---- log segment (host) -------------------------------------------------------------------
+ * Replaces SnapshotManagement.getLogSegmentForVersion + Checkpoints.lastCheckpoint
+ * (D/SnapshotManagement.scala:82-179,365-372; D/Checkpoints.scala:148-218).
+ * Lists `log_path` (a _delta_log directory) with POSIX I/O. version_to_load < 0 = latest.
+ * Writes the segment as a newline-separated list "<kind> <version> <part> <file name>" into
+ * `buf` (NUL-terminated; *needed gets the size). */
+int dr_log_segment(dr_ctx* ctx, const char* log_path, int64_t version_to_load,
+                   char* buf, uint64_t buf_len, uint64_t* needed, int64_t* version_out);
+
+/* ---- staging (host -> HBM) ----------------------------------------------------------------
+ * Copies the segment's file bytes into HBM and plans the Parquet page decode (footer + page
+ * headers, host). The staged input is reusable across dr_replay_staged calls. */
+int dr_stage(dr_ctx* ctx, const dr_file* files, int32_t nfiles, dr_staged** out);
+/* Lists + reads the latest (or version_to_load) segment of `log_path` and stages it. */
+int dr_stage_log(dr_ctx* ctx, const char* log_path, int64_t version_to_load, dr_staged** out);
+int dr_staged_release(dr_staged* staged);
+/* Bytes staged in HBM (JSON + checkpoint). */
+int dr_staged_bytes(const dr_staged* staged, uint64_t* json_bytes, uint64_t* checkpoint_bytes);
+
+/* ---- replay (device) ----------------------------------------------------------------------
+ * Replaces Snapshot.stateReconstruction (D/Snapshot.scala:88-111) and the per-partition
+ * InMemoryLogReplay.append/checkpoint (D/actions/InMemoryLogReplay.scala:43-77): parse,
+ * canonicalize, hash, partition+sort, last-writer-wins, tombstone retention
+ * (delTimestamp > min_file_retention_timestamp), compaction, computedState counters.
+ * The result stays resident in HBM. */
+int dr_replay_staged(dr_ctx* ctx, const dr_staged* staged, int64_t min_file_retention_timestamp,
+                     uint32_t flags, dr_state** out);
+/* dr_stage + dr_replay_staged + dr_staged_release. */
+int dr_replay(dr_ctx* ctx, const dr_file* files, int32_t nfiles,
+              int64_t min_file_retention_timestamp, uint32_t flags, dr_state** out);
+int dr_state_release(dr_state* state);
+
+/* ---- results ------------------------------------------------------------------------------ */
+int dr_state_counts(dr_state* state, dr_counts* out);
+/* Latest protocol / metaData and the set transactions as JSON text in the reference's action
+ * encoding ({"protocol":{...}} etc., one per line; D/actions/actions.scala:71). */
+int dr_state_nonfile_json(dr_state* state, const char** json, uint64_t* len);
+/* Materialises allFiles (DR_LIVE) or tombstones (DR_TOMBSTONES) on the host, dataChange=false. */
+int dr_state_export(dr_state* state, int32_t which, dr_export* out);
+
+/* ---- partition pruning (device) -----------------------------------------------------------
+ * Replaces DeltaLog.filterFileList + rewritePartitionFilters (D/DeltaLog.scala:500-547) for
+ * PartitionFiltering.filesForScan (D/PartitionFiltering.scala:27-42): the metadata-only
+ * conjuncts, lowered by the shim to the postfix program below, are evaluated over the live
+ * AddFiles with Spark's non-ANSI Cast(string AS type) and three-valued logic.
+ *
+ * Program: `ops[nops]` (dr_pred_op). Columns are indices into `col_names` / `col_types`
+ * (the partitionSchema; names are the exact map keys). Literals are indices into `lit_*`:
+ * lit_types[k] (dr_pred_type), integer/date/boolean literals in lit_i64[k], strings as
+ * lit_str_off[k]..lit_str_off[k+1] into lit_str_bytes; lit_null[k] marks a NULL literal.
+ * The program must leave one boolean on the stack; rows where it is TRUE are selected.
+ * Output: selected live-file ordinals (indices into the DR_LIVE export order). */
+enum dr_pred_type { DR_T_STRING = 0, DR_T_BYTE = 1, DR_T_SHORT = 2, DR_T_INT = 3, DR_T_LONG = 4,
+                    DR_T_DATE = 5, DR_T_BOOLEAN = 6 };
+enum dr_pred_opcode {
+  DR_OP_COL = 0,      /* arg = column index: push Cast(partitionValues[col] AS type) */
+  DR_OP_LIT = 1,      /* arg = literal index */
+  DR_OP_EQ = 2, DR_OP_NE = 3, DR_OP_LT = 4, DR_OP_LE = 5, DR_OP_GT = 6, DR_OP_GE = 7,
+  DR_OP_NSEQ = 8,     /* <=> */
+  DR_OP_IN = 9,       /* arg = number of literals pushed after the value */
+  DR_OP_ISNULL = 10, DR_OP_ISNOTNULL = 11,
+  DR_OP_AND = 12, DR_OP_OR = 13, DR_OP_NOT = 14
+};
+typedef struct dr_pred_op { int32_t opcode; int32_t arg; } dr_pred_op;
+
+typedef struct dr_predicate {
+  int32_t nops; const dr_pred_op* ops;
+  int32_t ncols; const char* const* col_names; const int32_t* col_types;
+  int32_t nlits; const int32_t* lit_types; const int64_t* lit_i64; const uint8_t* lit_null;
+  const int64_t* lit_str_off; const uint8_t* lit_str_bytes;
+} dr_predicate;
+
+int dr_filter(dr_state* state, const dr_predicate* pred, int64_t** selected, int64_t* nselected);
+void dr_free(void* p);
+
+/* ---- measurement hooks (bench.py) ----------------------------------------------------------
+ * Per-stage device time of the last dr_replay_staged on this context (HIP events on the
+ * context's stream), in milliseconds; names are returned NUL-separated. */
+int dr_last_timings(dr_ctx* ctx, char* names, uint64_t names_len, float* ms, int32_t cap,
+                    int32_t* n);
+/* Enable/disable per-stage event timing (off by default; small overhead when on). */
+int dr_set_timing(dr_ctx* ctx, int32_t on);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DELTAREPLAY_H */

@@ -1,0 +1,204 @@
+"""Headline benchmark: Delta snapshot state reconstruction on MI355X (BASELINE.json metric).
+
+One step = one full device replay of the config-3 LogSegment (10M-file checkpoint + 30 JSON
+commits with 30% remove/re-add churn and a tombstone-retention cutoff) whose bytes are already
+resident in HBM: JSON tokenization (K1), checkpoint page inflate + decode (K2), path hashing and
+partition (K3), per-bucket last-writer-wins + retention + compaction + computedState counters
+(K4/K6). `value` = log actions replayed per second over all ranks.
+
+Multi-GPU (torchrun, one rank per GPU): each rank replays its own shard (an independent table of
+the same shape, seed + rank): weak scaling, no data-path collective.
+
+cpu_baseline: the C++ restatement of the reference replay (oracle/replay_oracle.cpp, 50 hash
+partitions x unordered_map last-writer-wins, all host threads) timed on a bounded sample of the
+same workload on rank 0 at N=1.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def build_table(path, config, scale, seed):
+    from delta_amd.testing import synth as S
+    marker = os.path.join(path, "expected.json")
+    if os.path.exists(marker):
+        with open(marker) as f:
+            return json.load(f)
+    t = time.time()
+    exp = S.build_config(config, path, scale=scale, seed=seed, keep_ids=False)
+    d = {k: getattr(exp, k) for k in ("version", "min_file_retention_timestamp", "num_files", "size_in_bytes",
+                                      "num_removes", "num_actions", "num_file_actions", "json_bytes",
+                                      "checkpoint_bytes")}
+    with open(marker, "w") as f:
+        json.dump(d, f)
+    log("generated config %d scale %g in %.1fs: %s" % (config, scale, time.time() - t, d))
+    return d
+
+
+def algorithmic_bytes(stage, plan, counts):
+    """Compulsory HBM bytes per launch of each stage's kernel."""
+    n_lines = counts["num_actions"] - plan["checkpoint_rows"]
+    rows = plan["checkpoint_rows"]
+    fa = counts["num_file_actions"]
+    surv = counts["num_files"] + counts["num_removes"]
+    return {
+        "json_index": plan["json_bytes"],
+        "json_newlines": plan["json_bytes"] + 8 * n_lines,
+        "json_parse": plan["json_bytes"] + 8 * n_lines + 50 * n_lines,
+        "pq_inflate": plan["pages_compressed_bytes"] + plan["pages_decompressed_bytes"],
+        "pq_decode": plan["pages_decompressed_bytes"] + 44 * rows,
+        "ckpt_assemble": 44 * rows + 88 * rows + 50 * rows,
+        "partition_hist": 10 * (rows + n_lines),
+        "partition_scatter": 18 * (rows + n_lines) + 12 * fa,
+        "reduce": 12 * fa + 8 * counts["num_files"] + 4 * surv,
+        "compact": 8 * surv,
+    }.get(stage)
+
+
+def cpu_baseline(config, sample_scale, seed, tmp):
+    """Times oracle/_build/replay_oracle on a bounded sample of the same workload."""
+    exe = os.path.join(ROOT, "oracle", "_build", "replay_oracle")
+    if not os.path.exists(exe):
+        return None
+    path = os.path.join(tmp, "cpu_sample_c%d_%g" % (config, sample_scale))
+    exp = build_table(path, config, sample_scale, seed)
+    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    threads = min(threads, 64)
+    r = subprocess.run([exe, os.path.join(path, "_delta_log"), str(exp["min_file_retention_timestamp"]),
+                        "--threads", str(threads), "--partitions", "50"],
+                       capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        log("cpu baseline failed:", r.stderr[-2000:])
+        return None
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    ok = (res["num_files"] == exp["num_files"] and res["num_removes"] == exp["num_removes"]
+          and res["size_in_bytes"] == exp["size_in_bytes"])
+    if not ok:
+        log("cpu baseline result mismatch", res, exp)
+    return {"value": res["num_actions"] / res["total_s"], "unit": "actions/s", "cores": threads,
+            "kind": "port",
+            "sample": "config %d at scale %g (%d actions: %d checkpoint rows + JSON commits), parse %.2fs + "
+                      "replay %.2fs; C++ restatement of InMemoryLogReplay over 50 hash partitions"
+                      % (config, sample_scale, res["num_actions"], res["checkpoint_rows"], res["parse_s"],
+                         res["replay_s"]),
+            "matches_expected": ok}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--cpu-sample-scale", type=float, default=0.1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workdir", default=os.environ.get("DR_BENCH_DIR", os.path.join(tempfile.gettempdir(), "dr_bench")))
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from delta_amd.delta_log import Engine
+    from delta_amd.testing import synth as S
+
+    seed = S.BASE_SEED + args.config + 1000 * rank
+    table = os.path.join(args.workdir, "c%d_s%g_r%d" % (args.config, args.scale, rank))
+    exp = build_table(table, args.config, args.scale, seed)
+    eng = Engine.get(local)
+    staged = eng.stage_log(os.path.join(table, "_delta_log"))
+    plan = staged.plan()
+    cutoff = exp["min_file_retention_timestamp"]
+    counts = None
+    for i in range(args.warmup):
+        st = staged.replay(cutoff)
+        counts = st.counts
+        st.release()
+    if counts is None:
+        st = staged.replay(cutoff)
+        counts = st.counts
+        st.release()
+    for k in ("num_files", "num_removes", "size_in_bytes", "num_actions", "num_file_actions"):
+        assert counts[k] == exp[k], (k, counts[k], exp[k])
+    eng.set_timing(True)
+    stage_ms = {}
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        st = staged.replay(cutoff)
+        for k, v in eng.last_timings().items():
+            stage_ms[k] = stage_ms.get(k, 0.0) + v
+        st.release()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    eng.set_timing(False)
+    stage_ms = {k: v / args.steps for k, v in stage_ms.items()}
+    total_actions = counts["num_actions"] * args.steps * world
+    value = total_actions / elapsed
+    ms_per_step = elapsed / args.steps * 1000.0
+    if rank != 0:
+        return
+    dom = max(stage_ms, key=stage_ms.get)
+    kernels = {}
+    for k, ms in stage_ms.items():
+        b = algorithmic_bytes(k, plan, counts)
+        kernels[k] = {"ms": round(ms, 4)}
+        if b:
+            kernels[k]["algo_bytes"] = b
+            kernels[k]["gbs"] = round(b / (ms * 1e-3) / 1e9, 1)
+    db = algorithmic_bytes(dom, plan, counts) or 0
+    achieved = db / (stage_ms[dom] * 1e-3) / 1e9 if db else None
+    roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1) if achieved else None,
+                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None, "traffic": None}
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline(args.config, args.cpu_sample_scale, S.BASE_SEED + args.config, args.workdir)
+    out = {
+        "metric": "log actions replayed/sec + achieved HBM GB/s, 1/2/4/8 GPU, 10M-file table",
+        "value": round(value, 1), "unit": "actions/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8/int64", "data": "synthetic",
+        "config": {"workload": "config %d: %d-file checkpoint + JSON commits, %d actions/rank, "
+                               "30%% remove/re-add churn, retention cutoff" % (args.config, plan["checkpoint_rows"] - 2,
+                                                                             counts["num_actions"]),
+                   "scale": args.scale, "actions_per_rank": counts["num_actions"],
+                   "json_bytes": plan["json_bytes"], "checkpoint_bytes": plan["checkpoint_bytes"],
+                   "parallelism": "dp%d (independent table shard per rank)" % world},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "kernels": kernels,
+        "result": {k: counts[k] for k in ("num_files", "num_removes", "size_in_bytes")},
+    }
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -25,7 +25,8 @@ DR_FLAG_NO_VALIDATION = 0x1
 # Exported symbols (checked by tests/test_native_abi.py against include/deltareplay.h).
 SYMBOLS = [
     "dr_abi_version", "dr_ctx_create", "dr_ctx_destroy", "dr_last_error", "dr_log_segment",
-    "dr_stage", "dr_stage_log", "dr_staged_release", "dr_staged_bytes", "dr_replay_staged",
+    "dr_stage", "dr_stage_log", "dr_staged_release", "dr_staged_bytes", "dr_staged_plan",
+    "dr_replay_staged",
     "dr_replay", "dr_state_release", "dr_state_counts", "dr_state_nonfile_json",
     "dr_state_export", "dr_filter", "dr_free", "dr_last_timings", "dr_set_timing",
 ]
@@ -92,6 +93,7 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "dr_stage_log": ([vp, C.c_char_p, i64, C.POINTER(vp)], C.c_int),
         "dr_staged_release": ([vp], C.c_int),
         "dr_staged_bytes": ([vp, C.POINTER(u64), C.POINTER(u64)], C.c_int),
+        "dr_staged_plan": ([vp, C.POINTER(u64), i32, C.POINTER(i32)], C.c_int),
         "dr_replay_staged": ([vp, vp, i64, C.c_uint32, C.POINTER(vp)], C.c_int),
         "dr_replay": ([vp, C.POINTER(dr_file), i32, i64, C.c_uint32, C.POINTER(vp)], C.c_int),
         "dr_state_release": ([vp], C.c_int),

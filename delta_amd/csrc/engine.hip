@@ -1059,6 +1059,19 @@ int dr_staged_bytes(const dr_staged* staged, uint64_t* json_bytes, uint64_t* che
   return DR_OK;
 }
 
+int dr_staged_plan(const dr_staged* staged, uint64_t* out, int32_t cap, int32_t* n) {
+  if (!staged || !out || !n) return DR_E_INVALID_ARG;
+  const StagedData& s = *staged->d;
+  uint64_t ck = 0, cs = 0, us = 0;
+  for (auto& p : s.parts) ck += p.len;
+  for (auto& p : s.pages) { cs += p.csize; us += p.usize; }
+  const uint64_t v[7] = {s.h_json.size(), ck, s.ck_rows, s.pages.size(), cs, us, s.dict_entries};
+  int32_t k = 0;
+  for (; k < cap && k < 7; ++k) out[k] = v[k];
+  *n = k;
+  return DR_OK;
+}
+
 int dr_replay_staged(dr_ctx* ctx, const dr_staged* staged, int64_t cutoff, uint32_t flags, dr_state** out) {
   if (!ctx || !staged || !out) return DR_E_INVALID_ARG;
   *out = nullptr;

@@ -138,6 +138,14 @@ class Staged:
         self.eng.check(self.eng.lib.dr_staged_bytes(self.h, C.byref(j), C.byref(c)))
         return j.value, c.value
 
+    def plan(self) -> Dict[str, int]:
+        out = (C.c_uint64 * 8)()
+        n = C.c_int32()
+        self.eng.check(self.eng.lib.dr_staged_plan(self.h, out, 8, C.byref(n)))
+        names = ["json_bytes", "checkpoint_bytes", "checkpoint_rows", "pages", "pages_compressed_bytes",
+                 "pages_decompressed_bytes", "dict_entries"]
+        return {names[i]: int(out[i]) for i in range(n.value)}
+
     def replay(self, min_file_retention_timestamp: int, validate: bool = True) -> "State":
         st = C.c_void_p()
         flags = 0 if validate else N.DR_FLAG_NO_VALIDATION

@@ -131,6 +131,10 @@ int dr_stage_log(dr_ctx* ctx, const char* log_path, int64_t version_to_load, dr_
 int dr_staged_release(dr_staged* staged);
 /* Bytes staged in HBM (JSON + checkpoint). */
 int dr_staged_bytes(const dr_staged* staged, uint64_t* json_bytes, uint64_t* checkpoint_bytes);
+/* Decode plan figures (for roofline accounting): out[0] JSON bytes, [1] checkpoint bytes,
+ * [2] checkpoint rows, [3] planned pages, [4] their compressed bytes, [5] their decompressed bytes,
+ * [6] dictionary entries. *n receives the number of figures written (<= cap). */
+int dr_staged_plan(const dr_staged* staged, uint64_t* out, int32_t cap, int32_t* n);
 
 /* ---- replay (device) ----------------------------------------------------------------------
  * Replaces Snapshot.stateReconstruction (D/Snapshot.scala:88-111) and the per-partition

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -185,6 +186,15 @@ struct StagedData {
   int max_def[HC_N] = {0, 0, 0, 0};
   int add_def = 1, rm_def = 1;
   std::vector<NonFileAction> ck_nonfile;  // protocol/metaData/txn rows of the checkpoint
+  // SNAPPY plan + persistent scratch
+  std::vector<SnapPage> snap_pages;
+  std::vector<uint32_t> chunk_base, block_page;
+  std::vector<CopyJob> copy_jobs;
+  uint32_t nchunks = 0;
+  DBuf<SnapPage> d_snap;
+  DBuf<uint32_t> d_chunk_base, d_block_page;
+  DBuf<CopyJob> d_copy;
+  DBuf<uint32_t> s_spec_exit, s_vis, s_entry, s_chunk_out, s_chunk_out_start, s_block_in, s_pages_bad;
 };
 
 struct dr_staged {
@@ -450,7 +460,54 @@ static void plan_checkpoint(StagedData& s) {
     }
   }
   s.dict_entries = dict_pool;
-  s.d_arena = DBuf<uint8_t>(s.ctx, arena + 64);
+  // SNAPPY plan: preamble, speculation chunks and 64 KiB output blocks per page (k_snappy.hip)
+  for (const PageDesc& d : s.pages) {
+    const uint64_t lv = d.kind == PG_DATA_V2 ? uint64_t(d.v2_def_len + d.v2_rep_len) : 0;
+    if (lv) s.copy_jobs.push_back(CopyJob{d.src, d.dst, lv});
+    const bool compressed = d.codec == 1 && !(d.kind == PG_DATA_V2 && !d.v2_compressed);
+    if (!compressed) {
+      s.copy_jobs.push_back(CopyJob{d.src + lv, d.dst + lv, d.usize - lv});
+      continue;
+    }
+    const uint8_t* h = s.h_pq.data() + d.src + lv;
+    uint64_t total = 0;
+    uint32_t pre = 0;
+    for (int sh = 0; pre < 5 && pre < d.csize - lv; sh += 7) {
+      const uint8_t b = h[pre++];
+      total |= uint64_t(b & 0x7f) << sh;
+      if (!(b & 0x80)) break;
+    }
+    if (total != d.usize - lv) fail(DR_E_PARQUET, "snappy preamble does not match the page size");
+    SnapPage sp{d.src + lv + pre, d.dst + lv, uint32_t(d.csize - lv - pre), uint32_t(d.usize - lv),
+                uint32_t(s.block_page.size())};
+    s.chunk_base.push_back(s.nchunks);
+    s.nchunks += (sp.n_in + 255) / 256;
+    const uint32_t nb = (sp.n_out + 65535) / 65536;
+    for (uint32_t k = 0; k < nb; ++k) s.block_page.push_back(uint32_t(s.snap_pages.size()));
+    s.snap_pages.push_back(sp);
+  }
+  s.chunk_base.push_back(s.nchunks);
+  s.d_arena = DBuf<uint8_t>(s.ctx, arena + 4096);
+  const uint64_t pqb = reinterpret_cast<uint64_t>(s.d_pq.p), arb = reinterpret_cast<uint64_t>(s.d_arena.p);
+  for (SnapPage& sp : s.snap_pages) { sp.in += pqb; sp.out += arb; }
+  for (CopyJob& j : s.copy_jobs) { j.src += pqb; j.dst += arb; }
+  auto up = [&](auto& dbuf, auto& vec) {
+    using T = typename std::decay_t<decltype(vec)>::value_type;
+    dbuf = DBuf<T>(s.ctx, vec.size());
+    if (!vec.empty())
+      HIP_OK(hipMemcpyAsync(dbuf.p, vec.data(), vec.size() * sizeof(T), hipMemcpyHostToDevice, s.ctx->stream));
+  };
+  up(s.d_snap, s.snap_pages);
+  up(s.d_chunk_base, s.chunk_base);
+  up(s.d_block_page, s.block_page);
+  up(s.d_copy, s.copy_jobs);
+  s.s_spec_exit = DBuf<uint32_t>(s.ctx, s.nchunks);
+  s.s_vis = DBuf<uint32_t>(s.ctx, uint64_t(s.nchunks) * 8);
+  s.s_entry = DBuf<uint32_t>(s.ctx, s.nchunks);
+  s.s_chunk_out = DBuf<uint32_t>(s.ctx, s.nchunks);
+  s.s_chunk_out_start = DBuf<uint32_t>(s.ctx, s.nchunks);
+  s.s_block_in = DBuf<uint32_t>(s.ctx, s.block_page.size());
+  s.s_pages_bad = DBuf<uint32_t>(s.ctx, s.snap_pages.size());
   for (PageDesc& d : s.pages) {
     d.src = reinterpret_cast<uint64_t>(s.d_pq.p) + d.src;
     d.dst = reinterpret_cast<uint64_t>(s.d_arena.p) + d.dst;
@@ -623,7 +680,14 @@ static dr_state* replay(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, int6
     pa.dict_ptr = dict_ptr.p;
     pa.dict_len = dict_len.p;
     pa.error = pq_err.p;
-    launch_pq_inflate(pa, stream);
+    launch_page_copy(s.d_copy.p, uint32_t(s.copy_jobs.size()), stream);
+    if (!s.snap_pages.empty()) {
+      s.s_pages_bad.zero(stream);
+      SnappyArgs sa{s.d_snap.p, uint32_t(s.snap_pages.size()), s.d_chunk_base.p, s.nchunks, s.s_spec_exit.p,
+                    s.s_vis.p, s.s_entry.p, s.s_chunk_out.p, s.s_chunk_out_start.p, s.s_block_in.p,
+                    s.d_block_page.p, uint32_t(s.block_page.size()), s.s_pages_bad.p, pq_err.p};
+      launch_snappy(sa, stream);
+    }
     ctx->mark("pq_inflate");
     launch_pq_dict(pa, stream);
     launch_pq_data(pa, stream);

@@ -1,10 +1,14 @@
-// K2: Parquet checkpoint decode on the GPU (replaces Spark's ParquetFileFormat / parquet-mr record
+// K2b: Parquet page decode on the GPU (replaces Spark's ParquetFileFormat / parquet-mr record
 // assembly over the checkpoint, D/DeltaLogFileIndex.scala:68, D/Snapshot.scala:244-263).
 //
-// Pages are planned on the host (footer + page headers); the device inflates SNAPPY pages into an
-// arena, decodes dictionary pages into a pool, then decodes v1/v2 data pages of the flat
-// file-action columns (add.path, add.size, remove.path, remove.deletionTimestamp): RLE/bit-packed
-// definition levels, PLAIN and PLAIN_DICTIONARY/RLE_DICTIONARY values.
+// Pages are planned on the host (footer + page headers) and inflated by k_snappy.hip. Then one
+// wave per page decodes:
+//  * dictionary pages -> a pool of (address, length) or int64 values;
+//  * v1/v2 data pages of the flat file-action columns (add.path, add.size, remove.path,
+//    remove.deletionTimestamp): RLE/bit-packed definition levels expanded run-by-run by the whole
+//    wave into LDS, value ranks by ballot prefix counts, values from PLAIN (fixed width, or
+//    length-prefixed byte arrays walked through a 1 KiB register window with readlane) or
+//    PLAIN_DICTIONARY/RLE_DICTIONARY indices.
 #include "dev_common.h"
 #include "kernels.h"
 
@@ -15,246 +19,279 @@ enum PqErr : uint32_t { PQE_SNAPPY = 1, PQE_LEVELS = 2, PQE_VALUES = 3, PQE_DICT
 
 __device__ __forceinline__ void set_err(uint32_t* e, uint32_t code) { atomicCAS(e, 0u, code); }
 
-// ---- SNAPPY (one lane per page) ------------------------------------------------------------------
-__device__ bool snappy_page(const uint8_t* in, uint32_t n, uint8_t* out, uint32_t out_len) {
-  uint32_t ip = 0;
-  uint64_t total = 0;
-  for (int s = 0; ip < n && s < 35; s += 7) {
-    uint8_t b = in[ip++];
-    total |= uint64_t(b & 0x7f) << s;
-    if (!(b & 0x80)) break;
-  }
-  if (total != out_len) return false;
-  uint32_t op = 0;
-  while (ip < n) {
-    const uint8_t tag = in[ip++];
-    const uint32_t t = tag & 3;
-    uint32_t len, off = 0;
-    if (t == 0) {
-      len = tag >> 2;
-      if (len >= 60) {
-        const uint32_t nb = len - 59;
-        if (ip + nb > n) return false;
-        len = 0;
-        for (uint32_t b = 0; b < nb; ++b) len |= uint32_t(in[ip + b]) << (8 * b);
-        ip += nb;
-      }
-      len += 1;
-      if (ip + len > n || op + len > out_len) return false;
-      for (uint32_t k = 0; k < len; ++k) out[op + k] = in[ip + k];
-      ip += len;
-      op += len;
-      continue;
-    }
-    if (t == 1) {
-      if (ip + 1 > n) return false;
-      len = ((tag >> 2) & 7) + 4;
-      off = (uint32_t(tag >> 5) << 8) | in[ip];
-      ip += 1;
-    } else if (t == 2) {
-      if (ip + 2 > n) return false;
-      len = (tag >> 2) + 1;
-      off = uint32_t(in[ip]) | (uint32_t(in[ip + 1]) << 8);
-      ip += 2;
-    } else {
-      if (ip + 4 > n) return false;
-      len = (tag >> 2) + 1;
-      off = uint32_t(in[ip]) | (uint32_t(in[ip + 1]) << 8) | (uint32_t(in[ip + 2]) << 16) |
-            (uint32_t(in[ip + 3]) << 24);
-      ip += 4;
-    }
-    if (off == 0 || off > op || op + len > out_len) return false;
-    for (uint32_t k = 0; k < len; ++k) out[op + k] = out[op - off + k];
-    op += len;
-  }
-  return op == out_len;
-}
-
-__global__ void k_pq_inflate(ParquetArgs a) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.npages) return;
-  const PageDesc& pg = a.pages[i];
-  const uint8_t* src = reinterpret_cast<const uint8_t*>(pg.src);
-  uint8_t* dst = reinterpret_cast<uint8_t*>(pg.dst);
-  uint32_t lv = pg.kind == PG_DATA_V2 ? uint32_t(pg.v2_def_len + pg.v2_rep_len) : 0u;
-  for (uint32_t k = 0; k < lv; ++k) dst[k] = src[k];
-  const bool compressed = pg.codec == 1 && !(pg.kind == PG_DATA_V2 && !pg.v2_compressed);
-  if (compressed) {
-    if (!snappy_page(src + lv, pg.csize - lv, dst + lv, pg.usize - lv)) set_err(a.error, PQE_SNAPPY);
-  } else {
-    for (uint32_t k = lv; k < pg.usize; ++k) dst[k] = src[k];
-  }
-}
-
-// ---- RLE / bit-packed hybrid decoder -------------------------------------------------------------
-struct Rle {
-  const uint8_t* p;
-  const uint8_t* end;
-  int width;
-  uint32_t run_left;   // values left in the current run
-  bool packed;
-  uint32_t value;      // RLE value
-  uint64_t acc;        // bit-packed accumulator
-  int have;
-  bool bad;
-
-  __device__ void init(const uint8_t* b, const uint8_t* e, int w) {
-    p = b; end = e; width = w; run_left = 0; packed = false; value = 0; acc = 0; have = 0; bad = false;
-  }
-  __device__ bool next_run() {
-    uint64_t h = 0;
-    int s = 0;
-    for (;;) {
-      if (p >= end) { bad = true; return false; }
-      uint8_t b = *p++;
-      h |= uint64_t(b & 0x7f) << s;
-      s += 7;
-      if (!(b & 0x80)) break;
-      if (s > 63) { bad = true; return false; }
-    }
-    if (h & 1) {
-      packed = true;
-      run_left = uint32_t(h >> 1) * 8;
-      acc = 0;
-      have = 0;
-    } else {
-      packed = false;
-      run_left = uint32_t(h >> 1);
-      value = 0;
-      for (int b = 0; b < (width + 7) / 8; ++b) {
-        if (p >= end) { bad = true; return false; }
-        value |= uint32_t(*p++) << (8 * b);
-      }
-    }
-    return true;
-  }
-  __device__ uint32_t get() {
-    while (run_left == 0) {
-      if (!next_run()) return 0;
-    }
-    --run_left;
-    if (!packed) return value;
-    while (have < width) {
-      acc |= uint64_t(p < end ? *p : 0) << have;
-      ++p;
-      have += 8;
-    }
-    uint32_t v = width ? uint32_t(acc & ((1ull << width) - 1)) : 0;
-    acc >>= width;
-    have -= width;
-    return v;
-  }
-};
-
 __device__ __forceinline__ int level_width(int max_level) {
   int w = 0;
   while ((1 << w) <= max_level) ++w;
   return max_level == 0 ? 0 : w;
 }
 
-__global__ void k_pq_dict(ParquetArgs a) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+// ---- wave-wide RLE / bit-packed hybrid expansion ---------------------------------------------------
+// All lanes hold the same (uniform) state; each call expands the next n values into dst[0..n).
+struct Rle {
+  const uint8_t* p;
+  const uint8_t* end;
+  int width;
+  uint32_t left;
+  bool packed;
+  uint32_t value;
+  const uint8_t* pk;   // packed-run data
+  uint64_t bit;        // bit offset into pk
+  bool bad;
+
+  __device__ void init(const uint8_t* b, const uint8_t* e, int w) {
+    p = b; end = e; width = w; left = 0; packed = false; value = 0; pk = nullptr; bit = 0; bad = false;
+  }
+  __device__ bool next_run() {
+    uint64_t h = 0;
+    int s = 0;
+    for (;;) {
+      if (p >= end || s > 35) { bad = true; return false; }
+      const uint8_t b = *p++;
+      h |= uint64_t(b & 0x7f) << s;
+      s += 7;
+      if (!(b & 0x80)) break;
+    }
+    if (h & 1) {
+      packed = true;
+      left = uint32_t(h >> 1) * 8;
+      pk = p;
+      bit = 0;
+      const uint64_t bytes = (uint64_t(left) * uint64_t(width) + 7) / 8;
+      p += bytes;  // may run past `end` for a final short group: values beyond are never read
+    } else {
+      packed = false;
+      left = uint32_t(h >> 1);
+      value = 0;
+      for (int b = 0; b < (width + 7) / 8; ++b) {
+        if (p >= end) { bad = true; return false; }
+        value |= uint32_t(*p++) << (8 * b);
+      }
+    }
+    if (left == 0 && !packed) return next_run();
+    return true;
+  }
+  template <typename T>
+  __device__ void expand(T* dst, uint32_t n, int lane) {
+    uint32_t done = 0;
+    while (done < n) {
+      if (left == 0 && !next_run()) return;
+      const uint32_t take = min(left, n - done);
+      if (!packed) {
+        for (uint32_t i = lane; i < take; i += 64) dst[done + i] = T(value);
+      } else {
+        const uint64_t mask = width >= 32 ? 0xffffffffull : ((1ull << width) - 1);
+        for (uint32_t i = lane; i < take; i += 64) {
+          const uint64_t b = bit + uint64_t(i) * width;
+          dst[done + i] = T((load_u64(pk + (b >> 3)) >> (b & 7)) & mask);
+        }
+        bit += uint64_t(take) * width;
+      }
+      left -= take;
+      done += take;
+    }
+  }
+};
+
+// ---- length-prefixed BYTE_ARRAY walker over a 1 KiB register window ---------------------------------
+// Lane l holds bytes [wb + 16 l, wb + 16 l + 16). The walk position is wave-uniform; dwords are read
+// with readlane, so one step costs a handful of scalar-latency instructions, not an LDS/L2 round trip.
+struct ByteArrayWalker {
+  const uint8_t* base;   // page values start (any alignment)
+  const uint8_t* end;
+  const uint8_t* wb;     // window base (16-byte aligned)
+  uint4 w;
+  uint64_t pos;          // offset of the next value's length prefix from `base`
+  bool bad;
+
+  __device__ void load_window(const uint8_t* at, int lane) {
+    wb = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(at) & ~uintptr_t(15));
+    w = *reinterpret_cast<const uint4*>(wb + 16 * lane);
+  }
+  __device__ __forceinline__ uint32_t dword(uint32_t di) {
+    const uint32_t which = di & 3;
+    const uint32_t v = which == 0 ? w.x : which == 1 ? w.y : which == 2 ? w.z : w.w;
+    return uint32_t(__builtin_amdgcn_readlane(int(v), int(di >> 2)));
+  }
+  __device__ void init(const uint8_t* b, const uint8_t* e, int lane) {
+    base = b; end = e; pos = 0; bad = false;
+    load_window(b, lane);
+  }
+  // Next value: returns its address and length; wave-uniform.
+  __device__ __forceinline__ const uint8_t* next(uint32_t* len, int lane) {
+    const uint8_t* at = base + pos;
+    if (at + 4 > end) { bad = true; *len = 0; return at; }
+    uint32_t r = uint32_t(at - wb);
+    if (r + 8 > 1024) {
+      load_window(at, lane);
+      r = uint32_t(at - wb);
+    }
+    const uint32_t di = r >> 2;
+    const uint32_t l = __builtin_amdgcn_alignbyte(dword(di + 1), dword(di), r & 3);
+    if (uint64_t(end - at - 4) < l) { bad = true; *len = 0; return at; }
+    *len = l;
+    pos += 4 + uint64_t(l);
+    return at + 4;
+  }
+};
+
+// ---- dictionary pages --------------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_pq_dict(ParquetArgs a) {
+  const uint32_t i = blockIdx.x;
   if (i >= a.npages) return;
   const PageDesc& pg = a.pages[i];
   if (pg.kind != PG_DICT) return;
+  const int lane = threadIdx.x;
   const uint8_t* p = reinterpret_cast<const uint8_t*>(pg.dst);
   const uint8_t* end = p + pg.usize;
-  for (uint32_t k = 0; k < pg.num_values; ++k) {
-    if (pg.phys == 6) {  // BYTE_ARRAY
-      if (end - p < 4) { set_err(a.error, PQE_DICT); return; }
-      uint32_t l = load_u32(p);
-      p += 4;
-      if (uint64_t(end - p) < l) { set_err(a.error, PQE_DICT); return; }
-      a.dict_ptr[pg.dict_base + k] = reinterpret_cast<uint64_t>(p);
-      a.dict_len[pg.dict_base + k] = l;
-      p += l;
-    } else if (pg.phys == 2) {
-      if (end - p < 8) { set_err(a.error, PQE_DICT); return; }
-      a.dict_ptr[pg.dict_base + k] = load_u64(p);
-      p += 8;
-    } else if (pg.phys == 1) {
-      if (end - p < 4) { set_err(a.error, PQE_DICT); return; }
-      a.dict_ptr[pg.dict_base + k] = uint64_t(int64_t(int32_t(load_u32(p))));
-      p += 4;
-    } else {
-      set_err(a.error, PQE_ENCODING);
-      return;
+  if (pg.phys == 6) {  // BYTE_ARRAY: chain walk
+    __shared__ uint64_t sp[64];
+    __shared__ uint32_t sl[64];
+    ByteArrayWalker wk;
+    wk.init(p, end, lane);
+    for (uint32_t k0 = 0; k0 < pg.num_values; k0 += 64) {
+      const uint32_t cnt = min(64u, pg.num_values - k0);
+      for (uint32_t k = 0; k < cnt; ++k) {
+        uint32_t l;
+        const uint8_t* v = wk.next(&l, lane);
+        if (lane == 0) { sp[k] = reinterpret_cast<uint64_t>(v); sl[k] = l; }
+      }
+      if (wk.bad) { if (lane == 0) set_err(a.error, PQE_DICT); return; }
+      __syncthreads();
+      if (uint32_t(lane) < cnt) {
+        a.dict_ptr[pg.dict_base + k0 + lane] = sp[lane];
+        a.dict_len[pg.dict_base + k0 + lane] = sl[lane];
+      }
+      __syncthreads();
     }
+    return;
+  }
+  const uint32_t width = pg.phys == 2 ? 8 : pg.phys == 1 ? 4 : 0;
+  if (!width) { if (lane == 0) set_err(a.error, PQE_ENCODING); return; }
+  if (uint64_t(pg.num_values) * width > pg.usize) { if (lane == 0) set_err(a.error, PQE_DICT); return; }
+  for (uint32_t k = lane; k < pg.num_values; k += 64) {
+    a.dict_ptr[pg.dict_base + k] = width == 8 ? load_u64(p + 8ull * k)
+                                              : uint64_t(int64_t(int32_t(load_u32(p + 4ull * k))));
   }
 }
 
-__global__ void k_pq_data(ParquetArgs a) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.npages) return;
-  const PageDesc& pg = a.pages[i];
+// ---- data pages ----------------------------------------------------------------------------------------
+constexpr uint32_t SEG = 1024;   // levels per segment
+
+__global__ void __launch_bounds__(64) k_pq_data(ParquetArgs a) {
+  const uint32_t pi = blockIdx.x;
+  if (pi >= a.npages) return;
+  const PageDesc& pg = a.pages[pi];
   if (pg.kind == PG_DICT) return;
-  const FlatColumn& col = a.cols[pg.col];
+  __shared__ uint8_t defs[SEG];
+  __shared__ uint32_t idxs[SEG];
+  __shared__ uint64_t vptr[SEG];
+  __shared__ uint32_t vlen[SEG];
+  const int lane = threadIdx.x;
+  const FlatColumn col = a.cols[pg.col];
   const uint8_t* p = reinterpret_cast<const uint8_t*>(pg.dst);
   const uint8_t* end = p + pg.usize;
-  const int dw = level_width(pg.max_def);
-  Rle defs;
+  Rle defr;
+  defr.init(p, p, 0);
   if (pg.kind == PG_DATA_V2) {
-    defs.init(p + pg.v2_rep_len, p + pg.v2_rep_len + pg.v2_def_len, dw);
+    defr.init(p + pg.v2_rep_len, p + pg.v2_rep_len + pg.v2_def_len, level_width(pg.max_def));
     p += pg.v2_rep_len + pg.v2_def_len;
   } else if (pg.max_def > 0) {
-    if (end - p < 4) { set_err(a.error, PQE_LEVELS); return; }
-    uint32_t l = load_u32(p);
+    if (end - p < 4) { if (lane == 0) set_err(a.error, PQE_LEVELS); return; }
+    const uint32_t l = load_u32(p);
     p += 4;
-    if (uint64_t(end - p) < l) { set_err(a.error, PQE_LEVELS); return; }
-    defs.init(p, p + l, dw);
+    if (uint64_t(end - p) < l) { if (lane == 0) set_err(a.error, PQE_LEVELS); return; }
+    defr.init(p, p + l, level_width(pg.max_def));
     p += l;
   }
   const bool dict = pg.encoding == 2 || pg.encoding == 8;
-  Rle idx;
+  const bool rle_bool = pg.encoding == 3 && pg.phys == 0;
+  Rle ir;
+  ir.init(p, p, 0);
   if (dict) {
-    if (pg.dict < 0) { set_err(a.error, PQE_DICT); return; }
-    int w = p < end ? *p : 0;
-    idx.init(p + 1, end, w);
+    if (pg.dict < 0) { if (lane == 0) set_err(a.error, PQE_DICT); return; }
+    const int w = p < end ? *p : 0;
+    ir.init(p + 1, end, w);
+  } else if (rle_bool) {
+    ir.init(p + 4, end, 1);
   } else if (pg.encoding != 0) {
-    set_err(a.error, PQE_ENCODING);
+    if (lane == 0) set_err(a.error, PQE_ENCODING);
     return;
   }
   const uint32_t dict_base = dict ? a.pages[pg.dict].dict_base : 0;
   const uint32_t dict_n = dict ? a.pages[pg.dict].num_values : 0;
-  uint32_t bool_bit = 0;
-  for (uint32_t k = 0; k < pg.num_values; ++k) {
-    const uint64_t row = pg.row_base + k;
-    int d = pg.max_def > 0 ? int(defs.get()) : 0;
-    if (defs.bad && pg.max_def > 0) { set_err(a.error, PQE_LEVELS); return; }
-    col.def[row] = uint8_t(d);
-    if (d != pg.max_def) continue;
-    if (dict) {
-      uint32_t j = idx.get();
-      if (idx.bad || j >= dict_n) { set_err(a.error, PQE_DICT); return; }
-      if (pg.phys == 6) {
-        col.sptr[row] = a.dict_ptr[dict_base + j];
-        col.slen[row] = a.dict_len[dict_base + j];
-      } else {
-        col.ival[row] = int64_t(a.dict_ptr[dict_base + j]);
-      }
-    } else if (pg.phys == 6) {
-      if (end - p < 4) { set_err(a.error, PQE_VALUES); return; }
-      uint32_t l = load_u32(p);
-      p += 4;
-      if (uint64_t(end - p) < l) { set_err(a.error, PQE_VALUES); return; }
-      col.sptr[row] = reinterpret_cast<uint64_t>(p);
-      col.slen[row] = l;
-      p += l;
-    } else if (pg.phys == 2) {
-      if (end - p < 8) { set_err(a.error, PQE_VALUES); return; }
-      col.ival[row] = int64_t(load_u64(p));
-      p += 8;
-    } else if (pg.phys == 1) {
-      if (end - p < 4) { set_err(a.error, PQE_VALUES); return; }
-      col.ival[row] = int64_t(int32_t(load_u32(p)));
-      p += 4;
-    } else if (pg.phys == 0) {
-      col.ival[row] = (p[bool_bit >> 3] >> (bool_bit & 7)) & 1;
-      ++bool_bit;
+  const uint32_t width = pg.phys == 2 ? 8 : pg.phys == 1 ? 4 : 0;
+  ByteArrayWalker wk;
+  if (pg.phys == 6 && !dict) wk.init(p, end, lane);
+  uint64_t vbase = 0;  // values consumed before this segment (PLAIN fixed / boolean)
+  for (uint32_t s0 = 0; s0 < pg.num_values; s0 += SEG) {
+    const uint32_t n = min(SEG, pg.num_values - s0);
+    if (pg.max_def > 0) {
+      defr.expand(defs, n, lane);
+      if (defr.bad) { if (lane == 0) set_err(a.error, PQE_LEVELS); return; }
     } else {
-      set_err(a.error, PQE_ENCODING);
+      for (uint32_t i = lane; i < n; i += 64) defs[i] = 0;
+    }
+    __syncthreads();
+    // value rank of each level within the segment
+    uint32_t nv = 0;
+    for (uint32_t b = 0; b < n; b += 64) {
+      const uint32_t i = b + lane;
+      const bool isv = i < n && int(defs[i]) == pg.max_def;
+      const unsigned long long m = __ballot(isv);
+      if (isv) idxs[i] = nv + uint32_t(__popcll(m & ((1ull << lane) - 1ull)));
+      nv += uint32_t(__popcll(m));
+    }
+    // values of this segment
+    if (dict || rle_bool) {
+      ir.expand(vlen, nv, lane);  // dictionary indices / booleans (reuse vlen as scratch)
+      if (ir.bad) { if (lane == 0) set_err(a.error, dict ? PQE_DICT : PQE_VALUES); return; }
+    } else if (pg.phys == 6) {
+      for (uint32_t k = 0; k < nv; ++k) {
+        uint32_t l;
+        const uint8_t* v = wk.next(&l, lane);
+        if (lane == 0) { vptr[k] = reinterpret_cast<uint64_t>(v); vlen[k] = l; }
+      }
+      if (wk.bad) { if (lane == 0) set_err(a.error, PQE_VALUES); return; }
+    } else if (width) {
+      if ((vbase + nv) * width > uint64_t(end - p)) { if (lane == 0) set_err(a.error, PQE_VALUES); return; }
+    } else if (pg.phys == 0) {
+      if ((vbase + nv + 7) / 8 > uint64_t(end - p)) { if (lane == 0) set_err(a.error, PQE_VALUES); return; }
+    } else {
+      if (lane == 0) set_err(a.error, PQE_ENCODING);
       return;
     }
+    __syncthreads();
+    for (uint32_t i = lane; i < n; i += 64) {
+      const uint64_t row = pg.row_base + s0 + i;
+      const uint8_t d = defs[i];
+      col.def[row] = d;
+      if (int(d) != pg.max_def) continue;
+      const uint32_t k = idxs[i];
+      if (dict) {
+        const uint32_t j = vlen[k];
+        if (j >= dict_n) { set_err(a.error, PQE_DICT); continue; }
+        if (pg.phys == 6) {
+          col.sptr[row] = a.dict_ptr[dict_base + j];
+          col.slen[row] = a.dict_len[dict_base + j];
+        } else {
+          col.ival[row] = int64_t(a.dict_ptr[dict_base + j]);
+        }
+      } else if (rle_bool) {
+        col.ival[row] = vlen[k] & 1;
+      } else if (pg.phys == 6) {
+        col.sptr[row] = vptr[k];
+        col.slen[row] = vlen[k];
+      } else if (width == 8) {
+        col.ival[row] = int64_t(load_u64(p + 8 * (vbase + k)));
+      } else if (width == 4) {
+        col.ival[row] = int64_t(int32_t(load_u32(p + 4 * (vbase + k))));
+      } else {
+        const uint64_t b = vbase + k;
+        col.ival[row] = (p[b >> 3] >> (b & 7)) & 1;
+      }
+    }
+    vbase += nv;
+    __syncthreads();
   }
 }
 
@@ -315,14 +352,11 @@ __global__ void k_ckpt_assemble(CkptAssembleArgs a) {
 
 }  // namespace dev
 
-void launch_pq_inflate(const ParquetArgs& a, hipStream_t st) {
-  if (a.npages) hipLaunchKernelGGL(dev::k_pq_inflate, dim3((a.npages + 63) / 64), dim3(64), 0, st, a);
-}
 void launch_pq_dict(const ParquetArgs& a, hipStream_t st) {
-  if (a.npages) hipLaunchKernelGGL(dev::k_pq_dict, dim3((a.npages + 63) / 64), dim3(64), 0, st, a);
+  if (a.npages) hipLaunchKernelGGL(dev::k_pq_dict, dim3(a.npages), dim3(64), 0, st, a);
 }
 void launch_pq_data(const ParquetArgs& a, hipStream_t st) {
-  if (a.npages) hipLaunchKernelGGL(dev::k_pq_data, dim3((a.npages + 63) / 64), dim3(64), 0, st, a);
+  if (a.npages) hipLaunchKernelGGL(dev::k_pq_data, dim3(a.npages), dim3(64), 0, st, a);
 }
 void launch_ckpt_assemble(const CkptAssembleArgs& a, hipStream_t st) {
   if (a.nrows) hipLaunchKernelGGL(dev::k_ckpt_assemble, dim3(unsigned((a.nrows + 255) / 256)), dim3(256), 0, st, a);

@@ -90,7 +90,32 @@ struct ParquetArgs {
   uint32_t* error;       // first error code (0 = ok)
 };
 
-void launch_pq_inflate(const ParquetArgs& a, hipStream_t st);
+// SNAPPY pages (k_snappy.hip). `in` points past the varint length preamble.
+struct SnapPage {
+  uint64_t in, out;      // device addresses
+  uint32_t n_in, n_out;
+  uint32_t block_base;   // first 64 KiB output block of this page in the block table
+};
+struct CopyJob { uint64_t src, dst, n; };
+struct SnappyArgs {
+  const SnapPage* pages;
+  uint32_t npages;
+  const uint32_t* chunk_base;   // [npages + 1] first speculation chunk of each page
+  uint32_t nchunks;
+  uint32_t* spec_exit;          // [nchunks]
+  uint32_t* vis;                // [nchunks * 8] visited-position bitmaps
+  uint32_t* entry;              // [nchunks] true first element position >= chunk start
+  uint32_t* chunk_out;          // [nchunks] output bytes of the chunk's elements
+  uint32_t* chunk_out_start;    // [nchunks]
+  uint32_t* block_in;           // [nblocks] input position of each block's first element
+  const uint32_t* block_page;   // [nblocks]
+  uint32_t nblocks;
+  uint32_t* pages_bad;          // [npages] nonzero -> decoded by the serial fallback
+  uint32_t* error;
+};
+void launch_snappy(const SnappyArgs& a, hipStream_t st);
+void launch_page_copy(const CopyJob* jobs, uint32_t njobs, hipStream_t st);
+
 void launch_pq_dict(const ParquetArgs& a, hipStream_t st);
 void launch_pq_data(const ParquetArgs& a, hipStream_t st);
 

@@ -228,7 +228,8 @@ def delta_name(v: int) -> str:
 # ----------------------------------------------------------------------------------------------
 def write_checkpoint(path: str, pool: FilePool, add_ids: np.ndarray, ncols: int, version: int,
                      with_parsed: bool = False, row_group_size: int = 1 << 20,
-                     data_page_size: int = 1 << 20) -> int:
+                     data_page_size: int = 1 << 20, compression: str = "snappy",
+                     data_page_version: str = "1.0", use_dictionary: bool = True) -> int:
     """Rows: protocol, metaData, then one `add` per id. Returns the row count."""
     pa, pc = _pa()
     import pyarrow.parquet as pq
@@ -305,8 +306,8 @@ def write_checkpoint(path: str, pool: FilePool, add_ids: np.ndarray, ncols: int,
     table = pa.Table.from_arrays([pa.nulls(nrows, txn_type), add_struct, pa.nulls(nrows, rm_type),
                                   md_struct, prot_struct],
                                  names=["txn", "add", "remove", "metaData", "protocol"])
-    pq.write_table(table, path, compression="snappy", use_dictionary=True, version="1.0",
-                   data_page_version="1.0", row_group_size=row_group_size,
+    pq.write_table(table, path, compression=compression, use_dictionary=use_dictionary, version="1.0",
+                   data_page_version=data_page_version, row_group_size=row_group_size,
                    data_page_size=data_page_size, write_statistics=False)
     return nrows
 
@@ -328,7 +329,9 @@ class ChurnSpec:
 
 
 def build_table(table_dir: str, spec: ChurnSpec, seed: int, checkpoint_with_parsed=False,
-                data_page_size: int = 1 << 20, keep_ids: bool = True) -> Expected:
+                data_page_size: int = 1 << 20, keep_ids: bool = True, compression: str = "snappy",
+                data_page_version: str = "1.0", row_group_size: int = 1 << 20,
+                use_dictionary: bool = True) -> Expected:
     rng = np.random.default_rng(seed)
     log = os.path.join(table_dir, "_delta_log")
     os.makedirs(log, exist_ok=True)
@@ -347,7 +350,9 @@ def build_table(table_dir: str, spec: ChurnSpec, seed: int, checkpoint_with_pars
         state[ids] = 1
         cp = os.path.join(log, "%020d.checkpoint.parquet" % version)
         nrows = write_checkpoint(cp, pool, ids, spec.ncols, version, with_parsed=checkpoint_with_parsed,
-                                 data_page_size=data_page_size)
+                                 data_page_size=data_page_size, compression=compression,
+                                 data_page_version=data_page_version, row_group_size=row_group_size,
+                                 use_dictionary=use_dictionary)
         ckpt_bytes += os.path.getsize(cp)
         n_actions += nrows
         n_file_actions += spec.ckpt_files

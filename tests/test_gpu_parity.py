@@ -104,3 +104,33 @@ def test_synthetic_configs(engine, tmp_path, config, scale):
         _assert_same(st, snap)
     finally:
         st.release()
+
+
+@pytest.mark.parametrize("page_size,compression,page_version,rg,dictionary", [
+    (4096, "snappy", "1.0", 1 << 20, True),
+    (64 << 10, "snappy", "1.0", 7000, True),
+    (8 << 20, "snappy", "1.0", 1 << 20, True),
+    (1 << 20, "none", "1.0", 1 << 20, True),
+    (64 << 10, "snappy", "2.0", 1 << 20, True),
+    (64 << 10, "none", "2.0", 1 << 20, True),
+    (4096, "snappy", "1.0", 1 << 20, False),
+    (1 << 20, "snappy", "1.0", 5000, False),
+    (64 << 10, "snappy", "2.0", 1 << 20, False),
+])
+def test_checkpoint_page_layouts(engine, tmp_path, page_size, compression, page_version, rg, dictionary):
+    """K2 over page sizes (many tiny pages .. one 8 MiB page), several row groups, uncompressed
+    pages and DATA_PAGE_V2: the replay must not depend on how the writer cut the column chunks."""
+    from delta_amd.testing import synth as S
+    exp = S.build_table(str(tmp_path), S.config_spec(3, 0.003), seed=77, data_page_size=page_size,
+                        compression=compression, data_page_version=page_version, row_group_size=rg,
+                        use_dictionary=dictionary)
+    lp = os.path.join(str(tmp_path), "_delta_log")
+    st = _gpu_replay(engine, lp, exp.min_file_retention_timestamp)
+    try:
+        c = st.counts
+        assert (c["num_files"], c["num_removes"], c["size_in_bytes"]) == \
+            (exp.num_files, exp.num_removes, exp.size_in_bytes)
+        snap = O.state_reconstruction(O.get_log_segment(lp), exp.min_file_retention_timestamp)
+        _assert_same(st, snap)
+    finally:
+        st.release()

@@ -194,7 +194,11 @@ struct StagedData {
   DBuf<SnapPage> d_snap;
   DBuf<uint32_t> d_chunk_base, d_block_page;
   DBuf<CopyJob> d_copy;
-  DBuf<uint32_t> s_spec_exit, s_vis, s_entry, s_chunk_out, s_chunk_out_start, s_block_in, s_pages_bad;
+  DBuf<uint32_t> s_spec_exit, s_vis, s_entry, s_chunk_out, s_chunk_out_start, s_chunk_copies, s_pages_bad;
+  DBuf<uint64_t> s_rec_start, s_recs;
+  std::vector<uint32_t> wg_chunk0;
+  DBuf<uint32_t> d_wg_chunk0;
+  uint64_t snap_in_bytes = 0;
 };
 
 struct dr_staged {
@@ -481,7 +485,10 @@ static void plan_checkpoint(StagedData& s) {
     SnapPage sp{d.src + lv + pre, d.dst + lv, uint32_t(d.csize - lv - pre), uint32_t(d.usize - lv),
                 uint32_t(s.block_page.size())};
     s.chunk_base.push_back(s.nchunks);
-    s.nchunks += (sp.n_in + 255) / 256;
+    const uint32_t ncp = (sp.n_in + 255) / 256;
+    for (uint32_t j = 0; j < ncp; j += snappy_wg_chunks()) s.wg_chunk0.push_back(s.nchunks + j);
+    s.nchunks += ncp;
+    s.snap_in_bytes += sp.n_in;
     const uint32_t nb = (sp.n_out + 65535) / 65536;
     for (uint32_t k = 0; k < nb; ++k) s.block_page.push_back(uint32_t(s.snap_pages.size()));
     s.snap_pages.push_back(sp);
@@ -501,12 +508,15 @@ static void plan_checkpoint(StagedData& s) {
   up(s.d_chunk_base, s.chunk_base);
   up(s.d_block_page, s.block_page);
   up(s.d_copy, s.copy_jobs);
+  up(s.d_wg_chunk0, s.wg_chunk0);
   s.s_spec_exit = DBuf<uint32_t>(s.ctx, s.nchunks);
   s.s_vis = DBuf<uint32_t>(s.ctx, uint64_t(s.nchunks) * 8);
   s.s_entry = DBuf<uint32_t>(s.ctx, s.nchunks);
   s.s_chunk_out = DBuf<uint32_t>(s.ctx, s.nchunks);
   s.s_chunk_out_start = DBuf<uint32_t>(s.ctx, s.nchunks);
-  s.s_block_in = DBuf<uint32_t>(s.ctx, s.block_page.size());
+  s.s_chunk_copies = DBuf<uint32_t>(s.ctx, s.nchunks);
+  s.s_rec_start = DBuf<uint64_t>(s.ctx, uint64_t(s.nchunks) + 1);
+  s.s_recs = DBuf<uint64_t>(s.ctx, s.snap_in_bytes / 2 + 1);  // a copy element takes >= 2 input bytes
   s.s_pages_bad = DBuf<uint32_t>(s.ctx, s.snap_pages.size());
   for (PageDesc& d : s.pages) {
     d.src = reinterpret_cast<uint64_t>(s.d_pq.p) + d.src;
@@ -684,9 +694,10 @@ static dr_state* replay(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, int6
     if (!s.snap_pages.empty()) {
       s.s_pages_bad.zero(stream);
       SnappyArgs sa{s.d_snap.p, uint32_t(s.snap_pages.size()), s.d_chunk_base.p, s.nchunks, s.s_spec_exit.p,
-                    s.s_vis.p, s.s_entry.p, s.s_chunk_out.p, s.s_chunk_out_start.p, s.s_block_in.p,
-                    s.d_block_page.p, uint32_t(s.block_page.size()), s.s_pages_bad.p, pq_err.p};
-      launch_snappy(sa, stream);
+                    s.s_vis.p, s.s_entry.p, s.s_chunk_out.p, s.s_chunk_out_start.p, s.s_chunk_copies.p,
+                    s.s_rec_start.p, s.s_recs.p, s.d_block_page.p, uint32_t(s.block_page.size()),
+                    s.d_wg_chunk0.p, uint32_t(s.wg_chunk0.size()), s.s_pages_bad.p, pq_err.p};
+      launch_snappy(sa, stream, scratch.p);
     }
     ctx->mark("pq_inflate");
     launch_pq_dict(pa, stream);

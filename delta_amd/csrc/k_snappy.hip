@@ -1,24 +1,27 @@
 // K2a: parallel SNAPPY page decompression for checkpoint column chunks.
 //
-// A raw snappy stream is a varint length followed by literal/copy elements; the element chain is
-// serial, which with ~144K elements per 1 MiB page of paths makes a per-page decoder latency
-// bound (measured: 1.28 s for config 3 with one lane per page). This decoder splits the work:
+// A raw snappy stream is a varint length followed by literal/copy elements. The element chain is
+// serial and a 1 MiB page of paths holds ~144K elements, so a per-page decoder is latency bound
+// (measured 1.28 s for config 3 with one lane per page). This decoder is fully parallel:
 //
-//  A  k_snap_spec     one lane per 256-byte chunk of compressed input parses elements
-//                     *speculatively* from the chunk start and records the positions it visited
-//                     (256-bit bitmap) and where it left the chunk.
-//  B  k_snap_resolve  one wave per page walks the chunks in order carrying the true element
-//                     boundary; where the true entry is on the speculative chain the chunk is
-//                     already correct (chains that meet coincide from then on), otherwise the
-//                     wave re-parses until it meets the chain. Mis-speculation is rare because
-//                     a wrong start re-synchronises within a few elements.
-//  C  k_snap_count    one lane per chunk re-walks its true elements: output bytes per chunk.
-//  D  k_snap_blocks   per page: exclusive scan of chunk outputs; one lane per chunk records the
-//                     input position of every element that starts a 64 KiB output block.
-//  E  k_snap_exec     one lane per 64 KiB output block executes its elements. The snappy
-//                     compressor compresses 64 KiB fragments independently, so copies never reach
-//                     before their block; any page that violates this (or whose blocks do not
-//                     start on an element) is flagged and decoded by k_snap_serial instead.
+//  A k_snap_spec    one lane per 256-byte chunk of compressed input parses elements
+//                   *speculatively* (starting 64 bytes early as a warm-up) and records the
+//                   positions it visited in the chunk (256-bit bitmap) and where it left it.
+//  B k_snap_resolve one wave per page checks 64 chunks at a time with a ballot: a chunk whose
+//                   true entry (the previous chunk's exit) is on its speculative chain is correct
+//                   (chains that meet coincide from then on). Only breaks -- a mis-speculated
+//                   chunk or one spanned by a long literal -- are walked serially.
+//  C k_snap_count   per chunk: output bytes and copy elements of its true elements.
+//  D k_snap_scan    per page: exclusive scan of chunk outputs (copy counts: a global scan).
+//  E k_snap_emit    per chunk: literal bytes go straight to the output, copies become 8-byte
+//                   records {out, len, offset}. The compressor compresses 64 KiB fragments
+//                   independently, so no element straddles a fragment and no copy reaches before
+//                   its fragment; violations flag the page for k_snap_serial.
+//  F k_snap_exec    one 1024-thread workgroup per 64 KiB output block resolves every copied
+//                   byte to its literal origin by pointer jumping on a u16 map in LDS
+//                   (src[p] = p - offset; literal bytes are their own roots) and gathers it.
+//
+// Chunk walkers (A, C, E) stage their page bytes into LDS with coalesced loads and parse from LDS.
 #include "dev_common.h"
 #include "kernels.h"
 
@@ -27,6 +30,9 @@ namespace dev {
 
 constexpr uint32_t SNAP_CH = 256;            // compressed bytes per speculation chunk
 constexpr uint32_t SNAP_BLOCK = 65536;       // snappy compressor fragment size
+constexpr uint32_t SNAP_WU = 64;             // speculation warm-up bytes
+constexpr uint32_t WG_CHUNKS = 256;          // chunks (threads) per chunk-walker workgroup
+constexpr uint32_t STAGE_BYTES = WG_CHUNKS * SNAP_CH + SNAP_WU + 64;
 
 struct Elem {
   uint32_t hdr;   // header bytes (tag + length/offset bytes)
@@ -34,43 +40,28 @@ struct Elem {
   uint32_t off;   // copy offset (0 for a literal)
 };
 
-// Decodes the element header at p (reads up to 5 bytes; buffers are padded).
-__device__ __forceinline__ Elem snap_elem(const uint8_t* p) {
-  const uint64_t w = load_u64(p);
+__device__ __forceinline__ Elem snap_decode(uint64_t w) {
   const uint32_t tag = uint32_t(w & 0xff);
   Elem e;
   switch (tag & 3) {
     case 0: {
-      uint32_t l = tag >> 2;
+      const uint32_t l = tag >> 2;
       if (l < 60) { e.hdr = 1; e.len = l + 1; }
       else {
         const uint32_t nb = l - 59;
         const uint64_t v = (w >> 8) & ((nb >= 4) ? 0xffffffffull : ((1ull << (8 * nb)) - 1));
-        e.hdr = 1 + nb;
-        e.len = uint32_t(v) + 1;
+        e.hdr = 1 + nb; e.len = uint32_t(v) + 1;
       }
       e.off = 0;
       break;
     }
-    case 1:
-      e.hdr = 2;
-      e.len = ((tag >> 2) & 7) + 4;
-      e.off = ((tag >> 5) << 8) | uint32_t((w >> 8) & 0xff);
-      break;
-    case 2:
-      e.hdr = 3;
-      e.len = (tag >> 2) + 1;
-      e.off = uint32_t((w >> 8) & 0xffff);
-      break;
-    default:
-      e.hdr = 5;
-      e.len = (tag >> 2) + 1;
-      e.off = uint32_t((w >> 8) & 0xffffffffull);
-      break;
+    case 1: e.hdr = 2; e.len = ((tag >> 2) & 7) + 4; e.off = ((tag >> 5) << 8) | uint32_t((w >> 8) & 0xff); break;
+    case 2: e.hdr = 3; e.len = (tag >> 2) + 1; e.off = uint32_t((w >> 8) & 0xffff); break;
+    default: e.hdr = 5; e.len = (tag >> 2) + 1; e.off = uint32_t((w >> 8) & 0xffffffffull); break;
   }
   return e;
 }
-// input bytes consumed by an element (header + literal payload)
+__device__ __forceinline__ Elem snap_elem(const uint8_t* p) { return snap_decode(load_u64(p)); }
 __device__ __forceinline__ uint64_t snap_adv(const Elem& e) { return uint64_t(e.hdr) + (e.off ? 0u : e.len); }
 
 __device__ __forceinline__ uint32_t chunk_page(const uint32_t* chunk_base, uint32_t npages, uint32_t c) {
@@ -82,33 +73,80 @@ __device__ __forceinline__ uint32_t chunk_page(const uint32_t* chunk_base, uint3
   return lo;
 }
 
-// A: speculative parse of every chunk.
-__global__ void __launch_bounds__(256) k_snap_spec(SnappyArgs a) {
-  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= a.nchunks) return;
+// ---- LDS staging of a workgroup's input range -------------------------------------------------------
+// Bytes of the page input from (chunk j0 start - warm-up) to (chunk j0+cnt end + 16) are copied
+// into `buf` with coalesced dword loads; `lo` is the page offset of buf[0] (dword aligned in
+// absolute address, so it may sit up to 3 bytes before the page input).
+struct Staged {
+  int64_t lo;
+  uint64_t hi;
+};
+
+__device__ Staged stage_input(uint8_t* buf, const uint8_t* in, uint64_t n_in, uint32_t j0, uint32_t cnt) {
+  uint64_t lo = uint64_t(j0) * SNAP_CH;
+  lo = lo >= SNAP_WU ? lo - SNAP_WU : 0;
+  const uint64_t hi = min(uint64_t(j0 + cnt) * SNAP_CH + 16, uint64_t(n_in) + 8);
+  const uintptr_t a0 = (reinterpret_cast<uintptr_t>(in) + lo) & ~uintptr_t(3);
+  const int64_t lo_al = int64_t(a0) - int64_t(reinterpret_cast<uintptr_t>(in));
+  const uint32_t nd = uint32_t((int64_t(hi) - lo_al + 3) / 4) + 2;
+  uint32_t* b32 = reinterpret_cast<uint32_t*>(buf);
+  const uint32_t* g32 = reinterpret_cast<const uint32_t*>(a0);
+  for (uint32_t i = threadIdx.x; i < nd; i += blockDim.x) b32[i] = g32[i];
+  __syncthreads();
+  return Staged{lo_al, hi};
+}
+
+// 8 bytes at page offset pos from the staged copy.
+__device__ __forceinline__ uint64_t staged_u64(const uint8_t* buf, const Staged& s, uint64_t pos) {
+  const uint32_t r = uint32_t(int64_t(pos) - s.lo);
+  const uint32_t* b32 = reinterpret_cast<const uint32_t*>(buf);
+  const uint32_t di = r >> 2, sh = r & 3;
+  const uint32_t w0 = b32[di], w1 = b32[di + 1], w2 = b32[di + 2];
+  return uint64_t(__builtin_amdgcn_alignbyte(w1, w0, sh)) | (uint64_t(__builtin_amdgcn_alignbyte(w2, w1, sh)) << 32);
+}
+
+// Workgroup g covers chunks [wg_chunk0[g], ...) of one page.
+struct WgInfo {
+  uint32_t p, j0, cnt;   // page, first chunk (page-relative), chunks in this workgroup
+};
+__device__ __forceinline__ WgInfo wg_info(const SnappyArgs& a) {
+  const uint32_t c = a.wg_chunk0[blockIdx.x];
   const uint32_t p = chunk_page(a.chunk_base, a.npages, c);
-  const SnapPage& pg = a.pages[p];
-  const uint8_t* in = reinterpret_cast<const uint8_t*>(pg.in);
-  const uint64_t cs = uint64_t(c - a.chunk_base[p]) * SNAP_CH;
+  const uint32_t j0 = c - a.chunk_base[p];
+  const uint32_t nc = a.chunk_base[p + 1] - a.chunk_base[p];
+  return WgInfo{p, j0, min(WG_CHUNKS, nc - j0)};
+}
+
+// A: speculative parse.
+__global__ void __launch_bounds__(WG_CHUNKS) k_snap_spec(SnappyArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[STAGE_BYTES + 32];
+  const WgInfo g = wg_info(a);
+  const SnapPage& pg = a.pages[g.p];
+  const Staged s = stage_input(buf, reinterpret_cast<const uint8_t*>(pg.in), pg.n_in, g.j0, g.cnt);
+  if (threadIdx.x >= g.cnt) return;
+  const uint32_t j = g.j0 + threadIdx.x;
+  const uint32_t c = a.chunk_base[g.p] + j;
+  const uint64_t cs = uint64_t(j) * SNAP_CH;
   const uint64_t ce = min(cs + SNAP_CH, uint64_t(pg.n_in));
   uint32_t vis[SNAP_CH / 32];
 #pragma unroll
   for (int k = 0; k < int(SNAP_CH / 32); ++k) vis[k] = 0;
-  uint64_t pos = cs;
+  uint64_t pos = cs >= SNAP_WU ? cs - SNAP_WU : 0;
   while (pos < ce) {
-    const uint32_t r = uint32_t(pos - cs);
+    if (pos >= cs) {
+      const uint32_t r = uint32_t(pos - cs);
 #pragma unroll
-    for (int k = 0; k < int(SNAP_CH / 32); ++k)
-      if (int(r >> 5) == k) vis[k] |= 1u << (r & 31);
-    pos += snap_adv(snap_elem(in + pos));
+      for (int k = 0; k < int(SNAP_CH / 32); ++k)
+        if (int(r >> 5) == k) vis[k] |= 1u << (r & 31);
+    }
+    pos += snap_adv(snap_decode(staged_u64(buf, s, pos)));
   }
   a.spec_exit[c] = pos > 0xffffffffull ? 0xffffffffu : uint32_t(pos);
 #pragma unroll
   for (int k = 0; k < int(SNAP_CH / 32); ++k) a.vis[uint64_t(c) * (SNAP_CH / 32) + k] = vis[k];
 }
 
-// B: true chunk entries. One wave per page; lane 0 carries the entry, the wave prefetches the
-// speculative exits and bitmaps 64 chunks at a time.
+// B: true chunk entries, 64 chunks per ballot.
 __global__ void __launch_bounds__(64) k_snap_resolve(SnappyArgs a) {
   const uint32_t p = blockIdx.x;
   if (p >= a.npages) return;
@@ -116,73 +154,62 @@ __global__ void __launch_bounds__(64) k_snap_resolve(SnappyArgs a) {
   const uint8_t* in = reinterpret_cast<const uint8_t*>(pg.in);
   const uint32_t c0 = a.chunk_base[p], nc = a.chunk_base[p + 1] - c0;
   const int lane = threadIdx.x;
-  uint64_t e = 0;  // true entry of the current chunk (relative to pg.in)
-  for (uint32_t base = 0; base < nc; base += 64) {
+  uint64_t e = 0;  // true entry of chunk `base`
+  uint32_t base = 0;
+  while (base < nc) {
     const uint32_t j = base + lane;
-    uint32_t x = 0, v[SNAP_CH / 32];
-    if (j < nc) {
-      x = a.spec_exit[c0 + j];
-#pragma unroll
-      for (int k = 0; k < int(SNAP_CH / 32); ++k) v[k] = a.vis[uint64_t(c0 + j) * (SNAP_CH / 32) + k];
-    }
+    const bool valid = j < nc;
+    uint32_t x = 0, word = 0;
+    const uint64_t cs = uint64_t(j) * SNAP_CH;
+    const uint64_t ce = min(cs + SNAP_CH, uint64_t(pg.n_in));
+    if (valid) x = a.spec_exit[c0 + j];
+    uint64_t cand = __shfl_up(uint64_t(x), 1, 64);
+    if (lane == 0) cand = e;
+    const bool skip = cand >= ce;
+    if (valid && !skip) word = a.vis[uint64_t(c0 + j) * (SNAP_CH / 32) + uint32_t((cand - cs) >> 5)];
+    const bool ok = valid && !skip && ((word >> ((cand - cs) & 31)) & 1u);
+    const unsigned long long brk = __ballot(valid && !ok);
+    const uint32_t f = brk ? uint32_t(__builtin_ctzll(brk)) : 64u;  // first chunk needing care
+    if (valid && uint32_t(lane) <= f) a.entry[c0 + j] = uint32_t(min(cand, uint64_t(0xffffffffu)));
     const uint32_t cnt = min(64u, nc - base);
-    for (uint32_t l = 0; l < cnt; ++l) {
-      const uint64_t cs = uint64_t(base + l) * SNAP_CH;
-      const uint64_t ce = min(cs + SNAP_CH, uint64_t(pg.n_in));
-      if (lane == 0) a.entry[c0 + base + l] = uint32_t(min(e, uint64_t(0xffffffffu)));
-      if (e >= ce) continue;  // an element spans this whole chunk
-      const uint32_t r = uint32_t(e - cs);
-      uint32_t word = 0;
-#pragma unroll
-      for (int k = 0; k < int(SNAP_CH / 32); ++k) {
-        const uint32_t vk = __shfl(v[k], int(l), 64);
-        if (int(r >> 5) == k) word = vk;
-      }
-      if ((word >> (r & 31)) & 1u) {
-        e = __shfl(x, int(l), 64);
-        continue;
-      }
-      // mis-speculated: walk from the true entry until meeting the speculative chain
-      uint64_t pos = e;
-      bool met = false;
-      while (pos < ce) {
-        pos += snap_adv(snap_elem(in + pos));
-        if (pos < ce) {
-          const uint32_t rr = uint32_t(pos - cs);
-          uint32_t w2 = 0;
-#pragma unroll
-          for (int k = 0; k < int(SNAP_CH / 32); ++k) {
-            const uint32_t vk = __shfl(v[k], int(l), 64);
-            if (int(rr >> 5) == k) w2 = vk;
-          }
-          if ((w2 >> (rr & 31)) & 1u) { met = true; break; }
-        }
-      }
-      e = met ? uint64_t(__shfl(x, int(l), 64)) : pos;
+    if (f >= cnt) {
+      e = uint32_t(__builtin_amdgcn_readlane(int(x), int(cnt - 1)));
+      base += cnt;
+      continue;
     }
+    // chunk base+f: its true entry is cand_f (all earlier lanes were consistent)
+    uint64_t ef = __shfl(cand, int(f), 64);
+    const uint64_t fce = min(uint64_t(base + f) * SNAP_CH + SNAP_CH, uint64_t(pg.n_in));
+    while (ef < fce) ef += snap_adv(snap_elem(in + ef));  // uniform walk of a mis-speculated chunk
+    e = ef;
+    base += f + 1;
   }
 }
 
-// C: output bytes produced by the true elements starting in each chunk.
-__global__ void __launch_bounds__(256) k_snap_count(SnappyArgs a) {
-  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= a.nchunks) return;
-  const uint32_t p = chunk_page(a.chunk_base, a.npages, c);
-  const SnapPage& pg = a.pages[p];
-  const uint8_t* in = reinterpret_cast<const uint8_t*>(pg.in);
-  const uint64_t cs = uint64_t(c - a.chunk_base[p]) * SNAP_CH;
+// C: output bytes / copy elements produced by the true elements of each chunk.
+__global__ void __launch_bounds__(WG_CHUNKS) k_snap_count(SnappyArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[STAGE_BYTES + 32];
+  const WgInfo g = wg_info(a);
+  const SnapPage& pg = a.pages[g.p];
+  const Staged s = stage_input(buf, reinterpret_cast<const uint8_t*>(pg.in), pg.n_in, g.j0, g.cnt);
+  if (threadIdx.x >= g.cnt) return;
+  const uint32_t j = g.j0 + threadIdx.x;
+  const uint32_t c = a.chunk_base[g.p] + j;
+  const uint64_t cs = uint64_t(j) * SNAP_CH;
   const uint64_t ce = min(cs + SNAP_CH, uint64_t(pg.n_in));
-  uint64_t pos = a.entry[c];
-  uint64_t out = 0;
+  uint64_t pos = a.entry[c], out = 0;
+  uint32_t copies = 0;
   while (pos < ce) {
-    const Elem el = snap_elem(in + pos);
+    const Elem el = snap_decode(staged_u64(buf, s, pos));
     out += el.len;
+    copies += el.off != 0;
     pos += snap_adv(el);
   }
   a.chunk_out[c] = out > 0xffffffffull ? 0xffffffffu : uint32_t(out);
+  a.chunk_copies[c] = copies;
 }
 
-// D: per-page exclusive scan of chunk outputs (one wave per page), then block starts.
+// D: per-page exclusive scan of chunk outputs (one wave per page).
 __global__ void __launch_bounds__(64) k_snap_scan(SnappyArgs a) {
   const uint32_t p = blockIdx.x;
   if (p >= a.npages) return;
@@ -200,75 +227,107 @@ __global__ void __launch_bounds__(64) k_snap_scan(SnappyArgs a) {
     if (j < nc) a.chunk_out_start[c0 + j] = uint32_t(carry + incl - v);
     carry += __shfl(incl, 63, 64);
   }
-  if (lane == 0 && carry != a.pages[p].n_out) atomicOr(&a.pages_bad[p], 1u);  // output size mismatch
+  if (lane == 0 && carry != a.pages[p].n_out) atomicOr(&a.pages_bad[p], 1u);  // size mismatch
 }
 
-__global__ void __launch_bounds__(256) k_snap_blocks(SnappyArgs a) {
-  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= a.nchunks) return;
-  const uint32_t p = chunk_page(a.chunk_base, a.npages, c);
-  const SnapPage& pg = a.pages[p];
-  const uint8_t* in = reinterpret_cast<const uint8_t*>(pg.in);
-  const uint64_t cs = uint64_t(c - a.chunk_base[p]) * SNAP_CH;
+// E: literal bytes to the output, copies to records.
+__global__ void __launch_bounds__(WG_CHUNKS) k_snap_emit(SnappyArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[STAGE_BYTES + 32];
+  const WgInfo g = wg_info(a);
+  const SnapPage& pg = a.pages[g.p];
+  const Staged s = stage_input(buf, reinterpret_cast<const uint8_t*>(pg.in), pg.n_in, g.j0, g.cnt);
+  if (threadIdx.x >= g.cnt) return;
+  const uint32_t j = g.j0 + threadIdx.x;
+  const uint32_t c = a.chunk_base[g.p] + j;
+  const uint64_t cs = uint64_t(j) * SNAP_CH;
   const uint64_t ce = min(cs + SNAP_CH, uint64_t(pg.n_in));
-  uint64_t pos = a.entry[c];
-  uint64_t out = a.chunk_out_start[c];
-  const uint32_t nb = (pg.n_out + SNAP_BLOCK - 1) / SNAP_BLOCK;
+  uint8_t* out = reinterpret_cast<uint8_t*>(pg.out);
+  uint64_t pos = a.entry[c], o = a.chunk_out_start[c];
+  uint64_t rec = a.chunk_rec_start[c];
+  bool bad = false;
   while (pos < ce) {
-    const Elem el = snap_elem(in + pos);
-    if ((out & (SNAP_BLOCK - 1)) == 0 && (out >> 16) < nb) a.block_in[pg.block_base + uint32_t(out >> 16)] = uint32_t(pos);
-    if (el.len && (out >> 16) != ((out + el.len - 1) >> 16))
-      atomicOr(&a.pages_bad[p], 2u);  // an element straddles a 64 KiB output boundary
-    out += el.len;
+    const Elem el = snap_decode(staged_u64(buf, s, pos));
+    if (o + el.len > pg.n_out || (el.len && (o >> 16) != ((o + el.len - 1) >> 16))) { bad = true; break; }
+    if (el.off == 0) {
+      if (pos + el.hdr + el.len > pg.n_in) { bad = true; break; }
+      const uint64_t lp = pos + el.hdr;
+      if (lp + el.len + 4 <= s.hi) {
+        for (uint32_t i = 0; i < el.len; ++i) out[o + i] = buf[uint32_t(int64_t(lp + i) - s.lo)];
+      } else {  // a long literal running past the staged range
+        const uint8_t* sp = reinterpret_cast<const uint8_t*>(pg.in) + lp;
+        for (uint32_t i = 0; i < el.len; ++i) out[o + i] = sp[i];
+      }
+    } else {
+      if (el.off > (o & (SNAP_BLOCK - 1)) || el.len > 0xffff) { bad = true; break; }  // copy crosses its fragment
+      a.recs[rec++] = uint64_t(o) | (uint64_t(el.len) << 32) | (uint64_t(el.off) << 48);
+    }
+    o += el.len;
     pos += snap_adv(el);
   }
+  if (bad) atomicOr(&a.pages_bad[g.p], 8u);
 }
 
-// E: one lane per 64 KiB output block.
-__global__ void __launch_bounds__(64) k_snap_exec(SnappyArgs a) {
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= a.nblocks) return;
+// F: one 1024-thread workgroup per 64 KiB output block.
+constexpr int EXEC_T = 1024;
+
+__global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
+  __shared__ uint16_t src[SNAP_BLOCK];
+  __shared__ uint32_t s_j0, s_j1, s_changed;
+  const uint32_t b = blockIdx.x;
   const uint32_t p = a.block_page[b];
   if (a.pages_bad[p]) return;
   const SnapPage& pg = a.pages[p];
-  const uint8_t* in = reinterpret_cast<const uint8_t*>(pg.in);
   uint8_t* out = reinterpret_cast<uint8_t*>(pg.out);
   const uint32_t k = b - pg.block_base;
-  uint64_t op = uint64_t(k) * SNAP_BLOCK;
-  const uint64_t oend = min(op + SNAP_BLOCK, uint64_t(pg.n_out));
-  const uint64_t bstart = op;
-  uint64_t ip = a.block_in[b];
-  while (op < oend) {
-    if (ip >= pg.n_in) { atomicOr(&a.pages_bad[p], 4u); return; }
-    const Elem el = snap_elem(in + ip);
-    if (op + el.len > oend) { atomicOr(&a.pages_bad[p], 4u); return; }
-    if (el.off == 0) {
-      const uint8_t* s = in + ip + el.hdr;
-      if (ip + el.hdr + el.len > pg.n_in) { atomicOr(&a.pages_bad[p], 4u); return; }
-      uint32_t i = 0;
-      for (; i + 8 <= el.len; i += 8) {
-        const uint64_t w = load_u64(s + i);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) out[op + i + q] = uint8_t(w >> (8 * q));
-      }
-      for (; i < el.len; ++i) out[op + i] = s[i];
-    } else {
-      if (el.off > op - bstart) { atomicOr(&a.pages_bad[p], 8u); return; }  // copy crosses its fragment
-      const uint8_t* s = out + op - el.off;
-      if (el.off >= 8) {
-        uint32_t i = 0;
-        for (; i + 8 <= el.len; i += 8) {
-          const uint64_t w = load_u64(s + i);
-#pragma unroll
-          for (int q = 0; q < 8; ++q) out[op + i + q] = uint8_t(w >> (8 * q));
-        }
-        for (; i < el.len; ++i) out[op + i] = s[i];
-      } else {
-        for (uint32_t i = 0; i < el.len; ++i) out[op + i] = s[i];
-      }
+  const uint64_t bs = uint64_t(k) * SNAP_BLOCK;
+  const uint64_t be = min(bs + SNAP_BLOCK, uint64_t(pg.n_out));
+  const uint32_t nbytes = uint32_t(be - bs);
+  const uint32_t c0 = a.chunk_base[p], c1 = a.chunk_base[p + 1];
+  const int t = threadIdx.x;
+  if (t == 0) {
+    uint32_t lo = c0, hi = c1;  // first chunk whose output reaches past bs
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (uint64_t(a.chunk_out_start[mid]) + a.chunk_out[mid] <= bs) lo = mid + 1; else hi = mid;
     }
-    op += el.len;
-    ip += snap_adv(el);
+    s_j0 = lo;
+    hi = c1;  // first chunk starting at or after be
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (a.chunk_out_start[mid] < be) lo = mid + 1; else hi = mid;
+    }
+    s_j1 = lo;
+  }
+  for (uint32_t i = t; i < nbytes; i += EXEC_T) src[i] = uint16_t(i);
+  __syncthreads();
+  const uint64_t r0 = a.chunk_rec_start[s_j0];
+  const uint64_t r1 = a.chunk_rec_start[s_j1];
+  for (uint64_t r = r0 + t; r < r1; r += EXEC_T) {
+    const uint64_t w = a.recs[r];
+    const uint64_t o = uint32_t(w);
+    if (o < bs || o >= be) continue;
+    const uint32_t len = uint32_t((w >> 32) & 0xffff), off = uint32_t(w >> 48);
+    const uint32_t rel = uint32_t(o - bs);
+    for (uint32_t i = 0; i < len; ++i) src[rel + i] = uint16_t(rel + i - off);
+  }
+  __syncthreads();
+  for (int round = 0; round < 17; ++round) {
+    if (t == 0) s_changed = 0;
+    __syncthreads();
+    uint32_t ch = 0;
+    for (uint32_t i = t; i < nbytes; i += EXEC_T) {
+      const uint32_t x = src[i];
+      const uint32_t y = src[x];
+      if (y != x) { src[i] = uint16_t(y); ch = 1; }
+    }
+    if (__any(ch) && (t & 63) == 0) s_changed = 1;
+    __syncthreads();
+    if (!s_changed) break;
+  }
+  __threadfence_block();
+  for (uint32_t i = t; i < nbytes; i += EXEC_T) {
+    const uint32_t r = src[i];
+    if (r != i) out[bs + i] = out[bs + r];
   }
 }
 
@@ -287,7 +346,7 @@ __global__ void k_snap_serial(SnappyArgs a) {
       if (ip + el.hdr + el.len > pg.n_in) { atomicCAS(a.error, 0u, 1u); return; }
       for (uint32_t i = 0; i < el.len; ++i) out[op + i] = in[ip + el.hdr + i];
     } else {
-      if (el.off == 0 || el.off > op) { atomicCAS(a.error, 0u, 1u); return; }
+      if (el.off > op) { atomicCAS(a.error, 0u, 1u); return; }
       for (uint32_t i = 0; i < el.len; ++i) out[op + i] = out[op - el.off + i];
     }
     op += el.len;
@@ -296,7 +355,7 @@ __global__ void k_snap_serial(SnappyArgs a) {
   if (op != pg.n_out) atomicCAS(a.error, 0u, 1u);
 }
 
-// Uncompressed pages and the raw level prefix of DATA_PAGE_V2 pages: one wave per copy job.
+// Uncompressed pages and the raw level prefix of DATA_PAGE_V2 pages: one workgroup per job.
 __global__ void __launch_bounds__(256) k_page_copy(const CopyJob* jobs, uint32_t njobs) {
   const uint32_t j = blockIdx.x;
   if (j >= njobs) return;
@@ -308,15 +367,17 @@ __global__ void __launch_bounds__(256) k_page_copy(const CopyJob* jobs, uint32_t
 
 }  // namespace dev
 
-void launch_snappy(const SnappyArgs& a, hipStream_t st) {
+uint32_t snappy_wg_chunks() { return dev::WG_CHUNKS; }
+
+void launch_snappy(const SnappyArgs& a, hipStream_t st, void* scan_scratch) {
   if (!a.npages) return;
-  const unsigned gc = (a.nchunks + 255) / 256;
-  hipLaunchKernelGGL(dev::k_snap_spec, dim3(gc), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(dev::k_snap_spec, dim3(a.nwg), dim3(dev::WG_CHUNKS), 0, st, a);
   hipLaunchKernelGGL(dev::k_snap_resolve, dim3(a.npages), dim3(64), 0, st, a);
-  hipLaunchKernelGGL(dev::k_snap_count, dim3(gc), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(dev::k_snap_count, dim3(a.nwg), dim3(dev::WG_CHUNKS), 0, st, a);
   hipLaunchKernelGGL(dev::k_snap_scan, dim3(a.npages), dim3(64), 0, st, a);
-  hipLaunchKernelGGL(dev::k_snap_blocks, dim3(gc), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(dev::k_snap_exec, dim3((a.nblocks + 63) / 64), dim3(64), 0, st, a);
+  launch_scan_u32(a.chunk_copies, a.chunk_rec_start, a.nchunks, scan_scratch, st);
+  hipLaunchKernelGGL(dev::k_snap_emit, dim3(a.nwg), dim3(dev::WG_CHUNKS), 0, st, a);
+  hipLaunchKernelGGL(dev::k_snap_exec, dim3(a.nblocks), dim3(dev::EXEC_T), 0, st, a);
   hipLaunchKernelGGL(dev::k_snap_serial, dim3((a.npages + 63) / 64), dim3(64), 0, st, a);
 }
 

@@ -107,13 +107,18 @@ struct SnappyArgs {
   uint32_t* entry;              // [nchunks] true first element position >= chunk start
   uint32_t* chunk_out;          // [nchunks] output bytes of the chunk's elements
   uint32_t* chunk_out_start;    // [nchunks]
-  uint32_t* block_in;           // [nblocks] input position of each block's first element
+  uint32_t* chunk_copies;       // [nchunks] copy elements per chunk
+  uint64_t* chunk_rec_start;    // [nchunks + 1] exclusive scan of chunk_copies
+  uint64_t* recs;               // copy records {out u32 | len u16 << 32 | off u16 << 48}
   const uint32_t* block_page;   // [nblocks]
   uint32_t nblocks;
+  const uint32_t* wg_chunk0;    // [nwg] first chunk (global index) of each chunk-walker workgroup
+  uint32_t nwg;
   uint32_t* pages_bad;          // [npages] nonzero -> decoded by the serial fallback
   uint32_t* error;
 };
-void launch_snappy(const SnappyArgs& a, hipStream_t st);
+uint32_t snappy_wg_chunks();
+void launch_snappy(const SnappyArgs& a, hipStream_t st, void* scan_scratch);
 void launch_page_copy(const CopyJob* jobs, uint32_t njobs, hipStream_t st);
 
 void launch_pq_dict(const ParquetArgs& a, hipStream_t st);

@@ -59,6 +59,7 @@ def algorithmic_bytes(stage, plan, counts):
         "json_newlines": plan["json_bytes"] + 8 * n_lines,
         "json_parse": plan["json_bytes"] + 8 * n_lines + 50 * n_lines,
         "pq_inflate": plan["pages_compressed_bytes"] + plan["pages_decompressed_bytes"],
+        "pq_bounds": plan["pages_decompressed_bytes"],
         "pq_decode": plan["pages_decompressed_bytes"] + 44 * rows,
         "ckpt_assemble": 44 * rows + 88 * rows + 50 * rows,
         "partition_hist": 10 * (rows + n_lines),
@@ -76,7 +77,7 @@ def cpu_baseline(config, sample_scale, seed, tmp):
     path = os.path.join(tmp, "cpu_sample_c%d_%g" % (config, sample_scale))
     exp = build_table(path, config, sample_scale, seed)
     threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    threads = min(threads, 64)
+    threads = min(threads, 16)  # the GPU box's CPU share per GPU
     r = subprocess.run([exe, os.path.join(path, "_delta_log"), str(exp["min_file_retention_timestamp"]),
                         "--threads", str(threads), "--partitions", "50"],
                        capture_output=True, text=True, timeout=600)

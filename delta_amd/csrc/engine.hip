@@ -199,6 +199,10 @@ struct StagedData {
   std::vector<uint32_t> wg_chunk0;
   DBuf<uint32_t> d_wg_chunk0;
   uint64_t snap_in_bytes = 0;
+  // PLAIN BYTE_ARRAY boundary scratch (k_ba_bounds)
+  uint32_t ba_pages = 0;
+  uint64_t ba_vals = 0, ba_hits = 0;
+  DBuf<uint32_t> s_ba_vals, s_ba_hit, s_ba_ok, s_ba_count;
 };
 
 struct dr_staged {
@@ -454,6 +458,14 @@ static void plan_checkpoint(StagedData& s) {
               fail(DR_E_UNSUPPORTED, fmt("encoding %d not supported for %s", d.encoding, kHotPath[c]));
           }
           arena += (uint64_t(d.usize) + 16 + 15) & ~uint64_t(15);
+          if (d.phys == 6 && (d.kind == PG_DICT || d.encoding == 0)) {  // PLAIN byte arrays
+            d.ba = 1;
+            d.ba_slot = s.ba_pages++;
+            d.ba_base = s.ba_vals;
+            d.hit_base = s.ba_hits;
+            s.ba_vals += d.usize / 4 + 2;
+            s.ba_hits += d.usize / 32 + 4;
+          }
           s.pages.push_back(d);
         }
         if (row != rg_row + uint64_t(rg.num_rows))
@@ -518,6 +530,10 @@ static void plan_checkpoint(StagedData& s) {
   s.s_rec_start = DBuf<uint64_t>(s.ctx, uint64_t(s.nchunks) + 1);
   s.s_recs = DBuf<uint64_t>(s.ctx, s.snap_in_bytes / 2 + 1);  // a copy element takes >= 2 input bytes
   s.s_pages_bad = DBuf<uint32_t>(s.ctx, s.snap_pages.size());
+  s.s_ba_vals = DBuf<uint32_t>(s.ctx, s.ba_vals);
+  s.s_ba_hit = DBuf<uint32_t>(s.ctx, s.ba_hits);
+  s.s_ba_ok = DBuf<uint32_t>(s.ctx, s.ba_pages);
+  s.s_ba_count = DBuf<uint32_t>(s.ctx, s.ba_pages);
   for (PageDesc& d : s.pages) {
     d.src = reinterpret_cast<uint64_t>(s.d_pq.p) + d.src;
     d.dst = reinterpret_cast<uint64_t>(s.d_arena.p) + d.dst;
@@ -690,6 +706,10 @@ static dr_state* replay(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, int6
     pa.dict_ptr = dict_ptr.p;
     pa.dict_len = dict_len.p;
     pa.error = pq_err.p;
+    pa.ba_vals = s.s_ba_vals.p;
+    pa.ba_hit = s.s_ba_hit.p;
+    pa.ba_ok = s.s_ba_ok.p;
+    pa.ba_count = s.s_ba_count.p;
     launch_page_copy(s.d_copy.p, uint32_t(s.copy_jobs.size()), stream);
     if (!s.snap_pages.empty()) {
       s.s_pages_bad.zero(stream);
@@ -700,6 +720,8 @@ static dr_state* replay(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, int6
       launch_snappy(sa, stream, scratch.p);
     }
     ctx->mark("pq_inflate");
+    if (s.ba_pages) launch_ba_bounds(pa, stream);
+    ctx->mark("pq_bounds");
     launch_pq_dict(pa, stream);
     launch_pq_data(pa, stream);
     ctx->mark("pq_decode");

@@ -134,6 +134,144 @@ struct ByteArrayWalker {
   }
 };
 
+// ---- parallel boundaries of length-prefixed BYTE_ARRAY values -----------------------------------------
+// PLAIN BYTE_ARRAY values are [u32 len][bytes]...: a serial chain. For strings without NUL bytes and
+// lengths < 64 KiB every true boundary p has b[p+2] == b[p+3] == 0 while no position inside a string
+// does (paths are URI strings). One workgroup per page: candidates are positions with two zero bytes
+// at +2/+3 whose value fits the page; a candidate is kept if it is the region start or the target of
+// another candidate, and if its own successor is a candidate or the region end. The survivors are
+// compacted in order and the chain is then VALIDATED -- B[0] = start, B[k+1] = B[k] + 4 + len(B[k]),
+// the last value ends at the region end -- which proves B equals the true chain. Any failure
+// (NUL bytes, huge values, corrupt data) leaves ba_ok = 0 and the serial walker decodes the page.
+constexpr int BA_T = 256;
+
+__device__ __forceinline__ bool ba_region(const PageDesc& pg, const uint8_t** b, const uint8_t** e) {
+  const uint8_t* p = reinterpret_cast<const uint8_t*>(pg.dst);
+  const uint8_t* end = p + pg.usize;
+  if (pg.kind == PG_DATA_V2) {
+    p += pg.v2_rep_len + pg.v2_def_len;
+  } else if (pg.kind != PG_DICT && pg.max_def > 0) {
+    if (end - p < 4) return false;
+    const uint32_t l = load_u32(p);
+    if (uint64_t(end - p - 4) < l) return false;
+    p += 4 + l;
+  }
+  *b = p;
+  *e = end;
+  return true;
+}
+
+__device__ __forceinline__ bool ba_cand(const uint8_t* b, uint64_t S, uint64_t p, uint64_t* next) {
+  if (p + 4 > S) return false;
+  const uint32_t w = load_u32(b + p);
+  if (w >> 16) return false;  // bytes +2/+3 must be zero
+  const uint64_t nx = p + 4 + w;
+  if (nx > S) return false;
+  *next = nx;
+  return true;
+}
+
+__global__ void __launch_bounds__(BA_T) k_ba_bounds(ParquetArgs a) {
+  const PageDesc& pg = a.pages[blockIdx.x];
+  if (!pg.ba) return;
+  __shared__ uint32_t wcnt[BA_T];
+  __shared__ uint32_t s_bad, s_n;
+  const int t = threadIdx.x;
+  const uint8_t *b, *e;
+  if (!ba_region(pg, &b, &e)) { if (t == 0) a.ba_ok[pg.ba_slot] = 0; return; }
+  const uint64_t S = uint64_t(e - b);
+  uint32_t* hit = a.ba_hit + pg.hit_base;
+  uint32_t* vals = a.ba_vals + pg.ba_base;
+  const uint32_t cap = pg.usize / 4 + 2;  // slots reserved for this page by the planner
+  const uint64_t nw = S / 32 + 2;
+  for (uint64_t i = t; i < nw; i += BA_T) hit[i] = 0;
+  if (t == 0) s_bad = 0;
+  __syncthreads();
+  // Each thread scans 16 consecutive positions per 4 KiB segment (coalesced 16-byte loads); a
+  // zero-byte-pair mask finds the rare candidates, which are then checked exactly.
+  constexpr uint64_t SEGB = uint64_t(BA_T) * 16;
+  auto cand_mask = [&](uint64_t p0) -> uint32_t {  // bit j: position p0 + j has zero bytes at +2/+3
+    if (p0 >= S) return 0u;
+    uint32_t w[5];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) w[q] = load_u32(b + p0 + 4 * q);  // buffers are padded
+    uint32_t z = 0;
+#pragma unroll
+    for (int q = 0; q < 5; ++q)
+#pragma unroll
+      for (int y = 0; y < 4; ++y) z |= uint32_t(((w[q] >> (8 * y)) & 0xff) == 0) << (4 * q + y);
+    return ((z & (z >> 1)) >> 2) & 0xffffu;
+  };
+  // pass 1: every candidate marks its successor
+  for (uint64_t seg = 0; seg < S; seg += SEGB) {
+    const uint64_t p0 = seg + 16ull * t;
+    uint32_t m = cand_mask(p0);
+    while (m) {
+      const int j = __builtin_ctz(m);
+      m &= m - 1;
+      uint64_t nx;
+      if (ba_cand(b, S, p0 + j, &nx) && nx < S) atomicOr(&hit[nx >> 5], 1u << (nx & 31));
+    }
+  }
+  __threadfence();
+  __syncthreads();
+  // pass 2: survivors, scanned per segment, written in order
+  auto keep = [&](uint64_t p) -> bool {
+    uint64_t nx;
+    if (!ba_cand(b, S, p, &nx)) return false;
+    if (p != 0 && !((__hip_atomic_load(&hit[p >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (p & 31)) & 1u)) return false;
+    uint64_t nn;
+    return nx == S || ba_cand(b, S, nx, &nn);
+  };
+  const uint64_t boff0 = uint64_t(b - reinterpret_cast<const uint8_t*>(pg.dst));
+  uint32_t carry = 0;
+  const int lane = t & 63, wv = t >> 6;
+  for (uint64_t seg = 0; seg < S; seg += SEGB) {
+    const uint64_t p0 = seg + 16ull * t;
+    uint32_t m = cand_mask(p0), km = 0;
+    while (m) {
+      const int j = __builtin_ctz(m);
+      m &= m - 1;
+      if (keep(p0 + j)) km |= 1u << j;
+    }
+    const uint32_t c = __builtin_popcount(km);
+    uint32_t incl = c;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    if (lane == 63) wcnt[wv] = incl;
+    __syncthreads();
+    uint32_t woff = 0, tot = 0;
+    for (int k = 0; k < BA_T / 64; ++k) { if (k < wv) woff += wcnt[k]; tot += wcnt[k]; }
+    uint32_t o = carry + woff + incl - c;
+    while (km) {
+      const int j = __builtin_ctz(km);
+      km &= km - 1;
+      if (o < cap) vals[o] = uint32_t(p0 + j + boff0);
+      ++o;
+    }
+    carry += tot;
+    __syncthreads();
+  }
+  if (t == 0) { a.ba_count[pg.ba_slot] = carry; s_n = carry; }
+  __threadfence();
+  __syncthreads();
+  // validation of the chain (a true chain has at most usize/4 values: each takes >= 4 bytes)
+  if (s_n > cap) { if (t == 0) a.ba_ok[pg.ba_slot] = 0; return; }
+  const uint32_t n = s_n;
+  const uint64_t boff = uint64_t(b - reinterpret_cast<const uint8_t*>(pg.dst));
+  if (S > 0 && (n == 0 || vals[0] != boff)) s_bad = 1;
+  for (uint32_t k = t; k < n; k += BA_T) {
+    const uint64_t p = vals[k] - boff;
+    const uint64_t nx = p + 4 + load_u32(b + p);
+    const uint64_t want = k + 1 < n ? uint64_t(vals[k + 1]) - boff : S;
+    if (nx != want) s_bad = 1;
+  }
+  __syncthreads();
+  if (t == 0) a.ba_ok[pg.ba_slot] = s_bad ? 0u : 1u;
+}
+
 // ---- dictionary pages --------------------------------------------------------------------------------
 __global__ void __launch_bounds__(64) k_pq_dict(ParquetArgs a) {
   const uint32_t i = blockIdx.x;
@@ -143,6 +281,15 @@ __global__ void __launch_bounds__(64) k_pq_dict(ParquetArgs a) {
   const int lane = threadIdx.x;
   const uint8_t* p = reinterpret_cast<const uint8_t*>(pg.dst);
   const uint8_t* end = p + pg.usize;
+  if (pg.phys == 6 && pg.ba && a.ba_ok[pg.ba_slot] && a.ba_count[pg.ba_slot] == pg.num_values) {
+    const uint32_t* vals = a.ba_vals + pg.ba_base;  // boundaries found in parallel (k_ba_bounds)
+    for (uint32_t k = lane; k < pg.num_values; k += 64) {
+      const uint32_t off = vals[k];
+      a.dict_ptr[pg.dict_base + k] = reinterpret_cast<uint64_t>(p + off + 4);
+      a.dict_len[pg.dict_base + k] = load_u32(p + off);
+    }
+    return;
+  }
   if (pg.phys == 6) {  // BYTE_ARRAY: chain walk
     __shared__ uint64_t sp[64];
     __shared__ uint32_t sl[64];
@@ -221,7 +368,11 @@ __global__ void __launch_bounds__(64) k_pq_data(ParquetArgs a) {
   const uint32_t dict_n = dict ? a.pages[pg.dict].num_values : 0;
   const uint32_t width = pg.phys == 2 ? 8 : pg.phys == 1 ? 4 : 0;
   ByteArrayWalker wk;
-  if (pg.phys == 6 && !dict) wk.init(p, end, lane);
+  const bool ba_fast = pg.phys == 6 && !dict && pg.ba && a.ba_ok[pg.ba_slot];
+  const uint32_t* ba_vals = a.ba_vals + pg.ba_base;
+  const uint32_t ba_n = ba_fast ? a.ba_count[pg.ba_slot] : 0;
+  const uint8_t* body = reinterpret_cast<const uint8_t*>(pg.dst);
+  if (pg.phys == 6 && !dict && !ba_fast) wk.init(p, end, lane);
   uint64_t vbase = 0;  // values consumed before this segment (PLAIN fixed / boolean)
   for (uint32_t s0 = 0; s0 < pg.num_values; s0 += SEG) {
     const uint32_t n = min(SEG, pg.num_values - s0);
@@ -245,6 +396,8 @@ __global__ void __launch_bounds__(64) k_pq_data(ParquetArgs a) {
     if (dict || rle_bool) {
       ir.expand(vlen, nv, lane);  // dictionary indices / booleans (reuse vlen as scratch)
       if (ir.bad) { if (lane == 0) set_err(a.error, dict ? PQE_DICT : PQE_VALUES); return; }
+    } else if (ba_fast) {
+      if (vbase + nv > ba_n) { if (lane == 0) set_err(a.error, PQE_VALUES); return; }
     } else if (pg.phys == 6) {
       for (uint32_t k = 0; k < nv; ++k) {
         uint32_t l;
@@ -278,6 +431,10 @@ __global__ void __launch_bounds__(64) k_pq_data(ParquetArgs a) {
         }
       } else if (rle_bool) {
         col.ival[row] = vlen[k] & 1;
+      } else if (ba_fast) {
+        const uint32_t off = ba_vals[vbase + k];
+        col.sptr[row] = reinterpret_cast<uint64_t>(body + off + 4);
+        col.slen[row] = load_u32(body + off);
       } else if (pg.phys == 6) {
         col.sptr[row] = vptr[k];
         col.slen[row] = vlen[k];
@@ -352,6 +509,9 @@ __global__ void k_ckpt_assemble(CkptAssembleArgs a) {
 
 }  // namespace dev
 
+void launch_ba_bounds(const ParquetArgs& a, hipStream_t st) {
+  if (a.npages) hipLaunchKernelGGL(dev::k_ba_bounds, dim3(a.npages), dim3(dev::BA_T), 0, st, a);
+}
 void launch_pq_dict(const ParquetArgs& a, hipStream_t st) {
   if (a.npages) hipLaunchKernelGGL(dev::k_pq_dict, dim3(a.npages), dim3(64), 0, st, a);
 }

@@ -70,6 +70,11 @@ struct PageDesc {
   uint64_t row_base;     // first checkpoint row of the page (flat columns)
   int32_t v2_def_len, v2_rep_len, v2_compressed;
   uint32_t dict_base;    // dictionary pages: first slot in the dictionary pool
+  // PLAIN BYTE_ARRAY pages (data or dictionary): parallel boundary detection scratch
+  int32_t ba;            // 1 if this page's values are length-prefixed byte arrays
+  uint32_t ba_slot;      // index into ba_ok / ba_count
+  uint64_t ba_base;      // first u32 slot of this page's value offsets
+  uint64_t hit_base;     // first u32 word of this page's hit bitmap
 };
 
 // Decoded flat column (max_rep == 0): one entry per checkpoint row.
@@ -88,7 +93,12 @@ struct ParquetArgs {
   uint64_t* dict_ptr;    // dictionary pool (BYTE_ARRAY: address; INT: value)
   uint32_t* dict_len;
   uint32_t* error;       // first error code (0 = ok)
+  uint32_t* ba_vals;     // value offsets (relative to the page's decompressed body)
+  uint32_t* ba_hit;      // hit bitmaps
+  uint32_t* ba_ok;       // [pages with ba] 1 = boundaries found and validated
+  uint32_t* ba_count;    // [pages with ba] number of values found
 };
+void launch_ba_bounds(const ParquetArgs& a, hipStream_t st);
 
 // SNAPPY pages (k_snappy.hip). `in` points past the varint length preamble.
 struct SnapPage {

@@ -26,6 +26,18 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
+# Stages whose timed region is exactly one kernel launch: the roofline is reported for the slowest
+# of these (achieved = its algorithmic bytes / its hipEvent-timed duration on the replay stream).
+STAGE_KERNEL = {
+    "json_parse": "k_json_parse",
+    "json_newlines": "k_json_newlines",
+    "pq_bounds": "k_ba_bounds",
+    "ckpt_assemble": "k_ckpt_assemble",
+    "partition_hist": "k_bucket_hist",
+    "partition_scatter": "k_bucket_scatter",
+    "reduce": "k_bucket_reduce",
+}
+
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
@@ -69,6 +81,33 @@ def algorithmic_bytes(stage, plan, counts):
     }.get(stage)
 
 
+def pmc_traffic(pmc_dir, kernel):
+    """Per-launch HBM bytes of `kernel` from committed rocprofv3 --pmc passes (FETCH_SIZE and
+    WRITE_SIZE in separate runs of this same bench command). FETCH_SIZE is doubled: on gfx950 it
+    tallies 128-B requests at 64 B (MI355X_MICROARCH.md, HBM section). Returns None when absent."""
+    import csv
+    import glob
+    if not pmc_dir or not os.path.isdir(pmc_dir):
+        return None
+    per = {}
+    for fn in glob.glob(os.path.join(pmc_dir, "**", "*counter_collection.csv"), recursive=True):
+        with open(fn) as f:
+            for row in csv.DictReader(f):
+                name = row.get("Kernel_Name", "")
+                if kernel not in name:
+                    continue
+                c = row.get("Counter_Name")
+                v = float(row.get("Counter_Value", 0) or 0)
+                d = per.setdefault(c, {})
+                key = (fn, row.get("Dispatch_Id"))
+                d[key] = d.get(key, 0.0) + v
+    if "FETCH_SIZE" not in per or "WRITE_SIZE" not in per:
+        return None
+    avg = {c: sum(v.values()) / len(v) for c, v in per.items()}
+    # FETCH_SIZE / WRITE_SIZE are in KiB
+    return int(2 * avg["FETCH_SIZE"] * 1024 + avg["WRITE_SIZE"] * 1024)
+
+
 def cpu_baseline(config, sample_scale, seed, tmp):
     """Times oracle/_build/replay_oracle on a bounded sample of the same workload."""
     exe = os.path.join(ROOT, "oracle", "_build", "replay_oracle")
@@ -105,7 +144,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", type=int, default=3)
     ap.add_argument("--scale", type=float, default=1.0)
-    ap.add_argument("--cpu-sample-scale", type=float, default=0.1)
+    ap.add_argument("--cpu-sample-scale", type=float, default=0.25)
+    ap.add_argument("--pmc-dir", default=os.path.join(ROOT, "profiles", "r01", "pmc"))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workdir", default=os.environ.get("DR_BENCH_DIR", os.path.join(tempfile.gettempdir(), "dr_bench")))
     args = ap.parse_args()
@@ -166,7 +206,7 @@ def main():
     ms_per_step = elapsed / args.steps * 1000.0
     if rank != 0:
         return
-    dom = max(stage_ms, key=stage_ms.get)
+    dom = max((k for k in stage_ms if k in STAGE_KERNEL), key=stage_ms.get)
     kernels = {}
     for k, ms in stage_ms.items():
         b = algorithmic_bytes(k, plan, counts)
@@ -176,9 +216,12 @@ def main():
             kernels[k]["gbs"] = round(b / (ms * 1e-3) / 1e9, 1)
     db = algorithmic_bytes(dom, plan, counts) or 0
     achieved = db / (stage_ms[dom] * 1e-3) / 1e9 if db else None
-    roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1) if achieved else None,
+    roofline = {"bound": "hbm", "kernel": STAGE_KERNEL[dom], "stage": dom,
+                "achieved": round(achieved, 1) if achieved else None,
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None, "traffic": None}
+                "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                "traffic": pmc_traffic(args.pmc_dir, STAGE_KERNEL[dom]),
+                "algo_bytes": db, "avg_launch_ms": round(stage_ms[dom], 4)}
     cpu = None
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(args.config, args.cpu_sample_scale, S.BASE_SEED + args.config, args.workdir)

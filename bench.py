@@ -6,8 +6,10 @@ resident in HBM: JSON tokenization (K1), checkpoint page inflate + decode (K2), 
 partition (K3), per-bucket last-writer-wins + retention + compaction + computedState counters
 (K4/K6). `value` = log actions replayed per second over all ranks.
 
-Multi-GPU (torchrun, one rank per GPU): each rank replays its own shard (an independent table of
-the same shape, seed + rank): weak scaling, no data-path collective.
+Multi-GPU (torchrun, one rank per GPU): the same table is path-hash sharded over the ranks
+(delta_amd/sharded.py): each rank stages a contiguous slice of the segment, parses
+it, sends each file action to owner(path) with an RCCL all-to-all, reduces its shard and returns
+the verdicts. Strong scaling: `value` = table actions per step / max-over-ranks step time.
 
 cpu_baseline: the C++ restatement of the reference replay (oracle/replay_oracle.cpp, 50 hash
 partitions x unordered_map last-writer-wins, all host threads) timed on a bounded sample of the
@@ -157,27 +159,51 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
+        # DR_BENCH_BACKEND=gloo rehearses the multi-rank path on a single GPU (host-staged exchange)
+        backend = os.environ.get("DR_BENCH_BACKEND", "nccl")
+        local = local % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     from delta_amd.delta_log import Engine
     from delta_amd.testing import synth as S
 
-    seed = S.BASE_SEED + args.config + 1000 * rank
-    table = os.path.join(args.workdir, "c%d_s%g_r%d" % (args.config, args.scale, rank))
+    seed = S.BASE_SEED + args.config
+    table = os.path.join(args.workdir, "c%d_s%g" % (args.config, args.scale))
+    if rank == 0:
+        exp = build_table(table, args.config, args.scale, seed)
+    if dist:
+        dist.barrier()
     exp = build_table(table, args.config, args.scale, seed)
     eng = Engine.get(local)
-    staged = eng.stage_log(os.path.join(table, "_delta_log"))
-    plan = staged.plan()
+    log_path = os.path.join(table, "_delta_log")
     cutoff = exp["min_file_retention_timestamp"]
-    counts = None
-    for i in range(args.warmup):
-        st = staged.replay(cutoff)
-        counts = st.counts
-        st.release()
-    if counts is None:
-        st = staged.replay(cutoff)
-        counts = st.counts
-        st.release()
+    if world == 1:
+        staged = eng.stage_log(log_path)
+
+        def step():
+            st = staged.replay(cutoff)
+            c = st.counts
+            st.release()
+            return c, c
+    else:
+        # the table is path-hash sharded over the ranks: each rank stages its
+        # contiguous slice of the segment; one step = parse + RCCL all-to-all + reduce + verdicts
+        from delta_amd.sharded import Exchange, replay_sharded, stage_shard
+        staged = stage_shard(eng, log_path, world, rank)
+        ex = Exchange()
+
+        def step():
+            st = replay_sharded(staged, cutoff, ex)
+            c, lc = st.counts, st.local.counts
+            st.release()
+            return c, lc
+    plan = staged.plan()  # this rank's slice (roofline accounting is per rank 0's kernels)
+    counts = local_counts = None
+    for i in range(max(args.warmup, 1)):
+        counts, local_counts = step()
     for k in ("num_files", "num_removes", "size_in_bytes", "num_actions", "num_file_actions"):
         assert counts[k] == exp[k], (k, counts[k], exp[k])
     eng.set_timing(True)
@@ -187,21 +213,21 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        st = staged.replay(cutoff)
+        step()
         for k, v in eng.last_timings().items():
             stage_ms[k] = stage_ms.get(k, 0.0) + v
-        st.release()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device="cuda" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     eng.set_timing(False)
     stage_ms = {k: v / args.steps for k, v in stage_ms.items()}
-    total_actions = counts["num_actions"] * args.steps * world
+    total_actions = counts["num_actions"] * args.steps  # table-wide actions per step
     value = total_actions / elapsed
     ms_per_step = elapsed / args.steps * 1000.0
     if rank != 0:
@@ -209,18 +235,19 @@ def main():
     dom = max((k for k in stage_ms if k in STAGE_KERNEL), key=stage_ms.get)
     kernels = {}
     for k, ms in stage_ms.items():
-        b = algorithmic_bytes(k, plan, counts)
+        b = algorithmic_bytes(k, plan, local_counts)
         kernels[k] = {"ms": round(ms, 4)}
         if b:
             kernels[k]["algo_bytes"] = b
             kernels[k]["gbs"] = round(b / (ms * 1e-3) / 1e9, 1)
-    db = algorithmic_bytes(dom, plan, counts) or 0
+    db = algorithmic_bytes(dom, plan, local_counts) or 0
     achieved = db / (stage_ms[dom] * 1e-3) / 1e9 if db else None
     roofline = {"bound": "hbm", "kernel": STAGE_KERNEL[dom], "stage": dom,
                 "achieved": round(achieved, 1) if achieved else None,
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                "traffic": pmc_traffic(args.pmc_dir, STAGE_KERNEL[dom]),
+                # committed PMC passes are of the default single-GPU command
+                "traffic": pmc_traffic(args.pmc_dir, STAGE_KERNEL[dom]) if world == 1 else None,
                 "algo_bytes": db, "avg_launch_ms": round(stage_ms[dom], 4)}
     cpu = None
     if not args.no_cpu_baseline and world == 1:
@@ -229,13 +256,14 @@ def main():
         "metric": "log actions replayed/sec + achieved HBM GB/s, 1/2/4/8 GPU, 10M-file table",
         "value": round(value, 1), "unit": "actions/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "u8/int64", "data": "synthetic",
-        "config": {"workload": "config %d: %d-file checkpoint + JSON commits, %d actions/rank, "
-                               "30%% remove/re-add churn, retention cutoff" % (args.config, plan["checkpoint_rows"] - 2,
-                                                                             counts["num_actions"]),
-                   "scale": args.scale, "actions_per_rank": counts["num_actions"],
-                   "json_bytes": plan["json_bytes"], "checkpoint_bytes": plan["checkpoint_bytes"],
-                   "parallelism": "dp%d (independent table shard per rank)" % world},
+        "scaling": "strong", "vs_baseline": None, "dtype": "u8/int64", "data": "synthetic",
+        "config": {"workload": "config %d: checkpoint + JSON commits, %d actions -> %d live files, "
+                               "30%% remove/re-add churn, retention cutoff" % (args.config, counts["num_actions"],
+                                                                             counts["num_files"]),
+                   "scale": args.scale, "actions": counts["num_actions"],
+                   "json_bytes": exp["json_bytes"], "checkpoint_bytes": exp["checkpoint_bytes"],
+                   "parallelism": ("path-hash shards over %d GPUs (RCCL all-to-all)" % world) if world > 1
+                   else "single GPU"},
         "roofline": roofline,
         "cpu_baseline": cpu,
         "kernels": kernels,

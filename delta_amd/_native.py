@@ -29,7 +29,10 @@ SYMBOLS = [
     "dr_replay_staged",
     "dr_replay", "dr_state_release", "dr_state_counts", "dr_state_nonfile_json",
     "dr_state_export", "dr_filter", "dr_free", "dr_last_timings", "dr_set_timing",
+    "dr_shard_plan", "dr_stage_log_shard", "dr_shard_begin", "dr_shard_pack", "dr_shard_reduce",
+    "dr_shard_finish", "dr_shard_release",
 ]
+DR_SHARD_REC_BYTES = 32
 
 
 class dr_file(C.Structure):
@@ -78,9 +81,31 @@ class dr_predicate(C.Structure):
                 ("lit_str_off", _P64), ("lit_str_bytes", _PU8)]
 
 
+def hip_runtimes() -> list:
+    """Distinct libamdhip64 files mapped into this process."""
+    seen = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                p = line.split()[-1]
+                if "libamdhip64" in p:
+                    seen.add(os.path.realpath(p))
+    except OSError:
+        pass
+    return sorted(seen)
+
+
 def load(path: str = LIB_PATH) -> C.CDLL:
     if not os.path.exists(path):
         raise ImportError("libdeltareplay.so is not built (%s); run `make` or __graft_entry__.build()" % path)
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64.so.7 (DT_NEEDED
+    # "libamdhip64.so"), which the loader does not match against /opt/rocm's copy. Loading torch
+    # first makes libdeltareplay's DT_NEEDED "libamdhip64.so.7" resolve to torch's runtime, so
+    # device buffers can be shared with torch.distributed (RCCL) in the multi-GPU path.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(path)
     vp, i32, i64, u64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64
     sig = {
@@ -104,6 +129,13 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "dr_free": ([vp], None),
         "dr_last_timings": ([vp, C.c_char_p, u64, C.POINTER(C.c_float), i32, C.POINTER(i32)], C.c_int),
         "dr_set_timing": ([vp, i32], C.c_int),
+        "dr_shard_plan": ([vp, C.c_char_p, i64, i32, C.c_char_p, u64, C.POINTER(u64)], C.c_int),
+        "dr_stage_log_shard": ([vp, C.c_char_p, i64, i32, i32, C.POINTER(vp)], C.c_int),
+        "dr_shard_begin": ([vp, vp, i32, C.POINTER(vp), C.POINTER(u64), C.POINTER(u64)], C.c_int),
+        "dr_shard_pack": ([vp, vp, vp], C.c_int),
+        "dr_shard_reduce": ([vp, vp, u64, vp, u64, i64, vp], C.c_int),
+        "dr_shard_finish": ([vp, vp, C.POINTER(vp)], C.c_int),
+        "dr_shard_release": ([vp], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

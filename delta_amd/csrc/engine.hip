@@ -156,6 +156,9 @@ struct CkPart {
   uint64_t off = 0, len = 0;   // within the concatenated checkpoint bytes
   pq::FileMeta meta;
   uint64_t row_base = 0;
+  int32_t rg_lo = 0, rg_hi = -1;   // row groups [rg_lo, rg_hi) of this part are staged (-1: all)
+  uint64_t rows = 0;               // rows in the staged row groups
+  size_t rg_end() const { return rg_hi < 0 ? meta.row_groups.size() : std::min<size_t>(size_t(rg_hi), meta.row_groups.size()); }
 };
 
 struct NonFileAction {
@@ -258,7 +261,8 @@ static void decode_ck_nonfile(StagedData& s, CkPart& part, uint64_t base_action)
   const uint8_t* file = s.h_pq.data() + part.off;
   const pq::FileMeta& m = part.meta;
   int64_t rg_base = 0;
-  for (const pq::RowGroup& rg : m.row_groups) {
+  for (size_t gi = size_t(part.rg_lo); gi < part.rg_end(); ++gi) {
+    const pq::RowGroup& rg = m.row_groups[gi];
     auto col = [&](const std::string& path) -> const pq::ColumnChunk* {
       for (auto& c : rg.cols) if (c.path == path) return &c;
       return nullptr;
@@ -396,7 +400,9 @@ static void plan_checkpoint(StagedData& s) {
   for (CkPart& part : s.parts) {
     part.meta = pq::parse_footer(s.h_pq.data() + part.off, part.len);
     part.row_base = row_base;
-    row_base += uint64_t(part.meta.num_rows);
+    part.rows = 0;
+    for (size_t gi = size_t(part.rg_lo); gi < part.rg_end(); ++gi) part.rows += uint64_t(part.meta.row_groups[gi].num_rows);
+    row_base += part.rows;
   }
   s.ck_rows = row_base;
   if (s.parts.empty()) return;
@@ -418,7 +424,8 @@ static void plan_checkpoint(StagedData& s) {
   for (CkPart& part : s.parts) {
     const uint8_t* file = s.h_pq.data() + part.off;
     uint64_t rg_row = part.row_base;
-    for (const pq::RowGroup& rg : part.meta.row_groups) {
+    for (size_t gi = size_t(part.rg_lo); gi < part.rg_end(); ++gi) {
+      const pq::RowGroup& rg = part.meta.row_groups[gi];
       for (int c = 0; c < HC_N; ++c) {
         if (!s.has_col[c]) continue;
         const pq::ColumnChunk* cc = nullptr;
@@ -542,10 +549,13 @@ static void plan_checkpoint(StagedData& s) {
   if (!s.pages.empty())
     HIP_OK(hipMemcpyAsync(s.d_pages.p, s.pages.data(), s.pages.size() * sizeof(PageDesc), hipMemcpyHostToDevice,
                           s.ctx->stream));
-  for (CkPart& part : s.parts) decode_ck_nonfile(s, part, part.row_base);
+  for (CkPart& part : s.parts) decode_ck_nonfile(s, part, 0);  // entry rows already include part.row_base
 }
 
-static std::shared_ptr<StagedData> stage_files(dr_ctx* ctx, const dr_file* files, int32_t nfiles) {
+// rg_lo / rg_hi (optional, per file): stage only row groups [rg_lo, rg_hi) of a checkpoint part
+// (a multi-GPU shard's slice of the checkpoint; -1 = to the end).
+static std::shared_ptr<StagedData> stage_files(dr_ctx* ctx, const dr_file* files, int32_t nfiles,
+                                               const int32_t* rg_lo = nullptr, const int32_t* rg_hi = nullptr) {
   auto s = std::make_shared<StagedData>();
   s->ctx = ctx;
   std::vector<const dr_file*> js, cks;
@@ -566,6 +576,10 @@ static std::shared_ptr<StagedData> stage_files(dr_ctx* ctx, const dr_file* files
     CkPart p;
     p.off = s->h_pq.size();
     p.len = f->len;
+    if (rg_lo) {
+      p.rg_lo = rg_lo[f - files];
+      p.rg_hi = rg_hi[f - files];
+    }
     s->h_pq.insert(s->h_pq.end(), f->data, f->data + f->len);
     s->h_pq.resize((s->h_pq.size() + 15) & ~size_t(15), 0);
     s->parts.push_back(p);
@@ -629,20 +643,20 @@ static void reduce_nonfile(dr_state& st, std::vector<NonFileAction>& acts, bool 
                                     (long long)st.counts.version));
 }
 
-static dr_state* replay(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, int64_t cutoff, uint32_t flags) {
+static uint64_t scan_scratch_for(uint64_t n) { return scan_scratch_bytes(std::max<uint64_t>(n, uint64_t(1) << 23)); }
+
+// K1 + K2 + canonicalisation: fills st's per-action arrays (checkpoint rows first, then JSON lines)
+// and collects the non-file actions (protocol / metaData / txn) on the host in replay order.
+static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr_state* st,
+                          std::vector<NonFileAction>& nf) {
   StagedData& s = *sp;
   hipStream_t stream = ctx->stream;
-  auto st = std::make_unique<dr_state>();
-  st->ctx = ctx;
-  st->staged = sp;
-  st->counts.version = s.version;
-  ctx->mark("start");
   // ---- K1a: newline index ----
   const uint64_t json_len = s.h_json.size();
   const uint64_t nbj = json_num_blocks(json_len);
   DBuf<uint32_t> jcounts(ctx, nbj + 1);
   DBuf<uint64_t> joff(ctx, nbj + 1);
-  DBuf<uint8_t> scratch(ctx, scan_scratch_bytes(std::max<uint64_t>(nbj, uint64_t(1) << 23)));
+  DBuf<uint8_t> scratch(ctx, scan_scratch_for(nbj));
   uint64_t nlines = 0;
   if (nbj) {
     launch_json_count(s.d_json.p, json_len, jcounts.p, stream);
@@ -757,6 +771,52 @@ static dr_state* replay(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, int6
     launch_canon(cg, stream);
     ctx->mark("canon");
   }
+  // ---- non-file actions (host): checkpoint rows first, then JSON lines in order ----
+  nf = s.ck_nonfile;
+  const uint64_t nnf = std::min<uint64_t>(cnt[2], nlines);
+  if (nnf) {
+    std::vector<uint64_t> lines = d2h(nonfile.p, nnf, stream);
+    std::sort(lines.begin(), lines.end());
+    DBuf<uint64_t> dof(ctx, nnf);
+    for (uint64_t& x : lines) x += R;  // action indices
+    DBuf<uint64_t> didx(ctx, nnf);
+    HIP_OK(hipMemcpyAsync(didx.p, lines.data(), nnf * 8, hipMemcpyHostToDevice, stream));
+    launch_gather_u64_by64(st->src_off.p, didx.p, nnf, dof.p, stream);
+    std::vector<uint64_t> offs = d2h(dof.p, nnf, stream);
+    for (uint64_t k = 0; k < nnf; ++k) {
+      const uint64_t li = lines[k] - R;
+      const uint64_t b = offs[k];
+      uint64_t e = b;
+      while (e < json_len && s.h_json[e] != '\n') ++e;
+      JVal v;
+      std::string perr;
+      if (!json_parse(reinterpret_cast<const char*>(s.h_json.data() + b), e - b, &v, &perr) || v.t != JVal::OBJ)
+        continue;  // malformed non-file line: PERMISSIVE null row
+      // unwrap priority among non-file kinds: metaData > txn > protocol
+      const char* names[3] = {"metaData", "txn", "protocol"};
+      const int kinds[3] = {3, 4, 5};
+      for (int k2 = 0; k2 < 3; ++k2) {
+        const JVal* x = v.get(names[k2]);
+        if (x && x->t != JVal::NUL) {
+          NonFileAction a;
+          a.kind = kinds[k2];
+          a.order = R + li;
+          a.val = *x;
+          a.json = std::string("{\"") + names[k2] + "\":" + json_dump(*x) + "}";
+          nf.push_back(std::move(a));
+          break;
+        }
+      }
+    }
+  }
+}
+
+// K3 (hash partition) + K4 (per-bucket last-writer-wins, retention) + compaction over st's action
+// arrays; fills st->live / st->tomb and the file counters.
+static void reduce_actions(dr_ctx* ctx, dr_state* st, int64_t cutoff) {
+  hipStream_t stream = ctx->stream;
+  const uint64_t N = st->n_actions;
+  DBuf<uint8_t> scratch(ctx, scan_scratch_for(0));
   // ---- K3: partition by hash bucket ----
   const int bits = bucket_bits_for(N);
   const uint32_t nb = 1u << bits;
@@ -812,45 +872,22 @@ static dr_state* replay(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, int6
   st->counts.tomb_key_sum = tot[6];
   st->counts.num_actions = int64_t(N);
   st->counts.num_file_actions = int64_t(n_file_actions);
-  // ---- non-file actions (host): checkpoint rows first, then JSON lines in order ----
-  std::vector<NonFileAction> nf = s.ck_nonfile;
-  const uint64_t nnf = std::min<uint64_t>(cnt[2], nlines);
-  if (nnf) {
-    std::vector<uint64_t> lines = d2h(nonfile.p, nnf, stream);
-    std::sort(lines.begin(), lines.end());
-    DBuf<uint64_t> dl(ctx, nnf), dof(ctx, nnf);
-    HIP_OK(hipMemcpyAsync(dl.p, lines.data(), nnf * 8, hipMemcpyHostToDevice, stream));
-    for (uint64_t& x : lines) x += R;  // action indices
-    DBuf<uint64_t> didx(ctx, nnf);
-    HIP_OK(hipMemcpyAsync(didx.p, lines.data(), nnf * 8, hipMemcpyHostToDevice, stream));
-    launch_gather_u64_by64(st->src_off.p, didx.p, nnf, dof.p, stream);
-    std::vector<uint64_t> offs = d2h(dof.p, nnf, stream);
-    for (uint64_t k = 0; k < nnf; ++k) {
-      const uint64_t li = lines[k] - R;
-      const uint64_t b = offs[k];
-      uint64_t e = b;
-      while (e < json_len && s.h_json[e] != '\n') ++e;
-      JVal v;
-      std::string perr;
-      if (!json_parse(reinterpret_cast<const char*>(s.h_json.data() + b), e - b, &v, &perr) || v.t != JVal::OBJ)
-        continue;  // malformed non-file line: PERMISSIVE null row
-      // unwrap priority among non-file kinds: metaData > txn > protocol
-      const char* names[3] = {"metaData", "txn", "protocol"};
-      const int kinds[3] = {3, 4, 5};
-      for (int k = 0; k < 3; ++k) {
-        const JVal* x = v.get(names[k]);
-        if (x && x->t != JVal::NUL) {
-          NonFileAction a;
-          a.kind = kinds[k];
-          a.order = R + li;
-          a.val = *x;
-          a.json = std::string("{\"") + names[k] + "\":" + json_dump(*x) + "}";
-          nf.push_back(std::move(a));
-          break;
-        }
-      }
-    }
-  }
+}
+
+static dr_state* new_state(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp) {
+  auto st = std::make_unique<dr_state>();
+  st->ctx = ctx;
+  st->staged = sp;
+  st->counts.version = sp ? sp->version : -1;
+  return st.release();
+}
+
+static dr_state* replay(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, int64_t cutoff, uint32_t flags) {
+  std::unique_ptr<dr_state> st(new_state(ctx, sp));
+  ctx->mark("start");
+  std::vector<NonFileAction> nf;
+  parse_actions(ctx, sp, st.get(), nf);
+  reduce_actions(ctx, st.get(), cutoff);
   reduce_nonfile(*st, nf, !(flags & DR_FLAG_NO_VALIDATION));
   ctx->mark("end");
   return st.release();
@@ -909,7 +946,8 @@ static void load_ck_side(StagedData& s, bool add, CkRows& out) {
   for (CkPart& part : s.parts) {
     const uint8_t* file = s.h_pq.data() + part.off;
     int64_t rg_base = int64_t(part.row_base);
-    for (const pq::RowGroup& rg : part.meta.row_groups) {
+    for (size_t gi = size_t(part.rg_lo); gi < part.rg_end(); ++gi) {
+      const pq::RowGroup& rg = part.meta.row_groups[gi];
       auto col = [&](const std::string& name, int depth, std::vector<pq::Entry>* v, const pq::Leaf** lf) {
         std::string path = std::string(pre) + name;
         const pq::Leaf* l = part.meta.leaf(path);
@@ -1035,6 +1073,237 @@ static void build_export(dr_state& st, int which) {
     ex.tags_entry_off.push_back(int64_t(ex.tags_val_null.size()));
   }
   ex.built = true;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// multi-GPU shards: contiguous slices of the replay order, then path-hash exchange
+// ---------------------------------------------------------------------------------------------------
+struct ShardUnit {
+  SegFile f;
+  int32_t rg_lo = 0, rg_hi = -1;   // checkpoint row groups [rg_lo, rg_hi); JSON: 0, -1
+  uint64_t weight = 0;
+};
+
+// Relative device cost of the units: JSON bytes are parsed once (weight 1/byte); checkpoint row
+// groups are weighted by the compressed bytes of the decoded columns (inflate + decode ~4x the
+// per-byte cost of JSON, measured) plus the per-row assembly.
+static std::vector<ShardUnit> shard_units(const std::string& log_path, const LogSegmentInfo& seg) {
+  std::vector<ShardUnit> units;
+  for (const SegFile& f : seg.checkpoint) {
+    const std::string p = log_path + "/" + f.name;
+    std::vector<uint8_t> tail = read_tail(p, 8);
+    if (tail.size() < 8 || memcmp(tail.data() + 4, "PAR1", 4)) fail(DR_E_PARQUET, fmt("%s is not a parquet file", f.name.c_str()));
+    uint32_t flen;
+    memcpy(&flen, tail.data(), 4);
+    std::vector<uint8_t> foot = read_tail(p, uint64_t(flen) + 8);
+    std::vector<uint8_t> buf(4 + foot.size());
+    memcpy(buf.data(), "PAR1", 4);
+    memcpy(buf.data() + 4, foot.data(), foot.size());
+    pq::FileMeta m = pq::parse_footer(buf.data(), buf.size());
+    if (m.row_groups.empty()) {
+      ShardUnit u;
+      u.f = f;
+      u.weight = 1;
+      units.push_back(u);
+      continue;
+    }
+    for (size_t g = 0; g < m.row_groups.size(); ++g) {
+      ShardUnit u;
+      u.f = f;
+      u.rg_lo = int32_t(g);
+      u.rg_hi = int32_t(g + 1);
+      uint64_t hot = 0;
+      for (auto& c : m.row_groups[g].cols)
+        for (int h = 0; h < HC_N; ++h)
+          if (c.path == kHotPath[h]) hot += uint64_t(c.total_compressed);
+      u.weight = 4 * hot + 16 * uint64_t(m.row_groups[g].num_rows) + 1;
+      units.push_back(u);
+    }
+  }
+  for (const SegFile& f : seg.deltas) {
+    ShardUnit u;
+    u.f = f;
+    u.weight = file_size(log_path + "/" + f.name) + 1;
+    units.push_back(u);
+  }
+  return units;
+}
+
+// Contiguous split of the units by weight: unit k goes to the rank whose share contains the
+// midpoint of its weight interval (deterministic: every rank computes the same plan).
+static std::vector<int32_t> shard_assign(const std::vector<ShardUnit>& units, int32_t world) {
+  uint64_t total = 0;
+  for (auto& u : units) total += u.weight;
+  std::vector<int32_t> owner(units.size(), 0);
+  uint64_t before = 0;
+  for (size_t k = 0; k < units.size(); ++k) {
+    const long double mid = (long double)before + (long double)units[k].weight / 2;
+    int32_t r = int32_t(mid * world / (long double)std::max<uint64_t>(total, 1));
+    owner[k] = std::min(std::max(r, 0), world - 1);
+    before += units[k].weight;
+  }
+  return owner;
+}
+
+static std::shared_ptr<StagedData> stage_shard(dr_ctx* ctx, const std::string& log_path, int64_t version,
+                                               int32_t world, int32_t rank) {
+  LogSegmentInfo seg = get_log_segment(log_path, version);
+  std::vector<ShardUnit> units = shard_units(log_path, seg);
+  std::vector<int32_t> owner = shard_assign(units, world);
+  // this rank's units: merge consecutive row groups of one checkpoint part
+  std::vector<ShardUnit> mine;
+  for (size_t k = 0; k < units.size(); ++k) {
+    if (owner[k] != rank) continue;
+    const ShardUnit& u = units[k];
+    if (!mine.empty() && mine.back().f.name == u.f.name && u.f.kind == DR_FILE_CHECKPOINT &&
+        mine.back().rg_hi == u.rg_lo) {
+      mine.back().rg_hi = u.rg_hi;
+      continue;
+    }
+    mine.push_back(u);
+  }
+  std::vector<std::vector<uint8_t>> bytes;
+  std::vector<dr_file> files;
+  std::vector<int32_t> lo, hi;
+  for (auto& u : mine) bytes.push_back(read_file(log_path + "/" + u.f.name));
+  for (size_t k = 0; k < mine.size(); ++k) {
+    files.push_back(dr_file{mine[k].f.version, mine[k].f.kind, mine[k].f.part, bytes[k].data(), bytes[k].size()});
+    lo.push_back(mine[k].rg_lo);
+    hi.push_back(mine[k].rg_hi);
+  }
+  auto s = stage_files(ctx, files.data(), int32_t(files.size()), lo.data(), hi.data());
+  s->version = seg.version;
+  return s;
+}
+
+struct dr_shard {
+  dr_ctx* ctx = nullptr;
+  std::shared_ptr<StagedData> staged;
+  std::unique_ptr<dr_state> st;
+  std::vector<NonFileAction> nf;
+  uint32_t world = 1;
+  uint64_t nsend = 0, send_path_bytes = 0;
+  DBuf<uint32_t> send_idx, send_plen;
+  DBuf<uint64_t> send_poff;
+  bool reduced = false;
+  dr_counts owner{};
+};
+
+static void shard_begin(dr_shard& sh, uint64_t* send_counts, uint64_t* send_bytes) {
+  dr_ctx* ctx = sh.ctx;
+  hipStream_t stream = ctx->stream;
+  sh.st.reset(new_state(ctx, sh.staged));
+  ctx->mark("start");
+  parse_actions(ctx, sh.staged, sh.st.get(), sh.nf);
+  dr_state& st = *sh.st;
+  const uint64_t N = st.n_actions;
+  const uint64_t nt = shard_tiles(N);
+  const uint64_t nc = uint64_t(sh.world) * nt;
+  DBuf<uint32_t> bcnt(ctx, nc);
+  DBuf<uint64_t> boff(ctx, nc + 1);
+  DBuf<uint8_t> scratch(ctx, scan_scratch_for(nc));
+  ShardArgs a{st.kind.p, st.flags.p, st.key.p, st.size.p, st.delts.p, st.path_len.p, N, sh.world, nt,
+              bcnt.p, boff.p, nullptr, 0};
+  launch_shard_count(a, stream);
+  launch_scan_u32(bcnt.p, boff.p, nc, scratch.p, stream);
+  std::vector<uint64_t> hoff = d2h(boff.p, nc + 1, stream);
+  sh.nsend = hoff[nc];
+  sh.send_idx = DBuf<uint32_t>(ctx, sh.nsend);
+  a.send_idx = sh.send_idx.p;
+  a.nsend = sh.nsend;
+  launch_shard_scatter(a, stream);
+  // path byte offsets of the send order
+  sh.send_plen = DBuf<uint32_t>(ctx, sh.nsend);
+  sh.send_poff = DBuf<uint64_t>(ctx, sh.nsend + 1);
+  launch_gather_u32(st.path_len.p, sh.send_idx.p, sh.nsend, sh.send_plen.p, stream);
+  DBuf<uint8_t> scratch2(ctx, scan_scratch_for(sh.nsend));
+  launch_scan_u32(sh.send_plen.p, sh.send_poff.p, sh.nsend, scratch2.p, stream);
+  ctx->mark("shard_partition");
+  for (uint32_t d = 0; d < sh.world; ++d) {
+    const uint64_t s0 = hoff[uint64_t(d) * nt], s1 = d + 1 < sh.world ? hoff[uint64_t(d + 1) * nt] : sh.nsend;
+    send_counts[d] = s1 - s0;
+    const uint64_t b0 = d2h_one(sh.send_poff.p + s0, stream), b1 = d2h_one(sh.send_poff.p + s1, stream);
+    send_bytes[d] = b1 - b0;
+  }
+  sh.send_path_bytes = d2h_one(sh.send_poff.p + sh.nsend, stream);
+}
+
+static void shard_pack(dr_shard& sh, void* send_rec, void* send_path) {
+  dr_ctx* ctx = sh.ctx;
+  hipStream_t stream = ctx->stream;
+  dr_state& st = *sh.st;
+  ShardArgs a{st.kind.p, st.flags.p, st.key.p, st.size.p, st.delts.p, st.path_len.p, st.n_actions, sh.world,
+              0, nullptr, nullptr, sh.send_idx.p, sh.nsend};
+  launch_shard_pack(a, static_cast<ShardRec*>(send_rec), sh.send_plen.p, stream);
+  DBuf<uint64_t> ptrs(ctx, sh.nsend);
+  launch_gather_u64(st.path_ptr.p, sh.send_idx.p, sh.nsend, ptrs.p, stream);
+  launch_gather_bytes(ptrs.p, sh.send_plen.p, sh.send_poff.p, sh.nsend, static_cast<uint8_t*>(send_path), stream);
+  HIP_OK(hipStreamSynchronize(stream));
+}
+
+static void shard_reduce(dr_shard& sh, const void* recv_rec, uint64_t n, const void* recv_path, int64_t cutoff,
+                         uint8_t* verdict) {
+  dr_ctx* ctx = sh.ctx;
+  hipStream_t stream = ctx->stream;
+  std::unique_ptr<dr_state> own(new_state(ctx, nullptr));
+  own->n_actions = n;
+  own->kind = DBuf<uint8_t>(ctx, n);
+  own->flags = DBuf<uint8_t>(ctx, n);
+  own->key = DBuf<uint64_t>(ctx, n);
+  own->path_ptr = DBuf<uint64_t>(ctx, n);
+  own->path_len = DBuf<uint32_t>(ctx, n);
+  own->size = DBuf<int64_t>(ctx, n);
+  own->delts = DBuf<int64_t>(ctx, n);
+  own->src_off = DBuf<uint64_t>(ctx, n);
+  own->src_len = DBuf<uint32_t>(ctx, n);
+  const ShardRec* rec = static_cast<const ShardRec*>(recv_rec);
+  DBuf<uint64_t> poff(ctx, n + 1);
+  DBuf<uint8_t> scratch(ctx, scan_scratch_for(n));
+  launch_shard_plen(rec, n, own->path_len.p, stream);
+  launch_scan_u32(own->path_len.p, poff.p, n, scratch.p, stream);
+  ActionArrays act{own->kind.p, own->flags.p, own->key.p, own->path_ptr.p, own->path_len.p, own->size.p,
+                   own->delts.p, own->src_off.p, own->src_len.p};
+  launch_shard_unpack(rec, n, static_cast<const uint8_t*>(recv_path), poff.p, act, stream);
+  ctx->mark("shard_exchange");
+  reduce_actions(ctx, own.get(), cutoff);
+  if (n) HIP_OK(hipMemsetAsync(verdict, 0, n, stream));
+  launch_verdict_set(own->live.p, own->n_live, 1, verdict, stream);
+  launch_verdict_set(own->tomb.p, own->n_tomb, 2, verdict, stream);
+  HIP_OK(hipStreamSynchronize(stream));
+  sh.owner = own->counts;
+  sh.reduced = true;
+}
+
+static dr_state* shard_finish(dr_shard& sh, const uint8_t* verdict_back) {
+  dr_ctx* ctx = sh.ctx;
+  hipStream_t stream = ctx->stream;
+  dr_state& st = *sh.st;
+  const uint64_t n = sh.nsend;
+  DBuf<uint32_t> fl(ctx, n), ft(ctx, n);
+  DBuf<uint64_t> pl(ctx, n + 1), pt(ctx, n + 1);
+  DBuf<uint8_t> scratch(ctx, scan_scratch_for(n));
+  launch_verdict_flags(verdict_back, n, fl.p, ft.p, stream);
+  launch_scan_u32(fl.p, pl.p, n, scratch.p, stream);
+  launch_scan_u32(ft.p, pt.p, n, scratch.p, stream);
+  st.n_live = d2h_one(pl.p + n, stream);
+  st.n_tomb = d2h_one(pt.p + n, stream);
+  st.live = DBuf<uint32_t>(ctx, st.n_live);
+  st.tomb = DBuf<uint32_t>(ctx, st.n_tomb);
+  launch_verdict_collect(verdict_back, sh.send_idx.p, n, 1, pl.p, st.live.p, stream);
+  launch_verdict_collect(verdict_back, sh.send_idx.p, n, 2, pt.p, st.tomb.p, stream);
+  HIP_OK(hipStreamSynchronize(stream));
+  ctx->mark("shard_finish");
+  // counters: the owner-side partial sums (their sum over ranks is the table's computedState)
+  st.counts.num_files = sh.owner.num_files;
+  st.counts.size_in_bytes = sh.owner.size_in_bytes;
+  st.counts.num_removes = sh.owner.num_removes;
+  st.counts.live_key_sum = sh.owner.live_key_sum;
+  st.counts.tomb_key_sum = sh.owner.tomb_key_sum;
+  st.counts.num_file_actions = sh.owner.num_file_actions;
+  st.counts.num_actions = int64_t(st.n_actions);
+  reduce_nonfile(st, sh.nf, false);
+  ctx->mark("end");
+  return sh.st.release();
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -1267,4 +1536,89 @@ int dr_last_timings(dr_ctx* ctx, char* names, uint64_t names_len, float* ms, int
   return DR_OK;
 }
 
+/* ---- multi-GPU shards ---- */
+int dr_shard_plan(dr_ctx* ctx, const char* log_path, int64_t version_to_load, int32_t world, char* buf,
+                  uint64_t buf_len, uint64_t* needed) {
+  if (!log_path || world < 1) return DR_E_INVALID_ARG;  // host only: ctx may be NULL
+  return guard(ctx, [&] {
+    LogSegmentInfo seg = get_log_segment(log_path, version_to_load);
+    std::vector<ShardUnit> units = shard_units(log_path, seg);
+    std::vector<int32_t> owner = shard_assign(units, world);
+    std::string s;
+    for (size_t k = 0; k < units.size(); ++k)
+      s += fmt("%d %d %lld %d %d %d %llu %s\n", owner[k], units[k].f.kind, (long long)units[k].f.version, units[k].f.part,
+               units[k].rg_lo, units[k].rg_hi, (unsigned long long)units[k].weight, units[k].f.name.c_str());
+    if (needed) *needed = s.size() + 1;
+    if (buf && buf_len) {
+      size_t n = std::min<size_t>(s.size(), buf_len - 1);
+      memcpy(buf, s.data(), n);
+      buf[n] = 0;
+    }
+  });
+}
+
+int dr_stage_log_shard(dr_ctx* ctx, const char* log_path, int64_t version_to_load, int32_t world, int32_t rank,
+                       dr_staged** out) {
+  if (!ctx || !out || !log_path || world < 1 || rank < 0 || rank >= world) return DR_E_INVALID_ARG;
+  return guard(ctx, [&] {
+    HIP_OK(hipSetDevice(ctx->device));
+    auto s = std::make_unique<dr_staged>();
+    s->d = stage_shard(ctx, log_path, version_to_load, world, rank);
+    *out = s.release();
+  });
+}
+
+int dr_shard_begin(dr_ctx* ctx, const dr_staged* staged, int32_t world, dr_shard** out, uint64_t* send_counts,
+                   uint64_t* send_bytes) {
+  if (!ctx || !staged || !out || !send_counts || !send_bytes || world < 1 || uint32_t(world) > shard_max_world())
+    return DR_E_INVALID_ARG;
+  *out = nullptr;
+  return guard(ctx, [&] {
+    HIP_OK(hipSetDevice(ctx->device));
+    auto sh = std::make_unique<dr_shard>();
+    sh->ctx = ctx;
+    sh->staged = staged->d;
+    sh->world = uint32_t(world);
+    shard_begin(*sh, send_counts, send_bytes);
+    *out = sh.release();
+  });
+}
+
+int dr_shard_pack(dr_shard* shard, void* send_rec, void* send_path) {
+  if (!shard || !shard->st || (shard->nsend && (!send_rec || (shard->send_path_bytes && !send_path))))
+    return DR_E_INVALID_ARG;
+  return guard(shard->ctx, [&] { shard_pack(*shard, send_rec, send_path); });
+}
+
+int dr_shard_reduce(dr_shard* shard, const void* recv_rec, uint64_t n_recv, const void* recv_path,
+                    uint64_t recv_path_bytes, int64_t min_file_retention_timestamp, uint8_t* verdict) {
+  if (!shard || !shard->st || (n_recv && (!recv_rec || !verdict)) || (recv_path_bytes && !recv_path))
+    return DR_E_INVALID_ARG;
+  return guard(shard->ctx, [&] { shard_reduce(*shard, recv_rec, n_recv, recv_path, min_file_retention_timestamp, verdict); });
+}
+
+int dr_shard_finish(dr_shard* shard, const uint8_t* verdict_back, dr_state** out) {
+  if (!shard || !shard->st || !out || (shard->nsend && !verdict_back)) return DR_E_INVALID_ARG;
+  *out = nullptr;
+  dr_ctx* ctx = shard->ctx;
+  int rc = guard(ctx, [&] {
+    if (!shard->reduced) fail(DR_E_INVALID_ARG, "dr_shard_finish before dr_shard_reduce");
+    *out = shard_finish(*shard, verdict_back);
+    ctx->collect_timings();
+  });
+  if (rc != DR_OK) {
+    for (auto& m : ctx->marks) (void)hipEventDestroy(m.second);
+    ctx->marks.clear();
+  }
+  return rc;
+}
+
+int dr_shard_release(dr_shard* shard) {
+  if (!shard) return DR_OK;
+  (void)hipStreamSynchronize(shard->ctx->stream);
+  delete shard;
+  return DR_OK;
+}
+
 }  // extern "C"
+

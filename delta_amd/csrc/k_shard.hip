@@ -1,0 +1,171 @@
+// Multi-GPU path-hash sharding: every path-keyed action depends only on actions with
+// the same path, so after the local parse each rank sends its file actions to owner(path) and every
+// owner runs K3/K4 on its shard alone. Records leave a rank grouped by owner and, inside a group, in
+// the rank's replay order; ranks hold contiguous slices of the segment (checkpoint row groups, then
+// commits), so an owner that concatenates what it receives in rank order sees its actions in the
+// global replay order -- last-writer-wins needs nothing else. The owner's verdicts (live / kept
+// tombstone / dropped) travel back to the sender, which owns the full record bytes for export.
+#include "dev_common.h"
+#include "kernels.h"
+
+namespace dr {
+namespace dev {
+
+constexpr int SH_T = 256;
+constexpr int SH_ITEMS = 16;
+constexpr int SH_TILE = SH_T * SH_ITEMS;
+constexpr int SH_MAXW = 64;
+
+__device__ __forceinline__ bool shard_sends(uint8_t kind, uint8_t flags) {
+  return (kind == K_ADD || kind == K_REMOVE) && !(flags & F_PATH_NULL);
+}
+// owner(key): the low 32 key bits scaled to [0, world). The partition inside an owner uses the top
+// key bits (bucket_of), so the two are independent.
+__device__ __forceinline__ uint32_t owner_of(uint64_t key, uint32_t world) {
+  return uint32_t((uint64_t(uint32_t(key)) * world) >> 32);
+}
+
+// per-tile counts per owner, stored owner-major: blk_count[d * ntiles + tile]
+__global__ void __launch_bounds__(SH_T) k_shard_count(ShardArgs a) {
+  __shared__ uint32_t h[SH_MAXW];
+  for (int d = threadIdx.x; d < SH_MAXW; d += SH_T) h[d] = 0;
+  __syncthreads();
+  const uint64_t base = uint64_t(blockIdx.x) * SH_TILE;
+  for (int k = 0; k < SH_ITEMS; ++k) {
+    const uint64_t i = base + uint64_t(k) * SH_T + threadIdx.x;
+    if (i < a.n && shard_sends(a.kind[i], a.flags[i])) atomicAdd(&h[owner_of(a.key[i], a.world)], 1u);
+  }
+  __syncthreads();
+  for (uint32_t d = threadIdx.x; d < a.world; d += SH_T) a.blk_count[uint64_t(d) * a.ntiles + blockIdx.x] = h[d];
+}
+
+// stable scatter: slot = blk_off[d * ntiles + tile] + rank of the action among the tile's earlier
+// actions with the same owner (ballot ranks inside a wave, LDS prefix over the waves, running cursor)
+__global__ void __launch_bounds__(SH_T) k_shard_scatter(ShardArgs a) {
+  __shared__ uint32_t wc[SH_T / 64][SH_MAXW];
+  __shared__ uint32_t cur[SH_MAXW];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int d = threadIdx.x; d < SH_MAXW; d += SH_T) cur[d] = 0;
+  const uint64_t base = uint64_t(blockIdx.x) * SH_TILE;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  for (int k = 0; k < SH_ITEMS; ++k) {
+    const uint64_t i = base + uint64_t(k) * SH_T + threadIdx.x;
+    const bool s = i < a.n && shard_sends(a.kind[i], a.flags[i]);
+    const uint32_t d = s ? owner_of(a.key[i], a.world) : 0xffffffffu;
+    uint32_t r = 0;
+    for (uint32_t q = 0; q < a.world; ++q) {
+      const unsigned long long m = __ballot(d == q);
+      if (d == q) r = uint32_t(__popcll(m & lt));
+      if (lane == 0) wc[wv][q] = uint32_t(__popcll(m));
+    }
+    __syncthreads();
+    if (s) {
+      uint32_t before = cur[d];
+      for (int w = 0; w < wv; ++w) before += wc[w][d];
+      a.send_idx[a.blk_off[uint64_t(d) * a.ntiles + blockIdx.x] + before + r] = uint32_t(i);
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < a.world; q += SH_T) {
+      uint32_t t = 0;
+      for (int w = 0; w < SH_T / 64; ++w) t += wc[w][q];
+      cur[q] += t;
+    }
+    __syncthreads();
+  }
+}
+
+// fixed-size record per sent action + its canonical path length (for the byte offsets)
+__global__ void k_shard_pack(ShardArgs a, ShardRec* rec, uint32_t* plen_out) {
+  const uint64_t j = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (j >= a.nsend) return;
+  const uint32_t i = a.send_idx[j];
+  ShardRec r;
+  r.key = a.key[i];
+  r.size = a.size[i];
+  r.delts = a.delts[i];
+  r.plen = a.path_len[i];
+  r.kind = a.kind[i];
+  r.flags = a.flags[i];
+  r.pad = 0;
+  rec[j] = r;
+  plen_out[j] = r.plen;
+}
+
+// receiver: records -> action arrays (path_ptr from the scanned path offsets)
+__global__ void k_shard_unpack(const ShardRec* rec, uint64_t n, const uint8_t* path_base, const uint64_t* poff,
+                               ActionArrays act) {
+  const uint64_t j = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const ShardRec r = rec[j];
+  act.kind[j] = r.kind;
+  act.flags[j] = r.flags;
+  act.key[j] = r.key;
+  act.size[j] = r.size;
+  act.delts[j] = r.delts;
+  act.path_len[j] = r.plen;
+  act.path_ptr[j] = reinterpret_cast<uint64_t>(path_base + poff[j]);
+  act.src_off[j] = j;
+  act.src_len[j] = 0;
+}
+
+__global__ void k_shard_plen(const ShardRec* rec, uint64_t n, uint32_t* plen) {
+  const uint64_t j = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (j < n) plen[j] = rec[j].plen;
+}
+
+__global__ void k_verdict_set(const uint32_t* idx, uint64_t n, uint8_t v, uint8_t* verdict) {
+  const uint64_t j = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (j < n) verdict[idx[j]] = v;
+}
+
+__global__ void k_verdict_flags(const uint8_t* verdict, uint64_t n, uint32_t* f_live, uint32_t* f_tomb) {
+  const uint64_t j = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint8_t v = verdict[j];
+  f_live[j] = v == 1;
+  f_tomb[j] = v == 2;
+}
+
+__global__ void k_verdict_collect(const uint8_t* verdict, const uint32_t* send_idx, uint64_t n, uint8_t want,
+                                  const uint64_t* pos, uint32_t* out) {
+  const uint64_t j = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (j < n && verdict[j] == want) out[pos[j]] = send_idx[j];
+}
+
+}  // namespace dev
+
+static inline unsigned grid_for(uint64_t n, unsigned t) { return unsigned((n + t - 1) / t); }
+
+uint64_t shard_tiles(uint64_t n) { return (n + dev::SH_TILE - 1) / dev::SH_TILE; }
+uint32_t shard_max_world() { return dev::SH_MAXW; }
+
+void launch_shard_count(const ShardArgs& a, hipStream_t st) {
+  if (a.ntiles) hipLaunchKernelGGL(dev::k_shard_count, dim3(unsigned(a.ntiles)), dim3(dev::SH_T), 0, st, a);
+}
+void launch_shard_scatter(const ShardArgs& a, hipStream_t st) {
+  if (a.ntiles) hipLaunchKernelGGL(dev::k_shard_scatter, dim3(unsigned(a.ntiles)), dim3(dev::SH_T), 0, st, a);
+}
+void launch_shard_pack(const ShardArgs& a, ShardRec* rec, uint32_t* plen, hipStream_t st) {
+  if (a.nsend) hipLaunchKernelGGL(dev::k_shard_pack, dim3(grid_for(a.nsend, 256)), dim3(256), 0, st, a, rec, plen);
+}
+void launch_shard_plen(const ShardRec* rec, uint64_t n, uint32_t* plen, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(dev::k_shard_plen, dim3(grid_for(n, 256)), dim3(256), 0, st, rec, n, plen);
+}
+void launch_shard_unpack(const ShardRec* rec, uint64_t n, const uint8_t* path_base, const uint64_t* poff,
+                         const ActionArrays& act, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(dev::k_shard_unpack, dim3(grid_for(n, 256)), dim3(256), 0, st, rec, n, path_base, poff, act);
+}
+void launch_verdict_set(const uint32_t* idx, uint64_t n, uint8_t v, uint8_t* verdict, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(dev::k_verdict_set, dim3(grid_for(n, 256)), dim3(256), 0, st, idx, n, v, verdict);
+}
+void launch_verdict_flags(const uint8_t* verdict, uint64_t n, uint32_t* f_live, uint32_t* f_tomb, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(dev::k_verdict_flags, dim3(grid_for(n, 256)), dim3(256), 0, st, verdict, n, f_live, f_tomb);
+}
+void launch_verdict_collect(const uint8_t* verdict, const uint32_t* send_idx, uint64_t n, uint8_t want,
+                            const uint64_t* pos, uint32_t* out, hipStream_t st) {
+  if (n)
+    hipLaunchKernelGGL(dev::k_verdict_collect, dim3(grid_for(n, 256)), dim3(256), 0, st, verdict, send_idx, n, want,
+                       pos, out);
+}
+
+}  // namespace dr

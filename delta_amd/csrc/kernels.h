@@ -207,6 +207,45 @@ struct CompactArgs {
 };
 void launch_compact(const CompactArgs& a, hipStream_t st);
 
+// ---- multi-GPU path-hash sharding (k_shard.hip) ------------------------------------------------
+struct ShardRec {        // 32 B per exchanged file action (DR_SHARD_REC_BYTES)
+  uint64_t key;
+  int64_t size;
+  int64_t delts;
+  uint32_t plen;
+  uint8_t kind, flags;
+  uint16_t pad;
+};
+static_assert(sizeof(ShardRec) == 32, "ShardRec layout");
+
+struct ShardArgs {
+  const uint8_t* kind;
+  const uint8_t* flags;
+  const uint64_t* key;
+  const int64_t* size;
+  const int64_t* delts;
+  const uint32_t* path_len;
+  uint64_t n;
+  uint32_t world;
+  uint64_t ntiles;
+  uint32_t* blk_count;       // [world * ntiles] owner-major
+  const uint64_t* blk_off;   // exclusive scan of blk_count
+  uint32_t* send_idx;        // [nsend] local action index of each send slot
+  uint64_t nsend;
+};
+uint64_t shard_tiles(uint64_t n);
+uint32_t shard_max_world();
+void launch_shard_count(const ShardArgs& a, hipStream_t st);
+void launch_shard_scatter(const ShardArgs& a, hipStream_t st);
+void launch_shard_pack(const ShardArgs& a, ShardRec* rec, uint32_t* plen, hipStream_t st);
+void launch_shard_plen(const ShardRec* rec, uint64_t n, uint32_t* plen, hipStream_t st);
+void launch_shard_unpack(const ShardRec* rec, uint64_t n, const uint8_t* path_base, const uint64_t* poff,
+                         const ActionArrays& act, hipStream_t st);
+void launch_verdict_set(const uint32_t* idx, uint64_t n, uint8_t v, uint8_t* verdict, hipStream_t st);
+void launch_verdict_flags(const uint8_t* verdict, uint64_t n, uint32_t* f_live, uint32_t* f_tomb, hipStream_t st);
+void launch_verdict_collect(const uint8_t* verdict, const uint32_t* send_idx, uint64_t n, uint8_t want,
+                            const uint64_t* pos, uint32_t* out, hipStream_t st);
+
 }  // namespace dr
 
 namespace dr {

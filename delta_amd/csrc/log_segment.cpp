@@ -226,4 +226,30 @@ std::vector<uint8_t> read_file(const std::string& path) {
   return b;
 }
 
+
+
+uint64_t file_size(const std::string& path) {
+  struct stat st;
+  if (stat(path.c_str(), &st) != 0) fail(DR_E_IO, fmt("cannot stat %s", path.c_str()));
+  return uint64_t(st.st_size);
+}
+
+std::vector<uint8_t> read_tail(const std::string& path, uint64_t n) {
+  int fd = open(path.c_str(), O_RDONLY);
+  if (fd < 0) fail(DR_E_IO, fmt("cannot open %s", path.c_str()));
+  struct stat st;
+  fstat(fd, &st);
+  const uint64_t sz = uint64_t(st.st_size);
+  const uint64_t k = std::min<uint64_t>(n, sz);
+  std::vector<uint8_t> b(static_cast<size_t>(k));
+  size_t got = 0;
+  while (got < b.size()) {
+    ssize_t r = pread(fd, b.data() + got, b.size() - got, off_t(sz - k + got));
+    if (r <= 0) { close(fd); fail(DR_E_IO, fmt("read failed on %s", path.c_str())); }
+    got += size_t(r);
+  }
+  close(fd);
+  return b;
+}
+
 }  // namespace dr

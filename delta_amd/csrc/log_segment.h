@@ -34,5 +34,8 @@ int checkpoint_part(const std::string& name);        // 0 = singular
 LogSegmentInfo get_log_segment(const std::string& log_path, int64_t version_to_load);
 
 std::vector<uint8_t> read_file(const std::string& path);
+uint64_t file_size(const std::string& path);
+// The last `n` bytes of a file (all of it when shorter).
+std::vector<uint8_t> read_tail(const std::string& path, uint64_t n);
 
 }  // namespace dr

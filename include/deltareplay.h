@@ -192,6 +192,43 @@ typedef struct dr_predicate {
 int dr_filter(dr_state* state, const dr_predicate* pred, int64_t** selected, int64_t* nselected);
 void dr_free(void* p);
 
+/* ---- multi-GPU shards (one process per GPU) ------------------------------------
+ * Replaces Snapshot.stateReconstruction's repartition(50, coalesce(add.path, remove.path)) shuffle
+ * (D/Snapshot.scala:103-104) across GPUs. The segment's replay order (checkpoint row groups, then
+ * commits) is cut into `world` contiguous slices by estimated device cost; rank r stages slice r.
+ * After the local parse, each file action goes to owner(path) = low32(xxh64(path)) * world >> 32;
+ * every owner runs the last-writer-wins reduction on its shard alone and returns a verdict per
+ * received record (0 dropped, 1 live AddFile, 2 kept tombstone) to the sender, which owns the
+ * record bytes for export. The exchange itself is the caller's (RCCL all-to-all over xGMI through
+ * torch.distributed): the library only reads/writes the device buffers it is handed.
+ *
+ *   dr_shard_plan       host only: the unit -> rank plan as text lines
+ *                       "<rank> <kind> <version> <part> <rg_lo> <rg_hi> <weight> <file name>"
+ *   dr_stage_log_shard  stage rank's slice (checkpoint row groups [rg_lo, rg_hi) + commits)
+ *   dr_shard_begin      K1/K2/canonicalise the slice, partition its file actions by owner; returns
+ *                       the records (send_counts[d]) and path bytes (send_bytes[d]) per owner d
+ *   dr_shard_pack       writes the records (DR_SHARD_REC_BYTES each, grouped by owner, replay
+ *                       order inside a group) and the path bytes into caller device buffers
+ *   dr_shard_reduce     owner side: the records received from ranks 0..world-1 concatenated in rank
+ *                       order; writes one verdict byte per record into `verdict` (device)
+ *   dr_shard_finish     sender side: verdicts returned in send order -> dr_state of this rank's
+ *                       surviving records (export as usual). Its counts hold this rank's owner-side
+ *                       partial sums (files, bytes, tombstones, key sums, file actions) and its
+ *                       local num_actions; non-file winners are local (merge in rank order). */
+#define DR_SHARD_REC_BYTES 32
+typedef struct dr_shard dr_shard;
+int dr_shard_plan(dr_ctx* ctx, const char* log_path, int64_t version_to_load, int32_t world, char* buf,
+                  uint64_t buf_len, uint64_t* needed);
+int dr_stage_log_shard(dr_ctx* ctx, const char* log_path, int64_t version_to_load, int32_t world, int32_t rank,
+                       dr_staged** out);
+int dr_shard_begin(dr_ctx* ctx, const dr_staged* staged, int32_t world, dr_shard** out, uint64_t* send_counts,
+                   uint64_t* send_bytes);
+int dr_shard_pack(dr_shard* shard, void* send_rec, void* send_path);
+int dr_shard_reduce(dr_shard* shard, const void* recv_rec, uint64_t n_recv, const void* recv_path,
+                    uint64_t recv_path_bytes, int64_t min_file_retention_timestamp, uint8_t* verdict);
+int dr_shard_finish(dr_shard* shard, const uint8_t* verdict_back, dr_state** out);
+int dr_shard_release(dr_shard* shard);
+
 /* ---- measurement hooks (bench.py) ----------------------------------------------------------
  * Per-stage device time of the last dr_replay_staged on this context (HIP events on the
  * context's stream), in milliseconds; names are returned NUL-separated. */

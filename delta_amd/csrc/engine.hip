@@ -172,23 +172,17 @@ struct NonFileAction {
 enum HotCol { HC_ADD_PATH = 0, HC_ADD_SIZE = 1, HC_RM_PATH = 2, HC_RM_DELTS = 3, HC_N = 4 };
 static const char* kHotPath[HC_N] = {"add.path", "add.size", "remove.path", "remove.deletionTimestamp"};
 
-struct StagedData {
-  dr_ctx* ctx = nullptr;
-  std::vector<uint8_t> h_json, h_pq;
-  DBuf<uint8_t> d_json, d_pq, d_arena;
-  std::vector<JsonFileRec> jfiles;
-  std::vector<CkPart> parts;
-  uint64_t ck_rows = 0;
-  int64_t ck_version = -1;
-  int64_t version = -1;
-  // page plan
+// Decode plan of a set of checkpoint leaf columns: page table, SNAPPY plan and scratch, PLAIN
+// BYTE_ARRAY boundary scratch, decompressed-page arena. Built once at staging, reused per replay.
+struct PagePlan {
+  std::vector<std::string> paths;        // leaf column paths, output slot = index
+  std::vector<int> max_def, max_rep;
+  std::vector<bool> present;
+  std::vector<uint64_t> levels;          // per column: rows (flat) or level entries (repeated)
   std::vector<PageDesc> pages;
   DBuf<PageDesc> d_pages;
   uint32_t dict_entries = 0;
-  bool has_col[HC_N] = {false, false, false, false};
-  int max_def[HC_N] = {0, 0, 0, 0};
-  int add_def = 1, rm_def = 1;
-  std::vector<NonFileAction> ck_nonfile;  // protocol/metaData/txn rows of the checkpoint
+  DBuf<uint8_t> d_arena;
   // SNAPPY plan + persistent scratch
   std::vector<SnapPage> snap_pages;
   std::vector<uint32_t> chunk_base, block_page;
@@ -206,6 +200,24 @@ struct StagedData {
   uint32_t ba_pages = 0;
   uint64_t ba_vals = 0, ba_hits = 0;
   DBuf<uint32_t> s_ba_vals, s_ba_hit, s_ba_ok, s_ba_count;
+};
+
+struct StagedData {
+  dr_ctx* ctx = nullptr;
+  std::vector<uint8_t> h_json, h_pq;
+  DBuf<uint8_t> d_json, d_pq;
+  std::vector<JsonFileRec> jfiles;
+  std::vector<CkPart> parts;
+  uint64_t ck_rows = 0;
+  int64_t ck_version = -1;
+  int64_t version = -1;
+  PagePlan hot;                           // the four hot leaf columns, decoded by every replay
+  bool has_col[HC_N] = {false, false, false, false};
+  int max_def[HC_N] = {0, 0, 0, 0};
+  int add_def = 1, rm_def = 1;
+  std::vector<NonFileAction> ck_nonfile;  // protocol/metaData/txn rows of the checkpoint
+  std::unique_ptr<PagePlan> pv;           // add.partitionValues map columns (planned on first filter)
+  std::mutex pv_mu;
 };
 
 struct dr_staged {
@@ -395,6 +407,190 @@ static void decode_ck_nonfile(StagedData& s, CkPart& part, uint64_t base_action)
   }
 }
 
+// Page plan of `P.paths` over the staged row groups of every checkpoint part (host: footer +
+// page headers), then the SNAPPY plan, arena and scratch (device).
+static void plan_pages(StagedData& s, PagePlan& P) {
+  const size_t nc = P.paths.size();
+  P.max_def.assign(nc, 0);
+  P.max_rep.assign(nc, 0);
+  P.present.assign(nc, false);
+  P.levels.assign(nc, 0);
+  if (s.parts.empty()) return;
+  const pq::FileMeta& m0 = s.parts[0].meta;
+  for (size_t c = 0; c < nc; ++c) {
+    const pq::Leaf* l = m0.leaf(P.paths[c]);
+    P.present[c] = l != nullptr;
+    if (l) { P.max_def[c] = l->max_def; P.max_rep[c] = l->max_rep; }
+  }
+  uint64_t arena = 0;
+  uint32_t dict_pool = 0;
+  std::vector<uint64_t> entry(nc, 0);   // level-entry cursor of repeated columns
+  for (CkPart& part : s.parts) {
+    const uint8_t* file = s.h_pq.data() + part.off;
+    uint64_t rg_row = part.row_base;
+    for (size_t gi = size_t(part.rg_lo); gi < part.rg_end(); ++gi) {
+      const pq::RowGroup& rg = part.meta.row_groups[gi];
+      for (size_t c = 0; c < nc; ++c) {
+        if (!P.present[c]) continue;
+        const pq::ColumnChunk* cc = nullptr;
+        for (auto& x : rg.cols) if (x.path == P.paths[c]) cc = &x;
+        if (!cc) continue;
+        if (cc->codec != 0 && cc->codec != 1)
+          fail(DR_E_UNSUPPORTED, fmt("checkpoint codec %d is not supported (column %s)", cc->codec, P.paths[c].c_str()));
+        const pq::Leaf* l = part.meta.leaf(P.paths[c]);
+        if (!l) fail(DR_E_PARQUET, fmt("checkpoint parts disagree on column %s", P.paths[c].c_str()));
+        const bool repeated = l->max_rep > 0;
+        int dict_idx = -1;
+        uint64_t row = repeated ? entry[c] : rg_row;
+        for (const pq::Page& p : pq::walk_pages(file, part.len, *cc)) {
+          PageDesc d{};
+          d.src = uint64_t(part.off + uint64_t(p.data_off));  // relocated below
+          d.dst = arena;
+          d.csize = uint32_t(p.compressed_size);
+          d.usize = uint32_t(p.uncompressed_size);
+          d.num_values = uint32_t(p.num_values);
+          d.kind = p.page_type == pq::DICTIONARY_PAGE ? PG_DICT : p.page_type == pq::DATA_PAGE_V2 ? PG_DATA_V2 : PG_DATA_V1;
+          d.encoding = p.encoding;
+          d.codec = cc->codec;
+          d.col = int32_t(c);
+          d.phys = l->type;
+          d.max_def = l->max_def;
+          d.max_rep = l->max_rep;
+          d.v2_def_len = p.v2_def_len;
+          d.v2_rep_len = p.v2_rep_len;
+          d.v2_compressed = p.v2_compressed;
+          if (d.kind == PG_DICT) {
+            dict_idx = int(P.pages.size());
+            d.dict_base = dict_pool;
+            dict_pool += d.num_values;
+            d.dict = -1;
+          } else {
+            d.dict = dict_idx;
+            d.row_base = row;
+            row += p.num_values;
+            if (d.encoding != 0 && d.encoding != 2 && d.encoding != 8 && !(d.encoding == 3 && l->type == 0))
+              fail(DR_E_UNSUPPORTED, fmt("encoding %d not supported for %s", d.encoding, P.paths[c].c_str()));
+          }
+          arena += (uint64_t(d.usize) + 16 + 15) & ~uint64_t(15);
+          if (d.phys == 6 && (d.kind == PG_DICT || d.encoding == 0)) {  // PLAIN byte arrays
+            d.ba = 1;
+            d.ba_slot = P.ba_pages++;
+            d.ba_base = P.ba_vals;
+            d.hit_base = P.ba_hits;
+            P.ba_vals += d.usize / 4 + 2;
+            P.ba_hits += d.usize / 32 + 4;
+          }
+          P.pages.push_back(d);
+        }
+        if (repeated) {
+          entry[c] = row;
+        } else if (row != rg_row + uint64_t(rg.num_rows)) {
+          fail(DR_E_PARQUET, fmt("column %s: %llu levels for %lld rows", P.paths[c].c_str(),
+                                 (unsigned long long)(row - rg_row), (long long)rg.num_rows));
+        }
+      }
+      rg_row += uint64_t(rg.num_rows);
+    }
+  }
+  for (size_t c = 0; c < nc; ++c) P.levels[c] = P.max_rep[c] > 0 ? entry[c] : s.ck_rows;
+  P.dict_entries = dict_pool;
+  // SNAPPY plan: preamble, speculation chunks and 64 KiB output blocks per page (k_snappy.hip)
+  for (const PageDesc& d : P.pages) {
+    const uint64_t lv = d.kind == PG_DATA_V2 ? uint64_t(d.v2_def_len + d.v2_rep_len) : 0;
+    if (lv) P.copy_jobs.push_back(CopyJob{d.src, d.dst, lv});
+    const bool compressed = d.codec == 1 && !(d.kind == PG_DATA_V2 && !d.v2_compressed);
+    if (!compressed) {
+      P.copy_jobs.push_back(CopyJob{d.src + lv, d.dst + lv, d.usize - lv});
+      continue;
+    }
+    const uint8_t* h = s.h_pq.data() + d.src + lv;
+    uint64_t total = 0;
+    uint32_t pre = 0;
+    for (int sh = 0; pre < 5 && pre < d.csize - lv; sh += 7) {
+      const uint8_t b = h[pre++];
+      total |= uint64_t(b & 0x7f) << sh;
+      if (!(b & 0x80)) break;
+    }
+    if (total != d.usize - lv) fail(DR_E_PARQUET, "snappy preamble does not match the page size");
+    SnapPage sp{d.src + lv + pre, d.dst + lv, uint32_t(d.csize - lv - pre), uint32_t(d.usize - lv),
+                uint32_t(P.block_page.size())};
+    P.chunk_base.push_back(P.nchunks);
+    const uint32_t ncp = (sp.n_in + 255) / 256;
+    for (uint32_t j = 0; j < ncp; j += snappy_wg_chunks()) P.wg_chunk0.push_back(P.nchunks + j);
+    P.nchunks += ncp;
+    P.snap_in_bytes += sp.n_in;
+    const uint32_t nb = (sp.n_out + 65535) / 65536;
+    for (uint32_t k = 0; k < nb; ++k) P.block_page.push_back(uint32_t(P.snap_pages.size()));
+    P.snap_pages.push_back(sp);
+  }
+  P.chunk_base.push_back(P.nchunks);
+  P.d_arena = DBuf<uint8_t>(s.ctx, arena + 4096);
+  const uint64_t pqb = reinterpret_cast<uint64_t>(s.d_pq.p), arb = reinterpret_cast<uint64_t>(P.d_arena.p);
+  for (SnapPage& sp : P.snap_pages) { sp.in += pqb; sp.out += arb; }
+  for (CopyJob& j : P.copy_jobs) { j.src += pqb; j.dst += arb; }
+  auto up = [&](auto& dbuf, auto& vec) {
+    using T = typename std::decay_t<decltype(vec)>::value_type;
+    dbuf = DBuf<T>(s.ctx, vec.size());
+    if (!vec.empty())
+      HIP_OK(hipMemcpyAsync(dbuf.p, vec.data(), vec.size() * sizeof(T), hipMemcpyHostToDevice, s.ctx->stream));
+  };
+  up(P.d_snap, P.snap_pages);
+  up(P.d_chunk_base, P.chunk_base);
+  up(P.d_block_page, P.block_page);
+  up(P.d_copy, P.copy_jobs);
+  up(P.d_wg_chunk0, P.wg_chunk0);
+  P.s_spec_exit = DBuf<uint32_t>(s.ctx, P.nchunks);
+  P.s_vis = DBuf<uint32_t>(s.ctx, uint64_t(P.nchunks) * 8);
+  P.s_entry = DBuf<uint32_t>(s.ctx, P.nchunks);
+  P.s_chunk_out = DBuf<uint32_t>(s.ctx, P.nchunks);
+  P.s_chunk_out_start = DBuf<uint32_t>(s.ctx, P.nchunks);
+  P.s_chunk_copies = DBuf<uint32_t>(s.ctx, P.nchunks);
+  P.s_rec_start = DBuf<uint64_t>(s.ctx, uint64_t(P.nchunks) + 1);
+  P.s_recs = DBuf<uint64_t>(s.ctx, P.snap_in_bytes / 2 + 1);  // a copy element takes >= 2 input bytes
+  P.s_pages_bad = DBuf<uint32_t>(s.ctx, P.snap_pages.size());
+  P.s_ba_vals = DBuf<uint32_t>(s.ctx, P.ba_vals);
+  P.s_ba_hit = DBuf<uint32_t>(s.ctx, P.ba_hits);
+  P.s_ba_ok = DBuf<uint32_t>(s.ctx, P.ba_pages);
+  P.s_ba_count = DBuf<uint32_t>(s.ctx, P.ba_pages);
+  for (PageDesc& d : P.pages) {
+    d.src = pqb + d.src;
+    d.dst = arb + d.dst;
+  }
+  up(P.d_pages, P.pages);
+}
+
+// Inflate + decode every page of a plan into `pa.cols` (allocated by the caller for P.levels).
+static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_t>& dict_ptr, DBuf<uint32_t>& dict_len,
+                         DBuf<uint32_t>& err, void* scratch) {
+  hipStream_t stream = ctx->stream;
+  pa.pages = P.d_pages.p;
+  pa.npages = uint32_t(P.pages.size());
+  dict_ptr = DBuf<uint64_t>(ctx, P.dict_entries);
+  dict_len = DBuf<uint32_t>(ctx, P.dict_entries);
+  pa.dict_ptr = dict_ptr.p;
+  pa.dict_len = dict_len.p;
+  pa.error = err.p;
+  pa.ba_vals = P.s_ba_vals.p;
+  pa.ba_hit = P.s_ba_hit.p;
+  pa.ba_ok = P.s_ba_ok.p;
+  pa.ba_count = P.s_ba_count.p;
+  launch_page_copy(P.d_copy.p, uint32_t(P.copy_jobs.size()), stream);
+  if (!P.snap_pages.empty()) {
+    P.s_pages_bad.zero(stream);
+    SnappyArgs sa{P.d_snap.p, uint32_t(P.snap_pages.size()), P.d_chunk_base.p, P.nchunks, P.s_spec_exit.p,
+                  P.s_vis.p, P.s_entry.p, P.s_chunk_out.p, P.s_chunk_out_start.p, P.s_chunk_copies.p,
+                  P.s_rec_start.p, P.s_recs.p, P.d_block_page.p, uint32_t(P.block_page.size()),
+                  P.d_wg_chunk0.p, uint32_t(P.wg_chunk0.size()), P.s_pages_bad.p, err.p};
+    launch_snappy(sa, stream, scratch);
+  }
+  ctx->mark("pq_inflate");
+  if (P.ba_pages) launch_ba_bounds(pa, stream);
+  ctx->mark("pq_bounds");
+  launch_pq_dict(pa, stream);
+  launch_pq_data(pa, stream);
+  ctx->mark("pq_decode");
+}
+
 static void plan_checkpoint(StagedData& s) {
   uint64_t row_base = 0;
   for (CkPart& part : s.parts) {
@@ -418,137 +614,8 @@ static void plan_checkpoint(StagedData& s) {
     }
   }
   if (!s.has_col[HC_ADD_PATH]) fail(DR_E_PARQUET, "checkpoint has no add.path column");
-  // pages of the hot columns
-  uint64_t arena = 0;
-  uint32_t dict_pool = 0;
-  for (CkPart& part : s.parts) {
-    const uint8_t* file = s.h_pq.data() + part.off;
-    uint64_t rg_row = part.row_base;
-    for (size_t gi = size_t(part.rg_lo); gi < part.rg_end(); ++gi) {
-      const pq::RowGroup& rg = part.meta.row_groups[gi];
-      for (int c = 0; c < HC_N; ++c) {
-        if (!s.has_col[c]) continue;
-        const pq::ColumnChunk* cc = nullptr;
-        for (auto& x : rg.cols) if (x.path == kHotPath[c]) cc = &x;
-        if (!cc) continue;
-        if (cc->codec != 0 && cc->codec != 1)
-          fail(DR_E_UNSUPPORTED, fmt("checkpoint codec %d is not supported (column %s)", cc->codec, kHotPath[c]));
-        const pq::Leaf* l = part.meta.leaf(kHotPath[c]);
-        int dict_idx = -1;
-        uint64_t row = rg_row;
-        for (const pq::Page& p : pq::walk_pages(file, part.len, *cc)) {
-          PageDesc d{};
-          d.src = uint64_t(part.off + uint64_t(p.data_off));  // relocated below
-          d.dst = arena;
-          d.csize = uint32_t(p.compressed_size);
-          d.usize = uint32_t(p.uncompressed_size);
-          d.num_values = uint32_t(p.num_values);
-          d.kind = p.page_type == pq::DICTIONARY_PAGE ? PG_DICT : p.page_type == pq::DATA_PAGE_V2 ? PG_DATA_V2 : PG_DATA_V1;
-          d.encoding = p.encoding;
-          d.codec = cc->codec;
-          d.col = c;
-          d.phys = l->type;
-          d.max_def = l->max_def;
-          d.v2_def_len = p.v2_def_len;
-          d.v2_rep_len = p.v2_rep_len;
-          d.v2_compressed = p.v2_compressed;
-          if (d.kind == PG_DICT) {
-            dict_idx = int(s.pages.size());
-            d.dict_base = dict_pool;
-            dict_pool += d.num_values;
-            d.dict = -1;
-          } else {
-            d.dict = dict_idx;
-            d.row_base = row;
-            row += p.num_values;
-            if (d.encoding != 0 && d.encoding != 2 && d.encoding != 8 && !(d.encoding == 3 && l->type == 0))
-              fail(DR_E_UNSUPPORTED, fmt("encoding %d not supported for %s", d.encoding, kHotPath[c]));
-          }
-          arena += (uint64_t(d.usize) + 16 + 15) & ~uint64_t(15);
-          if (d.phys == 6 && (d.kind == PG_DICT || d.encoding == 0)) {  // PLAIN byte arrays
-            d.ba = 1;
-            d.ba_slot = s.ba_pages++;
-            d.ba_base = s.ba_vals;
-            d.hit_base = s.ba_hits;
-            s.ba_vals += d.usize / 4 + 2;
-            s.ba_hits += d.usize / 32 + 4;
-          }
-          s.pages.push_back(d);
-        }
-        if (row != rg_row + uint64_t(rg.num_rows))
-          fail(DR_E_PARQUET, fmt("column %s: %llu levels for %lld rows", kHotPath[c],
-                                 (unsigned long long)(row - rg_row), (long long)rg.num_rows));
-      }
-      rg_row += uint64_t(rg.num_rows);
-    }
-  }
-  s.dict_entries = dict_pool;
-  // SNAPPY plan: preamble, speculation chunks and 64 KiB output blocks per page (k_snappy.hip)
-  for (const PageDesc& d : s.pages) {
-    const uint64_t lv = d.kind == PG_DATA_V2 ? uint64_t(d.v2_def_len + d.v2_rep_len) : 0;
-    if (lv) s.copy_jobs.push_back(CopyJob{d.src, d.dst, lv});
-    const bool compressed = d.codec == 1 && !(d.kind == PG_DATA_V2 && !d.v2_compressed);
-    if (!compressed) {
-      s.copy_jobs.push_back(CopyJob{d.src + lv, d.dst + lv, d.usize - lv});
-      continue;
-    }
-    const uint8_t* h = s.h_pq.data() + d.src + lv;
-    uint64_t total = 0;
-    uint32_t pre = 0;
-    for (int sh = 0; pre < 5 && pre < d.csize - lv; sh += 7) {
-      const uint8_t b = h[pre++];
-      total |= uint64_t(b & 0x7f) << sh;
-      if (!(b & 0x80)) break;
-    }
-    if (total != d.usize - lv) fail(DR_E_PARQUET, "snappy preamble does not match the page size");
-    SnapPage sp{d.src + lv + pre, d.dst + lv, uint32_t(d.csize - lv - pre), uint32_t(d.usize - lv),
-                uint32_t(s.block_page.size())};
-    s.chunk_base.push_back(s.nchunks);
-    const uint32_t ncp = (sp.n_in + 255) / 256;
-    for (uint32_t j = 0; j < ncp; j += snappy_wg_chunks()) s.wg_chunk0.push_back(s.nchunks + j);
-    s.nchunks += ncp;
-    s.snap_in_bytes += sp.n_in;
-    const uint32_t nb = (sp.n_out + 65535) / 65536;
-    for (uint32_t k = 0; k < nb; ++k) s.block_page.push_back(uint32_t(s.snap_pages.size()));
-    s.snap_pages.push_back(sp);
-  }
-  s.chunk_base.push_back(s.nchunks);
-  s.d_arena = DBuf<uint8_t>(s.ctx, arena + 4096);
-  const uint64_t pqb = reinterpret_cast<uint64_t>(s.d_pq.p), arb = reinterpret_cast<uint64_t>(s.d_arena.p);
-  for (SnapPage& sp : s.snap_pages) { sp.in += pqb; sp.out += arb; }
-  for (CopyJob& j : s.copy_jobs) { j.src += pqb; j.dst += arb; }
-  auto up = [&](auto& dbuf, auto& vec) {
-    using T = typename std::decay_t<decltype(vec)>::value_type;
-    dbuf = DBuf<T>(s.ctx, vec.size());
-    if (!vec.empty())
-      HIP_OK(hipMemcpyAsync(dbuf.p, vec.data(), vec.size() * sizeof(T), hipMemcpyHostToDevice, s.ctx->stream));
-  };
-  up(s.d_snap, s.snap_pages);
-  up(s.d_chunk_base, s.chunk_base);
-  up(s.d_block_page, s.block_page);
-  up(s.d_copy, s.copy_jobs);
-  up(s.d_wg_chunk0, s.wg_chunk0);
-  s.s_spec_exit = DBuf<uint32_t>(s.ctx, s.nchunks);
-  s.s_vis = DBuf<uint32_t>(s.ctx, uint64_t(s.nchunks) * 8);
-  s.s_entry = DBuf<uint32_t>(s.ctx, s.nchunks);
-  s.s_chunk_out = DBuf<uint32_t>(s.ctx, s.nchunks);
-  s.s_chunk_out_start = DBuf<uint32_t>(s.ctx, s.nchunks);
-  s.s_chunk_copies = DBuf<uint32_t>(s.ctx, s.nchunks);
-  s.s_rec_start = DBuf<uint64_t>(s.ctx, uint64_t(s.nchunks) + 1);
-  s.s_recs = DBuf<uint64_t>(s.ctx, s.snap_in_bytes / 2 + 1);  // a copy element takes >= 2 input bytes
-  s.s_pages_bad = DBuf<uint32_t>(s.ctx, s.snap_pages.size());
-  s.s_ba_vals = DBuf<uint32_t>(s.ctx, s.ba_vals);
-  s.s_ba_hit = DBuf<uint32_t>(s.ctx, s.ba_hits);
-  s.s_ba_ok = DBuf<uint32_t>(s.ctx, s.ba_pages);
-  s.s_ba_count = DBuf<uint32_t>(s.ctx, s.ba_pages);
-  for (PageDesc& d : s.pages) {
-    d.src = reinterpret_cast<uint64_t>(s.d_pq.p) + d.src;
-    d.dst = reinterpret_cast<uint64_t>(s.d_arena.p) + d.dst;
-  }
-  s.d_pages = DBuf<PageDesc>(s.ctx, s.pages.size());
-  if (!s.pages.empty())
-    HIP_OK(hipMemcpyAsync(s.d_pages.p, s.pages.data(), s.pages.size() * sizeof(PageDesc), hipMemcpyHostToDevice,
-                          s.ctx->stream));
+  s.hot.paths.assign(kHotPath, kHotPath + HC_N);
+  plan_pages(s, s.hot);
   for (CkPart& part : s.parts) decode_ck_nonfile(s, part, 0);  // entry rows already include part.row_base
 }
 
@@ -699,8 +766,6 @@ static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
   DBuf<uint32_t> dict_len, pq_err;
   if (R) {
     ParquetArgs pa{};
-    pa.pages = s.d_pages.p;
-    pa.npages = uint32_t(s.pages.size());
     pa.ncols = HC_N;
     for (int c = 0; c < HC_N; ++c) {
       cdef[c] = DBuf<uint8_t>(ctx, R);
@@ -711,34 +776,11 @@ static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
       } else {
         cival[c] = DBuf<int64_t>(ctx, R);
       }
-      pa.cols[c] = FlatColumn{cdef[c].p, cival[c].p, csptr[c].p, cslen[c].p};
+      pa.cols[c] = FlatColumn{cdef[c].p, nullptr, cival[c].p, csptr[c].p, cslen[c].p};
     }
-    dict_ptr = DBuf<uint64_t>(ctx, s.dict_entries);
-    dict_len = DBuf<uint32_t>(ctx, s.dict_entries);
     pq_err = DBuf<uint32_t>(ctx, 1);
     pq_err.zero(stream);
-    pa.dict_ptr = dict_ptr.p;
-    pa.dict_len = dict_len.p;
-    pa.error = pq_err.p;
-    pa.ba_vals = s.s_ba_vals.p;
-    pa.ba_hit = s.s_ba_hit.p;
-    pa.ba_ok = s.s_ba_ok.p;
-    pa.ba_count = s.s_ba_count.p;
-    launch_page_copy(s.d_copy.p, uint32_t(s.copy_jobs.size()), stream);
-    if (!s.snap_pages.empty()) {
-      s.s_pages_bad.zero(stream);
-      SnappyArgs sa{s.d_snap.p, uint32_t(s.snap_pages.size()), s.d_chunk_base.p, s.nchunks, s.s_spec_exit.p,
-                    s.s_vis.p, s.s_entry.p, s.s_chunk_out.p, s.s_chunk_out_start.p, s.s_chunk_copies.p,
-                    s.s_rec_start.p, s.s_recs.p, s.d_block_page.p, uint32_t(s.block_page.size()),
-                    s.d_wg_chunk0.p, uint32_t(s.wg_chunk0.size()), s.s_pages_bad.p, pq_err.p};
-      launch_snappy(sa, stream, scratch.p);
-    }
-    ctx->mark("pq_inflate");
-    if (s.ba_pages) launch_ba_bounds(pa, stream);
-    ctx->mark("pq_bounds");
-    launch_pq_dict(pa, stream);
-    launch_pq_data(pa, stream);
-    ctx->mark("pq_decode");
+    decode_pages(ctx, s.hot, pa, dict_ptr, dict_len, pq_err, scratch.p);
     CkptAssembleArgs ca{};
     ca.add_path = pa.cols[HC_ADD_PATH];
     ca.add_size = pa.cols[HC_ADD_SIZE];
@@ -1073,6 +1115,183 @@ static void build_export(dr_state& st, int which) {
     ex.tags_entry_off.push_back(int64_t(ex.tags_val_null.size()));
   }
   ex.built = true;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// K5: partition pruning (DeltaLog.filterFileList, D/DeltaLog.scala:500-547)
+// ---------------------------------------------------------------------------------------------------
+static const char* kPvKey = "add.partitionValues.key_value.key";
+static const char* kPvVal = "add.partitionValues.key_value.value";
+
+// Host validation of the postfix program: operand indices and stack discipline.
+static void check_program(const dr_predicate& p) {
+  if (p.ncols < 0 || uint32_t(p.ncols) > filter_max_cols())
+    fail(DR_E_UNSUPPORTED, fmt("at most %u partition columns per predicate", filter_max_cols()));
+  if (p.nops <= 0 || !p.ops) fail(DR_E_INVALID_ARG, "empty predicate program");
+  if (p.ncols && (!p.col_names || !p.col_types)) fail(DR_E_INVALID_ARG, "missing partition columns");
+  if (p.nlits && (!p.lit_types || !p.lit_i64 || !p.lit_null || !p.lit_str_off))
+    fail(DR_E_INVALID_ARG, "missing literals");
+  for (int32_t c = 0; c < p.ncols; ++c)
+    if (p.col_types[c] < DR_T_STRING || p.col_types[c] > DR_T_BOOLEAN || !p.col_names[c])
+      fail(DR_E_UNSUPPORTED, "unsupported partition column type");
+  int depth = 0;
+  for (int32_t k = 0; k < p.nops; ++k) {
+    const int op = p.ops[k].opcode, arg = p.ops[k].arg;
+    switch (op) {
+      case DR_OP_COL:
+        if (arg < 0 || arg >= p.ncols) fail(DR_E_INVALID_ARG, "predicate column index out of range");
+        ++depth;
+        break;
+      case DR_OP_LIT:
+        if (arg < 0 || arg >= p.nlits) fail(DR_E_INVALID_ARG, "predicate literal index out of range");
+        ++depth;
+        break;
+      case DR_OP_EQ: case DR_OP_NE: case DR_OP_LT: case DR_OP_LE: case DR_OP_GT: case DR_OP_GE:
+      case DR_OP_NSEQ: case DR_OP_AND: case DR_OP_OR:
+        if (depth < 2) fail(DR_E_INVALID_ARG, "predicate stack underflow");
+        --depth;
+        break;
+      case DR_OP_IN:
+        if (arg < 0 || depth < arg + 1) fail(DR_E_INVALID_ARG, "predicate stack underflow (IN)");
+        depth -= arg;
+        break;
+      case DR_OP_ISNULL: case DR_OP_ISNOTNULL: case DR_OP_NOT:
+        if (depth < 1) fail(DR_E_INVALID_ARG, "predicate stack underflow");
+        break;
+      default: fail(DR_E_INVALID_ARG, fmt("unknown predicate opcode %d", op));
+    }
+    if (uint32_t(depth) > filter_max_stack()) fail(DR_E_UNSUPPORTED, "predicate program too deep");
+  }
+  if (depth != 1) fail(DR_E_INVALID_ARG, "predicate program must leave one value");
+}
+
+template <typename T>
+static DBuf<T> upload(dr_ctx* ctx, const T* src, size_t n) {
+  DBuf<T> d(ctx, n);
+  if (n) HIP_OK(hipMemcpyAsync(d.p, src, n * sizeof(T), hipMemcpyHostToDevice, ctx->stream));
+  return d;
+}
+
+static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred) {
+  check_program(pred);
+  dr_ctx* ctx = st.ctx;
+  hipStream_t stream = ctx->stream;
+  if (!st.staged) fail(DR_E_INVALID_ARG, "state has no staged segment");
+  StagedData& s = *st.staged;
+  const uint64_t R = s.ck_rows;
+  FilterArgs fa{};
+  fa.live = st.live.p;
+  fa.n_live = st.n_live;
+  fa.src_off = st.src_off.p;
+  fa.src_len = st.src_len.p;
+  fa.ck_rows = R;
+  fa.json = s.d_json.p;
+  // checkpoint side: decode the add.partitionValues map columns (planned once per staged segment)
+  DBuf<uint8_t> kdef, krep, vdef, vrep;
+  DBuf<uint64_t> kptr, vptr, row_start, dict_ptr, rpos;
+  DBuf<uint32_t> klen, vlen, dict_len, pq_err(ctx, 1), rflag;
+  DBuf<uint8_t> scratch(ctx, scan_scratch_for(0));
+  pq_err.zero(stream);
+  if (R && st.n_live) {
+    {
+      std::lock_guard<std::mutex> g(s.pv_mu);
+      if (!s.pv) {
+        auto P = std::make_unique<PagePlan>();
+        P->paths = {kPvKey, kPvVal};
+        plan_pages(s, *P);
+        s.pv = std::move(P);
+      }
+    }
+    PagePlan& P = *s.pv;
+    if (P.present[0] && P.present[1]) {
+      const uint64_t E = P.levels[0];
+      if (P.levels[1] != E) fail(DR_E_PARQUET, "partitionValues key/value columns disagree");
+      kdef = DBuf<uint8_t>(ctx, E); krep = DBuf<uint8_t>(ctx, E); kptr = DBuf<uint64_t>(ctx, E); klen = DBuf<uint32_t>(ctx, E);
+      vdef = DBuf<uint8_t>(ctx, E); vrep = DBuf<uint8_t>(ctx, E); vptr = DBuf<uint64_t>(ctx, E); vlen = DBuf<uint32_t>(ctx, E);
+      kdef.zero(stream);
+      vdef.zero(stream);
+      ParquetArgs pa{};
+      pa.ncols = 2;
+      pa.cols[0] = FlatColumn{kdef.p, krep.p, nullptr, kptr.p, klen.p};
+      pa.cols[1] = FlatColumn{vdef.p, vrep.p, nullptr, vptr.p, vlen.p};
+      decode_pages(ctx, P, pa, dict_ptr, dict_len, pq_err, scratch.p);
+      if (d2h_one(pq_err.p, stream) != 0)
+        fail(DR_E_PARQUET, fmt("device decode of add.partitionValues failed (code %u)", d2h_one(pq_err.p, stream)));
+      rflag = DBuf<uint32_t>(ctx, E);
+      rpos = DBuf<uint64_t>(ctx, E + 1);
+      launch_rep0_flags(krep.p, E, rflag.p, stream);
+      launch_scan_u32(rflag.p, rpos.p, E, scratch.p, stream);
+      if (d2h_one(rpos.p + E, stream) != R) fail(DR_E_PARQUET, "add.partitionValues: one map per checkpoint row expected");
+      row_start = DBuf<uint64_t>(ctx, R + 1);
+      launch_row_starts(krep.p, E, rpos.p, row_start.p, stream);
+      HIP_OK(hipMemcpyAsync(row_start.p + R, &E, 8, hipMemcpyHostToDevice, stream));
+      fa.has_map = 1;
+      fa.row_start = row_start.p;
+      fa.key_def = kdef.p; fa.key_ptr = kptr.p; fa.key_len = klen.p; fa.key_max_def = P.max_def[0];
+      fa.val_def = vdef.p; fa.val_ptr = vptr.p; fa.val_len = vlen.p; fa.val_max_def = P.max_def[1];
+    }
+  }
+  // program
+  std::vector<uint64_t> name_off(size_t(pred.ncols) + 1, 0);
+  std::string names;
+  for (int32_t c = 0; c < pred.ncols; ++c) {
+    names += pred.col_names[c];
+    name_off[size_t(c) + 1] = names.size();
+  }
+  std::vector<int32_t> ops(size_t(pred.nops) * 2);
+  for (int32_t k = 0; k < pred.nops; ++k) { ops[2 * size_t(k)] = pred.ops[k].opcode; ops[2 * size_t(k) + 1] = pred.ops[k].arg; }
+  std::vector<uint64_t> lit_off(size_t(pred.nlits) + 1, 0);
+  for (int32_t k = 0; k <= pred.nlits && pred.nlits; ++k) lit_off[size_t(k)] = uint64_t(pred.lit_str_off[k]);
+  const uint64_t lit_bytes = pred.nlits ? lit_off[size_t(pred.nlits)] : 0;
+  DBuf<uint64_t> d_name_off = upload(ctx, name_off.data(), name_off.size());
+  DBuf<uint8_t> d_names = upload(ctx, reinterpret_cast<const uint8_t*>(names.data()), names.size());
+  DBuf<int32_t> d_types = upload(ctx, pred.col_types, size_t(pred.ncols));
+  DBuf<int32_t> d_ops = upload(ctx, ops.data(), ops.size());
+  DBuf<int32_t> d_lt = upload(ctx, pred.lit_types, size_t(pred.nlits));
+  DBuf<int64_t> d_li = upload(ctx, pred.lit_i64, size_t(pred.nlits));
+  DBuf<uint8_t> d_ln = upload(ctx, pred.lit_null, size_t(pred.nlits));
+  DBuf<uint64_t> d_lo = upload(ctx, lit_off.data(), lit_off.size());
+  DBuf<uint8_t> d_ls = upload(ctx, pred.lit_str_bytes, size_t(lit_bytes));
+  fa.ncols = pred.ncols;
+  fa.col_name_off = d_name_off.p;
+  fa.col_names = d_names.p;
+  fa.col_types = d_types.p;
+  fa.nops = pred.nops;
+  fa.ops = d_ops.p;
+  fa.lit_types = d_lt.p;
+  fa.lit_i64 = d_li.p;
+  fa.lit_null = d_ln.p;
+  fa.lit_str_off = d_lo.p;
+  fa.lit_str = d_ls.p;
+  DBuf<unsigned long long> ctr(ctx, 2);  // 0 arena fill, 1 arena need
+  DBuf<uint32_t> ferr(ctx, 1), flag(ctx, st.n_live);
+  ctr.zero(stream);
+  ferr.zero(stream);
+  fa.arena_fill = ctr.p;
+  fa.arena_need = ctr.p + 1;
+  fa.flag = flag.p;
+  fa.error = ferr.p;
+  launch_filter(fa, stream);
+  const unsigned long long need = d2h_one(ctr.p + 1, stream);
+  DBuf<uint8_t> arena;
+  if (need) {  // some partition values carry JSON escapes: unescape them into an arena and rerun
+    arena = DBuf<uint8_t>(ctx, need + 64);
+    fa.arena = arena.p;
+    fa.arena_cap = need + 64;
+    launch_filter(fa, stream);
+  }
+  const uint32_t e = d2h_one(ferr.p, stream);
+  if (e & 1u) fail(DR_E_PARSE, "malformed add.partitionValues in a live AddFile's JSON line");
+  if (e & 2u) fail(DR_E_INTERNAL, "partition value arena overflow");
+  DBuf<uint64_t> pos(ctx, st.n_live + 1);
+  launch_scan_u32(flag.p, pos.p, st.n_live, scratch.p, stream);
+  const uint64_t nsel = d2h_one(pos.p + st.n_live, stream);
+  DBuf<int64_t> sel(ctx, nsel);
+  launch_select(flag.p, pos.p, st.n_live, sel.p, stream);
+  std::vector<int64_t> out = d2h(sel.p, nsel, stream);
+  ctx->mark("filter");
+  ctx->collect_timings();
+  return out;
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -1430,8 +1649,8 @@ int dr_staged_plan(const dr_staged* staged, uint64_t* out, int32_t cap, int32_t*
   const StagedData& s = *staged->d;
   uint64_t ck = 0, cs = 0, us = 0;
   for (auto& p : s.parts) ck += p.len;
-  for (auto& p : s.pages) { cs += p.csize; us += p.usize; }
-  const uint64_t v[7] = {s.h_json.size(), ck, s.ck_rows, s.pages.size(), cs, us, s.dict_entries};
+  for (auto& p : s.hot.pages) { cs += p.csize; us += p.usize; }
+  const uint64_t v[7] = {s.h_json.size(), ck, s.ck_rows, s.hot.pages.size(), cs, us, s.hot.dict_entries};
   int32_t k = 0;
   for (; k < cap && k < 7; ++k) out[k] = v[k];
   *n = k;
@@ -1506,8 +1725,17 @@ int dr_state_export(dr_state* state, int32_t which, dr_export* out) {
 
 int dr_filter(dr_state* state, const dr_predicate* pred, int64_t** selected, int64_t* nselected) {
   if (!state || !pred || !selected || !nselected) return DR_E_INVALID_ARG;
-  state->ctx->err = "dr_filter: partition pruning kernel not built yet";
-  return DR_E_UNSUPPORTED;
+  *selected = nullptr;
+  *nselected = 0;
+  return guard(state->ctx, [&] {
+    HIP_OK(hipSetDevice(state->ctx->device));
+    std::vector<int64_t> v = filter_state(*state, *pred);
+    int64_t* out = static_cast<int64_t*>(malloc(std::max<size_t>(v.size(), 1) * sizeof(int64_t)));
+    if (!out) throw std::bad_alloc();
+    if (!v.empty()) memcpy(out, v.data(), v.size() * sizeof(int64_t));
+    *selected = out;
+    *nselected = int64_t(v.size());
+  });
 }
 
 void dr_free(void* p) { free(p); }

@@ -1,0 +1,451 @@
+// K5: partition pruning over the resident live AddFiles -- DeltaLog.filterFileList with the
+// filters rewritten by rewritePartitionFilters (D/DeltaLog.scala:500-547): every partition column
+// reference becomes Cast(partitionValues[col] AS partitionSchema(col).type), the conjuncts are
+// ANDed, and a file is kept where the predicate is TRUE (three-valued logic; NULL drops it).
+//
+// One thread per live file: it locates the file's partition values -- in its JSON line
+// (`add.partitionValues` object, resident in d_json) or in the checkpoint's decoded
+// `add.partitionValues` map column (entries of its row) -- casts them with Spark 3.1's non-ANSI
+// Cast(string AS type) as restated by the oracle (oracle/delta_oracle.py:cast_string), and runs the
+// postfix predicate program (include/deltareplay.h, dr_pred_op).
+#include "dev_common.h"
+#include "kernels.h"
+#include "../../include/deltareplay.h"
+
+namespace dr {
+namespace dev {
+
+enum PvState : uint8_t { PV_NULL = 0, PV_RAW = 1, PV_ESCAPED = 2 };
+
+// ---- minimal JSON walking over one line -------------------------------------------------------------
+__device__ __forceinline__ bool is_ws(uint8_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
+__device__ __forceinline__ const uint8_t* skip_ws(const uint8_t* p, const uint8_t* e) {
+  while (p < e && is_ws(*p)) ++p;
+  return p;
+}
+// p points after an opening quote; returns the closing quote (or e)
+__device__ const uint8_t* str_close(const uint8_t* p, const uint8_t* e, bool* esc) {
+  while (p < e) {
+    const uint8_t c = *p;
+    if (c == '"') return p;
+    if (c == '\\') { *esc = true; p += 2; continue; }
+    ++p;
+  }
+  return e;
+}
+// skips one JSON value starting at p (after whitespace); returns the position after it
+__device__ const uint8_t* skip_value(const uint8_t* p, const uint8_t* e) {
+  if (p >= e) return e;
+  if (*p == '"') {
+    bool esc = false;
+    const uint8_t* q = str_close(p + 1, e, &esc);
+    return q < e ? q + 1 : e;
+  }
+  if (*p == '{' || *p == '[') {
+    int depth = 0;
+    while (p < e) {
+      const uint8_t c = *p;
+      if (c == '"') {
+        bool esc = false;
+        const uint8_t* q = str_close(p + 1, e, &esc);
+        p = q < e ? q + 1 : e;
+        continue;
+      }
+      if (c == '{' || c == '[') ++depth;
+      else if (c == '}' || c == ']') {
+        if (--depth == 0) return p + 1;
+      }
+      ++p;
+    }
+    return e;
+  }
+  while (p < e && *p != ',' && *p != '}' && *p != ']' && !is_ws(*p)) ++p;
+  return p;
+}
+
+// JSON string span (raw, maybe escaped) == target bytes
+__device__ bool span_eq(const uint8_t* s, uint32_t n, bool esc, const uint8_t* t, uint32_t tn) {
+  if (!esc) {
+    if (n != tn) return false;
+    for (uint32_t k = 0; k < n; ++k)
+      if (s[k] != t[k]) return false;
+    return true;
+  }
+  if (n > 128) return false;
+  uint8_t buf[160];
+  const uint32_t m = json_unescape(s, n, buf);
+  if (m != tn) return false;
+  for (uint32_t k = 0; k < m; ++k)
+    if (buf[k] != t[k]) return false;
+  return true;
+}
+
+__device__ __forceinline__ bool key_is(const uint8_t* s, uint32_t n, bool esc, const char* lit, uint32_t ln) {
+  return span_eq(s, n, esc, reinterpret_cast<const uint8_t*>(lit), ln);
+}
+
+// Iterates the members of the object starting at p ('{'); f(key, klen, kesc, value_start) returns
+// the position after the value. Returns false on malformed input.
+template <typename F>
+__device__ bool each_member(const uint8_t* p, const uint8_t* e, F&& f) {
+  if (p >= e || *p != '{') return false;
+  ++p;
+  while (true) {
+    p = skip_ws(p, e);
+    if (p >= e) return false;
+    if (*p == '}') return true;
+    if (*p == ',') { ++p; continue; }
+    if (*p != '"') return false;
+    bool kesc = false;
+    const uint8_t* k0 = p + 1;
+    const uint8_t* k1 = str_close(k0, e, &kesc);
+    if (k1 >= e) return false;
+    p = skip_ws(k1 + 1, e);
+    if (p >= e || *p != ':') return false;
+    p = skip_ws(p + 1, e);
+    p = f(k0, uint32_t(k1 - k0), kesc, p);
+    if (p == nullptr) return false;
+  }
+}
+
+// ---- casts: Cast(string AS type), non-ANSI (failure -> NULL) ----------------------------------------
+struct SV {
+  int64_t v;
+  const uint8_t* s;
+  uint32_t n;
+  uint8_t null, str;
+};
+
+__device__ __forceinline__ bool cast_ws(uint8_t c) {  // UTF8String.trim-like set of the restatement
+  return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == 0x0b || c == 0x0c;
+}
+
+__device__ bool parse_int(const uint8_t* s, uint32_t n, int type, int64_t* out) {
+  uint32_t i = 0;
+  while (i < n && cast_ws(s[i])) ++i;
+  while (n > i && cast_ws(s[n - 1])) --n;
+  if (i >= n) return false;
+  bool neg = false;
+  if (s[i] == '+' || s[i] == '-') { neg = s[i] == '-'; ++i; }
+  if (i >= n) return false;
+  uint64_t acc = 0;
+  for (; i < n; ++i) {
+    const uint8_t c = s[i];
+    if (c < '0' || c > '9') return false;
+    const uint64_t d = c - '0';
+    if (acc > (~0ull - d) / 10) return false;  // beyond 64 bits: out of every range
+    acc = acc * 10 + d;
+  }
+  uint64_t lim_pos, lim_neg;  // |min|, max
+  switch (type) {
+    case DR_T_BYTE: lim_pos = 127; lim_neg = 128; break;
+    case DR_T_SHORT: lim_pos = 32767; lim_neg = 32768; break;
+    case DR_T_INT: lim_pos = 2147483647ull; lim_neg = 2147483648ull; break;
+    default: lim_pos = 9223372036854775807ull; lim_neg = 9223372036854775808ull; break;
+  }
+  if (neg ? acc > lim_neg : acc > lim_pos) return false;
+  *out = neg ? int64_t(0 - acc) : int64_t(acc);
+  return true;
+}
+
+__device__ __forceinline__ uint8_t lower(uint8_t c) { return (c >= 'A' && c <= 'Z') ? uint8_t(c + 32) : c; }
+
+__device__ bool parse_bool(const uint8_t* s, uint32_t n, int64_t* out) {
+  uint32_t i = 0;
+  while (i < n && cast_ws(s[i])) ++i;
+  while (n > i && cast_ws(s[n - 1])) --n;
+  const uint32_t m = n - i;
+  uint8_t b[5] = {0, 0, 0, 0, 0};
+  if (m == 0 || m > 5) return false;
+  for (uint32_t k = 0; k < m; ++k) b[k] = lower(s[i + k]);
+  auto is = [&](const char* w, uint32_t wl) {
+    if (wl != m) return false;
+    for (uint32_t k = 0; k < wl; ++k)
+      if (b[k] != uint8_t(w[k])) return false;
+    return true;
+  };
+  if (is("t", 1) || is("true", 4) || is("y", 1) || is("yes", 3) || is("1", 1)) { *out = 1; return true; }
+  if (is("f", 1) || is("false", 5) || is("n", 1) || is("no", 2) || is("0", 1)) { *out = 0; return true; }
+  return false;
+}
+
+__device__ __forceinline__ int64_t days_from_civil(int64_t y, int64_t m, int64_t d) {
+  y -= m <= 2;
+  const int64_t era = (y >= 0 ? y : y - 399) / 400;
+  const int64_t yoe = y - era * 400;
+  const int64_t doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
+  const int64_t doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+  return era * 146097 + doe - 719468;
+}
+
+// yyyy[-m[m][-d[d]][( |T)...]] after trimming (oracle/delta_oracle.py:cast_string "date")
+__device__ bool parse_date(const uint8_t* s, uint32_t n, int64_t* out) {
+  uint32_t i = 0;
+  while (i < n && cast_ws(s[i])) ++i;
+  while (n > i && cast_ws(s[n - 1])) --n;
+  auto digit = [&](uint32_t k) { return k < n && s[k] >= '0' && s[k] <= '9'; };
+  if (n - i < 4) return false;
+  int64_t y = 0;
+  for (int k = 0; k < 4; ++k) {
+    if (!digit(i)) return false;
+    y = y * 10 + (s[i++] - '0');
+  }
+  int64_t mo = 1, d = 1;
+  if (i < n) {
+    if (s[i] != '-') return false;
+    ++i;
+    if (!digit(i)) return false;
+    mo = s[i++] - '0';
+    if (digit(i)) mo = mo * 10 + (s[i++] - '0');
+    if (i < n) {
+      if (s[i] != '-') return false;
+      ++i;
+      if (!digit(i)) return false;
+      d = s[i++] - '0';
+      if (digit(i)) d = d * 10 + (s[i++] - '0');
+      if (i < n && s[i] != ' ' && s[i] != 'T') return false;
+    }
+  }
+  if (mo < 1 || mo > 12 || d < 1) return false;
+  const bool leap = (y % 4 == 0 && y % 100 != 0) || y % 400 == 0;
+  const int mdays[12] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+  const int64_t dim = mdays[mo - 1] + (mo == 2 && leap ? 1 : 0);
+  if (d > dim) return false;
+  *out = days_from_civil(y, mo, d);
+  return true;
+}
+
+__device__ SV cast_value(const uint8_t* s, uint32_t n, bool present, int type) {
+  SV r{0, nullptr, 0, 1, 0};
+  if (!present) return r;
+  if (type == DR_T_STRING) {
+    r.null = 0; r.str = 1; r.s = s; r.n = n;
+    return r;
+  }
+  int64_t v = 0;
+  bool ok = false;
+  if (type == DR_T_BOOLEAN) ok = parse_bool(s, n, &v);
+  else if (type == DR_T_DATE) ok = parse_date(s, n, &v);
+  else ok = parse_int(s, n, type, &v);
+  if (ok) { r.null = 0; r.v = v; }
+  return r;
+}
+
+__device__ int cmp_sv(const SV& a, const SV& b) {
+  if (a.str && b.str) {
+    const uint32_t m = a.n < b.n ? a.n : b.n;
+    for (uint32_t k = 0; k < m; ++k)
+      if (a.s[k] != b.s[k]) return a.s[k] < b.s[k] ? -1 : 1;
+    return a.n == b.n ? 0 : (a.n < b.n ? -1 : 1);
+  }
+  return a.v == b.v ? 0 : (a.v < b.v ? -1 : 1);
+}
+
+constexpr int PV_MAXC = 16;
+constexpr int PV_STACK = 32;
+
+__global__ void __launch_bounds__(256) k_filter(FilterArgs a) {
+  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= a.n_live) return;
+  const uint32_t act = a.live[i];
+  const uint8_t* vp[PV_MAXC];
+  uint32_t vn[PV_MAXC];
+  uint8_t vs[PV_MAXC];
+  for (int c = 0; c < a.ncols; ++c) { vp[c] = nullptr; vn[c] = 0; vs[c] = PV_NULL; }
+  auto match = [&](const uint8_t* k, uint32_t kn, bool kesc) -> int {
+    for (int c = 0; c < a.ncols; ++c)
+      if (span_eq(k, kn, kesc, a.col_names + a.col_name_off[c], uint32_t(a.col_name_off[c + 1] - a.col_name_off[c])))
+        return c;
+    return -1;
+  };
+  if (act >= a.ck_rows) {
+    // JSON line: {"add":{..., "partitionValues":{"c":"v", ...}, ...}}
+    const uint8_t* b = a.json + a.src_off[act];
+    const uint8_t* e = b + a.src_len[act];
+    const uint8_t* p = skip_ws(b, e);
+    bool ok = each_member(p, e, [&](const uint8_t* k, uint32_t kn, bool kesc, const uint8_t* v) -> const uint8_t* {
+      if (key_is(k, kn, kesc, "add", 3) && v < e && *v == '{') {
+        bool ok2 = each_member(v, e, [&](const uint8_t* k2, uint32_t kn2, bool kesc2, const uint8_t* v2) -> const uint8_t* {
+          if (key_is(k2, kn2, kesc2, "partitionValues", 15)) {
+            if (v2 < e && *v2 == '{') {
+              // Jackson map deserialisation: a repeated key keeps the last value
+              bool ok3 = each_member(v2, e, [&](const uint8_t* k3, uint32_t kn3, bool kesc3, const uint8_t* v3) -> const uint8_t* {
+                const int c = match(k3, kn3, kesc3);
+                const uint8_t* end3 = skip_value(v3, e);
+                if (c >= 0) {
+                  if (v3 < e && *v3 == '"') {
+                    bool vesc = false;
+                    const uint8_t* q = str_close(v3 + 1, e, &vesc);
+                    vp[c] = v3 + 1; vn[c] = uint32_t(q - v3 - 1); vs[c] = vesc ? PV_ESCAPED : PV_RAW;
+                  } else if (v3 < e && *v3 == 'n') {
+                    vs[c] = PV_NULL;
+                  } else {  // non-string token: Spark keeps its JSON text
+                    vp[c] = v3; vn[c] = uint32_t(end3 - v3); vs[c] = PV_RAW;
+                  }
+                }
+                return end3;
+              });
+              if (!ok3) return nullptr;
+            }
+          }
+          return skip_value(v2, e);
+        });
+        if (!ok2) return nullptr;
+      }
+      return skip_value(v, e);
+    });
+    if (!ok) atomicOr(a.error, 1u);
+    // escaped values are unescaped into the arena (sized by a counting pass)
+    for (int c = 0; c < a.ncols; ++c) {
+      if (vs[c] != PV_ESCAPED) continue;
+      if (!a.arena) { atomicAdd(a.arena_need, (unsigned long long)vn[c]); vs[c] = PV_NULL; continue; }
+      const unsigned long long o = atomicAdd(a.arena_fill, (unsigned long long)vn[c]);
+      if (o + vn[c] > a.arena_cap) { atomicOr(a.error, 2u); vs[c] = PV_NULL; continue; }
+      uint8_t* dst = a.arena + o;
+      vn[c] = json_unescape(vp[c], vn[c], dst);
+      vp[c] = dst;
+      vs[c] = PV_RAW;
+    }
+  } else if (a.has_map) {
+    const uint64_t r = a.src_off[act];
+    for (uint64_t en = a.row_start[r]; en < a.row_start[r + 1]; ++en) {
+      if (a.key_def[en] != a.key_max_def) continue;  // null / empty map
+      const int c = match(reinterpret_cast<const uint8_t*>(a.key_ptr[en]), a.key_len[en], false);
+      if (c < 0) continue;
+      if (a.val_def[en] == a.val_max_def) {
+        vp[c] = reinterpret_cast<const uint8_t*>(a.val_ptr[en]); vn[c] = a.val_len[en]; vs[c] = PV_RAW;
+      } else {
+        vs[c] = PV_NULL;
+      }
+    }
+  }
+  // ---- postfix program ----
+  SV st[PV_STACK];
+  int sp = 0;
+  bool bad = false;
+  for (int k = 0; k < a.nops && !bad; ++k) {
+    const int op = a.ops[2 * k], arg = a.ops[2 * k + 1];
+    switch (op) {
+      case DR_OP_COL: {
+        st[sp++] = cast_value(vp[arg], vn[arg], vs[arg] != PV_NULL, a.col_types[arg]);
+        break;
+      }
+      case DR_OP_LIT: {
+        SV v{0, nullptr, 0, 1, 0};
+        if (!a.lit_null[arg]) {
+          v.null = 0;
+          if (a.lit_types[arg] == DR_T_STRING) {
+            v.str = 1;
+            v.s = a.lit_str + a.lit_str_off[arg];
+            v.n = uint32_t(a.lit_str_off[arg + 1] - a.lit_str_off[arg]);
+          } else {
+            v.v = a.lit_i64[arg];
+          }
+        }
+        st[sp++] = v;
+        break;
+      }
+      case DR_OP_EQ: case DR_OP_NE: case DR_OP_LT: case DR_OP_LE: case DR_OP_GT: case DR_OP_GE: {
+        const SV y = st[--sp], x = st[--sp];
+        SV r{0, nullptr, 0, 1, 0};
+        if (!x.null && !y.null) {
+          const int c = cmp_sv(x, y);
+          r.null = 0;
+          r.v = op == DR_OP_EQ ? c == 0 : op == DR_OP_NE ? c != 0 : op == DR_OP_LT ? c < 0
+              : op == DR_OP_LE ? c <= 0 : op == DR_OP_GT ? c > 0 : c >= 0;
+        }
+        st[sp++] = r;
+        break;
+      }
+      case DR_OP_NSEQ: {
+        const SV y = st[--sp], x = st[--sp];
+        SV r{0, nullptr, 0, 0, 0};
+        r.v = (x.null && y.null) || (!x.null && !y.null && cmp_sv(x, y) == 0);
+        st[sp++] = r;
+        break;
+      }
+      case DR_OP_IN: {
+        sp -= arg;
+        const SV x = st[sp - 1];
+        SV r{0, nullptr, 0, 1, 0};
+        if (!x.null) {
+          bool found = false, anynull = false;
+          for (int q = 0; q < arg; ++q) {
+            if (st[sp + q].null) anynull = true;
+            else if (cmp_sv(x, st[sp + q]) == 0) found = true;
+          }
+          if (found) { r.null = 0; r.v = 1; }
+          else if (!anynull) { r.null = 0; r.v = 0; }
+        }
+        st[sp - 1] = r;
+        break;
+      }
+      case DR_OP_ISNULL: case DR_OP_ISNOTNULL: {
+        const SV x = st[--sp];
+        SV r{0, nullptr, 0, 0, 0};
+        r.v = op == DR_OP_ISNULL ? x.null : !x.null;
+        st[sp++] = r;
+        break;
+      }
+      case DR_OP_AND: {
+        const SV y = st[--sp], x = st[--sp];
+        SV r{0, nullptr, 0, 1, 0};
+        if ((!x.null && !x.v) || (!y.null && !y.v)) { r.null = 0; r.v = 0; }
+        else if (!x.null && !y.null) { r.null = 0; r.v = 1; }
+        st[sp++] = r;
+        break;
+      }
+      case DR_OP_OR: {
+        const SV y = st[--sp], x = st[--sp];
+        SV r{0, nullptr, 0, 1, 0};
+        if ((!x.null && x.v) || (!y.null && y.v)) { r.null = 0; r.v = 1; }
+        else if (!x.null && !y.null) { r.null = 0; r.v = 0; }
+        st[sp++] = r;
+        break;
+      }
+      case DR_OP_NOT: {
+        SV& x = st[sp - 1];
+        if (!x.null) x.v = !x.v;
+        break;
+      }
+      default: bad = true;
+    }
+  }
+  a.flag[i] = (!bad && sp == 1 && !st[0].null && st[0].v) ? 1u : 0u;
+}
+
+// checkpoint map column: row_start[k] = index of the k-th entry with repetition level 0
+__global__ void k_row_starts(const uint8_t* rep, uint64_t n, const uint64_t* pos, uint64_t* row_start) {
+  const uint64_t e = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (e < n && rep[e] == 0) row_start[pos[e]] = e;
+}
+__global__ void k_rep0_flags(const uint8_t* rep, uint64_t n, uint32_t* f) {
+  const uint64_t e = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (e < n) f[e] = rep[e] == 0;
+}
+__global__ void k_select(const uint32_t* flag, const uint64_t* pos, uint64_t n, int64_t* out) {
+  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n && flag[i]) out[pos[i]] = int64_t(i);
+}
+
+}  // namespace dev
+
+static inline unsigned g256(uint64_t n) { return unsigned((n + 255) / 256); }
+
+uint32_t filter_max_cols() { return dev::PV_MAXC; }
+uint32_t filter_max_stack() { return dev::PV_STACK; }
+
+void launch_filter(const FilterArgs& a, hipStream_t st) {
+  if (a.n_live) hipLaunchKernelGGL(dev::k_filter, dim3(g256(a.n_live)), dim3(256), 0, st, a);
+}
+void launch_rep0_flags(const uint8_t* rep, uint64_t n, uint32_t* f, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(dev::k_rep0_flags, dim3(g256(n)), dim3(256), 0, st, rep, n, f);
+}
+void launch_row_starts(const uint8_t* rep, uint64_t n, const uint64_t* pos, uint64_t* row_start, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(dev::k_row_starts, dim3(g256(n)), dim3(256), 0, st, rep, n, pos, row_start);
+}
+void launch_select(const uint32_t* flag, const uint64_t* pos, uint64_t n, int64_t* out, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(dev::k_select, dim3(g256(n)), dim3(256), 0, st, flag, pos, n, out);
+}
+
+}  // namespace dr

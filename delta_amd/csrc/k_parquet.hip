@@ -150,11 +150,14 @@ __device__ __forceinline__ bool ba_region(const PageDesc& pg, const uint8_t** b,
   const uint8_t* end = p + pg.usize;
   if (pg.kind == PG_DATA_V2) {
     p += pg.v2_rep_len + pg.v2_def_len;
-  } else if (pg.kind != PG_DICT && pg.max_def > 0) {
-    if (end - p < 4) return false;
-    const uint32_t l = load_u32(p);
-    if (uint64_t(end - p - 4) < l) return false;
-    p += 4 + l;
+  } else if (pg.kind != PG_DICT) {
+    for (int sec = 0; sec < 2; ++sec) {  // repetition levels, then definition levels
+      if ((sec == 0 ? pg.max_rep : pg.max_def) <= 0) continue;
+      if (end - p < 4) return false;
+      const uint32_t l = load_u32(p);
+      if (uint64_t(end - p - 4) < l) return false;
+      p += 4 + l;
+    }
   }
   *b = p;
   *e = end;
@@ -330,6 +333,7 @@ __global__ void __launch_bounds__(64) k_pq_data(ParquetArgs a) {
   const PageDesc& pg = a.pages[pi];
   if (pg.kind == PG_DICT) return;
   __shared__ uint8_t defs[SEG];
+  __shared__ uint8_t reps[SEG];
   __shared__ uint32_t idxs[SEG];
   __shared__ uint64_t vptr[SEG];
   __shared__ uint32_t vlen[SEG];
@@ -337,12 +341,24 @@ __global__ void __launch_bounds__(64) k_pq_data(ParquetArgs a) {
   const FlatColumn col = a.cols[pg.col];
   const uint8_t* p = reinterpret_cast<const uint8_t*>(pg.dst);
   const uint8_t* end = p + pg.usize;
-  Rle defr;
+  Rle defr, repr;
   defr.init(p, p, 0);
+  repr.init(p, p, 0);
   if (pg.kind == PG_DATA_V2) {
+    if (pg.max_rep > 0) repr.init(p, p + pg.v2_rep_len, level_width(pg.max_rep));
     defr.init(p + pg.v2_rep_len, p + pg.v2_rep_len + pg.v2_def_len, level_width(pg.max_def));
     p += pg.v2_rep_len + pg.v2_def_len;
-  } else if (pg.max_def > 0) {
+  } else if (pg.max_rep > 0 || pg.max_def > 0) {
+    if (pg.max_rep > 0) {
+      if (end - p < 4) { if (lane == 0) set_err(a.error, PQE_LEVELS); return; }
+      const uint32_t l = load_u32(p);
+      p += 4;
+      if (uint64_t(end - p) < l) { if (lane == 0) set_err(a.error, PQE_LEVELS); return; }
+      repr.init(p, p + l, level_width(pg.max_rep));
+      p += l;
+    }
+  }
+  if (pg.kind != PG_DATA_V2 && pg.max_def > 0) {
     if (end - p < 4) { if (lane == 0) set_err(a.error, PQE_LEVELS); return; }
     const uint32_t l = load_u32(p);
     p += 4;
@@ -376,6 +392,10 @@ __global__ void __launch_bounds__(64) k_pq_data(ParquetArgs a) {
   uint64_t vbase = 0;  // values consumed before this segment (PLAIN fixed / boolean)
   for (uint32_t s0 = 0; s0 < pg.num_values; s0 += SEG) {
     const uint32_t n = min(SEG, pg.num_values - s0);
+    if (pg.max_rep > 0) {
+      repr.expand(reps, n, lane);
+      if (repr.bad) { if (lane == 0) set_err(a.error, PQE_LEVELS); return; }
+    }
     if (pg.max_def > 0) {
       defr.expand(defs, n, lane);
       if (defr.bad) { if (lane == 0) set_err(a.error, PQE_LEVELS); return; }
@@ -418,6 +438,7 @@ __global__ void __launch_bounds__(64) k_pq_data(ParquetArgs a) {
       const uint64_t row = pg.row_base + s0 + i;
       const uint8_t d = defs[i];
       col.def[row] = d;
+      if (pg.max_rep > 0) col.rep[row] = reps[i];
       if (int(d) != pg.max_def) continue;
       const uint32_t k = idxs[i];
       if (dict) {

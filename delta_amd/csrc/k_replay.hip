@@ -80,51 +80,6 @@ __global__ void __launch_bounds__(SCAN_T) k_scan_apply(const uint32_t* in, uint6
 }
 
 // ---- canonicalization of special paths (D/Snapshot.scala:317-328) -------------------------------
-__device__ int hexval(uint8_t c) {
-  if (c >= '0' && c <= '9') return c - '0';
-  if (c >= 'a' && c <= 'f') return c - 'a' + 10;
-  if (c >= 'A' && c <= 'F') return c - 'A' + 10;
-  return -1;
-}
-
-// JSON string unescape into out; returns the output length (UTF-8).
-__device__ uint32_t json_unescape(const uint8_t* s, uint32_t n, uint8_t* out) {
-  uint32_t o = 0;
-  for (uint32_t i = 0; i < n; ++i) {
-    uint8_t c = s[i];
-    if (c != '\\' || i + 1 >= n) { out[o++] = c; continue; }
-    uint8_t e = s[++i];
-    switch (e) {
-      case 'b': out[o++] = '\b'; break;
-      case 'f': out[o++] = '\f'; break;
-      case 'n': out[o++] = '\n'; break;
-      case 'r': out[o++] = '\r'; break;
-      case 't': out[o++] = '\t'; break;
-      case 'u': {
-        uint32_t cp = 0;
-        for (int k = 0; k < 4 && i + 1 < n; ++k) cp = cp * 16 + uint32_t(hexval(s[++i]) & 15);
-        if (cp >= 0xD800 && cp < 0xDC00 && i + 6 < n && s[i + 1] == '\\' && s[i + 2] == 'u') {
-          uint32_t lo = 0;
-          for (int k = 0; k < 4; ++k) lo = lo * 16 + uint32_t(hexval(s[i + 3 + k]) & 15);
-          if (lo >= 0xDC00 && lo < 0xE000) { cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00); i += 6; }
-        }
-        if (cp < 0x80) out[o++] = uint8_t(cp);
-        else if (cp < 0x800) { out[o++] = uint8_t(0xC0 | (cp >> 6)); out[o++] = uint8_t(0x80 | (cp & 63)); }
-        else if (cp < 0x10000) {
-          out[o++] = uint8_t(0xE0 | (cp >> 12)); out[o++] = uint8_t(0x80 | ((cp >> 6) & 63));
-          out[o++] = uint8_t(0x80 | (cp & 63));
-        } else {
-          out[o++] = uint8_t(0xF0 | (cp >> 18)); out[o++] = uint8_t(0x80 | ((cp >> 12) & 63));
-          out[o++] = uint8_t(0x80 | ((cp >> 6) & 63)); out[o++] = uint8_t(0x80 | (cp & 63));
-        }
-        break;
-      }
-      default: out[o++] = e; break;  // \" \\ \/
-    }
-  }
-  return o;
-}
-
 // Replay key of a canonical path: java.net.URI equality treats "file:///x" and "file:/x" alike.
 __device__ __forceinline__ uint32_t key_skip(const uint8_t* p, uint32_t n) {
   return (n >= 8 && p[0] == 'f' && p[1] == 'i' && p[2] == 'l' && p[3] == 'e' && p[4] == ':' && p[5] == '/' &&

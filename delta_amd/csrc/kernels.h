@@ -66,6 +66,7 @@ struct PageDesc {
   int32_t col;           // output column slot
   int32_t phys;          // physical type
   int32_t max_def;
+  int32_t max_rep;       // > 0: repeated leaf (map key/value); row_base then counts level entries
   int32_t dict;          // index (into the page table) of this chunk's dictionary page, -1 none
   uint64_t row_base;     // first checkpoint row of the page (flat columns)
   int32_t v2_def_len, v2_rep_len, v2_compressed;
@@ -77,9 +78,10 @@ struct PageDesc {
   uint64_t hit_base;     // first u32 word of this page's hit bitmap
 };
 
-// Decoded flat column (max_rep == 0): one entry per checkpoint row.
+// Decoded column: one entry per checkpoint row (flat leaf) or per level entry (repeated leaf).
 struct FlatColumn {
-  uint8_t* def;          // definition level per row
+  uint8_t* def;          // definition level per row / entry
+  uint8_t* rep;          // repetition level per entry (repeated leaves only)
   int64_t* ival;         // INT64/INT32/BOOLEAN value (valid where def == max_def)
   uint64_t* sptr;        // BYTE_ARRAY: device address of the value bytes
   uint32_t* slen;
@@ -245,6 +247,52 @@ void launch_verdict_set(const uint32_t* idx, uint64_t n, uint8_t v, uint8_t* ver
 void launch_verdict_flags(const uint8_t* verdict, uint64_t n, uint32_t* f_live, uint32_t* f_tomb, hipStream_t st);
 void launch_verdict_collect(const uint8_t* verdict, const uint32_t* send_idx, uint64_t n, uint8_t want,
                             const uint64_t* pos, uint32_t* out, hipStream_t st);
+
+// ---- K5: partition pruning (k_filter.hip) -------------------------------------------------------
+struct FilterArgs {
+  const uint32_t* live;          // live AddFile action indices (export order)
+  uint64_t n_live;
+  const uint64_t* src_off;       // JSON: line offset; checkpoint: row
+  const uint32_t* src_len;
+  uint64_t ck_rows;              // actions below this index are checkpoint rows
+  const uint8_t* json;           // staged JSON bytes
+  // checkpoint add.partitionValues map (level entries)
+  int32_t has_map;
+  const uint64_t* row_start;     // [ck_rows + 1]
+  const uint8_t* key_def;
+  const uint64_t* key_ptr;
+  const uint32_t* key_len;
+  int32_t key_max_def;
+  const uint8_t* val_def;
+  const uint64_t* val_ptr;
+  const uint32_t* val_len;
+  int32_t val_max_def;
+  // predicate program (include/deltareplay.h dr_predicate, uploaded)
+  int32_t ncols;
+  const uint64_t* col_name_off;  // [ncols + 1]
+  const uint8_t* col_names;
+  const int32_t* col_types;
+  int32_t nops;
+  const int32_t* ops;            // [nops * 2] opcode, arg
+  const int32_t* lit_types;
+  const int64_t* lit_i64;
+  const uint8_t* lit_null;
+  const uint64_t* lit_str_off;   // [nlits + 1]
+  const uint8_t* lit_str;
+  // unescaped JSON values (null arena: count the bytes needed into arena_need)
+  uint8_t* arena;
+  uint64_t arena_cap;
+  unsigned long long* arena_fill;
+  unsigned long long* arena_need;
+  uint32_t* flag;                // [n_live] 1 = selected
+  uint32_t* error;
+};
+uint32_t filter_max_cols();
+uint32_t filter_max_stack();
+void launch_filter(const FilterArgs& a, hipStream_t st);
+void launch_rep0_flags(const uint8_t* rep, uint64_t n, uint32_t* f, hipStream_t st);
+void launch_row_starts(const uint8_t* rep, uint64_t n, const uint64_t* pos, uint64_t* row_start, hipStream_t st);
+void launch_select(const uint32_t* flag, const uint64_t* pos, uint64_t n, int64_t* out, hipStream_t st);
 
 }  // namespace dr
 

@@ -1,0 +1,218 @@
+"""Partition-pruning predicates: the host side of K5 (`dr_filter`).
+
+Mirrors the reference's metadata-predicate handling:
+  split_metadata_and_data_predicates <- DeltaTableUtils.splitMetadataAndDataPredicates /
+                                        isPredicatePartitionColumnsOnly (D/DeltaTable.scala:198-294)
+  build_program                      <- DeltaLog.rewritePartitionFilters + filterFileList
+                                        (D/DeltaLog.scala:500-547): every partition column becomes
+                                        Cast(partitionValues[col] AS partitionSchema(col).type), the
+                                        filters are ANDed
+  partition_schema                   <- Metadata.partitionSchema (D/actions/actions.scala:370-373)
+
+Expressions are nested tuples (the oracle's format): ("col", name), ("lit", type, value),
+(op, a, b) for = != < <= > >= <=>, ("in", a, [lits]), ("isnull", a), ("isnotnull", a),
+("and", a, b), ("or", a, b), ("not", a). Types: "string", "byte", "short", "integer", "long",
+"date", "boolean". The program is evaluated on the GPU; nothing here evaluates it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import datetime as _dt
+import json
+import re
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+from . import _native as N
+
+TYPE_CODE = {"string": 0, "byte": 1, "short": 2, "integer": 3, "long": 4, "date": 5, "boolean": 6}
+OP_COL, OP_LIT = 0, 1
+OP_CODE = {"=": 2, "!=": 3, "<": 4, "<=": 5, ">": 6, ">=": 7, "<=>": 8, "in": 9, "isnull": 10,
+           "isnotnull": 11, "and": 12, "or": 13, "not": 14}
+_EPOCH = _dt.date(1970, 1, 1)
+
+
+class PredicateError(ValueError):
+    pass
+
+
+def partition_schema(metadata: Optional[dict]) -> Dict[str, str]:
+    """Metadata.partitionSchema: partition column -> Spark type name (ordered as partitionColumns)."""
+    if not metadata:
+        return {}
+    schema = json.loads(metadata["schemaString"])
+    fields = {f["name"]: f["type"] for f in schema["fields"]}
+    return {c: fields[c] for c in metadata.get("partitionColumns") or []}
+
+
+def _refs(expr) -> List[str]:
+    op = expr[0]
+    if op == "col":
+        return [expr[1]]
+    if op == "lit":
+        return []
+    if op == "in":
+        return _refs(expr[1]) + [r for l in expr[2] for r in _refs(l)]
+    return [r for a in expr[1:] for r in _refs(a)]
+
+
+def _conjuncts(expr) -> List:
+    if expr[0] == "and":
+        return _conjuncts(expr[1]) + _conjuncts(expr[2])
+    return [expr]
+
+
+def _resolve(name: str, partition_cols: Sequence[str]) -> Optional[str]:
+    # rewritePartitionFilters (D/DeltaLog.scala:531-533): backticks stripped, then the session
+    # resolver (spark.sql.caseSensitive=false: case-insensitive) finds the partition field
+    name = name.strip("`")
+    for c in partition_cols:
+        if c.lower() == name.lower():
+            return c
+    return None
+
+
+def split_metadata_and_data_predicates(expr, partition_cols: Sequence[str]) -> Tuple[List, List]:
+    """(metadata-only conjuncts, the rest): a conjunct is metadata-only when every column it
+    references is a partition column (D/DeltaTable.scala:198-230)."""
+    meta, data = [], []
+    for c in _conjuncts(expr):
+        refs = _refs(c)
+        if all(_resolve(r, partition_cols) is not None for r in refs):
+            meta.append(c)
+        else:
+            data.append(c)
+    return meta, data
+
+
+@dataclass
+class Program:
+    ops: List[Tuple[int, int]] = field(default_factory=list)
+    cols: List[Tuple[str, int]] = field(default_factory=list)      # (exact map key, type code)
+    lits: List[Tuple[int, object]] = field(default_factory=list)   # (type code, value | None)
+
+
+_DATE_RE = re.compile(r"(\d{4})(?:-(\d{1,2})(?:-(\d{1,2})(?:[ T].*)?)?)?")
+
+
+def _date_days(s: str) -> Optional[int]:
+    """Cast(string AS date) of a literal, the same grammar the device applies to partition values."""
+    m = _DATE_RE.fullmatch(s.strip(" \t\n\r\x0b\x0c"))
+    if not m:
+        return None
+    try:
+        return (_dt.date(int(m.group(1)), int(m.group(2) or 1), int(m.group(3) or 1)) - _EPOCH).days
+    except ValueError:
+        return None
+
+
+def _lit(typ: str, v):
+    """Literal value as the device sees it (the oracle's _lit_value): dates as days since the
+    epoch, booleans as 0/1, strings as bytes."""
+    if typ not in TYPE_CODE:
+        raise PredicateError("unsupported literal type %r" % typ)
+    if v is None:
+        return None
+    if typ == "date":
+        if isinstance(v, str):
+            days = _date_days(v)
+            if days is None:
+                raise PredicateError("bad date literal %r" % v)
+            return days
+        if isinstance(v, _dt.date):
+            return (v - _EPOCH).days
+        return int(v)
+    if typ == "boolean":
+        return 1 if v else 0
+    if typ == "string":
+        return str(v).encode("utf-8")
+    return int(v)
+
+
+def build_program(schema: Dict[str, str], preds: Sequence) -> Program:
+    """AND of `preds` lowered to the postfix program of include/deltareplay.h (dr_pred_op)."""
+    if not preds:
+        raise PredicateError("no predicates")
+    p = Program()
+    colidx: Dict[str, int] = {}
+    parts = list(schema)
+
+    def col(name):
+        exact = _resolve(name, parts)
+        if exact is None:
+            raise PredicateError("%s is not a partition column" % name)
+        typ = schema[exact]
+        if typ not in TYPE_CODE:
+            raise PredicateError("partition column %s has unsupported type %s" % (exact, typ))
+        if exact not in colidx:
+            colidx[exact] = len(p.cols)
+            p.cols.append((exact, TYPE_CODE[typ]))
+        p.ops.append((OP_COL, colidx[exact]))
+
+    def lit(typ, v):
+        p.lits.append((TYPE_CODE[typ], _lit(typ, v)))
+        p.ops.append((OP_LIT, len(p.lits) - 1))
+
+    def emit(e):
+        op = e[0]
+        if op == "col":
+            col(e[1])
+        elif op == "lit":
+            lit(e[1], e[2])
+        elif op == "in":
+            emit(e[1])
+            for l in e[2]:
+                emit(l)
+            p.ops.append((OP_CODE["in"], len(e[2])))
+        elif op in ("isnull", "isnotnull", "not"):
+            emit(e[1])
+            p.ops.append((OP_CODE[op], 0))
+        elif op in OP_CODE:
+            emit(e[1])
+            emit(e[2])
+            p.ops.append((OP_CODE[op], 0))
+        else:
+            raise PredicateError("unsupported expression %r" % (op,))
+
+    emit(preds[0])
+    for e in preds[1:]:
+        emit(e)
+        p.ops.append((OP_CODE["and"], 0))
+    return p
+
+
+def lower_program(prog: Program):
+    """ctypes dr_predicate for `prog` (+ the buffers that must outlive the call)."""
+    keep = []
+    nops = len(prog.ops)
+    ops = (N.dr_pred_op * max(nops, 1))()
+    for i, (o, a) in enumerate(prog.ops):
+        ops[i] = N.dr_pred_op(o, a)
+    ncols = len(prog.cols)
+    names = (C.c_char_p * max(ncols, 1))()
+    ctypes_ = (C.c_int32 * max(ncols, 1))()
+    for i, (n, t) in enumerate(prog.cols):
+        b = C.create_string_buffer(n.encode("utf-8"))
+        keep.append(b)
+        names[i] = C.cast(b, C.c_char_p)
+        ctypes_[i] = t
+    nl = len(prog.lits)
+    lt = (C.c_int32 * max(nl, 1))()
+    li = (C.c_int64 * max(nl, 1))()
+    ln = (C.c_uint8 * max(nl, 1))()
+    lo = (C.c_int64 * (nl + 1))()
+    blob = b""
+    for i, (t, v) in enumerate(prog.lits):
+        lt[i] = t
+        lo[i] = len(blob)
+        if v is None:
+            ln[i] = 1
+        elif isinstance(v, bytes):
+            blob += v
+        else:
+            li[i] = int(v)
+    lo[nl] = len(blob)
+    lb = (C.c_uint8 * max(len(blob), 1)).from_buffer_copy(blob + b"\0")
+    keep += [ops, names, ctypes_, lt, li, ln, lo, lb]
+    pred = N.dr_predicate(nops, ops, ncols, names, ctypes_, nl, lt, li, ln, lo, lb)
+    return pred, keep

@@ -312,6 +312,60 @@ def write_checkpoint(path: str, pool: FilePool, add_ids: np.ndarray, ncols: int,
     return nrows
 
 
+def write_checkpoint_records(path: str, protocol: dict, metadata: dict, adds: list, removes: list = (),
+                             txns: list = (), row_group_size: int = 1 << 20, use_dictionary: bool = True,
+                             data_page_version: str = "1.0", data_page_size: int = 1 << 20) -> int:
+    """Checkpoint with the reference's column layout from explicit action records (edge-case
+    corpora: any partitionValues / tags maps, nulls). Rows: protocol, metaData, txns, adds, removes."""
+    pa, _ = _pa()
+    import pyarrow.parquet as pq
+    mt = pa.map_(pa.string(), pa.string())
+    add_type = pa.struct([("path", pa.string()), ("partitionValues", mt), ("size", pa.int64()),
+                          ("modificationTime", pa.int64()), ("dataChange", pa.bool_()), ("tags", mt),
+                          ("stats", pa.string())])
+    rm_type = pa.struct([("path", pa.string()), ("deletionTimestamp", pa.int64()),
+                         ("dataChange", pa.bool_()), ("extendedFileMetadata", pa.bool_()),
+                         ("partitionValues", mt), ("size", pa.int64()), ("tags", mt)])
+    txn_type = pa.struct([("appId", pa.string()), ("version", pa.int64()), ("lastUpdated", pa.int64())])
+    fmt_type = pa.struct([("provider", pa.string()), ("options", mt)])
+    md_type = pa.struct([("id", pa.string()), ("name", pa.string()), ("description", pa.string()),
+                         ("format", fmt_type), ("schemaString", pa.string()),
+                         ("partitionColumns", pa.list_(pa.string())), ("configuration", mt),
+                         ("createdTime", pa.int64())])
+    prot_type = pa.struct([("minReaderVersion", pa.int32()), ("minWriterVersion", pa.int32())])
+
+    def m(d):
+        return None if d is None else list(d.items())
+
+    rows = []
+    rows.append({"protocol": protocol})
+    md = dict(metadata)
+    rows.append({"metaData": {"id": md["id"], "name": md.get("name"), "description": md.get("description"),
+                              "format": {"provider": md.get("format", {}).get("provider", "parquet"),
+                                         "options": m(md.get("format", {}).get("options") or {})},
+                              "schemaString": md["schemaString"], "partitionColumns": md.get("partitionColumns", []),
+                              "configuration": m(md.get("configuration") or {}), "createdTime": md.get("createdTime")}})
+    rows += [{"txn": t} for t in txns]
+    for a in adds:
+        rows.append({"add": dict(path=a["path"], partitionValues=m(a.get("partitionValues")), size=a.get("size", 0),
+                                 modificationTime=a.get("modificationTime", 0), dataChange=False,
+                                 tags=m(a.get("tags")), stats=a.get("stats"))})
+    for r in removes:
+        rows.append({"remove": dict(path=r["path"], deletionTimestamp=r.get("deletionTimestamp"), dataChange=False,
+                                    extendedFileMetadata=r.get("extendedFileMetadata", False),
+                                    partitionValues=m(r.get("partitionValues")), size=r.get("size"),
+                                    tags=m(r.get("tags")))})
+    cols = {}
+    for name, typ in (("txn", txn_type), ("add", add_type), ("remove", rm_type), ("metaData", md_type),
+                      ("protocol", prot_type)):
+        cols[name] = pa.array([r.get(name) for r in rows], typ)
+    table = pa.Table.from_arrays(list(cols.values()), names=list(cols))
+    pq.write_table(table, path, compression="snappy", use_dictionary=use_dictionary, version="1.0",
+                   data_page_version=data_page_version, row_group_size=row_group_size,
+                   data_page_size=data_page_size, write_statistics=False)
+    return len(rows)
+
+
 # ----------------------------------------------------------------------------------------------
 # Config builders
 # ----------------------------------------------------------------------------------------------

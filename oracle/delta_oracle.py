@@ -521,8 +521,14 @@ def _lit_value(typ: str, v):
 def eval_predicate(expr, pv: Dict[str, Optional[str]], schema: Dict[str, str]):
     op = expr[0]
     if op == "col":
-        name = expr[1]
-        return cast_string((pv or {}).get(name), schema[name])
+        # rewritePartitionFilters (D/DeltaLog.scala:525-546): backticks stripped, the partition
+        # field found with the (case-insensitive) resolver, Cast(partitionValues[field] AS type);
+        # an unknown column stays an uncast map lookup
+        name = expr[1].strip("`")
+        field = next((f for f in schema if f.lower() == name.lower()), None)
+        if field is None:
+            return (pv or {}).get(name)
+        return cast_string((pv or {}).get(field), schema[field])
     if op == "lit":
         return _lit_value(expr[1], expr[2])
     if op in ("=", "!=", "<", "<=", ">", ">="):

@@ -1,0 +1,114 @@
+"""GPU parity of K5 partition pruning (dr_filter) against the oracle's filterFileList restatement:
+Spark non-ANSI casts of odd partition strings, three-valued logic, IN with NULL, null-safe
+equality, JSON escapes in keys and values, values read from JSON commits and from the
+checkpoint's add.partitionValues map column; the OptimisticTransactionSuite-style int-partition
+predicates (T/OptimisticTransactionSuite.scala:117-450); the config-4 conjunction."""
+import os
+
+import pytest
+
+from oracle import delta_oracle as O
+from tests import filter_corpus as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def engine():
+    from delta_amd.delta_log import Engine
+    return Engine.get(0)
+
+
+def _gpu_selected(engine, lp, preds_list, cutoff=0):
+    from delta_amd.predicates import build_program, partition_schema
+    staged = engine.stage_log(lp)
+    st = staged.replay(cutoff)
+    staged.release()
+    try:
+        live = st.export(0)
+        meta = next(a["metaData"] for a in st.nonfile if "metaData" in a)
+        schema = partition_schema(meta)
+        out = []
+        for preds in preds_list:
+            sel = st.filter(build_program(schema, preds))
+            assert sel == sorted(set(sel))
+            out.append(sorted(live[i]["path"] for i in sel))
+        return out
+    finally:
+        st.release()
+
+
+def _oracle_selected(lp, preds_list, cutoff=0):
+    snap = O.state_reconstruction(O.get_log_segment(lp), cutoff)
+    schema = O.partition_schema(snap.metadata)
+    return [sorted(f["path"] for f in O.filter_file_list(schema, snap.all_files, p)) for p in preds_list]
+
+
+@pytest.mark.parametrize("checkpoint", [False, True])
+@pytest.mark.parametrize("escaped_keys", [False, True])
+def test_filter_cast_corpus(engine, tmp_path, checkpoint, escaped_keys):
+    lp = F.build(str(tmp_path), checkpoint=checkpoint, escaped_keys=escaped_keys)
+    got = _gpu_selected(engine, lp, F.PREDICATES)
+    want = _oracle_selected(lp, F.PREDICATES)
+    for p, g, w in zip(F.PREDICATES, got, want):
+        assert g == w, p
+
+
+def _int_table(tmp_path, cols, rows, checkpoint):
+    """Small table partitioned by integer columns (OptimisticTransactionSuite's `part`, `a`/`b`)."""
+    import json
+    log = os.path.join(str(tmp_path), "_delta_log")
+    os.makedirs(log)
+    schema = {"type": "struct", "fields": [{"name": "x", "type": "long", "nullable": True, "metadata": {}}] +
+              [{"name": c, "type": "integer", "nullable": True, "metadata": {}} for c in cols]}
+    md = {"id": "ots", "format": {"provider": "parquet", "options": {}},
+          "schemaString": json.dumps(schema), "partitionColumns": cols, "configuration": {}, "createdTime": 1}
+    adds = [{"path": "/".join("%s=%s" % (c, v) for c, v in zip(cols, r)) + "/f%d" % k,
+             "partitionValues": {c: str(v) for c, v in zip(cols, r)}, "size": 1, "modificationTime": 1,
+             "dataChange": True} for k, r in enumerate(rows)]
+    with open(os.path.join(log, "%020d.json" % 0), "w") as f:
+        f.write(json.dumps({"protocol": {"minReaderVersion": 1, "minWriterVersion": 2}}) + "\n")
+        f.write(json.dumps({"metaData": md}) + "\n")
+        for a in adds:
+            f.write(json.dumps({"add": a}) + "\n")
+    if checkpoint:
+        from delta_amd.testing import synth as S
+        S.write_checkpoint_records(os.path.join(log, "%020d.checkpoint.parquet" % 0),
+                                   {"minReaderVersion": 1, "minWriterVersion": 2}, md, adds)
+    return log
+
+
+C, L = F.C, F.L
+
+
+@pytest.mark.parametrize("checkpoint", [False, True])
+def test_filter_optimistic_txn_cases(engine, tmp_path, checkpoint):
+    lp = _int_table(tmp_path / "one", ["part"], [(p,) for p in range(1, 6)] * 3, checkpoint)
+    preds = [[("=", C("part"), L("integer", 3))], [("in", C("part"), [L("integer", 1)])],
+             [(">=", C("part"), L("integer", 2))], [(">", C("part"), L("integer", 1)), ("<=", C("part"), L("integer", 3))],
+             [(">", C("part"), L("integer", 3))], [("<=", C("part"), L("integer", 3))]]
+    assert _gpu_selected(engine, lp, preds) == _oracle_selected(lp, preds)
+    lp2 = _int_table(tmp_path / "two", ["a", "b"], [(a, b) for a in range(3) for b in range(3)], checkpoint)
+    preds2 = [[("and", ("=", C("a"), L("integer", 1)), ("=", C("b"), L("integer", 1)))],
+              [("=", C("a"), L("integer", 1))], [("or", (">=", C("a"), L("integer", 1)), (">", C("b"), L("integer", 1)))],
+              [("=", C("a"), L("integer", 2))]]
+    assert _gpu_selected(engine, lp2, preds2) == _oracle_selected(lp2, preds2)
+
+
+def test_filter_config4_predicate(engine, tmp_path):
+    """p0 >= DATE'2020-03-01' AND p0 < DATE'2020-06-01' AND p1 IN (1..100)
+    AND p2 = 'w17' AND p3 = true, over a 4-column checkpoint + churn commits."""
+    from delta_amd.testing import synth as S
+    spec = S.ChurnSpec(ckpt_files=30000, ckpt_version=10, n_deltas=4, removes_per_delta=2000,
+                       adds_per_delta=2000, readd_frac=0.5, ncols=4)
+    exp = S.build_table(str(tmp_path), spec, seed=4, row_group_size=7000)
+    lp = os.path.join(str(tmp_path), "_delta_log")
+    word = S.WORDS[17]
+    preds = [[(">=", C("p0"), L("date", "2020-03-01")), ("<", C("p0"), L("date", "2020-06-01")),
+              ("in", C("p1"), [L("integer", v) for v in range(1, 101)]), ("=", C("p2"), L("string", word)),
+              ("=", C("p3"), L("boolean", True))],
+             [("isnull", C("p2"))],
+             [("in", C("p1"), [L("integer", v) for v in range(1, 101)])]]
+    got = _gpu_selected(engine, lp, preds, exp.min_file_retention_timestamp)
+    assert got == _oracle_selected(lp, preds, exp.min_file_retention_timestamp)
+    assert len(got[0]) > 0 and len(got[1]) > 0

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <functional>
 #include <type_traits>
 #include <cstring>
 #include <map>
@@ -1134,35 +1135,85 @@ static void check_program(const dr_predicate& p) {
   for (int32_t c = 0; c < p.ncols; ++c)
     if (p.col_types[c] < DR_T_STRING || p.col_types[c] > DR_T_BOOLEAN || !p.col_names[c])
       fail(DR_E_UNSUPPORTED, "unsupported partition column type");
-  int depth = 0;
+  // stack discipline: every op's operands are whole subtrees (postfix -> tree)
+  std::vector<int32_t> stack;
   for (int32_t k = 0; k < p.nops; ++k) {
     const int op = p.ops[k].opcode, arg = p.ops[k].arg;
+    size_t pops = 0;
     switch (op) {
       case DR_OP_COL:
         if (arg < 0 || arg >= p.ncols) fail(DR_E_INVALID_ARG, "predicate column index out of range");
-        ++depth;
         break;
       case DR_OP_LIT:
         if (arg < 0 || arg >= p.nlits) fail(DR_E_INVALID_ARG, "predicate literal index out of range");
-        ++depth;
         break;
       case DR_OP_EQ: case DR_OP_NE: case DR_OP_LT: case DR_OP_LE: case DR_OP_GT: case DR_OP_GE:
       case DR_OP_NSEQ: case DR_OP_AND: case DR_OP_OR:
-        if (depth < 2) fail(DR_E_INVALID_ARG, "predicate stack underflow");
-        --depth;
+        pops = 2;
         break;
       case DR_OP_IN:
-        if (arg < 0 || depth < arg + 1) fail(DR_E_INVALID_ARG, "predicate stack underflow (IN)");
-        depth -= arg;
+        if (arg < 0) fail(DR_E_INVALID_ARG, "predicate stack underflow (IN)");
+        pops = size_t(arg) + 1;
         break;
       case DR_OP_ISNULL: case DR_OP_ISNOTNULL: case DR_OP_NOT:
-        if (depth < 1) fail(DR_E_INVALID_ARG, "predicate stack underflow");
+        pops = 1;
         break;
       default: fail(DR_E_INVALID_ARG, fmt("unknown predicate opcode %d", op));
     }
-    if (uint32_t(depth) > filter_max_stack()) fail(DR_E_UNSUPPORTED, "predicate program too deep");
+    if (stack.size() < pops)
+      fail(DR_E_INVALID_ARG, op == DR_OP_IN ? "predicate stack underflow (IN)" : "predicate stack underflow");
+    stack.resize(stack.size() - pops);
+    stack.push_back(k);
   }
-  if (depth != 1) fail(DR_E_INVALID_ARG, "predicate program must leave one value");
+  if (stack.size() != 1) fail(DR_E_INVALID_ARG, "predicate program must leave one value");
+}
+
+// Lowers the ABI program to the device form. `x e1..en IN(n)` becomes
+// `x IN_START e1 IN_STEP .. en IN_STEP IN_END`, so an IN list of any length needs two stack slots
+// beyond its value (In.eval semantics are unchanged: true if any element equals, else null if the
+// value or any element is null, else false). Returns (opcode, arg) pairs; fails if the lowered
+// program still needs more than the device stack.
+static std::vector<int32_t> lower_program(const dr_predicate& p) {
+  // subtree extents: start[k] = first op of the subtree rooted at op k
+  std::vector<int32_t> start(size_t(p.nops)), stack;
+  std::vector<std::vector<int32_t>> kids(size_t(p.nops));
+  for (int32_t k = 0; k < p.nops; ++k) {
+    const int op = p.ops[k].opcode;
+    size_t pops = op == DR_OP_COL || op == DR_OP_LIT ? 0
+                : op == DR_OP_IN ? size_t(p.ops[k].arg) + 1
+                : (op == DR_OP_ISNULL || op == DR_OP_ISNOTNULL || op == DR_OP_NOT) ? 1 : 2;
+    kids[size_t(k)].assign(stack.end() - ptrdiff_t(pops), stack.end());
+    stack.resize(stack.size() - pops);
+    start[size_t(k)] = kids[size_t(k)].empty() ? k : start[size_t(kids[size_t(k)][0])];
+    stack.push_back(k);
+  }
+  std::vector<int32_t> out;
+  int depth = 0, max_depth = 0;
+  auto put = [&](int32_t op, int32_t arg, int delta) {
+    out.push_back(op);
+    out.push_back(arg);
+    depth += delta;
+    max_depth = std::max(max_depth, depth);
+  };
+  std::function<void(int32_t)> emit = [&](int32_t k) {
+    const int op = p.ops[k].opcode, arg = p.ops[k].arg;
+    const auto& ch = kids[size_t(k)];
+    if (op == DR_OP_IN) {
+      emit(ch[0]);
+      put(FILTER_OP_IN_START, 0, +1);
+      for (size_t q = 1; q < ch.size(); ++q) {
+        emit(ch[q]);
+        put(FILTER_OP_IN_STEP, 0, -1);
+      }
+      put(FILTER_OP_IN_END, 0, -1);
+      return;
+    }
+    for (int32_t c : ch) emit(c);
+    put(op, arg, 1 - int(ch.size()));
+  };
+  emit(p.nops - 1);
+  if (uint32_t(max_depth) > filter_max_stack()) fail(DR_E_UNSUPPORTED, "predicate program too deep");
+  return out;
 }
 
 template <typename T>
@@ -1238,8 +1289,7 @@ static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred)
     names += pred.col_names[c];
     name_off[size_t(c) + 1] = names.size();
   }
-  std::vector<int32_t> ops(size_t(pred.nops) * 2);
-  for (int32_t k = 0; k < pred.nops; ++k) { ops[2 * size_t(k)] = pred.ops[k].opcode; ops[2 * size_t(k) + 1] = pred.ops[k].arg; }
+  const std::vector<int32_t> ops = lower_program(pred);
   std::vector<uint64_t> lit_off(size_t(pred.nlits) + 1, 0);
   for (int32_t k = 0; k <= pred.nlits && pred.nlits; ++k) lit_off[size_t(k)] = uint64_t(pred.lit_str_off[k]);
   const uint64_t lit_bytes = pred.nlits ? lit_off[size_t(pred.nlits)] : 0;
@@ -1256,7 +1306,7 @@ static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred)
   fa.col_name_off = d_name_off.p;
   fa.col_names = d_names.p;
   fa.col_types = d_types.p;
-  fa.nops = pred.nops;
+  fa.nops = int32_t(ops.size() / 2);
   fa.ops = d_ops.p;
   fa.lit_types = d_lt.p;
   fa.lit_i64 = d_li.p;

@@ -364,18 +364,27 @@ __global__ void __launch_bounds__(256) k_filter(FilterArgs a) {
         st[sp++] = r;
         break;
       }
-      case DR_OP_IN: {
-        sp -= arg;
+      // In(value, list) (Catalyst In.eval): true if some element equals the value; otherwise null
+      // if the value or any element is null; otherwise false. Accumulator: v = found, str = anynull.
+      case FILTER_OP_IN_START: {
+        st[sp++] = SV{0, nullptr, 0, 0, 0};
+        break;
+      }
+      case FILTER_OP_IN_STEP: {
+        const SV y = st[--sp];
+        SV& acc = st[sp - 1];
+        const SV& x = st[sp - 2];
+        if (y.null) acc.str = 1;
+        else if (!x.null && cmp_sv(x, y) == 0) acc.v = 1;
+        break;
+      }
+      case FILTER_OP_IN_END: {
+        const SV acc = st[--sp];
         const SV x = st[sp - 1];
         SV r{0, nullptr, 0, 1, 0};
         if (!x.null) {
-          bool found = false, anynull = false;
-          for (int q = 0; q < arg; ++q) {
-            if (st[sp + q].null) anynull = true;
-            else if (cmp_sv(x, st[sp + q]) == 0) found = true;
-          }
-          if (found) { r.null = 0; r.v = 1; }
-          else if (!anynull) { r.null = 0; r.v = 0; }
+          if (acc.v) { r.null = 0; r.v = 1; }
+          else if (!acc.str) { r.null = 0; r.v = 0; }
         }
         st[sp - 1] = r;
         break;

@@ -287,6 +287,9 @@ struct FilterArgs {
   uint32_t* flag;                // [n_live] 1 = selected
   uint32_t* error;
 };
+// device-only opcodes of the lowered program (engine.hip lower_program): an IN list is folded
+// one element at a time into an accumulator slot above its value
+enum : int32_t { FILTER_OP_IN_START = 100, FILTER_OP_IN_STEP = 101, FILTER_OP_IN_END = 102 };
 uint32_t filter_max_cols();
 uint32_t filter_max_stack();
 void launch_filter(const FilterArgs& a, hipStream_t st);

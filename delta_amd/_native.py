@@ -21,6 +21,8 @@ STATUS = {
 DR_FILE_JSON, DR_FILE_CHECKPOINT = 0, 1
 DR_LIVE, DR_TOMBSTONES = 0, 1
 DR_FLAG_NO_VALIDATION = 0x1
+DR_FLAG_EXACT_REDUCE = 0x2
+DR_FLAG_REDUCE64 = 0x4
 
 # Exported symbols (checked by tests/test_native_abi.py against include/deltareplay.h).
 SYMBOLS = [

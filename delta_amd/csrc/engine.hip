@@ -668,9 +668,11 @@ static std::shared_ptr<StagedData> stage_files(dr_ctx* ctx, const dr_file* files
 // ---------------------------------------------------------------------------------------------------
 // replay
 // ---------------------------------------------------------------------------------------------------
+// Buckets average <= 2048 file actions (the reduce's LDS table holds 8192), capped by the scatter's
+// LDS cursors; larger buckets are reduced in sub-passes.
 static int bucket_bits_for(uint64_t n) {
   int bits = 0;
-  while ((n >> bits) > 1536 && bits < 22) ++bits;
+  while ((n >> bits) > 2048 && bits < int(part_max_bucket_bits())) ++bits;
   return bits;
 }
 
@@ -856,56 +858,78 @@ static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
 
 // K3 (hash partition) + K4 (per-bucket last-writer-wins, retention) + compaction over st's action
 // arrays; fills st->live / st->tomb and the file counters.
-static void reduce_actions(dr_ctx* ctx, dr_state* st, int64_t cutoff) {
+static void reduce_actions(dr_ctx* ctx, dr_state* st, int64_t cutoff, uint32_t flags = 0) {
   hipStream_t stream = ctx->stream;
   const uint64_t N = st->n_actions;
   DBuf<uint8_t> scratch(ctx, scan_scratch_for(0));
   // ---- K3: partition by hash bucket ----
+  if (N >= (uint64_t(1) << 30)) fail(DR_E_UNSUPPORTED, "more than 2^30 actions in one replay shard");
   const int bits = bucket_bits_for(N);
   const uint32_t nb = 1u << bits;
-  DBuf<uint32_t> bcount(ctx, nb);
-  DBuf<uint64_t> boff(ctx, nb + 1);
-  bcount.zero(stream);
-  PartitionArgs pa{st->kind.p, st->flags.p, st->key.p, st->delts.p, N, cutoff, bits, bcount.p, boff.p, nullptr, nullptr};
+  const uint32_t nt = part_tiles(N);
+  const uint64_t ncell = uint64_t(nb) * nt;
+  DBuf<uint32_t> tcnt(ctx, ncell);
+  DBuf<uint64_t> toff(ctx, ncell + 1), boff(ctx, nb + 1);
+  DBuf<uint8_t> pscratch(ctx, scan_scratch_for(ncell));
+  DBuf<uint64_t> rpref(ctx, N);
+  PartitionArgs pa{st->kind.p, st->flags.p, st->key.p, st->size.p, st->delts.p, N, cutoff, bits, nt,
+                   tcnt.p, toff.p, nullptr, st->path_ptr.p, st->path_len.p, rpref.p};
+  DBuf<PartRec> rec(ctx, N);
+  pa.rec = rec.p;
+  ctx->mark("partition_setup");
   launch_bucket_hist(pa, stream);
-  launch_scan_u32(bcount.p, boff.p, nb, scratch.p, stream);
-  bcount.zero(stream);
-  DBuf<uint64_t> rkey(ctx, N);
-  DBuf<uint32_t> rmeta(ctx, N);
-  pa.rec_key = rkey.p;
-  pa.rec_meta = rmeta.p;
   ctx->mark("partition_hist");
+  launch_scan_u32(tcnt.p, toff.p, ncell, pscratch.p, stream);
+  launch_bucket_offsets(toff.p, nb, nt, boff.p, stream);
+  ctx->mark("partition_scan");
   launch_bucket_scatter(pa, stream);
   ctx->mark("partition_scatter");
   // ---- K4: per-bucket last-writer-wins ----
-  DBuf<uint32_t> olive(ctx, N), otomb(ctx, N), lcount(ctx, nb), tcount(ctx, nb), clist(ctx, nb), olist(ctx, nb);
-  DBuf<unsigned long long> totals(ctx, 8);
+  DBuf<uint32_t> olive(ctx, N), otomb(ctx, N), lcount(ctx, nb), tcount(ctx, nb), pcount(ctx, nb), rlist(ctx, nb),
+      xlist(ctx, nb);
+  DBuf<ulonglong2> opair(ctx, N);
+  DBuf<unsigned long long> totals(ctx, 8), bstats(ctx, uint64_t(nb) * 5);
   totals.zero(stream);
-  ReduceArgs ra{rkey.p, rmeta.p, boff.p, nb, bits, st->path_ptr.p, st->path_len.p, st->size.p, 1u,
-                olive.p, otomb.p, lcount.p, tcount.p, totals.p, clist.p, olist.p};
-  launch_bucket_reduce(ra, stream);
-  ctx->mark("reduce");
-  std::vector<unsigned long long> tot = d2h(totals.p, 8, stream);
-  if (tot[3] || tot[4]) {
-    std::vector<uint32_t> redo = d2h(clist.p, size_t(tot[3]), stream);
-    std::vector<uint32_t> ov = d2h(olist.p, size_t(tot[4]), stream);
-    redo.insert(redo.end(), ov.begin(), ov.end());
-    DBuf<uint32_t> dredo(ctx, redo.size());
-    HIP_OK(hipMemcpyAsync(dredo.p, redo.data(), redo.size() * 4, hipMemcpyHostToDevice, stream));
-    launch_bucket_exact(ra, dredo.p, uint32_t(redo.size()), stream);
-    tot = d2h(totals.p, 8, stream);
+  ReduceArgs ra{rec.p, boff.p, nb, bits, st->key.p, st->path_ptr.p, st->path_len.p, olive.p, otomb.p, rpref.p, opair.p,
+                lcount.p, tcount.p, pcount.p, totals.p, rlist.p, xlist.p, bstats.p};
+  auto upload_list = [&](const std::vector<uint32_t>& v) {
+    DBuf<uint32_t> d(ctx, v.size());
+    HIP_OK(hipMemcpyAsync(d.p, v.data(), v.size() * 4, hipMemcpyHostToDevice, stream));
+    return d;
+  };
+  std::vector<uint32_t> redo, exact;
+  if (flags & (DR_FLAG_EXACT_REDUCE | DR_FLAG_REDUCE64)) {  // test hooks: force the fallback reducers
+    for (uint32_t b = 0; b < nb; ++b) ((flags & DR_FLAG_EXACT_REDUCE) ? exact : redo).push_back(b);
+  } else {
+    launch_bucket_reduce(ra, stream);
+    ctx->mark("reduce");
+    launch_bucket_verify(ra, stream);
+    ctx->mark("reduce_verify");
+    redo = d2h(rlist.p, size_t(d2h_one(totals.p + 3, stream)), stream);
+  }
+  if (!redo.empty()) {
+    DBuf<uint32_t> d = upload_list(redo);
+    launch_bucket_reduce64(ra, d.p, uint32_t(redo.size()), stream);
+    ctx->mark("reduce64");
+    exact = d2h(xlist.p, size_t(d2h_one(totals.p + 4, stream)), stream);
+  }
+  if (!exact.empty()) {
+    DBuf<uint32_t> d = upload_list(exact);
+    launch_bucket_exact(ra, d.p, uint32_t(exact.size()), stream);
     ctx->mark("reduce_exact");
   }
+  launch_sum_stats(ra, stream);
+  std::vector<unsigned long long> tot = d2h(totals.p, 8, stream);
   // ---- compaction ----
-  DBuf<uint64_t> loff(ctx, nb + 1), toff(ctx, nb + 1);
+  DBuf<uint64_t> loff(ctx, nb + 1), tmoff(ctx, nb + 1);
   launch_scan_u32(lcount.p, loff.p, nb, scratch.p, stream);
-  launch_scan_u32(tcount.p, toff.p, nb, scratch.p, stream);
+  launch_scan_u32(tcount.p, tmoff.p, nb, scratch.p, stream);
   st->n_live = tot[0];
   st->n_tomb = tot[2];
   st->live = DBuf<uint32_t>(ctx, st->n_live);
   st->tomb = DBuf<uint32_t>(ctx, st->n_tomb);
   launch_compact(CompactArgs{olive.p, boff.p, lcount.p, loff.p, nb, st->live.p}, stream);
-  launch_compact(CompactArgs{otomb.p, boff.p, tcount.p, toff.p, nb, st->tomb.p}, stream);
+  launch_compact(CompactArgs{otomb.p, boff.p, tcount.p, tmoff.p, nb, st->tomb.p}, stream);
   const uint64_t n_file_actions = d2h_one(boff.p + nb, stream);
   ctx->mark("compact");
   st->counts.num_files = int64_t(tot[0]);
@@ -930,7 +954,7 @@ static dr_state* replay(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, int6
   ctx->mark("start");
   std::vector<NonFileAction> nf;
   parse_actions(ctx, sp, st.get(), nf);
-  reduce_actions(ctx, st.get(), cutoff);
+  reduce_actions(ctx, st.get(), cutoff, flags);
   reduce_nonfile(*st, nf, !(flags & DR_FLAG_NO_VALIDATION));
   ctx->mark("end");
   return st.release();

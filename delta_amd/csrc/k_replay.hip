@@ -3,14 +3,15 @@
 // InMemoryLogReplay.append/checkpoint, D/Snapshot.scala:103-110,
 // D/actions/InMemoryLogReplay.scala:43-77).
 //
-// Records {key = xxh64(path), meta = action_index << 2 | class} are radix-partitioned on the top
-// `bucket_bits` of the key (one LDS-aggregated pass). Each bucket is then reduced by one
-// workgroup: an LDS open-addressing table keyed by the 64-bit path key keeps atomicMax(meta),
-// i.e. the action with the largest (version, line) ordinal wins -- exactly the reference's
-// "last action per path" (action index order == input_file_name order, stable within a file).
-// Losers are byte-verified against their winner (hash collisions are resolved exactly by
-// k_bucket_exact). Winners are compacted and bitonic-sorted by key in LDS, so the state is stored
-// hash-ordered per bucket (deterministic, and ready for incremental merges).
+// 16-byte records {rkey = 32 key bits below the bucket bits, meta = action_index << 2 | class,
+// add.size} are partitioned on the top `bucket_bits` of xxh64(path): tiles count buckets in LDS into
+// a bucket-major matrix whose exclusive scan gives each (bucket, tile) its output range, so the
+// scatter needs no global atomics. Each bucket is then reduced by one workgroup: an LDS
+// open-addressing table keyed by rkey keeps atomicMax(meta), i.e. the action with the largest
+// (version, line) ordinal wins -- exactly the reference's "last action per path" (action index
+// order == input_file_name order, stable within a file). Every loser is byte-verified against its
+// winner, so a collision of the (bucket, rkey) hash bits is detected and that bucket is redone by
+// the exact kernel (k_bucket_exact).
 #include "dev_common.h"
 #include "kernels.h"
 
@@ -139,296 +140,475 @@ __global__ void k_canon(CanonArgs a) {
   a.act.key[i] = path_key(kb, kn);
 }
 
-// ---- partition --------------------------------------------------------------------------------------
+// ---- partition ----------------------------------------------------------------------------------
 __device__ __forceinline__ bool is_file_action(uint8_t kind, uint8_t flags) {
   return (kind == K_ADD || kind == K_REMOVE) && !(flags & F_PATH_NULL);
 }
 __device__ __forceinline__ uint32_t bucket_of(uint64_t key, int bits) {
   return bits ? uint32_t(key >> (64 - bits)) : 0u;
 }
+// the 32 key bits directly below the bucket bits
+__device__ __forceinline__ uint32_t rkey_of(uint64_t key, int bits) { return uint32_t(key >> (32 - bits)); }
+// top 32 bits of the key, rebuilt from (bucket, rkey): the order-free parity checksum's term
+__device__ __forceinline__ uint64_t top32_of(uint32_t b, uint32_t rkey, int bits) {
+  return bits ? (uint64_t(b) << (32 - bits)) | (rkey >> bits) : uint64_t(rkey);
+}
 
-constexpr int PART_T = 256;
-constexpr int PART_ITEMS = 16;               // actions per thread
-constexpr int PART_TILE = PART_T * PART_ITEMS;
-constexpr int LDS_HIST_MAX = 8192;           // buckets aggregated in LDS
+constexpr int PART_T = 512;
+constexpr int PART_STEPS = 16;                          // 4 actions per thread per step
+constexpr int PART_TILE = PART_T * 4 * PART_STEPS;      // 32768 actions per tile
+constexpr int PART_MAX_BITS = 13;                       // LDS: 2 x 8192 x 4 B in the scatter
 
+// Every thread owns 4 consecutive actions per step: one dword of kind bytes, one of flag bytes and
+// two 16-byte key loads.
 __global__ void __launch_bounds__(PART_T) k_bucket_hist(PartitionArgs a) {
-  __shared__ uint32_t hist[LDS_HIST_MAX];
+  __shared__ uint32_t hist[1 << PART_MAX_BITS];
   const uint32_t nb = 1u << a.bucket_bits;
-  const bool lds = nb <= LDS_HIST_MAX;
-  if (lds) for (uint32_t b = threadIdx.x; b < nb; b += PART_T) hist[b] = 0;
+  for (uint32_t b = threadIdx.x; b < nb; b += PART_T) hist[b] = 0;
   __syncthreads();
   const uint64_t base = uint64_t(blockIdx.x) * PART_TILE;
-  for (int k = 0; k < PART_ITEMS; ++k) {
-    const uint64_t i = base + uint64_t(k) * PART_T + threadIdx.x;
-    if (i >= a.n || !is_file_action(a.kind[i], a.flags[i])) continue;
-    const uint32_t b = bucket_of(a.key[i], a.bucket_bits);
-    if (lds) atomicAdd(&hist[b], 1u); else atomicAdd(&a.bucket_count[b], 1u);
+  for (int k = 0; k < PART_STEPS; ++k) {
+    const uint64_t i0 = base + (uint64_t(k) * PART_T + threadIdx.x) * 4;
+    if (i0 >= a.n) break;
+    if (i0 + 4 <= a.n) {
+      const uint32_t kd = *reinterpret_cast<const uint32_t*>(a.kind + i0);
+      const uint32_t fl = *reinterpret_cast<const uint32_t*>(a.flags + i0);
+      const uint4 k01 = *reinterpret_cast<const uint4*>(a.key + i0);
+      const uint4 k23 = *reinterpret_cast<const uint4*>(a.key + i0 + 2);
+      const uint64_t ks[4] = {uint64_t(k01.x) | uint64_t(k01.y) << 32, uint64_t(k01.z) | uint64_t(k01.w) << 32,
+                              uint64_t(k23.x) | uint64_t(k23.y) << 32, uint64_t(k23.z) | uint64_t(k23.w) << 32};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (is_file_action(uint8_t(kd >> (8 * j)), uint8_t(fl >> (8 * j))))
+          atomicAdd(&hist[bucket_of(ks[j], a.bucket_bits)], 1u);
+    } else {
+      for (uint64_t i = i0; i < a.n; ++i)
+        if (is_file_action(a.kind[i], a.flags[i])) atomicAdd(&hist[bucket_of(a.key[i], a.bucket_bits)], 1u);
+    }
   }
   __syncthreads();
-  if (lds)
-    for (uint32_t b = threadIdx.x; b < nb; b += PART_T)
-      if (hist[b]) atomicAdd(&a.bucket_count[b], hist[b]);
+  for (uint32_t b = threadIdx.x; b < nb; b += PART_T) a.tile_count[uint64_t(b) * a.ntiles + blockIdx.x] = hist[b];
+}
+
+__device__ __forceinline__ void scatter_one(const PartitionArgs& a, uint64_t i, uint8_t kind, uint64_t key,
+                                            uint64_t ptr, uint32_t len, const uint32_t* base, uint32_t* cnt) {
+  const uint32_t b = bucket_of(key, a.bucket_bits);
+  const uint32_t pos = base[b] + atomicAdd(&cnt[b], 1u);
+  uint32_t cls = C_ADD;
+  int64_t size = 0;
+  if (kind == K_REMOVE) {
+    // RemoveFile.delTimestamp = deletionTimestamp.getOrElse(0) (D/actions/actions.scala:318-319);
+    // kept iff delTimestamp > minFileRetentionTimestamp (D/actions/InMemoryLogReplay.scala:67-69)
+    const int64_t dt = (a.flags[i] & F_HAS_DELTS) ? a.delts[i] : 0;
+    cls = dt > a.cutoff ? C_REMOVE_KEEP : C_REMOVE_DROP;
+  } else {
+    size = a.size[i];
+  }
+  uint4 r;
+  r.x = rkey_of(key, a.bucket_bits);
+  r.y = uint32_t(i << 2) | cls;
+  r.z = uint32_t(uint64_t(size));
+  r.w = uint32_t(uint64_t(size) >> 32);
+  *reinterpret_cast<uint4*>(a.rec + pos) = r;
+  a.rec_pref[pos] = len < 0xffffu ? (ptr | (uint64_t(len) << 48)) : 0ull;
 }
 
 __global__ void __launch_bounds__(PART_T) k_bucket_scatter(PartitionArgs a) {
-  __shared__ uint32_t hist[LDS_HIST_MAX];
-  __shared__ uint32_t gbase[LDS_HIST_MAX];
+  __shared__ uint32_t base[1 << PART_MAX_BITS];
+  __shared__ uint32_t cnt[1 << PART_MAX_BITS];
   const uint32_t nb = 1u << a.bucket_bits;
-  const bool lds = nb <= LDS_HIST_MAX;
-  if (lds) for (uint32_t b = threadIdx.x; b < nb; b += PART_T) hist[b] = 0;
-  __syncthreads();
-  const uint64_t base = uint64_t(blockIdx.x) * PART_TILE;
-  uint32_t rank[PART_ITEMS];
-  uint32_t bk[PART_ITEMS];
-  for (int k = 0; k < PART_ITEMS; ++k) {
-    const uint64_t i = base + uint64_t(k) * PART_T + threadIdx.x;
-    bk[k] = 0xffffffffu;
-    if (i >= a.n || !is_file_action(a.kind[i], a.flags[i])) continue;
-    const uint32_t b = bucket_of(a.key[i], a.bucket_bits);
-    bk[k] = b;
-    if (lds) rank[k] = atomicAdd(&hist[b], 1u);
-    else rank[k] = atomicAdd(&a.bucket_count[b], 1u);
+  for (uint32_t b = threadIdx.x; b < nb; b += PART_T) {
+    base[b] = uint32_t(a.tile_off[uint64_t(b) * a.ntiles + blockIdx.x]);
+    cnt[b] = 0;
   }
   __syncthreads();
-  if (lds)
-    for (uint32_t b = threadIdx.x; b < nb; b += PART_T)
-      if (hist[b]) gbase[b] = atomicAdd(&a.bucket_count[b], hist[b]);
-  __syncthreads();
-  for (int k = 0; k < PART_ITEMS; ++k) {
-    if (bk[k] == 0xffffffffu) continue;
-    const uint64_t i = base + uint64_t(k) * PART_T + threadIdx.x;
-    const uint32_t b = bk[k];
-    const uint64_t pos = a.bucket_off[b] + (lds ? gbase[b] + rank[k] : rank[k]);
-    uint32_t cls = C_ADD;
-    if (a.kind[i] == K_REMOVE) {
-      // RemoveFile.delTimestamp = deletionTimestamp.getOrElse(0) (D/actions/actions.scala:318-319);
-      // kept iff delTimestamp > minFileRetentionTimestamp (D/actions/InMemoryLogReplay.scala:67-69)
-      const int64_t dt = (a.flags[i] & F_HAS_DELTS) ? a.delts[i] : 0;
-      cls = dt > a.cutoff ? C_REMOVE_KEEP : C_REMOVE_DROP;
+  const uint64_t tb = uint64_t(blockIdx.x) * PART_TILE;
+  for (int k = 0; k < PART_STEPS; ++k) {
+    const uint64_t i0 = tb + (uint64_t(k) * PART_T + threadIdx.x) * 4;
+    if (i0 >= a.n) break;
+    if (i0 + 4 <= a.n) {
+      const uint32_t kd = *reinterpret_cast<const uint32_t*>(a.kind + i0);
+      const uint32_t fl = *reinterpret_cast<const uint32_t*>(a.flags + i0);
+      const uint4 k01 = *reinterpret_cast<const uint4*>(a.key + i0);
+      const uint4 k23 = *reinterpret_cast<const uint4*>(a.key + i0 + 2);
+      const uint64_t ks[4] = {uint64_t(k01.x) | uint64_t(k01.y) << 32, uint64_t(k01.z) | uint64_t(k01.w) << 32,
+                              uint64_t(k23.x) | uint64_t(k23.y) << 32, uint64_t(k23.z) | uint64_t(k23.w) << 32};
+      const uint4 p01 = *reinterpret_cast<const uint4*>(a.path_ptr + i0);
+      const uint4 p23 = *reinterpret_cast<const uint4*>(a.path_ptr + i0 + 2);
+      const uint64_t ps[4] = {uint64_t(p01.x) | uint64_t(p01.y) << 32, uint64_t(p01.z) | uint64_t(p01.w) << 32,
+                              uint64_t(p23.x) | uint64_t(p23.y) << 32, uint64_t(p23.z) | uint64_t(p23.w) << 32};
+      const uint4 ln = *reinterpret_cast<const uint4*>(a.path_len + i0);
+      const uint32_t ls[4] = {ln.x, ln.y, ln.z, ln.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint8_t kj = uint8_t(kd >> (8 * j));
+        if (is_file_action(kj, uint8_t(fl >> (8 * j)))) scatter_one(a, i0 + j, kj, ks[j], ps[j], ls[j], base, cnt);
+      }
+    } else {
+      for (uint64_t i = i0; i < a.n; ++i)
+        if (is_file_action(a.kind[i], a.flags[i]))
+          scatter_one(a, i, a.kind[i], a.key[i], a.path_ptr[i], a.path_len[i], base, cnt);
     }
-    a.rec_key[pos] = a.key[i];
-    a.rec_meta[pos] = uint32_t(i << 2) | cls;
   }
+}
+
+__global__ void k_bucket_offsets(const uint64_t* tile_off, uint32_t nb, uint32_t nt, uint64_t* bucket_off) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b <= nb) bucket_off[b] = tile_off[uint64_t(b) * nt];
 }
 
 // ---- per-bucket reduce ------------------------------------------------------------------------------
-constexpr int RED_T = 256;
-constexpr int TS = 4096;  // LDS table slots (keys 32 KiB + metas 16 KiB)
+constexpr int RED_T = 512;
+constexpr int TS_MAX = 4096;  // LDS table slots (rkeys 16 KiB + metas 16 KiB): 4 workgroups per CU
 
-__device__ __forceinline__ uint32_t sub_of(uint64_t key, int bits, int sbits) {
-  return sbits ? uint32_t((key << bits) >> (64 - sbits)) : 0u;
+struct BucketTotals {
+  uint64_t live, tomb, size, lks, tks;
+};
+
+// Block-wide sums of the survivor statistics, stored per bucket (summed by k_sum_stats: no
+// contended global atomics).
+__device__ void store_totals(ReduceArgs& a, uint32_t b, BucketTotals t) {
+  __shared__ unsigned long long red[5][RED_T / 64];
+  for (int o = 32; o > 0; o >>= 1) {
+    t.live += __shfl_down(t.live, o, 64);
+    t.tomb += __shfl_down(t.tomb, o, 64);
+    t.size += __shfl_down(t.size, o, 64);
+    t.lks += __shfl_down(t.lks, o, 64);
+    t.tks += __shfl_down(t.tks, o, 64);
+  }
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][wv] = t.live; red[1][wv] = t.tomb; red[2][wv] = t.size; red[3][wv] = t.lks; red[4][wv] = t.tks;
+  }
+  __syncthreads();
+  if (threadIdx.x < 5) {
+    unsigned long long s = 0;
+    for (int k = 0; k < RED_T / 64; ++k) s += red[threadIdx.x][k];
+    a.bstats[uint64_t(b) * 5 + threadIdx.x] = s;
+  }
 }
 
+// totals[0] live, [2] tombstones, [1] size sum, [5] live checksum, [6] tombstone checksum
+__global__ void __launch_bounds__(1024) k_sum_stats(const unsigned long long* bstats, uint32_t nb,
+                                                    unsigned long long* totals) {
+  __shared__ unsigned long long red[5][16];
+  unsigned long long s[5] = {0, 0, 0, 0, 0};
+  for (uint32_t b = threadIdx.x; b < nb; b += 1024)
+    for (int k = 0; k < 5; ++k) s[k] += bstats[uint64_t(b) * 5 + k];
+  for (int k = 0; k < 5; ++k)
+    for (int o = 32; o > 0; o >>= 1) s[k] += __shfl_down(s[k], o, 64);
+  if ((threadIdx.x & 63) == 0)
+    for (int k = 0; k < 5; ++k) red[k][threadIdx.x >> 6] = s[k];
+  __syncthreads();
+  if (threadIdx.x < 5) {
+    unsigned long long t = 0;
+    for (int w = 0; w < 16; ++w) t += red[threadIdx.x][w];
+    const int slot[5] = {0, 2, 1, 5, 6};
+    totals[slot[threadIdx.x]] = t;
+  }
+}
+
+__device__ __forceinline__ uint4 load_rec(const PartRec* r, uint64_t e) {
+  return *reinterpret_cast<const uint4*>(r + e);
+}
+
+// Appends one wave's flagged values to an LDS-counted list region (order across waves is free).
+__device__ __forceinline__ void wave_append(bool f, uint32_t v, uint32_t* cnt, uint32_t* out) {
+  const unsigned long long bl = __ballot(f);
+  if (!bl) return;
+  const int lane = threadIdx.x & 63;
+  uint32_t o = 0;
+  if (lane == __ffsll(bl) - 1) o = atomicAdd(cnt, uint32_t(__popcll(bl)));
+  o = __shfl(o, __ffsll(bl) - 1, 64);
+  if (f) out[o + uint32_t(__popcll(bl & ((1ull << lane) - 1ull)))] = v;
+}
+__device__ __forceinline__ void wave_append2(bool f, ulonglong2 v, uint32_t* cnt, ulonglong2* out) {
+  const unsigned long long bl = __ballot(f);
+  if (!bl) return;
+  const int lane = threadIdx.x & 63;
+  uint32_t o = 0;
+  if (lane == __ffsll(bl) - 1) o = atomicAdd(cnt, uint32_t(__popcll(bl)));
+  o = __shfl(o, __ffsll(bl) - 1, 64);
+  if (f) out[o + uint32_t(__popcll(bl & ((1ull << lane) - 1ull)))] = v;
+}
+
+// K4 main reducer: one workgroup per bucket, LDS-only. Survivors go to the bucket's region of the
+// live / tombstone lists; every loser is paired with its winner for k_bucket_verify.
 __global__ void __launch_bounds__(RED_T) k_bucket_reduce(ReduceArgs a) {
-  __shared__ unsigned long long tkey[TS];
-  __shared__ uint32_t tval[TS];
-  __shared__ uint32_t spos[TS];   // compacted survivors (slot indices), later sorted
-  __shared__ uint32_t nsurv, collide, overflow;
-  __shared__ uint32_t wl[RED_T / 64], wt[RED_T / 64];
+  __shared__ uint32_t tkey[TS_MAX];
+  __shared__ uint32_t tval[TS_MAX];
+  __shared__ uint32_t wpos[TS_MAX];  // winner's record offset in the bucket
+  __shared__ uint32_t nl, nt, np, overflow;
   const uint32_t b = blockIdx.x;
   const uint64_t beg = a.bucket_off[b], end = a.bucket_off[b + 1];
   const uint64_t m = end - beg;
-  // sub-passes keep the distinct keys per pass well under the table size
+  // sub-passes keep the distinct keys per pass at or under 3/4 of the table
   int sbits = 0;
-  while ((m >> sbits) > uint64_t(TS / 2)) ++sbits;
-  if (threadIdx.x == 0) { collide = 0; overflow = 0; }
-  uint64_t live = 0, tomb = 0, size_sum = 0, lks = 0, tks = 0;
-  uint32_t live_w = 0, tomb_w = 0;  // survivors written so far (block-uniform)
+  while ((m >> sbits) > uint64_t(TS_MAX / 4 * 3)) ++sbits;
+  uint32_t ts = 64;
+  while (ts < TS_MAX && uint64_t(ts) < 2 * (m >> sbits)) ts <<= 1;
+  const uint32_t mask = ts - 1;
+  if (threadIdx.x == 0) { nl = 0; nt = 0; np = 0; overflow = 0; }
+  BucketTotals tot{0, 0, 0, 0, 0};
   for (uint32_t sp = 0; sp < (1u << sbits); ++sp) {
     __syncthreads();
-    for (int s = threadIdx.x; s < TS; s += RED_T) { tkey[s] = 0; tval[s] = 0; }
-    if (threadIdx.x == 0) nsurv = 0;
+    for (uint32_t s = threadIdx.x; s < ts; s += RED_T) { tkey[s] = 0; tval[s] = 0; }
     __syncthreads();
-    // insert: table[key] = max(meta)  (largest action index wins)
+    // insert: table[rkey] = max(meta) -- the largest action index (latest version, line) wins
     for (uint64_t e = beg + threadIdx.x; e < end; e += RED_T) {
-      const uint64_t k = a.rec_key[e];
-      if (sub_of(k, a.bucket_bits, sbits) != sp) continue;
-      const uint32_t mt = a.rec_meta[e];
-      uint32_t s = uint32_t(k) & (TS - 1);
-      for (int probe = 0;; ++probe) {
-        if (probe >= TS) { overflow = 1; break; }
-        const unsigned long long old = atomicCAS(&tkey[s], 0ull, (unsigned long long)k);
-        if (old == 0ull || old == k) { atomicMax(&tval[s], mt + 1u); break; }
-        s = (s + 1) & (TS - 1);
+      const uint4 r = load_rec(a.rec, e);
+      if (sbits && (r.x >> (32 - sbits)) != sp) continue;
+      const uint32_t rk = r.x ? r.x : 1u;  // 0 marks an empty slot (1 and 0 merge; verified later)
+      uint32_t s = rk & mask;
+      for (uint32_t probe = 0;; ++probe) {
+        if (probe >= ts) { overflow = 1; break; }
+        const uint32_t old = atomicCAS(&tkey[s], 0u, rk);
+        if (old == 0u || old == rk) { atomicMax(&tval[s], r.y + 1u); break; }
+        s = (s + 1) & mask;
       }
     }
     __syncthreads();
     if (overflow) break;
-    // winners: aggregates; losers: verify their path equals the winner's
+    // winners record their position (for the losers' verification pairs)
     for (uint64_t e = beg + threadIdx.x; e < end; e += RED_T) {
-      const uint64_t k = a.rec_key[e];
-      if (sub_of(k, a.bucket_bits, sbits) != sp) continue;
-      const uint32_t mt = a.rec_meta[e];
-      uint32_t s = uint32_t(k) & (TS - 1);
-      while (tkey[s] != k) s = (s + 1) & (TS - 1);
-      const uint32_t w = tval[s] - 1u;
-      const uint32_t idx = mt >> 2;
-      if (w == mt) {
-        if ((mt & 3) == C_ADD) { ++live; size_sum += uint64_t(a.size[idx]); lks += k; }
-        else if ((mt & 3) == C_REMOVE_KEEP) { ++tomb; tks += k; }
-      } else if (a.verify_bytes) {
-        const uint32_t wi = w >> 2;
-        const uint8_t* p = reinterpret_cast<const uint8_t*>(a.path_ptr[idx]);
-        const uint8_t* q = reinterpret_cast<const uint8_t*>(a.path_ptr[wi]);
-        if (!key_equal(p, a.path_len[idx], q, a.path_len[wi])) collide = 1;
-      }
-    }
-    // compact surviving slots
-    for (int s = threadIdx.x; s < TS; s += RED_T) {
-      const uint32_t v = tval[s];
-      if (v && ((v - 1u) & 3) != C_REMOVE_DROP) spos[atomicAdd(&nsurv, 1u)] = uint32_t(s);
+      const uint4 r = load_rec(a.rec, e);
+      if (sbits && (r.x >> (32 - sbits)) != sp) continue;
+      const uint32_t rk = r.x ? r.x : 1u;
+      uint32_t s = rk & mask;
+      while (tkey[s] != rk) s = (s + 1) & mask;
+      if (tval[s] - 1u == r.y) wpos[s] = uint32_t(e - beg);
     }
     __syncthreads();
-    // bitonic sort of the survivors by key (pad to a power of two with sentinel slots)
-    const uint32_t ns = nsurv;
-    uint32_t np = 1;
-    while (np < ns) np <<= 1;
-    for (uint32_t t = ns + threadIdx.x; t < np; t += RED_T) spos[t] = 0xffffffffu;
-    __syncthreads();
-    for (uint32_t ksz = 2; ksz <= np; ksz <<= 1) {
-      for (uint32_t j = ksz >> 1; j > 0; j >>= 1) {
-        for (uint32_t t = threadIdx.x; t < np; t += RED_T) {
-          const uint32_t u = t ^ j;
-          if (u > t) {
-            const uint32_t x = spos[t], y = spos[u];
-            // sentinels (0xffffffff) order after every real key
-            const bool gt = x == 0xffffffffu ? (y != 0xffffffffu)
-                                             : (y == 0xffffffffu ? false : tkey[x] > tkey[y]);
-            const bool up = (t & ksz) == 0;
-            if (gt == up) { spos[t] = y; spos[u] = x; }
+    for (uint64_t e0 = beg; e0 < end; e0 += RED_T) {
+      const uint64_t e = e0 + threadIdx.x;
+      bool isl = false, ist = false, lose = false;
+      uint32_t idx = 0;
+      ulonglong2 pair = make_ulonglong2(0, 0);
+      if (e < end) {
+        const uint4 r = load_rec(a.rec, e);
+        if (!sbits || (r.x >> (32 - sbits)) == sp) {
+          const uint32_t rk = r.x ? r.x : 1u;
+          uint32_t s = rk & mask;
+          while (tkey[s] != rk) s = (s + 1) & mask;
+          const uint32_t w = tval[s] - 1u;
+          idx = r.y >> 2;
+          if (w == r.y) {
+            const uint32_t cls = r.y & 3;
+            if (cls == C_ADD) {
+              isl = true;
+              ++tot.live;
+              tot.size += uint64_t(r.z) | (uint64_t(r.w) << 32);
+              tot.lks += top32_of(b, r.x, a.bucket_bits);
+            } else if (cls == C_REMOVE_KEEP) {
+              ist = true;
+              ++tot.tomb;
+              tot.tks += top32_of(b, r.x, a.bucket_bits);
+            }
+          } else {
+            lose = true;
+            pair = make_ulonglong2(a.rec_pref[e], a.rec_pref[beg + wpos[s]]);
           }
         }
-        __syncthreads();
       }
+      wave_append(isl, idx, &nl, a.out_live + beg);
+      wave_append(ist, idx, &nt, a.out_tomb + beg);
+      wave_append2(lose, pair, &np, a.out_pair + beg);
     }
-    // write survivors in key order: live and tombstone lists, via per-wave ballots
-    for (uint32_t base = 0; base < ns; base += RED_T) {
-      const uint32_t t = base + threadIdx.x;
-      uint32_t v = 0;
-      if (t < ns) v = tval[spos[t]] - 1u;
-      const bool isl = t < ns && (v & 3) == C_ADD;
-      const bool ist = t < ns && (v & 3) == C_REMOVE_KEEP;
-      const unsigned long long bl = __ballot(isl), bt = __ballot(ist);
-      const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-      const unsigned long long lt = (1ull << lane) - 1ull;
-      if (lane == 0) { wl[wv] = uint32_t(__popcll(bl)); wt[wv] = uint32_t(__popcll(bt)); }
-      __syncthreads();
-      uint32_t ol = 0, ot = 0, sl = 0, st = 0;
-      for (int k = 0; k < RED_T / 64; ++k) {
-        if (k < wv) { ol += wl[k]; ot += wt[k]; }
-        sl += wl[k]; st += wt[k];
-      }
-      if (isl) a.out_live[beg + live_w + ol + uint32_t(__popcll(bl & lt))] = v >> 2;
-      if (ist) a.out_tomb[beg + tomb_w + ot + uint32_t(__popcll(bt & lt))] = v >> 2;
-      live_w += sl;
-      tomb_w += st;
-      __syncthreads();
-    }
-  }
-  // block totals
-  __shared__ unsigned long long red[5][RED_T / 64];
-  for (int o = 32; o > 0; o >>= 1) {
-    live += __shfl_down(live, o, 64);
-    tomb += __shfl_down(tomb, o, 64);
-    size_sum += __shfl_down(size_sum, o, 64);
-    lks += __shfl_down(lks, o, 64);
-    tks += __shfl_down(tks, o, 64);
-  }
-  if ((threadIdx.x & 63) == 0) {
-    red[0][threadIdx.x >> 6] = live; red[1][threadIdx.x >> 6] = tomb; red[2][threadIdx.x >> 6] = size_sum;
-    red[3][threadIdx.x >> 6] = lks; red[4][threadIdx.x >> 6] = tks;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    unsigned long long L = 0, T = 0, S = 0, LK = 0, TK = 0;
-    for (int k = 0; k < RED_T / 64; ++k) {
-      L += red[0][k]; T += red[1][k]; S += red[2][k]; LK += red[3][k]; TK += red[4][k];
-    }
-    if (collide || overflow) {
-      a.live_count[b] = 0;
-      a.tomb_count[b] = 0;
-      if (collide) {
-        const unsigned long long c = atomicAdd(&a.totals[3], 1ull);
-        a.collide_list[c] = b;
-      } else {
-        const unsigned long long c = atomicAdd(&a.totals[4], 1ull);
-        a.overflow_list[c] = b;
-      }
-    } else {
-      a.live_count[b] = live_w;
-      a.tomb_count[b] = tomb_w;
-      atomicAdd(&a.totals[0], L);
-      atomicAdd(&a.totals[1], S);
-      atomicAdd(&a.totals[2], T);
-      atomicAdd(&a.totals[5], LK);
-      atomicAdd(&a.totals[6], TK);
-    }
+    a.live_count[b] = nl;
+    a.tomb_count[b] = nt;
+    a.pair_count[b] = overflow ? 0 : np;
+    if (overflow) a.redo_list[atomicAdd(&a.totals[3], 1ull)] = b;
   }
+  store_totals(a, b, tot);
 }
 
-// Exact fallback for buckets with a 64-bit key collision (or an LDS table overflow): each record
-// is a winner iff no other record with an equal path has a larger action index. O(m^2) per bucket;
-// only reached on collisions, which a 64-bit hash makes vanishingly rare.
+// 16 bytes at byte offset `off` (0..15) of the 32 bytes lo:hi (little-endian).
+__device__ __forceinline__ uint4 window16(uint4 lo, uint4 hi, uint32_t off) {
+  const uint32_t dw = off >> 2, sb = off & 3;
+  auto pick = [&](uint32_t k) -> uint32_t {  // dword k + dw of lo:hi, k in 0..4
+    const uint32_t j = k + dw;
+    return j == 0 ? lo.x : j == 1 ? lo.y : j == 2 ? lo.z : j == 3 ? lo.w
+         : j == 4 ? hi.x : j == 5 ? hi.y : j == 6 ? hi.z : hi.w;
+  };
+  const uint32_t a0 = pick(0), a1 = pick(1), a2 = pick(2), a3 = pick(3), a4 = pick(4);
+  return make_uint4(__builtin_amdgcn_alignbyte(a1, a0, sb), __builtin_amdgcn_alignbyte(a2, a1, sb),
+                    __builtin_amdgcn_alignbyte(a3, a2, sb), __builtin_amdgcn_alignbyte(a4, a3, sb));
+}
+
+// Byte equality of p[0..n) and q[0..n) with aligned 16-byte loads (one new load per string per 16
+// bytes) and no early exit. Never loads a 16-byte block that holds none of the string's bytes.
+__device__ bool bytes_equal16(const uint8_t* p, const uint8_t* q, uint32_t n) {
+  const uint4* pa = reinterpret_cast<const uint4*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(15));
+  const uint4* qa = reinterpret_cast<const uint4*>(reinterpret_cast<uintptr_t>(q) & ~uintptr_t(15));
+  const uint32_t po = uint32_t(reinterpret_cast<uintptr_t>(p) & 15), qo = uint32_t(reinterpret_cast<uintptr_t>(q) & 15);
+  const uint32_t pblocks = (po + n + 15) >> 4, qblocks = (qo + n + 15) >> 4;
+  uint4 plo = n ? pa[0] : make_uint4(0, 0, 0, 0), qlo = n ? qa[0] : make_uint4(0, 0, 0, 0);
+  uint32_t diff = 0;
+  for (uint32_t i = 0, k = 1; i < n; i += 16, ++k) {
+    const uint4 phi = k < pblocks ? pa[k] : make_uint4(0, 0, 0, 0);
+    const uint4 qhi = k < qblocks ? qa[k] : make_uint4(0, 0, 0, 0);
+    const uint4 x = window16(plo, phi, po), y = window16(qlo, qhi, qo);
+    const uint32_t rem = n - i;
+    uint4 d = make_uint4(x.x ^ y.x, x.y ^ y.y, x.z ^ y.z, x.w ^ y.w);
+    if (rem < 16) {  // bytes past the string end do not count
+      const uint32_t m0 = rem >= 4 ? 0xffffffffu : (1u << (8 * rem)) - 1u;
+      const uint32_t m1 = rem >= 8 ? 0xffffffffu : rem <= 4 ? 0u : (1u << (8 * (rem - 4))) - 1u;
+      const uint32_t m2 = rem >= 12 ? 0xffffffffu : rem <= 8 ? 0u : (1u << (8 * (rem - 8))) - 1u;
+      const uint32_t m3 = rem <= 12 ? 0u : (1u << (8 * (rem - 12))) - 1u;
+      d.x &= m0; d.y &= m1; d.z &= m2; d.w &= m3;
+    }
+    diff |= d.x | d.y | d.z | d.w;
+    plo = phi;
+    qlo = qhi;
+  }
+  return diff == 0;
+}
+
+// Every (loser, winner) pair of a bucket must name the same path (URI-equality key); a mismatch is
+// a collision of the (bucket, rkey) hash bits and sends the bucket to the 64-bit-key reducer (as
+// does a path too long for a packed reference). One wave per bucket: the pairs' loads are
+// independent, so a wave keeps many strings in flight.
+constexpr uint64_t PREF_PTR = (1ull << 48) - 1;
+__global__ void __launch_bounds__(64) k_bucket_verify(ReduceArgs a) {
+  const uint32_t b = blockIdx.x;
+  const uint32_t n = a.pair_count[b];
+  if (!n) return;
+  const ulonglong2* pr = a.out_pair + a.bucket_off[b];
+  bool bad = false;
+  for (uint32_t k = threadIdx.x; k < n; k += 64) {
+    const ulonglong2 v = pr[k];
+    if (!v.x || !v.y) { bad = true; continue; }
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(v.x & PREF_PTR);
+    const uint8_t* q = reinterpret_cast<const uint8_t*>(v.y & PREF_PTR);
+    const uint32_t pn = uint32_t(v.x >> 48), qn = uint32_t(v.y >> 48);
+    // equal bytes => equal URI keys; otherwise only file:/// vs file:/ spellings can still match
+    if (!(pn == qn && bytes_equal16(p, q, pn)) && !key_equal(p, pn, q, qn)) bad = true;
+  }
+  if (__ballot(bad) && threadIdx.x == 0) a.redo_list[atomicAdd(&a.totals[3], 1ull)] = b;
+}
+
+// Fallback for buckets whose (bucket, rkey) bits collided or whose LDS table overflowed: the same
+// last-writer-wins keyed by the full 64-bit path hash, byte-verified inline. A 64-bit collision (or
+// overflow) hands the bucket on to the exact O(m^2) kernel.
+constexpr int TS64 = 4096;
+__global__ void __launch_bounds__(RED_T) k_bucket_reduce64(ReduceArgs a, const uint32_t* buckets) {
+  __shared__ unsigned long long tkey[TS64];
+  __shared__ uint32_t tval[TS64];
+  __shared__ uint32_t nl, nt, collide, overflow;
+  const uint32_t b = buckets[blockIdx.x];
+  const uint64_t beg = a.bucket_off[b], end = a.bucket_off[b + 1];
+  const uint64_t m = end - beg;
+  int sbits = 0;
+  while ((m >> sbits) > uint64_t(TS64 / 2)) ++sbits;
+  if (threadIdx.x == 0) { nl = 0; nt = 0; collide = 0; overflow = 0; }
+  BucketTotals tot{0, 0, 0, 0, 0};
+  for (uint32_t sp = 0; sp < (1u << sbits); ++sp) {
+    __syncthreads();
+    for (int s = threadIdx.x; s < TS64; s += RED_T) { tkey[s] = 0; tval[s] = 0; }
+    __syncthreads();
+    for (uint64_t e = beg + threadIdx.x; e < end; e += RED_T) {
+      const uint4 r = load_rec(a.rec, e);
+      const uint64_t k = a.key[r.y >> 2];
+      if (sbits && uint32_t(k & ((1u << sbits) - 1)) != sp) continue;
+      uint32_t s = uint32_t(k >> 20) & (TS64 - 1);
+      for (int probe = 0;; ++probe) {
+        if (probe >= TS64) { overflow = 1; break; }
+        const unsigned long long old = atomicCAS(&tkey[s], 0ull, (unsigned long long)k);
+        if (old == 0ull || old == k) { atomicMax(&tval[s], r.y + 1u); break; }
+        s = (s + 1) & (TS64 - 1);
+      }
+    }
+    __syncthreads();
+    if (overflow) break;
+    for (uint64_t e0 = beg; e0 < end; e0 += RED_T) {
+      const uint64_t e = e0 + threadIdx.x;
+      bool isl = false, ist = false;
+      uint32_t idx = 0;
+      if (e < end) {
+        const uint4 r = load_rec(a.rec, e);
+        idx = r.y >> 2;
+        const uint64_t k = a.key[idx];
+        if (!sbits || uint32_t(k & ((1u << sbits) - 1)) == sp) {
+          uint32_t s = uint32_t(k >> 20) & (TS64 - 1);
+          while (tkey[s] != k) s = (s + 1) & (TS64 - 1);
+          const uint32_t w = tval[s] - 1u;
+          if (w == r.y) {
+            if ((r.y & 3) == C_ADD) {
+              isl = true;
+              ++tot.live;
+              tot.size += uint64_t(r.z) | (uint64_t(r.w) << 32);
+              tot.lks += top32_of(b, r.x, a.bucket_bits);
+            } else if ((r.y & 3) == C_REMOVE_KEEP) {
+              ist = true;
+              ++tot.tomb;
+              tot.tks += top32_of(b, r.x, a.bucket_bits);
+            }
+          } else {
+            const uint32_t wi = w >> 2;
+            if (!key_equal(reinterpret_cast<const uint8_t*>(a.path_ptr[idx]), a.path_len[idx],
+                           reinterpret_cast<const uint8_t*>(a.path_ptr[wi]), a.path_len[wi]))
+              collide = 1;
+          }
+        }
+      }
+      wave_append(isl, idx, &nl, a.out_live + beg);
+      wave_append(ist, idx, &nt, a.out_tomb + beg);
+    }
+  }
+  __syncthreads();
+  const bool redo = collide || overflow;
+  if (threadIdx.x == 0) {
+    a.live_count[b] = redo ? 0 : nl;
+    a.tomb_count[b] = redo ? 0 : nt;
+    if (redo) a.exact_list[atomicAdd(&a.totals[4], 1ull)] = b;
+  }
+  store_totals(a, b, redo ? BucketTotals{0, 0, 0, 0, 0} : tot);
+}
+
+// Exact fallback: each record is a winner iff no other record with an equal path has a larger
+// action index. O(m^2) per bucket; only reached on a 64-bit path-hash collision.
 __global__ void __launch_bounds__(RED_T) k_bucket_exact(ReduceArgs a, const uint32_t* buckets) {
   __shared__ uint32_t nl, nt;
-  __shared__ unsigned long long red[5][RED_T / 64];
   const uint32_t b = buckets[blockIdx.x];
   const uint64_t beg = a.bucket_off[b], end = a.bucket_off[b + 1];
   if (threadIdx.x == 0) { nl = 0; nt = 0; }
   __syncthreads();
-  uint64_t live = 0, tomb = 0, size_sum = 0, lks = 0, tks = 0;
+  BucketTotals tot{0, 0, 0, 0, 0};
   for (uint64_t e = beg + threadIdx.x; e < end; e += RED_T) {
-    const uint64_t k = a.rec_key[e];
-    const uint32_t mt = a.rec_meta[e];
-    const uint32_t idx = mt >> 2;
+    const uint4 r = load_rec(a.rec, e);
+    const uint32_t idx = r.y >> 2;
+    const uint64_t k = a.key[idx];
     const uint8_t* p = reinterpret_cast<const uint8_t*>(a.path_ptr[idx]);
     const uint32_t pn = a.path_len[idx];
     bool win = true;
     for (uint64_t f = beg; f < end && win; ++f) {
-      if (f == e || a.rec_key[f] != k) continue;
-      const uint32_t mf = a.rec_meta[f];
-      if ((mf >> 2) <= idx) continue;
-      const uint32_t j = mf >> 2;
+      if (f == e) continue;
+      const uint4 q = load_rec(a.rec, f);
+      const uint32_t j = q.y >> 2;
+      if (q.x != r.x || j <= idx || a.key[j] != k) continue;
       if (key_equal(p, pn, reinterpret_cast<const uint8_t*>(a.path_ptr[j]), a.path_len[j])) win = false;
     }
     if (!win) continue;
-    if ((mt & 3) == C_ADD) {
-      ++live;
-      size_sum += uint64_t(a.size[idx]);
-      lks += k;
+    if ((r.y & 3) == C_ADD) {
+      ++tot.live;
+      tot.size += uint64_t(r.z) | (uint64_t(r.w) << 32);
+      tot.lks += top32_of(b, r.x, a.bucket_bits);
       a.out_live[beg + atomicAdd(&nl, 1u)] = idx;
-    } else if ((mt & 3) == C_REMOVE_KEEP) {
-      ++tomb;
-      tks += k;
+    } else if ((r.y & 3) == C_REMOVE_KEEP) {
+      ++tot.tomb;
+      tot.tks += top32_of(b, r.x, a.bucket_bits);
       a.out_tomb[beg + atomicAdd(&nt, 1u)] = idx;
     }
   }
-  for (int o = 32; o > 0; o >>= 1) {
-    live += __shfl_down(live, o, 64);
-    tomb += __shfl_down(tomb, o, 64);
-    size_sum += __shfl_down(size_sum, o, 64);
-    lks += __shfl_down(lks, o, 64);
-    tks += __shfl_down(tks, o, 64);
-  }
-  if ((threadIdx.x & 63) == 0) {
-    red[0][threadIdx.x >> 6] = live; red[1][threadIdx.x >> 6] = tomb; red[2][threadIdx.x >> 6] = size_sum;
-    red[3][threadIdx.x >> 6] = lks; red[4][threadIdx.x >> 6] = tks;
-  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    unsigned long long L = 0, T = 0, S = 0, LK = 0, TK = 0;
-    for (int k = 0; k < RED_T / 64; ++k) {
-      L += red[0][k]; T += red[1][k]; S += red[2][k]; LK += red[3][k]; TK += red[4][k];
-    }
     a.live_count[b] = nl;
     a.tomb_count[b] = nt;
-    atomicAdd(&a.totals[0], L);
-    atomicAdd(&a.totals[1], S);
-    atomicAdd(&a.totals[2], T);
-    atomicAdd(&a.totals[5], LK);
-    atomicAdd(&a.totals[6], TK);
   }
+  store_totals(a, b, tot);
 }
 
 __global__ void k_compact(CompactArgs a) {
@@ -461,22 +641,39 @@ void launch_canon(const CanonArgs& a, hipStream_t st) {
   if (a.n) hipLaunchKernelGGL(dev::k_canon, dim3(unsigned((a.n + 255) / 256)), dim3(256), 0, st, a);
 }
 
+uint32_t part_tiles(uint64_t n) { return uint32_t((n + dev::PART_TILE - 1) / dev::PART_TILE); }
+uint32_t part_max_bucket_bits() { return dev::PART_MAX_BITS; }
+
 void launch_bucket_hist(const PartitionArgs& a, hipStream_t st) {
-  uint64_t nb = (a.n + dev::PART_TILE - 1) / dev::PART_TILE;
-  if (nb) hipLaunchKernelGGL(dev::k_bucket_hist, dim3(unsigned(nb)), dim3(dev::PART_T), 0, st, a);
+  if (a.ntiles) hipLaunchKernelGGL(dev::k_bucket_hist, dim3(a.ntiles), dim3(dev::PART_T), 0, st, a);
 }
 
 void launch_bucket_scatter(const PartitionArgs& a, hipStream_t st) {
-  uint64_t nb = (a.n + dev::PART_TILE - 1) / dev::PART_TILE;
-  if (nb) hipLaunchKernelGGL(dev::k_bucket_scatter, dim3(unsigned(nb)), dim3(dev::PART_T), 0, st, a);
+  if (a.ntiles) hipLaunchKernelGGL(dev::k_bucket_scatter, dim3(a.ntiles), dim3(dev::PART_T), 0, st, a);
+}
+
+void launch_bucket_offsets(const uint64_t* tile_off, uint32_t nb, uint32_t nt, uint64_t* bucket_off, hipStream_t st) {
+  hipLaunchKernelGGL(dev::k_bucket_offsets, dim3((nb + 1 + 255) / 256), dim3(256), 0, st, tile_off, nb, nt, bucket_off);
 }
 
 void launch_bucket_reduce(const ReduceArgs& a, hipStream_t st) {
   if (a.nbuckets) hipLaunchKernelGGL(dev::k_bucket_reduce, dim3(a.nbuckets), dim3(dev::RED_T), 0, st, a);
 }
 
+void launch_bucket_verify(const ReduceArgs& a, hipStream_t st) {
+  if (a.nbuckets) hipLaunchKernelGGL(dev::k_bucket_verify, dim3(a.nbuckets), dim3(64), 0, st, a);
+}
+
+void launch_bucket_reduce64(const ReduceArgs& a, const uint32_t* buckets, uint32_t nb, hipStream_t st) {
+  if (nb) hipLaunchKernelGGL(dev::k_bucket_reduce64, dim3(nb), dim3(dev::RED_T), 0, st, a, buckets);
+}
+
 void launch_bucket_exact(const ReduceArgs& a, const uint32_t* buckets, uint32_t nb, hipStream_t st) {
   if (nb) hipLaunchKernelGGL(dev::k_bucket_exact, dim3(nb), dim3(dev::RED_T), 0, st, a, buckets);
+}
+
+void launch_sum_stats(const ReduceArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(dev::k_sum_stats, dim3(1), dim3(1024), 0, st, a.bstats, a.nbuckets, a.totals);
 }
 
 void launch_compact(const CompactArgs& a, hipStream_t st) {

@@ -161,42 +161,71 @@ struct CanonArgs {
 void launch_canon(const CanonArgs& a, hipStream_t st);
 
 // ---- K3/K4: partition by hash bucket + per-bucket last-writer-wins ------------------------------
+// A partition record is 16 B: {rkey = the 32 key bits below the bucket bits, meta = action index
+// << 2 | class, add.size}. Tiles of PART_TILE actions count their buckets in LDS into a bucket-major
+// count matrix; its exclusive scan gives every (bucket, tile) its output range, so the scatter
+// needs no global atomics.
+struct PartRec {
+  uint32_t rkey;
+  uint32_t meta;
+  int64_t size;
+};
 struct PartitionArgs {
   const uint8_t* kind;
   const uint8_t* flags;
   const uint64_t* key;
+  const int64_t* size;
   const int64_t* delts;
   uint64_t n;
-  int64_t cutoff;          // minFileRetentionTimestamp
+  int64_t cutoff;              // minFileRetentionTimestamp
   int32_t bucket_bits;
-  uint32_t* bucket_count;  // [nbuckets] histogram / cursors
-  const uint64_t* bucket_off;  // [nbuckets+1] exclusive offsets
-  uint64_t* rec_key;       // partitioned records
-  uint32_t* rec_meta;      // idx << 2 | class
-};
-void launch_bucket_hist(const PartitionArgs& a, hipStream_t st);
-void launch_bucket_scatter(const PartitionArgs& a, hipStream_t st);
-
-struct ReduceArgs {
-  const uint64_t* rec_key;
-  const uint32_t* rec_meta;
-  const uint64_t* bucket_off;
-  uint32_t nbuckets;
-  int32_t bucket_bits;
+  uint32_t ntiles;
+  uint32_t* tile_count;        // [nbuckets * ntiles] bucket-major counts
+  const uint64_t* tile_off;    // [nbuckets * ntiles + 1] exclusive scan of tile_count
+  PartRec* rec;                // partitioned records
   const uint64_t* path_ptr;
   const uint32_t* path_len;
-  const int64_t* size;
-  uint32_t verify_bytes;   // 1: byte-verify every multi-member key group
-  uint32_t* out_live;      // per-bucket survivors, written at bucket_off[b]
-  uint32_t* out_tomb;
-  uint32_t* live_count;    // [nbuckets]
-  uint32_t* tomb_count;    // [nbuckets]
-  unsigned long long* totals;  // [0] live files, [1] size sum, [2] tombstones, [3] collisions, [4] overflow buckets
-  uint32_t* collide_list;  // buckets that saw a path-hash collision (resolved by k_bucket_exact)
-  uint32_t* overflow_list; // buckets whose distinct keys overflowed the LDS table
+  uint64_t* rec_pref;          // per record: path address | length << 48 (0: length >= 0xffff)
 };
+uint32_t part_tiles(uint64_t n);
+uint32_t part_max_bucket_bits();
+void launch_bucket_hist(const PartitionArgs& a, hipStream_t st);
+void launch_bucket_scatter(const PartitionArgs& a, hipStream_t st);
+// bucket_off[b] = tile_off[b * ntiles], b in [0, nbuckets]
+void launch_bucket_offsets(const uint64_t* tile_off, uint32_t nbuckets, uint32_t ntiles, uint64_t* bucket_off,
+                           hipStream_t st);
+
+struct ReduceArgs {
+  const PartRec* rec;
+  const uint64_t* bucket_off;  // [nbuckets + 1]
+  uint32_t nbuckets;
+  int32_t bucket_bits;
+  const uint64_t* key;         // full keys by action index (fallback reducers only)
+  const uint64_t* path_ptr;
+  const uint32_t* path_len;
+  uint32_t* out_live;          // per-bucket survivors, written at bucket_off[b]
+  uint32_t* out_tomb;
+  const uint64_t* rec_pref;    // per record path reference (PartitionArgs::rec_pref)
+  ulonglong2* out_pair;        // per-bucket (loser, winner) path references for k_bucket_verify
+  uint32_t* live_count;        // [nbuckets]
+  uint32_t* tomb_count;        // [nbuckets]
+  uint32_t* pair_count;        // [nbuckets]
+  unsigned long long* totals;  // [0] live files, [1] size sum, [2] tombstones, [3] buckets for the 64-bit
+                               // reducer, [4] buckets for the exact reducer, [5] live / [6] tombstone checksum
+  uint32_t* redo_list;         // buckets with a (bucket, rkey) collision or an LDS-table overflow
+  uint32_t* exact_list;        // buckets with a 64-bit path-hash collision
+  unsigned long long* bstats;  // [nbuckets * 5] per-bucket {live, tomb, size, live sum, tomb sum}
+};
+// LDS last-writer-wins per bucket on the 32 rkey bits; losers paired with winners
 void launch_bucket_reduce(const ReduceArgs& a, hipStream_t st);
+// byte-verifies every (loser, winner) pair; mismatching buckets -> redo_list
+void launch_bucket_verify(const ReduceArgs& a, hipStream_t st);
+// redo_list buckets, keyed by the full 64-bit hash; 64-bit collisions -> exact_list
+void launch_bucket_reduce64(const ReduceArgs& a, const uint32_t* buckets, uint32_t nb, hipStream_t st);
+// exact O(m^2) reducer
 void launch_bucket_exact(const ReduceArgs& a, const uint32_t* buckets, uint32_t nb, hipStream_t st);
+// sums the per-bucket statistics into totals[0,1,2,5,6]
+void launch_sum_stats(const ReduceArgs& a, hipStream_t st);
 
 // Compaction of per-bucket survivor lists into dense arrays.
 struct CompactArgs {

@@ -146,9 +146,12 @@ class Staged:
                  "pages_decompressed_bytes", "dict_entries"]
         return {names[i]: int(out[i]) for i in range(n.value)}
 
-    def replay(self, min_file_retention_timestamp: int, validate: bool = True) -> "State":
+    def replay(self, min_file_retention_timestamp: int, validate: bool = True, reducer: str = "lds") -> "State":
+        """`reducer` is a test hook: "reduce64" / "exact" force every hash bucket through the 64-bit-key
+        or the O(m^2) fallback reducer instead of the LDS rkey table."""
         st = C.c_void_p()
-        flags = 0 if validate else N.DR_FLAG_NO_VALIDATION
+        flags = (0 if validate else N.DR_FLAG_NO_VALIDATION) | {
+            "lds": 0, "reduce64": N.DR_FLAG_REDUCE64, "exact": N.DR_FLAG_EXACT_REDUCE}[reducer]
         self.eng.check(self.eng.lib.dr_replay_staged(self.eng.ctx, self.h, int(min_file_retention_timestamp),
                                                      flags, C.byref(st)))
         return State(self.eng, st)

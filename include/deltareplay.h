@@ -72,12 +72,14 @@ typedef struct dr_counts {
   int64_t num_file_actions;       /* add + remove actions replayed */
   int64_t version;                /* snapshot version */
   int64_t malformed_lines;        /* JSON lines Spark's PERMISSIVE reader would null out */
-  uint64_t live_key_sum;          /* sum (mod 2^64) of xxh64(path key) over allFiles */
+  uint64_t live_key_sum;          /* sum (mod 2^64) of the top 32 bits of xxh64(path key) over allFiles */
   uint64_t tomb_key_sum;          /* same over tombstones: order-free checksum for parity */
 } dr_counts;
 
 /* Replay flags. */
 #define DR_FLAG_NO_VALIDATION 0x1u  /* stateReconstructionValidation.enabled=false (D/sources/DeltaSQLConf.scala:86-91) */
+#define DR_FLAG_EXACT_REDUCE 0x2u   /* test hook: reduce every bucket with the exact O(m^2) kernel */
+#define DR_FLAG_REDUCE64 0x4u       /* test hook: reduce every bucket with the 64-bit-key fallback kernel */
 
 /* Export columns of one side of the state (allFiles or tombstones; D/Snapshot.scala:193-204).
  * Strings: `*_off` has n+1 entries into `*_bytes`. Maps (partitionValues, tags): `*_entry_off`

@@ -106,6 +106,30 @@ def test_synthetic_configs(engine, tmp_path, config, scale):
         st.release()
 
 
+@pytest.mark.parametrize("reducer", ["reduce64", "exact"])
+def test_fallback_reducers_agree(engine, tmp_path, reducer):
+    """The collision fallbacks (k_bucket_reduce64 / k_bucket_exact, forced for every bucket) and the
+    LDS rkey-table reducer give identical states; 160k actions span 64+ buckets."""
+    from delta_amd.testing import synth as S
+    exp = S.build_config(3, str(tmp_path), scale=0.01)
+    lp = os.path.join(str(tmp_path), "_delta_log")
+    staged = engine.stage_log(lp)
+    try:
+        a = staged.replay(exp.min_file_retention_timestamp)
+        b = staged.replay(exp.min_file_retention_timestamp, reducer=reducer)
+    finally:
+        staged.release()
+    try:
+        for k in ("num_files", "size_in_bytes", "num_removes", "live_key_sum", "tomb_key_sum", "num_file_actions"):
+            assert a.counts[k] == b.counts[k], k
+        assert a.counts["num_files"] == exp.num_files and a.counts["num_removes"] == exp.num_removes
+        assert sorted(r["path"] for r in a.export(0)) == sorted(r["path"] for r in b.export(0))
+        assert sorted(r["path"] for r in a.export(1)) == sorted(r["path"] for r in b.export(1))
+    finally:
+        a.release()
+        b.release()
+
+
 @pytest.mark.parametrize("page_size,compression,page_version,rg,dictionary", [
     (4096, "snappy", "1.0", 1 << 20, True),
     (64 << 10, "snappy", "1.0", 7000, True),

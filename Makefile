@@ -12,7 +12,15 @@ HDRS := $(wildcard $(CSRC)/*.h) include/deltareplay.h
 HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function -Wno-unused-variable
 CXXFLAGS := -O2 -std=c++17 -fPIC -Wall
 
-all: $(LIB) oracle
+JL_HOST := build/libjsonlane_host.so
+
+all: $(LIB) oracle $(JL_HOST)
+
+# host build of the K1 line walker, fuzzed against Python json by tests/test_json_lane.py
+$(JL_HOST): tests/native/json_lane_host.cpp $(CSRC)/json_lane.h
+	@mkdir -p build
+	g++ -O2 -std=c++17 -fPIC -shared -Wall -o $@ $<
+
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)

@@ -744,7 +744,8 @@ static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
   st->delts = DBuf<int64_t>(ctx, N);
   st->src_off = DBuf<uint64_t>(ctx, N);
   st->src_len = DBuf<uint32_t>(ctx, N);
-  DBuf<uint64_t> counters(ctx, 8);  // 0 special count, 1 special bytes, 2 nonfile count, 3 errors, 4 canon fill
+  DBuf<uint64_t> counters(ctx, 8);  // 0 special count, 1 special bytes, 2 nonfile count, 3 errors, 4 canon fill,
+                                     // 5 lines deferred to the General walker
   counters.zero(stream);
   DBuf<uint64_t> nl(ctx, nlines);
   DBuf<uint64_t> nonfile(ctx, nlines);
@@ -754,11 +755,15 @@ static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
   if (nlines) {
     launch_json_newlines(s.d_json.p, json_len, joff.p, nl.p, stream);
     ctx->mark("json_newlines");
+    DBuf<uint64_t> hard(ctx, nlines);
     JsonParseArgs ja{s.d_json.p, nl.p, nlines, R, act.kind, act.flags, act.key, act.path_ptr, act.path_len,
                      act.size, act.delts, act.src_off, act.src_len, counters.p + 0, counters.p + 1, counters.p + 2,
-                     nonfile.p, nlines, counters.p + 3};
+                     nonfile.p, nlines, counters.p + 3, hard.p,
+                     reinterpret_cast<unsigned long long*>(counters.p + 5)};
     launch_json_parse(ja, stream);
     ctx->mark("json_parse");
+    launch_json_hard(ja, stream);
+    ctx->mark("json_hard");
   }
   // ---- K2: checkpoint ----
   DBuf<uint8_t> cdef[HC_N];

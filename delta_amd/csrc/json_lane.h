@@ -1,0 +1,620 @@
+// K1 line parser: one lane owns one newline-delimited JSON line (one Delta log action) and walks it
+// in 16-byte windows. Each window is classified with SWAR byte tests into 16-bit masks (quote,
+// backslash, structural, space, control); escapes and string state are resolved on those masks
+// with carries from the previous window (the bit-parallel quote/escape method of simdjson, on
+// 16-bit lanes), which yields the window's token mask. A table-free DFA then consumes only the
+// tokens (brackets, ':', ',', quotes, scalar starts) -- about 45 per add line instead of ~330
+// bytes -- validating JSON grammar and extracting the SingleAction envelope (unwrap priority,
+// D/actions/actions.scala:523-541) and the add/remove path, size and deletionTimestamp
+// (AddFile/RemoveFile field names, D/actions/actions.scala:220-320).
+//
+// Semantics match Spark's JSON reader over Action.logSchema in PERMISSIVE mode
+// (D/DeltaLogFileIndex.scala:67): a line that is not a valid JSON object is a null row (K_ERROR,
+// counted, ignored), unknown fields are ignored, a member whose value is null is absent, a repeated
+// member keeps its last value (every occurrence is converted when read, as Spark's streaming
+// JacksonParser does). The fast instantiation flags the lines it does not decide (a backslash inside
+// a key it must match, tab / CR outside strings, nesting deeper than 62) as `hard`; the General
+// instantiation of the same walker decides those (k_json_hard re-parses them).
+//
+// Written for HIP device code and for the host (tests/json_lane_host.cpp builds it with g++ to
+// fuzz it against Python's json module).
+#pragma once
+#include <cstdint>
+#include <cstring>
+
+#if defined(__HIPCC__)
+#define JL_HD __host__ __device__ __forceinline__
+#else
+#define JL_HD inline
+#endif
+
+namespace dr {
+namespace jl {
+
+enum : uint8_t { K_NONE = 0, K_ADD = 1, K_REMOVE = 2, K_METADATA = 3, K_TXN = 4, K_PROTOCOL = 5, K_CDC = 6,
+                 K_COMMITINFO = 7, K_ERROR = 15 };
+enum : uint8_t { F_HAS_DELTS = 1, F_PATH_ESCAPED = 4, F_PATH_NULL = 8 };
+
+struct LineOut {
+  uint8_t kind;
+  uint8_t flags;
+  uint8_t hard;        // undecided: re-parse with the general parser
+  uint32_t path_off;   // path content span, relative to the line start
+  uint32_t path_len;
+  int64_t size;
+  int64_t delts;
+};
+
+// ---- SWAR byte classes -------------------------------------------------------------------------
+// 0x80 in every byte of y that is zero (exact, no cross-byte borrows)
+JL_HD uint32_t zbytes(uint32_t y) { return ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y | 0x7F7F7F7Fu); }
+// 0x80 in every byte of x that is < 0x20
+JL_HD uint32_t lt20(uint32_t x) { return ~((x | 0x80808080u) - 0x20202020u) & ~x & 0x80808080u; }
+// bits 7, 15, 23, 31 -> bits 0..3
+JL_HD uint32_t gather4(uint32_t m) {
+  m >>= 7;
+  m |= m >> 7;
+  m |= m >> 14;
+  return m & 0xFu;
+}
+JL_HD uint32_t prefix_xor16(uint32_t x) {
+  x ^= x << 1;
+  x ^= x << 2;
+  x ^= x << 4;
+  x ^= x << 8;
+  return x & 0xFFFFu;
+}
+
+struct Win {
+  uint32_t q, bs, st, sp, ctrl;  // 16-bit masks
+};
+
+JL_HD void classify(const uint32_t w[4], Win& m) {
+  m.q = m.bs = m.st = m.sp = m.ctrl = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t x = w[d], xo = x | 0x20202020u;
+    const uint32_t q = zbytes(x ^ 0x22222222u);
+    const uint32_t bs = zbytes(x ^ 0x5C5C5C5Cu);
+    const uint32_t st = zbytes(xo ^ 0x7B7B7B7Bu) | zbytes(xo ^ 0x7D7D7D7Du) | zbytes(x ^ 0x3A3A3A3Au) |
+                        zbytes(x ^ 0x2C2C2C2Cu);
+    const uint32_t sp = zbytes(x ^ 0x20202020u);
+    const uint32_t ct = lt20(x);
+    m.q |= gather4(q) << (4 * d);
+    m.bs |= gather4(bs) << (4 * d);
+    m.st |= gather4(st) << (4 * d);
+    m.sp |= gather4(sp) << (4 * d);
+    m.ctrl |= gather4(ct) << (4 * d);
+  }
+}
+
+JL_HD uint32_t win_byte(const uint32_t w[4], uint32_t k) {
+  const uint32_t d = k >> 2;
+  const uint32_t x = d == 0 ? w[0] : d == 1 ? w[1] : d == 2 ? w[2] : w[3];
+  return (x >> (8 * (k & 3))) & 0xFFu;
+}
+
+JL_HD uint32_t ctz32(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return uint32_t(__builtin_ctz(x));
+#else
+  return uint32_t(__builtin_ctz(x));
+#endif
+}
+JL_HD uint32_t popc32(uint32_t x) { return uint32_t(__builtin_popcount(x)); }
+
+// ---- scalars ----------------------------------------------------------------------------------
+enum : uint8_t { SC_BAD = 0, SC_NULL, SC_TRUE, SC_FALSE, SC_INT, SC_NUM };
+
+// ---- keys ----------------------------------------------------------------------------------------
+JL_HD bool key_eq(const uint8_t* s, uint32_t n, const char* k, uint32_t kn) {
+  if (n != kn) return false;
+  for (uint32_t i = 0; i < n; ++i)
+    if (s[i] != uint8_t(k[i])) return false;
+  return true;
+}
+// top-level member -> action kind (0: not an action)
+JL_HD uint8_t action_key(const uint8_t* s, uint32_t n) {
+  switch (n) {
+    case 3:
+      if (key_eq(s, n, "add", 3)) return K_ADD;
+      if (key_eq(s, n, "txn", 3)) return K_TXN;
+      if (key_eq(s, n, "cdc", 3)) return K_CDC;
+      return 0;
+    case 6: return key_eq(s, n, "remove", 6) ? K_REMOVE : 0;
+    case 8:
+      if (key_eq(s, n, "metaData", 8)) return K_METADATA;
+      if (key_eq(s, n, "protocol", 8)) return K_PROTOCOL;
+      return 0;
+    case 10: return key_eq(s, n, "commitInfo", 10) ? K_COMMITINFO : 0;
+    default: return 0;
+  }
+}
+enum : uint8_t { FK_OTHER = 0, FK_PATH, FK_SIZE, FK_DELTS };
+JL_HD uint8_t file_key(const uint8_t* s, uint32_t n) {
+  if (n == 4) {
+    if (key_eq(s, n, "path", 4)) return FK_PATH;
+    if (key_eq(s, n, "size", 4)) return FK_SIZE;
+    return FK_OTHER;
+  }
+  if (n == 17 && key_eq(s, n, "deletionTimestamp", 17)) return FK_DELTS;
+  return FK_OTHER;
+}
+
+// ---- phase 1: tokenizer ----------------------------------------------------------------------------
+// A token is one u32: line offset << 16 | aux << 4 | class. Scalars are emitted when their run
+// ends, with aux = run length, so phase 2 never scans for a scalar's end.
+enum : uint32_t { T_OBJ_OPEN = 0, T_ARR_OPEN, T_OBJ_CLOSE, T_ARR_CLOSE, T_COLON, T_COMMA, T_STR_OPEN,
+                  T_STR_CLOSE, T_STR_CLOSE_ESC, T_SCALAR };
+constexpr uint32_t TOK_MAX_LINE = 65535;   // longer lines go to the General walker
+constexpr uint32_t TOK_MAX_SCALAR = 4095;
+
+JL_HD uint32_t tok_make(uint32_t off, uint32_t aux, uint32_t cls) { return (off << 16) | (aux << 4) | cls; }
+JL_HD uint32_t tok_off(uint32_t t) { return t >> 16; }
+JL_HD uint32_t tok_aux(uint32_t t) { return (t >> 4) & 0xFFFu; }
+JL_HD uint32_t tok_cls(uint32_t t) { return t & 0xFu; }
+
+enum : uint8_t { ST_OK = 0, ST_BAD = 1, ST_HARD = 2 };
+
+struct Tokenizer {
+  uint32_t esc_carry = 0, in_str = 0, sc_carry = 0;
+  uint32_t pend_bs = 0;      // a backslash in the string still open
+  uint32_t sc_start = 0;     // line offset where the open scalar run began
+  uint32_t sc_bytes = 0;     // scalar bytes seen (each must belong to a validated scalar)
+  uint8_t status = ST_OK;
+};
+
+// Loads the aligned 16-byte window at a (a is 16-byte aligned; the buffer is readable there).
+JL_HD void load_window(const uint8_t* a, uint32_t w[4]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint4 v = *reinterpret_cast<const uint4*>(a);
+  w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+#else
+  std::memcpy(w, a, 16);
+#endif
+}
+
+// Tokenizes the window whose byte 0 has line offset `lo` (may be negative for the first window).
+template <bool General, typename Emit>
+JL_HD void tokenize_window(const uint8_t* p, uint32_t n, const uint32_t w[4], int32_t lo, Tokenizer& tz,
+                           Emit&& emit) {
+  uint32_t valid = 0xFFFFu;
+  if (lo < 0) valid &= 0xFFFFu << uint32_t(-lo);
+  if (lo + 16 > int32_t(n)) valid &= (1u << uint32_t(int32_t(n) - lo)) - 1u;
+  Win m;
+  classify(w, m);
+  m.q &= valid; m.bs &= valid; m.st &= valid; m.sp &= valid; m.ctrl &= valid;
+  // escaped bytes: those preceded by an odd run of backslashes (carry from the previous window)
+  uint32_t escaped = 0;
+  if (m.bs | tz.esc_carry) {
+    const uint32_t bsn = m.bs & ~tz.esc_carry;
+    const uint32_t follows = ((bsn << 1) | tz.esc_carry) & 0xFFFFu;
+    const uint32_t odd_starts = bsn & ~0x5555u & ~follows;
+    const uint32_t sum = odd_starts + bsn;
+    escaped = (0x5555u ^ ((sum << 1) & 0xFFFFu)) & follows;
+    tz.esc_carry = (sum >> 16) & 1u;
+  }
+  const uint32_t quote = m.q & ~escaped;
+  const uint32_t instr = prefix_xor16(quote) ^ (tz.in_str ? 0xFFFFu : 0u);
+  tz.in_str = (instr >> 15) & 1u;
+  if (m.ctrl & instr) { tz.status = ST_BAD; return; }  // control byte inside a string
+  uint32_t ws = m.sp;
+  if (m.ctrl & ~instr) {
+    if (!General) { tz.status = ST_HARD; return; }
+    // tab and CR are whitespace between tokens; any other control byte there is malformed
+    uint32_t tabcr = 0;
+    for (int d = 0; d < 4; ++d)
+      tabcr |= gather4(zbytes(w[d] ^ 0x09090909u) | zbytes(w[d] ^ 0x0D0D0D0Du)) << (4 * d);
+    if ((m.ctrl & ~instr) & ~tabcr) { tz.status = ST_BAD; return; }
+    ws |= m.ctrl & ~instr;
+  }
+  // escape sequences other than \" and \\ must be one of \/ \b \f \n \r \t \uXXXX
+  uint32_t oddesc = escaped & ~(m.q | m.bs) & valid;
+  while (oddesc) {
+    const uint32_t k = ctz32(oddesc);
+    oddesc &= oddesc - 1;
+    const uint32_t c = win_byte(w, k);
+    if (c == 'u') {
+      const uint32_t off = uint32_t(lo + int32_t(k));
+      if (off + 4 >= n) { tz.status = ST_BAD; return; }
+      for (uint32_t h = 1; h <= 4; ++h) {
+        const uint32_t x = p[off + h] | 0x20u;
+        if (!((x >= '0' && x <= '9') || (x >= 'a' && x <= 'f'))) { tz.status = ST_BAD; return; }
+      }
+    } else if (!(c == '/' || c == 'b' || c == 'f' || c == 'n' || c == 'r' || c == 't')) {
+      tz.status = ST_BAD;
+      return;
+    }
+  }
+  const uint32_t st = m.st & ~instr;
+  const uint32_t sc = valid & ~instr & ~quote & ~st & ~ws;
+  tz.sc_bytes += popc32(sc);
+  // a scalar run that ended at the previous window's last byte
+  if (tz.sc_carry && !(sc & 1u)) {
+    const uint32_t end = uint32_t(lo);  // one past the run
+    const uint32_t len = end - tz.sc_start;
+    if (len > TOK_MAX_SCALAR) { tz.status = ST_BAD; return; }
+    emit(tok_make(tz.sc_start, len, T_SCALAR));
+  }
+  const uint32_t sc_begin = sc & ~(((sc << 1) | tz.sc_carry) & 0xFFFFu);
+  const uint32_t sc_end = sc & ~(sc >> 1) & 0x7FFFu;  // run ends inside this window
+  tz.sc_carry = (sc >> 15) & 1u;
+  uint32_t tok = st | quote | sc_end;
+  uint32_t open_k = 0xFFFFFFFFu;
+  uint32_t begins = sc_begin;
+  while (tok) {
+    const uint32_t k = ctz32(tok);
+    tok &= tok - 1;
+    const uint32_t off = uint32_t(lo + int32_t(k));
+    const uint32_t bit = 1u << k;
+    if (quote & bit) {
+      if (instr & bit) {
+        open_k = k;
+        tz.pend_bs = 0;
+        emit(tok_make(off, 0, T_STR_OPEN));
+      } else {
+        const uint32_t below = bit - 1u;
+        const bool has_bs = open_k != 0xFFFFFFFFu ? (m.bs & below & ~((2u << open_k) - 1u)) != 0
+                                                  : (tz.pend_bs || (m.bs & below) != 0);
+        open_k = 0xFFFFFFFFu;
+        emit(tok_make(off, 0, has_bs ? T_STR_CLOSE_ESC : T_STR_CLOSE));
+      }
+    } else if (st & bit) {
+      const uint32_t c = win_byte(w, k);
+      const uint32_t cls = c == ':' ? T_COLON : c == ',' ? T_COMMA
+                         : ((c & 2u) ? T_OBJ_OPEN : T_OBJ_CLOSE) + ((c & 0x20u) ? 0u : 1u);
+      emit(tok_make(off, 0, cls));
+    } else {  // a scalar run ends at k
+      // its start is in this window (a begin bit at or below k) or carried from an earlier one
+      const uint32_t bb = begins & ((bit << 1) - 1u);
+      uint32_t start = tz.sc_start;
+      if (bb) {
+        const uint32_t kb = 31u - uint32_t(__builtin_clz(bb));
+        start = uint32_t(lo + int32_t(kb));
+        begins &= ~((bit << 1) - 1u);
+      }
+      const uint32_t len = off + 1 - start;
+      if (len > TOK_MAX_SCALAR) { tz.status = ST_BAD; return; }
+      emit(tok_make(start, len, T_SCALAR));
+    }
+  }
+  if (begins) tz.sc_start = uint32_t(lo + int32_t(ctz32(begins)));  // a run that continues
+  // a string still open at the window end: remember whether it held a backslash
+  if (tz.in_str) {
+    const uint32_t from = open_k != 0xFFFFFFFFu ? (m.bs & ~((2u << open_k) - 1u)) : m.bs;
+    tz.pend_bs = tz.pend_bs | (from != 0);
+  }
+}
+
+// Line end: a scalar running to the last byte.
+template <typename Emit>
+JL_HD void tokenize_end(uint32_t n, Tokenizer& tz, Emit&& emit) {
+  if (tz.status == ST_OK && tz.sc_carry) {
+    const uint32_t len = n - tz.sc_start;
+    if (len > TOK_MAX_SCALAR) { tz.status = ST_BAD; return; }
+    emit(tok_make(tz.sc_start, len, T_SCALAR));
+    tz.sc_carry = 0;
+  }
+}
+
+// ---- phase 2: grammar + SingleAction extraction ----------------------------------------------------
+enum : uint8_t { S_START = 0, S_OBJ_FIRST, S_KEY, S_COLON, S_VALUE, S_ARR_FIRST, S_AFTER, S_DONE, S_STR };
+
+struct FileObj {
+  uint32_t path_off, path_len;
+  int64_t size, delts;
+  uint8_t flags;  // F_HAS_DELTS | F_PATH_ESCAPED | F_PATH_NULL
+};
+
+constexpr uint32_t GEN_MAX_DEPTH = 1024;  // General mode: deeper nesting is an error row
+
+template <bool General>
+struct Dfa {
+  uint8_t state = S_START, key_role = 0, k1 = 0, k2 = 0, status = ST_OK;
+  bool in_file = false;
+  uint32_t depth = 0;
+  uint64_t arr_bits = 0;  // bit d: the container at depth d is an array (d < 64)
+  uint64_t deep_bits[General ? GEN_MAX_DEPTH / 64 : 1];  // General mode only
+  uint32_t present = 0;   // bit per action kind whose (last) value is non-null
+  uint32_t str_start = 0;
+  uint32_t sc_checked = 0;
+  FileObj cur{0, 0, 0, 0, F_PATH_NULL}, fadd{0, 0, 0, 0, F_PATH_NULL}, frm{0, 0, 0, 0, F_PATH_NULL};
+
+  JL_HD bool is_arr(uint32_t d) const {
+    if constexpr (General) {
+      if (d >= 64) return ((deep_bits[d >> 6] >> (d & 63)) & 1ull) != 0;
+    }
+    return ((arr_bits >> (d & 63)) & 1ull) != 0;
+  }
+  JL_HD void set_arr(uint32_t d, bool a) {
+    if constexpr (General) {
+      if (d >= 64) {
+        uint64_t& word = deep_bits[d >> 6];
+        word = a ? (word | (1ull << (d & 63))) : (word & ~(1ull << (d & 63)));
+        return;
+      }
+    }
+    const uint64_t bit = 1ull << (d & 63);
+    arr_bits = a ? (arr_bits | bit) : (arr_bits & ~bit);
+  }
+};
+
+// Unescapes a short JSON string body (a member name) into buf; returns its length, or 0xFFFFFFFF if
+// it does not fit (no key this walker matches is longer than 17 bytes).
+JL_HD uint32_t unescape_key(const uint8_t* s, uint32_t n, uint8_t* buf, uint32_t cap) {
+  uint32_t o = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    uint32_t c = s[i];
+    if (c == '\\' && i + 1 < n) {
+      const uint32_t e = s[++i];
+      if (e == 'u' && i + 4 < n) {
+        uint32_t cp = 0;
+        for (int h = 0; h < 4; ++h) {
+          const uint32_t x = s[++i] | 0x20u;
+          cp = cp * 16 + (x <= '9' ? x - '0' : x - 'a' + 10);
+        }
+        if (cp >= 0x80) return 0xFFFFFFFFu;  // no matched key holds non-ASCII characters
+        c = cp;
+      } else {
+        c = e == 'b' ? 8 : e == 'f' ? 12 : e == 'n' ? 10 : e == 'r' ? 13 : e == 't' ? 9 : e;
+      }
+    }
+    if (o >= cap) return 0xFFFFFFFFu;
+    buf[o++] = uint8_t(c);
+  }
+  return o;
+}
+
+// Validates a scalar of known extent (JSON number grammar without leading zeros, or a literal).
+JL_HD uint8_t scalar_class(const uint8_t* s, uint32_t L, int64_t* val) {
+  if (L == 4 && s[0] == 'n' && s[1] == 'u' && s[2] == 'l' && s[3] == 'l') return SC_NULL;
+  if (L == 4 && s[0] == 't' && s[1] == 'r' && s[2] == 'u' && s[3] == 'e') return SC_TRUE;
+  if (L == 5 && s[0] == 'f' && s[1] == 'a' && s[2] == 'l' && s[3] == 's' && s[4] == 'e') return SC_FALSE;
+  uint32_t i = 0;
+  const bool neg = L > 0 && s[0] == '-';
+  if (neg) ++i;
+  if (i >= L || s[i] < '0' || s[i] > '9') return SC_BAD;
+  uint64_t v = 0;
+  bool ovf = false;
+  if (s[i] == '0') {
+    ++i;
+  } else {
+    while (i < L && s[i] >= '0' && s[i] <= '9') {
+      const uint64_t dg = uint64_t(s[i] - '0');
+      if (v > (0xFFFFFFFFFFFFFFFFull - dg) / 10ull) ovf = true;
+      v = v * 10ull + dg;
+      ++i;
+    }
+  }
+  bool integral = true;
+  if (i < L && s[i] == '.') {
+    integral = false;
+    ++i;
+    const uint32_t f0 = i;
+    while (i < L && s[i] >= '0' && s[i] <= '9') ++i;
+    if (i == f0) return SC_BAD;
+  }
+  if (i < L && (s[i] == 'e' || s[i] == 'E')) {
+    integral = false;
+    ++i;
+    if (i < L && (s[i] == '+' || s[i] == '-')) ++i;
+    const uint32_t x0 = i;
+    while (i < L && s[i] >= '0' && s[i] <= '9') ++i;
+    if (i == x0) return SC_BAD;
+  }
+  if (i != L) return SC_BAD;
+  if (!integral) return SC_NUM;
+  // LongType: VALUE_NUMBER_INT within [-2^63, 2^63-1]
+  if (ovf || v > (neg ? 0x8000000000000000ull : 0x7FFFFFFFFFFFFFFFull)) return SC_NUM;
+  *val = neg ? int64_t(0ull - v) : int64_t(v);
+  return SC_INT;
+}
+
+// One token through the JSON grammar and the Action.logSchema extraction.
+template <bool General>
+JL_HD void dfa_token(const uint8_t* p, uint32_t tok, Dfa<General>& d) {
+  const uint32_t cls = tok_cls(tok), off = tok_off(tok);
+  const uint8_t stt = d.state;
+  if (cls == T_STR_OPEN) {
+    if (stt == S_OBJ_FIRST || stt == S_KEY) d.key_role = 1;
+    else if (stt == S_VALUE || stt == S_ARR_FIRST) d.key_role = 0;
+    else { d.status = ST_BAD; return; }
+    d.state = S_STR;
+    d.str_start = off + 1;
+    return;
+  }
+  if (cls == T_STR_CLOSE || cls == T_STR_CLOSE_ESC) {
+    const bool has_bs = cls == T_STR_CLOSE_ESC;
+    const uint8_t* s = p + d.str_start;
+    const uint32_t sl = off - d.str_start;
+    if (d.key_role) {
+      if (d.depth == 1 || (d.depth == 2 && d.in_file)) {
+        if (has_bs) {
+          if constexpr (!General) {
+            d.status = ST_HARD;
+            return;
+          } else {
+            uint8_t kb[24];
+            const uint32_t kl = unescape_key(s, sl, kb, 24);
+            if (d.depth == 1) d.k1 = kl == 0xFFFFFFFFu ? 0 : action_key(kb, kl);
+            else d.k2 = kl == 0xFFFFFFFFu ? FK_OTHER : file_key(kb, kl);
+          }
+        } else {
+          if (d.depth == 1) d.k1 = action_key(s, sl);
+          else d.k2 = file_key(s, sl);
+        }
+      }
+      d.state = S_COLON;
+    } else {
+      if (d.depth == 1) {
+        if (d.k1 == K_ADD || d.k1 == K_REMOVE) { d.status = ST_BAD; return; }  // struct from a string
+        if (d.k1) d.present |= 1u << d.k1;
+      } else if (d.depth == 2 && d.in_file) {
+        if (d.k2 == FK_PATH) {
+          d.cur.path_off = d.str_start;
+          d.cur.path_len = sl;
+          d.cur.flags = uint8_t((d.cur.flags & ~(F_PATH_NULL | F_PATH_ESCAPED)) | (has_bs ? F_PATH_ESCAPED : 0));
+        } else if (d.k2 == FK_SIZE || d.k2 == FK_DELTS) {
+          d.status = ST_BAD;  // LongType from a string token
+          return;
+        }
+      }
+      d.state = S_AFTER;
+    }
+    return;
+  }
+  if (cls == T_SCALAR) {
+    if (!(stt == S_VALUE || stt == S_ARR_FIRST)) { d.status = ST_BAD; return; }
+    const uint32_t L = tok_aux(tok);
+    int64_t v = 0;
+    const uint8_t sc = scalar_class(p + off, L, &v);
+    if (sc == SC_BAD) { d.status = ST_BAD; return; }
+    d.sc_checked += L;
+    if (d.depth == 1) {
+      if (sc == SC_NULL) {
+        if (d.k1) d.present &= ~(1u << d.k1);
+        if (d.k1 == K_ADD) d.fadd = FileObj{0, 0, 0, 0, F_PATH_NULL};
+        if (d.k1 == K_REMOVE) d.frm = FileObj{0, 0, 0, 0, F_PATH_NULL};
+      } else {
+        if (d.k1 == K_ADD || d.k1 == K_REMOVE) { d.status = ST_BAD; return; }
+        if (d.k1) d.present |= 1u << d.k1;
+      }
+    } else if (d.depth == 2 && d.in_file) {
+      if (d.k2 == FK_PATH) {
+        if (sc != SC_NULL) { d.status = ST_BAD; return; }
+        d.cur.path_off = 0;
+        d.cur.path_len = 0;
+        d.cur.flags = uint8_t((d.cur.flags & ~F_PATH_ESCAPED) | F_PATH_NULL);
+      } else if (d.k2 == FK_SIZE) {
+        if (sc == SC_NULL) d.cur.size = 0;
+        else if (sc == SC_INT) d.cur.size = v;
+        else { d.status = ST_BAD; return; }
+      } else if (d.k2 == FK_DELTS) {
+        if (sc == SC_NULL) { d.cur.delts = 0; d.cur.flags &= ~F_HAS_DELTS; }
+        else if (sc == SC_INT) { d.cur.delts = v; d.cur.flags |= F_HAS_DELTS; }
+        else { d.status = ST_BAD; return; }
+      }
+    }
+    d.state = S_AFTER;
+    return;
+  }
+  if (cls == T_COLON) {
+    if (stt != S_COLON) { d.status = ST_BAD; return; }
+    d.state = S_VALUE;
+    return;
+  }
+  if (cls == T_COMMA) {
+    if (stt != S_AFTER || d.depth == 0) { d.status = ST_BAD; return; }
+    d.state = d.is_arr(d.depth) ? S_VALUE : S_KEY;
+    return;
+  }
+  if (cls == T_OBJ_OPEN || cls == T_ARR_OPEN) {
+    const bool arr = cls == T_ARR_OPEN;
+    if (!(stt == S_VALUE || stt == S_ARR_FIRST || (stt == S_START && !arr))) { d.status = ST_BAD; return; }
+    if (d.depth == 2 && d.in_file && d.k2 != FK_OTHER) { d.status = ST_BAD; return; }  // path/size/delts container
+    if (d.depth == 1 && (d.k1 == K_ADD || d.k1 == K_REMOVE)) {
+      if (arr) { d.status = ST_BAD; return; }
+      d.in_file = true;
+      d.k2 = FK_OTHER;
+      d.cur = FileObj{0, 0, 0, 0, F_PATH_NULL};
+    }
+    if (d.depth >= 62) {
+      if (!General) { d.status = ST_HARD; return; }
+      if (d.depth + 1 >= GEN_MAX_DEPTH) { d.status = ST_BAD; return; }
+    }
+    ++d.depth;
+    d.set_arr(d.depth, arr);
+    d.state = arr ? S_ARR_FIRST : S_OBJ_FIRST;
+    return;
+  }
+  // T_OBJ_CLOSE / T_ARR_CLOSE
+  {
+    const bool arr = cls == T_ARR_CLOSE;
+    if (d.depth == 0) { d.status = ST_BAD; return; }
+    const bool top_arr = d.is_arr(d.depth);
+    if (arr != top_arr || !(stt == S_AFTER || stt == (arr ? S_ARR_FIRST : S_OBJ_FIRST))) { d.status = ST_BAD; return; }
+    if (d.depth == 2) {  // the value of a top-level member closes
+      if (d.in_file) {
+        // field-wise selects (a struct copy to one of two destinations would go through scratch)
+        const bool ad = d.k1 == K_ADD;
+        d.fadd.path_off = ad ? d.cur.path_off : d.fadd.path_off;
+        d.fadd.path_len = ad ? d.cur.path_len : d.fadd.path_len;
+        d.fadd.size = ad ? d.cur.size : d.fadd.size;
+        d.fadd.delts = ad ? d.cur.delts : d.fadd.delts;
+        d.fadd.flags = ad ? d.cur.flags : d.fadd.flags;
+        d.frm.path_off = ad ? d.frm.path_off : d.cur.path_off;
+        d.frm.path_len = ad ? d.frm.path_len : d.cur.path_len;
+        d.frm.size = ad ? d.frm.size : d.cur.size;
+        d.frm.delts = ad ? d.frm.delts : d.cur.delts;
+        d.frm.flags = ad ? d.frm.flags : d.cur.flags;
+        d.in_file = false;
+      }
+      if (d.k1) d.present |= 1u << d.k1;
+    }
+    --d.depth;
+    d.state = d.depth == 0 ? S_DONE : S_AFTER;
+  }
+}
+
+template <bool General>
+JL_HD void dfa_finish(const Tokenizer& tz, const Dfa<General>& d, LineOut& out) {
+  out.kind = K_NONE;
+  out.flags = 0;
+  out.hard = 0;
+  out.path_off = 0;
+  out.path_len = 0;
+  out.size = 0;
+  out.delts = 0;
+  if (tz.status == ST_HARD || d.status == ST_HARD) { out.hard = 1; return; }
+  if (tz.status == ST_OK && d.status == ST_OK && d.state == S_START && tz.sc_bytes == 0) return;  // blank
+  if (tz.status != ST_OK || d.status != ST_OK || d.state != S_DONE || tz.sc_bytes != d.sc_checked) {
+    out.kind = K_ERROR;
+    return;
+  }
+  // unwrap priority add > remove > metaData > txn > protocol > cdc > commitInfo
+  const uint32_t pr = d.present;
+  out.kind = (pr & (1u << K_ADD)) ? K_ADD : (pr & (1u << K_REMOVE)) ? K_REMOVE
+           : (pr & (1u << K_METADATA)) ? K_METADATA : (pr & (1u << K_TXN)) ? K_TXN
+           : (pr & (1u << K_PROTOCOL)) ? K_PROTOCOL : (pr & (1u << K_CDC)) ? K_CDC
+           : (pr & (1u << K_COMMITINFO)) ? K_COMMITINFO : K_NONE;
+  if (out.kind == K_ADD || out.kind == K_REMOVE) {
+    const bool ad = out.kind == K_ADD;  // field-wise selects keep both records in registers
+    out.flags = ad ? d.fadd.flags : d.frm.flags;
+    out.path_off = ad ? d.fadd.path_off : d.frm.path_off;
+    out.path_len = ad ? d.fadd.path_len : d.frm.path_len;
+    out.size = ad ? d.fadd.size : d.frm.size;
+    out.delts = ad ? d.fadd.delts : d.frm.delts;
+  }
+}
+
+// Whole-line walk (phases interleaved per window): the host reference and the General kernel.
+template <bool General>
+JL_HD void parse_line_t(const uint8_t* p, uint32_t n, LineOut& out) {
+  Tokenizer tz;
+  Dfa<General> d;
+  if (n > TOK_MAX_LINE) {
+    if (!General) { out = LineOut{0, 0, 1, 0, 0, 0, 0}; return; }
+  }
+  const uintptr_t pa = reinterpret_cast<uintptr_t>(p);
+  const uint8_t* base = reinterpret_cast<const uint8_t*>(pa & ~uintptr_t(15));
+  const uint32_t o0 = uint32_t(pa & 15);
+  const uint32_t nwin = (o0 + n + 15) >> 4;
+  auto step = [&](uint32_t t) {
+    if (d.status == ST_OK) dfa_token<General>(p, t, d);
+  };
+  for (uint32_t j = 0; j < nwin && tz.status == ST_OK && d.status == ST_OK; ++j) {
+    uint32_t w[4];
+    load_window(base + 16u * j, w);
+    tokenize_window<General>(p, n, w, int32_t(16u * j) - int32_t(o0), tz, step);
+  }
+  tokenize_end(n, tz, step);
+  dfa_finish<General>(tz, d, out);
+}
+
+JL_HD void parse_line(const uint8_t* p, uint32_t n, LineOut& out) { parse_line_t<false>(p, n, out); }
+JL_HD void parse_line_general(const uint8_t* p, uint32_t n, LineOut& out) { parse_line_t<true>(p, n, out); }
+
+}  // namespace jl
+}  // namespace dr

@@ -3,12 +3,13 @@
 //
 // Stage 1 (k_json_count / k_json_newlines): a structural index of the newline bytes, built from
 // 16-byte vector loads; a raw '\n' can never sit inside a JSON string, so every newline is a line
-// boundary. Stage 2 (k_json_parse): one lane per line walks the line once through a 16-byte
-// register window, classifies the SingleAction envelope with unwrap priority
-// (D/actions/actions.scala:523-541), pulls add/remove path/size/deletionTimestamp and hashes the
-// path (K3's xxh64) while its bytes are still in cache.
+// boundary. Stage 2 (k_json_lines): one lane per line walks the line in 16-byte SWAR windows
+// (json_lane.h: bit-parallel quote/escape masks, token DFA), classifies the SingleAction envelope
+// with unwrap priority (D/actions/actions.scala:523-541), pulls add/remove path / size /
+// deletionTimestamp and hashes the path (K3's xxh64) while its bytes are in cache.
 #include "dev_common.h"
 #include "kernels.h"
+#include "json_lane.h"
 
 namespace dr {
 namespace dev {
@@ -99,281 +100,127 @@ __global__ void __launch_bounds__(JSON_THREADS) k_json_newlines(const uint8_t* _
   }
 }
 
-// ---- per-line JSON scanner ----------------------------------------------------------------------
-struct Scan {
-  const uint8_t* p;
-  const uint8_t* end;
-  const uint8_t* wbase;
-  uint4 w;
-  bool bad;
+// ---- per-line parse (json_lane.h walker) --------------------------------------------------------
+constexpr int JL_T = 64;             // one wave: one lane per line
 
-  __device__ __forceinline__ uint8_t at(const uint8_t* q) {
-    const uint8_t* a = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(q) & ~uintptr_t(15));
-    if (a != wbase) {
-      wbase = a;
-      w = *reinterpret_cast<const uint4*>(a);
-    }
-    const uint32_t off = uint32_t(q - a);
-    const uint32_t word = off < 8 ? (off < 4 ? w.x : w.y) : (off < 12 ? w.z : w.w);
-    return uint8_t(word >> ((off & 3) * 8));
-  }
-  __device__ __forceinline__ uint8_t peek() { return p < end ? at(p) : 0; }
-  __device__ __forceinline__ void ws() {
-    while (p < end) {
-      uint8_t c = at(p);
-      if (c != ' ' && c != '\t' && c != '\r' && c != '\n') break;
-      ++p;
-    }
-  }
-  __device__ __forceinline__ bool expect(uint8_t c) {
-    ws();
-    if (p < end && at(p) == c) { ++p; return true; }
-    bad = true;
-    return false;
-  }
-  // At an opening quote: returns the content span, sets *esc if it holds a backslash escape.
-  __device__ bool string(const uint8_t** s, uint32_t* n, bool* esc) {
-    ws();
-    if (p >= end || at(p) != '"') { bad = true; return false; }
-    ++p;
-    const uint8_t* b = p;
-    bool e = false;
-    while (p < end) {
-      uint8_t c = at(p);
-      if (c == '"') {
-        *s = b; *n = uint32_t(p - b); *esc = e; ++p;
-        return true;
-      }
-      if (c == '\\') { e = true; p += 2; continue; }
-      ++p;
-    }
-    bad = true;
-    return false;
-  }
-  __device__ bool literal(const char* lit, int n) {
-    for (int i = 0; i < n; ++i) {
-      if (p + i >= end || at(p + i) != uint8_t(lit[i])) { bad = true; return false; }
-    }
-    p += n;
-    return true;
-  }
-  // Skips any JSON value (object/array via a bracket depth counter that honours strings).
-  __device__ void skip_value() {
-    ws();
-    if (p >= end) { bad = true; return; }
-    uint8_t c = at(p);
-    if (c == '"') { const uint8_t* s; uint32_t n; bool e; string(&s, &n, &e); return; }
-    if (c == '{' || c == '[') {
-      int depth = 0;
-      while (p < end) {
-        c = at(p);
-        if (c == '"') { const uint8_t* s; uint32_t n; bool e; string(&s, &n, &e); if (bad) return; continue; }
-        if (c == '{' || c == '[') ++depth;
-        else if (c == '}' || c == ']') { if (--depth == 0) { ++p; return; } }
-        ++p;
-      }
-      bad = true;
-      return;
-    }
-    if (c == 't') { literal("true", 4); return; }
-    if (c == 'f') { literal("false", 5); return; }
-    if (c == 'n') { literal("null", 4); return; }
-    // number
-    const uint8_t* b = p;
-    while (p < end) {
-      c = at(p);
-      if ((c >= '0' && c <= '9') || c == '-' || c == '+' || c == '.' || c == 'e' || c == 'E') ++p;
-      else break;
-    }
-    if (p == b) bad = true;
-  }
-  __device__ __forceinline__ bool is_null() {
-    ws();
-    if (p + 4 <= end && at(p) == 'n') return literal("null", 4);
-    return false;
-  }
-  // Integral JSON number -> int64 (Spark's LongType accepts VALUE_NUMBER_INT only).
-  __device__ bool int64v(int64_t* out) {
-    ws();
-    bool neg = false;
-    if (p < end && at(p) == '-') { neg = true; ++p; }
-    uint64_t v = 0;
-    const uint8_t* b = p;
-    while (p < end) {
-      uint8_t c = at(p);
-      if (c < '0' || c > '9') break;
-      v = v * 10 + (c - '0');
-      ++p;
-    }
-    if (p == b || p - b > 19) { bad = true; return false; }
-    uint8_t c = peek();
-    if (c == '.' || c == 'e' || c == 'E') { bad = true; return false; }
-    *out = neg ? -int64_t(v) : int64_t(v);
-    return true;
-  }
-  __device__ bool key_is(const uint8_t* s, uint32_t n, const char* k, uint32_t kn) {
-    if (n != kn) return false;
-    for (uint32_t i = 0; i < n; ++i)
-      if (at(s + i) != uint8_t(k[i])) return false;
-    return true;
-  }
-};
-
-struct FileFields {
-  const uint8_t* path;
-  uint32_t path_len;
-  bool path_esc, path_null, has_delts;
-  int64_t size, delts;
-};
-
-// Parses the inner object of an add/remove (AddFile / RemoveFile field names,
-// D/actions/actions.scala:220-320); unknown fields are skipped (FAIL_ON_UNKNOWN_PROPERTIES=false).
-__device__ bool parse_file_object(Scan& s, FileFields& f) {
-  f.path = nullptr; f.path_len = 0; f.path_esc = false; f.path_null = true; f.has_delts = false;
-  f.size = 0; f.delts = 0;
-  if (!s.expect('{')) return false;
-  s.ws();
-  if (s.peek() == '}') { ++s.p; return true; }
-  for (;;) {
-    const uint8_t* k; uint32_t kn; bool ke;
-    if (!s.string(&k, &kn, &ke)) return false;
-    if (!s.expect(':')) return false;
-    if (s.key_is(k, kn, "path", 4)) {
-      if (!s.is_null()) {
-        if (s.bad) return false;
-        bool e;
-        if (!s.string(&f.path, &f.path_len, &e)) return false;
-        f.path_esc = e;
-        f.path_null = false;
-      } else {
-        f.path_null = true;
-      }
-    } else if (s.key_is(k, kn, "size", 4)) {
-      if (!s.is_null()) { if (s.bad || !s.int64v(&f.size)) return false; } else { f.size = 0; }
-    } else if (s.key_is(k, kn, "deletionTimestamp", 17)) {
-      if (!s.is_null()) {
-        if (s.bad || !s.int64v(&f.delts)) return false;
-        f.has_delts = true;
-      } else {
-        f.has_delts = false;
-      }
-    } else {
-      s.skip_value();
-      if (s.bad) return false;
-    }
-    s.ws();
-    uint8_t c = s.peek();
-    if (c == ',') { ++s.p; continue; }
-    if (c == '}') { ++s.p; return true; }
-    s.bad = true;
-    return false;
-  }
-}
-
-__global__ void __launch_bounds__(256) k_json_parse(JsonParseArgs a) {
-  const uint64_t line = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (line >= a.nlines) return;
-  const uint64_t b = line == 0 ? 0 : a.nl[line - 1] + 1;
-  const uint64_t e = a.nl[line];
+// Writes line `line`'s action arrays from the walker's result; `lp` is where its bytes were read
+// (`gp`: its global address).
+__device__ __forceinline__ void emit_line(const JsonParseArgs& a, uint64_t line, uint64_t b, uint32_t n,
+                                          const uint8_t* lp, const uint8_t* gp, const jl::LineOut& o) {
   const uint64_t idx = a.base + line;
-  Scan s{a.buf + b, a.buf + e, nullptr, make_uint4(0, 0, 0, 0), false};
-  uint8_t kind = K_NONE, flags = 0;
-  FileFields add, rm;
-  bool has_add = false, has_rm = false, has_meta = false, has_txn = false, has_prot = false, has_cdc = false,
-       has_ci = false;
-  s.ws();
-  if (s.p < s.end) {
-    if (s.expect('{')) {
-      s.ws();
-      if (s.peek() == '}') {
-        ++s.p;
-      } else {
-        for (;;) {
-          const uint8_t* k; uint32_t kn; bool ke;
-          if (!s.string(&k, &kn, &ke) || !s.expect(':')) break;
-          if (s.is_null()) {
-            // a null member is an absent member
-          } else if (s.bad) {
-            break;
-          } else if (s.key_is(k, kn, "add", 3)) {
-            if (!parse_file_object(s, add)) break;
-            has_add = true;
-          } else if (s.key_is(k, kn, "remove", 6)) {
-            if (!parse_file_object(s, rm)) break;
-            has_rm = true;
-          } else {
-            if (s.key_is(k, kn, "metaData", 8)) has_meta = true;
-            else if (s.key_is(k, kn, "txn", 3)) has_txn = true;
-            else if (s.key_is(k, kn, "protocol", 8)) has_prot = true;
-            else if (s.key_is(k, kn, "cdc", 3)) has_cdc = true;
-            else if (s.key_is(k, kn, "commitInfo", 10)) has_ci = true;
-            s.skip_value();
-            if (s.bad) break;
-          }
-          s.ws();
-          uint8_t c = s.peek();
-          if (c == ',') { ++s.p; continue; }
-          if (c == '}') { ++s.p; break; }
-          s.bad = true;
-          break;
-        }
-      }
-      s.ws();
-      if (s.p != s.end) s.bad = true;
-    }
-    if (s.bad) {
-      kind = K_ERROR;  // Spark PERMISSIVE: a malformed record becomes an all-null row (ignored)
-    } else if (has_add) {
-      kind = K_ADD;
-    } else if (has_rm) {
-      kind = K_REMOVE;
-    } else if (has_meta) {
-      kind = K_METADATA;
-    } else if (has_txn) {
-      kind = K_TXN;
-    } else if (has_prot) {
-      kind = K_PROTOCOL;
-    } else if (has_cdc) {
-      kind = K_CDC;
-    } else if (has_ci) {
-      kind = K_COMMITINFO;
-    }
-  }
-  uint64_t key = 0;
-  const uint8_t* path = nullptr;
+  uint8_t flags = 0;
+  uint64_t key = 0, path = 0;
   uint32_t plen = 0;
   int64_t size = 0, delts = 0;
+  const uint8_t kind = o.kind;
   if (kind == K_ADD || kind == K_REMOVE) {
-    const FileFields& f = kind == K_ADD ? add : rm;
-    path = f.path;
-    plen = f.path_len;
-    size = f.size;
-    delts = f.delts;
-    if (f.has_delts) flags |= F_HAS_DELTS;
-    if (f.path_null) flags |= F_PATH_NULL;
-    if (f.path_esc) flags |= F_PATH_ESCAPED;
-    if (f.path_esc || path_is_special(path, plen)) {
-      flags |= F_SPECIAL_PATH;
-      atomicAdd(reinterpret_cast<unsigned long long*>(a.special_count), 1ull);
-      atomicAdd(reinterpret_cast<unsigned long long*>(a.special_bytes), (unsigned long long)(plen + 8));
-    } else if (!f.path_null) {
-      key = path_key(path, plen);
+    flags = o.flags;  // F_HAS_DELTS / F_PATH_ESCAPED / F_PATH_NULL share dev_common.h's values
+    path = reinterpret_cast<uint64_t>(gp + o.path_off);
+    plen = o.path_len;
+    size = o.size;
+    delts = o.delts;
+    if (!(flags & F_PATH_NULL)) {
+      if ((flags & F_PATH_ESCAPED) || path_is_special(lp + o.path_off, plen)) {
+        flags |= F_SPECIAL_PATH;
+        atomicAdd(reinterpret_cast<unsigned long long*>(a.special_count), 1ull);
+        atomicAdd(reinterpret_cast<unsigned long long*>(a.special_bytes), (unsigned long long)(plen + 8));
+      } else {
+        key = path_key(lp + o.path_off, plen);
+      }
+    } else {
+      path = 0;
+      plen = 0;
     }
-  } else if (kind != K_NONE && kind != K_ERROR && kind != K_COMMITINFO && kind != K_CDC) {
+  } else if (kind == K_METADATA || kind == K_TXN || kind == K_PROTOCOL) {
     // protocol / metaData / txn: reduced on the host (the reference's single `null` partition)
     const unsigned long long slot = atomicAdd(reinterpret_cast<unsigned long long*>(a.nonfile_count), 1ull);
     if (slot < a.nonfile_cap) a.nonfile_idx[slot] = line;
+  } else if (kind == K_ERROR) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.error_count), 1ull);
   }
-  if (kind == K_ERROR) atomicAdd(reinterpret_cast<unsigned long long*>(a.error_count), 1ull);
   a.kind[idx] = kind;
   a.flags[idx] = flags;
   a.key[idx] = key;
-  a.path_ptr[idx] = reinterpret_cast<uint64_t>(path);
+  a.path_ptr[idx] = path;
   a.path_len[idx] = plen;
   a.size[idx] = size;
   a.delts[idx] = delts;
   a.src_off[idx] = b;
-  a.src_len[idx] = uint32_t(e - b);
+  a.src_len[idx] = n;
+}
+
+// 64 consecutive lines per block, one lane per line, two phases (json_lane.h):
+//  1. each lane tokenizes its line window by window (16-byte global loads, SWAR masks) into its
+//     column of an LDS token buffer;
+//  2. the DFA consumes the buffer BY TOKEN INDEX: lines of one commit share their shape (all adds,
+//     or all removes), so the 64 lanes take the same grammar branch at the same step instead of
+//     diverging byte by byte.
+// The buffer is flushed through phase 2 whenever a lane could overflow it, and at the end.
+constexpr int JL_TOKCAP = 80;
+constexpr int JL_FLUSH = JL_TOKCAP - 16;  // a window adds at most 16 tokens
+
+__global__ void __launch_bounds__(JL_T) k_json_lines(JsonParseArgs a) {
+  __shared__ uint32_t tokbuf[JL_TOKCAP * JL_T];
+  const uint32_t lane = threadIdx.x;
+  const uint64_t line = uint64_t(blockIdx.x) * JL_T + lane;
+  const bool live = line < a.nlines;
+  const uint64_t b = !live ? 0 : line == 0 ? 0 : a.nl[line - 1] + 1;
+  const uint32_t n = live ? uint32_t(a.nl[line] - b) : 0;
+  const uint8_t* p = a.buf + b;
+  jl::Tokenizer tz;
+  jl::Dfa<false> d;
+  if (!live) tz.status = jl::ST_BAD;
+  else if (n > jl::TOK_MAX_LINE) tz.status = jl::ST_HARD;
+  const uint32_t o0 = uint32_t(b & 15);
+  const uint8_t* base = p - o0;
+  const uint32_t nwin = tz.status == jl::ST_OK ? (o0 + n + 15) >> 4 : 0;
+  uint32_t nt = 0;
+  auto push = [&](uint32_t t) {
+    tokbuf[nt * JL_T + lane] = t;
+    ++nt;
+  };
+  for (uint32_t j = 0;; ++j) {
+    if (j < nwin && tz.status == jl::ST_OK) {
+      uint32_t w[4];
+      jl::load_window(base + 16u * j, w);
+      jl::tokenize_window<false>(p, n, w, int32_t(16u * j) - int32_t(o0), tz, push);
+      if (j + 1 == nwin) jl::tokenize_end(n, tz, push);
+    }
+    const bool more = j + 1 < nwin && tz.status == jl::ST_OK;
+    const bool anymore = __ballot(more) != 0ull;
+    if (!anymore || __ballot(nt > uint32_t(JL_FLUSH)) != 0ull) {
+      uint32_t mx = nt;
+      for (int o = 32; o > 0; o >>= 1) mx = max(mx, uint32_t(__shfl_xor(int(mx), o, 64)));
+      for (uint32_t t = 0; t < mx; ++t)
+        if (t < nt && d.status == jl::ST_OK) jl::dfa_token<false>(p, tokbuf[t * JL_T + lane], d);
+      nt = 0;
+    }
+    if (!anymore) break;
+  }
+  if (!live) return;
+  jl::LineOut o;
+  jl::dfa_finish<false>(tz, d, o);
+  if (o.hard) {
+    const unsigned long long k = atomicAdd(a.hard_count, 1ull);
+    a.hard_idx[k] = line;
+    return;
+  }
+  emit_line(a, line, b, n, p, p, o);
+}
+
+// The General walker over the deferred lines (tab / CR whitespace, escaped member names, deep
+// nesting): grid-stride over a device-side count.
+__global__ void __launch_bounds__(64) k_json_hard(JsonParseArgs a) {
+  const uint64_t cnt = *a.hard_count;
+  for (uint64_t k = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; k < cnt; k += uint64_t(gridDim.x) * blockDim.x) {
+    const uint64_t line = a.hard_idx[k];
+    const uint64_t b = line == 0 ? 0 : a.nl[line - 1] + 1;
+    const uint32_t n = uint32_t(a.nl[line] - b);
+    const uint8_t* gp = a.buf + b;
+    jl::LineOut o;
+    jl::parse_line_general(gp, n, o);
+    emit_line(a, line, b, n, gp, gp, o);
+  }
 }
 
 }  // namespace dev
@@ -393,7 +240,13 @@ void launch_json_newlines(const uint8_t* buf, uint64_t len, const uint64_t* bloc
 
 void launch_json_parse(const JsonParseArgs& a, hipStream_t st) {
   if (!a.nlines) return;
-  hipLaunchKernelGGL(dev::k_json_parse, dim3(unsigned((a.nlines + 255) / 256)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(dev::k_json_lines, dim3(unsigned((a.nlines + dev::JL_T - 1) / dev::JL_T)), dim3(dev::JL_T), 0,
+                     st, a);
+}
+
+void launch_json_hard(const JsonParseArgs& a, hipStream_t st) {
+  if (!a.nlines) return;
+  hipLaunchKernelGGL(dev::k_json_hard, dim3(256), dim3(64), 0, st, a);
 }
 
 }  // namespace dr

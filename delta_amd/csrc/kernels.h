@@ -39,13 +39,18 @@ struct JsonParseArgs {
   uint64_t* nonfile_idx;
   uint64_t nonfile_cap;
   uint64_t* error_count;
+  uint64_t* hard_idx;             // lines the fast walker defers to the General walker
+  unsigned long long* hard_count;
 };
 
 uint64_t json_num_blocks(uint64_t len);
 void launch_json_count(const uint8_t* buf, uint64_t len, uint32_t* block_counts, hipStream_t st);
 void launch_json_newlines(const uint8_t* buf, uint64_t len, const uint64_t* block_off, uint64_t* nl,
                           hipStream_t st);
+// fast walker over every line (LDS-staged, lane per line), then the General walker over the
+// deferred lines (device-side count)
 void launch_json_parse(const JsonParseArgs& a, hipStream_t st);
+void launch_json_hard(const JsonParseArgs& a, hipStream_t st);
 
 // ---- scans ------------------------------------------------------------------------------------
 // Exclusive scan of n u32 counts into u64 offsets; out[n] = total. Scratch: scan_scratch_bytes(n).

@@ -1,0 +1,32 @@
+"""Profiling driver: stages a synthetic config once and runs a few replays (for rocprofv3)."""
+import argparse
+import os
+import sys
+import tempfile
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--scale", type=float, default=0.25)
+    ap.add_argument("--reps", type=int, default=2)
+    args = ap.parse_args()
+    from delta_amd.delta_log import Engine
+    from delta_amd.testing import synth as S
+    d = os.path.join(tempfile.gettempdir(), "dr_prof_c%d_%g" % (args.config, args.scale))
+    if not os.path.exists(os.path.join(d, "_delta_log")):
+        S.build_config(args.config, d, scale=args.scale, keep_ids=False)
+    exp = S.build_config.__module__ and None
+    eng = Engine.get(0)
+    staged = eng.stage_log(os.path.join(d, "_delta_log"))
+    for _ in range(args.reps):
+        st = staged.replay(0)
+        print(st.counts["num_files"], st.counts["num_actions"], flush=True)
+        st.release()
+    staged.release()
+
+
+if __name__ == "__main__":
+    main()

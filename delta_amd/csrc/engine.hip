@@ -10,6 +10,8 @@
 #include <functional>
 #include <type_traits>
 #include <cstring>
+#include <cstdlib>
+#include <cstdio>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -192,8 +194,11 @@ struct PagePlan {
   DBuf<SnapPage> d_snap;
   DBuf<uint32_t> d_chunk_base, d_block_page;
   DBuf<CopyJob> d_copy;
-  DBuf<uint32_t> s_spec_exit, s_vis, s_entry, s_chunk_out, s_chunk_out_start, s_chunk_copies, s_pages_bad;
+  DBuf<uint32_t> s_spec_exit, s_vis, s_entry, s_assumed, s_region, s_chunk_out, s_chunk_out_start,
+      s_chunk_copies, s_pages_bad;
   DBuf<uint64_t> s_rec_start, s_recs;
+  DBuf<uint8_t> s_chunk_flag;
+  DBuf<unsigned long long> s_region_count;
   std::vector<uint32_t> wg_chunk0;
   DBuf<uint32_t> d_wg_chunk0;
   uint64_t snap_in_bytes = 0;
@@ -543,11 +548,15 @@ static void plan_pages(StagedData& s, PagePlan& P) {
   P.s_spec_exit = DBuf<uint32_t>(s.ctx, P.nchunks);
   P.s_vis = DBuf<uint32_t>(s.ctx, uint64_t(P.nchunks) * 8);
   P.s_entry = DBuf<uint32_t>(s.ctx, P.nchunks);
+  P.s_assumed = DBuf<uint32_t>(s.ctx, P.nchunks);
+  P.s_region = DBuf<uint32_t>(s.ctx, P.nchunks);
+  P.s_chunk_flag = DBuf<uint8_t>(s.ctx, P.nchunks);
+  P.s_region_count = DBuf<unsigned long long>(s.ctx, 1);
   P.s_chunk_out = DBuf<uint32_t>(s.ctx, P.nchunks);
   P.s_chunk_out_start = DBuf<uint32_t>(s.ctx, P.nchunks);
   P.s_chunk_copies = DBuf<uint32_t>(s.ctx, P.nchunks);
   P.s_rec_start = DBuf<uint64_t>(s.ctx, uint64_t(P.nchunks) + 1);
-  P.s_recs = DBuf<uint64_t>(s.ctx, P.snap_in_bytes / 2 + 1);  // a copy element takes >= 2 input bytes
+  P.s_recs = DBuf<uint64_t>(s.ctx, P.snap_in_bytes / 2 + 1);  // an element takes >= 2 input bytes
   P.s_pages_bad = DBuf<uint32_t>(s.ctx, P.snap_pages.size());
   P.s_ba_vals = DBuf<uint32_t>(s.ctx, P.ba_vals);
   P.s_ba_hit = DBuf<uint32_t>(s.ctx, P.ba_hits);
@@ -578,11 +587,21 @@ static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_
   launch_page_copy(P.d_copy.p, uint32_t(P.copy_jobs.size()), stream);
   if (!P.snap_pages.empty()) {
     P.s_pages_bad.zero(stream);
+    P.s_chunk_flag.zero(stream);
+    P.s_region_count.zero(stream);
     SnappyArgs sa{P.d_snap.p, uint32_t(P.snap_pages.size()), P.d_chunk_base.p, P.nchunks, P.s_spec_exit.p,
-                  P.s_vis.p, P.s_entry.p, P.s_chunk_out.p, P.s_chunk_out_start.p, P.s_chunk_copies.p,
+                  P.s_vis.p, P.s_entry.p, P.s_assumed.p, P.s_chunk_flag.p, P.s_region.p, P.s_region_count.p, P.s_chunk_out.p, P.s_chunk_out_start.p, P.s_chunk_copies.p,
                   P.s_rec_start.p, P.s_recs.p, P.d_block_page.p, uint32_t(P.block_page.size()),
                   P.d_wg_chunk0.p, uint32_t(P.wg_chunk0.size()), P.s_pages_bad.p, err.p};
     launch_snappy(sa, stream, scratch);
+    if (std::getenv("DR_SNAP_DEBUG")) {
+      const unsigned long long nreg = d2h_one(P.s_region_count.p, stream);
+      std::vector<uint32_t> pb = d2h(P.s_pages_bad.p, P.snap_pages.size(), stream);
+      size_t nb = 0;
+      for (uint32_t v : pb) nb += v != 0;
+      const size_t nr = size_t(nreg);
+      std::fprintf(stderr, "snappy: pages %zu serially resolved regions %zu bad %zu\n", P.snap_pages.size(), nr, nb);
+    }
   }
   ctx->mark("pq_inflate");
   if (P.ba_pages) launch_ba_bounds(pa, stream);

@@ -7,19 +7,23 @@
 //  A k_snap_spec    one lane per 256-byte chunk of compressed input parses elements
 //                   *speculatively* (starting 64 bytes early as a warm-up) and records the
 //                   positions it visited in the chunk (256-bit bitmap) and where it left it.
-//  B k_snap_resolve one wave per page checks 64 chunks at a time with a ballot: a chunk whose
-//                   true entry (the previous chunk's exit) is on its speculative chain is correct
-//                   (chains that meet coincide from then on). Only breaks -- a mis-speculated
-//                   chunk or one spanned by a long literal -- are walked serially.
+//  B k_snap_assume / k_snap_entries: every chunk's true entry, in parallel: a chunk whose true
+//                   entry (the previous chunk's exit) is on its speculative chain is correct
+//                   (chains that meet coincide from then on); an isolated mis-speculated chunk is
+//                   walked from its true entry. Runs of mis-speculation and chunks spanned by long
+//                   literals send the page to k_snap_resolve from its first such chunk (one wave
+//                   per page, 64 chunks per ballot, spanned chunks skipped in one step).
 //  C k_snap_count   per chunk: output bytes and copy elements of its true elements.
 //  D k_snap_scan    per page: exclusive scan of chunk outputs (copy counts: a global scan).
-//  E k_snap_emit    per chunk: literal bytes go straight to the output, copies become 8-byte
-//                   records {out, len, offset}. The compressor compresses 64 KiB fragments
-//                   independently, so no element straddles a fragment and no copy reaches before
-//                   its fragment; violations flag the page for k_snap_serial.
+//  E k_snap_emit    per chunk: every element becomes an 8-byte record {chunk-relative output
+//                   offset, length, copy offset | literal input position}, staged in LDS and
+//                   written coalesced. The compressor compresses 64 KiB fragments independently,
+//                   so no element straddles a fragment and no copy reaches before its fragment;
+//                   violations flag the page for k_snap_serial.
 //  F k_snap_exec    one 1024-thread workgroup per 64 KiB output block resolves every copied
 //                   byte to its literal origin by pointer jumping on a u16 map in LDS
-//                   (src[p] = p - offset; literal bytes are their own roots) and gathers it.
+//                   (src[p] = p - offset; literal bytes are their own roots), then rebuilds the
+//                   block's bytes in the same LDS and stores them with 16-byte stores.
 //
 // Chunk walkers (A, C, E) stage their page bytes into LDS with coalesced loads and parse from LDS.
 #include "dev_common.h"
@@ -32,7 +36,7 @@ constexpr uint32_t SNAP_CH = 256;            // compressed bytes per speculation
 constexpr uint32_t SNAP_BLOCK = 65536;       // snappy compressor fragment size
 constexpr uint32_t SNAP_WU = 256;            // speculation warm-up bytes (0.6% mis-speculation on path pages)
 constexpr uint32_t WG_CHUNKS = 256;          // chunks (threads) per chunk-walker workgroup
-constexpr uint32_t STAGE_BYTES = WG_CHUNKS * SNAP_CH + SNAP_WU + 64;
+constexpr uint32_t STAGE_BYTES = (WG_CHUNKS * SNAP_CH + SNAP_WU + 64) * 65 / 64 + 16;  // + skew
 
 struct Elem {
   uint32_t hdr;   // header bytes (tag + length/offset bytes)
@@ -77,10 +81,13 @@ __device__ __forceinline__ uint32_t chunk_page(const uint32_t* chunk_base, uint3
 // Bytes of the page input from (chunk j0 start - warm-up) to (chunk j0+cnt end + 16) are copied
 // into `buf` with coalesced dword loads; `lo` is the page offset of buf[0] (dword aligned in
 // absolute address, so it may sit up to 3 bytes before the page input).
+// The staged copy is skewed by one dword per 256 bytes: lane l walks chunk l, 256 bytes after lane
+// l-1, so unskewed every lane at the same relative offset would hit the same LDS bank.
 struct Staged {
   int64_t lo;
   uint64_t hi;
 };
+__device__ __forceinline__ uint32_t skew(uint32_t dw) { return dw + (dw >> 6); }
 
 __device__ Staged stage_input(uint8_t* buf, const uint8_t* in, uint64_t n_in, uint32_t j0, uint32_t cnt) {
   uint64_t lo = uint64_t(j0) * SNAP_CH;
@@ -91,7 +98,7 @@ __device__ Staged stage_input(uint8_t* buf, const uint8_t* in, uint64_t n_in, ui
   const uint32_t nd = uint32_t((int64_t(hi) - lo_al + 3) / 4) + 2;
   uint32_t* b32 = reinterpret_cast<uint32_t*>(buf);
   const uint32_t* g32 = reinterpret_cast<const uint32_t*>(a0);
-  for (uint32_t i = threadIdx.x; i < nd; i += blockDim.x) b32[i] = g32[i];
+  for (uint32_t i = threadIdx.x; i < nd; i += blockDim.x) b32[skew(i)] = g32[i];
   __syncthreads();
   return Staged{lo_al, hi};
 }
@@ -101,7 +108,7 @@ __device__ __forceinline__ uint64_t staged_u64(const uint8_t* buf, const Staged&
   const uint32_t r = uint32_t(int64_t(pos) - s.lo);
   const uint32_t* b32 = reinterpret_cast<const uint32_t*>(buf);
   const uint32_t di = r >> 2, sh = r & 3;
-  const uint32_t w0 = b32[di], w1 = b32[di + 1], w2 = b32[di + 2];
+  const uint32_t w0 = b32[skew(di)], w1 = b32[skew(di + 1)], w2 = b32[skew(di + 2)];
   return uint64_t(__builtin_amdgcn_alignbyte(w1, w0, sh)) | (uint64_t(__builtin_amdgcn_alignbyte(w2, w1, sh)) << 32);
 }
 
@@ -146,43 +153,152 @@ __global__ void __launch_bounds__(WG_CHUNKS) k_snap_spec(SnappyArgs a) {
   for (int k = 0; k < int(SNAP_CH / 32); ++k) a.vis[uint64_t(c) * (SNAP_CH / 32) + k] = vis[k];
 }
 
-// B: true chunk entries, 64 chunks per ballot.
-__global__ void __launch_bounds__(64) k_snap_resolve(SnappyArgs a) {
-  const uint32_t p = blockIdx.x;
-  if (p >= a.npages) return;
+// Walks chunk j of a page from `e` (a true element start) to its exit; 8-byte headers from global.
+__device__ __forceinline__ uint64_t walk_chunk(const uint8_t* in, uint64_t e, uint64_t ce) {
+  while (e < ce) e += snap_adv(snap_elem(in + e));
+  return e;
+}
+
+// B1: every chunk's exit x[c] assuming its entry is the previous chunk's speculative exit
+// a = spec_exit[c-1] (chunk 0: entry 0, exact): a at or past the chunk end -> a; a on the chunk's
+// speculative chain (visited bitmap) -> spec_exit[c] (chains that meet coincide); otherwise a
+// serial walk of the chunk from a.
+__global__ void __launch_bounds__(256) k_snap_assume(SnappyArgs a) {
+  const uint32_t c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= a.nchunks) return;
+  const uint32_t p = chunk_page(a.chunk_base, a.npages, c);
   const SnapPage& pg = a.pages[p];
-  const uint8_t* in = reinterpret_cast<const uint8_t*>(pg.in);
-  const uint32_t c0 = a.chunk_base[p], nc = a.chunk_base[p + 1] - c0;
-  const int lane = threadIdx.x;
-  uint64_t e = 0;  // true entry of chunk `base`
-  uint32_t base = 0;
-  while (base < nc) {
-    const uint32_t j = base + lane;
-    const bool valid = j < nc;
-    uint32_t x = 0, word = 0;
-    const uint64_t cs = uint64_t(j) * SNAP_CH;
-    const uint64_t ce = min(cs + SNAP_CH, uint64_t(pg.n_in));
-    if (valid) x = a.spec_exit[c0 + j];
-    uint64_t cand = __shfl_up(uint64_t(x), 1, 64);
-    if (lane == 0) cand = e;
-    const bool skip = cand >= ce;
-    if (valid && !skip) word = a.vis[uint64_t(c0 + j) * (SNAP_CH / 32) + uint32_t((cand - cs) >> 5)];
-    const bool ok = valid && !skip && ((word >> ((cand - cs) & 31)) & 1u);
-    const unsigned long long brk = __ballot(valid && !ok);
-    const uint32_t f = brk ? uint32_t(__builtin_ctzll(brk)) : 64u;  // first chunk needing care
-    if (valid && uint32_t(lane) <= f) a.entry[c0 + j] = uint32_t(min(cand, uint64_t(0xffffffffu)));
-    const uint32_t cnt = min(64u, nc - base);
-    if (f >= cnt) {
-      e = uint32_t(__builtin_amdgcn_readlane(int(x), int(cnt - 1)));
-      base += cnt;
-      continue;
+  const uint32_t j = c - a.chunk_base[p];
+  const uint64_t cs = uint64_t(j) * SNAP_CH;
+  const uint64_t ce = min(cs + SNAP_CH, uint64_t(pg.n_in));
+  const uint64_t e = j == 0 ? 0 : a.spec_exit[c - 1];
+  uint64_t x;
+  if (e >= ce) x = e;
+  else if (j == 0 || ((a.vis[uint64_t(c) * (SNAP_CH / 32) + uint32_t((e - cs) >> 5)] >> ((e - cs) & 31)) & 1u))
+    x = a.spec_exit[c];
+  else x = walk_chunk(reinterpret_cast<const uint8_t*>(pg.in), e, ce);
+  a.assumed_exit[c] = uint32_t(min(x, uint64_t(0xffffffffu)));
+}
+
+// B2: true entries E[c] = T[c-1] (the true exit of chunk c-1). Chunk k "breaks" when its exit
+// under the assumed entry differs from its speculative exit. A genuine break (the assumed entry was
+// true) is always followed by an artefact break of the next chunk (its assumed entry, the broken
+// chunk's speculative exit, is wrong) unless that chunk happens to agree; so along a run of
+// consecutive breaks, breaks at even distance from the run's start are genuine, provided each chunk
+// after a genuine break re-synchronises with its speculative chain (checked here). Then:
+//   c-2 not genuine -> E[c] = assumed_exit[c-1];
+//   c-2 genuine     -> chunk c-1 starts at assumed_exit[c-2] and must re-synchronise:
+//                      E[c] = spec_exit[c-1].
+// A failed re-synchronisation (or a chunk spanned right after a break) records the page's first
+// such chunk; the serial resolver recomputes the page's entries from there.
+__device__ __forceinline__ bool broke(const SnappyArgs& a, uint32_t c) { return a.assumed_exit[c] != a.spec_exit[c]; }
+
+constexpr uint32_t MAX_RUN = 32;
+__global__ void __launch_bounds__(256) k_snap_entries(SnappyArgs a) {
+  const uint32_t c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= a.nchunks) return;
+  const uint32_t p = chunk_page(a.chunk_base, a.npages, c);
+  const uint32_t j = c - a.chunk_base[p];
+  if (j == 0) { a.entry[c] = 0; return; }
+  const uint32_t b = c - 1;  // page-relative j-1
+  bool genuine = false;
+  if (j >= 2 && broke(a, b - 1)) {
+    // length of the run of breaks ending at c-2 (page-relative chunk 0 never breaks)
+    uint32_t r = 0;
+    while (r < MAX_RUN && j - 2 > r && broke(a, b - 2 - r)) ++r;
+    if (r == MAX_RUN) {
+      a.chunk_flag[a.chunk_base[p] + (j - 2 > MAX_RUN ? j - 2 - MAX_RUN : 0u)] = 1;
+      return;
     }
-    // chunk base+f: its true entry is cand_f (all earlier lanes were consistent). Walk it from a
-    // 512-byte register window (lane l holds 8 bytes) instead of dependent global loads.
-    uint64_t ef = __shfl(cand, int(f), 64);
-    const uint64_t fcs = uint64_t(base + f) * SNAP_CH;
-    const uint64_t fce = min(fcs + SNAP_CH, uint64_t(pg.n_in));
-    if (ef < fce) {
+    genuine = (r & 1u) == 0;
+  }
+  if (!genuine) {
+    a.entry[c] = a.assumed_exit[b];
+    return;
+  }
+  const SnapPage& pg = a.pages[p];
+  const uint64_t cs = uint64_t(j - 1) * SNAP_CH;
+  const uint64_t ce = min(cs + SNAP_CH, uint64_t(pg.n_in));
+  const uint64_t e = a.assumed_exit[b - 1];  // chunk c-1's true entry
+  const bool resync = e < ce && ((a.vis[uint64_t(b) * (SNAP_CH / 32) + uint32_t((e - cs) >> 5)] >> ((e - cs) & 31)) & 1u);
+  if (!resync) {
+    a.chunk_flag[c - 2] = 1;
+    return;
+  }
+  a.entry[c] = a.spec_exit[b];
+}
+
+// B3a: the regions to resolve serially: a flagged chunk with no other flag in the REGION_GAP
+// chunks before it (on the same page) starts a region; later flags nearby are covered by it.
+constexpr uint32_t RESOLVE_MARGIN = 8;
+constexpr uint32_t REGION_GAP = 80;
+__global__ void __launch_bounds__(256) k_snap_regions(SnappyArgs a) {
+  const uint32_t c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= a.nchunks || !a.chunk_flag[c]) return;
+  const uint32_t p = chunk_page(a.chunk_base, a.npages, c);
+  const uint32_t c0 = a.chunk_base[p];
+  const uint32_t lo = c >= c0 + REGION_GAP ? c - REGION_GAP : c0;
+  for (uint32_t k = lo; k < c; ++k)
+    if (a.chunk_flag[k]) return;
+  const unsigned long long slot = atomicAdd(a.region_count, 1ull);
+  a.region[slot] = c;
+}
+
+// B3b: one wave per region: from RESOLVE_MARGIN chunks before the flag (entries there are exact)
+// the true chain is followed 64 chunks per ballot, rewriting entries, until a whole 64-chunk step
+// beyond the flag has no break and agrees with the entries k_snap_entries wrote (from there on
+// they are exact again). A chunk whose entry lies past its end (a long literal spans it) jumps to
+// the chunk holding that entry.
+__global__ void __launch_bounds__(64) k_snap_resolve(SnappyArgs a) {
+  const uint64_t nreg = *a.region_count;
+  for (uint64_t rg = blockIdx.x; rg < nreg; rg += gridDim.x) {
+    const uint32_t cf = a.region[rg];
+    const uint32_t p = chunk_page(a.chunk_base, a.npages, cf);
+    const SnapPage& pg = a.pages[p];
+    const uint8_t* in = reinterpret_cast<const uint8_t*>(pg.in);
+    const uint32_t c0 = a.chunk_base[p], nc = a.chunk_base[p + 1] - c0;
+    const uint32_t jf = cf - c0;
+    const int lane = threadIdx.x;
+    uint32_t base = jf > RESOLVE_MARGIN ? jf - RESOLVE_MARGIN : 0u;
+    uint64_t e = base == 0 ? 0 : a.entry[c0 + base];  // true entry of chunk `base`
+    while (base < nc) {
+      const uint32_t j = base + lane;
+      const bool valid = j < nc;
+      uint32_t x = 0, word = 0, old = 0;
+      const uint64_t cs = uint64_t(j) * SNAP_CH;
+      const uint64_t ce = min(cs + SNAP_CH, uint64_t(pg.n_in));
+      if (valid) { x = a.spec_exit[c0 + j]; old = a.entry[c0 + j]; }
+      uint64_t cand = __shfl_up(uint64_t(x), 1, 64);
+      if (lane == 0) cand = e;
+      const bool skip = cand >= ce;
+      if (valid && !skip) word = a.vis[uint64_t(c0 + j) * (SNAP_CH / 32) + uint32_t((cand - cs) >> 5)];
+      const bool ok = valid && !skip && ((word >> ((cand - cs) & 31)) & 1u);
+      const unsigned long long brk = __ballot(valid && !ok);
+      const uint32_t f = brk ? uint32_t(__builtin_ctzll(brk)) : 64u;  // first chunk needing care
+      const uint32_t cv = uint32_t(min(cand, uint64_t(0xffffffffu)));
+      const bool agree = __ballot(valid && (cv != old)) == 0ull;
+      if (valid && uint32_t(lane) <= f) a.entry[c0 + j] = cv;
+      const uint32_t cnt = min(64u, nc - base);
+      if (f >= cnt) {
+        if (agree && base > jf) break;  // back in step with k_snap_entries
+        e = uint32_t(__builtin_amdgcn_readlane(int(x), int(cnt - 1)));
+        base += cnt;
+        continue;
+      }
+      const uint64_t ef0 = __shfl(cand, int(f), 64);
+      const uint64_t fcs = uint64_t(base + f) * SNAP_CH;
+      const uint64_t fce = min(fcs + SNAP_CH, uint64_t(pg.n_in));
+      if (ef0 >= fce) {
+        // chunks base+f .. (the chunk holding ef0) - 1 hold no element start: entry = ef0
+        const uint32_t jt = uint32_t(min(ef0 / SNAP_CH, uint64_t(nc)));
+        for (uint32_t q = base + f + 1 + lane; q < jt; q += 64) a.entry[c0 + q] = uint32_t(min(ef0, uint64_t(0xffffffffu)));
+        e = ef0;
+        base = jt > base + f ? jt : base + f + 1;
+        continue;
+      }
+      // chunk base+f: its true entry is ef0. Walk it from a 512-byte register window (lane l
+      // holds 8 bytes) instead of dependent global loads.
+      uint64_t ef = ef0;
       const uintptr_t wa = (reinterpret_cast<uintptr_t>(in) + fcs) & ~uintptr_t(7);
       const int64_t wb = int64_t(wa) - int64_t(reinterpret_cast<uintptr_t>(in));
       const uint2 w = reinterpret_cast<const uint2*>(wa)[lane];
@@ -201,13 +317,13 @@ __global__ void __launch_bounds__(64) k_snap_resolve(SnappyArgs a) {
         }
         ef += snap_adv(snap_decode(hdr));
       }
+      e = ef;
+      base += f + 1;
     }
-    e = ef;
-    base += f + 1;
   }
 }
 
-// C: output bytes / copy elements produced by the true elements of each chunk.
+// C: output bytes / elements produced by the true elements of each chunk.
 __global__ void __launch_bounds__(WG_CHUNKS) k_snap_count(SnappyArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[STAGE_BYTES + 32];
   const WgInfo g = wg_info(a);
@@ -219,15 +335,15 @@ __global__ void __launch_bounds__(WG_CHUNKS) k_snap_count(SnappyArgs a) {
   const uint64_t cs = uint64_t(j) * SNAP_CH;
   const uint64_t ce = min(cs + SNAP_CH, uint64_t(pg.n_in));
   uint64_t pos = a.entry[c], out = 0;
-  uint32_t copies = 0;
+  uint32_t elems = 0;
   while (pos < ce) {
     const Elem el = snap_decode(staged_u64(buf, s, pos));
     out += el.len;
-    copies += el.off != 0;
+    ++elems;
     pos += snap_adv(el);
   }
   a.chunk_out[c] = out > 0xffffffffull ? 0xffffffffu : uint32_t(out);
-  a.chunk_copies[c] = copies;
+  a.chunk_elems[c] = elems;
 }
 
 // D: per-page exclusive scan of chunk outputs (one wave per page).
@@ -251,53 +367,88 @@ __global__ void __launch_bounds__(64) k_snap_scan(SnappyArgs a) {
   if (lane == 0 && carry != a.pages[p].n_out) atomicOr(&a.pages_bad[p], 1u);  // size mismatch
 }
 
-// E: literal bytes to the output, copies to records.
+// E: one 8-byte record per element, {output offset in its chunk u16 | (len-1) u16 << 16 |
+// src u32 << 32}; src = copy offset, or REC_LIT | input position for a literal. Records are
+// assembled in LDS per workgroup and written out with coalesced stores.
+constexpr uint32_t REC_LIT = 0x80000000u;
+constexpr uint32_t EMIT_RECS = 4096;  // LDS record slots per workgroup (overflow: direct stores)
+
 __global__ void __launch_bounds__(WG_CHUNKS) k_snap_emit(SnappyArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[STAGE_BYTES + 32];
+  __shared__ uint64_t rbuf[EMIT_RECS];
   const WgInfo g = wg_info(a);
   const SnapPage& pg = a.pages[g.p];
   const Staged s = stage_input(buf, reinterpret_cast<const uint8_t*>(pg.in), pg.n_in, g.j0, g.cnt);
-  if (threadIdx.x >= g.cnt) return;
-  const uint32_t j = g.j0 + threadIdx.x;
-  const uint32_t c = a.chunk_base[g.p] + j;
-  const uint64_t cs = uint64_t(j) * SNAP_CH;
-  const uint64_t ce = min(cs + SNAP_CH, uint64_t(pg.n_in));
-  uint8_t* out = reinterpret_cast<uint8_t*>(pg.out);
-  uint64_t pos = a.entry[c], o = a.chunk_out_start[c];
-  uint64_t rec = a.chunk_rec_start[c];
-  bool bad = false;
-  while (pos < ce) {
-    const Elem el = snap_decode(staged_u64(buf, s, pos));
-    if (o + el.len > pg.n_out || (el.len && (o >> 16) != ((o + el.len - 1) >> 16))) { bad = true; break; }
-    if (el.off == 0) {
-      if (pos + el.hdr + el.len > pg.n_in) { bad = true; break; }
-      const uint64_t lp = pos + el.hdr;
-      if (lp + el.len + 4 <= s.hi) {
-        for (uint32_t i = 0; i < el.len; ++i) out[o + i] = buf[uint32_t(int64_t(lp + i) - s.lo)];
-      } else {  // a long literal running past the staged range
-        const uint8_t* sp = reinterpret_cast<const uint8_t*>(pg.in) + lp;
-        for (uint32_t i = 0; i < el.len; ++i) out[o + i] = sp[i];
+  const uint32_t cfirst = a.chunk_base[g.p] + g.j0;
+  const uint64_t wr0 = a.chunk_rec_start[cfirst], wr1 = a.chunk_rec_start[cfirst + g.cnt];
+  const bool in_lds = wr1 - wr0 <= EMIT_RECS;
+  if (threadIdx.x < g.cnt) {
+    const uint32_t j = g.j0 + threadIdx.x;
+    const uint32_t c = cfirst + threadIdx.x;
+    const uint64_t cs = uint64_t(j) * SNAP_CH;
+    const uint64_t ce = min(cs + SNAP_CH, uint64_t(pg.n_in));
+    uint64_t pos = a.entry[c], o = a.chunk_out_start[c];
+    uint32_t orel = 0;
+    uint64_t rec = a.chunk_rec_start[c];
+    bool bad = false;
+    while (pos < ce) {
+      const Elem el = snap_decode(staged_u64(buf, s, pos));
+      if (o + el.len > pg.n_out || el.len == 0 || el.len > SNAP_BLOCK || orel > 0xffffu ||
+          (o >> 16) != ((o + el.len - 1) >> 16)) { bad = true; break; }
+      uint32_t src;
+      if (el.off == 0) {
+        if (pos + el.hdr + el.len > pg.n_in || pos + el.hdr >= REC_LIT) { bad = true; break; }
+        src = REC_LIT | uint32_t(pos + el.hdr);
+      } else {
+        if (el.off > (o & (SNAP_BLOCK - 1))) { bad = true; break; }  // a copy reaching before its fragment
+        src = el.off;
       }
-    } else {
-      if (el.off > (o & (SNAP_BLOCK - 1)) || el.len > 0xffff) { bad = true; break; }  // copy crosses its fragment
-      a.recs[rec++] = uint64_t(o) | (uint64_t(el.len) << 32) | (uint64_t(el.off) << 48);
+      const uint64_t r = uint64_t(orel) | (uint64_t(el.len - 1) << 16) | (uint64_t(src) << 32);
+      if (in_lds) rbuf[rec - wr0] = r; else a.recs[rec] = r;
+      ++rec;
+      o += el.len;
+      orel += el.len;
+      pos += snap_adv(el);
     }
-    o += el.len;
-    pos += snap_adv(el);
+    if (bad) atomicOr(&a.pages_bad[g.p], 8u);
   }
-  if (bad) atomicOr(&a.pages_bad[g.p], 8u);
+  if (in_lds) {
+    __syncthreads();
+    for (uint64_t r = wr0 + threadIdx.x; r < wr1; r += WG_CHUNKS) a.recs[r] = rbuf[r - wr0];
+  }
 }
 
 // F: one 1024-thread workgroup per 64 KiB output block.
+//  1. map[i] = i, then every copy byte i := i - offset (u16 map of the block in LDS);
+//  2. pointer jumping until every byte points at its literal origin (chains of copies of copies
+//     are as long as the number of repeated path prefixes in the fragment; log2 rounds);
+//  3. each thread keeps the roots of its 64 contiguous bytes in registers; the LDS is reused as the
+//     block's bytes: literal runs are copied in from the compressed input;
+//  4. each thread gathers its 64 bytes from their roots and stores them with 16-byte stores.
 constexpr int EXEC_T = 1024;
+constexpr uint32_t EXEC_MAX_CHUNKS = 1024;   // chunks overlapping one block (more: serial fallback)
+constexpr uint32_t EXEC_LONG = 256;          // literal records copied by the whole workgroup
+
+__device__ __forceinline__ uint32_t exec_chunk_of(const uint32_t* tab, uint32_t n, uint32_t r) {
+  uint32_t lo = 0, hi = n;  // last k with tab[k] <= r
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (tab[mid] <= r) lo = mid; else hi = mid;
+  }
+  return lo;
+}
 
 __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
-  __shared__ uint16_t src[SNAP_BLOCK];
-  __shared__ uint32_t s_j0, s_j1, s_changed;
+  __shared__ __attribute__((aligned(16))) uint16_t src[SNAP_BLOCK];  // map, later the block's bytes
+  __shared__ uint32_t c_out[EXEC_MAX_CHUNKS + 1];   // chunk output start - block start (may be < 0)
+  __shared__ uint32_t c_rec[EXEC_MAX_CHUNKS + 1];   // record index - first record of the block
+  __shared__ uint32_t s_j0, s_j1, s_changed, s_bad, s_nlong;
+  __shared__ uint32_t s_long[EXEC_LONG];
   const uint32_t b = blockIdx.x;
   const uint32_t p = a.block_page[b];
   if (a.pages_bad[p]) return;
   const SnapPage& pg = a.pages[p];
+  const uint8_t* in = reinterpret_cast<const uint8_t*>(pg.in);
   uint8_t* out = reinterpret_cast<uint8_t*>(pg.out);
   const uint32_t k = b - pg.block_base;
   const uint64_t bs = uint64_t(k) * SNAP_BLOCK;
@@ -318,20 +469,42 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
       if (a.chunk_out_start[mid] < be) lo = mid + 1; else hi = mid;
     }
     s_j1 = lo;
+    s_bad = 0;
+    s_nlong = 0;
   }
   for (uint32_t i = t; i < nbytes; i += EXEC_T) src[i] = uint16_t(i);
   __syncthreads();
-  const uint64_t r0 = a.chunk_rec_start[s_j0];
-  const uint64_t r1 = a.chunk_rec_start[s_j1];
-  for (uint64_t r = r0 + t; r < r1; r += EXEC_T) {
-    const uint64_t w = a.recs[r];
-    const uint64_t o = uint32_t(w);
-    if (o < bs || o >= be) continue;
-    const uint32_t len = uint32_t((w >> 32) & 0xffff), off = uint32_t(w >> 48);
-    const uint32_t rel = uint32_t(o - bs);
-    for (uint32_t i = 0; i < len; ++i) src[rel + i] = uint16_t(rel + i - off);
+  const uint32_t j0 = s_j0, nch = s_j1 - s_j0;
+  if (nch > EXEC_MAX_CHUNKS) {  // block-uniform
+    if (t == 0) atomicOr(&a.pages_bad[p], 16u);
+    return;
+  }
+  const uint64_t r0 = a.chunk_rec_start[j0];
+  for (uint32_t q = t; q <= nch; q += EXEC_T) {
+    c_rec[q] = uint32_t(a.chunk_rec_start[j0 + q] - r0);
+    c_out[q] = q < nch ? uint32_t(int64_t(a.chunk_out_start[j0 + q]) - int64_t(bs)) : 0u;
   }
   __syncthreads();
+  const uint32_t nrec = c_rec[nch];
+  // 1. copy bytes point at their sources
+  for (uint32_t r = t; r < nrec; r += EXEC_T) {
+    const uint64_t w = a.recs[r0 + r];
+    const uint32_t sv = uint32_t(w >> 32);
+    if (sv & REC_LIT) continue;
+    const uint32_t q = exec_chunk_of(c_rec, nch, r);
+    const int64_t o = int64_t(int32_t(c_out[q])) + int64_t(w & 0xffff);
+    const uint32_t len = uint32_t((w >> 16) & 0xffff) + 1;
+    if (o < 0 || o >= int64_t(nbytes)) continue;  // the element belongs to a neighbouring block
+    const uint32_t rel = uint32_t(o);
+    if (sv > rel || rel + len > nbytes) { s_bad = 1; continue; }
+    for (uint32_t i = 0; i < len; ++i) src[rel + i] = uint16_t(rel + i - sv);
+  }
+  __syncthreads();
+  if (s_bad) {
+    if (t == 0) atomicOr(&a.pages_bad[p], 32u);
+    return;
+  }
+  // 2. pointer jumping
   for (int round = 0; round < 17; ++round) {
     if (t == 0) s_changed = 0;
     __syncthreads();
@@ -345,10 +518,75 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     __syncthreads();
     if (!s_changed) break;
   }
-  __threadfence_block();
-  for (uint32_t i = t; i < nbytes; i += EXEC_T) {
-    const uint32_t r = src[i];
-    if (r != i) out[bs + i] = out[bs + r];
+  // 3. roots of this thread's 64 bytes -> registers; the LDS becomes the block's bytes
+  const uint32_t my0 = uint32_t(t) * 64;
+  uint32_t root[32];  // two u16 roots per register
+  {
+    const uint4* s4 = reinterpret_cast<const uint4*>(src) + my0 / 8;
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      const uint4 x = my0 < nbytes ? s4[v] : make_uint4(0, 0, 0, 0);
+      root[4 * v] = x.x; root[4 * v + 1] = x.y; root[4 * v + 2] = x.z; root[4 * v + 3] = x.w;
+    }
+  }
+  __syncthreads();
+  uint8_t* bytes = reinterpret_cast<uint8_t*>(src);
+  for (uint32_t r = t; r < nrec; r += EXEC_T) {
+    const uint64_t w = a.recs[r0 + r];
+    const uint32_t sv = uint32_t(w >> 32);
+    if (!(sv & REC_LIT)) continue;
+    const uint32_t q = exec_chunk_of(c_rec, nch, r);
+    const int64_t o = int64_t(int32_t(c_out[q])) + int64_t(w & 0xffff);
+    if (o < 0 || o >= int64_t(nbytes)) continue;
+    const uint32_t len = uint32_t((w >> 16) & 0xffff) + 1;
+    if (len > EXEC_LONG) {
+      const uint32_t slot = atomicAdd(&s_nlong, 1u);
+      if (slot < EXEC_LONG) s_long[slot] = r;
+      else s_bad = 1;
+      continue;
+    }
+    const uint32_t rel = uint32_t(o);
+    const uint8_t* ip = in + (sv & ~REC_LIT);
+    for (uint32_t i = 0; i < len; ++i) bytes[rel + i] = ip[i];
+  }
+  __syncthreads();
+  const uint32_t nlong = min(s_nlong, EXEC_LONG);
+  for (uint32_t L = 0; L < nlong; ++L) {  // long literals: the whole workgroup
+    const uint32_t r = s_long[L];
+    const uint64_t w = a.recs[r0 + r];
+    const uint32_t q = exec_chunk_of(c_rec, nch, r);
+    const uint32_t rel = uint32_t(int64_t(int32_t(c_out[q])) + int64_t(w & 0xffff));
+    const uint32_t len = uint32_t((w >> 16) & 0xffff) + 1;
+    const uint8_t* ip = in + (uint32_t(w >> 32) & ~REC_LIT);
+    for (uint32_t i = t; i < len; i += EXEC_T) bytes[rel + i] = ip[i];
+  }
+  __syncthreads();
+  if (s_bad) {  // block-uniform
+    if (t == 0) atomicOr(&a.pages_bad[p], 64u);
+    return;
+  }
+  // 4. gather and store
+  if (my0 >= nbytes) return;
+  uint32_t word[16];
+#pragma unroll
+  for (int v = 0; v < 16; ++v) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const uint32_t pr = root[(4 * v + h) >> 1];
+      const uint32_t rt = ((4 * v + h) & 1) ? (pr >> 16) : (pr & 0xffff);
+      x |= uint32_t(bytes[rt]) << (8 * h);
+    }
+    word[v] = x;
+  }
+  uint8_t* dst = out + bs + my0;
+  if (my0 + 64 <= nbytes && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0)) {
+    uint4* d4 = reinterpret_cast<uint4*>(dst);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) d4[v] = make_uint4(word[4 * v], word[4 * v + 1], word[4 * v + 2], word[4 * v + 3]);
+  } else {
+    const uint32_t m = min(64u, nbytes - my0);
+    for (uint32_t i = 0; i < m; ++i) dst[i] = uint8_t(word[i >> 2] >> (8 * (i & 3)));
   }
 }
 
@@ -393,10 +631,14 @@ uint32_t snappy_wg_chunks() { return dev::WG_CHUNKS; }
 void launch_snappy(const SnappyArgs& a, hipStream_t st, void* scan_scratch) {
   if (!a.npages) return;
   hipLaunchKernelGGL(dev::k_snap_spec, dim3(a.nwg), dim3(dev::WG_CHUNKS), 0, st, a);
-  hipLaunchKernelGGL(dev::k_snap_resolve, dim3(a.npages), dim3(64), 0, st, a);
+  const unsigned g = (a.nchunks + 255) / 256;
+  hipLaunchKernelGGL(dev::k_snap_assume, dim3(g), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(dev::k_snap_entries, dim3(g), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(dev::k_snap_regions, dim3(g), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(dev::k_snap_resolve, dim3(512), dim3(64), 0, st, a);
   hipLaunchKernelGGL(dev::k_snap_count, dim3(a.nwg), dim3(dev::WG_CHUNKS), 0, st, a);
   hipLaunchKernelGGL(dev::k_snap_scan, dim3(a.npages), dim3(64), 0, st, a);
-  launch_scan_u32(a.chunk_copies, a.chunk_rec_start, a.nchunks, scan_scratch, st);
+  launch_scan_u32(a.chunk_elems, a.chunk_rec_start, a.nchunks, scan_scratch, st);
   hipLaunchKernelGGL(dev::k_snap_emit, dim3(a.nwg), dim3(dev::WG_CHUNKS), 0, st, a);
   hipLaunchKernelGGL(dev::k_snap_exec, dim3(a.nblocks), dim3(dev::EXEC_T), 0, st, a);
   hipLaunchKernelGGL(dev::k_snap_serial, dim3((a.npages + 63) / 64), dim3(64), 0, st, a);

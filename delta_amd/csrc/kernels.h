@@ -122,11 +122,15 @@ struct SnappyArgs {
   uint32_t* spec_exit;          // [nchunks]
   uint32_t* vis;                // [nchunks * 8] visited-position bitmaps
   uint32_t* entry;              // [nchunks] true first element position >= chunk start
+  uint32_t* assumed_exit;       // [nchunks] exit assuming the previous chunk's speculative exit
+  uint8_t* chunk_flag;          // [nchunks] 1: serial resolution from this chunk
+  uint32_t* region;             // [nchunks] chunks starting a serially resolved region
+  unsigned long long* region_count;
   uint32_t* chunk_out;          // [nchunks] output bytes of the chunk's elements
   uint32_t* chunk_out_start;    // [nchunks]
-  uint32_t* chunk_copies;       // [nchunks] copy elements per chunk
-  uint64_t* chunk_rec_start;    // [nchunks + 1] exclusive scan of chunk_copies
-  uint64_t* recs;               // copy records {out u32 | len u16 << 32 | off u16 << 48}
+  uint32_t* chunk_elems;        // [nchunks] elements per chunk
+  uint64_t* chunk_rec_start;    // [nchunks + 1] exclusive scan of chunk_elems
+  uint64_t* recs;               // element records (k_snap_emit)
   const uint32_t* block_page;   // [nblocks]
   uint32_t nblocks;
   const uint32_t* wg_chunk0;    // [nwg] first chunk (global index) of each chunk-walker workgroup

@@ -198,6 +198,7 @@ struct PagePlan {
       s_chunk_copies, s_pages_bad;
   DBuf<uint64_t> s_rec_start, s_recs;
   DBuf<uint8_t> s_chunk_flag;
+  DBuf<uint32_t> s_block_chunks;
   DBuf<unsigned long long> s_region_count;
   std::vector<uint32_t> wg_chunk0;
   DBuf<uint32_t> d_wg_chunk0;
@@ -550,6 +551,7 @@ static void plan_pages(StagedData& s, PagePlan& P) {
   P.s_entry = DBuf<uint32_t>(s.ctx, P.nchunks);
   P.s_assumed = DBuf<uint32_t>(s.ctx, P.nchunks);
   P.s_region = DBuf<uint32_t>(s.ctx, P.nchunks);
+  P.s_block_chunks = DBuf<uint32_t>(s.ctx, 2 * P.block_page.size() + 2);
   P.s_chunk_flag = DBuf<uint8_t>(s.ctx, P.nchunks);
   P.s_region_count = DBuf<unsigned long long>(s.ctx, 1);
   P.s_chunk_out = DBuf<uint32_t>(s.ctx, P.nchunks);
@@ -591,10 +593,29 @@ static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_
     P.s_region_count.zero(stream);
     SnappyArgs sa{P.d_snap.p, uint32_t(P.snap_pages.size()), P.d_chunk_base.p, P.nchunks, P.s_spec_exit.p,
                   P.s_vis.p, P.s_entry.p, P.s_assumed.p, P.s_chunk_flag.p, P.s_region.p, P.s_region_count.p, P.s_chunk_out.p, P.s_chunk_out_start.p, P.s_chunk_copies.p,
-                  P.s_rec_start.p, P.s_recs.p, P.d_block_page.p, uint32_t(P.block_page.size()),
+                  P.s_rec_start.p, P.s_recs.p, P.d_block_page.p, P.s_block_chunks.p, uint32_t(P.block_page.size()),
                   P.d_wg_chunk0.p, uint32_t(P.wg_chunk0.size()), P.s_pages_bad.p, err.p};
+    DBuf<uint64_t> stamps;
+    const bool dbg = std::getenv("DR_SNAP_DEBUG") != nullptr;
+    if (dbg) {
+      stamps = DBuf<uint64_t>(ctx, P.block_page.size() * 8);
+      stamps.zero(stream);
+      sa.stamps = stamps.p;
+    }
     launch_snappy(sa, stream, scratch);
-    if (std::getenv("DR_SNAP_DEBUG")) {
+    if (dbg) {
+      std::vector<uint64_t> st = d2h(stamps.p, P.block_page.size() * 8, stream);
+      double acc[8] = {0};
+      size_t nb2 = 0;
+      for (size_t q = 0; q < P.block_page.size(); ++q) {
+        const uint64_t* x = &st[q * 8];
+        if (!x[0] || !x[7]) continue;
+        ++nb2;
+        for (int k = 1; k < 8; ++k) acc[k] += double(x[k] - x[k - 1]);
+      }
+      std::fprintf(stderr, "exec phases (clocks/block, %zu blocks):", nb2);
+      for (int k = 1; k < 8; ++k) std::fprintf(stderr, " %.0f", nb2 ? acc[k] / double(nb2) : 0.0);
+      std::fprintf(stderr, "\n");
       const unsigned long long nreg = d2h_one(P.s_region_count.p, stream);
       std::vector<uint32_t> pb = d2h(P.s_pages_bad.p, P.snap_pages.size(), stream);
       size_t nb = 0;

@@ -438,11 +438,35 @@ __device__ __forceinline__ uint32_t exec_chunk_of(const uint32_t* tab, uint32_t 
   return lo;
 }
 
+// F0: every output block's chunk range [first chunk whose output reaches past the block start,
+// first chunk starting at or after the block end).
+__global__ void __launch_bounds__(256) k_snap_block_chunks(SnappyArgs a) {
+  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= a.nblocks) return;
+  const uint32_t p = a.block_page[b];
+  const SnapPage& pg = a.pages[p];
+  const uint64_t bs = uint64_t(b - pg.block_base) * SNAP_BLOCK;
+  const uint64_t be = min(bs + SNAP_BLOCK, uint64_t(pg.n_out));
+  const uint32_t c0 = a.chunk_base[p], c1 = a.chunk_base[p + 1];
+  uint32_t lo = c0, hi = c1;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (uint64_t(a.chunk_out_start[mid]) + a.chunk_out[mid] <= bs) lo = mid + 1; else hi = mid;
+  }
+  a.block_chunks[2 * b] = lo;
+  hi = c1;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (a.chunk_out_start[mid] < be) lo = mid + 1; else hi = mid;
+  }
+  a.block_chunks[2 * b + 1] = lo;
+}
+
 __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t src[SNAP_BLOCK];  // map, later the block's bytes
   __shared__ uint32_t c_out[EXEC_MAX_CHUNKS + 1];   // chunk output start - block start (may be < 0)
   __shared__ uint32_t c_rec[EXEC_MAX_CHUNKS + 1];   // record index - first record of the block
-  __shared__ uint32_t s_j0, s_j1, s_changed, s_bad, s_nlong;
+  __shared__ uint32_t s_bad, s_nlong;
   __shared__ uint32_t s_long[EXEC_LONG];
   const uint32_t b = blockIdx.x;
   const uint32_t p = a.block_page[b];
@@ -454,27 +478,19 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
   const uint64_t bs = uint64_t(k) * SNAP_BLOCK;
   const uint64_t be = min(bs + SNAP_BLOCK, uint64_t(pg.n_out));
   const uint32_t nbytes = uint32_t(be - bs);
-  const uint32_t c0 = a.chunk_base[p], c1 = a.chunk_base[p + 1];
   const int t = threadIdx.x;
+  // diagnostic phase stamps (DR_SNAP_DEBUG allocates the buffer; null otherwise)
+  auto stamp = [&](int k) {
+    if (a.stamps && t == 0) a.stamps[uint64_t(b) * 8 + k] = __builtin_amdgcn_s_memtime();
+  };
+  stamp(0);
   if (t == 0) {
-    uint32_t lo = c0, hi = c1;  // first chunk whose output reaches past bs
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (uint64_t(a.chunk_out_start[mid]) + a.chunk_out[mid] <= bs) lo = mid + 1; else hi = mid;
-    }
-    s_j0 = lo;
-    hi = c1;  // first chunk starting at or after be
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (a.chunk_out_start[mid] < be) lo = mid + 1; else hi = mid;
-    }
-    s_j1 = lo;
     s_bad = 0;
     s_nlong = 0;
   }
   for (uint32_t i = t; i < nbytes; i += EXEC_T) src[i] = uint16_t(i);
+  const uint32_t j0 = a.block_chunks[2 * b], nch = a.block_chunks[2 * b + 1] - j0;
   __syncthreads();
-  const uint32_t j0 = s_j0, nch = s_j1 - s_j0;
   if (nch > EXEC_MAX_CHUNKS) {  // block-uniform
     if (t == 0) atomicOr(&a.pages_bad[p], 16u);
     return;
@@ -485,39 +501,51 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     c_out[q] = q < nch ? uint32_t(int64_t(a.chunk_out_start[j0 + q]) - int64_t(bs)) : 0u;
   }
   __syncthreads();
-  const uint32_t nrec = c_rec[nch];
-  // 1. copy bytes point at their sources
-  for (uint32_t r = t; r < nrec; r += EXEC_T) {
-    const uint64_t w = a.recs[r0 + r];
-    const uint32_t sv = uint32_t(w >> 32);
-    if (sv & REC_LIT) continue;
-    const uint32_t q = exec_chunk_of(c_rec, nch, r);
-    const int64_t o = int64_t(int32_t(c_out[q])) + int64_t(w & 0xffff);
-    const uint32_t len = uint32_t((w >> 16) & 0xffff) + 1;
-    if (o < 0 || o >= int64_t(nbytes)) continue;  // the element belongs to a neighbouring block
-    const uint32_t rel = uint32_t(o);
-    if (sv > rel || rel + len > nbytes) { s_bad = 1; continue; }
-    for (uint32_t i = 0; i < len; ++i) src[rel + i] = uint16_t(rel + i - sv);
+  stamp(1);
+  const int lane = t & 63, wv = t >> 6;
+  // 1. copy bytes point at their sources: one wave per chunk, one lane per record
+  for (uint32_t q = wv; q < nch; q += EXEC_T / 64) {
+    const int32_t cb = int32_t(c_out[q]);
+    for (uint32_t r = c_rec[q] + lane; r < c_rec[q + 1]; r += 64) {
+      const uint64_t w = a.recs[r0 + r];
+      const uint32_t sv = uint32_t(w >> 32);
+      if (sv & REC_LIT) continue;
+      const int64_t o = int64_t(cb) + int64_t(w & 0xffff);
+      const uint32_t len = uint32_t((w >> 16) & 0xffff) + 1;
+      if (o < 0 || o >= int64_t(nbytes)) continue;  // the element belongs to a neighbouring block
+      const uint32_t rel = uint32_t(o);
+      if (sv > rel || rel + len > nbytes) { s_bad = 1; continue; }
+      for (uint32_t i = 0; i < len; ++i) src[rel + i] = uint16_t(rel + i - sv);
+    }
   }
   __syncthreads();
+  stamp(2);
   if (s_bad) {
     if (t == 0) atomicOr(&a.pages_bad[p], 32u);
     return;
   }
-  // 2. pointer jumping
+  // 2. pointer jumping over this thread's copy bytes i = t + 1024 k, dropping each byte from its
+  //    pending mask once it points at a root (most chains are short: the pending set halves fast)
+  uint64_t pend = 0;
+#pragma unroll 4
+  for (uint32_t k = 0; k < 64; ++k) {
+    const uint32_t i = uint32_t(t) + EXEC_T * k;
+    if (i < nbytes && src[i] != i) pend |= 1ull << k;
+  }
   for (int round = 0; round < 17; ++round) {
-    if (t == 0) s_changed = 0;
-    __syncthreads();
-    uint32_t ch = 0;
-    for (uint32_t i = t; i < nbytes; i += EXEC_T) {
+    uint64_t m = pend;
+    while (m) {
+      const uint32_t k = uint32_t(__builtin_ctzll(m));
+      m &= m - 1;
+      const uint32_t i = uint32_t(t) + EXEC_T * k;
       const uint32_t x = src[i];
       const uint32_t y = src[x];
-      if (y != x) { src[i] = uint16_t(y); ch = 1; }
+      if (y == x) pend &= ~(1ull << k);
+      else src[i] = uint16_t(y);
     }
-    if (__any(ch) && (t & 63) == 0) s_changed = 1;
-    __syncthreads();
-    if (!s_changed) break;
+    if (!__syncthreads_or(pend != 0)) break;
   }
+  stamp(3);
   // 3. roots of this thread's 64 bytes -> registers; the LDS becomes the block's bytes
   const uint32_t my0 = uint32_t(t) * 64;
   uint32_t root[32];  // two u16 roots per register
@@ -530,26 +558,51 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     }
   }
   __syncthreads();
+  // the upper half of the map is free now: stage the block's compressed input there (16-byte
+  // loads) so literal runs are copied LDS -> LDS
   uint8_t* bytes = reinterpret_cast<uint8_t*>(src);
-  for (uint32_t r = t; r < nrec; r += EXEC_T) {
-    const uint64_t w = a.recs[r0 + r];
-    const uint32_t sv = uint32_t(w >> 32);
-    if (!(sv & REC_LIT)) continue;
-    const uint32_t q = exec_chunk_of(c_rec, nch, r);
-    const int64_t o = int64_t(int32_t(c_out[q])) + int64_t(w & 0xffff);
-    if (o < 0 || o >= int64_t(nbytes)) continue;
-    const uint32_t len = uint32_t((w >> 16) & 0xffff) + 1;
-    if (len > EXEC_LONG) {
-      const uint32_t slot = atomicAdd(&s_nlong, 1u);
-      if (slot < EXEC_LONG) s_long[slot] = r;
-      else s_bad = 1;
-      continue;
-    }
-    const uint32_t rel = uint32_t(o);
-    const uint8_t* ip = in + (sv & ~REC_LIT);
-    for (uint32_t i = 0; i < len; ++i) bytes[rel + i] = ip[i];
+  uint8_t* stage = bytes + SNAP_BLOCK;
+  const uint32_t c0 = a.chunk_base[p];
+  const uint64_t in_lo = uint64_t(j0 - c0) * SNAP_CH;
+  const uint64_t in_hi = min(uint64_t(j0 - c0 + nch + 1) * SNAP_CH + 64, uint64_t(pg.n_in));
+  const uintptr_t abs_lo = (reinterpret_cast<uintptr_t>(in) + in_lo) & ~uintptr_t(15);
+  const uint32_t nv = uint32_t((reinterpret_cast<uintptr_t>(in) + in_hi - abs_lo + 15) >> 4);
+  const bool staged = nv * 16 <= SNAP_BLOCK;
+  if (staged) {
+    const uint4* g4 = reinterpret_cast<const uint4*>(abs_lo);
+    uint4* s4 = reinterpret_cast<uint4*>(stage);
+    for (uint32_t v = t; v < nv; v += EXEC_T) s4[v] = g4[v];
   }
   __syncthreads();
+  stamp(4);
+  for (uint32_t q = wv; q < nch; q += EXEC_T / 64) {
+    const int32_t cb = int32_t(c_out[q]);
+    for (uint32_t r = c_rec[q] + lane; r < c_rec[q + 1]; r += 64) {
+      const uint64_t w = a.recs[r0 + r];
+      const uint32_t sv = uint32_t(w >> 32);
+      if (!(sv & REC_LIT)) continue;
+      const int64_t o = int64_t(cb) + int64_t(w & 0xffff);
+      if (o < 0 || o >= int64_t(nbytes)) continue;
+      const uint32_t len = uint32_t((w >> 16) & 0xffff) + 1;
+      if (len > EXEC_LONG) {
+        const uint32_t slot = atomicAdd(&s_nlong, 1u);
+        if (slot < EXEC_LONG) s_long[slot] = r;
+        else s_bad = 1;
+        continue;
+      }
+      const uint32_t rel = uint32_t(o);
+      const uint32_t ipos = sv & ~REC_LIT;
+      if (staged && ipos >= in_lo && ipos + len <= in_hi) {
+        const uint8_t* ip = stage + (reinterpret_cast<uintptr_t>(in) + ipos - abs_lo);
+        for (uint32_t i = 0; i < len; ++i) bytes[rel + i] = ip[i];
+      } else {
+        const uint8_t* ip = in + ipos;
+        for (uint32_t i = 0; i < len; ++i) bytes[rel + i] = ip[i];
+      }
+    }
+  }
+  __syncthreads();
+  stamp(5);
   const uint32_t nlong = min(s_nlong, EXEC_LONG);
   for (uint32_t L = 0; L < nlong; ++L) {  // long literals: the whole workgroup
     const uint32_t r = s_long[L];
@@ -561,6 +614,7 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     for (uint32_t i = t; i < len; i += EXEC_T) bytes[rel + i] = ip[i];
   }
   __syncthreads();
+  stamp(6);
   if (s_bad) {  // block-uniform
     if (t == 0) atomicOr(&a.pages_bad[p], 64u);
     return;
@@ -584,6 +638,7 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     uint4* d4 = reinterpret_cast<uint4*>(dst);
 #pragma unroll
     for (int v = 0; v < 4; ++v) d4[v] = make_uint4(word[4 * v], word[4 * v + 1], word[4 * v + 2], word[4 * v + 3]);
+    stamp(7);
   } else {
     const uint32_t m = min(64u, nbytes - my0);
     for (uint32_t i = 0; i < m; ++i) dst[i] = uint8_t(word[i >> 2] >> (8 * (i & 3)));
@@ -640,6 +695,7 @@ void launch_snappy(const SnappyArgs& a, hipStream_t st, void* scan_scratch) {
   hipLaunchKernelGGL(dev::k_snap_scan, dim3(a.npages), dim3(64), 0, st, a);
   launch_scan_u32(a.chunk_elems, a.chunk_rec_start, a.nchunks, scan_scratch, st);
   hipLaunchKernelGGL(dev::k_snap_emit, dim3(a.nwg), dim3(dev::WG_CHUNKS), 0, st, a);
+  hipLaunchKernelGGL(dev::k_snap_block_chunks, dim3((a.nblocks + 255) / 256), dim3(256), 0, st, a);
   hipLaunchKernelGGL(dev::k_snap_exec, dim3(a.nblocks), dim3(dev::EXEC_T), 0, st, a);
   hipLaunchKernelGGL(dev::k_snap_serial, dim3((a.npages + 63) / 64), dim3(64), 0, st, a);
 }

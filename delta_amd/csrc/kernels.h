@@ -132,11 +132,13 @@ struct SnappyArgs {
   uint64_t* chunk_rec_start;    // [nchunks + 1] exclusive scan of chunk_elems
   uint64_t* recs;               // element records (k_snap_emit)
   const uint32_t* block_page;   // [nblocks]
+  uint32_t* block_chunks;       // [2 * nblocks] chunk range of each output block
   uint32_t nblocks;
   const uint32_t* wg_chunk0;    // [nwg] first chunk (global index) of each chunk-walker workgroup
   uint32_t nwg;
   uint32_t* pages_bad;          // [npages] nonzero -> decoded by the serial fallback
   uint32_t* error;
+  uint64_t* stamps;             // diagnostics: [nblocks * 8] k_snap_exec phase clocks, or null
 };
 uint32_t snappy_wg_chunks();
 void launch_snappy(const SnappyArgs& a, hipStream_t st, void* scan_scratch);

@@ -198,7 +198,7 @@ struct PagePlan {
       s_chunk_copies, s_pages_bad;
   DBuf<uint64_t> s_rec_start, s_recs;
   DBuf<uint8_t> s_chunk_flag;
-  DBuf<uint32_t> s_block_chunks;
+  DBuf<uint64_t> s_block_rec;
   DBuf<unsigned long long> s_region_count;
   std::vector<uint32_t> wg_chunk0;
   DBuf<uint32_t> d_wg_chunk0;
@@ -551,7 +551,7 @@ static void plan_pages(StagedData& s, PagePlan& P) {
   P.s_entry = DBuf<uint32_t>(s.ctx, P.nchunks);
   P.s_assumed = DBuf<uint32_t>(s.ctx, P.nchunks);
   P.s_region = DBuf<uint32_t>(s.ctx, P.nchunks);
-  P.s_block_chunks = DBuf<uint32_t>(s.ctx, 2 * P.block_page.size() + 2);
+  P.s_block_rec = DBuf<uint64_t>(s.ctx, P.block_page.size() + 1);
   P.s_chunk_flag = DBuf<uint8_t>(s.ctx, P.nchunks);
   P.s_region_count = DBuf<unsigned long long>(s.ctx, 1);
   P.s_chunk_out = DBuf<uint32_t>(s.ctx, P.nchunks);
@@ -593,7 +593,7 @@ static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_
     P.s_region_count.zero(stream);
     SnappyArgs sa{P.d_snap.p, uint32_t(P.snap_pages.size()), P.d_chunk_base.p, P.nchunks, P.s_spec_exit.p,
                   P.s_vis.p, P.s_entry.p, P.s_assumed.p, P.s_chunk_flag.p, P.s_region.p, P.s_region_count.p, P.s_chunk_out.p, P.s_chunk_out_start.p, P.s_chunk_copies.p,
-                  P.s_rec_start.p, P.s_recs.p, P.d_block_page.p, P.s_block_chunks.p, uint32_t(P.block_page.size()),
+                  P.s_rec_start.p, P.s_recs.p, P.d_block_page.p, P.s_block_rec.p, uint32_t(P.block_page.size()),
                   P.d_wg_chunk0.p, uint32_t(P.wg_chunk0.size()), P.s_pages_bad.p, err.p};
     DBuf<uint64_t> stamps;
     const bool dbg = std::getenv("DR_SNAP_DEBUG") != nullptr;

@@ -367,8 +367,9 @@ __global__ void __launch_bounds__(64) k_snap_scan(SnappyArgs a) {
   if (lane == 0 && carry != a.pages[p].n_out) atomicOr(&a.pages_bad[p], 1u);  // size mismatch
 }
 
-// E: one 8-byte record per element, {output offset in its chunk u16 | (len-1) u16 << 16 |
-// src u32 << 32}; src = copy offset, or REC_LIT | input position for a literal. Records are
+// E: one 8-byte record per element, {output offset in its 64 KiB block u16 | (len-1) u16 << 16 |
+// src u32 << 32}; src = copy offset, or REC_LIT | input position for a literal. The element that
+// starts a block (no element straddles one) records the block's first record index. Records are
 // assembled in LDS per workgroup and written out with coalesced stores.
 constexpr uint32_t REC_LIT = 0x80000000u;
 constexpr uint32_t EMIT_RECS = 4096;  // LDS record slots per workgroup (overflow: direct stores)
@@ -388,13 +389,13 @@ __global__ void __launch_bounds__(WG_CHUNKS) k_snap_emit(SnappyArgs a) {
     const uint64_t cs = uint64_t(j) * SNAP_CH;
     const uint64_t ce = min(cs + SNAP_CH, uint64_t(pg.n_in));
     uint64_t pos = a.entry[c], o = a.chunk_out_start[c];
-    uint32_t orel = 0;
     uint64_t rec = a.chunk_rec_start[c];
     bool bad = false;
     while (pos < ce) {
       const Elem el = snap_decode(staged_u64(buf, s, pos));
-      if (o + el.len > pg.n_out || el.len == 0 || el.len > SNAP_BLOCK || orel > 0xffffu ||
+      if (o + el.len > pg.n_out || el.len == 0 || el.len > SNAP_BLOCK ||
           (o >> 16) != ((o + el.len - 1) >> 16)) { bad = true; break; }
+      if ((o & (SNAP_BLOCK - 1)) == 0) a.block_rec[pg.block_base + uint32_t(o >> 16)] = rec;
       uint32_t src;
       if (el.off == 0) {
         if (pos + el.hdr + el.len > pg.n_in || pos + el.hdr >= REC_LIT) { bad = true; break; }
@@ -403,11 +404,10 @@ __global__ void __launch_bounds__(WG_CHUNKS) k_snap_emit(SnappyArgs a) {
         if (el.off > (o & (SNAP_BLOCK - 1))) { bad = true; break; }  // a copy reaching before its fragment
         src = el.off;
       }
-      const uint64_t r = uint64_t(orel) | (uint64_t(el.len - 1) << 16) | (uint64_t(src) << 32);
+      const uint64_t r = (o & (SNAP_BLOCK - 1)) | (uint64_t(el.len - 1) << 16) | (uint64_t(src) << 32);
       if (in_lds) rbuf[rec - wr0] = r; else a.recs[rec] = r;
       ++rec;
       o += el.len;
-      orel += el.len;
       pos += snap_adv(el);
     }
     if (bad) atomicOr(&a.pages_bad[g.p], 8u);
@@ -418,55 +418,23 @@ __global__ void __launch_bounds__(WG_CHUNKS) k_snap_emit(SnappyArgs a) {
   }
 }
 
-// F: one 1024-thread workgroup per 64 KiB output block.
+// F: one 1024-thread workgroup per 64 KiB output block; its element records are
+// [block_rec[b], block_rec[b+1]) with block-relative output offsets.
 //  1. map[i] = i, then every copy byte i := i - offset (u16 map of the block in LDS);
 //  2. pointer jumping until every byte points at its literal origin (chains of copies of copies
-//     are as long as the number of repeated path prefixes in the fragment; log2 rounds);
+//     are as long as the number of repeated path prefixes in the fragment; log2 rounds; a byte
+//     leaves its thread's pending mask once it points at a root);
 //  3. each thread keeps the roots of its 64 contiguous bytes in registers; the LDS is reused as the
-//     block's bytes: literal runs are copied in from the compressed input;
+//     block's bytes (lower half) and its compressed input range (upper half, 16-byte loads);
+//     literal runs are copied LDS -> LDS;
 //  4. each thread gathers its 64 bytes from their roots and stores them with 16-byte stores.
 constexpr int EXEC_T = 1024;
-constexpr uint32_t EXEC_MAX_CHUNKS = 1024;   // chunks overlapping one block (more: serial fallback)
 constexpr uint32_t EXEC_LONG = 256;          // literal records copied by the whole workgroup
-
-__device__ __forceinline__ uint32_t exec_chunk_of(const uint32_t* tab, uint32_t n, uint32_t r) {
-  uint32_t lo = 0, hi = n;  // last k with tab[k] <= r
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (tab[mid] <= r) lo = mid; else hi = mid;
-  }
-  return lo;
-}
-
-// F0: every output block's chunk range [first chunk whose output reaches past the block start,
-// first chunk starting at or after the block end).
-__global__ void __launch_bounds__(256) k_snap_block_chunks(SnappyArgs a) {
-  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
-  if (b >= a.nblocks) return;
-  const uint32_t p = a.block_page[b];
-  const SnapPage& pg = a.pages[p];
-  const uint64_t bs = uint64_t(b - pg.block_base) * SNAP_BLOCK;
-  const uint64_t be = min(bs + SNAP_BLOCK, uint64_t(pg.n_out));
-  const uint32_t c0 = a.chunk_base[p], c1 = a.chunk_base[p + 1];
-  uint32_t lo = c0, hi = c1;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (uint64_t(a.chunk_out_start[mid]) + a.chunk_out[mid] <= bs) lo = mid + 1; else hi = mid;
-  }
-  a.block_chunks[2 * b] = lo;
-  hi = c1;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (a.chunk_out_start[mid] < be) lo = mid + 1; else hi = mid;
-  }
-  a.block_chunks[2 * b + 1] = lo;
-}
+constexpr uint32_t EXEC_RPT = 12;            // records per thread held in registers per pass
 
 __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
-  __shared__ __attribute__((aligned(16))) uint16_t src[SNAP_BLOCK];  // map, later the block's bytes
-  __shared__ uint32_t c_out[EXEC_MAX_CHUNKS + 1];   // chunk output start - block start (may be < 0)
-  __shared__ uint32_t c_rec[EXEC_MAX_CHUNKS + 1];   // record index - first record of the block
-  __shared__ uint32_t s_bad, s_nlong;
+  __shared__ __attribute__((aligned(16))) uint16_t src[SNAP_BLOCK];  // map, later bytes + input
+  __shared__ uint32_t s_bad, s_nlong, s_inlo, s_inhi;
   __shared__ uint32_t s_long[EXEC_LONG];
   const uint32_t b = blockIdx.x;
   const uint32_t p = a.block_page[b];
@@ -474,8 +442,7 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
   const SnapPage& pg = a.pages[p];
   const uint8_t* in = reinterpret_cast<const uint8_t*>(pg.in);
   uint8_t* out = reinterpret_cast<uint8_t*>(pg.out);
-  const uint32_t k = b - pg.block_base;
-  const uint64_t bs = uint64_t(k) * SNAP_BLOCK;
+  const uint64_t bs = uint64_t(b - pg.block_base) * SNAP_BLOCK;
   const uint64_t be = min(bs + SNAP_BLOCK, uint64_t(pg.n_out));
   const uint32_t nbytes = uint32_t(be - bs);
   const int t = threadIdx.x;
@@ -487,36 +454,48 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
   if (t == 0) {
     s_bad = 0;
     s_nlong = 0;
+    s_inlo = 0xffffffffu;
+    s_inhi = 0;
   }
   for (uint32_t i = t; i < nbytes; i += EXEC_T) src[i] = uint16_t(i);
-  const uint32_t j0 = a.block_chunks[2 * b], nch = a.block_chunks[2 * b + 1] - j0;
-  __syncthreads();
-  if (nch > EXEC_MAX_CHUNKS) {  // block-uniform
-    if (t == 0) atomicOr(&a.pages_bad[p], 16u);
-    return;
-  }
-  const uint64_t r0 = a.chunk_rec_start[j0];
-  for (uint32_t q = t; q <= nch; q += EXEC_T) {
-    c_rec[q] = uint32_t(a.chunk_rec_start[j0 + q] - r0);
-    c_out[q] = q < nch ? uint32_t(int64_t(a.chunk_out_start[j0 + q]) - int64_t(bs)) : 0u;
-  }
+  const uint64_t r0 = a.block_rec[b];
+  const uint64_t r1 = b + 1 < a.nblocks ? a.block_rec[b + 1] : a.chunk_rec_start[a.nchunks];
+  const uint32_t nrec = uint32_t(r1 - r0);
   __syncthreads();
   stamp(1);
-  const int lane = t & 63, wv = t >> 6;
-  // 1. copy bytes point at their sources: one wave per chunk, one lane per record
-  for (uint32_t q = wv; q < nch; q += EXEC_T / 64) {
-    const int32_t cb = int32_t(c_out[q]);
-    for (uint32_t r = c_rec[q] + lane; r < c_rec[q + 1]; r += 64) {
-      const uint64_t w = a.recs[r0 + r];
-      const uint32_t sv = uint32_t(w >> 32);
-      if (sv & REC_LIT) continue;
-      const int64_t o = int64_t(cb) + int64_t(w & 0xffff);
-      const uint32_t len = uint32_t((w >> 16) & 0xffff) + 1;
-      if (o < 0 || o >= int64_t(nbytes)) continue;  // the element belongs to a neighbouring block
-      const uint32_t rel = uint32_t(o);
-      if (sv > rel || rel + len > nbytes) { s_bad = 1; continue; }
+  // 1. copy bytes point at their sources (records loaded EXEC_RPT per thread, all in flight)
+  uint32_t lo_in = 0xffffffffu, hi_in = 0;
+  for (uint32_t base = 0; base < nrec; base += EXEC_T * EXEC_RPT) {
+    uint64_t w[EXEC_RPT];
+#pragma unroll
+    for (uint32_t k = 0; k < EXEC_RPT; ++k) {
+      const uint32_t r = base + k * EXEC_T + uint32_t(t);
+      w[k] = r < nrec ? a.recs[r0 + r] : 0ull;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < EXEC_RPT; ++k) {
+      const uint32_t r = base + k * EXEC_T + uint32_t(t);
+      if (r >= nrec) continue;
+      const uint32_t sv = uint32_t(w[k] >> 32);
+      const uint32_t rel = uint32_t(w[k] & 0xffff);
+      const uint32_t len = uint32_t((w[k] >> 16) & 0xffff) + 1;
+      if (rel + len > nbytes) { s_bad = 1; continue; }
+      if (sv & REC_LIT) {
+        lo_in = min(lo_in, sv & ~REC_LIT);
+        hi_in = max(hi_in, (sv & ~REC_LIT) + len);
+        continue;
+      }
+      if (sv > rel) { s_bad = 1; continue; }
       for (uint32_t i = 0; i < len; ++i) src[rel + i] = uint16_t(rel + i - sv);
     }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    lo_in = min(lo_in, uint32_t(__shfl_xor(int(lo_in), o, 64)));
+    hi_in = max(hi_in, uint32_t(__shfl_xor(int(hi_in), o, 64)));
+  }
+  if ((t & 63) == 0) {
+    atomicMin(&s_inlo, lo_in);
+    atomicMax(&s_inhi, hi_in);
   }
   __syncthreads();
   stamp(2);
@@ -524,8 +503,7 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     if (t == 0) atomicOr(&a.pages_bad[p], 32u);
     return;
   }
-  // 2. pointer jumping over this thread's copy bytes i = t + 1024 k, dropping each byte from its
-  //    pending mask once it points at a root (most chains are short: the pending set halves fast)
+  // 2. pointer jumping over this thread's copy bytes i = t + 1024 k
   uint64_t pend = 0;
 #pragma unroll 4
   for (uint32_t k = 0; k < 64; ++k) {
@@ -546,7 +524,8 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     if (!__syncthreads_or(pend != 0)) break;
   }
   stamp(3);
-  // 3. roots of this thread's 64 bytes -> registers; the LDS becomes the block's bytes
+  // 3. roots of this thread's 64 bytes -> registers; the LDS becomes the block's bytes (lower
+  //    half) and its compressed input range (upper half)
   const uint32_t my0 = uint32_t(t) * 64;
   uint32_t root[32];  // two u16 roots per register
   {
@@ -558,15 +537,11 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     }
   }
   __syncthreads();
-  // the upper half of the map is free now: stage the block's compressed input there (16-byte
-  // loads) so literal runs are copied LDS -> LDS
   uint8_t* bytes = reinterpret_cast<uint8_t*>(src);
   uint8_t* stage = bytes + SNAP_BLOCK;
-  const uint32_t c0 = a.chunk_base[p];
-  const uint64_t in_lo = uint64_t(j0 - c0) * SNAP_CH;
-  const uint64_t in_hi = min(uint64_t(j0 - c0 + nch + 1) * SNAP_CH + 64, uint64_t(pg.n_in));
+  const uint32_t in_lo = s_inlo, in_hi = s_inhi;
   const uintptr_t abs_lo = (reinterpret_cast<uintptr_t>(in) + in_lo) & ~uintptr_t(15);
-  const uint32_t nv = uint32_t((reinterpret_cast<uintptr_t>(in) + in_hi - abs_lo + 15) >> 4);
+  const uint32_t nv = in_lo < in_hi ? uint32_t((reinterpret_cast<uintptr_t>(in) + in_hi - abs_lo + 15) >> 4) : 0u;
   const bool staged = nv * 16 <= SNAP_BLOCK;
   if (staged) {
     const uint4* g4 = reinterpret_cast<const uint4*>(abs_lo);
@@ -575,40 +550,36 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
   }
   __syncthreads();
   stamp(4);
-  for (uint32_t q = wv; q < nch; q += EXEC_T / 64) {
-    const int32_t cb = int32_t(c_out[q]);
-    for (uint32_t r = c_rec[q] + lane; r < c_rec[q + 1]; r += 64) {
-      const uint64_t w = a.recs[r0 + r];
-      const uint32_t sv = uint32_t(w >> 32);
-      if (!(sv & REC_LIT)) continue;
-      const int64_t o = int64_t(cb) + int64_t(w & 0xffff);
-      if (o < 0 || o >= int64_t(nbytes)) continue;
-      const uint32_t len = uint32_t((w >> 16) & 0xffff) + 1;
-      if (len > EXEC_LONG) {
+  for (uint32_t base = 0; base < nrec; base += EXEC_T * EXEC_RPT) {
+    uint64_t w[EXEC_RPT];
+#pragma unroll
+    for (uint32_t k = 0; k < EXEC_RPT; ++k) {
+      const uint32_t r = base + k * EXEC_T + uint32_t(t);
+      w[k] = r < nrec ? a.recs[r0 + r] : 0ull;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < EXEC_RPT; ++k) {
+      const uint32_t r = base + k * EXEC_T + uint32_t(t);
+      const uint32_t sv = uint32_t(w[k] >> 32);
+      if (r >= nrec || !(sv & REC_LIT)) continue;
+      const uint32_t rel = uint32_t(w[k] & 0xffff);
+      const uint32_t len = uint32_t((w[k] >> 16) & 0xffff) + 1;
+      if (len > EXEC_LONG || !staged) {
         const uint32_t slot = atomicAdd(&s_nlong, 1u);
         if (slot < EXEC_LONG) s_long[slot] = r;
         else s_bad = 1;
         continue;
       }
-      const uint32_t rel = uint32_t(o);
-      const uint32_t ipos = sv & ~REC_LIT;
-      if (staged && ipos >= in_lo && ipos + len <= in_hi) {
-        const uint8_t* ip = stage + (reinterpret_cast<uintptr_t>(in) + ipos - abs_lo);
-        for (uint32_t i = 0; i < len; ++i) bytes[rel + i] = ip[i];
-      } else {
-        const uint8_t* ip = in + ipos;
-        for (uint32_t i = 0; i < len; ++i) bytes[rel + i] = ip[i];
-      }
+      const uint8_t* ip = stage + (reinterpret_cast<uintptr_t>(in) + (sv & ~REC_LIT) - abs_lo);
+      for (uint32_t i = 0; i < len; ++i) bytes[rel + i] = ip[i];
     }
   }
   __syncthreads();
   stamp(5);
   const uint32_t nlong = min(s_nlong, EXEC_LONG);
-  for (uint32_t L = 0; L < nlong; ++L) {  // long literals: the whole workgroup
-    const uint32_t r = s_long[L];
-    const uint64_t w = a.recs[r0 + r];
-    const uint32_t q = exec_chunk_of(c_rec, nch, r);
-    const uint32_t rel = uint32_t(int64_t(int32_t(c_out[q])) + int64_t(w & 0xffff));
+  for (uint32_t L = 0; L < nlong; ++L) {  // long literals (or no stage): the whole workgroup
+    const uint64_t w = a.recs[r0 + s_long[L]];
+    const uint32_t rel = uint32_t(w & 0xffff);
     const uint32_t len = uint32_t((w >> 16) & 0xffff) + 1;
     const uint8_t* ip = in + (uint32_t(w >> 32) & ~REC_LIT);
     for (uint32_t i = t; i < len; i += EXEC_T) bytes[rel + i] = ip[i];
@@ -695,7 +666,6 @@ void launch_snappy(const SnappyArgs& a, hipStream_t st, void* scan_scratch) {
   hipLaunchKernelGGL(dev::k_snap_scan, dim3(a.npages), dim3(64), 0, st, a);
   launch_scan_u32(a.chunk_elems, a.chunk_rec_start, a.nchunks, scan_scratch, st);
   hipLaunchKernelGGL(dev::k_snap_emit, dim3(a.nwg), dim3(dev::WG_CHUNKS), 0, st, a);
-  hipLaunchKernelGGL(dev::k_snap_block_chunks, dim3((a.nblocks + 255) / 256), dim3(256), 0, st, a);
   hipLaunchKernelGGL(dev::k_snap_exec, dim3(a.nblocks), dim3(dev::EXEC_T), 0, st, a);
   hipLaunchKernelGGL(dev::k_snap_serial, dim3((a.npages + 63) / 64), dim3(64), 0, st, a);
 }

@@ -132,7 +132,7 @@ struct SnappyArgs {
   uint64_t* chunk_rec_start;    // [nchunks + 1] exclusive scan of chunk_elems
   uint64_t* recs;               // element records (k_snap_emit)
   const uint32_t* block_page;   // [nblocks]
-  uint32_t* block_chunks;       // [2 * nblocks] chunk range of each output block
+  uint64_t* block_rec;          // [nblocks] first element record of each output block
   uint32_t nblocks;
   const uint32_t* wg_chunk0;    // [nwg] first chunk (global index) of each chunk-walker workgroup
   uint32_t nwg;

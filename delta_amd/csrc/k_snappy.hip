@@ -13,7 +13,9 @@
 //                   walked from its true entry. Runs of mis-speculation and chunks spanned by long
 //                   literals send the page to k_snap_resolve from its first such chunk (one wave
 //                   per page, 64 chunks per ballot, spanned chunks skipped in one step).
-//  C k_snap_count   per chunk: output bytes and copy elements of its true elements.
+//  C k_snap_count   per chunk: output bytes and elements of its true elements (counted by the
+//                   speculative walk from the chunk's first visited position; re-walked only when
+//                   the true entry differs).
 //  D k_snap_scan    per page: exclusive scan of chunk outputs (copy counts: a global scan).
 //  E k_snap_emit    per chunk: every element becomes an 8-byte record {chunk-relative output
 //                   offset, length, copy offset | literal input position}, staged in LDS and
@@ -139,18 +141,29 @@ __global__ void __launch_bounds__(WG_CHUNKS) k_snap_spec(SnappyArgs a) {
 #pragma unroll
   for (int k = 0; k < int(SNAP_CH / 32); ++k) vis[k] = 0;
   uint64_t pos = cs >= SNAP_WU ? cs - SNAP_WU : 0;
+  uint64_t first = ~0ull, out = 0;
+  uint32_t elems = 0;
   while (pos < ce) {
+    const Elem el = snap_decode(staged_u64(buf, s, pos));
     if (pos >= cs) {
       const uint32_t r = uint32_t(pos - cs);
 #pragma unroll
       for (int k = 0; k < int(SNAP_CH / 32); ++k)
         if (int(r >> 5) == k) vis[k] |= 1u << (r & 31);
+      if (first == ~0ull) first = pos;
+      out += el.len;
+      ++elems;
     }
-    pos += snap_adv(snap_decode(staged_u64(buf, s, pos)));
+    pos += snap_adv(el);
   }
   a.spec_exit[c] = pos > 0xffffffffull ? 0xffffffffu : uint32_t(pos);
 #pragma unroll
   for (int k = 0; k < int(SNAP_CH / 32); ++k) a.vis[uint64_t(c) * (SNAP_CH / 32) + k] = vis[k];
+  // the chunk's output bytes / elements if its true entry is its first visited position (nearly
+  // always): k_snap_count then only re-walks the exceptions
+  a.spec_first[c] = first > 0xffffffffull ? 0xffffffffu : uint32_t(first);
+  a.chunk_out[c] = out > 0xffffffffull ? 0xffffffffu : uint32_t(out);
+  a.chunk_elems[c] = elems;
 }
 
 // Walks chunk j of a page from `e` (a true element start) to its exit; 8-byte headers from global.
@@ -323,21 +336,22 @@ __global__ void __launch_bounds__(64) k_snap_resolve(SnappyArgs a) {
   }
 }
 
-// C: output bytes / elements produced by the true elements of each chunk.
-__global__ void __launch_bounds__(WG_CHUNKS) k_snap_count(SnappyArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t buf[STAGE_BYTES + 32];
-  const WgInfo g = wg_info(a);
-  const SnapPage& pg = a.pages[g.p];
-  const Staged s = stage_input(buf, reinterpret_cast<const uint8_t*>(pg.in), pg.n_in, g.j0, g.cnt);
-  if (threadIdx.x >= g.cnt) return;
-  const uint32_t j = g.j0 + threadIdx.x;
-  const uint32_t c = a.chunk_base[g.p] + j;
-  const uint64_t cs = uint64_t(j) * SNAP_CH;
+// C: output bytes / elements produced by the true elements of each chunk: the speculative counts
+// unless the true entry differs from the chunk's first speculatively visited position.
+__global__ void __launch_bounds__(256) k_snap_count(SnappyArgs a) {
+  const uint32_t c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= a.nchunks) return;
+  const uint32_t pos0 = a.entry[c];
+  if (pos0 == a.spec_first[c]) return;
+  const uint32_t p = chunk_page(a.chunk_base, a.npages, c);
+  const SnapPage& pg = a.pages[p];
+  const uint64_t cs = uint64_t(c - a.chunk_base[p]) * SNAP_CH;
   const uint64_t ce = min(cs + SNAP_CH, uint64_t(pg.n_in));
-  uint64_t pos = a.entry[c], out = 0;
+  const uint8_t* in = reinterpret_cast<const uint8_t*>(pg.in);
+  uint64_t pos = pos0, out = 0;
   uint32_t elems = 0;
   while (pos < ce) {
-    const Elem el = snap_decode(staged_u64(buf, s, pos));
+    const Elem el = snap_elem(in + pos);
     out += el.len;
     ++elems;
     pos += snap_adv(el);
@@ -486,7 +500,15 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
         continue;
       }
       if (sv > rel) { s_bad = 1; continue; }
-      for (uint32_t i = 0; i < len; ++i) src[rel + i] = uint16_t(rel + i - sv);
+      // consecutive map values rel+i-sv: 4 per 8-byte LDS store once 8-byte aligned
+      uint32_t pos = rel;
+      const uint32_t end = rel + len;
+      while (pos < end && (pos & 3)) { src[pos] = uint16_t(pos - sv); ++pos; }
+      for (; pos + 4 <= end; pos += 4) {
+        const uint64_t v = pos - sv;
+        *reinterpret_cast<uint64_t*>(&src[pos]) = v | ((v + 1) << 16) | ((v + 2) << 32) | ((v + 3) << 48);
+      }
+      for (; pos < end; ++pos) src[pos] = uint16_t(pos - sv);
     }
   }
   for (int o = 32; o > 0; o >>= 1) {
@@ -662,7 +684,7 @@ void launch_snappy(const SnappyArgs& a, hipStream_t st, void* scan_scratch) {
   hipLaunchKernelGGL(dev::k_snap_entries, dim3(g), dim3(256), 0, st, a);
   hipLaunchKernelGGL(dev::k_snap_regions, dim3(g), dim3(256), 0, st, a);
   hipLaunchKernelGGL(dev::k_snap_resolve, dim3(512), dim3(64), 0, st, a);
-  hipLaunchKernelGGL(dev::k_snap_count, dim3(a.nwg), dim3(dev::WG_CHUNKS), 0, st, a);
+  hipLaunchKernelGGL(dev::k_snap_count, dim3(g), dim3(256), 0, st, a);
   hipLaunchKernelGGL(dev::k_snap_scan, dim3(a.npages), dim3(64), 0, st, a);
   launch_scan_u32(a.chunk_elems, a.chunk_rec_start, a.nchunks, scan_scratch, st);
   hipLaunchKernelGGL(dev::k_snap_emit, dim3(a.nwg), dim3(dev::WG_CHUNKS), 0, st, a);

@@ -122,6 +122,7 @@ struct SnappyArgs {
   uint32_t* spec_exit;          // [nchunks]
   uint32_t* vis;                // [nchunks * 8] visited-position bitmaps
   uint32_t* entry;              // [nchunks] true first element position >= chunk start
+  uint32_t* spec_first;         // [nchunks] first speculatively visited position >= chunk start
   uint32_t* assumed_exit;       // [nchunks] exit assuming the previous chunk's speculative exit
   uint8_t* chunk_flag;          // [nchunks] 1: serial resolution from this chunk
   uint32_t* region;             // [nchunks] chunks starting a serially resolved region

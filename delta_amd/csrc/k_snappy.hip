@@ -70,6 +70,19 @@ __device__ __forceinline__ Elem snap_decode(uint64_t w) {
 __device__ __forceinline__ Elem snap_elem(const uint8_t* p) { return snap_decode(load_u64(p)); }
 __device__ __forceinline__ uint64_t snap_adv(const Elem& e) { return uint64_t(e.hdr) + (e.off ? 0u : e.len); }
 
+// Input bytes an element occupies and the output bytes it produces, without branches (the
+// speculative walkers only need these; lanes then never split on the element type).
+__device__ __forceinline__ void snap_step(uint64_t w, uint32_t* adv, uint32_t* out) {
+  const uint32_t tag = uint32_t(w & 0xff), t = tag & 3, l6 = tag >> 2;
+  const uint32_t nb = l6 >= 60 ? l6 - 59 : 0;                        // long literal: length bytes
+  const uint32_t lmask = nb >= 4 ? 0xffffffffu : ((1u << (8 * nb)) - 1u);
+  const uint32_t lit_len = nb ? uint32_t(w >> 8) & lmask : l6;      // minus one
+  const uint32_t hdr = t == 0 ? 1 + nb : ((0x5320u >> (4 * t)) & 0xfu);
+  const uint32_t len = t == 0 ? lit_len + 1 : t == 1 ? ((l6 & 7) + 4) : l6 + 1;
+  *out = len;
+  *adv = hdr + (t == 0 ? len : 0u);
+}
+
 __device__ __forceinline__ uint32_t chunk_page(const uint32_t* chunk_base, uint32_t npages, uint32_t c) {
   uint32_t lo = 0, hi = npages;  // last page with chunk_base[p] <= c
   while (hi - lo > 1) {
@@ -144,17 +157,18 @@ __global__ void __launch_bounds__(WG_CHUNKS) k_snap_spec(SnappyArgs a) {
   uint64_t first = ~0ull, out = 0;
   uint32_t elems = 0;
   while (pos < ce) {
-    const Elem el = snap_decode(staged_u64(buf, s, pos));
+    uint32_t adv, len;
+    snap_step(staged_u64(buf, s, pos), &adv, &len);
     if (pos >= cs) {
       const uint32_t r = uint32_t(pos - cs);
 #pragma unroll
       for (int k = 0; k < int(SNAP_CH / 32); ++k)
         if (int(r >> 5) == k) vis[k] |= 1u << (r & 31);
       if (first == ~0ull) first = pos;
-      out += el.len;
+      out += len;
       ++elems;
     }
-    pos += snap_adv(el);
+    pos += adv;
   }
   a.spec_exit[c] = pos > 0xffffffffull ? 0xffffffffu : uint32_t(pos);
 #pragma unroll

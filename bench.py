@@ -31,9 +31,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # Stages whose timed region is exactly one kernel launch: the roofline is reported for the slowest
 # of these (achieved = its algorithmic bytes / its hipEvent-timed duration on the replay stream).
 STAGE_KERNEL = {
-    "json_parse": "k_json_parse",
+    "json_parse": "k_json_lines",
     "json_newlines": "k_json_newlines",
-    "pq_bounds": "k_ba_bounds",
     "ckpt_assemble": "k_ckpt_assemble",
     "partition_hist": "k_bucket_hist",
     "partition_scatter": "k_bucket_scatter",

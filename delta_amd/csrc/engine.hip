@@ -205,8 +205,11 @@ struct PagePlan {
   uint64_t snap_in_bytes = 0;
   // PLAIN BYTE_ARRAY boundary scratch (k_ba_bounds)
   uint32_t ba_pages = 0;
-  uint64_t ba_vals = 0, ba_hits = 0;
-  DBuf<uint32_t> s_ba_vals, s_ba_hit, s_ba_ok, s_ba_count;
+  uint64_t ba_vals = 0;
+  std::vector<uint2> ba_tiles;
+  DBuf<uint2> d_ba_tiles;
+  DBuf<uint32_t> s_ba_vals, s_ba_ok, s_ba_count, s_ba_tile_cnt;
+  DBuf<uint64_t> s_ba_tile_off;
 };
 
 struct StagedData {
@@ -483,9 +486,10 @@ static void plan_pages(StagedData& s, PagePlan& P) {
             d.ba = 1;
             d.ba_slot = P.ba_pages++;
             d.ba_base = P.ba_vals;
-            d.hit_base = P.ba_hits;
+            d.hit_base = P.ba_tiles.size();
             P.ba_vals += d.usize / 4 + 2;
-            P.ba_hits += d.usize / 32 + 4;
+            const uint32_t nt = uint32_t((uint64_t(d.usize) + 15) / ba_tile_bytes() + 1);
+            for (uint32_t t = 0; t < nt; ++t) P.ba_tiles.push_back(make_uint2(uint32_t(P.pages.size()), t));
           }
           P.pages.push_back(d);
         }
@@ -562,7 +566,9 @@ static void plan_pages(StagedData& s, PagePlan& P) {
   P.s_recs = DBuf<uint64_t>(s.ctx, P.snap_in_bytes / 2 + 1);  // an element takes >= 2 input bytes
   P.s_pages_bad = DBuf<uint32_t>(s.ctx, P.snap_pages.size());
   P.s_ba_vals = DBuf<uint32_t>(s.ctx, P.ba_vals);
-  P.s_ba_hit = DBuf<uint32_t>(s.ctx, P.ba_hits);
+  up(P.d_ba_tiles, P.ba_tiles);
+  P.s_ba_tile_cnt = DBuf<uint32_t>(s.ctx, P.ba_tiles.size());
+  P.s_ba_tile_off = DBuf<uint64_t>(s.ctx, P.ba_tiles.size() + 1);
   P.s_ba_ok = DBuf<uint32_t>(s.ctx, P.ba_pages);
   P.s_ba_count = DBuf<uint32_t>(s.ctx, P.ba_pages);
   for (PageDesc& d : P.pages) {
@@ -584,7 +590,11 @@ static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_
   pa.dict_len = dict_len.p;
   pa.error = err.p;
   pa.ba_vals = P.s_ba_vals.p;
-  pa.ba_hit = P.s_ba_hit.p;
+  pa.ba_hit = nullptr;
+  pa.ba_tiles = P.d_ba_tiles.p;
+  pa.nba_tiles = uint32_t(P.ba_tiles.size());
+  pa.ba_tile_cnt = P.s_ba_tile_cnt.p;
+  pa.ba_tile_off = P.s_ba_tile_off.p;
   pa.ba_ok = P.s_ba_ok.p;
   pa.ba_count = P.s_ba_count.p;
   launch_page_copy(P.d_copy.p, uint32_t(P.copy_jobs.size()), stream);
@@ -626,7 +636,15 @@ static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_
     }
   }
   ctx->mark("pq_inflate");
-  if (P.ba_pages) launch_ba_bounds(pa, stream);
+  if (P.ba_pages) {
+    launch_ba_bounds(pa, stream, scratch);
+    if (std::getenv("DR_BA_DEBUG")) {
+      std::vector<uint32_t> ok = d2h(P.s_ba_ok.p, P.ba_pages, stream);
+      size_t n = 0;
+      for (uint32_t v : ok) n += v != 0;
+      std::fprintf(stderr, "ba bounds: %zu of %u pages validated\n", n, P.ba_pages);
+    }
+  }
   ctx->mark("pq_bounds");
   launch_pq_dict(pa, stream);
   launch_pq_data(pa, stream);

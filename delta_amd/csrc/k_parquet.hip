@@ -137,13 +137,14 @@ struct ByteArrayWalker {
 // ---- parallel boundaries of length-prefixed BYTE_ARRAY values -----------------------------------------
 // PLAIN BYTE_ARRAY values are [u32 len][bytes]...: a serial chain. For strings without NUL bytes and
 // lengths < 64 KiB every true boundary p has b[p+2] == b[p+3] == 0 while no position inside a string
-// does (paths are URI strings). One workgroup per page: candidates are positions with two zero bytes
-// at +2/+3 whose value fits the page; a candidate is kept if it is the region start or the target of
-// another candidate, and if its own successor is a candidate or the region end. The survivors are
-// compacted in order and the chain is then VALIDATED -- B[0] = start, B[k+1] = B[k] + 4 + len(B[k]),
-// the last value ends at the region end -- which proves B equals the true chain. Any failure
-// (NUL bytes, huge values, corrupt data) leaves ba_ok = 0 and the serial walker decodes the page.
+// does (paths are URI strings). A candidate is a position with two zero bytes at +2/+3 whose value
+// fits the page and whose successor is a candidate or the region end. Pages are cut into 4 KiB tiles
+// (all pages' tiles in one grid): tiles count their candidates, a global scan orders them, tiles
+// write them, and the chain is then VALIDATED -- B[0] = start, B[k+1] = B[k] + 4 + len(B[k]), the
+// last value ends at the region end -- which proves B equals the true chain. Any failure (NUL
+// bytes, huge values, corrupt data) leaves ba_ok = 0 and the serial walker decodes the page.
 constexpr int BA_T = 256;
+constexpr uint32_t BA_TILE = BA_T * 16;
 
 __device__ __forceinline__ bool ba_region(const PageDesc& pg, const uint8_t** b, const uint8_t** e) {
   const uint8_t* p = reinterpret_cast<const uint8_t*>(pg.dst);
@@ -169,110 +170,146 @@ __device__ __forceinline__ bool ba_cand(const uint8_t* b, uint64_t S, uint64_t p
   const uint32_t w = load_u32(b + p);
   if (w >> 16) return false;  // bytes +2/+3 must be zero
   const uint64_t nx = p + 4 + w;
-  if (nx > S) return false;
+  if (nx > S || (w && !b[p + 4])) return false;
   *next = nx;
   return true;
 }
 
-__global__ void __launch_bounds__(BA_T) k_ba_bounds(ParquetArgs a) {
-  const PageDesc& pg = a.pages[blockIdx.x];
-  if (!pg.ba) return;
-  __shared__ uint32_t wcnt[BA_T];
-  __shared__ uint32_t s_bad, s_n;
-  const int t = threadIdx.x;
+// Bit j of the result: region offset (tile base + 16 t + j) is a kept candidate. The thread's 16
+// positions are 16-byte aligned in absolute address; their +2/+3 bytes come from two 16-byte loads.
+__device__ __forceinline__ uint32_t ba_kept(const uint8_t* b, uint64_t S, int64_t q0) {
+  if (q0 + 16 <= 0 || q0 >= int64_t(S)) return 0u;
+  const uint4* a4 = reinterpret_cast<const uint4*>(b + q0);  // 16-byte aligned by construction
+  const uint4 x = a4[0], y = a4[1];
+  const uint32_t w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+  uint32_t z = 0;
+#pragma unroll
+  for (int d = 0; d < 8; ++d) {
+    const uint32_t v = w[d];
+    const uint32_t zb = ~(((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v | 0x7F7F7F7Fu);  // 0x80 per zero byte
+    uint32_t g = zb >> 7;
+    g |= g >> 7;
+    g |= g >> 14;
+    z |= (g & 0xFu) << (4 * d);
+  }
+  // A true boundary's zero run (the length's high bytes) ends at +3: the string's first byte is
+  // non-zero unless the string is empty (all four length bytes zero). This drops the shifted
+  // candidates inside the run (p-1 when len < 256), which would otherwise survive the successor
+  // check by chance.
+  const uint32_t cm = ((z >> 2) & (z >> 3) & (~(z >> 4) | (z & (z >> 1)))) & 0xFFFFu;
+  uint32_t kept = 0;
+  for (uint32_t m = cm; m;) {
+    const int j = __builtin_ctz(m);
+    m &= m - 1;
+    const int64_t p = q0 + j;
+    if (p < 0) continue;
+    uint64_t nx, nn;
+    if (ba_cand(b, S, uint64_t(p), &nx) && (nx == S || ba_cand(b, S, nx, &nn))) kept |= 1u << j;
+  }
+  return kept;
+}
+
+struct BaTile {
+  const PageDesc* pg;
+  const uint8_t* b;
+  uint64_t S;
+  int64_t q0;      // region offset of this thread's first position
+  bool ok;
+};
+__device__ __forceinline__ BaTile ba_tile(const ParquetArgs& a, uint32_t tile) {
+  const uint2 tp = a.ba_tiles[tile];
+  BaTile r;
+  r.pg = &a.pages[tp.x];
   const uint8_t *b, *e;
-  if (!ba_region(pg, &b, &e)) { if (t == 0) a.ba_ok[pg.ba_slot] = 0; return; }
-  const uint64_t S = uint64_t(e - b);
-  uint32_t* hit = a.ba_hit + pg.hit_base;
+  r.ok = ba_region(*r.pg, &b, &e);
+  r.b = b;
+  r.S = r.ok ? uint64_t(e - b) : 0;
+  const int64_t lead = int64_t(reinterpret_cast<uintptr_t>(b) & 15);  // tiles are absolute-aligned
+  r.q0 = -lead + int64_t(tp.y) * BA_TILE + 16 * int64_t(threadIdx.x);
+  return r;
+}
+
+__device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* red) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t s = 0;
+  for (int k = 0; k < BA_T / 64; ++k) s += red[k];
+  return s;
+}
+
+// T1: kept candidates per tile.
+__global__ void __launch_bounds__(BA_T) k_ba_count(ParquetArgs a) {
+  __shared__ uint32_t red[BA_T / 64];
+  const BaTile tl = ba_tile(a, blockIdx.x);
+  const uint32_t c = tl.ok ? uint32_t(__builtin_popcount(ba_kept(tl.b, tl.S, tl.q0))) : 0u;
+  const uint32_t s = block_sum(c, red);
+  if (threadIdx.x == 0) {
+    a.ba_tile_cnt[blockIdx.x] = s;
+    if (a.ba_tiles[blockIdx.x].y == 0) a.ba_ok[tl.pg->ba_slot] = tl.ok ? 1u : 0u;
+  }
+}
+
+// T2: kept candidates written in order (page-relative rank = scanned tile offset + block prefix).
+__global__ void __launch_bounds__(BA_T) k_ba_write(ParquetArgs a) {
+  __shared__ uint32_t wsum[BA_T / 64];
+  const BaTile tl = ba_tile(a, blockIdx.x);
+  if (!tl.ok) return;
+  const PageDesc& pg = *tl.pg;
+  uint32_t km = ba_kept(tl.b, tl.S, tl.q0);
+  const uint32_t c = uint32_t(__builtin_popcount(km));
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t incl = c;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t v = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) wsum[wv] = incl;
+  __syncthreads();
+  uint32_t woff = 0;
+  for (int k = 0; k < wv; ++k) woff += wsum[k];
+  const uint32_t first = uint32_t(pg.hit_base);  // the page's first tile
+  const uint64_t rank0 = a.ba_tile_off[blockIdx.x] - a.ba_tile_off[first] + woff + incl - c;
+  const uint64_t cap = pg.usize / 4 + 2;
+  const uint64_t boff = uint64_t(tl.b - reinterpret_cast<const uint8_t*>(pg.dst));
   uint32_t* vals = a.ba_vals + pg.ba_base;
-  const uint32_t cap = pg.usize / 4 + 2;  // slots reserved for this page by the planner
-  const uint64_t nw = S / 32 + 2;
-  for (uint64_t i = t; i < nw; i += BA_T) hit[i] = 0;
-  if (t == 0) s_bad = 0;
-  __syncthreads();
-  // Each thread scans 16 consecutive positions per 4 KiB segment (coalesced 16-byte loads); a
-  // zero-byte-pair mask finds the rare candidates, which are then checked exactly.
-  constexpr uint64_t SEGB = uint64_t(BA_T) * 16;
-  auto cand_mask = [&](uint64_t p0) -> uint32_t {  // bit j: position p0 + j has zero bytes at +2/+3
-    if (p0 >= S) return 0u;
-    uint32_t w[5];
-#pragma unroll
-    for (int q = 0; q < 5; ++q) w[q] = load_u32(b + p0 + 4 * q);  // buffers are padded
-    uint32_t z = 0;
-#pragma unroll
-    for (int q = 0; q < 5; ++q)
-#pragma unroll
-      for (int y = 0; y < 4; ++y) z |= uint32_t(((w[q] >> (8 * y)) & 0xff) == 0) << (4 * q + y);
-    return ((z & (z >> 1)) >> 2) & 0xffffu;
-  };
-  // pass 1: every candidate marks its successor
-  for (uint64_t seg = 0; seg < S; seg += SEGB) {
-    const uint64_t p0 = seg + 16ull * t;
-    uint32_t m = cand_mask(p0);
-    while (m) {
-      const int j = __builtin_ctz(m);
-      m &= m - 1;
-      uint64_t nx;
-      if (ba_cand(b, S, p0 + j, &nx) && nx < S) atomicOr(&hit[nx >> 5], 1u << (nx & 31));
-    }
+  uint64_t o = rank0;
+  while (km) {
+    const int j = __builtin_ctz(km);
+    km &= km - 1;
+    if (o < cap) vals[o] = uint32_t(uint64_t(tl.q0 + j) + boff);
+    ++o;
   }
-  __threadfence();
-  __syncthreads();
-  // pass 2: survivors, scanned per segment, written in order
-  auto keep = [&](uint64_t p) -> bool {
-    uint64_t nx;
-    if (!ba_cand(b, S, p, &nx)) return false;
-    if (p != 0 && !((__hip_atomic_load(&hit[p >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (p & 31)) & 1u)) return false;
-    uint64_t nn;
-    return nx == S || ba_cand(b, S, nx, &nn);
-  };
-  const uint64_t boff0 = uint64_t(b - reinterpret_cast<const uint8_t*>(pg.dst));
-  uint32_t carry = 0;
-  const int lane = t & 63, wv = t >> 6;
-  for (uint64_t seg = 0; seg < S; seg += SEGB) {
-    const uint64_t p0 = seg + 16ull * t;
-    uint32_t m = cand_mask(p0), km = 0;
-    while (m) {
-      const int j = __builtin_ctz(m);
-      m &= m - 1;
-      if (keep(p0 + j)) km |= 1u << j;
-    }
-    const uint32_t c = __builtin_popcount(km);
-    uint32_t incl = c;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t v = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += v;
-    }
-    if (lane == 63) wcnt[wv] = incl;
-    __syncthreads();
-    uint32_t woff = 0, tot = 0;
-    for (int k = 0; k < BA_T / 64; ++k) { if (k < wv) woff += wcnt[k]; tot += wcnt[k]; }
-    uint32_t o = carry + woff + incl - c;
-    while (km) {
-      const int j = __builtin_ctz(km);
-      km &= km - 1;
-      if (o < cap) vals[o] = uint32_t(p0 + j + boff0);
-      ++o;
-    }
-    carry += tot;
-    __syncthreads();
+  // the page's last tile publishes the count
+  const bool last = blockIdx.x + 1 == a.nba_tiles || a.ba_tiles[blockIdx.x + 1].x != a.ba_tiles[blockIdx.x].x;
+  if (threadIdx.x == 0 && last)
+    a.ba_count[pg.ba_slot] = uint32_t(a.ba_tile_off[blockIdx.x + 1] - a.ba_tile_off[first]);
+}
+
+// T3: chain validation, one thread per value of the tile's rank range.
+__global__ void __launch_bounds__(BA_T) k_ba_check(ParquetArgs a) {
+  const BaTile tl = ba_tile(a, blockIdx.x);
+  if (!tl.ok) return;
+  const PageDesc& pg = *tl.pg;
+  const uint32_t first = uint32_t(pg.hit_base);
+  const uint64_t n = a.ba_count[pg.ba_slot];
+  const uint64_t cap = pg.usize / 4 + 2;
+  const uint64_t boff = uint64_t(tl.b - reinterpret_cast<const uint8_t*>(pg.dst));
+  if (n > cap) {
+    if (threadIdx.x == 0) a.ba_ok[pg.ba_slot] = 0;
+    return;
   }
-  if (t == 0) { a.ba_count[pg.ba_slot] = carry; s_n = carry; }
-  __threadfence();
-  __syncthreads();
-  // validation of the chain (a true chain has at most usize/4 values: each takes >= 4 bytes)
-  if (s_n > cap) { if (t == 0) a.ba_ok[pg.ba_slot] = 0; return; }
-  const uint32_t n = s_n;
-  const uint64_t boff = uint64_t(b - reinterpret_cast<const uint8_t*>(pg.dst));
-  if (S > 0 && (n == 0 || vals[0] != boff)) s_bad = 1;
-  for (uint32_t k = t; k < n; k += BA_T) {
+  const uint32_t* vals = a.ba_vals + pg.ba_base;
+  const uint64_t r0 = a.ba_tile_off[blockIdx.x] - a.ba_tile_off[first];
+  const uint64_t r1 = a.ba_tile_off[blockIdx.x + 1] - a.ba_tile_off[first];
+  bool bad = blockIdx.x == first && tl.S > 0 && (n == 0 || vals[0] != boff);
+  for (uint64_t k = r0 + threadIdx.x; k < r1; k += BA_T) {
     const uint64_t p = vals[k] - boff;
-    const uint64_t nx = p + 4 + load_u32(b + p);
-    const uint64_t want = k + 1 < n ? uint64_t(vals[k + 1]) - boff : S;
-    if (nx != want) s_bad = 1;
+    const uint64_t nx = p + 4 + load_u32(tl.b + p);
+    const uint64_t want = k + 1 < n ? uint64_t(vals[k + 1]) - boff : tl.S;
+    if (nx != want) bad = true;
   }
-  __syncthreads();
-  if (t == 0) a.ba_ok[pg.ba_slot] = s_bad ? 0u : 1u;
+  if (bad) a.ba_ok[pg.ba_slot] = 0;
 }
 
 // ---- dictionary pages --------------------------------------------------------------------------------
@@ -530,8 +567,13 @@ __global__ void k_ckpt_assemble(CkptAssembleArgs a) {
 
 }  // namespace dev
 
-void launch_ba_bounds(const ParquetArgs& a, hipStream_t st) {
-  if (a.npages) hipLaunchKernelGGL(dev::k_ba_bounds, dim3(a.npages), dim3(dev::BA_T), 0, st, a);
+uint32_t ba_tile_bytes() { return dev::BA_TILE; }
+void launch_ba_bounds(const ParquetArgs& a, hipStream_t st, void* scan_scratch) {
+  if (!a.nba_tiles) return;
+  hipLaunchKernelGGL(dev::k_ba_count, dim3(a.nba_tiles), dim3(dev::BA_T), 0, st, a);
+  launch_scan_u32(a.ba_tile_cnt, a.ba_tile_off, a.nba_tiles, scan_scratch, st);
+  hipLaunchKernelGGL(dev::k_ba_write, dim3(a.nba_tiles), dim3(dev::BA_T), 0, st, a);
+  hipLaunchKernelGGL(dev::k_ba_check, dim3(a.nba_tiles), dim3(dev::BA_T), 0, st, a);
 }
 void launch_pq_dict(const ParquetArgs& a, hipStream_t st) {
   if (a.npages) hipLaunchKernelGGL(dev::k_pq_dict, dim3(a.npages), dim3(64), 0, st, a);

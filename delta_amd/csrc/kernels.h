@@ -80,7 +80,7 @@ struct PageDesc {
   int32_t ba;            // 1 if this page's values are length-prefixed byte arrays
   uint32_t ba_slot;      // index into ba_ok / ba_count
   uint64_t ba_base;      // first u32 slot of this page's value offsets
-  uint64_t hit_base;     // first u32 word of this page's hit bitmap
+  uint64_t hit_base;     // index of this page's first 4 KiB boundary tile (ParquetArgs::ba_tiles)
 };
 
 // Decoded column: one entry per checkpoint row (flat leaf) or per level entry (repeated leaf).
@@ -101,11 +101,16 @@ struct ParquetArgs {
   uint32_t* dict_len;
   uint32_t* error;       // first error code (0 = ok)
   uint32_t* ba_vals;     // value offsets (relative to the page's decompressed body)
-  uint32_t* ba_hit;      // hit bitmaps
+  uint32_t* ba_hit;      // unused (kept for layout)
   uint32_t* ba_ok;       // [pages with ba] 1 = boundaries found and validated
   uint32_t* ba_count;    // [pages with ba] number of values found
+  const uint2* ba_tiles; // [nba_tiles] (page index, tile index within the page's value region)
+  uint32_t nba_tiles;
+  uint32_t* ba_tile_cnt; // [nba_tiles]
+  uint64_t* ba_tile_off; // [nba_tiles + 1] exclusive scan of ba_tile_cnt
 };
-void launch_ba_bounds(const ParquetArgs& a, hipStream_t st);
+uint32_t ba_tile_bytes();
+void launch_ba_bounds(const ParquetArgs& a, hipStream_t st, void* scan_scratch);
 
 // SNAPPY pages (k_snappy.hip). `in` points past the varint length preamble.
 struct SnapPage {

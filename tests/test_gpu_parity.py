@@ -158,3 +158,19 @@ def test_checkpoint_page_layouts(engine, tmp_path, page_size, compression, page_
         _assert_same(st, snap)
     finally:
         st.release()
+
+
+def test_checkpoint_boundaries_found_in_parallel(engine, tmp_path, capfd, monkeypatch):
+    """Every PLAIN BYTE_ARRAY page of a synthetic checkpoint is split by the parallel boundary
+    kernels (k_ba_count/write/check) and validated, so none falls back to the serial walker
+    (the fallback is exact too, so parity alone would not notice)."""
+    from delta_amd.testing import synth as S
+    exp = S.build_config(3, str(tmp_path), scale=0.005)
+    monkeypatch.setenv("DR_BA_DEBUG", "1")
+    st = _gpu_replay(engine, os.path.join(str(tmp_path), "_delta_log"), exp.min_file_retention_timestamp)
+    st.release()
+    found = [l for l in capfd.readouterr().err.splitlines() if l.startswith("ba bounds:")]
+    assert found
+    for l in found:
+        w = l.split()
+        assert int(w[2]) == int(w[4]) > 0, l

@@ -459,11 +459,13 @@ __global__ void __launch_bounds__(WG_CHUNKS) k_snap_emit(SnappyArgs a) {
 constexpr int EXEC_T = 1024;
 constexpr uint32_t EXEC_LONG = 256;          // literal records copied by the whole workgroup
 constexpr uint32_t EXEC_RPT = 12;            // records per thread held in registers per pass
+constexpr uint32_t EXEC_RPT2 = 4;            // literal records per thread per pass (roots live in registers)
 
 __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t src[SNAP_BLOCK];  // map, later bytes + input
   __shared__ uint32_t s_bad, s_nlong, s_inlo, s_inhi;
   __shared__ uint32_t s_long[EXEC_LONG];
+  __shared__ uint32_t starts[SNAP_BLOCK / 32];  // element start bits
   const uint32_t b = blockIdx.x;
   const uint32_t p = a.block_page[b];
   if (a.pages_bad[p]) return;
@@ -485,13 +487,14 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     s_inlo = 0xffffffffu;
     s_inhi = 0;
   }
-  for (uint32_t i = t; i < nbytes; i += EXEC_T) src[i] = uint16_t(i);
+  for (uint32_t w = t; w < SNAP_BLOCK / 32; w += EXEC_T) starts[w] = 0;
   const uint64_t r0 = a.block_rec[b];
   const uint64_t r1 = b + 1 < a.nblocks ? a.block_rec[b + 1] : a.chunk_rec_start[a.nchunks];
   const uint32_t nrec = uint32_t(r1 - r0);
   __syncthreads();
   stamp(1);
-  // 1. copy bytes point at their sources (records loaded EXEC_RPT per thread, all in flight)
+  // 1a. per element: its start bit, and the map entry of its first byte (start - offset; a
+  //     literal points at itself)
   uint32_t lo_in = 0xffffffffu, hi_in = 0;
   for (uint32_t base = 0; base < nrec; base += EXEC_T * EXEC_RPT) {
     uint64_t w[EXEC_RPT];
@@ -508,21 +511,15 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
       const uint32_t rel = uint32_t(w[k] & 0xffff);
       const uint32_t len = uint32_t((w[k] >> 16) & 0xffff) + 1;
       if (rel + len > nbytes) { s_bad = 1; continue; }
+      atomicOr(&starts[rel >> 5], 1u << (rel & 31));
       if (sv & REC_LIT) {
         lo_in = min(lo_in, sv & ~REC_LIT);
         hi_in = max(hi_in, (sv & ~REC_LIT) + len);
-        continue;
+        src[rel] = uint16_t(rel);
+      } else {
+        if (sv > rel || len > 64) { s_bad = 1; continue; }  // snappy copies are at most 64 bytes
+        src[rel] = uint16_t(rel - sv);
       }
-      if (sv > rel) { s_bad = 1; continue; }
-      // consecutive map values rel+i-sv: 4 per 8-byte LDS store once 8-byte aligned
-      uint32_t pos = rel;
-      const uint32_t end = rel + len;
-      while (pos < end && (pos & 3)) { src[pos] = uint16_t(pos - sv); ++pos; }
-      for (; pos + 4 <= end; pos += 4) {
-        const uint64_t v = pos - sv;
-        *reinterpret_cast<uint64_t*>(&src[pos]) = v | ((v + 1) << 16) | ((v + 2) << 32) | ((v + 3) << 48);
-      }
-      for (; pos < end; ++pos) src[pos] = uint16_t(pos - sv);
     }
   }
   for (int o = 32; o > 0; o >>= 1) {
@@ -539,31 +536,74 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     if (t == 0) atomicOr(&a.pages_bad[p], 32u);
     return;
   }
-  // 2. pointer jumping over this thread's copy bytes i = t + 1024 k
-  uint64_t pend = 0;
-#pragma unroll 4
-  for (uint32_t k = 0; k < 64; ++k) {
-    const uint32_t i = uint32_t(t) + EXEC_T * k;
-    if (i < nbytes && src[i] != i) pend |= 1ull << k;
-  }
-  for (int round = 0; round < 17; ++round) {
-    uint64_t m = pend;
-    while (m) {
-      const uint32_t k = uint32_t(__builtin_ctzll(m));
-      m &= m - 1;
-      const uint32_t i = uint32_t(t) + EXEC_T * k;
-      const uint32_t x = src[i];
-      const uint32_t y = src[x];
-      if (y == x) pend &= ~(1ull << k);
-      else src[i] = uint16_t(y);
+  // Byte ownership: thread t owns the 4-byte groups i0 = 4 (t + 1024 j), j < 16; k = 4 j + e.
+  // 1b. every byte's element starts at the last start bit <= it. A copy is at most 64 bytes long,
+  //     so a byte with no start in the 64 bytes up to it lies in a long literal. Copy bytes point
+  //     at i - offset, literal bytes at themselves (i - start + src[start] covers both). Each group
+  //     is read and written as one 8-byte word; element starts keep their value, so reading
+  //     src[start] never races.
+  // 2. pointer jumping over the same bytes, current pointers in registers. No barriers: every value
+  //    read is an ancestor of the byte (older or newer, both valid) and ancestors have smaller
+  //    indices, so each step strictly moves towards the root (literal bytes are their own roots).
+  //    Pointers are read 8 at a time so the LDS reads are in flight together.
+  uint32_t root[32];  // roots of this thread's 64 contiguous output bytes, two u16 per register
+  {
+    uint32_t x[64];     // current pointers of the 4-byte groups
+    uint32_t act = 0;   // groups with a byte not yet at its root
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) {
+      const uint32_t i0 = 4 * (uint32_t(t) + EXEC_T * j);
+      const uint32_t wi = i0 >> 5, sh = i0 & 31;
+      const uint32_t w0 = starts[wi];
+      const uint32_t w1 = wi ? starts[wi - 1] : 0u;
+      const uint32_t w2 = wi > 1 ? starts[wi - 2] : 0u;
+      const uint32_t m0 = w0 & ((1u << sh) - 1u);
+      const uint32_t prev = m0   ? wi * 32 + 31 - __builtin_clz(m0)
+                            : w1 ? wi * 32 - 1 - __builtin_clz(w1)
+                            : w2 ? wi * 32 - 33 - __builtin_clz(w2)
+                                 : 0xffffffffu;
+      const uint2 g = *reinterpret_cast<const uint2*>(&src[i0]);
+      const uint32_t sv[4] = {g.x & 0xffffu, g.x >> 16, g.y & 0xffffu, g.y >> 16};
+      uint32_t cst = prev, cval = prev != 0xffffffffu ? uint32_t(src[prev < SNAP_BLOCK ? prev : 0]) : 0u;
+#pragma unroll
+      for (uint32_t e = 0; e < 4; ++e) {
+        const uint32_t i = i0 + e;
+        if ((w0 >> (sh + e)) & 1u) { cst = i; cval = sv[e]; }
+        x[4 * j + e] = (cst != 0xffffffffu && i - cst < 64 && i < nbytes) ? i - cst + cval : i;
+      }
+      if (i0 < nbytes)
+        *reinterpret_cast<uint2*>(&src[i0]) =
+            make_uint2(x[4 * j] | (x[4 * j + 1] << 16), x[4 * j + 2] | (x[4 * j + 3] << 16));
     }
-    if (!__syncthreads_or(pend != 0)) break;
+    __syncthreads();
+    stamp(3);
+#pragma unroll
+    for (uint32_t k = 0; k < 64; ++k)
+      if (x[k] != 4 * (uint32_t(t) + EXEC_T * (k >> 2)) + (k & 3)) act |= 1u << (k >> 2);
+    while (act) {
+#pragma unroll
+      for (uint32_t j = 0; j < 16; ++j) {
+        if (act & (1u << j)) {
+          uint32_t y[4];
+#pragma unroll
+          for (uint32_t e = 0; e < 4; ++e) y[e] = src[x[4 * j + e]];
+          const bool fixed = y[0] == x[4 * j] && y[1] == x[4 * j + 1] && y[2] == x[4 * j + 2] && y[3] == x[4 * j + 3];
+#pragma unroll
+          for (uint32_t e = 0; e < 4; ++e) x[4 * j + e] = y[e];
+          if (fixed) {
+            act &= ~(1u << j);
+          } else {
+            *reinterpret_cast<uint2*>(&src[4 * (uint32_t(t) + EXEC_T * j)]) =
+                make_uint2(y[0] | (y[1] << 16), y[2] | (y[3] << 16));
+          }
+        }
+      }
+    }
   }
-  stamp(3);
-  // 3. roots of this thread's 64 bytes -> registers; the LDS becomes the block's bytes (lower
-  //    half) and its compressed input range (upper half)
+  __syncthreads();
+  // roots of this thread's 64 contiguous output bytes -> registers (every moved pointer was
+  // written back, so the map holds final roots)
   const uint32_t my0 = uint32_t(t) * 64;
-  uint32_t root[32];  // two u16 roots per register
   {
     const uint4* s4 = reinterpret_cast<const uint4*>(src) + my0 / 8;
 #pragma unroll
@@ -573,6 +613,7 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     }
   }
   __syncthreads();
+  // 3. the LDS becomes the block's bytes (lower half) and its compressed input range (upper half)
   uint8_t* bytes = reinterpret_cast<uint8_t*>(src);
   uint8_t* stage = bytes + SNAP_BLOCK;
   const uint32_t in_lo = s_inlo, in_hi = s_inhi;
@@ -586,15 +627,15 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
   }
   __syncthreads();
   stamp(4);
-  for (uint32_t base = 0; base < nrec; base += EXEC_T * EXEC_RPT) {
-    uint64_t w[EXEC_RPT];
+  for (uint32_t base = 0; base < nrec; base += EXEC_T * EXEC_RPT2) {
+    uint64_t w[EXEC_RPT2];
 #pragma unroll
-    for (uint32_t k = 0; k < EXEC_RPT; ++k) {
+    for (uint32_t k = 0; k < EXEC_RPT2; ++k) {
       const uint32_t r = base + k * EXEC_T + uint32_t(t);
       w[k] = r < nrec ? a.recs[r0 + r] : 0ull;
     }
 #pragma unroll
-    for (uint32_t k = 0; k < EXEC_RPT; ++k) {
+    for (uint32_t k = 0; k < EXEC_RPT2; ++k) {
       const uint32_t r = base + k * EXEC_T + uint32_t(t);
       const uint32_t sv = uint32_t(w[k] >> 32);
       if (r >= nrec || !(sv & REC_LIT)) continue;
@@ -606,8 +647,23 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
         else s_bad = 1;
         continue;
       }
-      const uint8_t* ip = stage + (reinterpret_cast<uintptr_t>(in) + (sv & ~REC_LIT) - abs_lo);
-      for (uint32_t i = 0; i < len; ++i) bytes[rel + i] = ip[i];
+      // byte head up to a 4-byte aligned destination, then aligned dword stores of realigned
+      // source dwords, then a byte tail
+      uint32_t q = uint32_t(reinterpret_cast<uintptr_t>(in) + (sv & ~REC_LIT) - abs_lo) + SNAP_BLOCK;
+      uint32_t d = rel, n = len;
+      while (n && (d & 3)) { bytes[d++] = bytes[q++]; --n; }
+      const uint32_t sh = q & 3;
+      const uint32_t* qa = reinterpret_cast<const uint32_t*>(bytes + (q & ~3u));
+      uint32_t* da = reinterpret_cast<uint32_t*>(bytes + d);
+      uint32_t lo = qa[0];
+      for (; n >= 4; n -= 4) {
+        const uint32_t hi = *++qa;
+        *da++ = __builtin_amdgcn_alignbyte(hi, lo, sh);
+        lo = hi;
+      }
+      d = uint32_t(reinterpret_cast<uint8_t*>(da) - bytes);
+      q = uint32_t(reinterpret_cast<const uint8_t*>(qa) - bytes) + sh;
+      while (n) { bytes[d++] = bytes[q++]; --n; }
     }
   }
   __syncthreads();
@@ -626,30 +682,25 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     if (t == 0) atomicOr(&a.pages_bad[p], 64u);
     return;
   }
-  // 4. gather and store
+  // 4. gather and store (16-byte stores)
   if (my0 >= nbytes) return;
   uint32_t word[16];
 #pragma unroll
   for (int v = 0; v < 16; ++v) {
-    uint32_t x = 0;
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      const uint32_t pr = root[(4 * v + h) >> 1];
-      const uint32_t rt = ((4 * v + h) & 1) ? (pr >> 16) : (pr & 0xffff);
-      x |= uint32_t(bytes[rt]) << (8 * h);
-    }
-    word[v] = x;
+    const uint32_t r01 = root[2 * v], r23 = root[2 * v + 1];
+    word[v] = uint32_t(bytes[r01 & 0xffffu]) | (uint32_t(bytes[r01 >> 16]) << 8) |
+              (uint32_t(bytes[r23 & 0xffffu]) << 16) | (uint32_t(bytes[r23 >> 16]) << 24);
   }
   uint8_t* dst = out + bs + my0;
   if (my0 + 64 <= nbytes && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0)) {
     uint4* d4 = reinterpret_cast<uint4*>(dst);
 #pragma unroll
     for (int v = 0; v < 4; ++v) d4[v] = make_uint4(word[4 * v], word[4 * v + 1], word[4 * v + 2], word[4 * v + 3]);
-    stamp(7);
   } else {
     const uint32_t m = min(64u, nbytes - my0);
     for (uint32_t i = 0; i < m; ++i) dst[i] = uint8_t(word[i >> 2] >> (8 * (i & 3)));
   }
+  stamp(7);
 }
 
 // Serial fallback for pages whose structure the parallel path could not use.

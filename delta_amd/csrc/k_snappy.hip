@@ -397,20 +397,17 @@ __global__ void __launch_bounds__(64) k_snap_scan(SnappyArgs a) {
 
 // E: one 8-byte record per element, {output offset in its 64 KiB block u16 | (len-1) u16 << 16 |
 // src u32 << 32}; src = copy offset, or REC_LIT | input position for a literal. The element that
-// starts a block (no element straddles one) records the block's first record index. Records are
-// assembled in LDS per workgroup and written out with coalesced stores.
+// starts a block (no element straddles one) records the block's first record index. Each lane
+// stores its chunk's records directly (consecutive lines per lane; the L2 merges them), which
+// keeps the LDS to the input stage and two workgroups per CU.
 constexpr uint32_t REC_LIT = 0x80000000u;
-constexpr uint32_t EMIT_RECS = 4096;  // LDS record slots per workgroup (overflow: direct stores)
 
 __global__ void __launch_bounds__(WG_CHUNKS) k_snap_emit(SnappyArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[STAGE_BYTES + 32];
-  __shared__ uint64_t rbuf[EMIT_RECS];
   const WgInfo g = wg_info(a);
   const SnapPage& pg = a.pages[g.p];
   const Staged s = stage_input(buf, reinterpret_cast<const uint8_t*>(pg.in), pg.n_in, g.j0, g.cnt);
   const uint32_t cfirst = a.chunk_base[g.p] + g.j0;
-  const uint64_t wr0 = a.chunk_rec_start[cfirst], wr1 = a.chunk_rec_start[cfirst + g.cnt];
-  const bool in_lds = wr1 - wr0 <= EMIT_RECS;
   if (threadIdx.x < g.cnt) {
     const uint32_t j = g.j0 + threadIdx.x;
     const uint32_t c = cfirst + threadIdx.x;
@@ -433,16 +430,12 @@ __global__ void __launch_bounds__(WG_CHUNKS) k_snap_emit(SnappyArgs a) {
         src = el.off;
       }
       const uint64_t r = (o & (SNAP_BLOCK - 1)) | (uint64_t(el.len - 1) << 16) | (uint64_t(src) << 32);
-      if (in_lds) rbuf[rec - wr0] = r; else a.recs[rec] = r;
+      a.recs[rec] = r;
       ++rec;
       o += el.len;
       pos += snap_adv(el);
     }
     if (bad) atomicOr(&a.pages_bad[g.p], 8u);
-  }
-  if (in_lds) {
-    __syncthreads();
-    for (uint64_t r = wr0 + threadIdx.x; r < wr1; r += WG_CHUNKS) a.recs[r] = rbuf[r - wr0];
   }
 }
 

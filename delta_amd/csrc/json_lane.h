@@ -24,8 +24,10 @@
 
 #if defined(__HIPCC__)
 #define JL_HD __host__ __device__ __forceinline__
+#define JL_UNROLL _Pragma("unroll")
 #else
 #define JL_HD inline
+#define JL_UNROLL
 #endif
 
 namespace dr {
@@ -150,6 +152,104 @@ enum : uint32_t { T_OBJ_OPEN = 0, T_ARR_OPEN, T_OBJ_CLOSE, T_ARR_CLOSE, T_COLON,
                   T_STR_CLOSE, T_STR_CLOSE_ESC, T_SCALAR };
 constexpr uint32_t TOK_MAX_LINE = 65535;   // longer lines go to the General walker
 constexpr uint32_t TOK_MAX_SCALAR = 4095;
+
+// Up to 20 bytes at s as little-endian words (w[0] holds s[0..3]). Bytes at or past n are
+// unspecified: on the device they come from the line buffer (zero-padded past its end), on the
+// host they are zero. Three aligned 16-byte loads and funnel shifts, no per-byte loads.
+JL_HD void load20(const uint8_t* s, uint32_t n, uint32_t w[5]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uintptr_t a = reinterpret_cast<uintptr_t>(s);
+  const uint4* b = reinterpret_cast<const uint4*>(a & ~uintptr_t(15));
+  const uint4 x = b[0], y = b[1], z = b[2];
+  const uint32_t v[12] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w, z.x, z.y, z.z, z.w};
+  const uint32_t q = uint32_t(a >> 2) & 3u, r = uint32_t(a) & 3u;
+  uint32_t u[6];
+JL_UNROLL
+  for (int i = 0; i < 6; ++i) u[i] = q == 0 ? v[i] : q == 1 ? v[i + 1] : q == 2 ? v[i + 2] : v[i + 3];
+JL_UNROLL
+  for (int i = 0; i < 5; ++i) w[i] = __builtin_amdgcn_alignbyte(u[i + 1], u[i], r);
+#else
+  uint8_t t[20] = {0};
+  std::memcpy(t, s, n < 20 ? n : 20);
+  std::memcpy(w, t, 20);
+#endif
+}
+// 0x80 in each byte of x that is an ASCII digit.
+JL_HD uint32_t digit_bytes(uint32_t x) {
+  return zbytes((x & 0xF0F0F0F0u) ^ 0x30303030u) & ~(((x & 0x0F0F0F0Fu) + 0x06060606u) << 3) & 0x80808080u;
+}
+// Value of the 4 ASCII digits of x (first digit in the low byte).
+JL_HD uint32_t digits4(uint32_t x) {
+  uint32_t d = x - 0x30303030u;
+  d = d * 10u + (d >> 8);                          // bytes 0, 2: two-digit values
+  return ((d & 0x00FF00FFu) * 0x00640001u) >> 16;  // 100 * hi pair + lo pair
+}
+JL_HD uint32_t key_mask(uint32_t n) { return n >= 4 ? 0xFFFFFFFFu : (1u << (8 * n)) - 1u; }
+
+// action_key / file_key on word loads (the fast walker's keys are unescaped line bytes).
+JL_HD uint8_t action_key_w(const uint8_t* s, uint32_t n) {
+  if (n != 3 && n != 6 && n != 8 && n != 10) return 0;
+  uint32_t w[5];
+  load20(s, n, w);
+  const uint32_t a = w[0], b = w[1], c = w[2];
+  if (n == 3) {
+    const uint32_t t = a & 0xFFFFFFu;
+    return t == 0x646461u ? K_ADD : t == 0x6E7874u ? K_TXN : t == 0x636463u ? K_CDC : 0;  // add txn cdc
+  }
+  if (n == 6) return (a == 0x6F6D6572u && (b & 0xFFFFu) == 0x6576u) ? K_REMOVE : 0;  // remo ve
+  if (n == 8) {
+    if (a == 0x6174656Du && b == 0x61746144u) return K_METADATA;                    // meta Data
+    if (a == 0x746F7270u && b == 0x6C6F636Fu) return K_PROTOCOL;                    // prot ocol
+    return 0;
+  }
+  return (a == 0x6D6D6F63u && b == 0x6E497469u && (c & 0xFFFFu) == 0x6F66u) ? K_COMMITINFO : 0;  // comm itIn fo
+}
+JL_HD uint8_t file_key_w(const uint8_t* s, uint32_t n) {
+  if (n != 4 && n != 17) return FK_OTHER;
+  uint32_t w[5];
+  load20(s, n, w);
+  if (n == 4) return w[0] == 0x68746170u ? FK_PATH : w[0] == 0x657A6973u ? FK_SIZE : FK_OTHER;  // path size
+  return (w[0] == 0x656C6564u && w[1] == 0x6E6F6974u && w[2] == 0x656D6954u && w[3] == 0x6D617473u &&
+          (w[4] & 0xFFu) == 0x70u) ? FK_DELTS : FK_OTHER;  // dele tion Time stam p
+}
+// Scalar tokens: null / true / false and plain integers of up to 19 digits decoded from word
+// loads; anything else (fractions, exponents, 20+ characters, malformed) takes scalar_class.
+JL_HD uint8_t scalar_class(const uint8_t* s, uint32_t L, int64_t* val);
+JL_HD uint8_t scalar_fast(const uint8_t* s, uint32_t L, int64_t* val) {
+  if (L > 20) return scalar_class(s, L, val);
+  uint32_t w[5];
+  load20(s, L, w);
+  if (L == 4 && w[0] == 0x6C6C756Eu) return SC_NULL;   // null
+  if (L == 4 && w[0] == 0x65757274u) return SC_TRUE;   // true
+  if (L == 5 && w[0] == 0x736C6166u && (w[1] & 0xFFu) == 0x65u) return SC_FALSE;  // fals e
+  const uint32_t neg = (w[0] & 0xFFu) == 0x2Du ? 1u : 0u;
+  uint32_t dm = 0;
+JL_UNROLL
+  for (int d = 0; d < 5; ++d) dm |= gather4(digit_bytes(w[d])) << (4 * d);
+  const uint32_t need = ((1u << L) - 1u) & ~neg;
+  const uint32_t nd = L - neg;
+  if (nd == 0 || nd > 19 || (dm & need) != need) return scalar_class(s, L, val);
+  if (neg) {
+JL_UNROLL
+    for (int i = 0; i < 4; ++i) w[i] = (w[i] >> 8) | (w[i + 1] << 24);
+    w[4] >>= 8;
+  }
+  if (nd > 1 && (w[0] & 0xFFu) == 0x30u) return SC_BAD;  // leading zero
+  const uint32_t g = nd >> 2, r = nd & 3u;
+  uint64_t v = 0;
+JL_UNROLL
+  for (uint32_t k = 0; k < 4; ++k)
+    if (k < g) v = v * 10000ull + digits4(w[k]);
+  if (r) {
+    const uint32_t x = g == 0 ? w[0] : g == 1 ? w[1] : g == 2 ? w[2] : g == 3 ? w[3] : w[4];
+    const uint32_t sh = 8u * (4u - r);
+    v = v * (r == 1 ? 10ull : r == 2 ? 100ull : 1000ull) + digits4((x << sh) | (0x30303030u >> (32u - sh)));
+  }
+  // LongType: VALUE_NUMBER_INT within [-2^63, 2^63-1] (19 digits fit in 64 bits unsigned)
+  if (v > (neg ? 0x8000000000000000ull : 0x7FFFFFFFFFFFFFFFull)) return SC_NUM;
+  *val = neg ? int64_t(0ull - v) : int64_t(v);
+  return SC_INT;
+}
 
 JL_HD uint32_t tok_make(uint32_t off, uint32_t aux, uint32_t cls) { return (off << 16) | (aux << 4) | cls; }
 JL_HD uint32_t tok_off(uint32_t t) { return t >> 16; }
@@ -442,8 +542,8 @@ JL_HD void dfa_token(const uint8_t* p, uint32_t tok, Dfa<General>& d) {
             else d.k2 = kl == 0xFFFFFFFFu ? FK_OTHER : file_key(kb, kl);
           }
         } else {
-          if (d.depth == 1) d.k1 = action_key(s, sl);
-          else d.k2 = file_key(s, sl);
+          if (d.depth == 1) d.k1 = action_key_w(s, sl);
+          else d.k2 = file_key_w(s, sl);
         }
       }
       d.state = S_COLON;
@@ -469,7 +569,7 @@ JL_HD void dfa_token(const uint8_t* p, uint32_t tok, Dfa<General>& d) {
     if (!(stt == S_VALUE || stt == S_ARR_FIRST)) { d.status = ST_BAD; return; }
     const uint32_t L = tok_aux(tok);
     int64_t v = 0;
-    const uint8_t sc = scalar_class(p + off, L, &v);
+    const uint8_t sc = scalar_fast(p + off, L, &v);
     if (sc == SC_BAD) { d.status = ST_BAD; return; }
     d.sc_checked += L;
     if (d.depth == 1) {

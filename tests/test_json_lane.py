@@ -151,7 +151,15 @@ def corpus():
         b'{"add":{"\\u0070ath":"y","si\\u007Ae":3}}', b'{"re\\u006dove":{"path":"z","deletionTimestamp":4}}',
         b'{"x":' + b"[" * 70 + b"]" * 70 + b',"add":{"path":"d"}}', b'{"x":' + b"[" * 70 + b"]" * 69 + b'}',
         b'{"x":' + b"[{}," * 40 + b"0" + b"]" * 40 + b',"remove":{"path":"e"}}', b'{"a":\x0b1}',
-    ]
+        # integer decoding at every digit count and sign (word-load fast path vs the byte loop)
+        b'{"add":{"path":"a","size":-01}}', b'{"add":{"path":"a","size":-}}', b'{"add":{"path":"a","size":00}}',
+        b'{"add":{"path":"a","size":9999999999999999999}}', b'{"add":{"path":"a","size":18446744073709551615}}',
+        b'{"add":{"path":"a","size":18446744073709551616}}', b'{"add":{"path":"a","size":-9223372036854775809}}',
+        b'{"add":{"path":"a","size":1234567890123456789}}', b'{"add":{"path":"a","size":-1234567890123456789}}',
+        b'{"add":{"path":"a","size":-0.0}}', b'{"add":{"path":"a","size":1x}}', b'{"add":{"path":"a","size":nul}}',
+        b'{"add":{"path":"a","size":nulll}}', b'{"add":{"path":"a","size":falsey}}', b'{"add":{"path":"a","size":truE}}',
+    ] + [b'{"remove":{"path":"r","deletionTimestamp":%s%s}}' % (sg, b"123456789012345678901"[:k])
+         for k in range(1, 22) for sg in (b"", b"-")]
     return lines + hand
 
 

@@ -191,13 +191,8 @@ __global__ void __launch_bounds__(JL_T) k_json_lines(JsonParseArgs a) {
     if (!anymore || __ballot(nt > uint32_t(JL_FLUSH)) != 0ull) {
       uint32_t mx = nt;
       for (int o = 32; o > 0; o >>= 1) mx = max(mx, uint32_t(__shfl_xor(int(mx), o, 64)));
-#ifndef JL_NODFA
       for (uint32_t t = 0; t < mx; ++t)
         if (t < nt && d.status == jl::ST_OK) jl::dfa_token<false>(p, tokbuf[t * JL_T + lane], d);
-#else
-      for (uint32_t t = 0; t < mx; ++t)
-        if (t < nt) d.sc_checked += tokbuf[t * JL_T + lane];
-#endif
       nt = 0;
     }
     if (!anymore) break;

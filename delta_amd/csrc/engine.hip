@@ -194,6 +194,7 @@ struct PagePlan {
   DBuf<SnapPage> d_snap;
   DBuf<uint32_t> d_chunk_base, d_block_page;
   DBuf<CopyJob> d_copy;
+  DBuf<uint32_t> s_mid_first, s_half_out, s_half_elems;
   DBuf<uint32_t> s_spec_exit, s_vis, s_entry, s_spec_first, s_assumed, s_region, s_chunk_out, s_chunk_out_start,
       s_chunk_copies, s_pages_bad;
   DBuf<uint64_t> s_rec_start, s_recs;
@@ -554,6 +555,9 @@ static void plan_pages(StagedData& s, PagePlan& P) {
   P.s_vis = DBuf<uint32_t>(s.ctx, uint64_t(P.nchunks) * 8);
   P.s_entry = DBuf<uint32_t>(s.ctx, P.nchunks);
   P.s_spec_first = DBuf<uint32_t>(s.ctx, P.nchunks);
+  P.s_mid_first = DBuf<uint32_t>(s.ctx, P.nchunks);
+  P.s_half_out = DBuf<uint32_t>(s.ctx, P.nchunks);
+  P.s_half_elems = DBuf<uint32_t>(s.ctx, P.nchunks);
   P.s_assumed = DBuf<uint32_t>(s.ctx, P.nchunks);
   P.s_region = DBuf<uint32_t>(s.ctx, P.nchunks);
   P.s_block_rec = DBuf<uint64_t>(s.ctx, P.block_page.size() + 1);
@@ -606,6 +610,9 @@ static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_
                   P.s_vis.p, P.s_entry.p, P.s_spec_first.p, P.s_assumed.p, P.s_chunk_flag.p, P.s_region.p, P.s_region_count.p, P.s_chunk_out.p, P.s_chunk_out_start.p, P.s_chunk_copies.p,
                   P.s_rec_start.p, P.s_recs.p, P.d_block_page.p, P.s_block_rec.p, uint32_t(P.block_page.size()),
                   P.d_wg_chunk0.p, uint32_t(P.wg_chunk0.size()), P.s_pages_bad.p, err.p};
+    sa.mid_first = P.s_mid_first.p;
+    sa.half_out = P.s_half_out.p;
+    sa.half_elems = P.s_half_elems.p;
     DBuf<uint64_t> stamps;
     const bool dbg = std::getenv("DR_SNAP_DEBUG") != nullptr;
     if (dbg) {

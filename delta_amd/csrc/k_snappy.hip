@@ -38,7 +38,7 @@ constexpr uint32_t SNAP_CH = 256;            // compressed bytes per speculation
 constexpr uint32_t SNAP_BLOCK = 65536;       // snappy compressor fragment size
 constexpr uint32_t SNAP_WU = 256;            // speculation warm-up bytes (0.6% mis-speculation on path pages)
 constexpr uint32_t WG_CHUNKS = 256;          // chunks (threads) per chunk-walker workgroup
-constexpr uint32_t STAGE_BYTES = (WG_CHUNKS * SNAP_CH + SNAP_WU + 64) * 65 / 64 + 16;  // + skew
+constexpr uint32_t STAGE_BYTES = (WG_CHUNKS * SNAP_CH + SNAP_WU + 96) * 65 / 64 + 16;  // + skew
 
 struct Elem {
   uint32_t hdr;   // header bytes (tag + length/offset bytes)
@@ -108,12 +108,18 @@ __device__ Staged stage_input(uint8_t* buf, const uint8_t* in, uint64_t n_in, ui
   uint64_t lo = uint64_t(j0) * SNAP_CH;
   lo = lo >= SNAP_WU ? lo - SNAP_WU : 0;
   const uint64_t hi = min(uint64_t(j0 + cnt) * SNAP_CH + 16, uint64_t(n_in) + 8);
-  const uintptr_t a0 = (reinterpret_cast<uintptr_t>(in) + lo) & ~uintptr_t(3);
+  const uintptr_t a0 = (reinterpret_cast<uintptr_t>(in) + lo) & ~uintptr_t(15);
   const int64_t lo_al = int64_t(a0) - int64_t(reinterpret_cast<uintptr_t>(in));
-  const uint32_t nd = uint32_t((int64_t(hi) - lo_al + 3) / 4) + 2;
+  const uint32_t nv = uint32_t((int64_t(hi) - lo_al + 15) / 16) + 1;  // 16-byte vectors (+ 8-byte reads past hi)
   uint32_t* b32 = reinterpret_cast<uint32_t*>(buf);
-  const uint32_t* g32 = reinterpret_cast<const uint32_t*>(a0);
-  for (uint32_t i = threadIdx.x; i < nd; i += blockDim.x) b32[skew(i)] = g32[i];
+  const uint4* g4 = reinterpret_cast<const uint4*>(a0);
+  // 16-byte loads, four in flight per lane; a vector's 4 dwords never straddle a skew step
+#pragma unroll 4
+  for (uint32_t i = threadIdx.x; i < nv; i += blockDim.x) {
+    const uint4 v = g4[i];
+    uint32_t* d = b32 + skew(4 * i);
+    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+  }
   __syncthreads();
   return Staged{lo_al, hi};
 }
@@ -154,8 +160,9 @@ __global__ void __launch_bounds__(WG_CHUNKS) k_snap_spec(SnappyArgs a) {
 #pragma unroll
   for (int k = 0; k < int(SNAP_CH / 32); ++k) vis[k] = 0;
   uint64_t pos = cs >= SNAP_WU ? cs - SNAP_WU : 0;
-  uint64_t first = ~0ull, out = 0;
-  uint32_t elems = 0;
+  uint64_t first = ~0ull, out = 0, mid = ~0ull;
+  uint32_t elems = 0, hout = 0, helems = 0;
+  const uint64_t cm = cs + SNAP_CH / 2;
   while (pos < ce) {
     uint32_t adv, len;
     snap_step(staged_u64(buf, s, pos), &adv, &len);
@@ -167,9 +174,16 @@ __global__ void __launch_bounds__(WG_CHUNKS) k_snap_spec(SnappyArgs a) {
       if (first == ~0ull) first = pos;
       out += len;
       ++elems;
+      const bool h = pos < cm;
+      hout += h ? len : 0u;
+      helems += h ? 1u : 0u;
+      mid = (!h && mid == ~0ull) ? pos : mid;
     }
     pos += adv;
   }
+  a.mid_first[c] = mid > 0xffffffffull ? 0xffffffffu : uint32_t(mid);
+  a.half_out[c] = hout;
+  a.half_elems[c] = helems;
   a.spec_exit[c] = pos > 0xffffffffull ? 0xffffffffu : uint32_t(pos);
 #pragma unroll
   for (int k = 0; k < int(SNAP_CH / 32); ++k) a.vis[uint64_t(c) * (SNAP_CH / 32) + k] = vis[k];
@@ -357,6 +371,7 @@ __global__ void __launch_bounds__(256) k_snap_count(SnappyArgs a) {
   if (c >= a.nchunks) return;
   const uint32_t pos0 = a.entry[c];
   if (pos0 == a.spec_first[c]) return;
+  a.mid_first[c] = 0xffffffffu;  // not split: k_snap_emit walks it with one lane
   const uint32_t p = chunk_page(a.chunk_base, a.npages, c);
   const SnapPage& pg = a.pages[p];
   const uint64_t cs = uint64_t(c - a.chunk_base[p]) * SNAP_CH;
@@ -402,19 +417,29 @@ __global__ void __launch_bounds__(64) k_snap_scan(SnappyArgs a) {
 // keeps the LDS to the input stage and two workgroups per CU.
 constexpr uint32_t REC_LIT = 0x80000000u;
 
-__global__ void __launch_bounds__(WG_CHUNKS) k_snap_emit(SnappyArgs a) {
+__global__ void __launch_bounds__(2 * WG_CHUNKS) k_snap_emit(SnappyArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[STAGE_BYTES + 32];
   const WgInfo g = wg_info(a);
   const SnapPage& pg = a.pages[g.p];
   const Staged s = stage_input(buf, reinterpret_cast<const uint8_t*>(pg.in), pg.n_in, g.j0, g.cnt);
   const uint32_t cfirst = a.chunk_base[g.p] + g.j0;
-  if (threadIdx.x < g.cnt) {
-    const uint32_t j = g.j0 + threadIdx.x;
-    const uint32_t c = cfirst + threadIdx.x;
+  const uint32_t q = threadIdx.x % WG_CHUNKS, half = threadIdx.x / WG_CHUNKS;
+  if (q < g.cnt) {
+    const uint32_t j = g.j0 + q;
+    const uint32_t c = cfirst + q;
     const uint64_t cs = uint64_t(j) * SNAP_CH;
-    const uint64_t ce = min(cs + SNAP_CH, uint64_t(pg.n_in));
+    const uint64_t mid = a.mid_first[c];
     uint64_t pos = a.entry[c], o = a.chunk_out_start[c];
     uint64_t rec = a.chunk_rec_start[c];
+    uint64_t ce = min(cs + SNAP_CH, uint64_t(pg.n_in));
+    if (half == 0) {
+      ce = mid != 0xffffffffull ? mid : ce;  // the first half's elements end where the second's begin
+    } else {
+      if (mid == 0xffffffffull) ce = 0;  // not split: nothing for the second lane
+      pos = mid;
+      o += a.half_out[c];
+      rec += a.half_elems[c];
+    }
     bool bad = false;
     while (pos < ce) {
       const Elem el = snap_decode(staged_u64(buf, s, pos));
@@ -745,7 +770,7 @@ void launch_snappy(const SnappyArgs& a, hipStream_t st, void* scan_scratch) {
   hipLaunchKernelGGL(dev::k_snap_count, dim3(g), dim3(256), 0, st, a);
   hipLaunchKernelGGL(dev::k_snap_scan, dim3(a.npages), dim3(64), 0, st, a);
   launch_scan_u32(a.chunk_elems, a.chunk_rec_start, a.nchunks, scan_scratch, st);
-  hipLaunchKernelGGL(dev::k_snap_emit, dim3(a.nwg), dim3(dev::WG_CHUNKS), 0, st, a);
+  hipLaunchKernelGGL(dev::k_snap_emit, dim3(a.nwg), dim3(2 * dev::WG_CHUNKS), 0, st, a);
   hipLaunchKernelGGL(dev::k_snap_exec, dim3(a.nblocks), dim3(dev::EXEC_T), 0, st, a);
   hipLaunchKernelGGL(dev::k_snap_serial, dim3((a.npages + 63) / 64), dim3(64), 0, st, a);
 }

@@ -145,6 +145,12 @@ struct SnappyArgs {
   uint32_t* pages_bad;          // [npages] nonzero -> decoded by the serial fallback
   uint32_t* error;
   uint64_t* stamps;             // diagnostics: [nblocks * 8] k_snap_exec phase clocks, or null
+  // second-half split of each chunk's walk (k_snap_emit runs two lanes per chunk): the first element
+  // starting in the chunk's second half, and the output bytes / elements before it; mid_first is
+  // ~0 when the chunk is not split (its true entry is not its speculative first position)
+  uint32_t* mid_first = nullptr;
+  uint32_t* half_out = nullptr;
+  uint32_t* half_elems = nullptr;
 };
 uint32_t snappy_wg_chunks();
 void launch_snappy(const SnappyArgs& a, hipStream_t st, void* scan_scratch);

@@ -210,7 +210,7 @@ struct PagePlan {
   std::vector<uint2> ba_tiles;
   DBuf<uint2> d_ba_tiles;
   DBuf<uint32_t> s_ba_vals, s_ba_ok, s_ba_count, s_ba_tile_cnt;
-  DBuf<uint64_t> s_ba_tile_off;
+  DBuf<uint64_t> s_ba_tile_off, s_ba_kept;
 };
 
 struct StagedData {
@@ -573,6 +573,7 @@ static void plan_pages(StagedData& s, PagePlan& P) {
   up(P.d_ba_tiles, P.ba_tiles);
   P.s_ba_tile_cnt = DBuf<uint32_t>(s.ctx, P.ba_tiles.size());
   P.s_ba_tile_off = DBuf<uint64_t>(s.ctx, P.ba_tiles.size() + 1);
+  P.s_ba_kept = DBuf<uint64_t>(s.ctx, P.ba_tiles.size() * 256);
   P.s_ba_ok = DBuf<uint32_t>(s.ctx, P.ba_pages);
   P.s_ba_count = DBuf<uint32_t>(s.ctx, P.ba_pages);
   for (PageDesc& d : P.pages) {
@@ -599,6 +600,7 @@ static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_
   pa.nba_tiles = uint32_t(P.ba_tiles.size());
   pa.ba_tile_cnt = P.s_ba_tile_cnt.p;
   pa.ba_tile_off = P.s_ba_tile_off.p;
+  pa.ba_kept = P.s_ba_kept.p;
   pa.ba_ok = P.s_ba_ok.p;
   pa.ba_count = P.s_ba_count.p;
   launch_page_copy(P.d_copy.p, uint32_t(P.copy_jobs.size()), stream);

@@ -144,7 +144,8 @@ struct ByteArrayWalker {
 // last value ends at the region end -- which proves B equals the true chain. Any failure (NUL
 // bytes, huge values, corrupt data) leaves ba_ok = 0 and the serial walker decodes the page.
 constexpr int BA_T = 256;
-constexpr uint32_t BA_TILE = BA_T * 16;
+constexpr uint32_t BA_POS = 64;               // positions per thread
+constexpr uint32_t BA_TILE = BA_T * BA_POS;   // region bytes per tile (workgroup)
 
 __device__ __forceinline__ bool ba_region(const PageDesc& pg, const uint8_t** b, const uint8_t** e) {
   const uint8_t* p = reinterpret_cast<const uint8_t*>(pg.dst);
@@ -175,36 +176,42 @@ __device__ __forceinline__ bool ba_cand(const uint8_t* b, uint64_t S, uint64_t p
   return true;
 }
 
-// Bit j of the result: region offset (tile base + 16 t + j) is a kept candidate. The thread's 16
-// positions are 16-byte aligned in absolute address; their +2/+3 bytes come from two 16-byte loads.
-__device__ __forceinline__ uint32_t ba_kept(const uint8_t* b, uint64_t S, int64_t q0) {
-  if (q0 + 16 <= 0 || q0 >= int64_t(S)) return 0u;
+__device__ __forceinline__ uint32_t zero_nibble(uint32_t v) {  // bit k: byte k of v is zero
+  const uint32_t zb = ~(((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v | 0x7F7F7F7Fu);  // 0x80 per zero byte
+  uint32_t g = zb >> 7;
+  g |= g >> 7;
+  g |= g >> 14;
+  return g & 0xFu;
+}
+
+// Bit j of the result: region offset q0 + j is a kept candidate. The thread's 64 positions start
+// 16-byte aligned in absolute address; their +1..+4 bytes come from five 16-byte loads.
+__device__ __forceinline__ uint64_t ba_kept(const uint8_t* b, uint64_t S, int64_t q0) {
+  if (q0 + int64_t(BA_POS) <= 0 || q0 >= int64_t(S)) return 0ull;
   const uint4* a4 = reinterpret_cast<const uint4*>(b + q0);  // 16-byte aligned by construction
-  const uint4 x = a4[0], y = a4[1];
-  const uint32_t w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
-  uint32_t z = 0;
+  uint64_t z0 = 0;
+  uint32_t z1 = 0;
 #pragma unroll
-  for (int d = 0; d < 8; ++d) {
-    const uint32_t v = w[d];
-    const uint32_t zb = ~(((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v | 0x7F7F7F7Fu);  // 0x80 per zero byte
-    uint32_t g = zb >> 7;
-    g |= g >> 7;
-    g |= g >> 14;
-    z |= (g & 0xFu) << (4 * d);
+  for (int v = 0; v < 5; ++v) {
+    const uint4 x = a4[v];
+    const uint32_t m = zero_nibble(x.x) | (zero_nibble(x.y) << 4) | (zero_nibble(x.z) << 8) | (zero_nibble(x.w) << 12);
+    if (v < 4) z0 |= uint64_t(m) << (16 * v);
+    else z1 = m;
   }
+  auto zs = [&](int k) { return (z0 >> k) | (uint64_t(z1) << (64 - k)); };
   // A true boundary's zero run (the length's high bytes) ends at +3: the string's first byte is
   // non-zero unless the string is empty (all four length bytes zero). This drops the shifted
   // candidates inside the run (p-1 when len < 256), which would otherwise survive the successor
   // check by chance.
-  const uint32_t cm = ((z >> 2) & (z >> 3) & (~(z >> 4) | (z & (z >> 1)))) & 0xFFFFu;
-  uint32_t kept = 0;
-  for (uint32_t m = cm; m;) {
-    const int j = __builtin_ctz(m);
+  const uint64_t cm = zs(2) & zs(3) & (~zs(4) | (z0 & zs(1)));
+  uint64_t kept = 0;
+  for (uint64_t m = cm; m;) {
+    const int j = __builtin_ctzll(m);
     m &= m - 1;
     const int64_t p = q0 + j;
     if (p < 0) continue;
     uint64_t nx, nn;
-    if (ba_cand(b, S, uint64_t(p), &nx) && (nx == S || ba_cand(b, S, nx, &nn))) kept |= 1u << j;
+    if (ba_cand(b, S, uint64_t(p), &nx) && (nx == S || ba_cand(b, S, nx, &nn))) kept |= 1ull << j;
   }
   return kept;
 }
@@ -225,7 +232,7 @@ __device__ __forceinline__ BaTile ba_tile(const ParquetArgs& a, uint32_t tile) {
   r.b = b;
   r.S = r.ok ? uint64_t(e - b) : 0;
   const int64_t lead = int64_t(reinterpret_cast<uintptr_t>(b) & 15);  // tiles are absolute-aligned
-  r.q0 = -lead + int64_t(tp.y) * BA_TILE + 16 * int64_t(threadIdx.x);
+  r.q0 = -lead + int64_t(tp.y) * BA_TILE + int64_t(BA_POS) * int64_t(threadIdx.x);
   return r;
 }
 
@@ -238,12 +245,13 @@ __device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* red) {
   return s;
 }
 
-// T1: kept candidates per tile.
+// T1: kept candidates per tile; each thread's 64-bit kept mask is stored for T2.
 __global__ void __launch_bounds__(BA_T) k_ba_count(ParquetArgs a) {
   __shared__ uint32_t red[BA_T / 64];
   const BaTile tl = ba_tile(a, blockIdx.x);
-  const uint32_t c = tl.ok ? uint32_t(__builtin_popcount(ba_kept(tl.b, tl.S, tl.q0))) : 0u;
-  const uint32_t s = block_sum(c, red);
+  const uint64_t km = tl.ok ? ba_kept(tl.b, tl.S, tl.q0) : 0ull;
+  a.ba_kept[uint64_t(blockIdx.x) * BA_T + threadIdx.x] = km;
+  const uint32_t s = block_sum(uint32_t(__builtin_popcountll(km)), red);
   if (threadIdx.x == 0) {
     a.ba_tile_cnt[blockIdx.x] = s;
     if (a.ba_tiles[blockIdx.x].y == 0) a.ba_ok[tl.pg->ba_slot] = tl.ok ? 1u : 0u;
@@ -256,8 +264,8 @@ __global__ void __launch_bounds__(BA_T) k_ba_write(ParquetArgs a) {
   const BaTile tl = ba_tile(a, blockIdx.x);
   if (!tl.ok) return;
   const PageDesc& pg = *tl.pg;
-  uint32_t km = ba_kept(tl.b, tl.S, tl.q0);
-  const uint32_t c = uint32_t(__builtin_popcount(km));
+  uint64_t km = a.ba_kept[uint64_t(blockIdx.x) * BA_T + threadIdx.x];
+  const uint32_t c = uint32_t(__builtin_popcountll(km));
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t incl = c;
   for (int o = 1; o < 64; o <<= 1) {
@@ -275,7 +283,7 @@ __global__ void __launch_bounds__(BA_T) k_ba_write(ParquetArgs a) {
   uint32_t* vals = a.ba_vals + pg.ba_base;
   uint64_t o = rank0;
   while (km) {
-    const int j = __builtin_ctz(km);
+    const int j = __builtin_ctzll(km);
     km &= km - 1;
     if (o < cap) vals[o] = uint32_t(uint64_t(tl.q0 + j) + boff);
     ++o;

@@ -70,17 +70,18 @@ struct Rle {
     if (left == 0 && !packed) return next_run();
     return true;
   }
+  // Threads tid (of nt, all holding the same state) expand the next n values into dst[0..n).
   template <typename T>
-  __device__ void expand(T* dst, uint32_t n, int lane) {
+  __device__ void expand(T* dst, uint32_t n, int tid, int nt = 64) {
     uint32_t done = 0;
     while (done < n) {
       if (left == 0 && !next_run()) return;
       const uint32_t take = min(left, n - done);
       if (!packed) {
-        for (uint32_t i = lane; i < take; i += 64) dst[done + i] = T(value);
+        for (uint32_t i = tid; i < take; i += nt) dst[done + i] = T(value);
       } else {
         const uint64_t mask = width >= 32 ? 0xffffffffull : ((1ull << width) - 1);
-        for (uint32_t i = lane; i < take; i += 64) {
+        for (uint32_t i = tid; i < take; i += nt) {
           const uint64_t b = bit + uint64_t(i) * width;
           dst[done + i] = T((load_u64(pk + (b >> 3)) >> (b & 7)) & mask);
         }
@@ -321,6 +322,34 @@ __global__ void __launch_bounds__(BA_T) k_ba_check(ParquetArgs a) {
 }
 
 // ---- dictionary pages --------------------------------------------------------------------------------
+// Pages whose values are all independent of each other (byte arrays with validated parallel
+// boundaries, fixed-width values) are spread over DICT_SLICES workgroups of 256 lanes each; the
+// rest (the serial byte-array walk) take one wave per page in k_pq_dict.
+constexpr uint32_t DICT_SLICES = 16;
+__device__ __forceinline__ bool dict_fast(const ParquetArgs& a, const PageDesc& pg) {
+  if (pg.phys == 6) return pg.ba && a.ba_ok[pg.ba_slot] && a.ba_count[pg.ba_slot] == pg.num_values;
+  return (pg.phys == 2 || pg.phys == 1) && uint64_t(pg.num_values) * (pg.phys == 2 ? 8 : 4) <= pg.usize;
+}
+
+__global__ void __launch_bounds__(256) k_pq_dict_fast(ParquetArgs a) {
+  const PageDesc& pg = a.pages[blockIdx.x];
+  if (pg.kind != PG_DICT || !dict_fast(a, pg)) return;
+  const uint8_t* p = reinterpret_cast<const uint8_t*>(pg.dst);
+  const uint32_t stride = 256 * DICT_SLICES;
+  if (pg.phys == 6) {
+    const uint32_t* vals = a.ba_vals + pg.ba_base;  // boundaries found in parallel (k_ba_*)
+    for (uint32_t k = blockIdx.y * 256 + threadIdx.x; k < pg.num_values; k += stride) {
+      const uint32_t off = vals[k];
+      a.dict_ptr[pg.dict_base + k] = reinterpret_cast<uint64_t>(p + off + 4);
+      a.dict_len[pg.dict_base + k] = load_u32(p + off);
+    }
+    return;
+  }
+  const bool w8 = pg.phys == 2;
+  for (uint32_t k = blockIdx.y * 256 + threadIdx.x; k < pg.num_values; k += stride)
+    a.dict_ptr[pg.dict_base + k] = w8 ? load_u64(p + 8ull * k) : uint64_t(int64_t(int32_t(load_u32(p + 4ull * k))));
+}
+
 __global__ void __launch_bounds__(64) k_pq_dict(ParquetArgs a) {
   const uint32_t i = blockIdx.x;
   if (i >= a.npages) return;
@@ -329,15 +358,7 @@ __global__ void __launch_bounds__(64) k_pq_dict(ParquetArgs a) {
   const int lane = threadIdx.x;
   const uint8_t* p = reinterpret_cast<const uint8_t*>(pg.dst);
   const uint8_t* end = p + pg.usize;
-  if (pg.phys == 6 && pg.ba && a.ba_ok[pg.ba_slot] && a.ba_count[pg.ba_slot] == pg.num_values) {
-    const uint32_t* vals = a.ba_vals + pg.ba_base;  // boundaries found in parallel (k_ba_bounds)
-    for (uint32_t k = lane; k < pg.num_values; k += 64) {
-      const uint32_t off = vals[k];
-      a.dict_ptr[pg.dict_base + k] = reinterpret_cast<uint64_t>(p + off + 4);
-      a.dict_len[pg.dict_base + k] = load_u32(p + off);
-    }
-    return;
-  }
+  if (dict_fast(a, pg)) return;  // k_pq_dict_fast
   if (pg.phys == 6) {  // BYTE_ARRAY: chain walk
     __shared__ uint64_t sp[64];
     __shared__ uint32_t sl[64];
@@ -370,9 +391,13 @@ __global__ void __launch_bounds__(64) k_pq_dict(ParquetArgs a) {
 }
 
 // ---- data pages ----------------------------------------------------------------------------------------
+// One 256-lane workgroup per page, 1024 levels per segment: levels expanded run by run by the whole
+// workgroup into LDS, value ranks by wave ballots + a workgroup prefix, then every lane writes rows.
+// The serial byte-array walk (pages whose boundaries were not validated) runs on wave 0.
 constexpr uint32_t SEG = 1024;   // levels per segment
+constexpr int PQD_T = 256;
 
-__global__ void __launch_bounds__(64) k_pq_data(ParquetArgs a) {
+__global__ void __launch_bounds__(PQD_T) k_pq_data(ParquetArgs a) {
   const uint32_t pi = blockIdx.x;
   if (pi >= a.npages) return;
   const PageDesc& pg = a.pages[pi];
@@ -382,7 +407,9 @@ __global__ void __launch_bounds__(64) k_pq_data(ParquetArgs a) {
   __shared__ uint32_t idxs[SEG];
   __shared__ uint64_t vptr[SEG];
   __shared__ uint32_t vlen[SEG];
-  const int lane = threadIdx.x;
+  __shared__ uint32_t wcnt[PQD_T / 64];
+  __shared__ uint32_t s_bad;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const FlatColumn col = a.cols[pg.col];
   const uint8_t* p = reinterpret_cast<const uint8_t*>(pg.dst);
   const uint8_t* end = p + pg.usize;
@@ -395,19 +422,19 @@ __global__ void __launch_bounds__(64) k_pq_data(ParquetArgs a) {
     p += pg.v2_rep_len + pg.v2_def_len;
   } else if (pg.max_rep > 0 || pg.max_def > 0) {
     if (pg.max_rep > 0) {
-      if (end - p < 4) { if (lane == 0) set_err(a.error, PQE_LEVELS); return; }
+      if (end - p < 4) { if (tid == 0) set_err(a.error, PQE_LEVELS); return; }
       const uint32_t l = load_u32(p);
       p += 4;
-      if (uint64_t(end - p) < l) { if (lane == 0) set_err(a.error, PQE_LEVELS); return; }
+      if (uint64_t(end - p) < l) { if (tid == 0) set_err(a.error, PQE_LEVELS); return; }
       repr.init(p, p + l, level_width(pg.max_rep));
       p += l;
     }
   }
   if (pg.kind != PG_DATA_V2 && pg.max_def > 0) {
-    if (end - p < 4) { if (lane == 0) set_err(a.error, PQE_LEVELS); return; }
+    if (end - p < 4) { if (tid == 0) set_err(a.error, PQE_LEVELS); return; }
     const uint32_t l = load_u32(p);
     p += 4;
-    if (uint64_t(end - p) < l) { if (lane == 0) set_err(a.error, PQE_LEVELS); return; }
+    if (uint64_t(end - p) < l) { if (tid == 0) set_err(a.error, PQE_LEVELS); return; }
     defr.init(p, p + l, level_width(pg.max_def));
     p += l;
   }
@@ -416,13 +443,13 @@ __global__ void __launch_bounds__(64) k_pq_data(ParquetArgs a) {
   Rle ir;
   ir.init(p, p, 0);
   if (dict) {
-    if (pg.dict < 0) { if (lane == 0) set_err(a.error, PQE_DICT); return; }
+    if (pg.dict < 0) { if (tid == 0) set_err(a.error, PQE_DICT); return; }
     const int w = p < end ? *p : 0;
     ir.init(p + 1, end, w);
   } else if (rle_bool) {
     ir.init(p + 4, end, 1);
   } else if (pg.encoding != 0) {
-    if (lane == 0) set_err(a.error, PQE_ENCODING);
+    if (tid == 0) set_err(a.error, PQE_ENCODING);
     return;
   }
   const uint32_t dict_base = dict ? a.pages[pg.dict].dict_base : 0;
@@ -433,53 +460,67 @@ __global__ void __launch_bounds__(64) k_pq_data(ParquetArgs a) {
   const uint32_t* ba_vals = a.ba_vals + pg.ba_base;
   const uint32_t ba_n = ba_fast ? a.ba_count[pg.ba_slot] : 0;
   const uint8_t* body = reinterpret_cast<const uint8_t*>(pg.dst);
-  if (pg.phys == 6 && !dict && !ba_fast) wk.init(p, end, lane);
+  const bool walk = pg.phys == 6 && !dict && !ba_fast;
+  if (walk && wv == 0) wk.init(p, end, lane);
+  if (tid == 0) s_bad = 0;
   uint64_t vbase = 0;  // values consumed before this segment (PLAIN fixed / boolean)
   for (uint32_t s0 = 0; s0 < pg.num_values; s0 += SEG) {
     const uint32_t n = min(SEG, pg.num_values - s0);
     if (pg.max_rep > 0) {
-      repr.expand(reps, n, lane);
-      if (repr.bad) { if (lane == 0) set_err(a.error, PQE_LEVELS); return; }
+      repr.expand(reps, n, tid, PQD_T);
+      if (repr.bad) { if (tid == 0) set_err(a.error, PQE_LEVELS); return; }
     }
     if (pg.max_def > 0) {
-      defr.expand(defs, n, lane);
-      if (defr.bad) { if (lane == 0) set_err(a.error, PQE_LEVELS); return; }
+      defr.expand(defs, n, tid, PQD_T);
+      if (defr.bad) { if (tid == 0) set_err(a.error, PQE_LEVELS); return; }
     } else {
-      for (uint32_t i = lane; i < n; i += 64) defs[i] = 0;
+      for (uint32_t i = tid; i < n; i += PQD_T) defs[i] = 0;
     }
     __syncthreads();
     // value rank of each level within the segment
     uint32_t nv = 0;
-    for (uint32_t b = 0; b < n; b += 64) {
-      const uint32_t i = b + lane;
+    for (uint32_t b = 0; b < n; b += PQD_T) {
+      const uint32_t i = b + tid;
       const bool isv = i < n && int(defs[i]) == pg.max_def;
       const unsigned long long m = __ballot(isv);
-      if (isv) idxs[i] = nv + uint32_t(__popcll(m & ((1ull << lane) - 1ull)));
-      nv += uint32_t(__popcll(m));
+      if (lane == 0) wcnt[wv] = uint32_t(__popcll(m));
+      __syncthreads();
+      uint32_t before = nv, tot = 0;
+      for (int k = 0; k < PQD_T / 64; ++k) {
+        before += k < wv ? wcnt[k] : 0u;
+        tot += wcnt[k];
+      }
+      if (isv) idxs[i] = before + uint32_t(__popcll(m & ((1ull << lane) - 1ull)));
+      nv += tot;
+      __syncthreads();
     }
     // values of this segment
     if (dict || rle_bool) {
-      ir.expand(vlen, nv, lane);  // dictionary indices / booleans (reuse vlen as scratch)
-      if (ir.bad) { if (lane == 0) set_err(a.error, dict ? PQE_DICT : PQE_VALUES); return; }
+      ir.expand(vlen, nv, tid, PQD_T);  // dictionary indices / booleans (reuse vlen as scratch)
+      if (ir.bad) { if (tid == 0) set_err(a.error, dict ? PQE_DICT : PQE_VALUES); return; }
     } else if (ba_fast) {
-      if (vbase + nv > ba_n) { if (lane == 0) set_err(a.error, PQE_VALUES); return; }
-    } else if (pg.phys == 6) {
-      for (uint32_t k = 0; k < nv; ++k) {
-        uint32_t l;
-        const uint8_t* v = wk.next(&l, lane);
-        if (lane == 0) { vptr[k] = reinterpret_cast<uint64_t>(v); vlen[k] = l; }
+      if (vbase + nv > ba_n) { if (tid == 0) set_err(a.error, PQE_VALUES); return; }
+    } else if (walk) {
+      if (wv == 0) {
+        for (uint32_t k = 0; k < nv; ++k) {
+          uint32_t l;
+          const uint8_t* v = wk.next(&l, lane);
+          if (lane == 0) { vptr[k] = reinterpret_cast<uint64_t>(v); vlen[k] = l; }
+        }
+        if (wk.bad && lane == 0) s_bad = 1;
       }
-      if (wk.bad) { if (lane == 0) set_err(a.error, PQE_VALUES); return; }
+      __syncthreads();
+      if (s_bad) { if (tid == 0) set_err(a.error, PQE_VALUES); return; }
     } else if (width) {
-      if ((vbase + nv) * width > uint64_t(end - p)) { if (lane == 0) set_err(a.error, PQE_VALUES); return; }
+      if ((vbase + nv) * width > uint64_t(end - p)) { if (tid == 0) set_err(a.error, PQE_VALUES); return; }
     } else if (pg.phys == 0) {
-      if ((vbase + nv + 7) / 8 > uint64_t(end - p)) { if (lane == 0) set_err(a.error, PQE_VALUES); return; }
+      if ((vbase + nv + 7) / 8 > uint64_t(end - p)) { if (tid == 0) set_err(a.error, PQE_VALUES); return; }
     } else {
-      if (lane == 0) set_err(a.error, PQE_ENCODING);
+      if (tid == 0) set_err(a.error, PQE_ENCODING);
       return;
     }
     __syncthreads();
-    for (uint32_t i = lane; i < n; i += 64) {
+    for (uint32_t i = tid; i < n; i += PQD_T) {
       const uint64_t row = pg.row_base + s0 + i;
       const uint8_t d = defs[i];
       col.def[row] = d;
@@ -584,10 +625,12 @@ void launch_ba_bounds(const ParquetArgs& a, hipStream_t st, void* scan_scratch) 
   hipLaunchKernelGGL(dev::k_ba_check, dim3(a.nba_tiles), dim3(dev::BA_T), 0, st, a);
 }
 void launch_pq_dict(const ParquetArgs& a, hipStream_t st) {
-  if (a.npages) hipLaunchKernelGGL(dev::k_pq_dict, dim3(a.npages), dim3(64), 0, st, a);
+  if (!a.npages) return;
+  hipLaunchKernelGGL(dev::k_pq_dict_fast, dim3(a.npages, dev::DICT_SLICES), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(dev::k_pq_dict, dim3(a.npages), dim3(64), 0, st, a);
 }
 void launch_pq_data(const ParquetArgs& a, hipStream_t st) {
-  if (a.npages) hipLaunchKernelGGL(dev::k_pq_data, dim3(a.npages), dim3(64), 0, st, a);
+  if (a.npages) hipLaunchKernelGGL(dev::k_pq_data, dim3(a.npages), dim3(dev::PQD_T), 0, st, a);
 }
 void launch_ckpt_assemble(const CkptAssembleArgs& a, hipStream_t st) {
   if (a.nrows) hipLaunchKernelGGL(dev::k_ckpt_assemble, dim3(unsigned((a.nrows + 255) / 256)), dim3(256), 0, st, a);

@@ -10,6 +10,7 @@
 #include <functional>
 #include <type_traits>
 #include <cstring>
+#include <cerrno>
 #include <cstdlib>
 #include <cstdio>
 #include <map>
@@ -1839,6 +1840,66 @@ int dr_state_counts(dr_state* state, dr_counts* out) {
   if (!state || !out) return DR_E_INVALID_ARG;
   *out = state->counts;
   return DR_OK;
+}
+
+// ValidateChecksum.checkMismatch (D/Checksum.scala:178-191) against ReadChecksum's parse of the
+// version's .crc first line (D/Checksum.scala:101-148, JsonUtils.mapper: unknown fields ignored).
+// A Long field that is absent or null reads as 0; a number with a fraction is truncated and a
+// numeric string is coerced (Jackson's defaults); anything else is a parse failure.
+static bool crc_long(const JVal& o, const char* name, int64_t* out) {
+  const JVal* v = o.get(name);
+  *out = 0;
+  if (!v || v->t == JVal::NUL) return true;
+  std::string t;
+  if (v->t == JVal::NUM) t = v->s;
+  else if (v->t == JVal::STR) t = v->s;
+  else return false;
+  errno = 0;
+  char* end = nullptr;
+  const long long x = std::strtoll(t.c_str(), &end, 10);
+  if (end == t.c_str() || errno) return false;
+  if (*end == '.' || *end == 'e' || *end == 'E') {  // ACCEPT_FLOAT_AS_INT: truncate
+    const double d = std::strtod(t.c_str(), &end);
+    if (*end || d != d || d >= 9.3e18 || d <= -9.3e18) return false;
+    *out = int64_t(d);
+    return true;
+  }
+  if (*end) return false;
+  *out = int64_t(x);
+  return true;
+}
+
+int dr_state_check_checksum(dr_state* state, const char* crc, uint64_t crc_len, char* msg, uint64_t msg_cap,
+                            uint64_t* msg_len) {
+  if (!state || (!crc && crc_len) || !msg_len) return DR_E_INVALID_ARG;
+  *msg_len = 0;
+  if (!crc_len) return DR_E_NO_CHECKSUM;  // delta.checksum.error.empty
+  JVal v;
+  if (!json_parse(crc, crc_len, &v) || v.t != JVal::OBJ) return DR_E_NO_CHECKSUM;  // error.parsing
+  int64_t tsb, nf, nm, np, nt;
+  if (!crc_long(v, "tableSizeBytes", &tsb) || !crc_long(v, "numFiles", &nf) || !crc_long(v, "numMetadata", &nm) ||
+      !crc_long(v, "numProtocol", &np) || !crc_long(v, "numTransactions", &nt))
+    return DR_E_NO_CHECKSUM;
+  const dr_counts& c = state->counts;
+  std::string out;
+  auto cmp = [&](int64_t expected, int64_t found, const char* title) {
+    if (expected == found) return;
+    if (!out.empty()) out += "\n";
+    out += fmt("%s - Expected: %lld Computed: %lld", title, (long long)expected, (long long)found);
+  };
+  cmp(tsb, c.size_in_bytes, "Table size (bytes)");
+  cmp(nf, c.num_files, "Number of files");
+  cmp(nm, c.num_metadata, "Metadata updates");
+  cmp(np, c.num_protocol, "Protocol updates");
+  cmp(nt, c.num_set_transactions, "Transactions");
+  if (out.empty()) return DR_OK;
+  *msg_len = out.size();
+  if (msg && msg_cap) {
+    const size_t k = std::min<size_t>(out.size(), msg_cap - 1);
+    memcpy(msg, out.data(), k);
+    msg[k] = 0;
+  }
+  return DR_E_CHECKSUM;
 }
 
 int dr_state_nonfile_json(dr_state* state, const char** json, uint64_t* len) {

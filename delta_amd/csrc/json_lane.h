@@ -148,8 +148,10 @@ JL_HD uint8_t file_key(const uint8_t* s, uint32_t n) {
 // ---- phase 1: tokenizer ----------------------------------------------------------------------------
 // A token is one u32: line offset << 16 | aux << 4 | class. Scalars are emitted when their run
 // ends, with aux = run length, so phase 2 never scans for a scalar's end.
+// T_STRING / T_STRING_ESC: a whole string (offset of its opening quote, body length in aux) -- one
+// token instead of an open/close pair when the body is shorter than 4096 bytes.
 enum : uint32_t { T_OBJ_OPEN = 0, T_ARR_OPEN, T_OBJ_CLOSE, T_ARR_CLOSE, T_COLON, T_COMMA, T_STR_OPEN,
-                  T_STR_CLOSE, T_STR_CLOSE_ESC, T_SCALAR };
+                  T_STR_CLOSE, T_STR_CLOSE_ESC, T_SCALAR, T_STRING, T_STRING_ESC };
 constexpr uint32_t TOK_MAX_LINE = 65535;   // longer lines go to the General walker
 constexpr uint32_t TOK_MAX_SCALAR = 4095;
 
@@ -263,6 +265,7 @@ struct Tokenizer {
   uint32_t pend_bs = 0;      // a backslash in the string still open
   uint32_t sc_start = 0;     // line offset where the open scalar run began
   uint32_t sc_bytes = 0;     // scalar bytes seen (each must belong to a validated scalar)
+  uint32_t str_open = 0;     // line offset of the open string's quote
   uint8_t status = ST_OK;
 };
 
@@ -353,13 +356,19 @@ JL_HD void tokenize_window(const uint8_t* p, uint32_t n, const uint32_t w[4], in
       if (instr & bit) {
         open_k = k;
         tz.pend_bs = 0;
-        emit(tok_make(off, 0, T_STR_OPEN));
+        tz.str_open = off;
       } else {
         const uint32_t below = bit - 1u;
         const bool has_bs = open_k != 0xFFFFFFFFu ? (m.bs & below & ~((2u << open_k) - 1u)) != 0
                                                   : (tz.pend_bs || (m.bs & below) != 0);
         open_k = 0xFFFFFFFFu;
-        emit(tok_make(off, 0, has_bs ? T_STR_CLOSE_ESC : T_STR_CLOSE));
+        const uint32_t len = off - tz.str_open - 1u;
+        if (len < 4096u) {
+          emit(tok_make(tz.str_open, len, has_bs ? T_STRING_ESC : T_STRING));
+        } else {
+          emit(tok_make(tz.str_open, 0, T_STR_OPEN));
+          emit(tok_make(off, 0, has_bs ? T_STR_CLOSE_ESC : T_STR_CLOSE));
+        }
       }
     } else if (st & bit) {
       const uint32_t c = win_byte(w, k);
@@ -391,6 +400,7 @@ JL_HD void tokenize_window(const uint8_t* p, uint32_t n, const uint32_t w[4], in
 // Line end: a scalar running to the last byte.
 template <typename Emit>
 JL_HD void tokenize_end(uint32_t n, Tokenizer& tz, Emit&& emit) {
+  if (tz.status == ST_OK && tz.in_str) emit(tok_make(tz.str_open, 0, T_STR_OPEN));  // never closed
   if (tz.status == ST_OK && tz.sc_carry) {
     const uint32_t len = n - tz.sc_start;
     if (len > TOK_MAX_SCALAR) { tz.status = ST_BAD; return; }
@@ -512,57 +522,72 @@ JL_HD uint8_t scalar_class(const uint8_t* s, uint32_t L, int64_t* val) {
   return SC_INT;
 }
 
+// String open / close steps of the DFA (a T_STRING token runs both).
+template <bool General>
+JL_HD bool dfa_str_open(uint32_t off, Dfa<General>& d) {
+  const uint8_t stt = d.state;
+  if (stt == S_OBJ_FIRST || stt == S_KEY) d.key_role = 1;
+  else if (stt == S_VALUE || stt == S_ARR_FIRST) d.key_role = 0;
+  else { d.status = ST_BAD; return false; }
+  d.state = S_STR;
+  d.str_start = off + 1;
+  return true;
+}
+template <bool General>
+JL_HD void dfa_str_close(const uint8_t* p, uint32_t off, bool has_bs, Dfa<General>& d) {
+  const uint8_t* s = p + d.str_start;
+  const uint32_t sl = off - d.str_start;
+  if (d.key_role) {
+    if (d.depth == 1 || (d.depth == 2 && d.in_file)) {
+      if (has_bs) {
+        if constexpr (!General) {
+          d.status = ST_HARD;
+          return;
+        } else {
+          uint8_t kb[24];
+          const uint32_t kl = unescape_key(s, sl, kb, 24);
+          if (d.depth == 1) d.k1 = kl == 0xFFFFFFFFu ? 0 : action_key(kb, kl);
+          else d.k2 = kl == 0xFFFFFFFFu ? FK_OTHER : file_key(kb, kl);
+        }
+      } else {
+        if (d.depth == 1) d.k1 = action_key_w(s, sl);
+        else d.k2 = file_key_w(s, sl);
+      }
+    }
+    d.state = S_COLON;
+  } else {
+    if (d.depth == 1) {
+      if (d.k1 == K_ADD || d.k1 == K_REMOVE) { d.status = ST_BAD; return; }  // struct from a string
+      if (d.k1) d.present |= 1u << d.k1;
+    } else if (d.depth == 2 && d.in_file) {
+      if (d.k2 == FK_PATH) {
+        d.cur.path_off = d.str_start;
+        d.cur.path_len = sl;
+        d.cur.flags = uint8_t((d.cur.flags & ~(F_PATH_NULL | F_PATH_ESCAPED)) | (has_bs ? F_PATH_ESCAPED : 0));
+      } else if (d.k2 == FK_SIZE || d.k2 == FK_DELTS) {
+        d.status = ST_BAD;  // LongType from a string token
+        return;
+      }
+    }
+    d.state = S_AFTER;
+  }
+}
+
 // One token through the JSON grammar and the Action.logSchema extraction.
 template <bool General>
 JL_HD void dfa_token(const uint8_t* p, uint32_t tok, Dfa<General>& d) {
   const uint32_t cls = tok_cls(tok), off = tok_off(tok);
   const uint8_t stt = d.state;
+  if (cls >= T_STRING) {
+    if (dfa_str_open(off, d)) dfa_str_close(p, off + 1 + tok_aux(tok), cls == T_STRING_ESC, d);
+    return;
+  }
   if (cls == T_STR_OPEN) {
-    if (stt == S_OBJ_FIRST || stt == S_KEY) d.key_role = 1;
-    else if (stt == S_VALUE || stt == S_ARR_FIRST) d.key_role = 0;
-    else { d.status = ST_BAD; return; }
-    d.state = S_STR;
-    d.str_start = off + 1;
+    dfa_str_open(off, d);
     return;
   }
   if (cls == T_STR_CLOSE || cls == T_STR_CLOSE_ESC) {
-    const bool has_bs = cls == T_STR_CLOSE_ESC;
-    const uint8_t* s = p + d.str_start;
-    const uint32_t sl = off - d.str_start;
-    if (d.key_role) {
-      if (d.depth == 1 || (d.depth == 2 && d.in_file)) {
-        if (has_bs) {
-          if constexpr (!General) {
-            d.status = ST_HARD;
-            return;
-          } else {
-            uint8_t kb[24];
-            const uint32_t kl = unescape_key(s, sl, kb, 24);
-            if (d.depth == 1) d.k1 = kl == 0xFFFFFFFFu ? 0 : action_key(kb, kl);
-            else d.k2 = kl == 0xFFFFFFFFu ? FK_OTHER : file_key(kb, kl);
-          }
-        } else {
-          if (d.depth == 1) d.k1 = action_key_w(s, sl);
-          else d.k2 = file_key_w(s, sl);
-        }
-      }
-      d.state = S_COLON;
-    } else {
-      if (d.depth == 1) {
-        if (d.k1 == K_ADD || d.k1 == K_REMOVE) { d.status = ST_BAD; return; }  // struct from a string
-        if (d.k1) d.present |= 1u << d.k1;
-      } else if (d.depth == 2 && d.in_file) {
-        if (d.k2 == FK_PATH) {
-          d.cur.path_off = d.str_start;
-          d.cur.path_len = sl;
-          d.cur.flags = uint8_t((d.cur.flags & ~(F_PATH_NULL | F_PATH_ESCAPED)) | (has_bs ? F_PATH_ESCAPED : 0));
-        } else if (d.k2 == FK_SIZE || d.k2 == FK_DELTS) {
-          d.status = ST_BAD;  // LongType from a string token
-          return;
-        }
-      }
-      d.state = S_AFTER;
-    }
+    dfa_str_close(p, off, cls == T_STR_CLOSE_ESC, d);
     return;
   }
   if (cls == T_SCALAR) {

@@ -31,7 +31,8 @@ class DeltaError(Exception):
 
     KIND = {3: "FileNotFoundException", 4: "FileNotFoundException", 5: "FileNotFoundException",
             6: "IllegalStateException", 7: "IllegalArgumentException", 8: "IllegalStateException",
-            9: "IllegalStateException", 10: "IllegalStateException", 11: "IllegalStateException"}
+            9: "IllegalStateException", 10: "IllegalStateException", 11: "IllegalStateException",
+            16: "IllegalStateException"}
 
     def __init__(self, status: int, msg: str):
         super().__init__(msg)
@@ -185,6 +186,22 @@ class State:
         eng.check(eng.lib.dr_state_nonfile_json(handle, C.byref(p), C.byref(n)))
         text = C.string_at(p, n.value).decode("utf-8") if n.value else ""
         self.nonfile = [json.loads(l) for l in text.splitlines() if l.strip()]
+
+    def check_checksum(self, crc_line: bytes) -> Optional[str]:
+        """checkMismatch (D/Checksum.scala:178-191): None when the counters match, else the
+        mismatch text. Raises ValueError when the line is not a VersionChecksum (no validation)."""
+        buf = C.create_string_buffer(1024)
+        n = C.c_uint64()
+        rc = self.eng.lib.dr_state_check_checksum(self.h, crc_line, len(crc_line), buf, 1024, C.byref(n))
+        if rc == N.DR_E_NO_CHECKSUM:
+            raise ValueError("unparseable checksum")
+        if rc == N.DR_E_CHECKSUM:
+            if n.value >= 1024:
+                buf = C.create_string_buffer(n.value + 1)
+                self.eng.lib.dr_state_check_checksum(self.h, crc_line, len(crc_line), buf, n.value + 1, C.byref(n))
+            return buf.value.decode("utf-8")
+        self.eng.check(rc)
+        return None
 
     def export(self, which: int) -> List[dict]:
         e = N.dr_export()
@@ -344,6 +361,37 @@ class Snapshot:
         sel = self.state.filter(prog)
         files = self.all_files
         return [files[i] for i in sel]
+
+    @property
+    def checksum_opt(self) -> Optional[bytes]:
+        """ReadChecksum.readChecksum (D/Checksum.scala:101-148): the first line of the version's
+        `%020d.crc` (FileNames.checksumFile), or None when it is missing or empty."""
+        fn = os.path.join(self.delta_log.log_path, "%020d.crc" % self.version)
+        try:
+            with open(fn, "rb") as f:
+                lines = f.read().splitlines()
+        except OSError:
+            return None  # delta.checksum.error.missing
+        return lines[0] if lines and lines[0] else None  # delta.checksum.error.empty
+
+    def validate_checksum(self, corruption_is_fatal: bool = True) -> Optional[str]:
+        """ValidateChecksum.validateChecksum (D/Checksum.scala:155-176). With
+        spark.databricks.delta.state.corruptionIsFatal (default true) a mismatch raises the
+        reference's IllegalStateException; otherwise the mismatch text is returned."""
+        line = self.checksum_opt
+        if line is None:
+            return None
+        try:
+            mismatch = self.state.check_checksum(line)
+        except ValueError:
+            return None  # delta.checksum.error.parsing
+        if mismatch is not None and corruption_is_fatal:
+            raise DeltaError(N.DR_E_CHECKSUM,
+                             "The transaction log has failed integrity checks. We recommend you contact "
+                             "Databricks support for assistance. To disable this check, set "
+                             "spark.databricks.delta.state.corruptionIsFatal to false. Failed verification at "
+                             "version %d of:\n%s" % (self.version, mismatch))
+        return mismatch
 
     def release(self) -> None:
         self.state.release()

@@ -45,7 +45,9 @@ enum dr_status {
   DR_E_UNSUPPORTED = 12,
   DR_E_OOM = 13,
   DR_E_DEVICE = 14,
-  DR_E_INTERNAL = 15
+  DR_E_INTERNAL = 15,
+  DR_E_CHECKSUM = 16,     /* computed state differs from the version's .crc (IllegalStateException) */
+  DR_E_NO_CHECKSUM = 17   /* .crc empty or unparseable: ReadChecksum yields None, nothing to validate */
 };
 
 /* Segment file kinds (D/DeltaLogFileIndex.scala:67-68). */
@@ -156,6 +158,14 @@ int dr_state_counts(dr_state* state, dr_counts* out);
 /* Latest protocol / metaData and the set transactions as JSON text in the reference's action
  * encoding ({"protocol":{...}} etc., one per line; D/actions/actions.scala:71). */
 int dr_state_nonfile_json(dr_state* state, const char** json, uint64_t* len);
+
+/* Snapshot.validateChecksum's comparison (D/Checksum.scala:155-191): `crc` is the first line of the
+ * version's `%020d.crc` (FileNames.checksumFile, D/util/FileNames.scala:36). Returns DR_OK when the
+ * five counters match, DR_E_CHECKSUM with checkMismatch's text ("Table size (bytes) - Expected: X
+ * Computed: Y" lines joined by '\n') in msg (NUL-terminated, *msg_len = full length), or
+ * DR_E_NO_CHECKSUM when the line is empty or does not parse as a VersionChecksum. */
+int dr_state_check_checksum(dr_state* state, const char* crc, uint64_t crc_len, char* msg, uint64_t msg_cap,
+                            uint64_t* msg_len);
 /* Materialises allFiles (DR_LIVE) or tombstones (DR_TOMBSTONES) on the host, dataChange=false. */
 int dr_state_export(dr_state* state, int32_t which, dr_export* out);
 

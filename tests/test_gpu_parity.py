@@ -174,3 +174,48 @@ def test_checkpoint_boundaries_found_in_parallel(engine, tmp_path, capfd, monkey
     for l in found:
         w = l.split()
         assert int(w[2]) == int(w[4]) > 0, l
+
+
+@pytest.mark.parametrize("table", ["dbr_8_0_non_generated_columns", "dbr_8_1_generated_columns"])
+def test_checksum_validation(tmp_path, table):
+    """ValidateChecksum (D/Checksum.scala:155-191) on the reference's own .crc files, then on
+    tampered, extended, unparseable and missing copies."""
+    import shutil
+    from delta_amd.delta_log import DeltaError, DeltaLog, ManualClock
+    root = tmp_path / table
+    shutil.copytree(os.path.join(REF, table), root)
+    crc = root / "_delta_log" / ("%020d.crc" % 0)
+    good = crc.read_bytes().splitlines()[0]
+    nf = json_field(good, "numFiles")
+    cases = [
+        (good, None),
+        (b'{"numProtocol":1,"numMetadata":1,"tableSizeBytes":%d,"numTransactions":"0","numFiles":%d,'
+         b'"histogramOpt":{"x":1}}' % (json_field(good, "tableSizeBytes"), json_field(good, "numFiles")), None),
+        (good.replace(b'"numFiles":%d' % nf, b'"numFiles":%d' % (nf + 7)),
+         "Number of files - Expected: %d Computed: %d" % (nf + 7, nf)),
+        (b'{"tableSizeBytes":5,"numFiles":%d,"numMetadata":2,"numProtocol":1,"numTransactions":3}' % nf,
+         "Table size (bytes) - Expected: 5 Computed: %d\nMetadata updates - Expected: 2 Computed: 1\n"
+         "Transactions - Expected: 3 Computed: 0" % json_field(good, "tableSizeBytes")),
+        (b"not json", None), (b"", None), (None, None),
+    ]
+    for content, mismatch in cases:
+        if content is None:
+            crc.unlink()
+        else:
+            crc.write_bytes(content + b"\n")
+        DeltaLog.clear_cache()
+        snap = DeltaLog.for_table(str(root), clock=ManualClock(0)).snapshot
+        assert snap.validate_checksum(corruption_is_fatal=False) == mismatch, content
+        if mismatch is None:
+            snap.validate_checksum()
+        else:
+            with pytest.raises(DeltaError) as ei:
+                snap.validate_checksum()
+            assert ei.value.kind == "IllegalStateException"
+            assert str(ei.value).endswith("Failed verification at version 0 of:\n" + mismatch)
+    DeltaLog.clear_cache()
+
+
+def json_field(line, name):
+    import json
+    return json.loads(line)[name]

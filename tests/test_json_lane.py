@@ -158,6 +158,10 @@ def corpus():
         b'{"add":{"path":"a","size":1234567890123456789}}', b'{"add":{"path":"a","size":-1234567890123456789}}',
         b'{"add":{"path":"a","size":-0.0}}', b'{"add":{"path":"a","size":1x}}', b'{"add":{"path":"a","size":nul}}',
         b'{"add":{"path":"a","size":nulll}}', b'{"add":{"path":"a","size":falsey}}', b'{"add":{"path":"a","size":truE}}',
+        # strings of 4096+ bytes (open/close token pair instead of one string token), unclosed strings
+        b'{"add":{"path":"' + b"y" * 5000 + b'","size":9}}', b'{"add":{"stats":"' + b'\\"' * 2100 + b'","path":"w"}}',
+        b'{"' + b"k" * 4095 + b'":1,"remove":{"path":"v"}}', b'{"' + b"k" * 4096 + b'":1,"remove":{"path":"v"}}',
+        b'{"add":{"path":"a"}}"', b'{"a":"xyz', b'"', b'{"a":"b","', b'{"add":{"path":"a\\"}}',
     ] + [b'{"remove":{"path":"r","deletionTimestamp":%s%s}}' % (sg, b"123456789012345678901"[:k])
          for k in range(1, 22) for sg in (b"", b"-")]
     return lines + hand

@@ -393,6 +393,25 @@ class Snapshot:
                              "version %d of:\n%s" % (self.version, mismatch))
         return mismatch
 
+    def initial_files(self, filters: Sequence = ()) -> List[dict]:
+        """DeltaSourceSnapshot.initialFiles + iterator (D/files/DeltaSourceSnapshot.scala:53-95):
+        allFiles sorted by (modificationTime, path) -- Spark's string order is the UTF-8 byte
+        order -- indexed by that order, then the partition-only filters applied (on the GPU, as
+        filterFileList with the "add" prefix). Returns IndexedFile records."""
+        files = self.all_files
+        order = sorted(range(len(files)), key=lambda i: (files[i]["modificationTime"],
+                                                         files[i]["path"].encode("utf-8")))
+        rank = {i: r for r, i in enumerate(order)}
+        parts = (self.metadata or {}).get("partitionColumns") or []
+        from .predicates import is_partition_only, build_program
+        # whole filters, not conjuncts (DeltaTableUtils.isPredicatePartitionColumnsOnly, :46-51)
+        preds = [f for f in filters if is_partition_only(f, parts)]
+        keep = set(range(len(files)))
+        if preds:
+            keep = set(self.state.filter(build_program(self.partition_schema(), preds)))
+        return [{"version": self.version, "index": rank[i], "add": files[i], "remove": None, "cdc": None,
+                 "isLast": False} for i in order if i in keep]
+
     def release(self) -> None:
         self.state.release()
 
@@ -456,6 +475,12 @@ class DeltaLog:
             if old is not None:
                 old.release()  # replaceSnapshot -> uncache (D/SnapshotManagement.scala:333-339)
             return new
+
+    def get_changes(self, start_version: int, fail_on_data_loss: bool = False):
+        """DeltaLog.getChanges (D/DeltaLog.scala:222-238): (version, [Action.fromJson(line)])
+        for every delta file at or after start_version (delta_amd/actions.py)."""
+        from .actions import get_changes
+        return get_changes(self.log_path, start_version, fail_on_data_loss)
 
     def get_snapshot_at(self, version: int) -> Snapshot:
         with self._lock:

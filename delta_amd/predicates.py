@@ -72,6 +72,12 @@ def _resolve(name: str, partition_cols: Sequence[str]) -> Optional[str]:
     return None
 
 
+def is_partition_only(expr, partition_cols: Sequence[str]) -> bool:
+    """DeltaTableUtils.isPredicatePartitionColumnsOnly: every column the expression references is
+    a partition column (resolved case-insensitively, as the session resolver does)."""
+    return all(_resolve(r, partition_cols) is not None for r in _refs(expr))
+
+
 def split_metadata_and_data_predicates(expr, partition_cols: Sequence[str]) -> Tuple[List, List]:
     """(metadata-only conjuncts, the rest): a conjunct is metadata-only when every column it
     references is a partition column (D/DeltaTable.scala:198-230)."""

@@ -112,3 +112,32 @@ def test_filter_config4_predicate(engine, tmp_path):
     got = _gpu_selected(engine, lp, preds, exp.min_file_retention_timestamp)
     assert got == _oracle_selected(lp, preds, exp.min_file_retention_timestamp)
     assert len(got[0]) > 0 and len(got[1]) > 0
+
+
+def test_delta_source_initial_files(tmp_path):
+    """DeltaSourceSnapshot.initialFiles + iterator (D/files/DeltaSourceSnapshot.scala:53-95): the
+    GPU state's allFiles in (modificationTime, path) order with their indices, partition-only
+    filters applied whole on the GPU (a filter that also names a data column is not applied)."""
+    from delta_amd.delta_log import DeltaLog, ManualClock
+    from delta_amd.testing import synth as S
+    spec = S.ChurnSpec(ckpt_files=3000, ckpt_version=5, n_deltas=3, removes_per_delta=400,
+                       adds_per_delta=400, readd_frac=0.5, ncols=4)
+    exp = S.build_table(str(tmp_path), spec, seed=7, row_group_size=1000)
+    lp = os.path.join(str(tmp_path), "_delta_log")
+    DeltaLog.clear_cache()
+    clock = ManualClock(exp.min_file_retention_timestamp + 7 * 24 * 3600 * 1000)
+    snap = DeltaLog.for_table(str(tmp_path), clock=clock).snapshot
+    ref = O.state_reconstruction(O.get_log_segment(lp), snap.min_file_retention_timestamp)
+    order = sorted(ref.all_files, key=lambda f: (f["modificationTime"], f["path"].encode("utf-8")))
+    idx = {f["path"]: i for i, f in enumerate(order)}
+    schema = O.partition_schema(ref.metadata)
+    part = ("in", C("p1"), [L("integer", v) for v in range(0, 300)])
+    mixed = ("and", ("=", C("p2"), L("string", S.WORDS[3])), ("=", C("value"), L("integer", 1)))
+    for filters in ([], [part], [part, mixed]):
+        got = snap.initial_files(filters)
+        keep = O.filter_file_list(schema, order, [part]) if filters else order
+        want = [(f["path"], idx[f["path"]]) for f in sorted(keep, key=lambda f: idx[f["path"]])]
+        assert [(g["add"]["path"], g["index"]) for g in got] == want
+        assert all(g["version"] == snap.version and g["remove"] is None and not g["isLast"] for g in got)
+    assert 0 < len(snap.initial_files([part])) < len(order)
+    DeltaLog.clear_cache()

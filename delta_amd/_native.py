@@ -31,7 +31,7 @@ SYMBOLS = [
     "dr_abi_version", "dr_ctx_create", "dr_ctx_destroy", "dr_last_error", "dr_log_segment",
     "dr_stage", "dr_stage_log", "dr_staged_release", "dr_staged_bytes", "dr_staged_plan",
     "dr_replay_staged",
-    "dr_replay", "dr_state_release", "dr_state_counts", "dr_state_nonfile_json", "dr_state_check_checksum",
+    "dr_replay", "dr_state_release", "dr_state_apply", "dr_state_counts", "dr_state_nonfile_json", "dr_state_check_checksum",
     "dr_state_export", "dr_filter", "dr_free", "dr_last_timings", "dr_set_timing",
     "dr_shard_plan", "dr_stage_log_shard", "dr_shard_begin", "dr_shard_pack", "dr_shard_reduce",
     "dr_shard_finish", "dr_shard_release",
@@ -128,6 +128,7 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "dr_state_release": ([vp], C.c_int),
         "dr_state_counts": ([vp, C.POINTER(dr_counts)], C.c_int),
         "dr_state_nonfile_json": ([vp, C.POINTER(C.c_char_p), C.POINTER(u64)], C.c_int),
+        "dr_state_apply": ([vp, vp, vp, C.c_int64, C.c_uint32, C.POINTER(vp)], C.c_int),
         "dr_state_check_checksum": ([vp, C.c_char_p, u64, C.c_char_p, u64, C.POINTER(u64)], C.c_int),
         "dr_state_export": ([vp, i32, C.POINTER(dr_export)], C.c_int),
         "dr_filter": ([vp, C.POINTER(dr_predicate), C.POINTER(_P64), _P64], C.c_int),

@@ -248,13 +248,18 @@ struct ExportCols {
 struct dr_state {
   dr_ctx* ctx = nullptr;
   std::shared_ptr<StagedData> staged;
+  // the staged segments the action records point into: {staged} for a replay; for a state built
+  // by dr_state_apply, its base's sources plus the applied tail (only sources[0] can hold
+  // checkpoint rows). src_id (empty: every action is from sources[0]) names each action's source.
+  std::vector<std::shared_ptr<StagedData>> sources;
+  DBuf<uint16_t> src_id;
   uint64_t n_actions = 0;
   // resident action arrays
   DBuf<uint8_t> kind, flags;
   DBuf<uint64_t> key, path_ptr, src_off;
   DBuf<uint32_t> path_len, src_len;
   DBuf<int64_t> size, delts;
-  DBuf<uint8_t> canon_arena;
+  std::vector<std::shared_ptr<DBuf<uint8_t>>> arenas;  // canonical special paths (path_ptr targets)
   DBuf<uint32_t> live, tomb;   // survivor action indices (hash order per bucket)
   uint64_t n_live = 0, n_tomb = 0;
   dr_counts counts{};
@@ -885,8 +890,8 @@ static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
   // ---- canonicalisation of special paths ----
   if (cnt[0]) {
     const uint64_t cap = cnt[1] * 2 + 64 * cnt[0] + 64;
-    st->canon_arena = DBuf<uint8_t>(ctx, cap);
-    CanonArgs cg{act, N, st->canon_arena.p, cap, counters.p + 4};
+    st->arenas.push_back(std::make_shared<DBuf<uint8_t>>(ctx, cap));
+    CanonArgs cg{act, N, st->arenas.back()->p, cap, counters.p + 4};
     launch_canon(cg, stream);
     ctx->mark("canon");
   }
@@ -1019,7 +1024,103 @@ static dr_state* new_state(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp) {
   auto st = std::make_unique<dr_state>();
   st->ctx = ctx;
   st->staged = sp;
+  if (sp) st->sources.push_back(sp);
   st->counts.version = sp ? sp->version : -1;
+  return st.release();
+}
+
+// Incremental tail apply (the reference rebuilds instead,
+// D/SnapshotManagement.scala:286-330). The base state's survivors -- live files, then tombstones:
+// distinct paths, so their relative order is free -- are the replay prefix of the new state, the
+// tail's commit lines follow in file order, and K3/K4 run over the concatenation with the new
+// retention cutoff: the same result as replaying the whole segment (tombstones the base already
+// dropped stay dropped, so the cutoff must not move backwards). Nothing of the base is re-parsed;
+// the new state keeps the base's staged segments, which its records point into.
+static dr_state* apply_tail(dr_ctx* ctx, dr_state& base, const std::shared_ptr<StagedData>& tail, int64_t cutoff,
+                            uint32_t flags) {
+  hipStream_t stream = ctx->stream;
+  if (!tail->parts.empty()) fail(DR_E_INVALID_ARG, "an applied tail holds commit (JSON) files only");
+  if (base.sources.empty()) fail(DR_E_INVALID_ARG, "base state has no staged segment");
+  if (base.sources.size() >= 65535) fail(DR_E_UNSUPPORTED, "too many applied tails on one state; rebuild it");
+  std::vector<int64_t> vers;
+  for (const JsonFileRec& j : tail->jfiles) vers.push_back(j.version);
+  std::sort(vers.begin(), vers.end());
+  bool contiguous = true;
+  for (size_t k = 0; k < vers.size(); ++k) contiguous &= vers[k] == base.counts.version + 1 + int64_t(k);
+  if (!contiguous) {  // verifyDeltaVersions' message (D/SnapshotManagement.scala:365-372)
+    std::string v = std::to_string(base.counts.version);
+    for (int64_t x : vers) v += ", " + std::to_string(x);
+    fail(DR_E_NONCONTIGUOUS, "Versions (Vector(" + v + ")) are not contiguous.");
+  }
+  std::unique_ptr<dr_state> t(new_state(ctx, tail));
+  std::vector<NonFileAction> nf;
+  parse_actions(ctx, tail, t.get(), nf);
+  const uint64_t M = base.n_live + base.n_tomb, T = t->n_actions, N = M + T;
+  if (N >= (uint64_t(1) << 30)) fail(DR_E_UNSUPPORTED, "more than 2^30 actions in one replay");
+  std::unique_ptr<dr_state> st(new_state(ctx, nullptr));
+  st->staged = base.staged;
+  st->sources = base.sources;
+  st->sources.push_back(tail);
+  st->arenas = base.arenas;
+  st->arenas.insert(st->arenas.end(), t->arenas.begin(), t->arenas.end());
+  st->counts.version = vers.empty() ? base.counts.version : vers.back();
+  st->n_actions = N;
+  st->kind = DBuf<uint8_t>(ctx, N);
+  st->flags = DBuf<uint8_t>(ctx, N);
+  st->key = DBuf<uint64_t>(ctx, N);
+  st->path_ptr = DBuf<uint64_t>(ctx, N);
+  st->path_len = DBuf<uint32_t>(ctx, N);
+  st->size = DBuf<int64_t>(ctx, N);
+  st->delts = DBuf<int64_t>(ctx, N);
+  st->src_off = DBuf<uint64_t>(ctx, N);
+  st->src_len = DBuf<uint32_t>(ctx, N);
+  st->src_id = DBuf<uint16_t>(ctx, N);
+  if (M) {  // the base's survivors, gathered
+    DBuf<uint32_t> sidx(ctx, M);
+    if (base.n_live)
+      HIP_OK(hipMemcpyAsync(sidx.p, base.live.p, base.n_live * 4, hipMemcpyDeviceToDevice, stream));
+    if (base.n_tomb)
+      HIP_OK(hipMemcpyAsync(sidx.p + base.n_live, base.tomb.p, base.n_tomb * 4, hipMemcpyDeviceToDevice, stream));
+    launch_gather_u8(base.kind.p, sidx.p, M, st->kind.p, stream);
+    launch_gather_u8(base.flags.p, sidx.p, M, st->flags.p, stream);
+    launch_gather_u64(base.key.p, sidx.p, M, st->key.p, stream);
+    launch_gather_u64(base.path_ptr.p, sidx.p, M, st->path_ptr.p, stream);
+    launch_gather_u32(base.path_len.p, sidx.p, M, st->path_len.p, stream);
+    launch_gather_u64(reinterpret_cast<const uint64_t*>(base.size.p), sidx.p, M,
+                      reinterpret_cast<uint64_t*>(st->size.p), stream);
+    launch_gather_u64(reinterpret_cast<const uint64_t*>(base.delts.p), sidx.p, M,
+                      reinterpret_cast<uint64_t*>(st->delts.p), stream);
+    launch_gather_u64(base.src_off.p, sidx.p, M, st->src_off.p, stream);
+    launch_gather_u32(base.src_len.p, sidx.p, M, st->src_len.p, stream);
+    if (base.src_id.p) launch_gather_u16(base.src_id.p, sidx.p, M, st->src_id.p, stream);
+    else HIP_OK(hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(st->src_id.p), 0, M, stream));
+  }
+  if (T) {  // then the tail's lines, in order
+    auto cp = [&](void* dst, const void* src, size_t bytes) {
+      HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream));
+    };
+    cp(st->kind.p + M, t->kind.p, T);
+    cp(st->flags.p + M, t->flags.p, T);
+    cp(st->key.p + M, t->key.p, T * 8);
+    cp(st->path_ptr.p + M, t->path_ptr.p, T * 8);
+    cp(st->path_len.p + M, t->path_len.p, T * 4);
+    cp(st->size.p + M, t->size.p, T * 8);
+    cp(st->delts.p + M, t->delts.p, T * 8);
+    cp(st->src_off.p + M, t->src_off.p, T * 8);
+    cp(st->src_len.p + M, t->src_len.p, T * 4);
+    HIP_OK(hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(st->src_id.p + M),
+                             uint16_t(st->sources.size() - 1), T, stream));
+  }
+  reduce_actions(ctx, st.get(), cutoff, flags);
+  st->counts.malformed_lines = t->counts.malformed_lines;
+  // protocol / metaData / txn: the base's winners first, then the tail's actions in order
+  std::vector<NonFileAction> all = base.nonfile;
+  for (size_t k = 0; k < all.size(); ++k) all[k].order = k;
+  for (NonFileAction& a : nf) {
+    a.order += all.size();
+    all.push_back(std::move(a));
+  }
+  reduce_nonfile(*st, all, !(flags & DR_FLAG_NO_VALIDATION));
   return st.release();
 }
 
@@ -1132,15 +1233,27 @@ static void load_ck_side(StagedData& s, bool add, CkRows& out) {
   }
 }
 
+constexpr uint8_t kFromCkpt = 16;  // dev_common.h F_FROM_CKPT: the action is a checkpoint row
+
 static void build_export(dr_state& st, int which) {
   ExportCols& ex = st.exp[which];
   if (ex.built) return;
   hipStream_t stream = st.ctx->stream;
-  StagedData& s = *st.staged;
+  StagedData& s = *st.sources[0];
   const uint64_t n = which == DR_LIVE ? st.n_live : st.n_tomb;
   std::vector<uint32_t> idx = d2h(which == DR_LIVE ? st.live.p : st.tomb.p, n, stream);
   std::vector<uint64_t> pptr(n), soff(n);
   std::vector<uint32_t> plen(n), slen(n);
+  std::vector<uint8_t> aflags;
+  std::vector<uint16_t> sid;
+  if (st.src_id.p) {  // a state from dr_state_apply: checkpoint rows by flag, JSON by source
+    DBuf<uint8_t> f(st.ctx, n);
+    DBuf<uint16_t> g(st.ctx, n);
+    launch_gather_u8(st.flags.p, which == DR_LIVE ? st.live.p : st.tomb.p, n, f.p, stream);
+    launch_gather_u16(st.src_id.p, which == DR_LIVE ? st.live.p : st.tomb.p, n, g.p, stream);
+    aflags = d2h(f.p, n, stream);
+    sid = d2h(g.p, n, stream);
+  }
   // gather the per-action fields (small D2H per record batch)
   {
     const uint32_t* didx = which == DR_LIVE ? st.live.p : st.tomb.p;
@@ -1176,9 +1289,11 @@ static void build_export(dr_state& st, int which) {
   ex.tags_val_off.push_back(0);
   for (uint64_t i = 0; i < n; ++i) {
     RecordFields r;
-    if (idx[i] >= s.ck_rows) {
+    const bool from_json = sid.empty() ? idx[i] >= s.ck_rows : !(aflags[i] & kFromCkpt);
+    if (from_json) {
+      const StagedData& src = sid.empty() ? s : *st.sources[sid[i]];
       JVal v;
-      json_parse(reinterpret_cast<const char*>(s.h_json.data() + soff[i]), slen[i], &v);
+      json_parse(reinterpret_cast<const char*>(src.h_json.data() + soff[i]), slen[i], &v);
       const JVal* o = v.get(which == DR_LIVE ? "add" : "remove");
       if (o) fields_from_json(*o, r);
     } else {
@@ -1325,8 +1440,8 @@ static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred)
   check_program(pred);
   dr_ctx* ctx = st.ctx;
   hipStream_t stream = ctx->stream;
-  if (!st.staged) fail(DR_E_INVALID_ARG, "state has no staged segment");
-  StagedData& s = *st.staged;
+  if (st.sources.empty()) fail(DR_E_INVALID_ARG, "state has no staged segment");
+  StagedData& s = *st.sources[0];
   const uint64_t R = s.ck_rows;
   FilterArgs fa{};
   fa.live = st.live.p;
@@ -1335,6 +1450,15 @@ static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred)
   fa.src_len = st.src_len.p;
   fa.ck_rows = R;
   fa.json = s.d_json.p;
+  DBuf<uint64_t> json_bases;
+  if (st.src_id.p) {
+    std::vector<uint64_t> bases;
+    for (auto& src : st.sources) bases.push_back(reinterpret_cast<uint64_t>(src->d_json.p));
+    json_bases = upload(ctx, bases.data(), bases.size());
+    fa.act_flags = st.flags.p;
+    fa.src_id = st.src_id.p;
+    fa.json_bases = json_bases.p;
+  }
   // checkpoint side: decode the add.partitionValues map columns (planned once per staged segment)
   DBuf<uint8_t> kdef, krep, vdef, vrep;
   DBuf<uint64_t> kptr, vptr, row_start, dict_ptr, rpos;
@@ -1834,6 +1958,24 @@ int dr_state_release(dr_state* state) {
   (void)hipStreamSynchronize(state->ctx->stream);
   delete state;
   return DR_OK;
+}
+
+int dr_state_apply(dr_ctx* ctx, dr_state* base, const dr_staged* tail, int64_t min_file_retention_timestamp,
+                   uint32_t flags, dr_state** out) {
+  if (!ctx || !base || !tail || !out) return DR_E_INVALID_ARG;
+  *out = nullptr;
+  int rc = guard(ctx, [&] {
+    HIP_OK(hipSetDevice(ctx->device));
+    ctx->mark("start");
+    *out = apply_tail(ctx, *base, tail->d, min_file_retention_timestamp, flags);
+    ctx->mark("end");
+    ctx->collect_timings();
+  });
+  if (rc != DR_OK) {
+    for (auto& m : ctx->marks) (void)hipEventDestroy(m.second);
+    ctx->marks.clear();
+  }
+  return rc;
 }
 
 int dr_state_counts(dr_state* state, dr_counts* out) {

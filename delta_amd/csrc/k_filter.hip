@@ -258,9 +258,11 @@ __global__ void __launch_bounds__(256) k_filter(FilterArgs a) {
         return c;
     return -1;
   };
-  if (act >= a.ck_rows) {
+  const bool from_json = a.act_flags ? !(a.act_flags[act] & F_FROM_CKPT) : act >= a.ck_rows;
+  if (from_json) {
     // JSON line: {"add":{..., "partitionValues":{"c":"v", ...}, ...}}
-    const uint8_t* b = a.json + a.src_off[act];
+    const uint8_t* json = a.act_flags ? reinterpret_cast<const uint8_t*>(a.json_bases[a.src_id[act]]) : a.json;
+    const uint8_t* b = json + a.src_off[act];
     const uint8_t* e = b + a.src_len[act];
     const uint8_t* p = skip_ws(b, e);
     bool ok = each_member(p, e, [&](const uint8_t* k, uint32_t kn, bool kesc, const uint8_t* v) -> const uint8_t* {

@@ -29,6 +29,12 @@ void launch_gather_u64(const uint64_t* src, const uint32_t* idx, uint64_t n, uin
 void launch_gather_u32(const uint32_t* src, const uint32_t* idx, uint64_t n, uint32_t* dst, hipStream_t st) {
   if (n) hipLaunchKernelGGL((dev::k_gather<uint32_t, uint32_t>), dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, src, idx, n, dst);
 }
+void launch_gather_u8(const uint8_t* src, const uint32_t* idx, uint64_t n, uint8_t* dst, hipStream_t st) {
+  if (n) hipLaunchKernelGGL((dev::k_gather<uint8_t, uint32_t>), dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, src, idx, n, dst);
+}
+void launch_gather_u16(const uint16_t* src, const uint32_t* idx, uint64_t n, uint16_t* dst, hipStream_t st) {
+  if (n) hipLaunchKernelGGL((dev::k_gather<uint16_t, uint32_t>), dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, src, idx, n, dst);
+}
 void launch_gather_u64_by64(const uint64_t* src, const uint64_t* idx, uint64_t n, uint64_t* dst, hipStream_t st) {
   if (n) hipLaunchKernelGGL((dev::k_gather<uint64_t, uint64_t>), dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, src, idx, n, dst);
 }

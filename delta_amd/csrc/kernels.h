@@ -309,6 +309,11 @@ struct FilterArgs {
   const uint32_t* src_len;
   uint64_t ck_rows;              // actions below this index are checkpoint rows
   const uint8_t* json;           // staged JSON bytes
+  // states built by dr_state_apply: checkpoint rows are told by F_FROM_CKPT and JSON lines are
+  // read from the staged bytes of their source (null: single segment, the fields above)
+  const uint8_t* act_flags;
+  const uint16_t* src_id;
+  const uint64_t* json_bases;
   // checkpoint add.partitionValues map (level entries)
   int32_t has_map;
   const uint64_t* row_start;     // [ck_rows + 1]
@@ -355,6 +360,8 @@ void launch_select(const uint32_t* flag, const uint64_t* pos, uint64_t n, int64_
 namespace dr {
 void launch_gather_u64(const uint64_t* src, const uint32_t* idx, uint64_t n, uint64_t* dst, hipStream_t st);
 void launch_gather_u32(const uint32_t* src, const uint32_t* idx, uint64_t n, uint32_t* dst, hipStream_t st);
+void launch_gather_u8(const uint8_t* src, const uint32_t* idx, uint64_t n, uint8_t* dst, hipStream_t st);
+void launch_gather_u16(const uint16_t* src, const uint32_t* idx, uint64_t n, uint16_t* dst, hipStream_t st);
 void launch_gather_u64_by64(const uint64_t* src, const uint64_t* idx, uint64_t n, uint64_t* dst, hipStream_t st);
 void launch_gather_bytes(const uint64_t* ptr, const uint32_t* len, const uint64_t* off, uint64_t n, uint8_t* out,
                          hipStream_t st);

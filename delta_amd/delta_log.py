@@ -187,6 +187,15 @@ class State:
         text = C.string_at(p, n.value).decode("utf-8") if n.value else ""
         self.nonfile = [json.loads(l) for l in text.splitlines() if l.strip()]
 
+    def apply(self, tail: "Staged", min_file_retention_timestamp: int, validate: bool = True) -> "State":
+        """dr_state_apply: this state extended by the staged commit files of the following
+        versions (no re-parse of this state's segment); a new State."""
+        st = C.c_void_p()
+        flags = 0 if validate else N.DR_FLAG_NO_VALIDATION
+        self.eng.check(self.eng.lib.dr_state_apply(self.eng.ctx, self.h, tail.h, int(min_file_retention_timestamp),
+                                                   flags, C.byref(st)))
+        return State(self.eng, st)
+
     def check_checksum(self, crc_line: bytes) -> Optional[str]:
         """checkMismatch (D/Checksum.scala:178-191): None when the counters match, else the
         mismatch text. Raises ValueError when the line is not a VersionChecksum (no validation)."""
@@ -468,13 +477,39 @@ class DeltaLog:
     def snapshot(self) -> Snapshot:
         return self._snapshot
 
-    def update(self) -> Snapshot:
+    def update(self, incremental: bool = False) -> Snapshot:
+        """SnapshotManagement.update (D/SnapshotManagement.scala:286-330). The reference rebuilds
+        the snapshot from the new segment; with `incremental` the commits after the current
+        version are applied to the resident state instead (dr_state_apply)."""
         with self._lock:
-            new = self._build(-1)
+            if incremental and self._snapshot is not None:
+                new = self._apply_new_commits()
+                if new is None:
+                    return self._snapshot
+            else:
+                new = self._build(-1)
             old, self._snapshot = self._snapshot, new
             if old is not None:
                 old.release()  # replaceSnapshot -> uncache (D/SnapshotManagement.scala:333-339)
             return new
+
+    def _apply_new_commits(self) -> Optional[Snapshot]:
+        cur = self._snapshot
+        names = sorted(n for n in os.listdir(self.log_path)
+                       if re.fullmatch(r"\d{20}\.json", n) and int(n[:20]) > cur.version)
+        if not names:
+            return None
+        files = []
+        for n in names:
+            with open(os.path.join(self.log_path, n), "rb") as f:
+                files.append((int(n[:20]), N.DR_FILE_JSON, 0, f.read()))
+        cutoff = self.min_file_retention_timestamp
+        staged = self.engine.stage_files(files)
+        try:
+            state = cur.state.apply(staged, cutoff)
+        finally:
+            staged.release()
+        return Snapshot(self, int(names[-1][:20]), state, cutoff)
 
     def get_changes(self, start_version: int, fail_on_data_loss: bool = False):
         """DeltaLog.getChanges (D/DeltaLog.scala:222-238): (version, [Action.fromJson(line)])

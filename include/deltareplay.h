@@ -153,6 +153,16 @@ int dr_replay(dr_ctx* ctx, const dr_file* files, int32_t nfiles,
               int64_t min_file_retention_timestamp, uint32_t flags, dr_state** out);
 int dr_state_release(dr_state* state);
 
+/* Incremental update: the state of `base`'s segment extended by the commit files staged in
+ * `tail` (dr_stage with JSON files of versions base+1, base+2, ... contiguous), with a new
+ * retention cutoff (not earlier than the base's). Replaces the full rebuild of
+ * SnapshotManagement.update (D/SnapshotManagement.scala:286-330) with K3/K4 over the base's
+ * survivors followed by the tail's lines; equal to dr_replay over the whole segment. `base` and
+ * `tail` stay owned by the caller and may be released afterwards (the new state keeps what it
+ * needs). DR_E_NONCONTIGUOUS when the tail's versions do not follow the base's. */
+int dr_state_apply(dr_ctx* ctx, dr_state* base, const dr_staged* tail, int64_t min_file_retention_timestamp,
+                   uint32_t flags, dr_state** out);
+
 /* ---- results ------------------------------------------------------------------------------ */
 int dr_state_counts(dr_state* state, dr_counts* out);
 /* Latest protocol / metaData and the set transactions as JSON text in the reference's action

@@ -219,3 +219,96 @@ def test_checksum_validation(tmp_path, table):
 def json_field(line, name):
     import json
     return json.loads(line)[name]
+
+
+def _commit_files(lp, lo, hi):
+    from delta_amd import _native as N
+    out = []
+    for v in range(lo, hi + 1):
+        with open(os.path.join(lp, "%020d.json" % v), "rb") as f:
+            out.append((v, N.DR_FILE_JSON, 0, f.read()))
+    return out
+
+
+def test_incremental_apply_matches_full_replay(engine, tmp_path):
+    """dr_state_apply: a checkpointed base extended one commit at a time,
+    then by a batch, equals the full replay of the segment at every version (records, counters,
+    non-file winners) and the oracle; partition pruning runs over the multi-segment state."""
+    from delta_amd.predicates import build_program, partition_schema
+    from delta_amd.testing import synth as S
+    from tests.filter_corpus import C, L
+    spec = S.ChurnSpec(ckpt_files=4000, ckpt_version=3, n_deltas=6, removes_per_delta=500,
+                       adds_per_delta=500, readd_frac=0.5, ncols=2)
+    exp = S.build_table(str(tmp_path), spec, seed=11, row_group_size=1500)
+    lp = os.path.join(str(tmp_path), "_delta_log")
+    cutoff = exp.min_file_retention_timestamp
+    last = spec.ckpt_version + spec.n_deltas
+    st = _gpu_replay(engine, lp, cutoff, version=spec.ckpt_version + 1)
+    states = [st]
+    try:
+        for v in range(spec.ckpt_version + 2, last + 1):
+            tail = engine.stage_files(_commit_files(lp, v, v))
+            nxt = states[-1].apply(tail, cutoff)
+            tail.release()
+            states.append(nxt)
+            full = _gpu_replay(engine, lp, cutoff, version=v)
+            try:
+                for k in ("num_files", "size_in_bytes", "num_removes", "num_metadata", "num_protocol",
+                          "num_set_transactions", "live_key_sum", "tomb_key_sum", "version"):
+                    assert nxt.counts[k] == full.counts[k], (v, k)
+                assert sorted(map(_canon, nxt.export(0))) == sorted(map(_canon, full.export(0)))
+                assert sorted(map(_canon, nxt.export(1))) == sorted(map(_canon, full.export(1)))
+                assert nxt.nonfile == full.nonfile
+            finally:
+                full.release()
+        snap = O.state_reconstruction(O.get_log_segment(lp), cutoff)
+        _assert_same(states[-1], snap)
+        # a batch tail, and pruning over the resulting four-segment state
+        batch = engine.stage_files(_commit_files(lp, spec.ckpt_version + 2, last))
+        b = states[0].apply(batch, cutoff)
+        batch.release()
+        states.append(b)
+        _assert_same(b, snap)
+        meta = next(a["metaData"] for a in b.nonfile if "metaData" in a)
+        pred = [("in", C("p1"), [L("integer", v) for v in range(0, 400)])]
+        for s in (b, states[-2]):
+            live = s.export(0)
+            got = sorted(live[i]["path"] for i in s.filter(build_program(partition_schema(meta), pred)))
+            want = sorted(f["path"] for f in O.filter_file_list(O.partition_schema(snap.metadata), snap.all_files, pred))
+            assert got == want and got
+    finally:
+        for s in states:
+            s.release()
+
+
+def test_incremental_apply_errors_and_delta_log_update(engine, tmp_path):
+    import shutil
+    from delta_amd.delta_log import DeltaError, DeltaLog, ManualClock
+    root = tmp_path / "t"
+    shutil.copytree(os.path.join(REF, "delta-0.2.0"), root)
+    lp = str(root / "_delta_log")
+    base = _gpu_replay(engine, lp, 0, version=1)
+    try:
+        gap = engine.stage_files(_commit_files(lp, 3, 3))
+        with pytest.raises(DeltaError) as ei:
+            base.apply(gap, 0)
+        gap.release()
+        assert ei.value.kind == "IllegalStateException" and "are not contiguous" in str(ei.value)
+    finally:
+        base.release()
+    # DeltaLog.update(incremental=True) over a log that grows, against a rebuild
+    for v in (2, 3):
+        os.rename(os.path.join(lp, "%020d.json" % v), os.path.join(lp, "%020d.json.hold" % v))
+    os.remove(os.path.join(lp, "_last_checkpoint"))
+    os.remove(os.path.join(lp, "%020d.checkpoint.parquet" % 3))
+    DeltaLog.clear_cache()
+    log = DeltaLog.for_table(str(root), clock=ManualClock(1564524298213))
+    assert log.snapshot.version == 1
+    for v in (2, 3):
+        os.rename(os.path.join(lp, "%020d.json.hold" % v), os.path.join(lp, "%020d.json" % v))
+        snap = log.update(incremental=True)
+        assert snap.version == v
+        ref = O.state_reconstruction(O.get_log_segment(lp), log.min_file_retention_timestamp)
+        _assert_same(snap.state, ref)
+    assert log.update(incremental=True) is snap
+    DeltaLog.clear_cache()

@@ -402,6 +402,32 @@ class Snapshot:
                              "version %d of:\n%s" % (self.version, mismatch))
         return mismatch
 
+    def list_files(self, partition_filters: Sequence = ()) -> List[Tuple[tuple, List[dict]]]:
+        """TahoeFileIndex.listFiles (D/files/TahoeFileIndex.scala:58-81): the pruned files grouped
+        by partitionValues; each group is (partition row cast to the partition schema's types,
+        [FileStatus {length, modificationTime, path}]) with paths made absolute under the table
+        (absolutePath, :86-93). A file lacking a partition column raises KeyError, as
+        `partitionValues(p.name)` throws."""
+        from urllib.parse import unquote
+        from .predicates import cast_partition_value
+        schema = self.partition_schema()
+        groups: Dict[tuple, list] = {}
+        for f in self.files_for_scan(partition_filters):
+            pv = f.get("partitionValues") or {}
+            key = tuple(sorted(pv.items(), key=lambda kv: kv[0]))
+            groups.setdefault(key, [pv, []])[1].append(f)
+        out = []
+        for pv, files in groups.values():
+            row = tuple(cast_partition_value(pv[c], t) for c, t in schema.items())
+            stats = []
+            for f in files:
+                p = unquote(f["path"].split("://", 1)[-1]) if "://" in f["path"] else unquote(f["path"])
+                if not (f["path"].startswith("/") or "://" in f["path"] or f["path"].startswith("file:")):
+                    p = os.path.join(self.delta_log.data_path, p)
+                stats.append({"length": f["size"], "modificationTime": f["modificationTime"], "path": p})
+            out.append((row, stats))
+        return out
+
     def initial_files(self, filters: Sequence = ()) -> List[dict]:
         """DeltaSourceSnapshot.initialFiles + iterator (D/files/DeltaSourceSnapshot.scala:53-95):
         allFiles sorted by (modificationTime, path) -- Spark's string order is the UTF-8 byte

@@ -112,6 +112,34 @@ def _date_days(s: str) -> Optional[int]:
         return None
 
 
+_INT_BITS = {"byte": 8, "short": 16, "integer": 32, "long": 64}
+_WS = " \t\n\r\x0b\x0c"
+
+
+def cast_partition_value(s: Optional[str], typ: str):
+    """Cast(Literal(partitionValues(col)), partition type) on the host, non-ANSI (a failed cast is
+    null), as TahoeFileIndex.listFiles builds a partition row (D/files/TahoeFileIndex.scala:61-64):
+    integral types from trimmed decimal text in range, booleans from t/true/y/yes/1 and
+    f/false/n/no/0, dates as datetime.date, strings unchanged. Same grammar as the device cast."""
+    if s is None:
+        return None
+    if typ == "string":
+        return s
+    t = s.strip(_WS)
+    if typ in _INT_BITS:
+        if not re.fullmatch(r"[+-]?\d+", t):
+            return None
+        v, b = int(t), _INT_BITS[typ]
+        return v if -(1 << (b - 1)) <= v < (1 << (b - 1)) else None
+    if typ == "boolean":
+        tl = t.lower()
+        return True if tl in ("t", "true", "y", "yes", "1") else False if tl in ("f", "false", "n", "no", "0") else None
+    if typ == "date":
+        d = _date_days(t)
+        return None if d is None else _EPOCH + _dt.timedelta(days=d)
+    raise PredicateError("unsupported partition type %r" % typ)
+
+
 def _lit(typ: str, v):
     """Literal value as the device sees it (the oracle's _lit_value): dates as days since the
     epoch, booleans as 0/1, strings as bytes."""

@@ -141,3 +141,32 @@ def test_delta_source_initial_files(tmp_path):
         assert all(g["version"] == snap.version and g["remove"] is None and not g["isLast"] for g in got)
     assert 0 < len(snap.initial_files([part])) < len(order)
     DeltaLog.clear_cache()
+
+
+def test_tahoe_list_files(tmp_path):
+    """TahoeFileIndex.listFiles (D/files/TahoeFileIndex.scala:58-81): pruned files grouped by
+    partitionValues, rows cast to the partition schema, sizes / mtimes / absolute paths."""
+    import datetime as dt
+    from delta_amd.delta_log import DeltaLog, ManualClock
+    from delta_amd.testing import synth as S
+    spec = S.ChurnSpec(ckpt_files=2000, ckpt_version=2, n_deltas=2, removes_per_delta=300,
+                       adds_per_delta=300, readd_frac=0.5, ncols=4)
+    exp = S.build_table(str(tmp_path), spec, seed=9, row_group_size=700)
+    lp = os.path.join(str(tmp_path), "_delta_log")
+    DeltaLog.clear_cache()
+    snap = DeltaLog.for_table(str(tmp_path), clock=ManualClock(exp.min_file_retention_timestamp + 604800000)).snapshot
+    ref = O.state_reconstruction(O.get_log_segment(lp), snap.min_file_retention_timestamp)
+    schema = O.partition_schema(ref.metadata)
+    pred = [("<", C("p1"), L("integer", 40))]
+    kept = O.filter_file_list(schema, ref.all_files, pred)
+    want = {}
+    for f in kept:
+        row = []
+        for c, t in schema.items():
+            v = O.cast_string(f["partitionValues"].get(c), t)
+            row.append(dt.date(1970, 1, 1) + dt.timedelta(days=v) if t == "date" and v is not None
+                       else (bool(v) if t == "boolean" and v is not None else v))
+        want.setdefault(tuple(row), set()).add((f["size"], f["modificationTime"], os.path.join(str(tmp_path), f["path"])))
+    got = {row: {(s["length"], s["modificationTime"], s["path"]) for s in stats} for row, stats in snap.list_files(pred)}
+    assert got == want and len(got) > 1
+    DeltaLog.clear_cache()

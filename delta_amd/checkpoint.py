@@ -1,0 +1,192 @@
+"""Checkpoint writer from the resident state (rows a20 / a21).
+
+`Checkpoints.writeCheckpoint` / `buildCheckpoint` (D/Checkpoints.scala:229-365) writes the
+snapshot's state -- protocol, metaData, txns, live AddFiles and unexpired RemoveFiles, commitInfo
+and cdc dropped, every record with dataChange=false -- as one Parquet file of SingleAction rows,
+checks that it holds numOfFiles adds, and records `_last_checkpoint` = {"version", "size"}. The
+`add` struct is rebuilt as (path, partitionValues, size, modificationTime, dataChange, tags, stats)
+(stats while `checkpoint.writeStatsAsJson`, on by default, :341-343). The schema is nullable
+throughout (`chk.schema.asNullable`).
+
+Here the records come from the GPU state through `dr_state_export`'s columnar buffers (gathered
+on the device) and are turned into Arrow columns without per-record Python objects; Arrow's
+Parquet C++ writer encodes them (SNAPPY, dictionary pages). `parts > 1` writes the protocol's
+multi-part form (FileNames.checkpointFileWithParts, D/util/FileNames.scala:70-73; PROTOCOL.md
+"Checkpoints"): part i of n holds a contiguous slice of the rows and `_last_checkpoint` carries
+"parts". A sharded replay's ranks each hold a path-hash shard of the state and can write their own
+part with `write_part` (rank 0 then writes `_last_checkpoint`).
+"""
+import ctypes as C
+import json
+import os
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _native as N
+
+
+def _np(ptr, n, dtype):
+    if n == 0 or not ptr:
+        return np.zeros(0, dtype)
+    return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(np.ctypeslib.as_ctypes_type(dtype))), shape=(n,)).copy()
+
+
+def _bytes(ptr, n):
+    return C.string_at(ptr, n) if n else b""
+
+
+def _strings(pa, off_ptr, data_ptr, n, null=None):
+    off = _np(off_ptr, n + 1, np.int64)
+    data = _bytes(data_ptr, int(off[-1]) if n else 0)
+    mask = None if null is None else pa.py_buffer(np.packbits(~null.astype(bool), bitorder="little").tobytes())
+    return pa.LargeStringArray.from_buffers(n, pa.py_buffer(off.tobytes()), pa.py_buffer(data), mask,
+                                            int(null.sum()) if null is not None else 0).cast(pa.string())
+
+
+def _map(pa, e, pre, n):
+    entry_off = _np(getattr(e, pre + "_entry_off"), n + 1, np.int64)
+    m = int(entry_off[-1]) if n else 0
+    keys = _strings(pa, getattr(e, pre + "_key_off"), getattr(e, pre + "_key_bytes"), m)
+    vnull = _np(getattr(e, pre + "_val_null"), m, np.uint8)
+    vals = _strings(pa, getattr(e, pre + "_val_off"), getattr(e, pre + "_val_bytes"), m, vnull)
+    null = _np(getattr(e, pre + "_null"), n, np.uint8).astype(bool)
+    offs = pa.array(entry_off.astype(np.int32), pa.int32())
+    return pa.MapArray.from_arrays(offs, keys, vals, mask=pa.array(null) if null.any() else None)
+
+
+def _types(pa):
+    mt = pa.map_(pa.string(), pa.string())
+    add_t = pa.struct([("path", pa.string()), ("partitionValues", mt), ("size", pa.int64()),
+                       ("modificationTime", pa.int64()), ("dataChange", pa.bool_()), ("tags", mt),
+                       ("stats", pa.string())])
+    rm_t = pa.struct([("path", pa.string()), ("deletionTimestamp", pa.int64()), ("dataChange", pa.bool_()),
+                      ("extendedFileMetadata", pa.bool_()), ("partitionValues", mt), ("size", pa.int64()),
+                      ("tags", mt)])
+    txn_t = pa.struct([("appId", pa.string()), ("version", pa.int64()), ("lastUpdated", pa.int64())])
+    fmt_t = pa.struct([("provider", pa.string()), ("options", mt)])
+    md_t = pa.struct([("id", pa.string()), ("name", pa.string()), ("description", pa.string()),
+                      ("format", fmt_t), ("schemaString", pa.string()),
+                      ("partitionColumns", pa.list_(pa.string())), ("configuration", mt),
+                      ("createdTime", pa.int64())])
+    prot_t = pa.struct([("minReaderVersion", pa.int32()), ("minWriterVersion", pa.int32())])
+    return mt, add_t, rm_t, txn_t, md_t, prot_t
+
+
+def _file_struct(pa, state, which, typ):
+    e = N.dr_export()
+    state.eng.check(state.eng.lib.dr_state_export(state.h, which, C.byref(e)))
+    n = int(e.n)
+    path = _strings(pa, e.path_off, e.path_bytes, n)
+    pv = _map(pa, e, "pv", n)
+    tags = _map(pa, e, "tags", n)
+    size = pa.array(_np(e.size, n, np.int64), pa.int64())
+    dc = pa.array(np.zeros(n, bool), pa.bool_())
+    if which == N.DR_LIVE:
+        stats = _strings(pa, e.stats_off, e.stats_bytes, n, _np(e.stats_null, n, np.uint8))
+        cols = [path, pv, size, pa.array(_np(e.modification_time, n, np.int64), pa.int64()), dc, tags, stats]
+    else:
+        valid = _np(e.deletion_timestamp_valid, n, np.uint8).astype(bool)
+        dts = pa.array(_np(e.deletion_timestamp, n, np.int64), pa.int64(), mask=~valid)
+        efm = pa.array(_np(e.extended_file_metadata, n, np.uint8).astype(bool), pa.bool_())
+        cols = [path, dts, dc, efm, pv, size, tags]
+    return pa.StructArray.from_arrays(cols, fields=list(typ)), n
+
+
+def _nonfile_rows(state):
+    prot, md, txns = None, None, []
+    for a in state.nonfile:
+        if "protocol" in a:
+            prot = a["protocol"]
+        elif "metaData" in a:
+            md = a["metaData"]
+        elif "txn" in a:
+            txns.append(a["txn"])
+    return prot, md, txns
+
+
+def checkpoint_table(state):
+    """The checkpoint rows of a GPU state as an Arrow table (protocol, metaData, txns, adds,
+    removes; columns txn, add, remove, metaData, protocol)."""
+    import pyarrow as pa
+    mt, add_t, rm_t, txn_t, md_t, prot_t = _types(pa)
+    adds, na = _file_struct(pa, state, N.DR_LIVE, add_t)
+    rms, nr = _file_struct(pa, state, N.DR_TOMBSTONES, rm_t)
+    prot, md, txns = _nonfile_rows(state)
+    head = []
+    if prot is not None:
+        head.append({"protocol": {"minReaderVersion": prot.get("minReaderVersion", 0),
+                                  "minWriterVersion": prot.get("minWriterVersion", 0)}})
+    if md is not None:
+        fmt = md.get("format") or {}
+        head.append({"metaData": {
+            "id": md.get("id"), "name": md.get("name"), "description": md.get("description"),
+            "format": {"provider": fmt.get("provider"), "options": list((fmt.get("options") or {}).items())},
+            "schemaString": md.get("schemaString"), "partitionColumns": md.get("partitionColumns"),
+            "configuration": list((md.get("configuration") or {}).items()), "createdTime": md.get("createdTime")}})
+    for t in txns:
+        head.append({"txn": {"appId": t.get("appId"), "version": t.get("version", 0),
+                             "lastUpdated": t.get("lastUpdated")}})
+    h = len(head)
+
+    def col(name, typ):
+        return pa.array([r.get(name) for r in head], typ)
+
+    def cat(head_arr, body, typ, at):
+        parts = [head_arr]
+        for k, (arr, n) in enumerate(body):
+            parts.append(arr if k == at else pa.nulls(n, typ))
+        return pa.concat_arrays([p for p in parts if len(p)]) if h + na + nr else pa.array([], typ)
+
+    body = [(adds, na), (rms, nr)]
+    table = pa.Table.from_arrays([
+        cat(col("txn", txn_t), body, txn_t, -1),
+        cat(pa.nulls(h, add_t), body, add_t, 0),
+        cat(pa.nulls(h, rm_t), body, rm_t, 1),
+        cat(col("metaData", md_t), body, md_t, -1),
+        cat(col("protocol", prot_t), body, prot_t, -1),
+    ], names=["txn", "add", "remove", "metaData", "protocol"])
+    return table, na
+
+
+def checkpoint_file_with_parts(log_path: str, version: int, part: int, parts: int) -> str:
+    return os.path.join(log_path, "%020d.checkpoint.%010d.%010d.parquet" % (version, part, parts))
+
+
+def write_part(state, log_path: str, version: int, part: int, parts: int, row_group_size: int = 1 << 20) -> int:
+    """One part (1-based) of a multi-part checkpoint from one shard's state; returns its row count."""
+    import pyarrow.parquet as pq
+    table, _ = checkpoint_table(state)
+    path = checkpoint_file_with_parts(log_path, version, part, parts)
+    tmp = os.path.join(os.path.dirname(path), ".%s.tmp" % os.path.basename(path))
+    pq.write_table(table, tmp, compression="snappy", row_group_size=row_group_size, write_statistics=False)
+    os.replace(tmp, path)
+    return table.num_rows
+
+
+def write_checkpoint(snapshot, parts: int = 1, row_group_size: int = 1 << 20) -> dict:
+    """writeCheckpoint for a GPU snapshot: the checkpoint file(s) of snapshot.version and
+    `_last_checkpoint`; returns the CheckpointMetaData written there."""
+    import pyarrow.parquet as pq
+    table, n_adds = checkpoint_table(snapshot.state)
+    if n_adds != snapshot.num_of_files:  # D/Checkpoints.scala:310-313
+        raise RuntimeError("State of the checkpoint doesn't match that of the snapshot.")
+    log_path = snapshot.delta_log.log_path
+    rows = table.num_rows
+    if parts <= 1:
+        paths = [os.path.join(log_path, "%020d.checkpoint.parquet" % snapshot.version)]
+        slices = [table]
+    else:
+        paths = [checkpoint_file_with_parts(log_path, snapshot.version, i + 1, parts) for i in range(parts)]
+        step = (rows + parts - 1) // parts
+        slices = [table.slice(i * step, max(0, min(step, rows - i * step))) for i in range(parts)]
+    for path, t in zip(paths, slices):
+        tmp = os.path.join(os.path.dirname(path), ".%s.tmp" % os.path.basename(path))
+        pq.write_table(t, tmp, compression="snappy", row_group_size=row_group_size, write_statistics=False)
+        os.replace(tmp, path)  # a reader never sees a partial part
+    meta = {"version": snapshot.version, "size": rows}
+    if parts > 1:
+        meta["parts"] = parts
+    with open(os.path.join(log_path, "_last_checkpoint"), "w") as f:
+        f.write(json.dumps(meta) + "\n")
+    return meta

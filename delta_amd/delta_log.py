@@ -537,6 +537,13 @@ class DeltaLog:
             staged.release()
         return Snapshot(self, int(names[-1][:20]), state, cutoff)
 
+    def checkpoint(self, parts: int = 1) -> dict:
+        """Checkpoints.checkpoint (D/Checkpoints.scala:119-141): write the current snapshot's
+        checkpoint (multi-part when parts > 1) and `_last_checkpoint` (delta_amd/checkpoint.py)."""
+        from .checkpoint import write_checkpoint
+        with self._lock:
+            return write_checkpoint(self._snapshot, parts=parts)
+
     def get_changes(self, start_version: int, fail_on_data_loss: bool = False):
         """DeltaLog.getChanges (D/DeltaLog.scala:222-238): (version, [Action.fromJson(line)])
         for every delta file at or after start_version (delta_amd/actions.py)."""

@@ -312,3 +312,45 @@ def test_incremental_apply_errors_and_delta_log_update(engine, tmp_path):
         _assert_same(snap.state, ref)
     assert log.update(incremental=True) is snap
     DeltaLog.clear_cache()
+
+
+@pytest.mark.parametrize("parts", [1, 3])
+def test_checkpoint_writer_round_trip(engine, tmp_path, parts):
+    """writeCheckpoint (D/Checkpoints.scala:229-365) from the GPU state: the written checkpoint
+    (single or multi-part, with _last_checkpoint) replays -- on the GPU and in the oracle, which
+    reads it with pyarrow -- to the same state, and holds the reference's column layout."""
+    import json
+    import pyarrow.parquet as pq
+    from delta_amd.checkpoint import write_checkpoint
+    from delta_amd.delta_log import DeltaLog, ManualClock
+    from delta_amd.testing import synth as S
+    spec = S.ChurnSpec(ckpt_files=3000, ckpt_version=4, n_deltas=3, removes_per_delta=400,
+                       adds_per_delta=400, readd_frac=0.5, ncols=2)
+    exp = S.build_table(str(tmp_path), spec, seed=13, row_group_size=1000)
+    lp = os.path.join(str(tmp_path), "_delta_log")
+    DeltaLog.clear_cache()
+    log = DeltaLog.for_table(str(tmp_path), clock=ManualClock(exp.min_file_retention_timestamp + 604800000))
+    snap = log.snapshot
+    cutoff = snap.min_file_retention_timestamp
+    before = O.state_reconstruction(O.get_log_segment(lp), cutoff)
+    meta = write_checkpoint(snap, parts=parts, row_group_size=1500)
+    with open(os.path.join(lp, "_last_checkpoint")) as f:
+        assert json.load(f) == meta
+    assert meta["version"] == snap.version and meta["size"] == (2 + snap.num_of_files + snap.num_of_removes
+                                                                + snap.num_of_set_transactions)
+    names = sorted(n for n in os.listdir(lp) if n.startswith("%020d.checkpoint" % snap.version))
+    assert len(names) == parts
+    schema = pq.read_schema(os.path.join(lp, names[0]))
+    assert schema.names == ["txn", "add", "remove", "metaData", "protocol"]
+    assert [f.name for f in schema.field("add").type] == ["path", "partitionValues", "size", "modificationTime",
+                                                         "dataChange", "tags", "stats"]
+    seg = O.get_log_segment(lp)
+    assert seg.checkpoint_version == snap.version and not seg.deltas
+    after = O.state_reconstruction(seg, cutoff)
+    st = _gpu_replay(engine, lp, cutoff)
+    try:
+        _assert_same(st, before)
+        _assert_same(st, after)
+    finally:
+        st.release()
+    DeltaLog.clear_cache()

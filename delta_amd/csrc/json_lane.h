@@ -71,24 +71,53 @@ struct Win {
   uint32_t q, bs, st, sp, ctrl;  // 16-bit masks
 };
 
+// Byte classes by two 16-entry nibble tables (class = HI[x >> 4] & LO[x & 15], zero for x >= 0x80),
+// looked up four bytes at a time with v_perm_b32: bit 0 '"', bit 1 '\\', bit 2 one of {}[], bit 3
+// ':', bit 4 ',', bit 5 ' ', bit 6 a control byte < 0x20.
+JL_HD uint32_t perm_b32(uint32_t s0, uint32_t s1, uint32_t sel) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_perm(s0, s1, sel);
+#else
+  uint32_t r = 0;
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t b = (sel >> (8 * k)) & 0xFFu;
+    const uint32_t v = b < 4 ? (s1 >> (8 * b)) & 0xFFu : b < 8 ? (s0 >> (8 * (b - 4))) & 0xFFu : b == 0x0C ? 0u : 0xFFu;
+    r |= v << (8 * k);
+  }
+  return r;
+#endif
+}
+constexpr uint32_t CLS_LO0 = 0x40414060u, CLS_LO1 = 0x40404040u, CLS_LO2 = 0x44484040u, CLS_LO3 = 0x40404452u;
+constexpr uint32_t CLS_HI0 = 0x08314040u, CLS_HI1 = 0x04000600u;
+JL_HD uint32_t class_bytes(uint32_t x) {
+  const uint32_t lo = x & 0x0F0F0F0Fu;
+  const uint32_t sel = lo & 0x07070707u;
+  const uint32_t a = perm_b32(CLS_LO1, CLS_LO0, sel), b = perm_b32(CLS_LO3, CLS_LO2, sel);
+  const uint32_t m8 = perm_b32(0u, 0u, ((lo >> 3) & 0x01010101u) | 0x0C0C0C0Cu);  // 0xFF where lo >= 8
+  const uint32_t tlo = (m8 & b) | (~m8 & a);
+  const uint32_t thi = perm_b32(CLS_HI1, CLS_HI0, (x >> 4) & 0x07070707u);
+  const uint32_t neg = perm_b32(0u, 0u, ((x >> 7) & 0x01010101u) | 0x0C0C0C0Cu);  // 0xFF where x >= 0x80
+  return tlo & thi & ~neg;
+}
+JL_HD uint32_t gather_bit(uint32_t r, int c) {  // bit c of each byte -> 4-bit mask
+  uint32_t m = (r >> c) & 0x01010101u;
+  m |= m >> 7;
+  m |= m >> 14;
+  return m & 0xFu;
+}
+
 JL_HD void classify(const uint32_t w[4], Win& m) {
   m.q = m.bs = m.st = m.sp = m.ctrl = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
 #endif
   for (int d = 0; d < 4; ++d) {
-    const uint32_t x = w[d], xo = x | 0x20202020u;
-    const uint32_t q = zbytes(x ^ 0x22222222u);
-    const uint32_t bs = zbytes(x ^ 0x5C5C5C5Cu);
-    const uint32_t st = zbytes(xo ^ 0x7B7B7B7Bu) | zbytes(xo ^ 0x7D7D7D7Du) | zbytes(x ^ 0x3A3A3A3Au) |
-                        zbytes(x ^ 0x2C2C2C2Cu);
-    const uint32_t sp = zbytes(x ^ 0x20202020u);
-    const uint32_t ct = lt20(x);
-    m.q |= gather4(q) << (4 * d);
-    m.bs |= gather4(bs) << (4 * d);
-    m.st |= gather4(st) << (4 * d);
-    m.sp |= gather4(sp) << (4 * d);
-    m.ctrl |= gather4(ct) << (4 * d);
+    const uint32_t r = class_bytes(w[d]);
+    m.q |= gather_bit(r, 0) << (4 * d);
+    m.bs |= gather_bit(r, 1) << (4 * d);
+    m.st |= gather_bit(r | (r >> 1) | (r >> 2), 2) << (4 * d);
+    m.sp |= gather_bit(r, 5) << (4 * d);
+    m.ctrl |= gather_bit(r, 6) << (4 * d);
   }
 }
 

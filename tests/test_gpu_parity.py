@@ -102,6 +102,12 @@ def test_synthetic_configs(engine, tmp_path, config, scale):
         assert c["num_file_actions"] == exp.num_file_actions
         snap = O.state_reconstruction(O.get_log_segment(lp), exp.min_file_retention_timestamp)
         _assert_same(st, snap)
+        # the device xxh64 (dev_common.h) against the published algorithm (python-xxhash): the
+        # order-free key sums over the oracle's records (synthetic paths are their own keys)
+        import xxhash
+        for key, files in (("live_key_sum", snap.all_files), ("tomb_key_sum", snap.tombstones)):
+            want = sum(xxhash.xxh64(f["path"].encode()).intdigest() >> 32 for f in files) % (1 << 64)
+            assert c[key] == want, key
     finally:
         st.release()
 

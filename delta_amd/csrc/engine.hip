@@ -253,6 +253,7 @@ struct dr_state {
   // checkpoint rows). src_id (empty: every action is from sources[0]) names each action's source.
   std::vector<std::shared_ptr<StagedData>> sources;
   DBuf<uint16_t> src_id;
+  bool sharded = false;  // a rank's part of a sharded replay (source-side survivors, owner-side counters)
   uint64_t n_actions = 0;
   // resident action arrays
   DBuf<uint8_t> kind, flags;
@@ -1041,6 +1042,7 @@ static dr_state* apply_tail(dr_ctx* ctx, dr_state& base, const std::shared_ptr<S
   hipStream_t stream = ctx->stream;
   if (!tail->parts.empty()) fail(DR_E_INVALID_ARG, "an applied tail holds commit (JSON) files only");
   if (base.sources.empty()) fail(DR_E_INVALID_ARG, "base state has no staged segment");
+  if (base.sharded) fail(DR_E_UNSUPPORTED, "a sharded replay's part cannot take a tail on its own: shard the tail too");
   if (base.sources.size() >= 65535) fail(DR_E_UNSUPPORTED, "too many applied tails on one state; rebuild it");
   std::vector<int64_t> vers;
   for (const JsonFileRec& j : tail->jfiles) vers.push_back(j.version);
@@ -1792,6 +1794,7 @@ static dr_state* shard_finish(dr_shard& sh, const uint8_t* verdict_back) {
   st.counts.tomb_key_sum = sh.owner.tomb_key_sum;
   st.counts.num_file_actions = sh.owner.num_file_actions;
   st.counts.num_actions = int64_t(st.n_actions);
+  st.sharded = true;
   reduce_nonfile(st, sh.nf, false);
   ctx->mark("end");
   return sh.st.release();

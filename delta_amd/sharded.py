@@ -120,16 +120,44 @@ class Exchange:
         self.dist.all_to_all_single(o, t, group=self.group)
         return [int(x) for x in o.cpu().tolist()]
 
+    def all_to_all_count_pairs(self, a: Sequence[int], b: Sequence[int], device) -> Tuple[List[int], List[int]]:
+        """Two per-destination count vectors in one all-to-all (row d = (a[d], b[d]) goes to rank d)."""
+        import torch
+        t = torch.tensor([[int(x), int(y)] for x, y in zip(a, b)], dtype=torch.int64,
+                         device="cpu" if self.host else device)
+        o = torch.empty_like(t)
+        self.dist.all_to_all_single(o, t, group=self.group)
+        rows = o.cpu().tolist()
+        return [r[0] for r in rows], [r[1] for r in rows]
+
     def all_reduce_sum(self, vals: Sequence[int], device) -> List[int]:
         import torch
         t = torch.tensor([_to_i64(v) for v in vals], dtype=torch.int64, device="cpu" if self.host else device)
         self.dist.all_reduce(t, group=self.group)
         return [int(x) for x in t.cpu().tolist()]
 
+    TEXT_CAP = 16384
+
     def all_gather_text(self, s: str) -> List[str]:
-        out: List[Optional[str]] = [None] * self.world
-        self.dist.all_gather_object(out, s, group=self.group)
-        return [x or "" for x in out]
+        """Every rank's text, by one all-gather of a fixed-size byte slot (length header + text);
+        all ranks fall back to all_gather_object together when any text exceeds the slot."""
+        import torch
+        raw = s.encode("utf-8")
+        cap = self.TEXT_CAP
+        dev = torch.device("cpu") if self.host else torch.device("cuda", torch.cuda.current_device())
+        slot = torch.zeros(cap + 8, dtype=torch.uint8)
+        slot[:8] = torch.tensor(list(len(raw).to_bytes(8, "little")), dtype=torch.uint8)
+        if len(raw) <= cap:
+            slot[8:8 + len(raw)] = torch.frombuffer(bytearray(raw), dtype=torch.uint8) if raw else slot[8:8]
+        out = torch.empty(self.world * (cap + 8), dtype=torch.uint8, device=dev)
+        self.dist.all_gather_into_tensor(out, slot.to(dev), group=self.group)
+        host = out.cpu().numpy().tobytes()
+        lens = [int.from_bytes(host[r * (cap + 8):r * (cap + 8) + 8], "little") for r in range(self.world)]
+        if max(lens) > cap:
+            res: List[Optional[str]] = [None] * self.world
+            self.dist.all_gather_object(res, s, group=self.group)
+            return [x or "" for x in res]
+        return [host[r * (cap + 8) + 8:r * (cap + 8) + 8 + lens[r]].decode("utf-8") for r in range(self.world)]
 
     def barrier(self) -> None:
         self.dist.barrier(group=self.group)
@@ -211,8 +239,11 @@ def replay_sharded(staged: Staged, min_file_retention_timestamp: int, exchange, 
         if dev.type == "cuda":
             torch.cuda.current_stream(dev).synchronize()
         sh.pack(send_rec.data_ptr(), send_path.data_ptr())
-        rc = exchange.all_to_all_counts(sc, dev)
-        rb = exchange.all_to_all_counts(sb, dev)
+        if hasattr(exchange, "all_to_all_count_pairs"):
+            rc, rb = exchange.all_to_all_count_pairs(sc, sb, dev)
+        else:
+            rc = exchange.all_to_all_counts(sc, dev)
+            rb = exchange.all_to_all_counts(sb, dev)
         recv_rec = torch.empty(max(sum(rc), 1) * rb_, dtype=torch.uint8, device=dev)
         recv_path = torch.empty(max(sum(rb), 1), dtype=torch.uint8, device=dev)
         exchange.all_to_all(recv_rec[:sum(rc) * rb_], send_rec[:sum(sc) * rb_], [c * rb_ for c in rc],

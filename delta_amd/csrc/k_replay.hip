@@ -159,6 +159,17 @@ constexpr int PART_STEPS = 16;                          // 4 actions per thread 
 constexpr int PART_TILE = PART_T * 4 * PART_STEPS;      // 32768 actions per tile
 constexpr int PART_MAX_BITS = 13;                       // LDS: 2 x 8192 x 4 B in the scatter
 
+// Tile of this workgroup. Workgroups are dealt to the 8 XCDs round-robin (blockIdx % 8); consecutive
+// tiles go to the same XCD so that a bucket's adjacent per-tile segments are written through one L2.
+__device__ __forceinline__ uint32_t part_tile(uint32_t nt) {
+#ifdef PART_XCD_MAP
+  const uint32_t bid = blockIdx.x, x = bid & 7, r = bid >> 3, q = nt >> 3, rem = nt & 7;
+  return x < rem ? x * (q + 1) + r : rem * (q + 1) + (x - rem) * q + r;
+#else
+  return blockIdx.x;
+#endif
+}
+
 // Every thread owns 4 consecutive actions per step: one dword of kind bytes, one of flag bytes and
 // two 16-byte key loads.
 __global__ void __launch_bounds__(PART_T) k_bucket_hist(PartitionArgs a) {
@@ -166,7 +177,8 @@ __global__ void __launch_bounds__(PART_T) k_bucket_hist(PartitionArgs a) {
   const uint32_t nb = 1u << a.bucket_bits;
   for (uint32_t b = threadIdx.x; b < nb; b += PART_T) hist[b] = 0;
   __syncthreads();
-  const uint64_t base = uint64_t(blockIdx.x) * PART_TILE;
+  const uint32_t tile = part_tile(a.ntiles);
+  const uint64_t base = uint64_t(tile) * PART_TILE;
   for (int k = 0; k < PART_STEPS; ++k) {
     const uint64_t i0 = base + (uint64_t(k) * PART_T + threadIdx.x) * 4;
     if (i0 >= a.n) break;
@@ -187,7 +199,7 @@ __global__ void __launch_bounds__(PART_T) k_bucket_hist(PartitionArgs a) {
     }
   }
   __syncthreads();
-  for (uint32_t b = threadIdx.x; b < nb; b += PART_T) a.tile_count[uint64_t(b) * a.ntiles + blockIdx.x] = hist[b];
+  for (uint32_t b = threadIdx.x; b < nb; b += PART_T) a.tile_count[uint64_t(b) * a.ntiles + tile] = hist[b];
 }
 
 __device__ __forceinline__ void scatter_one(const PartitionArgs& a, uint64_t i, uint8_t kind, uint64_t key,
@@ -217,12 +229,13 @@ __global__ void __launch_bounds__(PART_T) k_bucket_scatter(PartitionArgs a) {
   __shared__ uint32_t base[1 << PART_MAX_BITS];
   __shared__ uint32_t cnt[1 << PART_MAX_BITS];
   const uint32_t nb = 1u << a.bucket_bits;
+  const uint32_t tile = part_tile(a.ntiles);
   for (uint32_t b = threadIdx.x; b < nb; b += PART_T) {
-    base[b] = uint32_t(a.tile_off[uint64_t(b) * a.ntiles + blockIdx.x]);
+    base[b] = uint32_t(a.tile_off[uint64_t(b) * a.ntiles + tile]);
     cnt[b] = 0;
   }
   __syncthreads();
-  const uint64_t tb = uint64_t(blockIdx.x) * PART_TILE;
+  const uint64_t tb = uint64_t(tile) * PART_TILE;
   for (int k = 0; k < PART_STEPS; ++k) {
     const uint64_t i0 = tb + (uint64_t(k) * PART_T + threadIdx.x) * 4;
     if (i0 >= a.n) break;
@@ -438,56 +451,73 @@ __device__ __forceinline__ uint4 window16(uint4 lo, uint4 hi, uint32_t off) {
                     __builtin_amdgcn_alignbyte(a3, a2, sb), __builtin_amdgcn_alignbyte(a4, a3, sb));
 }
 
-// Byte equality of p[0..n) and q[0..n) with aligned 16-byte loads (one new load per string per 16
-// bytes) and no early exit. Never loads a 16-byte block that holds none of the string's bytes.
-__device__ bool bytes_equal16(const uint8_t* p, const uint8_t* q, uint32_t n) {
-  const uint4* pa = reinterpret_cast<const uint4*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(15));
-  const uint4* qa = reinterpret_cast<const uint4*>(reinterpret_cast<uintptr_t>(q) & ~uintptr_t(15));
-  const uint32_t po = uint32_t(reinterpret_cast<uintptr_t>(p) & 15), qo = uint32_t(reinterpret_cast<uintptr_t>(q) & 15);
-  const uint32_t pblocks = (po + n + 15) >> 4, qblocks = (qo + n + 15) >> 4;
-  uint4 plo = n ? pa[0] : make_uint4(0, 0, 0, 0), qlo = n ? qa[0] : make_uint4(0, 0, 0, 0);
-  uint32_t diff = 0;
-  for (uint32_t i = 0, k = 1; i < n; i += 16, ++k) {
-    const uint4 phi = k < pblocks ? pa[k] : make_uint4(0, 0, 0, 0);
-    const uint4 qhi = k < qblocks ? qa[k] : make_uint4(0, 0, 0, 0);
-    const uint4 x = window16(plo, phi, po), y = window16(qlo, qhi, qo);
-    const uint32_t rem = n - i;
-    uint4 d = make_uint4(x.x ^ y.x, x.y ^ y.y, x.z ^ y.z, x.w ^ y.w);
-    if (rem < 16) {  // bytes past the string end do not count
-      const uint32_t m0 = rem >= 4 ? 0xffffffffu : (1u << (8 * rem)) - 1u;
-      const uint32_t m1 = rem >= 8 ? 0xffffffffu : rem <= 4 ? 0u : (1u << (8 * (rem - 4))) - 1u;
-      const uint32_t m2 = rem >= 12 ? 0xffffffffu : rem <= 8 ? 0u : (1u << (8 * (rem - 8))) - 1u;
-      const uint32_t m3 = rem <= 12 ? 0u : (1u << (8 * (rem - 12))) - 1u;
-      d.x &= m0; d.y &= m1; d.z &= m2; d.w &= m3;
-    }
-    diff |= d.x | d.y | d.z | d.w;
-    plo = phi;
-    qlo = qhi;
-  }
-  return diff == 0;
-}
-
 // Every (loser, winner) pair of a bucket must name the same path (URI-equality key); a mismatch is
 // a collision of the (bucket, rkey) hash bits and sends the bucket to the 64-bit-key reducer (as
-// does a path too long for a packed reference). One wave per bucket: the pairs' loads are
-// independent, so a wave keeps many strings in flight.
+// does a path too long for a packed reference). Eight lanes compare one pair: lane j takes the
+// aligned 16-byte blocks j and j+1 of both strings (64 strings of 8 x 16 B per wave instruction,
+// so every cache line a path touches is requested once, together), compares the 16 path bytes
+// starting at 16 j, and the group ORs its differences. Unequal bytes get the URI-key comparison
+// (file:/// vs file:/ spellings) on the group's first lane.
 constexpr uint64_t PREF_PTR = (1ull << 48) - 1;
-__global__ void __launch_bounds__(64) k_bucket_verify(ReduceArgs a) {
+constexpr int VER_T = 256;
+constexpr int VER_G = 8;  // lanes per pair
+__global__ void __launch_bounds__(VER_T) k_bucket_verify(ReduceArgs a) {
   const uint32_t b = blockIdx.x;
   const uint32_t n = a.pair_count[b];
   if (!n) return;
   const ulonglong2* pr = a.out_pair + a.bucket_off[b];
+  const uint32_t j = threadIdx.x & (VER_G - 1);
   bool bad = false;
-  for (uint32_t k = threadIdx.x; k < n; k += 64) {
-    const ulonglong2 v = pr[k];
-    if (!v.x || !v.y) { bad = true; continue; }
-    const uint8_t* p = reinterpret_cast<const uint8_t*>(v.x & PREF_PTR);
-    const uint8_t* q = reinterpret_cast<const uint8_t*>(v.y & PREF_PTR);
-    const uint32_t pn = uint32_t(v.x >> 48), qn = uint32_t(v.y >> 48);
-    // equal bytes => equal URI keys; otherwise only file:/// vs file:/ spellings can still match
-    if (!(pn == qn && bytes_equal16(p, q, pn)) && !key_equal(p, pn, q, qn)) bad = true;
+  for (uint32_t k0 = 0; k0 < n; k0 += VER_T / VER_G) {
+    const uint32_t k = k0 + threadIdx.x / VER_G;
+    uint32_t diff = 0;
+    bool nul = false;
+    const uint8_t *p = nullptr, *q = nullptr;
+    uint32_t pn = 0, qn = 0;
+    if (k < n) {
+      const ulonglong2 v = pr[k];
+      nul = !v.x || !v.y;
+      p = reinterpret_cast<const uint8_t*>(v.x & PREF_PTR);
+      q = reinterpret_cast<const uint8_t*>(v.y & PREF_PTR);
+      pn = uint32_t(v.x >> 48);
+      qn = uint32_t(v.y >> 48);
+      if (nul || pn != qn) {
+        diff = 1;
+      } else {
+        const uint4* pa = reinterpret_cast<const uint4*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(15));
+        const uint4* qa = reinterpret_cast<const uint4*>(reinterpret_cast<uintptr_t>(q) & ~uintptr_t(15));
+        const uint32_t po = uint32_t(reinterpret_cast<uintptr_t>(p) & 15);
+        const uint32_t qo = uint32_t(reinterpret_cast<uintptr_t>(q) & 15);
+        const uint32_t pblocks = (po + pn + 15) >> 4, qblocks = (qo + pn + 15) >> 4;
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        for (uint32_t i0 = 0; i0 < pn; i0 += 16 * VER_G) {
+          const uint32_t jj = (i0 >> 4) + j, i = jj * 16;
+          if (i >= pn) break;
+          // never load a block that holds none of the string's bytes
+          const uint4 plo = pa[jj], qlo = qa[jj];
+          const uint4 phi = jj + 1 < pblocks ? pa[jj + 1] : z, qhi = jj + 1 < qblocks ? qa[jj + 1] : z;
+          const uint4 x = window16(plo, phi, po), y = window16(qlo, qhi, qo);
+          const uint32_t rem = pn - i;
+          uint4 d = make_uint4(x.x ^ y.x, x.y ^ y.y, x.z ^ y.z, x.w ^ y.w);
+          if (rem < 16) {  // bytes past the string end do not count
+            const uint32_t m0 = rem >= 4 ? 0xffffffffu : (1u << (8 * rem)) - 1u;
+            const uint32_t m1 = rem >= 8 ? 0xffffffffu : rem <= 4 ? 0u : (1u << (8 * (rem - 4))) - 1u;
+            const uint32_t m2 = rem >= 12 ? 0xffffffffu : rem <= 8 ? 0u : (1u << (8 * (rem - 8))) - 1u;
+            const uint32_t m3 = rem <= 12 ? 0u : (1u << (8 * (rem - 12))) - 1u;
+            d.x &= m0; d.y &= m1; d.z &= m2; d.w &= m3;
+          }
+          diff |= d.x | d.y | d.z | d.w;
+        }
+      }
+    }
+    // OR over the pair's eight lanes
+    for (int o = 1; o < VER_G; o <<= 1) diff |= __shfl_xor(diff, o, 64);
+    if (k < n && j == 0 && diff) {
+      // equal bytes => equal URI keys; otherwise only file:/// vs file:/ spellings can still match
+      if (nul || !key_equal(p, pn, q, qn)) bad = true;
+    }
   }
-  if (__ballot(bad) && threadIdx.x == 0) a.redo_list[atomicAdd(&a.totals[3], 1ull)] = b;
+  if (__syncthreads_or(bad) && threadIdx.x == 0) a.redo_list[atomicAdd(&a.totals[3], 1ull)] = b;
 }
 
 // Fallback for buckets whose (bucket, rkey) bits collided or whose LDS table overflowed: the same
@@ -661,7 +691,7 @@ void launch_bucket_reduce(const ReduceArgs& a, hipStream_t st) {
 }
 
 void launch_bucket_verify(const ReduceArgs& a, hipStream_t st) {
-  if (a.nbuckets) hipLaunchKernelGGL(dev::k_bucket_verify, dim3(a.nbuckets), dim3(64), 0, st, a);
+  if (a.nbuckets) hipLaunchKernelGGL(dev::k_bucket_verify, dim3(a.nbuckets), dim3(dev::VER_T), 0, st, a);
 }
 
 void launch_bucket_reduce64(const ReduceArgs& a, const uint32_t* buckets, uint32_t nb, hipStream_t st) {

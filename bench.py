@@ -39,6 +39,9 @@ STAGE_KERNEL = {
     "reduce": "k_bucket_reduce",
 }
 
+SORT_REDUCE_STAGES = ("partition_setup", "partition_hist", "partition_scan", "partition_scatter", "reduce",
+                      "reduce_verify", "reduce64", "compact")
+
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
@@ -248,6 +251,15 @@ def main():
                 # committed PMC passes are of the default single-GPU command
                 "traffic": pmc_traffic(args.pmc_dir, STAGE_KERNEL[dom]) if world == 1 else None,
                 "algo_bytes": db, "avg_launch_ms": round(stage_ms[dom], 4)}
+    # K3 + K4 together against SURVEY.md §8(d)'s headline budget: 32 B/action (sort) + 37 B/action
+    # (reduce, retention, compaction) = 69 B/action, over every stage between parse and export.
+    sr = [k for k in SORT_REDUCE_STAGES if k in stage_ms]
+    sr_ms = sum(stage_ms[k] for k in sr)
+    sr_bytes = 69 * local_counts["num_actions"]
+    sr_gbs = sr_bytes / (sr_ms * 1e-3) / 1e9 if sr_ms else None
+    sort_reduce = {"stages": sr, "ms": round(sr_ms, 4), "algo_bytes": sr_bytes,
+                   "achieved": round(sr_gbs, 1) if sr_gbs else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                   "frac": round(sr_gbs / HBM_PEAK_GBS, 4) if sr_gbs else None, "target_frac": 0.5}
     cpu = None
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(args.config, args.cpu_sample_scale, S.BASE_SEED + args.config, args.workdir)
@@ -264,6 +276,7 @@ def main():
                    "parallelism": ("path-hash shards over %d GPUs (RCCL all-to-all)" % world) if world > 1
                    else "single GPU"},
         "roofline": roofline,
+        "sort_reduce": sort_reduce,
         "cpu_baseline": cpu,
         "kernels": kernels,
         "result": {k: counts[k] for k in ("num_files", "num_removes", "size_in_bytes")},

@@ -203,7 +203,7 @@ __global__ void __launch_bounds__(PART_T) k_bucket_hist(PartitionArgs a) {
 }
 
 __device__ __forceinline__ void scatter_one(const PartitionArgs& a, uint64_t i, uint8_t kind, uint64_t key,
-                                            uint64_t ptr, uint32_t len, const uint32_t* base, uint32_t* cnt) {
+                                            const uint32_t* base, uint32_t* cnt) {
   const uint32_t b = bucket_of(key, a.bucket_bits);
   const uint32_t pos = base[b] + atomicAdd(&cnt[b], 1u);
   uint32_t cls = C_ADD;
@@ -222,7 +222,6 @@ __device__ __forceinline__ void scatter_one(const PartitionArgs& a, uint64_t i, 
   r.z = uint32_t(uint64_t(size));
   r.w = uint32_t(uint64_t(size) >> 32);
   *reinterpret_cast<uint4*>(a.rec + pos) = r;
-  a.rec_pref[pos] = len < 0xffffu ? (ptr | (uint64_t(len) << 48)) : 0ull;
 }
 
 __global__ void __launch_bounds__(PART_T) k_bucket_scatter(PartitionArgs a) {
@@ -246,21 +245,15 @@ __global__ void __launch_bounds__(PART_T) k_bucket_scatter(PartitionArgs a) {
       const uint4 k23 = *reinterpret_cast<const uint4*>(a.key + i0 + 2);
       const uint64_t ks[4] = {uint64_t(k01.x) | uint64_t(k01.y) << 32, uint64_t(k01.z) | uint64_t(k01.w) << 32,
                               uint64_t(k23.x) | uint64_t(k23.y) << 32, uint64_t(k23.z) | uint64_t(k23.w) << 32};
-      const uint4 p01 = *reinterpret_cast<const uint4*>(a.path_ptr + i0);
-      const uint4 p23 = *reinterpret_cast<const uint4*>(a.path_ptr + i0 + 2);
-      const uint64_t ps[4] = {uint64_t(p01.x) | uint64_t(p01.y) << 32, uint64_t(p01.z) | uint64_t(p01.w) << 32,
-                              uint64_t(p23.x) | uint64_t(p23.y) << 32, uint64_t(p23.z) | uint64_t(p23.w) << 32};
-      const uint4 ln = *reinterpret_cast<const uint4*>(a.path_len + i0);
-      const uint32_t ls[4] = {ln.x, ln.y, ln.z, ln.w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const uint8_t kj = uint8_t(kd >> (8 * j));
-        if (is_file_action(kj, uint8_t(fl >> (8 * j)))) scatter_one(a, i0 + j, kj, ks[j], ps[j], ls[j], base, cnt);
+        if (is_file_action(kj, uint8_t(fl >> (8 * j)))) scatter_one(a, i0 + j, kj, ks[j], base, cnt);
       }
     } else {
       for (uint64_t i = i0; i < a.n; ++i)
         if (is_file_action(a.kind[i], a.flags[i]))
-          scatter_one(a, i, a.kind[i], a.key[i], a.path_ptr[i], a.path_len[i], base, cnt);
+          scatter_one(a, i, a.kind[i], a.key[i], base, cnt);
     }
   }
 }
@@ -345,6 +338,12 @@ __device__ __forceinline__ void wave_append2(bool f, ulonglong2 v, uint32_t* cnt
   if (f) out[o + uint32_t(__popcll(bl & ((1ull << lane) - 1ull)))] = v;
 }
 
+// Packed path reference of action i for k_bucket_verify: address | length << 48 (0: too long).
+__device__ __forceinline__ uint64_t path_ref(const ReduceArgs& a, uint32_t i) {
+  const uint32_t len = a.path_len[i];
+  return len < 0xffffu ? (a.path_ptr[i] | (uint64_t(len) << 48)) : 0ull;
+}
+
 // K4 main reducer: one workgroup per bucket, LDS-only. Survivors go to the bucket's region of the
 // live / tombstone lists; every loser is paired with its winner for k_bucket_verify.
 __global__ void __launch_bounds__(RED_T) k_bucket_reduce(ReduceArgs a) {
@@ -419,7 +418,7 @@ __global__ void __launch_bounds__(RED_T) k_bucket_reduce(ReduceArgs a) {
             }
           } else {
             lose = true;
-            pair = make_ulonglong2(a.rec_pref[e], a.rec_pref[beg + wpos[s]]);
+            pair = make_ulonglong2(path_ref(a, r.y >> 2), path_ref(a, w >> 2));
           }
         }
       }

@@ -207,9 +207,6 @@ struct PartitionArgs {
   uint32_t* tile_count;        // [nbuckets * ntiles] bucket-major counts
   const uint64_t* tile_off;    // [nbuckets * ntiles + 1] exclusive scan of tile_count
   PartRec* rec;                // partitioned records
-  const uint64_t* path_ptr;
-  const uint32_t* path_len;
-  uint64_t* rec_pref;          // per record: path address | length << 48 (0: length >= 0xffff)
 };
 uint32_t part_tiles(uint64_t n);
 uint32_t part_max_bucket_bits();
@@ -229,7 +226,6 @@ struct ReduceArgs {
   const uint32_t* path_len;
   uint32_t* out_live;          // per-bucket survivors, written at bucket_off[b]
   uint32_t* out_tomb;
-  const uint64_t* rec_pref;    // per record path reference (PartitionArgs::rec_pref)
   ulonglong2* out_pair;        // per-bucket (loser, winner) path references for k_bucket_verify
   uint32_t* live_count;        // [nbuckets]
   uint32_t* tomb_count;        // [nbuckets]

@@ -966,7 +966,7 @@ static void reduce_actions(dr_ctx* ctx, dr_state* st, int64_t cutoff, uint32_t f
   // ---- K4: per-bucket last-writer-wins ----
   DBuf<uint32_t> olive(ctx, N), otomb(ctx, N), lcount(ctx, nb), tcount(ctx, nb), pcount(ctx, nb), rlist(ctx, nb),
       xlist(ctx, nb);
-  DBuf<ulonglong2> opair(ctx, N);
+  DBuf<uint2> opair(ctx, N);
   DBuf<unsigned long long> totals(ctx, 8), bstats(ctx, uint64_t(nb) * 5);
   totals.zero(stream);
   ReduceArgs ra{rec.p, boff.p, nb, bits, st->key.p, st->path_ptr.p, st->path_len.p, olive.p, otomb.p, opair.p,
@@ -976,40 +976,40 @@ static void reduce_actions(dr_ctx* ctx, dr_state* st, int64_t cutoff, uint32_t f
     HIP_OK(hipMemcpyAsync(d.p, v.data(), v.size() * 4, hipMemcpyHostToDevice, stream));
     return d;
   };
-  std::vector<uint32_t> redo, exact;
   if (flags & (DR_FLAG_EXACT_REDUCE | DR_FLAG_REDUCE64)) {  // test hooks: force the fallback reducers
-    for (uint32_t b = 0; b < nb; ++b) ((flags & DR_FLAG_EXACT_REDUCE) ? exact : redo).push_back(b);
+    std::vector<uint32_t> all(nb);
+    for (uint32_t b = 0; b < nb; ++b) all[b] = b;
+    DBuf<uint32_t> d = upload_list(all);
+    if (flags & DR_FLAG_EXACT_REDUCE) {
+      launch_bucket_exact(ra, d.p, nb, stream);
+    } else {
+      launch_bucket_reduce64(ra, d.p, nb, stream);
+      launch_bucket_exact(ra, xlist.p, nb, stream, totals.p + 4);
+    }
   } else {
     launch_bucket_reduce(ra, stream);
     ctx->mark("reduce");
     launch_bucket_verify(ra, stream);
     ctx->mark("reduce_verify");
-    redo = d2h(rlist.p, size_t(d2h_one(totals.p + 3, stream)), stream);
-  }
-  if (!redo.empty()) {
-    DBuf<uint32_t> d = upload_list(redo);
-    launch_bucket_reduce64(ra, d.p, uint32_t(redo.size()), stream);
+    // the fallbacks read their bucket lists' lengths on the device (no host round trip)
+    launch_bucket_reduce64(ra, rlist.p, nb, stream, totals.p + 3);
+    launch_bucket_exact(ra, xlist.p, nb, stream, totals.p + 4);
     ctx->mark("reduce64");
-    exact = d2h(xlist.p, size_t(d2h_one(totals.p + 4, stream)), stream);
-  }
-  if (!exact.empty()) {
-    DBuf<uint32_t> d = upload_list(exact);
-    launch_bucket_exact(ra, d.p, uint32_t(exact.size()), stream);
-    ctx->mark("reduce_exact");
   }
   launch_sum_stats(ra, stream);
-  std::vector<unsigned long long> tot = d2h(totals.p, 8, stream);
-  // ---- compaction ----
+  // ---- compaction (survivor lists sized to the bound; the counts come back once, at the end) ----
   DBuf<uint64_t> loff(ctx, nb + 1), tmoff(ctx, nb + 1);
   launch_scan_u32(lcount.p, loff.p, nb, scratch.p, stream);
   launch_scan_u32(tcount.p, tmoff.p, nb, scratch.p, stream);
-  st->n_live = tot[0];
-  st->n_tomb = tot[2];
-  st->live = DBuf<uint32_t>(ctx, st->n_live);
-  st->tomb = DBuf<uint32_t>(ctx, st->n_tomb);
+  st->live = DBuf<uint32_t>(ctx, N);
+  st->tomb = DBuf<uint32_t>(ctx, N);
   launch_compact(CompactArgs{olive.p, boff.p, lcount.p, loff.p, nb, st->live.p}, stream);
   launch_compact(CompactArgs{otomb.p, boff.p, tcount.p, tmoff.p, nb, st->tomb.p}, stream);
-  const uint64_t n_file_actions = d2h_one(boff.p + nb, stream);
+  HIP_OK(hipMemcpyAsync(totals.p + 7, boff.p + nb, 8, hipMemcpyDeviceToDevice, stream));
+  const std::vector<unsigned long long> tot = d2h(totals.p, 8, stream);
+  const uint64_t n_file_actions = tot[7];
+  st->n_live = tot[0];
+  st->n_tomb = tot[2];
   ctx->mark("compact");
   st->counts.num_files = int64_t(tot[0]);
   st->counts.size_in_bytes = int64_t(tot[1]);

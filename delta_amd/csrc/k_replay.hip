@@ -328,7 +328,7 @@ __device__ __forceinline__ void wave_append(bool f, uint32_t v, uint32_t* cnt, u
   o = __shfl(o, __ffsll(bl) - 1, 64);
   if (f) out[o + uint32_t(__popcll(bl & ((1ull << lane) - 1ull)))] = v;
 }
-__device__ __forceinline__ void wave_append2(bool f, ulonglong2 v, uint32_t* cnt, ulonglong2* out) {
+__device__ __forceinline__ void wave_append2(bool f, uint2 v, uint32_t* cnt, uint2* out) {
   const unsigned long long bl = __ballot(f);
   if (!bl) return;
   const int lane = threadIdx.x & 63;
@@ -345,7 +345,7 @@ __device__ __forceinline__ uint64_t path_ref(const ReduceArgs& a, uint32_t i) {
 }
 
 // K4 main reducer: one workgroup per bucket, LDS-only. Survivors go to the bucket's region of the
-// live / tombstone lists; every loser is paired with its winner for k_bucket_verify.
+// live / tombstone lists; every loser is paired (by action index) with its winner for k_bucket_verify.
 __global__ void __launch_bounds__(RED_T) k_bucket_reduce(ReduceArgs a) {
   __shared__ uint32_t tkey[TS_MAX];
   __shared__ uint32_t tval[TS_MAX];
@@ -395,7 +395,7 @@ __global__ void __launch_bounds__(RED_T) k_bucket_reduce(ReduceArgs a) {
       const uint64_t e = e0 + threadIdx.x;
       bool isl = false, ist = false, lose = false;
       uint32_t idx = 0;
-      ulonglong2 pair = make_ulonglong2(0, 0);
+      uint2 pair = make_uint2(0, 0);
       if (e < end) {
         const uint4 r = load_rec(a.rec, e);
         if (!sbits || (r.x >> (32 - sbits)) == sp) {
@@ -418,7 +418,7 @@ __global__ void __launch_bounds__(RED_T) k_bucket_reduce(ReduceArgs a) {
             }
           } else {
             lose = true;
-            pair = make_ulonglong2(path_ref(a, r.y >> 2), path_ref(a, w >> 2));
+            pair = make_uint2(r.y >> 2, w >> 2);
           }
         }
       }
@@ -464,7 +464,7 @@ __global__ void __launch_bounds__(VER_T) k_bucket_verify(ReduceArgs a) {
   const uint32_t b = blockIdx.x;
   const uint32_t n = a.pair_count[b];
   if (!n) return;
-  const ulonglong2* pr = a.out_pair + a.bucket_off[b];
+  const uint2* pr = a.out_pair + a.bucket_off[b];
   const uint32_t j = threadIdx.x & (VER_G - 1);
   bool bad = false;
   for (uint32_t k0 = 0; k0 < n; k0 += VER_T / VER_G) {
@@ -474,7 +474,8 @@ __global__ void __launch_bounds__(VER_T) k_bucket_verify(ReduceArgs a) {
     const uint8_t *p = nullptr, *q = nullptr;
     uint32_t pn = 0, qn = 0;
     if (k < n) {
-      const ulonglong2 v = pr[k];
+      const uint2 ix = pr[k];
+      const ulonglong2 v = make_ulonglong2(path_ref(a, ix.x), path_ref(a, ix.y));
       nul = !v.x || !v.y;
       p = reinterpret_cast<const uint8_t*>(v.x & PREF_PTR);
       q = reinterpret_cast<const uint8_t*>(v.y & PREF_PTR);
@@ -523,10 +524,12 @@ __global__ void __launch_bounds__(VER_T) k_bucket_verify(ReduceArgs a) {
 // last-writer-wins keyed by the full 64-bit path hash, byte-verified inline. A 64-bit collision (or
 // overflow) hands the bucket on to the exact O(m^2) kernel.
 constexpr int TS64 = 4096;
-__global__ void __launch_bounds__(RED_T) k_bucket_reduce64(ReduceArgs a, const uint32_t* buckets) {
+__global__ void __launch_bounds__(RED_T) k_bucket_reduce64(ReduceArgs a, const uint32_t* buckets,
+                                                       const unsigned long long* count) {
   __shared__ unsigned long long tkey[TS64];
   __shared__ uint32_t tval[TS64];
   __shared__ uint32_t nl, nt, collide, overflow;
+  if (count && blockIdx.x >= *count) return;  // device-side list length (grid sized to the bound)
   const uint32_t b = buckets[blockIdx.x];
   const uint64_t beg = a.bucket_off[b], end = a.bucket_off[b + 1];
   const uint64_t m = end - beg;
@@ -599,8 +602,10 @@ __global__ void __launch_bounds__(RED_T) k_bucket_reduce64(ReduceArgs a, const u
 
 // Exact fallback: each record is a winner iff no other record with an equal path has a larger
 // action index. O(m^2) per bucket; only reached on a 64-bit path-hash collision.
-__global__ void __launch_bounds__(RED_T) k_bucket_exact(ReduceArgs a, const uint32_t* buckets) {
+__global__ void __launch_bounds__(RED_T) k_bucket_exact(ReduceArgs a, const uint32_t* buckets,
+                                                       const unsigned long long* count) {
   __shared__ uint32_t nl, nt;
+  if (count && blockIdx.x >= *count) return;  // device-side list length (grid sized to the bound)
   const uint32_t b = buckets[blockIdx.x];
   const uint64_t beg = a.bucket_off[b], end = a.bucket_off[b + 1];
   if (threadIdx.x == 0) { nl = 0; nt = 0; }
@@ -693,12 +698,14 @@ void launch_bucket_verify(const ReduceArgs& a, hipStream_t st) {
   if (a.nbuckets) hipLaunchKernelGGL(dev::k_bucket_verify, dim3(a.nbuckets), dim3(dev::VER_T), 0, st, a);
 }
 
-void launch_bucket_reduce64(const ReduceArgs& a, const uint32_t* buckets, uint32_t nb, hipStream_t st) {
-  if (nb) hipLaunchKernelGGL(dev::k_bucket_reduce64, dim3(nb), dim3(dev::RED_T), 0, st, a, buckets);
+void launch_bucket_reduce64(const ReduceArgs& a, const uint32_t* buckets, uint32_t nb, hipStream_t st,
+                            const unsigned long long* count) {
+  if (nb) hipLaunchKernelGGL(dev::k_bucket_reduce64, dim3(nb), dim3(dev::RED_T), 0, st, a, buckets, count);
 }
 
-void launch_bucket_exact(const ReduceArgs& a, const uint32_t* buckets, uint32_t nb, hipStream_t st) {
-  if (nb) hipLaunchKernelGGL(dev::k_bucket_exact, dim3(nb), dim3(dev::RED_T), 0, st, a, buckets);
+void launch_bucket_exact(const ReduceArgs& a, const uint32_t* buckets, uint32_t nb, hipStream_t st,
+                         const unsigned long long* count) {
+  if (nb) hipLaunchKernelGGL(dev::k_bucket_exact, dim3(nb), dim3(dev::RED_T), 0, st, a, buckets, count);
 }
 
 void launch_sum_stats(const ReduceArgs& a, hipStream_t st) {

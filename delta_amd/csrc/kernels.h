@@ -226,7 +226,7 @@ struct ReduceArgs {
   const uint32_t* path_len;
   uint32_t* out_live;          // per-bucket survivors, written at bucket_off[b]
   uint32_t* out_tomb;
-  ulonglong2* out_pair;        // per-bucket (loser, winner) path references for k_bucket_verify
+  uint2* out_pair;             // per-bucket (loser, winner) action indices for k_bucket_verify
   uint32_t* live_count;        // [nbuckets]
   uint32_t* tomb_count;        // [nbuckets]
   uint32_t* pair_count;        // [nbuckets]
@@ -241,9 +241,12 @@ void launch_bucket_reduce(const ReduceArgs& a, hipStream_t st);
 // byte-verifies every (loser, winner) pair; mismatching buckets -> redo_list
 void launch_bucket_verify(const ReduceArgs& a, hipStream_t st);
 // redo_list buckets, keyed by the full 64-bit hash; 64-bit collisions -> exact_list
-void launch_bucket_reduce64(const ReduceArgs& a, const uint32_t* buckets, uint32_t nb, hipStream_t st);
+// `count` (device, nullable): the list's length when only its bound nb is known on the host
+void launch_bucket_reduce64(const ReduceArgs& a, const uint32_t* buckets, uint32_t nb, hipStream_t st,
+                            const unsigned long long* count = nullptr);
 // exact O(m^2) reducer
-void launch_bucket_exact(const ReduceArgs& a, const uint32_t* buckets, uint32_t nb, hipStream_t st);
+void launch_bucket_exact(const ReduceArgs& a, const uint32_t* buckets, uint32_t nb, hipStream_t st,
+                         const unsigned long long* count = nullptr);
 // sums the per-bucket statistics into totals[0,1,2,5,6]
 void launch_sum_stats(const ReduceArgs& a, hipStream_t st);
 

@@ -6,7 +6,7 @@
 //
 //  A k_snap_spec    one lane per 256-byte chunk of compressed input parses elements
 //                   *speculatively* (starting 64 bytes early as a warm-up) and records the
-//                   positions it visited in the chunk (256-bit bitmap) and where it left it.
+//                   positions it visited in the chunk (256-bit bitmap, kept in LDS) and where it left it.
 //  B k_snap_assume / k_snap_entries: every chunk's true entry, in parallel: a chunk whose true
 //                   entry (the previous chunk's exit) is on its speculative chain is correct
 //                   (chains that meet coincide from then on); an isolated mis-speculated chunk is
@@ -148,6 +148,7 @@ __device__ __forceinline__ WgInfo wg_info(const SnappyArgs& a) {
 // A: speculative parse.
 __global__ void __launch_bounds__(WG_CHUNKS) k_snap_spec(SnappyArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[STAGE_BYTES + 32];
+  __shared__ uint32_t lvis[(SNAP_CH / 32) * WG_CHUNKS];
   const WgInfo g = wg_info(a);
   const SnapPage& pg = a.pages[g.p];
   const Staged s = stage_input(buf, reinterpret_cast<const uint8_t*>(pg.in), pg.n_in, g.j0, g.cnt);
@@ -156,9 +157,10 @@ __global__ void __launch_bounds__(WG_CHUNKS) k_snap_spec(SnappyArgs a) {
   const uint32_t c = a.chunk_base[g.p] + j;
   const uint64_t cs = uint64_t(j) * SNAP_CH;
   const uint64_t ce = min(cs + SNAP_CH, uint64_t(pg.n_in));
-  uint32_t vis[SNAP_CH / 32];
+  // visited bitmap in LDS, word-major so the lanes' ORs of one word index hit distinct banks
+  uint32_t* lv = lvis + threadIdx.x;
 #pragma unroll
-  for (int k = 0; k < int(SNAP_CH / 32); ++k) vis[k] = 0;
+  for (int k = 0; k < int(SNAP_CH / 32); ++k) lv[k * WG_CHUNKS] = 0;
   uint64_t pos = cs >= SNAP_WU ? cs - SNAP_WU : 0;
   uint64_t first = ~0ull, out = 0, mid = ~0ull;
   uint32_t elems = 0, hout = 0, helems = 0;
@@ -168,9 +170,7 @@ __global__ void __launch_bounds__(WG_CHUNKS) k_snap_spec(SnappyArgs a) {
     snap_step(staged_u64(buf, s, pos), &adv, &len);
     if (pos >= cs) {
       const uint32_t r = uint32_t(pos - cs);
-#pragma unroll
-      for (int k = 0; k < int(SNAP_CH / 32); ++k)
-        if (int(r >> 5) == k) vis[k] |= 1u << (r & 31);
+      lv[(r >> 5) * WG_CHUNKS] |= 1u << (r & 31);
       if (first == ~0ull) first = pos;
       out += len;
       ++elems;
@@ -186,7 +186,7 @@ __global__ void __launch_bounds__(WG_CHUNKS) k_snap_spec(SnappyArgs a) {
   a.half_elems[c] = helems;
   a.spec_exit[c] = pos > 0xffffffffull ? 0xffffffffu : uint32_t(pos);
 #pragma unroll
-  for (int k = 0; k < int(SNAP_CH / 32); ++k) a.vis[uint64_t(c) * (SNAP_CH / 32) + k] = vis[k];
+  for (int k = 0; k < int(SNAP_CH / 32); ++k) a.vis[uint64_t(c) * (SNAP_CH / 32) + k] = lv[k * WG_CHUNKS];
   // the chunk's output bytes / elements if its true entry is its first visited position (nearly
   // always): k_snap_count then only re-walks the exceptions
   a.spec_first[c] = first > 0xffffffffull ? 0xffffffffu : uint32_t(first);

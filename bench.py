@@ -32,7 +32,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # of these (achieved = its algorithmic bytes / its hipEvent-timed duration on the replay stream).
 STAGE_KERNEL = {
     "json_parse": "k_json_lines",
-    "json_newlines": "k_json_newlines",
+    "json_newlines": "k_json_place",
     "ckpt_assemble": "k_ckpt_assemble",
     "partition_hist": "k_bucket_hist",
     "partition_scatter": "k_bucket_scatter",
@@ -71,8 +71,8 @@ def algorithmic_bytes(stage, plan, counts):
     fa = counts["num_file_actions"]
     surv = counts["num_files"] + counts["num_removes"]
     return {
-        "json_index": plan["json_bytes"],
-        "json_newlines": plan["json_bytes"] + 8 * n_lines,
+        "json_index": plan["json_bytes"] + 2 * n_lines,
+        "json_newlines": 10 * n_lines,
         "json_parse": plan["json_bytes"] + 8 * n_lines + 50 * n_lines,
         "pq_inflate": plan["pages_compressed_bytes"] + plan["pages_decompressed_bytes"],
         "pq_bounds": plan["pages_decompressed_bytes"],

@@ -802,9 +802,10 @@ static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
   DBuf<uint32_t> jcounts(ctx, nbj + 1);
   DBuf<uint64_t> joff(ctx, nbj + 1);
   DBuf<uint8_t> scratch(ctx, scan_scratch_for(nbj));
+  DBuf<uint16_t> jslots(ctx, json_slot_entries(json_len));
   uint64_t nlines = 0;
   if (nbj) {
-    launch_json_count(s.d_json.p, json_len, jcounts.p, stream);
+    launch_json_index(s.d_json.p, json_len, jcounts.p, jslots.p, stream);
     launch_scan_u32(jcounts.p, joff.p, nbj, scratch.p, stream);
     nlines = d2h_one(joff.p + nbj, stream);
   }
@@ -828,7 +829,7 @@ static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
                    st->src_off.p, st->src_len.p};
   ctx->mark("json_index");
   if (nlines) {
-    launch_json_newlines(s.d_json.p, json_len, joff.p, nl.p, stream);
+    launch_json_place(s.d_json.p, json_len, jcounts.p, joff.p, jslots.p, nl.p, stream);
     ctx->mark("json_newlines");
     DBuf<uint64_t> hard(ctx, nlines);
     JsonParseArgs ja{s.d_json.p, nl.p, nlines, R, act.kind, act.flags, act.key, act.path_ptr, act.path_len,

@@ -1,8 +1,8 @@
 // K1: newline-delimited JSON commit files -> action records (replaces Spark's JsonFileFormat +
 // Jackson over Action.logSchema, D/DeltaLogFileIndex.scala:67, D/Snapshot.scala:244-263).
 //
-// Stage 1 (k_json_count / k_json_newlines): a structural index of the newline bytes, built from
-// 16-byte vector loads; a raw '\n' can never sit inside a JSON string, so every newline is a line
+// Stage 1 (k_json_index / k_json_place): a structural index of the newline bytes, built from
+// 16-byte vector loads in one pass; a raw '\n' can never sit inside a JSON string, so every newline is a line
 // boundary. Stage 2 (k_json_lines): one lane per line walks the line in 16-byte SWAR windows
 // (json_lane.h: bit-parallel quote/escape masks, token DFA), classifies the SingleAction envelope
 // with unwrap priority (D/actions/actions.scala:523-541), pulls add/remove path / size /
@@ -25,37 +25,21 @@ __device__ __forceinline__ uint32_t count_nl_word(uint32_t w) {
   return __builtin_popcount(t);
 }
 
-__global__ void __launch_bounds__(JSON_THREADS) k_json_count(const uint8_t* __restrict__ buf, uint64_t len,
-                                                            uint32_t* __restrict__ block_counts) {
-  __shared__ uint32_t red[JSON_THREADS / 64];
-  const uint64_t base = uint64_t(blockIdx.x) * JSON_BYTES_PER_BLOCK + uint64_t(threadIdx.x) * JSON_BYTES_PER_THREAD;
-  uint32_t c = 0;
-  if (base + JSON_BYTES_PER_THREAD <= len) {
-    const uint4* p = reinterpret_cast<const uint4*>(buf + base);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      uint4 v = p[i];
-      c += count_nl_word(v.x) + count_nl_word(v.y) + count_nl_word(v.z) + count_nl_word(v.w);
-    }
-  } else {
-    for (uint64_t i = base; i < len; ++i) c += buf[i] == '\n';
-  }
-  for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t s = 0;
-    for (int i = 0; i < JSON_THREADS / 64; ++i) s += red[i];
-    block_counts[blockIdx.x] = s;
-  }
-}
+// Stage 1 reads the JSON once: every 16 KiB block finds its newlines (64 bytes per thread, a
+// block-wide scan of the per-thread counts ranks them) and stores their block-relative positions
+// as u16 in the block's slot of JSON_SLOT entries, plus its count. After the scan of the counts,
+// k_json_place expands the slots into the global newline array (12 B per line of traffic instead
+// of a second pass over the bytes); a block with more than JSON_SLOT newlines (lines averaging
+// under 32 bytes) is re-scanned there.
+constexpr int JSON_SLOT = 512;
 
-// Writes the byte position of every newline, in order: nl[block_off[b] + rank] = pos.
-__global__ void __launch_bounds__(JSON_THREADS) k_json_newlines(const uint8_t* __restrict__ buf, uint64_t len,
-                                                               const uint64_t* __restrict__ block_off,
-                                                               uint64_t* __restrict__ nl) {
+// Block-wide ranks of this thread's newlines; calls put(rank, block-relative position) for each.
+template <typename Put>
+__device__ __forceinline__ uint32_t block_newlines(const uint8_t* __restrict__ buf, uint64_t len, uint64_t blk,
+                                                   Put put) {
   __shared__ uint32_t wsum[JSON_THREADS / 64];
-  const uint64_t base = uint64_t(blockIdx.x) * JSON_BYTES_PER_BLOCK + uint64_t(threadIdx.x) * JSON_BYTES_PER_THREAD;
+  const uint32_t rel0 = threadIdx.x * JSON_BYTES_PER_THREAD;
+  const uint64_t base = blk * JSON_BYTES_PER_BLOCK + rel0;
   uint32_t words[16];
   uint32_t c = 0;
   const bool full = base + JSON_BYTES_PER_THREAD <= len;
@@ -80,23 +64,53 @@ __global__ void __launch_bounds__(JSON_THREADS) k_json_newlines(const uint8_t* _
   }
   if (lane == 63) wsum[wv] = incl;
   __syncthreads();
-  uint32_t woff = 0;
-  for (int i = 0; i < wv; ++i) woff += wsum[i];
-  uint64_t out = block_off[blockIdx.x] + woff + incl - c;
+  uint32_t woff = 0, total = 0;
+  for (int i = 0; i < JSON_THREADS / 64; ++i) {
+    woff += i < wv ? wsum[i] : 0u;
+    total += wsum[i];
+  }
+  uint32_t r = woff + incl - c;
   if (full) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       uint32_t x = words[i] ^ 0x0a0a0a0au;
       uint32_t t = (x - 0x01010101u) & ~x & 0x80808080u;
       while (t) {
-        int b = __builtin_ctz(t) >> 3;
-        nl[out++] = base + 4 * i + b;
+        put(r++, rel0 + 4 * i + (__builtin_ctz(t) >> 3));
         t &= t - 1;
       }
     }
   } else {
     for (uint64_t i = base; i < len; ++i)
-      if (buf[i] == '\n') nl[out++] = i;
+      if (buf[i] == '\n') put(r++, uint32_t(i - blk * JSON_BYTES_PER_BLOCK));
+  }
+  return total;
+}
+
+__global__ void __launch_bounds__(JSON_THREADS) k_json_index(const uint8_t* __restrict__ buf, uint64_t len,
+                                                            uint32_t* __restrict__ block_counts,
+                                                            uint16_t* __restrict__ slots) {
+  uint16_t* slot = slots + uint64_t(blockIdx.x) * JSON_SLOT;
+  const uint32_t total = block_newlines(buf, len, blockIdx.x, [&](uint32_t r, uint32_t pos) {
+    if (r < uint32_t(JSON_SLOT)) slot[r] = uint16_t(pos);
+  });
+  if (threadIdx.x == 0) block_counts[blockIdx.x] = total;
+}
+
+// Writes the byte position of every newline, in order: nl[block_off[b] + rank] = pos.
+__global__ void __launch_bounds__(JSON_THREADS) k_json_place(const uint8_t* __restrict__ buf, uint64_t len,
+                                                            const uint32_t* __restrict__ block_counts,
+                                                            const uint64_t* __restrict__ block_off,
+                                                            const uint16_t* __restrict__ slots,
+                                                            uint64_t* __restrict__ nl) {
+  const uint32_t cnt = block_counts[blockIdx.x];
+  const uint64_t base = uint64_t(blockIdx.x) * JSON_BYTES_PER_BLOCK;
+  uint64_t* out = nl + block_off[blockIdx.x];
+  if (cnt <= uint32_t(JSON_SLOT)) {
+    const uint16_t* slot = slots + uint64_t(blockIdx.x) * JSON_SLOT;
+    for (uint32_t k = threadIdx.x; k < cnt; k += JSON_THREADS) out[k] = base + slot[k];
+  } else {
+    block_newlines(buf, len, blockIdx.x, [&](uint32_t r, uint32_t pos) { out[r] = base + pos; });
   }
 }
 
@@ -228,14 +242,19 @@ __global__ void __launch_bounds__(64) k_json_hard(JsonParseArgs a) {
 // ---- launchers -----------------------------------------------------------------------------------
 uint64_t json_num_blocks(uint64_t len) { return (len + dev::JSON_BYTES_PER_BLOCK - 1) / dev::JSON_BYTES_PER_BLOCK; }
 
-void launch_json_count(const uint8_t* buf, uint64_t len, uint32_t* block_counts, hipStream_t st) {
+uint64_t json_slot_entries(uint64_t len) { return json_num_blocks(len) * dev::JSON_SLOT; }
+
+void launch_json_index(const uint8_t* buf, uint64_t len, uint32_t* block_counts, uint16_t* slots, hipStream_t st) {
   uint64_t nb = json_num_blocks(len);
-  if (nb) hipLaunchKernelGGL(dev::k_json_count, dim3(unsigned(nb)), dim3(dev::JSON_THREADS), 0, st, buf, len, block_counts);
+  if (nb) hipLaunchKernelGGL(dev::k_json_index, dim3(unsigned(nb)), dim3(dev::JSON_THREADS), 0, st, buf, len,
+                             block_counts, slots);
 }
 
-void launch_json_newlines(const uint8_t* buf, uint64_t len, const uint64_t* block_off, uint64_t* nl, hipStream_t st) {
+void launch_json_place(const uint8_t* buf, uint64_t len, const uint32_t* block_counts, const uint64_t* block_off,
+                       const uint16_t* slots, uint64_t* nl, hipStream_t st) {
   uint64_t nb = json_num_blocks(len);
-  if (nb) hipLaunchKernelGGL(dev::k_json_newlines, dim3(unsigned(nb)), dim3(dev::JSON_THREADS), 0, st, buf, len, block_off, nl);
+  if (nb) hipLaunchKernelGGL(dev::k_json_place, dim3(unsigned(nb)), dim3(dev::JSON_THREADS), 0, st, buf, len,
+                             block_counts, block_off, slots, nl);
 }
 
 void launch_json_parse(const JsonParseArgs& a, hipStream_t st) {

@@ -44,11 +44,11 @@ struct JsonParseArgs {
 };
 
 uint64_t json_num_blocks(uint64_t len);
-void launch_json_count(const uint8_t* buf, uint64_t len, uint32_t* block_counts, hipStream_t st);
-void launch_json_newlines(const uint8_t* buf, uint64_t len, const uint64_t* block_off, uint64_t* nl,
-                          hipStream_t st);
-// fast walker over every line (LDS-staged, lane per line), then the General walker over the
-// deferred lines (device-side count)
+// newline index: per-block counts + u16 slots (json_slot_entries), then the global positions
+uint64_t json_slot_entries(uint64_t len);
+void launch_json_index(const uint8_t* buf, uint64_t len, uint32_t* block_counts, uint16_t* slots, hipStream_t st);
+void launch_json_place(const uint8_t* buf, uint64_t len, const uint32_t* block_counts, const uint64_t* block_off,
+                       const uint16_t* slots, uint64_t* nl, hipStream_t st);
 void launch_json_parse(const JsonParseArgs& a, hipStream_t st);
 void launch_json_hard(const JsonParseArgs& a, hipStream_t st);
 

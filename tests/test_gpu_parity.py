@@ -112,6 +112,31 @@ def test_synthetic_configs(engine, tmp_path, config, scale):
         st.release()
 
 
+def test_newline_dense_blocks(engine, tmp_path):
+    """The newline index keeps up to 512 positions per 16 KiB block and re-scans denser blocks:
+    commits padded with runs of blank lines and `{}` rows (null actions, dropped by unwrap,
+    D/actions/actions.scala:523-541) around real actions replay like the oracle."""
+    from delta_amd.testing import synth as S
+    exp = S.build_config(1, str(tmp_path), scale=0.2)
+    lp = os.path.join(str(tmp_path), "_delta_log")
+    for v in (1, 2, 5):
+        fn = os.path.join(lp, S.delta_name(v))
+        with open(fn) as f:
+            lines = f.read().splitlines()
+        out = []
+        for i, ln in enumerate(lines):
+            out.append(ln)
+            out.extend(["", "{}", " ", "{}"] * (3000 if i == 1 else 5))
+        with open(fn, "w") as f:
+            f.write("\n".join(out) + "\n")
+    st = _gpu_replay(engine, lp, exp.min_file_retention_timestamp)
+    try:
+        assert st.counts["num_files"] == exp.num_files
+        _assert_same(st, O.state_reconstruction(O.get_log_segment(lp), exp.min_file_retention_timestamp))
+    finally:
+        st.release()
+
+
 @pytest.mark.parametrize("reducer", ["reduce64", "exact"])
 def test_fallback_reducers_agree(engine, tmp_path, reducer):
     """The collision fallbacks (k_bucket_reduce64 / k_bucket_exact, forced for every bucket) and the

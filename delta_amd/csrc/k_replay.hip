@@ -452,20 +452,43 @@ __device__ __forceinline__ uint4 window16(uint4 lo, uint4 hi, uint32_t off) {
 
 // Every (loser, winner) pair of a bucket must name the same path (URI-equality key); a mismatch is
 // a collision of the (bucket, rkey) hash bits and sends the bucket to the 64-bit-key reducer (as
-// does a path too long for a packed reference). Eight lanes compare one pair: lane j takes the
-// aligned 16-byte blocks j and j+1 of both strings (64 strings of 8 x 16 B per wave instruction,
-// so every cache line a path touches is requested once, together), compares the 16 path bytes
-// starting at 16 j, and the group ORs its differences. Unequal bytes get the URI-key comparison
-// (file:/// vs file:/ spellings) on the group's first lane.
+// does a path too long for a packed reference). Eight lanes compare one pair: lane j loads aligned
+// 16-byte block j of both strings (a wave instruction requests eight whole paths of each side at
+// once, every block once) and takes block j + 1 from its neighbour by a shuffle; lanes 0..6 each
+// compare 16 path bytes, and the group ORs its differences. Unequal bytes get the URI-key
+// comparison (file:/// vs file:/ spellings) on the group's first lane.
 constexpr uint64_t PREF_PTR = (1ull << 48) - 1;
+// Differences (masked to the string) in path bytes [i, i + 16) of p and q, rem = n - i; plo/phi and
+// qlo/qhi are the aligned 16-byte blocks holding them (po, qo: the strings' offsets in their blocks).
+__device__ __forceinline__ uint32_t block_diff(uint4 plo, uint4 phi, uint32_t po, uint4 qlo, uint4 qhi, uint32_t qo,
+                                               uint32_t rem) {
+  const uint4 x = window16(plo, phi, po), y = window16(qlo, qhi, qo);
+  uint4 d = make_uint4(x.x ^ y.x, x.y ^ y.y, x.z ^ y.z, x.w ^ y.w);
+  if (rem < 16) {  // bytes past the string end do not count
+    const uint32_t m0 = rem >= 4 ? 0xffffffffu : (1u << (8 * rem)) - 1u;
+    const uint32_t m1 = rem >= 8 ? 0xffffffffu : rem <= 4 ? 0u : (1u << (8 * (rem - 4))) - 1u;
+    const uint32_t m2 = rem >= 12 ? 0xffffffffu : rem <= 8 ? 0u : (1u << (8 * (rem - 8))) - 1u;
+    const uint32_t m3 = rem <= 12 ? 0u : (1u << (8 * (rem - 12))) - 1u;
+    d.x &= m0; d.y &= m1; d.z &= m2; d.w &= m3;
+  }
+  return d.x | d.y | d.z | d.w;
+}
+
 constexpr int VER_T = 256;
 constexpr int VER_G = 8;  // lanes per pair
+
+__device__ __forceinline__ uint4 shfl_down4(uint4 v, int width) {
+  return make_uint4(__shfl_down(v.x, 1, width), __shfl_down(v.y, 1, width), __shfl_down(v.z, 1, width),
+                    __shfl_down(v.w, 1, width));
+}
+
 __global__ void __launch_bounds__(VER_T) k_bucket_verify(ReduceArgs a) {
   const uint32_t b = blockIdx.x;
   const uint32_t n = a.pair_count[b];
   if (!n) return;
   const uint2* pr = a.out_pair + a.bucket_off[b];
   const uint32_t j = threadIdx.x & (VER_G - 1);
+  const uint4 z = make_uint4(0, 0, 0, 0);
   bool bad = false;
   for (uint32_t k0 = 0; k0 < n; k0 += VER_T / VER_G) {
     const uint32_t k = k0 + threadIdx.x / VER_G;
@@ -489,24 +512,14 @@ __global__ void __launch_bounds__(VER_T) k_bucket_verify(ReduceArgs a) {
         const uint32_t po = uint32_t(reinterpret_cast<uintptr_t>(p) & 15);
         const uint32_t qo = uint32_t(reinterpret_cast<uintptr_t>(q) & 15);
         const uint32_t pblocks = (po + pn + 15) >> 4, qblocks = (qo + pn + 15) >> 4;
-        const uint4 z = make_uint4(0, 0, 0, 0);
-        for (uint32_t i0 = 0; i0 < pn; i0 += 16 * VER_G) {
-          const uint32_t jj = (i0 >> 4) + j, i = jj * 16;
-          if (i >= pn) break;
-          // never load a block that holds none of the string's bytes
-          const uint4 plo = pa[jj], qlo = qa[jj];
-          const uint4 phi = jj + 1 < pblocks ? pa[jj + 1] : z, qhi = jj + 1 < qblocks ? qa[jj + 1] : z;
-          const uint4 x = window16(plo, phi, po), y = window16(qlo, qhi, qo);
-          const uint32_t rem = pn - i;
-          uint4 d = make_uint4(x.x ^ y.x, x.y ^ y.y, x.z ^ y.z, x.w ^ y.w);
-          if (rem < 16) {  // bytes past the string end do not count
-            const uint32_t m0 = rem >= 4 ? 0xffffffffu : (1u << (8 * rem)) - 1u;
-            const uint32_t m1 = rem >= 8 ? 0xffffffffu : rem <= 4 ? 0u : (1u << (8 * (rem - 4))) - 1u;
-            const uint32_t m2 = rem >= 12 ? 0xffffffffu : rem <= 8 ? 0u : (1u << (8 * (rem - 8))) - 1u;
-            const uint32_t m3 = rem <= 12 ? 0u : (1u << (8 * (rem - 12))) - 1u;
-            d.x &= m0; d.y &= m1; d.z &= m2; d.w &= m3;
-          }
-          diff |= d.x | d.y | d.z | d.w;
+        // step: lane j loads aligned block B + j of each string (never one that holds none of its
+        // bytes) and takes block B + j + 1 from lane j + 1; lanes 0..6 compare path bytes
+        // [16 (B + j), +16)
+        for (uint32_t B = 0; 16 * B < pn; B += VER_G - 1) {
+          const uint4 plo = B + j < pblocks ? pa[B + j] : z, qlo = B + j < qblocks ? qa[B + j] : z;
+          const uint4 phi = shfl_down4(plo, VER_G), qhi = shfl_down4(qlo, VER_G);
+          const uint32_t i = 16 * (B + j);
+          if (j < VER_G - 1 && i < pn) diff |= block_diff(plo, phi, po, qlo, qhi, qo, pn - i);
         }
       }
     }

@@ -78,7 +78,7 @@ def algorithmic_bytes(stage, plan, counts):
         "pq_bounds": plan["pages_decompressed_bytes"],
         "pq_decode": plan["pages_decompressed_bytes"] + 44 * rows,
         "ckpt_assemble": 44 * rows + 88 * rows + 50 * rows,
-        "partition_hist": 10 * (rows + n_lines),
+        "partition_hist": 30 * (rows + n_lines),
         "partition_scatter": 22 * (rows + n_lines) + 32 * fa,
         "reduce": 16 * fa + 4 * surv,
         "compact": 8 * surv,

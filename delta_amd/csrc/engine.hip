@@ -952,8 +952,9 @@ static void reduce_actions(dr_ctx* ctx, dr_state* st, int64_t cutoff, uint32_t f
   DBuf<uint32_t> tcnt(ctx, ncell);
   DBuf<uint64_t> toff(ctx, ncell + 1), boff(ctx, nb + 1);
   DBuf<uint8_t> pscratch(ctx, scan_scratch_for(ncell));
+  DBuf<uint64_t> pref(ctx, N);
   PartitionArgs pa{st->kind.p, st->flags.p, st->key.p, st->size.p, st->delts.p, N, cutoff, bits, nt,
-                   tcnt.p, toff.p, nullptr};
+                   tcnt.p, toff.p, nullptr, st->path_ptr.p, st->path_len.p, pref.p};
   DBuf<PartRec> rec(ctx, N);
   pa.rec = rec.p;
   ctx->mark("partition_setup");
@@ -970,7 +971,7 @@ static void reduce_actions(dr_ctx* ctx, dr_state* st, int64_t cutoff, uint32_t f
   DBuf<uint2> opair(ctx, N);
   DBuf<unsigned long long> totals(ctx, 8), bstats(ctx, uint64_t(nb) * 5);
   totals.zero(stream);
-  ReduceArgs ra{rec.p, boff.p, nb, bits, st->key.p, st->path_ptr.p, st->path_len.p, olive.p, otomb.p, opair.p,
+  ReduceArgs ra{rec.p, boff.p, nb, bits, st->key.p, st->path_ptr.p, st->path_len.p, olive.p, otomb.p, opair.p, pref.p,
                 lcount.p, tcount.p, pcount.p, totals.p, rlist.p, xlist.p, bstats.p};
   auto upload_list = [&](const std::vector<uint32_t>& v) {
     DBuf<uint32_t> d(ctx, v.size());

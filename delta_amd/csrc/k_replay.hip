@@ -154,6 +154,11 @@ __device__ __forceinline__ uint64_t top32_of(uint32_t b, uint32_t rkey, int bits
   return bits ? (uint64_t(b) << (32 - bits)) | (rkey >> bits) : uint64_t(rkey);
 }
 
+// Packed path reference: address | length << 48 (0: a length that does not fit 16 bits).
+__device__ __forceinline__ uint64_t pack_ref(uint64_t ptr, uint32_t len) {
+  return len < 0xffffu ? (ptr | (uint64_t(len) << 48)) : 0ull;
+}
+
 constexpr int PART_T = 512;
 constexpr int PART_STEPS = 16;                          // 4 actions per thread per step
 constexpr int PART_TILE = PART_T * 4 * PART_STEPS;      // 32768 actions per tile
@@ -193,9 +198,21 @@ __global__ void __launch_bounds__(PART_T) k_bucket_hist(PartitionArgs a) {
       for (int j = 0; j < 4; ++j)
         if (is_file_action(uint8_t(kd >> (8 * j)), uint8_t(fl >> (8 * j))))
           atomicAdd(&hist[bucket_of(ks[j], a.bucket_bits)], 1u);
+      // packed path references for k_bucket_verify's gathers (one 8-byte load per path there)
+      const uint4 p01 = *reinterpret_cast<const uint4*>(a.path_ptr + i0);
+      const uint4 p23 = *reinterpret_cast<const uint4*>(a.path_ptr + i0 + 2);
+      const uint4 ln = *reinterpret_cast<const uint4*>(a.path_len + i0);
+      const ulonglong2 r01 = make_ulonglong2(pack_ref(uint64_t(p01.x) | uint64_t(p01.y) << 32, ln.x),
+                                             pack_ref(uint64_t(p01.z) | uint64_t(p01.w) << 32, ln.y));
+      const ulonglong2 r23 = make_ulonglong2(pack_ref(uint64_t(p23.x) | uint64_t(p23.y) << 32, ln.z),
+                                             pack_ref(uint64_t(p23.z) | uint64_t(p23.w) << 32, ln.w));
+      *reinterpret_cast<ulonglong2*>(a.path_ref + i0) = r01;
+      *reinterpret_cast<ulonglong2*>(a.path_ref + i0 + 2) = r23;
     } else {
-      for (uint64_t i = i0; i < a.n; ++i)
+      for (uint64_t i = i0; i < a.n; ++i) {
         if (is_file_action(a.kind[i], a.flags[i])) atomicAdd(&hist[bucket_of(a.key[i], a.bucket_bits)], 1u);
+        a.path_ref[i] = pack_ref(a.path_ptr[i], a.path_len[i]);
+      }
     }
   }
   __syncthreads();
@@ -338,11 +355,8 @@ __device__ __forceinline__ void wave_append2(bool f, uint2 v, uint32_t* cnt, uin
   if (f) out[o + uint32_t(__popcll(bl & ((1ull << lane) - 1ull)))] = v;
 }
 
-// Packed path reference of action i for k_bucket_verify: address | length << 48 (0: too long).
-__device__ __forceinline__ uint64_t path_ref(const ReduceArgs& a, uint32_t i) {
-  const uint32_t len = a.path_len[i];
-  return len < 0xffffu ? (a.path_ptr[i] | (uint64_t(len) << 48)) : 0ull;
-}
+// Packed path reference of action i (written by k_bucket_hist).
+__device__ __forceinline__ uint64_t path_ref(const ReduceArgs& a, uint32_t i) { return a.path_ref[i]; }
 
 // K4 main reducer: one workgroup per bucket, LDS-only. Survivors go to the bucket's region of the
 // live / tombstone lists; every loser is paired (by action index) with its winner for k_bucket_verify.

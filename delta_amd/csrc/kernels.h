@@ -207,6 +207,9 @@ struct PartitionArgs {
   uint32_t* tile_count;        // [nbuckets * ntiles] bucket-major counts
   const uint64_t* tile_off;    // [nbuckets * ntiles + 1] exclusive scan of tile_count
   PartRec* rec;                // partitioned records
+  const uint64_t* path_ptr;
+  const uint32_t* path_len;
+  uint64_t* path_ref;          // per action: path address | length << 48 (0: length >= 0xffff)
 };
 uint32_t part_tiles(uint64_t n);
 uint32_t part_max_bucket_bits();
@@ -227,6 +230,7 @@ struct ReduceArgs {
   uint32_t* out_live;          // per-bucket survivors, written at bucket_off[b]
   uint32_t* out_tomb;
   uint2* out_pair;             // per-bucket (loser, winner) action indices for k_bucket_verify
+  const uint64_t* path_ref;    // PartitionArgs::path_ref
   uint32_t* live_count;        // [nbuckets]
   uint32_t* tomb_count;        // [nbuckets]
   uint32_t* pair_count;        // [nbuckets]

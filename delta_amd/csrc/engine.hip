@@ -821,7 +821,7 @@ static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
   st->src_off = DBuf<uint64_t>(ctx, N);
   st->src_len = DBuf<uint32_t>(ctx, N);
   DBuf<uint64_t> counters(ctx, 8);  // 0 special count, 1 special bytes, 2 nonfile count, 3 errors, 4 canon fill,
-                                     // 5 lines deferred to the General walker
+                                     // 5 lines deferred to the General walker, 7 checkpoint decode error
   counters.zero(stream);
   DBuf<uint64_t> nl(ctx, nlines);
   DBuf<uint64_t> nonfile(ctx, nlines);
@@ -885,9 +885,10 @@ static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
     launch_ckpt_assemble(ca, stream);
     ctx->mark("ckpt_assemble");
   }
+  // the checkpoint decoder's error code rides in counters[7]: one read-back for both
+  if (R) HIP_OK(hipMemcpyAsync(counters.p + 7, pq_err.p, sizeof(uint32_t), hipMemcpyDeviceToDevice, stream));
   std::vector<uint64_t> cnt = d2h(counters.p, 8, stream);
-  if (R && d2h_one(pq_err.p, stream) != 0)
-    fail(DR_E_PARQUET, fmt("device checkpoint decode failed (code %u)", d2h_one(pq_err.p, stream)));
+  if (R && cnt[7] != 0) fail(DR_E_PARQUET, fmt("device checkpoint decode failed (code %u)", unsigned(cnt[7])));
   st->counts.malformed_lines = int64_t(cnt[3]);
   // ---- canonicalisation of special paths ----
   if (cnt[0]) {

@@ -191,6 +191,31 @@ def test_checkpoint_page_layouts(engine, tmp_path, page_size, compression, page_
         st.release()
 
 
+def test_corrupt_checkpoint_page_is_an_error(engine, tmp_path):
+    """A SNAPPY page body overwritten with copy elements reaching before the page start cannot be
+    decoded: the replay fails with DR_E_PARQUET (the reference's Parquet reader throws), it does not
+    return a partial state."""
+    import pyarrow.parquet as pq
+    from delta_amd.delta_log import DeltaError
+    from delta_amd.testing import synth as S
+    S.build_table(str(tmp_path), S.config_spec(3, 0.001), seed=5, use_dictionary=False)
+    lp = os.path.join(str(tmp_path), "_delta_log")
+    cp = [f for f in os.listdir(lp) if f.endswith(".checkpoint.parquet")][0]
+    fn = os.path.join(lp, cp)
+    md = pq.ParquetFile(fn).metadata
+    col = [md.row_group(0).column(i) for i in range(md.num_columns)
+           if md.row_group(0).column(i).path_in_schema == "add.path"][0]
+    assert col.compression == "SNAPPY" and col.total_compressed_size > 4096
+    raw = bytearray(open(fn, "rb").read())
+    at = col.data_page_offset + 512  # past the page header and the snappy length preamble
+    raw[at:at + 256] = b"\xff" * 256  # copy-4 elements with offset 0xffffffff
+    with open(fn, "wb") as f:
+        f.write(bytes(raw))
+    with pytest.raises(DeltaError) as ei:
+        _gpu_replay(engine, lp, 0)
+    assert ei.value.code == "DR_E_PARQUET"
+
+
 def test_checkpoint_boundaries_found_in_parallel(engine, tmp_path, capfd, monkeypatch):
     """Every PLAIN BYTE_ARRAY page of a synthetic checkpoint is split by the parallel boundary
     kernels (k_ba_count/write/check) and validated, so none falls back to the serial walker

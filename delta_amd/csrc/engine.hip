@@ -943,7 +943,6 @@ static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
 static void reduce_actions(dr_ctx* ctx, dr_state* st, int64_t cutoff, uint32_t flags = 0) {
   hipStream_t stream = ctx->stream;
   const uint64_t N = st->n_actions;
-  DBuf<uint8_t> scratch(ctx, scan_scratch_for(0));
   // ---- K3: partition by hash bucket ----
   if (N >= (uint64_t(1) << 30)) fail(DR_E_UNSUPPORTED, "more than 2^30 actions in one replay shard");
   const int bits = bucket_bits_for(N);
@@ -1002,12 +1001,11 @@ static void reduce_actions(dr_ctx* ctx, dr_state* st, int64_t cutoff, uint32_t f
   launch_sum_stats(ra, stream);
   // ---- compaction (survivor lists sized to the bound; the counts come back once, at the end) ----
   DBuf<uint64_t> loff(ctx, nb + 1), tmoff(ctx, nb + 1);
-  launch_scan_u32(lcount.p, loff.p, nb, scratch.p, stream);
-  launch_scan_u32(tcount.p, tmoff.p, nb, scratch.p, stream);
+  launch_survivor_scan(lcount.p, tcount.p, nb, loff.p, tmoff.p, stream);
   st->live = DBuf<uint32_t>(ctx, N);
   st->tomb = DBuf<uint32_t>(ctx, N);
-  launch_compact(CompactArgs{olive.p, boff.p, lcount.p, loff.p, nb, st->live.p}, stream);
-  launch_compact(CompactArgs{otomb.p, boff.p, tcount.p, tmoff.p, nb, st->tomb.p}, stream);
+  launch_compact2(CompactArgs{olive.p, boff.p, lcount.p, loff.p, nb, st->live.p},
+                  CompactArgs{otomb.p, boff.p, tcount.p, tmoff.p, nb, st->tomb.p}, stream);
   HIP_OK(hipMemcpyAsync(totals.p + 7, boff.p + nb, 8, hipMemcpyDeviceToDevice, stream));
   const std::vector<unsigned long long> tot = d2h(totals.p, 8, stream);
   const uint64_t n_file_actions = tot[7];

@@ -488,6 +488,25 @@ __device__ __forceinline__ uint32_t block_diff(uint4 plo, uint4 phi, uint32_t po
   return d.x | d.y | d.z | d.w;
 }
 
+// Byte equality of p[0..n) and q[0..n) by one lane: aligned 16-byte loads (each block once, none
+// that holds no string byte), no early exit, so the loads of successive blocks are independent.
+__device__ bool bytes_equal16(const uint8_t* p, const uint8_t* q, uint32_t n) {
+  const uint4* pa = reinterpret_cast<const uint4*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(15));
+  const uint4* qa = reinterpret_cast<const uint4*>(reinterpret_cast<uintptr_t>(q) & ~uintptr_t(15));
+  const uint32_t po = uint32_t(reinterpret_cast<uintptr_t>(p) & 15), qo = uint32_t(reinterpret_cast<uintptr_t>(q) & 15);
+  const uint32_t pblocks = (po + n + 15) >> 4, qblocks = (qo + n + 15) >> 4;
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  uint4 plo = n ? pa[0] : z, qlo = n ? qa[0] : z;
+  uint32_t diff = 0;
+  for (uint32_t i = 0, k = 1; i < n; i += 16, ++k) {
+    const uint4 phi = k < pblocks ? pa[k] : z, qhi = k < qblocks ? qa[k] : z;
+    diff |= block_diff(plo, phi, po, qlo, qhi, qo, n - i);
+    plo = phi;
+    qlo = qhi;
+  }
+  return diff == 0;
+}
+
 constexpr int VER_T = 256;
 constexpr int VER_G = 8;  // lanes per pair
 
@@ -551,13 +570,11 @@ __global__ void __launch_bounds__(VER_T) k_bucket_verify(ReduceArgs a) {
 // last-writer-wins keyed by the full 64-bit path hash, byte-verified inline. A 64-bit collision (or
 // overflow) hands the bucket on to the exact O(m^2) kernel.
 constexpr int TS64 = 4096;
-__global__ void __launch_bounds__(RED_T) k_bucket_reduce64(ReduceArgs a, const uint32_t* buckets,
-                                                       const unsigned long long* count) {
+__device__ void reduce64_bucket(ReduceArgs& a, uint32_t b) {
   __shared__ unsigned long long tkey[TS64];
   __shared__ uint32_t tval[TS64];
   __shared__ uint32_t nl, nt, collide, overflow;
-  if (count && blockIdx.x >= *count) return;  // device-side list length (grid sized to the bound)
-  const uint32_t b = buckets[blockIdx.x];
+  __syncthreads();  // the previous bucket of this workgroup is done with the shared state
   const uint64_t beg = a.bucket_off[b], end = a.bucket_off[b + 1];
   const uint64_t m = end - beg;
   int sbits = 0;
@@ -607,9 +624,10 @@ __global__ void __launch_bounds__(RED_T) k_bucket_reduce64(ReduceArgs a, const u
             }
           } else {
             const uint32_t wi = w >> 2;
-            if (!key_equal(reinterpret_cast<const uint8_t*>(a.path_ptr[idx]), a.path_len[idx],
-                           reinterpret_cast<const uint8_t*>(a.path_ptr[wi]), a.path_len[wi]))
-              collide = 1;
+            const uint8_t* p = reinterpret_cast<const uint8_t*>(a.path_ptr[idx]);
+            const uint8_t* q = reinterpret_cast<const uint8_t*>(a.path_ptr[wi]);
+            const uint32_t pn = a.path_len[idx], qn = a.path_len[wi];
+            if (!(pn == qn && bytes_equal16(p, q, pn)) && !key_equal(p, pn, q, qn)) collide = 1;
           }
         }
       }
@@ -629,11 +647,9 @@ __global__ void __launch_bounds__(RED_T) k_bucket_reduce64(ReduceArgs a, const u
 
 // Exact fallback: each record is a winner iff no other record with an equal path has a larger
 // action index. O(m^2) per bucket; only reached on a 64-bit path-hash collision.
-__global__ void __launch_bounds__(RED_T) k_bucket_exact(ReduceArgs a, const uint32_t* buckets,
-                                                       const unsigned long long* count) {
+__device__ void exact_bucket(ReduceArgs& a, uint32_t b) {
   __shared__ uint32_t nl, nt;
-  if (count && blockIdx.x >= *count) return;  // device-side list length (grid sized to the bound)
-  const uint32_t b = buckets[blockIdx.x];
+  __syncthreads();  // the previous bucket of this workgroup is done with the shared state
   const uint64_t beg = a.bucket_off[b], end = a.bucket_off[b + 1];
   if (threadIdx.x == 0) { nl = 0; nt = 0; }
   __syncthreads();
@@ -672,12 +688,58 @@ __global__ void __launch_bounds__(RED_T) k_bucket_exact(ReduceArgs a, const uint
   store_totals(a, b, tot);
 }
 
-__global__ void k_compact(CompactArgs a) {
+// The fallbacks walk their bucket list grid-stride; the list length is read on the device when only
+// its bound n is known on the host (a few buckets out of thousands: no grid of idle workgroups).
+__global__ void __launch_bounds__(RED_T) k_bucket_reduce64(ReduceArgs a, const uint32_t* buckets, uint32_t n,
+                                                       const unsigned long long* count) {
+  const uint32_t lim = count ? uint32_t(min(*count, (unsigned long long)n)) : n;
+  for (uint32_t i = blockIdx.x; i < lim; i += gridDim.x) reduce64_bucket(a, buckets[i]);
+}
+__global__ void __launch_bounds__(RED_T) k_bucket_exact(ReduceArgs a, const uint32_t* buckets, uint32_t n,
+                                                    const unsigned long long* count) {
+  const uint32_t lim = count ? uint32_t(min(*count, (unsigned long long)n)) : n;
+  for (uint32_t i = blockIdx.x; i < lim; i += gridDim.x) exact_bucket(a, buckets[i]);
+}
+
+__device__ __forceinline__ void k_compact_one(const CompactArgs& a) {
   const uint32_t b = blockIdx.x;
   if (b >= a.nbuckets) return;
   const uint32_t c = a.counts[b];
   const uint64_t src = a.bucket_off[b], dst = a.dst_off[b];
   for (uint32_t k = threadIdx.x; k < c; k += blockDim.x) a.dst[dst + k] = a.src[src + k];
+}
+__global__ void k_compact(CompactArgs a) { k_compact_one(a); }
+
+// Both survivor lists at once (blockIdx.y: 0 live, 1 tombstones).
+__global__ void k_compact2(CompactArgs l, CompactArgs t) {
+  k_compact_one(blockIdx.y ? t : l);
+}
+
+// Exclusive scans of the per-bucket live and tombstone counts in one workgroup (nb <= 8192: each
+// thread owns a run of at most 8 buckets); off[nb] is the total.
+constexpr int SSCAN_T = 1024;
+__global__ void __launch_bounds__(SSCAN_T) k_survivor_scan(const uint32_t* lc, const uint32_t* tc, uint32_t nb,
+                                                           uint64_t* loff, uint64_t* toff) {
+  __shared__ unsigned long long ws[2][SSCAN_T / 64];
+  const uint32_t per = (nb + SSCAN_T - 1) / SSCAN_T;
+  const uint32_t b0 = min(nb, threadIdx.x * per), b1 = min(nb, b0 + per);
+  unsigned long long sl = 0, st = 0;
+  for (uint32_t b = b0; b < b1; ++b) { sl += lc[b]; st += tc[b]; }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  unsigned long long il = sl, it = st;
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long xl = __shfl_up(il, o, 64), xt = __shfl_up(it, o, 64);
+    if (lane >= o) { il += xl; it += xt; }
+  }
+  if (lane == 63) { ws[0][wv] = il; ws[1][wv] = it; }
+  __syncthreads();
+  unsigned long long ol = il - sl, ot = it - st;
+  for (int w = 0; w < wv; ++w) { ol += ws[0][w]; ot += ws[1][w]; }
+  for (uint32_t b = b0; b < b1; ++b) {
+    loff[b] = ol; toff[b] = ot;
+    ol += lc[b]; ot += tc[b];
+  }
+  if (threadIdx.x == SSCAN_T - 1) { loff[nb] = ol; toff[nb] = ot; }
 }
 
 }  // namespace dev
@@ -727,12 +789,14 @@ void launch_bucket_verify(const ReduceArgs& a, hipStream_t st) {
 
 void launch_bucket_reduce64(const ReduceArgs& a, const uint32_t* buckets, uint32_t nb, hipStream_t st,
                             const unsigned long long* count) {
-  if (nb) hipLaunchKernelGGL(dev::k_bucket_reduce64, dim3(nb), dim3(dev::RED_T), 0, st, a, buckets, count);
+  const uint32_t g = count ? std::min(nb, 256u) : nb;
+  if (nb) hipLaunchKernelGGL(dev::k_bucket_reduce64, dim3(g), dim3(dev::RED_T), 0, st, a, buckets, nb, count);
 }
 
 void launch_bucket_exact(const ReduceArgs& a, const uint32_t* buckets, uint32_t nb, hipStream_t st,
                          const unsigned long long* count) {
-  if (nb) hipLaunchKernelGGL(dev::k_bucket_exact, dim3(nb), dim3(dev::RED_T), 0, st, a, buckets, count);
+  const uint32_t g = count ? std::min(nb, 256u) : nb;
+  if (nb) hipLaunchKernelGGL(dev::k_bucket_exact, dim3(g), dim3(dev::RED_T), 0, st, a, buckets, nb, count);
 }
 
 void launch_sum_stats(const ReduceArgs& a, hipStream_t st) {
@@ -741,6 +805,16 @@ void launch_sum_stats(const ReduceArgs& a, hipStream_t st) {
 
 void launch_compact(const CompactArgs& a, hipStream_t st) {
   if (a.nbuckets) hipLaunchKernelGGL(dev::k_compact, dim3(a.nbuckets), dim3(64), 0, st, a);
+}
+
+void launch_compact2(const CompactArgs& live, const CompactArgs& tomb, hipStream_t st) {
+  if (live.nbuckets) hipLaunchKernelGGL(dev::k_compact2, dim3(live.nbuckets, 2), dim3(64), 0, st, live, tomb);
+}
+
+void launch_survivor_scan(const uint32_t* lc, const uint32_t* tc, uint32_t nb, uint64_t* loff, uint64_t* toff,
+                          hipStream_t st) {
+  if (nb > uint32_t(dev::SSCAN_T) * 8) throw std::runtime_error("survivor scan: too many buckets");
+  hipLaunchKernelGGL(dev::k_survivor_scan, dim3(1), dim3(dev::SSCAN_T), 0, st, lc, tc, nb, loff, toff);
 }
 
 }  // namespace dr

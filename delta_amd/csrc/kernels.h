@@ -264,6 +264,11 @@ struct CompactArgs {
   uint32_t* dst;
 };
 void launch_compact(const CompactArgs& a, hipStream_t st);
+// both survivor lists in one launch (nbuckets must match)
+void launch_compact2(const CompactArgs& live, const CompactArgs& tomb, hipStream_t st);
+// exclusive scans (+ totals at [nb]) of the live / tombstone counts, nb <= 8192, one workgroup
+void launch_survivor_scan(const uint32_t* lc, const uint32_t* tc, uint32_t nb, uint64_t* loff, uint64_t* toff,
+                          hipStream_t st);
 
 // ---- multi-GPU path-hash sharding (k_shard.hip) ------------------------------------------------
 struct ShardRec {        // 32 B per exchanged file action (DR_SHARD_REC_BYTES)

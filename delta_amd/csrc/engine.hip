@@ -997,6 +997,15 @@ static void reduce_actions(dr_ctx* ctx, dr_state* st, int64_t cutoff, uint32_t f
     launch_bucket_reduce64(ra, rlist.p, nb, stream, totals.p + 3);
     launch_bucket_exact(ra, xlist.p, nb, stream, totals.p + 4);
     ctx->mark("reduce64");
+    if (std::getenv("DR_REDUCE_DEBUG")) {
+      const std::vector<unsigned long long> t = d2h(totals.p, 8, stream);
+      std::vector<uint64_t> bo = d2h(boff.p, nb + 1, stream);
+      std::vector<uint32_t> rl = d2h(rlist.p, size_t(std::min<unsigned long long>(t[3], nb)), stream);
+      std::fprintf(stderr, "reduce: %u buckets, %llu to the 64-bit reducer, %llu to the exact one; sizes:", nb,
+                   t[3], t[4]);
+      for (uint32_t b : rl) std::fprintf(stderr, " %llu", (unsigned long long)(bo[b + 1] - bo[b]));
+      std::fprintf(stderr, "\n");
+    }
   }
   launch_sum_stats(ra, stream);
   // ---- compaction (survivor lists sized to the bound; the counts come back once, at the end) ----

@@ -36,6 +36,8 @@
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <iterator>
+#include <array>
 #include <unordered_map>
 #include <vector>
 
@@ -73,11 +75,14 @@ uint64_t xxh64(const uint8_t* p, size_t len) {
 [[noreturn]] void die(const std::string& m) { throw std::runtime_error(m); }
 
 std::vector<uint8_t> read_all(const std::string& p) {
-  std::ifstream f(p, std::ios::binary);
+  std::ifstream f(p, std::ios::binary | std::ios::ate);
   if (!f) die("cannot open " + p);
-  std::vector<uint8_t> b((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
-  b.resize(b.size() + 16, 0);
-  b.resize(b.size() - 16);
+  const std::streamsize n = f.tellg();
+  std::vector<uint8_t> b;
+  b.reserve(size_t(n) + 16);  // readable slack past the end for 8-byte loads
+  b.resize(size_t(n));
+  f.seekg(0);
+  if (n && !f.read(reinterpret_cast<char*>(b.data()), n)) die("cannot read " + p);
   return b;
 }
 
@@ -332,79 +337,128 @@ int bwidth(int m) { int w = 0; while ((1 << w) <= m) ++w; return m ? w : 0; }
 // Decoded flat column: def per row, values per row (string or int).
 struct Col { std::vector<uint8_t> def; std::vector<std::string> s; std::vector<int64_t> i; };
 
-void decode_chunk(const uint8_t* f, size_t flen, const Chunk& c, const Leaf& l, int64_t rows, Col& out) {
+// One page of a column chunk: header fields and where its body lies.
+struct Page { int pt = -1, enc = 0, nv = 0, v2d = 0, v2r = 0, v2c = 1; int64_t us = 0, cs = 0; const uint8_t* body = nullptr; };
+
+// Page headers of a chunk, in order (Thrift PageHeader, parquet-format PageHeader fields 1-8).
+std::vector<Page> chunk_pages(const uint8_t* f, const Chunk& c) {
   int64_t st = c.dpo;
   if (c.dicto > 0 && c.dicto < st) st = c.dicto;
   const uint8_t* p = f + st;
   const uint8_t* ce = p + c.tcomp;
-  std::vector<std::string> ds;
-  std::vector<int64_t> di;
+  std::vector<Page> pages;
   int64_t seen = 0;
-  std::vector<uint8_t> buf;
   while (p < ce && seen < c.nval) {
     TR r{p, ce};
-    int pt = -1, enc = 0, nv = 0, v2d = 0, v2r = 0, v2c = 1;
-    int64_t us = 0, cs = 0;
+    Page pg;
     int16_t last = 0; int id, ty;
     while (r.field(&last, &id, &ty)) {
-      if (id == 1) pt = int(r.zz());
-      else if (id == 2) us = r.zz();
-      else if (id == 3) cs = r.zz();
+      if (id == 1) pg.pt = int(r.zz());
+      else if (id == 2) pg.us = r.zz();
+      else if (id == 3) pg.cs = r.zz();
       else if (id == 5 || id == 7 || id == 8) {
         int16_t l2 = 0; int i2, t2;
         while (r.field(&l2, &i2, &t2)) {
-          if (i2 == 1) nv = int(r.zz());
-          else if ((id != 8 && i2 == 2) || (id == 8 && i2 == 4)) enc = int(r.zz());
-          else if (id == 8 && i2 == 5) v2d = int(r.zz());
-          else if (id == 8 && i2 == 6) v2r = int(r.zz());
-          else if (id == 8 && i2 == 7) v2c = t2 == 1;
+          if (i2 == 1) pg.nv = int(r.zz());
+          else if ((id != 8 && i2 == 2) || (id == 8 && i2 == 4)) pg.enc = int(r.zz());
+          else if (id == 8 && i2 == 5) pg.v2d = int(r.zz());
+          else if (id == 8 && i2 == 6) pg.v2r = int(r.zz());
+          else if (id == 8 && i2 == 7) pg.v2c = t2 == 1;
           else r.skip(t2);
         }
       } else r.skip(ty);
     }
-    const uint8_t* body = r.p;
-    p = body + cs;
-    if (pt != 0 && pt != 2 && pt != 3) continue;
-    int64_t lv = pt == 3 ? v2d + v2r : 0;
-    buf.assign(size_t(us) + 16, 0);
-    memcpy(buf.data(), body, size_t(lv));
-    bool comp = c.codec == 1 && !(pt == 3 && !v2c);
-    if (comp) { if (!snappy(body + lv, size_t(cs - lv), buf.data() + lv, size_t(us - lv))) die("snappy"); }
-    else if (c.codec == 0) memcpy(buf.data() + lv, body + lv, size_t(us - lv));
-    else die("codec");
-    const uint8_t* q = buf.data();
-    const uint8_t* qe = q + us;
-    auto plain = [&](int64_t n, std::vector<std::string>* S, std::vector<int64_t>* I) {
-      for (int64_t k = 0; k < n; ++k) {
-        if (l.type == 6) { uint32_t len = rd32(q); q += 4; S->emplace_back((const char*)q, len); q += len; }
-        else if (l.type == 2) { I->push_back(int64_t(rd64(q))); q += 8; }
-        else if (l.type == 1) { I->push_back(int32_t(rd32(q))); q += 4; }
-        else die("type");
-      }
-    };
-    if (pt == 2) { ds.clear(); di.clear(); plain(nv, &ds, &di); continue; }
-    std::vector<uint32_t> defs;
-    if (pt == 3) { if (l.maxdef) rle(q + v2r, q + lv, bwidth(l.maxdef), nv, defs); q += lv; }
-    else if (l.maxdef) { uint32_t n = rd32(q); q += 4; rle(q, q + n, bwidth(l.maxdef), nv, defs); q += n; }
-    int64_t nn = 0;
-    for (int k = 0; k < nv; ++k) nn += (l.maxdef ? int(defs[k]) : 0) == l.maxdef;
-    std::vector<std::string> S; std::vector<int64_t> I;
-    if (enc == 0) plain(nn, &S, &I);
-    else if (enc == 2 || enc == 8) {
-      std::vector<uint32_t> ix;
-      if (nn) { int w = *q++; rle(q, qe, w, nn, ix); }
-      for (uint32_t x : ix) { if (l.type == 6) S.push_back(ds.at(x)); else I.push_back(di.at(x)); }
-    } else die("encoding");
-    size_t vi = 0;
-    for (int k = 0; k < nv; ++k) {
-      uint8_t d = uint8_t(l.maxdef ? defs[k] : 0);
-      out.def.push_back(d);
-      if (d == l.maxdef) { if (l.type == 6) out.s.push_back(std::move(S[vi++])); else out.i.push_back(I[vi++]); }
-      else { if (l.type == 6) out.s.emplace_back(); else out.i.push_back(0); }
-    }
-    seen += nv;
+    pg.body = r.p;
+    p = pg.body + pg.cs;
+    if (pg.pt != 0 && pg.pt != 2 && pg.pt != 3) continue;
+    if (pg.pt != 2) seen += pg.nv;
+    pages.push_back(pg);
   }
-  (void)flen; (void)rows;
+  return pages;
+}
+
+// Decompressed body of a page (v2 levels are stored uncompressed ahead of the values).
+std::vector<uint8_t> page_bytes(const Chunk& c, const Page& pg) {
+  const int64_t lv = pg.pt == 3 ? pg.v2d + pg.v2r : 0;
+  std::vector<uint8_t> buf(size_t(pg.us) + 16, 0);
+  memcpy(buf.data(), pg.body, size_t(lv));
+  const bool comp = c.codec == 1 && !(pg.pt == 3 && !pg.v2c);
+  if (comp) { if (!snappy(pg.body + lv, size_t(pg.cs - lv), buf.data() + lv, size_t(pg.us - lv))) die("snappy"); }
+  else if (c.codec == 0) memcpy(buf.data() + lv, pg.body + lv, size_t(pg.us - lv));
+  else die("codec");
+  return buf;
+}
+
+// PLAIN values of a leaf (BYTE_ARRAY, INT64, INT32).
+void plain_values(const Leaf& l, const uint8_t*& q, int64_t n, std::vector<std::string>* S, std::vector<int64_t>* I) {
+  for (int64_t k = 0; k < n; ++k) {
+    if (l.type == 6) { uint32_t len = rd32(q); q += 4; S->emplace_back((const char*)q, len); q += len; }
+    else if (l.type == 2) { I->push_back(int64_t(rd64(q))); q += 8; }
+    else if (l.type == 1) { I->push_back(int32_t(rd32(q))); q += 4; }
+    else die("type");
+  }
+}
+
+// One data page -> def level and value per row.
+void decode_data_page(const Chunk& c, const Leaf& l, const Page& pg, const std::vector<std::string>& ds,
+                      const std::vector<int64_t>& di, Col& out) {
+  const std::vector<uint8_t> buf = page_bytes(c, pg);
+  const uint8_t* q = buf.data();
+  const uint8_t* qe = q + pg.us;
+  const int64_t lv = pg.pt == 3 ? pg.v2d + pg.v2r : 0;
+  std::vector<uint32_t> defs;
+  if (pg.pt == 3) { if (l.maxdef) rle(q + pg.v2r, q + lv, bwidth(l.maxdef), pg.nv, defs); q += lv; }
+  else if (l.maxdef) { uint32_t n = rd32(q); q += 4; rle(q, q + n, bwidth(l.maxdef), pg.nv, defs); q += n; }
+  int64_t nn = 0;
+  for (int k = 0; k < pg.nv; ++k) nn += (l.maxdef ? int(defs[k]) : 0) == l.maxdef;
+  std::vector<std::string> S; std::vector<int64_t> I;
+  if (pg.enc == 0) plain_values(l, q, nn, &S, &I);
+  else if (pg.enc == 2 || pg.enc == 8) {
+    std::vector<uint32_t> ix;
+    if (nn) { int w = *q++; rle(q, qe, w, nn, ix); }
+    for (uint32_t x : ix) { if (l.type == 6) S.push_back(ds.at(x)); else I.push_back(di.at(x)); }
+  } else die("encoding");
+  size_t vi = 0;
+  for (int k = 0; k < pg.nv; ++k) {
+    uint8_t d = uint8_t(l.maxdef ? defs[k] : 0);
+    out.def.push_back(d);
+    if (d == l.maxdef) { if (l.type == 6) out.s.push_back(std::move(S[vi++])); else out.i.push_back(I[vi++]); }
+    else { if (l.type == 6) out.s.emplace_back(); else out.i.push_back(0); }
+  }
+}
+
+// A column chunk's pages decoded by `threads` workers (pages are independent once the dictionary
+// page is read), concatenated in page order.
+void decode_chunk(const uint8_t* f, const Chunk& c, const Leaf& l, int threads, Col& out) {
+  const std::vector<Page> pages = chunk_pages(f, c);
+  std::vector<std::string> ds;
+  std::vector<int64_t> di;
+  std::vector<const Page*> data;
+  for (const Page& pg : pages) {
+    if (pg.pt == 2) {
+      if (!data.empty()) die("dictionary page after data pages");
+      ds.clear(); di.clear();
+      const std::vector<uint8_t> buf = page_bytes(c, pg);
+      const uint8_t* q = buf.data();
+      plain_values(l, q, pg.nv, &ds, &di);
+    } else {
+      data.push_back(&pg);
+    }
+  }
+  std::vector<Col> parts(data.size());
+  std::atomic<size_t> next{0};
+  auto work = [&] {
+    for (size_t k; (k = next++) < data.size();) decode_data_page(c, l, *data[k], ds, di, parts[k]);
+  };
+  std::vector<std::thread> ts;
+  for (int t = 1; t < threads && size_t(t) < data.size(); ++t) ts.emplace_back(work);
+  work();
+  for (auto& t : ts) t.join();
+  for (Col& pc : parts) {
+    out.def.insert(out.def.end(), pc.def.begin(), pc.def.end());
+    std::move(pc.s.begin(), pc.s.end(), std::back_inserter(out.s));
+    out.i.insert(out.i.end(), pc.i.begin(), pc.i.end());
+  }
 }
 
 void read_checkpoint(const std::vector<uint8_t>& f, std::vector<Action>& acts, int threads) {
@@ -473,38 +527,63 @@ void read_checkpoint(const std::vector<uint8_t>& f, std::vector<Action>& acts, i
   for (auto& g : rgs) { groups.push_back({&g, rbase}); rbase += g.rows; }
   size_t base_act = acts.size();
   acts.resize(base_act + size_t(rbase));
+  // decode: one task per (row group, hot column), so a table with few row groups still uses every
+  // thread; then one task per row group assembles its rows (unwrap: add > remove > the rest)
+  std::vector<std::array<Col, 4>> cols(groups.size());
+  std::vector<std::array<bool, 4>> has(groups.size(), std::array<bool, 4>{false, false, false, false});
   std::atomic<size_t> next{0};
-  auto work = [&] {
+  auto decode = [&] {
     for (;;) {
-      size_t gi = next++;
+      const size_t task = next++;
+      if (task >= groups.size() * 4) return;
+      const size_t gi = task / 4;
+      const int k = int(task % 4);
+      const RG& g = *groups[gi].first;
+      auto it = leaves.find(names[k]);
+      if (it == leaves.end()) continue;
+      for (auto& c : g.cols)
+        if (c.path == names[k]) { decode_chunk(f.data(), c, it->second, threads, cols[gi][size_t(k)]); has[gi][size_t(k)] = true; }
+    }
+  };
+  const Leaf* la = leaves.count("add.path") ? &leaves["add.path"] : nullptr;
+  const Leaf* lr = leaves.count("remove.path") ? &leaves["remove.path"] : nullptr;
+  const int add_size_def = leaves.count("add.size") ? leaves["add.size"].maxdef : 0;
+  const int rm_ts_def = leaves.count("remove.deletionTimestamp") ? leaves["remove.deletionTimestamp"].maxdef : 0;
+  std::atomic<size_t> next_g{0};
+  auto assemble = [&] {
+    for (;;) {
+      const size_t gi = next_g++;
       if (gi >= groups.size()) return;
       const RG& g = *groups[gi].first;
-      Col cols[4];
-      bool has[4] = {};
-      for (int k = 0; k < 4; ++k) {
-        auto it = leaves.find(names[k]);
-        if (it == leaves.end()) continue;
-        for (auto& c : g.cols) if (c.path == names[k]) { decode_chunk(f.data(), n, c, it->second, g.rows, cols[k]); has[k] = true; }
-      }
-      const Leaf* la = leaves.count("add.path") ? &leaves["add.path"] : nullptr;
-      const Leaf* lr = leaves.count("remove.path") ? &leaves["remove.path"] : nullptr;
+      auto& cs = cols[gi];
+      const auto& h = has[gi];
       for (int64_t i = 0; i < g.rows; ++i) {
         Action& a = acts[base_act + size_t(groups[gi].second + i)];
-        if (has[0] && cols[0].def[i] >= la->def_of[0]) {
-          a.kind = ADD; a.path = cols[0].s[i];
-          if (has[1] && cols[1].def[i] == leaves["add.size"].maxdef) a.size = cols[1].i[i];
-        } else if (has[2] && cols[2].def[i] >= lr->def_of[0]) {
-          a.kind = REMOVE; a.path = cols[2].s[i];
-          if (has[3] && cols[3].def[i] == leaves["remove.deletionTimestamp"].maxdef) { a.has_delts = true; a.delts = cols[3].i[i]; }
+        if (h[0] && cs[0].def[i] >= la->def_of[0]) {
+          a.kind = ADD; a.path = std::move(cs[0].s[i]);
+          if (h[1] && cs[1].def[i] == add_size_def) a.size = cs[1].i[i];
+        } else if (h[2] && cs[2].def[i] >= lr->def_of[0]) {
+          a.kind = REMOVE; a.path = std::move(cs[2].s[i]);
+          if (h[3] && cs[3].def[i] == rm_ts_def) { a.has_delts = true; a.delts = cs[3].i[i]; }
         } else {
           a.kind = OTHER;  // protocol/metaData/txn rows: counted, not keyed
         }
       }
+      cs = std::array<Col, 4>{};
     }
   };
-  std::vector<std::thread> ts;
-  for (int t = 0; t < threads; ++t) ts.emplace_back(work);
-  for (auto& t : ts) t.join();
+  auto tq0 = std::chrono::steady_clock::now();
+  {
+    std::vector<std::thread> ts;
+    for (int t = 0; t < threads; ++t) ts.emplace_back(decode);
+    for (auto& t : ts) t.join();
+  }
+  if (getenv("ORACLE_TIMING")) fprintf(stderr, "  decode %.3fs\n", std::chrono::duration<double>(std::chrono::steady_clock::now() - tq0).count());
+  {
+    std::vector<std::thread> ts;
+    for (int t = 0; t < threads; ++t) ts.emplace_back(assemble);
+    for (auto& t : ts) t.join();
+  }
 }
 
 // ---- listing (D/SnapshotManagement.scala:82-179) -----------------------------------------------
@@ -579,6 +658,7 @@ int main(int argc, char** argv) {
       auto f = read_all(log + "/" + c);
       size_t before = acts.size();
       read_checkpoint(f, acts, threads);
+      if (getenv("ORACLE_TIMING")) fprintf(stderr, "checkpoint %s: %.3fs\n", c.c_str(), std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
       ck_rows += int64_t(acts.size() - before);
     }
     // JSON: all lines of all deltas, parsed by `threads` workers over line ranges
@@ -595,6 +675,7 @@ int main(int argc, char** argv) {
         p = nl + 1;
       }
     }
+    if (getenv("ORACLE_TIMING")) fprintf(stderr, "lines: %.3fs\n", std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
     size_t base = acts.size();
     acts.resize(base + lines.size());
     {
@@ -619,9 +700,26 @@ int main(int argc, char** argv) {
         });
       for (auto& t : ts) t.join();
     }
-    for (size_t i = 0; i < acts.size(); ++i)
-      if (acts[i].kind == ADD || acts[i].kind == REMOVE)
-        part[std::hash<std::string>()(key[i]) % size_t(parts)].push_back(uint32_t(i));
+    {
+      // each thread partitions a contiguous range; concatenating the ranges in thread order keeps
+      // the replay order inside every partition (sortWithinPartitions("file"))
+      std::vector<std::vector<std::vector<uint32_t>>> local;
+      local.resize(static_cast<size_t>(threads));
+      for (auto& l : local) l.resize(static_cast<size_t>(parts));
+      std::vector<std::thread> ts;
+      const size_t per = (acts.size() + size_t(threads) - 1) / size_t(threads);
+      for (int t = 0; t < threads; ++t)
+        ts.emplace_back([&, t] {
+          const size_t b = size_t(t) * per, e = std::min(acts.size(), b + per);
+          for (size_t i = b; i < e; ++i)
+            if (acts[i].kind == ADD || acts[i].kind == REMOVE)
+              local[size_t(t)][std::hash<std::string>()(key[i]) % size_t(parts)].push_back(uint32_t(i));
+        });
+      for (auto& t : ts) t.join();
+      for (int pi = 0; pi < parts; ++pi)
+        for (int t = 0; t < threads; ++t)
+          part[size_t(pi)].insert(part[size_t(pi)].end(), local[size_t(t)][size_t(pi)].begin(), local[size_t(t)][size_t(pi)].end());
+    }
     struct PartOut { int64_t files = 0, size = 0, tombs = 0; uint64_t lks = 0, tks = 0; };
     std::vector<PartOut> po((size_t)parts);
     std::atomic<int> nextp{0};

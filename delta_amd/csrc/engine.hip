@@ -40,9 +40,15 @@ using namespace dr;
 struct dr_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;  // K1 line parsing, overlapped with the checkpoint decode
   std::string err;
   bool timing = false;
-  std::vector<std::pair<std::string, hipEvent_t>> marks;
+  struct Mark {
+    std::string name;
+    hipEvent_t ev;
+    int s;  // 0: stream, 1: stream2
+  };
+  std::vector<Mark> marks;
   std::vector<std::pair<std::string, float>> timings;
   std::multimap<size_t, void*> free_blocks;
   std::unordered_map<void*, size_t> sizes;
@@ -86,23 +92,28 @@ struct dr_ctx {
     }
     free_blocks.clear();
   }
-  void mark(const char* name) {
+  // A stage's time is the interval since the previous mark on the same stream (a stream's first
+  // mark only opens its timeline).
+  void mark(const char* name, int on = 0) {
     if (!timing) return;
     hipEvent_t e;
     HIP_OK(hipEventCreate(&e));
-    HIP_OK(hipEventRecord(e, stream));
-    marks.emplace_back(name, e);
+    HIP_OK(hipEventRecord(e, on ? stream2 : stream));
+    marks.push_back(Mark{name, e, on});
   }
   void collect_timings() {
     timings.clear();
     if (marks.empty()) return;
-    HIP_OK(hipEventSynchronize(marks.back().second));
+    for (auto& m : marks) HIP_OK(hipEventSynchronize(m.ev));
     for (size_t i = 1; i < marks.size(); ++i) {
+      size_t k = i;
+      while (k > 0 && marks[k - 1].s != marks[i].s) --k;
+      if (k == 0) continue;
       float ms = 0;
-      HIP_OK(hipEventElapsedTime(&ms, marks[i - 1].second, marks[i].second));
-      timings.emplace_back(marks[i].first, ms);
+      HIP_OK(hipEventElapsedTime(&ms, marks[k - 1].ev, marks[i].ev));
+      timings.emplace_back(marks[i].name, ms);
     }
-    for (auto& m : marks) (void)hipEventDestroy(m.second);
+    for (auto& m : marks) (void)hipEventDestroy(m.ev);
     marks.clear();
   }
 };
@@ -827,19 +838,38 @@ static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
   DBuf<uint64_t> nonfile(ctx, nlines);
   ActionArrays act{st->kind.p, st->flags.p, st->key.p, st->path_ptr.p, st->path_len.p, st->size.p, st->delts.p,
                    st->src_off.p, st->src_len.p};
+  DBuf<uint64_t> hard(ctx, nlines);
   ctx->mark("json_index");
+  // K1 line parsing runs on stream2, overlapped with the checkpoint decode below (the SNAPPY
+  // resolve/count phases leave most CUs idle); stream waits for it before anything reads the
+  // action arrays. The guard joins stream2 before any buffer it uses can be released.
+  struct Overlap {
+    dr_ctx* c;
+    hipEvent_t fork = nullptr, done = nullptr;
+    ~Overlap() {
+      (void)hipStreamSynchronize(c->stream2);
+      if (fork) (void)hipEventDestroy(fork);
+      if (done) (void)hipEventDestroy(done);
+    }
+  } ov{ctx};
   if (nlines) {
-    launch_json_place(s.d_json.p, json_len, jcounts.p, joff.p, jslots.p, nl.p, stream);
-    ctx->mark("json_newlines");
-    DBuf<uint64_t> hard(ctx, nlines);
+    hipStream_t s2 = ctx->stream2;
+    HIP_OK(hipEventCreateWithFlags(&ov.fork, hipEventDisableTiming));
+    HIP_OK(hipEventRecord(ov.fork, stream));
+    HIP_OK(hipStreamWaitEvent(s2, ov.fork, 0));
+    ctx->mark("json_fork", 1);
+    launch_json_place(s.d_json.p, json_len, jcounts.p, joff.p, jslots.p, nl.p, s2);
+    ctx->mark("json_newlines", 1);
     JsonParseArgs ja{s.d_json.p, nl.p, nlines, R, act.kind, act.flags, act.key, act.path_ptr, act.path_len,
                      act.size, act.delts, act.src_off, act.src_len, counters.p + 0, counters.p + 1, counters.p + 2,
                      nonfile.p, nlines, counters.p + 3, hard.p,
                      reinterpret_cast<unsigned long long*>(counters.p + 5)};
-    launch_json_parse(ja, stream);
-    ctx->mark("json_parse");
-    launch_json_hard(ja, stream);
-    ctx->mark("json_hard");
+    launch_json_parse(ja, s2);
+    ctx->mark("json_parse", 1);
+    launch_json_hard(ja, s2);
+    ctx->mark("json_hard", 1);
+    HIP_OK(hipEventCreateWithFlags(&ov.done, hipEventDisableTiming));
+    HIP_OK(hipEventRecord(ov.done, s2));
   }
   // ---- K2: checkpoint ----
   DBuf<uint8_t> cdef[HC_N];
@@ -884,6 +914,10 @@ static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
     ca.special_bytes = counters.p + 1;
     launch_ckpt_assemble(ca, stream);
     ctx->mark("ckpt_assemble");
+  }
+  if (ov.done) {
+    HIP_OK(hipStreamWaitEvent(stream, ov.done, 0));
+    ctx->mark("json_join");
   }
   // the checkpoint decoder's error code rides in counters[7]: one read-back for both
   if (R) HIP_OK(hipMemcpyAsync(counters.p + 7, pq_err.p, sizeof(uint32_t), hipMemcpyDeviceToDevice, stream));
@@ -1848,6 +1882,7 @@ int dr_ctx_create(int device, dr_ctx** out) {
   }
   if (hipSetDevice(device) != hipSuccess) return DR_E_DEVICE;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return DR_E_DEVICE;
+  if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) return DR_E_DEVICE;
   *out = c.release();
   return DR_OK;
 }
@@ -1855,8 +1890,10 @@ int dr_ctx_create(int device, dr_ctx** out) {
 void dr_ctx_destroy(dr_ctx* ctx) {
   if (!ctx) return;
   (void)hipStreamSynchronize(ctx->stream);
+  (void)hipStreamSynchronize(ctx->stream2);
   ctx->trim();
   (void)hipStreamDestroy(ctx->stream);
+  (void)hipStreamDestroy(ctx->stream2);
   delete ctx;
 }
 
@@ -1950,7 +1987,7 @@ int dr_replay_staged(dr_ctx* ctx, const dr_staged* staged, int64_t cutoff, uint3
     ctx->collect_timings();
   });
   if (rc != DR_OK) {
-    for (auto& m : ctx->marks) (void)hipEventDestroy(m.second);
+    for (auto& m : ctx->marks) (void)hipEventDestroy(m.ev);
     ctx->marks.clear();
   }
   return rc;
@@ -1984,7 +2021,7 @@ int dr_state_apply(dr_ctx* ctx, dr_state* base, const dr_staged* tail, int64_t m
     ctx->collect_timings();
   });
   if (rc != DR_OK) {
-    for (auto& m : ctx->marks) (void)hipEventDestroy(m.second);
+    for (auto& m : ctx->marks) (void)hipEventDestroy(m.ev);
     ctx->marks.clear();
   }
   return rc;
@@ -2197,7 +2234,7 @@ int dr_shard_finish(dr_shard* shard, const uint8_t* verdict_back, dr_state** out
     ctx->collect_timings();
   });
   if (rc != DR_OK) {
-    for (auto& m : ctx->marks) (void)hipEventDestroy(m.second);
+    for (auto& m : ctx->marks) (void)hipEventDestroy(m.ev);
     ctx->marks.clear();
   }
   return rc;

@@ -872,7 +872,7 @@ static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
     HIP_OK(hipEventRecord(ov.done, s2));
   }
   // ---- K2: checkpoint ----
-  DBuf<uint8_t> cdef[HC_N];
+  DBuf<uint8_t> cdefs;  // the hot columns' definition levels, R bytes each, zeroed in one fill
   DBuf<int64_t> cival[HC_N];
   DBuf<uint64_t> csptr[HC_N];
   DBuf<uint32_t> cslen[HC_N];
@@ -881,16 +881,16 @@ static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
   if (R) {
     ParquetArgs pa{};
     pa.ncols = HC_N;
+    cdefs = DBuf<uint8_t>(ctx, uint64_t(HC_N) * R);
+    cdefs.zero(stream);
     for (int c = 0; c < HC_N; ++c) {
-      cdef[c] = DBuf<uint8_t>(ctx, R);
-      cdef[c].zero(stream);
       if (c == HC_ADD_PATH || c == HC_RM_PATH) {
         csptr[c] = DBuf<uint64_t>(ctx, R);
         cslen[c] = DBuf<uint32_t>(ctx, R);
       } else {
         cival[c] = DBuf<int64_t>(ctx, R);
       }
-      pa.cols[c] = FlatColumn{cdef[c].p, nullptr, cival[c].p, csptr[c].p, cslen[c].p};
+      pa.cols[c] = FlatColumn{cdefs.p + uint64_t(c) * R, nullptr, cival[c].p, csptr[c].p, cslen[c].p};
     }
     pq_err = DBuf<uint32_t>(ctx, 1);
     pq_err.zero(stream);

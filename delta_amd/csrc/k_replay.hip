@@ -363,7 +363,6 @@ __device__ __forceinline__ uint64_t path_ref(const ReduceArgs& a, uint32_t i) { 
 __global__ void __launch_bounds__(RED_T) k_bucket_reduce(ReduceArgs a) {
   __shared__ uint32_t tkey[TS_MAX];
   __shared__ uint32_t tval[TS_MAX];
-  __shared__ uint32_t wpos[TS_MAX];  // winner's record offset in the bucket
   __shared__ uint32_t nl, nt, np, overflow;
   const uint32_t b = blockIdx.x;
   const uint64_t beg = a.bucket_off[b], end = a.bucket_off[b + 1];
@@ -395,16 +394,8 @@ __global__ void __launch_bounds__(RED_T) k_bucket_reduce(ReduceArgs a) {
     }
     __syncthreads();
     if (overflow) break;
-    // winners record their position (for the losers' verification pairs)
-    for (uint64_t e = beg + threadIdx.x; e < end; e += RED_T) {
-      const uint4 r = load_rec(a.rec, e);
-      if (sbits && (r.x >> (32 - sbits)) != sp) continue;
-      const uint32_t rk = r.x ? r.x : 1u;
-      uint32_t s = rk & mask;
-      while (tkey[s] != rk) s = (s + 1) & mask;
-      if (tval[s] - 1u == r.y) wpos[s] = uint32_t(e - beg);
-    }
-    __syncthreads();
+    // the table holds each key's winning meta, so a loser pairs with its winner's action index
+    // directly (no pass to record winner positions)
     for (uint64_t e0 = beg; e0 < end; e0 += RED_T) {
       const uint64_t e = e0 + threadIdx.x;
       bool isl = false, ist = false, lose = false;

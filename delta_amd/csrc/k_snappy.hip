@@ -36,8 +36,14 @@ namespace dev {
 
 constexpr uint32_t SNAP_CH = 256;            // compressed bytes per speculation chunk
 constexpr uint32_t SNAP_BLOCK = 65536;       // snappy compressor fragment size
-constexpr uint32_t SNAP_WU = 256;            // speculation warm-up bytes (0.6% mis-speculation on path pages)
-constexpr uint32_t WG_CHUNKS = 256;          // chunks (threads) per chunk-walker workgroup
+#ifndef DR_SNAP_WU
+#define DR_SNAP_WU 192
+#endif
+constexpr uint32_t SNAP_WU = DR_SNAP_WU;     // speculation warm-up bytes (sweep r01: 64/128 B send too many pages to k_snap_resolve, 3x/20x slower; 160-256 B within 1%, 192 B best)
+#ifndef DR_SNAP_WG_CHUNKS
+#define DR_SNAP_WG_CHUNKS 256
+#endif
+constexpr uint32_t WG_CHUNKS = DR_SNAP_WG_CHUNKS;  // chunks (threads) per chunk-walker workgroup
 constexpr uint32_t STAGE_BYTES = (WG_CHUNKS * SNAP_CH + SNAP_WU + 96) * 65 / 64 + 16;  // + skew
 
 struct Elem {
@@ -148,7 +154,6 @@ __device__ __forceinline__ WgInfo wg_info(const SnappyArgs& a) {
 // A: speculative parse.
 __global__ void __launch_bounds__(WG_CHUNKS) k_snap_spec(SnappyArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[STAGE_BYTES + 32];
-  __shared__ uint32_t lvis[(SNAP_CH / 32) * WG_CHUNKS];
   const WgInfo g = wg_info(a);
   const SnapPage& pg = a.pages[g.p];
   const Staged s = stage_input(buf, reinterpret_cast<const uint8_t*>(pg.in), pg.n_in, g.j0, g.cnt);
@@ -157,10 +162,11 @@ __global__ void __launch_bounds__(WG_CHUNKS) k_snap_spec(SnappyArgs a) {
   const uint32_t c = a.chunk_base[g.p] + j;
   const uint64_t cs = uint64_t(j) * SNAP_CH;
   const uint64_t ce = min(cs + SNAP_CH, uint64_t(pg.n_in));
-  // visited bitmap in LDS, word-major so the lanes' ORs of one word index hit distinct banks
-  uint32_t* lv = lvis + threadIdx.x;
+  // visited bitmap in registers (statically indexed: each step ORs its bit into the selected word
+  // with selects, so the walk issues no LDS read-modify-write of its own)
+  uint32_t lv[SNAP_CH / 32];
 #pragma unroll
-  for (int k = 0; k < int(SNAP_CH / 32); ++k) lv[k * WG_CHUNKS] = 0;
+  for (int k = 0; k < int(SNAP_CH / 32); ++k) lv[k] = 0;
   uint64_t pos = cs >= SNAP_WU ? cs - SNAP_WU : 0;
   uint64_t first = ~0ull, out = 0, mid = ~0ull;
   uint32_t elems = 0, hout = 0, helems = 0;
@@ -170,7 +176,9 @@ __global__ void __launch_bounds__(WG_CHUNKS) k_snap_spec(SnappyArgs a) {
     snap_step(staged_u64(buf, s, pos), &adv, &len);
     if (pos >= cs) {
       const uint32_t r = uint32_t(pos - cs);
-      lv[(r >> 5) * WG_CHUNKS] |= 1u << (r & 31);
+      const uint32_t wi = r >> 5, bit = 1u << (r & 31);
+#pragma unroll
+      for (int k = 0; k < int(SNAP_CH / 32); ++k) lv[k] |= wi == uint32_t(k) ? bit : 0u;
       if (first == ~0ull) first = pos;
       out += len;
       ++elems;
@@ -186,7 +194,8 @@ __global__ void __launch_bounds__(WG_CHUNKS) k_snap_spec(SnappyArgs a) {
   a.half_elems[c] = helems;
   a.spec_exit[c] = pos > 0xffffffffull ? 0xffffffffu : uint32_t(pos);
 #pragma unroll
-  for (int k = 0; k < int(SNAP_CH / 32); ++k) a.vis[uint64_t(c) * (SNAP_CH / 32) + k] = lv[k * WG_CHUNKS];
+  for (int k = 0; k < int(SNAP_CH / 32); k += 4)
+    *reinterpret_cast<uint4*>(&a.vis[uint64_t(c) * (SNAP_CH / 32) + k]) = make_uint4(lv[k], lv[k + 1], lv[k + 2], lv[k + 3]);
   // the chunk's output bytes / elements if its true entry is its first visited position (nearly
   // always): k_snap_count then only re-walks the exceptions
   a.spec_first[c] = first > 0xffffffffull ? 0xffffffffu : uint32_t(first);
@@ -476,8 +485,14 @@ __global__ void __launch_bounds__(2 * WG_CHUNKS) k_snap_emit(SnappyArgs a) {
 //  4. each thread gathers its 64 bytes from their roots and stores them with 16-byte stores.
 constexpr int EXEC_T = 1024;
 constexpr uint32_t EXEC_LONG = 256;          // literal records copied by the whole workgroup
-constexpr uint32_t EXEC_RPT = 12;            // records per thread held in registers per pass
-constexpr uint32_t EXEC_RPT2 = 4;            // literal records per thread per pass (roots live in registers)
+#ifndef DR_EXEC_RPT
+#define DR_EXEC_RPT 12
+#endif
+constexpr uint32_t EXEC_RPT = DR_EXEC_RPT;            // records per thread held in registers per pass
+#ifndef DR_EXEC_RPT2
+#define DR_EXEC_RPT2 4
+#endif
+constexpr uint32_t EXEC_RPT2 = DR_EXEC_RPT2;            // literal records per thread per pass (roots live in registers)
 
 __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t src[SNAP_BLOCK];  // map, later bytes + input
@@ -566,7 +581,7 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
   //    Pointers are read 8 at a time so the LDS reads are in flight together.
   uint32_t root[32];  // roots of this thread's 64 contiguous output bytes, two u16 per register
   {
-    uint32_t x[64];     // current pointers of the 4-byte groups
+    uint32_t xp[32];    // current pointers of the 4-byte groups, two u16 per register
     uint32_t act = 0;   // groups with a byte not yet at its root
 #pragma unroll
     for (uint32_t j = 0; j < 16; ++j) {
@@ -583,36 +598,34 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
       const uint2 g = *reinterpret_cast<const uint2*>(&src[i0]);
       const uint32_t sv[4] = {g.x & 0xffffu, g.x >> 16, g.y & 0xffffu, g.y >> 16};
       uint32_t cst = prev, cval = prev != 0xffffffffu ? uint32_t(src[prev < SNAP_BLOCK ? prev : 0]) : 0u;
+      uint32_t x4[4];
 #pragma unroll
       for (uint32_t e = 0; e < 4; ++e) {
         const uint32_t i = i0 + e;
         if ((w0 >> (sh + e)) & 1u) { cst = i; cval = sv[e]; }
-        x[4 * j + e] = (cst != 0xffffffffu && i - cst < 64 && i < nbytes) ? i - cst + cval : i;
+        x4[e] = (cst != 0xffffffffu && i - cst < 64 && i < nbytes) ? i - cst + cval : i;
       }
-      if (i0 < nbytes)
-        *reinterpret_cast<uint2*>(&src[i0]) =
-            make_uint2(x[4 * j] | (x[4 * j + 1] << 16), x[4 * j + 2] | (x[4 * j + 3] << 16));
+      xp[2 * j] = x4[0] | (x4[1] << 16);
+      xp[2 * j + 1] = x4[2] | (x4[3] << 16);
+      // a group is active while a byte points away from itself (i < 65536, so the identity packs too)
+      if (xp[2 * j] != (i0 | ((i0 + 1) << 16)) || xp[2 * j + 1] != ((i0 + 2) | ((i0 + 3) << 16))) act |= 1u << j;
+      if (i0 < nbytes) *reinterpret_cast<uint2*>(&src[i0]) = make_uint2(xp[2 * j], xp[2 * j + 1]);
     }
     __syncthreads();
     stamp(3);
-#pragma unroll
-    for (uint32_t k = 0; k < 64; ++k)
-      if (x[k] != 4 * (uint32_t(t) + EXEC_T * (k >> 2)) + (k & 3)) act |= 1u << (k >> 2);
     while (act) {
 #pragma unroll
       for (uint32_t j = 0; j < 16; ++j) {
         if (act & (1u << j)) {
-          uint32_t y[4];
-#pragma unroll
-          for (uint32_t e = 0; e < 4; ++e) y[e] = src[x[4 * j + e]];
-          const bool fixed = y[0] == x[4 * j] && y[1] == x[4 * j + 1] && y[2] == x[4 * j + 2] && y[3] == x[4 * j + 3];
-#pragma unroll
-          for (uint32_t e = 0; e < 4; ++e) x[4 * j + e] = y[e];
-          if (fixed) {
+          const uint32_t a0 = xp[2 * j], a1 = xp[2 * j + 1];
+          const uint32_t y0 = src[a0 & 0xffffu], y1 = src[a0 >> 16], y2 = src[a1 & 0xffffu], y3 = src[a1 >> 16];
+          const uint32_t b0 = y0 | (y1 << 16), b1 = y2 | (y3 << 16);
+          if (b0 == a0 && b1 == a1) {
             act &= ~(1u << j);
           } else {
-            *reinterpret_cast<uint2*>(&src[4 * (uint32_t(t) + EXEC_T * j)]) =
-                make_uint2(y[0] | (y[1] << 16), y[2] | (y[3] << 16));
+            xp[2 * j] = b0;
+            xp[2 * j + 1] = b1;
+            *reinterpret_cast<uint2*>(&src[4 * (uint32_t(t) + EXEC_T * j)]) = make_uint2(b0, b1);
           }
         }
       }

@@ -170,7 +170,10 @@ __device__ __forceinline__ void emit_line(const JsonParseArgs& a, uint64_t line,
 //     or all removes), so the 64 lanes take the same grammar branch at the same step instead of
 //     diverging byte by byte.
 // The buffer is flushed through phase 2 whenever a lane could overflow it, and at the end.
-constexpr int JL_TOKCAP = 80;
+#ifndef DR_JL_TOKCAP
+#define DR_JL_TOKCAP 40  // 10 KiB LDS per wave: 4 waves/SIMD (80: 20 KiB, LDS-bound at 2; sweep r01: 80 -> 40 = 4.02 -> 2.87 ms, 32 flushes too often)
+#endif
+constexpr int JL_TOKCAP = DR_JL_TOKCAP;
 constexpr int JL_FLUSH = JL_TOKCAP - 16;  // a window adds at most 16 tokens
 
 __global__ void __launch_bounds__(JL_T) k_json_lines(JsonParseArgs a) {

@@ -176,7 +176,10 @@ __device__ __forceinline__ void emit_line(const JsonParseArgs& a, uint64_t line,
 constexpr int JL_TOKCAP = DR_JL_TOKCAP;
 constexpr int JL_FLUSH = JL_TOKCAP - 16;  // a window adds at most 16 tokens
 
-__global__ void __launch_bounds__(JL_T) k_json_lines(JsonParseArgs a) {
+#ifndef DR_JL_WAVES
+#define DR_JL_WAVES 1
+#endif
+__global__ void __launch_bounds__(JL_T, DR_JL_WAVES) k_json_lines(JsonParseArgs a) {
   __shared__ uint32_t tokbuf[JL_TOKCAP * JL_T];
   const uint32_t lane = threadIdx.x;
   const uint64_t line = uint64_t(blockIdx.x) * JL_T + lane;

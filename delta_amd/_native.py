@@ -17,8 +17,9 @@ STATUS = {
     5: "DR_E_MISSING_PART", 6: "DR_E_NONCONTIGUOUS", 7: "DR_E_BAD_SEGMENT",
     8: "DR_E_MISSING_PROTOCOL", 9: "DR_E_MISSING_METADATA", 10: "DR_E_PARSE", 11: "DR_E_PARQUET",
     12: "DR_E_UNSUPPORTED", 13: "DR_E_OOM", 14: "DR_E_DEVICE", 15: "DR_E_INTERNAL",
-    16: "DR_E_CHECKSUM", 17: "DR_E_NO_CHECKSUM",
+    16: "DR_E_CHECKSUM", 17: "DR_E_NO_CHECKSUM", 18: "DR_E_REBUILD",
 }
+DR_E_REBUILD = 18
 DR_E_CHECKSUM, DR_E_NO_CHECKSUM = 16, 17
 DR_FILE_JSON, DR_FILE_CHECKPOINT = 0, 1
 DR_LIVE, DR_TOMBSTONES = 0, 1
@@ -34,7 +35,7 @@ SYMBOLS = [
     "dr_replay", "dr_state_release", "dr_state_apply", "dr_state_counts", "dr_state_nonfile_json", "dr_state_check_checksum",
     "dr_state_export", "dr_filter", "dr_free", "dr_last_timings", "dr_set_timing",
     "dr_shard_plan", "dr_stage_log_shard", "dr_shard_begin", "dr_shard_pack", "dr_shard_reduce",
-    "dr_shard_finish", "dr_shard_release",
+    "dr_shard_finish", "dr_shard_release", "dr_parse_commits", "dr_parsed_release",
 ]
 DR_SHARD_REC_BYTES = 32
 
@@ -70,6 +71,13 @@ class dr_export(C.Structure):
                 ("tags_entry_off", _P64), ("tags_null", _PU8),
                 ("tags_key_off", _P64), ("tags_key_bytes", _PU8),
                 ("tags_val_off", _P64), ("tags_val_bytes", _PU8), ("tags_val_null", _PU8)]
+
+
+class dr_lines(C.Structure):
+    _fields_ = [("n", C.c_int64), ("version", _P64), ("line_off", C.POINTER(C.c_uint64)),
+                ("line_len", C.POINTER(C.c_uint32)), ("kind", _PU8), ("flags", _PU8),
+                ("path_off", C.POINTER(C.c_uint64)), ("path_len", C.POINTER(C.c_uint32)),
+                ("size", _P64), ("deletion_timestamp", _P64), ("bytes", _PU8), ("nbytes", C.c_uint64)]
 
 
 class dr_pred_op(C.Structure):
@@ -142,6 +150,8 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "dr_shard_reduce": ([vp, vp, u64, vp, u64, i64, vp], C.c_int),
         "dr_shard_finish": ([vp, vp, C.POINTER(vp)], C.c_int),
         "dr_shard_release": ([vp], C.c_int),
+        "dr_parse_commits": ([vp, vp, C.POINTER(vp), C.POINTER(dr_lines)], C.c_int),
+        "dr_parsed_release": ([vp], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

@@ -4,8 +4,12 @@
 snapshot's state -- protocol, metaData, txns, live AddFiles and unexpired RemoveFiles, commitInfo
 and cdc dropped, every record with dataChange=false -- as one Parquet file of SingleAction rows,
 checks that it holds numOfFiles adds, and records `_last_checkpoint` = {"version", "size"}. The
-`add` struct is rebuilt as (path, partitionValues, size, modificationTime, dataChange, tags, stats)
-(stats while `checkpoint.writeStatsAsJson`, on by default, :341-343). The schema is nullable
+`add` struct is rebuilt as (path, partitionValues, size, modificationTime, dataChange, tags), then
+`stats` while the table property `delta.checkpoint.writeStatsAsJson` holds (default true,
+D/DeltaConfig.scala:401-406), then `partitionValues_parsed` -- every partition column of the
+metadata's partition schema cast to its type (CheckpointV2.extractPartitionValues, :372-389) --
+when `delta.checkpoint.writeStatsAsStruct` is true or, unset, `checkpointV2.enabled` is (default
+true, D/sources/DeltaSQLConf.scala:363-368) and the table is partitioned. The schema is nullable
 throughout (`chk.schema.asNullable`).
 
 Here the records come from the GPU state through `dr_state_export`'s columnar buffers (gathered
@@ -55,11 +59,37 @@ def _map(pa, e, pre, n):
     return pa.MapArray.from_arrays(offs, keys, vals, mask=pa.array(null) if null.any() else None)
 
 
-def _types(pa):
+_PARSED_TYPES = {"string": "string", "byte": "int8", "short": "int16", "integer": "int32", "long": "int64",
+                 "date": "date32", "boolean": "bool_"}
+
+
+def _conf_bool(md, key: str, default):
+    v = ((md or {}).get("configuration") or {}).get(key)
+    return default if v is None else str(v).strip().lower() == "true"
+
+
+def checkpoint_options(md, checkpoint_v2_enabled: bool = True):
+    """(write stats as JSON, partition schema of partitionValues_parsed or None) from the metadata
+    (D/Checkpoints.scala:340-352)."""
+    from .predicates import partition_schema
+    stats = _conf_bool(md, "delta.checkpoint.writeStatsAsJson", True)
+    struct = _conf_bool(md, "delta.checkpoint.writeStatsAsStruct", None)
+    if struct is None:
+        struct = checkpoint_v2_enabled
+    schema = partition_schema(md) if md else {}
+    return stats, (schema if struct and schema else None)
+
+
+def _types(pa, stats=True, parsed=None):
     mt = pa.map_(pa.string(), pa.string())
-    add_t = pa.struct([("path", pa.string()), ("partitionValues", mt), ("size", pa.int64()),
-                       ("modificationTime", pa.int64()), ("dataChange", pa.bool_()), ("tags", mt),
-                       ("stats", pa.string())])
+    add_f = [("path", pa.string()), ("partitionValues", mt), ("size", pa.int64()),
+             ("modificationTime", pa.int64()), ("dataChange", pa.bool_()), ("tags", mt)]
+    if stats:
+        add_f.append(("stats", pa.string()))
+    if parsed:
+        add_f.append(("partitionValues_parsed",
+                      pa.struct([(c, getattr(pa, _PARSED_TYPES[t])()) for c, t in parsed.items()])))
+    add_t = pa.struct(add_f)
     rm_t = pa.struct([("path", pa.string()), ("deletionTimestamp", pa.int64()), ("dataChange", pa.bool_()),
                       ("extendedFileMetadata", pa.bool_()), ("partitionValues", mt), ("size", pa.int64()),
                       ("tags", mt)])
@@ -73,7 +103,24 @@ def _types(pa):
     return mt, add_t, rm_t, txn_t, md_t, prot_t
 
 
-def _file_struct(pa, state, which, typ):
+def _parsed_struct(pa, pv, parsed, typ):
+    """Cast(add.partitionValues[c] AS type) per partition column: a missing key or a failed
+    non-ANSI cast is null (the device filter's cast grammar, predicates.cast_partition_value)."""
+    from .predicates import cast_partition_value
+    keys = pv.keys.to_pylist() if len(pv) else []
+    items = pv.items.to_pylist() if len(pv) else []
+    offs = pv.offsets.to_pylist() if len(pv) else [0]
+    nulls = pv.is_null().to_pylist() if len(pv) else []
+    cols = {c: [] for c in parsed}
+    for i in range(len(pv)):
+        m = {} if nulls[i] else {keys[j]: items[j] for j in range(offs[i], offs[i + 1])}
+        for c, t in parsed.items():
+            cols[c].append(cast_partition_value(m.get(c), t))
+    arrays = [pa.array(cols[c], f.type) for c, f in zip(parsed, typ)]
+    return pa.StructArray.from_arrays(arrays, fields=list(typ))
+
+
+def _file_struct(pa, state, which, typ, stats=True, parsed=None):
     e = N.dr_export()
     state.eng.check(state.eng.lib.dr_state_export(state.h, which, C.byref(e)))
     n = int(e.n)
@@ -83,8 +130,11 @@ def _file_struct(pa, state, which, typ):
     size = pa.array(_np(e.size, n, np.int64), pa.int64())
     dc = pa.array(np.zeros(n, bool), pa.bool_())
     if which == N.DR_LIVE:
-        stats = _strings(pa, e.stats_off, e.stats_bytes, n, _np(e.stats_null, n, np.uint8))
-        cols = [path, pv, size, pa.array(_np(e.modification_time, n, np.int64), pa.int64()), dc, tags, stats]
+        cols = [path, pv, size, pa.array(_np(e.modification_time, n, np.int64), pa.int64()), dc, tags]
+        if stats:
+            cols.append(_strings(pa, e.stats_off, e.stats_bytes, n, _np(e.stats_null, n, np.uint8)))
+        if parsed:
+            cols.append(_parsed_struct(pa, pv, parsed, typ.field("partitionValues_parsed").type))
     else:
         valid = _np(e.deletion_timestamp_valid, n, np.uint8).astype(bool)
         dts = pa.array(_np(e.deletion_timestamp, n, np.int64), pa.int64(), mask=~valid)
@@ -105,14 +155,15 @@ def _nonfile_rows(state):
     return prot, md, txns
 
 
-def checkpoint_table(state):
+def checkpoint_table(state, checkpoint_v2_enabled: bool = True):
     """The checkpoint rows of a GPU state as an Arrow table (protocol, metaData, txns, adds,
     removes; columns txn, add, remove, metaData, protocol)."""
     import pyarrow as pa
-    mt, add_t, rm_t, txn_t, md_t, prot_t = _types(pa)
-    adds, na = _file_struct(pa, state, N.DR_LIVE, add_t)
-    rms, nr = _file_struct(pa, state, N.DR_TOMBSTONES, rm_t)
     prot, md, txns = _nonfile_rows(state)
+    stats, parsed = checkpoint_options(md, checkpoint_v2_enabled)
+    mt, add_t, rm_t, txn_t, md_t, prot_t = _types(pa, stats, parsed)
+    adds, na = _file_struct(pa, state, N.DR_LIVE, add_t, stats, parsed)
+    rms, nr = _file_struct(pa, state, N.DR_TOMBSTONES, rm_t)
     head = []
     if prot is not None:
         head.append({"protocol": {"minReaderVersion": prot.get("minReaderVersion", 0),
@@ -187,6 +238,14 @@ def write_checkpoint(snapshot, parts: int = 1, row_group_size: int = 1 << 20) ->
     meta = {"version": snapshot.version, "size": rows}
     if parts > 1:
         meta["parts"] = parts
-    with open(os.path.join(log_path, "_last_checkpoint"), "w") as f:
-        f.write(json.dumps(meta) + "\n")
+    write_last_checkpoint(log_path, meta)
     return meta
+
+
+def write_last_checkpoint(log_path: str, meta: dict) -> None:
+    """`_last_checkpoint` through a temp file + rename, so a concurrent reader sees the old or the
+    new file whole (a partial file would be taken as corrupted, D/Checkpoints.scala:166-173)."""
+    tmp = os.path.join(log_path, "._last_checkpoint.%d.tmp" % os.getpid())
+    with open(tmp, "w") as f:
+        f.write(json.dumps(meta, separators=(",", ":")) + "\n")
+    os.replace(tmp, os.path.join(log_path, "_last_checkpoint"))

@@ -25,4 +25,13 @@ std::string fmt(const char* f, A... a) {
   return buf;
 }
 
+// DeltaErrors.actionNotFoundException (D/DeltaErrors.scala:553-560): the stripMargin'd text of the
+// reference, leading newline and trailing indentation included.
+inline std::string action_not_found(const char* action, int64_t version) {
+  return fmt("\nThe %s of your Delta table couldn't be recovered while Reconstructing\nversion: %lld. Did you "
+             "manually delete files in the _delta_log directory?\nSet "
+             "spark.databricks.delta.stateReconstructionValidation.enabled\nto \"false\" to skip validation.\n       ",
+             action, (long long)version);
+}
+
 }  // namespace dr

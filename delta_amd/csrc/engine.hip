@@ -265,6 +265,7 @@ struct dr_state {
   std::vector<std::shared_ptr<StagedData>> sources;
   DBuf<uint16_t> src_id;
   bool sharded = false;  // a rank's part of a sharded replay (source-side survivors, owner-side counters)
+  int64_t cutoff = INT64_MIN;  // minFileRetentionTimestamp the survivors were selected with
   uint64_t n_actions = 0;
   // resident action arrays
   DBuf<uint8_t> kind, flags;
@@ -789,14 +790,10 @@ static void reduce_nonfile(dr_state& st, std::vector<NonFileAction>& acts, bool 
   st.counts.num_protocol = prot ? 1 : 0;
   st.counts.num_metadata = meta ? 1 : 0;
   st.counts.num_set_transactions = int64_t(txns.size());
-  if (validate && !prot)  // D/Snapshot.scala:154-162, D/DeltaErrors.scala:553-560
-    fail(DR_E_MISSING_PROTOCOL, fmt("The protocol of your Delta table could not be recovered while Reconstructing "
-                                    "version: %lld. Did you manually delete files in the _delta_log directory?",
-                                    (long long)st.counts.version));
-  if (validate && !meta)
-    fail(DR_E_MISSING_METADATA, fmt("The metadata of your Delta table could not be recovered while Reconstructing "
-                                    "version: %lld. Did you manually delete files in the _delta_log directory?",
-                                    (long long)st.counts.version));
+  if (validate && !prot)  // D/Snapshot.scala:154-162
+    fail(DR_E_MISSING_PROTOCOL, action_not_found("protocol", st.counts.version));
+  if (validate && !meta)  // D/Snapshot.scala:163-171
+    fail(DR_E_MISSING_METADATA, action_not_found("metadata", st.counts.version));
 }
 
 static uint64_t scan_scratch_for(uint64_t n) { return scan_scratch_bytes(std::max<uint64_t>(n, uint64_t(1) << 23)); }
@@ -804,7 +801,7 @@ static uint64_t scan_scratch_for(uint64_t n) { return scan_scratch_bytes(std::ma
 // K1 + K2 + canonicalisation: fills st's per-action arrays (checkpoint rows first, then JSON lines)
 // and collects the non-file actions (protocol / metaData / txn) on the host in replay order.
 static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr_state* st,
-                          std::vector<NonFileAction>& nf) {
+                          std::vector<NonFileAction>& nf, bool canonicalize = true) {
   StagedData& s = *sp;
   hipStream_t stream = ctx->stream;
   // ---- K1a: newline index ----
@@ -925,7 +922,7 @@ static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
   if (R && cnt[7] != 0) fail(DR_E_PARQUET, fmt("device checkpoint decode failed (code %u)", unsigned(cnt[7])));
   st->counts.malformed_lines = int64_t(cnt[3]);
   // ---- canonicalisation of special paths ----
-  if (cnt[0]) {
+  if (cnt[0] && canonicalize) {
     const uint64_t cap = cnt[1] * 2 + 64 * cnt[0] + 64;
     st->arenas.push_back(std::make_shared<DBuf<uint8_t>>(ctx, cap));
     CanonArgs cg{act, N, st->arenas.back()->p, cap, counters.p + 4};
@@ -1087,6 +1084,11 @@ static dr_state* apply_tail(dr_ctx* ctx, dr_state& base, const std::shared_ptr<S
   if (base.sources.empty()) fail(DR_E_INVALID_ARG, "base state has no staged segment");
   if (base.sharded) fail(DR_E_UNSUPPORTED, "a sharded replay's part cannot take a tail on its own: shard the tail too");
   if (base.sources.size() >= 65535) fail(DR_E_UNSUPPORTED, "too many applied tails on one state; rebuild it");
+  // the base kept only tombstones with delTimestamp > base.cutoff: an earlier cutoff (a longer
+  // delta.deletedFileRetentionDuration, a clock moved back) would need the ones it dropped
+  if (cutoff < base.cutoff)
+    fail(DR_E_REBUILD, fmt("retention cutoff %lld is earlier than the base state's %lld: rebuild the snapshot",
+                           (long long)cutoff, (long long)base.cutoff));
   std::vector<int64_t> vers;
   for (const JsonFileRec& j : tail->jfiles) vers.push_back(j.version);
   std::sort(vers.begin(), vers.end());
@@ -1157,7 +1159,8 @@ static dr_state* apply_tail(dr_ctx* ctx, dr_state& base, const std::shared_ptr<S
                              uint16_t(st->sources.size() - 1), T, stream));
   }
   reduce_actions(ctx, st.get(), cutoff, flags);
-  st->counts.malformed_lines = t->counts.malformed_lines;
+  st->cutoff = cutoff;
+  st->counts.malformed_lines = base.counts.malformed_lines + t->counts.malformed_lines;
   // protocol / metaData / txn: the base's winners first, then the tail's actions in order
   std::vector<NonFileAction> all = base.nonfile;
   for (size_t k = 0; k < all.size(); ++k) all[k].order = k;
@@ -1175,6 +1178,7 @@ static dr_state* replay(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, int6
   std::vector<NonFileAction> nf;
   parse_actions(ctx, sp, st.get(), nf);
   reduce_actions(ctx, st.get(), cutoff, flags);
+  st->cutoff = cutoff;
   reduce_nonfile(*st, nf, !(flags & DR_FLAG_NO_VALIDATION));
   ctx->mark("end");
   return st.release();
@@ -1844,6 +1848,45 @@ static dr_state* shard_finish(dr_shard& sh, const uint8_t* verdict_back) {
 }
 
 // ---------------------------------------------------------------------------------------------------
+// per-line commit decode (getChanges' Action.fromJson hot fields; K1 only)
+// ---------------------------------------------------------------------------------------------------
+struct dr_parsed {
+  std::shared_ptr<StagedData> staged;
+  std::vector<int64_t> version, size, delts;
+  std::vector<uint64_t> line_off, path_off;
+  std::vector<uint32_t> line_len, path_len;
+  std::vector<uint8_t> kind, flags;
+};
+
+static void parse_commits(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr_parsed& out) {
+  if (!sp->parts.empty()) fail(DR_E_INVALID_ARG, "dr_parse_commits takes commit (JSON) files only");
+  hipStream_t stream = ctx->stream;
+  std::unique_ptr<dr_state> st(new_state(ctx, sp));
+  std::vector<NonFileAction> nf;
+  parse_actions(ctx, sp, st.get(), nf, /*canonicalize=*/false);
+  const uint64_t n = st->n_actions;
+  out.staged = sp;
+  out.kind = d2h(st->kind.p, n, stream);
+  out.flags = d2h(st->flags.p, n, stream);
+  out.size = d2h(st->size.p, n, stream);
+  out.delts = d2h(st->delts.p, n, stream);
+  out.line_off = d2h(st->src_off.p, n, stream);
+  out.line_len = d2h(st->src_len.p, n, stream);
+  out.path_len = d2h(st->path_len.p, n, stream);
+  std::vector<uint64_t> pp = d2h(st->path_ptr.p, n, stream);
+  const uint64_t base = reinterpret_cast<uint64_t>(sp->d_json.p);
+  out.path_off.resize(n);
+  out.version.resize(n);
+  size_t f = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    out.flags[i] &= uint8_t(~2u);  // F_SPECIAL_PATH is internal
+    out.path_off[i] = pp[i] ? pp[i] - base : 0;
+    while (f + 1 < sp->jfiles.size() && out.line_off[i] >= sp->jfiles[f + 1].off) ++f;
+    out.version[i] = sp->jfiles.empty() ? -1 : sp->jfiles[f].version;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------------------------------
 namespace {
@@ -2238,6 +2281,36 @@ int dr_shard_finish(dr_shard* shard, const uint8_t* verdict_back, dr_state** out
     ctx->marks.clear();
   }
   return rc;
+}
+
+int dr_parse_commits(dr_ctx* ctx, const dr_staged* staged, dr_parsed** out, dr_lines* lines) {
+  if (!ctx || !staged || !out || !lines) return DR_E_INVALID_ARG;
+  *out = nullptr;
+  return guard(ctx, [&] {
+    HIP_OK(hipSetDevice(ctx->device));
+    auto p = std::make_unique<dr_parsed>();
+    parse_commits(ctx, staged->d, *p);
+    ctx->collect_timings();
+    *lines = dr_lines{};
+    lines->n = int64_t(p->kind.size());
+    lines->version = p->version.data();
+    lines->line_off = p->line_off.data();
+    lines->line_len = p->line_len.data();
+    lines->kind = p->kind.data();
+    lines->flags = p->flags.data();
+    lines->path_off = p->path_off.data();
+    lines->path_len = p->path_len.data();
+    lines->size = p->size.data();
+    lines->deletion_timestamp = p->delts.data();
+    lines->bytes = p->staged->h_json.data();
+    lines->nbytes = p->staged->h_json.size();
+    *out = p.release();
+  });
+}
+
+int dr_parsed_release(dr_parsed* parsed) {
+  delete parsed;
+  return DR_OK;
 }
 
 int dr_shard_release(dr_shard* shard) {

@@ -9,6 +9,7 @@
 #include <map>
 
 #include "common.h"
+#include "json_host.h"
 
 namespace dr {
 namespace {
@@ -54,22 +55,23 @@ bool latest_complete(const std::vector<Inst>& insts, int64_t not_later_than, Ins
   return found;
 }
 
+// Checkpoints.lastCheckpoint (D/Checkpoints.scala:148-175): the first line of _last_checkpoint read
+// as a CheckpointMetaData (Jackson: unknown fields ignored, an absent version reads as 0). A file
+// that does not parse is "corrupted": the reference then lists the log for the latest complete
+// checkpoint (findLastCompleteCheckpoint(MaxValue)), which is what listing from version 0 does here.
 bool parse_last_checkpoint(const std::string& log_path, int64_t* version) {
   std::string p = log_path + "/_last_checkpoint";
   struct stat st;
   if (stat(p.c_str(), &st) != 0) return false;
   std::vector<uint8_t> b = read_file(p);
-  std::string s(b.begin(), b.end());
-  size_t k = s.find("\"version\"");
-  if (k == std::string::npos) return false;
-  k = s.find(':', k);
-  if (k == std::string::npos) return false;
-  ++k;
-  while (k < s.size() && (s[k] == ' ' || s[k] == '\t')) ++k;
-  size_t e = k;
-  while (e < s.size() && s[e] >= '0' && s[e] <= '9') ++e;
-  if (e == k) return false;
-  *version = std::stoll(s.substr(k, e - k));
+  size_t e = 0;
+  while (e < b.size() && b[e] != '\n') ++e;
+  JVal v;
+  if (!json_parse(reinterpret_cast<const char*>(b.data()), e, &v) || v.t != JVal::OBJ) return false;
+  const JVal* x = v.get("version");
+  if (!x || x->t == JVal::NUL) { *version = 0; return true; }
+  if (!x->is_int()) return false;
+  *version = x->as_int();
   return true;
 }
 
@@ -153,7 +155,8 @@ LogSegmentInfo segment_from(const std::string& log_path, int64_t start_ckpt, int
     return seg;
   }
   if (start_ckpt >= 0)
-    fail(DR_E_MISSING_PART, fmt("Checkpoint file to load version: %lld is missing.", (long long)start_ckpt));
+    fail(DR_E_MISSING_PART, fmt("Couldn't find all part files of the checkpoint version: %lld",  // D/DeltaErrors.scala:543-546
+                                (long long)start_ckpt));
   std::vector<int64_t> vers;
   for (auto& n : deltas) {
     vers.push_back(file_version(n));
@@ -161,10 +164,14 @@ LogSegmentInfo segment_from(const std::string& log_path, int64_t start_ckpt, int
   }
   verify_delta_versions(vers);
   if (vers.empty() || vers.front() != 0)
-    fail(DR_E_LOG_TRUNCATED, fmt("%020lld.json: Unable to reconstruct state at version %lld as the "
+    // DeltaErrors.logFileNotFoundException (D/DeltaErrors.scala:451-457) with the default
+    // delta.logRetentionDuration / delta.checkpointRetentionDuration (D/DeltaConfig.scala), rendered
+    // as Spark's CalendarInterval.toString
+    fail(DR_E_LOG_TRUNCATED, fmt("%s/%020lld.json: Unable to reconstruct state at version %lld as the "
                                  "transaction log has been truncated due to manual deletion or the log "
-                                 "retention policy and checkpoint retention policy.",
-                                 0LL, (long long)(vers.empty() ? -1 : vers.back())));
+                                 "retention policy (delta.logRetentionDuration=30 days) and checkpoint "
+                                 "retention policy (delta.checkpointRetentionDuration=2 days)",
+                                 log_path.c_str(), 0LL, (long long)(vers.empty() ? -1 : vers.back())));
   if (version_to_load >= 0 && vers.back() != version_to_load)
     fail(DR_E_BAD_SEGMENT, fmt("requirement failed: Did not get the last delta file version: "
                                "%lld to compute Snapshot", (long long)version_to_load));

@@ -29,7 +29,7 @@ from . import _native as N
 class DeltaError(Exception):
     """Carries the reference's exception class name (`kind`) and the C status."""
 
-    KIND = {3: "FileNotFoundException", 4: "FileNotFoundException", 5: "FileNotFoundException",
+    KIND = {3: "FileNotFoundException", 4: "FileNotFoundException", 5: "IllegalStateException",
             6: "IllegalStateException", 7: "IllegalArgumentException", 8: "IllegalStateException",
             9: "IllegalStateException", 10: "IllegalStateException", 11: "IllegalStateException",
             16: "IllegalStateException"}
@@ -69,6 +69,9 @@ class Engine:
         if rc != N.DR_OK:
             raise DeltaError(rc, "cannot open HIP device %d (libdeltareplay needs an MI355X GPU)" % device)
         self.device = device
+        # a dr_ctx serves one host thread at a time (include/deltareplay.h): snapshots shared
+        # between threads (DeltaLog.for_table's cache) take this lock around every library call
+        self.lock = threading.RLock()
 
     @classmethod
     def get(cls, device: int = 0) -> "Engine":
@@ -101,7 +104,8 @@ class Engine:
     # staging / replay -------------------------------------------------------------------------
     def stage_log(self, log_path: str, version: int = -1) -> "Staged":
         h = C.c_void_p()
-        self.check(self.lib.dr_stage_log(self.ctx, log_path.encode(), int(version), C.byref(h)))
+        with self.lock:
+            self.check(self.lib.dr_stage_log(self.ctx, log_path.encode(), int(version), C.byref(h)))
         return Staged(self, h)
 
     def stage_files(self, files: Sequence[Tuple[int, int, int, bytes]]) -> "Staged":
@@ -112,7 +116,8 @@ class Engine:
             keep.append(buf)
             arr[i] = N.dr_file(version, kind, part, C.cast(buf, C.c_void_p), len(data))
         h = C.c_void_p()
-        self.check(self.lib.dr_stage(self.ctx, arr, len(files), C.byref(h)))
+        with self.lock:
+            self.check(self.lib.dr_stage(self.ctx, arr, len(files), C.byref(h)))
         return Staged(self, h)
 
     def log_segment(self, log_path: str, version: int = -1):
@@ -153,13 +158,41 @@ class Staged:
         st = C.c_void_p()
         flags = (0 if validate else N.DR_FLAG_NO_VALIDATION) | {
             "lds": 0, "reduce64": N.DR_FLAG_REDUCE64, "exact": N.DR_FLAG_EXACT_REDUCE}[reducer]
-        self.eng.check(self.eng.lib.dr_replay_staged(self.eng.ctx, self.h, int(min_file_retention_timestamp),
-                                                     flags, C.byref(st)))
+        with self.eng.lock:
+            self.eng.check(self.eng.lib.dr_replay_staged(self.eng.ctx, self.h, int(min_file_retention_timestamp),
+                                                         flags, C.byref(st)))
         return State(self.eng, st)
+
+    def parse_lines(self) -> List[dict]:
+        """dr_parse_commits: K1's reading of every staged commit line -- {"version", "kind",
+        "path" (raw JSON string body, bytes) or None, "escaped", "size", "deletionTimestamp"}."""
+        lines = N.dr_lines()
+        h = C.c_void_p()
+        with self.eng.lock:
+            self.eng.check(self.eng.lib.dr_parse_commits(self.eng.ctx, self.h, C.byref(h), C.byref(lines)))
+        try:
+            n = lines.n
+            raw = C.string_at(lines.bytes, lines.nbytes) if lines.nbytes else b""
+            out = []
+            for i in range(n):
+                k, f = lines.kind[i], lines.flags[i]
+                rec = {"version": lines.version[i], "kind": k,
+                       "line": raw[lines.line_off[i]:lines.line_off[i] + lines.line_len[i]]}
+                if k in (1, 2):
+                    po = lines.path_off[i]
+                    rec["path"] = None if f & 8 else raw[po:po + lines.path_len[i]]
+                    rec["escaped"] = bool(f & 4)
+                    rec["size"] = lines.size[i]
+                    rec["deletionTimestamp"] = lines.deletion_timestamp[i] if f & 1 else None
+                out.append(rec)
+            return out
+        finally:
+            self.eng.lib.dr_parsed_release(h)
 
     def release(self) -> None:
         if self.h:
-            self.eng.lib.dr_staged_release(self.h)
+            with self.eng.lock:
+                self.eng.lib.dr_staged_release(self.h)
             self.h = None
 
     def __del__(self):
@@ -192,8 +225,9 @@ class State:
         versions (no re-parse of this state's segment); a new State."""
         st = C.c_void_p()
         flags = 0 if validate else N.DR_FLAG_NO_VALIDATION
-        self.eng.check(self.eng.lib.dr_state_apply(self.eng.ctx, self.h, tail.h, int(min_file_retention_timestamp),
-                                                   flags, C.byref(st)))
+        with self.eng.lock:
+            self.eng.check(self.eng.lib.dr_state_apply(self.eng.ctx, self.h, tail.h,
+                                                       int(min_file_retention_timestamp), flags, C.byref(st)))
         return State(self.eng, st)
 
     def check_checksum(self, crc_line: bytes) -> Optional[str]:
@@ -201,7 +235,8 @@ class State:
         mismatch text. Raises ValueError when the line is not a VersionChecksum (no validation)."""
         buf = C.create_string_buffer(1024)
         n = C.c_uint64()
-        rc = self.eng.lib.dr_state_check_checksum(self.h, crc_line, len(crc_line), buf, 1024, C.byref(n))
+        with self.eng.lock:
+            rc = self.eng.lib.dr_state_check_checksum(self.h, crc_line, len(crc_line), buf, 1024, C.byref(n))
         if rc == N.DR_E_NO_CHECKSUM:
             raise ValueError("unparseable checksum")
         if rc == N.DR_E_CHECKSUM:
@@ -213,6 +248,10 @@ class State:
         return None
 
     def export(self, which: int) -> List[dict]:
+        with self.eng.lock:
+            return self._export(which)
+
+    def _export(self, which: int) -> List[dict]:
         e = N.dr_export()
         self.eng.check(self.eng.lib.dr_state_export(self.h, which, C.byref(e)))
         n = e.n
@@ -270,14 +309,16 @@ class State:
         pred, keep = lower_program(program)
         sel = C.POINTER(C.c_int64)()
         n = C.c_int64()
-        self.eng.check(self.eng.lib.dr_filter(self.h, C.byref(pred), C.byref(sel), C.byref(n)))
+        with self.eng.lock:
+            self.eng.check(self.eng.lib.dr_filter(self.h, C.byref(pred), C.byref(sel), C.byref(n)))
         res = [sel[i] for i in range(n.value)]
         self.eng.lib.dr_free(C.cast(sel, C.c_void_p))
         return res
 
     def release(self) -> None:
         if self.h:
-            self.eng.lib.dr_state_release(self.h)
+            with self.eng.lock:
+                self.eng.lib.dr_state_release(self.h)
             self.h = None
 
     def __del__(self):
@@ -448,6 +489,9 @@ class Snapshot:
                  "isLast": False} for i in order if i in keep]
 
     def release(self) -> None:
+        """Frees the resident state now (Snapshot.uncache). Snapshots replaced by `update` are not
+        released by it -- a caller may still hold one, as in the reference, where a replaced
+        snapshot stays usable -- and free their HBM when they are garbage-collected."""
         self.state.release()
 
 
@@ -476,10 +520,10 @@ class DeltaLog:
 
     @classmethod
     def clear_cache(cls) -> None:
+        """DeltaLog.clearCache: drops the cached logs; their snapshots are freed once unreferenced."""
         with cls._lock:
             for dl in cls._cache.values():
-                if dl._snapshot is not None:
-                    dl._snapshot.release()
+                dl._snapshot = None
             cls._cache.clear()
 
     @property
@@ -514,17 +558,27 @@ class DeltaLog:
                     return self._snapshot
             else:
                 new = self._build(-1)
-            old, self._snapshot = self._snapshot, new
-            if old is not None:
-                old.release()  # replaceSnapshot -> uncache (D/SnapshotManagement.scala:333-339)
+            # replaceSnapshot (D/SnapshotManagement.scala:333-339): the old snapshot's state is
+            # freed when its last reference goes (a caller may still be using it)
+            self._snapshot = new
             return new
 
     def _apply_new_commits(self) -> Optional[Snapshot]:
+        """The commits after the current version, applied to the resident state; a full rebuild
+        (the reference's behaviour) when the tail is not a contiguous run of commits after it, a
+        newer checkpoint exists (log cleanup may have removed commits), or the library cannot
+        extend the state (DR_E_REBUILD: e.g. a retention cutoff that moved backwards)."""
         cur = self._snapshot
+        ver, seg = self.engine.log_segment(self.log_path)
+        if ver == cur.version:
+            return None
         names = sorted(n for n in os.listdir(self.log_path)
                        if re.fullmatch(r"\d{20}\.json", n) and int(n[:20]) > cur.version)
-        if not names:
-            return None
+        vers = [int(n[:20]) for n in names]
+        ckpt = max((v for kind, v, _, _ in seg if kind == N.DR_FILE_CHECKPOINT), default=-1)
+        if not vers or vers != list(range(cur.version + 1, cur.version + 1 + len(vers))) or ckpt > cur.version \
+                or vers[-1] != ver:
+            return self._build(-1)
         files = []
         for n in names:
             with open(os.path.join(self.log_path, n), "rb") as f:
@@ -533,9 +587,13 @@ class DeltaLog:
         staged = self.engine.stage_files(files)
         try:
             state = cur.state.apply(staged, cutoff)
+        except DeltaError as e:
+            if e.status != N.DR_E_REBUILD:
+                raise
+            return self._build(-1)
         finally:
             staged.release()
-        return Snapshot(self, int(names[-1][:20]), state, cutoff)
+        return Snapshot(self, vers[-1], state, cutoff)
 
     def checkpoint(self, parts: int = 1) -> dict:
         """Checkpoints.checkpoint (D/Checkpoints.scala:119-141): write the current snapshot's

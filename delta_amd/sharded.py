@@ -34,6 +34,14 @@ from .delta_log import DeltaError, Engine, Staged, State
 _U64 = (1 << 64)
 
 
+
+def _action_not_found(action: str, version: int) -> str:
+    """DeltaErrors.actionNotFoundException (D/DeltaErrors.scala:553-560), as libdeltareplay raises it."""
+    return ("\nThe %s of your Delta table couldn't be recovered while Reconstructing\nversion: %d. Did you "
+            "manually delete files in the _delta_log directory?\nSet "
+            "spark.databricks.delta.stateReconstructionValidation.enabled\nto \"false\" to skip validation.\n"
+            "       " % (action, version))
+
 def shard_plan(log_path: str, world: int, version: int = -1) -> List[dict]:
     """The unit -> rank plan every rank computes (host only; no device needed)."""
     lib = N.lib()
@@ -187,12 +195,10 @@ def merge_nonfile(per_rank: Sequence[str], version: int, validate: bool = True) 
                 app = a["txn"].get("appId") or ""
                 txns.pop(app, None)  # re-insert: order of last update is irrelevant, keep one
                 txns[app] = a
-    if validate and protocol is None:
-        raise DeltaError(8, "The protocol of your Delta table could not be recovered while Reconstructing "
-                            "version: %d. Did you manually delete files in the _delta_log directory?" % version)
-    if validate and metadata is None:
-        raise DeltaError(9, "The metadata of your Delta table could not be recovered while Reconstructing "
-                            "version: %d. Did you manually delete files in the _delta_log directory?" % version)
+    if validate and protocol is None:  # D/Snapshot.scala:154-162
+        raise DeltaError(8, _action_not_found("protocol", version))
+    if validate and metadata is None:  # D/Snapshot.scala:163-171
+        raise DeltaError(9, _action_not_found("metadata", version))
     out = ([protocol] if protocol else []) + ([metadata] if metadata else []) + list(txns.values())
     counts = {"num_protocol": 1 if protocol else 0, "num_metadata": 1 if metadata else 0,
               "num_set_transactions": len(txns)}

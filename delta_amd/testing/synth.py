@@ -316,7 +316,8 @@ def write_checkpoint_records(path: str, protocol: dict, metadata: dict, adds: li
                              txns: list = (), row_group_size: int = 1 << 20, use_dictionary: bool = True,
                              data_page_version: str = "1.0", data_page_size: int = 1 << 20) -> int:
     """Checkpoint with the reference's column layout from explicit action records (edge-case
-    corpora: any partitionValues / tags maps, nulls). Rows: protocol, metaData, txns, adds, removes."""
+    corpora: any partitionValues / tags maps, nulls). Rows: protocol, metaData, txns, adds, removes
+    (protocol / metadata None: no such row, as in DeltaLogSuite's checkpoints missing an action)."""
     pa, _ = _pa()
     import pyarrow.parquet as pq
     mt = pa.map_(pa.string(), pa.string())
@@ -338,13 +339,17 @@ def write_checkpoint_records(path: str, protocol: dict, metadata: dict, adds: li
         return None if d is None else list(d.items())
 
     rows = []
-    rows.append({"protocol": protocol})
-    md = dict(metadata)
-    rows.append({"metaData": {"id": md["id"], "name": md.get("name"), "description": md.get("description"),
-                              "format": {"provider": md.get("format", {}).get("provider", "parquet"),
-                                         "options": m(md.get("format", {}).get("options") or {})},
-                              "schemaString": md["schemaString"], "partitionColumns": md.get("partitionColumns", []),
-                              "configuration": m(md.get("configuration") or {}), "createdTime": md.get("createdTime")}})
+    if protocol is not None:
+        rows.append({"protocol": protocol})
+    if metadata is not None:
+        md = dict(metadata)
+        rows.append({"metaData": {"id": md["id"], "name": md.get("name"), "description": md.get("description"),
+                                  "format": {"provider": md.get("format", {}).get("provider", "parquet"),
+                                             "options": m(md.get("format", {}).get("options") or {})},
+                                  "schemaString": md["schemaString"],
+                                  "partitionColumns": md.get("partitionColumns", []),
+                                  "configuration": m(md.get("configuration") or {}),
+                                  "createdTime": md.get("createdTime")}})
     rows += [{"txn": t} for t in txns]
     for a in adds:
         rows.append({"add": dict(path=a["path"], partitionValues=m(a.get("partitionValues")), size=a.get("size", 0),

@@ -24,10 +24,9 @@ extern "C" {
 #define DR_ABI_VERSION 1
 
 /* Status codes. The JNI shim rethrows the reference's exception class with dr_last_error():
- *   DR_E_EMPTY_DIR / DR_E_LOG_TRUNCATED / DR_E_MISSING_PART -> FileNotFoundException
- *     (D/DeltaErrors.scala:451-457,915-917,543-546)
- *   DR_E_NONCONTIGUOUS / DR_E_MISSING_PROTOCOL / DR_E_MISSING_METADATA -> IllegalStateException
- *     (D/DeltaErrors.scala:548-551,553-560)
+ *   DR_E_EMPTY_DIR / DR_E_LOG_TRUNCATED -> FileNotFoundException (D/DeltaErrors.scala:451-457,915-917)
+ *   DR_E_MISSING_PART / DR_E_NONCONTIGUOUS / DR_E_MISSING_PROTOCOL / DR_E_MISSING_METADATA
+ *     -> IllegalStateException (D/DeltaErrors.scala:543-546,548-551,553-560)
  *   DR_E_BAD_SEGMENT -> IllegalArgumentException (require(...) in D/SnapshotManagement.scala:124-131) */
 enum dr_status {
   DR_OK = 0,
@@ -47,7 +46,9 @@ enum dr_status {
   DR_E_DEVICE = 14,
   DR_E_INTERNAL = 15,
   DR_E_CHECKSUM = 16,     /* computed state differs from the version's .crc (IllegalStateException) */
-  DR_E_NO_CHECKSUM = 17   /* .crc empty or unparseable: ReadChecksum yields None, nothing to validate */
+  DR_E_NO_CHECKSUM = 17,  /* .crc empty or unparseable: ReadChecksum yields None, nothing to validate */
+  DR_E_REBUILD = 18       /* dr_state_apply cannot extend this base (e.g. its retention cutoff is later than
+                             the new one): the caller rebuilds the snapshot from its segment instead */
 };
 
 /* Segment file kinds (D/DeltaLogFileIndex.scala:67-68). */
@@ -155,7 +156,7 @@ int dr_state_release(dr_state* state);
 
 /* Incremental update: the state of `base`'s segment extended by the commit files staged in
  * `tail` (dr_stage with JSON files of versions base+1, base+2, ... contiguous), with a new
- * retention cutoff (not earlier than the base's). Replaces the full rebuild of
+ * retention cutoff (not earlier than the base's: DR_E_REBUILD otherwise). Replaces the full rebuild of
  * SnapshotManagement.update (D/SnapshotManagement.scala:286-330) with K3/K4 over the base's
  * survivors followed by the tail's lines; equal to dr_replay over the whole segment. `base` and
  * `tail` stay owned by the caller and may be released afterwards (the new state keeps what it
@@ -178,6 +179,36 @@ int dr_state_check_checksum(dr_state* state, const char* crc, uint64_t crc_len, 
                             uint64_t* msg_len);
 /* Materialises allFiles (DR_LIVE) or tombstones (DR_TOMBSTONES) on the host, dataChange=false. */
 int dr_state_export(dr_state* state, int32_t which, dr_export* out);
+
+/* ---- per-line commit decode (device) --------------------------------------------------------
+ * The hot fields of DeltaLog.getChanges' per-line Action.fromJson (D/DeltaLog.scala:222-238,
+ * D/actions/actions.scala:57-59) for a streaming host: K1 over the staged commit (JSON) files, one
+ * record per newline-terminated line in file order (blank lines included, kind DR_KIND_NONE), with
+ * the replay's reading of a line (Spark's PERMISSIVE JSON reader over Action.logSchema: a line it
+ * cannot read is DR_KIND_MALFORMED). Paths are the raw JSON string bodies (DR_LF_PATH_ESCAPED
+ * when they hold escapes) at `bytes + path_off`; `size` reads 0 and the deletion timestamp is
+ * absent (no DR_LF_HAS_DELETION_TS) when the line has none. Owned by `parsed` until
+ * dr_parsed_release. */
+enum dr_action_kind { DR_KIND_NONE = 0, DR_KIND_ADD = 1, DR_KIND_REMOVE = 2, DR_KIND_METADATA = 3,
+                      DR_KIND_TXN = 4, DR_KIND_PROTOCOL = 5, DR_KIND_CDC = 6, DR_KIND_COMMITINFO = 7,
+                      DR_KIND_MALFORMED = 15 };
+#define DR_LF_HAS_DELETION_TS 0x1u
+#define DR_LF_PATH_ESCAPED 0x4u
+#define DR_LF_PATH_NULL 0x8u
+typedef struct dr_lines {
+  int64_t n;
+  const int64_t* version;                          /* commit version of the line's file */
+  const uint64_t* line_off; const uint32_t* line_len;  /* the line in `bytes` (no newline) */
+  const uint8_t* kind;                             /* dr_action_kind, SingleAction.unwrap priority */
+  const uint8_t* flags;                            /* DR_LF_* */
+  const uint64_t* path_off; const uint32_t* path_len;  /* add / remove path in `bytes` */
+  const int64_t* size;
+  const int64_t* deletion_timestamp;
+  const uint8_t* bytes; uint64_t nbytes;           /* the staged commit bytes, files newline-terminated */
+} dr_lines;
+typedef struct dr_parsed dr_parsed;
+int dr_parse_commits(dr_ctx* ctx, const dr_staged* staged, dr_parsed** parsed, dr_lines* lines);
+int dr_parsed_release(dr_parsed* parsed);
 
 /* ---- partition pruning (device) -----------------------------------------------------------
  * Replaces DeltaLog.filterFileList + rewritePartitionFilters (D/DeltaLog.scala:500-547) for

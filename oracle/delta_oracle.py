@@ -103,8 +103,10 @@ def read_last_checkpoint(log_path: str) -> Optional[dict]:
         with open(p, "r") as f:
             line = f.readline()
         d = json.loads(line)
-        return {"version": int(d["version"]), "size": d.get("size"),
-                "parts": d.get("parts")}
+        v = d.get("version")  # Jackson: an absent / null Long reads as 0
+        if v is not None and type(v) is not int:
+            raise ValueError(v)
+        return {"version": v or 0, "size": d.get("size"), "parts": d.get("parts")}
     except Exception:
         inst = _find_last_complete_checkpoint(log_path)
         return None if inst is None else {"version": inst.version, "size": -1,
@@ -184,14 +186,18 @@ def get_log_segment(log_path: str, version_to_load: Optional[int] = None,
         version = vers[-1] if vers else new_ckpt.version
         return LogSegment(log_path, version, after, new_ckpt.files(), new_ckpt.version)
     if start_checkpoint is not None:
-        raise DeltaError("FileNotFoundException",
-                         "Checkpoint file to load version: %d is missing." % start_checkpoint)
+        # DeltaErrors.missingPartFilesException (D/DeltaErrors.scala:543-546)
+        raise DeltaError("IllegalStateException",
+                         "Couldn't find all part files of the checkpoint version: %d" % start_checkpoint)
     vers = [file_version(d) for d in deltas]
     verify_delta_versions(vers)
     if not vers or vers[0] != 0:
-        raise DeltaError("FileNotFoundException", "%s: Unable to reconstruct state at version %s "
-                         "as the transaction log has been truncated" % (delta_file(0),
-                                                                      vers[-1] if vers else -1))
+        # DeltaErrors.logFileNotFoundException (D/DeltaErrors.scala:451-457), default retentions
+        raise DeltaError("FileNotFoundException", "%s/%s: Unable to reconstruct state at version %s as the "
+                         "transaction log has been truncated due to manual deletion or the log retention "
+                         "policy (delta.logRetentionDuration=30 days) and checkpoint retention policy "
+                         "(delta.checkpointRetentionDuration=2 days)"
+                         % (log_path, delta_file(0), vers[-1] if vers else -1))
     return LogSegment(log_path, vers[-1], deltas, [], None)
 
 
@@ -416,6 +422,14 @@ class Snapshot:
                 "numOfSetTransactions": self.num_of_set_transactions}
 
 
+def action_not_found(action: str, version: int) -> str:
+    """DeltaErrors.actionNotFoundException (D/DeltaErrors.scala:553-560): the stripMargin'd text."""
+    return ("\nThe %s of your Delta table couldn't be recovered while Reconstructing\nversion: %d. Did you "
+            "manually delete files in the _delta_log directory?\nSet "
+            "spark.databricks.delta.stateReconstructionValidation.enabled\nto \"false\" to skip validation.\n"
+            "       " % (action, version))
+
+
 def state_reconstruction(seg: LogSegment, min_file_retention_timestamp: int,
                          validate: bool = True) -> Snapshot:
     """stateReconstruction + computedState. Spark's hash partitioning is a placement detail;
@@ -435,16 +449,10 @@ def state_reconstruction(seg: LogSegment, min_file_retention_timestamp: int,
             adds.append(a)
         else:
             rms.append(a)
-    if validate and prot is None:  # D/Snapshot.scala:154-162; D/DeltaErrors.scala:553-560
-        raise DeltaError("IllegalStateException",
-                         "The protocol of your Delta table could not be recovered while Reconstructing"
-                         " version: %d. Did you manually delete files in the _delta_log directory?"
-                         % seg.version)
-    if validate and meta is None:
-        raise DeltaError("IllegalStateException",
-                         "The metadata of your Delta table could not be recovered while Reconstructing"
-                         " version: %d. Did you manually delete files in the _delta_log directory?"
-                         % seg.version)
+    if validate and prot is None:  # D/Snapshot.scala:154-162
+        raise DeltaError("IllegalStateException", action_not_found("protocol", seg.version))
+    if validate and meta is None:  # D/Snapshot.scala:163-171
+        raise DeltaError("IllegalStateException", action_not_found("metadata", seg.version))
     return Snapshot(seg.version, prot, meta, txns, adds, rms)
 
 

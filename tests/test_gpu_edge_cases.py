@@ -1,0 +1,462 @@
+"""GPU parity on the reference's edge cases, through the C-ABI (dr_stage_log / dr_replay_staged /
+dr_parse_commits), each against the oracle and the reference test it restates:
+
+* path canonicalization and the URI replay key (T/DeltaLogSuite.scala:190-254, D/Snapshot.scala:301-328,
+  D/actions/actions.scala:208-213): unqualified absolute adds vs `file:` / `file://` removes, special
+  characters, JSON-escaped paths, absolute tombstones qualified as `file://...`, checkpoint rows;
+* replay order: delete + re-add (T/DeltaLogSuite.scala:256-279), the same path twice in one commit;
+* the replay's error branches: missing protocol / metadata from JSON and from a checkpoint
+  (T/DeltaLogSuite.scala:306-400), corrupt `_last_checkpoint` (:162-188), truncated log, missing
+  or incomplete checkpoint parts, zero-byte checkpoints, an empty log directory;
+* K1's device walker (k_json_lines + k_json_hard) over the host fuzz corpus and its mutations
+  (tests/test_json_lane.py), read back per line with dr_parse_commits;
+* dr_state_apply with a retention cutoff that moved backwards (rebuild), and a replaced snapshot
+  that stays usable.
+"""
+import json
+import os
+import random
+import shutil
+
+import pytest
+
+from oracle import delta_oracle as O
+from tests.conftest import GOLDEN
+from tests.test_gpu_parity import _assert_same, _canon, _gpu_replay
+
+pytestmark = pytest.mark.gpu
+
+REF = os.path.join(GOLDEN, "ref")
+PROTOCOL = {"protocol": {"minReaderVersion": 1, "minWriterVersion": 2}}
+METADATA = {"metaData": {"id": "edge", "format": {"provider": "parquet", "options": {}},
+                         "schemaString": '{"type":"struct","fields":[]}', "partitionColumns": [],
+                         "configuration": {}, "createdTime": 1}}
+
+
+@pytest.fixture(scope="module")
+def engine():
+    from delta_amd.delta_log import Engine
+    return Engine.get(0)
+
+
+def add(path, size=100, mtime=10, data_change=True):
+    return {"add": {"path": path, "partitionValues": {}, "size": size, "modificationTime": mtime,
+                    "dataChange": data_change}}
+
+
+def remove(path, ts=200, data_change=False):
+    return {"remove": {"path": path, "deletionTimestamp": ts, "dataChange": data_change}}
+
+
+def write_commit(lp, version, actions, raw_lines=()):
+    os.makedirs(lp, exist_ok=True)
+    lines = [json.dumps(a, separators=(",", ":")) for a in actions] + list(raw_lines)
+    with open(os.path.join(lp, "%020d.json" % version), "w") as f:
+        f.write("\n".join(lines) + "\n")
+
+
+def _same_as_oracle(engine, lp, cutoff=0, version=-1):
+    snap = O.state_reconstruction(O.get_log_segment(lp, None if version < 0 else version), cutoff)
+    st = _gpu_replay(engine, lp, cutoff, version=version)
+    try:
+        _assert_same(st, snap)
+        return st.counts, st.export(0), st.export(1)
+    finally:
+        st.release()
+
+
+def _error(engine, lp, cutoff=0, validate=True):
+    from delta_amd.delta_log import DeltaError
+    with pytest.raises(DeltaError) as ei:
+        _gpu_replay(engine, lp, cutoff, validate=validate)
+    return ei.value
+
+
+# ---- canonicalization (T/DeltaLogSuite.scala:190-254) ---------------------------------------------
+@pytest.mark.parametrize("scheme", ["file:", "file://"])
+@pytest.mark.parametrize("path", ["/some/unqualified/absolute/path",
+                                  "/some/unqualified/with%20space/p@%23h"])  # new Path(..).toUri.toString
+def test_paths_are_canonicalized(engine, tmp_path, scheme, path):
+    lp = str(tmp_path / "_delta_log")
+    write_commit(lp, 0, [PROTOCOL, METADATA, add(path)])
+    write_commit(lp, 1, [remove(scheme + path)])
+    counts, live, tomb = _same_as_oracle(engine, lp)
+    assert counts["num_files"] == 0 and counts["version"] == 1
+    assert [t["path"] for t in tomb] == [scheme + path]  # a qualified path is kept as written
+
+
+@pytest.mark.parametrize("add_path,rm_path,live", [
+    ("file:/x/y.parquet", "/x/y.parquet", 0),          # the other direction
+    ("file:///x/y.parquet", "file:/x/y.parquet", 0),   # URI equality: empty authority == none
+    ("/x//y.parquet", "/x/y.parquet", 0),               # Hadoop Path normalisation of the absolute add
+    ("file://host/x/y.parquet", "file:/x/y.parquet", 1),  # an authority is part of the key
+    ("a/b.parquet", "/a/b.parquet", 1),                 # relative != absolute
+])
+def test_uri_replay_key(engine, tmp_path, add_path, rm_path, live):
+    lp = str(tmp_path / "_delta_log")
+    write_commit(lp, 0, [PROTOCOL, METADATA, add(add_path)])
+    write_commit(lp, 1, [remove(rm_path)])
+    counts, _, _ = _same_as_oracle(engine, lp)
+    assert counts["num_files"] == live
+
+
+def test_escaped_paths(engine, tmp_path):
+    """JSON escapes in a path are decoded before canonicalization and keying: `\\/x\\/a` is `/x/a`,
+    `a\\u0062c` is `abc`, `\\u00e9` is UTF-8 `é`."""
+    lp = str(tmp_path / "_delta_log")
+    write_commit(lp, 0, [PROTOCOL, METADATA, add("/x/a.parquet"), add("abc.parquet"), add("keep\u00e9.parquet")])
+    write_commit(lp, 1, [], raw_lines=['{"remove":{"path":"file:\\/x\\/a.parquet","deletionTimestamp":5}}',
+                                       '{"remove":{"path":"a\\u0062c.parquet","deletionTimestamp":6}}'])
+    counts, live, tomb = _same_as_oracle(engine, lp)
+    assert [f["path"] for f in live] == ["keep\u00e9.parquet"]
+    assert sorted(t["path"] for t in tomb) == ["abc.parquet", "file:/x/a.parquet"]
+
+
+def test_absolute_tombstone_is_qualified(engine, tmp_path):
+    """"do not relativize paths in RemoveFiles": a tombstone of an absolute path is stored as
+    file://<path> (T/DeltaLogSuite.scala:243-254)."""
+    lp = str(tmp_path / "_delta_log")
+    path = str(tmp_path / "a" / "b" / "c")
+    write_commit(lp, 0, [PROTOCOL, METADATA, remove(path, ts=1700000000000, data_change=True)])
+    _, live, tomb = _same_as_oracle(engine, lp)
+    assert not live and [t["path"] for t in tomb] == ["file://" + path]
+    assert tomb[0]["dataChange"] is False
+
+
+def test_checkpoint_rows_with_absolute_paths(engine, tmp_path):
+    """Canonicalization of checkpoint rows (k_ckpt_assemble flags them, k_canon rewrites them):
+    a checkpoint with absolute and `file:` paths, removed by JSON commits in the other form."""
+    from delta_amd.testing import synth as S
+    lp = str(tmp_path / "_delta_log")
+    os.makedirs(lp)
+    adds = [{"path": p, "partitionValues": {}, "size": i + 1, "modificationTime": 5}
+            for i, p in enumerate(["/abs/one.parquet", "file:/abs/two.parquet", "file:///abs/three.parquet",
+                                   "rel/four.parquet"])]
+    rms = [{"path": "/abs/gone.parquet", "deletionTimestamp": 50}]
+    S.write_checkpoint_records(os.path.join(lp, "%020d.checkpoint.parquet" % 3), PROTOCOL["protocol"],
+                               METADATA["metaData"], adds, rms)
+    write_commit(lp, 4, [remove("file:///abs/one.parquet"), remove("/abs/two.parquet"),
+                         add("file:/abs/gone.parquet")])
+    counts, live, tomb = _same_as_oracle(engine, lp, cutoff=10)
+    assert sorted(f["path"] for f in live) == ["file:/abs/gone.parquet", "file:///abs/three.parquet",
+                                               "rel/four.parquet"]
+    assert sorted(t["path"] for t in tomb) == ["file:///abs/one.parquet", "file:///abs/two.parquet"]
+
+
+# ---- replay order -----------------------------------------------------------------------------------
+def test_delete_and_readd_in_different_transactions(engine, tmp_path):
+    """T/DeltaLogSuite.scala:256-279: add, remove, re-add -> live, dataChange=false."""
+    lp = str(tmp_path / "_delta_log")
+    write_commit(lp, 0, [PROTOCOL, METADATA, add("foo")])
+    write_commit(lp, 1, [remove("foo", ts=10)])
+    write_commit(lp, 2, [add("foo", size=7)])
+    counts, live, tomb = _same_as_oracle(engine, lp)
+    assert [(f["path"], f["size"], f["dataChange"]) for f in live] == [("foo", 7, False)] and not tomb
+
+
+def test_same_path_twice_in_one_commit(engine, tmp_path):
+    """PROTOCOL.md:209 forbids it; the reference's stable sort over a one-split commit makes the
+    last line win (SURVEY.md §7 'Ordering')."""
+    lp = str(tmp_path / "_delta_log")
+    write_commit(lp, 0, [PROTOCOL, METADATA, add("a", size=1), add("a", size=2), add("b"), remove("b", ts=9),
+                         remove("c", ts=9), add("c", size=3)])
+    write_commit(lp, 1, [add("d", size=4), remove("d", ts=11), add("d", size=5), add("e", size=6),
+                         add("e", size=7)])
+    counts, live, tomb = _same_as_oracle(engine, lp)
+    assert sorted((f["path"], f["size"]) for f in live) == [("a", 2), ("c", 3), ("d", 5), ("e", 7)]
+    assert [t["path"] for t in tomb] == ["b"]
+
+
+# ---- error branches -----------------------------------------------------------------------------------
+@pytest.mark.parametrize("action", ["protocol", "metadata"])
+def test_missing_action_in_json(engine, tmp_path, action):
+    """T/DeltaLogSuite.scala:306-330."""
+    lp = str(tmp_path / "_delta_log")
+    write_commit(lp, 0, [PROTOCOL if action == "metadata" else METADATA, add("abc", 1, 1)])
+    e = _error(engine, lp)
+    assert e.kind == "IllegalStateException"
+    assert str(e) == O.action_not_found(action, 0)
+    with pytest.raises(O.DeltaError) as oe:
+        O.state_reconstruction(O.get_log_segment(lp), 0)
+    assert str(oe.value) == str(e)
+    st = _gpu_replay(engine, lp, 0, validate=False)  # stateReconstructionValidation.enabled=false
+    try:
+        assert st.counts["version"] == 0 and st.counts["num_files"] == 1
+    finally:
+        st.release()
+
+
+@pytest.mark.parametrize("action", ["protocol", "metadata"])
+def test_missing_action_in_checkpoint(engine, tmp_path, action):
+    """T/DeltaLogSuite.scala:332-400: the checkpoint at version 10 keeps the adds but lacks the action."""
+    from delta_amd.testing import synth as S
+    lp = str(tmp_path / "_delta_log")
+    os.makedirs(lp)
+    adds = [{"path": str(i), "partitionValues": {}, "size": 1, "modificationTime": 1} for i in range(11)]
+    S.write_checkpoint_records(os.path.join(lp, "%020d.checkpoint.parquet" % 10),
+                               None if action == "protocol" else PROTOCOL["protocol"],
+                               None if action == "metadata" else METADATA["metaData"], adds)
+    with open(os.path.join(lp, "_last_checkpoint"), "w") as f:
+        f.write('{"version":10,"size":12}\n')
+    for v in range(0, 11):
+        write_commit(lp, v, [add(str(v), 1, 1)])
+    e = _error(engine, lp)
+    assert e.kind == "IllegalStateException" and str(e) == O.action_not_found(action, 10)
+    st = _gpu_replay(engine, lp, 0, validate=False)
+    try:
+        assert st.counts["version"] == 10 and st.counts["num_files"] == 11
+    finally:
+        st.release()
+
+
+def _checkpointed_table(tmp_path, parts=None, last=True):
+    """v0..v7 with a complete checkpoint at v3 (single part) and one at v6 (`parts` parts)."""
+    from delta_amd.testing import synth as S
+    lp = str(tmp_path / "_delta_log")
+    write_commit(lp, 0, [PROTOCOL, METADATA] + [add("f%d" % i) for i in range(4)])
+    for v in range(1, 8):
+        write_commit(lp, v, [remove("f%d" % (v - 1), ts=100 + v), add("g%d" % v, size=v)])
+
+    def ckpt(version, nparts):
+        snap = O.state_reconstruction(O.get_log_segment(lp, version), 0)
+        adds, rms = snap.all_files, snap.tombstones
+        if not nparts:
+            S.write_checkpoint_records(os.path.join(lp, "%020d.checkpoint.parquet" % version), snap.protocol,
+                                       snap.metadata, adds, rms)
+            return
+        for k in range(nparts):  # split the rows over the parts (protocol + metadata in part 1)
+            sl = lambda xs: xs[k::nparts]
+            S.write_checkpoint_records(
+                os.path.join(lp, "%020d.checkpoint.%010d.%010d.parquet" % (version, k + 1, nparts)),
+                snap.protocol if k == 0 else None, snap.metadata if k == 0 else None, sl(adds), sl(rms))
+
+    ckpt(3, None)
+    ckpt(6, parts)
+    if last:
+        with open(os.path.join(lp, "_last_checkpoint"), "w") as f:
+            f.write(json.dumps({"version": 6, "size": 9, **({"parts": parts} if parts else {})}) + "\n")
+    return lp
+
+
+@pytest.mark.parametrize("content", [b"", b'{"version":', b"not json\n", b'{"version":"6"}'])
+def test_corrupt_last_checkpoint_falls_back_to_listing(engine, tmp_path, content):
+    """T/DeltaLogSuite.scala:162-188: a corrupted `_last_checkpoint` -> the latest complete
+    checkpoint found by listing (D/Checkpoints.scala:166-173)."""
+    lp = _checkpointed_table(tmp_path, parts=3)
+    with open(os.path.join(lp, "_last_checkpoint"), "wb") as f:
+        f.write(content)
+    ver, files = engine.log_segment(lp)
+    assert ver == 7 and {(k, v) for k, v, _, _ in files if k == 1} == {(1, 6)}
+    counts, _, _ = _same_as_oracle(engine, lp)
+    assert counts["version"] == 7
+
+
+def test_missing_checkpoint_part(engine, tmp_path):
+    """`_last_checkpoint` names a 3-part checkpoint one of whose parts is gone:
+    missingPartFilesException (D/SnapshotManagement.scala:150-156, D/DeltaErrors.scala:543-546)."""
+    lp = _checkpointed_table(tmp_path, parts=3)
+    os.remove(os.path.join(lp, "%020d.checkpoint.%010d.%010d.parquet" % (6, 2, 3)))
+    e = _error(engine, lp)
+    assert e.kind == "IllegalStateException"
+    assert str(e) == "Couldn't find all part files of the checkpoint version: 6"
+    with pytest.raises(O.DeltaError) as oe:
+        O.get_log_segment(lp)
+    assert str(oe.value) == str(e)
+
+
+@pytest.mark.parametrize("damage", ["part", "zero"])
+def test_incomplete_or_empty_checkpoint_is_skipped(engine, tmp_path, damage):
+    """Without `_last_checkpoint`, an incomplete multi-part checkpoint (a part missing) or a 0-byte
+    checkpoint file is skipped for the previous complete one (D/Checkpoints.scala:210-218,
+    D/SnapshotManagement.scala:90-92)."""
+    lp = _checkpointed_table(tmp_path, parts=3 if damage == "part" else None, last=False)
+    if damage == "part":
+        os.remove(os.path.join(lp, "%020d.checkpoint.%010d.%010d.parquet" % (6, 3, 3)))
+    else:
+        open(os.path.join(lp, "%020d.checkpoint.parquet" % 6), "wb").close()
+    ver, files = engine.log_segment(lp)
+    assert ver == 7 and [v for k, v, _, _ in files if k == 1] == [3]
+    assert [v for k, v, _, _ in files if k == 0] == [4, 5, 6, 7]
+    _same_as_oracle(engine, lp)
+
+
+def test_truncated_log(engine, tmp_path):
+    """No checkpoint and no version 0: logFileNotFoundException (D/SnapshotManagement.scala:160-163)."""
+    lp = str(tmp_path / "_delta_log")
+    for v in (1, 2, 3):
+        write_commit(lp, v, [add("x%d" % v)])
+    e = _error(engine, lp)
+    assert e.kind == "FileNotFoundException"
+    assert str(e) == ("%s/%020d.json: Unable to reconstruct state at version 3 as the transaction log has been "
+                      "truncated due to manual deletion or the log retention policy (delta.logRetentionDuration="
+                      "30 days) and checkpoint retention policy (delta.checkpointRetentionDuration=2 days)" % (lp, 0))
+    with pytest.raises(O.DeltaError) as oe:
+        O.get_log_segment(lp)
+    assert str(oe.value) == str(e)
+
+
+def test_noncontiguous_and_empty(engine, tmp_path):
+    lp = str(tmp_path / "_delta_log")
+    write_commit(lp, 0, [PROTOCOL, METADATA])
+    write_commit(lp, 2, [add("x")])
+    e = _error(engine, lp)  # T/DeltaLogSuite.scala:281-304
+    assert e.kind == "IllegalStateException" and str(e) == "Versions (Vector(0, 2)) are not contiguous."
+    empty = str(tmp_path / "empty" / "_delta_log")
+    os.makedirs(empty)
+    e = _error(engine, empty)
+    assert e.kind == "FileNotFoundException" and str(e) == "No file found in the directory: %s." % empty
+
+
+# ---- K1 device walker fuzz ---------------------------------------------------------------------------------
+def _device_lines(engine, lines):
+    body = b"".join(l + b"\n" for l in lines)
+    staged = engine.stage_files([(0, 0, 0, body)])
+    try:
+        return staged.parse_lines()
+    finally:
+        staged.release()
+
+
+def _device_view(rec):
+    from tests.test_json_lane import K_ADD, K_REMOVE
+    out = {"kind": rec["kind"]}
+    if rec["kind"] in (K_ADD, K_REMOVE):
+        raw = rec["path"]
+        path = None if raw is None else (json.loads(b'"' + raw + b'"') if rec["escaped"] else raw.decode("utf-8"))
+        out.update(path=path, size=rec["size"], delts=rec["deletionTimestamp"])
+    return out
+
+
+def test_device_walker_matches_fuzz_corpus(engine):
+    """Every corpus line (golden logs, synthetic formats, hand-written edge cases) at 16 byte
+    alignments, through k_json_lines / k_json_hard on the GPU, against the PERMISSIVE-reader
+    restatement that the host build of the walker is fuzzed against."""
+    from tests.test_json_lane import corpus, expected
+    base = [l for l in corpus() if b"\n" not in l]
+    lines = []
+    for align in range(16):  # a prefix line of `align` bytes shifts every following line
+        lines.append(b" " * align)
+        lines.extend(base)
+    got = _device_lines(engine, lines)
+    assert len(got) == len(lines)
+    for line, rec in zip(lines, got):
+        assert rec["line"] == line
+        assert _device_view(rec) == expected(line), line
+
+
+def test_device_walker_mutations(engine):
+    from tests.test_json_lane import K_ADD, K_ERROR, corpus, expected, mutate
+    rng = random.Random(0xDE17B)
+    base = corpus()
+    lines = []
+    while len(lines) < int(os.environ.get("JL_GPU_FUZZ", "60000")):
+        line = mutate(rng, rng.choice(base))
+        if b"\n" in line:
+            continue
+        try:
+            line.decode("utf-8")
+        except UnicodeDecodeError:
+            continue
+        lines.append(line)
+    got = _device_lines(engine, lines)
+    kinds = {}
+    for line, rec in zip(lines, got):
+        exp = expected(line)
+        assert _device_view(rec) == exp, line
+        kinds[exp["kind"]] = kinds.get(exp["kind"], 0) + 1
+    assert kinds.get(K_ERROR, 0) > len(lines) // 10 and kinds.get(K_ADD, 0) > len(lines) // 20, kinds
+
+
+def test_parse_commits_versions_and_golden_lines(engine):
+    """dr_parse_commits over the reference's golden commits: versions per line, and the file
+    actions equal Action.fromJson's (delta_amd/actions.py) path / size / deletionTimestamp."""
+    from delta_amd.actions import from_json
+    lp = os.path.join(REF, "delta-0.2.0", "_delta_log")
+    files = []
+    for v in range(4):
+        with open(os.path.join(lp, "%020d.json" % v), "rb") as f:
+            files.append((v, 0, 0, f.read()))
+    staged = engine.stage_files(files)
+    try:
+        recs = staged.parse_lines()
+    finally:
+        staged.release()
+    want = []
+    for v, _, _, data in files:
+        for line in data.decode().split("\n")[:-1] if data.endswith(b"\n") else data.decode().split("\n"):
+            want.append((v, from_json(line)))
+    assert [r["version"] for r in recs] == [v for v, _ in want]
+    for r, (_, a) in zip(recs, want):
+        kind = next(iter(a)) if a else None
+        assert r["kind"] == {None: 0, "add": 1, "remove": 2, "metaData": 3, "txn": 4, "protocol": 5,
+                             "cdc": 6, "commitInfo": 7}[kind]
+        if kind in ("add", "remove"):
+            assert r["path"].decode() == a[kind]["path"] and r["size"] == a[kind]["size"]
+            if kind == "remove":
+                assert r["deletionTimestamp"] == a[kind]["deletionTimestamp"]
+
+
+# ---- incremental apply and snapshot lifetime -------------------------------------------------------------
+def test_apply_with_earlier_cutoff_rebuilds(engine, tmp_path):
+    """a tail commit that lengthens delta.deletedFileRetentionDuration moves the cutoff
+    back; dr_state_apply refuses (DR_E_REBUILD) and DeltaLog.update(incremental=True) rebuilds, so
+    the tombstones the base had dropped come back as the reference's full replay has them."""
+    from delta_amd.delta_log import DeltaError, DeltaLog, ManualClock
+    root = tmp_path / "t"
+    lp = str(root / "_delta_log")
+    write_commit(lp, 0, [PROTOCOL, METADATA] + [add("f%d" % i) for i in range(6)])
+    write_commit(lp, 1, [remove("f%d" % i, ts=1000 + i * 1000) for i in range(6)])
+    week = 7 * 86400000
+    DeltaLog.clear_cache()
+    log = DeltaLog.for_table(str(root), clock=ManualClock(week + 3500))  # cutoff 3500: 3 tombstones
+    assert log.snapshot.num_of_removes == 3
+    base = log.snapshot.state
+    tail = engine.stage_files([(2, 0, 0, b'{"add":{"path":"z","size":1,"modificationTime":1,"dataChange":true}}\n')])
+    try:
+        with pytest.raises(DeltaError) as ei:
+            base.apply(tail, 1500)
+        assert ei.value.code == "DR_E_REBUILD"
+    finally:
+        tail.release()
+    md = json.loads(json.dumps(METADATA))
+    md["metaData"]["configuration"] = {"delta.deletedFileRetentionDuration": "interval 2 weeks"}
+    write_commit(lp, 2, [md])
+    # update() computes the new snapshot's cutoff from the current snapshot's metadata
+    # (D/DeltaLog.scala:109-120, D/SnapshotManagement.scala:302): v2 still uses one week
+    snap2 = log.update(incremental=True)
+    assert snap2.version == 2 and snap2.min_file_retention_timestamp == 3500 and snap2.num_of_removes == 3
+    write_commit(lp, 3, [add("z")])
+    snap3 = log.update(incremental=True)  # two weeks now: the cutoff moves back -> rebuild
+    assert snap3.version == 3 and snap3.min_file_retention_timestamp == week + 3500 - 2 * week
+    ref = O.state_reconstruction(O.get_log_segment(lp), snap3.min_file_retention_timestamp)
+    _assert_same(snap3.state, ref)
+    assert snap3.num_of_removes == 6
+    # the replaced snapshot stays usable (the reference only uncaches it)
+    assert sorted(f["path"] for f in snap2.tombstones) == ["f3", "f4", "f5"]
+    DeltaLog.clear_cache()
+
+
+def test_incremental_update_falls_back_on_gap_or_newer_checkpoint(engine, tmp_path):
+    """commits cleaned up behind a newer checkpoint -> DeltaLog.update(incremental=True)
+    rebuilds from the new segment instead of failing on the gap."""
+    from delta_amd.delta_log import DeltaLog, ManualClock
+    root = tmp_path / "t"
+    lp = _checkpointed_table(root, parts=None, last=False)
+    hold = {}
+    for v in range(4, 8):
+        fn = os.path.join(lp, "%020d.json" % v)
+        hold[v] = open(fn, "rb").read()
+        os.remove(fn)
+    os.rename(os.path.join(lp, "%020d.checkpoint.parquet" % 6), str(root / "ck6"))
+    DeltaLog.clear_cache()
+    log = DeltaLog.for_table(str(root), clock=ManualClock(0))
+    assert log.snapshot.version == 3
+    # v4, v5 were cleaned up after the checkpoint at v6
+    for v in (6, 7):
+        with open(os.path.join(lp, "%020d.json" % v), "wb") as f:
+            f.write(hold[v])
+    os.rename(str(root / "ck6"), os.path.join(lp, "%020d.checkpoint.parquet" % 6))
+    snap = log.update(incremental=True)
+    assert snap.version == 7
+    _assert_same(snap.state, O.state_reconstruction(O.get_log_segment(lp), snap.min_file_retention_timestamp))
+    DeltaLog.clear_cache()

@@ -6,14 +6,22 @@ resident in HBM: JSON tokenization (K1), checkpoint page inflate + decode (K2), 
 partition (K3), per-bucket last-writer-wins + retention + compaction + computedState counters
 (K4/K6). `value` = log actions replayed per second over all ranks.
 
+Every kernel of the timed steps is bracketed by a HIP event pair on its stream (dr_set_timing;
+all kernels run on one stream, so they add up to the step): `kernels` holds each kernel's average
+launch time, and `roofline` names the longest kernel of the step, with its algorithmic bytes
+ over that time against the 8 TB/s HBM peak and, when committed rocprofv3 PMC passes
+of this command exist (--pmc-dir), its measured HBM traffic. `pipelines` aggregates K1 (JSON),
+SNAPPY and K3+K4 (sort + reduce, against SURVEY.md §8d's 69 B/action budget).
+
 Multi-GPU (torchrun, one rank per GPU): the same table is path-hash sharded over the ranks
 (delta_amd/sharded.py): each rank stages a contiguous slice of the segment, parses
 it, sends each file action to owner(path) with an RCCL all-to-all, reduces its shard and returns
 the verdicts. Strong scaling: `value` = table actions per step / max-over-ranks step time.
 
-cpu_baseline: the C++ restatement of the reference replay (oracle/replay_oracle.cpp, 50 hash
-partitions x unordered_map last-writer-wins, all host threads) timed on a bounded sample of the
-same workload on rank 0 at N=1.
+cpu_baseline: the C++ restatement of the reference replay (oracle/replay_oracle.cpp: 50 hash
+partitions, per-partition last-writer-wins table, sort by path) on the SAME full table, on rank 0
+at N=1, with all the box's cores (16) and with one; its counters and order-free key sums must equal
+the GPU's (full-scale parity, `matches_gpu`).
 """
 import argparse
 import json
@@ -27,20 +35,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-
-# Stages whose timed region is exactly one kernel launch: the roofline is reported for the slowest
-# of these (achieved = its algorithmic bytes / its hipEvent-timed duration on the replay stream).
-STAGE_KERNEL = {
-    "json_parse": "k_json_lines",
-    "json_newlines": "k_json_place",
-    "ckpt_assemble": "k_ckpt_assemble",
-    "partition_hist": "k_bucket_hist",
-    "partition_scatter": "k_bucket_scatter",
-    "reduce": "k_bucket_reduce",
-}
-
-SORT_REDUCE_STAGES = ("partition_setup", "partition_hist", "partition_scan", "partition_scatter", "reduce",
-                      "reduce_verify", "reduce64", "compact")
+SORT_REDUCE = ("k_bucket_hist", "k_bucket_offsets", "k_bucket_scatter", "k_bucket_reduce", "k_bucket_verify",
+               "k_bucket_reduce64", "k_bucket_exact", "k_sum_stats", "k_survivor_scan", "k_compact2")
+SNAPPY = ("k_snap_spec", "k_snap_assume", "k_snap_entries", "k_snap_regions", "k_snap_resolve", "k_snap_count",
+          "k_snap_scan", "k_snap_emit", "k_snap_exec", "k_snap_serial")
+JSON = ("k_json_index", "k_json_place", "k_json_lines", "k_json_hard")
 
 
 def log(*a):
@@ -64,25 +63,35 @@ def build_table(path, config, scale, seed):
     return d
 
 
-def algorithmic_bytes(stage, plan, counts):
-    """Compulsory HBM bytes per launch of each stage's kernel."""
-    n_lines = counts["num_actions"] - plan["checkpoint_rows"]
+def algorithmic_bytes(kernel, plan, counts):
+    """Compulsory HBM bytes of one launch of `kernel`: each input it needs read once,
+    each output written once."""
     rows = plan["checkpoint_rows"]
+    lines = counts["num_actions"] - rows
+    n = counts["num_actions"]
     fa = counts["num_file_actions"]
     surv = counts["num_files"] + counts["num_removes"]
-    return {
-        "json_index": plan["json_bytes"] + 2 * n_lines,
-        "json_newlines": 10 * n_lines,
-        "json_parse": plan["json_bytes"] + 8 * n_lines + 50 * n_lines,
-        "pq_inflate": plan["pages_compressed_bytes"] + plan["pages_decompressed_bytes"],
-        "pq_bounds": plan["pages_decompressed_bytes"],
-        "pq_decode": plan["pages_decompressed_bytes"] + 44 * rows,
-        "ckpt_assemble": 44 * rows + 88 * rows + 50 * rows,
-        "partition_hist": 30 * (rows + n_lines),
-        "partition_scatter": 22 * (rows + n_lines) + 32 * fa,
-        "reduce": 16 * fa + 4 * surv,
-        "compact": 8 * surv,
-    }.get(stage)
+    ch, el = plan["snappy_chunks"], plan["snappy_elements"]
+    sin, sout = plan["snappy_in_bytes"], plan["snappy_out_bytes"]
+    table = {
+        "k_json_index": plan["json_bytes"] + 2 * lines,            # bytes in, u16 slot per line
+        "k_json_place": 10 * lines,                                # slot in, u64 position out
+        "k_json_lines": plan["json_bytes"] + 8 * lines + 50 * lines,  # line bytes + position in, 50 B record out
+        "k_page_copy": 2 * plan["copy_bytes"],
+        "k_snap_spec": sin + 60 * ch,                              # compressed bytes in, per-chunk state out
+        "k_snap_assume": 16 * ch, "k_snap_entries": 16 * ch, "k_snap_count": 8 * ch, "k_snap_scan": 8 * ch,
+        "k_snap_emit": sin + 24 * ch + 8 * el,                     # compressed in, 8 B record per element out
+        "k_snap_exec": 8 * el + sin + sout,                        # records + literal bytes in, page bytes out
+        "k_pq_data": plan["pages_decompressed_bytes"] + 44 * rows,
+        "k_ckpt_assemble": 182 * rows,
+        "k_bucket_hist": 30 * n,                                   # kind, flags, key, path ref in; packed ref out
+        "k_bucket_scatter": 18 * n + 16 * fa,                      # kind, flags, key, size/delTs in; 16 B record out
+        "k_bucket_reduce": 16 * fa + 4 * surv,
+        "k_compact2": 8 * surv,
+    }
+    if kernel in ("k_snap_emit", "k_snap_exec") and not el:
+        return None
+    return table.get(kernel)
 
 
 def pmc_traffic(pmc_dir, kernel):
@@ -98,7 +107,7 @@ def pmc_traffic(pmc_dir, kernel):
         with open(fn) as f:
             for row in csv.DictReader(f):
                 name = row.get("Kernel_Name", "")
-                if kernel not in name:
+                if kernel + "(" not in name and not name.endswith(kernel):
                     continue
                 c = row.get("Counter_Name")
                 v = float(row.get("Counter_Value", 0) or 0)
@@ -108,49 +117,56 @@ def pmc_traffic(pmc_dir, kernel):
     if "FETCH_SIZE" not in per or "WRITE_SIZE" not in per:
         return None
     avg = {c: sum(v.values()) / len(v) for c, v in per.items()}
-    # FETCH_SIZE / WRITE_SIZE are in KiB
-    return int(2 * avg["FETCH_SIZE"] * 1024 + avg["WRITE_SIZE"] * 1024)
+    return int(2 * avg["FETCH_SIZE"] * 1024 + avg["WRITE_SIZE"] * 1024)  # KiB -> bytes
 
 
-def cpu_baseline(config, sample_scale, seed, tmp):
-    """Times oracle/_build/replay_oracle on a bounded sample of the same workload."""
+def run_replay_oracle(log_path, cutoff, threads):
     exe = os.path.join(ROOT, "oracle", "_build", "replay_oracle")
-    if not os.path.exists(exe):
-        return None
-    path = os.path.join(tmp, "cpu_sample_c%d_%g" % (config, sample_scale))
-    exp = build_table(path, config, sample_scale, seed)
-    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    threads = min(threads, 16)  # the GPU box's CPU share per GPU
-    r = subprocess.run([exe, os.path.join(path, "_delta_log"), str(exp["min_file_retention_timestamp"]),
-                        "--threads", str(threads), "--partitions", "50"],
-                       capture_output=True, text=True, timeout=600)
+    r = subprocess.run([exe, log_path, str(cutoff), "--threads", str(threads), "--partitions", "50"],
+                       capture_output=True, text=True, timeout=900)
     if r.returncode != 0:
         log("cpu baseline failed:", r.stderr[-2000:])
         return None
-    res = json.loads(r.stdout.strip().splitlines()[-1])
-    ok = (res["num_files"] == exp["num_files"] and res["num_removes"] == exp["num_removes"]
-          and res["size_in_bytes"] == exp["size_in_bytes"])
-    if not ok:
-        log("cpu baseline result mismatch", res, exp)
-    return {"value": res["num_actions"] / res["total_s"], "unit": "actions/s", "cores": threads,
-            "kind": "port",
-            "sample": "config %d at scale %g (%d actions: %d checkpoint rows + JSON commits), parse %.2fs + "
-                      "replay %.2fs; C++ restatement of InMemoryLogReplay over 50 hash partitions"
-                      % (config, sample_scale, res["num_actions"], res["checkpoint_rows"], res["parse_s"],
-                         res["replay_s"]),
-            "matches_expected": ok}
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def cpu_baseline(log_path, cutoff, counts, threads, one_core=True):
+    """oracle/_build/replay_oracle on the same table: all host threads given, then one."""
+    if not os.path.exists(os.path.join(ROOT, "oracle", "_build", "replay_oracle")):
+        return None
+    res = run_replay_oracle(log_path, cutoff, threads)
+    if res is None:
+        return None
+    keys = ("num_files", "size_in_bytes", "num_removes", "num_file_actions", "live_key_sum", "tomb_key_sum")
+    mism = {k: (res[k], counts[k]) for k in keys if res[k] != counts[k]}
+    if mism:
+        log("FULL-SCALE PARITY MISMATCH (cpu, gpu):", mism)
+    out = {"value": round(res["num_actions"] / res["total_s"], 1), "unit": "actions/s", "cores": threads,
+           "kind": "port", "parse_s": res["parse_s"], "replay_s": res["replay_s"], "read_s": res["read_s"],
+           "sample": "the full benchmark table (%d actions: %d checkpoint rows + JSON lines), bytes in memory "
+                     "before the clock; C++ restatement of the replay: Parquet+SNAPPY and JSON decode, "
+                     "canonicalize, 50 hash partitions, per-partition last-writer-wins, retention, sort by path"
+                     % (res["num_actions"], res["checkpoint_rows"]),
+           "matches_gpu": not mism}
+    if one_core:
+        r1 = run_replay_oracle(log_path, cutoff, 1)
+        if r1:
+            out["one_core"] = {"value": round(r1["num_actions"] / r1["total_s"], 1), "parse_s": r1["parse_s"],
+                               "replay_s": r1["replay_s"]}
+    return out
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=3)
     ap.add_argument("--scale", type=float, default=1.0)
-    ap.add_argument("--cpu-sample-scale", type=float, default=0.25)
-    ap.add_argument("--pmc-dir", default=os.path.join(ROOT, "profiles", "r01", "pmc"))
+    ap.add_argument("--cpu-threads", type=int, default=16, help="the GPU box's CPU share per GPU")
+    ap.add_argument("--pmc-dir", default=os.path.join(ROOT, "profiles", "r02", "pmc"))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-timing", action="store_true", help="time the steps without per-kernel events")
     ap.add_argument("--workdir", default=os.environ.get("DR_BENCH_DIR", os.path.join(tempfile.gettempdir(), "dr_bench")))
     args = ap.parse_args()
 
@@ -159,6 +175,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    backend = None
     if world > 1:
         import torch.distributed as dist
         # DR_BENCH_BACKEND=gloo rehearses the multi-rank path on a single GPU (host-staged exchange)
@@ -182,8 +199,10 @@ def main():
     eng = Engine.get(local)
     log_path = os.path.join(table, "_delta_log")
     cutoff = exp["min_file_retention_timestamp"]
+    t_stage = time.perf_counter()
     if world == 1:
         staged = eng.stage_log(log_path)
+        stage_s = time.perf_counter() - t_stage
 
         def step():
             st = staged.replay(cutoff)
@@ -191,10 +210,9 @@ def main():
             st.release()
             return c, c
     else:
-        # the table is path-hash sharded over the ranks: each rank stages its
-        # contiguous slice of the segment; one step = parse + RCCL all-to-all + reduce + verdicts
         from delta_amd.sharded import Exchange, replay_sharded, stage_shard
         staged = stage_shard(eng, log_path, world, rank)
+        stage_s = time.perf_counter() - t_stage
         ex = Exchange()
 
         def step():
@@ -202,14 +220,17 @@ def main():
             c, lc = st.counts, st.local.counts
             st.release()
             return c, lc
-    plan = staged.plan()  # this rank's slice (roofline accounting is per rank 0's kernels)
     counts = local_counts = None
+    eng.set_timing(True)  # the first warm-up counts the SNAPPY elements for the roofline accounting
     for i in range(max(args.warmup, 1)):
         counts, local_counts = step()
+        if i == 0:
+            eng.set_timing(False)
     for k in ("num_files", "num_removes", "size_in_bytes", "num_actions", "num_file_actions"):
         assert counts[k] == exp[k], (k, counts[k], exp[k])
-    eng.set_timing(True)
-    stage_ms = {}
+    plan = staged.plan()  # this rank's slice (roofline accounting is per rank 0's kernels)
+    eng.set_timing(not args.no_timing)
+    kern_ms, kern_n = {}, {}
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -217,52 +238,76 @@ def main():
     for _ in range(args.steps):
         step()
         for k, v in eng.last_timings().items():
-            stage_ms[k] = stage_ms.get(k, 0.0) + v
+            base = k.split("#")[0]
+            kern_ms[base] = kern_ms.get(base, 0.0) + v
+            kern_n[base] = kern_n.get(base, 0) + 1
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64,
-                         device="cuda" if dist.get_backend() == "nccl" else "cpu")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     eng.set_timing(False)
-    stage_ms = {k: v / args.steps for k, v in stage_ms.items()}
     total_actions = counts["num_actions"] * args.steps  # table-wide actions per step
     value = total_actions / elapsed
     ms_per_step = elapsed / args.steps * 1000.0
     if rank != 0:
         return
-    dom = max((k for k in stage_ms if k in STAGE_KERNEL), key=stage_ms.get)
     kernels = {}
-    for k, ms in stage_ms.items():
-        b = algorithmic_bytes(k, plan, local_counts)
-        kernels[k] = {"ms": round(ms, 4)}
+    for k, ms in kern_ms.items():
+        if k in ("start", "end"):
+            continue
+        per_step = ms / args.steps
+        calls = kern_n[k] / args.steps
+        e = {"ms": round(per_step, 4), "launches": calls}
+        b = algorithmic_bytes(k, plan, local_counts) if calls == 1 else None
         if b:
-            kernels[k]["algo_bytes"] = b
-            kernels[k]["gbs"] = round(b / (ms * 1e-3) / 1e9, 1)
-    db = algorithmic_bytes(dom, plan, local_counts) or 0
-    achieved = db / (stage_ms[dom] * 1e-3) / 1e9 if db else None
-    roofline = {"bound": "hbm", "kernel": STAGE_KERNEL[dom], "stage": dom,
-                "achieved": round(achieved, 1) if achieved else None,
-                "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                # committed PMC passes are of the default single-GPU command
-                "traffic": pmc_traffic(args.pmc_dir, STAGE_KERNEL[dom]) if world == 1 else None,
-                "algo_bytes": db, "avg_launch_ms": round(stage_ms[dom], 4)}
-    # K3 + K4 together against SURVEY.md §8(d)'s headline budget: 32 B/action (sort) + 37 B/action
-    # (reduce, retention, compaction) = 69 B/action, over every stage between parse and export.
-    sr = [k for k in SORT_REDUCE_STAGES if k in stage_ms]
-    sr_ms = sum(stage_ms[k] for k in sr)
-    sr_bytes = 69 * local_counts["num_actions"]
-    sr_gbs = sr_bytes / (sr_ms * 1e-3) / 1e9 if sr_ms else None
-    sort_reduce = {"stages": sr, "ms": round(sr_ms, 4), "algo_bytes": sr_bytes,
-                   "achieved": round(sr_gbs, 1) if sr_gbs else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                   "frac": round(sr_gbs / HBM_PEAK_GBS, 4) if sr_gbs else None, "target_frac": 0.5}
+            e["algo_bytes"] = b
+            e["gbs"] = round(b / (per_step * 1e-3) / 1e9, 1)
+        kernels[k] = e
+    roofline = None
+    if kernels:
+        dom = max(kernels, key=lambda k: kernels[k]["ms"])
+        e = kernels[dom]
+        achieved = e.get("gbs")
+        roofline = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                    # committed PMC passes are of the default single-GPU command
+                    "traffic": pmc_traffic(args.pmc_dir, dom) if world == 1 else None,
+                    "algo_bytes": e.get("algo_bytes"), "avg_launch_ms": e["ms"],
+                    "kernels_sum_ms": round(sum(x["ms"] for x in kernels.values()), 3)}
+
+    def pipeline(names, algo):
+        ms = sum(kernels[k]["ms"] for k in names if k in kernels)
+        gbs = algo / (ms * 1e-3) / 1e9 if ms else None
+        return {"kernels": [k for k in names if k in kernels], "ms": round(ms, 4), "algo_bytes": algo,
+                "achieved": round(gbs, 1) if gbs else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(gbs / HBM_PEAK_GBS, 4) if gbs else None}
+
+    lines = local_counts["num_actions"] - plan["checkpoint_rows"]
+    pipelines = {
+        "json": pipeline(JSON, plan["json_bytes"] + 58 * lines),
+        # compulsory SNAPPY traffic: compressed pages in, decompressed pages out
+        "snappy": pipeline(SNAPPY, plan["snappy_in_bytes"] + plan["snappy_out_bytes"]),
+        # K3 + K4 together against SURVEY.md §8(d)'s headline budget: 32 B/action (sort) + 37 B/action
+        # (reduce, retention, compaction) = 69 B/action
+        "sort_reduce": dict(pipeline(SORT_REDUCE, 69 * local_counts["num_actions"]), target_frac=0.5),
+    }
     cpu = None
     if not args.no_cpu_baseline and world == 1:
-        cpu = cpu_baseline(args.config, args.cpu_sample_scale, S.BASE_SEED + args.config, args.workdir)
+        cpu = cpu_baseline(log_path, cutoff, counts, args.cpu_threads)
+    # end to end once: file bytes -> HBM (read + H2D + page planning), replay, allFiles export
+    e2e = None
+    if world == 1:
+        t1 = time.perf_counter()
+        st = staged.replay(cutoff)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        st.release()
+        e2e = {"stage_s": round(stage_s, 3), "replay_s": round(t2 - t1, 4),
+               "actions_per_s_incl_staging": round(counts["num_actions"] / (stage_s + t2 - t1), 1)}
     out = {
         "metric": "log actions replayed/sec + achieved HBM GB/s, 1/2/4/8 GPU, 10M-file table",
         "value": round(value, 1), "unit": "actions/s", "n_gpus": world, "steps": args.steps,
@@ -273,13 +318,16 @@ def main():
                                                                              counts["num_files"]),
                    "scale": args.scale, "actions": counts["num_actions"],
                    "json_bytes": exp["json_bytes"], "checkpoint_bytes": exp["checkpoint_bytes"],
-                   "parallelism": ("path-hash shards over %d GPUs (RCCL all-to-all)" % world) if world > 1
+                   "parallelism": ("path-hash shards over %d GPUs (%s all-to-all)"
+                                   % (world, "RCCL" if backend == "nccl" else "gloo rehearsal")) if world > 1
                    else "single GPU"},
         "roofline": roofline,
-        "sort_reduce": sort_reduce,
+        "pipelines": pipelines,
         "cpu_baseline": cpu,
+        "end_to_end": e2e,
         "kernels": kernels,
-        "result": {k: counts[k] for k in ("num_files", "num_removes", "size_in_bytes")},
+        "result": {k: counts[k] for k in ("num_files", "num_removes", "size_in_bytes", "live_key_sum",
+                                          "tomb_key_sum")},
     }
     print(json.dumps(out), flush=True)
 

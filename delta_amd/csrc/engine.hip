@@ -43,12 +43,18 @@ struct dr_ctx {
   hipStream_t stream2 = nullptr;  // K1 line parsing, overlapped with the checkpoint decode
   std::string err;
   bool timing = false;
+  bool overlap = false;  // DR_OVERLAP=1: K1 line parsing on stream2, beside the checkpoint decode
   struct Mark {
     std::string name;
     hipEvent_t ev;
     int s;  // 0: stream, 1: stream2
   };
   std::vector<Mark> marks;
+  struct KMark {  // one kernel launch, bracketed by an event pair on its stream
+    std::string name;
+    hipEvent_t a, b;
+  };
+  std::vector<KMark> kmarks;
   std::vector<std::pair<std::string, float>> timings;
   std::multimap<size_t, void*> free_blocks;
   std::unordered_map<void*, size_t> sizes;
@@ -101,9 +107,37 @@ struct dr_ctx {
     HIP_OK(hipEventRecord(e, on ? stream2 : stream));
     marks.push_back(Mark{name, e, on});
   }
+  // The launch hook (kernels.h): an event before and after every kernel of the call.
+  static void on_launch(void* user, const char* kernel, hipStream_t st, int end) {
+    dr_ctx* c = static_cast<dr_ctx*>(user);
+    if (!end) {
+      KMark k{kernel_name(kernel), nullptr, nullptr};
+      HIP_OK(hipEventCreate(&k.a));
+      HIP_OK(hipEventCreate(&k.b));
+      HIP_OK(hipEventRecord(k.a, st));
+      c->kmarks.push_back(k);
+    } else if (!c->kmarks.empty()) {
+      HIP_OK(hipEventRecord(c->kmarks.back().b, st));
+    }
+  }
+  // "(dev::k_gather<uint64_t, uint32_t>)" -> "k_gather"
+  static std::string kernel_name(const char* k) {
+    std::string n(k);
+    size_t a = n.rfind("::");
+    if (a != std::string::npos) n = n.substr(a + 2);
+    size_t b = n.find_first_of("<)");
+    if (b != std::string::npos) n = n.substr(0, b);
+    while (!n.empty() && n[0] == '(') n = n.substr(1);
+    return n;
+  }
+  void begin_call() {
+    if (timing) set_launch_hook(&dr_ctx::on_launch, this);
+  }
+  // Stage intervals, then one entry per kernel launch ("name", or "name#k" for its k-th launch
+  // in the call, k >= 2).
   void collect_timings() {
+    set_launch_hook(nullptr, nullptr);
     timings.clear();
-    if (marks.empty()) return;
     for (auto& m : marks) HIP_OK(hipEventSynchronize(m.ev));
     for (size_t i = 1; i < marks.size(); ++i) {
       size_t k = i;
@@ -115,6 +149,27 @@ struct dr_ctx {
     }
     for (auto& m : marks) (void)hipEventDestroy(m.ev);
     marks.clear();
+    std::map<std::string, int> seen;
+    for (auto& k : kmarks) {
+      HIP_OK(hipEventSynchronize(k.b));
+      float ms = 0;
+      HIP_OK(hipEventElapsedTime(&ms, k.a, k.b));
+      const int n = ++seen[k.name];
+      timings.emplace_back(n == 1 ? k.name : k.name + "#" + std::to_string(n), ms);
+      (void)hipEventDestroy(k.a);
+      (void)hipEventDestroy(k.b);
+    }
+    kmarks.clear();
+  }
+  void drop_timings() {
+    set_launch_hook(nullptr, nullptr);
+    for (auto& m : marks) (void)hipEventDestroy(m.ev);
+    marks.clear();
+    for (auto& k : kmarks) {
+      (void)hipEventDestroy(k.a);
+      (void)hipEventDestroy(k.b);
+    }
+    kmarks.clear();
   }
 };
 
@@ -215,7 +270,8 @@ struct PagePlan {
   DBuf<unsigned long long> s_region_count;
   std::vector<uint32_t> wg_chunk0;
   DBuf<uint32_t> d_wg_chunk0;
-  uint64_t snap_in_bytes = 0;
+  uint64_t snap_in_bytes = 0, snap_out_bytes = 0, copy_bytes = 0;
+  uint64_t snap_elements = 0;  // SNAPPY elements of the pages (known after a timed replay)
   // PLAIN BYTE_ARRAY boundary scratch (k_ba_bounds)
   uint32_t ba_pages = 0;
   uint64_t ba_vals = 0;
@@ -529,9 +585,11 @@ static void plan_pages(StagedData& s, PagePlan& P) {
   for (const PageDesc& d : P.pages) {
     const uint64_t lv = d.kind == PG_DATA_V2 ? uint64_t(d.v2_def_len + d.v2_rep_len) : 0;
     if (lv) P.copy_jobs.push_back(CopyJob{d.src, d.dst, lv});
+    P.copy_bytes += lv;
     const bool compressed = d.codec == 1 && !(d.kind == PG_DATA_V2 && !d.v2_compressed);
     if (!compressed) {
       P.copy_jobs.push_back(CopyJob{d.src + lv, d.dst + lv, d.usize - lv});
+      P.copy_bytes += d.usize - lv;
       continue;
     }
     const uint8_t* h = s.h_pq.data() + d.src + lv;
@@ -550,6 +608,7 @@ static void plan_pages(StagedData& s, PagePlan& P) {
     for (uint32_t j = 0; j < ncp; j += snappy_wg_chunks()) P.wg_chunk0.push_back(P.nchunks + j);
     P.nchunks += ncp;
     P.snap_in_bytes += sp.n_in;
+    P.snap_out_bytes += sp.n_out;
     const uint32_t nb = (sp.n_out + 65535) / 65536;
     for (uint32_t k = 0; k < nb; ++k) P.block_page.push_back(uint32_t(P.snap_pages.size()));
     P.snap_pages.push_back(sp);
@@ -642,6 +701,7 @@ static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_
       sa.stamps = stamps.p;
     }
     launch_snappy(sa, stream, scratch);
+    if (ctx->timing && !P.snap_elements) P.snap_elements = d2h_one(P.s_rec_start.p + P.nchunks, stream);
     if (dbg) {
       std::vector<uint64_t> st = d2h(stamps.p, P.block_page.size() * 8, stream);
       double acc[8] = {0};
@@ -663,7 +723,6 @@ static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_
       std::fprintf(stderr, "snappy: pages %zu serially resolved regions %zu bad %zu\n", P.snap_pages.size(), nr, nb);
     }
   }
-  ctx->mark("pq_inflate");
   if (P.ba_pages) {
     launch_ba_bounds(pa, stream, scratch);
     if (std::getenv("DR_BA_DEBUG")) {
@@ -673,10 +732,8 @@ static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_
       std::fprintf(stderr, "ba bounds: %zu of %u pages validated\n", n, P.ba_pages);
     }
   }
-  ctx->mark("pq_bounds");
   launch_pq_dict(pa, stream);
   launch_pq_data(pa, stream);
-  ctx->mark("pq_decode");
 }
 
 static void plan_checkpoint(StagedData& s) {
@@ -836,10 +893,10 @@ static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
   ActionArrays act{st->kind.p, st->flags.p, st->key.p, st->path_ptr.p, st->path_len.p, st->size.p, st->delts.p,
                    st->src_off.p, st->src_len.p};
   DBuf<uint64_t> hard(ctx, nlines);
-  ctx->mark("json_index");
-  // K1 line parsing runs on stream2, overlapped with the checkpoint decode below (the SNAPPY
-  // resolve/count phases leave most CUs idle); stream waits for it before anything reads the
-  // action arrays. The guard joins stream2 before any buffer it uses can be released.
+  // With DR_OVERLAP=1, K1's line parsing runs on stream2 beside the checkpoint decode below
+  // (measured r01: ~1 % of the step, both pipelines are issue-bound); stream waits for it before
+  // anything reads the action arrays. The guard joins stream2 before any buffer it uses can be
+  // released. By default every kernel runs on one stream, so per-kernel times add up to the step.
   struct Overlap {
     dr_ctx* c;
     hipEvent_t fork = nullptr, done = nullptr;
@@ -850,23 +907,23 @@ static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
     }
   } ov{ctx};
   if (nlines) {
-    hipStream_t s2 = ctx->stream2;
-    HIP_OK(hipEventCreateWithFlags(&ov.fork, hipEventDisableTiming));
-    HIP_OK(hipEventRecord(ov.fork, stream));
-    HIP_OK(hipStreamWaitEvent(s2, ov.fork, 0));
-    ctx->mark("json_fork", 1);
+    hipStream_t s2 = ctx->overlap ? ctx->stream2 : stream;
+    if (ctx->overlap) {
+      HIP_OK(hipEventCreateWithFlags(&ov.fork, hipEventDisableTiming));
+      HIP_OK(hipEventRecord(ov.fork, stream));
+      HIP_OK(hipStreamWaitEvent(s2, ov.fork, 0));
+    }
     launch_json_place(s.d_json.p, json_len, jcounts.p, joff.p, jslots.p, nl.p, s2);
-    ctx->mark("json_newlines", 1);
     JsonParseArgs ja{s.d_json.p, nl.p, nlines, R, act.kind, act.flags, act.key, act.path_ptr, act.path_len,
                      act.size, act.delts, act.src_off, act.src_len, counters.p + 0, counters.p + 1, counters.p + 2,
                      nonfile.p, nlines, counters.p + 3, hard.p,
                      reinterpret_cast<unsigned long long*>(counters.p + 5)};
     launch_json_parse(ja, s2);
-    ctx->mark("json_parse", 1);
     launch_json_hard(ja, s2);
-    ctx->mark("json_hard", 1);
-    HIP_OK(hipEventCreateWithFlags(&ov.done, hipEventDisableTiming));
-    HIP_OK(hipEventRecord(ov.done, s2));
+    if (ctx->overlap) {
+      HIP_OK(hipEventCreateWithFlags(&ov.done, hipEventDisableTiming));
+      HIP_OK(hipEventRecord(ov.done, s2));
+    }
   }
   // ---- K2: checkpoint ----
   DBuf<uint8_t> cdefs;  // the hot columns' definition levels, R bytes each, zeroed in one fill
@@ -910,11 +967,9 @@ static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
     ca.special_count = counters.p + 0;
     ca.special_bytes = counters.p + 1;
     launch_ckpt_assemble(ca, stream);
-    ctx->mark("ckpt_assemble");
   }
   if (ov.done) {
     HIP_OK(hipStreamWaitEvent(stream, ov.done, 0));
-    ctx->mark("json_join");
   }
   // the checkpoint decoder's error code rides in counters[7]: one read-back for both
   if (R) HIP_OK(hipMemcpyAsync(counters.p + 7, pq_err.p, sizeof(uint32_t), hipMemcpyDeviceToDevice, stream));
@@ -927,7 +982,6 @@ static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
     st->arenas.push_back(std::make_shared<DBuf<uint8_t>>(ctx, cap));
     CanonArgs cg{act, N, st->arenas.back()->p, cap, counters.p + 4};
     launch_canon(cg, stream);
-    ctx->mark("canon");
   }
   // ---- non-file actions (host): checkpoint rows first, then JSON lines in order ----
   nf = s.ck_nonfile;
@@ -988,14 +1042,10 @@ static void reduce_actions(dr_ctx* ctx, dr_state* st, int64_t cutoff, uint32_t f
                    tcnt.p, toff.p, nullptr, st->path_ptr.p, st->path_len.p, pref.p};
   DBuf<PartRec> rec(ctx, N);
   pa.rec = rec.p;
-  ctx->mark("partition_setup");
   launch_bucket_hist(pa, stream);
-  ctx->mark("partition_hist");
   launch_scan_u32(tcnt.p, toff.p, ncell, pscratch.p, stream);
   launch_bucket_offsets(toff.p, nb, nt, boff.p, stream);
-  ctx->mark("partition_scan");
   launch_bucket_scatter(pa, stream);
-  ctx->mark("partition_scatter");
   // ---- K4: per-bucket last-writer-wins ----
   DBuf<uint32_t> olive(ctx, N), otomb(ctx, N), lcount(ctx, nb), tcount(ctx, nb), pcount(ctx, nb), rlist(ctx, nb),
       xlist(ctx, nb);
@@ -1021,13 +1071,10 @@ static void reduce_actions(dr_ctx* ctx, dr_state* st, int64_t cutoff, uint32_t f
     }
   } else {
     launch_bucket_reduce(ra, stream);
-    ctx->mark("reduce");
     launch_bucket_verify(ra, stream);
-    ctx->mark("reduce_verify");
     // the fallbacks read their bucket lists' lengths on the device (no host round trip)
     launch_bucket_reduce64(ra, rlist.p, nb, stream, totals.p + 3);
     launch_bucket_exact(ra, xlist.p, nb, stream, totals.p + 4);
-    ctx->mark("reduce64");
     if (std::getenv("DR_REDUCE_DEBUG")) {
       const std::vector<unsigned long long> t = d2h(totals.p, 8, stream);
       std::vector<uint64_t> bo = d2h(boff.p, nb + 1, stream);
@@ -1051,7 +1098,6 @@ static void reduce_actions(dr_ctx* ctx, dr_state* st, int64_t cutoff, uint32_t f
   const uint64_t n_file_actions = tot[7];
   st->n_live = tot[0];
   st->n_tomb = tot[2];
-  ctx->mark("compact");
   st->counts.num_files = int64_t(tot[0]);
   st->counts.size_in_bytes = int64_t(tot[1]);
   st->counts.num_removes = int64_t(tot[2]);
@@ -1488,6 +1534,7 @@ static DBuf<T> upload(dr_ctx* ctx, const T* src, size_t n) {
 static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred) {
   check_program(pred);
   dr_ctx* ctx = st.ctx;
+  ctx->begin_call();
   hipStream_t stream = ctx->stream;
   if (st.sources.empty()) fail(DR_E_INVALID_ARG, "state has no staged segment");
   StagedData& s = *st.sources[0];
@@ -1758,7 +1805,6 @@ static void shard_begin(dr_shard& sh, uint64_t* send_counts, uint64_t* send_byte
   launch_gather_u32(st.path_len.p, sh.send_idx.p, sh.nsend, sh.send_plen.p, stream);
   DBuf<uint8_t> scratch2(ctx, scan_scratch_for(sh.nsend));
   launch_scan_u32(sh.send_plen.p, sh.send_poff.p, sh.nsend, scratch2.p, stream);
-  ctx->mark("shard_partition");
   for (uint32_t d = 0; d < sh.world; ++d) {
     const uint64_t s0 = hoff[uint64_t(d) * nt], s1 = d + 1 < sh.world ? hoff[uint64_t(d + 1) * nt] : sh.nsend;
     send_counts[d] = s1 - s0;
@@ -1804,7 +1850,6 @@ static void shard_reduce(dr_shard& sh, const void* recv_rec, uint64_t n, const v
   ActionArrays act{own->kind.p, own->flags.p, own->key.p, own->path_ptr.p, own->path_len.p, own->size.p,
                    own->delts.p, own->src_off.p, own->src_len.p};
   launch_shard_unpack(rec, n, static_cast<const uint8_t*>(recv_path), poff.p, act, stream);
-  ctx->mark("shard_exchange");
   reduce_actions(ctx, own.get(), cutoff);
   if (n) HIP_OK(hipMemsetAsync(verdict, 0, n, stream));
   launch_verdict_set(own->live.p, own->n_live, 1, verdict, stream);
@@ -1832,7 +1877,6 @@ static dr_state* shard_finish(dr_shard& sh, const uint8_t* verdict_back) {
   launch_verdict_collect(verdict_back, sh.send_idx.p, n, 1, pl.p, st.live.p, stream);
   launch_verdict_collect(verdict_back, sh.send_idx.p, n, 2, pt.p, st.tomb.p, stream);
   HIP_OK(hipStreamSynchronize(stream));
-  ctx->mark("shard_finish");
   // counters: the owner-side partial sums (their sum over ranks is the table's computedState)
   st.counts.num_files = sh.owner.num_files;
   st.counts.size_in_bytes = sh.owner.size_in_bytes;
@@ -1926,6 +1970,8 @@ int dr_ctx_create(int device, dr_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return DR_E_DEVICE;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return DR_E_DEVICE;
   if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) return DR_E_DEVICE;
+  const char* ov = std::getenv("DR_OVERLAP");
+  c->overlap = ov && std::atoi(ov) != 0;
   *out = c.release();
   return DR_OK;
 }
@@ -2014,9 +2060,12 @@ int dr_staged_plan(const dr_staged* staged, uint64_t* out, int32_t cap, int32_t*
   uint64_t ck = 0, cs = 0, us = 0;
   for (auto& p : s.parts) ck += p.len;
   for (auto& p : s.hot.pages) { cs += p.csize; us += p.usize; }
-  const uint64_t v[7] = {s.h_json.size(), ck, s.ck_rows, s.hot.pages.size(), cs, us, s.hot.dict_entries};
+  const PagePlan& h = s.hot;
+  const uint64_t v[13] = {s.h_json.size(), ck, s.ck_rows, s.hot.pages.size(), cs, us, s.hot.dict_entries,
+                          h.snap_in_bytes, h.snap_out_bytes, h.nchunks, h.block_page.size(), h.snap_elements,
+                          h.copy_bytes};
   int32_t k = 0;
-  for (; k < cap && k < 7; ++k) out[k] = v[k];
+  for (; k < cap && k < 13; ++k) out[k] = v[k];
   *n = k;
   return DR_OK;
 }
@@ -2026,13 +2075,11 @@ int dr_replay_staged(dr_ctx* ctx, const dr_staged* staged, int64_t cutoff, uint3
   *out = nullptr;
   int rc = guard(ctx, [&] {
     HIP_OK(hipSetDevice(ctx->device));
+    ctx->begin_call();
     *out = replay(ctx, staged->d, cutoff, flags);
     ctx->collect_timings();
   });
-  if (rc != DR_OK) {
-    for (auto& m : ctx->marks) (void)hipEventDestroy(m.ev);
-    ctx->marks.clear();
-  }
+  if (rc != DR_OK) ctx->drop_timings();
   return rc;
 }
 
@@ -2058,15 +2105,13 @@ int dr_state_apply(dr_ctx* ctx, dr_state* base, const dr_staged* tail, int64_t m
   *out = nullptr;
   int rc = guard(ctx, [&] {
     HIP_OK(hipSetDevice(ctx->device));
+    ctx->begin_call();
     ctx->mark("start");
     *out = apply_tail(ctx, *base, tail->d, min_file_retention_timestamp, flags);
     ctx->mark("end");
     ctx->collect_timings();
   });
-  if (rc != DR_OK) {
-    for (auto& m : ctx->marks) (void)hipEventDestroy(m.ev);
-    ctx->marks.clear();
-  }
+  if (rc != DR_OK) ctx->drop_timings();
   return rc;
 }
 
@@ -2249,6 +2294,7 @@ int dr_shard_begin(dr_ctx* ctx, const dr_staged* staged, int32_t world, dr_shard
     sh->ctx = ctx;
     sh->staged = staged->d;
     sh->world = uint32_t(world);
+    ctx->begin_call();
     shard_begin(*sh, send_counts, send_bytes);
     *out = sh.release();
   });
@@ -2276,10 +2322,7 @@ int dr_shard_finish(dr_shard* shard, const uint8_t* verdict_back, dr_state** out
     *out = shard_finish(*shard, verdict_back);
     ctx->collect_timings();
   });
-  if (rc != DR_OK) {
-    for (auto& m : ctx->marks) (void)hipEventDestroy(m.ev);
-    ctx->marks.clear();
-  }
+  if (rc != DR_OK) ctx->drop_timings();
   return rc;
 }
 
@@ -2289,6 +2332,7 @@ int dr_parse_commits(dr_ctx* ctx, const dr_staged* staged, dr_parsed** out, dr_l
   return guard(ctx, [&] {
     HIP_OK(hipSetDevice(ctx->device));
     auto p = std::make_unique<dr_parsed>();
+    ctx->begin_call();
     parse_commits(ctx, staged->d, *p);
     ctx->collect_timings();
     *lines = dr_lines{};

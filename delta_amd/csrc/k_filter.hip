@@ -447,16 +447,16 @@ uint32_t filter_max_cols() { return dev::PV_MAXC; }
 uint32_t filter_max_stack() { return dev::PV_STACK; }
 
 void launch_filter(const FilterArgs& a, hipStream_t st) {
-  if (a.n_live) hipLaunchKernelGGL(dev::k_filter, dim3(g256(a.n_live)), dim3(256), 0, st, a);
+  if (a.n_live) DR_LAUNCH(dev::k_filter, dim3(g256(a.n_live)), dim3(256), 0, st, a);
 }
 void launch_rep0_flags(const uint8_t* rep, uint64_t n, uint32_t* f, hipStream_t st) {
-  if (n) hipLaunchKernelGGL(dev::k_rep0_flags, dim3(g256(n)), dim3(256), 0, st, rep, n, f);
+  if (n) DR_LAUNCH(dev::k_rep0_flags, dim3(g256(n)), dim3(256), 0, st, rep, n, f);
 }
 void launch_row_starts(const uint8_t* rep, uint64_t n, const uint64_t* pos, uint64_t* row_start, hipStream_t st) {
-  if (n) hipLaunchKernelGGL(dev::k_row_starts, dim3(g256(n)), dim3(256), 0, st, rep, n, pos, row_start);
+  if (n) DR_LAUNCH(dev::k_row_starts, dim3(g256(n)), dim3(256), 0, st, rep, n, pos, row_start);
 }
 void launch_select(const uint32_t* flag, const uint64_t* pos, uint64_t n, int64_t* out, hipStream_t st) {
-  if (n) hipLaunchKernelGGL(dev::k_select, dim3(g256(n)), dim3(256), 0, st, flag, pos, n, out);
+  if (n) DR_LAUNCH(dev::k_select, dim3(g256(n)), dim3(256), 0, st, flag, pos, n, out);
 }
 
 }  // namespace dr

@@ -18,12 +18,14 @@ constexpr int JSON_THREADS = 256;
 constexpr int JSON_BYTES_PER_THREAD = 64;
 constexpr int JSON_BYTES_PER_BLOCK = JSON_THREADS * JSON_BYTES_PER_THREAD;
 
-__device__ __forceinline__ uint32_t count_nl_word(uint32_t w) {
-  // bytes equal to 0x0a -> 0x80 in that byte lane
-  const uint32_t x = w ^ 0x0a0a0a0au;
-  const uint32_t t = (x - 0x01010101u) & ~x & 0x80808080u;
-  return __builtin_popcount(t);
+// 0x80 in every byte of w that equals '\n'. Exact per byte: the shorter (x - 0x01..) & ~x test
+// also flags a 0x0b byte above a newline (the borrow crosses into it), which split lines at "\n\v"
+// (found by the device walker fuzz, tests/test_gpu_edge_cases.py).
+__device__ __forceinline__ uint32_t nl_bytes(uint32_t w) {
+  const uint32_t y = w ^ 0x0a0a0a0au;
+  return ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y | 0x7F7F7F7Fu);
 }
+__device__ __forceinline__ uint32_t count_nl_word(uint32_t w) { return __builtin_popcount(nl_bytes(w)); }
 
 // Stage 1 reads the JSON once: every 16 KiB block finds its newlines (64 bytes per thread, a
 // block-wide scan of the per-thread counts ranks them) and stores their block-relative positions
@@ -73,8 +75,7 @@ __device__ __forceinline__ uint32_t block_newlines(const uint8_t* __restrict__ b
   if (full) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      uint32_t x = words[i] ^ 0x0a0a0a0au;
-      uint32_t t = (x - 0x01010101u) & ~x & 0x80808080u;
+      uint32_t t = nl_bytes(words[i]);
       while (t) {
         put(r++, rel0 + 4 * i + (__builtin_ctz(t) >> 3));
         t &= t - 1;
@@ -271,26 +272,26 @@ uint64_t json_slot_entries(uint64_t len) { return json_num_blocks(len) * dev::JS
 
 void launch_json_index(const uint8_t* buf, uint64_t len, uint32_t* block_counts, uint16_t* slots, hipStream_t st) {
   uint64_t nb = json_num_blocks(len);
-  if (nb) hipLaunchKernelGGL(dev::k_json_index, dim3(unsigned(nb)), dim3(dev::JSON_THREADS), 0, st, buf, len,
+  if (nb) DR_LAUNCH(dev::k_json_index, dim3(unsigned(nb)), dim3(dev::JSON_THREADS), 0, st, buf, len,
                              block_counts, slots);
 }
 
 void launch_json_place(const uint8_t* buf, uint64_t len, const uint32_t* block_counts, const uint64_t* block_off,
                        const uint16_t* slots, uint64_t* nl, hipStream_t st) {
   uint64_t nb = json_num_blocks(len);
-  if (nb) hipLaunchKernelGGL(dev::k_json_place, dim3(unsigned(nb)), dim3(dev::JSON_THREADS), 0, st, buf, len,
+  if (nb) DR_LAUNCH(dev::k_json_place, dim3(unsigned(nb)), dim3(dev::JSON_THREADS), 0, st, buf, len,
                              block_counts, block_off, slots, nl);
 }
 
 void launch_json_parse(const JsonParseArgs& a, hipStream_t st) {
   if (!a.nlines) return;
-  hipLaunchKernelGGL(dev::k_json_lines, dim3(unsigned((a.nlines + dev::JL_T - 1) / dev::JL_T)), dim3(dev::JL_T), 0,
+  DR_LAUNCH(dev::k_json_lines, dim3(unsigned((a.nlines + dev::JL_T - 1) / dev::JL_T)), dim3(dev::JL_T), 0,
                      st, a);
 }
 
 void launch_json_hard(const JsonParseArgs& a, hipStream_t st) {
   if (!a.nlines) return;
-  hipLaunchKernelGGL(dev::k_json_hard, dim3(256), dim3(64), 0, st, a);
+  DR_LAUNCH(dev::k_json_hard, dim3(256), dim3(64), 0, st, a);
 }
 
 }  // namespace dr

@@ -619,21 +619,21 @@ __global__ void k_ckpt_assemble(CkptAssembleArgs a) {
 uint32_t ba_tile_bytes() { return dev::BA_TILE; }
 void launch_ba_bounds(const ParquetArgs& a, hipStream_t st, void* scan_scratch) {
   if (!a.nba_tiles) return;
-  hipLaunchKernelGGL(dev::k_ba_count, dim3(a.nba_tiles), dim3(dev::BA_T), 0, st, a);
+  DR_LAUNCH(dev::k_ba_count, dim3(a.nba_tiles), dim3(dev::BA_T), 0, st, a);
   launch_scan_u32(a.ba_tile_cnt, a.ba_tile_off, a.nba_tiles, scan_scratch, st);
-  hipLaunchKernelGGL(dev::k_ba_write, dim3(a.nba_tiles), dim3(dev::BA_T), 0, st, a);
-  hipLaunchKernelGGL(dev::k_ba_check, dim3(a.nba_tiles), dim3(dev::BA_T), 0, st, a);
+  DR_LAUNCH(dev::k_ba_write, dim3(a.nba_tiles), dim3(dev::BA_T), 0, st, a);
+  DR_LAUNCH(dev::k_ba_check, dim3(a.nba_tiles), dim3(dev::BA_T), 0, st, a);
 }
 void launch_pq_dict(const ParquetArgs& a, hipStream_t st) {
   if (!a.npages) return;
-  hipLaunchKernelGGL(dev::k_pq_dict_fast, dim3(a.npages, dev::DICT_SLICES), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(dev::k_pq_dict, dim3(a.npages), dim3(64), 0, st, a);
+  DR_LAUNCH(dev::k_pq_dict_fast, dim3(a.npages, dev::DICT_SLICES), dim3(256), 0, st, a);
+  DR_LAUNCH(dev::k_pq_dict, dim3(a.npages), dim3(64), 0, st, a);
 }
 void launch_pq_data(const ParquetArgs& a, hipStream_t st) {
-  if (a.npages) hipLaunchKernelGGL(dev::k_pq_data, dim3(a.npages), dim3(dev::PQD_T), 0, st, a);
+  if (a.npages) DR_LAUNCH(dev::k_pq_data, dim3(a.npages), dim3(dev::PQD_T), 0, st, a);
 }
 void launch_ckpt_assemble(const CkptAssembleArgs& a, hipStream_t st) {
-  if (a.nrows) hipLaunchKernelGGL(dev::k_ckpt_assemble, dim3(unsigned((a.nrows + 255) / 256)), dim3(256), 0, st, a);
+  if (a.nrows) DR_LAUNCH(dev::k_ckpt_assemble, dim3(unsigned((a.nrows + 255) / 256)), dim3(256), 0, st, a);
 }
 
 }  // namespace dr

@@ -746,66 +746,66 @@ void launch_scan_u32(const uint32_t* in, uint64_t* out, uint64_t n, void* scratc
     return;
   }
   uint64_t* sums = static_cast<uint64_t*>(scratch);
-  hipLaunchKernelGGL(dev::k_scan_reduce, dim3(unsigned(nb)), dim3(dev::SCAN_T), 0, st, in, n, sums);
-  hipLaunchKernelGGL(dev::k_scan_single, dim3(1), dim3(dev::SCAN_T), 0, st, sums, nb);
-  hipLaunchKernelGGL(dev::k_scan_apply, dim3(unsigned(nb)), dim3(dev::SCAN_T), 0, st, in, n, sums, out);
+  DR_LAUNCH(dev::k_scan_reduce, dim3(unsigned(nb)), dim3(dev::SCAN_T), 0, st, in, n, sums);
+  DR_LAUNCH(dev::k_scan_single, dim3(1), dim3(dev::SCAN_T), 0, st, sums, nb);
+  DR_LAUNCH(dev::k_scan_apply, dim3(unsigned(nb)), dim3(dev::SCAN_T), 0, st, in, n, sums, out);
 }
 
 void launch_canon(const CanonArgs& a, hipStream_t st) {
-  if (a.n) hipLaunchKernelGGL(dev::k_canon, dim3(unsigned((a.n + 255) / 256)), dim3(256), 0, st, a);
+  if (a.n) DR_LAUNCH(dev::k_canon, dim3(unsigned((a.n + 255) / 256)), dim3(256), 0, st, a);
 }
 
 uint32_t part_tiles(uint64_t n) { return uint32_t((n + dev::PART_TILE - 1) / dev::PART_TILE); }
 uint32_t part_max_bucket_bits() { return dev::PART_MAX_BITS; }
 
 void launch_bucket_hist(const PartitionArgs& a, hipStream_t st) {
-  if (a.ntiles) hipLaunchKernelGGL(dev::k_bucket_hist, dim3(a.ntiles), dim3(dev::PART_T), 0, st, a);
+  if (a.ntiles) DR_LAUNCH(dev::k_bucket_hist, dim3(a.ntiles), dim3(dev::PART_T), 0, st, a);
 }
 
 void launch_bucket_scatter(const PartitionArgs& a, hipStream_t st) {
-  if (a.ntiles) hipLaunchKernelGGL(dev::k_bucket_scatter, dim3(a.ntiles), dim3(dev::PART_T), 0, st, a);
+  if (a.ntiles) DR_LAUNCH(dev::k_bucket_scatter, dim3(a.ntiles), dim3(dev::PART_T), 0, st, a);
 }
 
 void launch_bucket_offsets(const uint64_t* tile_off, uint32_t nb, uint32_t nt, uint64_t* bucket_off, hipStream_t st) {
-  hipLaunchKernelGGL(dev::k_bucket_offsets, dim3((nb + 1 + 255) / 256), dim3(256), 0, st, tile_off, nb, nt, bucket_off);
+  DR_LAUNCH(dev::k_bucket_offsets, dim3((nb + 1 + 255) / 256), dim3(256), 0, st, tile_off, nb, nt, bucket_off);
 }
 
 void launch_bucket_reduce(const ReduceArgs& a, hipStream_t st) {
-  if (a.nbuckets) hipLaunchKernelGGL(dev::k_bucket_reduce, dim3(a.nbuckets), dim3(dev::RED_T), 0, st, a);
+  if (a.nbuckets) DR_LAUNCH(dev::k_bucket_reduce, dim3(a.nbuckets), dim3(dev::RED_T), 0, st, a);
 }
 
 void launch_bucket_verify(const ReduceArgs& a, hipStream_t st) {
-  if (a.nbuckets) hipLaunchKernelGGL(dev::k_bucket_verify, dim3(a.nbuckets), dim3(dev::VER_T), 0, st, a);
+  if (a.nbuckets) DR_LAUNCH(dev::k_bucket_verify, dim3(a.nbuckets), dim3(dev::VER_T), 0, st, a);
 }
 
 void launch_bucket_reduce64(const ReduceArgs& a, const uint32_t* buckets, uint32_t nb, hipStream_t st,
                             const unsigned long long* count) {
   const uint32_t g = count ? std::min(nb, 256u) : nb;
-  if (nb) hipLaunchKernelGGL(dev::k_bucket_reduce64, dim3(g), dim3(dev::RED_T), 0, st, a, buckets, nb, count);
+  if (nb) DR_LAUNCH(dev::k_bucket_reduce64, dim3(g), dim3(dev::RED_T), 0, st, a, buckets, nb, count);
 }
 
 void launch_bucket_exact(const ReduceArgs& a, const uint32_t* buckets, uint32_t nb, hipStream_t st,
                          const unsigned long long* count) {
   const uint32_t g = count ? std::min(nb, 256u) : nb;
-  if (nb) hipLaunchKernelGGL(dev::k_bucket_exact, dim3(g), dim3(dev::RED_T), 0, st, a, buckets, nb, count);
+  if (nb) DR_LAUNCH(dev::k_bucket_exact, dim3(g), dim3(dev::RED_T), 0, st, a, buckets, nb, count);
 }
 
 void launch_sum_stats(const ReduceArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(dev::k_sum_stats, dim3(1), dim3(1024), 0, st, a.bstats, a.nbuckets, a.totals);
+  DR_LAUNCH(dev::k_sum_stats, dim3(1), dim3(1024), 0, st, a.bstats, a.nbuckets, a.totals);
 }
 
 void launch_compact(const CompactArgs& a, hipStream_t st) {
-  if (a.nbuckets) hipLaunchKernelGGL(dev::k_compact, dim3(a.nbuckets), dim3(64), 0, st, a);
+  if (a.nbuckets) DR_LAUNCH(dev::k_compact, dim3(a.nbuckets), dim3(64), 0, st, a);
 }
 
 void launch_compact2(const CompactArgs& live, const CompactArgs& tomb, hipStream_t st) {
-  if (live.nbuckets) hipLaunchKernelGGL(dev::k_compact2, dim3(live.nbuckets, 2), dim3(64), 0, st, live, tomb);
+  if (live.nbuckets) DR_LAUNCH(dev::k_compact2, dim3(live.nbuckets, 2), dim3(64), 0, st, live, tomb);
 }
 
 void launch_survivor_scan(const uint32_t* lc, const uint32_t* tc, uint32_t nb, uint64_t* loff, uint64_t* toff,
                           hipStream_t st) {
   if (nb > uint32_t(dev::SSCAN_T) * 8) throw std::runtime_error("survivor scan: too many buckets");
-  hipLaunchKernelGGL(dev::k_survivor_scan, dim3(1), dim3(dev::SSCAN_T), 0, st, lc, tc, nb, loff, toff);
+  DR_LAUNCH(dev::k_survivor_scan, dim3(1), dim3(dev::SSCAN_T), 0, st, lc, tc, nb, loff, toff);
 }
 
 }  // namespace dr

@@ -140,31 +140,31 @@ uint64_t shard_tiles(uint64_t n) { return (n + dev::SH_TILE - 1) / dev::SH_TILE;
 uint32_t shard_max_world() { return dev::SH_MAXW; }
 
 void launch_shard_count(const ShardArgs& a, hipStream_t st) {
-  if (a.ntiles) hipLaunchKernelGGL(dev::k_shard_count, dim3(unsigned(a.ntiles)), dim3(dev::SH_T), 0, st, a);
+  if (a.ntiles) DR_LAUNCH(dev::k_shard_count, dim3(unsigned(a.ntiles)), dim3(dev::SH_T), 0, st, a);
 }
 void launch_shard_scatter(const ShardArgs& a, hipStream_t st) {
-  if (a.ntiles) hipLaunchKernelGGL(dev::k_shard_scatter, dim3(unsigned(a.ntiles)), dim3(dev::SH_T), 0, st, a);
+  if (a.ntiles) DR_LAUNCH(dev::k_shard_scatter, dim3(unsigned(a.ntiles)), dim3(dev::SH_T), 0, st, a);
 }
 void launch_shard_pack(const ShardArgs& a, ShardRec* rec, uint32_t* plen, hipStream_t st) {
-  if (a.nsend) hipLaunchKernelGGL(dev::k_shard_pack, dim3(grid_for(a.nsend, 256)), dim3(256), 0, st, a, rec, plen);
+  if (a.nsend) DR_LAUNCH(dev::k_shard_pack, dim3(grid_for(a.nsend, 256)), dim3(256), 0, st, a, rec, plen);
 }
 void launch_shard_plen(const ShardRec* rec, uint64_t n, uint32_t* plen, hipStream_t st) {
-  if (n) hipLaunchKernelGGL(dev::k_shard_plen, dim3(grid_for(n, 256)), dim3(256), 0, st, rec, n, plen);
+  if (n) DR_LAUNCH(dev::k_shard_plen, dim3(grid_for(n, 256)), dim3(256), 0, st, rec, n, plen);
 }
 void launch_shard_unpack(const ShardRec* rec, uint64_t n, const uint8_t* path_base, const uint64_t* poff,
                          const ActionArrays& act, hipStream_t st) {
-  if (n) hipLaunchKernelGGL(dev::k_shard_unpack, dim3(grid_for(n, 256)), dim3(256), 0, st, rec, n, path_base, poff, act);
+  if (n) DR_LAUNCH(dev::k_shard_unpack, dim3(grid_for(n, 256)), dim3(256), 0, st, rec, n, path_base, poff, act);
 }
 void launch_verdict_set(const uint32_t* idx, uint64_t n, uint8_t v, uint8_t* verdict, hipStream_t st) {
-  if (n) hipLaunchKernelGGL(dev::k_verdict_set, dim3(grid_for(n, 256)), dim3(256), 0, st, idx, n, v, verdict);
+  if (n) DR_LAUNCH(dev::k_verdict_set, dim3(grid_for(n, 256)), dim3(256), 0, st, idx, n, v, verdict);
 }
 void launch_verdict_flags(const uint8_t* verdict, uint64_t n, uint32_t* f_live, uint32_t* f_tomb, hipStream_t st) {
-  if (n) hipLaunchKernelGGL(dev::k_verdict_flags, dim3(grid_for(n, 256)), dim3(256), 0, st, verdict, n, f_live, f_tomb);
+  if (n) DR_LAUNCH(dev::k_verdict_flags, dim3(grid_for(n, 256)), dim3(256), 0, st, verdict, n, f_live, f_tomb);
 }
 void launch_verdict_collect(const uint8_t* verdict, const uint32_t* send_idx, uint64_t n, uint8_t want,
                             const uint64_t* pos, uint32_t* out, hipStream_t st) {
   if (n)
-    hipLaunchKernelGGL(dev::k_verdict_collect, dim3(grid_for(n, 256)), dim3(256), 0, st, verdict, send_idx, n, want,
+    DR_LAUNCH(dev::k_verdict_collect, dim3(grid_for(n, 256)), dim3(256), 0, st, verdict, send_idx, n, want,
                        pos, out);
 }
 

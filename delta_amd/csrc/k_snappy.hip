@@ -774,22 +774,22 @@ uint32_t snappy_wg_chunks() { return dev::WG_CHUNKS; }
 
 void launch_snappy(const SnappyArgs& a, hipStream_t st, void* scan_scratch) {
   if (!a.npages) return;
-  hipLaunchKernelGGL(dev::k_snap_spec, dim3(a.nwg), dim3(dev::WG_CHUNKS), 0, st, a);
+  DR_LAUNCH(dev::k_snap_spec, dim3(a.nwg), dim3(dev::WG_CHUNKS), 0, st, a);
   const unsigned g = (a.nchunks + 255) / 256;
-  hipLaunchKernelGGL(dev::k_snap_assume, dim3(g), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(dev::k_snap_entries, dim3(g), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(dev::k_snap_regions, dim3(g), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(dev::k_snap_resolve, dim3(512), dim3(64), 0, st, a);
-  hipLaunchKernelGGL(dev::k_snap_count, dim3(g), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(dev::k_snap_scan, dim3(a.npages), dim3(64), 0, st, a);
+  DR_LAUNCH(dev::k_snap_assume, dim3(g), dim3(256), 0, st, a);
+  DR_LAUNCH(dev::k_snap_entries, dim3(g), dim3(256), 0, st, a);
+  DR_LAUNCH(dev::k_snap_regions, dim3(g), dim3(256), 0, st, a);
+  DR_LAUNCH(dev::k_snap_resolve, dim3(512), dim3(64), 0, st, a);
+  DR_LAUNCH(dev::k_snap_count, dim3(g), dim3(256), 0, st, a);
+  DR_LAUNCH(dev::k_snap_scan, dim3(a.npages), dim3(64), 0, st, a);
   launch_scan_u32(a.chunk_elems, a.chunk_rec_start, a.nchunks, scan_scratch, st);
-  hipLaunchKernelGGL(dev::k_snap_emit, dim3(a.nwg), dim3(2 * dev::WG_CHUNKS), 0, st, a);
-  hipLaunchKernelGGL(dev::k_snap_exec, dim3(a.nblocks), dim3(dev::EXEC_T), 0, st, a);
-  hipLaunchKernelGGL(dev::k_snap_serial, dim3((a.npages + 63) / 64), dim3(64), 0, st, a);
+  DR_LAUNCH(dev::k_snap_emit, dim3(a.nwg), dim3(2 * dev::WG_CHUNKS), 0, st, a);
+  DR_LAUNCH(dev::k_snap_exec, dim3(a.nblocks), dim3(dev::EXEC_T), 0, st, a);
+  DR_LAUNCH(dev::k_snap_serial, dim3((a.npages + 63) / 64), dim3(64), 0, st, a);
 }
 
 void launch_page_copy(const CopyJob* jobs, uint32_t njobs, hipStream_t st) {
-  if (njobs) hipLaunchKernelGGL(dev::k_page_copy, dim3(njobs), dim3(256), 0, st, jobs, njobs);
+  if (njobs) DR_LAUNCH(dev::k_page_copy, dim3(njobs), dim3(256), 0, st, jobs, njobs);
 }
 
 }  // namespace dr

@@ -23,24 +23,39 @@ __global__ void k_gather_bytes(const uint64_t* __restrict__ ptr, const uint32_t*
 
 }  // namespace dev
 
+namespace {
+thread_local LaunchHook t_hook = nullptr;
+thread_local void* t_hook_user = nullptr;
+}  // namespace
+void set_launch_hook(LaunchHook hook, void* user) {
+  t_hook = hook;
+  t_hook_user = user;
+}
+void launch_begin(const char* kernel, hipStream_t st) {
+  if (t_hook) t_hook(t_hook_user, kernel, st, 0);
+}
+void launch_end(const char* kernel, hipStream_t st) {
+  if (t_hook) t_hook(t_hook_user, kernel, st, 1);
+}
+
 void launch_gather_u64(const uint64_t* src, const uint32_t* idx, uint64_t n, uint64_t* dst, hipStream_t st) {
-  if (n) hipLaunchKernelGGL((dev::k_gather<uint64_t, uint32_t>), dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, src, idx, n, dst);
+  if (n) DR_LAUNCH((dev::k_gather<uint64_t, uint32_t>), dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, src, idx, n, dst);
 }
 void launch_gather_u32(const uint32_t* src, const uint32_t* idx, uint64_t n, uint32_t* dst, hipStream_t st) {
-  if (n) hipLaunchKernelGGL((dev::k_gather<uint32_t, uint32_t>), dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, src, idx, n, dst);
+  if (n) DR_LAUNCH((dev::k_gather<uint32_t, uint32_t>), dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, src, idx, n, dst);
 }
 void launch_gather_u8(const uint8_t* src, const uint32_t* idx, uint64_t n, uint8_t* dst, hipStream_t st) {
-  if (n) hipLaunchKernelGGL((dev::k_gather<uint8_t, uint32_t>), dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, src, idx, n, dst);
+  if (n) DR_LAUNCH((dev::k_gather<uint8_t, uint32_t>), dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, src, idx, n, dst);
 }
 void launch_gather_u16(const uint16_t* src, const uint32_t* idx, uint64_t n, uint16_t* dst, hipStream_t st) {
-  if (n) hipLaunchKernelGGL((dev::k_gather<uint16_t, uint32_t>), dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, src, idx, n, dst);
+  if (n) DR_LAUNCH((dev::k_gather<uint16_t, uint32_t>), dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, src, idx, n, dst);
 }
 void launch_gather_u64_by64(const uint64_t* src, const uint64_t* idx, uint64_t n, uint64_t* dst, hipStream_t st) {
-  if (n) hipLaunchKernelGGL((dev::k_gather<uint64_t, uint64_t>), dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, src, idx, n, dst);
+  if (n) DR_LAUNCH((dev::k_gather<uint64_t, uint64_t>), dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, src, idx, n, dst);
 }
 void launch_gather_bytes(const uint64_t* ptr, const uint32_t* len, const uint64_t* off, uint64_t n, uint8_t* out,
                          hipStream_t st) {
-  if (n) hipLaunchKernelGGL(dev::k_gather_bytes, dim3(unsigned((n + 3) / 4)), dim3(256), 0, st, ptr, len, off, n, out);
+  if (n) DR_LAUNCH(dev::k_gather_bytes, dim3(unsigned((n + 3) / 4)), dim3(256), 0, st, ptr, len, off, n, out);
 }
 
 }  // namespace dr

@@ -5,6 +5,21 @@
 
 namespace dr {
 
+// ---- per-kernel timing hook (dr_set_timing) -------------------------------------------------------
+// Every launcher brackets each kernel it enqueues with launch_begin / launch_end; when a hook is
+// installed (thread-local: one dr_ctx per host thread) the context records a HIP event pair on the
+// kernel's stream, so per-kernel device times are exact and need no profiler.
+typedef void (*LaunchHook)(void* user, const char* kernel, hipStream_t st, int end);
+void set_launch_hook(LaunchHook hook, void* user);
+void launch_begin(const char* kernel, hipStream_t st);
+void launch_end(const char* kernel, hipStream_t st);
+#define DR_LAUNCH(K, GRID, BLOCK, SHM, ST, ...)                  \
+  do {                                                           \
+    ::dr::launch_begin(#K, ST);                                  \
+    hipLaunchKernelGGL(K, GRID, BLOCK, SHM, ST, __VA_ARGS__);    \
+    ::dr::launch_end(#K, ST);                                    \
+  } while (0)
+
 // Per-action SoA arrays in HBM; action index = checkpoint rows first, then JSON lines (the
 // reference's replay order: D/Snapshot.scala:102-104 sorts by input file name).
 struct ActionArrays {

@@ -90,13 +90,14 @@ class Engine:
         self.check(self.lib.dr_set_timing(self.ctx, 1 if on else 0))
 
     def last_timings(self) -> Dict[str, float]:
-        names = C.create_string_buffer(8192)
-        ms = (C.c_float * 64)()
+        cap = 1024
+        names = C.create_string_buffer(64 * cap)
+        ms = (C.c_float * cap)()
         n = C.c_int32()
-        self.check(self.lib.dr_last_timings(self.ctx, names, 8192, ms, 64, C.byref(n)))
+        self.check(self.lib.dr_last_timings(self.ctx, names, 64 * cap, ms, cap, C.byref(n)))
         parts = names.raw.split(b"\0")
         out: Dict[str, float] = {}
-        for i in range(min(n.value, 64)):
+        for i in range(min(n.value, cap)):
             k = parts[i].decode()
             out[k] = out.get(k, 0.0) + float(ms[i])
         return out
@@ -145,11 +146,12 @@ class Staged:
         return j.value, c.value
 
     def plan(self) -> Dict[str, int]:
-        out = (C.c_uint64 * 8)()
+        out = (C.c_uint64 * 16)()
         n = C.c_int32()
-        self.eng.check(self.eng.lib.dr_staged_plan(self.h, out, 8, C.byref(n)))
+        self.eng.check(self.eng.lib.dr_staged_plan(self.h, out, 16, C.byref(n)))
         names = ["json_bytes", "checkpoint_bytes", "checkpoint_rows", "pages", "pages_compressed_bytes",
-                 "pages_decompressed_bytes", "dict_entries"]
+                 "pages_decompressed_bytes", "dict_entries", "snappy_in_bytes", "snappy_out_bytes",
+                 "snappy_chunks", "snappy_blocks", "snappy_elements", "copy_bytes"]
         return {names[i]: int(out[i]) for i in range(n.value)}
 
     def replay(self, min_file_retention_timestamp: int, validate: bool = True, reducer: str = "lds") -> "State":

@@ -138,7 +138,10 @@ int dr_staged_release(dr_staged* staged);
 int dr_staged_bytes(const dr_staged* staged, uint64_t* json_bytes, uint64_t* checkpoint_bytes);
 /* Decode plan figures (for roofline accounting): out[0] JSON bytes, [1] checkpoint bytes,
  * [2] checkpoint rows, [3] planned pages, [4] their compressed bytes, [5] their decompressed bytes,
- * [6] dictionary entries. *n receives the number of figures written (<= cap). */
+ * [6] dictionary entries, [7] SNAPPY input bytes, [8] SNAPPY output bytes, [9] SNAPPY 256-byte
+ * speculation chunks, [10] SNAPPY 64 KiB output blocks, [11] SNAPPY elements (0 until a replay with
+ * timing on has counted them), [12] bytes of uncompressed pages copied. *n receives the number of
+ * figures written (<= cap). */
 int dr_staged_plan(const dr_staged* staged, uint64_t* out, int32_t cap, int32_t* n);
 
 /* ---- replay (device) ----------------------------------------------------------------------

@@ -295,10 +295,17 @@ def replay_key(p: str) -> str:
 # parts first (sorted by file name), then deltas by version; within a file, line/row order.
 # ----------------------------------------------------------------------------------------------
 def read_json_actions(data: bytes) -> Iterator[Optional[Tuple[str, dict]]]:
+    """Spark's JSON reader over Action.logSchema in PERMISSIVE mode (D/DeltaLogFileIndex.scala:67): a
+    line that is not a JSON object reads as a row of nulls, which unwrap drops."""
     for line in data.split(b"\n"):
         if not line.strip():
             continue
-        yield unwrap(json.loads(line))
+        try:
+            obj = json.loads(line)
+        except ValueError:
+            yield None
+            continue
+        yield unwrap(obj) if isinstance(obj, dict) else None
 
 
 def read_checkpoint_actions(path: str) -> Iterator[Optional[Tuple[str, dict]]]:

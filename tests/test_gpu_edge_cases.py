@@ -138,8 +138,8 @@ def test_checkpoint_rows_with_absolute_paths(engine, tmp_path):
     write_commit(lp, 4, [remove("file:///abs/one.parquet"), remove("/abs/two.parquet"),
                          add("file:/abs/gone.parquet")])
     counts, live, tomb = _same_as_oracle(engine, lp, cutoff=10)
-    assert sorted(f["path"] for f in live) == ["file:/abs/gone.parquet", "file:///abs/three.parquet",
-                                               "rel/four.parquet"]
+    assert sorted(f["path"] for f in live) == sorted(["file:/abs/gone.parquet", "file:///abs/three.parquet",
+                                                      "rel/four.parquet"])
     assert sorted(t["path"] for t in tomb) == ["file:///abs/one.parquet", "file:///abs/two.parquet"]
 
 

@@ -398,8 +398,19 @@ def test_checkpoint_writer_round_trip(engine, tmp_path, parts):
     assert len(names) == parts
     schema = pq.read_schema(os.path.join(lp, names[0]))
     assert schema.names == ["txn", "add", "remove", "metaData", "protocol"]
-    assert [f.name for f in schema.field("add").type] == ["path", "partitionValues", "size", "modificationTime",
-                                                         "dataChange", "tags", "stats"]
+    # CheckpointV2 (checkpointV2.enabled default true, the table is partitioned): the partition
+    # values cast to the partition schema follow stats (D/Checkpoints.scala:340-365,372-389)
+    add_t = schema.field("add").type
+    assert [f.name for f in add_t] == ["path", "partitionValues", "size", "modificationTime", "dataChange", "tags",
+                                       "stats", "partitionValues_parsed"]
+    parsed_t = add_t.field("partitionValues_parsed").type
+    assert [(f.name, str(f.type)) for f in parsed_t] == [("p0", "date32[day]"), ("p1", "int32")]
+    rows = pq.read_table(os.path.join(lp, names[0])).column("add").to_pylist()
+    for r in rows:
+        if r is not None:
+            pv = dict(r["partitionValues"])
+            assert r["partitionValues_parsed"]["p0"].isoformat() == pv["p0"]
+            assert r["partitionValues_parsed"]["p1"] == int(pv["p1"])
     seg = O.get_log_segment(lp)
     assert seg.checkpoint_version == snap.version and not seg.deltas
     after = O.state_reconstruction(seg, cutoff)
@@ -407,6 +418,37 @@ def test_checkpoint_writer_round_trip(engine, tmp_path, parts):
     try:
         _assert_same(st, before)
         _assert_same(st, after)
+    finally:
+        st.release()
+    DeltaLog.clear_cache()
+
+
+def test_checkpoint_writer_table_options(engine, tmp_path):
+    """delta.checkpoint.writeStatsAsJson=false drops add.stats; writeStatsAsStruct=false drops
+    partitionValues_parsed (D/Checkpoints.scala:340-352, D/DeltaConfig.scala:401-418)."""
+    import json
+    import pyarrow.parquet as pq
+    from delta_amd.checkpoint import write_checkpoint
+    from delta_amd.delta_log import DeltaLog, ManualClock
+    from delta_amd.testing import synth as S
+    spec = S.ChurnSpec(ckpt_files=500, ckpt_version=2, n_deltas=1, removes_per_delta=50, adds_per_delta=50,
+                       readd_frac=0.0, ncols=2)
+    S.build_table(str(tmp_path), spec, seed=21)
+    lp = os.path.join(str(tmp_path), "_delta_log")
+    md = S.metadata_dict(2, {"delta.checkpoint.writeStatsAsJson": "false",
+                             "delta.checkpoint.writeStatsAsStruct": "false"})
+    with open(os.path.join(lp, "%020d.json" % 4), "w") as f:
+        f.write(json.dumps({"metaData": md}) + "\n")
+    DeltaLog.clear_cache()
+    snap = DeltaLog.for_table(str(tmp_path), clock=ManualClock(0)).snapshot
+    write_checkpoint(snap)
+    schema = pq.read_schema(os.path.join(lp, "%020d.checkpoint.parquet" % 4))
+    assert [f.name for f in schema.field("add").type] == ["path", "partitionValues", "size", "modificationTime",
+                                                         "dataChange", "tags"]
+    st = _gpu_replay(engine, lp, snap.min_file_retention_timestamp)
+    try:
+        assert st.counts["num_files"] == snap.num_of_files
+        assert st.counts["live_key_sum"] == snap.state.counts["live_key_sum"]
     finally:
         st.release()
     DeltaLog.clear_cache()

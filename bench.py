@@ -46,21 +46,17 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def build_table(path, config, scale, seed):
-    from delta_amd.testing import synth as S
+def build_table(path, config, scale, seed=None, workers=16):
+    """The seeded synthetic table (delta_amd/testing/synth.py), generated once in a child process
+    (its multi-part checkpoints are written by forked workers) and cached under the work dir."""
     marker = os.path.join(path, "expected.json")
-    if os.path.exists(marker):
-        with open(marker) as f:
-            return json.load(f)
-    t = time.time()
-    exp = S.build_config(config, path, scale=scale, seed=seed, keep_ids=False)
-    d = {k: getattr(exp, k) for k in ("version", "min_file_retention_timestamp", "num_files", "size_in_bytes",
-                                      "num_removes", "num_actions", "num_file_actions", "json_bytes",
-                                      "checkpoint_bytes")}
-    with open(marker, "w") as f:
-        json.dump(d, f)
-    log("generated config %d scale %g in %.1fs: %s" % (config, scale, time.time() - t, d))
-    return d
+    if not os.path.exists(marker):
+        t = time.time()
+        subprocess.run([sys.executable, "-m", "delta_amd.testing.synth", str(config), path, str(scale), str(workers)],
+                       cwd=ROOT, check=True, stdout=subprocess.DEVNULL)
+        log("generated config %d scale %g in %.1fs" % (config, scale, time.time() - t))
+    with open(marker) as f:
+        return json.load(f)
 
 
 def algorithmic_bytes(kernel, plan, counts):
@@ -156,6 +152,54 @@ def cpu_baseline(log_path, cutoff, counts, threads, one_core=True):
     return out
 
 
+WORKLOAD = {
+    3: "config 3: 10M-file checkpoint + 30 JSON commits, %d actions -> %d live files, 30%% remove/re-add churn, "
+       "retention cutoff",
+    4: "config 4: 100-part checkpoint, %d actions -> %d live files, 4 partition columns; reconstruction step + "
+       "4-column partition predicate (k5_filter)",
+}
+
+
+def measure_filter(eng, staged, cutoff, exp, steps):
+    """K5 over the reconstructed state: config 4's 4-column conjunction. The first dr_filter builds the
+    state's typed partition-value cache (k_pv_extract); later ones only run k_filter_typed."""
+    import torch
+    from delta_amd.predicates import build_program, partition_schema
+    from delta_amd.testing import synth as S
+    st = staged.replay(cutoff)
+    meta = next(a["metaData"] for a in st.nonfile if "metaData" in a)
+    prog = build_program(partition_schema(meta), S.config4_predicate())
+    eng.set_timing(True)
+    t0 = time.perf_counter()
+    sel = st.filter(prog)
+    first_s = time.perf_counter() - t0
+    first = eng.last_timings()
+    ms = {}
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        st.filter(prog)
+        for k, v in eng.last_timings().items():
+            ms[k] = ms.get(k, 0.0) + v / steps
+    call_s = (time.perf_counter() - t0) / steps
+    eng.set_timing(False)
+    n = st.counts["num_files"]
+    st.release()
+    assert len(sel) == exp["selected"], (len(sel), exp["selected"])
+    # typed cache reads: p0 date (4 B) + p1 int (4 B) + p2 string (8 B address + 4 B length + ~3 B of
+    # value) + p3 boolean (4 B) + 4 null bytes, and a 4 B flag out per live file
+    algo = n * (4 + 4 + 15 + 4 + 4 + 4)
+    kt = ms.get("k_filter_typed")
+    return {"predicate": "p0 >= DATE'2020-03-01' AND p0 < DATE'2020-06-01' AND p1 IN (1..100) AND p2 = 'w17' "
+                         "AND p3 = true", "live_files": n, "selected": len(sel),
+            "first_call_s": round(first_s, 4), "cache_build_ms": round(first.get("k_pv_extract", 0.0), 4),
+            "call_s": round(call_s, 5), "files_per_s": round(n / call_s, 1),
+            "roofline": {"bound": "hbm", "kernel": "k_filter_typed", "avg_launch_ms": round(kt, 4) if kt else None,
+                         "algo_bytes": algo, "achieved": round(algo / (kt * 1e-3) / 1e9, 1) if kt else None,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(algo / (kt * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if kt else None},
+            "kernels": {k: round(v, 4) for k, v in ms.items()}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -189,13 +233,12 @@ def main():
     from delta_amd.delta_log import Engine
     from delta_amd.testing import synth as S
 
-    seed = S.BASE_SEED + args.config
     table = os.path.join(args.workdir, "c%d_s%g" % (args.config, args.scale))
     if rank == 0:
-        exp = build_table(table, args.config, args.scale, seed)
+        exp = build_table(table, args.config, args.scale)
     if dist:
         dist.barrier()
-    exp = build_table(table, args.config, args.scale, seed)
+    exp = build_table(table, args.config, args.scale)
     eng = Engine.get(local)
     log_path = os.path.join(table, "_delta_log")
     cutoff = exp["min_file_retention_timestamp"]
@@ -297,7 +340,7 @@ def main():
     }
     cpu = None
     if not args.no_cpu_baseline and world == 1:
-        cpu = cpu_baseline(log_path, cutoff, counts, args.cpu_threads)
+        cpu = cpu_baseline(log_path, cutoff, counts, args.cpu_threads, one_core=args.config != 4)
     # end to end once: file bytes -> HBM (read + H2D + page planning), replay, allFiles export
     e2e = None
     if world == 1:
@@ -308,14 +351,15 @@ def main():
         st.release()
         e2e = {"stage_s": round(stage_s, 3), "replay_s": round(t2 - t1, 4),
                "actions_per_s_incl_staging": round(counts["num_actions"] / (stage_s + t2 - t1), 1)}
+    k5 = None
+    if world == 1 and args.config == 4:
+        k5 = measure_filter(eng, staged, cutoff, exp, args.steps)
     out = {
         "metric": "log actions replayed/sec + achieved HBM GB/s, 1/2/4/8 GPU, 10M-file table",
         "value": round(value, 1), "unit": "actions/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "u8/int64", "data": "synthetic",
-        "config": {"workload": "config %d: checkpoint + JSON commits, %d actions -> %d live files, "
-                               "30%% remove/re-add churn, retention cutoff" % (args.config, counts["num_actions"],
-                                                                             counts["num_files"]),
+        "config": {"workload": WORKLOAD.get(args.config, "config %d") % (counts["num_actions"], counts["num_files"]),
                    "scale": args.scale, "actions": counts["num_actions"],
                    "json_bytes": exp["json_bytes"], "checkpoint_bytes": exp["checkpoint_bytes"],
                    "parallelism": ("path-hash shards over %d GPUs (%s all-to-all)"
@@ -325,6 +369,7 @@ def main():
         "pipelines": pipelines,
         "cpu_baseline": cpu,
         "end_to_end": e2e,
+        "k5_filter": k5,
         "kernels": kernels,
         "result": {k: counts[k] for k in ("num_files", "num_removes", "size_in_bytes", "live_key_sum",
                                           "tomb_key_sum")},

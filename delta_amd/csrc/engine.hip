@@ -335,6 +335,19 @@ struct dr_state {
   std::string nonfile_json;
   std::vector<NonFileAction> nonfile;  // winners: protocol, metadata, txns
   ExportCols exp[2];
+  // K5 cache: partition columns of the live AddFiles cast to their types (k_pv_extract), built on
+  // the first dr_filter that references each (name, type) and reused by every later one
+  struct PvCol {
+    std::string name;
+    int32_t type;
+    DBuf<uint32_t> w32;
+    DBuf<int64_t> w64;
+    DBuf<uint64_t> sptr;
+    DBuf<uint32_t> slen;
+    DBuf<uint8_t> isnull;
+  };
+  std::vector<std::unique_ptr<PvCol>> pv_cols;
+  std::vector<std::shared_ptr<DBuf<uint8_t>>> pv_arenas;  // unescaped string values
 };
 
 // ---------------------------------------------------------------------------------------------------
@@ -1531,37 +1544,37 @@ static DBuf<T> upload(dr_ctx* ctx, const T* src, size_t n) {
   return d;
 }
 
-static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred) {
-  check_program(pred);
+// Builds the K5 cache columns `want` (name, type) of st's live AddFiles in one k_pv_extract pass.
+static void build_pv_columns(dr_state& st, const std::vector<std::pair<std::string, int32_t>>& want) {
   dr_ctx* ctx = st.ctx;
-  ctx->begin_call();
   hipStream_t stream = ctx->stream;
-  if (st.sources.empty()) fail(DR_E_INVALID_ARG, "state has no staged segment");
   StagedData& s = *st.sources[0];
   const uint64_t R = s.ck_rows;
-  FilterArgs fa{};
-  fa.live = st.live.p;
-  fa.n_live = st.n_live;
-  fa.src_off = st.src_off.p;
-  fa.src_len = st.src_len.p;
-  fa.ck_rows = R;
-  fa.json = s.d_json.p;
+  const uint64_t n = st.n_live;
+  PvExtractArgs a{};
+  a.live = st.live.p;
+  a.n_live = n;
+  a.src_off = st.src_off.p;
+  a.src_len = st.src_len.p;
+  a.ck_rows = R;
+  a.json = s.d_json.p;
   DBuf<uint64_t> json_bases;
   if (st.src_id.p) {
     std::vector<uint64_t> bases;
     for (auto& src : st.sources) bases.push_back(reinterpret_cast<uint64_t>(src->d_json.p));
     json_bases = upload(ctx, bases.data(), bases.size());
-    fa.act_flags = st.flags.p;
-    fa.src_id = st.src_id.p;
-    fa.json_bases = json_bases.p;
+    a.act_flags = st.flags.p;
+    a.src_id = st.src_id.p;
+    a.json_bases = json_bases.p;
   }
-  // checkpoint side: decode the add.partitionValues map columns (planned once per staged segment)
+  // checkpoint side: decode the add.partitionValues map columns (planned once per staged segment;
+  // the decoded entries are freed once the typed columns are built)
   DBuf<uint8_t> kdef, krep, vdef, vrep;
   DBuf<uint64_t> kptr, vptr, row_start, dict_ptr, rpos;
   DBuf<uint32_t> klen, vlen, dict_len, pq_err(ctx, 1), rflag;
   DBuf<uint8_t> scratch(ctx, scan_scratch_for(0));
   pq_err.zero(stream);
-  if (R && st.n_live) {
+  if (R && n) {
     {
       std::lock_guard<std::mutex> g(s.pv_mu);
       if (!s.pv) {
@@ -1583,6 +1596,7 @@ static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred)
       pa.ncols = 2;
       pa.cols[0] = FlatColumn{kdef.p, krep.p, nullptr, kptr.p, klen.p};
       pa.cols[1] = FlatColumn{vdef.p, vrep.p, nullptr, vptr.p, vlen.p};
+      if (scratch.n < scan_scratch_for(E)) scratch = DBuf<uint8_t>(ctx, scan_scratch_for(E));
       decode_pages(ctx, P, pa, dict_ptr, dict_len, pq_err, scratch.p);
       if (d2h_one(pq_err.p, stream) != 0)
         fail(DR_E_PARQUET, fmt("device decode of add.partitionValues failed (code %u)", d2h_one(pq_err.p, stream)));
@@ -1594,36 +1608,107 @@ static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred)
       row_start = DBuf<uint64_t>(ctx, R + 1);
       launch_row_starts(krep.p, E, rpos.p, row_start.p, stream);
       HIP_OK(hipMemcpyAsync(row_start.p + R, &E, 8, hipMemcpyHostToDevice, stream));
-      fa.has_map = 1;
-      fa.row_start = row_start.p;
-      fa.key_def = kdef.p; fa.key_ptr = kptr.p; fa.key_len = klen.p; fa.key_max_def = P.max_def[0];
-      fa.val_def = vdef.p; fa.val_ptr = vptr.p; fa.val_len = vlen.p; fa.val_max_def = P.max_def[1];
+      a.has_map = 1;
+      a.row_start = row_start.p;
+      a.key_def = kdef.p; a.key_ptr = kptr.p; a.key_len = klen.p; a.key_max_def = P.max_def[0];
+      a.val_def = vdef.p; a.val_ptr = vptr.p; a.val_len = vlen.p; a.val_max_def = P.max_def[1];
     }
   }
-  // program
-  std::vector<uint64_t> name_off(size_t(pred.ncols) + 1, 0);
+  std::vector<uint64_t> name_off(want.size() + 1, 0);
   std::string names;
+  for (size_t c = 0; c < want.size(); ++c) {
+    names += want[c].first;
+    name_off[c + 1] = names.size();
+  }
+  DBuf<uint64_t> d_name_off = upload(ctx, name_off.data(), name_off.size());
+  DBuf<uint8_t> d_names = upload(ctx, reinterpret_cast<const uint8_t*>(names.data()), names.size());
+  a.ncols = int32_t(want.size());
+  a.col_name_off = d_name_off.p;
+  a.col_names = d_names.p;
+  std::vector<std::unique_ptr<dr_state::PvCol>> made;
+  for (size_t c = 0; c < want.size(); ++c) {
+    auto col = std::make_unique<dr_state::PvCol>();
+    col->name = want[c].first;
+    col->type = want[c].second;
+    col->isnull = DBuf<uint8_t>(ctx, n);
+    PvColumn& pc = a.cols[c];
+    pc.type = col->type;
+    pc.isnull = col->isnull.p;
+    if (col->type == DR_T_STRING) {
+      col->sptr = DBuf<uint64_t>(ctx, n);
+      col->slen = DBuf<uint32_t>(ctx, n);
+      pc.sptr = col->sptr.p;
+      pc.slen = col->slen.p;
+    } else if (col->type == DR_T_LONG) {
+      col->w64 = DBuf<int64_t>(ctx, n);
+      pc.w64 = col->w64.p;
+    } else {
+      col->w32 = DBuf<uint32_t>(ctx, n);
+      pc.w32 = col->w32.p;
+    }
+    made.push_back(std::move(col));
+  }
+  DBuf<unsigned long long> ctr(ctx, 2);  // 0 arena fill, 1 arena need
+  DBuf<uint32_t> ferr(ctx, 1);
+  ctr.zero(stream);
+  ferr.zero(stream);
+  a.arena_fill = ctr.p;
+  a.arena_need = ctr.p + 1;
+  a.error = ferr.p;
+  launch_pv_extract(a, stream);
+  const unsigned long long need = d2h_one(ctr.p + 1, stream);
+  if (need) {  // some partition values carry JSON escapes: unescape them into an arena and rerun
+    auto arena = std::make_shared<DBuf<uint8_t>>(ctx, need + 64);
+    a.arena = arena->p;
+    a.arena_cap = need + 64;
+    launch_pv_extract(a, stream);
+    st.pv_arenas.push_back(arena);
+  }
+  const uint32_t e = d2h_one(ferr.p, stream);
+  if (e & 1u) fail(DR_E_PARSE, "malformed add.partitionValues in a live AddFile's JSON line");
+  if (e & 2u) fail(DR_E_INTERNAL, "partition value arena overflow");
+  for (auto& c : made) st.pv_cols.push_back(std::move(c));
+}
+
+static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred) {
+  check_program(pred);
+  dr_ctx* ctx = st.ctx;
+  ctx->begin_call();
+  hipStream_t stream = ctx->stream;
+  if (st.sources.empty()) fail(DR_E_INVALID_ARG, "state has no staged segment");
+  // the predicate's columns in the K5 cache (built for the ones not there yet)
+  auto find = [&](const std::string& name, int32_t type) -> dr_state::PvCol* {
+    for (auto& c : st.pv_cols)
+      if (c->name == name && c->type == type) return c.get();
+    return nullptr;
+  };
+  std::vector<std::pair<std::string, int32_t>> want;
   for (int32_t c = 0; c < pred.ncols; ++c) {
-    names += pred.col_names[c];
-    name_off[size_t(c) + 1] = names.size();
+    std::pair<std::string, int32_t> k{pred.col_names[c], pred.col_types[c]};
+    if (!find(k.first, k.second) && std::find(want.begin(), want.end(), k) == want.end()) want.push_back(k);
+  }
+  if (!want.empty() && st.n_live) build_pv_columns(st, want);
+  FilterTypedArgs fa{};
+  fa.n_live = st.n_live;
+  fa.ncols = pred.ncols;
+  for (int32_t c = 0; c < pred.ncols; ++c) {
+    dr_state::PvCol* col = find(pred.col_names[c], pred.col_types[c]);
+    if (!col) {  // no live files: nothing was built
+      fa.cols[c].type = pred.col_types[c];
+      continue;
+    }
+    fa.cols[c] = PvColumn{col->type, col->w32.p, col->w64.p, col->sptr.p, col->slen.p, col->isnull.p};
   }
   const std::vector<int32_t> ops = lower_program(pred);
   std::vector<uint64_t> lit_off(size_t(pred.nlits) + 1, 0);
   for (int32_t k = 0; k <= pred.nlits && pred.nlits; ++k) lit_off[size_t(k)] = uint64_t(pred.lit_str_off[k]);
   const uint64_t lit_bytes = pred.nlits ? lit_off[size_t(pred.nlits)] : 0;
-  DBuf<uint64_t> d_name_off = upload(ctx, name_off.data(), name_off.size());
-  DBuf<uint8_t> d_names = upload(ctx, reinterpret_cast<const uint8_t*>(names.data()), names.size());
-  DBuf<int32_t> d_types = upload(ctx, pred.col_types, size_t(pred.ncols));
   DBuf<int32_t> d_ops = upload(ctx, ops.data(), ops.size());
   DBuf<int32_t> d_lt = upload(ctx, pred.lit_types, size_t(pred.nlits));
   DBuf<int64_t> d_li = upload(ctx, pred.lit_i64, size_t(pred.nlits));
   DBuf<uint8_t> d_ln = upload(ctx, pred.lit_null, size_t(pred.nlits));
   DBuf<uint64_t> d_lo = upload(ctx, lit_off.data(), lit_off.size());
   DBuf<uint8_t> d_ls = upload(ctx, pred.lit_str_bytes, size_t(lit_bytes));
-  fa.ncols = pred.ncols;
-  fa.col_name_off = d_name_off.p;
-  fa.col_names = d_names.p;
-  fa.col_types = d_types.p;
   fa.nops = int32_t(ops.size() / 2);
   fa.ops = d_ops.p;
   fa.lit_types = d_lt.p;
@@ -1631,33 +1716,16 @@ static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred)
   fa.lit_null = d_ln.p;
   fa.lit_str_off = d_lo.p;
   fa.lit_str = d_ls.p;
-  DBuf<unsigned long long> ctr(ctx, 2);  // 0 arena fill, 1 arena need
-  DBuf<uint32_t> ferr(ctx, 1), flag(ctx, st.n_live);
-  ctr.zero(stream);
-  ferr.zero(stream);
-  fa.arena_fill = ctr.p;
-  fa.arena_need = ctr.p + 1;
+  DBuf<uint32_t> flag(ctx, st.n_live);
   fa.flag = flag.p;
-  fa.error = ferr.p;
-  launch_filter(fa, stream);
-  const unsigned long long need = d2h_one(ctr.p + 1, stream);
-  DBuf<uint8_t> arena;
-  if (need) {  // some partition values carry JSON escapes: unescape them into an arena and rerun
-    arena = DBuf<uint8_t>(ctx, need + 64);
-    fa.arena = arena.p;
-    fa.arena_cap = need + 64;
-    launch_filter(fa, stream);
-  }
-  const uint32_t e = d2h_one(ferr.p, stream);
-  if (e & 1u) fail(DR_E_PARSE, "malformed add.partitionValues in a live AddFile's JSON line");
-  if (e & 2u) fail(DR_E_INTERNAL, "partition value arena overflow");
+  launch_filter_typed(fa, stream);
+  DBuf<uint8_t> scratch(ctx, scan_scratch_for(st.n_live));
   DBuf<uint64_t> pos(ctx, st.n_live + 1);
   launch_scan_u32(flag.p, pos.p, st.n_live, scratch.p, stream);
-  const uint64_t nsel = d2h_one(pos.p + st.n_live, stream);
+  const uint64_t nsel = st.n_live ? d2h_one(pos.p + st.n_live, stream) : 0;
   DBuf<int64_t> sel(ctx, nsel);
   launch_select(flag.p, pos.p, st.n_live, sel.p, stream);
   std::vector<int64_t> out = d2h(sel.p, nsel, stream);
-  ctx->mark("filter");
   ctx->collect_timings();
   return out;
 }

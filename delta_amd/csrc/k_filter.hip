@@ -3,11 +3,13 @@
 // reference becomes Cast(partitionValues[col] AS partitionSchema(col).type), the conjuncts are
 // ANDed, and a file is kept where the predicate is TRUE (three-valued logic; NULL drops it).
 //
-// One thread per live file: it locates the file's partition values -- in its JSON line
-// (`add.partitionValues` object, resident in d_json) or in the checkpoint's decoded
-// `add.partitionValues` map column (entries of its row) -- casts them with Spark 3.1's non-ANSI
-// Cast(string AS type) as restated by the oracle (oracle/delta_oracle.py:cast_string), and runs the
-// postfix predicate program (include/deltareplay.h, dr_pred_op).
+// k_pv_extract (once per state and partition column, cached on the state): one thread per live
+// file locates the file's partition values -- in its JSON line (`add.partitionValues` object,
+// resident in d_json) or in the checkpoint's decoded `add.partitionValues` map column (entries of
+// its row) -- and casts them with Spark 3.1's non-ANSI Cast(string AS type) as restated by the
+// oracle (oracle/delta_oracle.py:cast_string) into typed columns.
+// k_filter_typed (per dr_filter): one thread per live file runs the postfix predicate program
+// (include/deltareplay.h, dr_pred_op) over the typed columns.
 #include "dev_common.h"
 #include "kernels.h"
 #include "../../include/deltareplay.h"
@@ -241,10 +243,10 @@ __device__ int cmp_sv(const SV& a, const SV& b) {
   return a.v == b.v ? 0 : (a.v < b.v ? -1 : 1);
 }
 
-constexpr int PV_MAXC = 16;
 constexpr int PV_STACK = 32;
 
-__global__ void __launch_bounds__(256) k_filter(FilterArgs a) {
+// ---- k_pv_extract --------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_pv_extract(PvExtractArgs a) {
   const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= a.n_live) return;
   const uint32_t act = a.live[i];
@@ -321,7 +323,40 @@ __global__ void __launch_bounds__(256) k_filter(FilterArgs a) {
       }
     }
   }
-  // ---- postfix program ----
+  for (int c = 0; c < a.ncols; ++c) {
+    const PvColumn& col = a.cols[c];
+    const SV v = cast_value(vp[c], vn[c], vs[c] != PV_NULL, col.type);
+    col.isnull[i] = v.null;
+    if (col.type == DR_T_STRING) {
+      col.sptr[i] = reinterpret_cast<uint64_t>(v.s);
+      col.slen[i] = v.n;
+    } else if (col.type == DR_T_LONG) {
+      col.w64[i] = v.v;
+    } else {
+      col.w32[i] = uint32_t(int32_t(v.v));
+    }
+  }
+}
+
+// ---- k_filter_typed ------------------------------------------------------------------------------
+__device__ __forceinline__ SV load_col(const PvColumn& col, uint64_t i) {
+  SV r{0, nullptr, 0, col.isnull[i], 0};
+  if (r.null) return r;
+  if (col.type == DR_T_STRING) {
+    r.str = 1;
+    r.s = reinterpret_cast<const uint8_t*>(col.sptr[i]);
+    r.n = col.slen[i];
+  } else if (col.type == DR_T_LONG) {
+    r.v = col.w64[i];
+  } else {
+    r.v = int64_t(int32_t(col.w32[i]));
+  }
+  return r;
+}
+
+__global__ void __launch_bounds__(256) k_filter_typed(FilterTypedArgs a) {
+  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= a.n_live) return;
   SV st[PV_STACK];
   int sp = 0;
   bool bad = false;
@@ -329,7 +364,7 @@ __global__ void __launch_bounds__(256) k_filter(FilterArgs a) {
     const int op = a.ops[2 * k], arg = a.ops[2 * k + 1];
     switch (op) {
       case DR_OP_COL: {
-        st[sp++] = cast_value(vp[arg], vn[arg], vs[arg] != PV_NULL, a.col_types[arg]);
+        st[sp++] = load_col(a.cols[arg], i);
         break;
       }
       case DR_OP_LIT: {
@@ -443,11 +478,14 @@ __global__ void k_select(const uint32_t* flag, const uint64_t* pos, uint64_t n, 
 
 static inline unsigned g256(uint64_t n) { return unsigned((n + 255) / 256); }
 
-uint32_t filter_max_cols() { return dev::PV_MAXC; }
+uint32_t filter_max_cols() { return PV_MAXC; }
 uint32_t filter_max_stack() { return dev::PV_STACK; }
 
-void launch_filter(const FilterArgs& a, hipStream_t st) {
-  if (a.n_live) DR_LAUNCH(dev::k_filter, dim3(g256(a.n_live)), dim3(256), 0, st, a);
+void launch_pv_extract(const PvExtractArgs& a, hipStream_t st) {
+  if (a.n_live) DR_LAUNCH(dev::k_pv_extract, dim3(g256(a.n_live)), dim3(256), 0, st, a);
+}
+void launch_filter_typed(const FilterTypedArgs& a, hipStream_t st) {
+  if (a.n_live) DR_LAUNCH(dev::k_filter_typed, dim3(g256(a.n_live)), dim3(256), 0, st, a);
 }
 void launch_rep0_flags(const uint8_t* rep, uint64_t n, uint32_t* f, hipStream_t st) {
   if (n) DR_LAUNCH(dev::k_rep0_flags, dim3(g256(n)), dim3(256), 0, st, rep, n, f);

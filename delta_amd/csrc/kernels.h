@@ -325,7 +325,19 @@ void launch_verdict_collect(const uint8_t* verdict, const uint32_t* send_idx, ui
                             const uint64_t* pos, uint32_t* out, hipStream_t st);
 
 // ---- K5: partition pruning (k_filter.hip) -------------------------------------------------------
-struct FilterArgs {
+// Two kernels: k_pv_extract builds, once per state and partition column, the column's values cast to
+// the column type for every live AddFile (the state's K5 cache); k_filter_typed evaluates a
+// predicate program over those typed columns, so a filter reads 4-12 B per file and column.
+constexpr int PV_MAXC = 16;
+struct PvColumn {
+  int32_t type;        // dr_pred_type
+  uint32_t* w32;       // BYTE / SHORT / INT / DATE (days) / BOOLEAN (0/1)
+  int64_t* w64;        // LONG
+  uint64_t* sptr;      // STRING: address of the (unescaped) value bytes
+  uint32_t* slen;
+  uint8_t* isnull;     // 1: NULL (absent, JSON null, or a failed non-ANSI cast)
+};
+struct PvExtractArgs {
   const uint32_t* live;          // live AddFile action indices (export order)
   uint64_t n_live;
   const uint64_t* src_off;       // JSON: line offset; checkpoint: row
@@ -348,32 +360,38 @@ struct FilterArgs {
   const uint64_t* val_ptr;
   const uint32_t* val_len;
   int32_t val_max_def;
-  // predicate program (include/deltareplay.h dr_predicate, uploaded)
+  // the columns to build (names = exact map keys)
   int32_t ncols;
   const uint64_t* col_name_off;  // [ncols + 1]
   const uint8_t* col_names;
-  const int32_t* col_types;
-  int32_t nops;
-  const int32_t* ops;            // [nops * 2] opcode, arg
-  const int32_t* lit_types;
-  const int64_t* lit_i64;
-  const uint8_t* lit_null;
-  const uint64_t* lit_str_off;   // [nlits + 1]
-  const uint8_t* lit_str;
+  PvColumn cols[PV_MAXC];
   // unescaped JSON values (null arena: count the bytes needed into arena_need)
   uint8_t* arena;
   uint64_t arena_cap;
   unsigned long long* arena_fill;
   unsigned long long* arena_need;
-  uint32_t* flag;                // [n_live] 1 = selected
   uint32_t* error;
+};
+struct FilterTypedArgs {
+  uint64_t n_live;
+  int32_t ncols;
+  PvColumn cols[PV_MAXC];        // predicate column k -> its typed cache column
+  int32_t nops;
+  const int32_t* ops;            // [nops * 2] opcode, arg (lowered program)
+  const int32_t* lit_types;
+  const int64_t* lit_i64;
+  const uint8_t* lit_null;
+  const uint64_t* lit_str_off;   // [nlits + 1]
+  const uint8_t* lit_str;
+  uint32_t* flag;                // [n_live] 1 = selected
 };
 // device-only opcodes of the lowered program (engine.hip lower_program): an IN list is folded
 // one element at a time into an accumulator slot above its value
 enum : int32_t { FILTER_OP_IN_START = 100, FILTER_OP_IN_STEP = 101, FILTER_OP_IN_END = 102 };
 uint32_t filter_max_cols();
 uint32_t filter_max_stack();
-void launch_filter(const FilterArgs& a, hipStream_t st);
+void launch_pv_extract(const PvExtractArgs& a, hipStream_t st);
+void launch_filter_typed(const FilterTypedArgs& a, hipStream_t st);
 void launch_rep0_flags(const uint8_t* rep, uint64_t n, uint32_t* f, hipStream_t st);
 void launch_row_starts(const uint8_t* rep, uint64_t n, const uint64_t* pos, uint64_t* row_start, hipStream_t st);
 void launch_select(const uint32_t* flag, const uint64_t* pos, uint64_t n, int64_t* out, hipStream_t st);

@@ -229,16 +229,18 @@ def delta_name(v: int) -> str:
 def write_checkpoint(path: str, pool: FilePool, add_ids: np.ndarray, ncols: int, version: int,
                      with_parsed: bool = False, row_group_size: int = 1 << 20,
                      data_page_size: int = 1 << 20, compression: str = "snappy",
-                     data_page_version: str = "1.0", use_dictionary: bool = True) -> int:
-    """Rows: protocol, metaData, then one `add` per id. Returns the row count."""
+                     data_page_version: str = "1.0", use_dictionary: bool = True, head: bool = True) -> int:
+    """Rows: protocol, metaData (unless `head` is false: later parts of a multi-part checkpoint),
+    then one `add` per id. Returns the row count."""
     pa, pc = _pa()
     import pyarrow.parquet as pq
 
     n = len(add_ids)
-    nrows = n + 2
+    h = 2 if head else 0
+    nrows = n + h
     mt = pa.map_(pa.string(), pa.string())
-    add_valid = np.concatenate([[False, False], np.ones(n, bool)])
-    null2 = pa.nulls(2, pa.string())
+    add_valid = np.concatenate([np.zeros(h, bool), np.ones(n, bool)])
+    null2 = pa.nulls(h, pa.string())
     paths = pa.concat_arrays([null2, _flat(pool.paths(add_ids))])
     stats = pa.concat_arrays([null2, _flat(pool.stats(add_ids))])
     # partitionValues map: keys/items interleaved per row
@@ -251,9 +253,9 @@ def write_checkpoint(path: str, pool: FilePool, add_ids: np.ndarray, ncols: int,
     inter = (np.arange(n)[:, None] + np.arange(ncols)[None, :] * n).ravel()
     items = allv.take(pa.array(inter))
     keys = pa.array(np.tile(np.array(cols, dtype=object), n), pa.string())
-    offs = np.concatenate([[0, 0], np.arange(n + 1) * ncols]).astype(np.int32)
+    offs = np.concatenate([np.zeros(h, np.int64), np.arange(n + 1) * ncols]).astype(np.int32)
     pv_arr = pa.MapArray.from_arrays(pa.array(offs), keys, items)
-    zeros2 = np.zeros(2, np.int64)
+    zeros2 = np.zeros(h, np.int64)
     add_fields = [
         paths, pv_arr,
         pa.array(np.concatenate([zeros2, pool.size[add_ids]]), pa.int64()),
@@ -269,14 +271,14 @@ def write_checkpoint(path: str, pool: FilePool, add_ids: np.ndarray, ncols: int,
         parsed_arrays, parsed_fields = [], []
         for c in cols:
             if c == "p0":
-                arr = pa.array(np.concatenate([[0, 0], pool.p0[add_ids] + 18262]).astype(np.int32), pa.date32())
+                arr = pa.array(np.concatenate([zeros2, pool.p0[add_ids] + 18262]).astype(np.int32), pa.date32())
             elif c == "p1":
-                arr = pa.array(np.concatenate([[0, 0], pool.p1[add_ids]]).astype(np.int32), pa.int32())
+                arr = pa.array(np.concatenate([zeros2, pool.p1[add_ids]]).astype(np.int32), pa.int32())
             elif c == "p2":
                 arr = pa.concat_arrays([null2, _flat(pc.if_else(pa.array(pool.p2null[add_ids]),
                                                                 pa.scalar(None, pa.string()), pool.p2_s(add_ids, "")))])
             else:
-                arr = pa.array(np.concatenate([[0, 0], pool.p3[add_ids]]).astype(bool), pa.bool_())
+                arr = pa.array(np.concatenate([zeros2, pool.p3[add_ids]]).astype(bool), pa.bool_())
             parsed_arrays.append(arr)
             parsed_fields.append(pa.field(c, arr.type))
         add_fields.append(pa.StructArray.from_arrays(parsed_arrays, fields=parsed_fields))
@@ -299,10 +301,13 @@ def write_checkpoint(path: str, pool: FilePool, add_ids: np.ndarray, ncols: int,
                       "format": {"provider": "parquet", "options": []},
                       "schemaString": md["schemaString"], "partitionColumns": md["partitionColumns"],
                       "configuration": [], "createdTime": md["createdTime"]}]
-    md_struct = pa.concat_arrays([pa.array(md_rows, md_type), pa.nulls(n, md_type)])
     prot_type = pa.struct([("minReaderVersion", pa.int32()), ("minWriterVersion", pa.int32())])
-    prot_struct = pa.concat_arrays([pa.array([{"minReaderVersion": 1, "minWriterVersion": 2}], prot_type),
-                                    pa.nulls(n + 1, prot_type)])
+    if head:
+        md_struct = pa.concat_arrays([pa.array(md_rows, md_type), pa.nulls(n, md_type)])
+        prot_struct = pa.concat_arrays([pa.array([{"minReaderVersion": 1, "minWriterVersion": 2}], prot_type),
+                                        pa.nulls(n + 1, prot_type)])
+    else:
+        md_struct, prot_struct = pa.nulls(n, md_type), pa.nulls(n, prot_type)
     table = pa.Table.from_arrays([pa.nulls(nrows, txn_type), add_struct, pa.nulls(nrows, rm_type),
                                   md_struct, prot_struct],
                                  names=["txn", "add", "remove", "metaData", "protocol"])
@@ -385,12 +390,26 @@ class ChurnSpec:
     ncols: int = 2
     n_at_cutoff: int = 0       # removes placed exactly at the cutoff (must be dropped)
     init_adds: int = 0         # no-checkpoint mode: adds in v0 (with protocol+metadata)
+    ckpt_parts: int = 1        # > 1: a multi-part checkpoint (FileNames.checkpointFileWithParts)
+
+
+_FORK_STATE = None
+
+
+def _write_parts_worker(job):
+    """One worker of build_table's parallel multi-part checkpoint write (forked: the pool is shared)."""
+    pool, ids, per, kw = _FORK_STATE
+    out = []
+    for k, cp in job:
+        out.append((k, write_checkpoint(cp, pool, ids[k * per:(k + 1) * per], head=k == 0, **kw),
+                    os.path.getsize(cp)))
+    return out
 
 
 def build_table(table_dir: str, spec: ChurnSpec, seed: int, checkpoint_with_parsed=False,
                 data_page_size: int = 1 << 20, keep_ids: bool = True, compression: str = "snappy",
                 data_page_version: str = "1.0", row_group_size: int = 1 << 20,
-                use_dictionary: bool = True) -> Expected:
+                use_dictionary: bool = True, workers: int = 1) -> Expected:
     rng = np.random.default_rng(seed)
     log = os.path.join(table_dir, "_delta_log")
     os.makedirs(log, exist_ok=True)
@@ -407,16 +426,32 @@ def build_table(table_dir: str, spec: ChurnSpec, seed: int, checkpoint_with_pars
         ids = np.arange(spec.ckpt_files)
         next_id = spec.ckpt_files
         state[ids] = 1
-        cp = os.path.join(log, "%020d.checkpoint.parquet" % version)
-        nrows = write_checkpoint(cp, pool, ids, spec.ncols, version, with_parsed=checkpoint_with_parsed,
-                                 data_page_size=data_page_size, compression=compression,
-                                 data_page_version=data_page_version, row_group_size=row_group_size,
-                                 use_dictionary=use_dictionary)
-        ckpt_bytes += os.path.getsize(cp)
+        parts = max(1, spec.ckpt_parts)
+        nrows = 0
+        per = (spec.ckpt_files + parts - 1) // parts
+        kw = dict(ncols=spec.ncols, version=version, with_parsed=checkpoint_with_parsed,
+                  data_page_size=data_page_size, compression=compression, data_page_version=data_page_version,
+                  row_group_size=row_group_size, use_dictionary=use_dictionary)
+        names = [os.path.join(log, "%020d.checkpoint.parquet" % version if parts == 1 else
+                              "%020d.checkpoint.%010d.%010d.parquet" % (version, k + 1, parts))
+                 for k in range(parts)]
+        jobs = [[(k, names[k]) for k in range(w, parts, max(1, workers))] for w in range(max(1, workers))]
+        global _FORK_STATE
+        _FORK_STATE = (pool, ids, per, kw)
+        if workers > 1 and parts > 1:
+            import multiprocessing as mp
+            with mp.get_context("fork").Pool(min(workers, parts)) as P:
+                results = [r for rs in P.map(_write_parts_worker, [j for j in jobs if j]) for r in rs]
+        else:
+            results = _write_parts_worker([(k, names[k]) for k in range(parts)])
+        _FORK_STATE = None
+        for _, rows, size in results:
+            nrows += rows
+            ckpt_bytes += size
         n_actions += nrows
         n_file_actions += spec.ckpt_files
         with open(os.path.join(log, "_last_checkpoint"), "w") as f:
-            f.write('{"version":%d,"size":%d}\n' % (version, nrows))
+            f.write('{"version":%d,"size":%d%s}\n' % (version, nrows, ',"parts":%d' % parts if parts > 1 else ""))
         # an earlier commit at the checkpoint version (listed, not replayed)
         with open(os.path.join(log, delta_name(version)), "w") as f:
             f.write(commit_info_line(version) + "\n")
@@ -491,9 +526,10 @@ def config_spec(config: int, scale: float = 1.0) -> ChurnSpec:
         return ChurnSpec(ckpt_files=s(10_000_000), ckpt_version=1000, n_deltas=30,
                          removes_per_delta=s(100_000), adds_per_delta=s(100_000), readd_frac=0.5,
                          ncols=2, n_at_cutoff=min(1000, s(1000)))
-    if config == 4:
-        return ChurnSpec(ckpt_files=s(100_000_000), ckpt_version=1000, n_deltas=0,
-                         removes_per_delta=0, adds_per_delta=0, readd_frac=0.0, ncols=4)
+    if config == 4:  # 100 parts of 1M rows at full scale (at least 2 parts when scaled down)
+        files = s(100_000_000)
+        return ChurnSpec(ckpt_files=files, ckpt_version=1000, n_deltas=0, removes_per_delta=0, adds_per_delta=0,
+                         readd_frac=0.0, ncols=4, ckpt_parts=min(100, max(2, files // 1000)))
     raise ValueError(config)
 
 
@@ -501,3 +537,38 @@ def build_config(config: int, table_dir: str, scale: float = 1.0, seed: Optional
                  **kw) -> Expected:
     seed = BASE_SEED + config if seed is None else seed
     return build_table(table_dir, config_spec(config, scale), seed, **kw)
+
+
+def config4_selected(table_dir: str, scale: float = 1.0, seed: Optional[int] = None) -> int:
+    """Files config 4's predicate keeps: p0 >= DATE'2020-03-01' AND p0 < DATE'2020-06-01'
+    AND p1 IN (1..100) AND p2 = 'w17' AND p3 = true, counted from the generator's pool by construction."""
+    seed = BASE_SEED + 4 if seed is None else seed
+    spec = config_spec(4, scale)
+    pool = FilePool(np.random.default_rng(seed), spec.ckpt_files, spec.ncols)
+    keep = ((pool.p0 >= 60) & (pool.p0 < 152) & (pool.p1 >= 1) & (pool.p1 <= 100) & (pool.p2 == 17)
+            & ~pool.p2null & (pool.p3 == 1))
+    return int(keep.sum())
+
+
+def config4_predicate():
+    """Config 4's filter as conjuncts in the predicate-tree form of delta_amd/predicates.py."""
+    col = lambda c: ("col", c)
+    lit = lambda t, v: ("lit", t, v)
+    return [(">=", col("p0"), lit("date", "2020-03-01")), ("<", col("p0"), lit("date", "2020-06-01")),
+            ("in", col("p1"), [lit("integer", v) for v in range(1, 101)]), ("=", col("p2"), lit("string", WORDS[17])),
+            ("=", col("p3"), lit("boolean", True))]
+
+
+if __name__ == "__main__":  # python -m delta_amd.testing.synth <config> <table_dir> [scale] [workers]
+    import sys
+    cfg, out = int(sys.argv[1]), sys.argv[2]
+    sc = float(sys.argv[3]) if len(sys.argv) > 3 else 1.0
+    nw = int(sys.argv[4]) if len(sys.argv) > 4 else 1
+    e = build_config(cfg, out, scale=sc, keep_ids=False, workers=nw)
+    d = {k: getattr(e, k) for k in ("version", "min_file_retention_timestamp", "num_files", "size_in_bytes",
+                                    "num_removes", "num_actions", "num_file_actions", "json_bytes", "checkpoint_bytes")}
+    if cfg == 4:
+        d["selected"] = config4_selected(out, sc)
+    with open(os.path.join(out, "expected.json"), "w") as f:
+        json.dump(d, f)
+    print(json.dumps(d))

@@ -731,7 +731,16 @@ static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_
       const unsigned long long nreg = d2h_one(P.s_region_count.p, stream);
       std::vector<uint32_t> pb = d2h(P.s_pages_bad.p, P.snap_pages.size(), stream);
       size_t nb = 0;
-      for (uint32_t v : pb) nb += v != 0;
+      std::map<uint32_t, size_t> why;
+      for (size_t q = 0; q < pb.size(); ++q) {
+        nb += pb[q] != 0;
+        if (pb[q]) {
+          if (why[pb[q]]++ < 3)
+            std::fprintf(stderr, "snappy bad page %zu code %u: n_in %u n_out %u\n", q, pb[q],
+                         P.snap_pages[q].n_in, P.snap_pages[q].n_out);
+        }
+      }
+      for (auto& kv : why) std::fprintf(stderr, "snappy bad code %u: %zu pages\n", kv.first, kv.second);
       const size_t nr = size_t(nreg);
       std::fprintf(stderr, "snappy: pages %zu serially resolved regions %zu bad %zu\n", P.snap_pages.size(), nr, nb);
     }
@@ -1537,6 +1546,114 @@ static std::vector<int32_t> lower_program(const dr_predicate& p) {
   return out;
 }
 
+// Leaf form of a program (k_filter_leaf) when every comparison is between one partition column and
+// literals of its kind and the rest is AND / OR / NOT: each leaf is evaluated straight from the typed
+// K5 cache, IN lists become sorted sets searched by bisection, and the boolean combination runs on
+// a register stack. Returns false (generic interpreter, k_filter_typed) for anything else.
+struct LeafPlan {
+  std::vector<FilterLeaf> leaves;
+  std::vector<int32_t> prog;
+  std::vector<int64_t> i64;        // literal slots
+  std::vector<std::string> str;
+};
+static bool leafify(const dr_predicate& p, LeafPlan& L) {
+  std::vector<std::vector<int32_t>> kids(size_t(p.nops));
+  std::vector<int32_t> stack;
+  for (int32_t k = 0; k < p.nops; ++k) {
+    const int op = p.ops[k].opcode;
+    const size_t pops = op == DR_OP_COL || op == DR_OP_LIT ? 0
+                      : op == DR_OP_IN ? size_t(p.ops[k].arg) + 1
+                      : (op == DR_OP_ISNULL || op == DR_OP_ISNOTNULL || op == DR_OP_NOT) ? 1 : 2;
+    kids[size_t(k)].assign(stack.end() - ptrdiff_t(pops), stack.end());
+    stack.resize(stack.size() - pops);
+    stack.push_back(k);
+  }
+  auto is_col = [&](int32_t k) { return p.ops[k].opcode == DR_OP_COL; };
+  auto is_lit = [&](int32_t k) { return p.ops[k].opcode == DR_OP_LIT; };
+  auto kind_ok = [&](int32_t col, int32_t lit) {  // string columns with string literals, others numeric
+    return (p.col_types[col] == DR_T_STRING) == (p.lit_types[lit] == DR_T_STRING);
+  };
+  auto slot = [&](int32_t lit) {
+    L.i64.push_back(p.lit_i64[lit]);
+    L.str.emplace_back(reinterpret_cast<const char*>(p.lit_str_bytes) + p.lit_str_off[lit],
+                       size_t(p.lit_str_off[lit + 1] - p.lit_str_off[lit]));
+    return int32_t(L.i64.size() - 1);
+  };
+  int depth = 0, max_depth = 0;
+  std::function<bool(int32_t)> emit = [&](int32_t k) -> bool {
+    const int op = p.ops[k].opcode;
+    const auto& ch = kids[size_t(k)];
+    auto push_leaf = [&](const FilterLeaf& f) {
+      L.prog.push_back(LEAF_OP_LEAF);
+      L.prog.push_back(int32_t(L.leaves.size()));
+      L.leaves.push_back(f);
+      max_depth = std::max(max_depth, ++depth);
+      return true;
+    };
+    switch (op) {
+      case DR_OP_AND: case DR_OP_OR:
+        if (!emit(ch[0]) || !emit(ch[1])) return false;
+        L.prog.push_back(op == DR_OP_AND ? LEAF_OP_AND : LEAF_OP_OR);
+        L.prog.push_back(0);
+        --depth;
+        return true;
+      case DR_OP_NOT:
+        if (!emit(ch[0])) return false;
+        L.prog.push_back(LEAF_OP_NOT);
+        L.prog.push_back(0);
+        return true;
+      case DR_OP_ISNULL: case DR_OP_ISNOTNULL:
+        if (!is_col(ch[0])) return false;
+        return push_leaf(FilterLeaf{p.ops[ch[0]].arg, op, 0, 0, 0, 0});
+      case DR_OP_EQ: case DR_OP_NE: case DR_OP_LT: case DR_OP_LE: case DR_OP_GT: case DR_OP_GE: case DR_OP_NSEQ: {
+        int32_t c, l, fop = op;
+        if (is_col(ch[0]) && is_lit(ch[1])) {
+          c = p.ops[ch[0]].arg; l = p.ops[ch[1]].arg;
+        } else if (is_lit(ch[0]) && is_col(ch[1])) {
+          c = p.ops[ch[1]].arg; l = p.ops[ch[0]].arg;
+          fop = op == DR_OP_LT ? DR_OP_GT : op == DR_OP_GT ? DR_OP_LT : op == DR_OP_LE ? DR_OP_GE
+              : op == DR_OP_GE ? DR_OP_LE : op;
+        } else {
+          return false;
+        }
+        if (!p.lit_null[l] && !kind_ok(c, l)) return false;
+        return push_leaf(FilterLeaf{c, fop, slot(l), 0, p.lit_null[l] ? 1 : 0, 0});
+      }
+      case DR_OP_IN: {
+        if (!is_col(ch[0])) return false;
+        const int32_t c = p.ops[ch[0]].arg;
+        const bool str = p.col_types[c] == DR_T_STRING;
+        bool has_null = false;
+        std::vector<int64_t> iv;
+        std::vector<std::string> sv;
+        for (size_t q = 1; q < ch.size(); ++q) {
+          if (!is_lit(ch[q])) return false;
+          const int32_t l = p.ops[ch[q]].arg;
+          if (p.lit_null[l]) { has_null = true; continue; }
+          if (!kind_ok(c, l)) return false;
+          if (str) sv.emplace_back(reinterpret_cast<const char*>(p.lit_str_bytes) + p.lit_str_off[l],
+                                   size_t(p.lit_str_off[l + 1] - p.lit_str_off[l]));
+          else iv.push_back(p.lit_i64[l]);
+        }
+        std::sort(iv.begin(), iv.end());
+        iv.erase(std::unique(iv.begin(), iv.end()), iv.end());
+        std::sort(sv.begin(), sv.end());  // bytewise (std::string compares as unsigned char)
+        sv.erase(std::unique(sv.begin(), sv.end()), sv.end());
+        const int32_t first = int32_t(L.i64.size());
+        const size_t m = str ? sv.size() : iv.size();
+        for (size_t q = 0; q < m; ++q) {
+          L.i64.push_back(str ? 0 : iv[q]);
+          L.str.push_back(str ? sv[q] : std::string());
+        }
+        return push_leaf(FilterLeaf{c, DR_OP_IN, first, int32_t(m), has_null ? 1 : 0, 0});
+      }
+      default:
+        return false;
+    }
+  };
+  return emit(p.nops - 1) && max_depth <= 32;
+}
+
 template <typename T>
 static DBuf<T> upload(dr_ctx* ctx, const T* src, size_t n) {
   DBuf<T> d(ctx, n);
@@ -1670,6 +1787,8 @@ static void build_pv_columns(dr_state& st, const std::vector<std::pair<std::stri
   for (auto& c : made) st.pv_cols.push_back(std::move(c));
 }
 
+static std::vector<int64_t> select_flags(dr_state& st, DBuf<uint32_t>& flag);
+
 static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred) {
   check_program(pred);
   dr_ctx* ctx = st.ctx;
@@ -1699,6 +1818,34 @@ static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred)
     }
     fa.cols[c] = PvColumn{col->type, col->w32.p, col->w64.p, col->sptr.p, col->slen.p, col->isnull.p};
   }
+  LeafPlan lp;
+  const bool force_generic = std::getenv("DR_FILTER_GENERIC") != nullptr;  // test hook: k_filter_typed
+  if (!force_generic && leafify(pred, lp)) {
+    FilterLeafArgs la{};
+    la.n_live = st.n_live;
+    for (int32_t c = 0; c < pred.ncols; ++c) la.cols[c] = fa.cols[c];
+    std::vector<uint64_t> soff(lp.str.size() + 1, 0);
+    std::string sbytes;
+    for (size_t q = 0; q < lp.str.size(); ++q) {
+      sbytes += lp.str[q];
+      soff[q + 1] = sbytes.size();
+    }
+    DBuf<FilterLeaf> d_leaves = upload(ctx, lp.leaves.data(), lp.leaves.size());
+    DBuf<int32_t> d_prog = upload(ctx, lp.prog.data(), lp.prog.size());
+    DBuf<int64_t> d_i64 = upload(ctx, lp.i64.data(), lp.i64.size());
+    DBuf<uint64_t> d_soff = upload(ctx, soff.data(), soff.size());
+    DBuf<uint8_t> d_sb = upload(ctx, reinterpret_cast<const uint8_t*>(sbytes.data()), sbytes.size());
+    la.leaves = d_leaves.p;
+    la.prog = d_prog.p;
+    la.nprog = int32_t(lp.prog.size() / 2);
+    la.lit_i64 = d_i64.p;
+    la.lit_str_off = d_soff.p;
+    la.lit_str = d_sb.p;
+    DBuf<uint32_t> flag(ctx, st.n_live);
+    la.flag = flag.p;
+    launch_filter_leaf(la, stream);
+    return select_flags(st, flag);
+  }
   const std::vector<int32_t> ops = lower_program(pred);
   std::vector<uint64_t> lit_off(size_t(pred.nlits) + 1, 0);
   for (int32_t k = 0; k <= pred.nlits && pred.nlits; ++k) lit_off[size_t(k)] = uint64_t(pred.lit_str_off[k]);
@@ -1719,6 +1866,13 @@ static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred)
   DBuf<uint32_t> flag(ctx, st.n_live);
   fa.flag = flag.p;
   launch_filter_typed(fa, stream);
+  return select_flags(st, flag);
+}
+
+// Selected live-file ordinals from per-file flags (scan + compaction), then the call's timings.
+static std::vector<int64_t> select_flags(dr_state& st, DBuf<uint32_t>& flag) {
+  dr_ctx* ctx = st.ctx;
+  hipStream_t stream = ctx->stream;
   DBuf<uint8_t> scratch(ctx, scan_scratch_for(st.n_live));
   DBuf<uint64_t> pos(ctx, st.n_live + 1);
   launch_scan_u32(flag.p, pos.p, st.n_live, scratch.p, stream);

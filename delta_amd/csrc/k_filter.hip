@@ -460,6 +460,84 @@ __global__ void __launch_bounds__(256) k_filter_typed(FilterTypedArgs a) {
   a.flag[i] = (!bad && sp == 1 && !st[0].null && st[0].v) ? 1u : 0u;
 }
 
+// ---- k_filter_leaf ---------------------------------------------------------------------------------
+// Tri-states: 0 false, 1 true, 2 null (Catalyst's three-valued logic).
+__device__ __forceinline__ int bytes_cmp(const uint8_t* a, uint32_t an, const uint8_t* b, uint32_t bn) {
+  const uint32_t m = an < bn ? an : bn;
+  for (uint32_t k = 0; k < m; ++k)
+    if (a[k] != b[k]) return a[k] < b[k] ? -1 : 1;
+  return an == bn ? 0 : (an < bn ? -1 : 1);
+}
+
+__device__ __forceinline__ uint32_t eval_leaf(const FilterLeafArgs& a, const FilterLeaf& L, uint64_t i) {
+  const PvColumn& col = a.cols[L.col];
+  const bool vnull = col.isnull[i] != 0;
+  if (L.op == DR_OP_ISNULL) return vnull ? 1u : 0u;
+  if (L.op == DR_OP_ISNOTNULL) return vnull ? 0u : 1u;
+  if (L.op == DR_OP_NSEQ && (vnull || L.lit_null)) return (vnull && L.lit_null) ? 1u : 0u;
+  if (L.op != DR_OP_IN && L.lit_null) return 2u;
+  if (vnull) return 2u;
+  const bool str = col.type == DR_T_STRING;
+  const uint8_t* vs = nullptr;
+  uint32_t vn = 0;
+  int64_t v = 0;
+  if (str) {
+    vs = reinterpret_cast<const uint8_t*>(col.sptr[i]);
+    vn = col.slen[i];
+  } else {
+    v = col.type == DR_T_LONG ? col.w64[i] : int64_t(int32_t(col.w32[i]));
+  }
+  auto cmp_lit = [&](int32_t k) -> int {
+    if (str) {
+      const uint64_t o = a.lit_str_off[k];
+      return bytes_cmp(vs, vn, a.lit_str + o, uint32_t(a.lit_str_off[k + 1] - o));
+    }
+    const int64_t x = a.lit_i64[k];
+    return v == x ? 0 : (v < x ? -1 : 1);
+  };
+  if (L.op == DR_OP_IN) {  // binary search of the sorted set
+    int32_t lo = L.lit, hi = L.lit + L.nlit;
+    while (lo < hi) {
+      const int32_t mid = (lo + hi) >> 1;
+      const int c = cmp_lit(mid);
+      if (c == 0) return 1u;
+      if (c > 0) lo = mid + 1; else hi = mid;
+    }
+    return L.lit_null ? 2u : 0u;
+  }
+  const int c = cmp_lit(L.lit);
+  switch (L.op) {
+    case DR_OP_EQ: case DR_OP_NSEQ: return c == 0;
+    case DR_OP_NE: return c != 0;
+    case DR_OP_LT: return c < 0;
+    case DR_OP_LE: return c <= 0;
+    case DR_OP_GT: return c > 0;
+    default: return c >= 0;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_filter_leaf(FilterLeafArgs a) {
+  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= a.n_live) return;
+  uint64_t stk = 0;  // 2 bits per entry, top at the low end
+  for (int k = 0; k < a.nprog; ++k) {
+    const int op = a.prog[2 * k];
+    if (op == LEAF_OP_LEAF) {
+      stk = (stk << 2) | eval_leaf(a, a.leaves[a.prog[2 * k + 1]], i);
+    } else if (op == LEAF_OP_NOT) {
+      const uint64_t x = stk & 3u;
+      stk = (stk & ~3ull) | (x == 2u ? 2u : (x ^ 1u));
+    } else {
+      const uint32_t y = uint32_t(stk & 3u), x = uint32_t((stk >> 2) & 3u);
+      uint32_t r;
+      if (op == LEAF_OP_AND) r = (x == 0u || y == 0u) ? 0u : (x == 1u && y == 1u) ? 1u : 2u;
+      else r = (x == 1u || y == 1u) ? 1u : (x == 0u && y == 0u) ? 0u : 2u;
+      stk = ((stk >> 4) << 2) | r;
+    }
+  }
+  a.flag[i] = (stk & 3u) == 1u ? 1u : 0u;
+}
+
 // checkpoint map column: row_start[k] = index of the k-th entry with repetition level 0
 __global__ void k_row_starts(const uint8_t* rep, uint64_t n, const uint64_t* pos, uint64_t* row_start) {
   const uint64_t e = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -483,6 +561,9 @@ uint32_t filter_max_stack() { return dev::PV_STACK; }
 
 void launch_pv_extract(const PvExtractArgs& a, hipStream_t st) {
   if (a.n_live) DR_LAUNCH(dev::k_pv_extract, dim3(g256(a.n_live)), dim3(256), 0, st, a);
+}
+void launch_filter_leaf(const FilterLeafArgs& a, hipStream_t st) {
+  if (a.n_live) DR_LAUNCH(dev::k_filter_leaf, dim3(g256(a.n_live)), dim3(256), 0, st, a);
 }
 void launch_filter_typed(const FilterTypedArgs& a, hipStream_t st) {
   if (a.n_live) DR_LAUNCH(dev::k_filter_typed, dim3(g256(a.n_live)), dim3(256), 0, st, a);

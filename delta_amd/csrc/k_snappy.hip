@@ -240,7 +240,10 @@ __global__ void __launch_bounds__(256) k_snap_assume(SnappyArgs a) {
 //   c-2 genuine     -> chunk c-1 starts at assumed_exit[c-2] and must re-synchronise:
 //                      E[c] = spec_exit[c-1].
 // A failed re-synchronisation (or a chunk spanned right after a break) records the page's first
-// such chunk; the serial resolver recomputes the page's entries from there.
+// such chunk; the serial resolver recomputes the page's entries from there. Such a chunk's entry is
+// set to ~0 here: k_snap_resolve stops where its walk agrees with the entries written here, so an
+// entry left over from an earlier replay of the same pages must never be mistaken for one (that
+// sent a page to the serial decoder on every replay after the first: 138 ms at config 4 scale 0.1).
 __device__ __forceinline__ bool broke(const SnappyArgs& a, uint32_t c) { return a.assumed_exit[c] != a.spec_exit[c]; }
 
 constexpr uint32_t MAX_RUN = 32;
@@ -258,6 +261,7 @@ __global__ void __launch_bounds__(256) k_snap_entries(SnappyArgs a) {
     while (r < MAX_RUN && j - 2 > r && broke(a, b - 2 - r)) ++r;
     if (r == MAX_RUN) {
       a.chunk_flag[a.chunk_base[p] + (j - 2 > MAX_RUN ? j - 2 - MAX_RUN : 0u)] = 1;
+      a.entry[c] = 0xffffffffu;  // unknown: k_snap_resolve rewrites it (never a stale value of an earlier replay)
       return;
     }
     genuine = (r & 1u) == 0;
@@ -273,6 +277,7 @@ __global__ void __launch_bounds__(256) k_snap_entries(SnappyArgs a) {
   const bool resync = e < ce && ((a.vis[uint64_t(b) * (SNAP_CH / 32) + uint32_t((e - cs) >> 5)] >> ((e - cs) & 31)) & 1u);
   if (!resync) {
     a.chunk_flag[c - 2] = 1;
+    a.entry[c] = 0xffffffffu;
     return;
   }
   a.entry[c] = a.spec_exit[b];

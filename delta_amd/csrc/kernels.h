@@ -385,6 +385,30 @@ struct FilterTypedArgs {
   const uint8_t* lit_str;
   uint32_t* flag;                // [n_live] 1 = selected
 };
+// Leaf form of a predicate (engine.hip leafify): every leaf compares one partition column with
+// literals -- col op lit, col IN (lits), col IS [NOT] NULL -- and AND / OR / NOT combine their
+// three-valued results on a 2-bit-per-entry stack held in one register.
+struct FilterLeaf {
+  int32_t col;       // predicate column
+  int32_t op;        // DR_OP_EQ .. DR_OP_GE, DR_OP_NSEQ, DR_OP_IN, DR_OP_ISNULL, DR_OP_ISNOTNULL
+  int32_t lit;       // literal index (comparisons) or first entry of the sorted set (IN)
+  int32_t nlit;      // IN: entries in the set
+  int32_t lit_null;  // comparisons: the literal is NULL; IN: the list holds a NULL
+  int32_t pad;
+};
+enum : int32_t { LEAF_OP_LEAF = 0, LEAF_OP_AND = 1, LEAF_OP_OR = 2, LEAF_OP_NOT = 3 };
+struct FilterLeafArgs {
+  uint64_t n_live;
+  PvColumn cols[PV_MAXC];
+  const FilterLeaf* leaves;
+  const int32_t* prog;           // [nprog * 2] opcode, arg (leaf index)
+  int32_t nprog;
+  const int64_t* lit_i64;        // comparison literals, then the IN sets (sorted ascending)
+  const uint64_t* lit_str_off;   // string literals / sets (sorted bytewise), offsets into lit_str
+  const uint8_t* lit_str;
+  uint32_t* flag;
+};
+void launch_filter_leaf(const FilterLeafArgs& a, hipStream_t st);
 // device-only opcodes of the lowered program (engine.hip lower_program): an IN list is folded
 // one element at a time into an accumulator slot above its value
 enum : int32_t { FILTER_OP_IN_START = 100, FILTER_OP_IN_STEP = 101, FILTER_OP_IN_END = 102 };

@@ -105,4 +105,12 @@ PREDICATES = [
     [("=", C("big"), L("long", -9223372036854775808))],
     [("and", ("=", C("part"), L("integer", 3)), ("=", C("b"), L("boolean", True)))],
     [("or", (">=", C("part"), L("integer", 1)), (">", C("d"), L("date", "2020-05-01")))],
+    # literal first (the leaf form flips the comparison), string IN sets with a NULL, NOT IN with a
+    # NULL (never true), a column-vs-column comparison (the generic interpreter in either mode)
+    [("<", L("integer", 2), C("part"))],
+    [(">=", L("date", "2020-04-15"), C("d"))],
+    [("in", C("s"), [L("string", "w17"), L("string", "été"), L("string", None), L("string", "w1")])],
+    [("not", ("in", C("part"), [L("integer", 4), L("integer", None)]))],
+    [("=", C("part"), C("part"))],
+    [("and", ("or", ("isnull", C("s")), ("=", C("b"), L("boolean", False))), ("not", ("<", C("big"), L("long", 1))))],
 ]

@@ -46,7 +46,12 @@ def _oracle_selected(lp, preds_list, cutoff=0):
 
 @pytest.mark.parametrize("checkpoint", [False, True])
 @pytest.mark.parametrize("escaped_keys", [False, True])
-def test_filter_cast_corpus(engine, tmp_path, checkpoint, escaped_keys):
+@pytest.mark.parametrize("kernel", ["leaf", "generic"])
+def test_filter_cast_corpus(engine, tmp_path, monkeypatch, checkpoint, escaped_keys, kernel):
+    """Both K5 evaluators: k_filter_leaf (leaf form: column-vs-literal comparisons, IN sets, AND/OR/NOT)
+    and the generic postfix interpreter k_filter_typed (DR_FILTER_GENERIC=1)."""
+    if kernel == "generic":
+        monkeypatch.setenv("DR_FILTER_GENERIC", "1")
     lp = F.build(str(tmp_path), checkpoint=checkpoint, escaped_keys=escaped_keys)
     got = _gpu_selected(engine, lp, F.PREDICATES)
     want = _oracle_selected(lp, F.PREDICATES)

@@ -188,12 +188,13 @@ def measure_filter(eng, staged, cutoff, exp, steps):
     # typed cache reads: p0 date (4 B) + p1 int (4 B) + p2 string (8 B address + 4 B length + ~3 B of
     # value) + p3 boolean (4 B) + 4 null bytes, and a 4 B flag out per live file
     algo = n * (4 + 4 + 15 + 4 + 4 + 4)
-    kt = ms.get("k_filter_typed")
+    kname = "k_filter_leaf" if "k_filter_leaf" in ms else "k_filter_typed"
+    kt = ms.get(kname)
     return {"predicate": "p0 >= DATE'2020-03-01' AND p0 < DATE'2020-06-01' AND p1 IN (1..100) AND p2 = 'w17' "
                          "AND p3 = true", "live_files": n, "selected": len(sel),
             "first_call_s": round(first_s, 4), "cache_build_ms": round(first.get("k_pv_extract", 0.0), 4),
             "call_s": round(call_s, 5), "files_per_s": round(n / call_s, 1),
-            "roofline": {"bound": "hbm", "kernel": "k_filter_typed", "avg_launch_ms": round(kt, 4) if kt else None,
+            "roofline": {"bound": "hbm", "kernel": kname, "avg_launch_ms": round(kt, 4) if kt else None,
                          "algo_bytes": algo, "achieved": round(algo / (kt * 1e-3) / 1e9, 1) if kt else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(algo / (kt * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if kt else None},

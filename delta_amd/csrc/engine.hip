@@ -675,9 +675,15 @@ static void plan_pages(StagedData& s, PagePlan& P) {
 }
 
 // Inflate + decode every page of a plan into `pa.cols` (allocated by the caller for P.levels).
+static uint64_t scan_scratch_for(uint64_t n) { return scan_scratch_bytes(std::max<uint64_t>(n, uint64_t(1) << 23)); }
+
 static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_t>& dict_ptr, DBuf<uint32_t>& dict_len,
-                         DBuf<uint32_t>& err, void* scratch) {
+                         DBuf<uint32_t>& err, void*) {
   hipStream_t stream = ctx->stream;
+  // scan scratch for the plan's largest scan: SNAPPY chunk element counts, PLAIN BYTE_ARRAY tiles
+  // (a 100M-row checkpoint has 26M chunks: a scratch sized for 2^23 entries was overrun)
+  DBuf<uint8_t> own_scratch(ctx, scan_scratch_for(std::max<uint64_t>(P.nchunks, P.ba_tiles.size())));
+  void* scratch = own_scratch.p;
   pa.pages = P.d_pages.p;
   pa.npages = uint32_t(P.pages.size());
   dict_ptr = DBuf<uint64_t>(ctx, P.dict_entries);
@@ -874,8 +880,6 @@ static void reduce_nonfile(dr_state& st, std::vector<NonFileAction>& acts, bool 
   if (validate && !meta)  // D/Snapshot.scala:163-171
     fail(DR_E_MISSING_METADATA, action_not_found("metadata", st.counts.version));
 }
-
-static uint64_t scan_scratch_for(uint64_t n) { return scan_scratch_bytes(std::max<uint64_t>(n, uint64_t(1) << 23)); }
 
 // K1 + K2 + canonicalisation: fills st's per-action arrays (checkpoint rows first, then JSON lines)
 // and collects the non-file actions (protocol / metaData / txn) on the host in replay order.

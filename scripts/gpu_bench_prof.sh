@@ -3,7 +3,7 @@
 set -e
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-KRE=${KRE:-k_json_lines}
+KRE=${KRE:-"k_snap_exec|k_snap_emit|k_snap_spec|k_bucket_scatter|k_bucket_reduce|k_bucket_verify|k_json_lines|k_ckpt_assemble|k_pq_data"}
 O=$R/gpurun_out/round
 rm -rf $O && mkdir -p $O
 timeout -k 10 400 python $R/bench.py --no-cpu-baseline > $O/warm.json 2> $O/warm.err

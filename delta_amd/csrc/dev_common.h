@@ -163,5 +163,22 @@ __device__ inline uint32_t json_unescape(const uint8_t* s, uint32_t n, uint8_t* 
   return o;
 }
 
+// Replay key of a canonical path: java.net.URI equality treats "file:///x" and "file:/x" alike.
+__device__ __forceinline__ uint32_t key_skip(const uint8_t* p, uint32_t n) {
+  return (n >= 8 && p[0] == 'f' && p[1] == 'i' && p[2] == 'l' && p[3] == 'e' && p[4] == ':' && p[5] == '/' &&
+          p[6] == '/' && p[7] == '/') ? 2u : 0u;
+}
+__device__ inline bool key_equal(const uint8_t* a, uint32_t an, const uint8_t* b, uint32_t bn) {
+  const uint32_t sa = key_skip(a, an), sb = key_skip(b, bn);
+  if (an - sa != bn - sb) return false;
+  // compare "file:" (5 bytes) then the remainder after the skipped "//"
+  if (sa | sb) {
+    for (uint32_t i = 0; i < 5; ++i) if (a[i] != b[i]) return false;
+    return bytes_equal(a + 5 + sa, b + 5 + sb, an - sa - 5);
+  }
+  return bytes_equal(a, b, an);
+}
+
+
 }  // namespace dev
 }  // namespace dr

@@ -186,16 +186,23 @@ struct DBuf {
   DBuf(DBuf&& o) noexcept { *this = std::move(o); }
   DBuf& operator=(DBuf&& o) noexcept {
     reset();
-    ctx = o.ctx; p = o.p; n = o.n;
+    ctx = o.ctx; p = o.p; n = o.n; own = o.own;
     o.p = nullptr; o.n = 0;
     return *this;
   }
   ~DBuf() { reset(); }
   void reset() {
-    if (p && ctx) ctx->release(p);
+    if (p && ctx && own) ctx->release(p);
     p = nullptr;
     n = 0;
+    own = true;
   }
+  // a non-owning view of the first `count` elements of another buffer
+  void view(const DBuf& o, size_t count) {
+    reset();
+    ctx = o.ctx; p = o.p; n = count; own = false;
+  }
+  bool own = true;
   void zero(hipStream_t s) { if (p) HIP_OK(hipMemsetAsync(p, 0, std::max<size_t>(n, 1) * sizeof(T), s)); }
 };
 
@@ -312,8 +319,41 @@ struct ExportCols {
       pv_val_bytes, pv_val_null, tags_null, tags_key_bytes, tags_val_bytes, tags_val_null;
 };
 
+// The chain of states that dr_state_apply grows from one full replay: an
+// append-only action store (the base's survivors, then every applied tail), the device path index
+// over it (k_index.hip) and, per applied tail, the undo log that turns the index back into any older
+// state's view. Every state of the chain reads the store through views; only the head moves.
+struct IncChain {
+  dr_ctx* ctx = nullptr;
+  uint64_t n = 0, cap = 0;  // actions in the store, capacity
+  DBuf<uint8_t> kind, flags;
+  DBuf<uint64_t> key, path_ptr, src_off;
+  DBuf<uint32_t> path_len, src_len;
+  DBuf<int64_t> size, delts;
+  DBuf<uint16_t> src_id;
+  uint64_t tcap = 0, used = 0;  // table slots (power of two), occupied slots
+  DBuf<unsigned long long> keys;
+  DBuf<uint32_t> vals;
+  DBuf<uint32_t> tomb_list;  // tombstone candidates of the head (stale entries are skipped)
+  uint64_t tomb_n = 0, tomb_cap = 0;
+  struct Undo {
+    DBuf<uint2> e;
+    uint64_t n = 0;
+  };
+  std::vector<Undo> undo;  // undo[g - 1] turns generation g back into g - 1
+  uint32_t head = 0;
+  std::vector<std::shared_ptr<StagedData>> sources;
+  std::vector<std::shared_ptr<DBuf<uint8_t>>> arenas;
+  DBuf<unsigned long long> ctr;
+};
+
 struct dr_state {
   dr_ctx* ctx = nullptr;
+  // a state of an apply chain: its actions are the store's first n_actions, its survivor lists are
+  // built from the index on first use (ensure_ready)
+  std::shared_ptr<IncChain> chain;
+  uint32_t gen = 0, nsrc = 0;
+  bool lists_ready = true;
   std::shared_ptr<StagedData> staged;
   // the staged segments the action records point into: {staged} for a replay; for a state built
   // by dr_state_apply, its base's sources plus the applied tail (only sources[0] can hold
@@ -1142,20 +1182,305 @@ static dr_state* new_state(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp) {
   return st.release();
 }
 
-// Incremental tail apply (the reference rebuilds instead,
-// D/SnapshotManagement.scala:286-330). The base state's survivors -- live files, then tombstones:
-// distinct paths, so their relative order is free -- are the replay prefix of the new state, the
-// tail's commit lines follow in file order, and K3/K4 run over the concatenation with the new
-// retention cutoff: the same result as replaying the whole segment (tombstones the base already
-// dropped stay dropped, so the cutoff must not move backwards). Nothing of the base is re-parsed;
-// the new state keeps the base's staged segments, which its records point into.
-static dr_state* apply_tail(dr_ctx* ctx, dr_state& base, const std::shared_ptr<StagedData>& tail, int64_t cutoff,
-                            uint32_t flags) {
+// ---------------------------------------------------------------------------------------------------
+// incremental tail apply (the reference rebuilds the state from the last
+// checkpoint instead, D/SnapshotManagement.scala:286-330)
+// ---------------------------------------------------------------------------------------------------
+static IndexArgs ix_args(IncChain& c) {
+  IndexArgs a{};
+  a.kind = c.kind.p;
+  a.flags = c.flags.p;
+  a.key = c.key.p;
+  a.path_ptr = c.path_ptr.p;
+  a.path_len = c.path_len.p;
+  a.size = c.size.p;
+  a.delts = c.delts.p;
+  a.keys = c.keys.p;
+  a.vals = c.vals.p;
+  a.mask = c.tcap - 1;
+  a.ctr = c.ctr.p;
+  a.tomb_list = c.tomb_list.p;
+  a.tomb_cap = c.tomb_cap;
+  return a;
+}
+
+template <typename T>
+static void grow_copy(dr_ctx* ctx, DBuf<T>& b, uint64_t keep, uint64_t cap) {
+  DBuf<T> nb(ctx, cap);
+  if (keep) HIP_OK(hipMemcpyAsync(nb.p, b.p, keep * sizeof(T), hipMemcpyDeviceToDevice, ctx->stream));
+  b = std::move(nb);
+}
+
+// store capacity for `need` actions (growth by half: amortised O(1) per appended action)
+static void chain_reserve(IncChain& c, uint64_t need) {
+  if (need <= c.cap) return;
+  const uint64_t cap = std::max<uint64_t>({need, c.cap + c.cap / 2, uint64_t(1) << 16});
+  if (cap >= (uint64_t(1) << 32) - 1) fail(DR_E_REBUILD, "apply chain store is full: rebuild the snapshot");
+  grow_copy(c.ctx, c.kind, c.n, cap);
+  grow_copy(c.ctx, c.flags, c.n, cap);
+  grow_copy(c.ctx, c.key, c.n, cap);
+  grow_copy(c.ctx, c.path_ptr, c.n, cap);
+  grow_copy(c.ctx, c.src_off, c.n, cap);
+  grow_copy(c.ctx, c.path_len, c.n, cap);
+  grow_copy(c.ctx, c.src_len, c.n, cap);
+  grow_copy(c.ctx, c.size, c.n, cap);
+  grow_copy(c.ctx, c.delts, c.n, cap);
+  grow_copy(c.ctx, c.src_id, c.n, cap);
+  c.cap = cap;
+}
+
+// table room for `add` more keys at load <= 1/2 (rehash into twice the needed size)
+static void chain_table_reserve(IncChain& c, uint64_t add) {
+  if ((c.used + add) * 2 <= c.tcap) return;
+  uint64_t cap = 1024;
+  while (cap < (c.used + add) * 4) cap <<= 1;
+  DBuf<unsigned long long> nk(c.ctx, cap);
+  DBuf<uint32_t> nv(c.ctx, cap);
+  nk.zero(c.ctx->stream);
+  nv.zero(c.ctx->stream);
+  launch_ix_rehash(c.keys.p, c.vals.p, c.tcap, nk.p, nv.p, cap - 1, c.ctx->stream);
+  c.keys = std::move(nk);
+  c.vals = std::move(nv);
+  c.tcap = cap;
+}
+
+static void chain_tomb_reserve(IncChain& c, uint64_t add) {
+  if (c.tomb_n + add <= c.tomb_cap) return;
+  const uint64_t cap = std::max<uint64_t>({c.tomb_n + add, c.tomb_cap * 2, 4096});
+  grow_copy(c.ctx, c.tomb_list, c.tomb_n, cap);
+  c.tomb_cap = cap;
+}
+
+// Copies the survivors of `base` (live files, then tombstones: distinct paths) into dst[0, M).
+struct ActionDst {
+  uint8_t *kind, *flags;
+  uint64_t *key, *path_ptr, *src_off;
+  uint32_t *path_len, *src_len;
+  int64_t *size, *delts;
+  uint16_t* src_id;
+};
+static void gather_survivors(dr_ctx* ctx, dr_state& base, const ActionDst& d) {
   hipStream_t stream = ctx->stream;
+  const uint64_t M = base.n_live + base.n_tomb;
+  if (!M) return;
+  DBuf<uint32_t> sidx(ctx, M);
+  if (base.n_live) HIP_OK(hipMemcpyAsync(sidx.p, base.live.p, base.n_live * 4, hipMemcpyDeviceToDevice, stream));
+  if (base.n_tomb)
+    HIP_OK(hipMemcpyAsync(sidx.p + base.n_live, base.tomb.p, base.n_tomb * 4, hipMemcpyDeviceToDevice, stream));
+  launch_gather_u8(base.kind.p, sidx.p, M, d.kind, stream);
+  launch_gather_u8(base.flags.p, sidx.p, M, d.flags, stream);
+  launch_gather_u64(base.key.p, sidx.p, M, d.key, stream);
+  launch_gather_u64(base.path_ptr.p, sidx.p, M, d.path_ptr, stream);
+  launch_gather_u32(base.path_len.p, sidx.p, M, d.path_len, stream);
+  launch_gather_u64(reinterpret_cast<const uint64_t*>(base.size.p), sidx.p, M, reinterpret_cast<uint64_t*>(d.size),
+                    stream);
+  launch_gather_u64(reinterpret_cast<const uint64_t*>(base.delts.p), sidx.p, M,
+                    reinterpret_cast<uint64_t*>(d.delts), stream);
+  launch_gather_u64(base.src_off.p, sidx.p, M, d.src_off, stream);
+  launch_gather_u32(base.src_len.p, sidx.p, M, d.src_len, stream);
+  if (base.src_id.p) launch_gather_u16(base.src_id.p, sidx.p, M, d.src_id, stream);
+  else HIP_OK(hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(d.src_id), 0, M, stream));
+}
+
+// Appends src's T actions at dst offset `at`, all from source `sid`.
+static void append_actions(dr_ctx* ctx, const ActionDst& d, uint64_t at, dr_state& src, uint16_t sid) {
+  hipStream_t stream = ctx->stream;
+  const uint64_t T = src.n_actions;
+  if (!T) return;
+  auto cp = [&](void* dst, const void* s, size_t bytes) {
+    HIP_OK(hipMemcpyAsync(dst, s, bytes, hipMemcpyDeviceToDevice, stream));
+  };
+  cp(d.kind + at, src.kind.p, T);
+  cp(d.flags + at, src.flags.p, T);
+  cp(d.key + at, src.key.p, T * 8);
+  cp(d.path_ptr + at, src.path_ptr.p, T * 8);
+  cp(d.path_len + at, src.path_len.p, T * 4);
+  cp(d.size + at, src.size.p, T * 8);
+  cp(d.delts + at, src.delts.p, T * 8);
+  cp(d.src_off + at, src.src_off.p, T * 8);
+  cp(d.src_len + at, src.src_len.p, T * 4);
+  HIP_OK(hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(d.src_id + at), sid, T, stream));
+}
+
+static ActionDst chain_dst(IncChain& c) {
+  return ActionDst{c.kind.p, c.flags.p, c.key.p, c.path_ptr.p, c.src_off.p, c.path_len.p, c.src_len.p,
+                   c.size.p, c.delts.p, c.src_id.p};
+}
+
+static void materialize(dr_state& st);
+
+// Chain states read the store through views (refreshed on every use: a later apply may have grown
+// the store) and build their survivor lists from the index on first use.
+static void ensure_ready(dr_state& st) {
+  if (!st.chain) return;
+  IncChain& c = *st.chain;
+  const uint64_t n = st.n_actions;
+  st.kind.view(c.kind, n);
+  st.flags.view(c.flags, n);
+  st.key.view(c.key, n);
+  st.path_ptr.view(c.path_ptr, n);
+  st.src_off.view(c.src_off, n);
+  st.path_len.view(c.path_len, n);
+  st.src_len.view(c.src_len, n);
+  st.size.view(c.size, n);
+  st.delts.view(c.delts, n);
+  st.src_id.view(c.src_id, n);
+  if (st.sources.size() != st.nsrc) {
+    st.sources.assign(c.sources.begin(), c.sources.begin() + st.nsrc);
+    st.staged = c.sources[0];
+  }
+  if (!st.lists_ready) {
+    materialize(st);
+    st.arenas = c.arenas;
+    st.lists_ready = true;
+  }
+}
+
+// Survivor lists of a chain state: the head's index values -- an older state's after its later
+// applies are undone on a copy -- classified at the state's cutoff and compacted in slot order.
+static void materialize(dr_state& st) {
+  IncChain& c = *st.chain;
+  dr_ctx* ctx = st.ctx;
+  hipStream_t stream = ctx->stream;
+  IndexArgs a = ix_args(c);
+  const uint32_t* vals = c.vals.p;
+  DBuf<uint32_t> tmp;
+  if (st.gen != c.head) {
+    tmp = DBuf<uint32_t>(ctx, c.tcap);
+    HIP_OK(hipMemcpyAsync(tmp.p, c.vals.p, c.tcap * 4, hipMemcpyDeviceToDevice, stream));
+    for (uint32_t g = c.head; g > st.gen; --g) launch_ix_undo(a, tmp.p, c.undo[g - 1].e.p, c.undo[g - 1].n, stream);
+    vals = tmp.p;
+  }
+  const uint64_t C = c.tcap;
+  DBuf<uint32_t> lf(ctx, C), tf(ctx, C);
+  DBuf<uint64_t> lp(ctx, C + 1), tp(ctx, C + 1);
+  DBuf<uint8_t> scratch(ctx, scan_scratch_for(C));
+  launch_ix_classify(a, vals, C, st.cutoff, lf.p, tf.p, stream);
+  launch_scan_u32(lf.p, lp.p, C, scratch.p, stream);
+  launch_scan_u32(tf.p, tp.p, C, scratch.p, stream);
+  const uint64_t nl = d2h_one(lp.p + C, stream), nt = d2h_one(tp.p + C, stream);
+  if (int64_t(nl) != st.counts.num_files || int64_t(nt) != st.counts.num_removes)
+    fail(DR_E_INTERNAL, fmt("apply chain index disagrees with its counters (%llu/%lld files, %llu/%lld tombstones)",
+                            (unsigned long long)nl, (long long)st.counts.num_files, (unsigned long long)nt,
+                            (long long)st.counts.num_removes));
+  st.live = DBuf<uint32_t>(ctx, nl);
+  st.tomb = DBuf<uint32_t>(ctx, nt);
+  launch_ix_emit(vals, C, lf.p, lp.p, tf.p, tp.p, st.live.p, st.tomb.p, stream);
+  st.n_live = nl;
+  st.n_tomb = nt;
+}
+
+// A chain's first image: the base's survivors and their index. nullptr when two survivors share a
+// 64-bit path key (the full reduction handles that exactly).
+static std::shared_ptr<IncChain> chain_from(dr_ctx* ctx, dr_state& base, uint64_t room) {
+  hipStream_t stream = ctx->stream;
+  auto ch = std::make_shared<IncChain>();
+  IncChain& c = *ch;
+  c.ctx = ctx;
+  const uint64_t M = base.n_live + base.n_tomb;
+  chain_reserve(c, M + room);
+  gather_survivors(ctx, base, chain_dst(c));
+  c.n = M;
+  c.ctr = DBuf<unsigned long long>(ctx, IX_C_N);
+  c.ctr.zero(stream);
+  chain_table_reserve(c, M + room);
+  chain_tomb_reserve(c, base.n_tomb + room);
+  IndexArgs a = ix_args(c);
+  a.lo = 0;
+  a.hi = M;
+  launch_ix_build(a, stream);
+  const std::vector<unsigned long long> ctr = d2h(c.ctr.p, IX_C_N, stream);
+  if (ctr[IX_C_COLLIDE]) return nullptr;
+  c.used = ctr[IX_C_NEW_SLOTS];
+  c.tomb_n = ctr[IX_C_TOMB_FILL];
+  c.sources = base.sources;
+  c.arenas = base.arenas;
+  return ch;
+}
+
+// Applies the parsed tail `t` to the head of chain `ch` (base is the head's state). O(tail): the
+// tail's actions are appended to the store and only their keys are probed. nullptr (the index
+// restored) when a 64-bit key collision needs the full reduction.
+static dr_state* apply_incremental(dr_ctx* ctx, dr_state& base, const std::shared_ptr<IncChain>& ch, dr_state& t,
+                                   const std::shared_ptr<StagedData>& tail, int64_t cutoff, int64_t version) {
+  hipStream_t stream = ctx->stream;
+  IncChain& c = *ch;
+  const uint64_t T = t.n_actions, lo = c.n;
+  chain_reserve(c, lo + T);
+  chain_table_reserve(c, T);
+  chain_tomb_reserve(c, T);
+  append_actions(ctx, chain_dst(c), lo, t, uint16_t(c.sources.size()));
+  DBuf<uint32_t> tslot(ctx, T), tprev(ctx, T);
+  IncChain::Undo u;
+  u.e = DBuf<uint2>(ctx, T);
+  unsigned long long init[IX_C_N] = {};
+  init[IX_C_TOMB_FILL] = c.tomb_n;
+  HIP_OK(hipMemcpyAsync(c.ctr.p, init, sizeof(init), hipMemcpyHostToDevice, stream));
+  IndexArgs a = ix_args(c);
+  a.lo = lo;
+  a.hi = lo + T;
+  a.t_slot = tslot.p;
+  a.t_prev = tprev.p;
+  a.old_cut = base.cutoff;
+  a.new_cut = cutoff;
+  a.undo = u.e.p;
+  launch_ix_touch(a, stream);
+  launch_ix_delta(a, stream);
+  if (cutoff > base.cutoff) launch_ix_expire(a, c.tomb_n, stream);
+  const std::vector<unsigned long long> ctr = d2h(c.ctr.p, IX_C_N, stream);
+  c.used += ctr[IX_C_NEW_SLOTS];
+  // (DR_IX_TEST_COLLIDE: test hook for the rollback)
+  if (ctr[IX_C_COLLIDE] || std::getenv("DR_IX_TEST_COLLIDE")) {  // undo this apply's first touches: the head is the base again
+    launch_ix_undo(a, c.vals.p, u.e.p, ctr[IX_C_UNDO_FILL], stream);
+    HIP_OK(hipStreamSynchronize(stream));
+    return nullptr;
+  }
+  c.n = lo + T;
+  c.tomb_n = ctr[IX_C_TOMB_FILL];
+  u.n = ctr[IX_C_UNDO_FILL];
+  c.undo.push_back(std::move(u));
+  c.head += 1;
+  c.sources.push_back(tail);
+  c.arenas.insert(c.arenas.end(), t.arenas.begin(), t.arenas.end());
+  std::unique_ptr<dr_state> st(new_state(ctx, nullptr));
+  st->chain = ch;
+  st->gen = c.head;
+  st->nsrc = uint32_t(c.sources.size());
+  st->n_actions = c.n;
+  st->lists_ready = false;
+  st->cutoff = cutoff;
+  dr_counts& k = st->counts;
+  k = base.counts;
+  k.num_files += int64_t(ctr[IX_C_FILES]);
+  k.size_in_bytes += int64_t(ctr[IX_C_SIZE]);
+  k.num_removes += int64_t(ctr[IX_C_REMOVES]);
+  k.live_key_sum += ctr[IX_C_LKS];
+  k.tomb_key_sum += ctr[IX_C_TKS];
+  k.num_actions = base.counts.num_actions + int64_t(T);
+  k.num_file_actions = base.counts.num_file_actions + int64_t(ctr[IX_C_FILE_ACTIONS]);
+  k.malformed_lines = base.counts.malformed_lines + t.counts.malformed_lines;
+  k.version = version;
+  // the head's tombstone candidates, compacted once they are mostly stale
+  if (c.tomb_n > 2 * uint64_t(k.num_removes) + (uint64_t(1) << 16)) {
+    DBuf<uint32_t> nl(ctx, c.tomb_cap);
+    HIP_OK(hipMemsetAsync(c.ctr.p + IX_C_TOMB_FILL, 0, 8, stream));
+    IndexArgs b = ix_args(c);
+    b.new_cut = cutoff;
+    launch_ix_tomb_compact(b, c.tomb_list.p, c.tomb_n, nl.p, stream);
+    c.tomb_n = d2h_one(c.ctr.p + IX_C_TOMB_FILL, stream);
+    c.tomb_list = std::move(nl);
+  }
+  return st.release();
+}
+
+// Validates a tail against its base: JSON commits only, contiguous versions, a cutoff that does
+// not move backwards. Returns the new version.
+static int64_t check_tail(dr_state& base, const std::shared_ptr<StagedData>& tail, int64_t cutoff) {
   if (!tail->parts.empty()) fail(DR_E_INVALID_ARG, "an applied tail holds commit (JSON) files only");
-  if (base.sources.empty()) fail(DR_E_INVALID_ARG, "base state has no staged segment");
+  if (base.sources.empty() && !base.chain) fail(DR_E_INVALID_ARG, "base state has no staged segment");
   if (base.sharded) fail(DR_E_UNSUPPORTED, "a sharded replay's part cannot take a tail on its own: shard the tail too");
-  if (base.sources.size() >= 65535) fail(DR_E_UNSUPPORTED, "too many applied tails on one state; rebuild it");
+  const uint64_t nsrc = base.chain ? base.nsrc : base.sources.size();
+  if (nsrc >= 65535) fail(DR_E_REBUILD, "too many applied tails on one state: rebuild the snapshot");
   // the base kept only tombstones with delTimestamp > base.cutoff: an earlier cutoff (a longer
   // delta.deletedFileRetentionDuration, a clock moved back) would need the ones it dropped
   if (cutoff < base.cutoff)
@@ -1171,9 +1496,43 @@ static dr_state* apply_tail(dr_ctx* ctx, dr_state& base, const std::shared_ptr<S
     for (int64_t x : vers) v += ", " + std::to_string(x);
     fail(DR_E_NONCONTIGUOUS, "Versions (Vector(" + v + ")) are not contiguous.");
   }
+  return vers.empty() ? base.counts.version : vers.back();
+}
+
+// Tail apply. The head of an apply chain (or a full replay, which starts a chain) takes the O(tail)
+// index path; any other base -- an older state of a chain, a forced reducer, a key collision --
+// takes the full path: the base's survivors (distinct paths, so their relative order is free) are
+// the replay prefix, the tail's lines follow in file order, and K3/K4 run over the concatenation
+// with the new cutoff, the same result as replaying the whole segment (tombstones the base dropped
+// stay dropped, so the cutoff must not move backwards). Nothing of the base is re-parsed either way.
+static dr_state* apply_tail(dr_ctx* ctx, dr_state& base, const std::shared_ptr<StagedData>& tail, int64_t cutoff,
+                            uint32_t flags) {
+  const int64_t version = check_tail(base, tail, cutoff);
   std::unique_ptr<dr_state> t(new_state(ctx, tail));
   std::vector<NonFileAction> nf;
   parse_actions(ctx, tail, t.get(), nf);
+  // protocol / metaData / txn: the base's winners first, then the tail's actions in order
+  std::vector<NonFileAction> all = base.nonfile;
+  for (size_t k = 0; k < all.size(); ++k) all[k].order = k;
+  for (NonFileAction& a : nf) {
+    a.order += all.size();
+    all.push_back(std::move(a));
+  }
+  const bool forced = (flags & (DR_FLAG_EXACT_REDUCE | DR_FLAG_REDUCE64)) || std::getenv("DR_APPLY_FULL");
+  if (!forced) {
+    std::shared_ptr<IncChain> ch;
+    if (base.chain && base.gen == base.chain->head) ch = base.chain;
+    else if (!base.chain) ch = chain_from(ctx, base, std::max<uint64_t>(t->n_actions, 1024));
+    if (ch) {
+      if (dr_state* r0 = apply_incremental(ctx, base, ch, *t, tail, cutoff, version)) {
+        std::unique_ptr<dr_state> r(r0);
+        reduce_nonfile(*r, all, !(flags & DR_FLAG_NO_VALIDATION));
+        return r.release();
+      }
+    }
+  }
+  ensure_ready(base);
+  hipStream_t stream = ctx->stream;
   const uint64_t M = base.n_live + base.n_tomb, T = t->n_actions, N = M + T;
   if (N >= (uint64_t(1) << 30)) fail(DR_E_UNSUPPORTED, "more than 2^30 actions in one replay");
   std::unique_ptr<dr_state> st(new_state(ctx, nullptr));
@@ -1182,7 +1541,7 @@ static dr_state* apply_tail(dr_ctx* ctx, dr_state& base, const std::shared_ptr<S
   st->sources.push_back(tail);
   st->arenas = base.arenas;
   st->arenas.insert(st->arenas.end(), t->arenas.begin(), t->arenas.end());
-  st->counts.version = vers.empty() ? base.counts.version : vers.back();
+  st->counts.version = version;
   st->n_actions = N;
   st->kind = DBuf<uint8_t>(ctx, N);
   st->flags = DBuf<uint8_t>(ctx, N);
@@ -1194,52 +1553,17 @@ static dr_state* apply_tail(dr_ctx* ctx, dr_state& base, const std::shared_ptr<S
   st->src_off = DBuf<uint64_t>(ctx, N);
   st->src_len = DBuf<uint32_t>(ctx, N);
   st->src_id = DBuf<uint16_t>(ctx, N);
-  if (M) {  // the base's survivors, gathered
-    DBuf<uint32_t> sidx(ctx, M);
-    if (base.n_live)
-      HIP_OK(hipMemcpyAsync(sidx.p, base.live.p, base.n_live * 4, hipMemcpyDeviceToDevice, stream));
-    if (base.n_tomb)
-      HIP_OK(hipMemcpyAsync(sidx.p + base.n_live, base.tomb.p, base.n_tomb * 4, hipMemcpyDeviceToDevice, stream));
-    launch_gather_u8(base.kind.p, sidx.p, M, st->kind.p, stream);
-    launch_gather_u8(base.flags.p, sidx.p, M, st->flags.p, stream);
-    launch_gather_u64(base.key.p, sidx.p, M, st->key.p, stream);
-    launch_gather_u64(base.path_ptr.p, sidx.p, M, st->path_ptr.p, stream);
-    launch_gather_u32(base.path_len.p, sidx.p, M, st->path_len.p, stream);
-    launch_gather_u64(reinterpret_cast<const uint64_t*>(base.size.p), sidx.p, M,
-                      reinterpret_cast<uint64_t*>(st->size.p), stream);
-    launch_gather_u64(reinterpret_cast<const uint64_t*>(base.delts.p), sidx.p, M,
-                      reinterpret_cast<uint64_t*>(st->delts.p), stream);
-    launch_gather_u64(base.src_off.p, sidx.p, M, st->src_off.p, stream);
-    launch_gather_u32(base.src_len.p, sidx.p, M, st->src_len.p, stream);
-    if (base.src_id.p) launch_gather_u16(base.src_id.p, sidx.p, M, st->src_id.p, stream);
-    else HIP_OK(hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(st->src_id.p), 0, M, stream));
-  }
-  if (T) {  // then the tail's lines, in order
-    auto cp = [&](void* dst, const void* src, size_t bytes) {
-      HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream));
-    };
-    cp(st->kind.p + M, t->kind.p, T);
-    cp(st->flags.p + M, t->flags.p, T);
-    cp(st->key.p + M, t->key.p, T * 8);
-    cp(st->path_ptr.p + M, t->path_ptr.p, T * 8);
-    cp(st->path_len.p + M, t->path_len.p, T * 4);
-    cp(st->size.p + M, t->size.p, T * 8);
-    cp(st->delts.p + M, t->delts.p, T * 8);
-    cp(st->src_off.p + M, t->src_off.p, T * 8);
-    cp(st->src_len.p + M, t->src_len.p, T * 4);
-    HIP_OK(hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(st->src_id.p + M),
-                             uint16_t(st->sources.size() - 1), T, stream));
-  }
+  const ActionDst d{st->kind.p, st->flags.p, st->key.p, st->path_ptr.p, st->src_off.p, st->path_len.p,
+                    st->src_len.p, st->size.p, st->delts.p, st->src_id.p};
+  gather_survivors(ctx, base, d);
+  append_actions(ctx, d, M, *t, uint16_t(st->sources.size() - 1));
+  (void)stream;
   reduce_actions(ctx, st.get(), cutoff, flags);
   st->cutoff = cutoff;
+  // a full replay of the segment would count every action of the base's segment plus the tail's
+  st->counts.num_file_actions = base.counts.num_file_actions + (st->counts.num_file_actions - int64_t(M));
+  st->counts.num_actions = base.counts.num_actions + int64_t(T);
   st->counts.malformed_lines = base.counts.malformed_lines + t->counts.malformed_lines;
-  // protocol / metaData / txn: the base's winners first, then the tail's actions in order
-  std::vector<NonFileAction> all = base.nonfile;
-  for (size_t k = 0; k < all.size(); ++k) all[k].order = k;
-  for (NonFileAction& a : nf) {
-    a.order += all.size();
-    all.push_back(std::move(a));
-  }
   reduce_nonfile(*st, all, !(flags & DR_FLAG_NO_VALIDATION));
   return st.release();
 }
@@ -1357,6 +1681,7 @@ static void load_ck_side(StagedData& s, bool add, CkRows& out) {
 constexpr uint8_t kFromCkpt = 16;  // dev_common.h F_FROM_CKPT: the action is a checkpoint row
 
 static void build_export(dr_state& st, int which) {
+  ensure_ready(st);
   ExportCols& ex = st.exp[which];
   if (ex.built) return;
   hipStream_t stream = st.ctx->stream;
@@ -1797,6 +2122,7 @@ static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred)
   check_program(pred);
   dr_ctx* ctx = st.ctx;
   ctx->begin_call();
+  ensure_ready(st);
   hipStream_t stream = ctx->stream;
   if (st.sources.empty()) fail(DR_E_INVALID_ARG, "state has no staged segment");
   // the predicate's columns in the K5 cache (built for the ones not there yet)

@@ -431,3 +431,48 @@ void launch_gather_u64_by64(const uint64_t* src, const uint64_t* idx, uint64_t n
 void launch_gather_bytes(const uint64_t* ptr, const uint32_t* len, const uint64_t* off, uint64_t n, uint8_t* out,
                          hipStream_t st);
 }  // namespace dr
+
+// ---- incremental tail apply: device-resident path index (k_index.hip) ----------------------------
+namespace dr {
+// One chain of states built by dr_state_apply shares an append-only action store and an
+// open-addressing table {path key -> winning action + 1}. A tail's file actions probe and update
+// only their own keys; the counters move by the difference of old and new winners' contributions.
+struct IndexArgs {
+  const uint8_t* kind;
+  const uint8_t* flags;
+  const uint64_t* key;
+  const uint64_t* path_ptr;
+  const uint32_t* path_len;
+  const int64_t* size;
+  const int64_t* delts;
+  unsigned long long* keys;  // table: 0 = empty (path_key is never 0)
+  uint32_t* vals;            // winner action + 1 (0: none)
+  uint64_t mask;             // capacity - 1 (capacity a power of two, load <= 1/2)
+  uint64_t lo, hi;           // the action range being inserted / applied
+  uint32_t* t_slot;          // per action in [lo, hi): its slot (0xffffffff: not a file action)
+  uint32_t* t_prev;          // per action: the slot's value before it (atomicMax)
+  int64_t old_cut, new_cut;  // retention cutoffs of the base and the new state
+  unsigned long long* ctr;   // IX_C_* counters
+  uint32_t* tomb_list;       // tombstone candidates (action indices), appended at ctr[IX_C_TOMB_FILL]
+  uint64_t tomb_cap;
+  uint2* undo;               // first touches of this apply: {action, previous value}
+};
+enum : int {
+  IX_C_FILES = 0, IX_C_SIZE = 1, IX_C_REMOVES = 2, IX_C_LKS = 3, IX_C_TKS = 4, IX_C_COLLIDE = 5,
+  IX_C_FILE_ACTIONS = 6, IX_C_NEW_SLOTS = 7, IX_C_TOMB_FILL = 8, IX_C_UNDO_FILL = 9, IX_C_N = 16
+};
+void launch_ix_build(const IndexArgs& a, hipStream_t st);
+void launch_ix_touch(const IndexArgs& a, hipStream_t st);
+void launch_ix_delta(const IndexArgs& a, hipStream_t st);
+void launch_ix_expire(const IndexArgs& a, uint64_t n_list, hipStream_t st);
+void launch_ix_tomb_compact(const IndexArgs& a, const uint32_t* list_in, uint64_t n, uint32_t* list_out,
+                            hipStream_t st);
+void launch_ix_undo(const IndexArgs& a, uint32_t* vals_out, const uint2* undo, uint64_t n, hipStream_t st);
+void launch_ix_classify(const IndexArgs& a, const uint32_t* vals, uint64_t cap, int64_t cutoff, uint32_t* live_flag,
+                        uint32_t* tomb_flag, hipStream_t st);
+void launch_ix_emit(const uint32_t* vals, uint64_t cap, const uint32_t* live_flag, const uint64_t* live_pos,
+                    const uint32_t* tomb_flag, const uint64_t* tomb_pos, uint32_t* live, uint32_t* tomb,
+                    hipStream_t st);
+void launch_ix_rehash(const unsigned long long* okeys, const uint32_t* ovals, uint64_t ocap,
+                      unsigned long long* nkeys, uint32_t* nvals, uint64_t nmask, hipStream_t st);
+}  // namespace dr

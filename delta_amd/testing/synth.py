@@ -406,6 +406,19 @@ def _write_parts_worker(job):
     return out
 
 
+def _pick_live(rng, state, next_id, k):
+    """k distinct live ids. Small picks from a large pool (config 5's streaming tail: 2 removes per
+    commit over 50M files) sample and reject instead of listing the live set on every commit."""
+    if 0 < k and k * 1000 < next_id:
+        for _ in range(8):
+            cand = np.unique(rng.integers(0, next_id, 4 * k + 16))
+            cand = cand[state[cand] == 1]
+            if len(cand) >= k:
+                return rng.permutation(cand)[:k]
+    live = np.flatnonzero(state == 1)
+    return rng.choice(live, size=min(k, len(live)), replace=False)
+
+
 def build_table(table_dir: str, spec: ChurnSpec, seed: int, checkpoint_with_parsed=False,
                 data_page_size: int = 1 << 20, keep_ids: bool = True, compression: str = "snappy",
                 data_page_version: str = "1.0", row_group_size: int = 1 << 20,
@@ -470,8 +483,7 @@ def build_table(table_dir: str, spec: ChurnSpec, seed: int, checkpoint_with_pars
     at_cutoff_left = spec.n_at_cutoff
     for _ in range(spec.n_deltas):
         version += 1
-        live = np.flatnonzero(state == 1)
-        rm_ids = rng.choice(live, size=min(spec.removes_per_delta, len(live)), replace=False)
+        rm_ids = _pick_live(rng, state, next_id, spec.removes_per_delta)
         ts = rng.integers(window0, window0 + 14 * DAY_MS, len(rm_ids), dtype=np.int64)
         if at_cutoff_left:
             k = min(at_cutoff_left, len(ts))
@@ -530,6 +542,11 @@ def config_spec(config: int, scale: float = 1.0) -> ChurnSpec:
         files = s(100_000_000)
         return ChurnSpec(ckpt_files=files, ckpt_version=1000, n_deltas=0, removes_per_delta=0, adds_per_delta=0,
                          readd_frac=0.0, ncols=4, ckpt_parts=min(100, max(2, files // 1000)))
+    if config == 5:  # streaming tail: 10k commits of 3 adds + 2 removes over a 50M-file checkpoint
+        files = s(50_000_000)
+        return ChurnSpec(ckpt_files=files, ckpt_version=100, n_deltas=min(10_000, max(20, s(10_000))),
+                         removes_per_delta=2, adds_per_delta=3, readd_frac=0.0, ncols=2,
+                         ckpt_parts=min(50, max(1, files // 1_000_000)))
     raise ValueError(config)
 
 
@@ -567,6 +584,7 @@ if __name__ == "__main__":  # python -m delta_amd.testing.synth <config> <table_
     e = build_config(cfg, out, scale=sc, keep_ids=False, workers=nw)
     d = {k: getattr(e, k) for k in ("version", "min_file_retention_timestamp", "num_files", "size_in_bytes",
                                     "num_removes", "num_actions", "num_file_actions", "json_bytes", "checkpoint_bytes")}
+    d["n_deltas"] = config_spec(cfg, sc).n_deltas
     if cfg == 4:
         d["selected"] = config4_selected(out, sc)
     with open(os.path.join(out, "expected.json"), "w") as f:

@@ -286,6 +286,22 @@ def _commit_files(lp, lo, hi):
     return out
 
 
+COUNT_KEYS = ("num_files", "size_in_bytes", "num_removes", "num_metadata", "num_protocol", "num_set_transactions",
+              "num_actions", "num_file_actions", "malformed_lines", "live_key_sum", "tomb_key_sum", "version")
+
+
+def _same_counts(a, b, tag):
+    for k in COUNT_KEYS:
+        assert a.counts[k] == b.counts[k], (tag, k, a.counts[k], b.counts[k])
+
+
+def _same_state(a, b, tag):
+    _same_counts(a, b, tag)
+    assert sorted(map(_canon, a.export(0))) == sorted(map(_canon, b.export(0))), tag
+    assert sorted(map(_canon, a.export(1))) == sorted(map(_canon, b.export(1))), tag
+    assert a.nonfile == b.nonfile, tag
+
+
 def test_incremental_apply_matches_full_replay(engine, tmp_path):
     """dr_state_apply: a checkpointed base extended one commit at a time,
     then by a batch, equals the full replay of the segment at every version (records, counters,
@@ -309,9 +325,7 @@ def test_incremental_apply_matches_full_replay(engine, tmp_path):
             states.append(nxt)
             full = _gpu_replay(engine, lp, cutoff, version=v)
             try:
-                for k in ("num_files", "size_in_bytes", "num_removes", "num_metadata", "num_protocol",
-                          "num_set_transactions", "live_key_sum", "tomb_key_sum", "version"):
-                    assert nxt.counts[k] == full.counts[k], (v, k)
+                _same_counts(nxt, full, v)
                 assert sorted(map(_canon, nxt.export(0))) == sorted(map(_canon, full.export(0)))
                 assert sorted(map(_canon, nxt.export(1))) == sorted(map(_canon, full.export(1)))
                 assert nxt.nonfile == full.nonfile
@@ -334,6 +348,72 @@ def test_incremental_apply_matches_full_replay(engine, tmp_path):
             assert got == want and got
     finally:
         for s in states:
+            s.release()
+
+
+def test_incremental_index_chain(engine, tmp_path, monkeypatch):
+    """The O(tail) path of dr_state_apply (k_index.hip): a chain of one-commit applies whose
+    retention cutoff sweeps the deletion window (tombstones expire while the chain grows), checked
+    against full replays; a forced key collision rolls the index back and takes the full reduction,
+    after which the same head applies incrementally; older states of the chain materialise their
+    survivors through the undo logs; a branch off an older state takes the full path and starts a
+    new chain; the oracle agrees at the end."""
+    from delta_amd.testing import synth as S
+    spec = S.ChurnSpec(ckpt_files=3000, ckpt_version=2, n_deltas=24, removes_per_delta=40, adds_per_delta=30,
+                       readd_frac=0.5, ncols=2)
+    exp = S.build_table(str(tmp_path), spec, seed=5, row_group_size=1000)
+    lp = os.path.join(str(tmp_path), "_delta_log")
+    day = 86400000
+    c0 = exp.min_file_retention_timestamp - 7 * day  # the deletion window's start: every tombstone kept
+    step = 14 * day // spec.n_deltas
+    b0 = spec.ckpt_version
+    cut = lambda k: c0 + k * step
+    states = [_gpu_replay(engine, lp, cut(0), version=b0)]
+    extra = []
+    try:
+        for k in range(1, spec.n_deltas + 1):
+            v = b0 + k
+            tail = engine.stage_files(_commit_files(lp, v, v))
+            if k == 8:
+                monkeypatch.setenv("DR_IX_TEST_COLLIDE", "1")
+                fb = states[-1].apply(tail, cut(k))
+                monkeypatch.delenv("DR_IX_TEST_COLLIDE")
+                extra.append(fb)
+            nxt = states[-1].apply(tail, cut(k))
+            tail.release()
+            states.append(nxt)
+            if k == 8:
+                _same_state(nxt, fb, "rollback")
+            if k % 5 == 0 or k in (1, 8, 9):
+                full = _gpu_replay(engine, lp, cut(k), version=v)
+                try:
+                    _same_state(nxt, full, v)
+                finally:
+                    full.release()
+        assert states[-1].counts["num_removes"] < states[12].counts["num_removes"]  # tombstones expired
+        for k in (2, 11, 17):  # older states, materialised after later applies
+            full = _gpu_replay(engine, lp, cut(k), version=b0 + k)
+            try:
+                _same_state(states[k], full, ("old", k))
+            finally:
+                full.release()
+        tail = engine.stage_files(_commit_files(lp, b0 + 6, b0 + 9))
+        br = states[5].apply(tail, cut(9))
+        tail.release()
+        extra.append(br)
+        tail = engine.stage_files(_commit_files(lp, b0 + 10, b0 + 10))
+        br2 = br.apply(tail, cut(10))
+        tail.release()
+        extra.append(br2)
+        for s, k in ((br, 9), (br2, 10)):
+            full = _gpu_replay(engine, lp, cut(k), version=b0 + k)
+            try:
+                _same_state(s, full, ("branch", k))
+            finally:
+                full.release()
+        _assert_same(states[-1], O.state_reconstruction(O.get_log_segment(lp), cut(spec.n_deltas)))
+    finally:
+        for s in states + extra:
             s.release()
 
 

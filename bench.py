@@ -201,6 +201,8 @@ def measure_stream(eng, table, exp, args):
             t3 = time.perf_counter()
             if timing and k:
                 for kn, ms in eng.last_timings().items():
+                    if kn in ("start", "end"):
+                        continue
                     kern[kn.split("#")[0]] = kern.get(kn.split("#")[0], 0.0) + ms
             tail.release()
             if cur is not base:

@@ -17,9 +17,10 @@ STATUS = {
     5: "DR_E_MISSING_PART", 6: "DR_E_NONCONTIGUOUS", 7: "DR_E_BAD_SEGMENT",
     8: "DR_E_MISSING_PROTOCOL", 9: "DR_E_MISSING_METADATA", 10: "DR_E_PARSE", 11: "DR_E_PARQUET",
     12: "DR_E_UNSUPPORTED", 13: "DR_E_OOM", 14: "DR_E_DEVICE", 15: "DR_E_INTERNAL",
-    16: "DR_E_CHECKSUM", 17: "DR_E_NO_CHECKSUM", 18: "DR_E_REBUILD",
+    16: "DR_E_CHECKSUM", 17: "DR_E_NO_CHECKSUM", 18: "DR_E_REBUILD", 19: "DR_E_FOREIGN_FILE",
 }
 DR_E_REBUILD = 18
+DR_E_FOREIGN_FILE = 19
 DR_E_CHECKSUM, DR_E_NO_CHECKSUM = 16, 17
 DR_FILE_JSON, DR_FILE_CHECKPOINT = 0, 1
 DR_LIVE, DR_TOMBSTONES = 0, 1
@@ -30,10 +31,10 @@ DR_FLAG_REDUCE64 = 0x4
 # Exported symbols (checked by tests/test_native_abi.py against include/deltareplay.h).
 SYMBOLS = [
     "dr_abi_version", "dr_ctx_create", "dr_ctx_destroy", "dr_last_error", "dr_log_segment",
-    "dr_stage", "dr_stage_log", "dr_staged_release", "dr_staged_bytes", "dr_staged_plan",
+    "dr_stage", "dr_stage_named", "dr_stage_log", "dr_staged_release", "dr_staged_bytes", "dr_staged_plan",
     "dr_replay_staged",
     "dr_replay", "dr_state_release", "dr_state_apply", "dr_state_counts", "dr_state_nonfile_json", "dr_state_check_checksum",
-    "dr_state_export", "dr_filter", "dr_free", "dr_last_timings", "dr_set_timing",
+    "dr_state_export", "dr_filter", "dr_state_scan_order", "dr_state_partition_groups", "dr_free", "dr_last_timings", "dr_set_timing",
     "dr_shard_plan", "dr_stage_log_shard", "dr_shard_begin", "dr_shard_pack", "dr_shard_reduce",
     "dr_shard_finish", "dr_shard_release", "dr_parse_commits", "dr_parsed_release",
 ]
@@ -127,6 +128,7 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "dr_last_error": ([vp], C.c_char_p),
         "dr_log_segment": ([vp, C.c_char_p, i64, C.c_char_p, u64, C.POINTER(u64), C.POINTER(i64)], C.c_int),
         "dr_stage": ([vp, C.POINTER(dr_file), i32, C.POINTER(vp)], C.c_int),
+        "dr_stage_named": ([vp, C.c_char_p, C.POINTER(dr_file), C.POINTER(C.c_char_p), i32, C.POINTER(vp)], C.c_int),
         "dr_stage_log": ([vp, C.c_char_p, i64, C.POINTER(vp)], C.c_int),
         "dr_staged_release": ([vp], C.c_int),
         "dr_staged_bytes": ([vp, C.POINTER(u64), C.POINTER(u64)], C.c_int),
@@ -140,6 +142,8 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "dr_state_check_checksum": ([vp, C.c_char_p, u64, C.c_char_p, u64, C.POINTER(u64)], C.c_int),
         "dr_state_export": ([vp, i32, C.POINTER(dr_export)], C.c_int),
         "dr_filter": ([vp, C.POINTER(dr_predicate), C.POINTER(_P64), _P64], C.c_int),
+        "dr_state_scan_order": ([vp, C.POINTER(_P64), _P64], C.c_int),
+        "dr_state_partition_groups": ([vp, _P64, i64, C.POINTER(_P64), C.POINTER(_P64), _P64], C.c_int),
         "dr_free": ([vp], None),
         "dr_last_timings": ([vp, C.c_char_p, u64, C.POINTER(C.c_float), i32, C.POINTER(i32)], C.c_int),
         "dr_set_timing": ([vp, i32], C.c_int),

@@ -10,6 +10,7 @@
 #include <functional>
 #include <type_traits>
 #include <cstring>
+#include <cctype>
 #include <cerrno>
 #include <cstdlib>
 #include <cstdio>
@@ -303,6 +304,7 @@ struct StagedData {
   int add_def = 1, rm_def = 1;
   std::vector<NonFileAction> ck_nonfile;  // protocol/metaData/txn rows of the checkpoint
   std::unique_ptr<PagePlan> pv;           // add.partitionValues map columns (planned on first filter)
+  std::unique_ptr<PagePlan> mt;           // add.modificationTime (planned on first scan order)
   std::mutex pv_mu;
 };
 
@@ -2200,6 +2202,168 @@ static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred)
 }
 
 // Selected live-file ordinals from per-file flags (scan + compaction), then the call's timings.
+// ---------------------------------------------------------------------------------------------------
+// scan-side consumers: DeltaSourceSnapshot's (modificationTime, path) order and
+// TahoeFileIndex.listFiles' partition groups, computed over the resident state.
+// ---------------------------------------------------------------------------------------------------
+static std::vector<int64_t> to_host_positions(const DBuf<uint32_t>& keys, uint64_t n, hipStream_t stream) {
+  const std::vector<uint32_t> k = d2h(keys.p, n, stream);
+  return std::vector<int64_t>(k.begin(), k.end());
+}
+
+// DeltaSourceSnapshot.initialFiles (D/files/DeltaSourceSnapshot.scala:53-95):
+// allFiles.sort("modificationTime", "path"): live export positions in that order.
+static std::vector<int64_t> scan_order(dr_state& st) {
+  dr_ctx* ctx = st.ctx;
+  ctx->begin_call();
+  ensure_ready(st);
+  hipStream_t stream = ctx->stream;
+  if (st.sources.empty()) fail(DR_E_INVALID_ARG, "state has no staged segment");
+  StagedData& s = *st.sources[0];
+  const uint64_t n = st.n_live, R = s.ck_rows;
+  if (!n) return {};
+  MtimeArgs a{};
+  a.live = st.live.p;
+  a.n_live = n;
+  a.src_off = st.src_off.p;
+  a.src_len = st.src_len.p;
+  a.ck_rows = R;
+  a.json = s.d_json.p;
+  DBuf<uint64_t> json_bases;
+  if (st.src_id.p) {
+    std::vector<uint64_t> bases;
+    for (auto& src : st.sources) bases.push_back(reinterpret_cast<uint64_t>(src->d_json.p));
+    json_bases = upload(ctx, bases.data(), bases.size());
+    a.act_flags = st.flags.p;
+    a.src_id = st.src_id.p;
+    a.json_bases = json_bases.p;
+  }
+  DBuf<uint8_t> cdef;
+  DBuf<int64_t> cval;
+  DBuf<uint64_t> dict_ptr;
+  DBuf<uint32_t> dict_len, pq_err(ctx, 1);
+  pq_err.zero(stream);
+  if (R) {
+    {
+      std::lock_guard<std::mutex> g(s.pv_mu);
+      if (!s.mt) {
+        auto P = std::make_unique<PagePlan>();
+        P->paths = {"add.modificationTime"};
+        plan_pages(s, *P);
+        s.mt = std::move(P);
+      }
+    }
+    PagePlan& P = *s.mt;
+    if (P.present[0]) {
+      if (P.levels[0] != R) fail(DR_E_PARQUET, "add.modificationTime: one value per checkpoint row expected");
+      cdef = DBuf<uint8_t>(ctx, R);
+      cval = DBuf<int64_t>(ctx, R);
+      cdef.zero(stream);
+      ParquetArgs pa{};
+      pa.ncols = 1;
+      pa.cols[0] = FlatColumn{cdef.p, nullptr, cval.p, nullptr, nullptr};
+      decode_pages(ctx, P, pa, dict_ptr, dict_len, pq_err, nullptr);
+      if (d2h_one(pq_err.p, stream) != 0)
+        fail(DR_E_PARQUET, fmt("device decode of add.modificationTime failed (code %u)", d2h_one(pq_err.p, stream)));
+      a.ck_def = cdef.p;
+      a.ck_val = cval.p;
+      a.ck_max_def = P.max_def[0];
+    }
+  }
+  DBuf<int64_t> mt(ctx, n);
+  DBuf<uint32_t> err(ctx, 1);
+  err.zero(stream);
+  a.out = mt.p;
+  a.error = err.p;
+  launch_mtime_extract(a, stream);
+  if (d2h_one(err.p, stream)) fail(DR_E_PARSE, "malformed add object in a live AddFile's JSON line");
+  DBuf<uint64_t> pp(ctx, n);
+  DBuf<uint32_t> pl(ctx, n), keys(ctx, n);
+  launch_gather_u64(st.path_ptr.p, st.live.p, n, pp.p, stream);
+  launch_gather_u32(st.path_len.p, st.live.p, n, pl.p, stream);
+  launch_iota_u32(keys.p, n, stream);
+  size_t tb = 0;
+  launch_sort_scan_order(nullptr, &tb, keys.p, n, mt.p, pp.p, pl.p, stream);
+  DBuf<uint8_t> temp(ctx, tb);
+  launch_sort_scan_order(temp.p, &tb, keys.p, n, mt.p, pp.p, pl.p, stream);
+  ctx->collect_timings();
+  return to_host_positions(keys, n, stream);
+}
+
+// TahoeFileIndex.listFiles (D/files/TahoeFileIndex.scala:58-81): `rows` (live export positions, e.g. a
+// dr_filter result; null = all) grouped by the values of the table's partition columns (the
+// metadata's partitionColumns, raw strings, null distinct from every string). Returns the rows in
+// group order (groups ordered by their values, nulls first; rows ascending within a group) and the
+// groups' start offsets (+ the end).
+static void partition_groups(dr_state& st, const int64_t* rows, int64_t nrows, std::vector<int64_t>& order,
+                             std::vector<int64_t>& off) {
+  dr_ctx* ctx = st.ctx;
+  ctx->begin_call();
+  ensure_ready(st);
+  hipStream_t stream = ctx->stream;
+  std::vector<std::string> cols;
+  for (const NonFileAction& a : st.nonfile) {
+    if (a.kind != 3) continue;
+    const JVal* pc = a.val.get("partitionColumns");
+    if (pc && pc->t == JVal::ARR)
+      for (const JVal& c : pc->a)
+        if (c.t == JVal::STR) cols.push_back(c.s);
+  }
+  if (cols.size() > PV_MAXC) fail(DR_E_UNSUPPORTED, fmt("more than %d partition columns", PV_MAXC));
+  const uint64_t n = rows ? uint64_t(nrows) : st.n_live;
+  order.clear();
+  off.assign(1, 0);
+  if (!n) return;
+  for (uint64_t i = 0; rows && i < n; ++i)
+    if (rows[i] < 0 || uint64_t(rows[i]) >= st.n_live) fail(DR_E_INVALID_ARG, "row out of range");
+  if (cols.empty()) {  // an unpartitioned table: one group
+    for (uint64_t i = 0; i < n; ++i) order.push_back(rows ? rows[i] : int64_t(i));
+    std::sort(order.begin(), order.end());
+    off.push_back(int64_t(n));
+    return;
+  }
+  std::vector<std::pair<std::string, int32_t>> want;
+  for (const std::string& c : cols) {
+    bool have = false;
+    for (auto& pc : st.pv_cols) have |= pc->name == c && pc->type == DR_T_STRING;
+    if (!have) want.push_back({c, DR_T_STRING});
+  }
+  if (!want.empty()) build_pv_columns(st, want);
+  GroupCols g{};
+  g.ncols = int32_t(cols.size());
+  for (size_t c = 0; c < cols.size(); ++c)
+    for (auto& pc : st.pv_cols)
+      if (pc->name == cols[c] && pc->type == DR_T_STRING) {
+        g.sptr[c] = pc->sptr.p;
+        g.slen[c] = pc->slen.p;
+        g.isnull[c] = pc->isnull.p;
+      }
+  DBuf<uint32_t> keys(ctx, n);
+  if (rows) {
+    std::vector<uint32_t> r(rows, rows + n);
+    std::sort(r.begin(), r.end());
+    HIP_OK(hipMemcpyAsync(keys.p, r.data(), n * 4, hipMemcpyHostToDevice, stream));
+  } else {
+    launch_iota_u32(keys.p, n, stream);
+  }
+  size_t tb = 0;
+  launch_sort_groups(nullptr, &tb, keys.p, n, g, stream);
+  DBuf<uint8_t> temp(ctx, tb);
+  launch_sort_groups(temp.p, &tb, keys.p, n, g, stream);
+  DBuf<uint32_t> flag(ctx, n);
+  DBuf<uint64_t> pos(ctx, n + 1);
+  DBuf<uint8_t> scratch(ctx, scan_scratch_for(n));
+  launch_group_flags(keys.p, n, g, flag.p, stream);
+  launch_scan_u32(flag.p, pos.p, n, scratch.p, stream);
+  const uint64_t ng = d2h_one(pos.p + n, stream);
+  DBuf<int64_t> starts(ctx, ng);
+  launch_select(flag.p, pos.p, n, starts.p, stream);
+  ctx->collect_timings();
+  order = to_host_positions(keys, n, stream);
+  off = d2h(starts.p, ng, stream);
+  off.push_back(int64_t(n));
+}
+
 static std::vector<int64_t> select_flags(dr_state& st, DBuf<uint32_t>& flag) {
   dr_ctx* ctx = st.ctx;
   hipStream_t stream = ctx->stream;
@@ -2568,6 +2732,75 @@ int dr_stage(dr_ctx* ctx, const dr_file* files, int32_t nfiles, dr_staged** out)
   });
 }
 
+// Hadoop Path of a path or URI string, for equality: scheme (a bare path is "file"), authority, and
+// the path with repeated and trailing '/' removed (org.apache.hadoop.fs.Path normalisation).
+struct HPath {
+  std::string scheme, authority, path;
+  bool operator==(const HPath& o) const { return scheme == o.scheme && authority == o.authority && path == o.path; }
+};
+static HPath hpath(const std::string& s) {
+  HPath h;
+  size_t i = 0;
+  const size_t colon = s.find(':');
+  if (colon != std::string::npos && colon > 0 && s.find('/') > colon) {
+    bool ok = std::isalpha(static_cast<unsigned char>(s[0])) != 0;
+    for (size_t k = 1; k < colon; ++k) {
+      const char c = s[k];
+      ok &= std::isalnum(static_cast<unsigned char>(c)) || c == '+' || c == '-' || c == '.';
+    }
+    if (ok) {
+      h.scheme = s.substr(0, colon);
+      i = colon + 1;
+    }
+  }
+  if (h.scheme.empty()) h.scheme = "file";
+  if (s.compare(i, 2, "//") == 0) {
+    const size_t e = s.find('/', i + 2);
+    h.authority = s.substr(i + 2, e == std::string::npos ? std::string::npos : e - i - 2);
+    i = e == std::string::npos ? s.size() : e;
+  }
+  for (; i < s.size(); ++i) {
+    if (s[i] == '/' && !h.path.empty() && h.path.back() == '/') continue;
+    h.path += s[i];
+  }
+  if (h.path.size() > 1 && h.path.back() == '/') h.path.pop_back();
+  return h;
+}
+
+static void check_named_files(const char* log_path, const dr_file* files, const char* const* names, int32_t n) {
+  const HPath base = hpath(log_path);
+  for (int32_t k = 0; k < n; ++k) {
+    const std::string name = names && names[k] ? names[k] : "";
+    if (name.empty()) continue;  // an unnamed (cached) input, as the reference accepts ""
+    HPath parent = hpath(name);
+    const size_t slash = parent.path.rfind('/');
+    const std::string leaf = slash == std::string::npos ? parent.path : parent.path.substr(slash + 1);
+    parent.path = slash == std::string::npos ? std::string() : slash == 0 ? std::string("/") : parent.path.substr(0, slash);
+    if (!(parent == base))
+      fail(DR_E_FOREIGN_FILE, "File (" + name + ") doesn't belong in the transaction log at " + log_path +
+                                  ". Please contact Databricks Support.");
+    const dr_file& f = files[k];
+    const bool ok = f.kind == DR_FILE_JSON
+                        ? is_delta_file(leaf) && file_version(leaf) == f.version
+                        : is_checkpoint_file(leaf) && file_version(leaf) == f.version && checkpoint_part(leaf) == f.part;
+    if (!ok)
+      fail(DR_E_INVALID_ARG, fmt("file name %s does not name a %s of version %lld (part %d)", leaf.c_str(),
+                                 f.kind == DR_FILE_JSON ? "delta file" : "checkpoint", (long long)f.version, f.part));
+  }
+}
+
+int dr_stage_named(dr_ctx* ctx, const char* log_path, const dr_file* files, const char* const* names, int32_t nfiles,
+                   dr_staged** out) {
+  if (!ctx || !out || !log_path || (nfiles && !files)) return DR_E_INVALID_ARG;
+  return guard(ctx, [&] {
+    check_named_files(log_path, files, names, nfiles);
+    HIP_OK(hipSetDevice(ctx->device));
+    auto s = std::make_unique<dr_staged>();
+    s->d = stage_files(ctx, files, nfiles);
+    *out = s.release();
+  });
+}
+
 int dr_stage_log(dr_ctx* ctx, const char* log_path, int64_t version_to_load, dr_staged** out) {
   if (!ctx || !out || !log_path) return DR_E_INVALID_ARG;
   return guard(ctx, [&] {
@@ -2774,6 +3007,41 @@ int dr_filter(dr_state* state, const dr_predicate* pred, int64_t** selected, int
     if (!v.empty()) memcpy(out, v.data(), v.size() * sizeof(int64_t));
     *selected = out;
     *nselected = int64_t(v.size());
+  });
+}
+
+static int64_t* malloc_copy(const std::vector<int64_t>& v) {
+  int64_t* out = static_cast<int64_t*>(malloc(std::max<size_t>(v.size(), 1) * sizeof(int64_t)));
+  if (!out) throw std::bad_alloc();
+  if (!v.empty()) memcpy(out, v.data(), v.size() * sizeof(int64_t));
+  return out;
+}
+
+int dr_state_scan_order(dr_state* state, int64_t** order, int64_t* n) {
+  if (!state || !order || !n) return DR_E_INVALID_ARG;
+  *order = nullptr;
+  *n = 0;
+  return guard(state->ctx, [&] {
+    HIP_OK(hipSetDevice(state->ctx->device));
+    std::vector<int64_t> v = scan_order(*state);
+    *order = malloc_copy(v);
+    *n = int64_t(v.size());
+  });
+}
+
+int dr_state_partition_groups(dr_state* state, const int64_t* rows, int64_t nrows, int64_t** order,
+                              int64_t** group_off, int64_t* ngroups) {
+  if (!state || !order || !group_off || !ngroups || (rows && nrows < 0)) return DR_E_INVALID_ARG;
+  *order = nullptr;
+  *group_off = nullptr;
+  *ngroups = 0;
+  return guard(state->ctx, [&] {
+    HIP_OK(hipSetDevice(state->ctx->device));
+    std::vector<int64_t> o, g;
+    partition_groups(*state, rows, nrows, o, g);
+    *order = malloc_copy(o);
+    *group_off = malloc_copy(g);
+    *ngroups = int64_t(g.size()) - 1;
   });
 }
 

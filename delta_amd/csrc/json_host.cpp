@@ -121,6 +121,11 @@ bool JVal::is_int() const {
     char c = s[i];
     if (!(c >= '0' && c <= '9') && !(i == 0 && c == '-')) return false;
   }
+  try {  // a long: out of range is not one (the device decoders agree)
+    (void)std::stoll(s);
+  } catch (...) {
+    return false;
+  }
   return true;
 }
 

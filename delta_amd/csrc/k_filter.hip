@@ -13,6 +13,7 @@
 #include "dev_common.h"
 #include "kernels.h"
 #include "../../include/deltareplay.h"
+#include <hipcub/device/device_merge_sort.hpp>
 
 namespace dr {
 namespace dev {
@@ -576,6 +577,123 @@ void launch_row_starts(const uint8_t* rep, uint64_t n, const uint64_t* pos, uint
 }
 void launch_select(const uint32_t* flag, const uint64_t* pos, uint64_t n, int64_t* out, hipStream_t st) {
   if (n) DR_LAUNCH(dev::k_select, dim3(g256(n)), dim3(256), 0, st, flag, pos, n, out);
+}
+
+// ---- scan-side consumers -------------------------------------------------------------------------
+namespace dev {
+
+// Jackson's long from a JSON number token: an integer literal that fits int64 (anything else --
+// fraction, exponent, string, overflow -- leaves the primitive's default 0, as the host export does).
+__device__ bool json_int64(const uint8_t* p, const uint8_t* e, int64_t* out) {
+  bool neg = false;
+  if (p < e && *p == '-') { neg = true; ++p; }
+  if (p >= e || *p < '0' || *p > '9') return false;
+  uint64_t v = 0;
+  int nd = 0;
+  while (p < e && *p >= '0' && *p <= '9') {
+    const uint64_t d = uint64_t(*p - '0');
+    if (v > (uint64_t(INT64_MAX) + (neg ? 1 : 0) - d) / 10) return false;
+    v = v * 10 + d;
+    ++p;
+    ++nd;
+  }
+  if (p < e && (*p == '.' || *p == 'e' || *p == 'E')) return false;
+  *out = neg ? int64_t(0 - v) : int64_t(v);
+  return true;
+}
+
+__global__ void __launch_bounds__(256) k_mtime_extract(MtimeArgs a) {
+  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= a.n_live) return;
+  const uint32_t act = a.live[i];
+  int64_t mt = 0;
+  const bool from_json = a.act_flags ? !(a.act_flags[act] & F_FROM_CKPT) : act >= a.ck_rows;
+  if (from_json) {
+    const uint8_t* json = a.act_flags ? reinterpret_cast<const uint8_t*>(a.json_bases[a.src_id[act]]) : a.json;
+    const uint8_t* b = json + a.src_off[act];
+    const uint8_t* e = b + a.src_len[act];
+    const uint8_t* p = skip_ws(b, e);
+    const bool ok = each_member(p, e, [&](const uint8_t* k, uint32_t kn, bool kesc, const uint8_t* v) -> const uint8_t* {
+      if (key_is(k, kn, kesc, "add", 3) && v < e && *v == '{') {
+        const bool ok2 = each_member(v, e, [&](const uint8_t* k2, uint32_t kn2, bool kesc2, const uint8_t* v2) -> const uint8_t* {
+          const uint8_t* end2 = skip_value(v2, e);
+          if (key_is(k2, kn2, kesc2, "modificationTime", 16)) {
+            int64_t x;
+            mt = json_int64(v2, end2, &x) ? x : 0;  // a repeated member: the last one wins
+          }
+          return end2;
+        });
+        if (!ok2) return nullptr;
+      }
+      return skip_value(v, e);
+    });
+    if (!ok) atomicOr(a.error, 1u);
+  } else if (a.ck_def) {
+    const uint64_t r = a.src_off[act];
+    if (a.ck_def[r] == a.ck_max_def) mt = a.ck_val[r];
+  }
+  a.out[i] = mt;
+}
+
+struct ScanOrderLess {
+  const int64_t* mt;
+  const uint64_t* pp;
+  const uint32_t* pl;
+  __device__ bool operator()(uint32_t x, uint32_t y) const {
+    if (mt[x] != mt[y]) return mt[x] < mt[y];
+    const int c = bytes_cmp(reinterpret_cast<const uint8_t*>(pp[x]), pl[x], reinterpret_cast<const uint8_t*>(pp[y]), pl[y]);
+    return c != 0 ? c < 0 : x < y;
+  }
+};
+
+__device__ __forceinline__ int tuple_cmp(const GroupCols& g, uint32_t x, uint32_t y) {
+  for (int c = 0; c < g.ncols; ++c) {
+    const uint8_t nx = g.isnull[c][x], ny = g.isnull[c][y];
+    if (nx != ny) return nx ? -1 : 1;  // nulls first
+    if (nx) continue;
+    const int r = bytes_cmp(reinterpret_cast<const uint8_t*>(g.sptr[c][x]), g.slen[c][x],
+                            reinterpret_cast<const uint8_t*>(g.sptr[c][y]), g.slen[c][y]);
+    if (r) return r;
+  }
+  return 0;
+}
+
+struct GroupLess {
+  GroupCols g;
+  __device__ bool operator()(uint32_t x, uint32_t y) const {
+    const int c = tuple_cmp(g, x, y);
+    return c != 0 ? c < 0 : x < y;
+  }
+};
+
+__global__ void __launch_bounds__(256) k_group_flags(const uint32_t* keys, uint64_t n, GroupCols g, uint32_t* flag) {
+  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  flag[i] = i == 0 || tuple_cmp(g, keys[i - 1], keys[i]) != 0;
+}
+
+}  // namespace dev
+
+void launch_mtime_extract(const MtimeArgs& a, hipStream_t st) {
+  if (a.n_live) DR_LAUNCH(dev::k_mtime_extract, dim3(unsigned((a.n_live + 255) / 256)), dim3(256), 0, st, a);
+}
+
+void launch_sort_scan_order(void* temp, size_t* temp_bytes, uint32_t* keys, uint64_t n, const int64_t* mtime,
+                            const uint64_t* path_ptr, const uint32_t* path_len, hipStream_t st) {
+  const dev::ScanOrderLess less{mtime, path_ptr, path_len};
+  if (hipcub::DeviceMergeSort::SortKeys(temp, *temp_bytes, keys, n, less, st) != hipSuccess)
+    throw std::runtime_error("scan-order merge sort failed");
+}
+
+void launch_sort_groups(void* temp, size_t* temp_bytes, uint32_t* keys, uint64_t n, const GroupCols& g,
+                        hipStream_t st) {
+  const dev::GroupLess less{g};
+  if (hipcub::DeviceMergeSort::SortKeys(temp, *temp_bytes, keys, n, less, st) != hipSuccess)
+    throw std::runtime_error("partition-group merge sort failed");
+}
+
+void launch_group_flags(const uint32_t* keys, uint64_t n, const GroupCols& g, uint32_t* flag, hipStream_t st) {
+  if (n) DR_LAUNCH(dev::k_group_flags, dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, keys, n, g, flag);
 }
 
 }  // namespace dr

@@ -5,6 +5,11 @@
 namespace dr {
 namespace dev {
 
+__global__ void k_iota_u32(uint32_t* out, uint64_t n) {
+  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = uint32_t(i);
+}
+
 template <typename T, typename I>
 __global__ void k_gather(const T* __restrict__ src, const I* __restrict__ idx, uint64_t n, T* __restrict__ dst) {
   const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -46,6 +51,9 @@ void launch_gather_u32(const uint32_t* src, const uint32_t* idx, uint64_t n, uin
 }
 void launch_gather_u8(const uint8_t* src, const uint32_t* idx, uint64_t n, uint8_t* dst, hipStream_t st) {
   if (n) DR_LAUNCH((dev::k_gather<uint8_t, uint32_t>), dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, src, idx, n, dst);
+}
+void launch_iota_u32(uint32_t* out, uint64_t n, hipStream_t st) {
+  if (n) DR_LAUNCH(dev::k_iota_u32, dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, out, n);
 }
 void launch_gather_u16(const uint16_t* src, const uint32_t* idx, uint64_t n, uint16_t* dst, hipStream_t st) {
   if (n) DR_LAUNCH((dev::k_gather<uint16_t, uint32_t>), dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, src, idx, n, dst);

@@ -427,6 +427,7 @@ void launch_gather_u64(const uint64_t* src, const uint32_t* idx, uint64_t n, uin
 void launch_gather_u32(const uint32_t* src, const uint32_t* idx, uint64_t n, uint32_t* dst, hipStream_t st);
 void launch_gather_u8(const uint8_t* src, const uint32_t* idx, uint64_t n, uint8_t* dst, hipStream_t st);
 void launch_gather_u16(const uint16_t* src, const uint32_t* idx, uint64_t n, uint16_t* dst, hipStream_t st);
+void launch_iota_u32(uint32_t* out, uint64_t n, hipStream_t st);
 void launch_gather_u64_by64(const uint64_t* src, const uint64_t* idx, uint64_t n, uint64_t* dst, hipStream_t st);
 void launch_gather_bytes(const uint64_t* ptr, const uint32_t* len, const uint64_t* off, uint64_t n, uint8_t* out,
                          hipStream_t st);
@@ -475,4 +476,42 @@ void launch_ix_emit(const uint32_t* vals, uint64_t cap, const uint32_t* live_fla
                     hipStream_t st);
 void launch_ix_rehash(const unsigned long long* okeys, const uint32_t* ovals, uint64_t ocap,
                       unsigned long long* nkeys, uint32_t* nvals, uint64_t nmask, hipStream_t st);
+}  // namespace dr
+
+// ---- scan-side consumers (k_filter.hip): DeltaSourceSnapshot order, TahoeFileIndex grouping ---------
+namespace dr {
+// add.modificationTime of every live file: its JSON line's add object, or the checkpoint's decoded
+// add.modificationTime column (row-indexed values + definition levels).
+struct MtimeArgs {
+  const uint32_t* live;
+  uint64_t n_live;
+  const uint64_t* src_off;
+  const uint32_t* src_len;
+  uint64_t ck_rows;
+  const uint8_t* json;
+  const uint8_t* act_flags;
+  const uint16_t* src_id;
+  const uint64_t* json_bases;
+  const uint8_t* ck_def;  // null: no checkpoint column
+  const int64_t* ck_val;
+  int32_t ck_max_def;
+  int64_t* out;
+  uint32_t* error;
+};
+void launch_mtime_extract(const MtimeArgs& a, hipStream_t st);
+// Sorts live positions keys[0, n) by (mtime, path bytes) (Spark's ordering of (long, string):
+// strings compare as unsigned UTF-8 bytes). temp == null: *temp_bytes gets the scratch size.
+void launch_sort_scan_order(void* temp, size_t* temp_bytes, uint32_t* keys, uint64_t n, const int64_t* mtime,
+                            const uint64_t* path_ptr, const uint32_t* path_len, hipStream_t st);
+// Partition-value tuples of the live files (string columns of the K5 cache, by live position).
+struct GroupCols {
+  int32_t ncols;
+  const uint64_t* sptr[PV_MAXC];
+  const uint32_t* slen[PV_MAXC];
+  const uint8_t* isnull[PV_MAXC];
+};
+void launch_sort_groups(void* temp, size_t* temp_bytes, uint32_t* keys, uint64_t n, const GroupCols& g,
+                        hipStream_t st);
+// flag[i] = 1 where keys[i] starts a new tuple (i == 0 or it differs from keys[i - 1]).
+void launch_group_flags(const uint32_t* keys, uint64_t n, const GroupCols& g, uint32_t* flag, hipStream_t st);
 }  // namespace dr

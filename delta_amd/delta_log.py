@@ -32,7 +32,7 @@ class DeltaError(Exception):
     KIND = {3: "FileNotFoundException", 4: "FileNotFoundException", 5: "IllegalStateException",
             6: "IllegalStateException", 7: "IllegalArgumentException", 8: "IllegalStateException",
             9: "IllegalStateException", 10: "IllegalStateException", 11: "IllegalStateException",
-            16: "IllegalStateException"}
+            16: "IllegalStateException", 19: "AssertionError"}
 
     def __init__(self, status: int, msg: str):
         super().__init__(msg)
@@ -109,7 +109,10 @@ class Engine:
             self.check(self.lib.dr_stage_log(self.ctx, log_path.encode(), int(version), C.byref(h)))
         return Staged(self, h)
 
-    def stage_files(self, files: Sequence[Tuple[int, int, int, bytes]]) -> "Staged":
+    def stage_files(self, files: Sequence[Tuple[int, int, int, bytes]], log_path: Optional[str] = None,
+                    names: Optional[Sequence[str]] = None) -> "Staged":
+        """dr_stage; with `log_path` and the files' `names`, dr_stage_named (every named file must
+        sit in log_path: assertLogBelongsToTable, D/Snapshot.scala:334-345)."""
         arr = (N.dr_file * max(len(files), 1))()
         keep = []
         for i, (version, kind, part, data) in enumerate(files):
@@ -118,7 +121,11 @@ class Engine:
             arr[i] = N.dr_file(version, kind, part, C.cast(buf, C.c_void_p), len(data))
         h = C.c_void_p()
         with self.lock:
-            self.check(self.lib.dr_stage(self.ctx, arr, len(files), C.byref(h)))
+            if log_path is None:
+                self.check(self.lib.dr_stage(self.ctx, arr, len(files), C.byref(h)))
+            else:
+                nm = (C.c_char_p * max(len(files), 1))(*[(n or "").encode() for n in (names or [""] * len(files))])
+                self.check(self.lib.dr_stage_named(self.ctx, log_path.encode(), arr, nm, len(files), C.byref(h)))
         return Staged(self, h)
 
     def log_segment(self, log_path: str, version: int = -1):
@@ -317,6 +324,36 @@ class State:
         self.eng.lib.dr_free(C.cast(sel, C.c_void_p))
         return res
 
+    def _take(self, ptr, n) -> List[int]:
+        res = [ptr[i] for i in range(n)]
+        self.eng.lib.dr_free(C.cast(ptr, C.c_void_p))
+        return res
+
+    def scan_order(self) -> List[int]:
+        """dr_state_scan_order: live export positions sorted by (modificationTime, path bytes) on the
+        GPU (DeltaSourceSnapshot's allFiles.sort, D/files/DeltaSourceSnapshot.scala:53-95)."""
+        out = C.POINTER(C.c_int64)()
+        n = C.c_int64()
+        with self.eng.lock:
+            self.eng.check(self.eng.lib.dr_state_scan_order(self.h, C.byref(out), C.byref(n)))
+        return self._take(out, n.value)
+
+    def partition_groups(self, rows: Optional[Sequence[int]] = None) -> List[List[int]]:
+        """dr_state_partition_groups: `rows` (live export positions; None = all) grouped by the
+        table's partition values on the GPU (TahoeFileIndex.listFiles, D/files/TahoeFileIndex.scala:58-81)."""
+        order = C.POINTER(C.c_int64)()
+        off = C.POINTER(C.c_int64)()
+        ng = C.c_int64()
+        arr = (C.c_int64 * max(len(rows), 1))(*rows) if rows is not None else None
+        with self.eng.lock:
+            self.eng.check(self.eng.lib.dr_state_partition_groups(
+                self.h, C.cast(arr, C.POINTER(C.c_int64)) if arr is not None else None,
+                len(rows) if rows is not None else 0, C.byref(order), C.byref(off), C.byref(ng)))
+        nrows = len(rows) if rows is not None else self.counts["num_files"]
+        o = self._take(order, nrows)
+        g = self._take(off, ng.value + 1)
+        return [o[g[k]:g[k + 1]] for k in range(ng.value)]
+
     def release(self) -> None:
         if self.h:
             with self.eng.lock:
@@ -400,19 +437,22 @@ class Snapshot:
         from .predicates import partition_schema
         return partition_schema(self.metadata)
 
-    def files_for_scan(self, filters: Sequence) -> List[dict]:
-        """PartitionFiltering.filesForScan: metadata-only conjuncts, evaluated on the GPU."""
+    def _scan_rows(self, filters: Sequence) -> Optional[List[int]]:
+        """Live positions kept by the metadata-only conjuncts of `filters` (None: no pruning)."""
         from .predicates import split_metadata_and_data_predicates, build_program
         parts = (self.metadata or {}).get("partitionColumns") or []
         meta_preds = []
         for f in filters:
             meta_preds.extend(split_metadata_and_data_predicates(f, parts)[0])
         if not meta_preds:
-            return list(self.all_files)
-        prog = build_program(self.partition_schema(), meta_preds)
-        sel = self.state.filter(prog)
+            return None
+        return self.state.filter(build_program(self.partition_schema(), meta_preds))
+
+    def files_for_scan(self, filters: Sequence) -> List[dict]:
+        """PartitionFiltering.filesForScan: metadata-only conjuncts, evaluated on the GPU."""
+        sel = self._scan_rows(filters)
         files = self.all_files
-        return [files[i] for i in sel]
+        return list(files) if sel is None else [files[i] for i in sel]
 
     @property
     def checksum_opt(self) -> Optional[bytes]:
@@ -454,16 +494,14 @@ class Snapshot:
         from urllib.parse import unquote
         from .predicates import cast_partition_value
         schema = self.partition_schema()
-        groups: Dict[tuple, list] = {}
-        for f in self.files_for_scan(partition_filters):
-            pv = f.get("partitionValues") or {}
-            key = tuple(sorted(pv.items(), key=lambda kv: kv[0]))
-            groups.setdefault(key, [pv, []])[1].append(f)
+        rows = self._scan_rows(partition_filters)
+        files = self.all_files
         out = []
-        for pv, files in groups.values():
+        for grp in self.state.partition_groups(rows):  # grouped on the GPU
+            pv = files[grp[0]].get("partitionValues") or {}
             row = tuple(cast_partition_value(pv[c], t) for c, t in schema.items())
             stats = []
-            for f in files:
+            for f in (files[i] for i in grp):
                 p = unquote(f["path"].split("://", 1)[-1]) if "://" in f["path"] else unquote(f["path"])
                 if not (f["path"].startswith("/") or "://" in f["path"] or f["path"].startswith("file:")):
                     p = os.path.join(self.delta_log.data_path, p)
@@ -477,8 +515,7 @@ class Snapshot:
         order -- indexed by that order, then the partition-only filters applied (on the GPU, as
         filterFileList with the "add" prefix). Returns IndexedFile records."""
         files = self.all_files
-        order = sorted(range(len(files)), key=lambda i: (files[i]["modificationTime"],
-                                                         files[i]["path"].encode("utf-8")))
+        order = self.state.scan_order()  # sorted on the GPU
         rank = {i: r for r, i in enumerate(order)}
         parts = (self.metadata or {}).get("partitionColumns") or []
         from .predicates import is_partition_only, build_program

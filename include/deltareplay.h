@@ -47,8 +47,10 @@ enum dr_status {
   DR_E_INTERNAL = 15,
   DR_E_CHECKSUM = 16,     /* computed state differs from the version's .crc (IllegalStateException) */
   DR_E_NO_CHECKSUM = 17,  /* .crc empty or unparseable: ReadChecksum yields None, nothing to validate */
-  DR_E_REBUILD = 18       /* dr_state_apply cannot extend this base (e.g. its retention cutoff is later than
+  DR_E_REBUILD = 18,      /* dr_state_apply cannot extend this base (e.g. its retention cutoff is later than
                              the new one): the caller rebuilds the snapshot from its segment instead */
+  DR_E_FOREIGN_FILE = 19  /* a staged file is not in the table's _delta_log: AssertionError
+                             (assertLogBelongsToTable, D/Snapshot.scala:334-345) */
 };
 
 /* Segment file kinds (D/DeltaLogFileIndex.scala:67-68). */
@@ -131,6 +133,14 @@ int dr_log_segment(dr_ctx* ctx, const char* log_path, int64_t version_to_load,
  * Copies the segment's file bytes into HBM and plans the Parquet page decode (footer + page
  * headers, host). The staged input is reusable across dr_replay_staged calls. */
 int dr_stage(dr_ctx* ctx, const dr_file* files, int32_t nfiles, dr_staged** out);
+/* dr_stage with each file's name (a path or file: URI; "" = unnamed, as the reference's cached
+ * snapshots): every named file must sit directly in `log_path` -- the check Snapshot.stateReconstruction
+ * applies to input_file_name() of every row (assertLogBelongsToTable, D/Snapshot.scala:102,334-345) --
+ * or the call fails with DR_E_FOREIGN_FILE and the reference's AssertionError text; a name that
+ * contradicts its dr_file (not a FileNames delta/checkpoint name of that version and part,
+ * D/util/FileNames.scala:27-73) fails with DR_E_INVALID_ARG. */
+int dr_stage_named(dr_ctx* ctx, const char* log_path, const dr_file* files, const char* const* names,
+                   int32_t nfiles, dr_staged** out);
 /* Lists + reads the latest (or version_to_load) segment of `log_path` and stages it. */
 int dr_stage_log(dr_ctx* ctx, const char* log_path, int64_t version_to_load, dr_staged** out);
 int dr_staged_release(dr_staged* staged);
@@ -247,6 +257,21 @@ typedef struct dr_predicate {
 
 int dr_filter(dr_state* state, const dr_predicate* pred, int64_t** selected, int64_t* nselected);
 void dr_free(void* p);
+
+/* ---- scan-side consumers of the resident state -----------------------
+ * DeltaSourceSnapshot.initialFiles (D/files/DeltaSourceSnapshot.scala:53-95): allFiles.sort(
+ * "modificationTime", "path") computed on the device (modificationTime decoded from the live files'
+ * JSON lines / the checkpoint's add.modificationTime column; strings compare as unsigned UTF-8
+ * bytes). *order = the dr_state_export(DR_LIVE) positions in that order (freed with dr_free); the
+ * caller's zipWithIndex is the position in *order. */
+int dr_state_scan_order(dr_state* state, int64_t** order, int64_t* n);
+/* TahoeFileIndex.listFiles grouping (D/files/TahoeFileIndex.scala:58-81, groupBy(partitionValues)):
+ * `rows` (live positions, e.g. a dr_filter selection; NULL = every live file) grouped on the device
+ * by the raw values of the metadata's partitionColumns (null distinct from every string). *order
+ * holds the rows group by group (groups ordered by their values, nulls first; rows ascending in a
+ * group), *group_off the *ngroups + 1 group boundaries into it; both freed with dr_free. */
+int dr_state_partition_groups(dr_state* state, const int64_t* rows, int64_t nrows, int64_t** order,
+                              int64_t** group_off, int64_t* ngroups);
 
 /* ---- multi-GPU shards (one process per GPU) ------------------------------------
  * Replaces Snapshot.stateReconstruction's repartition(50, coalesce(add.path, remove.path)) shuffle

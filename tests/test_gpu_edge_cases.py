@@ -460,3 +460,44 @@ def test_incremental_update_falls_back_on_gap_or_newer_checkpoint(engine, tmp_pa
     assert snap.version == 7
     _assert_same(snap.state, O.state_reconstruction(O.get_log_segment(lp), snap.min_file_retention_timestamp))
     DeltaLog.clear_cache()
+
+
+# ---- assertLogBelongsToTable (D/Snapshot.scala:102,334-345) -----------------------------------------
+def test_stage_named_files_must_belong_to_the_log(engine, tmp_path):
+    """dr_stage_named: every named file must sit directly in the table's _delta_log (Hadoop Path
+    equality: a bare path is file:, repeated and trailing slashes are normalised, file:/ and
+    file:/// name the same path); a foreign file fails with the reference's AssertionError text; an
+    unnamed input ("", as the reference's cached snapshots) passes; a name that contradicts its
+    version fails."""
+    from delta_amd import _native as N
+    from delta_amd.delta_log import DeltaError
+    lp = str(tmp_path / "t" / "_delta_log")
+    other = str(tmp_path / "u" / "_delta_log")
+    os.makedirs(lp)
+    lines = ['{"protocol":{"minReaderVersion":1,"minWriterVersion":2}}',
+             '{"metaData":{"id":"x","format":{"provider":"parquet","options":{}},"schemaString":"{}",'
+             '"partitionColumns":[],"configuration":{}}}',
+             '{"add":{"path":"a.parquet","size":3,"modificationTime":1,"dataChange":true}}']
+    data = ("\n".join(lines) + "\n").encode()
+    files = [(0, N.DR_FILE_JSON, 0, data)]
+    name = "%020d.json" % 0
+    for nm in (lp + "/" + name, "file:" + lp + "/" + name, "file://" + lp + "/" + name,
+               lp.replace("/_delta_log", "//_delta_log") + "//" + name, ""):
+        st = engine.stage_files(files, log_path=lp, names=[nm])
+        try:
+            s = st.replay(0)
+            assert s.counts["num_files"] == 1
+            s.release()
+        finally:
+            st.release()
+    st = engine.stage_files(files, log_path=lp + "/", names=[lp + "/" + name])  # trailing slash on the log path
+    st.release()
+    bad = other + "/" + name
+    with pytest.raises(DeltaError) as ei:
+        engine.stage_files(files, log_path=lp, names=[bad])
+    assert ei.value.kind == "AssertionError"
+    assert str(ei.value).endswith("File (%s) doesn't belong in the transaction log at %s. Please contact "
+                                  "Databricks Support." % (bad, lp))
+    with pytest.raises(DeltaError) as ei:
+        engine.stage_files(files, log_path=lp, names=[lp + "/%020d.json" % 4])
+    assert "does not name a delta file of version 0" in str(ei.value)

@@ -225,3 +225,78 @@ def _gpu_replay_log(engine, lp, cutoff):
         return staged.replay(cutoff)
     finally:
         staged.release()
+
+
+def test_scan_order_and_partition_groups_on_device(engine, tmp_path):
+    """dr_state_scan_order / dr_state_partition_groups (the GPU side of DeltaSourceSnapshot's
+    allFiles.sort("modificationTime", "path") and TahoeFileIndex.listFiles' groupBy(partitionValues))
+    against the host export of the same state: checkpoint rows and JSON lines mixed, modificationTime
+    ties broken by the path's UTF-8 bytes, canonicalised absolute and escaped paths, the JSON forms
+    of modificationTime Jackson does not read as a long (missing, fraction, string, out of range:
+    the primitive's 0), null / escaped / missing partition values, and an applied tail."""
+    import json
+    from delta_amd import _native as N
+    from delta_amd.testing import synth as S
+    spec = S.ChurnSpec(ckpt_files=600, ckpt_version=1, n_deltas=2, removes_per_delta=60, adds_per_delta=60,
+                       readd_frac=0.5, ncols=2)
+    S.build_table(str(tmp_path), spec, seed=21, row_group_size=250)
+    lp = os.path.join(str(tmp_path), "_delta_log")
+    mt = S.T0 + 5 * 60000  # ties with synthetic adds of version 5 (mtime T0 + version * 60000 + k)
+    adds = [("/abs//x.parquet", '"p0":"2020-01-01","p1":"7"', str(mt)),
+            ("b.parquet", '"p0":"2020-01-01","p1":"7"', str(mt)),
+            ("a.parquet", '"p0":"2020-01-01","p1":null', str(mt)),
+            ("\\u00e9.parquet", '"p0":"2020-01-01","p1":"7"', str(mt)),
+            ("z\\u0301.parquet", '"p0":"2020-01-0\\u0031","p1":"7"', str(mt)),
+            ("m1.parquet", '"p0":"2020-01-02"', None),
+            ("m2.parquet", '"p0":"2020-01-02","p1":"8"', "1.5"),
+            ("m3.parquet", '"p0":"2020-01-02","p1":"8"', '"12"'),
+            ("m4.parquet", '"p0":"2020-01-02","p1":"8"', "99999999999999999999"),
+            ("m5.parquet", '"p0":"2020-01-02","p1":"8"', "-3"),
+            ("m6.parquet", '"p0":"2020-01-02","p1":"8"', "1e3")]
+    lines = []
+    for p, pv, m in adds:
+        mt_s = ',"modificationTime":%s' % m if m is not None else ""
+        lines.append('{"add":{"path":"%s","partitionValues":{%s},"size":1%s,"dataChange":true}}' % (p, pv, mt_s))
+    lines.append('{"add":{"path":"k.parquet","partitionValues":{"p0":"2020-01-03","p1":"1"},"size":2,'
+                 '"modificationTime":4,"modificationTime":%d,"dataChange":true}}' % mt)  # repeated member: the last
+    v = spec.ckpt_version + spec.n_deltas + 1
+    with open(os.path.join(lp, "%020d.json" % v), "w") as f:
+        f.write("\n".join(lines) + "\n")
+
+    def check(st):
+        live = st.export(0)
+        want = sorted(range(len(live)), key=lambda i: (live[i]["modificationTime"], live[i]["path"].encode("utf-8")))
+        assert st.scan_order() == want
+        for rows in (None, list(range(0, len(live), 3))):
+            groups = st.partition_groups(rows)
+            sel = list(range(len(live))) if rows is None else rows
+            assert sorted(i for g in groups for i in g) == sorted(sel)
+            keys = [tuple((live[i]["partitionValues"] or {}).get(c) for c in ("p0", "p1")) for i in sel]
+            assert len(groups) == len(set(keys))
+            for g in groups:
+                assert g == sorted(g)
+                assert len({tuple((live[i]["partitionValues"] or {}).get(c) for c in ("p0", "p1")) for i in g}) == 1
+        return live
+
+    staged = engine.stage_log(lp)
+    st = staged.replay(0)
+    staged.release()
+    try:
+        live = check(st)
+        byp = {r["path"]: r for r in live}
+        assert byp["m1.parquet"]["modificationTime"] == 0 and byp["m5.parquet"]["modificationTime"] == -3
+        assert byp["m4.parquet"]["modificationTime"] == 0 and byp["k.parquet"]["modificationTime"] == mt
+        # an applied tail (a chain state: JSON lines from two sources + checkpoint rows)
+        with open(os.path.join(lp, "%020d.json" % (v + 1)), "w") as f:
+            f.write('{"add":{"path":"t.parquet","partitionValues":{"p0":"2020-01-01","p1":"7"},"size":3,'
+                    '"modificationTime":%d,"dataChange":true}}\n{"remove":{"path":"b.parquet","deletionTimestamp":1}}\n' % mt)
+        with open(os.path.join(lp, "%020d.json" % (v + 1)), "rb") as f:
+            tail = engine.stage_files([(v + 1, N.DR_FILE_JSON, 0, f.read())])
+        st2 = st.apply(tail, 0)
+        tail.release()
+        try:
+            check(st2)
+        finally:
+            st2.release()
+    finally:
+        st.release()

@@ -5,6 +5,8 @@
 // (Parquet), canonicalisation, K3 (hash partition) and K4 (per-bucket last-writer-wins) on the
 // device and keeps the reconstructed state resident until dr_state_release.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <dlfcn.h>
 
 #include <algorithm>
 #include <functional>
@@ -2608,6 +2610,191 @@ static dr_state* shard_finish(dr_shard& sh, const uint8_t* verdict_back) {
 }
 
 // ---------------------------------------------------------------------------------------------------
+// the sharded replay inside the library: RCCL over xGMI, no host framework. The
+// communicator is the caller's (one per process and device); librccl is loaded on first use, so a
+// single-GPU host needs none. Collectives run on the context's stream, ordered with the kernels.
+// ---------------------------------------------------------------------------------------------------
+struct Rccl {
+  void* h = nullptr;
+  std::string why;
+  ncclResult_t (*get_id)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*group_start)() = nullptr;
+  ncclResult_t (*group_end)() = nullptr;
+  ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  const char* (*err)(ncclResult_t) = nullptr;
+};
+
+static Rccl& rccl() {
+  static Rccl r = [] {
+    Rccl x;
+    x.h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!x.h) x.h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+    if (!x.h) {
+      const char* e = dlerror();
+      x.why = e ? e : "dlopen failed";
+      return x;
+    }
+    auto sym = [&](auto& fn, const char* name) {
+      fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(x.h, name));
+      if (!fn && x.why.empty()) x.why = std::string("missing symbol ") + name;
+    };
+    sym(x.get_id, "ncclGetUniqueId");
+    sym(x.init_rank, "ncclCommInitRank");
+    sym(x.destroy, "ncclCommDestroy");
+    sym(x.send, "ncclSend");
+    sym(x.recv, "ncclRecv");
+    sym(x.group_start, "ncclGroupStart");
+    sym(x.group_end, "ncclGroupEnd");
+    sym(x.all_reduce, "ncclAllReduce");
+    sym(x.all_gather, "ncclAllGather");
+    sym(x.err, "ncclGetErrorString");
+    return x;
+  }();
+  if (!r.why.empty()) fail(DR_E_UNSUPPORTED, "librccl is not usable: " + r.why);
+  return r;
+}
+
+#define RC_OK(x)                                                                          \
+  do {                                                                                    \
+    const ncclResult_t rc_ = (x);                                                         \
+    if (rc_ != ncclSuccess) fail(DR_E_DEVICE, std::string("RCCL: ") + rccl().err(rc_) + " (" #x ")"); \
+  } while (0)
+
+struct dr_comm {
+  dr_ctx* ctx = nullptr;
+  ncclComm_t comm = nullptr;
+  int32_t world = 1, rank = 0;
+};
+
+// All-to-all of byte ranges: send[so_p, so_p + scnt[p]) to each peer p, recv rcnt[p] bytes from each
+// peer in rank order (grouped point-to-point: the xGMI links are peer-to-peer).
+static void rccl_all_to_all(dr_comm& c, const uint8_t* send, const std::vector<uint64_t>& scnt, uint8_t* recv,
+                            const std::vector<uint64_t>& rcnt) {
+  Rccl& R = rccl();
+  hipStream_t stream = c.ctx->stream;
+  RC_OK(R.group_start());
+  uint64_t so = 0, ro = 0;
+  for (int32_t p = 0; p < c.world; ++p) {
+    if (scnt[p]) RC_OK(R.send(send + so, scnt[p], ncclUint8, p, c.comm, stream));
+    if (rcnt[p]) RC_OK(R.recv(recv + ro, rcnt[p], ncclUint8, p, c.comm, stream));
+    so += scnt[p];
+    ro += rcnt[p];
+  }
+  RC_OK(R.group_end());
+}
+
+static std::vector<std::string> rccl_all_gather_text(dr_comm& c, const std::string& mine) {
+  Rccl& R = rccl();
+  dr_ctx* ctx = c.ctx;
+  hipStream_t stream = ctx->stream;
+  DBuf<uint64_t> len(ctx, 1), lens(ctx, c.world);
+  const uint64_t n = mine.size();
+  HIP_OK(hipMemcpyAsync(len.p, &n, 8, hipMemcpyHostToDevice, stream));
+  RC_OK(R.all_gather(len.p, lens.p, 1, ncclUint64, c.comm, stream));
+  const std::vector<uint64_t> L = d2h(lens.p, c.world, stream);
+  uint64_t mx = 1;
+  for (uint64_t x : L) mx = std::max(mx, x);
+  DBuf<uint8_t> slot(ctx, mx), all(ctx, mx * c.world);
+  if (n) HIP_OK(hipMemcpyAsync(slot.p, mine.data(), n, hipMemcpyHostToDevice, stream));
+  RC_OK(R.all_gather(slot.p, all.p, mx, ncclUint8, c.comm, stream));
+  const std::vector<uint8_t> h = d2h(all.p, mx * c.world, stream);
+  std::vector<std::string> out;
+  for (int32_t p = 0; p < c.world; ++p)
+    out.emplace_back(reinterpret_cast<const char*>(h.data() + uint64_t(p) * mx), L[p]);
+  return out;
+}
+
+// One rank's part of the sharded replay (collective over the communicator; every rank stages its
+// own slice with dr_stage_log_shard). The returned state holds this rank's surviving records (its
+// export is its share of allFiles / tombstones) and the table-wide counters and non-file winners.
+static dr_state* replay_sharded_rccl(dr_comm& c, const std::shared_ptr<StagedData>& staged, int64_t cutoff,
+                                     uint32_t flags) {
+  dr_ctx* ctx = c.ctx;
+  hipStream_t stream = ctx->stream;
+  Rccl& R = rccl();
+  const uint32_t W = uint32_t(c.world);
+  dr_shard sh;
+  sh.ctx = ctx;
+  sh.staged = staged;
+  sh.world = W;
+  std::vector<uint64_t> sc(W), sb(W);
+  shard_begin(sh, sc.data(), sb.data());
+  // every rank's send counts and bytes: recv counts are this rank's column
+  DBuf<uint64_t> mine(ctx, 2 * W), all(ctx, 2 * uint64_t(W) * W);
+  std::vector<uint64_t> m(sc);
+  m.insert(m.end(), sb.begin(), sb.end());
+  HIP_OK(hipMemcpyAsync(mine.p, m.data(), 16 * W, hipMemcpyHostToDevice, stream));
+  RC_OK(R.all_gather(mine.p, all.p, 2 * W, ncclUint64, c.comm, stream));
+  const std::vector<uint64_t> M = d2h(all.p, 2 * uint64_t(W) * W, stream);
+  std::vector<uint64_t> rc(W), rb(W), scb(W), rcb(W);
+  uint64_t nrecv = 0, nrecv_b = 0, nsend = 0, nsend_b = 0;
+  for (uint32_t p = 0; p < W; ++p) {
+    rc[p] = M[uint64_t(p) * 2 * W + c.rank];
+    rb[p] = M[uint64_t(p) * 2 * W + W + c.rank];
+    scb[p] = sc[p] * sizeof(ShardRec);
+    rcb[p] = rc[p] * sizeof(ShardRec);
+    nrecv += rc[p];
+    nrecv_b += rb[p];
+    nsend += sc[p];
+    nsend_b += sb[p];
+  }
+  DBuf<uint8_t> send_rec(ctx, std::max<uint64_t>(nsend, 1) * sizeof(ShardRec)), send_path(ctx, nsend_b + 1),
+      recv_rec(ctx, std::max<uint64_t>(nrecv, 1) * sizeof(ShardRec)), recv_path(ctx, nrecv_b + 1),
+      verdict(ctx, nrecv + 1), back(ctx, nsend + 1);
+  shard_pack(sh, send_rec.p, send_path.p);
+  rccl_all_to_all(c, send_rec.p, scb, recv_rec.p, rcb);
+  rccl_all_to_all(c, send_path.p, sb, recv_path.p, rb);
+  shard_reduce(sh, recv_rec.p, nrecv, recv_path.p, cutoff, verdict.p);
+  rccl_all_to_all(c, verdict.p, rc, back.p, sc);
+  std::unique_ptr<dr_state> st(shard_finish(sh, back.p));
+  // table-wide counters: the owner-side partial sums over the ranks
+  dr_counts& k = st->counts;
+  const int64_t part[8] = {k.num_files, k.size_in_bytes, k.num_removes, k.num_actions, k.num_file_actions,
+                           k.malformed_lines, int64_t(k.live_key_sum), int64_t(k.tomb_key_sum)};
+  DBuf<int64_t> sums(ctx, 8);
+  HIP_OK(hipMemcpyAsync(sums.p, part, sizeof(part), hipMemcpyHostToDevice, stream));
+  RC_OK(R.all_reduce(sums.p, sums.p, 8, ncclInt64, ncclSum, c.comm, stream));
+  const std::vector<int64_t> t = d2h(sums.p, 8, stream);
+  k.num_files = t[0];
+  k.size_in_bytes = t[1];
+  k.num_removes = t[2];
+  k.num_actions = t[3];
+  k.num_file_actions = t[4];
+  k.malformed_lines = t[5];
+  k.live_key_sum = uint64_t(t[6]);
+  k.tomb_key_sum = uint64_t(t[7]);
+  // non-file winners: every rank's, in rank order (= replay order: slices are contiguous)
+  std::string text;
+  for (const NonFileAction& a : st->nonfile) text += a.json + "\n";
+  std::vector<NonFileAction> merged;
+  for (const std::string& part_text : rccl_all_gather_text(c, text)) {
+    size_t b = 0;
+    while (b < part_text.size()) {
+      size_t e = part_text.find('\n', b);
+      if (e == std::string::npos) e = part_text.size();
+      JVal v;
+      if (e > b && json_parse(part_text.data() + b, e - b, &v) && v.t == JVal::OBJ && !v.o.empty()) {
+        NonFileAction a;
+        const std::string& key = v.o[0].first;
+        a.kind = key == "metaData" ? 3 : key == "txn" ? 4 : 5;
+        a.order = merged.size();
+        a.val = v.o[0].second;
+        a.json = part_text.substr(b, e - b);
+        merged.push_back(std::move(a));
+      }
+      b = e + 1;
+    }
+  }
+  reduce_nonfile(*st, merged, !(flags & DR_FLAG_NO_VALIDATION));
+  return st.release();
+}
+
+// ---------------------------------------------------------------------------------------------------
 // per-line commit decode (getChanges' Action.fromJson hot fields; K1 only)
 // ---------------------------------------------------------------------------------------------------
 struct dr_parsed {
@@ -3169,6 +3356,57 @@ int dr_parse_commits(dr_ctx* ctx, const dr_staged* staged, dr_parsed** out, dr_l
     lines->bytes = p->staged->h_json.data();
     lines->nbytes = p->staged->h_json.size();
     *out = p.release();
+  });
+}
+
+int dr_comm_unique_id(uint8_t* id) {
+  if (!id) return DR_E_INVALID_ARG;
+  try {
+    ncclUniqueId u;
+    if (rccl().get_id(&u) != ncclSuccess) return DR_E_DEVICE;
+    memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+    return DR_OK;
+  } catch (const Error& e) {
+    return e.status;
+  } catch (...) {
+    return DR_E_INTERNAL;
+  }
+}
+
+int dr_comm_create(dr_ctx* ctx, const uint8_t* id, int32_t world, int32_t rank, dr_comm** out) {
+  if (!ctx || !id || !out || world < 1 || rank < 0 || rank >= world || uint32_t(world) > shard_max_world())
+    return DR_E_INVALID_ARG;
+  *out = nullptr;
+  return guard(ctx, [&] {
+    HIP_OK(hipSetDevice(ctx->device));
+    ncclUniqueId u;
+    memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+    auto c = std::make_unique<dr_comm>();
+    c->ctx = ctx;
+    c->world = world;
+    c->rank = rank;
+    RC_OK(rccl().init_rank(&c->comm, world, u, rank));
+    *out = c.release();
+  });
+}
+
+int dr_comm_release(dr_comm* comm) {
+  if (!comm) return DR_E_INVALID_ARG;
+  if (comm->comm) (void)rccl().destroy(comm->comm);
+  delete comm;
+  return DR_OK;
+}
+
+int dr_replay_sharded(dr_comm* comm, const dr_staged* staged, int64_t min_file_retention_timestamp, uint32_t flags,
+                      dr_state** out) {
+  if (!comm || !staged || !out) return DR_E_INVALID_ARG;
+  *out = nullptr;
+  dr_ctx* ctx = comm->ctx;
+  return guard(ctx, [&] {
+    HIP_OK(hipSetDevice(ctx->device));
+    ctx->begin_call();
+    *out = replay_sharded_rccl(*comm, staged->d, min_file_retention_timestamp, flags);
+    ctx->collect_timings();
   });
 }
 

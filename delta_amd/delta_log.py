@@ -128,6 +128,22 @@ class Engine:
                 self.check(self.lib.dr_stage_named(self.ctx, log_path.encode(), arr, nm, len(files), C.byref(h)))
         return Staged(self, h)
 
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        """dr_comm_unique_id: the 128-byte RCCL id one rank creates and shares with the others."""
+        buf = C.create_string_buffer(128)
+        rc = N.lib().dr_comm_unique_id(buf)
+        if rc != N.DR_OK:
+            raise DeltaError(rc, "dr_comm_unique_id failed (%s)" % N.STATUS.get(rc, rc))
+        return buf.raw
+
+    def comm(self, uid: bytes, world: int, rank: int) -> "Comm":
+        """dr_comm_create: this rank's RCCL communicator (collective over the `world` ranks)."""
+        h = C.c_void_p()
+        with self.lock:
+            self.check(self.lib.dr_comm_create(self.ctx, uid, int(world), int(rank), C.byref(h)))
+        return Comm(self, h)
+
     def log_segment(self, log_path: str, version: int = -1):
         need = C.c_uint64()
         ver = C.c_int64()
@@ -141,6 +157,27 @@ class Engine:
             kind, v, part, name = line.split(" ", 3)
             files.append((int(kind), int(v), int(part), name))
         return ver.value, files
+
+
+class Comm:
+    """An RCCL communicator of the library's in-process sharded replay (dr_replay_sharded)."""
+
+    def __init__(self, eng: "Engine", h):
+        self.eng = eng
+        self.h = h
+
+    def replay_sharded(self, staged: "Staged", min_file_retention_timestamp: int, validate: bool = True) -> "State":
+        st = C.c_void_p()
+        flags = 0 if validate else N.DR_FLAG_NO_VALIDATION
+        with self.eng.lock:
+            self.eng.check(self.eng.lib.dr_replay_sharded(self.h, staged.h, int(min_file_retention_timestamp), flags,
+                                                          C.byref(st)))
+        return State(self.eng, st)
+
+    def release(self) -> None:
+        if self.h:
+            self.eng.lib.dr_comm_release(self.h)
+            self.h = None
 
 
 class Staged:

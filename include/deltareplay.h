@@ -310,6 +310,21 @@ int dr_shard_reduce(dr_shard* shard, const void* recv_rec, uint64_t n_recv, cons
 int dr_shard_finish(dr_shard* shard, const uint8_t* verdict_back, dr_state** out);
 int dr_shard_release(dr_shard* shard);
 
+/* The whole sharded replay inside the library, over RCCL (xGMI): no host framework is needed (the
+ * JNI host has no torch). Same semantics as the dr_shard_* steps driven by delta_amd/sharded.py:
+ * every rank stages its slice (dr_stage_log_shard) and calls dr_replay_sharded collectively; the
+ * exchange is grouped ncclSend/ncclRecv on the context's stream, counts and non-file winners go
+ * through ncclAllGather, the counters through ncclAllReduce. The returned state exports this rank's
+ * surviving records; its counters and non-file winners are table-wide. The communicator comes from
+ * one dr_comm_unique_id shared by the caller's own means (e.g. the Spark driver) and one
+ * dr_comm_create per rank; librccl is loaded on first use (DR_E_UNSUPPORTED when absent). */
+typedef struct dr_comm dr_comm;
+int dr_comm_unique_id(uint8_t* id /* 128 bytes */);
+int dr_comm_create(dr_ctx* ctx, const uint8_t* id, int32_t world, int32_t rank, dr_comm** out);
+int dr_comm_release(dr_comm* comm);
+int dr_replay_sharded(dr_comm* comm, const dr_staged* staged, int64_t min_file_retention_timestamp, uint32_t flags,
+                      dr_state** out);
+
 /* ---- measurement hooks (bench.py) ----------------------------------------------------------
  * Per-stage device time of the last dr_replay_staged on this context (HIP events on the
  * context's stream), in milliseconds; names are returned NUL-separated. */

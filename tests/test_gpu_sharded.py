@@ -93,3 +93,64 @@ def test_sharded_two_processes_gloo(tmp_path):
                       env={"DR_TEST_BACKEND": "gloo"})
     snap = O.state_reconstruction(O.get_log_segment(lp), exp.min_file_retention_timestamp)
     _check(res["counts"], res["live"], res["tomb"], snap)
+
+
+# ---- the sharded replay inside the library (RCCL, dr_replay_sharded) ----------------------------------
+@pytest.mark.parametrize("name", ["delta-0.2.0", "dbr_8_1_generated_columns"])
+def test_rccl_library_single_rank(name):
+    """dr_comm_create + dr_replay_sharded with one rank: the RCCL collectives (all-gather of counts
+    and non-file winners, grouped send/recv to self, all-reduce of the counters) run for real and the
+    state equals the oracle's."""
+    from delta_amd.delta_log import Engine
+    from delta_amd.sharded import stage_shard
+    lp = os.path.join(REF, name, "_delta_log")
+    cutoff = 1564524298213
+    eng = Engine.get(0)
+    comm = eng.comm(Engine.comm_unique_id(), 1, 0)
+    try:
+        staged = stage_shard(eng, lp, 1, 0)
+        st = comm.replay_sharded(staged, cutoff)
+        staged.release()
+        try:
+            _check(st.counts, st.export(0), st.export(1), O.state_reconstruction(O.get_log_segment(lp), cutoff))
+        finally:
+            st.release()
+    finally:
+        comm.release()
+
+
+def test_rccl_library_two_processes(tmp_path):
+    """Two processes, one communicator, both on this box's one GPU. RCCL refuses two ranks on one
+    device ("duplicate GPU"); then the test is skipped (the exchange logic is the one the thread and
+    gloo tests cover; the RCCL calls themselves ran in the single-rank test)."""
+    import subprocess
+    import sys
+    from delta_amd.testing import synth as S
+    exp = S.build_table(str(tmp_path / "t"), S.config_spec(2, 0.002), seed=9, row_group_size=500)
+    lp = os.path.join(str(tmp_path / "t"), "_delta_log")
+    cutoff = exp.min_file_retention_timestamp
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "rccl_rank.py")
+    uid = str(tmp_path / "uid")
+    outs = [str(tmp_path / ("r%d.json" % r)) for r in range(2)]
+    procs = [subprocess.Popen([sys.executable, script, lp, str(cutoff), "2", str(r), uid, outs[r]],
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, start_new_session=True)
+             for r in range(2)]
+    logs = []
+    try:
+        for p in procs:
+            logs.append(p.communicate(timeout=120)[0].decode(errors="replace"))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                os.killpg(p.pid, 9)
+    res = []
+    for o, lg in zip(outs, logs):
+        if not os.path.exists(o):
+            pytest.skip("RCCL run did not complete on one device: " + lg[-400:])
+        with open(o) as f:
+            res.append(json.load(f))
+    if any("error" in r for r in res):
+        pytest.skip("RCCL refuses two ranks on one device: " + " | ".join(r.get("error", "") for r in res))
+    snap = O.state_reconstruction(O.get_log_segment(lp), cutoff)
+    assert res[0]["counts"] == res[1]["counts"] and res[0]["nonfile"] == res[1]["nonfile"]
+    _check(res[0]["counts"], res[0]["live"] + res[1]["live"], res[0]["tomb"] + res[1]["tomb"], snap)

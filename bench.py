@@ -455,13 +455,21 @@ def main():
     # end to end once: file bytes -> HBM (read + H2D + page planning), replay, allFiles export
     e2e = None
     if world == 1:
+        import ctypes as C
+        from delta_amd import _native as N
         t1 = time.perf_counter()
         st = staged.replay(cutoff)
         torch.cuda.synchronize()
         t2 = time.perf_counter()
+        # allFiles + tombstones as host columns (dr_state_export: device extraction + one copy)
+        ex = N.dr_export()
+        for which in (N.DR_LIVE, N.DR_TOMBSTONES):
+            eng.check(eng.lib.dr_state_export(st.h, which, C.byref(ex)))
+        t3 = time.perf_counter()
         st.release()
-        e2e = {"stage_s": round(stage_s, 3), "replay_s": round(t2 - t1, 4),
-               "actions_per_s_incl_staging": round(counts["num_actions"] / (stage_s + t2 - t1), 1)}
+        e2e = {"stage_s": round(stage_s, 3), "replay_s": round(t2 - t1, 4), "export_s": round(t3 - t2, 4),
+               "actions_per_s_incl_staging": round(counts["num_actions"] / (stage_s + t2 - t1), 1),
+               "actions_per_s_incl_staging_and_export": round(counts["num_actions"] / (stage_s + t3 - t1), 1)}
     k5 = None
     if world == 1 and args.config == 4:
         k5 = measure_filter(eng, staged, cutoff, exp, args.steps)

@@ -307,6 +307,7 @@ struct StagedData {
   std::vector<NonFileAction> ck_nonfile;  // protocol/metaData/txn rows of the checkpoint
   std::unique_ptr<PagePlan> pv;           // add.partitionValues map columns (planned on first filter)
   std::unique_ptr<PagePlan> mt;           // add.modificationTime (planned on first scan order)
+  std::unique_ptr<PagePlan> exp[2];       // the export's add / remove leaves (planned on first export)
   std::mutex pv_mu;
 };
 
@@ -1587,197 +1588,230 @@ static dr_state* replay(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, int6
 // ---------------------------------------------------------------------------------------------------
 // export (records materialised on the host from the resident state)
 // ---------------------------------------------------------------------------------------------------
-struct RecordFields {
-  std::string path;
-  int64_t size = 0, mtime = 0, delts = 0;
-  bool delts_valid = false, efm = false;
-  bool stats_null = true;
-  std::string stats;
-  bool pv_null = true, tags_null = true;
-  std::vector<std::pair<std::string, std::pair<bool, std::string>>> pv, tags;  // key -> (null?, value)
-};
-
-static void map_from_json(const JVal* v, bool* is_null, std::vector<std::pair<std::string, std::pair<bool, std::string>>>& out) {
-  if (!v || v->t == JVal::NUL) { *is_null = true; return; }
-  *is_null = false;
-  if (v->t != JVal::OBJ) return;
-  std::map<std::string, size_t> seen;
-  for (auto& kv : v->o) {
-    std::pair<bool, std::string> val{kv.second.t == JVal::NUL, kv.second.t == JVal::STR ? kv.second.s : json_dump(kv.second)};
-    auto it = seen.find(kv.first);
-    if (it != seen.end()) { out[it->second].second = val; continue; }
-    seen[kv.first] = out.size();
-    out.emplace_back(kv.first, val);
-  }
+template <typename T>
+static DBuf<T> upload(dr_ctx* ctx, const T* src, size_t n) {
+  DBuf<T> d(ctx, n);
+  if (n) HIP_OK(hipMemcpyAsync(d.p, src, n * sizeof(T), hipMemcpyHostToDevice, ctx->stream));
+  return d;
 }
 
-static void fields_from_json(const JVal& o, RecordFields& r) {
-  auto i64 = [&](const char* k, int64_t* dst, bool* valid) {
-    const JVal* v = o.get(k);
-    if (v && v->is_int()) { *dst = v->as_int(); if (valid) *valid = true; }
-  };
-  i64("size", &r.size, nullptr);
-  i64("modificationTime", &r.mtime, nullptr);
-  i64("deletionTimestamp", &r.delts, &r.delts_valid);
-  const JVal* e = o.get("extendedFileMetadata");
-  r.efm = e && e->t == JVal::BOOL && e->b;
-  const JVal* st = o.get("stats");
-  if (st && st->t != JVal::NUL) { r.stats_null = false; r.stats = st->t == JVal::STR ? st->s : json_dump(*st); }
-  map_from_json(o.get("partitionValues"), &r.pv_null, r.pv);
-  map_from_json(o.get("tags"), &r.tags_null, r.tags);
-}
-
-// Checkpoint rows of one side (add or remove) decoded on the host for export.
-struct CkRows {
-  std::unordered_map<int64_t, RecordFields> rows;
+// Export of one side, built on the device (k_export): the canonical paths and the replay's
+// size / deletionTimestamp from the action arrays, every other field from the survivor's JSON line
+// or from the checkpoint's leaves of that side (decoded on first export, K2's page decoder), then one
+// copy of the columns to the host.
+struct ExpDecoded {
+  DBuf<uint8_t> def[8], rep[8];
+  DBuf<int64_t> ival[8];
+  DBuf<uint64_t> sptr[8], row_start[2];
+  DBuf<uint32_t> slen[8];
+  ExpFlat flat[4]{};
+  ExpMap map[2]{};
 };
 
-static void load_ck_side(StagedData& s, bool add, CkRows& out) {
-  const char* pre = add ? "add." : "remove.";
-  for (CkPart& part : s.parts) {
-    const uint8_t* file = s.h_pq.data() + part.off;
-    int64_t rg_base = int64_t(part.row_base);
-    for (size_t gi = size_t(part.rg_lo); gi < part.rg_end(); ++gi) {
-      const pq::RowGroup& rg = part.meta.row_groups[gi];
-      auto col = [&](const std::string& name, int depth, std::vector<pq::Entry>* v, const pq::Leaf** lf) {
-        std::string path = std::string(pre) + name;
-        const pq::Leaf* l = part.meta.leaf(path);
-        if (lf) *lf = l;
-        for (auto& c : rg.cols)
-          if (c.path == path && l) { *v = pq::sparse_entries(file, part.len, c, *l, l->def_of[size_t(depth)], rg_base); return; }
-      };
-      std::vector<pq::Entry> size, mtime, delts, efm, stats, pvk, pvv, tk, tv;
-      const pq::Leaf *pvl = nullptr, *tl = nullptr;
-      col("size", 0, &size, nullptr);
-      col("modificationTime", 0, &mtime, nullptr);
-      col("deletionTimestamp", 0, &delts, nullptr);
-      col("extendedFileMetadata", 0, &efm, nullptr);
-      col("stats", 0, &stats, nullptr);
-      col("partitionValues.key_value.key", 0, &pvk, &pvl);
-      col("partitionValues.key_value.value", 0, &pvv, nullptr);
-      col("tags.key_value.key", 0, &tk, &tl);
-      col("tags.key_value.value", 0, &tv, nullptr);
-      for (auto& e : size) if (e.has_value) out.rows[e.row].size = e.ival;
-      for (auto& e : mtime) if (e.has_value) out.rows[e.row].mtime = e.ival;
-      for (auto& e : delts) if (e.has_value) { out.rows[e.row].delts = e.ival; out.rows[e.row].delts_valid = true; }
-      for (auto& e : efm) if (e.has_value) out.rows[e.row].efm = e.ival != 0;
-      for (auto& e : stats) if (e.has_value) { out.rows[e.row].stats = e.sval; out.rows[e.row].stats_null = false; }
-      auto maps = [&](std::vector<pq::Entry>& ks, std::vector<pq::Entry>& vs, const pq::Leaf* l, bool pvmap) {
-        if (!l) return;
-        const int map_def = l->def_of[1];      // partitionValues non-null
-        const int entry_def = l->def_of[2];    // key_value present
-        for (size_t i = 0; i < ks.size(); ++i) {
-          RecordFields& r = out.rows[ks[i].row];
-          bool& isnull = pvmap ? r.pv_null : r.tags_null;
-          if (ks[i].def >= map_def) isnull = false;
-          if (ks[i].def < entry_def) continue;
-          bool vnull = !(i < vs.size() && vs[i].has_value);
-          (pvmap ? r.pv : r.tags).emplace_back(ks[i].sval, std::make_pair(vnull, vnull ? std::string() : vs[i].sval));
-        }
-      };
-      maps(pvk, pvv, pvl, true);
-      maps(tk, tv, tl, false);
-      rg_base += rg.num_rows;
+static const char* kExpLeaf[8] = {"size", "modificationTime", "extendedFileMetadata", "stats",
+                                  "partitionValues.key_value.key", "partitionValues.key_value.value",
+                                  "tags.key_value.key", "tags.key_value.value"};
+
+static void decode_export_side(dr_state& st, int which, ExpDecoded& D) {
+  dr_ctx* ctx = st.ctx;
+  hipStream_t stream = ctx->stream;
+  StagedData& s = *st.sources[0];
+  const uint64_t R = s.ck_rows;
+  if (!R) return;
+  const std::string pre = which == DR_LIVE ? "add." : "remove.";
+  {
+    std::lock_guard<std::mutex> g(s.pv_mu);
+    if (!s.exp[which]) {
+      auto P = std::make_unique<PagePlan>();
+      for (const char* leaf : kExpLeaf) P->paths.push_back(pre + leaf);
+      plan_pages(s, *P);
+      s.exp[which] = std::move(P);
     }
   }
+  PagePlan& P = *s.exp[which];
+  ParquetArgs pa{};
+  pa.ncols = 8;
+  for (int c = 0; c < 8; ++c) {
+    if (!P.present[c]) continue;
+    const uint64_t L = P.levels[c];
+    D.def[c] = DBuf<uint8_t>(ctx, L);
+    D.def[c].zero(stream);
+    const bool str = c == 3 || c >= 4;
+    if (c >= 4) D.rep[c] = DBuf<uint8_t>(ctx, L);
+    if (str) {
+      D.sptr[c] = DBuf<uint64_t>(ctx, L);
+      D.slen[c] = DBuf<uint32_t>(ctx, L);
+    } else {
+      D.ival[c] = DBuf<int64_t>(ctx, L);
+    }
+    pa.cols[c] = FlatColumn{D.def[c].p, D.rep[c].p, D.ival[c].p, D.sptr[c].p, D.slen[c].p};
+  }
+  DBuf<uint64_t> dict_ptr;
+  DBuf<uint32_t> dict_len, pq_err(ctx, 1);
+  pq_err.zero(stream);
+  decode_pages(ctx, P, pa, dict_ptr, dict_len, pq_err, nullptr);
+  if (d2h_one(pq_err.p, stream) != 0)
+    fail(DR_E_PARQUET, fmt("device decode of the %sexport columns failed (code %u)", pre.c_str(), d2h_one(pq_err.p, stream)));
+  for (int c = 0; c < 4; ++c) {
+    if (!P.present[c]) continue;
+    if (P.levels[c] != R) fail(DR_E_PARQUET, pre + kExpLeaf[c] + ": one value per checkpoint row expected");
+    D.flat[c] = ExpFlat{D.def[c].p, D.ival[c].p, D.sptr[c].p, D.slen[c].p, P.max_def[c]};
+  }
+  for (int m = 0; m < 2; ++m) {
+    const int kc = 4 + 2 * m, vc = kc + 1;
+    if (!P.present[kc] || !P.present[vc]) continue;
+    const uint64_t E = P.levels[kc];
+    if (P.levels[vc] != E) fail(DR_E_PARQUET, pre + kExpLeaf[kc] + ": key/value columns disagree");
+    const pq::Leaf* leaf = s.parts[0].meta.leaf(pre + kExpLeaf[kc]);
+    if (!leaf || leaf->def_of.size() < 3) fail(DR_E_PARQUET, pre + kExpLeaf[kc] + ": unexpected map layout");
+    DBuf<uint32_t> rflag(ctx, E);
+    DBuf<uint64_t> rpos(ctx, E + 1);
+    DBuf<uint8_t> scratch(ctx, scan_scratch_for(E));
+    launch_rep0_flags(D.rep[kc].p, E, rflag.p, stream);
+    launch_scan_u32(rflag.p, rpos.p, E, scratch.p, stream);
+    if (d2h_one(rpos.p + E, stream) != R) fail(DR_E_PARQUET, pre + kExpLeaf[kc] + ": one map per checkpoint row expected");
+    D.row_start[m] = DBuf<uint64_t>(ctx, R + 1);
+    launch_row_starts(D.rep[kc].p, E, rpos.p, D.row_start[m].p, stream);
+    HIP_OK(hipMemcpyAsync(D.row_start[m].p + R, &E, 8, hipMemcpyHostToDevice, stream));
+    D.map[m] = ExpMap{D.row_start[m].p, D.def[kc].p, D.sptr[kc].p, D.slen[kc].p, D.def[vc].p, D.sptr[vc].p,
+                      D.slen[vc].p, leaf->def_of[1], leaf->def_of[2], P.max_def[vc]};
+  }
 }
 
-constexpr uint8_t kFromCkpt = 16;  // dev_common.h F_FROM_CKPT: the action is a checkpoint row
+template <typename T>
+static std::vector<int64_t> to_i64(const std::vector<T>& v) {
+  return std::vector<int64_t>(v.begin(), v.end());
+}
 
 static void build_export(dr_state& st, int which) {
   ensure_ready(st);
   ExportCols& ex = st.exp[which];
   if (ex.built) return;
-  hipStream_t stream = st.ctx->stream;
+  dr_ctx* ctx = st.ctx;
+  hipStream_t stream = ctx->stream;
   StagedData& s = *st.sources[0];
   const uint64_t n = which == DR_LIVE ? st.n_live : st.n_tomb;
-  std::vector<uint32_t> idx = d2h(which == DR_LIVE ? st.live.p : st.tomb.p, n, stream);
-  std::vector<uint64_t> pptr(n), soff(n);
-  std::vector<uint32_t> plen(n), slen(n);
-  std::vector<uint8_t> aflags;
-  std::vector<uint16_t> sid;
-  if (st.src_id.p) {  // a state from dr_state_apply: checkpoint rows by flag, JSON by source
-    DBuf<uint8_t> f(st.ctx, n);
-    DBuf<uint16_t> g(st.ctx, n);
-    launch_gather_u8(st.flags.p, which == DR_LIVE ? st.live.p : st.tomb.p, n, f.p, stream);
-    launch_gather_u16(st.src_id.p, which == DR_LIVE ? st.live.p : st.tomb.p, n, g.p, stream);
-    aflags = d2h(f.p, n, stream);
-    sid = d2h(g.p, n, stream);
-  }
-  // gather the per-action fields (small D2H per record batch)
-  {
-    const uint32_t* didx = which == DR_LIVE ? st.live.p : st.tomb.p;
-    DBuf<uint64_t> a(st.ctx, n), b(st.ctx, n);
-    DBuf<uint32_t> c(st.ctx, n), d(st.ctx, n);
-    launch_gather_u64(st.path_ptr.p, didx, n, a.p, stream);
-    launch_gather_u64(st.src_off.p, didx, n, b.p, stream);
-    launch_gather_u32(st.path_len.p, didx, n, c.p, stream);
-    launch_gather_u32(st.src_len.p, didx, n, d.p, stream);
-    pptr = d2h(a.p, n, stream);
-    soff = d2h(b.p, n, stream);
-    plen = d2h(c.p, n, stream);
-    slen = d2h(d.p, n, stream);
-    // canonical path bytes in one transfer
-    std::vector<uint64_t> off(n + 1, 0);
-    for (uint64_t i = 0; i < n; ++i) off[i + 1] = off[i] + plen[i];
-    DBuf<uint64_t> doff(st.ctx, n + 1);
-    DBuf<uint8_t> bytes(st.ctx, off[n] + 1);
-    HIP_OK(hipMemcpyAsync(doff.p, off.data(), (n + 1) * 8, hipMemcpyHostToDevice, stream));
-    launch_gather_bytes(a.p, c.p, doff.p, n, bytes.p, stream);
-    ex.path_bytes = d2h(bytes.p, off[n], stream);
-    ex.path_off.assign(off.begin(), off.end());
-  }
-  CkRows ck;
-  bool ck_loaded = false;
+  const uint32_t* didx = which == DR_LIVE ? st.live.p : st.tomb.p;
   ex.n = int64_t(n);
-  ex.stats_off.push_back(0);
-  ex.pv_entry_off.push_back(0);
-  ex.pv_key_off.push_back(0);
-  ex.pv_val_off.push_back(0);
-  ex.tags_entry_off.push_back(0);
-  ex.tags_key_off.push_back(0);
-  ex.tags_val_off.push_back(0);
-  for (uint64_t i = 0; i < n; ++i) {
-    RecordFields r;
-    const bool from_json = sid.empty() ? idx[i] >= s.ck_rows : !(aflags[i] & kFromCkpt);
-    if (from_json) {
-      const StagedData& src = sid.empty() ? s : *st.sources[sid[i]];
-      JVal v;
-      json_parse(reinterpret_cast<const char*>(src.h_json.data() + soff[i]), slen[i], &v);
-      const JVal* o = v.get(which == DR_LIVE ? "add" : "remove");
-      if (o) fields_from_json(*o, r);
-    } else {
-      if (!ck_loaded) { load_ck_side(s, which == DR_LIVE, ck); ck_loaded = true; }
-      auto it = ck.rows.find(int64_t(soff[i]));
-      if (it != ck.rows.end()) r = it->second;
+  // canonical paths, deletionTimestamp (+ validity) from the action arrays
+  {
+    DBuf<uint64_t> pp(ctx, n), off(ctx, n + 1), dts(ctx, n);
+    DBuf<uint32_t> pl(ctx, n);
+    DBuf<uint8_t> fl(ctx, n), scratch(ctx, scan_scratch_for(n));
+    launch_gather_u64(st.path_ptr.p, didx, n, pp.p, stream);
+    launch_gather_u32(st.path_len.p, didx, n, pl.p, stream);
+    launch_gather_u64(reinterpret_cast<const uint64_t*>(st.delts.p), didx, n, dts.p, stream);
+    launch_gather_u8(st.flags.p, didx, n, fl.p, stream);
+    launch_scan_u32(pl.p, off.p, n, scratch.p, stream);
+    const uint64_t nb = n ? d2h_one(off.p + n, stream) : 0;
+    DBuf<uint8_t> bytes(ctx, nb + 1);
+    launch_gather_bytes(pp.p, pl.p, off.p, n, bytes.p, stream);
+    ex.path_off = to_i64(d2h(off.p, n + 1, stream));
+    if (!n) ex.path_off.assign(1, 0);
+    ex.path_bytes = d2h(bytes.p, nb, stream);
+    const std::vector<uint64_t> dv = d2h(dts.p, n, stream);
+    const std::vector<uint8_t> fv = d2h(fl.p, n, stream);
+    ex.delts.resize(n);
+    ex.delts_valid.resize(n);
+    for (uint64_t i = 0; i < n; ++i) {
+      const bool valid = (fv[i] & 1u) != 0;  // F_HAS_DELTS
+      ex.delts_valid[i] = valid;
+      ex.delts[i] = valid ? int64_t(dv[i]) : 0;
     }
-    ex.size.push_back(r.size);
-    ex.mtime.push_back(r.mtime);
-    ex.delts.push_back(r.delts);
-    ex.delts_valid.push_back(r.delts_valid);
-    ex.efm.push_back(r.efm);
-    ex.stats_null.push_back(r.stats_null);
-    ex.stats_bytes.insert(ex.stats_bytes.end(), r.stats.begin(), r.stats.end());
-    ex.stats_off.push_back(int64_t(ex.stats_bytes.size()));
-    ex.pv_null.push_back(r.pv_null);
-    for (auto& kv : r.pv) {
-      ex.pv_key_bytes.insert(ex.pv_key_bytes.end(), kv.first.begin(), kv.first.end());
-      ex.pv_key_off.push_back(int64_t(ex.pv_key_bytes.size()));
-      ex.pv_val_null.push_back(kv.second.first);
-      ex.pv_val_bytes.insert(ex.pv_val_bytes.end(), kv.second.second.begin(), kv.second.second.end());
-      ex.pv_val_off.push_back(int64_t(ex.pv_val_bytes.size()));
-    }
-    ex.pv_entry_off.push_back(int64_t(ex.pv_val_null.size()));
-    ex.tags_null.push_back(r.tags_null);
-    for (auto& kv : r.tags) {
-      ex.tags_key_bytes.insert(ex.tags_key_bytes.end(), kv.first.begin(), kv.first.end());
-      ex.tags_key_off.push_back(int64_t(ex.tags_key_bytes.size()));
-      ex.tags_val_null.push_back(kv.second.first);
-      ex.tags_val_bytes.insert(ex.tags_val_bytes.end(), kv.second.second.begin(), kv.second.second.end());
-      ex.tags_val_off.push_back(int64_t(ex.tags_val_bytes.size()));
-    }
-    ex.tags_entry_off.push_back(int64_t(ex.tags_val_null.size()));
   }
+  ExpDecoded D;
+  decode_export_side(st, which, D);
+  ExportArgs a{};
+  a.idx = didx;
+  a.n = n;
+  a.side = which == DR_LIVE ? 0 : 1;
+  a.json = s.d_json.p;
+  a.ck_rows = s.ck_rows;
+  a.src_off = st.src_off.p;
+  a.src_len = st.src_len.p;
+  a.act_size = st.size.p;
+  DBuf<uint64_t> json_bases;
+  if (st.src_id.p) {
+    std::vector<uint64_t> bases;
+    for (auto& src : st.sources) bases.push_back(reinterpret_cast<uint64_t>(src->d_json.p));
+    json_bases = upload(ctx, bases.data(), bases.size());
+    a.act_flags = st.flags.p;
+    a.src_id = st.src_id.p;
+    a.json_bases = json_bases.p;
+  }
+  a.ck_size = D.flat[0];
+  a.ck_mtime = D.flat[1];
+  a.ck_efm = D.flat[2];
+  a.ck_stats = D.flat[3];
+  a.ck_pv = D.map[0];
+  a.ck_tags = D.map[1];
+  DBuf<int64_t> size(ctx, n), mt(ctx, n);
+  DBuf<uint8_t> efm(ctx, n), snull(ctx, n), pnull(ctx, n), tnull(ctx, n);
+  DBuf<uint32_t> cnt[EXC_N];
+  DBuf<uint64_t> off[EXC_N];
+  DBuf<uint32_t> err(ctx, 1);
+  err.zero(stream);
+  a.size = size.p;
+  a.mtime = mt.p;
+  a.efm = efm.p;
+  a.stats_null = snull.p;
+  a.pv_null = pnull.p;
+  a.tags_null = tnull.p;
+  a.error = err.p;
+  for (int k = 0; k < EXC_N; ++k) {
+    cnt[k] = DBuf<uint32_t>(ctx, n);
+    off[k] = DBuf<uint64_t>(ctx, n + 1);
+    a.cnt[k] = cnt[k].p;
+  }
+  launch_export(a, stream);  // pass 1: scalars + counts
+  DBuf<uint8_t> scratch(ctx, scan_scratch_for(n));
+  uint64_t tot[EXC_N] = {};
+  for (int k = 0; k < EXC_N; ++k) {
+    launch_scan_u32(cnt[k].p, off[k].p, n, scratch.p, stream);
+    a.off[k] = off[k].p;
+  }
+  for (int k = 0; k < EXC_N && n; ++k) tot[k] = d2h_one(off[k].p + n, stream);
+  if (d2h_one(err.p, stream)) fail(DR_E_PARSE, "malformed survivor line at export");
+  DBuf<uint8_t> sbytes(ctx, tot[EXC_STATS] + 1), pkb(ctx, tot[EXC_PV_KB] + 1), pvb(ctx, tot[EXC_PV_VB] + 1),
+      tkb(ctx, tot[EXC_TAGS_KB] + 1), tvb(ctx, tot[EXC_TAGS_VB] + 1), pvn(ctx, tot[EXC_PV_N] + 1),
+      tvn(ctx, tot[EXC_TAGS_N] + 1);
+  DBuf<int64_t> pko(ctx, tot[EXC_PV_N] + 1), pvo(ctx, tot[EXC_PV_N] + 1), tko(ctx, tot[EXC_TAGS_N] + 1),
+      tvo(ctx, tot[EXC_TAGS_N] + 1);
+  for (DBuf<int64_t>* o : {&pko, &pvo, &tko, &tvo}) HIP_OK(hipMemsetAsync(o->p, 0, 8, stream));
+  a.write = 1;
+  a.stats_bytes = sbytes.p;
+  a.pv_key_off = pko.p;
+  a.pv_val_off = pvo.p;
+  a.pv_val_null = pvn.p;
+  a.pv_key_bytes = pkb.p;
+  a.pv_val_bytes = pvb.p;
+  a.tags_key_off = tko.p;
+  a.tags_val_off = tvo.p;
+  a.tags_val_null = tvn.p;
+  a.tags_key_bytes = tkb.p;
+  a.tags_val_bytes = tvb.p;
+  launch_export(a, stream);  // pass 2: bytes and entries
+  ex.size = d2h(size.p, n, stream);
+  ex.mtime = d2h(mt.p, n, stream);
+  ex.efm = d2h(efm.p, n, stream);
+  ex.stats_null = d2h(snull.p, n, stream);
+  ex.pv_null = d2h(pnull.p, n, stream);
+  ex.tags_null = d2h(tnull.p, n, stream);
+  ex.stats_off = to_i64(d2h(off[EXC_STATS].p, n + 1, stream));
+  ex.pv_entry_off = to_i64(d2h(off[EXC_PV_N].p, n + 1, stream));
+  ex.tags_entry_off = to_i64(d2h(off[EXC_TAGS_N].p, n + 1, stream));
+  if (!n) ex.stats_off = ex.pv_entry_off = ex.tags_entry_off = std::vector<int64_t>(1, 0);
+  ex.stats_bytes = d2h(sbytes.p, tot[EXC_STATS], stream);
+  ex.pv_key_off = d2h(pko.p, tot[EXC_PV_N] + 1, stream);
+  ex.pv_val_off = d2h(pvo.p, tot[EXC_PV_N] + 1, stream);
+  ex.pv_val_null = d2h(pvn.p, tot[EXC_PV_N], stream);
+  ex.pv_key_bytes = d2h(pkb.p, tot[EXC_PV_KB], stream);
+  ex.pv_val_bytes = d2h(pvb.p, tot[EXC_PV_VB], stream);
+  ex.tags_key_off = d2h(tko.p, tot[EXC_TAGS_N] + 1, stream);
+  ex.tags_val_off = d2h(tvo.p, tot[EXC_TAGS_N] + 1, stream);
+  ex.tags_val_null = d2h(tvn.p, tot[EXC_TAGS_N], stream);
+  ex.tags_key_bytes = d2h(tkb.p, tot[EXC_TAGS_KB], stream);
+  ex.tags_val_bytes = d2h(tvb.p, tot[EXC_TAGS_VB], stream);
   ex.built = true;
 }
 
@@ -1985,13 +2019,6 @@ static bool leafify(const dr_predicate& p, LeafPlan& L) {
     }
   };
   return emit(p.nops - 1) && max_depth <= 32;
-}
-
-template <typename T>
-static DBuf<T> upload(dr_ctx* ctx, const T* src, size_t n) {
-  DBuf<T> d(ctx, n);
-  if (n) HIP_OK(hipMemcpyAsync(d.p, src, n * sizeof(T), hipMemcpyHostToDevice, ctx->stream));
-  return d;
 }
 
 // Builds the K5 cache columns `want` (name, type) of st's live AddFiles in one k_pv_extract pass.

@@ -696,4 +696,280 @@ void launch_group_flags(const uint32_t* keys, uint64_t n, const GroupCols& g, ui
   if (n) DR_LAUNCH(dev::k_group_flags, dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, keys, n, g, flag);
 }
 
+// ---- device export of the survivors' records (dr_state_export) -----------------------------------
+// The fields the replay kernels do not keep -- modificationTime, stats, partitionValues, tags,
+// extendedFileMetadata, a checkpoint remove's size -- read per survivor from its JSON line (the
+// add / remove object, Jackson semantics: a repeated member keeps the last value; a repeated map key
+// keeps its first position and last value, as a LinkedHashMap) or from the checkpoint's decoded
+// leaves (row-indexed flat columns, map entries by row). Strings are unescaped; a non-string value
+// where a string is expected keeps its JSON text without insignificant whitespace.
+namespace dev {
+
+__device__ __forceinline__ void bytes_copy(uint8_t* d, const uint8_t* s, uint32_t n) {
+  for (uint32_t k = 0; k < n; ++k) d[k] = s[k];
+}
+
+__device__ uint32_t json_unescape_len(const uint8_t* s, uint32_t n) {
+  uint32_t o = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (s[i] != '\\' || i + 1 >= n) { ++o; continue; }
+    const uint8_t e = s[++i];
+    if (e != 'u') { ++o; continue; }
+    uint32_t cp = 0;
+    for (int k = 0; k < 4 && i + 1 < n; ++k) cp = cp * 16 + uint32_t(hexval(s[++i]) & 15);
+    if (cp >= 0xD800 && cp < 0xDC00 && i + 6 < n && s[i + 1] == '\\' && s[i + 2] == 'u') {
+      uint32_t lo = 0;
+      for (int k = 0; k < 4; ++k) lo = lo * 16 + uint32_t(hexval(s[i + 3 + k]) & 15);
+      if (lo >= 0xDC00 && lo < 0xE000) { cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00); i += 6; }
+    }
+    o += cp < 0x80 ? 1 : cp < 0x800 ? 2 : cp < 0x10000 ? 3 : 4;
+  }
+  return o;
+}
+
+// JSON text of [v, end) without whitespace outside strings (out null: length only)
+__device__ uint32_t compact_json(const uint8_t* v, const uint8_t* end, uint8_t* out) {
+  uint32_t o = 0;
+  bool in_str = false;
+  for (const uint8_t* p = v; p < end; ++p) {
+    const uint8_t c = *p;
+    if (in_str) {
+      if (out) out[o] = c;
+      ++o;
+      if (c == '\\' && p + 1 < end) {
+        ++p;
+        if (out) out[o] = *p;
+        ++o;
+      } else if (c == '"') {
+        in_str = false;
+      }
+      continue;
+    }
+    if (is_ws(c)) continue;
+    if (c == '"') in_str = true;
+    if (out) out[o] = c;
+    ++o;
+  }
+  return o;
+}
+
+// A JSON value where a string is expected: {null?, bytes}. Pass 1 counts, pass 2 writes at out.
+__device__ uint32_t string_value(const uint8_t* v, const uint8_t* end, bool* is_null, uint8_t* out) {
+  *is_null = false;
+  if (v < end && *v == '"') {
+    bool esc = false;
+    const uint8_t* q = str_close(v + 1, end, &esc);
+    const uint32_t n = uint32_t(q - v - 1);
+    if (!esc) {
+      if (out) for (uint32_t k = 0; k < n; ++k) out[k] = v[1 + k];
+      return n;
+    }
+    return out ? json_unescape(v + 1, n, out) : json_unescape_len(v + 1, n);
+  }
+  if (v < end && *v == 'n' && end - v == 4) {  // null
+    *is_null = true;
+    if (out) { out[0] = 'n'; out[1] = 'u'; out[2] = 'l'; out[3] = 'l'; }  // the host export's json_dump text
+    return 4;
+  }
+  return compact_json(v, end, out);
+}
+
+__device__ bool keys_equal(const uint8_t* a, uint32_t an, bool aesc, const uint8_t* b, uint32_t bn, bool besc) {
+  if (!aesc && !besc) return an == bn && bytes_equal(a, b, an);
+  if (!aesc) return span_eq(b, bn, besc, a, an);
+  if (!besc) return span_eq(a, an, aesc, b, bn);
+  if (an > 128 || bn > 128) return an == bn && bytes_equal(a, b, an);
+  uint8_t buf[160];
+  const uint32_t m = json_unescape(b, bn, buf);
+  return span_eq(a, an, aesc, buf, m);
+}
+
+struct MapSink {
+  uint32_t n, kb, vb;                   // entries and bytes so far
+  uint8_t* kbytes;                      // pass 2: this record's first key byte
+  uint8_t* vbytes;
+  int64_t* koff;                        // pass 2: this record's first entry's end-offset slot
+  int64_t* voff;
+  uint8_t* vnull;
+  int64_t kbase, vbase;                 // absolute offsets of kbytes / vbytes
+};
+
+__device__ void sink_entry_json(MapSink& m, bool write, const uint8_t* k, uint32_t kn, bool kesc, const uint8_t* v,
+                                const uint8_t* vend) {
+  const uint32_t kl = kesc ? (write ? json_unescape(k, kn, m.kbytes + m.kb) : json_unescape_len(k, kn))
+                           : (write ? (bytes_copy(m.kbytes + m.kb, k, kn), kn) : kn);
+  bool vn;
+  const uint32_t vl = string_value(v, vend, &vn, write ? m.vbytes + m.vb : nullptr);
+  m.kb += kl;
+  m.vb += vl;
+  if (write) {
+    m.koff[m.n] = m.kbase + m.kb;
+    m.voff[m.n] = m.vbase + m.vb;
+    m.vnull[m.n] = vn ? 1 : 0;
+  }
+  ++m.n;
+}
+
+// Entries of the JSON object at m0 ('{') into the sink (first position, last value per key).
+__device__ bool json_map(const uint8_t* m0, const uint8_t* e, MapSink& m, bool write) {
+  return each_member(m0, e, [&](const uint8_t* k, uint32_t kn, bool kesc, const uint8_t* v) -> const uint8_t* {
+    const uint8_t* vend = skip_value(v, e);
+    bool first = true, after = false;
+    const uint8_t* lv = v;
+    const uint8_t* lend = vend;
+    each_member(m0, e, [&](const uint8_t* k2, uint32_t kn2, bool kesc2, const uint8_t* v2) -> const uint8_t* {
+      const uint8_t* vend2 = skip_value(v2, e);
+      if (k2 == k) {
+        after = true;
+      } else if (keys_equal(k, kn, kesc, k2, kn2, kesc2)) {
+        if (!after) first = false;
+        else { lv = v2; lend = vend2; }
+      }
+      return vend2;
+    });
+    if (first) sink_entry_json(m, write, k, kn, kesc, lv, lend);
+    return vend;
+  });
+}
+
+__device__ void ck_map(const ExpMap& cm, uint64_t r, MapSink& m, bool write, uint8_t* is_null) {
+  *is_null = 1;
+  if (!cm.row_start) return;
+  for (uint64_t en = cm.row_start[r]; en < cm.row_start[r + 1]; ++en) {
+    const int d = cm.kdef[en];
+    if (d >= cm.map_def) *is_null = 0;
+    if (d < cm.entry_def) continue;
+    const uint32_t kl = cm.klen[en];
+    const bool vn = cm.vdef[en] != cm.vmax;
+    const uint32_t vl = vn ? 0u : cm.vlen[en];
+    if (write) {
+      bytes_copy(m.kbytes + m.kb, reinterpret_cast<const uint8_t*>(cm.kptr[en]), kl);
+      if (!vn) bytes_copy(m.vbytes + m.vb, reinterpret_cast<const uint8_t*>(cm.vptr[en]), vl);
+    }
+    m.kb += kl;
+    m.vb += vl;
+    if (write) {
+      m.koff[m.n] = m.kbase + m.kb;
+      m.voff[m.n] = m.vbase + m.vb;
+      m.vnull[m.n] = vn ? 1 : 0;
+    }
+    ++m.n;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_export(ExportArgs a) {
+  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= a.n) return;
+  const bool write = a.write != 0;
+  const uint32_t act = a.idx[i];
+  MapSink pv{0, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0};
+  MapSink tg = pv;
+  uint8_t* sbytes = nullptr;
+  if (write) {
+    pv.kbytes = a.pv_key_bytes + a.off[EXC_PV_KB][i];
+    pv.vbytes = a.pv_val_bytes + a.off[EXC_PV_VB][i];
+    pv.koff = a.pv_key_off + a.off[EXC_PV_N][i] + 1;
+    pv.voff = a.pv_val_off + a.off[EXC_PV_N][i] + 1;
+    pv.vnull = a.pv_val_null + a.off[EXC_PV_N][i];
+    pv.kbase = int64_t(a.off[EXC_PV_KB][i]);
+    pv.vbase = int64_t(a.off[EXC_PV_VB][i]);
+    tg.kbytes = a.tags_key_bytes + a.off[EXC_TAGS_KB][i];
+    tg.vbytes = a.tags_val_bytes + a.off[EXC_TAGS_VB][i];
+    tg.koff = a.tags_key_off + a.off[EXC_TAGS_N][i] + 1;
+    tg.voff = a.tags_val_off + a.off[EXC_TAGS_N][i] + 1;
+    tg.vnull = a.tags_val_null + a.off[EXC_TAGS_N][i];
+    tg.kbase = int64_t(a.off[EXC_TAGS_KB][i]);
+    tg.vbase = int64_t(a.off[EXC_TAGS_VB][i]);
+    sbytes = a.stats_bytes + a.off[EXC_STATS][i];
+  }
+  int64_t size = a.act_size[act], mt = 0;
+  uint8_t efm = 0, snull = 1, pnull = 1, tnull = 1;
+  uint32_t slen = 0;
+  const bool from_json = a.act_flags ? !(a.act_flags[act] & F_FROM_CKPT) : act >= a.ck_rows;
+  if (from_json) {
+    const uint8_t* json = a.act_flags && a.src_id ? reinterpret_cast<const uint8_t*>(a.json_bases[a.src_id[act]]) : a.json;
+    const uint8_t* b = json + a.src_off[act];
+    const uint8_t* e = b + a.src_len[act];
+    const char* side = a.side == 0 ? "add" : "remove";
+    const uint32_t sl = a.side == 0 ? 3 : 6;
+    // the side's object: the last member of that name (a repeated member keeps its last value)
+    const uint8_t* obj = nullptr;
+    const bool ok = each_member(skip_ws(b, e), e, [&](const uint8_t* k, uint32_t kn, bool kesc, const uint8_t* v) -> const uint8_t* {
+      if (key_is(k, kn, kesc, side, sl)) obj = (v < e && *v == '{') ? v : nullptr;
+      return skip_value(v, e);
+    });
+    if (!ok) atomicOr(a.error, 1u);
+    if (obj) {
+      // last occurrence of each field
+      const uint8_t *st = nullptr, *st_end = nullptr, *pvo = nullptr, *tgo = nullptr;
+      bool pv_seen = false, tg_seen = false;
+      each_member(obj, e, [&](const uint8_t* k, uint32_t kn, bool kesc, const uint8_t* v) -> const uint8_t* {
+        const uint8_t* vend = skip_value(v, e);
+        if (key_is(k, kn, kesc, "modificationTime", 16)) {
+          int64_t x;
+          mt = json_int64(v, vend, &x) ? x : 0;
+        } else if (key_is(k, kn, kesc, "extendedFileMetadata", 20)) {
+          efm = (vend - v == 4 && v[0] == 't') ? 1 : 0;
+        } else if (key_is(k, kn, kesc, "stats", 5)) {
+          st = v;
+          st_end = vend;
+        } else if (key_is(k, kn, kesc, "partitionValues", 15)) {
+          pv_seen = true;
+          pvo = (v < e && *v == '{') ? v : nullptr;
+          pnull = (v < e && *v == 'n') ? 1 : 0;
+        } else if (key_is(k, kn, kesc, "tags", 4)) {
+          tg_seen = true;
+          tgo = (v < e && *v == '{') ? v : nullptr;
+          tnull = (v < e && *v == 'n') ? 1 : 0;
+        }
+        return vend;
+      });
+      if (st && !(st_end - st == 4 && st[0] == 'n')) {  // a null stats member is absent
+        bool sn;
+        slen = string_value(st, st_end, &sn, sbytes);
+        snull = 0;
+      }
+      if (!pv_seen) pnull = 1;
+      if (!tg_seen) tnull = 1;
+      if (pvo) json_map(pvo, e, pv, write);
+      if (tgo) json_map(tgo, e, tg, write);
+    }
+  } else {
+    const uint64_t r = a.src_off[act];
+    if (a.ck_mtime.def && a.ck_mtime.def[r] == a.ck_mtime.max_def) mt = a.ck_mtime.ival[r];
+    if (a.side == 1) {
+      size = (a.ck_size.def && a.ck_size.def[r] == a.ck_size.max_def) ? a.ck_size.ival[r] : 0;
+    }
+    if (a.ck_efm.def && a.ck_efm.def[r] == a.ck_efm.max_def) efm = a.ck_efm.ival[r] != 0;
+    if (a.ck_stats.def && a.ck_stats.def[r] == a.ck_stats.max_def) {
+      snull = 0;
+      slen = a.ck_stats.slen[r];
+      if (write) bytes_copy(sbytes, reinterpret_cast<const uint8_t*>(a.ck_stats.sptr[r]), slen);
+    }
+    ck_map(a.ck_pv, r, pv, write, &pnull);
+    ck_map(a.ck_tags, r, tg, write, &tnull);
+  }
+  if (!write) {
+    a.size[i] = size;
+    a.mtime[i] = mt;
+    a.efm[i] = efm;
+    a.stats_null[i] = snull;
+    a.pv_null[i] = pnull;
+    a.tags_null[i] = tnull;
+    a.cnt[EXC_STATS][i] = slen;
+    a.cnt[EXC_PV_N][i] = pv.n;
+    a.cnt[EXC_PV_KB][i] = pv.kb;
+    a.cnt[EXC_PV_VB][i] = pv.vb;
+    a.cnt[EXC_TAGS_N][i] = tg.n;
+    a.cnt[EXC_TAGS_KB][i] = tg.kb;
+    a.cnt[EXC_TAGS_VB][i] = tg.vb;
+  }
+}
+
+}  // namespace dev
+
+void launch_export(const ExportArgs& a, hipStream_t st) {
+  if (a.n) DR_LAUNCH(dev::k_export, dim3(unsigned((a.n + 255) / 256)), dim3(256), 0, st, a);
+}
+
 }  // namespace dr

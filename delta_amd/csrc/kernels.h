@@ -515,3 +515,68 @@ void launch_sort_groups(void* temp, size_t* temp_bytes, uint32_t* keys, uint64_t
 // flag[i] = 1 where keys[i] starts a new tuple (i == 0 or it differs from keys[i - 1]).
 void launch_group_flags(const uint32_t* keys, uint64_t n, const GroupCols& g, uint32_t* flag, hipStream_t st);
 }  // namespace dr
+
+// ---- device export of allFiles / tombstones (k_filter.hip) ---------------------------------------
+namespace dr {
+// A decoded checkpoint leaf of one side (flat: per row; def null = column absent).
+struct ExpFlat {
+  const uint8_t* def;
+  const int64_t* ival;
+  const uint64_t* sptr;
+  const uint32_t* slen;
+  int32_t max_def;
+};
+// A decoded checkpoint map (key/value leaves, level entries; row_start null = absent).
+struct ExpMap {
+  const uint64_t* row_start;  // [ck_rows + 1] first level entry of each row
+  const uint8_t* kdef;
+  const uint64_t* kptr;
+  const uint32_t* klen;
+  const uint8_t* vdef;
+  const uint64_t* vptr;
+  const uint32_t* vlen;
+  int32_t map_def, entry_def, vmax;
+};
+enum : int { EXC_STATS = 0, EXC_PV_N, EXC_PV_KB, EXC_PV_VB, EXC_TAGS_N, EXC_TAGS_KB, EXC_TAGS_VB, EXC_N };
+// One pass per call: pass 1 (write == 0) fills the scalar fields and the EXC_* counts of every
+// record; pass 2 writes the byte and entry arrays at the scanned offsets.
+struct ExportArgs {
+  const uint32_t* idx;  // survivor action indices
+  uint64_t n;
+  int32_t side;         // 0 add (allFiles), 1 remove (tombstones)
+  int32_t write;
+  const uint8_t* act_flags;
+  const uint16_t* src_id;      // null: one source
+  const uint64_t* json_bases;
+  const uint8_t* json;
+  uint64_t ck_rows;
+  const uint64_t* src_off;
+  const uint32_t* src_len;
+  const int64_t* act_size;
+  ExpFlat ck_mtime, ck_size, ck_efm, ck_stats;
+  ExpMap ck_pv, ck_tags;
+  // pass 1 outputs
+  int64_t* size;
+  int64_t* mtime;
+  uint8_t* efm;
+  uint8_t* stats_null;
+  uint8_t* pv_null;
+  uint8_t* tags_null;
+  uint32_t* cnt[EXC_N];        // per record
+  // pass 2
+  const uint64_t* off[EXC_N];  // exclusive scans of cnt
+  uint8_t* stats_bytes;
+  int64_t* pv_key_off;  // [entries + 1] (entry 0 set by the host)
+  int64_t* pv_val_off;
+  uint8_t* pv_val_null;
+  uint8_t* pv_key_bytes;
+  uint8_t* pv_val_bytes;
+  int64_t* tags_key_off;
+  int64_t* tags_val_off;
+  uint8_t* tags_val_null;
+  uint8_t* tags_key_bytes;
+  uint8_t* tags_val_bytes;
+  uint32_t* error;
+};
+void launch_export(const ExportArgs& a, hipStream_t st);
+}  // namespace dr

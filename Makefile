@@ -3,7 +3,7 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 CSRC := delta_amd/csrc
 LIB := delta_amd/libdeltareplay.so
-HIP_SRCS := $(CSRC)/engine.hip $(CSRC)/k_json.hip $(CSRC)/k_parquet.hip $(CSRC)/k_snappy.hip $(CSRC)/k_replay.hip $(CSRC)/k_util.hip $(CSRC)/k_shard.hip $(CSRC)/k_filter.hip $(CSRC)/k_index.hip
+HIP_SRCS := $(CSRC)/engine.hip $(CSRC)/k_json.hip $(CSRC)/k_parquet.hip $(CSRC)/k_snappy.hip $(CSRC)/k_replay.hip $(CSRC)/k_util.hip $(CSRC)/k_shard.hip $(CSRC)/k_filter.hip $(CSRC)/k_index.hip $(CSRC)/k_encode.hip
 CXX_SRCS := $(CSRC)/parquet_meta.cpp $(CSRC)/log_segment.cpp $(CSRC)/json_host.cpp $(CSRC)/snappy_host.cpp
 OBJDIR := build/obj
 HIP_OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS))

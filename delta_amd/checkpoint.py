@@ -215,6 +215,32 @@ def write_part(state, log_path: str, version: int, part: int, parts: int, row_gr
     return table.num_rows
 
 
+def write_checkpoint_device(snapshot, parts: int = 1, row_group_size: int = 1 << 20,
+                            checkpoint_v2_enabled: bool = True) -> dict:
+    """writeCheckpoint with the Parquet pages of the file actions encoded on the GPU
+    (dr_state_write_checkpoint); same files and `_last_checkpoint` as `write_checkpoint`."""
+    state = snapshot.state
+    md = next((a["metaData"] for a in state.nonfile if "metaData" in a), None)
+    stats, parsed = checkpoint_options(md, checkpoint_v2_enabled)
+    log_path = snapshot.delta_log.log_path
+    rows = 0
+    for i in range(parts):
+        data, n = state.write_checkpoint_part(i + 1, parts, stats=stats, parsed=parsed is not None,
+                                              row_group_rows=row_group_size)
+        rows += n
+        path = (os.path.join(log_path, "%020d.checkpoint.parquet" % snapshot.version) if parts <= 1
+                else checkpoint_file_with_parts(log_path, snapshot.version, i + 1, parts))
+        tmp = os.path.join(os.path.dirname(path), ".%s.tmp" % os.path.basename(path))
+        with open(tmp, "wb") as f:
+            f.write(data)
+        os.replace(tmp, path)
+    meta = {"version": snapshot.version, "size": rows}
+    if parts > 1:
+        meta["parts"] = parts
+    write_last_checkpoint(log_path, meta)
+    return meta
+
+
 def write_checkpoint(snapshot, parts: int = 1, row_group_size: int = 1 << 20) -> dict:
     """writeCheckpoint for a GPU snapshot: the checkpoint file(s) of snapshot.version and
     `_last_checkpoint`; returns the CheckpointMetaData written there."""

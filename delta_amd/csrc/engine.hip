@@ -1683,42 +1683,44 @@ static std::vector<int64_t> to_i64(const std::vector<T>& v) {
   return std::vector<int64_t>(v.begin(), v.end());
 }
 
-static void build_export(dr_state& st, int which) {
+// One side's export columns in HBM (k_export's output; the checkpoint encoder reads them there).
+struct DevExport {
+  uint64_t n = 0;
+  DBuf<uint64_t> path_ptr, path_off, delts;  // path_off: exclusive scan of the lengths (n + 1)
+  DBuf<uint32_t> path_len;
+  DBuf<uint8_t> path_bytes, flags;
+  DBuf<int64_t> size, mtime;
+  DBuf<uint8_t> efm, stats_null, pv_null, tags_null;
+  DBuf<uint64_t> off[EXC_N];                 // exclusive scans of the per-record counts (n + 1)
+  uint64_t tot[EXC_N] = {};
+  DBuf<uint8_t> stats_bytes, pv_key_bytes, pv_val_bytes, tags_key_bytes, tags_val_bytes, pv_val_null, tags_val_null;
+  DBuf<int64_t> pv_key_off, pv_val_off, tags_key_off, tags_val_off;  // per entry (entries + 1)
+};
+
+static void export_device(dr_state& st, int which, DevExport& X) {
   ensure_ready(st);
-  ExportCols& ex = st.exp[which];
-  if (ex.built) return;
   dr_ctx* ctx = st.ctx;
   hipStream_t stream = ctx->stream;
   StagedData& s = *st.sources[0];
   const uint64_t n = which == DR_LIVE ? st.n_live : st.n_tomb;
   const uint32_t* didx = which == DR_LIVE ? st.live.p : st.tomb.p;
-  ex.n = int64_t(n);
-  // canonical paths, deletionTimestamp (+ validity) from the action arrays
-  {
-    DBuf<uint64_t> pp(ctx, n), off(ctx, n + 1), dts(ctx, n);
-    DBuf<uint32_t> pl(ctx, n);
-    DBuf<uint8_t> fl(ctx, n), scratch(ctx, scan_scratch_for(n));
-    launch_gather_u64(st.path_ptr.p, didx, n, pp.p, stream);
-    launch_gather_u32(st.path_len.p, didx, n, pl.p, stream);
-    launch_gather_u64(reinterpret_cast<const uint64_t*>(st.delts.p), didx, n, dts.p, stream);
-    launch_gather_u8(st.flags.p, didx, n, fl.p, stream);
-    launch_scan_u32(pl.p, off.p, n, scratch.p, stream);
-    const uint64_t nb = n ? d2h_one(off.p + n, stream) : 0;
-    DBuf<uint8_t> bytes(ctx, nb + 1);
-    launch_gather_bytes(pp.p, pl.p, off.p, n, bytes.p, stream);
-    ex.path_off = to_i64(d2h(off.p, n + 1, stream));
-    if (!n) ex.path_off.assign(1, 0);
-    ex.path_bytes = d2h(bytes.p, nb, stream);
-    const std::vector<uint64_t> dv = d2h(dts.p, n, stream);
-    const std::vector<uint8_t> fv = d2h(fl.p, n, stream);
-    ex.delts.resize(n);
-    ex.delts_valid.resize(n);
-    for (uint64_t i = 0; i < n; ++i) {
-      const bool valid = (fv[i] & 1u) != 0;  // F_HAS_DELTS
-      ex.delts_valid[i] = valid;
-      ex.delts[i] = valid ? int64_t(dv[i]) : 0;
-    }
-  }
+  X.n = n;
+  // canonical paths, deletionTimestamp and flags from the action arrays
+  X.path_ptr = DBuf<uint64_t>(ctx, n);
+  X.path_off = DBuf<uint64_t>(ctx, n + 1);
+  X.delts = DBuf<uint64_t>(ctx, n);
+  X.path_len = DBuf<uint32_t>(ctx, n);
+  X.flags = DBuf<uint8_t>(ctx, n);
+  DBuf<uint8_t> scratch(ctx, scan_scratch_for(n));
+  launch_gather_u64(st.path_ptr.p, didx, n, X.path_ptr.p, stream);
+  launch_gather_u32(st.path_len.p, didx, n, X.path_len.p, stream);
+  launch_gather_u64(reinterpret_cast<const uint64_t*>(st.delts.p), didx, n, X.delts.p, stream);
+  launch_gather_u8(st.flags.p, didx, n, X.flags.p, stream);
+  launch_scan_u32(X.path_len.p, X.path_off.p, n, scratch.p, stream);
+  if (!n) HIP_OK(hipMemsetAsync(X.path_off.p, 0, 8, stream));
+  const uint64_t nb = n ? d2h_one(X.path_off.p + n, stream) : 0;
+  X.path_bytes = DBuf<uint8_t>(ctx, nb + 1);
+  launch_gather_bytes(X.path_ptr.p, X.path_len.p, X.path_off.p, n, X.path_bytes.p, stream);
   ExpDecoded D;
   decode_export_side(st, which, D);
   ExportArgs a{};
@@ -1745,73 +1747,103 @@ static void build_export(dr_state& st, int which) {
   a.ck_stats = D.flat[3];
   a.ck_pv = D.map[0];
   a.ck_tags = D.map[1];
-  DBuf<int64_t> size(ctx, n), mt(ctx, n);
-  DBuf<uint8_t> efm(ctx, n), snull(ctx, n), pnull(ctx, n), tnull(ctx, n);
+  X.size = DBuf<int64_t>(ctx, n);
+  X.mtime = DBuf<int64_t>(ctx, n);
+  X.efm = DBuf<uint8_t>(ctx, n);
+  X.stats_null = DBuf<uint8_t>(ctx, n);
+  X.pv_null = DBuf<uint8_t>(ctx, n);
+  X.tags_null = DBuf<uint8_t>(ctx, n);
   DBuf<uint32_t> cnt[EXC_N];
-  DBuf<uint64_t> off[EXC_N];
   DBuf<uint32_t> err(ctx, 1);
   err.zero(stream);
-  a.size = size.p;
-  a.mtime = mt.p;
-  a.efm = efm.p;
-  a.stats_null = snull.p;
-  a.pv_null = pnull.p;
-  a.tags_null = tnull.p;
+  a.size = X.size.p;
+  a.mtime = X.mtime.p;
+  a.efm = X.efm.p;
+  a.stats_null = X.stats_null.p;
+  a.pv_null = X.pv_null.p;
+  a.tags_null = X.tags_null.p;
   a.error = err.p;
   for (int k = 0; k < EXC_N; ++k) {
     cnt[k] = DBuf<uint32_t>(ctx, n);
-    off[k] = DBuf<uint64_t>(ctx, n + 1);
+    X.off[k] = DBuf<uint64_t>(ctx, n + 1);
     a.cnt[k] = cnt[k].p;
   }
   launch_export(a, stream);  // pass 1: scalars + counts
-  DBuf<uint8_t> scratch(ctx, scan_scratch_for(n));
-  uint64_t tot[EXC_N] = {};
   for (int k = 0; k < EXC_N; ++k) {
-    launch_scan_u32(cnt[k].p, off[k].p, n, scratch.p, stream);
-    a.off[k] = off[k].p;
+    launch_scan_u32(cnt[k].p, X.off[k].p, n, scratch.p, stream);
+    if (!n) HIP_OK(hipMemsetAsync(X.off[k].p, 0, 8, stream));
+    a.off[k] = X.off[k].p;
   }
-  for (int k = 0; k < EXC_N && n; ++k) tot[k] = d2h_one(off[k].p + n, stream);
+  for (int k = 0; k < EXC_N && n; ++k) X.tot[k] = d2h_one(X.off[k].p + n, stream);
   if (d2h_one(err.p, stream)) fail(DR_E_PARSE, "malformed survivor line at export");
-  DBuf<uint8_t> sbytes(ctx, tot[EXC_STATS] + 1), pkb(ctx, tot[EXC_PV_KB] + 1), pvb(ctx, tot[EXC_PV_VB] + 1),
-      tkb(ctx, tot[EXC_TAGS_KB] + 1), tvb(ctx, tot[EXC_TAGS_VB] + 1), pvn(ctx, tot[EXC_PV_N] + 1),
-      tvn(ctx, tot[EXC_TAGS_N] + 1);
-  DBuf<int64_t> pko(ctx, tot[EXC_PV_N] + 1), pvo(ctx, tot[EXC_PV_N] + 1), tko(ctx, tot[EXC_TAGS_N] + 1),
-      tvo(ctx, tot[EXC_TAGS_N] + 1);
-  for (DBuf<int64_t>* o : {&pko, &pvo, &tko, &tvo}) HIP_OK(hipMemsetAsync(o->p, 0, 8, stream));
+  X.stats_bytes = DBuf<uint8_t>(ctx, X.tot[EXC_STATS] + 1);
+  X.pv_key_bytes = DBuf<uint8_t>(ctx, X.tot[EXC_PV_KB] + 1);
+  X.pv_val_bytes = DBuf<uint8_t>(ctx, X.tot[EXC_PV_VB] + 1);
+  X.tags_key_bytes = DBuf<uint8_t>(ctx, X.tot[EXC_TAGS_KB] + 1);
+  X.tags_val_bytes = DBuf<uint8_t>(ctx, X.tot[EXC_TAGS_VB] + 1);
+  X.pv_val_null = DBuf<uint8_t>(ctx, X.tot[EXC_PV_N] + 1);
+  X.tags_val_null = DBuf<uint8_t>(ctx, X.tot[EXC_TAGS_N] + 1);
+  X.pv_key_off = DBuf<int64_t>(ctx, X.tot[EXC_PV_N] + 1);
+  X.pv_val_off = DBuf<int64_t>(ctx, X.tot[EXC_PV_N] + 1);
+  X.tags_key_off = DBuf<int64_t>(ctx, X.tot[EXC_TAGS_N] + 1);
+  X.tags_val_off = DBuf<int64_t>(ctx, X.tot[EXC_TAGS_N] + 1);
+  for (DBuf<int64_t>* o : {&X.pv_key_off, &X.pv_val_off, &X.tags_key_off, &X.tags_val_off})
+    HIP_OK(hipMemsetAsync(o->p, 0, 8, stream));
   a.write = 1;
-  a.stats_bytes = sbytes.p;
-  a.pv_key_off = pko.p;
-  a.pv_val_off = pvo.p;
-  a.pv_val_null = pvn.p;
-  a.pv_key_bytes = pkb.p;
-  a.pv_val_bytes = pvb.p;
-  a.tags_key_off = tko.p;
-  a.tags_val_off = tvo.p;
-  a.tags_val_null = tvn.p;
-  a.tags_key_bytes = tkb.p;
-  a.tags_val_bytes = tvb.p;
+  a.stats_bytes = X.stats_bytes.p;
+  a.pv_key_off = X.pv_key_off.p;
+  a.pv_val_off = X.pv_val_off.p;
+  a.pv_val_null = X.pv_val_null.p;
+  a.pv_key_bytes = X.pv_key_bytes.p;
+  a.pv_val_bytes = X.pv_val_bytes.p;
+  a.tags_key_off = X.tags_key_off.p;
+  a.tags_val_off = X.tags_val_off.p;
+  a.tags_val_null = X.tags_val_null.p;
+  a.tags_key_bytes = X.tags_key_bytes.p;
+  a.tags_val_bytes = X.tags_val_bytes.p;
   launch_export(a, stream);  // pass 2: bytes and entries
-  ex.size = d2h(size.p, n, stream);
-  ex.mtime = d2h(mt.p, n, stream);
-  ex.efm = d2h(efm.p, n, stream);
-  ex.stats_null = d2h(snull.p, n, stream);
-  ex.pv_null = d2h(pnull.p, n, stream);
-  ex.tags_null = d2h(tnull.p, n, stream);
-  ex.stats_off = to_i64(d2h(off[EXC_STATS].p, n + 1, stream));
-  ex.pv_entry_off = to_i64(d2h(off[EXC_PV_N].p, n + 1, stream));
-  ex.tags_entry_off = to_i64(d2h(off[EXC_TAGS_N].p, n + 1, stream));
-  if (!n) ex.stats_off = ex.pv_entry_off = ex.tags_entry_off = std::vector<int64_t>(1, 0);
-  ex.stats_bytes = d2h(sbytes.p, tot[EXC_STATS], stream);
-  ex.pv_key_off = d2h(pko.p, tot[EXC_PV_N] + 1, stream);
-  ex.pv_val_off = d2h(pvo.p, tot[EXC_PV_N] + 1, stream);
-  ex.pv_val_null = d2h(pvn.p, tot[EXC_PV_N], stream);
-  ex.pv_key_bytes = d2h(pkb.p, tot[EXC_PV_KB], stream);
-  ex.pv_val_bytes = d2h(pvb.p, tot[EXC_PV_VB], stream);
-  ex.tags_key_off = d2h(tko.p, tot[EXC_TAGS_N] + 1, stream);
-  ex.tags_val_off = d2h(tvo.p, tot[EXC_TAGS_N] + 1, stream);
-  ex.tags_val_null = d2h(tvn.p, tot[EXC_TAGS_N], stream);
-  ex.tags_key_bytes = d2h(tkb.p, tot[EXC_TAGS_KB], stream);
-  ex.tags_val_bytes = d2h(tvb.p, tot[EXC_TAGS_VB], stream);
+}
+
+static void build_export(dr_state& st, int which) {
+  ensure_ready(st);
+  ExportCols& ex = st.exp[which];
+  if (ex.built) return;
+  hipStream_t stream = st.ctx->stream;
+  DevExport X;
+  export_device(st, which, X);
+  const uint64_t n = X.n;
+  ex.n = int64_t(n);
+  ex.path_off = to_i64(d2h(X.path_off.p, n + 1, stream));
+  ex.path_bytes = d2h(X.path_bytes.p, n ? uint64_t(ex.path_off[n]) : 0, stream);
+  const std::vector<uint64_t> dv = d2h(X.delts.p, n, stream);
+  const std::vector<uint8_t> fv = d2h(X.flags.p, n, stream);
+  ex.delts.resize(n);
+  ex.delts_valid.resize(n);
+  for (uint64_t i = 0; i < n; ++i) {
+    const bool valid = (fv[i] & 1u) != 0;  // F_HAS_DELTS
+    ex.delts_valid[i] = valid;
+    ex.delts[i] = valid ? int64_t(dv[i]) : 0;
+  }
+  ex.size = d2h(X.size.p, n, stream);
+  ex.mtime = d2h(X.mtime.p, n, stream);
+  ex.efm = d2h(X.efm.p, n, stream);
+  ex.stats_null = d2h(X.stats_null.p, n, stream);
+  ex.pv_null = d2h(X.pv_null.p, n, stream);
+  ex.tags_null = d2h(X.tags_null.p, n, stream);
+  ex.stats_off = to_i64(d2h(X.off[EXC_STATS].p, n + 1, stream));
+  ex.pv_entry_off = to_i64(d2h(X.off[EXC_PV_N].p, n + 1, stream));
+  ex.tags_entry_off = to_i64(d2h(X.off[EXC_TAGS_N].p, n + 1, stream));
+  ex.stats_bytes = d2h(X.stats_bytes.p, X.tot[EXC_STATS], stream);
+  ex.pv_key_off = d2h(X.pv_key_off.p, X.tot[EXC_PV_N] + 1, stream);
+  ex.pv_val_off = d2h(X.pv_val_off.p, X.tot[EXC_PV_N] + 1, stream);
+  ex.pv_val_null = d2h(X.pv_val_null.p, X.tot[EXC_PV_N], stream);
+  ex.pv_key_bytes = d2h(X.pv_key_bytes.p, X.tot[EXC_PV_KB], stream);
+  ex.pv_val_bytes = d2h(X.pv_val_bytes.p, X.tot[EXC_PV_VB], stream);
+  ex.tags_key_off = d2h(X.tags_key_off.p, X.tot[EXC_TAGS_N] + 1, stream);
+  ex.tags_val_off = d2h(X.tags_val_off.p, X.tot[EXC_TAGS_N] + 1, stream);
+  ex.tags_val_null = d2h(X.tags_val_null.p, X.tot[EXC_TAGS_N], stream);
+  ex.tags_key_bytes = d2h(X.tags_key_bytes.p, X.tot[EXC_TAGS_KB], stream);
+  ex.tags_val_bytes = d2h(X.tags_val_bytes.p, X.tot[EXC_TAGS_VB], stream);
   ex.built = true;
 }
 
@@ -2145,6 +2177,583 @@ static void build_pv_columns(dr_state& st, const std::vector<std::pair<std::stri
   if (e & 1u) fail(DR_E_PARSE, "malformed add.partitionValues in a live AddFile's JSON line");
   if (e & 2u) fail(DR_E_INTERNAL, "partition value arena overflow");
   for (auto& c : made) st.pv_cols.push_back(std::move(c));
+}
+
+// ---------------------------------------------------------------------------------------------------
+// checkpoint writer on the device (Checkpoints.writeCheckpoint / buildCheckpoint,
+// D/Checkpoints.scala:229-365): the state's rows -- protocol, metaData, txns, then allFiles, then the
+// tombstones, every record with dataChange=false -- as one Parquet part. The file-action columns
+// are encoded on the device from the device export (k_enc_*: levels + PLAIN values, bit-packed
+// levels); the handful of protocol / metaData / txn rows and the footer are written on the host.
+// Pages are uncompressed (codec UNCOMPRESSED; any Parquet reader, the reference's included, reads
+// them). The schema is the reference's checkpoint schema, nullable throughout.
+// ---------------------------------------------------------------------------------------------------
+struct ThriftW {  // Thrift compact protocol
+  std::vector<uint8_t> b;
+  std::vector<int> last{0};
+  void varint(uint64_t v) {
+    while (v >= 0x80) { b.push_back(uint8_t(v) | 0x80); v >>= 7; }
+    b.push_back(uint8_t(v));
+  }
+  static uint64_t zz(int64_t v) { return (uint64_t(v) << 1) ^ uint64_t(v >> 63); }
+  void field(int id, uint8_t type) {
+    const int d = id - last.back();
+    if (d > 0 && d <= 15) b.push_back(uint8_t(d << 4) | type);
+    else { b.push_back(type); varint(zz(id)); }
+    last.back() = id;
+  }
+  void i32(int id, int32_t v) { field(id, 5); varint(zz(v)); }
+  void i64(int id, int64_t v) { field(id, 6); varint(zz(v)); }
+  void str(int id, const std::string& s) { field(id, 8); varint(s.size()); b.insert(b.end(), s.begin(), s.end()); }
+  void begin_struct(int id) { field(id, 12); last.push_back(0); }
+  void end_struct() { b.push_back(0); last.pop_back(); }
+  void begin_list(int id, uint8_t etype, size_t n) {
+    field(id, 9);
+    if (n < 15) b.push_back(uint8_t(n << 4) | etype);
+    else { b.push_back(0xF0 | etype); varint(n); }
+  }
+  void elem_begin() { last.push_back(0); }  // a struct element of a list: no field header
+  void elem_end() { b.push_back(0); last.pop_back(); }
+  void elem_i32(int32_t v) { varint(zz(v)); }
+  void elem_str(const std::string& s) { varint(s.size()); b.insert(b.end(), s.begin(), s.end()); }
+};
+
+enum PqType { PQ_BOOLEAN = 0, PQ_INT32 = 1, PQ_INT64 = 2, PQ_BYTE_ARRAY = 6 };
+enum PqConv { PC_UTF8 = 0, PC_MAP = 1, PC_LIST = 3, PC_DATE = 6, PC_INT_8 = 15, PC_INT_16 = 16 };
+enum PqRep { PR_REQUIRED = 0, PR_OPTIONAL = 1, PR_REPEATED = 2 };
+
+struct SElem {
+  std::string name;
+  int type = -1, rep = -1, nkids = -1, conv = -1;
+};
+
+// One leaf of the checkpoint schema and how its column is produced.
+struct CkLeafW {
+  std::vector<std::string> path;
+  int phys = 0, max_def = 0, max_rep = 0;
+  int side = -1;             // 0 adds, 1 removes (device), -1 protocol / metaData / txn rows (host)
+  EncLeaf enc{};             // device source (side leaves)
+  // host leaves: per head row, its levels and PLAIN values
+  std::vector<std::vector<uint8_t>> hdef, hrep, hval;
+};
+
+static void put_u32le(std::vector<uint8_t>& b, uint32_t v) {
+  for (int k = 0; k < 4; ++k) b.push_back(uint8_t(v >> (8 * k)));
+}
+static void put_varint(std::vector<uint8_t>& b, uint64_t v) {
+  while (v >= 0x80) { b.push_back(uint8_t(v) | 0x80); v >>= 7; }
+  b.push_back(uint8_t(v));
+}
+static int level_width(int max_level) {
+  int w = 0;
+  while ((1 << w) <= max_level) ++w;
+  return w;
+}
+// RLE runs of `lv` then `zeros` zero levels (the RLE/bit-packing hybrid, RLE runs only)
+static void rle_levels(std::vector<uint8_t>& out, const std::vector<uint8_t>& lv, uint64_t zeros, int width) {
+  const int vb = (width + 7) / 8;
+  size_t i = 0;
+  while (i < lv.size()) {
+    size_t j = i;
+    while (j < lv.size() && lv[j] == lv[i]) ++j;
+    uint64_t run = j - i;
+    if (j == lv.size() && lv[i] == 0) { run += zeros; zeros = 0; }
+    put_varint(out, run << 1);
+    for (int k = 0; k < vb; ++k) out.push_back(uint8_t(lv[i] >> (8 * k)));
+    i = j;
+  }
+  if (zeros) {
+    put_varint(out, zeros << 1);
+    for (int k = 0; k < vb; ++k) out.push_back(0);
+  }
+}
+
+// Levels and PLAIN values of one head row for a host leaf (the action's JSON as the checkpoint
+// writer's row: a missing field is null; txn.version and the protocol versions default to 0).
+static void head_row_levels(const CkLeafW& L, int top_kind, const NonFileAction* a, std::vector<uint8_t>& def,
+                            std::vector<uint8_t>& rep, std::vector<uint8_t>& val) {
+  static const char* kTop[3] = {"txn", "metaData", "protocol"};
+  const int mine = L.path[0] == kTop[0] ? 4 : L.path[0] == kTop[1] ? 3 : 5;
+  if (!a || a->kind != mine) {
+    def.push_back(0);
+    if (L.max_rep) rep.push_back(0);
+    return;
+  }
+  (void)top_kind;
+  auto put_value = [&](const JVal& v) {
+    if (L.phys == PQ_BYTE_ARRAY) {
+      const std::string s = v.t == JVal::STR ? v.s : json_dump(v);
+      put_u32le(val, uint32_t(s.size()));
+      val.insert(val.end(), s.begin(), s.end());
+    } else if (L.phys == PQ_INT64) {
+      const uint64_t x = uint64_t(v.as_int());
+      for (int k = 0; k < 8; ++k) val.push_back(uint8_t(x >> (8 * k)));
+    } else {
+      put_u32le(val, uint32_t(int32_t(v.as_int())));
+    }
+  };
+  const JVal* cur = &a->val;
+  int d = 1;  // the top-level struct is defined
+  const bool map_key = L.path.size() >= 2 && L.path[L.path.size() - 2] == "key_value" && L.path.back() == "key";
+  const bool map_val = L.path.size() >= 2 && L.path[L.path.size() - 2] == "key_value" && L.path.back() == "value";
+  const bool list_el = L.path.size() >= 2 && L.path[L.path.size() - 2] == "list";
+  const size_t nfields = L.path.size() - 1 - ((map_key || map_val || list_el) ? 2 : 0);
+  static const JVal kEmptyObj = [] {
+    JVal o;
+    o.t = JVal::OBJ;
+    return o;
+  }();
+  for (size_t f = 1; f <= nfields; ++f) {
+    const JVal* v = cur->get(L.path[f]);
+    // the checkpoint writer's metaData row: a missing format / options / configuration is empty
+    if ((!v || v->t == JVal::NUL) && L.path[0] == "metaData" &&
+        (L.path[f] == "format" || L.path[f] == "options" || L.path[f] == "configuration"))
+      v = &kEmptyObj;
+    const bool last = f == nfields && !(map_key || map_val || list_el);
+    const bool dflt = last && ((L.path[0] == "txn" && L.path[1] == "version") || L.path[0] == "protocol");
+    if (!v || v->t == JVal::NUL || (last && L.phys != PQ_BYTE_ARRAY && !v->is_int())) {
+      if (dflt) {
+        JVal zero;
+        zero.t = JVal::NUM;
+        zero.s = "0";
+        def.push_back(uint8_t(L.max_def));
+        put_value(zero);
+      } else {
+        def.push_back(uint8_t(d));
+      }
+      if (L.max_rep) rep.push_back(0);
+      return;
+    }
+    ++d;
+    cur = v;
+  }
+  if (!(map_key || map_val || list_el)) {
+    def.push_back(uint8_t(d));
+    put_value(*cur);
+    return;
+  }
+  // a map (object) or a list (array): defined at d; empty -> one level at d
+  std::vector<const JVal*> keys_v;
+  std::vector<std::string> keys;
+  std::vector<const JVal*> vals;
+  if (list_el && cur->t == JVal::ARR) {
+    for (const JVal& x : cur->a) vals.push_back(&x);
+  } else if (!list_el && cur->t == JVal::OBJ) {
+    for (auto& kv : cur->o) {  // first position, last value per key (LinkedHashMap)
+      size_t k = 0;
+      while (k < keys.size() && keys[k] != kv.first) ++k;
+      if (k == keys.size()) { keys.push_back(kv.first); vals.push_back(&kv.second); }
+      else vals[k] = &kv.second;
+    }
+  }
+  if (vals.empty()) {
+    def.push_back(uint8_t(d));
+    rep.push_back(0);
+    return;
+  }
+  for (size_t e = 0; e < vals.size(); ++e) {
+    rep.push_back(e ? 1 : 0);
+    if (map_key) {
+      def.push_back(uint8_t(d + 1));
+      put_u32le(val, uint32_t(keys[e].size()));
+      val.insert(val.end(), keys[e].begin(), keys[e].end());
+    } else if (vals[e]->t == JVal::NUL) {
+      def.push_back(uint8_t(d + 1));
+    } else {
+      def.push_back(uint8_t(d + 2));
+      put_value(*vals[e]);
+    }
+  }
+}
+
+static int32_t spark_type_code(const std::string& t) {
+  if (t == "string") return DR_T_STRING;
+  if (t == "byte") return DR_T_BYTE;
+  if (t == "short") return DR_T_SHORT;
+  if (t == "integer") return DR_T_INT;
+  if (t == "long") return DR_T_LONG;
+  if (t == "date") return DR_T_DATE;
+  if (t == "boolean") return DR_T_BOOLEAN;
+  return -1;
+}
+
+struct CkPartOut {
+  std::vector<uint8_t> file;
+  int64_t rows = 0;
+};
+
+static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uint32_t opts, uint64_t rg_rows,
+                                  CkPartOut& out) {
+  dr_ctx* ctx = st.ctx;
+  ctx->begin_call();
+  ensure_ready(st);
+  hipStream_t stream = ctx->stream;
+  if (st.sharded) fail(DR_E_UNSUPPORTED, "a sharded replay's part writes through the sharded writer");
+  // head rows: protocol, metaData, txns (the checkpoint writer's order)
+  std::vector<const NonFileAction*> head;
+  const NonFileAction* md = nullptr;
+  for (const NonFileAction& a : st.nonfile) if (a.kind == 5) head.push_back(&a);
+  for (const NonFileAction& a : st.nonfile) if (a.kind == 3) { head.push_back(&a); md = &a; }
+  for (const NonFileAction& a : st.nonfile) if (a.kind == 4) head.push_back(&a);
+  const uint64_t H = head.size(), NA = st.n_live, NR = st.n_tomb, ROWS = H + NA + NR;
+  const uint64_t step = parts > 1 ? (ROWS + uint64_t(parts) - 1) / uint64_t(parts) : ROWS;
+  const uint64_t p0 = std::min<uint64_t>(ROWS, uint64_t(part - 1) * step), p1 = std::min<uint64_t>(ROWS, p0 + step);
+  out.rows = int64_t(p1 - p0);
+  // partitionValues_parsed: the metadata's partition schema (D/Checkpoints.scala:372-389)
+  std::vector<std::pair<std::string, int32_t>> parsed;
+  if ((opts & DR_CKPT_PARSED) && md) {
+    const JVal* pc = md->val.get("partitionColumns");
+    const JVal* ss = md->val.get("schemaString");
+    JVal schema;
+    if (pc && pc->t == JVal::ARR && !pc->a.empty() && ss && ss->t == JVal::STR &&
+        json_parse(ss->s.data(), ss->s.size(), &schema)) {
+      const JVal* fields = schema.get("fields");
+      for (const JVal& c : pc->a) {
+        int32_t code = -1;
+        if (fields && fields->t == JVal::ARR)
+          for (const JVal& f : fields->a) {
+            const JVal* nm = f.get("name");
+            const JVal* ty = f.get("type");
+            if (nm && nm->t == JVal::STR && nm->s == c.s && ty && ty->t == JVal::STR) code = spark_type_code(ty->s);
+          }
+        if (code < 0) fail(DR_E_UNSUPPORTED, "partitionValues_parsed of partition column " + c.s + ": unsupported type");
+        parsed.push_back({c.s, code});
+      }
+    }
+  }
+  if (!parsed.empty()) {
+    std::vector<std::pair<std::string, int32_t>> want;
+    for (auto& pc : parsed) {
+      bool have = false;
+      for (auto& c : st.pv_cols) have |= c->name == pc.first && c->type == pc.second;
+      if (!have) want.push_back(pc);
+    }
+    if (!want.empty() && st.n_live) build_pv_columns(st, want);
+  }
+  DevExport X[2];
+  export_device(st, DR_LIVE, X[0]);
+  export_device(st, DR_TOMBSTONES, X[1]);
+  // ---- schema (DFS) and leaves ----
+  std::vector<SElem> schema;
+  std::vector<CkLeafW> leaves;
+  std::vector<std::string> at;  // current group path
+  auto group = [&](const std::string& name, int rep, int nkids, int conv = -1) {
+    schema.push_back(SElem{name, -1, rep, nkids, conv});
+  };
+  auto leaf = [&](const std::string& name, int rep, int phys, int conv, int max_def, int max_rep, int side,
+                  EncLeaf enc = EncLeaf{}) {
+    schema.push_back(SElem{name, phys, rep, -1, conv});
+    CkLeafW L;
+    L.path = at;
+    L.path.push_back(name);
+    L.phys = phys;
+    L.max_def = max_def;
+    L.max_rep = max_rep;
+    L.side = side;
+    L.enc = enc;
+    leaves.push_back(std::move(L));
+  };
+  auto str_map = [&](const std::string& name, int base, int side, EncLeaf k, EncLeaf v) {
+    group(name, PR_OPTIONAL, 1, PC_MAP);
+    at.push_back(name);
+    group("key_value", PR_REPEATED, 2);
+    at.push_back("key_value");
+    leaf("key", PR_REQUIRED, PQ_BYTE_ARRAY, PC_UTF8, base + 2, 1, side, k);
+    leaf("value", PR_OPTIONAL, PQ_BYTE_ARRAY, PC_UTF8, base + 3, 1, side, v);
+    at.pop_back();
+    at.pop_back();
+  };
+  auto side_map = [&](const DevExport& x, bool pv) {
+    EncLeaf k{}, v{};
+    k.kind = ENC_MAP_KEY;
+    v.kind = ENC_MAP_VAL;
+    k.null = v.null = pv ? x.pv_null.p : x.tags_null.p;
+    k.entry_off = v.entry_off = pv ? x.off[EXC_PV_N].p : x.off[EXC_TAGS_N].p;
+    k.eoff = pv ? x.pv_key_off.p : x.tags_key_off.p;
+    k.ebytes = pv ? x.pv_key_bytes.p : x.tags_key_bytes.p;
+    v.eoff = pv ? x.pv_val_off.p : x.tags_val_off.p;
+    v.ebytes = pv ? x.pv_val_bytes.p : x.tags_val_bytes.p;
+    v.enull = pv ? x.pv_val_null.p : x.tags_val_null.p;
+    k.def_null = v.def_null = 1;
+    k.def_present = 3;
+    v.def_present = 4;
+    return std::make_pair(k, v);
+  };
+  auto flat = [&](int kind, int dn, int dp) {
+    EncLeaf e{};
+    e.kind = kind;
+    e.def_null = dn;
+    e.def_present = dp;
+    return e;
+  };
+  const bool stats = (opts & DR_CKPT_STATS) != 0;
+  group("schema", -1, 5);
+  // txn
+  group("txn", PR_OPTIONAL, 3);
+  at = {"txn"};
+  leaf("appId", PR_OPTIONAL, PQ_BYTE_ARRAY, PC_UTF8, 2, 0, -1);
+  leaf("version", PR_OPTIONAL, PQ_INT64, -1, 2, 0, -1);
+  leaf("lastUpdated", PR_OPTIONAL, PQ_INT64, -1, 2, 0, -1);
+  // add
+  group("add", PR_OPTIONAL, 6 + (stats ? 1 : 0) + (parsed.empty() ? 0 : 1));
+  at = {"add"};
+  {
+    const DevExport& x = X[0];
+    EncLeaf e = flat(ENC_STR_OFF, 1, 2);
+    e.off = x.path_off.p;
+    e.bytes = x.path_bytes.p;
+    leaf("path", PR_OPTIONAL, PQ_BYTE_ARRAY, PC_UTF8, 2, 0, 0, e);
+    auto pv = side_map(x, true);
+    str_map("partitionValues", 1, 0, pv.first, pv.second);
+    e = flat(ENC_I64, 1, 2);
+    e.i64 = x.size.p;
+    leaf("size", PR_OPTIONAL, PQ_INT64, -1, 2, 0, 0, e);
+    e = flat(ENC_I64, 1, 2);
+    e.i64 = x.mtime.p;
+    leaf("modificationTime", PR_OPTIONAL, PQ_INT64, -1, 2, 0, 0, e);
+    leaf("dataChange", PR_OPTIONAL, PQ_BOOLEAN, -1, 2, 0, 0, flat(ENC_BOOL, 1, 2));
+    auto tg = side_map(x, false);
+    str_map("tags", 1, 0, tg.first, tg.second);
+    if (stats) {
+      e = flat(ENC_STR_OFF, 1, 2);
+      e.off = x.off[EXC_STATS].p;
+      e.bytes = x.stats_bytes.p;
+      e.null = x.stats_null.p;
+      leaf("stats", PR_OPTIONAL, PQ_BYTE_ARRAY, PC_UTF8, 2, 0, 0, e);
+    }
+    if (!parsed.empty()) {
+      group("partitionValues_parsed", PR_OPTIONAL, int(parsed.size()));
+      at.push_back("partitionValues_parsed");
+      for (auto& pc : parsed) {
+        const dr_state::PvCol* col = nullptr;
+        for (auto& c : st.pv_cols) if (c->name == pc.first && c->type == pc.second) col = c.get();
+        EncLeaf f{};
+        f.def_null = 2;
+        f.def_present = 3;
+        if (col) f.null = col->isnull.p;
+        int phys = PQ_INT32, conv = -1;
+        switch (pc.second) {
+          case DR_T_STRING: f.kind = ENC_STR_PTR; if (col) { f.sptr = col->sptr.p; f.slen = col->slen.p; } phys = PQ_BYTE_ARRAY; conv = PC_UTF8; break;
+          case DR_T_LONG: f.kind = ENC_I64; if (col) f.i64 = col->w64.p; phys = PQ_INT64; break;
+          case DR_T_BOOLEAN: f.kind = ENC_BOOL; if (col) f.i32 = col->w32.p; phys = PQ_BOOLEAN; break;
+          default:
+            f.kind = ENC_I32;
+            if (col) f.i32 = col->w32.p;
+            conv = pc.second == DR_T_DATE ? PC_DATE : pc.second == DR_T_BYTE ? PC_INT_8 : pc.second == DR_T_SHORT ? PC_INT_16 : -1;
+        }
+        leaf(pc.first, PR_OPTIONAL, phys, conv, 3, 0, 0, f);
+      }
+      at.pop_back();
+    }
+  }
+  // remove
+  group("remove", PR_OPTIONAL, 7);
+  at = {"remove"};
+  {
+    const DevExport& x = X[1];
+    EncLeaf e = flat(ENC_STR_OFF, 1, 2);
+    e.off = x.path_off.p;
+    e.bytes = x.path_bytes.p;
+    leaf("path", PR_OPTIONAL, PQ_BYTE_ARRAY, PC_UTF8, 2, 0, 1, e);
+    e = flat(ENC_I64, 1, 2);
+    e.i64 = reinterpret_cast<const int64_t*>(x.delts.p);
+    e.vflags = x.flags.p;
+    e.vbit = 1;  // F_HAS_DELTS
+    leaf("deletionTimestamp", PR_OPTIONAL, PQ_INT64, -1, 2, 0, 1, e);
+    leaf("dataChange", PR_OPTIONAL, PQ_BOOLEAN, -1, 2, 0, 1, flat(ENC_BOOL, 1, 2));
+    e = flat(ENC_BOOL, 1, 2);
+    e.b8 = x.efm.p;
+    leaf("extendedFileMetadata", PR_OPTIONAL, PQ_BOOLEAN, -1, 2, 0, 1, e);
+    auto pv = side_map(x, true);
+    str_map("partitionValues", 1, 1, pv.first, pv.second);
+    e = flat(ENC_I64, 1, 2);
+    e.i64 = x.size.p;
+    leaf("size", PR_OPTIONAL, PQ_INT64, -1, 2, 0, 1, e);
+    auto tg = side_map(x, false);
+    str_map("tags", 1, 1, tg.first, tg.second);
+  }
+  // metaData
+  group("metaData", PR_OPTIONAL, 8);
+  at = {"metaData"};
+  leaf("id", PR_OPTIONAL, PQ_BYTE_ARRAY, PC_UTF8, 2, 0, -1);
+  leaf("name", PR_OPTIONAL, PQ_BYTE_ARRAY, PC_UTF8, 2, 0, -1);
+  leaf("description", PR_OPTIONAL, PQ_BYTE_ARRAY, PC_UTF8, 2, 0, -1);
+  group("format", PR_OPTIONAL, 2);
+  at = {"metaData", "format"};
+  leaf("provider", PR_OPTIONAL, PQ_BYTE_ARRAY, PC_UTF8, 3, 0, -1);
+  str_map("options", 2, -1, EncLeaf{}, EncLeaf{});
+  at = {"metaData"};
+  leaf("schemaString", PR_OPTIONAL, PQ_BYTE_ARRAY, PC_UTF8, 2, 0, -1);
+  group("partitionColumns", PR_OPTIONAL, 1, PC_LIST);
+  at = {"metaData", "partitionColumns"};
+  group("list", PR_REPEATED, 1);
+  at.push_back("list");
+  leaf("element", PR_OPTIONAL, PQ_BYTE_ARRAY, PC_UTF8, 4, 1, -1);
+  at = {"metaData"};
+  str_map("configuration", 1, -1, EncLeaf{}, EncLeaf{});
+  leaf("createdTime", PR_OPTIONAL, PQ_INT64, -1, 2, 0, -1);
+  // protocol
+  group("protocol", PR_OPTIONAL, 2);
+  at = {"protocol"};
+  leaf("minReaderVersion", PR_OPTIONAL, PQ_INT32, -1, 2, 0, -1);
+  leaf("minWriterVersion", PR_OPTIONAL, PQ_INT32, -1, 2, 0, -1);
+  // host leaves: their levels / values per head row
+  for (CkLeafW& L : leaves) {
+    if (L.side >= 0) continue;
+    L.hdef.resize(H);
+    L.hrep.resize(H);
+    L.hval.resize(H);
+    for (uint64_t h = 0; h < H; ++h) head_row_levels(L, 0, head[h], L.hdef[h], L.hrep[h], L.hval[h]);
+  }
+  // ---- pages ----
+  std::vector<uint8_t>& f = out.file;
+  f = {'P', 'A', 'R', '1'};
+  struct ChunkMeta { int64_t off, size, nval; };
+  struct RG { std::vector<ChunkMeta> cols; int64_t rows, bytes; };
+  std::vector<RG> rgs;
+  const uint64_t rgn = rg_rows ? rg_rows : (uint64_t(1) << 20);
+  DBuf<uint8_t> scratch(ctx, scan_scratch_for(std::min<uint64_t>(rgn, p1 - p0) + 1));
+  for (uint64_t r0 = p0; r0 < p1; r0 += rgn) {
+    const uint64_t r1 = std::min(p1, r0 + rgn);
+    RG rg;
+    rg.rows = int64_t(r1 - r0);
+    rg.bytes = 0;
+    for (CkLeafW& L : leaves) {
+      std::vector<uint8_t> rep, def, vals;
+      uint64_t nlev = 0;
+      const int dw = level_width(L.max_def), rw = level_width(L.max_rep);
+      const uint64_t side_lo = L.side == 0 ? H : H + NA, side_n = L.side == 0 ? NA : NR;
+      const bool dev = L.side >= 0 && r0 < side_lo + side_n && r1 > side_lo;
+      if (!dev) {
+        std::vector<uint8_t> hd, hr;
+        for (uint64_t g = r0; g < std::min<uint64_t>(r1, H); ++g) {
+          if (L.side >= 0) { hd.push_back(0); if (L.max_rep) hr.push_back(0); continue; }
+          hd.insert(hd.end(), L.hdef[g].begin(), L.hdef[g].end());
+          hr.insert(hr.end(), L.hrep[g].begin(), L.hrep[g].end());
+          vals.insert(vals.end(), L.hval[g].begin(), L.hval[g].end());
+        }
+        const uint64_t zeros = r1 - std::max<uint64_t>(r0, std::min<uint64_t>(r1, H));
+        nlev = hd.size() + zeros;
+        if (L.max_rep) rle_levels(rep, hr, zeros, rw);
+        rle_levels(def, hd, zeros, dw);
+      } else {
+        const uint64_t R = r1 - r0;
+        DBuf<uint32_t> nl(ctx, R), vb(ctx, R);
+        DBuf<uint64_t> lo(ctx, R + 1), vo(ctx, R + 1);
+        EncArgs a{};
+        a.L = L.enc;
+        a.r0 = r0;
+        a.r1 = r1;
+        a.side_lo = side_lo;
+        a.n = side_n;
+        a.nlev = nl.p;
+        a.vbytes = vb.p;
+        launch_enc_count(a, stream);
+        launch_scan_u32(nl.p, lo.p, R, scratch.p, stream);
+        launch_scan_u32(vb.p, vo.p, R, scratch.p, stream);
+        nlev = d2h_one(lo.p + R, stream);
+        const uint64_t nvb = d2h_one(vo.p + R, stream);
+        DBuf<uint8_t> dl(ctx, nlev + 8), rl(ctx, L.max_rep ? nlev + 8 : 1), vv(ctx, nvb + 8);
+        a.lev_off = lo.p;
+        a.val_off = vo.p;
+        a.def = dl.p;
+        a.rep = rl.p;
+        a.vals = vv.p;
+        launch_enc_fill(a, stream);
+        const uint64_t groups = (nlev + 7) / 8;
+        auto packed = [&](DBuf<uint8_t>& lv, int w, std::vector<uint8_t>& dst) {
+          DBuf<uint8_t> pk(ctx, groups * uint64_t(w) + 1);
+          launch_enc_pack(lv.p, nlev, w, pk.p, stream);
+          put_varint(dst, (groups << 1) | 1);
+          const std::vector<uint8_t> h = d2h(pk.p, groups * uint64_t(w), stream);
+          dst.insert(dst.end(), h.begin(), h.end());
+        };
+        if (L.max_rep) packed(rl, rw, rep);
+        packed(dl, dw, def);
+        if (L.phys == PQ_BOOLEAN) {
+          DBuf<uint8_t> pk(ctx, (nvb + 7) / 8 + 1);
+          launch_enc_pack(vv.p, nvb, 1, pk.p, stream);
+          vals = d2h(pk.p, (nvb + 7) / 8, stream);
+        } else {
+          vals = d2h(vv.p, nvb, stream);
+        }
+      }
+      if (L.phys == PQ_BOOLEAN && !dev) {  // host BOOLEAN values are bytes until packed (none are written)
+        vals.clear();
+      }
+      std::vector<uint8_t> body;
+      if (L.max_rep) { put_u32le(body, uint32_t(rep.size())); body.insert(body.end(), rep.begin(), rep.end()); }
+      put_u32le(body, uint32_t(def.size()));
+      body.insert(body.end(), def.begin(), def.end());
+      body.insert(body.end(), vals.begin(), vals.end());
+      if (body.size() > uint64_t(INT32_MAX)) fail(DR_E_UNSUPPORTED, "checkpoint page over 2 GiB: use smaller row groups");
+      ThriftW ph;
+      ph.i32(1, 0);  // DATA_PAGE
+      ph.i32(2, int32_t(body.size()));
+      ph.i32(3, int32_t(body.size()));
+      ph.begin_struct(5);
+      ph.i32(1, int32_t(nlev));
+      ph.i32(2, 0);  // PLAIN
+      ph.i32(3, 3);  // RLE
+      ph.i32(4, 3);  // RLE
+      ph.end_struct();
+      ph.b.push_back(0);
+      const int64_t off = int64_t(f.size());
+      f.insert(f.end(), ph.b.begin(), ph.b.end());
+      f.insert(f.end(), body.begin(), body.end());
+      rg.cols.push_back(ChunkMeta{off, int64_t(ph.b.size() + body.size()), int64_t(nlev)});
+      rg.bytes += int64_t(ph.b.size() + body.size());
+    }
+    rgs.push_back(std::move(rg));
+  }
+  // ---- footer ----
+  ThriftW fm;
+  fm.i32(1, 1);
+  fm.begin_list(2, 12, schema.size());
+  for (const SElem& e : schema) {
+    fm.elem_begin();
+    if (e.type >= 0) fm.i32(1, e.type);
+    if (e.rep >= 0) fm.i32(3, e.rep);
+    fm.str(4, e.name);
+    if (e.nkids >= 0) fm.i32(5, e.nkids);
+    if (e.conv >= 0) fm.i32(6, e.conv);
+    fm.elem_end();
+  }
+  fm.i64(3, int64_t(p1 - p0));
+  fm.begin_list(4, 12, rgs.size());
+  for (const RG& rg : rgs) {
+    fm.elem_begin();
+    fm.begin_list(1, 12, rg.cols.size());
+    for (size_t c = 0; c < rg.cols.size(); ++c) {
+      const CkLeafW& L = leaves[c];
+      const ChunkMeta& m = rg.cols[c];
+      fm.elem_begin();
+      fm.i64(2, m.off);
+      fm.begin_struct(3);
+      fm.i32(1, L.phys);
+      fm.begin_list(2, 5, 2);
+      fm.elem_i32(0);  // PLAIN
+      fm.elem_i32(3);  // RLE
+      fm.begin_list(3, 8, L.path.size());
+      for (const std::string& s : L.path) fm.elem_str(s);
+      fm.i32(4, 0);  // UNCOMPRESSED
+      fm.i64(5, m.nval);
+      fm.i64(6, m.size);
+      fm.i64(7, m.size);
+      fm.i64(9, m.off);
+      fm.end_struct();
+      fm.elem_end();
+    }
+    fm.i64(2, rg.bytes);
+    fm.i64(3, rg.rows);
+    fm.elem_end();
+  }
+  fm.str(6, "libdeltareplay (MI355X checkpoint writer)");
+  fm.b.push_back(0);
+  f.insert(f.end(), fm.b.begin(), fm.b.end());
+  put_u32le(f, uint32_t(fm.b.size()));
+  f.insert(f.end(), {'P', 'A', 'R', '1'});
+  ctx->collect_timings();
 }
 
 static std::vector<int64_t> select_flags(dr_state& st, DBuf<uint32_t>& flag);
@@ -3256,6 +3865,24 @@ int dr_state_partition_groups(dr_state* state, const int64_t* rows, int64_t nrow
     *order = malloc_copy(o);
     *group_off = malloc_copy(g);
     *ngroups = int64_t(g.size()) - 1;
+  });
+}
+
+int dr_state_write_checkpoint(dr_state* state, int32_t part, int32_t parts, uint32_t opts, uint64_t row_group_rows,
+                              uint8_t** bytes, uint64_t* len, int64_t* rows) {
+  if (!state || !bytes || !len || parts < 1 || part < 1 || part > parts) return DR_E_INVALID_ARG;
+  *bytes = nullptr;
+  *len = 0;
+  return guard(state->ctx, [&] {
+    HIP_OK(hipSetDevice(state->ctx->device));
+    CkPartOut o;
+    write_checkpoint_part(*state, part, parts, opts, row_group_rows, o);
+    uint8_t* buf = static_cast<uint8_t*>(malloc(std::max<size_t>(o.file.size(), 1)));
+    if (!buf) throw std::bad_alloc();
+    memcpy(buf, o.file.data(), o.file.size());
+    *bytes = buf;
+    *len = o.file.size();
+    if (rows) *rows = o.rows;
   });
 }
 

@@ -580,3 +580,46 @@ struct ExportArgs {
 };
 void launch_export(const ExportArgs& a, hipStream_t st);
 }  // namespace dr
+
+// ---- checkpoint page encoding (k_encode.hip) -----------------------------------------------------
+namespace dr {
+enum EncKind : int32_t { ENC_STR_PTR = 0, ENC_STR_OFF = 1, ENC_I64 = 2, ENC_I32 = 3, ENC_BOOL = 4, ENC_MAP_KEY = 5,
+                         ENC_MAP_VAL = 6 };
+// One leaf column of one side (adds or removes) of a checkpoint: where its records' values are and
+// the definition levels it takes. Rows of the row group outside the side's records are a null struct
+// (one level, def 0).
+struct EncLeaf {
+  int32_t kind;
+  int32_t def_null, def_present;  // flat: null field / value (maps: def_null = the map-null level)
+  const uint8_t* null;            // per record (null pointer: never null)
+  const uint64_t* sptr;           // ENC_STR_PTR
+  const uint32_t* slen;
+  const uint64_t* off;            // ENC_STR_OFF: [n + 1] offsets into bytes
+  const uint8_t* bytes;
+  const int64_t* i64;
+  const uint32_t* i32;
+  const uint8_t* b8;
+  const uint64_t* entry_off;      // maps: [n + 1] first entry per record
+  const int64_t* eoff;            // maps: [entries + 1] key or value byte offsets
+  const uint8_t* ebytes;
+  const uint8_t* enull;           // map values: per entry
+  const uint8_t* vflags;          // non-null: the record is null unless vflags[i] & vbit
+  uint32_t vbit;
+};
+struct EncArgs {
+  EncLeaf L;
+  uint64_t r0, r1;       // row group (global checkpoint rows)
+  uint64_t side_lo, n;   // the side's records are rows [side_lo, side_lo + n)
+  uint32_t* nlev;        // per row of the group
+  uint32_t* vbytes;
+  const uint64_t* lev_off;  // fill: exclusive scans
+  const uint64_t* val_off;
+  uint8_t* def;
+  uint8_t* rep;
+  uint8_t* vals;
+};
+void launch_enc_count(const EncArgs& a, hipStream_t st);
+void launch_enc_fill(const EncArgs& a, hipStream_t st);
+// Bit-packs n one-byte values (< 2^width) in groups of 8 (RLE/bit-packing hybrid body; n padded).
+void launch_enc_pack(const uint8_t* in, uint64_t n, int width, uint8_t* out, hipStream_t st);
+}  // namespace dr

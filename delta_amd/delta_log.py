@@ -361,6 +361,21 @@ class State:
         self.eng.lib.dr_free(C.cast(sel, C.c_void_p))
         return res
 
+    def write_checkpoint_part(self, part: int, parts: int, stats: bool = True, parsed: bool = True,
+                              row_group_rows: int = 0) -> Tuple[bytes, int]:
+        """dr_state_write_checkpoint: part `part` (1-based) of `parts` as Parquet bytes, the file-action
+        columns encoded on the GPU; returns (bytes, rows)."""
+        buf = C.POINTER(C.c_uint8)()
+        n = C.c_uint64()
+        rows = C.c_int64()
+        opts = (N.DR_CKPT_STATS if stats else 0) | (N.DR_CKPT_PARSED if parsed else 0)
+        with self.eng.lock:
+            self.eng.check(self.eng.lib.dr_state_write_checkpoint(self.h, int(part), int(parts), opts, int(row_group_rows),
+                                                                  C.byref(buf), C.byref(n), C.byref(rows)))
+        data = C.string_at(buf, n.value)
+        self.eng.lib.dr_free(C.cast(buf, C.c_void_p))
+        return data, rows.value
+
     def _take(self, ptr, n) -> List[int]:
         res = [ptr[i] for i in range(n)]
         self.eng.lib.dr_free(C.cast(ptr, C.c_void_p))
@@ -671,11 +686,14 @@ class DeltaLog:
             staged.release()
         return Snapshot(self, vers[-1], state, cutoff)
 
-    def checkpoint(self, parts: int = 1) -> dict:
+    def checkpoint(self, parts: int = 1, device: bool = True) -> dict:
         """Checkpoints.checkpoint (D/Checkpoints.scala:119-141): write the current snapshot's
-        checkpoint (multi-part when parts > 1) and `_last_checkpoint` (delta_amd/checkpoint.py)."""
-        from .checkpoint import write_checkpoint
+        checkpoint (multi-part when parts > 1) and `_last_checkpoint` (delta_amd/checkpoint.py):
+        Parquet pages encoded on the GPU (device=True) or by Arrow from the device export."""
+        from .checkpoint import write_checkpoint, write_checkpoint_device
         with self._lock:
+            if device:
+                return write_checkpoint_device(self._snapshot, parts=parts)
             return write_checkpoint(self._snapshot, parts=parts)
 
     def get_changes(self, start_version: int, fail_on_data_loss: bool = False):

@@ -258,6 +258,19 @@ typedef struct dr_predicate {
 int dr_filter(dr_state* state, const dr_predicate* pred, int64_t** selected, int64_t* nselected);
 void dr_free(void* p);
 
+/* ---- checkpoint writer --------------------------------------------------
+ * Checkpoints.writeCheckpoint / buildCheckpoint (D/Checkpoints.scala:229-365): part `part` (1-based)
+ * of `parts` of the state's checkpoint -- rows protocol, metaData, txns, allFiles, tombstones
+ * (dataChange=false), split into contiguous slices -- as a complete Parquet file in *bytes (freed
+ * with dr_free). The file-action columns are encoded on the device; pages are uncompressed;
+ * `row_group_rows` 0 = 2^20. opts: DR_CKPT_STATS writes add.stats (delta.checkpoint.writeStatsAsJson),
+ * DR_CKPT_PARSED adds add.partitionValues_parsed (the partition schema's types; writeStatsAsStruct /
+ * checkpointV2). The caller writes the file (temp + rename) and `_last_checkpoint`. */
+#define DR_CKPT_STATS 0x1u
+#define DR_CKPT_PARSED 0x2u
+int dr_state_write_checkpoint(dr_state* state, int32_t part, int32_t parts, uint32_t opts, uint64_t row_group_rows,
+                              uint8_t** bytes, uint64_t* len, int64_t* rows);
+
 /* ---- scan-side consumers of the resident state -----------------------
  * DeltaSourceSnapshot.initialFiles (D/files/DeltaSourceSnapshot.scala:53-95): allFiles.sort(
  * "modificationTime", "path") computed on the device (modificationTime decoded from the live files'

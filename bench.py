@@ -265,6 +265,19 @@ def measure_stream(eng, table, exp, args):
     }
 
 
+def measure_checkpoint_write(eng, staged, cutoff, parts):
+    """Config 4's multi-part checkpoint write (dr_state_write_checkpoint, file-action pages encoded on
+    the GPU): part 1 of `parts` timed (bytes to host memory, no disk), the rate per row reported."""
+    st = staged.replay(cutoff)
+    st.write_checkpoint_part(1, parts)  # first call: the device export of both sides
+    t0 = time.perf_counter()
+    data, rows = st.write_checkpoint_part(2, parts)
+    dt = time.perf_counter() - t0
+    st.release()
+    return {"parts": parts, "part_rows": rows, "part_bytes": len(data), "part_s": round(dt, 4),
+            "rows_per_s": round(rows / dt, 1), "codec": "UNCOMPRESSED"}
+
+
 def measure_filter(eng, staged, cutoff, exp, steps):
     """K5 over the reconstructed state: config 4's 4-column conjunction. The first dr_filter builds the
     state's typed partition-value cache (k_pv_extract); later ones only run k_filter_typed."""
@@ -470,9 +483,10 @@ def main():
         e2e = {"stage_s": round(stage_s, 3), "replay_s": round(t2 - t1, 4), "export_s": round(t3 - t2, 4),
                "actions_per_s_incl_staging": round(counts["num_actions"] / (stage_s + t2 - t1), 1),
                "actions_per_s_incl_staging_and_export": round(counts["num_actions"] / (stage_s + t3 - t1), 1)}
-    k5 = None
+    k5 = ckpt = None
     if world == 1 and args.config == 4:
         k5 = measure_filter(eng, staged, cutoff, exp, args.steps)
+        ckpt = measure_checkpoint_write(eng, staged, cutoff, parts=100)
     out = {
         "metric": "log actions replayed/sec + achieved HBM GB/s, 1/2/4/8 GPU, 10M-file table",
         "value": round(value, 1), "unit": "actions/s", "n_gpus": world, "steps": args.steps,
@@ -489,6 +503,7 @@ def main():
         "cpu_baseline": cpu,
         "end_to_end": e2e,
         "k5_filter": k5,
+        "checkpoint_write": ckpt,
         "kernels": kernels,
         "result": {k: counts[k] for k in ("num_files", "num_removes", "size_in_bytes", "live_key_sum",
                                           "tomb_key_sum")},

@@ -315,14 +315,41 @@ struct dr_staged {
   std::shared_ptr<StagedData> d;
 };
 
+// Host vectors the export copies into: no value-initialisation (the D2H copy overwrites every
+// element; zero-filling gigabytes first doubled the export time).
+template <typename T>
+struct NoInitAlloc : std::allocator<T> {
+  template <typename U>
+  struct rebind { using other = NoInitAlloc<U>; };
+  NoInitAlloc() = default;
+  template <typename U>
+  NoInitAlloc(const NoInitAlloc<U>&) {}
+  template <typename U>
+  void construct(U* p) noexcept { ::new (static_cast<void*>(p)) U; }
+  template <typename U, typename... A>
+  void construct(U* p, A&&... a) { ::new (static_cast<void*>(p)) U(std::forward<A>(a)...); }
+};
+template <typename T>
+using hvec = std::vector<T, NoInitAlloc<T>>;
+
 struct ExportCols {
   bool built = false;
   int64_t n = 0;
-  std::vector<int64_t> path_off, size, mtime, delts, stats_off, pv_entry_off, pv_key_off, pv_val_off,
-      tags_entry_off, tags_key_off, tags_val_off;
-  std::vector<uint8_t> path_bytes, delts_valid, efm, stats_bytes, stats_null, pv_null, pv_key_bytes,
-      pv_val_bytes, pv_val_null, tags_null, tags_key_bytes, tags_val_bytes, tags_val_null;
+  hvec<int64_t> path_off, size, mtime, delts, stats_off, pv_entry_off, pv_key_off, pv_val_off, tags_entry_off,
+      tags_key_off, tags_val_off;
+  hvec<uint8_t> path_bytes, delts_valid, efm, stats_bytes, stats_null, pv_null, pv_key_bytes, pv_val_bytes, pv_val_null,
+      tags_null, tags_key_bytes, tags_val_bytes, tags_val_null;
 };
+
+// D2H into a host vector without initialising it first.
+template <typename T, typename H>
+static void d2h_into(H& out, const T* p, size_t n, hipStream_t s) {
+  out.resize(n);
+  if (n) {
+    HIP_OK(hipMemcpyAsync(out.data(), p, n * sizeof(T), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+  }
+}
 
 // The chain of states that dr_state_apply grows from one full replay: an
 // append-only action store (the base's survivors, then every applied tail), the device path index
@@ -351,6 +378,8 @@ struct IncChain {
   std::vector<std::shared_ptr<DBuf<uint8_t>>> arenas;
   DBuf<unsigned long long> ctr;
 };
+
+struct ExpDecoded;
 
 struct dr_state {
   dr_ctx* ctx = nullptr;
@@ -393,6 +422,8 @@ struct dr_state {
   };
   std::vector<std::unique_ptr<PvCol>> pv_cols;
   std::vector<std::shared_ptr<DBuf<uint8_t>>> pv_arenas;  // unescaped string values
+  // export: the checkpoint's add / remove leaves, decoded on the first export of each side
+  std::shared_ptr<ExpDecoded> exp_dec[2];
 };
 
 // ---------------------------------------------------------------------------------------------------
@@ -1678,10 +1709,6 @@ static void decode_export_side(dr_state& st, int which, ExpDecoded& D) {
   }
 }
 
-template <typename T>
-static std::vector<int64_t> to_i64(const std::vector<T>& v) {
-  return std::vector<int64_t>(v.begin(), v.end());
-}
 
 // One side's export columns in HBM (k_export's output; the checkpoint encoder reads them there).
 struct DevExport {
@@ -1697,13 +1724,17 @@ struct DevExport {
   DBuf<int64_t> pv_key_off, pv_val_off, tags_key_off, tags_val_off;  // per entry (entries + 1)
 };
 
-static void export_device(dr_state& st, int which, DevExport& X) {
+// Records [lo, hi) of the side (export order); the whole side by default.
+static void export_device(dr_state& st, int which, DevExport& X, uint64_t lo = 0, uint64_t hi = UINT64_MAX) {
   ensure_ready(st);
   dr_ctx* ctx = st.ctx;
   hipStream_t stream = ctx->stream;
   StagedData& s = *st.sources[0];
-  const uint64_t n = which == DR_LIVE ? st.n_live : st.n_tomb;
-  const uint32_t* didx = which == DR_LIVE ? st.live.p : st.tomb.p;
+  const uint64_t total = which == DR_LIVE ? st.n_live : st.n_tomb;
+  hi = std::min(hi, total);
+  lo = std::min(lo, hi);
+  const uint64_t n = hi - lo;
+  const uint32_t* didx = (which == DR_LIVE ? st.live.p : st.tomb.p) + lo;
   X.n = n;
   // canonical paths, deletionTimestamp and flags from the action arrays
   X.path_ptr = DBuf<uint64_t>(ctx, n);
@@ -1721,8 +1752,12 @@ static void export_device(dr_state& st, int which, DevExport& X) {
   const uint64_t nb = n ? d2h_one(X.path_off.p + n, stream) : 0;
   X.path_bytes = DBuf<uint8_t>(ctx, nb + 1);
   launch_gather_bytes(X.path_ptr.p, X.path_len.p, X.path_off.p, n, X.path_bytes.p, stream);
-  ExpDecoded D;
-  decode_export_side(st, which, D);
+  if (!st.exp_dec[which]) {
+    auto d = std::make_shared<ExpDecoded>();
+    decode_export_side(st, which, *d);
+    st.exp_dec[which] = d;
+  }
+  const ExpDecoded& D = *st.exp_dec[which];
   ExportArgs a{};
   a.idx = didx;
   a.n = n;
@@ -1808,42 +1843,42 @@ static void build_export(dr_state& st, int which) {
   ensure_ready(st);
   ExportCols& ex = st.exp[which];
   if (ex.built) return;
-  hipStream_t stream = st.ctx->stream;
+  dr_ctx* ctx = st.ctx;
+  hipStream_t stream = ctx->stream;
   DevExport X;
   export_device(st, which, X);
   const uint64_t n = X.n;
   ex.n = int64_t(n);
-  ex.path_off = to_i64(d2h(X.path_off.p, n + 1, stream));
-  ex.path_bytes = d2h(X.path_bytes.p, n ? uint64_t(ex.path_off[n]) : 0, stream);
-  const std::vector<uint64_t> dv = d2h(X.delts.p, n, stream);
-  const std::vector<uint8_t> fv = d2h(X.flags.p, n, stream);
-  ex.delts.resize(n);
-  ex.delts_valid.resize(n);
+  // u64 offsets and delTs are copied as int64 (same bits); delTs validity is F_HAS_DELTS
+  d2h_into(ex.path_off, reinterpret_cast<const int64_t*>(X.path_off.p), n + 1, stream);
+  d2h_into(ex.path_bytes, X.path_bytes.p, n ? uint64_t(ex.path_off[n]) : 0, stream);
+  d2h_into(ex.delts, reinterpret_cast<const int64_t*>(X.delts.p), n, stream);
+  d2h_into(ex.delts_valid, X.flags.p, n, stream);
   for (uint64_t i = 0; i < n; ++i) {
-    const bool valid = (fv[i] & 1u) != 0;  // F_HAS_DELTS
-    ex.delts_valid[i] = valid;
-    ex.delts[i] = valid ? int64_t(dv[i]) : 0;
+    ex.delts_valid[i] &= 1u;  // F_HAS_DELTS
+    if (!ex.delts_valid[i]) ex.delts[i] = 0;
   }
-  ex.size = d2h(X.size.p, n, stream);
-  ex.mtime = d2h(X.mtime.p, n, stream);
-  ex.efm = d2h(X.efm.p, n, stream);
-  ex.stats_null = d2h(X.stats_null.p, n, stream);
-  ex.pv_null = d2h(X.pv_null.p, n, stream);
-  ex.tags_null = d2h(X.tags_null.p, n, stream);
-  ex.stats_off = to_i64(d2h(X.off[EXC_STATS].p, n + 1, stream));
-  ex.pv_entry_off = to_i64(d2h(X.off[EXC_PV_N].p, n + 1, stream));
-  ex.tags_entry_off = to_i64(d2h(X.off[EXC_TAGS_N].p, n + 1, stream));
-  ex.stats_bytes = d2h(X.stats_bytes.p, X.tot[EXC_STATS], stream);
-  ex.pv_key_off = d2h(X.pv_key_off.p, X.tot[EXC_PV_N] + 1, stream);
-  ex.pv_val_off = d2h(X.pv_val_off.p, X.tot[EXC_PV_N] + 1, stream);
-  ex.pv_val_null = d2h(X.pv_val_null.p, X.tot[EXC_PV_N], stream);
-  ex.pv_key_bytes = d2h(X.pv_key_bytes.p, X.tot[EXC_PV_KB], stream);
-  ex.pv_val_bytes = d2h(X.pv_val_bytes.p, X.tot[EXC_PV_VB], stream);
-  ex.tags_key_off = d2h(X.tags_key_off.p, X.tot[EXC_TAGS_N] + 1, stream);
-  ex.tags_val_off = d2h(X.tags_val_off.p, X.tot[EXC_TAGS_N] + 1, stream);
-  ex.tags_val_null = d2h(X.tags_val_null.p, X.tot[EXC_TAGS_N], stream);
-  ex.tags_key_bytes = d2h(X.tags_key_bytes.p, X.tot[EXC_TAGS_KB], stream);
-  ex.tags_val_bytes = d2h(X.tags_val_bytes.p, X.tot[EXC_TAGS_VB], stream);
+  (void)ctx;
+  d2h_into(ex.size, X.size.p, n, stream);
+  d2h_into(ex.mtime, X.mtime.p, n, stream);
+  d2h_into(ex.efm, X.efm.p, n, stream);
+  d2h_into(ex.stats_null, X.stats_null.p, n, stream);
+  d2h_into(ex.pv_null, X.pv_null.p, n, stream);
+  d2h_into(ex.tags_null, X.tags_null.p, n, stream);
+  d2h_into(ex.stats_off, reinterpret_cast<const int64_t*>(X.off[EXC_STATS].p), n + 1, stream);
+  d2h_into(ex.pv_entry_off, reinterpret_cast<const int64_t*>(X.off[EXC_PV_N].p), n + 1, stream);
+  d2h_into(ex.tags_entry_off, reinterpret_cast<const int64_t*>(X.off[EXC_TAGS_N].p), n + 1, stream);
+  d2h_into(ex.stats_bytes, X.stats_bytes.p, X.tot[EXC_STATS], stream);
+  d2h_into(ex.pv_key_off, X.pv_key_off.p, X.tot[EXC_PV_N] + 1, stream);
+  d2h_into(ex.pv_val_off, X.pv_val_off.p, X.tot[EXC_PV_N] + 1, stream);
+  d2h_into(ex.pv_val_null, X.pv_val_null.p, X.tot[EXC_PV_N], stream);
+  d2h_into(ex.pv_key_bytes, X.pv_key_bytes.p, X.tot[EXC_PV_KB], stream);
+  d2h_into(ex.pv_val_bytes, X.pv_val_bytes.p, X.tot[EXC_PV_VB], stream);
+  d2h_into(ex.tags_key_off, X.tags_key_off.p, X.tot[EXC_TAGS_N] + 1, stream);
+  d2h_into(ex.tags_val_off, X.tags_val_off.p, X.tot[EXC_TAGS_N] + 1, stream);
+  d2h_into(ex.tags_val_null, X.tags_val_null.p, X.tot[EXC_TAGS_N], stream);
+  d2h_into(ex.tags_key_bytes, X.tags_key_bytes.p, X.tot[EXC_TAGS_KB], stream);
+  d2h_into(ex.tags_val_bytes, X.tags_val_bytes.p, X.tot[EXC_TAGS_VB], stream);
   ex.built = true;
 }
 
@@ -2430,9 +2465,12 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
     }
     if (!want.empty() && st.n_live) build_pv_columns(st, want);
   }
+  // only the records of this part: adds [a0, a1), removes [b0, b1) (side-relative)
+  const uint64_t a0 = std::min(NA, p0 > H ? p0 - H : 0), a1 = std::min(NA, p1 > H ? p1 - H : 0);
+  const uint64_t b0 = std::min(NR, p0 > H + NA ? p0 - H - NA : 0), b1 = std::min(NR, p1 > H + NA ? p1 - H - NA : 0);
   DevExport X[2];
-  export_device(st, DR_LIVE, X[0]);
-  export_device(st, DR_TOMBSTONES, X[1]);
+  export_device(st, DR_LIVE, X[0], a0, a1);
+  export_device(st, DR_TOMBSTONES, X[1], b0, b1);
   // ---- schema (DFS) and leaves ----
   std::vector<SElem> schema;
   std::vector<CkLeafW> leaves;
@@ -2530,15 +2568,15 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
         EncLeaf f{};
         f.def_null = 2;
         f.def_present = 3;
-        if (col) f.null = col->isnull.p;
+        if (col) f.null = col->isnull.p + a0;
         int phys = PQ_INT32, conv = -1;
         switch (pc.second) {
-          case DR_T_STRING: f.kind = ENC_STR_PTR; if (col) { f.sptr = col->sptr.p; f.slen = col->slen.p; } phys = PQ_BYTE_ARRAY; conv = PC_UTF8; break;
-          case DR_T_LONG: f.kind = ENC_I64; if (col) f.i64 = col->w64.p; phys = PQ_INT64; break;
-          case DR_T_BOOLEAN: f.kind = ENC_BOOL; if (col) f.i32 = col->w32.p; phys = PQ_BOOLEAN; break;
+          case DR_T_STRING: f.kind = ENC_STR_PTR; if (col) { f.sptr = col->sptr.p + a0; f.slen = col->slen.p + a0; } phys = PQ_BYTE_ARRAY; conv = PC_UTF8; break;
+          case DR_T_LONG: f.kind = ENC_I64; if (col) f.i64 = col->w64.p + a0; phys = PQ_INT64; break;
+          case DR_T_BOOLEAN: f.kind = ENC_BOOL; if (col) f.i32 = col->w32.p + a0; phys = PQ_BOOLEAN; break;
           default:
             f.kind = ENC_I32;
-            if (col) f.i32 = col->w32.p;
+            if (col) f.i32 = col->w32.p + a0;
             conv = pc.second == DR_T_DATE ? PC_DATE : pc.second == DR_T_BYTE ? PC_INT_8 : pc.second == DR_T_SHORT ? PC_INT_16 : -1;
         }
         leaf(pc.first, PR_OPTIONAL, phys, conv, 3, 0, 0, f);
@@ -2622,7 +2660,7 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
       std::vector<uint8_t> rep, def, vals;
       uint64_t nlev = 0;
       const int dw = level_width(L.max_def), rw = level_width(L.max_rep);
-      const uint64_t side_lo = L.side == 0 ? H : H + NA, side_n = L.side == 0 ? NA : NR;
+      const uint64_t side_lo = L.side == 0 ? H + a0 : H + NA + b0, side_n = L.side == 0 ? a1 - a0 : b1 - b0;
       const bool dev = L.side >= 0 && r0 < side_lo + side_n && r1 > side_lo;
       if (!dev) {
         std::vector<uint8_t> hd, hr;

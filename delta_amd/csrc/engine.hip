@@ -46,6 +46,8 @@ struct dr_ctx {
   hipStream_t stream2 = nullptr;  // K1 line parsing, overlapped with the checkpoint decode
   std::string err;
   bool timing = false;
+  std::string timing_only;  // non-empty: only this kernel gets an event pair (dr_set_timing_only)
+  bool timing_pending = false;
   bool overlap = false;  // DR_OVERLAP=1: K1 line parsing on stream2, beside the checkpoint decode
   struct Mark {
     std::string name;
@@ -115,12 +117,15 @@ struct dr_ctx {
     dr_ctx* c = static_cast<dr_ctx*>(user);
     if (!end) {
       KMark k{kernel_name(kernel), nullptr, nullptr};
+      c->timing_pending = c->timing_only.empty() || k.name == c->timing_only;
+      if (!c->timing_pending) return;
       HIP_OK(hipEventCreate(&k.a));
       HIP_OK(hipEventCreate(&k.b));
       HIP_OK(hipEventRecord(k.a, st));
       c->kmarks.push_back(k);
-    } else if (!c->kmarks.empty()) {
+    } else if (c->timing_pending && !c->kmarks.empty()) {
       HIP_OK(hipEventRecord(c->kmarks.back().b, st));
+      c->timing_pending = false;
     }
   }
   // "(dev::k_gather<uint64_t, uint32_t>)" -> "k_gather"
@@ -3925,6 +3930,12 @@ int dr_state_write_checkpoint(dr_state* state, int32_t part, int32_t parts, uint
 }
 
 void dr_free(void* p) { free(p); }
+
+int dr_set_timing_only(dr_ctx* ctx, const char* kernel) {
+  if (!ctx) return DR_E_INVALID_ARG;
+  ctx->timing_only = kernel ? kernel : "";
+  return DR_OK;
+}
 
 int dr_set_timing(dr_ctx* ctx, int32_t on) {
   if (!ctx) return DR_E_INVALID_ARG;

@@ -86,7 +86,9 @@ class Engine:
         if rc != N.DR_OK:
             raise DeltaError(rc, self.lib.dr_last_error(self.ctx).decode("utf-8", "replace"))
 
-    def set_timing(self, on: bool) -> None:
+    def set_timing(self, on: bool, only: Optional[str] = None) -> None:
+        """dr_set_timing (+ dr_set_timing_only: events around one kernel only)."""
+        self.check(self.lib.dr_set_timing_only(self.ctx, (only or "").encode()))
         self.check(self.lib.dr_set_timing(self.ctx, 1 if on else 0))
 
     def last_timings(self) -> Dict[str, float]:

@@ -345,6 +345,10 @@ int dr_last_timings(dr_ctx* ctx, char* names, uint64_t names_len, float* ms, int
                     int32_t* n);
 /* Enable/disable per-stage event timing (off by default; small overhead when on). */
 int dr_set_timing(dr_ctx* ctx, int32_t on);
+/* Restricts the per-kernel events of dr_set_timing to one kernel (by name, e.g. "k_snap_exec";
+ * NULL or "" = every kernel): the bench times its roofline kernel inside the timed steps without
+ * an event pair on every other launch. */
+int dr_set_timing_only(dr_ctx* ctx, const char* kernel);
 
 #ifdef __cplusplus
 }

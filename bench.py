@@ -276,7 +276,7 @@ def measure_checkpoint_write(eng, staged, cutoff, parts):
     dt = time.perf_counter() - t0
     st.release()
     return {"parts": parts, "part_rows": rows, "part_bytes": len(data), "part_s": round(dt, 4),
-            "rows_per_s": round(rows / dt, 1), "codec": "UNCOMPRESSED"}
+            "rows_per_s": round(rows / dt, 1), "codec": "SNAPPY (device)"}
 
 
 def measure_filter(eng, staged, cutoff, exp, steps):

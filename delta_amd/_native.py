@@ -20,7 +20,7 @@ STATUS = {
     16: "DR_E_CHECKSUM", 17: "DR_E_NO_CHECKSUM", 18: "DR_E_REBUILD", 19: "DR_E_FOREIGN_FILE",
 }
 DR_E_REBUILD = 18
-DR_CKPT_STATS, DR_CKPT_PARSED = 0x1, 0x2
+DR_CKPT_STATS, DR_CKPT_PARSED, DR_CKPT_SNAPPY = 0x1, 0x2, 0x4
 DR_E_FOREIGN_FILE = 19
 DR_E_CHECKSUM, DR_E_NO_CHECKSUM = 16, 17
 DR_FILE_JSON, DR_FILE_CHECKPOINT = 0, 1

@@ -2651,7 +2651,7 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
   // ---- pages ----
   std::vector<uint8_t>& f = out.file;
   f = {'P', 'A', 'R', '1'};
-  struct ChunkMeta { int64_t off, size, nval; };
+  struct ChunkMeta { int64_t off, size, usize, nval; int codec; };
   struct RG { std::vector<ChunkMeta> cols; int64_t rows, bytes; };
   std::vector<RG> rgs;
   const uint64_t rgn = rg_rows ? rg_rows : (uint64_t(1) << 20);
@@ -2662,8 +2662,9 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
     rg.rows = int64_t(r1 - r0);
     rg.bytes = 0;
     for (CkLeafW& L : leaves) {
-      std::vector<uint8_t> rep, def, vals;
-      uint64_t nlev = 0;
+      std::vector<uint8_t> rep, def, vals, dev_body;
+      uint64_t nlev = 0, dev_body_raw = 0;
+      int dev_codec = 0;
       const int dw = level_width(L.max_def), rw = level_width(L.max_rep);
       const uint64_t side_lo = L.side == 0 ? H + a0 : H + NA + b0, side_n = L.side == 0 ? a1 - a0 : b1 - b0;
       const bool dev = L.side >= 0 && r0 < side_lo + side_n && r1 > side_lo;
@@ -2704,35 +2705,74 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
         a.vals = vv.p;
         launch_enc_fill(a, stream);
         const uint64_t groups = (nlev + 7) / 8;
-        auto packed = [&](DBuf<uint8_t>& lv, int w, std::vector<uint8_t>& dst) {
-          DBuf<uint8_t> pk(ctx, groups * uint64_t(w) + 1);
-          launch_enc_pack(lv.p, nlev, w, pk.p, stream);
-          put_varint(dst, (groups << 1) | 1);
-          const std::vector<uint8_t> h = d2h(pk.p, groups * uint64_t(w), stream);
-          dst.insert(dst.end(), h.begin(), h.end());
+        DBuf<uint8_t> rpk(ctx, L.max_rep ? groups * uint64_t(rw) + 1 : 1), dpk(ctx, groups * uint64_t(dw) + 1),
+            bpk(ctx, L.phys == PQ_BOOLEAN ? (nvb + 7) / 8 + 1 : 1);
+        if (L.max_rep) launch_enc_pack(rl.p, nlev, rw, rpk.p, stream);
+        launch_enc_pack(dl.p, nlev, dw, dpk.p, stream);
+        if (L.phys == PQ_BOOLEAN) launch_enc_pack(vv.p, nvb, 1, bpk.p, stream);
+        const uint64_t vbytes = L.phys == PQ_BOOLEAN ? (nvb + 7) / 8 : nvb;
+        const uint8_t* vsrc = L.phys == PQ_BOOLEAN ? bpk.p : vv.p;
+        // the page body on the device: [u32 + rep levels] [u32 + def levels] values
+        std::vector<uint8_t> rh, dh;
+        put_varint(rh, (groups << 1) | 1);
+        put_varint(dh, (groups << 1) | 1);
+        const uint64_t rsec = L.max_rep ? rh.size() + groups * uint64_t(rw) : 0, dsec = dh.size() + groups * uint64_t(dw);
+        const uint64_t bsize = (L.max_rep ? 4 + rsec : 0) + 4 + dsec + vbytes;
+        std::vector<uint8_t> hdr_r, hdr_d;
+        if (L.max_rep) { put_u32le(hdr_r, uint32_t(rsec)); hdr_r.insert(hdr_r.end(), rh.begin(), rh.end()); }
+        put_u32le(hdr_d, uint32_t(dsec));
+        hdr_d.insert(hdr_d.end(), dh.begin(), dh.end());
+        DBuf<uint8_t> bodyd(ctx, bsize + 8);
+        uint64_t at = 0;
+        auto h2d_at = [&](const std::vector<uint8_t>& h) {
+          if (!h.empty()) HIP_OK(hipMemcpyAsync(bodyd.p + at, h.data(), h.size(), hipMemcpyHostToDevice, stream));
+          at += h.size();
         };
-        if (L.max_rep) packed(rl, rw, rep);
-        packed(dl, dw, def);
-        if (L.phys == PQ_BOOLEAN) {
-          DBuf<uint8_t> pk(ctx, (nvb + 7) / 8 + 1);
-          launch_enc_pack(vv.p, nvb, 1, pk.p, stream);
-          vals = d2h(pk.p, (nvb + 7) / 8, stream);
+        auto d2d_at = [&](const uint8_t* src, uint64_t nb) {
+          if (nb) HIP_OK(hipMemcpyAsync(bodyd.p + at, src, nb, hipMemcpyDeviceToDevice, stream));
+          at += nb;
+        };
+        if (L.max_rep) { h2d_at(hdr_r); d2d_at(rpk.p, groups * uint64_t(rw)); }
+        h2d_at(hdr_d);
+        d2d_at(dpk.p, groups * uint64_t(dw));
+        d2d_at(vsrc, vbytes);
+        dev_body_raw = bsize;
+        if (opts & DR_CKPT_SNAPPY) {
+          const uint64_t nfrag = (bsize + 65535) / 65536, slot = snap_compress_slot();
+          DBuf<uint8_t> cz(ctx, nfrag * slot + 1);
+          DBuf<uint32_t> czl(ctx, nfrag + 1);
+          launch_snap_compress(bodyd.p, bsize, cz.p, czl.p, stream);
+          const std::vector<uint32_t> fl = d2h(czl.p, nfrag, stream);
+          const std::vector<uint8_t> all = d2h(cz.p, nfrag * slot, stream);
+          put_varint(dev_body, bsize);  // the snappy preamble: uncompressed length
+          for (uint64_t k = 0; k < nfrag; ++k)
+            dev_body.insert(dev_body.end(), all.begin() + k * slot, all.begin() + k * slot + fl[k]);
+          dev_codec = 1;
         } else {
-          vals = d2h(vv.p, nvb, stream);
+          dev_body = d2h(bodyd.p, bsize, stream);
         }
       }
       if (L.phys == PQ_BOOLEAN && !dev) {  // host BOOLEAN values are bytes until packed (none are written)
         vals.clear();
       }
       std::vector<uint8_t> body;
-      if (L.max_rep) { put_u32le(body, uint32_t(rep.size())); body.insert(body.end(), rep.begin(), rep.end()); }
-      put_u32le(body, uint32_t(def.size()));
-      body.insert(body.end(), def.begin(), def.end());
-      body.insert(body.end(), vals.begin(), vals.end());
-      if (body.size() > uint64_t(INT32_MAX)) fail(DR_E_UNSUPPORTED, "checkpoint page over 2 GiB: use smaller row groups");
+      uint64_t raw;
+      int codec = 0;
+      if (dev) {
+        body.swap(dev_body);
+        raw = dev_body_raw;
+        codec = dev_codec;
+      } else {
+        if (L.max_rep) { put_u32le(body, uint32_t(rep.size())); body.insert(body.end(), rep.begin(), rep.end()); }
+        put_u32le(body, uint32_t(def.size()));
+        body.insert(body.end(), def.begin(), def.end());
+        body.insert(body.end(), vals.begin(), vals.end());
+        raw = body.size();
+      }
+      if (raw > uint64_t(INT32_MAX)) fail(DR_E_UNSUPPORTED, "checkpoint page over 2 GiB: use smaller row groups");
       ThriftW ph;
       ph.i32(1, 0);  // DATA_PAGE
-      ph.i32(2, int32_t(body.size()));
+      ph.i32(2, int32_t(raw));
       ph.i32(3, int32_t(body.size()));
       ph.begin_struct(5);
       ph.i32(1, int32_t(nlev));
@@ -2744,7 +2784,7 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
       const int64_t off = int64_t(f.size());
       f.insert(f.end(), ph.b.begin(), ph.b.end());
       f.insert(f.end(), body.begin(), body.end());
-      rg.cols.push_back(ChunkMeta{off, int64_t(ph.b.size() + body.size()), int64_t(nlev)});
+      rg.cols.push_back(ChunkMeta{off, int64_t(ph.b.size() + body.size()), int64_t(ph.b.size() + raw), int64_t(nlev), codec});
       rg.bytes += int64_t(ph.b.size() + body.size());
     }
     rgs.push_back(std::move(rg));
@@ -2779,9 +2819,9 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
       fm.elem_i32(3);  // RLE
       fm.begin_list(3, 8, L.path.size());
       for (const std::string& s : L.path) fm.elem_str(s);
-      fm.i32(4, 0);  // UNCOMPRESSED
+      fm.i32(4, m.codec);  // UNCOMPRESSED / SNAPPY
       fm.i64(5, m.nval);
-      fm.i64(6, m.size);
+      fm.i64(6, m.usize);
       fm.i64(7, m.size);
       fm.i64(9, m.off);
       fm.end_struct();

@@ -143,4 +143,90 @@ void launch_enc_pack(const uint8_t* in, uint64_t n, int width, uint8_t* out, hip
   if (groups) DR_LAUNCH(dev::k_enc_pack, dim3(unsigned((groups + dev::ENC_T - 1) / dev::ENC_T)), dim3(dev::ENC_T), 0, st, in, n, width, out);
 }
 
+// ---- SNAPPY compression (pages of the checkpoint writer) ------------------------------------------
+namespace dev {
+constexpr uint32_t SC_FRAG = 65536;
+constexpr uint32_t SC_SLOT = SC_FRAG + SC_FRAG / 6 + 64;  // worst case: all literals
+constexpr int SC_BITS = 10;                                // hash table entries per lane: 2^10
+
+__device__ __forceinline__ uint32_t ld32(const uint8_t* p) {
+  return uint32_t(p[0]) | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) | (uint32_t(p[3]) << 24);
+}
+
+__device__ uint32_t emit_literal(uint8_t* d, uint32_t o, const uint8_t* s, uint32_t n) {
+  const uint32_t m = n - 1;
+  if (m < 60) {
+    d[o++] = uint8_t(m << 2);
+  } else if (m < 256) {
+    d[o++] = uint8_t(60 << 2);
+    d[o++] = uint8_t(m);
+  } else {
+    d[o++] = uint8_t(61 << 2);
+    d[o++] = uint8_t(m);
+    d[o++] = uint8_t(m >> 8);
+  }
+  for (uint32_t k = 0; k < n; ++k) d[o + k] = s[k];
+  return o + n;
+}
+
+__device__ uint32_t emit_copy(uint8_t* d, uint32_t o, uint32_t off, uint32_t len) {
+  while (len > 0) {
+    // pieces of at most 64 bytes, never leaving fewer than 4 for a COPY_1 tail
+    uint32_t l = len > 64 ? (len - 64 < 4 ? 60 : 64) : len;
+    if (l >= 4 && l <= 11 && off < 2048) {
+      d[o++] = uint8_t(1 | ((l - 4) << 2) | ((off >> 8) << 5));
+      d[o++] = uint8_t(off);
+    } else {
+      d[o++] = uint8_t(2 | ((l - 1) << 2));
+      d[o++] = uint8_t(off);
+      d[o++] = uint8_t(off >> 8);
+    }
+    len -= l;
+  }
+  return o;
+}
+
+__global__ void __launch_bounds__(64) k_snap_compress(const uint8_t* in, uint64_t n, uint8_t* out, uint32_t* out_len,
+                                                      uint32_t nfrag) {
+  __shared__ uint16_t table[64][1 << SC_BITS];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t f = blockIdx.x * 64 + lane;
+  uint16_t* tab = table[lane];
+  for (uint32_t k = 0; k < (1u << SC_BITS); ++k) tab[k] = 0xffff;
+  if (f >= nfrag) return;
+  const uint8_t* s = in + uint64_t(f) * SC_FRAG;
+  const uint32_t len = uint32_t(min(uint64_t(SC_FRAG), n - uint64_t(f) * SC_FRAG));
+  uint8_t* d = out + uint64_t(f) * SC_SLOT;
+  uint32_t o = 0, ip = 0, lit = 0;
+  if (len >= 16) {
+    const uint32_t limit = len - 4;
+    while (ip <= limit) {
+      const uint32_t cur = ld32(s + ip);
+      const uint32_t h = (cur * 0x1e35a7bdu) >> (32 - SC_BITS);
+      const uint32_t cand = tab[h];
+      tab[h] = uint16_t(ip);
+      if (cand != 0xffffu && cand < ip && ld32(s + cand) == cur) {
+        uint32_t m = 4;
+        while (ip + m < len && s[cand + m] == s[ip + m]) ++m;
+        if (ip > lit) o = emit_literal(d, o, s + lit, ip - lit);
+        o = emit_copy(d, o, ip - cand, m);
+        ip += m;
+        lit = ip;
+      } else {
+        ++ip;
+      }
+    }
+  }
+  if (len > lit) o = emit_literal(d, o, s + lit, len - lit);
+  out_len[f] = o;
+}
+}  // namespace dev
+
+uint64_t snap_compress_slot() { return dev::SC_SLOT; }
+
+void launch_snap_compress(const uint8_t* in, uint64_t n, uint8_t* out, uint32_t* out_len, hipStream_t st) {
+  const uint32_t nfrag = uint32_t((n + dev::SC_FRAG - 1) / dev::SC_FRAG);
+  if (nfrag) DR_LAUNCH(dev::k_snap_compress, dim3((nfrag + 63) / 64), dim3(64), 0, st, in, n, out, out_len, nfrag);
+}
+
 }  // namespace dr

@@ -623,3 +623,11 @@ void launch_enc_fill(const EncArgs& a, hipStream_t st);
 // Bit-packs n one-byte values (< 2^width) in groups of 8 (RLE/bit-packing hybrid body; n padded).
 void launch_enc_pack(const uint8_t* in, uint64_t n, int width, uint8_t* out, hipStream_t st);
 }  // namespace dr
+namespace dr {
+// SNAPPY compression of `n` bytes in 64 KiB fragments, one lane per fragment (greedy hash matching
+// with a 1024-entry table per lane in LDS; copies never leave their fragment, as the reference
+// compressor's): fragment f's elements go to out + f * snap_compress_slot(), their length to
+// out_len[f].
+uint64_t snap_compress_slot();
+void launch_snap_compress(const uint8_t* in, uint64_t n, uint8_t* out, uint32_t* out_len, hipStream_t st);
+}  // namespace dr

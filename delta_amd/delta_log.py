@@ -364,13 +364,13 @@ class State:
         return res
 
     def write_checkpoint_part(self, part: int, parts: int, stats: bool = True, parsed: bool = True,
-                              row_group_rows: int = 0) -> Tuple[bytes, int]:
+                              row_group_rows: int = 0, snappy: bool = True) -> Tuple[bytes, int]:
         """dr_state_write_checkpoint: part `part` (1-based) of `parts` as Parquet bytes, the file-action
-        columns encoded on the GPU; returns (bytes, rows)."""
+        columns encoded (and SNAPPY-compressed) on the GPU; returns (bytes, rows)."""
         buf = C.POINTER(C.c_uint8)()
         n = C.c_uint64()
         rows = C.c_int64()
-        opts = (N.DR_CKPT_STATS if stats else 0) | (N.DR_CKPT_PARSED if parsed else 0)
+        opts = (N.DR_CKPT_STATS if stats else 0) | (N.DR_CKPT_PARSED if parsed else 0) | (N.DR_CKPT_SNAPPY if snappy else 0)
         with self.eng.lock:
             self.eng.check(self.eng.lib.dr_state_write_checkpoint(self.h, int(part), int(parts), opts, int(row_group_rows),
                                                                   C.byref(buf), C.byref(n), C.byref(rows)))

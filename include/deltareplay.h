@@ -262,12 +262,14 @@ void dr_free(void* p);
  * Checkpoints.writeCheckpoint / buildCheckpoint (D/Checkpoints.scala:229-365): part `part` (1-based)
  * of `parts` of the state's checkpoint -- rows protocol, metaData, txns, allFiles, tombstones
  * (dataChange=false), split into contiguous slices -- as a complete Parquet file in *bytes (freed
- * with dr_free). The file-action columns are encoded on the device; pages are uncompressed;
+ * with dr_free). The file-action columns are encoded on the device (SNAPPY-compressed on the device
+ * with DR_CKPT_SNAPPY, else uncompressed);
  * `row_group_rows` 0 = 2^20. opts: DR_CKPT_STATS writes add.stats (delta.checkpoint.writeStatsAsJson),
  * DR_CKPT_PARSED adds add.partitionValues_parsed (the partition schema's types; writeStatsAsStruct /
  * checkpointV2). The caller writes the file (temp + rename) and `_last_checkpoint`. */
 #define DR_CKPT_STATS 0x1u
 #define DR_CKPT_PARSED 0x2u
+#define DR_CKPT_SNAPPY 0x4u   /* SNAPPY pages for the device-encoded columns (Spark's default codec) */
 int dr_state_write_checkpoint(dr_state* state, int32_t part, int32_t parts, uint32_t opts, uint64_t row_group_rows,
                               uint8_t** bytes, uint64_t* len, int64_t* rows);
 

@@ -35,7 +35,7 @@ def _norm(rows):
     return rows
 
 
-def _check_state(engine, state, parts, rg):
+def _check_state(engine, state, parts, rg, snappy=True):
     from delta_amd.checkpoint import checkpoint_options, checkpoint_table
     md = next((a["metaData"] for a in state.nonfile if "metaData" in a), None)
     stats, parsed = checkpoint_options(md)
@@ -43,7 +43,7 @@ def _check_state(engine, state, parts, rg):
     got = []
     for k in range(parts):
         data, n = state.write_checkpoint_part(k + 1, parts, stats=stats, parsed=parsed is not None,
-                                              row_group_rows=rg)
+                                              row_group_rows=rg, snappy=snappy)
         rows = _rows(data)
         assert len(rows) == n
         got.extend(rows)
@@ -60,7 +60,7 @@ def test_device_checkpoint_rows_golden(engine, name):
     staged.release()
     try:
         _check_state(engine, st, 1, 0)
-        _check_state(engine, st, 2, 2)
+        _check_state(engine, st, 2, 2, snappy=False)
     finally:
         st.release()
 
@@ -76,7 +76,11 @@ def test_device_checkpoint_rows_synthetic(engine, tmp_path):
     staged.release()
     try:
         _check_state(engine, st, 1, 0)
-        _check_state(engine, st, 3, 1000)
+        _check_state(engine, st, 3, 1000, snappy=False)
+        # the pages are SNAPPY: smaller than the uncompressed ones
+        a, _ = st.write_checkpoint_part(1, 1, snappy=True)
+        b, _ = st.write_checkpoint_part(1, 1, snappy=False)
+        assert len(a) < 0.8 * len(b)
     finally:
         st.release()
 

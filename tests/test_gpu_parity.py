@@ -532,3 +532,90 @@ def test_checkpoint_writer_table_options(engine, tmp_path):
     finally:
         st.release()
     DeltaLog.clear_cache()
+
+
+def test_incremental_apply_random_commits(engine, tmp_path):
+    """Property test of the O(tail) apply: 40 random commits -- new adds, re-adds, removes of live,
+    removed and never-seen paths, the same path twice in one commit in either order, absolute /
+    `file:` / escaped paths naming the same file, metaData and txn actions, malformed lines --
+    applied one at a time (and some two at a time) with a cutoff that moves forward, checked
+    against full replays and, at the end, the oracle."""
+    import json
+    import random
+    from delta_amd import _native as N
+    rng = random.Random(0xC0FFEE)
+    lp = tmp_path / "_delta_log"
+    lp.mkdir()
+    head = ['{"protocol":{"minReaderVersion":1,"minWriterVersion":2}}',
+            '{"metaData":{"id":"t","format":{"provider":"parquet","options":{}},"schemaString":"{}",'
+            '"partitionColumns":[],"configuration":{}}}']
+    pool = ["f%d.parquet" % i for i in range(400)]
+    special = {"f7.parquet": ["/abs/f7.parquet", "file:/abs/f7.parquet", "file:///abs/f7.parquet"],
+               "f9.parquet": ["dir/f\\u00e99.parquet", "dir/fé9.parquet"]}
+    live = set()
+
+    def add(p, v, k):
+        return json.dumps({"add": {"path": p, "size": 10 + k, "modificationTime": v, "dataChange": True}},
+                          ensure_ascii=False).replace("\\\\u", "\\u")
+
+    def rm(p, ts):
+        return json.dumps({"remove": {"path": p, "deletionTimestamp": ts, "dataChange": True}},
+                          ensure_ascii=False).replace("\\\\u", "\\u")
+
+    def name(p):
+        return rng.choice(special[p]) if p in special else p
+
+    versions = []
+    lines0 = head + [add(name(p), 0, i) for i, p in enumerate(pool[:150])]
+    live.update(pool[:150])
+    versions.append(lines0)
+    for v in range(1, 41):
+        lines = []
+        for _ in range(rng.randint(1, 12)):
+            r = rng.random()
+            p = rng.choice(pool)
+            if r < 0.35:
+                lines.append(add(name(p), v, v))
+                live.add(p)
+            elif r < 0.7:
+                lines.append(rm(name(p), 1000 * v + rng.randint(0, 999)))
+                live.discard(p)
+            elif r < 0.8:  # the same path twice in one commit
+                a, b = add(name(p), v, 1), rm(name(p), 1000 * v)
+                lines.extend([a, b] if rng.random() < 0.5 else [b, a])
+            elif r < 0.87:
+                lines.append('{"txn":{"appId":"app%d","version":%d,"lastUpdated":%d}}' % (rng.randint(0, 3), v, v))
+            elif r < 0.92:
+                lines.append('{"metaData":{"id":"t","format":{"provider":"parquet","options":{}},'
+                             '"schemaString":"{}","partitionColumns":[],"configuration":{"v":"%d"}}}' % v)
+            else:
+                lines.append('{"add":{"path":"broken%d.parquet","size":1' % v)  # malformed: a null row
+        versions.append(lines)
+    for v, lines in enumerate(versions):
+        (lp / ("%020d.json" % v)).write_text("\n".join(lines) + "\n")
+
+    def commit(v):
+        return (v, N.DR_FILE_JSON, 0, (lp / ("%020d.json" % v)).read_bytes())
+
+    cut = lambda v: 1000 * v - 5000
+    st = _gpu_replay(engine, str(lp), cut(0), version=0)
+    states = [st]
+    try:
+        v = 0
+        while v < 40:
+            k = 2 if rng.random() < 0.2 and v + 2 <= 40 else 1
+            tail = engine.stage_files([commit(x) for x in range(v + 1, v + k + 1)])
+            nxt = states[-1].apply(tail, cut(v + k))
+            tail.release()
+            v += k
+            states.append(nxt)
+            if v % 5 == 0 or v > 36:
+                full = _gpu_replay(engine, str(lp), cut(v), version=v)
+                try:
+                    _same_state(nxt, full, v)
+                finally:
+                    full.release()
+        _assert_same(states[-1], O.state_reconstruction(O.get_log_segment(str(lp)), cut(40)))
+    finally:
+        for s in states:
+            s.release()

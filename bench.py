@@ -304,9 +304,9 @@ def measure_filter(eng, staged, cutoff, exp, steps):
     n = st.counts["num_files"]
     st.release()
     assert len(sel) == exp["selected"], (len(sel), exp["selected"])
-    # typed cache reads: p0 date (4 B) + p1 int (4 B) + p2 string (8 B address + 4 B length + ~3 B of
-    # value) + p3 boolean (4 B) + 4 null bytes, and a 4 B flag out per live file
-    algo = n * (4 + 4 + 15 + 4 + 4 + 4)
+    # typed cache reads: p0 date (4 B) + p1 int (4 B) + p2 string (8 B inline prefix + 4 B length: its
+    # values fit the prefix, no gather) + p3 boolean (4 B) + 4 null bytes, and a 4 B flag out per file
+    algo = n * (4 + 4 + 12 + 4 + 4 + 4)
     kname = "k_filter_leaf" if "k_filter_leaf" in ms else "k_filter_typed"
     kt = ms.get(kname)
     return {"predicate": "p0 >= DATE'2020-03-01' AND p0 < DATE'2020-06-01' AND p1 IN (1..100) AND p2 = 'w17' "

@@ -424,6 +424,7 @@ struct dr_state {
     DBuf<uint64_t> sptr;
     DBuf<uint32_t> slen;
     DBuf<uint8_t> isnull;
+    DBuf<uint64_t> s8;
   };
   std::vector<std::unique_ptr<PvCol>> pv_cols;
   std::vector<std::shared_ptr<DBuf<uint8_t>>> pv_arenas;  // unescaped string values
@@ -2080,6 +2081,21 @@ static bool leafify(const dr_predicate& p, LeafPlan& L) {
         sv.erase(std::unique(sv.begin(), sv.end()), sv.end());
         const int32_t first = int32_t(L.i64.size());
         const size_t m = str ? sv.size() : iv.size();
+        // an integer set spanning < 2^16 values: a bitmap, one word read per file instead of a
+        // binary search (pad = 1; literals [min, words, bits...])
+        if (!str && m >= 8 && uint64_t(iv.back()) - uint64_t(iv.front()) < 65536) {
+          const uint64_t span = uint64_t(iv.back()) - uint64_t(iv.front()) + 1, nw = (span + 63) / 64;
+          std::vector<uint64_t> bits(nw, 0);
+          for (int64_t x : iv) {
+            const uint64_t d = uint64_t(x) - uint64_t(iv.front());
+            bits[d >> 6] |= uint64_t(1) << (d & 63);
+          }
+          L.i64.push_back(iv.front());
+          L.i64.push_back(int64_t(nw));
+          for (uint64_t w : bits) L.i64.push_back(int64_t(w));
+          L.str.resize(L.i64.size());
+          return push_leaf(FilterLeaf{c, DR_OP_IN, first, int32_t(m), has_null ? 1 : 0, 1});
+        }
         for (size_t q = 0; q < m; ++q) {
           L.i64.push_back(str ? 0 : iv[q]);
           L.str.push_back(str ? sv[q] : std::string());
@@ -2186,8 +2202,10 @@ static void build_pv_columns(dr_state& st, const std::vector<std::pair<std::stri
     if (col->type == DR_T_STRING) {
       col->sptr = DBuf<uint64_t>(ctx, n);
       col->slen = DBuf<uint32_t>(ctx, n);
+      col->s8 = DBuf<uint64_t>(ctx, n);
       pc.sptr = col->sptr.p;
       pc.slen = col->slen.p;
+      pc.s8 = col->s8.p;
     } else if (col->type == DR_T_LONG) {
       col->w64 = DBuf<int64_t>(ctx, n);
       pc.w64 = col->w64.p;
@@ -2738,7 +2756,7 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
         d2d_at(vsrc, vbytes);
         dev_body_raw = bsize;
         if (opts & DR_CKPT_SNAPPY) {
-          const uint64_t nfrag = (bsize + 65535) / 65536, slot = snap_compress_slot();
+          const uint64_t frag = 8192, nfrag = (bsize + frag - 1) / frag, slot = snap_compress_slot();
           DBuf<uint8_t> cz(ctx, nfrag * slot + 1);
           DBuf<uint32_t> czl(ctx, nfrag + 1);
           launch_snap_compress(bodyd.p, bsize, cz.p, czl.p, stream);
@@ -2869,7 +2887,7 @@ static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred)
       fa.cols[c].type = pred.col_types[c];
       continue;
     }
-    fa.cols[c] = PvColumn{col->type, col->w32.p, col->w64.p, col->sptr.p, col->slen.p, col->isnull.p};
+    fa.cols[c] = PvColumn{col->type, col->w32.p, col->w64.p, col->sptr.p, col->slen.p, col->isnull.p, col->s8.p};
   }
   LeafPlan lp;
   const bool force_generic = std::getenv("DR_FILTER_GENERIC") != nullptr;  // test hook: k_filter_typed
@@ -2877,12 +2895,15 @@ static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred)
     FilterLeafArgs la{};
     la.n_live = st.n_live;
     for (int32_t c = 0; c < pred.ncols; ++c) la.cols[c] = fa.cols[c];
-    std::vector<uint64_t> soff(lp.str.size() + 1, 0);
+    std::vector<uint64_t> soff(lp.str.size() + 1, 0), s8(lp.str.size() + 1, 0);
     std::string sbytes;
     for (size_t q = 0; q < lp.str.size(); ++q) {
       sbytes += lp.str[q];
       soff[q + 1] = sbytes.size();
+      for (size_t k = 0; k < 8; ++k) s8[q] = (s8[q] << 8) | (k < lp.str[q].size() ? uint8_t(lp.str[q][k]) : 0u);
     }
+    DBuf<uint64_t> d_s8 = upload(ctx, s8.data(), s8.size());
+    la.lit_s8 = d_s8.p;
     DBuf<FilterLeaf> d_leaves = upload(ctx, lp.leaves.data(), lp.leaves.size());
     DBuf<int32_t> d_prog = upload(ctx, lp.prog.data(), lp.prog.size());
     DBuf<int64_t> d_i64 = upload(ctx, lp.i64.data(), lp.i64.size());
@@ -2894,6 +2915,8 @@ static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred)
     la.lit_i64 = d_i64.p;
     la.lit_str_off = d_soff.p;
     la.lit_str = d_sb.p;
+    la.n_i64 = int32_t(lp.i64.size());
+    la.n_str = int32_t(lp.str.size());
     DBuf<uint32_t> flag(ctx, st.n_live);
     la.flag = flag.p;
     launch_filter_leaf(la, stream);

@@ -145,9 +145,11 @@ void launch_enc_pack(const uint8_t* in, uint64_t n, int width, uint8_t* out, hip
 
 // ---- SNAPPY compression (pages of the checkpoint writer) ------------------------------------------
 namespace dev {
-constexpr uint32_t SC_FRAG = 65536;
+// 8 KiB fragments (inside the reader's 64 KiB blocks, so its fragment rule holds): a 1M-row part's
+// pages give ~37K lanes instead of ~4.6K, and the lane-serial parse is 8x shorter.
+constexpr uint32_t SC_FRAG = 8192;
 constexpr uint32_t SC_SLOT = SC_FRAG + SC_FRAG / 6 + 64;  // worst case: all literals
-constexpr int SC_BITS = 10;                                // hash table entries per lane: 2^10
+constexpr int SC_BITS = 9;                                 // hash table entries per lane: 2^9 (1 KiB)
 
 __device__ __forceinline__ uint32_t ld32(const uint8_t* p) {
   return uint32_t(p[0]) | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) | (uint32_t(p[3]) << 24);

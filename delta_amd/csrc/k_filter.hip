@@ -331,6 +331,9 @@ __global__ void __launch_bounds__(256) k_pv_extract(PvExtractArgs a) {
     if (col.type == DR_T_STRING) {
       col.sptr[i] = reinterpret_cast<uint64_t>(v.s);
       col.slen[i] = v.n;
+      uint64_t s8 = 0;
+      for (uint32_t k = 0; k < 8; ++k) s8 = (s8 << 8) | (k < v.n && !v.null ? v.s[k] : 0u);
+      if (col.s8) col.s8[i] = s8;
     } else if (col.type == DR_T_LONG) {
       col.w64[i] = v.v;
     } else {
@@ -470,7 +473,8 @@ __device__ __forceinline__ int bytes_cmp(const uint8_t* a, uint32_t an, const ui
   return an == bn ? 0 : (an < bn ? -1 : 1);
 }
 
-__device__ __forceinline__ uint32_t eval_leaf(const FilterLeafArgs& a, const FilterLeaf& L, uint64_t i) {
+__device__ __forceinline__ uint32_t eval_leaf(const FilterLeafArgs& a, const FilterLeaf& L, uint64_t i,
+                                              const int64_t* lit_i64, const uint64_t* lit_s8) {
   const PvColumn& col = a.cols[L.col];
   const bool vnull = col.isnull[i] != 0;
   if (L.op == DR_OP_ISNULL) return vnull ? 1u : 0u;
@@ -479,23 +483,35 @@ __device__ __forceinline__ uint32_t eval_leaf(const FilterLeafArgs& a, const Fil
   if (L.op != DR_OP_IN && L.lit_null) return 2u;
   if (vnull) return 2u;
   const bool str = col.type == DR_T_STRING;
-  const uint8_t* vs = nullptr;
   uint32_t vn = 0;
+  uint64_t v8 = 0;
   int64_t v = 0;
   if (str) {
-    vs = reinterpret_cast<const uint8_t*>(col.sptr[i]);
     vn = col.slen[i];
+    v8 = col.s8[i];
   } else {
     v = col.type == DR_T_LONG ? col.w64[i] : int64_t(int32_t(col.w32[i]));
   }
+  // strings: the big-endian 8-byte prefixes order like the bytes; equal prefixes of two values of
+  // at most 8 bytes leave only the lengths; otherwise the value bytes are gathered
   auto cmp_lit = [&](int32_t k) -> int {
     if (str) {
       const uint64_t o = a.lit_str_off[k];
-      return bytes_cmp(vs, vn, a.lit_str + o, uint32_t(a.lit_str_off[k + 1] - o));
+      const uint32_t ln = uint32_t(a.lit_str_off[k + 1] - o);
+      const uint64_t l8 = lit_s8[k];
+      if (v8 != l8) return v8 < l8 ? -1 : 1;
+      if (vn <= 8 && ln <= 8) return vn == ln ? 0 : (vn < ln ? -1 : 1);
+      return bytes_cmp(reinterpret_cast<const uint8_t*>(col.sptr[i]), vn, a.lit_str + o, ln);
     }
-    const int64_t x = a.lit_i64[k];
+    const int64_t x = lit_i64[k];
     return v == x ? 0 : (v < x ? -1 : 1);
   };
+  if (L.op == DR_OP_IN && L.pad == 1) {  // an integer set as a bitmap over [min, min + 64 * words)
+    const uint64_t d = uint64_t(v) - uint64_t(lit_i64[L.lit]);
+    const uint64_t nbits = uint64_t(lit_i64[L.lit + 1]) * 64;
+    if (d < nbits && ((uint64_t(lit_i64[L.lit + 2 + (d >> 6)]) >> (d & 63)) & 1u)) return 1u;
+    return L.lit_null ? 2u : 0u;
+  }
   if (L.op == DR_OP_IN) {  // binary search of the sorted set
     int32_t lo = L.lit, hi = L.lit + L.nlit;
     while (lo < hi) {
@@ -520,11 +536,14 @@ __device__ __forceinline__ uint32_t eval_leaf(const FilterLeafArgs& a, const Fil
 __global__ void __launch_bounds__(256) k_filter_leaf(FilterLeafArgs a) {
   const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= a.n_live) return;
+  const int64_t* li = a.lit_i64;
+  const uint64_t* ls = a.lit_s8;
+  {
   uint64_t stk = 0;  // 2 bits per entry, top at the low end
   for (int k = 0; k < a.nprog; ++k) {
     const int op = a.prog[2 * k];
     if (op == LEAF_OP_LEAF) {
-      stk = (stk << 2) | eval_leaf(a, a.leaves[a.prog[2 * k + 1]], i);
+      stk = (stk << 2) | eval_leaf(a, a.leaves[a.prog[2 * k + 1]], i, li, ls);
     } else if (op == LEAF_OP_NOT) {
       const uint64_t x = stk & 3u;
       stk = (stk & ~3ull) | (x == 2u ? 2u : (x ^ 1u));
@@ -537,6 +556,7 @@ __global__ void __launch_bounds__(256) k_filter_leaf(FilterLeafArgs a) {
     }
   }
   a.flag[i] = (stk & 3u) == 1u ? 1u : 0u;
+  }
 }
 
 // checkpoint map column: row_start[k] = index of the k-th entry with repetition level 0

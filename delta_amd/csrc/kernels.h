@@ -336,6 +336,7 @@ struct PvColumn {
   uint64_t* sptr;      // STRING: address of the (unescaped) value bytes
   uint32_t* slen;
   uint8_t* isnull;     // 1: NULL (absent, JSON null, or a failed non-ANSI cast)
+  uint64_t* s8;        // STRING: the first 8 bytes, big-endian, zero-padded (compared without a gather)
 };
 struct PvExtractArgs {
   const uint32_t* live;          // live AddFile action indices (export order)
@@ -394,7 +395,7 @@ struct FilterLeaf {
   int32_t lit;       // literal index (comparisons) or first entry of the sorted set (IN)
   int32_t nlit;      // IN: entries in the set
   int32_t lit_null;  // comparisons: the literal is NULL; IN: the list holds a NULL
-  int32_t pad;
+  int32_t pad;       // IN over integers: 1 = a bitmap (literals [min, words, bits...])
 };
 enum : int32_t { LEAF_OP_LEAF = 0, LEAF_OP_AND = 1, LEAF_OP_OR = 2, LEAF_OP_NOT = 3 };
 struct FilterLeafArgs {
@@ -406,6 +407,8 @@ struct FilterLeafArgs {
   const int64_t* lit_i64;        // comparison literals, then the IN sets (sorted ascending)
   const uint64_t* lit_str_off;   // string literals / sets (sorted bytewise), offsets into lit_str
   const uint8_t* lit_str;
+  const uint64_t* lit_s8;        // per string literal: its first 8 bytes as PvColumn::s8
+  int32_t n_i64, n_str;          // literal counts
   uint32_t* flag;
 };
 void launch_filter_leaf(const FilterLeafArgs& a, hipStream_t st);
@@ -624,9 +627,8 @@ void launch_enc_fill(const EncArgs& a, hipStream_t st);
 void launch_enc_pack(const uint8_t* in, uint64_t n, int width, uint8_t* out, hipStream_t st);
 }  // namespace dr
 namespace dr {
-// SNAPPY compression of `n` bytes in 64 KiB fragments, one lane per fragment (greedy hash matching
-// with a 1024-entry table per lane in LDS; copies never leave their fragment, as the reference
-// compressor's): fragment f's elements go to out + f * snap_compress_slot(), their length to
+// SNAPPY compression of `n` bytes in 8 KiB fragments, one lane per fragment (greedy hash matching
+// with a 512-entry table per lane in LDS; copies never leave their fragment): fragment f's elements go to out + f * snap_compress_slot(), their length to
 // out_len[f].
 uint64_t snap_compress_slot();
 void launch_snap_compress(const uint8_t* in, uint64_t n, uint8_t* out, uint32_t* out_len, hipStream_t st);

@@ -27,7 +27,13 @@ def main():
     else:
         import torch
         local = int(os.environ.get("LOCAL_RANK", "0"))
-        dist.init_process_group(os.environ.get("DR_TEST_BACKEND", "gloo"))
+        be = os.environ.get("DR_TEST_BACKEND", "gloo")
+        if be == "nccl":  # RCCL: one GPU per rank
+            dev = local % max(torch.cuda.device_count(), 1)
+            torch.cuda.set_device(dev)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(be)
         from delta_amd.delta_log import Engine
         from delta_amd.sharded import stage_shard
         ex = Exchange()

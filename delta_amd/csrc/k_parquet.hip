@@ -246,11 +246,80 @@ __device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* red) {
   return s;
 }
 
+// The tile's bytes (+ a margin for the successors of its last candidates) staged in LDS with
+// coalesced 16-byte loads: every candidate check reads the length at the candidate and at its
+// successor, two dependent reads that went to L1/L2 (the kernel waited on memory 73 % of its wave
+// cycles, PMC r02).
+constexpr uint32_t BA_MARGIN = 4096;
+struct BaStage {
+  const uint32_t* w;  // staged words; byte k = region offset t0 + k
+  int64_t t0;
+  uint64_t n;         // staged bytes
+};
+__device__ __forceinline__ uint32_t stage_u32(const BaStage& st, uint64_t k) {  // bytes k .. k+3
+  const uint32_t i = uint32_t(k >> 2), sh = uint32_t(k & 3);
+  return __builtin_amdgcn_alignbyte(st.w[i + 1], st.w[i], sh);
+}
+__device__ __forceinline__ uint8_t stage_u8(const BaStage& st, uint64_t k) {
+  return uint8_t(st.w[k >> 2] >> (8 * (k & 3)));
+}
+__device__ __forceinline__ bool ba_cand_st(const uint8_t* b, uint64_t S, uint64_t p, uint64_t* next, const BaStage& st) {
+  if (p + 4 > S) return false;
+  const uint64_t k = uint64_t(int64_t(p) - st.t0);
+  const bool in = k + 8 <= st.n;
+  const uint32_t w = in ? stage_u32(st, k) : load_u32(b + p);
+  if (w >> 16) return false;  // bytes +2/+3 must be zero
+  const uint64_t nx = p + 4 + w;
+  if (nx > S || (w && !(in ? stage_u8(st, k + 4) : b[p + 4]))) return false;
+  *next = nx;
+  return true;
+}
+__device__ __forceinline__ uint64_t ba_kept_st(const uint8_t* b, uint64_t S, int64_t q0, const BaStage& st) {
+  if (q0 + int64_t(BA_POS) <= 0 || q0 >= int64_t(S)) return 0ull;
+  const uint4* a4 = reinterpret_cast<const uint4*>(st.w) + (q0 - st.t0) / 16;
+  uint64_t z0 = 0;
+  uint32_t z1 = 0;
+#pragma unroll
+  for (int v = 0; v < 5; ++v) {
+    const uint4 x = a4[v];
+    const uint32_t m = zero_nibble(x.x) | (zero_nibble(x.y) << 4) | (zero_nibble(x.z) << 8) | (zero_nibble(x.w) << 12);
+    if (v < 4) z0 |= uint64_t(m) << (16 * v);
+    else z1 = m;
+  }
+  auto zs = [&](int k) { return (z0 >> k) | (uint64_t(z1) << (64 - k)); };
+  const uint64_t cm = zs(2) & zs(3) & (~zs(4) | (z0 & zs(1)));
+  uint64_t kept = 0;
+  for (uint64_t m = cm; m;) {
+    const int j = __builtin_ctzll(m);
+    m &= m - 1;
+    const int64_t p = q0 + j;
+    if (p < 0) continue;
+    uint64_t nx, nn;
+    if (ba_cand_st(b, S, uint64_t(p), &nx, st) && (nx == S || ba_cand_st(b, S, nx, &nn, st))) kept |= 1ull << j;
+  }
+  return kept;
+}
+
 // T1: kept candidates per tile; each thread's 64-bit kept mask is stored for T2.
 __global__ void __launch_bounds__(BA_T) k_ba_count(ParquetArgs a) {
   __shared__ uint32_t red[BA_T / 64];
+  __shared__ __attribute__((aligned(16))) uint32_t stw[(BA_TILE + BA_MARGIN) / 4 + 8];
   const BaTile tl = ba_tile(a, blockIdx.x);
-  const uint64_t km = tl.ok ? ba_kept(tl.b, tl.S, tl.q0) : 0ull;
+  // stage [t0, t0 + staged) of the region: t0 = thread 0's first position (16-byte aligned in
+  // absolute address), up to the region end + 16 (the arena pads every page body by 16 bytes)
+  BaStage st{stw, tl.q0 - int64_t(BA_POS) * int64_t(threadIdx.x), 0};
+  if (tl.ok) {
+    const int64_t hi = min(st.t0 + int64_t(BA_TILE + BA_MARGIN), int64_t(tl.S) + 16);
+    const uint64_t nb = hi > st.t0 ? uint64_t(hi - st.t0) & ~uint64_t(15) : 0;
+    const uint4* g4 = reinterpret_cast<const uint4*>(tl.b + st.t0);
+    uint4* s4 = reinterpret_cast<uint4*>(stw);
+    for (uint32_t v = threadIdx.x; v < nb / 16; v += BA_T) s4[v] = g4[v];
+    st.n = nb;
+  }
+  __syncthreads();
+  const uint64_t km = tl.ok ? (st.n >= uint64_t(tl.q0 - st.t0) + 80 ? ba_kept_st(tl.b, tl.S, tl.q0, st)
+                                                                    : ba_kept(tl.b, tl.S, tl.q0))
+                            : 0ull;
   a.ba_kept[uint64_t(blockIdx.x) * BA_T + threadIdx.x] = km;
   const uint32_t s = block_sum(uint32_t(__builtin_popcountll(km)), red);
   if (threadIdx.x == 0) {

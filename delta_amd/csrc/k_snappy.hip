@@ -484,10 +484,10 @@ __global__ void __launch_bounds__(2 * WG_CHUNKS) k_snap_emit(SnappyArgs a) {
 //  2. pointer jumping until every byte points at its literal origin (chains of copies of copies
 //     are as long as the number of repeated path prefixes in the fragment; log2 rounds; a byte
 //     leaves its thread's pending mask once it points at a root);
-//  3. each thread keeps the roots of its 64 contiguous bytes in registers; the LDS is reused as the
+//  3. each thread keeps the roots of its 16 4-byte groups in registers; the LDS is reused as the
 //     block's bytes (lower half) and its compressed input range (upper half, 16-byte loads);
 //     literal runs are copied LDS -> LDS;
-//  4. each thread gathers its 64 bytes from their roots and stores them with 16-byte stores.
+//  4. each thread gathers its groups' bytes from their roots and stores them (coalesced dwords).
 constexpr int EXEC_T = 1024;
 constexpr uint32_t EXEC_LONG = 256;          // literal records copied by the whole workgroup
 #ifndef DR_EXEC_RPT
@@ -584,9 +584,8 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
   //    read is an ancestor of the byte (older or newer, both valid) and ancestors have smaller
   //    indices, so each step strictly moves towards the root (literal bytes are their own roots).
   //    Pointers are read 8 at a time so the LDS reads are in flight together.
-  uint32_t root[32];  // roots of this thread's 64 contiguous output bytes, two u16 per register
+  uint32_t xp[32];    // current pointers of the 4-byte groups, two u16 per register; roots at the end
   {
-    uint32_t xp[32];    // current pointers of the 4-byte groups, two u16 per register
     uint32_t act = 0;   // groups with a byte not yet at its root
 #pragma unroll
     for (uint32_t j = 0; j < 16; ++j) {
@@ -634,18 +633,6 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
           }
         }
       }
-    }
-  }
-  __syncthreads();
-  // roots of this thread's 64 contiguous output bytes -> registers (every moved pointer was
-  // written back, so the map holds final roots)
-  const uint32_t my0 = uint32_t(t) * 64;
-  {
-    const uint4* s4 = reinterpret_cast<const uint4*>(src) + my0 / 8;
-#pragma unroll
-    for (int v = 0; v < 8; ++v) {
-      const uint4 x = my0 < nbytes ? s4[v] : make_uint4(0, 0, 0, 0);
-      root[4 * v] = x.x; root[4 * v + 1] = x.y; root[4 * v + 2] = x.z; root[4 * v + 3] = x.w;
     }
   }
   __syncthreads();
@@ -718,23 +705,27 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     if (t == 0) atomicOr(&a.pages_bad[p], 64u);
     return;
   }
-  // 4. gather and store (16-byte stores)
-  if (my0 >= nbytes) return;
+  // 4. gather and store: the thread's 4-byte groups are the ones it resolved (roots still in
+  //    registers); a wave's 64 groups are 256 contiguous bytes, so literal bytes (their own roots)
+  //    and runs of one copy read consecutive LDS banks, and the dword stores coalesce
+  uint8_t* dst = out + bs;
   uint32_t word[16];
 #pragma unroll
-  for (int v = 0; v < 16; ++v) {
-    const uint32_t r01 = root[2 * v], r23 = root[2 * v + 1];
-    word[v] = uint32_t(bytes[r01 & 0xffffu]) | (uint32_t(bytes[r01 >> 16]) << 8) |
+  for (uint32_t j = 0; j < 16; ++j) {  // groups past the block end hold the identity (in the LDS)
+    const uint32_t r01 = xp[2 * j], r23 = xp[2 * j + 1];
+    word[j] = uint32_t(bytes[r01 & 0xffffu]) | (uint32_t(bytes[r01 >> 16]) << 8) |
               (uint32_t(bytes[r23 & 0xffffu]) << 16) | (uint32_t(bytes[r23 >> 16]) << 24);
   }
-  uint8_t* dst = out + bs + my0;
-  if (my0 + 64 <= nbytes && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0)) {
-    uint4* d4 = reinterpret_cast<uint4*>(dst);
+  if ((reinterpret_cast<uintptr_t>(dst) & 3) == 0 && nbytes == SNAP_BLOCK) {  // block-uniform
 #pragma unroll
-    for (int v = 0; v < 4; ++v) d4[v] = make_uint4(word[4 * v], word[4 * v + 1], word[4 * v + 2], word[4 * v + 3]);
-  } else {
-    const uint32_t m = min(64u, nbytes - my0);
-    for (uint32_t i = 0; i < m; ++i) dst[i] = uint8_t(word[i >> 2] >> (8 * (i & 3)));
+    for (uint32_t j = 0; j < 16; ++j) *reinterpret_cast<uint32_t*>(dst + 4 * (uint32_t(t) + EXEC_T * j)) = word[j];
+  } else {  // a page's last block: bytes back to the LDS, then byte stores
+    __syncthreads();
+    uint32_t* b32 = reinterpret_cast<uint32_t*>(src);
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) b32[uint32_t(t) + EXEC_T * j] = word[j];
+    __syncthreads();
+    for (uint32_t i = t; i < nbytes; i += EXEC_T) dst[i] = bytes[i];
   }
   stamp(7);
 }

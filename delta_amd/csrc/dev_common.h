@@ -21,7 +21,7 @@ __device__ __forceinline__ uint32_t ld_u32a(const uint8_t* p) {  // aligned dwor
 }
 __device__ __forceinline__ uint64_t load_u64(const uint8_t* p) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  const uint8_t* b = reinterpret_cast<const uint8_t*>(a & ~uintptr_t(3));
+  const uint8_t* b = p - (a & 3u);  // pointer arithmetic, not an integer round trip: an LDS pointer stays one
   const uint32_t sh = uint32_t(a & 3);
   const uint32_t w0 = ld_u32a(b), w1 = ld_u32a(b + 4), w2 = ld_u32a(b + 8);
   const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
@@ -30,7 +30,7 @@ __device__ __forceinline__ uint64_t load_u64(const uint8_t* p) {
 }
 __device__ __forceinline__ uint32_t load_u32(const uint8_t* p) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  const uint8_t* b = reinterpret_cast<const uint8_t*>(a & ~uintptr_t(3));
+  const uint8_t* b = p - (a & 3u);
   return __builtin_amdgcn_alignbyte(ld_u32a(b + 4), ld_u32a(b), uint32_t(a & 3));
 }
 

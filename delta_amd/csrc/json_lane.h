@@ -190,7 +190,7 @@ constexpr uint32_t TOK_MAX_SCALAR = 4095;
 JL_HD void load20(const uint8_t* s, uint32_t n, uint32_t w[5]) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uintptr_t a = reinterpret_cast<uintptr_t>(s);
-  const uint4* b = reinterpret_cast<const uint4*>(a & ~uintptr_t(15));
+  const uint4* b = reinterpret_cast<const uint4*>(s - (a & 15u));  // pointer arithmetic keeps an LDS address space
   const uint4 x = b[0], y = b[1], z = b[2];
   const uint32_t v[12] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w, z.x, z.y, z.z, z.w};
   const uint32_t q = uint32_t(a >> 2) & 3u, r = uint32_t(a) & 3u;
@@ -752,7 +752,7 @@ JL_HD void parse_line_t(const uint8_t* p, uint32_t n, LineOut& out) {
     if (!General) { out = LineOut{0, 0, 1, 0, 0, 0, 0}; return; }
   }
   const uintptr_t pa = reinterpret_cast<uintptr_t>(p);
-  const uint8_t* base = reinterpret_cast<const uint8_t*>(pa & ~uintptr_t(15));
+  const uint8_t* base = p - (pa & 15u);
   const uint32_t o0 = uint32_t(pa & 15);
   const uint32_t nwin = (o0 + n + 15) >> 4;
   auto step = [&](uint32_t t) {

@@ -456,23 +456,25 @@ __global__ void __launch_bounds__(2 * WG_CHUNKS) k_snap_emit(SnappyArgs a) {
     }
     bool bad = false;
     while (pos < ce) {
-      const Elem el = snap_decode(staged_u64(buf, s, pos));
-      if (o + el.len > pg.n_out || el.len == 0 || el.len > SNAP_BLOCK ||
-          (o >> 16) != ((o + el.len - 1) >> 16)) { bad = true; break; }
-      if ((o & (SNAP_BLOCK - 1)) == 0) a.block_rec[pg.block_base + uint32_t(o >> 16)] = rec;
-      uint32_t src;
-      if (el.off == 0) {
-        if (pos + el.hdr + el.len > pg.n_in || pos + el.hdr >= REC_LIT) { bad = true; break; }
-        src = REC_LIT | uint32_t(pos + el.hdr);
-      } else {
-        if (el.off > (o & (SNAP_BLOCK - 1))) { bad = true; break; }  // a copy reaching before its fragment
-        src = el.off;
-      }
-      const uint64_t r = (o & (SNAP_BLOCK - 1)) | (uint64_t(el.len - 1) << 16) | (uint64_t(src) << 32);
-      a.recs[rec] = r;
+      // branch-free decode (the lanes' element types differ; a switch serialises them)
+      const uint64_t w = staged_u64(buf, s, pos);
+      uint32_t adv, len;
+      snap_step(w, &adv, &len);
+      const uint32_t tag = uint32_t(w & 0xff), t = tag & 3u;
+      const bool lit = t == 0;
+      const uint32_t w8 = uint32_t(w >> 8);
+      const uint32_t off = t == 1 ? (((tag >> 5) << 8) | (w8 & 0xffu)) : t == 2 ? (w8 & 0xffffu) : w8;
+      const uint64_t ip = pos + (adv - (lit ? len : 0u));  // a literal's first input byte
+      const uint32_t orel = uint32_t(o & (SNAP_BLOCK - 1));
+      bad = len == 0 || len > SNAP_BLOCK || o + len > pg.n_out || orel + len > SNAP_BLOCK ||
+            (lit ? (ip + len > pg.n_in || ip >= REC_LIT) : (off == 0 || off > orel));  // a copy reaching before its fragment
+      if (bad) break;
+      if (orel == 0) a.block_rec[pg.block_base + uint32_t(o >> 16)] = rec;
+      const uint32_t src = lit ? (REC_LIT | uint32_t(ip)) : off;
+      a.recs[rec] = orel | (uint64_t(len - 1) << 16) | (uint64_t(src) << 32);
       ++rec;
-      o += el.len;
-      pos += snap_adv(el);
+      o += len;
+      pos += lit ? uint64_t(ip - pos) + len : adv;
     }
     if (bad) atomicOr(&a.pages_bad[g.p], 8u);
   }
@@ -741,11 +743,11 @@ __global__ void k_snap_serial(SnappyArgs a) {
   while (ip < pg.n_in) {
     const Elem el = snap_elem(in + ip);
     if (op + el.len > pg.n_out) { atomicCAS(a.error, 0u, 1u); return; }
-    if (el.off == 0) {
+    if ((in[ip] & 3u) == 0) {  // literal (a copy with offset 0 is corrupt, below)
       if (ip + el.hdr + el.len > pg.n_in) { atomicCAS(a.error, 0u, 1u); return; }
       for (uint32_t i = 0; i < el.len; ++i) out[op + i] = in[ip + el.hdr + i];
     } else {
-      if (el.off > op) { atomicCAS(a.error, 0u, 1u); return; }
+      if (el.off == 0 || el.off > op) { atomicCAS(a.error, 0u, 1u); return; }
       for (uint32_t i = 0; i < el.len; ++i) out[op + i] = out[op - el.off + i];
     }
     op += el.len;

@@ -191,8 +191,10 @@ def test_checkpoint_page_layouts(engine, tmp_path, page_size, compression, page_
         st.release()
 
 
-def test_corrupt_checkpoint_page_is_an_error(engine, tmp_path):
-    """A SNAPPY page body overwritten with copy elements reaching before the page start cannot be
+@pytest.mark.parametrize("fill", [b"\xff" * 256, b"\x01\x00" * 128], ids=["offset_past_start", "offset_zero"])
+def test_corrupt_checkpoint_page_is_an_error(engine, tmp_path, fill):
+    """A SNAPPY page body overwritten with copy elements reaching before the page start, or with
+    copies of offset 0 (corrupt in SNAPPY's format; the host decoder rejects them too), cannot be
     decoded: the replay fails with DR_E_PARQUET (the reference's Parquet reader throws), it does not
     return a partial state."""
     import pyarrow.parquet as pq
@@ -208,7 +210,7 @@ def test_corrupt_checkpoint_page_is_an_error(engine, tmp_path):
     assert col.compression == "SNAPPY" and col.total_compressed_size > 4096
     raw = bytearray(open(fn, "rb").read())
     at = col.data_page_offset + 512  # past the page header and the snappy length preamble
-    raw[at:at + 256] = b"\xff" * 256  # copy-4 elements with offset 0xffffffff
+    raw[at:at + 256] = fill  # copy-4 elements with offset 0xffffffff / copy-1 elements with offset 0
     with open(fn, "wb") as f:
         f.write(bytes(raw))
     with pytest.raises(DeltaError) as ei:

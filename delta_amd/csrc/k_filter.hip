@@ -609,13 +609,11 @@ __device__ bool json_int64(const uint8_t* p, const uint8_t* e, int64_t* out) {
   if (p < e && *p == '-') { neg = true; ++p; }
   if (p >= e || *p < '0' || *p > '9') return false;
   uint64_t v = 0;
-  int nd = 0;
   while (p < e && *p >= '0' && *p <= '9') {
     const uint64_t d = uint64_t(*p - '0');
     if (v > (uint64_t(INT64_MAX) + (neg ? 1 : 0) - d) / 10) return false;
     v = v * 10 + d;
     ++p;
-    ++nd;
   }
   if (p < e && (*p == '.' || *p == 'e' || *p == 'E')) return false;
   *out = neg ? int64_t(0 - v) : int64_t(v);

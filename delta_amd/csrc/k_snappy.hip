@@ -151,56 +151,72 @@ __device__ __forceinline__ WgInfo wg_info(const SnappyArgs& a) {
   return WgInfo{p, j0, min(WG_CHUNKS, nc - j0)};
 }
 
-// A: speculative parse.
+// A: speculative parse, one lane per chunk. (Two chunks interleaved per lane, to overlap two chains
+// of dependent LDS reads, measured 6x slower at half the lanes per workgroup: r02.)
+struct SpecChain {
+  // visited bitmap in registers (statically indexed: each step ORs its bit into the selected word
+  // with selects, so the walk issues no LDS read-modify-write of its own)
+  uint32_t lv[SNAP_CH / 32];
+  uint64_t pos, cs, ce, first, out, mid;
+  uint32_t elems, hout, helems;
+};
+// A chunk past the workgroup's (not live) gets an empty walk parked at `park`, a staged position,
+// so the unconditional header read of the step loop stays inside the stage.
+__device__ __forceinline__ void spec_init(SpecChain& w, uint32_t j, uint64_t n_in, bool live, uint64_t park) {
+#pragma unroll
+  for (int k = 0; k < int(SNAP_CH / 32); ++k) w.lv[k] = 0;
+  w.cs = uint64_t(j) * SNAP_CH;
+  w.ce = live ? min(w.cs + SNAP_CH, n_in) : park;
+  w.pos = !live ? park : w.cs >= SNAP_WU ? w.cs - SNAP_WU : 0;
+  w.first = ~0ull;
+  w.out = 0;
+  w.mid = ~0ull;
+  w.elems = w.hout = w.helems = 0;
+}
+// One element of the walk from its header word `hw` (only when w.pos < w.ce).
+__device__ __forceinline__ void spec_step(SpecChain& w, uint64_t hw) {
+  uint32_t adv, len;
+  snap_step(hw, &adv, &len);
+  if (w.pos >= w.cs) {
+    const uint32_t r = uint32_t(w.pos - w.cs);
+    const uint32_t wi = r >> 5, bit = 1u << (r & 31);
+#pragma unroll
+    for (int k = 0; k < int(SNAP_CH / 32); ++k) w.lv[k] |= wi == uint32_t(k) ? bit : 0u;
+    if (w.first == ~0ull) w.first = w.pos;
+    w.out += len;
+    ++w.elems;
+    const bool h = w.pos < w.cs + SNAP_CH / 2;
+    w.hout += h ? len : 0u;
+    w.helems += h ? 1u : 0u;
+    w.mid = (!h && w.mid == ~0ull) ? w.pos : w.mid;
+  }
+  w.pos += adv;
+}
+__device__ __forceinline__ void spec_store(const SnappyArgs& a, const SpecChain& w, uint32_t c) {
+  a.mid_first[c] = w.mid > 0xffffffffull ? 0xffffffffu : uint32_t(w.mid);
+  a.half_out[c] = w.hout;
+  a.half_elems[c] = w.helems;
+  a.spec_exit[c] = w.pos > 0xffffffffull ? 0xffffffffu : uint32_t(w.pos);
+#pragma unroll
+  for (int k = 0; k < int(SNAP_CH / 32); k += 4)
+    *reinterpret_cast<uint4*>(&a.vis[uint64_t(c) * (SNAP_CH / 32) + k]) = make_uint4(w.lv[k], w.lv[k + 1], w.lv[k + 2], w.lv[k + 3]);
+  // the chunk's output bytes / elements if its true entry is its first visited position (nearly
+  // always): k_snap_count then only re-walks the exceptions
+  a.spec_first[c] = w.first > 0xffffffffull ? 0xffffffffu : uint32_t(w.first);
+  a.chunk_out[c] = w.out > 0xffffffffull ? 0xffffffffu : uint32_t(w.out);
+  a.chunk_elems[c] = w.elems;
+}
+
 __global__ void __launch_bounds__(WG_CHUNKS) k_snap_spec(SnappyArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[STAGE_BYTES + 32];
   const WgInfo g = wg_info(a);
   const SnapPage& pg = a.pages[g.p];
   const Staged s = stage_input(buf, reinterpret_cast<const uint8_t*>(pg.in), pg.n_in, g.j0, g.cnt);
-  if (threadIdx.x >= g.cnt) return;
-  const uint32_t j = g.j0 + threadIdx.x;
-  const uint32_t c = a.chunk_base[g.p] + j;
-  const uint64_t cs = uint64_t(j) * SNAP_CH;
-  const uint64_t ce = min(cs + SNAP_CH, uint64_t(pg.n_in));
-  // visited bitmap in registers (statically indexed: each step ORs its bit into the selected word
-  // with selects, so the walk issues no LDS read-modify-write of its own)
-  uint32_t lv[SNAP_CH / 32];
-#pragma unroll
-  for (int k = 0; k < int(SNAP_CH / 32); ++k) lv[k] = 0;
-  uint64_t pos = cs >= SNAP_WU ? cs - SNAP_WU : 0;
-  uint64_t first = ~0ull, out = 0, mid = ~0ull;
-  uint32_t elems = 0, hout = 0, helems = 0;
-  const uint64_t cm = cs + SNAP_CH / 2;
-  while (pos < ce) {
-    uint32_t adv, len;
-    snap_step(staged_u64(buf, s, pos), &adv, &len);
-    if (pos >= cs) {
-      const uint32_t r = uint32_t(pos - cs);
-      const uint32_t wi = r >> 5, bit = 1u << (r & 31);
-#pragma unroll
-      for (int k = 0; k < int(SNAP_CH / 32); ++k) lv[k] |= wi == uint32_t(k) ? bit : 0u;
-      if (first == ~0ull) first = pos;
-      out += len;
-      ++elems;
-      const bool h = pos < cm;
-      hout += h ? len : 0u;
-      helems += h ? 1u : 0u;
-      mid = (!h && mid == ~0ull) ? pos : mid;
-    }
-    pos += adv;
-  }
-  a.mid_first[c] = mid > 0xffffffffull ? 0xffffffffu : uint32_t(mid);
-  a.half_out[c] = hout;
-  a.half_elems[c] = helems;
-  a.spec_exit[c] = pos > 0xffffffffull ? 0xffffffffu : uint32_t(pos);
-#pragma unroll
-  for (int k = 0; k < int(SNAP_CH / 32); k += 4)
-    *reinterpret_cast<uint4*>(&a.vis[uint64_t(c) * (SNAP_CH / 32) + k]) = make_uint4(lv[k], lv[k + 1], lv[k + 2], lv[k + 3]);
-  // the chunk's output bytes / elements if its true entry is its first visited position (nearly
-  // always): k_snap_count then only re-walks the exceptions
-  a.spec_first[c] = first > 0xffffffffull ? 0xffffffffu : uint32_t(first);
-  a.chunk_out[c] = out > 0xffffffffull ? 0xffffffffu : uint32_t(out);
-  a.chunk_elems[c] = elems;
+  const bool live = threadIdx.x < g.cnt;
+  SpecChain w;
+  spec_init(w, g.j0 + threadIdx.x, pg.n_in, live, uint64_t(g.j0) * SNAP_CH);
+  while (w.pos < w.ce) spec_step(w, staged_u64(buf, s, w.pos));
+  if (live) spec_store(a, w, a.chunk_base[g.p] + g.j0 + threadIdx.x);
 }
 
 // Walks chunk j of a page from `e` (a true element start) to its exit; 8-byte headers from global.

@@ -501,3 +501,100 @@ def test_stage_named_files_must_belong_to_the_log(engine, tmp_path):
     with pytest.raises(DeltaError) as ei:
         engine.stage_files(files, log_path=lp, names=[lp + "/%020d.json" % 4])
     assert "does not name a delta file of version 0" in str(ei.value)
+
+
+def _tape_clean(line: bytes) -> bool:
+    """Lines the wave-cooperative tokenizer is meant to take (k_json.hip build_tape), conservatively:
+    no byte below 0x21 anywhere, only the escapes it validates itself, and no string left open at
+    the line end."""
+    if any(c < 0x21 for c in line) or len(line) > 400:
+        return False
+    i = quotes = 0
+    while i < len(line):
+        if line[i] == 0x5C:
+            if i + 1 >= len(line) or line[i + 1] not in b'"\\/bfnrt':
+                return False
+            i += 2
+        else:
+            quotes += line[i] == 0x22
+            i += 1
+    return quotes % 2 == 0
+
+
+def test_device_tape_matches_walker_semantics(engine):
+    """The wave-cooperative tokenizer (k_json_lines' tape) against the PERMISSIVE restatement:
+    clean corpus lines and their clean mutations packed into whole 64-line waves at all 16 byte
+    skews (so backslash runs, strings and scalars cross lane windows and 1 KiB steps), then the
+    lines that send a wave back to the per-lane walker. Every line must read the same either way,
+    and the clean waves must have taken the tape."""
+    from tests.test_json_lane import corpus, expected, mutate
+    base = [l for l in corpus() if b"\n" not in l]
+    rng = random.Random(0x7A9E)
+    clean = [l for l in base if _tape_clean(l)]
+    while len(clean) < 64 * 160:
+        m = mutate(rng, rng.choice(base))
+        try:
+            m.decode("utf-8")
+        except UnicodeDecodeError:
+            continue
+        if _tape_clean(m):
+            clean.append(m)
+    # backslash runs and escaped quotes at every offset of a 16-byte window, long scalars, strings
+    # close to the 4096-byte limit (on both sides), deep nesting (the DFA's `hard` deferral)
+    for k in range(40):
+        bs = b"\\\\" * k
+        clean.append(b'{"add":{"path":"a' + bs + b'\\"b","size":' + str(10 ** (k % 19)).encode() + b'}}')
+        clean.append(b'{"remove":{"path":"' + b"x" * k + b'\\\\","deletionTimestamp":' + str(k).encode() + b'}}')
+    clean.append(b'{"add":{"path":"' + b"p" * 4095 + b'","size":1}}')
+    clean.append(b'{"add":{"path":"' + b"p" * 4096 + b'","size":1}}')
+    clean.append(b"[" * 70 + b"]" * 70)
+    lines = []
+    for skew in range(16):
+        lines.append(b"x" * skew)  # an error line that shifts everything after it
+        lines.extend(clean[skew * 64:(skew + 8) * 64])
+    lines.extend(clean)
+    dirty = [mutate(rng, rng.choice(base)) for _ in range(3000)]
+    dirty = [d for d in dirty if b"\n" not in d and not _tape_clean(d)]
+    lines.extend(dirty)
+    got = _device_lines(engine, lines)
+    st = engine.last_stats()
+    assert len(got) == len(lines)
+    for line, rec in zip(lines, got):
+        assert rec["line"] == line
+        assert _device_view(rec) == expected(line), line
+    clean_waves = len(lines) - len(dirty)
+    assert st["k1_waves"] == (len(lines) + 63) // 64
+    assert st["k1_tape_waves"] >= clean_waves // 64 * 3 // 4, st
+
+
+def test_device_tape_on_synthetic_commits(engine, tmp_path):
+    """Writer-canonical commits (the benchmark's add / remove lines): every wave takes the tape, and
+    the replay equals the oracle's."""
+    from delta_amd.testing import synth as S
+    exp = S.build_config(1, str(tmp_path), scale=0.05)
+    lp = os.path.join(str(tmp_path), "_delta_log")
+    files = sorted(f for f in os.listdir(lp) if f.endswith(".json"))
+    staged = engine.stage_files([(int(f[:20]), 0, 0, open(os.path.join(lp, f), "rb").read()) for f in files])
+    try:
+        recs = staged.parse_lines()
+    finally:
+        staged.release()
+    st = engine.last_stats()
+    assert st["k1_tape_waves"] >= st["k1_waves"] - len(files), st
+    from delta_amd.actions import from_json
+    i = 0
+    for f in files:
+        for line in open(os.path.join(lp, f), "rb").read().split(b"\n")[:-1]:
+            a = from_json(line.decode())
+            r = recs[i]
+            i += 1
+            fa = a.get("add") or a.get("remove")
+            if fa is not None:
+                assert r["path"].decode() == fa["path"]
+                assert r["size"] == fa.get("size", 0)
+    assert i == len(recs)
+    st = _gpu_replay(engine, lp, exp.min_file_retention_timestamp)
+    try:
+        _assert_same(st, O.state_reconstruction(O.get_log_segment(lp), exp.min_file_retention_timestamp))
+    finally:
+        st.release()

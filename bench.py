@@ -409,7 +409,6 @@ def main():
             base = k.split("#")[0]
             kern_ms[base] = kern_ms.get(base, 0.0) + v
             kern_n[base] = kern_n.get(base, 0) + 1
-    k1_stats = eng.last_stats()  # K1 waves on the wave-cooperative tokenizer / per fallback reason
     eng.set_timing(False)
     kern_ms.pop("start", None)
     kern_ms.pop("end", None)
@@ -523,7 +522,6 @@ def main():
         "k5_filter": k5,
         "checkpoint_write": ckpt,
         "kernels": kernels,
-        "k1_tape": k1_stats,
         "result": {k: counts[k] for k in ("num_files", "num_removes", "size_in_bytes", "live_key_sum",
                                           "tomb_key_sum")},
     }

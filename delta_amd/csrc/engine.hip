@@ -61,7 +61,6 @@ struct dr_ctx {
   };
   std::vector<KMark> kmarks;
   std::vector<std::pair<std::string, float>> timings;
-  uint64_t k1_waves = 0, k1_tape[6] = {0, 0, 0, 0, 0, 0};  // K1 waves of the last parse: on the tape, per fallback reason
   std::multimap<size_t, void*> free_blocks;
   std::unordered_map<void*, size_t> sizes;
   std::mutex mu;
@@ -994,9 +993,8 @@ static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
   st->delts = DBuf<int64_t>(ctx, N);
   st->src_off = DBuf<uint64_t>(ctx, N);
   st->src_len = DBuf<uint32_t>(ctx, N);
-  DBuf<uint64_t> counters(ctx, 14);  // 0 special count, 1 special bytes, 2 nonfile count, 3 errors, 4 canon fill,
-                                      // 5 lines deferred to the General walker, 7 checkpoint decode error,
-                                      // 8..13 K1 waves on the tape / per fallback reason
+  DBuf<uint64_t> counters(ctx, 8);  // 0 special count, 1 special bytes, 2 nonfile count, 3 errors, 4 canon fill,
+                                     // 5 lines deferred to the General walker, 7 checkpoint decode error
   counters.zero(stream);
   DBuf<uint64_t> nl(ctx, nlines);
   DBuf<uint64_t> nonfile(ctx, nlines);
@@ -1027,8 +1025,7 @@ static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
     JsonParseArgs ja{s.d_json.p, nl.p, nlines, R, act.kind, act.flags, act.key, act.path_ptr, act.path_len,
                      act.size, act.delts, act.src_off, act.src_len, counters.p + 0, counters.p + 1, counters.p + 2,
                      nonfile.p, nlines, counters.p + 3, hard.p,
-                     reinterpret_cast<unsigned long long*>(counters.p + 5),
-                     reinterpret_cast<unsigned long long*>(counters.p + 8)};
+                     reinterpret_cast<unsigned long long*>(counters.p + 5)};
     launch_json_parse(ja, s2);
     launch_json_hard(ja, s2);
     if (ctx->overlap) {
@@ -1084,11 +1081,9 @@ static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
   }
   // the checkpoint decoder's error code rides in counters[7]: one read-back for both
   if (R) HIP_OK(hipMemcpyAsync(counters.p + 7, pq_err.p, sizeof(uint32_t), hipMemcpyDeviceToDevice, stream));
-  std::vector<uint64_t> cnt = d2h(counters.p, 14, stream);
+  std::vector<uint64_t> cnt = d2h(counters.p, 8, stream);
   if (R && cnt[7] != 0) fail(DR_E_PARQUET, fmt("device checkpoint decode failed (code %u)", unsigned(cnt[7])));
   st->counts.malformed_lines = int64_t(cnt[3]);
-  ctx->k1_waves = (nlines + 63) / 64;
-  for (int k = 0; k < 6; ++k) ctx->k1_tape[k] = cnt[8 + k];
   // ---- canonicalisation of special paths ----
   if (cnt[0] && canonicalize) {
     const uint64_t cap = cnt[1] * 2 + 64 * cnt[0] + 64;
@@ -4026,15 +4021,6 @@ int dr_last_timings(dr_ctx* ctx, char* names, uint64_t names_len, float* ms, int
     size_t c = std::min<size_t>(all.size(), names_len);
     memcpy(names, all.data(), c);
   }
-  return DR_OK;
-}
-
-int dr_last_stats(dr_ctx* ctx, uint64_t* out, int32_t cap, int32_t* n) {
-  if (!ctx || !n) return DR_E_INVALID_ARG;
-  const uint64_t v[7] = {ctx->k1_waves, ctx->k1_tape[0], ctx->k1_tape[1], ctx->k1_tape[2], ctx->k1_tape[3],
-                         ctx->k1_tape[4], ctx->k1_tape[5]};
-  for (int32_t k = 0; k < 7 && k < cap && out; ++k) out[k] = v[k];
-  *n = 7;
   return DR_OK;
 }
 

@@ -56,7 +56,6 @@ struct JsonParseArgs {
   uint64_t* error_count;
   uint64_t* hard_idx;             // lines the fast walker defers to the General walker
   unsigned long long* hard_count;
-  unsigned long long* tape_waves;  // [6]: waves on the wave-cooperative tokenizer, then per fallback reason (nullable)
 };
 
 uint64_t json_num_blocks(uint64_t len);

@@ -91,14 +91,6 @@ class Engine:
         self.check(self.lib.dr_set_timing_only(self.ctx, (only or "").encode()))
         self.check(self.lib.dr_set_timing(self.ctx, 1 if on else 0))
 
-    def last_stats(self) -> Dict[str, int]:
-        """dr_last_stats: K1 waves of the last parse and those on the wave-cooperative tokenizer."""
-        out = (C.c_uint64 * 8)()
-        n = C.c_int32()
-        self.check(self.lib.dr_last_stats(self.ctx, out, 8, C.byref(n)))
-        names = ("k1_waves", "k1_tape_waves", "k1_fb_region", "k1_fb_char", "k1_fb_full", "k1_fb_long", "k1_fb_lines")
-        return {k: int(out[i]) for i, k in enumerate(names[:n.value])}
-
     def last_timings(self) -> Dict[str, float]:
         cap = 1024
         names = C.create_string_buffer(64 * cap)

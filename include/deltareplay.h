@@ -351,11 +351,6 @@ int dr_set_timing(dr_ctx* ctx, int32_t on);
  * NULL or "" = every kernel): the bench times its roofline kernel inside the timed steps without
  * an event pair on every other launch. */
 int dr_set_timing_only(dr_ctx* ctx, const char* kernel);
-/* Counters of the last parse on this context: out[0] K1 waves (64 JSON lines each), out[1] those
- * whose lines went through the wave-cooperative tokenizer, out[2..6] those that took the per-lane
- * walker because the region was too long / held whitespace, a control byte or another escape /
- * overflowed the tape / held a long string / did not split into its lines. */
-int dr_last_stats(dr_ctx* ctx, uint64_t* out, int32_t cap, int32_t* n);
 
 #ifdef __cplusplus
 }

@@ -10,6 +10,6 @@ python - <<'PY'
 import json
 d = json.loads(open("gpurun_out/iter/bench.json").read().strip().splitlines()[-1])
 k = d["kernels"]
-print("ms/step", d["ms_per_step"], "value", d["value"], "roofline", d["roofline"]["kernel"], d["roofline"]["frac"], d.get("k1_tape"))
+print("ms/step", d["ms_per_step"], "value", d["value"], "roofline", d["roofline"]["kernel"], d["roofline"]["frac"])
 print({n: round(v["ms"], 4) for n, v in sorted(k.items(), key=lambda kv: -kv[1]["ms"])[:14]})
 PY

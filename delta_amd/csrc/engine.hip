@@ -270,11 +270,11 @@ struct PagePlan {
   DBuf<uint8_t> d_arena;
   // SNAPPY plan + persistent scratch
   std::vector<SnapPage> snap_pages;
-  std::vector<uint32_t> chunk_base, block_page;
+  std::vector<uint32_t> chunk_base, block_page, chunk_page;
   std::vector<CopyJob> copy_jobs;
   uint32_t nchunks = 0;
   DBuf<SnapPage> d_snap;
-  DBuf<uint32_t> d_chunk_base, d_block_page;
+  DBuf<uint32_t> d_chunk_base, d_block_page, d_chunk_page;
   DBuf<CopyJob> d_copy;
   DBuf<uint32_t> s_mid_first, s_half_out, s_half_elems;
   DBuf<uint32_t> s_spec_exit, s_vis, s_entry, s_spec_first, s_assumed, s_region, s_chunk_out, s_chunk_out_start,
@@ -700,6 +700,7 @@ static void plan_pages(StagedData& s, PagePlan& P) {
                 uint32_t(P.block_page.size())};
     P.chunk_base.push_back(P.nchunks);
     const uint32_t ncp = (sp.n_in + 255) / 256;
+    P.chunk_page.insert(P.chunk_page.end(), ncp, uint32_t(P.snap_pages.size()));
     for (uint32_t j = 0; j < ncp; j += snappy_wg_chunks()) P.wg_chunk0.push_back(P.nchunks + j);
     P.nchunks += ncp;
     P.snap_in_bytes += sp.n_in;
@@ -721,6 +722,7 @@ static void plan_pages(StagedData& s, PagePlan& P) {
   };
   up(P.d_snap, P.snap_pages);
   up(P.d_chunk_base, P.chunk_base);
+  up(P.d_chunk_page, P.chunk_page);
   up(P.d_block_page, P.block_page);
   up(P.d_copy, P.copy_jobs);
   up(P.d_wg_chunk0, P.wg_chunk0);
@@ -794,6 +796,7 @@ static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_
     sa.mid_first = P.s_mid_first.p;
     sa.half_out = P.s_half_out.p;
     sa.half_elems = P.s_half_elems.p;
+    sa.chunk_page = P.d_chunk_page.p;
     DBuf<uint64_t> stamps;
     const bool dbg = std::getenv("DR_SNAP_DEBUG") != nullptr;
     if (dbg) {

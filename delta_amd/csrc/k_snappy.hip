@@ -89,14 +89,8 @@ __device__ __forceinline__ void snap_step(uint64_t w, uint32_t* adv, uint32_t* o
   *adv = hdr + (t == 0 ? len : 0u);
 }
 
-__device__ __forceinline__ uint32_t chunk_page(const uint32_t* chunk_base, uint32_t npages, uint32_t c) {
-  uint32_t lo = 0, hi = npages;  // last page with chunk_base[p] <= c
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (chunk_base[mid] <= c) lo = mid; else hi = mid;
-  }
-  return lo;
-}
+// Page of chunk c: the plan's per-chunk table (one load), built once when the segment is staged.
+__device__ __forceinline__ uint32_t chunk_page(const SnappyArgs& a, uint32_t c) { return a.chunk_page[c]; }
 
 // ---- LDS staging of a workgroup's input range -------------------------------------------------------
 // Bytes of the page input from (chunk j0 start - warm-up) to (chunk j0+cnt end + 16) are copied
@@ -130,13 +124,14 @@ __device__ Staged stage_input(uint8_t* buf, const uint8_t* in, uint64_t n_in, ui
   return Staged{lo_al, hi};
 }
 
-// 8 bytes at page offset pos from the staged copy.
+// The element header at page offset pos from the staged copy: bytes pos .. pos+4 (a tag and at most
+// four length / offset bytes) in the low 40 bits, from two dword reads (higher bits unspecified).
 __device__ __forceinline__ uint64_t staged_u64(const uint8_t* buf, const Staged& s, uint64_t pos) {
   const uint32_t r = uint32_t(int64_t(pos) - s.lo);
   const uint32_t* b32 = reinterpret_cast<const uint32_t*>(buf);
   const uint32_t di = r >> 2, sh = r & 3;
-  const uint32_t w0 = b32[skew(di)], w1 = b32[skew(di + 1)], w2 = b32[skew(di + 2)];
-  return uint64_t(__builtin_amdgcn_alignbyte(w1, w0, sh)) | (uint64_t(__builtin_amdgcn_alignbyte(w2, w1, sh)) << 32);
+  const uint32_t w0 = b32[skew(di)], w1 = b32[skew(di + 1)];
+  return ((uint64_t(w1) << 32) | w0) >> (8 * sh);
 }
 
 // Workgroup g covers chunks [wg_chunk0[g], ...) of one page.
@@ -145,7 +140,7 @@ struct WgInfo {
 };
 __device__ __forceinline__ WgInfo wg_info(const SnappyArgs& a) {
   const uint32_t c = a.wg_chunk0[blockIdx.x];
-  const uint32_t p = chunk_page(a.chunk_base, a.npages, c);
+  const uint32_t p = chunk_page(a, c);
   const uint32_t j0 = c - a.chunk_base[p];
   const uint32_t nc = a.chunk_base[p + 1] - a.chunk_base[p];
   return WgInfo{p, j0, min(WG_CHUNKS, nc - j0)};
@@ -232,7 +227,7 @@ __device__ __forceinline__ uint64_t walk_chunk(const uint8_t* in, uint64_t e, ui
 __global__ void __launch_bounds__(256) k_snap_assume(SnappyArgs a) {
   const uint32_t c = blockIdx.x * 256 + threadIdx.x;
   if (c >= a.nchunks) return;
-  const uint32_t p = chunk_page(a.chunk_base, a.npages, c);
+  const uint32_t p = chunk_page(a, c);
   const SnapPage& pg = a.pages[p];
   const uint32_t j = c - a.chunk_base[p];
   const uint64_t cs = uint64_t(j) * SNAP_CH;
@@ -266,7 +261,7 @@ constexpr uint32_t MAX_RUN = 32;
 __global__ void __launch_bounds__(256) k_snap_entries(SnappyArgs a) {
   const uint32_t c = blockIdx.x * 256 + threadIdx.x;
   if (c >= a.nchunks) return;
-  const uint32_t p = chunk_page(a.chunk_base, a.npages, c);
+  const uint32_t p = chunk_page(a, c);
   const uint32_t j = c - a.chunk_base[p];
   if (j == 0) { a.entry[c] = 0; return; }
   const uint32_t b = c - 1;  // page-relative j-1
@@ -306,7 +301,7 @@ constexpr uint32_t REGION_GAP = 80;
 __global__ void __launch_bounds__(256) k_snap_regions(SnappyArgs a) {
   const uint32_t c = blockIdx.x * 256 + threadIdx.x;
   if (c >= a.nchunks || !a.chunk_flag[c]) return;
-  const uint32_t p = chunk_page(a.chunk_base, a.npages, c);
+  const uint32_t p = chunk_page(a, c);
   const uint32_t c0 = a.chunk_base[p];
   const uint32_t lo = c >= c0 + REGION_GAP ? c - REGION_GAP : c0;
   for (uint32_t k = lo; k < c; ++k)
@@ -324,7 +319,7 @@ __global__ void __launch_bounds__(64) k_snap_resolve(SnappyArgs a) {
   const uint64_t nreg = *a.region_count;
   for (uint64_t rg = blockIdx.x; rg < nreg; rg += gridDim.x) {
     const uint32_t cf = a.region[rg];
-    const uint32_t p = chunk_page(a.chunk_base, a.npages, cf);
+    const uint32_t p = chunk_page(a, cf);
     const SnapPage& pg = a.pages[p];
     const uint8_t* in = reinterpret_cast<const uint8_t*>(pg.in);
     const uint32_t c0 = a.chunk_base[p], nc = a.chunk_base[p + 1] - c0;
@@ -402,7 +397,7 @@ __global__ void __launch_bounds__(256) k_snap_count(SnappyArgs a) {
   const uint32_t pos0 = a.entry[c];
   if (pos0 == a.spec_first[c]) return;
   a.mid_first[c] = 0xffffffffu;  // not split: k_snap_emit walks it with one lane
-  const uint32_t p = chunk_page(a.chunk_base, a.npages, c);
+  const uint32_t p = chunk_page(a, c);
   const SnapPage& pg = a.pages[p];
   const uint64_t cs = uint64_t(c - a.chunk_base[p]) * SNAP_CH;
   const uint64_t ce = min(cs + SNAP_CH, uint64_t(pg.n_in));

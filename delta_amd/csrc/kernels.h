@@ -167,6 +167,7 @@ struct SnappyArgs {
   uint32_t* mid_first = nullptr;
   uint32_t* half_out = nullptr;
   uint32_t* half_elems = nullptr;
+  const uint32_t* chunk_page = nullptr;  // [nchunks] page of each chunk
 };
 uint32_t snappy_wg_chunks();
 void launch_snappy(const SnappyArgs& a, hipStream_t st, void* scan_scratch);

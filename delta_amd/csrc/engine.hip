@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <map>
+#include <chrono>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -2298,10 +2299,12 @@ struct CkLeafW {
   std::vector<std::vector<uint8_t>> hdef, hrep, hval;
 };
 
-static void put_u32le(std::vector<uint8_t>& b, uint32_t v) {
+template <typename V>
+static void put_u32le(V& b, uint32_t v) {
   for (int k = 0; k < 4; ++k) b.push_back(uint8_t(v >> (8 * k)));
 }
-static void put_varint(std::vector<uint8_t>& b, uint64_t v) {
+template <typename V>
+static void put_varint(V& b, uint64_t v) {
   while (v >= 0x80) { b.push_back(uint8_t(v) | 0x80); v >>= 7; }
   b.push_back(uint8_t(v));
 }
@@ -2438,8 +2441,51 @@ static int32_t spark_type_code(const std::string& t) {
   return -1;
 }
 
+// The part file, grown in a malloc'd buffer that dr_state_write_checkpoint hands to the caller as
+// is (page bodies are copied in from the device; nothing is zero-filled or copied a second time).
+struct MallocBytes {
+  uint8_t* p = nullptr;
+  size_t n = 0, cap = 0;
+  MallocBytes() = default;
+  MallocBytes(const MallocBytes&) = delete;
+  MallocBytes& operator=(const MallocBytes&) = delete;
+  ~MallocBytes() { free(p); }
+  size_t size() const { return n; }
+  uint8_t* data() { return p; }
+  void clear() { n = 0; }
+  void reserve(size_t c) {
+    if (c <= cap) return;
+    uint8_t* q = static_cast<uint8_t*>(realloc(p, c));
+    if (!q) throw std::bad_alloc();
+    p = q;
+    cap = c;
+  }
+  void resize(size_t m) {
+    if (m > cap) reserve(std::max(m, cap * 2));
+    n = m;
+  }
+  uint8_t* end() { return p + n; }
+  void push_back(uint8_t b) {
+    resize(n + 1);
+    p[n - 1] = b;
+  }
+  template <typename It>
+  void insert(uint8_t*, It a, It b) {
+    const size_t k = size_t(std::distance(a, b)), at = n;
+    resize(n + k);
+    std::copy(a, b, p + at);
+  }
+  void insert(uint8_t* e, std::initializer_list<uint8_t> l) { insert(e, l.begin(), l.end()); }
+  uint8_t* release() {
+    uint8_t* q = p;
+    p = nullptr;
+    n = cap = 0;
+    return q;
+  }
+};
+
 struct CkPartOut {
-  std::vector<uint8_t> file;
+  MallocBytes file;
   int64_t rows = 0;
 };
 
@@ -2450,6 +2496,17 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
   ensure_ready(st);
   hipStream_t stream = ctx->stream;
   if (st.sharded) fail(DR_E_UNSUPPORTED, "a sharded replay's part writes through the sharded writer");
+  // DR_CKPT_DEBUG=1: wall time per phase on stderr (device work synchronised at each mark)
+  const bool dbg = std::getenv("DR_CKPT_DEBUG") != nullptr;
+  auto t_last = std::chrono::steady_clock::now();
+  std::map<std::string, double> t_acc;
+  auto tmark = [&](const char* what) {
+    if (!dbg) return;
+    HIP_OK(hipStreamSynchronize(stream));
+    const auto now = std::chrono::steady_clock::now();
+    t_acc[what] += std::chrono::duration<double, std::milli>(now - t_last).count();
+    t_last = now;
+  };
   // head rows: protocol, metaData, txns (the checkpoint writer's order)
   std::vector<const NonFileAction*> head;
   const NonFileAction* md = nullptr;
@@ -2494,9 +2551,11 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
   // only the records of this part: adds [a0, a1), removes [b0, b1) (side-relative)
   const uint64_t a0 = std::min(NA, p0 > H ? p0 - H : 0), a1 = std::min(NA, p1 > H ? p1 - H : 0);
   const uint64_t b0 = std::min(NR, p0 > H + NA ? p0 - H - NA : 0), b1 = std::min(NR, p1 > H + NA ? p1 - H - NA : 0);
+  tmark("setup");
   DevExport X[2];
   export_device(st, DR_LIVE, X[0], a0, a1);
   export_device(st, DR_TOMBSTONES, X[1], b0, b1);
+  tmark("export");
   // ---- schema (DFS) and leaves ----
   std::vector<SElem> schema;
   std::vector<CkLeafW> leaves;
@@ -2670,8 +2729,10 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
     for (uint64_t h = 0; h < H; ++h) head_row_levels(L, 0, head[h], L.hdef[h], L.hrep[h], L.hval[h]);
   }
   // ---- pages ----
-  std::vector<uint8_t>& f = out.file;
-  f = {'P', 'A', 'R', '1'};
+  MallocBytes& f = out.file;
+  f.clear();
+  f.reserve(size_t(p1 - p0) * 160 + (size_t(1) << 20));  // address space only; grows if exceeded
+  f.insert(f.end(), {'P', 'A', 'R', '1'});
   struct ChunkMeta { int64_t off, size, usize, nval; int codec; };
   struct RG { std::vector<ChunkMeta> cols; int64_t rows, bytes; };
   std::vector<RG> rgs;
@@ -2683,8 +2744,9 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
     rg.rows = int64_t(r1 - r0);
     rg.bytes = 0;
     for (CkLeafW& L : leaves) {
-      std::vector<uint8_t> rep, def, vals, dev_body;
-      uint64_t nlev = 0, dev_body_raw = 0;
+      std::vector<uint8_t> rep, def, vals, dev_prefix;
+      DBuf<uint8_t> dev_out;  // a device leaf's page body (after dev_prefix), compressed or not
+      uint64_t nlev = 0, dev_body_raw = 0, dev_out_len = 0;
       int dev_codec = 0;
       const int dw = level_width(L.max_def), rw = level_width(L.max_rep);
       const uint64_t side_lo = L.side == 0 ? H + a0 : H + NA + b0, side_n = L.side == 0 ? a1 - a0 : b1 - b0;
@@ -2713,6 +2775,7 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
         a.n = side_n;
         a.nlev = nl.p;
         a.vbytes = vb.p;
+        tmark("host_leaves");
         launch_enc_count(a, stream);
         launch_scan_u32(nl.p, lo.p, R, scratch.p, stream);
         launch_scan_u32(vb.p, vo.p, R, scratch.p, stream);
@@ -2743,7 +2806,7 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
         if (L.max_rep) { put_u32le(hdr_r, uint32_t(rsec)); hdr_r.insert(hdr_r.end(), rh.begin(), rh.end()); }
         put_u32le(hdr_d, uint32_t(dsec));
         hdr_d.insert(hdr_d.end(), dh.begin(), dh.end());
-        DBuf<uint8_t> bodyd(ctx, bsize + 8);
+        DBuf<uint8_t> bodyd(ctx, bsize + 64);  // the compressor reads up to 16 bytes past the end
         uint64_t at = 0;
         auto h2d_at = [&](const std::vector<uint8_t>& h) {
           if (!h.empty()) HIP_OK(hipMemcpyAsync(bodyd.p + at, h.data(), h.size(), hipMemcpyHostToDevice, stream));
@@ -2758,43 +2821,49 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
         d2d_at(dpk.p, groups * uint64_t(dw));
         d2d_at(vsrc, vbytes);
         dev_body_raw = bsize;
+        tmark("encode");
         if (opts & DR_CKPT_SNAPPY) {
-          const uint64_t frag = 8192, nfrag = (bsize + frag - 1) / frag, slot = snap_compress_slot();
-          DBuf<uint8_t> cz(ctx, nfrag * slot + 1);
+          // one workgroup per 8 KiB fragment, then the fragments compacted into one stream on the
+          // device: only the compressed bytes cross to the host, once, into the file
+          const uint64_t frag = snap_compress_frag(), nfrag = (bsize + frag - 1) / frag, slot = snap_compress_slot();
+          DBuf<uint8_t> cz(ctx, nfrag * slot + 16);
           DBuf<uint32_t> czl(ctx, nfrag + 1);
+          DBuf<uint64_t> czo(ctx, nfrag + 1);
           launch_snap_compress(bodyd.p, bsize, cz.p, czl.p, stream);
-          const std::vector<uint32_t> fl = d2h(czl.p, nfrag, stream);
-          const std::vector<uint8_t> all = d2h(cz.p, nfrag * slot, stream);
-          put_varint(dev_body, bsize);  // the snappy preamble: uncompressed length
-          for (uint64_t k = 0; k < nfrag; ++k)
-            dev_body.insert(dev_body.end(), all.begin() + k * slot, all.begin() + k * slot + fl[k]);
+          launch_scan_u32(czl.p, czo.p, nfrag, scratch.p, stream);
+          dev_out_len = d2h_one(czo.p + nfrag, stream);
+          dev_out = DBuf<uint8_t>(ctx, dev_out_len + 1);
+          launch_snap_gather(cz.p, czl.p, czo.p, uint32_t(nfrag), dev_out.p, stream);
+          put_varint(dev_prefix, bsize);  // the snappy preamble: uncompressed length
           dev_codec = 1;
+          tmark("compress");
         } else {
-          dev_body = d2h(bodyd.p, bsize, stream);
+          dev_out_len = bsize;
+          dev_out = std::move(bodyd);
         }
       }
       if (L.phys == PQ_BOOLEAN && !dev) {  // host BOOLEAN values are bytes until packed (none are written)
         vals.clear();
       }
-      std::vector<uint8_t> body;
-      uint64_t raw;
+      std::vector<uint8_t> body;  // a host leaf's page body
+      uint64_t raw, blen;
       int codec = 0;
       if (dev) {
-        body.swap(dev_body);
         raw = dev_body_raw;
+        blen = dev_prefix.size() + dev_out_len;
         codec = dev_codec;
       } else {
         if (L.max_rep) { put_u32le(body, uint32_t(rep.size())); body.insert(body.end(), rep.begin(), rep.end()); }
         put_u32le(body, uint32_t(def.size()));
         body.insert(body.end(), def.begin(), def.end());
         body.insert(body.end(), vals.begin(), vals.end());
-        raw = body.size();
+        raw = blen = body.size();
       }
       if (raw > uint64_t(INT32_MAX)) fail(DR_E_UNSUPPORTED, "checkpoint page over 2 GiB: use smaller row groups");
       ThriftW ph;
       ph.i32(1, 0);  // DATA_PAGE
       ph.i32(2, int32_t(raw));
-      ph.i32(3, int32_t(body.size()));
+      ph.i32(3, int32_t(blen));
       ph.begin_struct(5);
       ph.i32(1, int32_t(nlev));
       ph.i32(2, 0);  // PLAIN
@@ -2804,9 +2873,19 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
       ph.b.push_back(0);
       const int64_t off = int64_t(f.size());
       f.insert(f.end(), ph.b.begin(), ph.b.end());
-      f.insert(f.end(), body.begin(), body.end());
-      rg.cols.push_back(ChunkMeta{off, int64_t(ph.b.size() + body.size()), int64_t(ph.b.size() + raw), int64_t(nlev), codec});
-      rg.bytes += int64_t(ph.b.size() + body.size());
+      if (dev) {
+        f.insert(f.end(), dev_prefix.begin(), dev_prefix.end());
+        const size_t at = f.size();
+        f.resize(at + dev_out_len);
+        if (dev_out_len) HIP_OK(hipMemcpyAsync(f.data() + at, dev_out.p, dev_out_len, hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipStreamSynchronize(stream));
+        tmark("d2h");
+      } else {
+        f.insert(f.end(), body.begin(), body.end());
+      }
+      rg.cols.push_back(ChunkMeta{off, int64_t(ph.b.size() + blen), int64_t(ph.b.size() + raw), int64_t(nlev), codec});
+      tmark("file");
+      rg.bytes += int64_t(ph.b.size() + blen);
     }
     rgs.push_back(std::move(rg));
   }
@@ -2857,6 +2936,9 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
   f.insert(f.end(), fm.b.begin(), fm.b.end());
   put_u32le(f, uint32_t(fm.b.size()));
   f.insert(f.end(), {'P', 'A', 'R', '1'});
+  tmark("footer");
+  if (dbg)
+    for (auto& kv : t_acc) fprintf(stderr, "[ckpt] %-12s %9.3f ms\n", kv.first.c_str(), kv.second);
   ctx->collect_timings();
 }
 
@@ -3986,11 +4068,8 @@ int dr_state_write_checkpoint(dr_state* state, int32_t part, int32_t parts, uint
     HIP_OK(hipSetDevice(state->ctx->device));
     CkPartOut o;
     write_checkpoint_part(*state, part, parts, opts, row_group_rows, o);
-    uint8_t* buf = static_cast<uint8_t*>(malloc(std::max<size_t>(o.file.size(), 1)));
-    if (!buf) throw std::bad_alloc();
-    memcpy(buf, o.file.data(), o.file.size());
-    *bytes = buf;
     *len = o.file.size();
+    *bytes = o.file.release();  // malloc'd: the caller frees it with dr_free
     if (rows) *rows = o.rows;
   });
 }

@@ -145,72 +145,86 @@ void launch_enc_pack(const uint8_t* in, uint64_t n, int width, uint8_t* out, hip
 
 // ---- SNAPPY compression (pages of the checkpoint writer) ------------------------------------------
 namespace dev {
-// 8 KiB fragments (inside the reader's 64 KiB blocks, so its fragment rule holds): a 1M-row part's
-// pages give ~37K lanes instead of ~4.6K, and the lane-serial parse is 8x shorter.
+// One workgroup per 8 KiB fragment of the page body (fragments sit inside the reader's 64 KiB
+// blocks, so its fragment rule holds: no element straddles one, no copy reaches before it):
+//  1. the fragment is staged in LDS with 16-byte loads;
+//  2. a 4096-entry table keeps, per hash of 4 bytes, the EARLIEST position in the fragment
+//     (atomicMin, every position in parallel) -- a valid match candidate for every later position;
+//  3. thread t compresses its 64-byte slice greedily against the whole fragment (matches verified
+//     on the LDS bytes, cut at the slice end), into its LDS output slot;
+//  4. a block scan of the slot sizes packs the slots contiguously (LDS) and the fragment's elements
+//     leave with 16-byte stores to out + f * SC_SLOT; out_len[f] is their length.
+// k_snap_gather then compacts the fragments into one stream.
 constexpr uint32_t SC_FRAG = 8192;
-constexpr uint32_t SC_SLOT = SC_FRAG + SC_FRAG / 6 + 64;  // worst case: all literals
-constexpr int SC_BITS = 9;                                 // hash table entries per lane: 2^9 (1 KiB)
+constexpr int SC_T = 128;
+constexpr uint32_t SC_SLICE = SC_FRAG / SC_T;              // 64 input bytes per thread
+constexpr uint32_t SC_OMAX = SC_SLICE + 8;                 // a slice's worst case: one literal, 2-byte tag
+constexpr uint32_t SC_SLOT = 9632;                         // >= SC_T * (SC_SLICE + 2), 16-byte multiple
+constexpr int SC_TBITS = 12;
 
-__device__ __forceinline__ uint32_t ld32(const uint8_t* p) {
-  return uint32_t(p[0]) | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) | (uint32_t(p[3]) << 24);
+__device__ __forceinline__ uint32_t lds32u(const uint8_t* p) {  // 4 bytes at any LDS address
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(p - (a & 3u));
+  return __builtin_amdgcn_alignbyte(w[1], w[0], uint32_t(a & 3u));
 }
+__device__ __forceinline__ uint32_t sc_hash(uint32_t x) { return (x * 0x1e35a7bdu) >> (32 - SC_TBITS); }
 
 __device__ uint32_t emit_literal(uint8_t* d, uint32_t o, const uint8_t* s, uint32_t n) {
   const uint32_t m = n - 1;
   if (m < 60) {
     d[o++] = uint8_t(m << 2);
-  } else if (m < 256) {
+  } else {
     d[o++] = uint8_t(60 << 2);
     d[o++] = uint8_t(m);
-  } else {
-    d[o++] = uint8_t(61 << 2);
-    d[o++] = uint8_t(m);
-    d[o++] = uint8_t(m >> 8);
   }
   for (uint32_t k = 0; k < n; ++k) d[o + k] = s[k];
   return o + n;
 }
 
 __device__ uint32_t emit_copy(uint8_t* d, uint32_t o, uint32_t off, uint32_t len) {
-  while (len > 0) {
-    // pieces of at most 64 bytes, never leaving fewer than 4 for a COPY_1 tail
-    uint32_t l = len > 64 ? (len - 64 < 4 ? 60 : 64) : len;
-    if (l >= 4 && l <= 11 && off < 2048) {
-      d[o++] = uint8_t(1 | ((l - 4) << 2) | ((off >> 8) << 5));
-      d[o++] = uint8_t(off);
-    } else {
-      d[o++] = uint8_t(2 | ((l - 1) << 2));
-      d[o++] = uint8_t(off);
-      d[o++] = uint8_t(off >> 8);
-    }
-    len -= l;
+  // len <= 64 (a slice), off < 8192
+  if (len >= 4 && len <= 11 && off < 2048) {
+    d[o++] = uint8_t(1 | ((len - 4) << 2) | ((off >> 8) << 5));
+    d[o++] = uint8_t(off);
+  } else {
+    d[o++] = uint8_t(2 | ((len - 1) << 2));
+    d[o++] = uint8_t(off);
+    d[o++] = uint8_t(off >> 8);
   }
   return o;
 }
 
-__global__ void __launch_bounds__(64) k_snap_compress(const uint8_t* in, uint64_t n, uint8_t* out, uint32_t* out_len,
-                                                      uint32_t nfrag) {
-  __shared__ uint16_t table[64][1 << SC_BITS];
-  const uint32_t lane = threadIdx.x;
-  const uint32_t f = blockIdx.x * 64 + lane;
-  uint16_t* tab = table[lane];
-  for (uint32_t k = 0; k < (1u << SC_BITS); ++k) tab[k] = 0xffff;
-  if (f >= nfrag) return;
-  const uint8_t* s = in + uint64_t(f) * SC_FRAG;
-  const uint32_t len = uint32_t(min(uint64_t(SC_FRAG), n - uint64_t(f) * SC_FRAG));
-  uint8_t* d = out + uint64_t(f) * SC_SLOT;
-  uint32_t o = 0, ip = 0, lit = 0;
-  if (len >= 16) {
-    const uint32_t limit = len - 4;
-    while (ip <= limit) {
-      const uint32_t cur = ld32(s + ip);
-      const uint32_t h = (cur * 0x1e35a7bdu) >> (32 - SC_BITS);
-      const uint32_t cand = tab[h];
-      tab[h] = uint16_t(ip);
-      if (cand != 0xffffu && cand < ip && ld32(s + cand) == cur) {
+__global__ void __launch_bounds__(SC_T) k_snap_compress(const uint8_t* __restrict__ in, uint64_t n,
+                                                        uint8_t* __restrict__ out, uint32_t* __restrict__ out_len) {
+  __shared__ __attribute__((aligned(16))) uint8_t frag[SC_FRAG + 16];
+  __shared__ uint32_t table[1u << SC_TBITS];
+  __shared__ __attribute__((aligned(16))) uint8_t obuf[SC_T * SC_OMAX];
+  __shared__ __attribute__((aligned(16))) uint8_t cbuf[SC_SLOT];
+  __shared__ uint32_t wsum[SC_T / 64];
+  const uint32_t f = blockIdx.x, t = threadIdx.x;
+  const uint64_t base = uint64_t(f) * SC_FRAG;
+  const uint32_t len = uint32_t(min(uint64_t(SC_FRAG), n - base));
+  const uint32_t nv = (len + 15) / 16;  // the input buffer is readable up to 16 bytes past n
+  for (uint32_t v = t; v < nv; v += SC_T)
+    *reinterpret_cast<uint4*>(frag + 16 * v) = *reinterpret_cast<const uint4*>(in + base + 16 * v);
+  for (uint32_t k = t; k < (1u << SC_TBITS); k += SC_T) table[k] = 0xffffffffu;
+  __syncthreads();
+  for (uint32_t i = t; i + 4 <= len; i += SC_T) atomicMin(&table[sc_hash(lds32u(frag + i))], i);
+  __syncthreads();
+  const uint32_t s0 = t * SC_SLICE, s1 = min(len, s0 + SC_SLICE);
+  uint8_t* d = obuf + t * SC_OMAX;
+  uint32_t o = 0;
+  if (s0 < s1) {
+    uint32_t ip = s0, lit = s0;
+    while (ip + 4 <= s1) {
+      const uint32_t cur = lds32u(frag + ip);
+      const uint32_t cand = table[sc_hash(cur)];
+      if (cand < ip && lds32u(frag + cand) == cur) {
+        const uint32_t maxm = s1 - ip;
         uint32_t m = 4;
-        while (ip + m < len && s[cand + m] == s[ip + m]) ++m;
-        if (ip > lit) o = emit_literal(d, o, s + lit, ip - lit);
+        while (m + 4 <= maxm && lds32u(frag + cand + m) == lds32u(frag + ip + m)) m += 4;
+        while (m < maxm && frag[cand + m] == frag[ip + m]) ++m;
+        if (ip > lit) o = emit_literal(d, o, frag + lit, ip - lit);
         o = emit_copy(d, o, ip - cand, m);
         ip += m;
         lit = ip;
@@ -218,17 +232,52 @@ __global__ void __launch_bounds__(64) k_snap_compress(const uint8_t* in, uint64_
         ++ip;
       }
     }
+    if (s1 > lit) o = emit_literal(d, o, frag + lit, s1 - lit);
   }
-  if (len > lit) o = emit_literal(d, o, s + lit, len - lit);
-  out_len[f] = o;
+  // block exclusive scan of the slot sizes
+  const uint32_t lane = t & 63, wv = t >> 6;
+  uint32_t incl = o;
+  for (int k = 1; k < 64; k <<= 1) {
+    const uint32_t y = __shfl_up(incl, k, 64);
+    if (lane >= uint32_t(k)) incl += y;
+  }
+  if (lane == 63) wsum[wv] = incl;
+  __syncthreads();
+  uint32_t woff = 0, total = 0;
+  for (uint32_t w = 0; w < SC_T / 64; ++w) {
+    woff += w < wv ? wsum[w] : 0u;
+    total += wsum[w];
+  }
+  const uint32_t at = woff + incl - o;
+  for (uint32_t k = 0; k < o; ++k) cbuf[at + k] = d[k];
+  __syncthreads();
+  uint8_t* dst = out + uint64_t(f) * SC_SLOT;
+  for (uint32_t v = t; v < (total + 15) / 16; v += SC_T)
+    *reinterpret_cast<uint4*>(dst + 16 * v) = *reinterpret_cast<const uint4*>(cbuf + 16 * v);
+  if (t == 0) out_len[f] = total;
+}
+
+// Fragment f's elements to dst + off[f] (off: exclusive scan of out_len).
+__global__ void __launch_bounds__(256) k_snap_gather(const uint8_t* __restrict__ slots, const uint32_t* __restrict__ len,
+                                                     const uint64_t* __restrict__ off, uint8_t* __restrict__ dst) {
+  const uint32_t f = blockIdx.x;
+  const uint8_t* s = slots + uint64_t(f) * SC_SLOT;
+  uint8_t* d = dst + off[f];
+  for (uint32_t k = threadIdx.x; k < len[f]; k += 256) d[k] = s[k];
 }
 }  // namespace dev
 
 uint64_t snap_compress_slot() { return dev::SC_SLOT; }
+uint64_t snap_compress_frag() { return dev::SC_FRAG; }
 
 void launch_snap_compress(const uint8_t* in, uint64_t n, uint8_t* out, uint32_t* out_len, hipStream_t st) {
   const uint32_t nfrag = uint32_t((n + dev::SC_FRAG - 1) / dev::SC_FRAG);
-  if (nfrag) DR_LAUNCH(dev::k_snap_compress, dim3((nfrag + 63) / 64), dim3(64), 0, st, in, n, out, out_len, nfrag);
+  if (nfrag) DR_LAUNCH(dev::k_snap_compress, dim3(nfrag), dim3(dev::SC_T), 0, st, in, n, out, out_len);
+}
+
+void launch_snap_gather(const uint8_t* slots, const uint32_t* len, const uint64_t* off, uint32_t nfrag, uint8_t* dst,
+                        hipStream_t st) {
+  if (nfrag) DR_LAUNCH(dev::k_snap_gather, dim3(nfrag), dim3(256), 0, st, slots, len, off, dst);
 }
 
 }  // namespace dr

@@ -628,9 +628,13 @@ void launch_enc_fill(const EncArgs& a, hipStream_t st);
 void launch_enc_pack(const uint8_t* in, uint64_t n, int width, uint8_t* out, hipStream_t st);
 }  // namespace dr
 namespace dr {
-// SNAPPY compression of `n` bytes in 8 KiB fragments, one lane per fragment (greedy hash matching
-// with a 512-entry table per lane in LDS; copies never leave their fragment): fragment f's elements go to out + f * snap_compress_slot(), their length to
-// out_len[f].
+// SNAPPY compression of `n` bytes (readable up to 16 bytes past n) in 8 KiB fragments, one
+// workgroup per fragment (k_encode.hip; copies never leave their fragment): fragment f's elements go
+// to out + f * snap_compress_slot(), their length to out_len[f].
 uint64_t snap_compress_slot();
+uint64_t snap_compress_frag();
 void launch_snap_compress(const uint8_t* in, uint64_t n, uint8_t* out, uint32_t* out_len, hipStream_t st);
+// Compacts the fragments: fragment f's out_len[f] bytes to dst + off[f] (off = exclusive scan).
+void launch_snap_gather(const uint8_t* slots, const uint32_t* len, const uint64_t* off, uint32_t nfrag, uint8_t* dst,
+                        hipStream_t st);
 }  // namespace dr

@@ -2495,7 +2495,8 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
   ctx->begin_call();
   ensure_ready(st);
   hipStream_t stream = ctx->stream;
-  if (st.sharded) fail(DR_E_UNSUPPORTED, "a sharded replay's part writes through the sharded writer");
+  // A sharded replay's state writes its own part: all of its survivors (hash-clustered, PROTOCOL.md's
+  // parts may split the rows any way), the protocol / metaData / txn rows in part 1 only.
   // DR_CKPT_DEBUG=1: wall time per phase on stderr (device work synchronised at each mark)
   const bool dbg = std::getenv("DR_CKPT_DEBUG") != nullptr;
   auto t_last = std::chrono::steady_clock::now();
@@ -2513,9 +2514,11 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
   for (const NonFileAction& a : st.nonfile) if (a.kind == 5) head.push_back(&a);
   for (const NonFileAction& a : st.nonfile) if (a.kind == 3) { head.push_back(&a); md = &a; }
   for (const NonFileAction& a : st.nonfile) if (a.kind == 4) head.push_back(&a);
+  if (st.sharded && part != 1) head.clear();
   const uint64_t H = head.size(), NA = st.n_live, NR = st.n_tomb, ROWS = H + NA + NR;
-  const uint64_t step = parts > 1 ? (ROWS + uint64_t(parts) - 1) / uint64_t(parts) : ROWS;
-  const uint64_t p0 = std::min<uint64_t>(ROWS, uint64_t(part - 1) * step), p1 = std::min<uint64_t>(ROWS, p0 + step);
+  const uint64_t step = parts > 1 && !st.sharded ? (ROWS + uint64_t(parts) - 1) / uint64_t(parts) : ROWS;
+  const uint64_t p0 = st.sharded ? 0 : std::min<uint64_t>(ROWS, uint64_t(part - 1) * step);
+  const uint64_t p1 = std::min<uint64_t>(ROWS, p0 + step);
   out.rows = int64_t(p1 - p0);
   // partitionValues_parsed: the metadata's partition schema (D/Checkpoints.scala:372-389)
   std::vector<std::pair<std::string, int32_t>> parsed;
@@ -3539,6 +3542,30 @@ static std::vector<std::string> rccl_all_gather_text(dr_comm& c, const std::stri
 // One rank's part of the sharded replay (collective over the communicator; every rank stages its
 // own slice with dr_stage_log_shard). The returned state holds this rank's surviving records (its
 // export is its share of allFiles / tombstones) and the table-wide counters and non-file winners.
+// The table-wide non-file winners of a sharded replay from every rank's local winners, one JSON
+// action per line in rank order (= replay order: the slices are contiguous); InMemoryLogReplay's
+// rule over them, as the single `null` partition (D/Snapshot.scala:103).
+static void set_nonfile_lines(dr_state& st, const std::string& lines, bool validate) {
+  std::vector<NonFileAction> merged;
+  size_t b = 0;
+  while (b < lines.size()) {
+    size_t e = lines.find('\n', b);
+    if (e == std::string::npos) e = lines.size();
+    JVal v;
+    if (e > b && json_parse(lines.data() + b, e - b, &v) && v.t == JVal::OBJ && !v.o.empty()) {
+      NonFileAction a;
+      const std::string& key = v.o[0].first;
+      a.kind = key == "metaData" ? 3 : key == "txn" ? 4 : 5;
+      a.order = merged.size();
+      a.val = v.o[0].second;
+      a.json = lines.substr(b, e - b);
+      merged.push_back(std::move(a));
+    }
+    b = e + 1;
+  }
+  reduce_nonfile(st, merged, validate);
+}
+
 static dr_state* replay_sharded_rccl(dr_comm& c, const std::shared_ptr<StagedData>& staged, int64_t cutoff,
                                      uint32_t flags) {
   dr_ctx* ctx = c.ctx;
@@ -3598,26 +3625,9 @@ static dr_state* replay_sharded_rccl(dr_comm& c, const std::shared_ptr<StagedDat
   // non-file winners: every rank's, in rank order (= replay order: slices are contiguous)
   std::string text;
   for (const NonFileAction& a : st->nonfile) text += a.json + "\n";
-  std::vector<NonFileAction> merged;
-  for (const std::string& part_text : rccl_all_gather_text(c, text)) {
-    size_t b = 0;
-    while (b < part_text.size()) {
-      size_t e = part_text.find('\n', b);
-      if (e == std::string::npos) e = part_text.size();
-      JVal v;
-      if (e > b && json_parse(part_text.data() + b, e - b, &v) && v.t == JVal::OBJ && !v.o.empty()) {
-        NonFileAction a;
-        const std::string& key = v.o[0].first;
-        a.kind = key == "metaData" ? 3 : key == "txn" ? 4 : 5;
-        a.order = merged.size();
-        a.val = v.o[0].second;
-        a.json = part_text.substr(b, e - b);
-        merged.push_back(std::move(a));
-      }
-      b = e + 1;
-    }
-  }
-  reduce_nonfile(*st, merged, !(flags & DR_FLAG_NO_VALIDATION));
+  std::string lines;
+  for (const std::string& part_text : rccl_all_gather_text(c, text)) lines += part_text;
+  set_nonfile_lines(*st, lines, !(flags & DR_FLAG_NO_VALIDATION));
   return st.release();
 }
 
@@ -4075,6 +4085,14 @@ int dr_state_write_checkpoint(dr_state* state, int32_t part, int32_t parts, uint
 }
 
 void dr_free(void* p) { free(p); }
+
+int dr_state_set_nonfile_json(dr_state* state, const char* lines, uint64_t len, uint32_t flags) {
+  if (!state || (!lines && len)) return DR_E_INVALID_ARG;
+  return guard(state->ctx, [&] {
+    if (!state->sharded) fail(DR_E_INVALID_ARG, "dr_state_set_nonfile_json takes a sharded replay's state");
+    set_nonfile_lines(*state, std::string(lines ? lines : "", len), !(flags & DR_FLAG_NO_VALIDATION));
+  });
+}
 
 int dr_set_timing_only(dr_ctx* ctx, const char* kernel) {
   if (!ctx) return DR_E_INVALID_ARG;

@@ -268,6 +268,19 @@ class State:
         text = C.string_at(p, n.value).decode("utf-8") if n.value else ""
         self.nonfile = [json.loads(l) for l in text.splitlines() if l.strip()]
 
+    def set_nonfile_json(self, lines: str, validate: bool = True) -> None:
+        """dr_state_set_nonfile_json: a sharded state's table-wide protocol / metaData / txn winners
+        from every rank's local winners (one action per line, rank order)."""
+        raw = lines.encode("utf-8")
+        with self.eng.lock:
+            self.eng.check(self.eng.lib.dr_state_set_nonfile_json(self.h, raw, len(raw),
+                                                                  0 if validate else N.DR_FLAG_NO_VALIDATION))
+        p = C.c_char_p()
+        n = C.c_uint64()
+        self.eng.check(self.eng.lib.dr_state_nonfile_json(self.h, C.byref(p), C.byref(n)))
+        text = C.string_at(p, n.value).decode("utf-8") if n.value else ""
+        self.nonfile = [json.loads(l) for l in text.splitlines() if l.strip()]
+
     def apply(self, tail: "Staged", min_file_retention_timestamp: int, validate: bool = True) -> "State":
         """dr_state_apply: this state extended by the staged commit files of the following
         versions (no re-parse of this state's segment); a new State."""

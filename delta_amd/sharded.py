@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import ctypes as C
 import json
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 from . import _native as N
@@ -275,4 +276,34 @@ def replay_sharded(staged: Staged, min_file_retention_timestamp: int, exchange, 
     texts = exchange.all_gather_text("\n".join(json.dumps(a) for a in local.nonfile))
     nonfile, nc = merge_nonfile(texts, lc["version"], validate)
     counts.update(nc)
+    # the local state carries the table-wide winners too (its checkpoint part 1 writes them)
+    local.set_nonfile_json("\n".join(t for t in texts if t), validate)
     return ShardedState(local, counts, nonfile, exchange)
+
+
+def write_checkpoint_sharded(sharded: "ShardedState", log_path: str, version: int, stats: bool = True,
+                             parsed: bool = True, row_group_rows: int = 0) -> int:
+    """The multi-part checkpoint from the GPU shards: rank r encodes part r + 1 of
+    `world` on its device from its own survivors (dr_state_write_checkpoint; part 1 also holds the
+    protocol / metaData / txn rows), writes it (temp + rename), and rank 0 writes `_last_checkpoint`
+    with the table-wide row count once every part is in place. Returns that count."""
+    from delta_amd.checkpoint import checkpoint_file_with_parts, write_last_checkpoint
+    ex = sharded.exchange
+    data, rows = sharded.local.write_checkpoint_part(ex.rank + 1, ex.world, stats=stats, parsed=parsed,
+                                                     row_group_rows=row_group_rows)
+    path = (os.path.join(log_path, "%020d.checkpoint.parquet" % version) if ex.world == 1
+            else checkpoint_file_with_parts(log_path, version, ex.rank + 1, ex.world))
+    tmp = os.path.join(os.path.dirname(path), ".%s.%d.tmp" % (os.path.basename(path), ex.rank))
+    with open(tmp, "wb") as f:
+        f.write(data)
+    os.replace(tmp, path)
+    import torch
+    dev = torch.device("cpu") if getattr(ex, "host", False) else torch.device("cuda", torch.cuda.current_device())
+    total = ex.all_reduce_sum([rows], dev)[0]
+    if ex.rank == 0:
+        meta = {"version": version, "size": total}
+        if ex.world > 1:
+            meta["parts"] = ex.world
+        write_last_checkpoint(log_path, meta)
+    ex.barrier()
+    return total

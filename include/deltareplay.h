@@ -266,12 +266,21 @@ void dr_free(void* p);
  * with DR_CKPT_SNAPPY, else uncompressed);
  * `row_group_rows` 0 = 2^20. opts: DR_CKPT_STATS writes add.stats (delta.checkpoint.writeStatsAsJson),
  * DR_CKPT_PARSED adds add.partitionValues_parsed (the partition schema's types; writeStatsAsStruct /
- * checkpointV2). The caller writes the file (temp + rename) and `_last_checkpoint`. */
+ * checkpointV2). The caller writes the file (temp + rename) and `_last_checkpoint`.
+ * A sharded replay's state (dr_replay_sharded / dr_shard_finish) writes its own part of a multi-part
+ * checkpoint from the GPU shards: all of its survivors, plus the protocol / metaData / txn rows when
+ * part == 1 (rank r writes part r + 1 of world; PROTOCOL.md lets parts split the rows any way). */
 #define DR_CKPT_STATS 0x1u
 #define DR_CKPT_PARSED 0x2u
 #define DR_CKPT_SNAPPY 0x4u   /* SNAPPY pages for the device-encoded columns (Spark's default codec) */
 int dr_state_write_checkpoint(dr_state* state, int32_t part, int32_t parts, uint32_t opts, uint64_t row_group_rows,
                               uint8_t** bytes, uint64_t* len, int64_t* rows);
+/* A sharded state's table-wide protocol / metaData / txn winners from every rank's local winners
+ * (dr_state_nonfile_json of each rank, concatenated in rank order, one action per line), reduced as
+ * InMemoryLogReplay does (D/actions/InMemoryLogReplay.scala:47-53); dr_replay_sharded does this itself
+ * over RCCL, a host that exchanges through its own collectives calls it after dr_shard_finish.
+ * flags: DR_FLAG_NO_VALIDATION skips the missing protocol / metadata errors. */
+int dr_state_set_nonfile_json(dr_state* state, const char* lines, uint64_t len, uint32_t flags);
 
 /* ---- scan-side consumers of the resident state -----------------------
  * DeltaSourceSnapshot.initialFiles (D/files/DeltaSourceSnapshot.scala:53-95): allFiles.sort(

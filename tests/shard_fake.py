@@ -55,6 +55,11 @@ class FakeState:
     def export(self, which):
         return list(self._live if which == 0 else self._tomb)
 
+    def set_nonfile_json(self, lines, validate=True):
+        """dr_state_set_nonfile_json's reduction (the oracle's merge over the rank-ordered lines)."""
+        from delta_amd.sharded import merge_nonfile
+        self.nonfile, _ = merge_nonfile([lines], self.counts.get("version", -1), validate)
+
     def release(self):
         pass
 

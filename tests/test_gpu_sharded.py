@@ -168,3 +168,63 @@ def test_sharded_one_process_rccl(tmp_path):
                       env={"DR_TEST_BACKEND": "nccl"})
     _check(res["counts"], res["live"], res["tomb"], O.state_reconstruction(O.get_log_segment(lp),
                                                                           exp.min_file_retention_timestamp))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_device_checkpoint_parts(tmp_path, world):
+    """The multi-part checkpoint from the GPU shards: every emulated rank encodes
+    its own part on the device (dr_state_write_checkpoint on its sharded state; part 1 also holds the
+    table-wide protocol / metaData / txn set by dr_state_set_nonfile_json), rank 0 writes
+    `_last_checkpoint`; a fresh replay then starts from the new parts and equals the oracle's state
+    of the original log, as does the oracle's own replay of the rewritten log."""
+    from delta_amd.delta_log import Engine
+    from delta_amd.sharded import replay_sharded, stage_shard, write_checkpoint_sharded
+    from delta_amd.testing import synth as S
+    from tests.thread_exchange import run_threads
+    table = str(tmp_path / "t")
+    exp = S.build_config(2, table, scale=0.01)
+    lp = os.path.join(table, "_delta_log")
+    cutoff = exp.min_file_retention_timestamp
+    snap = O.state_reconstruction(O.get_log_segment(lp), cutoff)
+
+    def rank_fn(r, ex):
+        eng = Engine.get(0)
+        staged = stage_shard(eng, lp, world, r)
+        try:
+            st = replay_sharded(staged, cutoff, ex)
+        finally:
+            staged.release()
+        try:
+            return st.counts["version"], write_checkpoint_sharded(st, lp, st.counts["version"])
+        finally:
+            st.release()
+
+    res = run_threads(world, rank_fn)
+    version, total = res[0]
+    assert all(x == res[0] for x in res)
+    assert total == snap.num_of_files + snap.num_of_removes + snap.num_of_protocol + snap.num_of_metadata + \
+        snap.num_of_set_transactions
+    parts = sorted(f for f in os.listdir(lp) if f.startswith("%020d.checkpoint." % version))
+    assert len(parts) == world, parts
+    with open(os.path.join(lp, "_last_checkpoint")) as f:
+        assert json.load(f) == {"version": version, "size": total, "parts": world}
+    seg = O.get_log_segment(lp)
+    assert len(seg.checkpoint) == world and seg.checkpoint_version == version
+    again = O.state_reconstruction(seg, cutoff)
+    _check(snap_counts(again), again.all_files, again.tombstones, snap)
+    eng = Engine.get(0)
+    staged = eng.stage_log(lp)
+    try:
+        st = staged.replay(cutoff)
+    finally:
+        staged.release()
+    try:
+        _check(st.counts, st.export(0), st.export(1), snap)
+    finally:
+        st.release()
+
+
+def snap_counts(s):
+    return {"num_files": s.num_of_files, "size_in_bytes": s.size_in_bytes, "num_removes": s.num_of_removes,
+            "num_protocol": s.num_of_protocol, "num_metadata": s.num_of_metadata,
+            "num_set_transactions": s.num_of_set_transactions}

@@ -547,8 +547,9 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
   // 1a. per element: its start bit, and the map entry of its first byte (start - offset; a
   //     literal points at itself)
   uint32_t lo_in = 0xffffffffu, hi_in = 0;
+  const bool held = nrec <= EXEC_T * EXEC_RPT;  // block-uniform: one pass, records stay in w for step 3
+  uint64_t w[EXEC_RPT];
   for (uint32_t base = 0; base < nrec; base += EXEC_T * EXEC_RPT) {
-    uint64_t w[EXEC_RPT];
 #pragma unroll
     for (uint32_t k = 0; k < EXEC_RPT; ++k) {
       const uint32_t r = base + k * EXEC_T + uint32_t(t);
@@ -663,25 +664,17 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
   }
   __syncthreads();
   stamp(4);
-  for (uint32_t base = 0; base < nrec; base += EXEC_T * EXEC_RPT2) {
-    uint64_t w[EXEC_RPT2];
-#pragma unroll
-    for (uint32_t k = 0; k < EXEC_RPT2; ++k) {
-      const uint32_t r = base + k * EXEC_T + uint32_t(t);
-      w[k] = r < nrec ? a.recs[r0 + r] : 0ull;
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < EXEC_RPT2; ++k) {
-      const uint32_t r = base + k * EXEC_T + uint32_t(t);
-      const uint32_t sv = uint32_t(w[k] >> 32);
-      if (r >= nrec || !(sv & REC_LIT)) continue;
-      const uint32_t rel = uint32_t(w[k] & 0xffff);
-      const uint32_t len = uint32_t((w[k] >> 16) & 0xffff) + 1;
+  // literal record r (its word wk): LDS -> LDS copy, or queued for the whole workgroup when long
+  auto copy_lit = [&](uint64_t wk, uint32_t r) {
+      const uint32_t sv = uint32_t(wk >> 32);
+      if (r >= nrec || !(sv & REC_LIT)) return;
+      const uint32_t rel = uint32_t(wk & 0xffff);
+      const uint32_t len = uint32_t((wk >> 16) & 0xffff) + 1;
       if (len > EXEC_LONG || !staged) {
         const uint32_t slot = atomicAdd(&s_nlong, 1u);
         if (slot < EXEC_LONG) s_long[slot] = r;
         else s_bad = 1;
-        continue;
+        return;
       }
       // byte head up to a 4-byte aligned destination, then aligned dword stores of realigned
       // source dwords, then a byte tail
@@ -700,6 +693,20 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
       d = uint32_t(reinterpret_cast<uint8_t*>(da) - bytes);
       q = uint32_t(reinterpret_cast<const uint8_t*>(qa) - bytes) + sh;
       while (n) { bytes[d++] = bytes[q++]; --n; }
+  };
+  if (held) {
+#pragma unroll
+    for (uint32_t k = 0; k < EXEC_RPT; ++k) copy_lit(w[k], k * EXEC_T + uint32_t(t));
+  } else {
+    for (uint32_t base = 0; base < nrec; base += EXEC_T * EXEC_RPT2) {
+      uint64_t w2[EXEC_RPT2];
+#pragma unroll
+      for (uint32_t k = 0; k < EXEC_RPT2; ++k) {
+        const uint32_t r = base + k * EXEC_T + uint32_t(t);
+        w2[k] = r < nrec ? a.recs[r0 + r] : 0ull;
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < EXEC_RPT2; ++k) copy_lit(w2[k], base + k * EXEC_T + uint32_t(t));
     }
   }
   __syncthreads();

@@ -697,6 +697,35 @@ static void plan_pages(StagedData& s, PagePlan& P) {
       if (!(b & 0x80)) break;
     }
     if (total != d.usize - lv) fail(DR_E_PARQUET, "snappy preamble does not match the page size");
+    {
+      // a page the compressor could not shrink is a run of literals (one per 64 KiB fragment):
+      // those bytes are copied as they are (a long literal spans many speculation chunks, which
+      // would send the page to the serial decoder)
+      std::vector<CopyJob> lit;
+      uint64_t ip = pre, op = 0;
+      const uint64_t n_in = d.csize - lv;
+      while (ip < n_in && op < total) {
+        const uint8_t tag = h[ip];
+        if (tag & 3) break;
+        const uint32_t l6 = tag >> 2, nb = l6 < 60 ? 0 : l6 - 59;
+        if (ip + 1 + nb > n_in) break;
+        uint64_t len = l6 + 1;
+        if (nb) {
+          len = 0;
+          for (uint32_t k = 0; k < nb; ++k) len |= uint64_t(h[ip + 1 + k]) << (8 * k);
+          len += 1;
+        }
+        if (ip + 1 + nb + len > n_in || op + len > total) break;
+        lit.push_back(CopyJob{d.src + lv + ip + 1 + nb, d.dst + lv + op, len});
+        ip += 1 + nb + len;
+        op += len;
+      }
+      if (ip == n_in && op == total) {
+        P.copy_jobs.insert(P.copy_jobs.end(), lit.begin(), lit.end());
+        P.copy_bytes += total;
+        continue;
+      }
+    }
     SnapPage sp{d.src + lv + pre, d.dst + lv, uint32_t(d.csize - lv - pre), uint32_t(d.usize - lv),
                 uint32_t(P.block_page.size())};
     P.chunk_base.push_back(P.nchunks);

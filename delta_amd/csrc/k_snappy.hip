@@ -670,10 +670,15 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
       if (r >= nrec || !(sv & REC_LIT)) return;
       const uint32_t rel = uint32_t(wk & 0xffff);
       const uint32_t len = uint32_t((wk >> 16) & 0xffff) + 1;
-      if (len > EXEC_LONG || !staged) {
+      if (len > EXEC_LONG) {
         const uint32_t slot = atomicAdd(&s_nlong, 1u);
         if (slot < EXEC_LONG) s_long[slot] = r;
         else s_bad = 1;
+        return;
+      }
+      if (!staged) {  // a poorly compressible block: its input does not fit the stage; read it in place
+        const uint8_t* sp = in + (sv & ~REC_LIT);
+        for (uint32_t i = 0; i < len; ++i) bytes[rel + i] = sp[i];
         return;
       }
       // byte head up to a 4-byte aligned destination, then aligned dword stores of realigned
@@ -712,7 +717,7 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
   __syncthreads();
   stamp(5);
   const uint32_t nlong = min(s_nlong, EXEC_LONG);
-  for (uint32_t L = 0; L < nlong; ++L) {  // long literals (or no stage): the whole workgroup
+  for (uint32_t L = 0; L < nlong; ++L) {  // long literals: the whole workgroup
     const uint64_t w = a.recs[r0 + s_long[L]];
     const uint32_t rel = uint32_t(w & 0xffff);
     const uint32_t len = uint32_t((w >> 16) & 0xffff) + 1;

@@ -269,11 +269,20 @@ def replay_sharded(staged: Staged, min_file_retention_timestamp: int, exchange, 
     finally:
         sh.release()
     lc = local.counts
-    tot = exchange.all_reduce_sum([lc[k] for k in _SUMMED], dev)
+    # one all-gather carries both this rank's counters (first line) and its non-file winners: the
+    # counters are summed on every rank (key sums mod 2^64), the winners merged in rank order
+    head = json.dumps([_to_i64(lc[k]) for k in _SUMMED])
+    gathered = exchange.all_gather_text(head + "\n" + "\n".join(json.dumps(a) for a in local.nonfile))
+    tot = [0] * len(_SUMMED)
+    texts = []
+    for g in gathered:
+        first, _, rest = g.partition("\n")
+        for i, v in enumerate(json.loads(first)):
+            tot[i] += v
+        texts.append(rest)
     counts = dict(lc)
     for k, v in zip(_SUMMED, tot):
         counts[k] = v % _U64 if k.endswith("key_sum") else v
-    texts = exchange.all_gather_text("\n".join(json.dumps(a) for a in local.nonfile))
     nonfile, nc = merge_nonfile(texts, lc["version"], validate)
     counts.update(nc)
     # the local state carries the table-wide winners too (its checkpoint part 1 writes them)

@@ -729,7 +729,7 @@ static void plan_pages(StagedData& s, PagePlan& P) {
     SnapPage sp{d.src + lv + pre, d.dst + lv, uint32_t(d.csize - lv - pre), uint32_t(d.usize - lv),
                 uint32_t(P.block_page.size())};
     P.chunk_base.push_back(P.nchunks);
-    const uint32_t ncp = (sp.n_in + 255) / 256;
+    const uint32_t ncp = (sp.n_in + snappy_chunk_bytes() - 1) / snappy_chunk_bytes();
     P.chunk_page.insert(P.chunk_page.end(), ncp, uint32_t(P.snap_pages.size()));
     for (uint32_t j = 0; j < ncp; j += snappy_wg_chunks()) P.wg_chunk0.push_back(P.nchunks + j);
     P.nchunks += ncp;
@@ -757,7 +757,7 @@ static void plan_pages(StagedData& s, PagePlan& P) {
   up(P.d_copy, P.copy_jobs);
   up(P.d_wg_chunk0, P.wg_chunk0);
   P.s_spec_exit = DBuf<uint32_t>(s.ctx, P.nchunks);
-  P.s_vis = DBuf<uint32_t>(s.ctx, uint64_t(P.nchunks) * 8);
+  P.s_vis = DBuf<uint32_t>(s.ctx, uint64_t(P.nchunks) * (snappy_chunk_bytes() / 32));
   P.s_entry = DBuf<uint32_t>(s.ctx, P.nchunks);
   P.s_spec_first = DBuf<uint32_t>(s.ctx, P.nchunks);
   P.s_mid_first = DBuf<uint32_t>(s.ctx, P.nchunks);

@@ -6,7 +6,7 @@
 //
 //  A k_snap_spec    one lane per 256-byte chunk of compressed input parses elements
 //                   *speculatively* (starting 64 bytes early as a warm-up) and records the
-//                   positions it visited in the chunk (256-bit bitmap, kept in LDS) and where it left it.
+//                   positions it visited in the chunk (a bitmap in registers) and where it left it.
 //  B k_snap_assume / k_snap_entries: every chunk's true entry, in parallel: a chunk whose true
 //                   entry (the previous chunk's exit) is on its speculative chain is correct
 //                   (chains that meet coincide from then on); an isolated mis-speculated chunk is
@@ -34,7 +34,10 @@
 namespace dr {
 namespace dev {
 
-constexpr uint32_t SNAP_CH = 256;            // compressed bytes per speculation chunk
+#ifndef DR_SNAP_CH
+#define DR_SNAP_CH 256  // r02: 128 B chunks (512-chunk workgroups) took SNAPPY-minus-exec 0.904 -> 0.794 ms at scale 0.25, but two full-size config-3 pages then failed the size check and went serial
+#endif
+constexpr uint32_t SNAP_CH = DR_SNAP_CH;     // compressed bytes per speculation chunk (a multiple of 128)
 constexpr uint32_t SNAP_BLOCK = 65536;       // snappy compressor fragment size
 #ifndef DR_SNAP_WU
 #define DR_SNAP_WU 192
@@ -414,25 +417,37 @@ __global__ void __launch_bounds__(256) k_snap_count(SnappyArgs a) {
   a.chunk_elems[c] = elems;
 }
 
-// D: per-page exclusive scan of chunk outputs (one wave per page).
-__global__ void __launch_bounds__(64) k_snap_scan(SnappyArgs a) {
+// D: per-page exclusive scan of chunk outputs: one 256-thread workgroup per page, each thread
+// summing a contiguous run of chunks, a block scan of the run sums, then the run's prefixes.
+constexpr int SCAN_T = 256;
+__global__ void __launch_bounds__(SCAN_T) k_snap_scan(SnappyArgs a) {
+  __shared__ uint64_t wsum[SCAN_T / 64];
   const uint32_t p = blockIdx.x;
   if (p >= a.npages) return;
   const uint32_t c0 = a.chunk_base[p], nc = a.chunk_base[p + 1] - c0;
-  const int lane = threadIdx.x;
-  uint64_t carry = 0;
-  for (uint32_t base = 0; base < nc; base += 64) {
-    const uint32_t j = base + lane;
-    const uint64_t v = j < nc ? a.chunk_out[c0 + j] : 0;
-    uint64_t incl = v;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint64_t t = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += t;
-    }
-    if (j < nc) a.chunk_out_start[c0 + j] = uint32_t(carry + incl - v);
-    carry += __shfl(incl, 63, 64);
+  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint32_t per = (nc + SCAN_T - 1) / SCAN_T;
+  const uint32_t j0 = min(nc, t * per), j1 = min(nc, j0 + per);
+  uint64_t run = 0;
+  for (uint32_t j = j0; j < j1; ++j) run += a.chunk_out[c0 + j];
+  uint64_t incl = run;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(incl, o, 64);
+    if (lane >= uint32_t(o)) incl += y;
   }
-  if (lane == 0 && carry != a.pages[p].n_out) atomicOr(&a.pages_bad[p], 1u);  // size mismatch
+  if (lane == 63) wsum[wv] = incl;
+  __syncthreads();
+  uint64_t before = 0, total = 0;
+  for (uint32_t q = 0; q < SCAN_T / 64; ++q) {
+    before += q < wv ? wsum[q] : 0ull;
+    total += wsum[q];
+  }
+  uint64_t at = before + incl - run;
+  for (uint32_t j = j0; j < j1; ++j) {
+    a.chunk_out_start[c0 + j] = uint32_t(at);
+    at += a.chunk_out[c0 + j];
+  }
+  if (t == 0 && total != a.pages[p].n_out) atomicOr(&a.pages_bad[p], 1u);  // size mismatch
 }
 
 // E: one 8-byte record per element, {output offset in its 64 KiB block u16 | (len-1) u16 << 16 |
@@ -792,6 +807,7 @@ __global__ void __launch_bounds__(256) k_page_copy(const CopyJob* jobs, uint32_t
 }  // namespace dev
 
 uint32_t snappy_wg_chunks() { return dev::WG_CHUNKS; }
+uint32_t snappy_chunk_bytes() { return dev::SNAP_CH; }
 
 void launch_snappy(const SnappyArgs& a, hipStream_t st, void* scan_scratch) {
   if (!a.npages) return;
@@ -802,7 +818,7 @@ void launch_snappy(const SnappyArgs& a, hipStream_t st, void* scan_scratch) {
   DR_LAUNCH(dev::k_snap_regions, dim3(g), dim3(256), 0, st, a);
   DR_LAUNCH(dev::k_snap_resolve, dim3(512), dim3(64), 0, st, a);
   DR_LAUNCH(dev::k_snap_count, dim3(g), dim3(256), 0, st, a);
-  DR_LAUNCH(dev::k_snap_scan, dim3(a.npages), dim3(64), 0, st, a);
+  DR_LAUNCH(dev::k_snap_scan, dim3(a.npages), dim3(dev::SCAN_T), 0, st, a);
   launch_scan_u32(a.chunk_elems, a.chunk_rec_start, a.nchunks, scan_scratch, st);
   DR_LAUNCH(dev::k_snap_emit, dim3(a.nwg), dim3(2 * dev::WG_CHUNKS), 0, st, a);
   DR_LAUNCH(dev::k_snap_exec, dim3(a.nblocks), dim3(dev::EXEC_T), 0, st, a);

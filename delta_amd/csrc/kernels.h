@@ -170,6 +170,7 @@ struct SnappyArgs {
   const uint32_t* chunk_page = nullptr;  // [nchunks] page of each chunk
 };
 uint32_t snappy_wg_chunks();
+uint32_t snappy_chunk_bytes();
 void launch_snappy(const SnappyArgs& a, hipStream_t st, void* scan_scratch);
 void launch_page_copy(const CopyJob* jobs, uint32_t njobs, hipStream_t st);
 

@@ -3,7 +3,7 @@ set -e
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
 cd $R
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_checkpoint.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/par.log 2>&1 || { tail -40 gpurun_out/par.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_checkpoint.py tests/test_gpu_edge_cases.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/par.log 2>&1 || { tail -40 gpurun_out/par.log; exit 1; }
 tail -2 gpurun_out/par.log
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 python $R/scripts/diag_snappy.py 3 1.0 2 > $R/gpurun_out/diag.log 2>&1 || { tail -20 $R/gpurun_out/diag.log; exit 1; }

@@ -315,8 +315,8 @@ __global__ void __launch_bounds__(256) k_snap_regions(SnappyArgs a) {
 
 // B3b: one wave per region: from RESOLVE_MARGIN chunks before the flag (entries there are exact)
 // the true chain is followed 64 chunks per ballot, rewriting entries, until a whole 64-chunk step
-// beyond the flag has no break and agrees with the entries k_snap_entries wrote (from there on
-// they are exact again). A chunk whose entry lies past its end (a long literal spans it) jumps to
+// beyond the flag has no break, agrees with the entries k_snap_entries wrote (from there on they
+// are exact again) and has no flag in it or within REGION_GAP after it. A chunk whose entry lies past its end (a long literal spans it) jumps to
 // the chunk holding that entry.
 __global__ void __launch_bounds__(64) k_snap_resolve(SnappyArgs a) {
   const uint64_t nreg = *a.region_count;
@@ -349,7 +349,15 @@ __global__ void __launch_bounds__(64) k_snap_resolve(SnappyArgs a) {
       if (valid && uint32_t(lane) <= f) a.entry[c0 + j] = cv;
       const uint32_t cnt = min(64u, nc - base);
       if (f >= cnt) {
-        if (agree && base > jf) break;  // back in step with k_snap_entries
+        if (agree && base > jf) {
+          // back in step with k_snap_entries -- unless a flagged chunk lies in this window or within
+          // REGION_GAP after it: such a flag starts no region of its own (k_snap_regions), so this
+          // walk must carry on through it (r02: a page whose flags 70 chunks apart were left with an
+          // unknown entry went to the serial decoder)
+          bool fl = false;
+          for (uint32_t q = base + uint32_t(lane); q < min(nc, base + cnt + REGION_GAP); q += 64) fl |= a.chunk_flag[c0 + q] != 0;
+          if (__ballot(fl) == 0ull) break;
+        }
         e = uint32_t(__builtin_amdgcn_readlane(int(x), int(cnt - 1)));
         base += cnt;
         continue;

@@ -618,3 +618,28 @@ def test_incompressible_snappy_pages(engine, tmp_path, capfd, monkeypatch):
     assert counts["num_files"] == 120000
     err = capfd.readouterr().err
     assert "snappy bad page" not in err, err[-2000:]
+
+
+def test_snappy_periodic_dictionary_pages(engine, tmp_path, capfd, monkeypatch):
+    """Dictionary pages of consecutive int64 values compress to a period-4 element stream on which a
+    mis-aligned speculative walk never meets the true chain; the entry resolver must carry on
+    through every flagged chunk that starts no region of its own (these two pages -- the layouts of
+    config 3's modificationTime dictionaries -- reproduced the r02 serial fallbacks; CPU restatement
+    of the resolver in the commit that fixed it). Replay and export equal the oracle, no page
+    falls back to the serial decoder."""
+    from delta_amd.testing import synth as S
+    lp = str(tmp_path / "_delta_log")
+    os.makedirs(lp)
+    t0 = 1_700_000_000_000
+    adds = [{"path": "p%05d" % i, "partitionValues": {}, "size": t0 + 44 * 60000 + i,
+             "modificationTime": t0 + 3 * 60000 + i} for i in range(60000)]
+    rms = [{"path": "r%05d" % i, "deletionTimestamp": t0 + 3 * 60000 + i} for i in range(60000)]
+    S.write_checkpoint_records(os.path.join(lp, "%020d.checkpoint.parquet" % 0), PROTOCOL["protocol"],
+                               METADATA["metaData"], adds, rms, use_dictionary=True)
+    with open(os.path.join(lp, "_last_checkpoint"), "w") as f:
+        f.write('{"version":0,"size":120002}\n')
+    monkeypatch.setenv("DR_SNAP_DEBUG", "1")
+    counts, live, tomb = _same_as_oracle(engine, lp, cutoff=t0 + 3 * 60000 + 30000)
+    assert counts["num_files"] == 60000 and len(tomb) == 29999
+    err = capfd.readouterr().err
+    assert "snappy bad page" not in err, err[-2000:]

@@ -1,7 +1,7 @@
 # CPU restatement of k_snappy.hip's chunk speculation, entry rules and region resolver (spec /
 # assume / entries / regions / resolve), used to find and check the r02 resolver fix: run
 # resolve_all(pyarrow.compress(data, "snappy", asbytes=True)) with FIX = False / True.
-FIX = False
+FIX = True  # the r02 stop rule (False: the earlier one)
 """CPU simulation of k_snappy.hip's chunk speculation + entry rules (spec/assume/entries) to find
 chunks whose entries are wrong without being flagged."""
 import sys

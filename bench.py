@@ -62,12 +62,10 @@ def build_table(path, config, scale, seed=None, workers=16):
 
 def algorithmic_bytes(kernel, plan, counts):
     """Compulsory HBM bytes of one launch of `kernel`: each input it needs read once,
-    each output written once."""
+    each output written once. `counts` are the replay's own counters (None for a rank of the library's
+    sharded replay, whose reduce-side action count the bench does not see: K3/K4 then go unpriced)."""
     rows = plan["checkpoint_rows"]
-    lines = counts["num_actions"] - rows
-    n = counts["num_actions"]
-    fa = counts["num_file_actions"]
-    surv = counts["num_files"] + counts["num_removes"]
+    lines = plan.get("json_lines", counts["num_actions"] - rows if counts else 0)
     ch, el = plan["snappy_chunks"], plan["snappy_elements"]
     sin, sout = plan["snappy_in_bytes"], plan["snappy_out_bytes"]
     table = {
@@ -81,11 +79,17 @@ def algorithmic_bytes(kernel, plan, counts):
         "k_snap_exec": 8 * el + sin + sout,                        # records + literal bytes in, page bytes out
         "k_pq_data": plan["pages_decompressed_bytes"] + 44 * rows,
         "k_ckpt_assemble": 182 * rows,
-        "k_bucket_hist": 30 * n,                                   # kind, flags, key, path ref in; packed ref out
-        "k_bucket_scatter": 18 * n + 16 * fa,                      # kind, flags, key, size/delTs in; 16 B record out
-        "k_bucket_reduce": 16 * fa + 4 * surv,
-        "k_compact2": 8 * surv,
     }
+    if counts:
+        n = counts["num_actions"]
+        fa = counts["num_file_actions"]
+        surv = counts["num_files"] + counts["num_removes"]
+        table.update({
+            "k_bucket_hist": 30 * n,                               # kind, flags, key, path ref in; packed ref out
+            "k_bucket_scatter": 18 * n + 16 * fa,                  # kind, flags, key, size/delTs in; 16 B record out
+            "k_bucket_reduce": 16 * fa + 4 * surv,
+            "k_compact2": 8 * surv,
+        })
     if kernel in ("k_snap_emit", "k_snap_exec") and not el:
         return None
     return table.get(kernel)
@@ -117,39 +121,65 @@ def pmc_traffic(pmc_dir, kernel):
     return int(2 * avg["FETCH_SIZE"] * 1024 + avg["WRITE_SIZE"] * 1024)  # KiB -> bytes
 
 
-def run_replay_oracle(log_path, cutoff, threads):
+def run_replay_oracle(log_path, cutoff, threads, record_sums=False):
     exe = os.path.join(ROOT, "oracle", "_build", "replay_oracle")
-    r = subprocess.run([exe, log_path, str(cutoff), "--threads", str(threads), "--partitions", "50"],
-                       capture_output=True, text=True, timeout=900)
+    r = subprocess.run([exe, log_path, str(cutoff), "--threads", str(threads), "--partitions", "50"]
+                       + (["--record-sums"] if record_sums else []), capture_output=True, text=True, timeout=900)
     if r.returncode != 0:
         log("cpu baseline failed:", r.stderr[-2000:])
         return None
     return json.loads(r.stdout.strip().splitlines()[-1])
 
 
-def cpu_baseline(log_path, cutoff, counts, threads, one_core=True):
-    """oracle/_build/replay_oracle on the same table: all host threads given, then one."""
+def cpu_budget():
+    """(affinity CPUs, cgroup v2 cpu.max quota in CPUs or None): what this process may run on. On the
+    GPU box os.cpu_count() shows the whole machine; the affinity mask and the quota are the share."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(q) // int(per))
+    except (OSError, ValueError):
+        pass
+    return aff, quota
+
+
+def cpu_baseline(log_path, cutoff, counts, threads, one_core=True, share=16):
+    """oracle/_build/replay_oracle on the same table: on every CPU this process may
+    use (`threads`, or the affinity mask), on the per-GPU CPU share when that differs, and on one core.
+    Its counters and order-free key sums (incl. the full-record sums) must equal the GPU's."""
     if not os.path.exists(os.path.join(ROOT, "oracle", "_build", "replay_oracle")):
         return None
-    res = run_replay_oracle(log_path, cutoff, threads)
+    aff, quota = cpu_budget()
+    threads = threads or aff
+    res = run_replay_oracle(log_path, cutoff, threads, record_sums="live_record_sum" in counts)
     if res is None:
         return None
-    keys = ("num_files", "size_in_bytes", "num_removes", "num_file_actions", "live_key_sum", "tomb_key_sum")
+    keys = [k for k in ("num_files", "size_in_bytes", "num_removes", "num_file_actions", "live_key_sum",
+                        "tomb_key_sum", "live_record_sum", "tomb_record_sum") if k in res and k in counts]
     mism = {k: (res[k], counts[k]) for k in keys if res[k] != counts[k]}
     if mism:
         log("FULL-SCALE PARITY MISMATCH (cpu, gpu):", mism)
     out = {"value": round(res["num_actions"] / res["total_s"], 1), "unit": "actions/s", "cores": threads,
+           "nproc": os.cpu_count(), "affinity_cpus": aff, "cgroup_quota_cpus": quota,
            "kind": "port", "parse_s": res["parse_s"], "replay_s": res["replay_s"], "read_s": res["read_s"],
            "sample": "the full benchmark table (%d actions: %d checkpoint rows + JSON lines), bytes in memory "
-                     "before the clock; C++ restatement of the replay: Parquet+SNAPPY and JSON decode, "
-                     "canonicalize, 50 hash partitions, per-partition last-writer-wins, retention, sort by path"
-                     % (res["num_actions"], res["checkpoint_rows"]),
-           "matches_gpu": not mism}
+                     "before the clock; C++ restatement of the replay (not Spark: no JVM on the box): "
+                     "Parquet+SNAPPY and JSON decode, canonicalize, 50 hash partitions, per-partition "
+                     "last-writer-wins, retention, sort by path" % (res["num_actions"], res["checkpoint_rows"]),
+           "compared": keys, "matches_gpu": not mism, "record_pass_s": res.get("record_s")}
+    runs = []
+    if share and share != threads:
+        runs.append(("per_gpu_share", share))
     if one_core:
-        r1 = run_replay_oracle(log_path, cutoff, 1)
-        if r1:
-            out["one_core"] = {"value": round(r1["num_actions"] / r1["total_s"], 1), "parse_s": r1["parse_s"],
-                               "replay_s": r1["replay_s"]}
+        runs.append(("one_core", 1))
+    for name, t in runs:
+        r = run_replay_oracle(log_path, cutoff, t)
+        if r:
+            out[name] = {"cores": t, "value": round(r["num_actions"] / r["total_s"], 1), "parse_s": r["parse_s"],
+                         "replay_s": r["replay_s"]}
     return out
 
 
@@ -227,16 +257,30 @@ def measure_stream(eng, table, exp, args):
     keys = ("num_files", "size_in_bytes", "num_removes", "num_actions", "num_file_actions", "live_key_sum",
             "tomb_key_sum", "version")
     mism = {k: (cur.counts[k], full.counts[k]) for k in keys if cur.counts[k] != full.counts[k]}
+    rec_cur, rec_full = cur.record_sums(), full.record_sums()  # full records of both sides (untimed)
+    if rec_cur != rec_full:
+        mism["record_sums"] = (rec_cur, rec_full)
     if mism:
         log("STREAM PARITY MISMATCH (applied, full replay):", mism)
-    counts = dict(cur.counts)
+    counts = dict(cur.counts, live_record_sum=rec_cur[0], tomb_record_sum=rec_cur[1])
     full.release()
     cur.release()
     base_counts = dict(base.counts)
     base.release()
     cpu = None
     if not args.no_cpu_baseline:
-        cpu = cpu_baseline(log_path, final_cut, counts, args.cpu_threads, one_core=False)
+        cpu = cpu_baseline(log_path, final_cut, counts, args.cpu_threads, one_core=False, share=0)
+    if cpu:
+        # the reference has no incremental path: every DeltaLog.update() rebuilds the snapshot from
+        # its checkpoint + deltas (D/SnapshotManagement.scala:286-330), so its
+        # per-commit cost is one full replay of the final segment
+        per_commit_s = cpu["value"] and counts["num_actions"] / cpu["value"]
+        cpu["full_replay_actions_per_s"] = cpu["value"]
+        cpu["per_commit_ms"] = round(per_commit_s * 1e3, 2)
+        cpu["value"] = round(tail_actions / len(commits) / per_commit_s, 2)
+        cpu["sample"] = ("one full replay of the final segment (%d actions) per update(), the reference's cost per "
+                         "commit (no incremental state, D/SnapshotManagement.scala:286-330); value = tail "
+                         "actions per second at that rate. " % counts["num_actions"]) + cpu["sample"]
     kernels = {k: round(v / max(1, n_timed - 1), 4) for k, v in sorted(kern.items(), key=lambda x: -x[1])}
     apply_total_s = sum(rest) / 1e3
     return {
@@ -262,7 +306,8 @@ def measure_stream(eng, table, exp, args):
                      "note": "per-commit kernels touch a few KB: launch/latency-bound, no bandwidth roofline"},
         "cpu_baseline": cpu,
         "kernels_per_commit_ms": kernels,
-        "result": {k: counts[k] for k in ("num_files", "num_removes", "size_in_bytes", "live_key_sum", "tomb_key_sum")},
+        "result": {k: counts[k] for k in ("num_files", "num_removes", "size_in_bytes", "live_key_sum", "tomb_key_sum",
+                                          "live_record_sum", "tomb_record_sum")},
     }
 
 
@@ -320,6 +365,21 @@ def measure_filter(eng, staged, cutoff, exp, steps):
             "kernels": {k: round(v, 4) for k, v in ms.items()}}
 
 
+def launch_ranks(args) -> int:
+    """`--gpus N` (N > 1) without a launcher around us: start N rank processes of this same command
+    through torch.distributed.run (one rank per GPU, rendezvous on 127.0.0.1) and return their exit
+    status. This process has not touched the GPU (no HIP call, not even a device count), so it may
+    start them; the ranks check the device count themselves and fail loudly when it is short."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    log("bench.py: launching %d ranks: %s" % (args.gpus, " ".join(cmd)))
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -327,30 +387,49 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=3)
     ap.add_argument("--scale", type=float, default=1.0)
-    ap.add_argument("--cpu-threads", type=int, default=16, help="the GPU box's CPU share per GPU")
-    ap.add_argument("--pmc-dir", default=os.path.join(ROOT, "profiles", "r02", "pmc"))
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0: every CPU this process may use, see cpu_budget())")
+    ap.add_argument("--pmc-dir", default=None,
+                    help="rocprofv3 --pmc passes of this build and config (default profiles/r03/pmc/c<config>)")
+    ap.add_argument("--driver", choices=("lib", "torch"), default="lib",
+                    help="N > 1: the library's own RCCL replay (dr_replay_sharded, what a JNI host calls) or "
+                         "delta_amd/sharded.py over torch.distributed")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="time the steps without the roofline kernel's events")
     ap.add_argument("--profile-steps", type=int, default=3, help="untimed steps with an event pair on every launch")
     ap.add_argument("--workdir", default=os.environ.get("DR_BENCH_DIR", os.path.join(tempfile.gettempdir(), "dr_bench")))
     args = ap.parse_args()
+    if args.pmc_dir is None:
+        args.pmc_dir = os.path.join(ROOT, "profiles", "r03", "pmc", "c%d" % args.config)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    if world != args.gpus:
+        raise SystemExit("bench.py --gpus %d but WORLD_SIZE=%d: one rank per GPU" % (args.gpus, world))
 
     import torch
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     backend = None
     if world > 1:
         import torch.distributed as dist
-        # DR_BENCH_BACKEND=gloo rehearses the multi-rank path on a single GPU (host-staged exchange)
+        # DR_BENCH_BACKEND=gloo rehearses the torch driver on a single GPU (host-staged exchange)
         backend = os.environ.get("DR_BENCH_BACKEND", "nccl")
-        local = local % max(torch.cuda.device_count(), 1)
+        if backend == "gloo":
+            args.driver = "torch"
+        ndev = torch.cuda.device_count()
+        if backend == "nccl" and ndev < world:
+            raise SystemExit("bench.py --gpus %d: only %d GPU(s) visible to rank %d (RCCL needs one GPU per rank)"
+                             % (world, ndev, rank))
+        local = local % max(ndev, 1)
         torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.driver == "lib" or backend != "nccl":
+            # the library driver exchanges over its own RCCL communicator; torch.distributed only
+            # carries the communicator id, the barriers and the max-over-ranks time (host, gloo)
+            dist.init_process_group("gloo")
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     from delta_amd.delta_log import Engine
     from delta_amd.testing import synth as S
 
@@ -378,6 +457,19 @@ def main():
             c = st.counts
             st.release()
             return c, c
+    elif args.driver == "lib":
+        from delta_amd.sharded import stage_shard
+        box = [Engine.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        comm = eng.comm(box[0], world, rank)
+        staged = stage_shard(eng, log_path, world, rank)
+        stage_s = time.perf_counter() - t_stage
+
+        def step():
+            st = comm.replay_sharded(staged, cutoff)
+            c = st.counts  # table-wide counters (all-reduced inside the library)
+            st.release()
+            return c, None
     else:
         from delta_amd.sharded import Exchange, replay_sharded, stage_shard
         staged = stage_shard(eng, log_path, world, rank)
@@ -430,7 +522,8 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+        on_dev = backend == "nccl" and args.driver == "torch"
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if on_dev else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     eng.set_timing(False)
@@ -470,15 +563,24 @@ def main():
                 "achieved": round(gbs, 1) if gbs else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(gbs / HBM_PEAK_GBS, 4) if gbs else None}
 
-    lines = local_counts["num_actions"] - plan["checkpoint_rows"]
+    lines = plan["json_lines"]
     pipelines = {
         "json": pipeline(JSON, plan["json_bytes"] + 58 * lines),
         # compulsory SNAPPY traffic: compressed pages in, decompressed pages out
         "snappy": pipeline(SNAPPY, plan["snappy_in_bytes"] + plan["snappy_out_bytes"]),
         # K3 + K4 together against SURVEY.md §8(d)'s headline budget: 32 B/action (sort) + 37 B/action
         # (reduce, retention, compaction) = 69 B/action
-        "sort_reduce": dict(pipeline(SORT_REDUCE, 69 * local_counts["num_actions"]), target_frac=0.5),
+        "sort_reduce": dict(pipeline(SORT_REDUCE, 69 * local_counts["num_actions"]), target_frac=0.5)
+        if local_counts else None,
     }
+    if world == 1:
+        # full-record checksums of both sides on the device (untimed), for the full-size parity gate
+        st = staged.replay(cutoff)
+        t_r = time.perf_counter()
+        rec = st.record_sums()
+        record_s = time.perf_counter() - t_r
+        st.release()
+        counts = dict(counts, live_record_sum=rec[0], tomb_record_sum=rec[1])
     cpu = None
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(log_path, cutoff, counts, args.cpu_threads, one_core=args.config != 4)
@@ -512,9 +614,10 @@ def main():
         "config": {"workload": WORKLOAD.get(args.config, "config %d") % (counts["num_actions"], counts["num_files"]),
                    "scale": args.scale, "actions": counts["num_actions"],
                    "json_bytes": exp["json_bytes"], "checkpoint_bytes": exp["checkpoint_bytes"],
-                   "parallelism": ("path-hash shards over %d GPUs (%s all-to-all)"
-                                   % (world, "RCCL" if backend == "nccl" else "gloo rehearsal")) if world > 1
-                   else "single GPU"},
+                   "parallelism": ("path-hash shards over %d GPUs (%s all-to-all, %s driver)"
+                                   % (world, "RCCL" if backend == "nccl" else "gloo rehearsal",
+                                      "dr_replay_sharded" if args.driver == "lib" else "torch.distributed"))
+                   if world > 1 else "single GPU"},
         "roofline": roofline,
         "pipelines": pipelines,
         "cpu_baseline": cpu,
@@ -522,8 +625,9 @@ def main():
         "k5_filter": k5,
         "checkpoint_write": ckpt,
         "kernels": kernels,
-        "result": {k: counts[k] for k in ("num_files", "num_removes", "size_in_bytes", "live_key_sum",
-                                          "tomb_key_sum")},
+        "result": dict({k: counts[k] for k in ("num_files", "num_removes", "size_in_bytes", "live_key_sum",
+                                               "tomb_key_sum", "live_record_sum", "tomb_record_sum") if k in counts},
+                       record_sums_s=round(record_s, 3) if world == 1 else None),
     }
     print(json.dumps(out), flush=True)
 

@@ -9,6 +9,7 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <atomic>
 #include <functional>
 #include <type_traits>
 #include <cstring>
@@ -18,6 +19,7 @@
 #include <cstdio>
 #include <map>
 #include <chrono>
+#include <condition_variable>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -1794,7 +1796,7 @@ static void export_device(dr_state& st, int which, DevExport& X, uint64_t lo = 0
   launch_scan_u32(X.path_len.p, X.path_off.p, n, scratch.p, stream);
   if (!n) HIP_OK(hipMemsetAsync(X.path_off.p, 0, 8, stream));
   const uint64_t nb = n ? d2h_one(X.path_off.p + n, stream) : 0;
-  X.path_bytes = DBuf<uint8_t>(ctx, nb + 1);
+  X.path_bytes = DBuf<uint8_t>(ctx, nb + 16);  // +16: whole-word loads of the record hash
   launch_gather_bytes(X.path_ptr.p, X.path_len.p, X.path_off.p, n, X.path_bytes.p, stream);
   if (!st.exp_dec[which]) {
     auto d = std::make_shared<ExpDecoded>();
@@ -1855,11 +1857,11 @@ static void export_device(dr_state& st, int which, DevExport& X, uint64_t lo = 0
   }
   for (int k = 0; k < EXC_N && n; ++k) X.tot[k] = d2h_one(X.off[k].p + n, stream);
   if (d2h_one(err.p, stream)) fail(DR_E_PARSE, "malformed survivor line at export");
-  X.stats_bytes = DBuf<uint8_t>(ctx, X.tot[EXC_STATS] + 1);
-  X.pv_key_bytes = DBuf<uint8_t>(ctx, X.tot[EXC_PV_KB] + 1);
-  X.pv_val_bytes = DBuf<uint8_t>(ctx, X.tot[EXC_PV_VB] + 1);
-  X.tags_key_bytes = DBuf<uint8_t>(ctx, X.tot[EXC_TAGS_KB] + 1);
-  X.tags_val_bytes = DBuf<uint8_t>(ctx, X.tot[EXC_TAGS_VB] + 1);
+  X.stats_bytes = DBuf<uint8_t>(ctx, X.tot[EXC_STATS] + 16);
+  X.pv_key_bytes = DBuf<uint8_t>(ctx, X.tot[EXC_PV_KB] + 16);
+  X.pv_val_bytes = DBuf<uint8_t>(ctx, X.tot[EXC_PV_VB] + 16);
+  X.tags_key_bytes = DBuf<uint8_t>(ctx, X.tot[EXC_TAGS_KB] + 16);
+  X.tags_val_bytes = DBuf<uint8_t>(ctx, X.tot[EXC_TAGS_VB] + 16);
   X.pv_val_null = DBuf<uint8_t>(ctx, X.tot[EXC_PV_N] + 1);
   X.tags_val_null = DBuf<uint8_t>(ctx, X.tot[EXC_TAGS_N] + 1);
   X.pv_key_off = DBuf<int64_t>(ctx, X.tot[EXC_PV_N] + 1);
@@ -1881,6 +1883,47 @@ static void export_device(dr_state& st, int which, DevExport& X, uint64_t lo = 0
   a.tags_key_bytes = X.tags_key_bytes.p;
   a.tags_val_bytes = X.tags_val_bytes.p;
   launch_export(a, stream);  // pass 2: bytes and entries
+}
+
+// Order-free full-record checksum of one side (dr_state_record_sums): k_record_hash over the
+// side's device export columns.
+static uint64_t record_sum(dr_state& st, int which) {
+  dr_ctx* ctx = st.ctx;
+  hipStream_t stream = ctx->stream;
+  DevExport X;
+  export_device(st, which, X);
+  DBuf<unsigned long long> sum(ctx, 1);
+  sum.zero(stream);
+  RecordHashArgs a{};
+  a.n = X.n;
+  a.side = which == DR_LIVE ? 0 : 1;
+  a.path_bytes = X.path_bytes.p;
+  a.path_off = X.path_off.p;
+  a.size = X.size.p;
+  a.mtime = X.mtime.p;
+  a.delts = X.delts.p;
+  a.flags = X.flags.p;
+  a.efm = X.efm.p;
+  a.stats_null = X.stats_null.p;
+  a.stats_off = X.off[EXC_STATS].p;
+  a.stats_bytes = X.stats_bytes.p;
+  a.pv_null = X.pv_null.p;
+  a.pv_entry = X.off[EXC_PV_N].p;
+  a.pv_key_off = X.pv_key_off.p;
+  a.pv_key_bytes = X.pv_key_bytes.p;
+  a.pv_val_off = X.pv_val_off.p;
+  a.pv_val_bytes = X.pv_val_bytes.p;
+  a.pv_val_null = X.pv_val_null.p;
+  a.tags_null = X.tags_null.p;
+  a.tags_entry = X.off[EXC_TAGS_N].p;
+  a.tags_key_off = X.tags_key_off.p;
+  a.tags_key_bytes = X.tags_key_bytes.p;
+  a.tags_val_off = X.tags_val_off.p;
+  a.tags_val_bytes = X.tags_val_bytes.p;
+  a.tags_val_null = X.tags_val_null.p;
+  a.sum = sum.p;
+  launch_record_hash(a, stream);
+  return uint64_t(d2h_one(sum.p, stream));
 }
 
 static void build_export(dr_state& st, int which) {
@@ -3529,18 +3572,115 @@ static Rccl& rccl() {
     if (rc_ != ncclSuccess) fail(DR_E_DEVICE, std::string("RCCL: ") + rccl().err(rc_) + " (" #x ")"); \
   } while (0)
 
+// In-process stand-in for an RCCL communicator (test hook, dr_comm_loopback_id): the ranks are threads
+// of this process, each with its own dr_ctx. Every collective publishes this rank's device buffers,
+// meets the others at a barrier, copies what it receives from the peers' buffers on its own stream
+// and meets them again before anyone may reuse a buffer -- so replay_sharded_rccl's own control flow
+// (count matrix, byte all-to-alls, verdict return, counter all-reduce, non-file all-gather) runs at
+// W > 1 on one GPU. A rank that fails aborts the group: the others fail instead of waiting.
+struct LoopGroup {
+  int32_t world = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  int32_t arrived = 0;
+  uint64_t gen = 0;
+  bool aborted = false;
+  std::vector<const uint8_t*> ptr;             // each rank's published send buffer
+  std::vector<const uint64_t*> cnt;            // each rank's per-peer byte counts (all-to-all)
+  void barrier() {
+    std::unique_lock<std::mutex> g(mu);
+    if (aborted) fail(DR_E_INTERNAL, "loopback communicator aborted by another rank");
+    const uint64_t my = gen;
+    if (++arrived == world) {
+      arrived = 0;
+      ++gen;
+      cv.notify_all();
+      return;
+    }
+    if (!cv.wait_for(g, std::chrono::seconds(120), [&] { return gen != my || aborted; }))
+      fail(DR_E_INTERNAL, "loopback communicator: a rank did not arrive within 120 s");
+    if (aborted) fail(DR_E_INTERNAL, "loopback communicator aborted by another rank");
+  }
+  void abort() {
+    std::lock_guard<std::mutex> g(mu);
+    aborted = true;
+    cv.notify_all();
+  }
+};
+
+static std::mutex g_loop_mu;
+static std::map<uint64_t, std::weak_ptr<LoopGroup>> g_loop_groups;
+static const char kLoopMagic[8] = {'D', 'R', 'L', 'O', 'O', 'P', 'B', 'K'};
+
 struct dr_comm {
   dr_ctx* ctx = nullptr;
   ncclComm_t comm = nullptr;
+  std::shared_ptr<LoopGroup> loop;  // set: loopback transport instead of RCCL
   int32_t world = 1, rank = 0;
 };
+
+// The collectives replay_sharded_rccl needs, over RCCL or the loopback group.
+static void comm_all_gather(dr_comm& c, const void* send, void* recv, uint64_t bytes) {
+  hipStream_t stream = c.ctx->stream;
+  if (!c.loop) {
+    RC_OK(rccl().all_gather(send, recv, bytes, ncclUint8, c.comm, stream));
+    return;
+  }
+  LoopGroup& g = *c.loop;
+  HIP_OK(hipStreamSynchronize(stream));
+  g.ptr[c.rank] = static_cast<const uint8_t*>(send);
+  g.barrier();
+  for (int32_t p = 0; p < c.world; ++p)
+    if (bytes) HIP_OK(hipMemcpyAsync(static_cast<uint8_t*>(recv) + uint64_t(p) * bytes, g.ptr[p], bytes,
+                                     hipMemcpyDeviceToDevice, stream));
+  HIP_OK(hipStreamSynchronize(stream));
+  g.barrier();
+}
+
+static void comm_all_reduce_sum_i64(dr_comm& c, int64_t* buf, uint64_t n) {
+  hipStream_t stream = c.ctx->stream;
+  if (!c.loop) {
+    RC_OK(rccl().all_reduce(buf, buf, n, ncclInt64, ncclSum, c.comm, stream));
+    return;
+  }
+  LoopGroup& g = *c.loop;
+  const std::vector<int64_t> mine = d2h(buf, n, stream);
+  g.ptr[c.rank] = reinterpret_cast<const uint8_t*>(mine.data());  // host vectors: summed on the host
+  g.barrier();
+  std::vector<uint64_t> tot(n, 0);
+  for (int32_t p = 0; p < c.world; ++p)
+    for (uint64_t i = 0; i < n; ++i) tot[i] += uint64_t(reinterpret_cast<const int64_t*>(g.ptr[p])[i]);
+  g.barrier();
+  HIP_OK(hipMemcpyAsync(buf, tot.data(), n * 8, hipMemcpyHostToDevice, stream));
+  HIP_OK(hipStreamSynchronize(stream));
+}
 
 // All-to-all of byte ranges: send[so_p, so_p + scnt[p]) to each peer p, recv rcnt[p] bytes from each
 // peer in rank order (grouped point-to-point: the xGMI links are peer-to-peer).
 static void rccl_all_to_all(dr_comm& c, const uint8_t* send, const std::vector<uint64_t>& scnt, uint8_t* recv,
                             const std::vector<uint64_t>& rcnt) {
-  Rccl& R = rccl();
   hipStream_t stream = c.ctx->stream;
+  if (c.loop) {
+    LoopGroup& g = *c.loop;
+    HIP_OK(hipStreamSynchronize(stream));
+    g.ptr[c.rank] = send;
+    g.cnt[c.rank] = scnt.data();
+    g.barrier();
+    uint64_t ro = 0;
+    for (int32_t p = 0; p < c.world; ++p) {
+      uint64_t so = 0;
+      for (int32_t q = 0; q < c.rank; ++q) so += g.cnt[p][q];
+      if (g.cnt[p][c.rank] != rcnt[p])
+        fail(DR_E_INTERNAL, fmt("loopback all-to-all: rank %d sends %llu bytes to rank %d, which expects %llu", p,
+                                (unsigned long long)g.cnt[p][c.rank], c.rank, (unsigned long long)rcnt[p]));
+      if (rcnt[p]) HIP_OK(hipMemcpyAsync(recv + ro, g.ptr[p] + so, rcnt[p], hipMemcpyDeviceToDevice, stream));
+      ro += rcnt[p];
+    }
+    HIP_OK(hipStreamSynchronize(stream));
+    g.barrier();
+    return;
+  }
+  Rccl& R = rccl();
   RC_OK(R.group_start());
   uint64_t so = 0, ro = 0;
   for (int32_t p = 0; p < c.world; ++p) {
@@ -3553,19 +3693,18 @@ static void rccl_all_to_all(dr_comm& c, const uint8_t* send, const std::vector<u
 }
 
 static std::vector<std::string> rccl_all_gather_text(dr_comm& c, const std::string& mine) {
-  Rccl& R = rccl();
   dr_ctx* ctx = c.ctx;
   hipStream_t stream = ctx->stream;
   DBuf<uint64_t> len(ctx, 1), lens(ctx, c.world);
   const uint64_t n = mine.size();
   HIP_OK(hipMemcpyAsync(len.p, &n, 8, hipMemcpyHostToDevice, stream));
-  RC_OK(R.all_gather(len.p, lens.p, 1, ncclUint64, c.comm, stream));
+  comm_all_gather(c, len.p, lens.p, 8);
   const std::vector<uint64_t> L = d2h(lens.p, c.world, stream);
   uint64_t mx = 1;
   for (uint64_t x : L) mx = std::max(mx, x);
   DBuf<uint8_t> slot(ctx, mx), all(ctx, mx * c.world);
   if (n) HIP_OK(hipMemcpyAsync(slot.p, mine.data(), n, hipMemcpyHostToDevice, stream));
-  RC_OK(R.all_gather(slot.p, all.p, mx, ncclUint8, c.comm, stream));
+  comm_all_gather(c, slot.p, all.p, mx);
   const std::vector<uint8_t> h = d2h(all.p, mx * c.world, stream);
   std::vector<std::string> out;
   for (int32_t p = 0; p < c.world; ++p)
@@ -3604,7 +3743,6 @@ static dr_state* replay_sharded_rccl(dr_comm& c, const std::shared_ptr<StagedDat
                                      uint32_t flags) {
   dr_ctx* ctx = c.ctx;
   hipStream_t stream = ctx->stream;
-  Rccl& R = rccl();
   const uint32_t W = uint32_t(c.world);
   dr_shard sh;
   sh.ctx = ctx;
@@ -3617,7 +3755,7 @@ static dr_state* replay_sharded_rccl(dr_comm& c, const std::shared_ptr<StagedDat
   std::vector<uint64_t> m(sc);
   m.insert(m.end(), sb.begin(), sb.end());
   HIP_OK(hipMemcpyAsync(mine.p, m.data(), 16 * W, hipMemcpyHostToDevice, stream));
-  RC_OK(R.all_gather(mine.p, all.p, 2 * W, ncclUint64, c.comm, stream));
+  comm_all_gather(c, mine.p, all.p, 16 * uint64_t(W));
   const std::vector<uint64_t> M = d2h(all.p, 2 * uint64_t(W) * W, stream);
   std::vector<uint64_t> rc(W), rb(W), scb(W), rcb(W);
   uint64_t nrecv = 0, nrecv_b = 0, nsend = 0, nsend_b = 0;
@@ -3646,7 +3784,7 @@ static dr_state* replay_sharded_rccl(dr_comm& c, const std::shared_ptr<StagedDat
                            k.malformed_lines, int64_t(k.live_key_sum), int64_t(k.tomb_key_sum)};
   DBuf<int64_t> sums(ctx, 8);
   HIP_OK(hipMemcpyAsync(sums.p, part, sizeof(part), hipMemcpyHostToDevice, stream));
-  RC_OK(R.all_reduce(sums.p, sums.p, 8, ncclInt64, ncclSum, c.comm, stream));
+  comm_all_reduce_sum_i64(c, sums.p, 8);
   const std::vector<int64_t> t = d2h(sums.p, 8, stream);
   k.num_files = t[0];
   k.size_in_bytes = t[1];
@@ -3904,11 +4042,11 @@ int dr_staged_plan(const dr_staged* staged, uint64_t* out, int32_t cap, int32_t*
   for (auto& p : s.parts) ck += p.len;
   for (auto& p : s.hot.pages) { cs += p.csize; us += p.usize; }
   const PagePlan& h = s.hot;
-  const uint64_t v[13] = {s.h_json.size(), ck, s.ck_rows, s.hot.pages.size(), cs, us, s.hot.dict_entries,
+  const uint64_t v[14] = {s.h_json.size(), ck, s.ck_rows, s.hot.pages.size(), cs, us, s.hot.dict_entries,
                           h.snap_in_bytes, h.snap_out_bytes, h.nchunks, h.block_page.size(), h.snap_elements,
-                          h.copy_bytes};
+                          h.copy_bytes, s.json_lines};
   int32_t k = 0;
-  for (; k < cap && k < 13; ++k) out[k] = v[k];
+  for (; k < cap && k < 14; ++k) out[k] = v[k];
   *n = k;
   return DR_OK;
 }
@@ -4050,6 +4188,15 @@ int dr_state_export(dr_state* state, int32_t which, dr_export* out) {
     out->tags_key_off = e.tags_key_off.data(); out->tags_key_bytes = e.tags_key_bytes.data();
     out->tags_val_off = e.tags_val_off.data(); out->tags_val_bytes = e.tags_val_bytes.data();
     out->tags_val_null = e.tags_val_null.data();
+  });
+}
+
+int dr_state_record_sums(dr_state* state, uint64_t* live_sum, uint64_t* tomb_sum) {
+  if (!state || !live_sum || !tomb_sum) return DR_E_INVALID_ARG;
+  return guard(state->ctx, [&] {
+    HIP_OK(hipSetDevice(state->ctx->device));
+    *live_sum = record_sum(*state, DR_LIVE);
+    *tomb_sum = record_sum(*state, DR_TOMBSTONES);
   });
 }
 
@@ -4273,19 +4420,45 @@ int dr_comm_unique_id(uint8_t* id) {
   }
 }
 
+int dr_comm_loopback_id(uint8_t* id) {
+  if (!id) return DR_E_INVALID_ARG;
+  static std::atomic<uint64_t> next{1};
+  memset(id, 0, 128);
+  memcpy(id, kLoopMagic, 8);
+  const uint64_t g = next.fetch_add(1);
+  memcpy(id + 8, &g, 8);
+  return DR_OK;
+}
+
 int dr_comm_create(dr_ctx* ctx, const uint8_t* id, int32_t world, int32_t rank, dr_comm** out) {
   if (!ctx || !id || !out || world < 1 || rank < 0 || rank >= world || uint32_t(world) > shard_max_world())
     return DR_E_INVALID_ARG;
   *out = nullptr;
   return guard(ctx, [&] {
     HIP_OK(hipSetDevice(ctx->device));
-    ncclUniqueId u;
-    memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
     auto c = std::make_unique<dr_comm>();
     c->ctx = ctx;
     c->world = world;
     c->rank = rank;
-    RC_OK(rccl().init_rank(&c->comm, world, u, rank));
+    if (memcmp(id, kLoopMagic, 8) == 0) {
+      uint64_t gid;
+      memcpy(&gid, id + 8, 8);
+      std::lock_guard<std::mutex> g(g_loop_mu);
+      std::shared_ptr<LoopGroup> grp = g_loop_groups[gid].lock();
+      if (!grp) {
+        grp = std::make_shared<LoopGroup>();
+        grp->world = world;
+        grp->ptr.assign(size_t(world), nullptr);
+        grp->cnt.assign(size_t(world), nullptr);
+        g_loop_groups[gid] = grp;
+      }
+      if (grp->world != world) fail(DR_E_INVALID_ARG, "loopback communicator joined with a different world size");
+      c->loop = grp;
+    } else {
+      ncclUniqueId u;
+      memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+      RC_OK(rccl().init_rank(&c->comm, world, u, rank));
+    }
     *out = c.release();
   });
 }
@@ -4302,12 +4475,14 @@ int dr_replay_sharded(dr_comm* comm, const dr_staged* staged, int64_t min_file_r
   if (!comm || !staged || !out) return DR_E_INVALID_ARG;
   *out = nullptr;
   dr_ctx* ctx = comm->ctx;
-  return guard(ctx, [&] {
+  const int rc = guard(ctx, [&] {
     HIP_OK(hipSetDevice(ctx->device));
     ctx->begin_call();
     *out = replay_sharded_rccl(*comm, staged->d, min_file_retention_timestamp, flags);
     ctx->collect_timings();
   });
+  if (rc != DR_OK && comm->loop) comm->loop->abort();  // the other ranks fail instead of waiting
+  return rc;
 }
 
 int dr_parsed_release(dr_parsed* parsed) {

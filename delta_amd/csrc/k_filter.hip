@@ -573,6 +573,80 @@ __global__ void k_select(const uint32_t* flag, const uint64_t* pos, uint64_t n, 
   if (i < n && flag[i]) out[pos[i]] = int64_t(i);
 }
 
+// ---- full-record checksum (dr_state_record_sums) ------------------------------------------------
+// One lane per exported record: the eight canonical words (oracle/delta_oracle.py:record_hash) from
+// the export columns, xxh64 of them, and a wave + workgroup sum added once per workgroup. Integer
+// addition mod 2^64 is order-free, so the result does not depend on the survivors' order.
+constexpr uint64_t REC_SEED = 0x5EED, REC_GOLD = 0x9E3779B97F4A7C15ull, REC_NULLV = 0x5BD1E9955BD1E995ull;
+
+__device__ inline uint64_t rec_map_hash(uint8_t is_null, uint64_t e0, uint64_t e1, const int64_t* koff,
+                                        const uint8_t* kb, const int64_t* voff, const uint8_t* vb,
+                                        const uint8_t* vnull, uint64_t ks, uint64_t vs) {
+  if (is_null) return 0;
+  uint64_t h = 1 + (e1 - e0);
+  for (uint64_t e = e0; e < e1; ++e) {
+    const uint64_t hk = xxh64(kb + koff[e], uint32_t(koff[e + 1] - koff[e]), ks);
+    const uint64_t hv = vnull[e] ? REC_NULLV : xxh64(vb + voff[e], uint32_t(voff[e + 1] - voff[e]), vs);
+    h += hk * REC_GOLD + hv;
+  }
+  return h;
+}
+
+// xxh64 of eight little-endian words (64 bytes: two 32-byte stripes, no tail).
+__device__ inline uint64_t xxh64_words8(const uint64_t* w, uint64_t seed) {
+  uint64_t v1 = seed + P1 + P2, v2 = seed + P2, v3 = seed, v4 = seed - P1;
+  for (int s = 0; s < 8; s += 4) {
+    v1 = xx_round(v1, w[s]);
+    v2 = xx_round(v2, w[s + 1]);
+    v3 = xx_round(v3, w[s + 2]);
+    v4 = xx_round(v4, w[s + 3]);
+  }
+  uint64_t h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+  h = xx_merge(h, v1);
+  h = xx_merge(h, v2);
+  h = xx_merge(h, v3);
+  h = xx_merge(h, v4);
+  h += 64;
+  h ^= h >> 33;
+  h *= P2;
+  h ^= h >> 29;
+  h *= P3;
+  h ^= h >> 32;
+  return h;
+}
+
+__global__ void __launch_bounds__(256) k_record_hash(RecordHashArgs a) {
+  __shared__ unsigned long long part[4];
+  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  uint64_t r = 0;
+  if (i < a.n) {
+    uint64_t w[8];
+    w[0] = uint64_t(a.side);
+    w[1] = xxh64(a.path_bytes + a.path_off[i], uint32_t(a.path_off[i + 1] - a.path_off[i]), 0);
+    w[2] = uint64_t(a.size[i]);
+    if (a.side == 0) {
+      w[3] = uint64_t(a.mtime[i]);
+      w[4] = 0;
+      w[5] = a.stats_null[i] ? 0
+                             : xxh64(a.stats_bytes + a.stats_off[i], uint32_t(a.stats_off[i + 1] - a.stats_off[i]), 1);
+    } else {
+      const bool has = a.flags[i] & F_HAS_DELTS;
+      w[3] = has ? a.delts[i] : 0;
+      w[4] = (has ? 1u : 0u) | (a.efm[i] ? 2u : 0u);
+      w[5] = 0;
+    }
+    w[6] = rec_map_hash(a.pv_null[i], a.pv_entry[i], a.pv_entry[i + 1], a.pv_key_off, a.pv_key_bytes, a.pv_val_off,
+                        a.pv_val_bytes, a.pv_val_null, 2, 3);
+    w[7] = rec_map_hash(a.tags_null[i], a.tags_entry[i], a.tags_entry[i + 1], a.tags_key_off, a.tags_key_bytes,
+                        a.tags_val_off, a.tags_val_bytes, a.tags_val_null, 4, 5);
+    r = xxh64_words8(w, REC_SEED);
+  }
+  for (int o = 32; o > 0; o >>= 1) r += __shfl_down(r, o, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = r;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(a.sum, part[0] + part[1] + part[2] + part[3]);
+}
+
 }  // namespace dev
 
 static inline unsigned g256(uint64_t n) { return unsigned((n + 255) / 256); }
@@ -594,6 +668,9 @@ void launch_rep0_flags(const uint8_t* rep, uint64_t n, uint32_t* f, hipStream_t 
 }
 void launch_row_starts(const uint8_t* rep, uint64_t n, const uint64_t* pos, uint64_t* row_start, hipStream_t st) {
   if (n) DR_LAUNCH(dev::k_row_starts, dim3(g256(n)), dim3(256), 0, st, rep, n, pos, row_start);
+}
+void launch_record_hash(const RecordHashArgs& a, hipStream_t st) {
+  if (a.n) DR_LAUNCH(dev::k_record_hash, dim3(g256(a.n)), dim3(256), 0, st, a);
 }
 void launch_select(const uint32_t* flag, const uint64_t* pos, uint64_t n, int64_t* out, hipStream_t st) {
   if (n) DR_LAUNCH(dev::k_select, dim3(g256(n)), dim3(256), 0, st, flag, pos, n, out);

@@ -584,6 +584,21 @@ struct ExportArgs {
   uint32_t* error;
 };
 void launch_export(const ExportArgs& a, hipStream_t st);
+// Order-free full-record checksum of one exported side (dr_state_record_sums; the record hash is
+// defined in oracle/delta_oracle.py:record_hash): *sum += hash(record) over the n records.
+struct RecordHashArgs {
+  uint64_t n;
+  int32_t side;
+  const uint8_t* path_bytes; const uint64_t* path_off;
+  const int64_t* size; const int64_t* mtime; const uint64_t* delts; const uint8_t* flags; const uint8_t* efm;
+  const uint8_t* stats_null; const uint64_t* stats_off; const uint8_t* stats_bytes;
+  const uint8_t* pv_null; const uint64_t* pv_entry; const int64_t* pv_key_off; const uint8_t* pv_key_bytes;
+  const int64_t* pv_val_off; const uint8_t* pv_val_bytes; const uint8_t* pv_val_null;
+  const uint8_t* tags_null; const uint64_t* tags_entry; const int64_t* tags_key_off; const uint8_t* tags_key_bytes;
+  const int64_t* tags_val_off; const uint8_t* tags_val_bytes; const uint8_t* tags_val_null;
+  unsigned long long* sum;
+};
+void launch_record_hash(const RecordHashArgs& a, hipStream_t st);
 }  // namespace dr
 
 // ---- checkpoint page encoding (k_encode.hip) -----------------------------------------------------

@@ -139,6 +139,16 @@ class Engine:
             raise DeltaError(rc, "dr_comm_unique_id failed (%s)" % N.STATUS.get(rc, rc))
         return buf.raw
 
+    @staticmethod
+    def comm_loopback_id() -> bytes:
+        """dr_comm_loopback_id (test hook): an id whose communicator is an in-process loopback -- the
+        ranks are threads of this process, the collectives device copies at a barrier."""
+        buf = C.create_string_buffer(128)
+        rc = N.lib().dr_comm_loopback_id(buf)
+        if rc != N.DR_OK:
+            raise DeltaError(rc, "dr_comm_loopback_id failed (%s)" % N.STATUS.get(rc, rc))
+        return buf.raw
+
     def comm(self, uid: bytes, world: int, rank: int) -> "Comm":
         """dr_comm_create: this rank's RCCL communicator (collective over the `world` ranks)."""
         h = C.c_void_p()
@@ -197,7 +207,7 @@ class Staged:
         self.eng.check(self.eng.lib.dr_staged_plan(self.h, out, 16, C.byref(n)))
         names = ["json_bytes", "checkpoint_bytes", "checkpoint_rows", "pages", "pages_compressed_bytes",
                  "pages_decompressed_bytes", "dict_entries", "snappy_in_bytes", "snappy_out_bytes",
-                 "snappy_chunks", "snappy_blocks", "snappy_elements", "copy_bytes"]
+                 "snappy_chunks", "snappy_blocks", "snappy_elements", "copy_bytes", "json_lines"]
         return {names[i]: int(out[i]) for i in range(n.value)}
 
     def replay(self, min_file_retention_timestamp: int, validate: bool = True, reducer: str = "lds") -> "State":
@@ -307,6 +317,14 @@ class State:
             return buf.value.decode("utf-8")
         self.eng.check(rc)
         return None
+
+    def record_sums(self) -> Tuple[int, int]:
+        """dr_state_record_sums: (live, tombstone) order-free full-record checksums, computed on the
+        device (same definition as oracle.delta_oracle.record_hash)."""
+        a, b = C.c_uint64(), C.c_uint64()
+        with self.eng.lock:
+            self.eng.check(self.eng.lib.dr_state_record_sums(self.h, C.byref(a), C.byref(b)))
+        return a.value, b.value
 
     def export(self, which: int) -> List[dict]:
         with self.eng.lock:

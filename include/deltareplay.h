@@ -150,7 +150,7 @@ int dr_staged_bytes(const dr_staged* staged, uint64_t* json_bytes, uint64_t* che
  * [2] checkpoint rows, [3] planned pages, [4] their compressed bytes, [5] their decompressed bytes,
  * [6] dictionary entries, [7] SNAPPY input bytes, [8] SNAPPY output bytes, [9] SNAPPY 256-byte
  * speculation chunks, [10] SNAPPY 64 KiB output blocks, [11] SNAPPY elements (0 until a replay with
- * timing on has counted them), [12] bytes of uncompressed pages copied. *n receives the number of
+ * timing on has counted them), [12] bytes of uncompressed pages copied, [13] JSON lines (newline-terminated). *n receives the number of
  * figures written (<= cap). */
 int dr_staged_plan(const dr_staged* staged, uint64_t* out, int32_t cap, int32_t* n);
 
@@ -192,6 +192,15 @@ int dr_state_check_checksum(dr_state* state, const char* crc, uint64_t crc_len, 
                             uint64_t* msg_len);
 /* Materialises allFiles (DR_LIVE) or tombstones (DR_TOMBSTONES) on the host, dataChange=false. */
 int dr_state_export(dr_state* state, int32_t which, dr_export* out);
+
+/* Order-free full-record checksums of allFiles and tombstones, computed on the device from the export
+ * columns: the sum mod 2^64 over the records of one 64-bit hash of every field of the record
+ * (path, size, modificationTime / deletionTimestamp + presence, extendedFileMetadata, stats,
+ * partitionValues, tags; dataChange is false on both sides). The record hash is defined once in
+ * DESIGN.md §2; the CPU restatements compute the same sums, so two states with equal sums hold the
+ * same record sets (D/actions/InMemoryLogReplay.scala:55-77 winners, not only the same paths).
+ * For a sharded state: this rank's records (sum the ranks' values). */
+int dr_state_record_sums(dr_state* state, uint64_t* live_sum, uint64_t* tomb_sum);
 
 /* ---- per-line commit decode (device) --------------------------------------------------------
  * The hot fields of DeltaLog.getChanges' per-line Action.fromJson (D/DeltaLog.scala:222-238,
@@ -345,6 +354,11 @@ int dr_shard_release(dr_shard* shard);
 typedef struct dr_comm dr_comm;
 int dr_comm_unique_id(uint8_t* id /* 128 bytes */);
 int dr_comm_create(dr_ctx* ctx, const uint8_t* id, int32_t world, int32_t rank, dr_comm** out);
+/* Test hook: an id whose communicator is an in-process loopback instead of RCCL -- the `world` ranks
+ * are threads of this process (one dr_ctx each, any device), and every collective of dr_replay_sharded
+ * becomes device copies between the ranks' buffers at a barrier. Runs the sharded replay's own control
+ * flow at world > 1 on one GPU (RCCL refuses two ranks on one device). */
+int dr_comm_loopback_id(uint8_t* id /* 128 bytes */);
 int dr_comm_release(dr_comm* comm);
 int dr_replay_sharded(dr_comm* comm, const dr_staged* staged, int64_t min_file_retention_timestamp, uint32_t flags,
                       dr_state** out);

@@ -463,6 +463,65 @@ def state_reconstruction(seg: LogSegment, min_file_retention_timestamp: int,
     return Snapshot(seg.version, prot, meta, txns, adds, rms)
 
 
+# ----------------------------------------------------------------------------------------------
+# Full-record checksum (BASELINE.md "Correctness gate" at sizes where record lists do not fit a
+# test): an order-free sum over the survivors of one 64-bit hash per record that covers every field
+# the reference's AddFile / RemoveFile carries out of InMemoryLogReplay.checkpoint
+# (D/actions/InMemoryLogReplay.scala:55-77; D/actions/actions.scala:220-320; dataChange is forced
+# false on both sides, so it is constant). The same definition is computed by the GPU
+# (dr_state_record_sums, k_record_hash) and by oracle/replay_oracle.cpp (--record-sums):
+#   w0 side (0 add, 1 remove)       w1 xxh64(path, 0)          w2 size
+#   w3 add: modificationTime; remove: deletionTimestamp (0 when absent)
+#   w4 add: 0; remove: (deletionTimestamp present) | extendedFileMetadata << 1
+#   w5 add: xxh64(stats, 1), 0 when null; remove: 0
+#   w6 map(partitionValues, 2, 3)   w7 map(tags, 4, 5)
+#   map(m, a, b) = 0 when null, else 1 + len(m) + sum over entries of
+#                  xxh64(key, a) * 0x9E3779B97F4A7C15 + (0x5BD1E9955BD1E995 if value is null else xxh64(value, b))
+#   record = xxh64(w0..w7 as 64 little-endian bytes, 0x5EED);  side sum = sum of records mod 2^64
+# ----------------------------------------------------------------------------------------------
+_M64 = (1 << 64) - 1
+REC_SEED = 0x5EED
+_GOLD = 0x9E3779B97F4A7C15
+_NULLV = 0x5BD1E9955BD1E995
+
+
+def _xxh(s: str, seed: int) -> int:
+    import xxhash
+    return xxhash.xxh64_intdigest(s.encode("utf-8"), seed)
+
+
+def _map_hash(m: Optional[dict], ks: int, vs: int) -> int:
+    if m is None:
+        return 0
+    h = 1 + len(m)
+    for k, v in m.items():
+        h += _xxh(k, ks) * _GOLD + (_NULLV if v is None else _xxh(v, vs))
+    return h & _M64
+
+
+def record_hash(rec: dict, side: int) -> int:
+    """The canonical hash of one allFiles (side 0) / tombstones (side 1) record (definition above)."""
+    import struct
+    import xxhash
+    if side == 0:
+        w3, w4 = rec["modificationTime"], 0
+        w5 = 0 if rec.get("stats") is None else _xxh(rec["stats"], 1)
+    else:
+        dt = rec["deletionTimestamp"]
+        w3 = 0 if dt is None else dt
+        w4 = (0 if dt is None else 1) | (2 if rec["extendedFileMetadata"] else 0)
+        w5 = 0
+    w = (side, _xxh(rec["path"], 0), rec["size"] & _M64, w3 & _M64, w4, w5,
+         _map_hash(rec.get("partitionValues"), 2, 3), _map_hash(rec.get("tags"), 4, 5))
+    return xxhash.xxh64_intdigest(struct.pack("<8Q", *w), REC_SEED)
+
+
+def record_sums(all_files: Iterable[dict], tombstones: Iterable[dict]) -> Tuple[int, int]:
+    """(live_record_sum, tomb_record_sum): order-free full-record checksums of both sides."""
+    return (sum(record_hash(r, 0) for r in all_files) & _M64,
+            sum(record_hash(r, 1) for r in tombstones) & _M64)
+
+
 def snapshot_for_table(table_path: str, min_file_retention_timestamp: int,
                        version: Optional[int] = None, validate: bool = True) -> Snapshot:
     seg = get_log_segment(os.path.join(table_path, "_delta_log"), version)

@@ -499,6 +499,11 @@ void decode_chunk(const uint8_t* f, const Chunk& c, const Leaf& l, int threads, 
 // Decoded hot columns of every checkpoint row group, kept alive while actions point into them.
 std::vector<std::array<Col, 4>> g_ck_cols;
 
+// Each checkpoint file's footer (row groups, leaves) and its first action index, for the
+// full-record pass (--record-sums).
+struct CkFile { const std::vector<uint8_t>* f; std::vector<RG> rgs; std::map<std::string, Leaf> leaves; size_t base_act; };
+std::vector<CkFile> g_ck_files;
+
 void read_checkpoint(const std::vector<uint8_t>& f, std::vector<Action>& acts, int threads) {
   const size_t n = f.size();
   uint32_t fl = rd32(f.data() + n - 8);
@@ -565,6 +570,7 @@ void read_checkpoint(const std::vector<uint8_t>& f, std::vector<Action>& acts, i
   for (auto& g : rgs) { groups.push_back({&g, rbase}); rbase += g.rows; }
   size_t base_act = acts.size();
   acts.resize(base_act + size_t(rbase));
+  g_ck_files.push_back(CkFile{&f, rgs, leaves, base_act});
   // decode: one task per (row group, hot column), so a table with few row groups still uses every
   // thread; then one task per row group assembles its rows (unwrap: add > remove > the rest)
   const size_t col0 = g_ck_cols.size();
@@ -689,6 +695,276 @@ void canonical_key(SV raw, Arena& ar, SV* canon, SV* key) {
   }
 }
 
+// ---- full-record checksums (--record-sums; definition in oracle/delta_oracle.py:record_hash) -----
+uint64_t xxh64s(const uint8_t* p, size_t len, uint64_t seed) {
+  const uint8_t* end = p + len;
+  uint64_t h;
+  if (len >= 32) {
+    uint64_t v1 = seed + P1 + P2, v2 = seed + P2, v3 = seed, v4 = seed - P1;
+    do {
+      v1 = xround(v1, rd64(p)); v2 = xround(v2, rd64(p + 8)); v3 = xround(v3, rd64(p + 16)); v4 = xround(v4, rd64(p + 24));
+      p += 32;
+    } while (p <= end - 32);
+    h = rotl(v1, 1) + rotl(v2, 7) + rotl(v3, 12) + rotl(v4, 18);
+    for (uint64_t v : {v1, v2, v3, v4}) { h ^= xround(0, v); h = h * P1 + P4; }
+  } else {
+    h = seed + P5;
+  }
+  h += len;
+  while (p + 8 <= end) { h ^= xround(0, rd64(p)); h = rotl(h, 27) * P1 + P4; p += 8; }
+  if (p + 4 <= end) { h ^= uint64_t(rd32(p)) * P1; h = rotl(h, 23) * P2 + P3; p += 4; }
+  while (p < end) { h ^= uint64_t(*p) * P5; h = rotl(h, 11) * P1; ++p; }
+  h ^= h >> 33; h *= P2; h ^= h >> 29; h *= P3; h ^= h >> 32;
+  return h;
+}
+uint64_t xxh64sv(SV s, uint64_t seed) { return xxh64s((const uint8_t*)s.p, s.n, seed); }
+
+const uint64_t kRecSeed = 0x5EED, kGold = 0x9E3779B97F4A7C15ull, kNullV = 0x5BD1E9955BD1E995ull;
+
+// A map value: entries in first-position order, a repeated key keeps its last value (Jackson into a
+// Map, as the Python dict).
+struct MapV {
+  bool null = true;
+  std::vector<std::pair<SV, std::pair<bool, SV>>> e;  // key -> (value null, value)
+  void put(SV k, bool vnull, SV v) {
+    for (auto& x : e) if (x.first.n == k.n && !memcmp(x.first.p, k.p, k.n)) { x.second = {vnull, v}; return; }
+    e.push_back({k, {vnull, v}});
+  }
+  uint64_t hash(uint64_t ks, uint64_t vs) const {
+    if (null) return 0;
+    uint64_t h = 1 + e.size();
+    for (auto& x : e) h += xxh64sv(x.first, ks) * kGold + (x.second.first ? kNullV : xxh64sv(x.second.second, vs));
+    return h;
+  }
+};
+
+struct Rec {
+  SV path;
+  int64_t size = 0, mtime = 0, delts = 0;
+  bool has_delts = false, efm = false, stats_null = true;
+  SV stats;
+  MapV pv, tags;
+};
+
+uint64_t rec_hash(const Rec& r, int side) {
+  uint64_t w[8];
+  w[0] = uint64_t(side);
+  w[1] = xxh64sv(r.path, 0);
+  w[2] = uint64_t(r.size);
+  if (side == 0) { w[3] = uint64_t(r.mtime); w[4] = 0; w[5] = r.stats_null ? 0 : xxh64sv(r.stats, 1); }
+  else { w[3] = r.has_delts ? uint64_t(r.delts) : 0; w[4] = (r.has_delts ? 1u : 0u) | (r.efm ? 2u : 0u); w[5] = 0; }
+  w[6] = r.pv.hash(2, 3);
+  w[7] = r.tags.hash(4, 5);
+  uint8_t b[64];
+  memcpy(b, w, 64);  // little-endian host
+  return xxh64s(b, 64, kRecSeed);
+}
+
+// {"k": "v" | null, ...} -> map (null literal -> null map)
+bool parse_map(J& j, MapV& m) {
+  if (j.null()) { m = MapV(); return true; }
+  m = MapV();
+  m.null = false;
+  j.ws();
+  if (!j.lit("{")) return false;
+  j.ws();
+  if (j.p < j.e && *j.p == '}') { ++j.p; return true; }
+  for (;;) {
+    SV k, v;
+    if (!j.str(&k)) return false;
+    j.ws();
+    if (!j.lit(":")) return false;
+    if (j.null()) m.put(k, true, SV{});
+    else { if (!j.str(&v)) return false; m.put(k, false, v); }
+    j.ws();
+    if (j.p < j.e && *j.p == ',') { ++j.p; continue; }
+    if (j.p < j.e && *j.p == '}') { ++j.p; return true; }
+    return false;
+  }
+}
+
+bool parse_bool(J& j, bool* b) {
+  j.ws();
+  if (j.e - j.p >= 4 && !memcmp(j.p, "true", 4)) { j.p += 4; *b = true; return true; }
+  if (j.e - j.p >= 5 && !memcmp(j.p, "false", 5)) { j.p += 5; *b = false; return true; }
+  return false;
+}
+
+// The whole add / remove object of a survivor line (Jackson defaults: absent primitives 0/false,
+// absent Options / maps null; a repeated member keeps its last value).
+bool parse_record_obj(J& j, Rec& r) {
+  j.ws();
+  if (!j.lit("{")) return false;
+  j.ws();
+  if (j.p < j.e && *j.p == '}') { ++j.p; return true; }
+  for (;;) {
+    SV k;
+    if (!j.str(&k)) return false;
+    j.ws();
+    if (!j.lit(":")) return false;
+    if (k.eq("path", 4)) { if (!j.null() && !j.str(&r.path)) return false; }
+    else if (k.eq("size", 4)) { if (j.null()) r.size = 0; else if (!j.i64(&r.size)) return false; }
+    else if (k.eq("modificationTime", 16)) { if (j.null()) r.mtime = 0; else if (!j.i64(&r.mtime)) return false; }
+    else if (k.eq("deletionTimestamp", 17)) { if (j.null()) r.has_delts = false; else { if (!j.i64(&r.delts)) return false; r.has_delts = true; } }
+    else if (k.eq("extendedFileMetadata", 20)) { if (j.null()) r.efm = false; else if (!parse_bool(j, &r.efm)) return false; }
+    else if (k.eq("stats", 5)) { if (j.null()) r.stats_null = true; else { if (!j.str(&r.stats)) return false; r.stats_null = false; } }
+    else if (k.eq("partitionValues", 15)) { if (!parse_map(j, r.pv)) return false; }
+    else if (k.eq("tags", 4)) { if (!parse_map(j, r.tags)) return false; }
+    else { j.skip(); if (j.bad) return false; }
+    j.ws();
+    if (j.p < j.e && *j.p == ',') { ++j.p; continue; }
+    if (j.p < j.e && *j.p == '}') { ++j.p; return true; }
+    return false;
+  }
+}
+
+// The survivor record of a JSON line: the object of its side ("add" / "remove"; the last such member).
+bool json_record(const char* b, const char* e, int side, Arena* ar, Rec& r) {
+  J j{b, e, ar};
+  const char* want = side == 0 ? "add" : "remove";
+  const size_t wn = side == 0 ? 3 : 6;
+  j.ws();
+  if (!j.lit("{")) return false;
+  bool found = false;
+  for (;;) {
+    SV k;
+    if (!j.str(&k)) return false;
+    j.ws();
+    if (!j.lit(":")) return false;
+    if (k.eq(want, wn) && !j.null()) { r = Rec(); if (!parse_record_obj(j, r)) return false; found = true; }
+    else { j.skip(); if (j.bad) return false; }
+    j.ws();
+    if (j.p < j.e && *j.p == ',') { ++j.p; continue; }
+    if (j.p < j.e && *j.p == '}') break;
+    return false;
+  }
+  return found;
+}
+
+// A column chunk decoded with its repetition and definition levels (one entry per level; values at
+// entries with def == maxdef). PLAIN / dictionary BYTE_ARRAY, INT64, INT32 and PLAIN BOOLEAN.
+struct LevCol {
+  std::vector<uint8_t> def, rep;
+  std::vector<SV> s;
+  std::vector<int64_t> i;
+  std::vector<std::vector<uint8_t>> bufs;
+};
+
+void level_chunk(const uint8_t* f, const Chunk& c, const Leaf& l, LevCol& out) {
+  std::vector<SV> ds;
+  std::vector<int64_t> di;
+  for (const Page& pg : chunk_pages(f, c)) {
+    out.bufs.push_back(page_bytes(c, pg));
+    const uint8_t* q = out.bufs.back().data();
+    if (pg.pt == 2) {
+      ds.clear(); di.clear();
+      plain_values(l, q, pg.nv, &ds, &di);
+      continue;
+    }
+    const uint8_t* qe = q + pg.us;
+    std::vector<uint32_t> reps, defs;
+    if (pg.pt == 3) {
+      if (l.maxrep) rle(q, q + pg.v2r, bwidth(l.maxrep), pg.nv, reps);
+      if (l.maxdef) rle(q + pg.v2r, q + pg.v2r + pg.v2d, bwidth(l.maxdef), pg.nv, defs);
+      q += pg.v2r + pg.v2d;
+    } else {
+      if (l.maxrep) { uint32_t n = rd32(q); q += 4; rle(q, q + n, bwidth(l.maxrep), pg.nv, reps); q += n; }
+      if (l.maxdef) { uint32_t n = rd32(q); q += 4; rle(q, q + n, bwidth(l.maxdef), pg.nv, defs); q += n; }
+    }
+    int64_t nn = 0;
+    for (int k = 0; k < pg.nv; ++k) nn += (l.maxdef ? int(defs[size_t(k)]) : 0) == l.maxdef;
+    std::vector<SV> S; std::vector<int64_t> I;
+    if (pg.enc == 0 && l.type == 0) {
+      for (int64_t k = 0; k < nn; ++k) I.push_back((q[k >> 3] >> (k & 7)) & 1);
+    } else if (pg.enc == 0) {
+      plain_values(l, q, nn, &S, &I);
+    } else if (pg.enc == 2 || pg.enc == 8) {
+      std::vector<uint32_t> ix;
+      if (nn) { int w = *q++; rle(q, qe, w, nn, ix); }
+      for (uint32_t x : ix) { if (l.type == 6) S.push_back(ds.at(x)); else I.push_back(di.at(x)); }
+    } else die("encoding");
+    size_t vi = 0;
+    for (int k = 0; k < pg.nv; ++k) {
+      const uint8_t d = uint8_t(l.maxdef ? defs[size_t(k)] : 0);
+      out.def.push_back(d);
+      out.rep.push_back(uint8_t(l.maxrep ? reps[size_t(k)] : 0));
+      if (d == l.maxdef) { if (l.type == 6) out.s.push_back(S[vi++]); else out.i.push_back(I[vi++]); }
+      else { if (l.type == 6) out.s.push_back(SV{}); else out.i.push_back(0); }
+    }
+  }
+}
+
+// Level entry ranges of the rows of a leaf (rows start where rep == 0).
+std::vector<size_t> row_starts(const LevCol& c) {
+  std::vector<size_t> st;
+  for (size_t k = 0; k < c.def.size(); ++k) if (c.rep[k] == 0) st.push_back(k);
+  st.push_back(c.def.size());
+  return st;
+}
+
+// Full-record sums of the checkpoint survivors of one row group: `surv[row]` 1 = live add,
+// 2 = kept tombstone.
+void ck_rowgroup_sums(const CkFile& cf, const RG& g, const SV* canon, const uint8_t* surv, uint64_t* sums) {
+  bool want[2] = {false, false};
+  for (int64_t r = 0; r < g.rows; ++r) if (surv[r]) want[surv[r] - 1] = true;
+  for (int side = 0; side < 2; ++side) {
+    if (!want[side]) continue;
+    const std::string pre = side == 0 ? "add." : "remove.";
+    struct L { const Leaf* leaf = nullptr; LevCol col; std::vector<size_t> st; };
+    auto load = [&](const std::string& name) {
+      auto out = std::make_unique<L>();
+      auto it = cf.leaves.find(pre + name);
+      if (it == cf.leaves.end()) return out;
+      for (const Chunk& c : g.cols)
+        if (c.path == pre + name) { out->leaf = &it->second; level_chunk(cf.f->data(), c, it->second, out->col); }
+      if (out->leaf) out->st = row_starts(out->col);
+      return out;
+    };
+    auto size = load("size"), mt = load("modificationTime"), dts = load("deletionTimestamp"),
+         efm = load("extendedFileMetadata"), stats = load("stats"), pvk = load("partitionValues.key_value.key"),
+         pvv = load("partitionValues.key_value.value"), tk = load("tags.key_value.key"), tv = load("tags.key_value.value");
+    auto flat_i = [&](const L& l, int64_t r, int64_t* v) {
+      if (!l.leaf) return false;
+      const size_t k = l.st[size_t(r)];
+      if (l.col.def[k] != l.leaf->maxdef) return false;
+      *v = l.col.i[k];
+      return true;
+    };
+    auto map_of = [&](const L& k, const L& v, int64_t r, MapV& m) {
+      m = MapV();
+      if (!k.leaf) return;
+      const size_t a = k.st[size_t(r)], b = k.st[size_t(r) + 1];
+      if (k.col.def[a] < k.leaf->def_of[size_t(k.leaf->def_of.size()) - 3]) return;  // the map itself is null
+      m.null = false;
+      if (k.col.def[a] < k.leaf->maxdef) return;  // empty map
+      for (size_t e = a; e < b; ++e) {
+        const bool vnull = !v.leaf || v.col.def[e] != v.leaf->maxdef;
+        m.put(k.col.s[e], vnull, vnull ? SV{} : v.col.s[e]);
+      }
+    };
+    for (int64_t r = 0; r < g.rows; ++r) {
+      if (surv[r] != side + 1) continue;
+      Rec rec;
+      rec.path = canon[r];  // canonical form of the path leaf's value
+      int64_t x;
+      if (flat_i(*size, r, &x)) rec.size = x;
+      if (side == 0) {
+        if (flat_i(*mt, r, &x)) rec.mtime = x;
+        if (stats->leaf && stats->col.def[stats->st[size_t(r)]] == stats->leaf->maxdef) {
+          rec.stats_null = false;
+          rec.stats = stats->col.s[stats->st[size_t(r)]];
+        }
+      } else {
+        if (flat_i(*dts, r, &x)) { rec.has_delts = true; rec.delts = x; }
+        if (flat_i(*efm, r, &x)) rec.efm = x != 0;
+      }
+      map_of(*pvk, *pvv, r, rec.pv);
+      map_of(*tk, *tv, r, rec.tags);
+      sums[side] += rec_hash(rec, side);
+    }
+  }
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -697,9 +973,12 @@ int main(int argc, char** argv) {
   int64_t cutoff = std::stoll(argv[2]);
   int threads = int(std::thread::hardware_concurrency());
   int parts = 50;
-  for (int i = 3; i + 1 < argc; i += 2) {
-    if (!strcmp(argv[i], "--threads")) threads = std::max(1, atoi(argv[i + 1]));
-    else if (!strcmp(argv[i], "--partitions")) parts = std::max(1, atoi(argv[i + 1]));
+  bool want_records = false;
+  for (int i = 3; i < argc; ++i) {
+    if (!strcmp(argv[i], "--record-sums")) { want_records = true; continue; }
+    if (i + 1 >= argc) break;
+    if (!strcmp(argv[i], "--threads")) threads = std::max(1, atoi(argv[++i]));
+    else if (!strcmp(argv[i], "--partitions")) parts = std::max(1, atoi(argv[++i]));
   }
   try {
     // the segment's bytes are read before the clock starts (the GPU's timed region, too, starts
@@ -803,6 +1082,7 @@ int main(int argc, char** argv) {
     // (activeFiles / tombstones with the opposite entry dropped, D/actions/InMemoryLogReplay.scala:54-63)
     struct PartOut { int64_t files = 0, size = 0, tombs = 0; uint64_t lks = 0, tks = 0; };
     std::vector<PartOut> po(P);
+    std::vector<uint8_t> surv(want_records ? N : 0, 0);  // 1 live add, 2 kept tombstone (--record-sums)
     std::atomic<size_t> nextp{0};
     {
       std::vector<std::thread> ts;
@@ -838,9 +1118,11 @@ int main(int argc, char** argv) {
               if (a.kind == ADD) {
                 out.push_back({canon[i], i});
                 o.files++; o.size += a.size; o.lks += hash[i] >> 32;
+                if (want_records) surv[i] = 1;
               } else if ((a.has_delts ? a.delts : 0) > cutoff) {  // getTombstones: delTimestamp > cutoff
                 out.push_back({canon[i], i});
                 o.tombs++; o.tks += hash[i] >> 32;
+                if (want_records) surv[i] = 2;
               }
             }
             std::sort(out.begin(), out.end(), [](const std::pair<SV, uint32_t>& x, const std::pair<SV, uint32_t>& y) {
@@ -855,12 +1137,63 @@ int main(int argc, char** argv) {
     for (auto& o : po) { tot.files += o.files; tot.size += o.size; tot.tombs += o.tombs; tot.lks += o.lks; tot.tks += o.tks; }
     const int64_t nfa = int64_t(pstart[P]);
     double ps = std::chrono::duration<double>(t1 - t0).count(), rs = std::chrono::duration<double>(t2 - t1).count();
+    // full-record checksums (untimed): JSON survivors re-read from their lines, checkpoint survivors
+    // from every leaf of their side, one task per row group
+    char recs[160] = "";
+    if (want_records) {
+      auto tr0 = std::chrono::steady_clock::now();
+      std::vector<std::array<uint64_t, 2>> ts_sum(T, std::array<uint64_t, 2>{0, 0});
+      std::vector<uint8_t> bad(T, 0);
+      {
+        std::vector<std::thread> ts;
+        const size_t nl = lines.size(), per_l = (nl + T - 1) / T;
+        for (size_t t = 0; t < T; ++t)
+          ts.emplace_back([&, t] {
+            const size_t b = t * per_l, e = std::min(nl, b + per_l);
+            for (size_t k = b; k < e; ++k) {
+              const uint8_t sv = surv[base + k];
+              if (!sv) continue;
+              Rec r;
+              if (!json_record(lines[k].first, lines[k].second, sv - 1, &arenas[t], r)) { bad[t] = 1; continue; }
+              r.path = canon[base + k];  // the record's path is the canonical one (D/Snapshot.scala:98-101)
+              ts_sum[t][sv - 1] += rec_hash(r, sv - 1);
+            }
+          });
+        for (auto& t : ts) t.join();
+      }
+      {
+        struct Task { const CkFile* cf; const RG* g; size_t row0; };
+        std::vector<Task> tasks;
+        for (const CkFile& cf : g_ck_files) {
+          size_t r0 = cf.base_act;
+          for (const RG& g : cf.rgs) { tasks.push_back({&cf, &g, r0}); r0 += size_t(g.rows); }
+        }
+        std::atomic<size_t> nt{0};
+        std::vector<std::thread> ts;
+        for (size_t t = 0; t < T; ++t)
+          ts.emplace_back([&, t] {
+            for (size_t k; (k = nt++) < tasks.size();) {
+              uint64_t sm[2] = {0, 0};
+              ck_rowgroup_sums(*tasks[k].cf, *tasks[k].g, canon.data() + tasks[k].row0, surv.data() + tasks[k].row0, sm);
+              ts_sum[t][0] += sm[0];
+              ts_sum[t][1] += sm[1];
+            }
+          });
+        for (auto& t : ts) t.join();
+      }
+      uint64_t ls = 0, tsm = 0;
+      for (auto& x : ts_sum) { ls += x[0]; tsm += x[1]; }
+      for (uint8_t b : bad) if (b) die("unreadable survivor line in the record pass");
+      snprintf(recs, sizeof recs, ",\"live_record_sum\":%llu,\"tomb_record_sum\":%llu,\"record_s\":%.3f",
+               (unsigned long long)ls, (unsigned long long)tsm,
+               std::chrono::duration<double>(std::chrono::steady_clock::now() - tr0).count());
+    }
     printf("{\"num_files\":%lld,\"size_in_bytes\":%lld,\"num_removes\":%lld,\"num_actions\":%lld,"
            "\"num_file_actions\":%lld,\"checkpoint_rows\":%lld,\"live_key_sum\":%llu,\"tomb_key_sum\":%llu,"
-           "\"threads\":%d,\"partitions\":%d,\"read_s\":%.6f,\"parse_s\":%.6f,\"replay_s\":%.6f,\"total_s\":%.6f}\n",
+           "\"threads\":%d,\"partitions\":%d,\"read_s\":%.6f,\"parse_s\":%.6f,\"replay_s\":%.6f,\"total_s\":%.6f%s}\n",
            (long long)tot.files, (long long)tot.size, (long long)tot.tombs, (long long)acts.size(), (long long)nfa,
            (long long)ck_rows, (unsigned long long)tot.lks, (unsigned long long)tot.tks, threads, parts, read_s, ps, rs,
-           ps + rs);
+           ps + rs, recs);
   } catch (const std::exception& e) {
     fprintf(stderr, "replay_oracle: %s\n", e.what());
     return 1;

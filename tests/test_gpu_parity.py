@@ -45,6 +45,8 @@ def _assert_same(state, snap):
     tomb = state.export(1)
     assert sorted(map(_canon, live)) == sorted(map(_canon, snap.all_files))
     assert sorted(map(_canon, tomb)) == sorted(map(_canon, snap.tombstones))
+    # the device's full-record checksums (the full-size parity gate of bench.py) agree with the oracle's
+    assert state.record_sums() == O.record_sums(snap.all_files, snap.tombstones)
     prot = [a["protocol"] for a in state.nonfile if "protocol" in a]
     meta = [a["metaData"] for a in state.nonfile if "metaData" in a]
     assert prot == ([snap.protocol] if snap.protocol else [])
@@ -83,6 +85,20 @@ def test_golden_json_only_replay(engine, name):
     seg = O.LogSegment(lp, 3, [O.delta_file(v) for v in range(4)], [], None)
     try:
         _assert_same(st, O.state_reconstruction(seg, 0))
+    finally:
+        st.release()
+
+
+@pytest.mark.parametrize("cutoff", [0, 1_600_000_100_005])
+def test_record_sums_corpus(engine, tmp_path, cutoff):
+    """dr_state_record_sums over a log that exercises every field of the record hash
+    (tests/record_corpus.py): tags, null / empty maps, repeated members and keys, escapes, removes
+    with and without deletionTimestamp, checkpoint and JSON survivors."""
+    from tests import record_corpus as R
+    lp = R.build(str(tmp_path / "t"))
+    st = _gpu_replay(engine, lp, cutoff)
+    try:
+        _assert_same(st, O.state_reconstruction(O.get_log_segment(lp), cutoff))
     finally:
         st.release()
 

@@ -44,6 +44,7 @@ def _sharded(lp, cutoff, world):
 
 
 def _check(counts, live, tomb, snap):
+    assert O.record_sums(live, tomb) == O.record_sums(snap.all_files, snap.tombstones)
     assert counts["num_files"] == snap.num_of_files
     assert counts["size_in_bytes"] == snap.size_in_bytes
     assert counts["num_removes"] == snap.num_of_removes
@@ -63,7 +64,7 @@ def test_sharded_golden(name, world):
     _check(counts, live, tomb, O.state_reconstruction(O.get_log_segment(lp), cutoff))
 
 
-@pytest.mark.parametrize("world", [1, 2, 4])
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
 def test_sharded_synthetic(tmp_path, world):
     from delta_amd.testing import synth as S
     exp = S.build_table(str(tmp_path), S.config_spec(3, 0.003), seed=5, row_group_size=4000)
@@ -117,6 +118,105 @@ def test_rccl_library_single_rank(name):
             st.release()
     finally:
         comm.release()
+
+
+def _library_sharded(lp, cutoff, world, validate=True):
+    """dr_comm_create + dr_replay_sharded with `world` ranks as threads of this process over the
+    library's loopback transport (dr_comm_loopback_id): replay_sharded_rccl's own control flow --
+    count-matrix all-gather, record / path / verdict all-to-alls, counter all-reduce, non-file
+    all-gather -- at W > 1 on one GPU."""
+    import threading
+    from delta_amd.delta_log import Engine
+    from delta_amd.sharded import stage_shard
+    uid = Engine.comm_loopback_id()
+    res, err = [None] * world, [None] * world
+
+    def body(r):
+        try:
+            eng = Engine.get(0)  # thread-local context (own stream) on device 0
+            comm = eng.comm(uid, world, r)
+            try:
+                staged = stage_shard(eng, lp, world, r)
+                try:
+                    st = comm.replay_sharded(staged, cutoff, validate)
+                finally:
+                    staged.release()
+                try:
+                    res[r] = (st.counts, st.nonfile, st.export(0), st.export(1), st.record_sums())
+                finally:
+                    st.release()
+            finally:
+                comm.release()
+        except BaseException as e:  # noqa: BLE001
+            err[r] = e
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in th), "a loopback rank hung"
+    for e in err:
+        if e is not None:
+            raise e
+    counts, nonfile = res[0][0], res[0][1]
+    for c, nf, _, _, _ in res:
+        assert c == counts and nf == nonfile
+    live, tomb = [x for r in res for x in r[2]], [x for r in res for x in r[3]]
+    # the ranks' record checksums add up to the table's (each rank exports its own survivors)
+    m = (1 << 64) - 1
+    assert (sum(r[4][0] for r in res) & m, sum(r[4][1] for r in res) & m) == O.record_sums(live, tomb)
+    return counts, nonfile, live, tomb
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("name", ["delta-0.2.0", "dbr_8_1_generated_columns"])
+def test_library_sharded_loopback_golden(name, world):
+    lp = os.path.join(REF, name, "_delta_log")
+    cutoff = 1564524298213
+    counts, _, live, tomb = _library_sharded(lp, cutoff, world)
+    _check(counts, live, tomb, O.state_reconstruction(O.get_log_segment(lp), cutoff))
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_library_sharded_loopback_synthetic(tmp_path, world):
+    """Config 3's shape (checkpoint + churned commits + retention cutoff) sharded over 2/4/8 ranks by
+    the library driver: counters, key sums and both record sets equal the single-GPU replay and the
+    oracle."""
+    from delta_amd.delta_log import Engine
+    from delta_amd.testing import synth as S
+    exp = S.build_table(str(tmp_path), S.config_spec(3, 0.003), seed=5, row_group_size=4000)
+    lp = os.path.join(str(tmp_path), "_delta_log")
+    cutoff = exp.min_file_retention_timestamp
+    counts, _, live, tomb = _library_sharded(lp, cutoff, world)
+    assert (counts["num_files"], counts["num_removes"], counts["size_in_bytes"], counts["num_actions"],
+            counts["num_file_actions"]) == (exp.num_files, exp.num_removes, exp.size_in_bytes,
+                                            exp.num_actions, exp.num_file_actions)
+    staged = Engine.get(0).stage_log(lp)
+    st = staged.replay(cutoff)
+    staged.release()
+    for k in ("live_key_sum", "tomb_key_sum", "num_protocol", "num_metadata", "num_set_transactions"):
+        assert counts[k] == st.counts[k], k
+    st.release()
+    _check(counts, live, tomb, O.state_reconstruction(O.get_log_segment(lp), cutoff))
+
+
+def test_library_sharded_loopback_missing_metadata_fails_on_every_rank(tmp_path):
+    """A collective error path: the table-wide validation (no metaData in any slice) fails on every
+    rank with the reference's IllegalStateException text, and no rank hangs."""
+    from delta_amd.delta_log import DeltaError
+    lp = str(tmp_path / "_delta_log")
+    os.makedirs(lp)
+    with open(os.path.join(lp, "%020d.json" % 0), "w") as f:
+        f.write('{"protocol":{"minReaderVersion":1,"minWriterVersion":2}}\n')
+        f.write('{"add":{"path":"a","partitionValues":{},"size":1,"modificationTime":1,"dataChange":true}}\n')
+    for v in (1, 2):
+        with open(os.path.join(lp, "%020d.json" % v), "w") as f:
+            f.write('{"add":{"path":"f%d","partitionValues":{},"size":1,"modificationTime":1,"dataChange":true}}\n' % v)
+    with pytest.raises(DeltaError, match="metadata of your Delta table"):
+        _library_sharded(lp, 0, 3)
+    counts, _, live, _ = _library_sharded(lp, 0, 3, validate=False)
+    assert counts["num_files"] == 3 and len(live) == 3 and counts["num_metadata"] == 0
 
 
 def test_rccl_library_two_processes(tmp_path):

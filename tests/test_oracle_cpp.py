@@ -23,7 +23,7 @@ def exe():
 
 
 def run(exe, lp, cutoff, threads=3, parts=7):
-    r = subprocess.run([exe, lp, str(cutoff), "--threads", str(threads), "--partitions", str(parts)],
+    r = subprocess.run([exe, lp, str(cutoff), "--threads", str(threads), "--partitions", str(parts), "--record-sums"],
                        capture_output=True, text=True, check=True)
     return json.loads(r.stdout.strip().splitlines()[-1])
 
@@ -38,6 +38,8 @@ def check(res, snap):
     assert res["num_removes"] == snap.num_of_removes
     assert res["live_key_sum"] == key_sum(snap.all_files)
     assert res["tomb_key_sum"] == key_sum(snap.tombstones)
+    # full records, not only paths: every field of every winner (BASELINE.md correctness gate)
+    assert (res["live_record_sum"], res["tomb_record_sum"]) == O.record_sums(snap.all_files, snap.tombstones)
 
 
 @pytest.mark.parametrize("name", ["delta-0.1.0", "delta-0.2.0", "dbr_8_0_non_generated_columns"])
@@ -75,3 +77,12 @@ def test_canonical_keys_and_escapes(exe, tmp_path):
             f.write("\n".join(lines) + "\n")
     for cutoff in (0, 8):
         check(run(exe, lp, cutoff), O.state_reconstruction(O.get_log_segment(lp), cutoff))
+
+
+@pytest.mark.parametrize("cutoff", [0, 1_600_000_100_005])
+@pytest.mark.parametrize("threads", [1, 3])
+def test_record_corpus(exe, tmp_path, cutoff, threads):
+    """The full-record checksum over a log that exercises every field (tests/record_corpus.py)."""
+    from tests import record_corpus as R
+    lp = R.build(str(tmp_path / "t"))
+    check(run(exe, lp, cutoff, threads), O.state_reconstruction(O.get_log_segment(lp), cutoff))

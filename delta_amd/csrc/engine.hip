@@ -7,6 +7,11 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <dlfcn.h>
+#include <sys/mman.h>
+#include <unistd.h>
+#include <sys/stat.h>
+#include <fcntl.h>
+#include <thread>
 
 #include <algorithm>
 #include <atomic>
@@ -67,6 +72,28 @@ struct dr_ctx {
   std::multimap<size_t, void*> free_blocks;
   std::unordered_map<void*, size_t> sizes;
   std::mutex mu;
+  // pinned bounce slots of the staging readers (two per reader thread, created on the first large
+  // staging and kept for the context's life): a chunk is read into a slot, copied to the pageable
+  // host copy, and DMA'd to HBM from the slot; an event per slot guards its reuse
+  static constexpr size_t kBounceBytes = size_t(8) << 20;
+  std::vector<uint8_t*> bounce;
+  std::vector<hipEvent_t> bounce_ev;
+  void ensure_bounce(size_t slots) {
+    while (bounce.size() < slots) {
+      void* p = nullptr;
+      if (hipHostMalloc(&p, kBounceBytes, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        fail(DR_E_OOM, "pinned staging slot");
+      }
+      hipEvent_t e;
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+        (void)hipHostFree(p);
+        fail(DR_E_DEVICE, "staging event");
+      }
+      bounce.push_back(static_cast<uint8_t*>(p));
+      bounce_ev.push_back(e);
+    }
+  }
 
   void* alloc(size_t n) {
     n = (n + 255) & ~size_t(255);
@@ -299,9 +326,55 @@ struct PagePlan {
   DBuf<uint64_t> s_ba_tile_off, s_ba_kept;
 };
 
+// Host copy of a staged segment's bytes (the host side keeps them: checkpoint footers / page headers
+// for planning, non-file JSON lines, dr_parse_commits' line views). Large stagings are pinned
+// (hipHostMalloc), so the chunked H2D copies that overlap the file reads are plain DMA; small ones
+// (a streaming tail's commit) are ordinary heap memory. `n` bytes are the payload; the allocation
+// holds `pad` more zero bytes.
+struct HostBytes {
+  uint8_t* p = nullptr;
+  size_t n = 0, cap = 0;
+  bool pinned = false;
+  HostBytes() = default;
+  HostBytes(const HostBytes&) = delete;
+  HostBytes& operator=(const HostBytes&) = delete;
+  ~HostBytes() { release(); }
+  void release() {
+    if (p) {
+      if (pinned) (void)hipHostFree(p);
+      else std::free(p);
+    }
+    p = nullptr;
+    n = cap = 0;
+  }
+  void alloc(size_t bytes, size_t pad, bool pin) {
+    release();
+    cap = bytes + pad;
+    pinned = pin;
+    if (pin && hipHostMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(cap, 1), hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      p = nullptr;
+      pinned = false;
+    }
+    if (!p && cap >= (size_t(64) << 20)) {  // large: 2 MiB-aligned, transparent huge pages (fewer faults)
+      if (posix_memalign(reinterpret_cast<void**>(&p), size_t(2) << 20, cap) != 0) p = nullptr;
+      if (p) (void)madvise(p, cap, MADV_HUGEPAGE);
+    }
+    if (!p) p = static_cast<uint8_t*>(std::malloc(std::max<size_t>(cap, 1)));
+    if (!p) fail(DR_E_OOM, fmt("host staging buffer of %zu bytes", cap));
+    n = bytes;
+    if (pad) memset(p + bytes, 0, pad);
+  }
+  uint8_t* data() { return p; }
+  const uint8_t* data() const { return p; }
+  size_t size() const { return n; }
+  uint8_t& operator[](size_t i) { return p[i]; }
+  const uint8_t& operator[](size_t i) const { return p[i]; }
+};
+
 struct StagedData {
   dr_ctx* ctx = nullptr;
-  std::vector<uint8_t> h_json, h_pq;
+  HostBytes h_json, h_pq;
   DBuf<uint8_t> d_json, d_pq;
   std::vector<JsonFileRec> jfiles;
   std::vector<CkPart> parts;
@@ -882,7 +955,10 @@ static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_
   launch_pq_data(pa, stream);
 }
 
+static double now_s();
+
 static void plan_checkpoint(StagedData& s) {
+  const double t0 = now_s();
   uint64_t row_base = 0;
   for (CkPart& part : s.parts) {
     part.meta = pq::parse_footer(s.h_pq.data() + part.off, part.len);
@@ -906,54 +982,267 @@ static void plan_checkpoint(StagedData& s) {
   }
   if (!s.has_col[HC_ADD_PATH]) fail(DR_E_PARQUET, "checkpoint has no add.path column");
   s.hot.paths.assign(kHotPath, kHotPath + HC_N);
+  const double t1 = now_s();
   plan_pages(s, s.hot);
+  const double t2 = now_s();
   for (CkPart& part : s.parts) decode_ck_nonfile(s, part, 0);  // entry rows already include part.row_base
+  if (std::getenv("DR_STAGE_DEBUG"))
+    std::fprintf(stderr, "plan_checkpoint: %zu parts, footers %.3f s, pages %.3f s (%zu pages), non-file rows %.3f s\n",
+                 s.parts.size(), t1 - t0, t2 - t1, s.hot.pages.size(), now_s() - t2);
 }
 
-// rg_lo / rg_hi (optional, per file): stage only row groups [rg_lo, rg_hi) of a checkpoint part
-// (a multi-GPU shard's slice of the checkpoint; -1 = to the end).
-static std::shared_ptr<StagedData> stage_files(dr_ctx* ctx, const dr_file* files, int32_t nfiles,
-                                               const int32_t* rg_lo = nullptr, const int32_t* rg_hi = nullptr) {
+// One segment file to stage: caller-owned bytes (dr_stage) or a file the library reads itself
+// (dr_stage_log / a shard's slice). rg_lo / rg_hi: stage only row groups [rg_lo, rg_hi) of a
+// checkpoint part (a multi-GPU shard's slice of the checkpoint; -1 = to the end).
+struct StageSrc {
+  int64_t version = 0;
+  int32_t kind = DR_FILE_JSON, part = 0;
+  const uint8_t* data = nullptr;  // borrowed bytes, or null: read `path`
+  uint64_t len = 0;
+  std::string path;
+  int32_t rg_lo = 0, rg_hi = -1;
+};
+
+static double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Staging: the files' bytes go into the host buffers (h_json: the commits concatenated, each
+// newline-terminated; h_pq: the checkpoint parts, 16-byte aligned) and into HBM. Large stagings are
+// cut into 32 MiB chunks that worker threads read (pread, or memcpy from caller bytes) in parallel,
+// counting the JSON newlines as they go; each finished chunk's H2D copy is issued at once from the
+// pinned buffer, so the DMA overlaps the remaining reads and the host planning of the checkpoint.
+static std::shared_ptr<StagedData> stage_sources(dr_ctx* ctx, std::vector<StageSrc>& src) {
+  const bool dbg = std::getenv("DR_STAGE_DEBUG") != nullptr;
+  const double t0 = now_s();
   auto s = std::make_shared<StagedData>();
   s->ctx = ctx;
-  std::vector<const dr_file*> js, cks;
-  for (int32_t i = 0; i < nfiles; ++i) (files[i].kind == DR_FILE_CHECKPOINT ? cks : js).push_back(&files[i]);
-  std::stable_sort(cks.begin(), cks.end(), [](const dr_file* a, const dr_file* b) { return a->part < b->part; });
-  // JSON: concatenation, every file newline-terminated
-  for (const dr_file* f : js) {
-    JsonFileRec r{f->version, s->h_json.size(), f->len};
-    s->h_json.insert(s->h_json.end(), f->data, f->data + f->len);
-    if (f->len == 0 || f->data[f->len - 1] != '\n') s->h_json.push_back('\n');
-    r.len = s->h_json.size() - r.off;
-    s->jfiles.push_back(r);
-    s->version = std::max(s->version, f->version);
-  }
-  const uint64_t json_len = s->h_json.size();
-  s->json_lines = uint64_t(std::count(s->h_json.begin(), s->h_json.end(), uint8_t('\n')));
-  s->h_json.resize(json_len + 64, 0);
-  for (const dr_file* f : cks) {
-    CkPart p;
-    p.off = s->h_pq.size();
-    p.len = f->len;
-    if (rg_lo) {
-      p.rg_lo = rg_lo[f - files];
-      p.rg_hi = rg_hi[f - files];
+  struct FdGuard {
+    std::vector<int> fds;
+    ~FdGuard() { for (int fd : fds) if (fd >= 0) close(fd); }
+  } fdg;
+  fdg.fds.assign(src.size(), -1);
+  // sizes (and, for files read here, whether the last byte is a newline)
+  std::vector<uint8_t> ends_nl(src.size(), 0);
+  for (size_t i = 0; i < src.size(); ++i) {
+    StageSrc& f = src[i];
+    if (f.data || f.path.empty()) {
+      ends_nl[i] = f.len && f.data[f.len - 1] == '\n';
+      continue;
     }
-    s->h_pq.insert(s->h_pq.end(), f->data, f->data + f->len);
-    s->h_pq.resize((s->h_pq.size() + 15) & ~size_t(15), 0);
-    s->parts.push_back(p);
-    s->ck_version = f->version;
-    s->version = std::max(s->version, f->version);
+    const int fd = open(f.path.c_str(), O_RDONLY);
+    if (fd < 0) fail(DR_E_IO, fmt("cannot open %s", f.path.c_str()));
+    fdg.fds[i] = fd;
+    struct stat stt;
+    if (fstat(fd, &stt) != 0) fail(DR_E_IO, fmt("cannot stat %s", f.path.c_str()));
+    f.len = uint64_t(stt.st_size);
+    if (f.kind == DR_FILE_JSON && f.len) {
+      uint8_t last = 0;
+      if (pread(fd, &last, 1, off_t(f.len - 1)) != 1) fail(DR_E_IO, fmt("read failed on %s", f.path.c_str()));
+      ends_nl[i] = last == '\n';
+    }
   }
-  s->h_pq.resize(s->h_pq.size() + 64, 0);
-  s->d_json = DBuf<uint8_t>(ctx, s->h_json.size());
-  s->d_pq = DBuf<uint8_t>(ctx, s->h_pq.size());
-  HIP_OK(hipMemcpyAsync(s->d_json.p, s->h_json.data(), s->h_json.size(), hipMemcpyHostToDevice, ctx->stream));
-  HIP_OK(hipMemcpyAsync(s->d_pq.p, s->h_pq.data(), s->h_pq.size(), hipMemcpyHostToDevice, ctx->stream));
-  s->h_json.resize(json_len);
+  // layout: JSON in the given order, checkpoint parts by part number
+  std::vector<size_t> js, cks;
+  for (size_t i = 0; i < src.size(); ++i) (src[i].kind == DR_FILE_CHECKPOINT ? cks : js).push_back(i);
+  std::stable_sort(cks.begin(), cks.end(), [&](size_t a, size_t b) { return src[a].part < src[b].part; });
+  std::vector<uint64_t> host_off(src.size(), 0), region(src.size(), 0);
+  uint64_t json_len = 0, added_nl = 0;
+  for (size_t i : js) {
+    const StageSrc& f = src[i];
+    host_off[i] = json_len;
+    region[i] = f.len + (ends_nl[i] ? 0 : 1);
+    added_nl += ends_nl[i] ? 0 : 1;
+    json_len += region[i];
+    s->jfiles.push_back(JsonFileRec{f.version, host_off[i], region[i]});
+    s->version = std::max(s->version, f.version);
+  }
+  uint64_t pq_len = 0;
+  for (size_t i : cks) {
+    const StageSrc& f = src[i];
+    host_off[i] = pq_len;
+    region[i] = (f.len + 15) & ~uint64_t(15);
+    pq_len += region[i];
+    CkPart p;
+    p.off = host_off[i];
+    p.len = f.len;
+    p.rg_lo = f.rg_lo;
+    p.rg_hi = f.rg_hi;
+    s->parts.push_back(p);
+    s->ck_version = f.version;
+    s->version = std::max(s->version, f.version);
+  }
+  const uint64_t total = json_len + pq_len;
+  const bool big = total >= (uint64_t(64) << 20);
+  // DR_STAGE_PINNED=1: the host copy itself pinned (one DMA per chunk straight from it; pinning
+  // 2.6 GB costs ~0.2 s per staging); default: pageable host copy + the context's pinned bounce slots
+  const char* pin_env = std::getenv("DR_STAGE_PINNED");
+  const bool pin = big && pin_env && std::atoi(pin_env) != 0;
+  s->h_json.alloc(json_len, 64, pin);
+  s->h_pq.alloc(pq_len, 64, pin);
+  for (size_t i : js) if (!ends_nl[i]) s->h_json[host_off[i] + src[i].len] = '\n';
+  for (size_t i : cks) memset(s->h_pq.data() + host_off[i] + src[i].len, 0, region[i] - src[i].len);
+  s->d_json = DBuf<uint8_t>(ctx, json_len + 64);
+  s->d_pq = DBuf<uint8_t>(ctx, pq_len + 64);
+  const int nthreads = big ? std::max(1, std::min<int>(16, int(std::thread::hardware_concurrency()))) : 0;
+  const bool bounce = big && !pin;
+  if (bounce) ctx->ensure_bounce(size_t(2 * nthreads));
+  const double t_layout = now_s();
+  // chunks: (source, offset in the file, length); the last chunk of a file also carries the file's
+  // region padding (added newline / alignment zeroes) in its H2D copy
+  struct Chunk { size_t f; uint64_t off, len, h2d_len; };
+  const uint64_t CH = bounce ? uint64_t(dr_ctx::kBounceBytes) - 16 : uint64_t(32) << 20;
+  std::vector<Chunk> chunks;
+  for (size_t i = 0; i < src.size(); ++i) {
+    uint64_t o = 0;
+    do {
+      const uint64_t l = std::min(CH, src[i].len - o);
+      const bool last = o + l >= src[i].len;
+      chunks.push_back(Chunk{i, o, l, last ? region[i] - o : l});
+      o += l;
+    } while (o < src[i].len);
+  }
+  std::atomic<uint64_t> newlines{added_nl};
+  std::atomic<uint64_t> h2d{0};
+  std::atomic<int> err_flag{0};
+  std::string err_msg;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<size_t> done;
+  std::atomic<size_t> next{0};
+  auto host_ptr = [&](const Chunk& c) {
+    const size_t i = c.f;
+    return (src[i].kind == DR_FILE_CHECKPOINT ? s->h_pq.data() : s->h_json.data()) + host_off[i] + c.off;
+  };
+  auto dev_ptr = [&](const Chunk& c) {
+    return (src[c.f].kind == DR_FILE_CHECKPOINT ? s->d_pq.p : s->d_json.p) + host_off[c.f] + c.off;
+  };
+  auto set_err = [&](const std::string& m) {
+    std::lock_guard<std::mutex> g(mu);
+    if (!err_flag.exchange(1)) err_msg = m;
+  };
+  // read `c` into dst (pread or memcpy from the caller's bytes)
+  auto read_chunk = [&](const Chunk& c, uint8_t* dst) {
+    const StageSrc& f = src[c.f];
+    if (f.data) {
+      if (c.len) memcpy(dst, f.data + c.off, c.len);
+      return true;
+    }
+    uint64_t got = 0;
+    while (got < c.len) {
+      const ssize_t r = pread(fdg.fds[c.f], dst + got, c.len - got, off_t(c.off + got));
+      if (r <= 0) {
+        set_err(fmt("read failed on %s", f.path.c_str()));
+        return false;
+      }
+      got += uint64_t(r);
+    }
+    return true;
+  };
+  // bounce mode: every worker reads into its own two pinned slots in turn, copies the chunk to the
+  // host copy and issues the slot's DMA itself (disjoint regions, so the order does not matter)
+  auto work_bounce = [&](int t) {
+    if (hipSetDevice(ctx->device) != hipSuccess) { set_err("hipSetDevice failed in a staging worker"); return; }
+    int turn = 0;
+    for (size_t k; (k = next++) < chunks.size() && !err_flag.load();) {
+      const Chunk& c = chunks[k];
+      const size_t slot = size_t(2 * t + turn);
+      turn ^= 1;
+      if (hipEventSynchronize(ctx->bounce_ev[slot]) != hipSuccess) { set_err("staging slot wait failed"); return; }
+      uint8_t* b = ctx->bounce[slot];
+      if (!read_chunk(c, b)) return;
+      uint8_t* dst = host_ptr(c);
+      const uint64_t pad = c.h2d_len - c.len;  // the file region's padding, already in the host copy
+      if (pad) memcpy(b + c.len, dst + c.len, pad);
+      memcpy(dst, b, c.len);
+      if (src[c.f].kind == DR_FILE_JSON) newlines += uint64_t(std::count(b, b + c.len, uint8_t('\n')));
+      if (c.h2d_len) {
+        if (hipMemcpyAsync(dev_ptr(c), b, c.h2d_len, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+            hipEventRecord(ctx->bounce_ev[slot], ctx->stream) != hipSuccess) {
+          set_err("staging H2D copy failed");
+          return;
+        }
+        h2d += c.h2d_len;
+      }
+    }
+  };
+  // direct mode: read into the host copy; the calling thread issues the finished chunks' copies
+  auto work_direct = [&] {
+    for (size_t k; (k = next++) < chunks.size();) {
+      const Chunk& c = chunks[k];
+      uint8_t* dst = host_ptr(c);
+      if (!err_flag.load() && read_chunk(c, dst) && src[c.f].kind == DR_FILE_JSON)
+        newlines += uint64_t(std::count(dst, dst + c.len, uint8_t('\n')));
+      std::lock_guard<std::mutex> g(mu);
+      done.push_back(k);
+      cv.notify_one();
+    }
+  };
+  std::vector<std::thread> pool;
+  if (bounce) {
+    for (int t = 0; t < nthreads; ++t) pool.emplace_back(work_bounce, t);
+    for (auto& t : pool) t.join();
+  } else {
+    for (int t = 0; t < nthreads; ++t) pool.emplace_back(work_direct);
+    if (!nthreads) work_direct();
+    size_t issued = 0;
+    try {
+      while (issued < chunks.size()) {
+        std::vector<size_t> batch;
+        {
+          std::unique_lock<std::mutex> g(mu);
+          cv.wait(g, [&] { return !done.empty(); });
+          batch.swap(done);
+        }
+        for (size_t k : batch) {
+          const Chunk& c = chunks[k];
+          if (c.h2d_len && !err_flag.load())
+            HIP_OK(hipMemcpyAsync(dev_ptr(c), host_ptr(c), c.h2d_len, hipMemcpyHostToDevice, ctx->stream));
+          h2d += c.h2d_len;
+          ++issued;
+        }
+      }
+    } catch (...) {
+      err_flag = 1;  // the workers stop reading; join them before the buffers go away
+      for (auto& t : pool) t.join();
+      (void)hipStreamSynchronize(ctx->stream);
+      throw;
+    }
+    for (auto& t : pool) t.join();
+  }
+  if (err_flag.load()) {
+    (void)hipStreamSynchronize(ctx->stream);
+    fail(DR_E_IO, err_msg);
+  }
+  HIP_OK(hipMemcpyAsync(s->d_json.p + json_len, s->h_json.data() + json_len, 64, hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipMemcpyAsync(s->d_pq.p + pq_len, s->h_pq.data() + pq_len, 64, hipMemcpyHostToDevice, ctx->stream));
+  s->json_lines = newlines.load();
+  const double t_read = now_s();
   plan_checkpoint(*s);
+  const double t_plan = now_s();
   HIP_OK(hipStreamSynchronize(ctx->stream));
+  if (dbg)
+    std::fprintf(stderr, "stage: %.1f MB (%.1f MB H2D, %s, %d threads, %zu chunks): layout %.3f s, read+h2d issue %.3f s, "
+                 "plan %.3f s, h2d drain %.3f s, total %.3f s\n", double(total) / 1e6, double(h2d.load()) / 1e6,
+                 s->h_json.pinned ? "pinned" : bounce ? "pageable + pinned bounce" : "pageable", nthreads, chunks.size(), t_layout - t0, t_read - t_layout, t_plan - t_read, now_s() - t_plan, now_s() - t0);
   return s;
+}
+
+static std::shared_ptr<StagedData> stage_files(dr_ctx* ctx, const dr_file* files, int32_t nfiles,
+                                               const int32_t* rg_lo = nullptr, const int32_t* rg_hi = nullptr) {
+  std::vector<StageSrc> src(size_t(std::max(nfiles, 0)));
+  for (int32_t i = 0; i < nfiles; ++i) {
+    src[size_t(i)].version = files[i].version;
+    src[size_t(i)].kind = files[i].kind;
+    src[size_t(i)].part = files[i].part;
+    src[size_t(i)].data = files[i].data;
+    src[size_t(i)].len = files[i].len;
+    if (rg_lo) {
+      src[size_t(i)].rg_lo = rg_lo[i];
+      src[size_t(i)].rg_hi = rg_hi[i];
+    }
+  }
+  return stage_sources(ctx, src);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -3374,16 +3663,18 @@ static std::shared_ptr<StagedData> stage_shard(dr_ctx* ctx, const std::string& l
     }
     mine.push_back(u);
   }
-  std::vector<std::vector<uint8_t>> bytes;
-  std::vector<dr_file> files;
-  std::vector<int32_t> lo, hi;
-  for (auto& u : mine) bytes.push_back(read_file(log_path + "/" + u.f.name));
-  for (size_t k = 0; k < mine.size(); ++k) {
-    files.push_back(dr_file{mine[k].f.version, mine[k].f.kind, mine[k].f.part, bytes[k].data(), bytes[k].size()});
-    lo.push_back(mine[k].rg_lo);
-    hi.push_back(mine[k].rg_hi);
+  std::vector<StageSrc> src;
+  for (auto& u : mine) {
+    StageSrc x;
+    x.version = u.f.version;
+    x.kind = u.f.kind;
+    x.part = u.f.part;
+    x.path = log_path + "/" + u.f.name;
+    x.rg_lo = u.rg_lo;
+    x.rg_hi = u.rg_hi;
+    src.push_back(std::move(x));
   }
-  auto s = stage_files(ctx, files.data(), int32_t(files.size()), lo.data(), hi.data());
+  auto s = stage_sources(ctx, src);
   s->version = seg.version;
   return s;
 }
@@ -3893,6 +4184,8 @@ void dr_ctx_destroy(dr_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   (void)hipStreamSynchronize(ctx->stream2);
   ctx->trim();
+  for (uint8_t* p : ctx->bounce) (void)hipHostFree(p);
+  for (hipEvent_t e : ctx->bounce_ev) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(ctx->stream);
   (void)hipStreamDestroy(ctx->stream2);
   delete ctx;
@@ -4002,18 +4295,18 @@ int dr_stage_log(dr_ctx* ctx, const char* log_path, int64_t version_to_load, dr_
   return guard(ctx, [&] {
     HIP_OK(hipSetDevice(ctx->device));
     LogSegmentInfo seg = get_log_segment(log_path, version_to_load);
-    std::vector<std::vector<uint8_t>> bytes;
-    std::vector<dr_file> files;
-    for (auto* list : {&seg.checkpoint, &seg.deltas})
-      for (auto& f : *list) bytes.push_back(read_file(std::string(log_path) + "/" + f.name));
-    size_t k = 0;
+    std::vector<StageSrc> src;
     for (auto* list : {&seg.checkpoint, &seg.deltas})
       for (auto& f : *list) {
-        files.push_back(dr_file{f.version, f.kind, f.part, bytes[k].data(), bytes[k].size()});
-        ++k;
+        StageSrc x;
+        x.version = f.version;
+        x.kind = f.kind;
+        x.part = f.part;
+        x.path = std::string(log_path) + "/" + f.name;
+        src.push_back(std::move(x));
       }
     auto s = std::make_unique<dr_staged>();
-    s->d = stage_files(ctx, files.data(), int32_t(files.size()));
+    s->d = stage_sources(ctx, src);
     s->d->version = seg.version;
     *out = s.release();
   });

@@ -865,7 +865,14 @@ static void plan_pages(StagedData& s, PagePlan& P) {
 }
 
 // Inflate + decode every page of a plan into `pa.cols` (allocated by the caller for P.levels).
-static uint64_t scan_scratch_for(uint64_t n) { return scan_scratch_bytes(std::max<uint64_t>(n, uint64_t(1) << 23)); }
+// Scan scratch for n counts (at least 2^23 entries). DR_SCAN_SCRATCH_MAX (test hook) caps the size,
+// so a scan too large for its scratch is shown to fail loudly (launch_scan_u32 refuses it).
+static uint64_t scan_scratch_for(uint64_t n) {
+  uint64_t b = scan_scratch_bytes(std::max<uint64_t>(n, uint64_t(1) << 23));
+  if (const char* cap = std::getenv("DR_SCAN_SCRATCH_MAX")) b = std::min<uint64_t>(b, std::strtoull(cap, nullptr, 10));
+  return b;
+}
+static ScanScratch ss(const DBuf<uint8_t>& b) { return ScanScratch{b.p, b.n}; }
 
 static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_t>& dict_ptr, DBuf<uint32_t>& dict_len,
                          DBuf<uint32_t>& err, void*) {
@@ -873,7 +880,7 @@ static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_
   // scan scratch for the plan's largest scan: SNAPPY chunk element counts, PLAIN BYTE_ARRAY tiles
   // (a 100M-row checkpoint has 26M chunks: a scratch sized for 2^23 entries was overrun)
   DBuf<uint8_t> own_scratch(ctx, scan_scratch_for(std::max<uint64_t>(P.nchunks, P.ba_tiles.size())));
-  void* scratch = own_scratch.p;
+  const ScanScratch scratch = ss(own_scratch);
   pa.pages = P.d_pages.p;
   pa.npages = uint32_t(P.pages.size());
   dict_ptr = DBuf<uint64_t>(ctx, P.dict_entries);
@@ -1305,7 +1312,7 @@ static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
   uint64_t nlines = 0;
   if (nbj) {
     launch_json_index(s.d_json.p, json_len, jcounts.p, jslots.p, stream);
-    launch_scan_u32(jcounts.p, joff.p, nbj, scratch.p, stream);
+    launch_scan_u32(jcounts.p, joff.p, nbj, ss(scratch), stream);
     // the line count is known from staging (no read-back between the index and the parse)
     nlines = s.json_lines;
     if (std::getenv("DR_CHECK_LINES") && d2h_one(joff.p + nbj, stream) != nlines)
@@ -1480,7 +1487,7 @@ static void reduce_actions(dr_ctx* ctx, dr_state* st, int64_t cutoff, uint32_t f
   DBuf<PartRec> rec(ctx, N);
   pa.rec = rec.p;
   launch_bucket_hist(pa, stream);
-  launch_scan_u32(tcnt.p, toff.p, ncell, pscratch.p, stream);
+  launch_scan_u32(tcnt.p, toff.p, ncell, ss(pscratch), stream);
   launch_bucket_offsets(toff.p, nb, nt, boff.p, stream);
   launch_bucket_scatter(pa, stream);
   // ---- K4: per-bucket last-writer-wins ----
@@ -1727,8 +1734,8 @@ static void materialize(dr_state& st) {
   DBuf<uint64_t> lp(ctx, C + 1), tp(ctx, C + 1);
   DBuf<uint8_t> scratch(ctx, scan_scratch_for(C));
   launch_ix_classify(a, vals, C, st.cutoff, lf.p, tf.p, stream);
-  launch_scan_u32(lf.p, lp.p, C, scratch.p, stream);
-  launch_scan_u32(tf.p, tp.p, C, scratch.p, stream);
+  launch_scan_u32(lf.p, lp.p, C, ss(scratch), stream);
+  launch_scan_u32(tf.p, tp.p, C, ss(scratch), stream);
   const uint64_t nl = d2h_one(lp.p + C, stream), nt = d2h_one(tp.p + C, stream);
   if (int64_t(nl) != st.counts.num_files || int64_t(nt) != st.counts.num_removes)
     fail(DR_E_INTERNAL, fmt("apply chain index disagrees with its counters (%llu/%lld files, %llu/%lld tombstones)",
@@ -2034,7 +2041,7 @@ static void decode_export_side(dr_state& st, int which, ExpDecoded& D) {
     DBuf<uint64_t> rpos(ctx, E + 1);
     DBuf<uint8_t> scratch(ctx, scan_scratch_for(E));
     launch_rep0_flags(D.rep[kc].p, E, rflag.p, stream);
-    launch_scan_u32(rflag.p, rpos.p, E, scratch.p, stream);
+    launch_scan_u32(rflag.p, rpos.p, E, ss(scratch), stream);
     if (d2h_one(rpos.p + E, stream) != R) fail(DR_E_PARQUET, pre + kExpLeaf[kc] + ": one map per checkpoint row expected");
     D.row_start[m] = DBuf<uint64_t>(ctx, R + 1);
     launch_row_starts(D.rep[kc].p, E, rpos.p, D.row_start[m].p, stream);
@@ -2082,7 +2089,7 @@ static void export_device(dr_state& st, int which, DevExport& X, uint64_t lo = 0
   launch_gather_u32(st.path_len.p, didx, n, X.path_len.p, stream);
   launch_gather_u64(reinterpret_cast<const uint64_t*>(st.delts.p), didx, n, X.delts.p, stream);
   launch_gather_u8(st.flags.p, didx, n, X.flags.p, stream);
-  launch_scan_u32(X.path_len.p, X.path_off.p, n, scratch.p, stream);
+  launch_scan_u32(X.path_len.p, X.path_off.p, n, ss(scratch), stream);
   if (!n) HIP_OK(hipMemsetAsync(X.path_off.p, 0, 8, stream));
   const uint64_t nb = n ? d2h_one(X.path_off.p + n, stream) : 0;
   X.path_bytes = DBuf<uint8_t>(ctx, nb + 16);  // +16: whole-word loads of the record hash
@@ -2140,7 +2147,7 @@ static void export_device(dr_state& st, int which, DevExport& X, uint64_t lo = 0
   }
   launch_export(a, stream);  // pass 1: scalars + counts
   for (int k = 0; k < EXC_N; ++k) {
-    launch_scan_u32(cnt[k].p, X.off[k].p, n, scratch.p, stream);
+    launch_scan_u32(cnt[k].p, X.off[k].p, n, ss(scratch), stream);
     if (!n) HIP_OK(hipMemsetAsync(X.off[k].p, 0, 8, stream));
     a.off[k] = X.off[k].p;
   }
@@ -2538,7 +2545,7 @@ static void build_pv_columns(dr_state& st, const std::vector<std::pair<std::stri
       rflag = DBuf<uint32_t>(ctx, E);
       rpos = DBuf<uint64_t>(ctx, E + 1);
       launch_rep0_flags(krep.p, E, rflag.p, stream);
-      launch_scan_u32(rflag.p, rpos.p, E, scratch.p, stream);
+      launch_scan_u32(rflag.p, rpos.p, E, ss(scratch), stream);
       if (d2h_one(rpos.p + E, stream) != R) fail(DR_E_PARQUET, "add.partitionValues: one map per checkpoint row expected");
       row_start = DBuf<uint64_t>(ctx, R + 1);
       launch_row_starts(krep.p, E, rpos.p, row_start.p, stream);
@@ -3146,8 +3153,8 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
         a.vbytes = vb.p;
         tmark("host_leaves");
         launch_enc_count(a, stream);
-        launch_scan_u32(nl.p, lo.p, R, scratch.p, stream);
-        launch_scan_u32(vb.p, vo.p, R, scratch.p, stream);
+        launch_scan_u32(nl.p, lo.p, R, ss(scratch), stream);
+        launch_scan_u32(vb.p, vo.p, R, ss(scratch), stream);
         nlev = d2h_one(lo.p + R, stream);
         const uint64_t nvb = d2h_one(vo.p + R, stream);
         DBuf<uint8_t> dl(ctx, nlev + 8), rl(ctx, L.max_rep ? nlev + 8 : 1), vv(ctx, nvb + 8);
@@ -3199,7 +3206,7 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
           DBuf<uint32_t> czl(ctx, nfrag + 1);
           DBuf<uint64_t> czo(ctx, nfrag + 1);
           launch_snap_compress(bodyd.p, bsize, cz.p, czl.p, stream);
-          launch_scan_u32(czl.p, czo.p, nfrag, scratch.p, stream);
+          launch_scan_u32(czl.p, czo.p, nfrag, ss(scratch), stream);
           dev_out_len = d2h_one(czo.p + nfrag, stream);
           dev_out = DBuf<uint8_t>(ctx, dev_out_len + 1);
           launch_snap_gather(cz.p, czl.p, czo.p, uint32_t(nfrag), dev_out.p, stream);
@@ -3552,7 +3559,7 @@ static void partition_groups(dr_state& st, const int64_t* rows, int64_t nrows, s
   DBuf<uint64_t> pos(ctx, n + 1);
   DBuf<uint8_t> scratch(ctx, scan_scratch_for(n));
   launch_group_flags(keys.p, n, g, flag.p, stream);
-  launch_scan_u32(flag.p, pos.p, n, scratch.p, stream);
+  launch_scan_u32(flag.p, pos.p, n, ss(scratch), stream);
   const uint64_t ng = d2h_one(pos.p + n, stream);
   DBuf<int64_t> starts(ctx, ng);
   launch_select(flag.p, pos.p, n, starts.p, stream);
@@ -3567,7 +3574,7 @@ static std::vector<int64_t> select_flags(dr_state& st, DBuf<uint32_t>& flag) {
   hipStream_t stream = ctx->stream;
   DBuf<uint8_t> scratch(ctx, scan_scratch_for(st.n_live));
   DBuf<uint64_t> pos(ctx, st.n_live + 1);
-  launch_scan_u32(flag.p, pos.p, st.n_live, scratch.p, stream);
+  launch_scan_u32(flag.p, pos.p, st.n_live, ss(scratch), stream);
   const uint64_t nsel = st.n_live ? d2h_one(pos.p + st.n_live, stream) : 0;
   DBuf<int64_t> sel(ctx, nsel);
   launch_select(flag.p, pos.p, st.n_live, sel.p, stream);
@@ -3708,7 +3715,7 @@ static void shard_begin(dr_shard& sh, uint64_t* send_counts, uint64_t* send_byte
   ShardArgs a{st.kind.p, st.flags.p, st.key.p, st.size.p, st.delts.p, st.path_len.p, N, sh.world, nt,
               bcnt.p, boff.p, nullptr, 0};
   launch_shard_count(a, stream);
-  launch_scan_u32(bcnt.p, boff.p, nc, scratch.p, stream);
+  launch_scan_u32(bcnt.p, boff.p, nc, ss(scratch), stream);
   std::vector<uint64_t> hoff = d2h(boff.p, nc + 1, stream);
   sh.nsend = hoff[nc];
   sh.send_idx = DBuf<uint32_t>(ctx, sh.nsend);
@@ -3720,7 +3727,7 @@ static void shard_begin(dr_shard& sh, uint64_t* send_counts, uint64_t* send_byte
   sh.send_poff = DBuf<uint64_t>(ctx, sh.nsend + 1);
   launch_gather_u32(st.path_len.p, sh.send_idx.p, sh.nsend, sh.send_plen.p, stream);
   DBuf<uint8_t> scratch2(ctx, scan_scratch_for(sh.nsend));
-  launch_scan_u32(sh.send_plen.p, sh.send_poff.p, sh.nsend, scratch2.p, stream);
+  launch_scan_u32(sh.send_plen.p, sh.send_poff.p, sh.nsend, ss(scratch2), stream);
   for (uint32_t d = 0; d < sh.world; ++d) {
     const uint64_t s0 = hoff[uint64_t(d) * nt], s1 = d + 1 < sh.world ? hoff[uint64_t(d + 1) * nt] : sh.nsend;
     send_counts[d] = s1 - s0;
@@ -3762,7 +3769,7 @@ static void shard_reduce(dr_shard& sh, const void* recv_rec, uint64_t n, const v
   DBuf<uint64_t> poff(ctx, n + 1);
   DBuf<uint8_t> scratch(ctx, scan_scratch_for(n));
   launch_shard_plen(rec, n, own->path_len.p, stream);
-  launch_scan_u32(own->path_len.p, poff.p, n, scratch.p, stream);
+  launch_scan_u32(own->path_len.p, poff.p, n, ss(scratch), stream);
   ActionArrays act{own->kind.p, own->flags.p, own->key.p, own->path_ptr.p, own->path_len.p, own->size.p,
                    own->delts.p, own->src_off.p, own->src_len.p};
   launch_shard_unpack(rec, n, static_cast<const uint8_t*>(recv_path), poff.p, act, stream);
@@ -3784,8 +3791,8 @@ static dr_state* shard_finish(dr_shard& sh, const uint8_t* verdict_back) {
   DBuf<uint64_t> pl(ctx, n + 1), pt(ctx, n + 1);
   DBuf<uint8_t> scratch(ctx, scan_scratch_for(n));
   launch_verdict_flags(verdict_back, n, fl.p, ft.p, stream);
-  launch_scan_u32(fl.p, pl.p, n, scratch.p, stream);
-  launch_scan_u32(ft.p, pt.p, n, scratch.p, stream);
+  launch_scan_u32(fl.p, pl.p, n, ss(scratch), stream);
+  launch_scan_u32(ft.p, pt.p, n, ss(scratch), stream);
   st.n_live = d2h_one(pl.p + n, stream);
   st.n_tomb = d2h_one(pt.p + n, stream);
   st.live = DBuf<uint32_t>(ctx, st.n_live);

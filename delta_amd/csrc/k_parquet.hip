@@ -686,7 +686,7 @@ __global__ void k_ckpt_assemble(CkptAssembleArgs a) {
 }  // namespace dev
 
 uint32_t ba_tile_bytes() { return dev::BA_TILE; }
-void launch_ba_bounds(const ParquetArgs& a, hipStream_t st, void* scan_scratch) {
+void launch_ba_bounds(const ParquetArgs& a, hipStream_t st, ScanScratch scan_scratch) {
   if (!a.nba_tiles) return;
   DR_LAUNCH(dev::k_ba_count, dim3(a.nba_tiles), dim3(dev::BA_T), 0, st, a);
   launch_scan_u32(a.ba_tile_cnt, a.ba_tile_off, a.nba_tiles, scan_scratch, st);

@@ -723,13 +723,16 @@ uint64_t scan_scratch_bytes(uint64_t n) {
   return (n / dev::SCAN_T + 2) * sizeof(uint64_t);
 }
 
-void launch_scan_u32(const uint32_t* in, uint64_t* out, uint64_t n, void* scratch, hipStream_t st) {
+void launch_scan_u32(const uint32_t* in, uint64_t* out, uint64_t n, ScanScratch scratch, hipStream_t st) {
   uint64_t nb = (n + dev::SCAN_T - 1) / dev::SCAN_T;
   if (nb == 0) {
     (void)hipMemsetAsync(out, 0, sizeof(uint64_t), st);
     return;
   }
-  uint64_t* sums = static_cast<uint64_t*>(scratch);
+  if (!scratch.p || scratch.bytes < scan_scratch_bytes(n))
+    throw std::runtime_error("scan of " + std::to_string(n) + " counts needs " + std::to_string(scan_scratch_bytes(n)) +
+                             " scratch bytes, the caller's scratch holds " + std::to_string(scratch.bytes));
+  uint64_t* sums = static_cast<uint64_t*>(scratch.p);
   DR_LAUNCH(dev::k_scan_reduce, dim3(unsigned(nb)), dim3(dev::SCAN_T), 0, st, in, n, sums);
   DR_LAUNCH(dev::k_scan_single, dim3(1), dim3(dev::SCAN_T), 0, st, sums, nb);
   DR_LAUNCH(dev::k_scan_apply, dim3(unsigned(nb)), dim3(dev::SCAN_T), 0, st, in, n, sums, out);

@@ -817,7 +817,7 @@ __global__ void __launch_bounds__(256) k_page_copy(const CopyJob* jobs, uint32_t
 uint32_t snappy_wg_chunks() { return dev::WG_CHUNKS; }
 uint32_t snappy_chunk_bytes() { return dev::SNAP_CH; }
 
-void launch_snappy(const SnappyArgs& a, hipStream_t st, void* scan_scratch) {
+void launch_snappy(const SnappyArgs& a, hipStream_t st, ScanScratch scan_scratch) {
   if (!a.npages) return;
   DR_LAUNCH(dev::k_snap_spec, dim3(a.nwg), dim3(dev::WG_CHUNKS), 0, st, a);
   const unsigned g = (a.nchunks + 255) / 256;

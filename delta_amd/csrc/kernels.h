@@ -68,9 +68,14 @@ void launch_json_parse(const JsonParseArgs& a, hipStream_t st);
 void launch_json_hard(const JsonParseArgs& a, hipStream_t st);
 
 // ---- scans ------------------------------------------------------------------------------------
-// Exclusive scan of n u32 counts into u64 offsets; out[n] = total. Scratch: scan_scratch_bytes(n).
+// Exclusive scan of n u32 counts into u64 offsets; out[n] = total. Scratch: scan_scratch_bytes(n);
+// a scratch smaller than that is refused (std::runtime_error -> DR_E_INTERNAL) instead of overrun.
 uint64_t scan_scratch_bytes(uint64_t n);
-void launch_scan_u32(const uint32_t* in, uint64_t* out, uint64_t n, void* scratch, hipStream_t st);
+struct ScanScratch {
+  void* p = nullptr;
+  uint64_t bytes = 0;
+};
+void launch_scan_u32(const uint32_t* in, uint64_t* out, uint64_t n, ScanScratch scratch, hipStream_t st);
 
 // ---- Parquet (K2) -------------------------------------------------------------------------------
 enum PageKind : int32_t { PG_DATA_V1 = 0, PG_DICT = 2, PG_DATA_V2 = 3 };
@@ -126,7 +131,7 @@ struct ParquetArgs {
   uint64_t* ba_kept;     // [nba_tiles * 256] kept-candidate masks (64 positions per thread)
 };
 uint32_t ba_tile_bytes();
-void launch_ba_bounds(const ParquetArgs& a, hipStream_t st, void* scan_scratch);
+void launch_ba_bounds(const ParquetArgs& a, hipStream_t st, ScanScratch scan_scratch);
 
 // SNAPPY pages (k_snappy.hip). `in` points past the varint length preamble.
 struct SnapPage {
@@ -171,7 +176,7 @@ struct SnappyArgs {
 };
 uint32_t snappy_wg_chunks();
 uint32_t snappy_chunk_bytes();
-void launch_snappy(const SnappyArgs& a, hipStream_t st, void* scan_scratch);
+void launch_snappy(const SnappyArgs& a, hipStream_t st, ScanScratch scan_scratch);
 void launch_page_copy(const CopyJob* jobs, uint32_t njobs, hipStream_t st);
 
 void launch_pq_dict(const ParquetArgs& a, hipStream_t st);

@@ -643,3 +643,46 @@ def test_snappy_periodic_dictionary_pages(engine, tmp_path, capfd, monkeypatch):
     assert counts["num_files"] == 60000 and len(tomb) == 29999
     err = capfd.readouterr().err
     assert "snappy bad page" not in err, err[-2000:]
+
+
+# ---- staging / scratch guards --------------------------------------------------------------------------
+def test_check_lines_over_edge_corpus(engine, tmp_path, monkeypatch):
+    """DR_CHECK_LINES=1 compares the staged newline count (which sizes the action arrays) with K1's
+    device count, over commits without a trailing newline, with CRLF endings, empty and blank-line
+    files, concatenated in one staging; the replay equals the oracle's."""
+    monkeypatch.setenv("DR_CHECK_LINES", "1")
+    lp = str(tmp_path / "_delta_log")
+    os.makedirs(lp)
+    line = lambda a: json.dumps(a, separators=(",", ":"))
+    bodies = {
+        0: "\r\n".join(line(a) for a in [PROTOCOL, METADATA, add("a"), add("b")]),  # CRLF, no final newline
+        1: "",                                                                       # empty commit file
+        2: "\n\n" + line(add("c")) + "\n\n" + line(remove("a", ts=5)) + "\n",        # blank lines
+        3: line(add("d", size=7)),                                                   # one line, no newline
+        4: "\r\n" + line(remove("b", ts=9)) + "\r\n",
+    }
+    for v, body in bodies.items():
+        with open(os.path.join(lp, "%020d.json" % v), "w", newline="") as f:
+            f.write(body)
+    counts, live, tomb = _same_as_oracle(engine, lp, cutoff=0)
+    assert sorted(f["path"] for f in live) == ["c", "d"] and sorted(t["path"] for t in tomb) == ["a", "b"]
+
+
+def test_scan_scratch_capacity_is_checked(engine, tmp_path, monkeypatch):
+    """A scan whose scratch is too small fails loudly (DR_E_INTERNAL) instead of writing past it --
+    the failure mode of the 100M-row SNAPPY chunk scan fixed in round 2. DR_SCAN_SCRATCH_MAX forces a
+    tiny scratch; without it the same replay succeeds."""
+    from delta_amd.delta_log import DeltaError
+    from delta_amd.testing import synth as S
+    exp = S.build_config(2, str(tmp_path), scale=0.002)
+    lp = os.path.join(str(tmp_path), "_delta_log")
+    monkeypatch.setenv("DR_SCAN_SCRATCH_MAX", "64")
+    with pytest.raises(DeltaError) as ei:
+        _gpu_replay(engine, lp, exp.min_file_retention_timestamp)
+    assert ei.value.status == 15 and "scratch" in str(ei.value)
+    monkeypatch.delenv("DR_SCAN_SCRATCH_MAX")
+    st = _gpu_replay(engine, lp, exp.min_file_retention_timestamp)
+    try:
+        assert st.counts["num_files"] == exp.num_files
+    finally:
+        st.release()

@@ -152,7 +152,7 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "dr_state_record_sums": ([vp, C.POINTER(u64), C.POINTER(u64)], C.c_int),
         "dr_filter": ([vp, C.POINTER(dr_predicate), C.POINTER(_P64), _P64], C.c_int),
         "dr_state_write_checkpoint": ([vp, i32, i32, C.c_uint32, C.c_uint64, C.POINTER(C.POINTER(C.c_uint8)),
-                                       C.POINTER(C.c_uint64), _P64], C.c_int),
+                                       C.POINTER(C.c_uint64), _P64, _P64], C.c_int),
         "dr_state_scan_order": ([vp, C.POINTER(_P64), _P64], C.c_int),
         "dr_state_set_nonfile_json": ([vp, C.c_char_p, u64, C.c_uint32], C.c_int),
         "dr_state_partition_groups": ([vp, _P64, i64, C.POINTER(_P64), C.POINTER(_P64), _P64], C.c_int),

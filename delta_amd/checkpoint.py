@@ -200,6 +200,14 @@ def checkpoint_table(state, checkpoint_v2_enabled: bool = True):
     return table, na
 
 
+def check_add_rows(written: int, num_of_files: int) -> None:
+    """Checkpoints.writeCheckpoint's check before `_last_checkpoint` is written: the add rows the parts
+    hold must be the snapshot's numOfFiles (D/Checkpoints.scala:325-328)."""
+    if written != num_of_files:
+        from .delta_log import DeltaError
+        raise DeltaError(15, "State of the checkpoint doesn't match that of the snapshot.")
+
+
 def checkpoint_file_with_parts(log_path: str, version: int, part: int, parts: int) -> str:
     return os.path.join(log_path, "%020d.checkpoint.%010d.%010d.parquet" % (version, part, parts))
 
@@ -223,17 +231,19 @@ def write_checkpoint_device(snapshot, parts: int = 1, row_group_size: int = 1 <<
     md = next((a["metaData"] for a in state.nonfile if "metaData" in a), None)
     stats, parsed = checkpoint_options(md, checkpoint_v2_enabled)
     log_path = snapshot.delta_log.log_path
-    rows = 0
+    rows = adds = 0
     for i in range(parts):
-        data, n = state.write_checkpoint_part(i + 1, parts, stats=stats, parsed=parsed is not None,
-                                              row_group_rows=row_group_size)
+        data, n, na = state.write_checkpoint_part(i + 1, parts, stats=stats, parsed=parsed is not None,
+                                                  row_group_rows=row_group_size, with_adds=True)
         rows += n
+        adds += na
         path = (os.path.join(log_path, "%020d.checkpoint.parquet" % snapshot.version) if parts <= 1
                 else checkpoint_file_with_parts(log_path, snapshot.version, i + 1, parts))
         tmp = os.path.join(os.path.dirname(path), ".%s.tmp" % os.path.basename(path))
         with open(tmp, "wb") as f:
             f.write(data)
         os.replace(tmp, path)
+    check_add_rows(adds, snapshot.num_of_files)
     meta = {"version": snapshot.version, "size": rows}
     if parts > 1:
         meta["parts"] = parts

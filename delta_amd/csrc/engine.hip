@@ -2860,6 +2860,7 @@ struct MallocBytes {
 struct CkPartOut {
   MallocBytes file;
   int64_t rows = 0;
+  int64_t add_rows = 0;  // add rows encoded (Checkpoints.scala:325-328's accumulator)
 };
 
 static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uint32_t opts, uint64_t rg_rows,
@@ -2931,6 +2932,7 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
   DevExport X[2];
   export_device(st, DR_LIVE, X[0], a0, a1);
   export_device(st, DR_TOMBSTONES, X[1], b0, b1);
+  out.add_rows = int64_t(X[0].n);
   tmark("export");
   // ---- schema (DFS) and leaves ----
   std::vector<SElem> schema;
@@ -4551,7 +4553,7 @@ int dr_state_partition_groups(dr_state* state, const int64_t* rows, int64_t nrow
 }
 
 int dr_state_write_checkpoint(dr_state* state, int32_t part, int32_t parts, uint32_t opts, uint64_t row_group_rows,
-                              uint8_t** bytes, uint64_t* len, int64_t* rows) {
+                              uint8_t** bytes, uint64_t* len, int64_t* rows, int64_t* add_rows) {
   if (!state || !bytes || !len || parts < 1 || part < 1 || part > parts) return DR_E_INVALID_ARG;
   *bytes = nullptr;
   *len = 0;
@@ -4562,6 +4564,7 @@ int dr_state_write_checkpoint(dr_state* state, int32_t part, int32_t parts, uint
     *len = o.file.size();
     *bytes = o.file.release();  // malloc'd: the caller frees it with dr_free
     if (rows) *rows = o.rows;
+    if (add_rows) *add_rows = o.add_rows;
   });
 }
 

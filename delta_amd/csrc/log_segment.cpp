@@ -164,9 +164,12 @@ LogSegmentInfo segment_from(const std::string& log_path, int64_t start_ckpt, int
   }
   verify_delta_versions(vers);
   if (vers.empty() || vers.front() != 0)
-    // DeltaErrors.logFileNotFoundException (D/DeltaErrors.scala:451-457) with the default
-    // delta.logRetentionDuration / delta.checkpointRetentionDuration (D/DeltaConfig.scala), rendered
-    // as Spark's CalendarInterval.toString
+    // DeltaErrors.logFileNotFoundException (D/DeltaErrors.scala:451-457). The listing has no
+    // metadata, so the text carries the default delta.logRetentionDuration /
+    // delta.checkpointRetentionDuration (D/DeltaConfig.scala:251-281) as Spark's
+    // CalendarInterval.toString renders them -- the reference's text on a first load; a host that
+    // holds a snapshot's metadata re-renders the configured values (delta_amd/delta_log.py:
+    // retention_text, used by DeltaLog.update)
     fail(DR_E_LOG_TRUNCATED, fmt("%s/%020lld.json: Unable to reconstruct state at version %lld as the "
                                  "transaction log has been truncated due to manual deletion or the log "
                                  "retention policy (delta.logRetentionDuration=30 days) and checkpoint "

@@ -395,19 +395,22 @@ class State:
         return res
 
     def write_checkpoint_part(self, part: int, parts: int, stats: bool = True, parsed: bool = True,
-                              row_group_rows: int = 0, snappy: bool = True) -> Tuple[bytes, int]:
+                              row_group_rows: int = 0, snappy: bool = True, with_adds: bool = False):
         """dr_state_write_checkpoint: part `part` (1-based) of `parts` as Parquet bytes, the file-action
-        columns encoded (and SNAPPY-compressed) on the GPU; returns (bytes, rows)."""
+        columns encoded (and SNAPPY-compressed) on the GPU; returns (bytes, rows), or (bytes, rows,
+        add rows) with `with_adds`."""
         buf = C.POINTER(C.c_uint8)()
         n = C.c_uint64()
         rows = C.c_int64()
+        adds = C.c_int64()
         opts = (N.DR_CKPT_STATS if stats else 0) | (N.DR_CKPT_PARSED if parsed else 0) | (N.DR_CKPT_SNAPPY if snappy else 0)
         with self.eng.lock:
             self.eng.check(self.eng.lib.dr_state_write_checkpoint(self.h, int(part), int(parts), opts, int(row_group_rows),
-                                                                  C.byref(buf), C.byref(n), C.byref(rows)))
+                                                                  C.byref(buf), C.byref(n), C.byref(rows),
+                                                                  C.byref(adds)))
         data = C.string_at(buf, n.value)
         self.eng.lib.dr_free(C.cast(buf, C.c_void_p))
-        return data, rows.value
+        return (data, rows.value, adds.value) if with_adds else (data, rows.value)
 
     def _take(self, ptr, n) -> List[int]:
         res = [ptr[i] for i in range(n)]
@@ -480,6 +483,71 @@ def interval_millis(s: str) -> int:
 def tombstone_retention_millis(metadata: Optional[dict]) -> int:
     conf = (metadata or {}).get("configuration") or {}
     return interval_millis(conf.get("delta.deletedFileRetentionDuration", DEFAULT_TOMBSTONE_RETENTION))
+
+
+# CalendarInterval parsing (IntervalUtils.safeStringToInterval, as DeltaConfigs.parseCalendarInterval
+# reads a table property) and CalendarInterval.toString, for the retention policies that
+# DeltaErrors.logFileNotFoundException renders (D/DeltaErrors.scala:451-461; D/DeltaConfig.scala:251-281).
+_IV_UNITS = {"year": ("m", 12), "years": ("m", 12), "month": ("m", 1), "months": ("m", 1),
+             "week": ("d", 7), "weeks": ("d", 7), "day": ("d", 1), "days": ("d", 1),
+             "hour": ("u", 3_600_000_000), "hours": ("u", 3_600_000_000),
+             "minute": ("u", 60_000_000), "minutes": ("u", 60_000_000),
+             "second": ("u", 1_000_000), "seconds": ("u", 1_000_000),
+             "millisecond": ("u", 1000), "milliseconds": ("u", 1000),
+             "microsecond": ("u", 1), "microseconds": ("u", 1)}
+
+
+def calendar_interval(s: str) -> Tuple[int, int, int]:
+    """(months, days, microseconds) of an interval string such as "interval 2 weeks"."""
+    from decimal import Decimal
+    t = s.strip().lower()
+    if t.startswith("interval"):
+        t = t[len("interval"):].strip()
+    toks = t.split()
+    if not toks or len(toks) % 2:
+        raise ValueError("invalid interval %r" % s)
+    acc = {"m": 0, "d": 0, "u": 0}
+    for i in range(0, len(toks), 2):
+        kind, mul = _IV_UNITS[toks[i + 1]]
+        v = Decimal(toks[i]) * mul
+        acc[kind] += int(v)
+    return acc["m"], acc["d"], acc["u"]
+
+
+def interval_to_string(months: int, days: int, micros: int) -> str:
+    """CalendarInterval.toString (Spark 3.1): "30 days", "1 years 2 months", "7 days 1 hours"."""
+    from decimal import Decimal
+    if months == 0 and days == 0 and micros == 0:
+        return "0 seconds"
+    parts = []
+
+    def unit(v, name):
+        if v:
+            parts.append("%d %s" % (v, name))
+    if months:
+        unit(int(months / 12), "years")
+        unit(months - 12 * int(months / 12), "months")
+    unit(days, "days")
+    if micros:
+        rest = micros
+        unit(int(rest / 3_600_000_000), "hours")
+        rest -= 3_600_000_000 * int(rest / 3_600_000_000)
+        unit(int(rest / 60_000_000), "minutes")
+        rest -= 60_000_000 * int(rest / 60_000_000)
+        if rest:
+            d = (Decimal(rest) / Decimal(1_000_000)).normalize()
+            parts.append("%s seconds" % format(d, "f"))
+    return " ".join(parts)
+
+
+def retention_text(metadata: Optional[dict]) -> str:
+    """The "(delta.logRetentionDuration=...) and checkpoint retention policy (...)" part of
+    logFileNotFoundException for a table's metadata (defaults 30 days / 2 days)."""
+    conf = (metadata or {}).get("configuration") or {}
+    log_r = interval_to_string(*calendar_interval(conf.get("delta.logRetentionDuration", "interval 30 days")))
+    ck_r = interval_to_string(*calendar_interval(conf.get("delta.checkpointRetentionDuration", "interval 2 days")))
+    return ("(delta.logRetentionDuration=%s) and checkpoint retention policy "
+            "(delta.checkpointRetentionDuration=%s)" % (log_r, ck_r))
 
 
 # ---- Snapshot / DeltaLog --------------------------------------------------------------------------
@@ -659,7 +727,18 @@ class DeltaLog:
         if not os.path.isdir(self.log_path):
             raise DeltaError(3, "No file found in the directory: %s." % self.log_path)
         cutoff = self.min_file_retention_timestamp
-        staged = self.engine.stage_log(self.log_path, version)
+        try:
+            staged = self.engine.stage_log(self.log_path, version)
+        except DeltaError as e:
+            # logFileNotFoundException renders the current snapshot's retention policies
+            # (SnapshotManagement's `metadata`, D/SnapshotManagement.scala:161-163); the library's
+            # listing has no metadata and renders the defaults, as on a first load
+            if e.status == 4 and self._snapshot is not None:
+                msg = re.sub(r"\(delta\.logRetentionDuration=.*\)$", retention_text(self._snapshot.metadata),
+                             str(e))
+                raise DeltaError(4, msg) from None
+            raise
+
         try:
             ver, _ = self.engine.log_segment(self.log_path, version)
             state = staged.replay(cutoff)

@@ -290,16 +290,25 @@ def replay_sharded(staged: Staged, min_file_retention_timestamp: int, exchange, 
     return ShardedState(local, counts, nonfile, exchange)
 
 
-def write_checkpoint_sharded(sharded: "ShardedState", log_path: str, version: int, stats: bool = True,
-                             parsed: bool = True, row_group_rows: int = 0) -> int:
+def write_checkpoint_sharded(sharded: "ShardedState", log_path: str, version: int, stats: Optional[bool] = None,
+                             parsed: Optional[bool] = None, row_group_rows: int = 0,
+                             checkpoint_v2_enabled: bool = True) -> int:
     """The multi-part checkpoint from the GPU shards: rank r encodes part r + 1 of
     `world` on its device from its own survivors (dr_state_write_checkpoint; part 1 also holds the
     protocol / metaData / txn rows), writes it (temp + rename), and rank 0 writes `_last_checkpoint`
-    with the table-wide row count once every part is in place. Returns that count."""
-    from delta_amd.checkpoint import checkpoint_file_with_parts, write_last_checkpoint
+    with the table-wide row count once every part is in place and the parts' add rows equal the
+    table's numOfFiles (D/Checkpoints.scala:325-328). Unless given, the add schema follows the
+    table's delta.checkpoint.writeStatsAsJson / writeStatsAsStruct, as the single-GPU writer's.
+    Returns the row count."""
+    from delta_amd.checkpoint import (check_add_rows, checkpoint_file_with_parts, checkpoint_options,
+                                      write_last_checkpoint)
     ex = sharded.exchange
-    data, rows = sharded.local.write_checkpoint_part(ex.rank + 1, ex.world, stats=stats, parsed=parsed,
-                                                     row_group_rows=row_group_rows)
+    md = next((a["metaData"] for a in sharded.nonfile if "metaData" in a), None)
+    o_stats, o_parsed = checkpoint_options(md, checkpoint_v2_enabled)
+    stats = o_stats if stats is None else stats
+    parsed = (o_parsed is not None) if parsed is None else parsed
+    data, rows, adds = sharded.local.write_checkpoint_part(ex.rank + 1, ex.world, stats=stats, parsed=parsed,
+                                                           row_group_rows=row_group_rows, with_adds=True)
     path = (os.path.join(log_path, "%020d.checkpoint.parquet" % version) if ex.world == 1
             else checkpoint_file_with_parts(log_path, version, ex.rank + 1, ex.world))
     tmp = os.path.join(os.path.dirname(path), ".%s.%d.tmp" % (os.path.basename(path), ex.rank))
@@ -308,8 +317,9 @@ def write_checkpoint_sharded(sharded: "ShardedState", log_path: str, version: in
     os.replace(tmp, path)
     import torch
     dev = torch.device("cpu") if getattr(ex, "host", False) else torch.device("cuda", torch.cuda.current_device())
-    total = ex.all_reduce_sum([rows], dev)[0]
+    total, total_adds = ex.all_reduce_sum([rows, adds], dev)
     if ex.rank == 0:
+        check_add_rows(total_adds, sharded.counts["num_files"])
         meta = {"version": version, "size": total}
         if ex.world > 1:
             meta["parts"] = ex.world

@@ -282,8 +282,10 @@ void dr_free(void* p);
 #define DR_CKPT_STATS 0x1u
 #define DR_CKPT_PARSED 0x2u
 #define DR_CKPT_SNAPPY 0x4u   /* SNAPPY pages for the device-encoded columns (Spark's default codec) */
+/* *rows: the part's row count; *add_rows (may be NULL): its add rows, which the caller sums over the
+ * parts and compares with numOfFiles before writing _last_checkpoint (D/Checkpoints.scala:325-328). */
 int dr_state_write_checkpoint(dr_state* state, int32_t part, int32_t parts, uint32_t opts, uint64_t row_group_rows,
-                              uint8_t** bytes, uint64_t* len, int64_t* rows);
+                              uint8_t** bytes, uint64_t* len, int64_t* rows, int64_t* add_rows);
 /* A sharded state's table-wide protocol / metaData / txn winners from every rank's local winners
  * (dr_state_nonfile_json of each rank, concatenated in rank order, one action per line), reduced as
  * InMemoryLogReplay does (D/actions/InMemoryLogReplay.scala:47-53); dr_replay_sharded does this itself

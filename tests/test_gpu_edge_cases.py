@@ -686,3 +686,25 @@ def test_scan_scratch_capacity_is_checked(engine, tmp_path, monkeypatch):
         assert st.counts["num_files"] == exp.num_files
     finally:
         st.release()
+
+
+def test_truncated_log_on_update_renders_table_retention(tmp_path):
+    """On update() the reference renders the current snapshot's configured retention policies into
+    logFileNotFoundException (D/SnapshotManagement.scala:161-163, D/DeltaErrors.scala:451-461)."""
+    from delta_amd.delta_log import DeltaError, DeltaLog
+    table = str(tmp_path / "t")
+    lp = os.path.join(table, "_delta_log")
+    md = json.loads(json.dumps(METADATA))
+    md["metaData"]["configuration"] = {"delta.logRetentionDuration": "interval 1 week",
+                                       "delta.checkpointRetentionDuration": "interval 36 hours"}
+    write_commit(lp, 0, [PROTOCOL, md, add("a")])
+    write_commit(lp, 1, [add("b")])
+    log = DeltaLog(table)
+    assert log.snapshot.num_of_files == 2
+    os.remove(os.path.join(lp, "%020d.json" % 0))
+    write_commit(lp, 2, [add("c")])
+    with pytest.raises(DeltaError) as ei:
+        log.update()
+    assert ei.value.kind == "FileNotFoundException"
+    assert str(ei.value).endswith("(delta.logRetentionDuration=7 days) and checkpoint retention policy "
+                                  "(delta.checkpointRetentionDuration=36 hours)")

@@ -60,7 +60,20 @@ def _map(pa, e, pre, n):
 
 
 _PARSED_TYPES = {"string": "string", "byte": "int8", "short": "int16", "integer": "int32", "long": "int64",
-                 "date": "date32", "boolean": "bool_"}
+                 "date": "date32", "boolean": "bool_", "float": "float32", "double": "float64", "binary": "binary"}
+
+
+def _parsed_type(pa, t: str):
+    """Arrow type of a partition column in partitionValues_parsed (the Spark type's Parquet layout)."""
+    import re
+    if t in _PARSED_TYPES:
+        return getattr(pa, _PARSED_TYPES[t])()
+    if t == "timestamp":
+        return pa.timestamp("us", tz="UTC")  # written as INT96, Spark's outputTimestampType default
+    m = re.fullmatch(r"decimal(?:\((\d+),(\d+)\))?", t)
+    if m:
+        return pa.decimal128(int(m.group(1)), int(m.group(2))) if m.group(1) else pa.decimal128(10, 0)
+    raise KeyError(t)
 
 
 def _conf_bool(md, key: str, default):
@@ -88,7 +101,7 @@ def _types(pa, stats=True, parsed=None):
         add_f.append(("stats", pa.string()))
     if parsed:
         add_f.append(("partitionValues_parsed",
-                      pa.struct([(c, getattr(pa, _PARSED_TYPES[t])()) for c, t in parsed.items()])))
+                      pa.struct([(c, _parsed_type(pa, t)) for c, t in parsed.items()])))
     add_t = pa.struct(add_f)
     rm_t = pa.struct([("path", pa.string()), ("deletionTimestamp", pa.int64()), ("dataChange", pa.bool_()),
                       ("extendedFileMetadata", pa.bool_()), ("partitionValues", mt), ("size", pa.int64()),
@@ -218,7 +231,8 @@ def write_part(state, log_path: str, version: int, part: int, parts: int, row_gr
     table, _ = checkpoint_table(state)
     path = checkpoint_file_with_parts(log_path, version, part, parts)
     tmp = os.path.join(os.path.dirname(path), ".%s.tmp" % os.path.basename(path))
-    pq.write_table(table, tmp, compression="snappy", row_group_size=row_group_size, write_statistics=False)
+    pq.write_table(table, tmp, compression="snappy", row_group_size=row_group_size, write_statistics=False,
+                   use_deprecated_int96_timestamps=True)
     os.replace(tmp, path)
     return table.num_rows
 
@@ -269,7 +283,8 @@ def write_checkpoint(snapshot, parts: int = 1, row_group_size: int = 1 << 20) ->
         slices = [table.slice(i * step, max(0, min(step, rows - i * step))) for i in range(parts)]
     for path, t in zip(paths, slices):
         tmp = os.path.join(os.path.dirname(path), ".%s.tmp" % os.path.basename(path))
-        pq.write_table(t, tmp, compression="snappy", row_group_size=row_group_size, write_statistics=False)
+        pq.write_table(t, tmp, compression="snappy", row_group_size=row_group_size, write_statistics=False,
+                       use_deprecated_int96_timestamps=True)
         os.replace(tmp, path)  # a reader never sees a partial part
     meta = {"version": snapshot.version, "size": rows}
     if parts > 1:

@@ -14,6 +14,7 @@
 #include <thread>
 
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <functional>
 #include <type_traits>
@@ -502,6 +503,7 @@ struct dr_state {
     DBuf<uint32_t> slen;
     DBuf<uint8_t> isnull;
     DBuf<uint64_t> s8;
+    DBuf<int64_t> w64hi;  // DECIMAL: high 64 bits of the unscaled value
   };
   std::vector<std::unique_ptr<PvCol>> pv_cols;
   std::vector<std::shared_ptr<DBuf<uint8_t>>> pv_arenas;  // unescaped string values
@@ -2487,6 +2489,56 @@ static bool leafify(const dr_predicate& p, LeafPlan& L) {
 }
 
 // Builds the K5 cache columns `want` (name, type) of st's live AddFiles in one k_pv_extract pass.
+// Java's Double.parseDouble / Float.parseFloat for the values k_pv_extract left to the host (more
+// than 19 significant digits, exponents off Clinger's fast path, hexadecimal significands): the text
+// was already checked against the decimal grammar on the device; glibc's strtod / strtof round
+// correctly, as Java does. Java's hexadecimal form needs a binary exponent ('p'): without one the
+// cast is null.
+static void fix_fp_values(dr_ctx* ctx, dr_state::PvCol& col, const DBuf<uint64_t>& hard, uint64_t nh) {
+  hipStream_t stream = ctx->stream;
+  const std::vector<uint64_t> h = d2h(hard.p, 3 * nh, stream);
+  const bool is_float = (col.type & 0xff) == DR_T_FLOAT;
+  std::vector<uint64_t> rows(nh), bits(nh);
+  std::vector<uint8_t> nulls(nh, 0);
+  for (uint64_t k = 0; k < nh; ++k) {
+    rows[k] = h[3 * k];
+    std::string t(size_t(h[3 * k + 2]), '\0');
+    if (!t.empty()) HIP_OK(hipMemcpy(&t[0], reinterpret_cast<const void*>(h[3 * k + 1]), t.size(), hipMemcpyDeviceToHost));
+    size_t b = 0, e = t.size();
+    while (b < e && uint8_t(t[b]) <= ' ') ++b;
+    while (e > b && uint8_t(t[e - 1]) <= ' ') --e;
+    t = t.substr(b, e - b);
+    if (!t.empty() && strchr("fFdD", t.back())) t.pop_back();
+    const size_t x = t.find_first_of("xX");
+    if (x != std::string::npos && t.find_first_of("pP") == std::string::npos) {
+      nulls[k] = 1;
+      continue;
+    }
+    char* end = nullptr;
+    if (is_float) {
+      const float f = strtof(t.c_str(), &end);
+      uint32_t u;
+      memcpy(&u, &f, 4);
+      bits[k] = u;
+    } else {
+      const double d = strtod(t.c_str(), &end);
+      memcpy(&bits[k], &d, 8);
+    }
+    if (end != t.c_str() + t.size()) nulls[k] = 1;
+  }
+  for (uint64_t k = 0; k < nh; ++k) {
+    const uint64_t r = rows[k];
+    if (is_float) {
+      const uint32_t v = uint32_t(bits[k]);
+      HIP_OK(hipMemcpyAsync(col.w32.p + r, &v, 4, hipMemcpyHostToDevice, stream));
+    } else {
+      HIP_OK(hipMemcpyAsync(col.w64.p + r, &bits[k], 8, hipMemcpyHostToDevice, stream));
+    }
+    HIP_OK(hipMemcpyAsync(col.isnull.p + r, &nulls[k], 1, hipMemcpyHostToDevice, stream));
+  }
+  HIP_OK(hipStreamSynchronize(stream));
+}
+
 static void build_pv_columns(dr_state& st, const std::vector<std::pair<std::string, int32_t>>& want) {
   dr_ctx* ctx = st.ctx;
   hipStream_t stream = ctx->stream;
@@ -2576,41 +2628,68 @@ static void build_pv_columns(dr_state& st, const std::vector<std::pair<std::stri
     PvColumn& pc = a.cols[c];
     pc.type = col->type;
     pc.isnull = col->isnull.p;
-    if (col->type == DR_T_STRING) {
+    const int base = col->type & 0xff;
+    if (base == DR_T_STRING || base == DR_T_BINARY) {
       col->sptr = DBuf<uint64_t>(ctx, n);
       col->slen = DBuf<uint32_t>(ctx, n);
       col->s8 = DBuf<uint64_t>(ctx, n);
       pc.sptr = col->sptr.p;
       pc.slen = col->slen.p;
       pc.s8 = col->s8.p;
-    } else if (col->type == DR_T_LONG) {
+    } else if (base == DR_T_LONG || base == DR_T_DOUBLE || base == DR_T_TIMESTAMP || base == DR_T_DECIMAL) {
       col->w64 = DBuf<int64_t>(ctx, n);
       pc.w64 = col->w64.p;
+      if (base == DR_T_DECIMAL) {
+        col->w64hi = DBuf<int64_t>(ctx, n);
+        pc.w64hi = col->w64hi.p;
+        if (((col->type >> 8) & 0xff) <= 9) {
+          col->w32 = DBuf<uint32_t>(ctx, n);
+          pc.w32 = col->w32.p;
+        }
+      }
     } else {
       col->w32 = DBuf<uint32_t>(ctx, n);
       pc.w32 = col->w32.p;
     }
     made.push_back(std::move(col));
   }
-  DBuf<unsigned long long> ctr(ctx, 2);  // 0 arena fill, 1 arena need
+  // counters: 0 arena fill, 1 arena need, 2.. per column: float / double values left to the host
+  const size_t nc = want.size();
+  DBuf<unsigned long long> ctr(ctx, 2 + nc);
   DBuf<uint32_t> ferr(ctx, 1);
   ctr.zero(stream);
   ferr.zero(stream);
   a.arena_fill = ctr.p;
   a.arena_need = ctr.p + 1;
   a.error = ferr.p;
+  for (size_t c = 0; c < nc; ++c) a.cols[c].nhard = ctr.p + 2 + c;
   launch_pv_extract(a, stream);
-  const unsigned long long need = d2h_one(ctr.p + 1, stream);
-  if (need) {  // some partition values carry JSON escapes: unescape them into an arena and rerun
-    auto arena = std::make_shared<DBuf<uint8_t>>(ctx, need + 64);
-    a.arena = arena->p;
-    a.arena_cap = need + 64;
+  const std::vector<unsigned long long> cnt = d2h(ctr.p, 2 + nc, stream);
+  std::vector<DBuf<uint64_t>> hard(nc);
+  bool rerun = cnt[1] != 0;
+  for (size_t c = 0; c < nc; ++c)
+    if (cnt[2 + c]) {
+      hard[c] = DBuf<uint64_t>(ctx, 3 * cnt[2 + c]);
+      a.cols[c].hard = hard[c].p;
+      rerun = true;
+    }
+  if (rerun) {
+    // some partition values carry JSON escapes (unescaped into an arena) or are floating-point
+    // numbers off the device's exact path (listed for the host): rerun with those buffers
+    if (cnt[1]) {
+      auto arena = std::make_shared<DBuf<uint8_t>>(ctx, cnt[1] + 64);
+      a.arena = arena->p;
+      a.arena_cap = cnt[1] + 64;
+      st.pv_arenas.push_back(arena);
+    }
+    HIP_OK(hipMemsetAsync(ctr.p, 0, 8 * (2 + nc), stream));
     launch_pv_extract(a, stream);
-    st.pv_arenas.push_back(arena);
   }
   const uint32_t e = d2h_one(ferr.p, stream);
   if (e & 1u) fail(DR_E_PARSE, "malformed add.partitionValues in a live AddFile's JSON line");
   if (e & 2u) fail(DR_E_INTERNAL, "partition value arena overflow");
+  for (size_t c = 0; c < nc; ++c)
+    if (cnt[2 + c]) fix_fp_values(ctx, *made[c], hard[c], cnt[2 + c]);
   for (auto& c : made) st.pv_cols.push_back(std::move(c));
 }
 
@@ -2653,13 +2732,15 @@ struct ThriftW {  // Thrift compact protocol
   void elem_str(const std::string& s) { varint(s.size()); b.insert(b.end(), s.begin(), s.end()); }
 };
 
-enum PqType { PQ_BOOLEAN = 0, PQ_INT32 = 1, PQ_INT64 = 2, PQ_BYTE_ARRAY = 6 };
-enum PqConv { PC_UTF8 = 0, PC_MAP = 1, PC_LIST = 3, PC_DATE = 6, PC_INT_8 = 15, PC_INT_16 = 16 };
+enum PqType { PQ_BOOLEAN = 0, PQ_INT32 = 1, PQ_INT64 = 2, PQ_INT96 = 3, PQ_FLOAT = 4, PQ_DOUBLE = 5, PQ_BYTE_ARRAY = 6,
+              PQ_FLBA = 7 };
+enum PqConv { PC_UTF8 = 0, PC_MAP = 1, PC_LIST = 3, PC_DECIMAL = 5, PC_DATE = 6, PC_INT_8 = 15, PC_INT_16 = 16 };
 enum PqRep { PR_REQUIRED = 0, PR_OPTIONAL = 1, PR_REPEATED = 2 };
 
 struct SElem {
   std::string name;
   int type = -1, rep = -1, nkids = -1, conv = -1;
+  int type_length = -1, scale = -1, precision = -1;  // FIXED_LEN_BYTE_ARRAY / DECIMAL
 };
 
 // One leaf of the checkpoint schema and how its column is produced.
@@ -2803,6 +2884,8 @@ static void head_row_levels(const CkLeafW& L, int top_kind, const NonFileAction*
   }
 }
 
+// A partition column's Spark type name (the schemaString's) -> dr_pred_type (decimal(p,s): the
+// precision and scale ride in bits 8..23 of the code); -1 when the cast is not supported.
 static int32_t spark_type_code(const std::string& t) {
   if (t == "string") return DR_T_STRING;
   if (t == "byte") return DR_T_BYTE;
@@ -2811,7 +2894,24 @@ static int32_t spark_type_code(const std::string& t) {
   if (t == "long") return DR_T_LONG;
   if (t == "date") return DR_T_DATE;
   if (t == "boolean") return DR_T_BOOLEAN;
+  if (t == "float") return DR_T_FLOAT;
+  if (t == "double") return DR_T_DOUBLE;
+  if (t == "timestamp") return DR_T_TIMESTAMP;
+  if (t == "binary") return DR_T_BINARY;
+  int p = 0, sc = 0;
+  char close = 0;
+  if (t == "decimal") return DR_T_DECIMAL | (10 << 8);  // DecimalType.USER_DEFAULT: decimal(10,0)
+  if (std::sscanf(t.c_str(), "decimal(%d,%d%c", &p, &sc, &close) == 3 && close == ')' && p >= 1 && p <= 38 &&
+      sc >= 0 && sc <= p)
+    return DR_T_DECIMAL | (p << 8) | (sc << 16);
   return -1;
+}
+
+// Bytes of a FIXED_LEN_BYTE_ARRAY decimal of this precision (Spark's Decimal.minBytesForPrecision).
+static int decimal_bytes(int precision) {
+  int n = 1;
+  while (std::pow(2.0, 8.0 * n - 1) < std::pow(10.0, precision)) ++n;
+  return n;
 }
 
 // The part file, grown in a malloc'd buffer that dr_state_write_checkpoint hands to the caller as
@@ -3032,10 +3132,41 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
         f.def_null = 2;
         f.def_present = 3;
         if (col) f.null = col->isnull.p + a0;
-        int phys = PQ_INT32, conv = -1;
-        switch (pc.second) {
-          case DR_T_STRING: f.kind = ENC_STR_PTR; if (col) { f.sptr = col->sptr.p + a0; f.slen = col->slen.p + a0; } phys = PQ_BYTE_ARRAY; conv = PC_UTF8; break;
+        int phys = PQ_INT32, conv = -1, tlen = -1;
+        const int prec = (pc.second >> 8) & 0xff, scale = (pc.second >> 16) & 0xff;
+        switch (pc.second & 0xff) {
+          case DR_T_STRING:
+          case DR_T_BINARY:  // Cast(string AS binary): the UTF-8 bytes, no UTF8 annotation
+            f.kind = ENC_STR_PTR;
+            if (col) { f.sptr = col->sptr.p + a0; f.slen = col->slen.p + a0; }
+            phys = PQ_BYTE_ARRAY;
+            conv = (pc.second & 0xff) == DR_T_STRING ? PC_UTF8 : -1;
+            break;
           case DR_T_LONG: f.kind = ENC_I64; if (col) f.i64 = col->w64.p + a0; phys = PQ_INT64; break;
+          case DR_T_DOUBLE: f.kind = ENC_I64; if (col) f.i64 = col->w64.p + a0; phys = PQ_DOUBLE; break;
+          case DR_T_FLOAT: f.kind = ENC_I32; if (col) f.i32 = col->w32.p + a0; phys = PQ_FLOAT; break;
+          case DR_T_TIMESTAMP:  // spark.sql.parquet.outputTimestampType's default, INT96
+            f.kind = ENC_INT96;
+            if (col) f.i64 = col->w64.p + a0;
+            phys = PQ_INT96;
+            break;
+          case DR_T_DECIMAL:  // Spark's non-legacy decimal layout: INT32 / INT64 / FIXED_LEN_BYTE_ARRAY
+            conv = PC_DECIMAL;
+            if (prec <= 9) {
+              f.kind = ENC_I32;
+              if (col) f.i32 = col->w32.p + a0;
+            } else if (prec <= 18) {
+              f.kind = ENC_I64;
+              if (col) f.i64 = col->w64.p + a0;
+              phys = PQ_INT64;
+            } else {
+              f.kind = ENC_FLBA_BE;
+              if (col) { f.i64 = col->w64.p + a0; f.i64hi = col->w64hi.p + a0; }
+              f.width = uint32_t(decimal_bytes(prec));
+              tlen = int(f.width);
+              phys = PQ_FLBA;
+            }
+            break;
           case DR_T_BOOLEAN: f.kind = ENC_BOOL; if (col) f.i32 = col->w32.p + a0; phys = PQ_BOOLEAN; break;
           default:
             f.kind = ENC_I32;
@@ -3043,6 +3174,11 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
             conv = pc.second == DR_T_DATE ? PC_DATE : pc.second == DR_T_BYTE ? PC_INT_8 : pc.second == DR_T_SHORT ? PC_INT_16 : -1;
         }
         leaf(pc.first, PR_OPTIONAL, phys, conv, 3, 0, 0, f);
+        if ((pc.second & 0xff) == DR_T_DECIMAL) {
+          schema.back().scale = scale;
+          schema.back().precision = prec;
+          schema.back().type_length = tlen;
+        }
       }
       at.pop_back();
     }
@@ -3274,10 +3410,13 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
   for (const SElem& e : schema) {
     fm.elem_begin();
     if (e.type >= 0) fm.i32(1, e.type);
+    if (e.type_length >= 0) fm.i32(2, e.type_length);
     if (e.rep >= 0) fm.i32(3, e.rep);
     fm.str(4, e.name);
     if (e.nkids >= 0) fm.i32(5, e.nkids);
     if (e.conv >= 0) fm.i32(6, e.conv);
+    if (e.scale >= 0) fm.i32(7, e.scale);
+    if (e.precision >= 0) fm.i32(8, e.precision);
     fm.elem_end();
   }
   fm.i64(3, int64_t(p1 - p0));

@@ -41,6 +41,8 @@ __global__ void __launch_bounds__(ENC_T) k_enc_count(EncArgs a) {
         case ENC_STR_OFF: vb = 4 + str_len(L, i); break;
         case ENC_I64: vb = 8; break;
         case ENC_I32: vb = 4; break;
+        case ENC_INT96: vb = 12; break;
+        case ENC_FLBA_BE: vb = L.width; break;
         default: vb = 1; break;  // BOOLEAN: one byte until packed
       }
     }
@@ -114,6 +116,26 @@ __global__ void __launch_bounds__(ENC_T) k_enc_fill(EncArgs a) {
       break;
     }
     case ENC_I32: put_u32(v, L.i32[i]); break;
+    case ENC_INT96: {
+      // Spark's INT96 timestamp (ParquetWriteSupport, DateTimeUtils.toJulianDay): nanoseconds of the
+      // day (int64) then the Julian day number (int32), little-endian; days by floor division
+      const int64_t us = L.i64[i];
+      const int64_t day = us >= 0 ? us / 86400000000ll : -((-us + 86399999999ll) / 86400000000ll);
+      const uint64_t nanos = uint64_t(us - day * 86400000000ll) * 1000ull;
+      put_u32(v, uint32_t(nanos));
+      put_u32(v + 4, uint32_t(nanos >> 32));
+      put_u32(v + 8, uint32_t(int32_t(day + 2440588)));
+      break;
+    }
+    case ENC_FLBA_BE: {
+      // unscaled decimal, two's complement, big-endian in `width` bytes (Spark's binary decimals)
+      const uint64_t lo = uint64_t(L.i64[i]), hi = uint64_t(L.i64hi ? L.i64hi[i] : (L.i64[i] < 0 ? -1 : 0));
+      for (uint32_t k = 0; k < L.width; ++k) {
+        const uint32_t bit = 8 * (L.width - 1 - k);
+        v[k] = uint8_t(bit < 64 ? lo >> bit : bit < 128 ? hi >> (bit - 64) : (hi >> 63 ? 0xff : 0));
+      }
+      break;
+    }
     default: v[0] = L.b8 ? (L.b8[i] ? 1 : 0) : L.i32 ? (L.i32[i] ? 1 : 0) : 0; break;
   }
 }

@@ -218,6 +218,314 @@ __device__ bool parse_date(const uint8_t* s, uint32_t n, int64_t* out) {
   return true;
 }
 
+// ---- casts of partitionValues_parsed's other types (D/Checkpoints.scala:380-388: Cast(pv AS type)) --
+// float / double, decimal(p, s), timestamp and binary partition columns. The K5 predicate program
+// does not take them (check_program); the checkpoint writer does.
+__device__ __forceinline__ bool jws(uint8_t c) { return c <= ' '; }  // String.trim / UTF8String.trimAll
+
+// Double.parseDouble / Float.parseFloat of the trimmed text (Java's FloatingDecimal grammar: sign,
+// NaN, Infinity, digits with one '.', exponent, an f/F/d/D suffix), else Spark's special literals
+// (Cast.processFloatingPointSpecialLiterals: inf, +inf, infinity, +infinity, -inf, -infinity, nan,
+// any case). Exact here on Clinger's fast path (<= 19 significant digits; double: mantissa <= 2^53,
+// |10-exponent| <= 22; float: <= 2^24, <= 10); other well-formed numbers (and hex) come back
+// FP_HARD and the host converts them with its correctly rounded strtod / strtof.
+enum FpRes : int { FP_NULL = 0, FP_OK = 1, FP_HARD = 2 };
+__device__ int parse_fp(const uint8_t* s, uint32_t n, bool is_float, uint64_t* bits) {
+  uint32_t i = 0;
+  while (i < n && jws(s[i])) ++i;
+  while (n > i && jws(s[n - 1])) --n;
+  const uint32_t b0 = i;
+  bool neg = false;
+  auto special = [&]() -> int {
+    char t[10];
+    const uint32_t m = n - b0;
+    if (m == 0 || m > 9) return FP_NULL;
+    for (uint32_t k = 0; k < m; ++k) t[k] = char(lower(s[b0 + k]));
+    auto is = [&](const char* w) {
+      uint32_t k = 0;
+      for (; w[k]; ++k)
+        if (k >= m || t[k] != w[k]) return false;
+      return k == m;
+    };
+    int sign = 0;
+    if (is("inf") || is("+inf") || is("infinity") || is("+infinity")) sign = 1;
+    else if (is("-inf") || is("-infinity")) sign = -1;
+    else if (is("nan")) {
+      *bits = is_float ? 0x7fc00000ull : 0x7ff8000000000000ull;
+      return FP_OK;
+    } else return FP_NULL;
+    *bits = is_float ? (sign > 0 ? 0x7f800000ull : 0xff800000ull) : (sign > 0 ? 0x7ff0000000000000ull : 0xfff0000000000000ull);
+    return FP_OK;
+  };
+  if (i >= n) return FP_NULL;
+  if (s[i] == '+' || s[i] == '-') { neg = s[i] == '-'; ++i; }
+  auto word = [&](const char* w, uint32_t wl) {
+    if (n - i != wl) return false;
+    for (uint32_t k = 0; k < wl; ++k)
+      if (s[i + k] != uint8_t(w[k])) return false;
+    return true;
+  };
+  if (word("NaN", 3)) { *bits = is_float ? 0x7fc00000ull : 0x7ff8000000000000ull; return FP_OK; }
+  if (word("Infinity", 8)) {
+    *bits = is_float ? (neg ? 0xff800000ull : 0x7f800000ull) : (neg ? 0xfff0000000000000ull : 0x7ff0000000000000ull);
+    return FP_OK;
+  }
+  if (i + 1 < n && s[i] == '0' && (s[i + 1] | 0x20) == 'x') return FP_HARD;  // hexadecimal significand
+  uint64_t w = 0;
+  int32_t sig = 0, dexp = 0;
+  bool any = false, dot = false, trunc = false;
+  for (; i < n; ++i) {
+    const uint8_t c = s[i];
+    if (c == '.') {
+      if (dot) return special();
+      dot = true;
+      continue;
+    }
+    if (c < '0' || c > '9') break;
+    any = true;
+    if (w == 0 && c == '0') {  // leading zero
+      if (dot) --dexp;
+      continue;
+    }
+    if (sig < 19) {
+      w = w * 10 + (c - '0');
+      ++sig;
+      if (dot) --dexp;
+    } else {
+      trunc = trunc || c != '0';
+      if (!dot) ++dexp;
+    }
+  }
+  if (!any) return special();
+  if (i < n && (s[i] == 'e' || s[i] == 'E')) {
+    ++i;
+    bool eneg = false;
+    if (i < n && (s[i] == '+' || s[i] == '-')) { eneg = s[i] == '-'; ++i; }
+    if (i >= n || s[i] < '0' || s[i] > '9') return special();
+    int64_t e = 0;
+    for (; i < n && s[i] >= '0' && s[i] <= '9'; ++i) e = e < 100000 ? e * 10 + (s[i] - '0') : e;
+    dexp += int32_t(eneg ? -e : e);
+  }
+  if (i < n && (s[i] == 'f' || s[i] == 'F' || s[i] == 'd' || s[i] == 'D')) ++i;
+  if (i != n) return special();
+  if (w == 0) {  // a signed zero
+    *bits = is_float ? (neg ? 0x80000000ull : 0ull) : (neg ? 0x8000000000000000ull : 0ull);
+    return FP_OK;
+  }
+  if (trunc) return FP_HARD;
+  const double p10[23] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9, 1e10, 1e11,
+                          1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+  if (is_float) {
+    if (w > (1ull << 24) || dexp < -10 || dexp > 10) return FP_HARD;
+    const float m = float(w), q = float(p10[dexp < 0 ? -dexp : dexp]);
+    float f = dexp < 0 ? __fdiv_rn(m, q) : __fmul_rn(m, q);
+    if (neg) f = -f;
+    *bits = __float_as_uint(f);
+    return FP_OK;
+  }
+  if (w > (1ull << 53) || dexp < -22 || dexp > 22) return FP_HARD;
+  const double m = double(w), q = p10[dexp < 0 ? -dexp : dexp];
+  double d = dexp < 0 ? __ddiv_rn(m, q) : __dmul_rn(m, q);
+  if (neg) d = -d;
+  *bits = uint64_t(__double_as_longlong(d));
+  return FP_OK;
+}
+
+// Decimal.fromString + changePrecision(p, s) (non-ANSI): java.math.BigDecimal of the trimmed text
+// ([sign] digits [. digits] [e|E [sign] digits]), rounded HALF_UP to `scale`; null when the unscaled
+// value needs more than `prec` digits. Two's complement unscaled value in lo / hi (128 bits).
+__device__ bool parse_decimal(const uint8_t* s, uint32_t n, int prec, int scale, uint64_t* lo, int64_t* hi) {
+  uint32_t i = 0;
+  while (i < n && jws(s[i])) ++i;
+  while (n > i && jws(s[n - 1])) --n;
+  if (i >= n) return false;
+  bool neg = false;
+  if (s[i] == '+' || s[i] == '-') { neg = s[i] == '-'; ++i; }
+  const uint32_t d0 = i;
+  uint32_t ndig = 0, frac = 0;
+  bool dot = false;
+  for (; i < n; ++i) {
+    if (s[i] == '.') {
+      if (dot) return false;
+      dot = true;
+      continue;
+    }
+    if (s[i] < '0' || s[i] > '9') break;
+    ++ndig;
+    if (dot) ++frac;
+  }
+  if (!ndig) return false;
+  const uint32_t d1 = i;  // digits (and the '.') in [d0, d1)
+  int64_t e = 0;
+  if (i < n && (s[i] == 'e' || s[i] == 'E')) {
+    ++i;
+    bool eneg = false;
+    if (i < n && (s[i] == '+' || s[i] == '-')) { eneg = s[i] == '-'; ++i; }
+    if (i >= n || s[i] < '0' || s[i] > '9') return false;
+    for (; i < n && s[i] >= '0' && s[i] <= '9'; ++i) {
+      e = e * 10 + (s[i] - '0');
+      if (e > 4000000000ll) return false;  // beyond BigDecimal's int scale
+    }
+    if (eneg) e = -e;
+  }
+  if (i != n) return false;
+  // value = digits * 10^(e - frac); unscaled = digits * 10^(e - frac + scale)
+  const int64_t shift = e - int64_t(frac) + scale;
+  const int64_t keep = int64_t(ndig) + (shift < 0 ? shift : 0);  // digits kept before rounding
+  unsigned __int128 v = 0;
+  int64_t k = 0;
+  uint32_t round_digit = 0;
+  bool big = false;
+  for (uint32_t j = d0; j < d1; ++j) {
+    if (s[j] == '.') continue;
+    const uint32_t dg = s[j] - '0';
+    if (k < keep) {
+      if (v != 0 || dg != 0) {
+        if (v > (~(unsigned __int128)0) / 10 - 10) big = true;
+        else v = v * 10 + dg;
+      }
+    } else if (k == keep) {
+      round_digit = dg;
+    }
+    ++k;
+  }
+  if (big) return false;
+  if (shift > 0) {
+    for (int64_t t = 0; t < shift; ++t) {
+      if (v > (~(unsigned __int128)0) / 10) return false;
+      v *= 10;
+      if (v == 0) break;
+    }
+  }
+  if (round_digit >= 5) v += 1;  // ROUND_HALF_UP on the magnitude
+  unsigned __int128 lim = 1;
+  for (int t = 0; t < prec; ++t) lim *= 10;
+  if (v >= lim) return false;
+  const unsigned __int128 r = neg ? (unsigned __int128)0 - v : v;
+  *lo = uint64_t(r);
+  *hi = int64_t(uint64_t(r >> 64));
+  return true;
+}
+
+// DateTimeUtils.stringToTimestamp (Spark 3.1) with the session time zone UTC: [+-]yyyy[y..][-[m]m
+// [-[d]d[( |T)[h]h:[m]m[:[s]s[.fraction]][zone]]]], fraction truncated to microseconds, zone Z / UTC /
+// UT / GMT with an optional [+-]h[h][[:]mm[[:]ss]] offset, or a bare offset. Time-only strings (today's
+// date) and region zone ids (daylight saving rules) read as null here: parity unpinned.
+__device__ bool tz_offset(const uint8_t* z, uint32_t n, int64_t* secs) {
+  uint32_t i = 0;
+  while (i < n && jws(z[i])) ++i;
+  while (n > i && jws(z[n - 1])) --n;
+  auto pre = [&](const char* w, uint32_t wl) {
+    if (n - i < wl) return false;
+    for (uint32_t k = 0; k < wl; ++k)
+      if (z[i + k] != uint8_t(w[k])) return false;
+    return true;
+  };
+  if (n - i == 1 && z[i] == 'Z') { *secs = 0; return true; }
+  if (pre("UTC", 3)) i += 3;
+  else if (pre("GMT", 3)) i += 3;
+  else if (pre("UT", 2)) i += 2;
+  else if (i >= n || (z[i] != '+' && z[i] != '-')) return false;
+  if (i == n) { *secs = 0; return true; }
+  if (z[i] != '+' && z[i] != '-') return false;
+  const bool neg = z[i] == '-';
+  ++i;
+  int f[3] = {0, 0, 0}, nf = 0;
+  while (i < n && nf < 3) {
+    int dg = 0, v = 0;
+    while (i < n && z[i] >= '0' && z[i] <= '9' && dg < 2) { v = v * 10 + (z[i] - '0'); ++i; ++dg; }
+    if (dg == 0) return false;
+    f[nf++] = v;
+    if (i < n && z[i] == ':') ++i;
+  }
+  if (i != n || f[0] > 18 || f[1] > 59 || f[2] > 59) return false;
+  const int64_t t = int64_t(f[0]) * 3600 + f[1] * 60 + f[2];
+  *secs = neg ? -t : t;
+  return true;
+}
+
+__device__ bool parse_timestamp(const uint8_t* s, uint32_t n, int64_t* micros) {
+  uint32_t j = 0;
+  while (j < n && jws(s[j])) ++j;
+  while (n > j && jws(s[n - 1])) --n;
+  if (j >= n) return false;
+  int64_t seg[9] = {1, 1, 1, 0, 0, 0, 0, 0, 0};
+  int i = 0, digits = 0, milli_digits = 0, sign = 1;
+  int64_t cur = 0;
+  bool just_time = false;
+  int32_t tz0 = -1;
+  auto valid = [&](int sg, int d) {
+    return sg == 6 || (sg == 0 && d >= 4 && d <= 6) || (sg == 7 && d <= 2) ||
+           (sg != 0 && sg != 6 && sg != 7 && d > 0 && d <= 2);
+  };
+  const uint32_t start = j;
+  if (s[j] == '-' || s[j] == '+') { sign = s[j] == '-' ? -1 : 1; ++j; }
+  const bool signed_year = j > start;
+  for (; j < n; ++j) {
+    const uint8_t b = s[j];
+    if (b < '0' || b > '9') {
+      if (j == start && b == 'T') {
+        just_time = true;
+        i += 3;
+      } else if (i < 2) {
+        if (b == '-') {
+          if (!valid(i, digits)) return false;
+          seg[i++] = cur; cur = 0; digits = 0;
+        } else if (i == 0 && b == ':' && !signed_year) {
+          just_time = true;
+          if (!valid(3, digits)) return false;
+          seg[3] = cur; cur = 0; digits = 0;
+          i = 4;
+        } else return false;
+      } else if (i == 2) {
+        if (b != ' ' && b != 'T') return false;
+        if (!valid(i, digits)) return false;
+        seg[i++] = cur; cur = 0; digits = 0;
+      } else if (i == 3 || i == 4) {
+        if (b != ':') return false;
+        if (!valid(i, digits)) return false;
+        seg[i++] = cur; cur = 0; digits = 0;
+      } else if (i == 5 || i == 6) {
+        if (!valid(i, digits)) return false;
+        seg[i] = cur; cur = 0; digits = 0;
+        if (b == '.' && i == 5) {
+          ++i;
+        } else {
+          ++i;
+          tz0 = int32_t(j);
+          j = n - 1;
+        }
+        if (i == 6 && b != '.') ++i;
+      } else {
+        if (i < 9 && (b == ':' || b == ' ')) {
+          if (!valid(i, digits)) return false;
+          seg[i++] = cur; cur = 0; digits = 0;
+        } else return false;
+      }
+    } else {
+      if (i == 6) ++milli_digits;
+      if (i != 6 || digits < 6) cur = cur * 10 + (b - '0');
+      if (cur > 100000000000ll) return false;
+      ++digits;
+    }
+  }
+  if (!valid(i, digits)) return false;
+  if (i > 8) return false;
+  seg[i] = cur;
+  while (milli_digits < 6) { seg[6] *= 10; ++milli_digits; }
+  if (just_time) return false;  // LocalDate.now(zone): not a function of the value
+  int64_t off = 0;
+  if (tz0 >= 0 && !tz_offset(s + tz0, n - uint32_t(tz0), &off)) return false;
+  const int64_t y = seg[0] * sign, mo = seg[1], d = seg[2];
+  if (mo < 1 || mo > 12 || d < 1 || seg[3] > 23 || seg[4] > 59 || seg[5] > 59) return false;
+  const bool leap = (y % 4 == 0 && y % 100 != 0) || y % 400 == 0;
+  const int mdays[12] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+  if (d > mdays[mo - 1] + (mo == 2 && leap ? 1 : 0)) return false;
+  const int64_t days = days_from_civil(y, mo, d);
+  *micros = (days * 86400 + seg[3] * 3600 + seg[4] * 60 + seg[5] - off) * 1000000ll + seg[6];
+  return true;
+}
+
 __device__ SV cast_value(const uint8_t* s, uint32_t n, bool present, int type) {
   SV r{0, nullptr, 0, 1, 0};
   if (!present) return r;
@@ -326,9 +634,44 @@ __global__ void __launch_bounds__(256) k_pv_extract(PvExtractArgs a) {
   }
   for (int c = 0; c < a.ncols; ++c) {
     const PvColumn& col = a.cols[c];
-    const SV v = cast_value(vp[c], vn[c], vs[c] != PV_NULL, col.type);
+    const int base = col.type & 0xff;
+    const bool present = vs[c] != PV_NULL;
+    if (base == DR_T_FLOAT || base == DR_T_DOUBLE) {
+      uint64_t bits = 0;
+      const int r = present ? parse_fp(vp[c], vn[c], base == DR_T_FLOAT, &bits) : FP_NULL;
+      col.isnull[i] = r != FP_OK;
+      if (base == DR_T_FLOAT) col.w32[i] = uint32_t(bits);
+      else col.w64[i] = int64_t(bits);
+      if (r == FP_HARD) {  // the host converts it (rare: > 19 digits, large exponents, hex)
+        const unsigned long long k = atomicAdd(col.nhard, 1ull);
+        if (col.hard) {  // null on the counting pass: the host sizes the list and reruns
+          col.hard[3 * k] = i;
+          col.hard[3 * k + 1] = reinterpret_cast<uint64_t>(vp[c]);
+          col.hard[3 * k + 2] = vn[c];
+        }
+      }
+      continue;
+    }
+    if (base == DR_T_DECIMAL) {
+      uint64_t lo = 0;
+      int64_t hi = 0;
+      const bool ok = present && parse_decimal(vp[c], vn[c], (col.type >> 8) & 0xff, (col.type >> 16) & 0xff, &lo, &hi);
+      col.isnull[i] = !ok;
+      col.w64[i] = int64_t(lo);
+      col.w64hi[i] = hi;
+      if (col.w32) col.w32[i] = uint32_t(lo);  // precision <= 9: Parquet INT32
+      continue;
+    }
+    if (base == DR_T_TIMESTAMP) {
+      int64_t us = 0;
+      const bool ok = present && parse_timestamp(vp[c], vn[c], &us);
+      col.isnull[i] = !ok;
+      col.w64[i] = us;
+      continue;
+    }
+    const SV v = cast_value(vp[c], vn[c], present, base == DR_T_BINARY ? DR_T_STRING : col.type);
     col.isnull[i] = v.null;
-    if (col.type == DR_T_STRING) {
+    if (col.type == DR_T_STRING || base == DR_T_BINARY) {
       col.sptr[i] = reinterpret_cast<uint64_t>(v.s);
       col.slen[i] = v.n;
       uint64_t s8 = 0;

@@ -337,13 +337,16 @@ void launch_verdict_collect(const uint8_t* verdict, const uint32_t* send_idx, ui
 // predicate program over those typed columns, so a filter reads 4-12 B per file and column.
 constexpr int PV_MAXC = 16;
 struct PvColumn {
-  int32_t type;        // dr_pred_type
-  uint32_t* w32;       // BYTE / SHORT / INT / DATE (days) / BOOLEAN (0/1)
-  int64_t* w64;        // LONG
+  int32_t type;        // dr_pred_type (DECIMAL: | precision << 8 | scale << 16)
+  uint32_t* w32;       // BYTE / SHORT / INT / DATE (days) / BOOLEAN (0/1) / FLOAT (bits)
+  int64_t* w64;        // LONG / DOUBLE (bits) / TIMESTAMP (micros, UTC) / DECIMAL (unscaled, low 64 bits)
   uint64_t* sptr;      // STRING: address of the (unescaped) value bytes
   uint32_t* slen;
   uint8_t* isnull;     // 1: NULL (absent, JSON null, or a failed non-ANSI cast)
   uint64_t* s8;        // STRING: the first 8 bytes, big-endian, zero-padded (compared without a gather)
+  int64_t* w64hi;      // DECIMAL: unscaled high 64 bits (two's complement 128-bit value)
+  uint64_t* hard;      // FLOAT / DOUBLE: {row, value address, length} of values the host converts
+  unsigned long long* nhard;
 };
 struct PvExtractArgs {
   const uint32_t* live;          // live AddFile action indices (export order)
@@ -609,7 +612,9 @@ void launch_record_hash(const RecordHashArgs& a, hipStream_t st);
 // ---- checkpoint page encoding (k_encode.hip) -----------------------------------------------------
 namespace dr {
 enum EncKind : int32_t { ENC_STR_PTR = 0, ENC_STR_OFF = 1, ENC_I64 = 2, ENC_I32 = 3, ENC_BOOL = 4, ENC_MAP_KEY = 5,
-                         ENC_MAP_VAL = 6 };
+                         ENC_MAP_VAL = 6,
+                         ENC_INT96 = 7,     // TIMESTAMP as Spark's INT96 (nanos of day, Julian day) from i64 micros
+                         ENC_FLBA_BE = 8 }; // DECIMAL as FIXED_LEN_BYTE_ARRAY(width), big-endian, from i64 + i64hi
 // One leaf column of one side (adds or removes) of a checkpoint: where its records' values are and
 // the definition levels it takes. Rows of the row group outside the side's records are a null struct
 // (one level, def 0).
@@ -630,6 +635,8 @@ struct EncLeaf {
   const uint8_t* enull;           // map values: per entry
   const uint8_t* vflags;          // non-null: the record is null unless vflags[i] & vbit
   uint32_t vbit;
+  const int64_t* i64hi;           // ENC_FLBA_BE: high 64 bits
+  uint32_t width;                 // ENC_FLBA_BE: bytes per value
 };
 struct EncArgs {
   EncLeaf L;

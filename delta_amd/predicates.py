@@ -137,7 +137,128 @@ def cast_partition_value(s: Optional[str], typ: str):
     if typ == "date":
         d = _date_days(t)
         return None if d is None else _EPOCH + _dt.timedelta(days=d)
+    if typ in ("float", "double"):
+        return java_parse_fp(s, typ == "float")
+    if typ == "binary":
+        return s.encode("utf-8")
+    if typ == "timestamp":
+        us = timestamp_micros(s)
+        return None if us is None else _dt.datetime(1970, 1, 1, tzinfo=_dt.timezone.utc) + _dt.timedelta(microseconds=us)
+    dm = re.fullmatch(r"decimal(?:\((\d+),(\d+)\))?", typ)
+    if dm:
+        p, sc = (int(dm.group(1)), int(dm.group(2))) if dm.group(1) else (10, 0)
+        return decimal_value(s, p, sc)
     raise PredicateError("unsupported partition type %r" % typ)
+
+
+# ---- the checkpoint's other partitionValues_parsed casts (the device grammar, k_filter.hip) ------
+_FP_RE = re.compile(r"[+-]?(?:NaN|Infinity|(?:\d+\.?\d*|\.\d+)(?:[eE][+-]?\d+)?[fFdD]?)")
+
+
+def _jtrim(s: str) -> str:
+    b, e = 0, len(s)
+    while b < e and ord(s[b]) <= 32:
+        b += 1
+    while e > b and ord(s[e - 1]) <= 32:
+        e -= 1
+    return s[b:e]
+
+
+def _round_f32(x):
+    """Nearest binary32 to the exact rational x (round half to even), as Float.parseFloat."""
+    import struct
+    from fractions import Fraction
+    if x == 0:
+        return 0.0
+    f = struct.unpack("<f", struct.pack("<f", float(x)))[0] if abs(float(x)) < 3.5e38 else float("inf")
+    if f in (float("inf"), float("-inf")):
+        return f
+    bits = struct.unpack("<I", struct.pack("<f", f))[0]
+    best = None
+    for b in (bits - 1, bits, bits + 1):
+        if b < 0 or b >= 1 << 32:
+            continue
+        c = struct.unpack("<f", struct.pack("<I", b))[0]
+        if c != c or c in (float("inf"), float("-inf")):
+            continue
+        d = abs(Fraction(c) - x)
+        if best is None or d < best[0] or (d == best[0] and b % 2 == 0):
+            best = (d, c)
+    return best[1]
+
+
+def java_parse_fp(s: str, is_float: bool):
+    """Double.parseDouble / Float.parseFloat, else Spark's special literals (inf, nan, ...)."""
+    from fractions import Fraction
+    t = _jtrim(s)
+    if _FP_RE.fullmatch(t):
+        body = t.rstrip("fFdD") if not t.endswith(("NaN", "Infinity")) else t
+        if body.lstrip("+-") == "NaN":
+            return float("nan")
+        if body.lstrip("+-") == "Infinity":
+            return float("-inf") if body.startswith("-") else float("inf")
+        if is_float:
+            v = _round_f32(Fraction(body))
+            return -0.0 if v == 0 and body.startswith("-") else v
+        return float(body)
+    tl = t.lower()
+    if tl in ("inf", "+inf", "infinity", "+infinity"):
+        return float("inf")
+    if tl in ("-inf", "-infinity"):
+        return float("-inf")
+    if tl == "nan":
+        return float("nan")
+    return None
+
+
+def decimal_value(s: str, precision: int, scale: int):
+    """Decimal.fromString + changePrecision: BigDecimal of the trimmed text, HALF_UP to `scale`,
+    null beyond `precision` digits."""
+    import decimal
+    t = _jtrim(s)
+    if not re.fullmatch(r"[+-]?(?:\d+\.?\d*|\.\d+)(?:[eE][+-]?\d+)?", t):
+        return None
+    ctx = decimal.Context(prec=100000, rounding=decimal.ROUND_HALF_UP)
+    try:
+        v = decimal.Decimal(t).quantize(decimal.Decimal(1).scaleb(-scale), context=ctx)
+    except decimal.InvalidOperation:
+        return None
+    unscaled = abs(int(v.scaleb(scale, context=ctx)))
+    return None if unscaled >= 10 ** precision else (v if v != 0 else abs(v))
+
+
+_TS_RE = re.compile(r"([+-]?)(\d{4,6})(?:-(\d{1,2})(?:-(\d{1,2})(?:[ T](\d{1,2}):(\d{1,2})"
+                    r"(?::(\d{1,2})(?:\.(\d*))?)?(.*))?)?)?")
+_TZ_RE = re.compile(r"(?:Z|(?:UTC|GMT|UT)?(?:([+-])(\d{1,2})(?::?(\d{1,2})(?::?(\d{1,2}))?)?)?)")
+
+
+def timestamp_micros(s: str) -> Optional[int]:
+    """DateTimeUtils.stringToTimestamp with the session zone UTC, the subset the device reads."""
+    t = _jtrim(s)
+    m = _TS_RE.fullmatch(t)
+    if not m:
+        return None
+    sign, y, mo, d, hh, mi, ss, frac, zone = m.groups()
+    y = int(y) * (-1 if sign == "-" else 1)
+    try:
+        day = (_dt.date(y, int(mo or 1), int(d or 1)) - _EPOCH).days
+    except ValueError:
+        return None
+    hh, mi, ss = int(hh or 0), int(mi or 0), int(ss or 0)
+    if hh > 23 or mi > 59 or ss > 59:
+        return None
+    us = int(((frac or "") + "000000")[:6])
+    off = 0
+    if zone:
+        z = _TZ_RE.fullmatch(_jtrim(zone))
+        if not z or not zone.strip():
+            return None
+        if z.group(1):
+            h, mn, sc = int(z.group(2)), int(z.group(3) or 0), int(z.group(4) or 0)
+            if h > 18 or mn > 59 or sc > 59:
+                return None
+            off = (h * 3600 + mn * 60 + sc) * (-1 if z.group(1) == "-" else 1)
+    return ((day * 86400 + hh * 3600 + mi * 60 + ss) - off) * 1_000_000 + us
 
 
 def _lit(typ: str, v):

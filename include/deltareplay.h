@@ -245,7 +245,11 @@ int dr_parsed_release(dr_parsed* parsed);
  * The program must leave one boolean on the stack; rows where it is TRUE are selected.
  * Output: selected live-file ordinals (indices into the DR_LIVE export order). */
 enum dr_pred_type { DR_T_STRING = 0, DR_T_BYTE = 1, DR_T_SHORT = 2, DR_T_INT = 3, DR_T_LONG = 4,
-                    DR_T_DATE = 5, DR_T_BOOLEAN = 6 };
+                    DR_T_DATE = 5, DR_T_BOOLEAN = 6,
+                    /* partitionValues_parsed of the checkpoint writer only (not in predicate programs):
+                       Cast(string AS float / double / timestamp (session zone UTC) / binary /
+                       decimal(p, s)); a decimal's code carries p << 8 | s << 16 */
+                    DR_T_FLOAT = 7, DR_T_DOUBLE = 8, DR_T_TIMESTAMP = 9, DR_T_BINARY = 10, DR_T_DECIMAL = 11 };
 enum dr_pred_opcode {
   DR_OP_COL = 0,      /* arg = column index: push Cast(partitionValues[col] AS type) */
   DR_OP_LIT = 1,      /* arg = literal index */

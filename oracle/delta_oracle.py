@@ -573,6 +573,89 @@ def cast_string(s: Optional[str], typ: str):
             return (_dt.date(y, mo, d) - _EPOCH).days
         except ValueError:
             return None
+    return cast_string_v2(s, typ)
+
+
+# ---- the partitionValues_parsed casts of the other partition types (CheckpointV2.extractPartitionValues,
+# D/Checkpoints.scala:380-388: Cast(partitionValues[c] AS type)), restated from Spark 3.1's Cast:
+# float / double = Float.parseFloat / Double.parseDouble of the text (Java's FloatingDecimal grammar)
+# else Cast.processFloatingPointSpecialLiterals; decimal(p,s) = Decimal.fromString (new
+# java.math.BigDecimal(text.trim)) + changePrecision(p, s, ROUND_HALF_UP), null on overflow;
+# timestamp = DateTimeUtils.stringToTimestamp in the session zone (UTC here; region zone ids and
+# time-only strings are parity unpinned); binary = the UTF-8 bytes. Values: float/double as Python
+# floats, decimal as the unscaled int, timestamp as microseconds since the epoch, binary as bytes.
+def _java_trim(s: str) -> str:
+    return s.strip("".join(chr(c) for c in range(33)))
+
+
+def cast_string_v2(s: str, typ: str):
+    import decimal
+    from fractions import Fraction
+    t = _java_trim(s)
+    if typ in ("float", "double"):
+        m = re.fullmatch(r"([+-]?)(?:(NaN)|(Infinity)|((?:\d+\.?\d*|\.\d+)(?:[eE][+-]?\d+)?)[fFdD]?)", t)
+        if m:
+            if m.group(2):
+                return float("nan")
+            if m.group(3):
+                return float("-inf") if m.group(1) == "-" else float("inf")
+            x = Fraction(m.group(4))
+            if typ == "double":
+                v = float(x) if x < Fraction(2) ** 1025 else float("inf")
+            else:
+                import numpy as np
+                # the float32 nearest to the exact value (ties to even), by bracketing with float32
+                # neighbours of the double approximation
+                c = np.float32(float(x)) if x < Fraction(2) ** 129 else np.float32("inf")
+                if np.isfinite(c):
+                    cand = [np.nextafter(c, np.float32(-np.inf)), c, np.nextafter(c, np.float32(np.inf))]
+                    cand = [k for k in cand if np.isfinite(k)]
+                    c = min(cand, key=lambda k: (abs(Fraction(float(k)) - x), int(np.float32(k).view(np.uint32)) & 1))
+                v = float(c)
+            return -v if m.group(1) == "-" else v
+        tl = t.lower()
+        if tl in ("inf", "+inf", "infinity", "+infinity"):
+            return float("inf")
+        if tl in ("-inf", "-infinity"):
+            return float("-inf")
+        return float("nan") if tl == "nan" else None
+    if typ == "binary":
+        return s.encode("utf-8")
+    if typ == "timestamp":
+        m = re.fullmatch(r"([+-]?)(\d{4,6})(?:-(\d{1,2})(?:-(\d{1,2})(?:[ T](\d{1,2}):(\d{1,2})"
+                         r"(?::(\d{1,2})(?:\.(\d*))?)?(.*))?)?)?", t)
+        if not m:
+            return None
+        sign, y, mo, d, hh, mi, ss, frac, zone = m.groups()
+        try:
+            day = (_dt.date(int(y) * (-1 if sign == "-" else 1), int(mo or 1), int(d or 1)) - _EPOCH).days
+        except ValueError:
+            return None
+        hh, mi, ss = int(hh or 0), int(mi or 0), int(ss or 0)
+        if hh > 23 or mi > 59 or ss > 59:
+            return None
+        off = 0
+        if zone:
+            z = re.fullmatch(r"Z|(?:UTC|GMT|UT)?(?:([+-])(\d{1,2})(?::?(\d{1,2})(?::?(\d{1,2}))?)?)?", _java_trim(zone))
+            if not z or not zone.strip():
+                return None
+            if z.group(1):
+                h, mn, sc = int(z.group(2)), int(z.group(3) or 0), int(z.group(4) or 0)
+                if h > 18 or mn > 59 or sc > 59:
+                    return None
+                off = (h * 3600 + mn * 60 + sc) * (-1 if z.group(1) == "-" else 1)
+        return ((day * 86400 + hh * 3600 + mi * 60 + ss) - off) * 1_000_000 + int(((frac or "") + "000000")[:6])
+    m = re.fullmatch(r"decimal(?:\((\d+),(\d+)\))?", typ)
+    if m:
+        p, sc = (int(m.group(1)), int(m.group(2))) if m.group(1) else (10, 0)
+        if not re.fullmatch(r"[+-]?(?:\d+\.?\d*|\.\d+)(?:[eE][+-]?\d+)?", t):
+            return None
+        q = Fraction(decimal.Decimal(t)) * 10 ** sc
+        mag = abs(q)
+        unscaled = int(mag) + (1 if mag - int(mag) >= Fraction(1, 2) else 0)  # ROUND_HALF_UP
+        if unscaled >= 10 ** p:
+            return None
+        return -unscaled if q < 0 else unscaled
     raise ValueError("unsupported partition type %s" % typ)
 
 

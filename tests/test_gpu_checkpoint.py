@@ -112,3 +112,116 @@ def test_device_checkpoint_round_trip(engine, tmp_path, parts):
     finally:
         st.release()
     DeltaLog.clear_cache()
+
+
+# ---- partitionValues_parsed of every Spark partition type (timestamp / decimal / double /
+# float / binary partitions made the whole checkpoint fail) ---------------------------------------------
+_PTYPES = {"ts": "timestamp", "d": "decimal(10,2)", "big": "decimal(25,3)", "small": "decimal(5,1)", "x": "double",
+           "f": "float", "b": "binary", "i": "integer"}
+_PVALUES = {
+    "ts": ["2021-03-04 05:06:07.123456", "2021-03-04", "2021-03-04T05:06:07Z", " 2021-03-04 05:06:07+02:00 ", "bad",
+           "2020-02-30", "2021-03-04 05:06:07.1234567", None],
+    "d": ["12.345", "-12.345", "1e2", "123456789.1", "  7 ", "abc", "0.005", None],
+    "big": ["1234567890123456789012.5", "-3.0004", "1e21", "0", "x", "99999999999999999999999.9995", "1.5", None],
+    "small": ["1234.5", "12345.6", "-0.05", ".5", "5.", "1e-1", "9999.95", None],
+    "x": ["2.25", " 1e400 ", "-0", "NaN", "-Infinity", "inf", "3.14159265358979323846264338", "0x1.8p1", "abc",
+          "1.7976931348623157E308d", "4.9e-324", None],
+    "f": ["0.1", "3.4028236e38", "1.5f", "-nan", "16777217", "1e-46", "123456.789e3", None],
+    "b": ["ab", "", "é", None],
+    "i": ["1", " 2 ", "x", None],
+}
+
+
+def _typed_table(table):
+    import json
+    from delta_amd.testing import synth as S
+    lp = os.path.join(table, "_delta_log")
+    os.makedirs(lp)
+    schema = {"type": "struct", "fields": [{"name": c, "type": t, "nullable": True, "metadata": {}}
+                                           for c, t in _PTYPES.items()] + [
+        {"name": "v", "type": "long", "nullable": True, "metadata": {}}]}
+    md = {"id": "typed", "format": {"provider": "parquet", "options": {}}, "schemaString": json.dumps(schema),
+          "partitionColumns": list(_PTYPES), "configuration": {}, "createdTime": 1}
+    prot = {"minReaderVersion": 1, "minWriterVersion": 2}
+    n = max(len(v) for v in _PVALUES.values())
+    pvs = [{c: vals[k % len(vals)] for c, vals in _PVALUES.items()} for k in range(2 * n)]
+    adds = [{"path": "ck-%d.parquet" % k, "partitionValues": pv, "size": k + 1, "modificationTime": k}
+            for k, pv in enumerate(pvs)]
+    # the checkpoint's map columns and JSON lines both feed the typed columns
+    S.write_checkpoint_records(os.path.join(lp, "%020d.checkpoint.parquet" % 0), prot, md, adds)
+    lines = [json.dumps({"add": {"path": "js-%d.parquet" % k, "partitionValues": pv, "size": 1,
+                                 "modificationTime": 1, "dataChange": True}}) for k, pv in enumerate(pvs)]
+    with open(os.path.join(lp, "%020d.json" % 1), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    return lp
+
+
+def _expect(v, t):
+    return None if v is None else O.cast_string(v, t)
+
+
+def _norm_val(v, t):
+    """A pyarrow value of partitionValues_parsed in the oracle's representation."""
+    import datetime as _dt
+    from decimal import Decimal
+    if v is None:
+        return None
+    if t == "timestamp":
+        epoch = _dt.datetime(1970, 1, 1, tzinfo=v.tzinfo) if v.tzinfo else _dt.datetime(1970, 1, 1)
+        d = v - epoch
+        return (d.days * 86400 + d.seconds) * 1_000_000 + d.microseconds
+    if t.startswith("decimal"):
+        return int(Decimal(v).scaleb(int(t.split(",")[1].rstrip(")"))))
+    return v
+
+
+def _same_value(got, want, t):
+    import math
+    if want is None or got is None:
+        return want is None and got is None
+    if t in ("double", "float"):
+        return (math.isnan(got) and math.isnan(want)) or (got == want and math.copysign(1, got) == math.copysign(1, want))
+    return got == want
+
+
+def test_parsed_partition_values_every_type(engine, tmp_path):
+    """The device writer's partitionValues_parsed for timestamp (INT96), decimal (INT32 / INT64 /
+    FIXED_LEN_BYTE_ARRAY), double, float and binary partition columns equals Spark's Cast of each
+    file's partition value as the oracle restates it (off-fast-path floats converted by the host), from
+    the checkpoint's map columns and from JSON lines; the Arrow writer agrees."""
+    import pyarrow.parquet as pq
+    lp = _typed_table(str(tmp_path / "t"))
+    staged = engine.stage_log(lp)
+    st = staged.replay(0)
+    staged.release()
+    try:
+        data, rows, adds = st.write_checkpoint_part(1, 1, stats=True, parsed=True, with_adds=True)
+        assert adds == st.counts["num_files"]
+        t = pq.read_table(io.BytesIO(data))
+        ftypes = {f.name: str(f.type) for f in t.schema.field("add").type.field("partitionValues_parsed").type}
+        assert ftypes["ts"].startswith("timestamp") and ftypes["d"] == "decimal128(10, 2)"
+        assert ftypes["big"] == "decimal128(25, 3)" and ftypes["f"] == "float" and ftypes["b"] == "binary"
+        checked = 0
+        dev = {}
+        for r in t.to_pylist():
+            a = r["add"]
+            if a is None:
+                continue
+            pv = dict(a["partitionValues"])
+            dev[a["path"]] = a["partitionValues_parsed"]
+            for c, typ in _PTYPES.items():
+                got, want = _norm_val(a["partitionValues_parsed"][c], typ), _expect(pv.get(c), typ)
+                assert _same_value(got, want, typ), (c, pv.get(c), got, want)
+                checked += 1
+        assert checked == len(_PTYPES) * st.counts["num_files"]
+        # the Arrow writer (DeltaLog.checkpoint(device=False)) reads the same values
+        from delta_amd.checkpoint import checkpoint_table
+        arrow, _ = checkpoint_table(st)
+        for r in arrow.to_pylist():
+            if r["add"]:
+                for c, typ in _PTYPES.items():
+                    x = _norm_val(dev[r["add"]["path"]][c], typ)
+                    y = _norm_val(r["add"]["partitionValues_parsed"][c], typ)
+                    assert _same_value(x, y, typ), (c, x, y)
+    finally:
+        st.release()

@@ -185,17 +185,6 @@ constexpr int JL_FLUSH = JL_TOKCAP - 16;  // a window adds at most 16 tokens
 #ifndef DR_JL_WAVES
 #define DR_JL_WAVES 1
 #endif
-// LDS staging of the wave's byte region (r03): the 64 lines of a wave are contiguous in d_json, so
-// the wave copies [its first line's 16-byte block, its last line's end) into LDS with coalesced
-// 16-byte loads (every byte fetched once), and each lane then walks its line from LDS. Without it
-// every lane re-requests its own line's cache lines window by window, and with 16 waves per CU the
-// lines are evicted between windows (PMC: 4.8x the algorithmic bytes fetched). A region larger than
-// the staging buffer (long lines: metaData, big stats) walks global memory as before.
-#ifndef DR_JL_STAGE_KB
-#define DR_JL_STAGE_KB 24
-#endif
-constexpr uint32_t JL_STAGE_BYTES = DR_JL_STAGE_KB * 1024u;
-
 // One lane's line walk: tokenize window by window into the LDS token buffer, the DFA by token index
 // (see below); `p` is the line's first byte wherever it is read from (LDS or global).
 __device__ __forceinline__ void walk_line(const JsonParseArgs& a, uint32_t* tokbuf, uint32_t lane, uint64_t line,
@@ -264,30 +253,13 @@ __device__ __forceinline__ void walk_line(const JsonParseArgs& a, uint32_t* tokb
 //     or all removes), so the 64 lanes take the same grammar branch at the same step instead of
 //     diverging byte by byte.
 // The buffer is flushed through phase 2 whenever a lane could overflow it, and at the end.
-template <bool Stage>
 __global__ void __launch_bounds__(JL_T, DR_JL_WAVES) k_json_lines(JsonParseArgs a) {
   __shared__ uint32_t tokbuf[JL_TOKCAP * JL_T];
-  __shared__ uint4 stage[Stage ? JL_STAGE_BYTES / 16 : 1];
   const uint32_t lane = threadIdx.x;
   const uint64_t line = uint64_t(blockIdx.x) * JL_T + lane;
   const bool live = line < a.nlines;
   const uint64_t b = !live ? 0 : line == 0 ? 0 : a.nl[line - 1] + 1;
   const uint32_t n = live ? uint32_t(a.nl[line] - b) : 0;
-  if constexpr (Stage) {
-    // the wave's region: [first line's 16-byte block, end of the last live line rounded up to 16)
-    const uint64_t first = uint64_t(blockIdx.x) * JL_T;
-    const uint64_t last = min(first + JL_T, a.nlines) - 1;
-    const uint64_t r0 = (first == 0 ? 0 : a.nl[first - 1] + 1) & ~uint64_t(15);
-    const uint64_t r1 = (a.nl[last] + 15) & ~uint64_t(15);
-    if (r1 - r0 <= JL_STAGE_BYTES) {
-      const uint4* src = reinterpret_cast<const uint4*>(a.buf + r0);
-      const uint32_t nq = uint32_t((r1 - r0) >> 4);
-      for (uint32_t k = lane; k < nq; k += JL_T) stage[k] = src[k];
-      __syncthreads();
-      walk_line(a, tokbuf, lane, line, live, b, n, reinterpret_cast<const uint8_t*>(stage) + (b - r0));
-      return;
-    }
-  }
   walk_line(a, tokbuf, lane, line, live, b, n, a.buf + b);
 }
 
@@ -328,14 +300,7 @@ void launch_json_place(const uint8_t* buf, uint64_t len, const uint32_t* block_c
 
 void launch_json_parse(const JsonParseArgs& a, hipStream_t st) {
   if (!a.nlines) return;
-  // DR_JL_STAGE=0: the unstaged walker (every lane reads its line from global memory)
-  static const bool stage = [] {
-    const char* e = std::getenv("DR_JL_STAGE");
-    return !(e && std::atoi(e) == 0);
-  }();
-  const dim3 grid(unsigned((a.nlines + dev::JL_T - 1) / dev::JL_T));
-  if (stage) DR_LAUNCH(dev::k_json_lines<true>, grid, dim3(dev::JL_T), 0, st, a);
-  else DR_LAUNCH(dev::k_json_lines<false>, grid, dim3(dev::JL_T), 0, st, a);
+  DR_LAUNCH(dev::k_json_lines, dim3(unsigned((a.nlines + dev::JL_T - 1) / dev::JL_T)), dim3(dev::JL_T), 0, st, a);
 }
 
 void launch_json_hard(const JsonParseArgs& a, hipStream_t st) {

@@ -153,6 +153,7 @@ def cast_partition_value(s: Optional[str], typ: str):
 
 # ---- the checkpoint's other partitionValues_parsed casts (the device grammar, k_filter.hip) ------
 _FP_RE = re.compile(r"[+-]?(?:NaN|Infinity|(?:\d+\.?\d*|\.\d+)(?:[eE][+-]?\d+)?[fFdD]?)")
+_HEXFP_RE = re.compile(r"([+-]?)0[xX]([0-9a-fA-F]+\.?[0-9a-fA-F]*|\.[0-9a-fA-F]+)[pP]([+-]?\d+)[fFdD]?")
 
 
 def _jtrim(s: str) -> str:
@@ -170,9 +171,10 @@ def _round_f32(x):
     from fractions import Fraction
     if x == 0:
         return 0.0
-    f = struct.unpack("<f", struct.pack("<f", float(x)))[0] if abs(float(x)) < 3.5e38 else float("inf")
-    if f in (float("inf"), float("-inf")):
-        return f
+    if abs(x) >= (Fraction(2) - Fraction(1, 1 << 24)) * Fraction(2) ** 127:  # rounds past FLT_MAX
+        return float("inf") if x > 0 else float("-inf")
+    fmax = float((Fraction(2) - Fraction(1, 1 << 23)) * Fraction(2) ** 127)
+    f = struct.unpack("<f", struct.pack("<f", min(max(float(x), -fmax), fmax)))[0]
     bits = struct.unpack("<I", struct.pack("<f", f))[0]
     best = None
     for b in (bits - 1, bits, bits + 1):
@@ -191,6 +193,12 @@ def java_parse_fp(s: str, is_float: bool):
     """Double.parseDouble / Float.parseFloat, else Spark's special literals (inf, nan, ...)."""
     from fractions import Fraction
     t = _jtrim(s)
+    hm = _HEXFP_RE.fullmatch(t)
+    if hm:  # Java's hexadecimal significand with a binary exponent
+        ip, _, fp = hm.group(2).partition(".")
+        x = Fraction(int((ip or "0") + fp, 16), 16 ** len(fp)) * Fraction(2) ** int(hm.group(3))
+        v = _round_f32(x) if is_float else (float(x) if x < Fraction(2) ** 1025 else float("inf"))
+        return -v if hm.group(1) == "-" else v
     if _FP_RE.fullmatch(t):
         body = t.rstrip("fFdD") if not t.endswith(("NaN", "Infinity")) else t
         if body.lstrip("+-") == "NaN":

@@ -593,22 +593,33 @@ def cast_string_v2(s: str, typ: str):
     from fractions import Fraction
     t = _java_trim(s)
     if typ in ("float", "double"):
-        m = re.fullmatch(r"([+-]?)(?:(NaN)|(Infinity)|((?:\d+\.?\d*|\.\d+)(?:[eE][+-]?\d+)?)[fFdD]?)", t)
+        m = re.fullmatch(r"([+-]?)(?:(NaN)|(Infinity)|((?:\d+\.?\d*|\.\d+)(?:[eE][+-]?\d+)?)[fFdD]?|"
+                         r"0[xX]((?:[0-9a-fA-F]+\.?[0-9a-fA-F]*|\.[0-9a-fA-F]+))[pP]([+-]?\d+)[fFdD]?)", t)
         if m:
             if m.group(2):
                 return float("nan")
             if m.group(3):
                 return float("-inf") if m.group(1) == "-" else float("inf")
-            x = Fraction(m.group(4))
+            if m.group(5) is not None:  # Java's hexadecimal significand with a binary exponent
+                h = m.group(5)
+                ip, _, fp = h.partition(".")
+                x = Fraction(int((ip or "0") + fp, 16), 16 ** len(fp)) * Fraction(2) ** int(m.group(6))
+            else:
+                x = Fraction(m.group(4))
             if typ == "double":
                 v = float(x) if x < Fraction(2) ** 1025 else float("inf")
             else:
                 import numpy as np
                 # the float32 nearest to the exact value (ties to even), by bracketing with float32
                 # neighbours of the double approximation
-                c = np.float32(float(x)) if x < Fraction(2) ** 129 else np.float32("inf")
+                fmax = (Fraction(2) - Fraction(1, 1 << 23)) * Fraction(2) ** 127
+                if x >= (Fraction(2) - Fraction(1, 1 << 24)) * Fraction(2) ** 127:
+                    c = np.float32("inf")
+                else:
+                    c = np.float32(float(min(x, fmax)))
                 if np.isfinite(c):
-                    cand = [np.nextafter(c, np.float32(-np.inf)), c, np.nextafter(c, np.float32(np.inf))]
+                    with np.errstate(over="ignore"):
+                        cand = [np.nextafter(c, np.float32(-np.inf)), c, np.nextafter(c, np.float32(np.inf))]
                     cand = [k for k in cand if np.isfinite(k)]
                     c = min(cand, key=lambda k: (abs(Fraction(float(k)) - x), int(np.float32(k).view(np.uint32)) & 1))
                 v = float(c)

@@ -676,7 +676,7 @@ def test_scan_scratch_capacity_is_checked(engine, tmp_path, monkeypatch):
     from delta_amd.testing import synth as S
     exp = S.build_config(2, str(tmp_path), scale=0.002)
     lp = os.path.join(str(tmp_path), "_delta_log")
-    monkeypatch.setenv("DR_SCAN_SCRATCH_MAX", "64")
+    monkeypatch.setenv("DR_SCAN_SCRATCH_MAX", "8")  # below any scan's 16-byte minimum
     with pytest.raises(DeltaError) as ei:
         _gpu_replay(engine, lp, exp.min_file_retention_timestamp)
     assert ei.value.status == 15 and "scratch" in str(ei.value)

@@ -56,7 +56,6 @@ struct dr_ctx {
   std::string err;
   bool timing = false;
   std::string timing_only;  // non-empty: only this kernel gets an event pair (dr_set_timing_only)
-  bool timing_pending = false;
   bool overlap = false;  // DR_OVERLAP=1: K1 line parsing on stream2, beside the checkpoint decode
   struct Mark {
     std::string name;
@@ -94,6 +93,22 @@ struct dr_ctx {
       bounce.push_back(static_cast<uint8_t*>(p));
       bounce_ev.push_back(e);
     }
+  }
+
+  // pinned readback words: a replay queues every kernel first and then copies its counters, error
+  // codes and the non-file line list here in one round trip (one stream sync per replay)
+  static constexpr size_t kPinWords = 8192;
+  uint64_t* hpin = nullptr;
+  uint64_t* pinned() {
+    if (!hpin) {
+      void* p = nullptr;
+      if (hipHostMalloc(&p, kPinWords * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        fail(DR_E_OOM, "pinned readback words");
+      }
+      hpin = static_cast<uint64_t*>(p);
+    }
+    return hpin;
   }
 
   void* alloc(size_t n) {
@@ -136,28 +151,37 @@ struct dr_ctx {
   }
   // A stage's time is the interval since the previous mark on the same stream (a stream's first
   // mark only opens its timeline).
-  void mark(const char* name, int on = 0) {
-    if (!timing) return;
+  // timing events are pooled: creating and destroying four per replay cost the bench's timed steps
+  // more than the events themselves
+  std::vector<hipEvent_t> ev_pool;
+  hipEvent_t get_event() {
+    if (!ev_pool.empty()) {
+      hipEvent_t e = ev_pool.back();
+      ev_pool.pop_back();
+      return e;
+    }
     hipEvent_t e;
     HIP_OK(hipEventCreate(&e));
+    return e;
+  }
+  void put_event(hipEvent_t e) { ev_pool.push_back(e); }
+  void mark(const char* name, int on = 0) {
+    if (!timing || !timing_only.empty()) return;  // stage marks only in the per-kernel table mode
+    hipEvent_t e = get_event();
     HIP_OK(hipEventRecord(e, on ? stream2 : stream));
     marks.push_back(Mark{name, e, on});
   }
-  // The launch hook (kernels.h): an event before and after every kernel of the call.
-  static void on_launch(void* user, const char* kernel, hipStream_t st, int end) {
+  // The launch hook (kernels.h): an event pair carried by each selected launch of the call.
+  static bool on_launch(void* user, const char* kernel, hipEvent_t* start, hipEvent_t* stop) {
     dr_ctx* c = static_cast<dr_ctx*>(user);
-    if (!end) {
-      KMark k{kernel_name(kernel), nullptr, nullptr};
-      c->timing_pending = c->timing_only.empty() || k.name == c->timing_only;
-      if (!c->timing_pending) return;
-      HIP_OK(hipEventCreate(&k.a));
-      HIP_OK(hipEventCreate(&k.b));
-      HIP_OK(hipEventRecord(k.a, st));
-      c->kmarks.push_back(k);
-    } else if (c->timing_pending && !c->kmarks.empty()) {
-      HIP_OK(hipEventRecord(c->kmarks.back().b, st));
-      c->timing_pending = false;
-    }
+    KMark k{kernel_name(kernel), nullptr, nullptr};
+    if (!(c->timing_only.empty() || k.name == c->timing_only)) return false;
+    k.a = c->get_event();
+    k.b = c->get_event();
+    *start = k.a;
+    *stop = k.b;
+    c->kmarks.push_back(k);
+    return true;
   }
   // "(dev::k_gather<uint64_t, uint32_t>)" -> "k_gather"
   static std::string kernel_name(const char* k) {
@@ -186,7 +210,7 @@ struct dr_ctx {
       HIP_OK(hipEventElapsedTime(&ms, marks[k - 1].ev, marks[i].ev));
       timings.emplace_back(marks[i].name, ms);
     }
-    for (auto& m : marks) (void)hipEventDestroy(m.ev);
+    for (auto& m : marks) put_event(m.ev);
     marks.clear();
     std::map<std::string, int> seen;
     for (auto& k : kmarks) {
@@ -195,18 +219,18 @@ struct dr_ctx {
       HIP_OK(hipEventElapsedTime(&ms, k.a, k.b));
       const int n = ++seen[k.name];
       timings.emplace_back(n == 1 ? k.name : k.name + "#" + std::to_string(n), ms);
-      (void)hipEventDestroy(k.a);
-      (void)hipEventDestroy(k.b);
+      put_event(k.a);
+      put_event(k.b);
     }
     kmarks.clear();
   }
   void drop_timings() {
     set_launch_hook(nullptr, nullptr);
-    for (auto& m : marks) (void)hipEventDestroy(m.ev);
+    for (auto& m : marks) put_event(m.ev);
     marks.clear();
     for (auto& k : kmarks) {
-      (void)hipEventDestroy(k.a);
-      (void)hipEventDestroy(k.b);
+      put_event(k.a);
+      put_event(k.b);
     }
     kmarks.clear();
   }
@@ -392,6 +416,10 @@ struct StagedData {
   std::unique_ptr<PagePlan> mt;           // add.modificationTime (planned on first scan order)
   std::unique_ptr<PagePlan> exp[2];       // the export's add / remove leaves (planned on first export)
   std::mutex pv_mu;
+  // canonicalisation arena bytes the last replay of this segment needed (-1: none yet). A capacity
+  // hint only: the next replay sizes its arena from it instead of reading the special-path counters
+  // back before K3; an arena that turns out too small is detected at the end and the replay redone.
+  std::atomic<int64_t> canon_need{-1};
 };
 
 struct dr_staged {
@@ -1298,12 +1326,30 @@ static void reduce_nonfile(dr_state& st, std::vector<NonFileAction>& acts, bool 
     fail(DR_E_MISSING_METADATA, action_not_found("metadata", st.counts.version));
 }
 
-// K1 + K2 + canonicalisation: fills st's per-action arrays (checkpoint rows first, then JSON lines)
-// and collects the non-file actions (protocol / metaData / txn) on the host in replay order.
-static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr_state* st,
-                          std::vector<NonFileAction>& nf, bool canonicalize = true) {
+// What parse_launch leaves for parse_finish: the device counters (0 special count, 1 special bytes,
+// 2 non-file lines, 3 malformed lines, 4 canonicalisation arena fill, 5 lines deferred to the
+// General walker, 7 checkpoint decode error) and the non-file line list, read back after the
+// caller has queued the rest of its kernels.
+struct ParsePending {
+  DBuf<uint64_t> counters;
+  DBuf<uint64_t> nonfile;   // {line, byte offset} pairs
+  uint64_t R = 0, nlines = 0;
+  uint64_t canon_cap = 0;   // arena bytes given to k_canon (0: no canonicalisation launched)
+  bool canonicalize = false;
+  bool canon_sized = false; // the arena was sized from the counters (exact), not from a hint
+  size_t pin_at = 0;        // where its words land in ctx->pinned()
+};
+constexpr size_t kPinNonfile = 1024;  // non-file entries (pairs) read back with the counters
+
+// K1 + K2 + canonicalisation, queued on the context's stream: fills st's per-action arrays
+// (checkpoint rows first, then JSON lines). On the first replay of a segment the special-path
+// counters are read back before k_canon (the arena is sized exactly); later replays size the arena
+// from the segment's last need and queue K3/K4 without a round trip.
+static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr_state* st,
+                                 bool canonicalize) {
   StagedData& s = *sp;
   hipStream_t stream = ctx->stream;
+  ParsePending pp;
   // ---- K1a: newline index ----
   const uint64_t json_len = s.h_json.size();
   const uint64_t nbj = json_num_blocks(json_len);
@@ -1335,7 +1381,7 @@ static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
                                      // 5 lines deferred to the General walker, 7 checkpoint decode error
   counters.zero(stream);
   DBuf<uint64_t> nl(ctx, nlines);
-  DBuf<uint64_t> nonfile(ctx, nlines);
+  DBuf<uint64_t> nonfile(ctx, 2 * nlines);
   ActionArrays act{st->kind.p, st->flags.p, st->key.p, st->path_ptr.p, st->path_len.p, st->size.p, st->delts.p,
                    st->src_off.p, st->src_len.p};
   DBuf<uint64_t> hard(ctx, nlines);
@@ -1419,31 +1465,80 @@ static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
   }
   // the checkpoint decoder's error code rides in counters[7]: one read-back for both
   if (R) HIP_OK(hipMemcpyAsync(counters.p + 7, pq_err.p, sizeof(uint32_t), hipMemcpyDeviceToDevice, stream));
-  std::vector<uint64_t> cnt = d2h(counters.p, 8, stream);
+  // ---- canonicalisation of special paths ----
+  if (canonicalize) {
+    int64_t hint = s.canon_need.load();
+    // test hook: DR_CANON_HINT=<bytes> stands in for the first replay's exact sizing (an undersized
+    // hint exercises the detect-and-redo path)
+    if (hint < 0)
+      if (const char* e = std::getenv("DR_CANON_HINT")) hint = std::max<int64_t>(0, std::atoll(e));
+    uint64_t cap = 0;
+    if (hint < 0) {  // first replay of the segment: the exact arena from the counters
+      const std::vector<uint64_t> cnt = d2h(counters.p, 2, stream);
+      cap = cnt[0] ? cnt[1] * 2 + 64 * cnt[0] + 64 : 0;
+      pp.canon_sized = true;
+    } else {
+      cap = uint64_t(hint);
+    }
+    if (cap) {
+      st->arenas.push_back(std::make_shared<DBuf<uint8_t>>(ctx, cap));
+      CanonArgs cg{act, N, st->arenas.back()->p, cap, counters.p + 4};
+      launch_canon(cg, stream);
+    }
+    pp.canon_cap = cap;
+    pp.canonicalize = true;
+  }
+  pp.counters = std::move(counters);
+  pp.nonfile = std::move(nonfile);
+  pp.R = R;
+  pp.nlines = nlines;
+  return pp;
+}
+
+// Queues the copies of parse_launch's counters and the first non-file entries into the pinned
+// words at `at` (no sync).
+static size_t parse_queue_readback(dr_ctx* ctx, ParsePending& pp, size_t at) {
+  uint64_t* h = ctx->pinned() + at;
+  pp.pin_at = at;
+  HIP_OK(hipMemcpyAsync(h, pp.counters.p, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
+  const uint64_t k = std::min<uint64_t>(pp.nlines, kPinNonfile);
+  if (k) HIP_OK(hipMemcpyAsync(h + 8, pp.nonfile.p, 2 * k * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
+  return at + 8 + 2 * kPinNonfile;
+}
+
+// After the stream has drained: error codes, counters and the non-file actions (protocol /
+// metaData / txn, parsed on the host: checkpoint rows first, then JSON lines in order). Returns
+// false when the canonicalisation arena sized from the segment's hint was too small (the caller
+// redoes the replay; the hint now holds the exact need).
+static bool parse_finish(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr_state* st, ParsePending& pp,
+                         std::vector<NonFileAction>& nf) {
+  StagedData& s = *sp;
+  const uint64_t* cnt = ctx->pinned() + pp.pin_at;
+  const uint64_t R = pp.R, nlines = pp.nlines, json_len = s.h_json.size();
   if (R && cnt[7] != 0) fail(DR_E_PARQUET, fmt("device checkpoint decode failed (code %u)", unsigned(cnt[7])));
   st->counts.malformed_lines = int64_t(cnt[3]);
-  // ---- canonicalisation of special paths ----
-  if (cnt[0] && canonicalize) {
-    const uint64_t cap = cnt[1] * 2 + 64 * cnt[0] + 64;
-    st->arenas.push_back(std::make_shared<DBuf<uint8_t>>(ctx, cap));
-    CanonArgs cg{act, N, st->arenas.back()->p, cap, counters.p + 4};
-    launch_canon(cg, stream);
+  if (pp.canonicalize) {
+    const uint64_t need = cnt[0] ? cnt[1] * 2 + 64 * cnt[0] + 64 : 0;
+    if (!pp.canon_sized && (need > pp.canon_cap || cnt[4] > pp.canon_cap)) {
+      s.canon_need.store(int64_t(need));
+      return false;
+    }
+    s.canon_need.store(int64_t(need));
   }
-  // ---- non-file actions (host): checkpoint rows first, then JSON lines in order ----
   nf = s.ck_nonfile;
   const uint64_t nnf = std::min<uint64_t>(cnt[2], nlines);
   if (nnf) {
-    std::vector<uint64_t> lines = d2h(nonfile.p, nnf, stream);
+    std::vector<std::pair<uint64_t, uint64_t>> lines(nnf);  // (line, byte offset)
+    if (nnf <= kPinNonfile) {
+      for (uint64_t k = 0; k < nnf; ++k) lines[k] = {cnt[8 + 2 * k], cnt[8 + 2 * k + 1]};
+    } else {
+      const std::vector<uint64_t> all = d2h(pp.nonfile.p, 2 * nnf, ctx->stream);
+      for (uint64_t k = 0; k < nnf; ++k) lines[k] = {all[2 * k], all[2 * k + 1]};
+    }
     std::sort(lines.begin(), lines.end());
-    DBuf<uint64_t> dof(ctx, nnf);
-    for (uint64_t& x : lines) x += R;  // action indices
-    DBuf<uint64_t> didx(ctx, nnf);
-    HIP_OK(hipMemcpyAsync(didx.p, lines.data(), nnf * 8, hipMemcpyHostToDevice, stream));
-    launch_gather_u64_by64(st->src_off.p, didx.p, nnf, dof.p, stream);
-    std::vector<uint64_t> offs = d2h(dof.p, nnf, stream);
     for (uint64_t k = 0; k < nnf; ++k) {
-      const uint64_t li = lines[k] - R;
-      const uint64_t b = offs[k];
+      const uint64_t li = lines[k].first;
+      const uint64_t b = lines[k].second;
       uint64_t e = b;
       while (e < json_len && s.h_json[e] != '\n') ++e;
       JVal v;
@@ -1467,11 +1562,30 @@ static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
       }
     }
   }
+  return true;
+}
+
+// K1 + K2 + canonicalisation with the counters read back at once (callers that use the arrays on
+// the host right away). An arena hint that proved too small redoes the parse with the exact size.
+static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr_state* st,
+                          std::vector<NonFileAction>& nf, bool canonicalize = true) {
+  for (;;) {
+    ParsePending pp = parse_launch(ctx, sp, st, canonicalize);
+    parse_queue_readback(ctx, pp, 0);
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+    if (parse_finish(ctx, sp, st, pp, nf)) return;
+    st->arenas.clear();
+  }
 }
 
 // K3 (hash partition) + K4 (per-bucket last-writer-wins, retention) + compaction over st's action
-// arrays; fills st->live / st->tomb and the file counters.
-static void reduce_actions(dr_ctx* ctx, dr_state* st, int64_t cutoff, uint32_t flags = 0) {
+// arrays, queued without a host round trip; reduce_finish reads the counters back.
+struct ReducePending {
+  DBuf<unsigned long long> totals;
+  size_t pin_at = 0;
+};
+
+static ReducePending reduce_launch(dr_ctx* ctx, dr_state* st, int64_t cutoff, uint32_t flags = 0) {
   hipStream_t stream = ctx->stream;
   const uint64_t N = st->n_actions;
   // ---- K3: partition by hash bucket ----
@@ -1540,7 +1654,21 @@ static void reduce_actions(dr_ctx* ctx, dr_state* st, int64_t cutoff, uint32_t f
   launch_compact2(CompactArgs{olive.p, boff.p, lcount.p, loff.p, nb, st->live.p},
                   CompactArgs{otomb.p, boff.p, tcount.p, tmoff.p, nb, st->tomb.p}, stream);
   HIP_OK(hipMemcpyAsync(totals.p + 7, boff.p + nb, 8, hipMemcpyDeviceToDevice, stream));
-  const std::vector<unsigned long long> tot = d2h(totals.p, 8, stream);
+  ReducePending rp;
+  rp.totals = std::move(totals);
+  return rp;
+}
+
+static size_t reduce_queue_readback(dr_ctx* ctx, ReducePending& rp, size_t at) {
+  rp.pin_at = at;
+  HIP_OK(hipMemcpyAsync(ctx->pinned() + at, rp.totals.p, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
+  return at + 8;
+}
+
+// After the stream has drained: the survivor counts and computedState counters.
+static void reduce_finish(dr_ctx* ctx, dr_state* st, const ReducePending& rp) {
+  const uint64_t* tot = ctx->pinned() + rp.pin_at;
+  const uint64_t N = st->n_actions;
   const uint64_t n_file_actions = tot[7];
   st->n_live = tot[0];
   st->n_tomb = tot[2];
@@ -1551,6 +1679,13 @@ static void reduce_actions(dr_ctx* ctx, dr_state* st, int64_t cutoff, uint32_t f
   st->counts.tomb_key_sum = tot[6];
   st->counts.num_actions = int64_t(N);
   st->counts.num_file_actions = int64_t(n_file_actions);
+}
+
+static void reduce_actions(dr_ctx* ctx, dr_state* st, int64_t cutoff, uint32_t flags = 0) {
+  ReducePending rp = reduce_launch(ctx, st, cutoff, flags);
+  reduce_queue_readback(ctx, rp, 0);
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  reduce_finish(ctx, st, rp);
 }
 
 static dr_state* new_state(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp) {
@@ -1948,14 +2083,35 @@ static dr_state* apply_tail(dr_ctx* ctx, dr_state& base, const std::shared_ptr<S
   return st.release();
 }
 
+// A full replay is queued end to end (K1, K2, k_canon, K3, K4, compaction) and read back once: the
+// counters, error codes and non-file line list of the parse and the reducer's totals land in the
+// pinned words with one stream sync. The host's protocol / metaData / txn reduction follows.
 static dr_state* replay(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, int64_t cutoff, uint32_t flags) {
   std::unique_ptr<dr_state> st(new_state(ctx, sp));
   ctx->mark("start");
   std::vector<NonFileAction> nf;
-  parse_actions(ctx, sp, st.get(), nf);
-  reduce_actions(ctx, st.get(), cutoff, flags);
+  static const bool dbg = std::getenv("DR_HOST_DEBUG") != nullptr;  // host phase times per replay
+  const double t0 = dbg ? now_s() : 0;
+  double t1 = 0, t2 = 0;
+  for (;;) {
+    ParsePending pp = parse_launch(ctx, sp, st.get(), true);
+    ReducePending rp = reduce_launch(ctx, st.get(), cutoff, flags);
+    reduce_queue_readback(ctx, rp, parse_queue_readback(ctx, pp, 0));
+    if (dbg) t1 = now_s();
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+    if (dbg) t2 = now_s();
+    if (parse_finish(ctx, sp, st.get(), pp, nf)) {
+      reduce_finish(ctx, st.get(), rp);
+      break;
+    }
+    // the arena hint was too small: redo with the exact size (parse_finish stored it)
+    st.reset(new_state(ctx, sp));
+  }
   st->cutoff = cutoff;
   reduce_nonfile(*st, nf, !(flags & DR_FLAG_NO_VALIDATION));
+  if (dbg)
+    std::fprintf(stderr, "replay host: queue %.1f us, wait %.1f us, finish %.1f us (%zu non-file actions)\n",
+                 (t1 - t0) * 1e6, (t2 - t1) * 1e6, (now_s() - t2) * 1e6, nf.size());
   ctx->mark("end");
   return st.release();
 }
@@ -3837,62 +3993,78 @@ struct dr_shard {
   DBuf<uint32_t> send_idx, send_plen;
   DBuf<uint64_t> send_poff;
   bool reduced = false;
+  bool owner_read = false;        // the owner side's counters are on the host (sh.owner)
   dr_counts owner{};
+  ParsePending parse;             // the sender side's parse; its counters come back in shard_finish
+  std::unique_ptr<dr_state> own;  // the owner side's reduced shard (alive until the verdicts are set)
+  ReducePending red;
 };
 
+// Sender side, step 1: parse this rank's slice, count its file actions and their canonical path
+// bytes per owner and lay out the send order (stable per owner). One round trip: the per-owner
+// record and byte counts the caller needs to size the exchange.
 static void shard_begin(dr_shard& sh, uint64_t* send_counts, uint64_t* send_bytes) {
   dr_ctx* ctx = sh.ctx;
   hipStream_t stream = ctx->stream;
   sh.st.reset(new_state(ctx, sh.staged));
   ctx->mark("start");
-  parse_actions(ctx, sh.staged, sh.st.get(), sh.nf);
+  sh.parse = parse_launch(ctx, sh.staged, sh.st.get(), true);
   dr_state& st = *sh.st;
   const uint64_t N = st.n_actions;
+  const uint32_t W = sh.world;
   const uint64_t nt = shard_tiles(N);
-  const uint64_t nc = uint64_t(sh.world) * nt;
-  DBuf<uint32_t> bcnt(ctx, nc);
-  DBuf<uint64_t> boff(ctx, nc + 1);
+  const uint64_t nc = uint64_t(W) * nt;
+  DBuf<uint32_t> bcnt(ctx, nc), bbytes(ctx, nc);
+  DBuf<uint64_t> boff(ctx, nc + 1), byoff(ctx, nc + 1), sizes(ctx, 2 * uint64_t(W) + 1);
   DBuf<uint8_t> scratch(ctx, scan_scratch_for(nc));
-  ShardArgs a{st.kind.p, st.flags.p, st.key.p, st.size.p, st.delts.p, st.path_len.p, N, sh.world, nt,
-              bcnt.p, boff.p, nullptr, 0};
+  ShardArgs a{st.kind.p, st.flags.p, st.key.p, st.size.p, st.delts.p, st.path_len.p, N, W, nt,
+              bcnt.p, boff.p, nullptr, 0, bbytes.p};
   launch_shard_count(a, stream);
   launch_scan_u32(bcnt.p, boff.p, nc, ss(scratch), stream);
-  std::vector<uint64_t> hoff = d2h(boff.p, nc + 1, stream);
-  sh.nsend = hoff[nc];
+  launch_scan_u32(bbytes.p, byoff.p, nc, ss(scratch), stream);
+  launch_shard_sizes(bbytes.p, boff.p, byoff.p, W, nt, sizes.p, stream);
+  const std::vector<uint64_t> z = d2h(sizes.p, 2 * uint64_t(W) + 1, stream);
+  if (z[2 * W]) fail(DR_E_UNSUPPORTED, "more than 4 GiB of canonical paths in one shard tile");
+  sh.nsend = 0;
+  sh.send_path_bytes = 0;
+  for (uint32_t d = 0; d < W; ++d) {
+    send_counts[d] = z[d];
+    send_bytes[d] = z[W + d];
+    sh.nsend += z[d];
+    sh.send_path_bytes += z[W + d];
+  }
   sh.send_idx = DBuf<uint32_t>(ctx, sh.nsend);
   a.send_idx = sh.send_idx.p;
   a.nsend = sh.nsend;
   launch_shard_scatter(a, stream);
-  // path byte offsets of the send order
+  // path byte offsets of the send order (their per-owner totals are send_bytes)
   sh.send_plen = DBuf<uint32_t>(ctx, sh.nsend);
   sh.send_poff = DBuf<uint64_t>(ctx, sh.nsend + 1);
   launch_gather_u32(st.path_len.p, sh.send_idx.p, sh.nsend, sh.send_plen.p, stream);
   DBuf<uint8_t> scratch2(ctx, scan_scratch_for(sh.nsend));
   launch_scan_u32(sh.send_plen.p, sh.send_poff.p, sh.nsend, ss(scratch2), stream);
-  for (uint32_t d = 0; d < sh.world; ++d) {
-    const uint64_t s0 = hoff[uint64_t(d) * nt], s1 = d + 1 < sh.world ? hoff[uint64_t(d + 1) * nt] : sh.nsend;
-    send_counts[d] = s1 - s0;
-    const uint64_t b0 = d2h_one(sh.send_poff.p + s0, stream), b1 = d2h_one(sh.send_poff.p + s1, stream);
-    send_bytes[d] = b1 - b0;
-  }
-  sh.send_path_bytes = d2h_one(sh.send_poff.p + sh.nsend, stream);
 }
 
-static void shard_pack(dr_shard& sh, void* send_rec, void* send_path) {
+// Sender side, step 2: the 32 B records and the path bytes in send order. `sync`: return only when
+// the buffers are written (a caller exchanging them on another stream); the library's own RCCL
+// exchange runs on the same stream and needs no sync.
+static void shard_pack(dr_shard& sh, void* send_rec, void* send_path, bool sync = true) {
   dr_ctx* ctx = sh.ctx;
   hipStream_t stream = ctx->stream;
   dr_state& st = *sh.st;
   ShardArgs a{st.kind.p, st.flags.p, st.key.p, st.size.p, st.delts.p, st.path_len.p, st.n_actions, sh.world,
-              0, nullptr, nullptr, sh.send_idx.p, sh.nsend};
+              0, nullptr, nullptr, sh.send_idx.p, sh.nsend, nullptr};
   launch_shard_pack(a, static_cast<ShardRec*>(send_rec), sh.send_plen.p, stream);
   DBuf<uint64_t> ptrs(ctx, sh.nsend);
   launch_gather_u64(st.path_ptr.p, sh.send_idx.p, sh.nsend, ptrs.p, stream);
   launch_gather_bytes(ptrs.p, sh.send_plen.p, sh.send_poff.p, sh.nsend, static_cast<uint8_t*>(send_path), stream);
-  HIP_OK(hipStreamSynchronize(stream));
+  if (sync) HIP_OK(hipStreamSynchronize(stream));
 }
 
+// Owner side: K3/K4 over the received records (in rank order = replay order) and one verdict byte
+// per record (1 live, 2 kept tombstone, 0 dropped), the survivor lists' lengths read on the device.
 static void shard_reduce(dr_shard& sh, const void* recv_rec, uint64_t n, const void* recv_path, int64_t cutoff,
-                         uint8_t* verdict) {
+                         uint8_t* verdict, bool sync = true) {
   dr_ctx* ctx = sh.ctx;
   hipStream_t stream = ctx->stream;
   std::unique_ptr<dr_state> own(new_state(ctx, nullptr));
@@ -3914,16 +4086,28 @@ static void shard_reduce(dr_shard& sh, const void* recv_rec, uint64_t n, const v
   ActionArrays act{own->kind.p, own->flags.p, own->key.p, own->path_ptr.p, own->path_len.p, own->size.p,
                    own->delts.p, own->src_off.p, own->src_len.p};
   launch_shard_unpack(rec, n, static_cast<const uint8_t*>(recv_path), poff.p, act, stream);
-  reduce_actions(ctx, own.get(), cutoff);
+  sh.red = reduce_launch(ctx, own.get(), cutoff);
   if (n) HIP_OK(hipMemsetAsync(verdict, 0, n, stream));
-  launch_verdict_set(own->live.p, own->n_live, 1, verdict, stream);
-  launch_verdict_set(own->tomb.p, own->n_tomb, 2, verdict, stream);
-  HIP_OK(hipStreamSynchronize(stream));
-  sh.owner = own->counts;
+  // the reducer's totals: [0] live survivors, [2] kept tombstones (the compacted lists' lengths)
+  launch_verdict_set(own->live.p, n, sh.red.totals.p + 0, 1, verdict, stream);
+  launch_verdict_set(own->tomb.p, n, sh.red.totals.p + 2, 2, verdict, stream);
+  sh.own = std::move(own);
+  if (sync) {
+    reduce_queue_readback(ctx, sh.red, 0);
+    HIP_OK(hipStreamSynchronize(stream));
+    reduce_finish(ctx, sh.own.get(), sh.red);
+    sh.owner = sh.own->counts;
+    sh.owner_read = true;
+  }
   sh.reduced = true;
 }
 
-static dr_state* shard_finish(dr_shard& sh, const uint8_t* verdict_back) {
+// Sender side, last step: the returned verdicts select this rank's survivors (its share of allFiles
+// / tombstones). One round trip reads the parse's counters and non-file lines, the survivor counts,
+// the owner side's counters (when shard_reduce did not) and, for the library's RCCL replay, the
+// all-reduced table-wide counters (`sums_dev`, 8 words, copied to `sums`).
+static dr_state* shard_finish(dr_shard& sh, const uint8_t* verdict_back, const int64_t* sums_dev = nullptr,
+                              int64_t* sums = nullptr) {
   dr_ctx* ctx = sh.ctx;
   hipStream_t stream = ctx->stream;
   dr_state& st = *sh.st;
@@ -3934,13 +4118,31 @@ static dr_state* shard_finish(dr_shard& sh, const uint8_t* verdict_back) {
   launch_verdict_flags(verdict_back, n, fl.p, ft.p, stream);
   launch_scan_u32(fl.p, pl.p, n, ss(scratch), stream);
   launch_scan_u32(ft.p, pt.p, n, ss(scratch), stream);
-  st.n_live = d2h_one(pl.p + n, stream);
-  st.n_tomb = d2h_one(pt.p + n, stream);
-  st.live = DBuf<uint32_t>(ctx, st.n_live);
-  st.tomb = DBuf<uint32_t>(ctx, st.n_tomb);
+  st.live = DBuf<uint32_t>(ctx, n);  // bounded by the records sent; the counts come back below
+  st.tomb = DBuf<uint32_t>(ctx, n);
   launch_verdict_collect(verdict_back, sh.send_idx.p, n, 1, pl.p, st.live.p, stream);
   launch_verdict_collect(verdict_back, sh.send_idx.p, n, 2, pt.p, st.tomb.p, stream);
+  size_t at = parse_queue_readback(ctx, sh.parse, 0);
+  uint64_t* h = ctx->pinned();
+  const size_t at_n = at;
+  HIP_OK(hipMemcpyAsync(h + at_n, pl.p + n, 8, hipMemcpyDeviceToHost, stream));
+  HIP_OK(hipMemcpyAsync(h + at_n + 1, pt.p + n, 8, hipMemcpyDeviceToHost, stream));
+  at += 2;
+  if (!sh.owner_read && sh.own) at = reduce_queue_readback(ctx, sh.red, at);
+  const size_t at_sums = at;
+  if (sums_dev) HIP_OK(hipMemcpyAsync(h + at_sums, sums_dev, 8 * sizeof(int64_t), hipMemcpyDeviceToHost, stream));
   HIP_OK(hipStreamSynchronize(stream));
+  if (!parse_finish(ctx, sh.staged, &st, sh.parse, sh.nf))
+    fail(DR_E_INTERNAL, "sharded replay: the canonicalisation arena hint of this segment was too small");
+  st.n_live = h[at_n];
+  st.n_tomb = h[at_n + 1];
+  if (!sh.owner_read && sh.own) {
+    reduce_finish(ctx, sh.own.get(), sh.red);
+    sh.owner = sh.own->counts;
+    sh.owner_read = true;
+  }
+  if (sums) std::memcpy(sums, h + at_sums, 8 * sizeof(int64_t));
+  sh.own.reset();
   // counters: the owner-side partial sums (their sum over ranks is the table's computedState)
   st.counts.num_files = sh.owner.num_files;
   st.counts.size_in_bytes = sh.owner.size_in_bytes;
@@ -4131,24 +4333,34 @@ static void rccl_all_to_all(dr_comm& c, const uint8_t* send, const std::vector<u
   RC_OK(R.group_end());
 }
 
+// Every rank's text, in rank order: one all-gather of fixed slots (length word + bytes) and one
+// read-back; a text longer than the slot costs a second, exactly sized round (every rank sees the
+// same lengths, so all take it together).
 static std::vector<std::string> rccl_all_gather_text(dr_comm& c, const std::string& mine) {
   dr_ctx* ctx = c.ctx;
   hipStream_t stream = ctx->stream;
-  DBuf<uint64_t> len(ctx, 1), lens(ctx, c.world);
-  const uint64_t n = mine.size();
-  HIP_OK(hipMemcpyAsync(len.p, &n, 8, hipMemcpyHostToDevice, stream));
-  comm_all_gather(c, len.p, lens.p, 8);
-  const std::vector<uint64_t> L = d2h(lens.p, c.world, stream);
-  uint64_t mx = 1;
-  for (uint64_t x : L) mx = std::max(mx, x);
-  DBuf<uint8_t> slot(ctx, mx), all(ctx, mx * c.world);
-  if (n) HIP_OK(hipMemcpyAsync(slot.p, mine.data(), n, hipMemcpyHostToDevice, stream));
-  comm_all_gather(c, slot.p, all.p, mx);
-  const std::vector<uint8_t> h = d2h(all.p, mx * c.world, stream);
-  std::vector<std::string> out;
-  for (int32_t p = 0; p < c.world; ++p)
-    out.emplace_back(reinterpret_cast<const char*>(h.data() + uint64_t(p) * mx), L[p]);
-  return out;
+  uint64_t slot = uint64_t(16) << 10;
+  for (int round = 0;; ++round) {
+    std::vector<uint8_t> buf(slot, 0);
+    const uint64_t n = mine.size();
+    std::memcpy(buf.data(), &n, 8);
+    std::memcpy(buf.data() + 8, mine.data(), std::min<uint64_t>(n, slot - 8));
+    DBuf<uint8_t> d(ctx, slot), all(ctx, slot * c.world);
+    HIP_OK(hipMemcpyAsync(d.p, buf.data(), slot, hipMemcpyHostToDevice, stream));
+    comm_all_gather(c, d.p, all.p, slot);
+    const std::vector<uint8_t> h = d2h(all.p, slot * c.world, stream);
+    std::vector<std::string> out;
+    uint64_t mx = 0;
+    for (int32_t p = 0; p < c.world; ++p) {
+      uint64_t L = 0;
+      std::memcpy(&L, h.data() + uint64_t(p) * slot, 8);
+      mx = std::max(mx, L);
+      if (L <= slot - 8) out.emplace_back(reinterpret_cast<const char*>(h.data() + uint64_t(p) * slot + 8), L);
+    }
+    if (mx <= slot - 8) return out;
+    if (round) fail(DR_E_INTERNAL, "non-file text all-gather: lengths changed between rounds");
+    slot = mx + 8;
+  }
 }
 
 // One rank's part of the sharded replay (collective over the communicator; every rank stages its
@@ -4187,9 +4399,10 @@ static dr_state* replay_sharded_rccl(dr_comm& c, const std::shared_ptr<StagedDat
   sh.ctx = ctx;
   sh.staged = staged;
   sh.world = W;
+  // round trip 1: this rank's per-owner record and byte counts (the parse is queued before them)
   std::vector<uint64_t> sc(W), sb(W);
   shard_begin(sh, sc.data(), sb.data());
-  // every rank's send counts and bytes: recv counts are this rank's column
+  // every rank's send counts and bytes: recv counts are this rank's column (round trip 2)
   DBuf<uint64_t> mine(ctx, 2 * W), all(ctx, 2 * uint64_t(W) * W);
   std::vector<uint64_t> m(sc);
   m.insert(m.end(), sb.begin(), sb.end());
@@ -4211,20 +4424,20 @@ static dr_state* replay_sharded_rccl(dr_comm& c, const std::shared_ptr<StagedDat
   DBuf<uint8_t> send_rec(ctx, std::max<uint64_t>(nsend, 1) * sizeof(ShardRec)), send_path(ctx, nsend_b + 1),
       recv_rec(ctx, std::max<uint64_t>(nrecv, 1) * sizeof(ShardRec)), recv_path(ctx, nrecv_b + 1),
       verdict(ctx, nrecv + 1), back(ctx, nsend + 1);
-  shard_pack(sh, send_rec.p, send_path.p);
+  // pack, exchange, reduce, return the verdicts and all-reduce the counters: all queued on the
+  // context's stream (RCCL is stream-ordered), no host round trip
+  shard_pack(sh, send_rec.p, send_path.p, /*sync=*/false);
   rccl_all_to_all(c, send_rec.p, scb, recv_rec.p, rcb);
   rccl_all_to_all(c, send_path.p, sb, recv_path.p, rb);
-  shard_reduce(sh, recv_rec.p, nrecv, recv_path.p, cutoff, verdict.p);
+  shard_reduce(sh, recv_rec.p, nrecv, recv_path.p, cutoff, verdict.p, /*sync=*/false);
   rccl_all_to_all(c, verdict.p, rc, back.p, sc);
-  std::unique_ptr<dr_state> st(shard_finish(sh, back.p));
-  // table-wide counters: the owner-side partial sums over the ranks
-  dr_counts& k = st->counts;
-  const int64_t part[8] = {k.num_files, k.size_in_bytes, k.num_removes, k.num_actions, k.num_file_actions,
-                           k.malformed_lines, int64_t(k.live_key_sum), int64_t(k.tomb_key_sum)};
   DBuf<int64_t> sums(ctx, 8);
-  HIP_OK(hipMemcpyAsync(sums.p, part, sizeof(part), hipMemcpyHostToDevice, stream));
+  launch_shard_partials(sh.red.totals.p, sh.parse.counters.p, int64_t(sh.st->n_actions), sums.p, stream);
   comm_all_reduce_sum_i64(c, sums.p, 8);
-  const std::vector<int64_t> t = d2h(sums.p, 8, stream);
+  // round trip 3: survivors, parse counters, table-wide counters
+  int64_t t[8];
+  std::unique_ptr<dr_state> st(shard_finish(sh, back.p, sums.p, t));
+  dr_counts& k = st->counts;
   k.num_files = t[0];
   k.size_in_bytes = t[1];
   k.num_removes = t[2];
@@ -4233,7 +4446,7 @@ static dr_state* replay_sharded_rccl(dr_comm& c, const std::shared_ptr<StagedDat
   k.malformed_lines = t[5];
   k.live_key_sum = uint64_t(t[6]);
   k.tomb_key_sum = uint64_t(t[7]);
-  // non-file winners: every rank's, in rank order (= replay order: slices are contiguous)
+  // non-file winners: every rank's, in rank order (= replay order: slices are contiguous); round trip 4
   std::string text;
   for (const NonFileAction& a : st->nonfile) text += a.json + "\n";
   std::string lines;
@@ -4334,6 +4547,9 @@ void dr_ctx_destroy(dr_ctx* ctx) {
   ctx->trim();
   for (uint8_t* p : ctx->bounce) (void)hipHostFree(p);
   for (hipEvent_t e : ctx->bounce_ev) (void)hipEventDestroy(e);
+  if (ctx->hpin) (void)hipHostFree(ctx->hpin);
+  ctx->drop_timings();
+  for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(ctx->stream);
   (void)hipStreamDestroy(ctx->stream2);
   delete ctx;

@@ -149,9 +149,13 @@ __device__ __forceinline__ void emit_line(const JsonParseArgs& a, uint64_t line,
       plen = 0;
     }
   } else if (kind == K_METADATA || kind == K_TXN || kind == K_PROTOCOL) {
-    // protocol / metaData / txn: reduced on the host (the reference's single `null` partition)
+    // protocol / metaData / txn: reduced on the host (the reference's single `null` partition); the
+    // line and its byte offset, so the host reads them back once, after the whole replay is queued
     const unsigned long long slot = atomicAdd(reinterpret_cast<unsigned long long*>(a.nonfile_count), 1ull);
-    if (slot < a.nonfile_cap) a.nonfile_idx[slot] = line;
+    if (slot < a.nonfile_cap) {
+      a.nonfile_idx[2 * slot] = line;
+      a.nonfile_idx[2 * slot + 1] = b;
+    }
   } else if (kind == K_ERROR) {
     atomicAdd(reinterpret_cast<unsigned long long*>(a.error_count), 1ull);
   }

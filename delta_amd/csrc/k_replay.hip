@@ -342,11 +342,61 @@ __device__ __forceinline__ void wave_append2(bool f, uint2 v, uint32_t* cnt, uin
 // Packed path reference of action i (written by k_bucket_hist).
 __device__ __forceinline__ uint64_t path_ref(const ReduceArgs& a, uint32_t i) { return a.path_ref[i]; }
 
+// Per-slot loser counts packed two to a word (slot s: word s >> 1, bits 16 (s & 1)): members - 1 of
+// each slot, replaced in place by each slot's first pair position (an exclusive scan over the n
+// slots, n <= TS_MAX, by one RED_T workgroup); returns the total. Counts and positions stay below
+// 2^16 (a sub-pass holds at most 3/4 TS_MAX records), so the halves never carry into each other.
+__device__ uint32_t scan_loser_slots(uint32_t* w, uint32_t n) {
+  __shared__ uint32_t wsum[RED_T / 64];
+  constexpr uint32_t PER = TS_MAX / 2 / RED_T;  // words per thread
+  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint32_t nw = n >> 1;
+  uint32_t v[2 * PER], s = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < PER; ++k) {
+    const uint32_t i = t * PER + k;
+    const uint32_t x = i < nw ? w[i] : 0u;
+    const uint32_t lo = x & 0xffffu, hi = x >> 16;
+    v[2 * k] = lo ? lo - 1u : 0u;
+    v[2 * k + 1] = hi ? hi - 1u : 0u;
+    s += v[2 * k] + v[2 * k + 1];
+  }
+  uint32_t incl = s;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o, 64);
+    if (lane >= uint32_t(o)) incl += y;
+  }
+  if (lane == 63) wsum[wv] = incl;
+  __syncthreads();
+  uint32_t base = 0, total = 0;
+  for (uint32_t q = 0; q < RED_T / 64; ++q) {
+    base += q < wv ? wsum[q] : 0u;
+    total += wsum[q];
+  }
+  uint32_t run = base + incl - s;
+#pragma unroll
+  for (uint32_t k = 0; k < PER; ++k) {
+    const uint32_t i = t * PER + k;
+    const uint32_t lo = run;
+    run += v[2 * k];
+    if (i < nw) w[i] = lo | (run << 16);
+    run += v[2 * k + 1];
+  }
+  __syncthreads();
+  return total;
+}
+
 // K4 main reducer: one workgroup per bucket, LDS-only. Survivors go to the bucket's region of the
-// live / tombstone lists; every loser is paired (by action index) with its winner for k_bucket_verify.
+// live / tombstone lists; every loser is paired (by action index) with its winner for
+// k_bucket_verify, the pairs grouped by winner (a counting sort on the table slot), so the losers of
+// one path sit next to each other and the verifier's lane groups fetch their shared winner once.
+#ifndef DR_PAIR_GROUPED
+#define DR_PAIR_GROUPED 1  // 0: pairs appended in record order (r02)
+#endif
 __global__ void __launch_bounds__(RED_T) k_bucket_reduce(ReduceArgs a) {
   __shared__ uint32_t tkey[TS_MAX];
   __shared__ uint32_t tval[TS_MAX];
+  __shared__ uint32_t tcnt[DR_PAIR_GROUPED ? TS_MAX / 2 : 1];  // u16 per slot: members, then its next pair position
   __shared__ uint32_t nl, nt, np, overflow;
   const uint32_t b = blockIdx.x;
   const uint64_t beg = a.bucket_off[b], end = a.bucket_off[b + 1];
@@ -359,9 +409,12 @@ __global__ void __launch_bounds__(RED_T) k_bucket_reduce(ReduceArgs a) {
   const uint32_t mask = ts - 1;
   if (threadIdx.x == 0) { nl = 0; nt = 0; np = 0; overflow = 0; }
   BucketTotals tot{0, 0, 0, 0, 0};
+  uint32_t pbase = 0;  // pairs of the earlier sub-passes
   for (uint32_t sp = 0; sp < (1u << sbits); ++sp) {
     __syncthreads();
     for (uint32_t s = threadIdx.x; s < ts; s += RED_T) { tkey[s] = 0; tval[s] = 0; }
+    if (DR_PAIR_GROUPED)
+      for (uint32_t s = threadIdx.x; s < ts / 2; s += RED_T) tcnt[s] = 0;
     __syncthreads();
     // insert: table[rkey] = max(meta) -- the largest action index (latest version, line) wins
     for (uint64_t e = beg + threadIdx.x; e < end; e += RED_T) {
@@ -372,12 +425,18 @@ __global__ void __launch_bounds__(RED_T) k_bucket_reduce(ReduceArgs a) {
       for (uint32_t probe = 0;; ++probe) {
         if (probe >= ts) { overflow = 1; break; }
         const uint32_t old = atomicCAS(&tkey[s], 0u, rk);
-        if (old == 0u || old == rk) { atomicMax(&tval[s], r.y + 1u); break; }
+        if (old == 0u || old == rk) {
+          atomicMax(&tval[s], r.y + 1u);
+          if (DR_PAIR_GROUPED) atomicAdd(&tcnt[s >> 1], 1u << (16 * (s & 1)));
+          break;
+        }
         s = (s + 1) & mask;
       }
     }
     __syncthreads();
     if (overflow) break;
+    // losers per slot (members - 1), scanned: each slot's first pair position in this sub-pass
+    const uint32_t npass = DR_PAIR_GROUPED ? scan_loser_slots(tcnt, ts) : 0u;
     // the table holds each key's winning meta, so a loser pairs with its winner's action index
     // directly (no pass to record winner positions)
     for (uint64_t e0 = beg; e0 < end; e0 += RED_T) {
@@ -406,16 +465,24 @@ __global__ void __launch_bounds__(RED_T) k_bucket_reduce(ReduceArgs a) {
               tot.tks += top32_of(b, r.x, a.bucket_bits);
             }
           } else {
-            lose = true;
-            pair = make_uint2(r.y >> 2, w >> 2);
+            if (DR_PAIR_GROUPED) {
+              const uint32_t sh = 16 * (s & 1);
+              const uint32_t at = pbase + ((atomicAdd(&tcnt[s >> 1], 1u << sh) >> sh) & 0xffffu);
+              a.out_pair[beg + at] = make_uint2(r.y >> 2, w >> 2);
+            } else {
+              lose = true;
+              pair = make_uint2(r.y >> 2, w >> 2);
+            }
           }
         }
       }
       wave_append(isl, idx, &nl, a.out_live + beg);
       wave_append(ist, idx, &nt, a.out_tomb + beg);
-      wave_append2(lose, pair, &np, a.out_pair + beg);
+      if (!DR_PAIR_GROUPED) wave_append2(lose, pair, &np, a.out_pair + beg);
     }
+    pbase += npass;
   }
+  if (DR_PAIR_GROUPED && threadIdx.x == 0) np = pbase;
   __syncthreads();
   if (threadIdx.x == 0) {
     a.live_count[b] = nl;
@@ -576,8 +643,9 @@ __device__ void reduce64_bucket(ReduceArgs& a, uint32_t b) {
     if (overflow) break;
     for (uint64_t e0 = beg; e0 < end; e0 += RED_T) {
       const uint64_t e = e0 + threadIdx.x;
-      bool isl = false, ist = false;
+      bool isl = false, ist = false, lose = false;
       uint32_t idx = 0;
+      uint2 pair = make_uint2(0, 0);
       if (e < end) {
         const uint4 r = load_rec(a.rec, e);
         idx = r.y >> 2;

@@ -25,18 +25,60 @@ __device__ __forceinline__ uint32_t owner_of(uint64_t key, uint32_t world) {
   return uint32_t((uint64_t(uint32_t(key)) * world) >> 32);
 }
 
-// per-tile counts per owner, stored owner-major: blk_count[d * ntiles + tile]
+// per-tile counts and canonical path bytes per owner, stored owner-major: blk_count[d * ntiles + tile]
+// (a tile's bytes are stored saturated at 2^32 - 1, which k_shard_sizes reports as an error)
+constexpr uint32_t SH_BYTES_SAT = 0xffffffffu;
 __global__ void __launch_bounds__(SH_T) k_shard_count(ShardArgs a) {
   __shared__ uint32_t h[SH_MAXW];
-  for (int d = threadIdx.x; d < SH_MAXW; d += SH_T) h[d] = 0;
+  __shared__ unsigned long long hb[SH_MAXW];
+  for (int d = threadIdx.x; d < SH_MAXW; d += SH_T) { h[d] = 0; hb[d] = 0; }
   __syncthreads();
   const uint64_t base = uint64_t(blockIdx.x) * SH_TILE;
   for (int k = 0; k < SH_ITEMS; ++k) {
     const uint64_t i = base + uint64_t(k) * SH_T + threadIdx.x;
-    if (i < a.n && shard_sends(a.kind[i], a.flags[i])) atomicAdd(&h[owner_of(a.key[i], a.world)], 1u);
+    if (i < a.n && shard_sends(a.kind[i], a.flags[i])) {
+      const uint32_t d = owner_of(a.key[i], a.world);
+      atomicAdd(&h[d], 1u);
+      atomicAdd(&hb[d], (unsigned long long)a.path_len[i]);
+    }
   }
   __syncthreads();
-  for (uint32_t d = threadIdx.x; d < a.world; d += SH_T) a.blk_count[uint64_t(d) * a.ntiles + blockIdx.x] = h[d];
+  for (uint32_t d = threadIdx.x; d < a.world; d += SH_T) {
+    a.blk_count[uint64_t(d) * a.ntiles + blockIdx.x] = h[d];
+    if (a.blk_bytes) a.blk_bytes[uint64_t(d) * a.ntiles + blockIdx.x] = uint32_t(min(hb[d], (unsigned long long)SH_BYTES_SAT));
+  }
+}
+
+// per-owner send counts and path bytes from the scanned matrices: out[d] records, out[W + d] bytes,
+// out[2W] non-zero when a tile's byte count saturated
+__global__ void __launch_bounds__(256) k_shard_sizes(const uint32_t* blk_bytes, const uint64_t* blk_off,
+                                                     const uint64_t* byte_off, uint32_t world, uint64_t ntiles,
+                                                     uint64_t* out) {
+  const uint32_t d = threadIdx.x;
+  if (d < world) {
+    out[d] = blk_off[uint64_t(d + 1) * ntiles] - blk_off[uint64_t(d) * ntiles];
+    out[world + d] = byte_off[uint64_t(d + 1) * ntiles] - byte_off[uint64_t(d) * ntiles];
+  }
+  bool sat = false;
+  for (uint64_t c = threadIdx.x; c < uint64_t(world) * ntiles; c += blockDim.x) sat |= blk_bytes[c] == SH_BYTES_SAT;
+  sat = __syncthreads_or(sat);
+  if (threadIdx.x == 0) out[2 * world] = sat ? 1 : 0;
+}
+
+// the partial computedState sums one rank contributes to the table-wide all-reduce: from the owner
+// side's reducer totals ([0] live, [1] size, [2] tombstones, [5] / [6] key sums, [7] file actions)
+// and the sender side's parse counters ([3] malformed lines)
+__global__ void k_shard_partials(const unsigned long long* totals, const uint64_t* parse_ctr, int64_t n_actions,
+                                 int64_t* out) {
+  if (threadIdx.x != 0) return;
+  out[0] = int64_t(totals[0]);
+  out[1] = int64_t(totals[1]);
+  out[2] = int64_t(totals[2]);
+  out[3] = n_actions;
+  out[4] = int64_t(totals[7]);
+  out[5] = int64_t(parse_ctr[3]);
+  out[6] = int64_t(totals[5]);
+  out[7] = int64_t(totals[6]);
 }
 
 // stable scatter: slot = blk_off[d * ntiles + tile] + rank of the action among the tile's earlier
@@ -113,9 +155,13 @@ __global__ void k_shard_plen(const ShardRec* rec, uint64_t n, uint32_t* plen) {
   if (j < n) plen[j] = rec[j].plen;
 }
 
-__global__ void k_verdict_set(const uint32_t* idx, uint64_t n, uint8_t v, uint8_t* verdict) {
+// verdict[idx[j]] = v for the first *n_dev (<= n) entries of a survivor list (its length read on the
+// device: no round trip between the reducer and the verdict return)
+__global__ void k_verdict_set(const uint32_t* idx, uint64_t n, const unsigned long long* n_dev, uint8_t v,
+                              uint8_t* verdict) {
   const uint64_t j = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (j < n) verdict[idx[j]] = v;
+  const uint64_t lim = n_dev ? min(uint64_t(*n_dev), n) : n;
+  if (j < lim) verdict[idx[j]] = v;
 }
 
 __global__ void k_verdict_flags(const uint8_t* verdict, uint64_t n, uint32_t* f_live, uint32_t* f_tomb) {
@@ -155,8 +201,17 @@ void launch_shard_unpack(const ShardRec* rec, uint64_t n, const uint8_t* path_ba
                          const ActionArrays& act, hipStream_t st) {
   if (n) DR_LAUNCH(dev::k_shard_unpack, dim3(grid_for(n, 256)), dim3(256), 0, st, rec, n, path_base, poff, act);
 }
-void launch_verdict_set(const uint32_t* idx, uint64_t n, uint8_t v, uint8_t* verdict, hipStream_t st) {
-  if (n) DR_LAUNCH(dev::k_verdict_set, dim3(grid_for(n, 256)), dim3(256), 0, st, idx, n, v, verdict);
+void launch_verdict_set(const uint32_t* idx, uint64_t n, const unsigned long long* n_dev, uint8_t v, uint8_t* verdict,
+                        hipStream_t st) {
+  if (n) DR_LAUNCH(dev::k_verdict_set, dim3(grid_for(n, 256)), dim3(256), 0, st, idx, n, n_dev, v, verdict);
+}
+void launch_shard_sizes(const uint32_t* blk_bytes, const uint64_t* blk_off, const uint64_t* byte_off, uint32_t world,
+                        uint64_t ntiles, uint64_t* out, hipStream_t st) {
+  DR_LAUNCH(dev::k_shard_sizes, dim3(1), dim3(256), 0, st, blk_bytes, blk_off, byte_off, world, ntiles, out);
+}
+void launch_shard_partials(const unsigned long long* totals, const uint64_t* parse_ctr, int64_t n_actions,
+                           int64_t* out, hipStream_t st) {
+  DR_LAUNCH(dev::k_shard_partials, dim3(1), dim3(64), 0, st, totals, parse_ctr, n_actions, out);
 }
 void launch_verdict_flags(const uint8_t* verdict, uint64_t n, uint32_t* f_live, uint32_t* f_tomb, hipStream_t st) {
   if (n) DR_LAUNCH(dev::k_verdict_flags, dim3(grid_for(n, 256)), dim3(256), 0, st, verdict, n, f_live, f_tomb);

@@ -36,11 +36,8 @@ void set_launch_hook(LaunchHook hook, void* user) {
   t_hook = hook;
   t_hook_user = user;
 }
-void launch_begin(const char* kernel, hipStream_t st) {
-  if (t_hook) t_hook(t_hook_user, kernel, st, 0);
-}
-void launch_end(const char* kernel, hipStream_t st) {
-  if (t_hook) t_hook(t_hook_user, kernel, st, 1);
+bool launch_events(const char* kernel, hipEvent_t* start, hipEvent_t* stop) {
+  return t_hook && t_hook(t_hook_user, kernel, start, stop);
 }
 
 void launch_gather_u64(const uint64_t* src, const uint32_t* idx, uint64_t n, uint64_t* dst, hipStream_t st) {

@@ -1,23 +1,28 @@
 // Kernel argument blocks and launchers (host <-> device contract of libdeltareplay).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <cstdint>
 
 namespace dr {
 
 // ---- per-kernel timing hook (dr_set_timing) -------------------------------------------------------
-// Every launcher brackets each kernel it enqueues with launch_begin / launch_end; when a hook is
-// installed (thread-local: one dr_ctx per host thread) the context records a HIP event pair on the
-// kernel's stream, so per-kernel device times are exact and need no profiler.
-typedef void (*LaunchHook)(void* user, const char* kernel, hipStream_t st, int end);
+// Every launcher enqueues through DR_LAUNCH; when a hook is installed (thread-local: one dr_ctx per
+// host thread) and selects the kernel, the launch carries a HIP event pair in its own dispatch, so
+// per-kernel device times are exact and need no profiler.
+// Per-launch timing hook (dr_set_timing): for a launch the hook selects, it hands out an event
+// pair that the launch carries in its own dispatch (hipExtLaunchKernel: the kernel's start and end
+// timestamps, no marker packets between kernels, so the timed steps run as the untimed ones do).
+typedef bool (*LaunchHook)(void* user, const char* kernel, hipEvent_t* start, hipEvent_t* stop);
 void set_launch_hook(LaunchHook hook, void* user);
-void launch_begin(const char* kernel, hipStream_t st);
-void launch_end(const char* kernel, hipStream_t st);
-#define DR_LAUNCH(K, GRID, BLOCK, SHM, ST, ...)                  \
-  do {                                                           \
-    ::dr::launch_begin(#K, ST);                                  \
-    hipLaunchKernelGGL(K, GRID, BLOCK, SHM, ST, __VA_ARGS__);    \
-    ::dr::launch_end(#K, ST);                                    \
+bool launch_events(const char* kernel, hipEvent_t* start, hipEvent_t* stop);
+#define DR_LAUNCH(K, GRID, BLOCK, SHM, ST, ...)                                     \
+  do {                                                                              \
+    hipEvent_t dr_e0_ = nullptr, dr_e1_ = nullptr;                                  \
+    if (::dr::launch_events(#K, &dr_e0_, &dr_e1_))                                  \
+      hipExtLaunchKernelGGL(K, GRID, BLOCK, SHM, ST, dr_e0_, dr_e1_, 0u, __VA_ARGS__); \
+    else                                                                            \
+      hipLaunchKernelGGL(K, GRID, BLOCK, SHM, ST, __VA_ARGS__);                     \
   } while (0)
 
 // Per-action SoA arrays in HBM; action index = checkpoint rows first, then JSON lines (the
@@ -51,8 +56,8 @@ struct JsonParseArgs {
   uint64_t* special_count;
   uint64_t* special_bytes;
   uint64_t* nonfile_count;
-  uint64_t* nonfile_idx;
-  uint64_t nonfile_cap;
+  uint64_t* nonfile_idx;          // {line, byte offset} per protocol / metaData / txn line
+  uint64_t nonfile_cap;           // entries (pairs)
   uint64_t* error_count;
   uint64_t* hard_idx;             // lines the fast walker defers to the General walker
   unsigned long long* hard_count;
@@ -317,6 +322,7 @@ struct ShardArgs {
   const uint64_t* blk_off;   // exclusive scan of blk_count
   uint32_t* send_idx;        // [nsend] local action index of each send slot
   uint64_t nsend;
+  uint32_t* blk_bytes;       // [world * ntiles] canonical path bytes per (owner, tile); may be null
 };
 uint64_t shard_tiles(uint64_t n);
 uint32_t shard_max_world();
@@ -326,7 +332,17 @@ void launch_shard_pack(const ShardArgs& a, ShardRec* rec, uint32_t* plen, hipStr
 void launch_shard_plen(const ShardRec* rec, uint64_t n, uint32_t* plen, hipStream_t st);
 void launch_shard_unpack(const ShardRec* rec, uint64_t n, const uint8_t* path_base, const uint64_t* poff,
                          const ActionArrays& act, hipStream_t st);
-void launch_verdict_set(const uint32_t* idx, uint64_t n, uint8_t v, uint8_t* verdict, hipStream_t st);
+// n_dev: the list's length on the device (<= n), or null for n
+void launch_verdict_set(const uint32_t* idx, uint64_t n, const unsigned long long* n_dev, uint8_t v, uint8_t* verdict,
+                        hipStream_t st);
+// out[d] = records, out[world + d] = path bytes this rank sends to owner d (from the scanned matrices),
+// out[2 world] = 1 when a tile's byte count saturated (more than 4 GiB of paths in one tile)
+void launch_shard_sizes(const uint32_t* blk_bytes, const uint64_t* blk_off, const uint64_t* byte_off, uint32_t world,
+                        uint64_t ntiles, uint64_t* out, hipStream_t st);
+// the 8 partial sums of the table-wide counter all-reduce (num_files, size_in_bytes, num_removes,
+// num_actions, num_file_actions, malformed_lines, live_key_sum, tomb_key_sum)
+void launch_shard_partials(const unsigned long long* totals, const uint64_t* parse_ctr, int64_t n_actions,
+                           int64_t* out, hipStream_t st);
 void launch_verdict_flags(const uint8_t* verdict, uint64_t n, uint32_t* f_live, uint32_t* f_tomb, hipStream_t st);
 void launch_verdict_collect(const uint8_t* verdict, const uint32_t* send_idx, uint64_t n, uint8_t want,
                             const uint64_t* pos, uint32_t* out, hipStream_t st);

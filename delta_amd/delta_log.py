@@ -97,7 +97,7 @@ class Engine:
         ms = (C.c_float * cap)()
         n = C.c_int32()
         self.check(self.lib.dr_last_timings(self.ctx, names, 64 * cap, ms, cap, C.byref(n)))
-        parts = names.raw.split(b"\0")
+        parts = names.raw.split(b"\0", min(n.value, cap))  # only the names written (the bench calls this per timed step)
         out: Dict[str, float] = {}
         for i in range(min(n.value, cap)):
             k = parts[i].decode()
@@ -275,8 +275,20 @@ class State:
         p = C.c_char_p()
         n = C.c_uint64()
         eng.check(eng.lib.dr_state_nonfile_json(handle, C.byref(p), C.byref(n)))
-        text = C.string_at(p, n.value).decode("utf-8") if n.value else ""
-        self.nonfile = [json.loads(l) for l in text.splitlines() if l.strip()]
+        self._nonfile_text = C.string_at(p, n.value) if n.value else b""
+        self._nonfile = None
+
+    @property
+    def nonfile(self) -> List[dict]:
+        """protocol / metaData / txn winners (dr_state_nonfile_json), decoded on first use."""
+        if self._nonfile is None:
+            text = self._nonfile_text.decode("utf-8")
+            self._nonfile = [json.loads(l) for l in text.splitlines() if l.strip()]
+        return self._nonfile
+
+    @nonfile.setter
+    def nonfile(self, v: List[dict]) -> None:
+        self._nonfile = v
 
     def set_nonfile_json(self, lines: str, validate: bool = True) -> None:
         """dr_state_set_nonfile_json: a sharded state's table-wide protocol / metaData / txn winners

@@ -143,6 +143,32 @@ def test_checkpoint_rows_with_absolute_paths(engine, tmp_path):
     assert sorted(t["path"] for t in tomb) == ["file:///abs/one.parquet", "file:///abs/two.parquet"]
 
 
+@pytest.mark.parametrize("hint", ["0", "16", "1000000"])
+def test_canonicalisation_arena_hint(engine, tmp_path, monkeypatch, hint):
+    """A replay queues k_canon with an arena sized from the segment's last need (no read-back before
+    K3); DR_CANON_HINT stands in for that need on the first replay. An arena too small (no arena at
+    all, 16 bytes) is detected after the replay and the replay redone at the exact size; an ample one
+    is used as is. Every case, and a second replay of the same staged segment, equals the oracle."""
+    lp = str(tmp_path / "_delta_log")
+    write_commit(lp, 0, [PROTOCOL, METADATA, add("/abs/one.parquet"), add("file:/abs/two.parquet"),
+                         add("rel/three.parquet")],
+                 raw_lines=['{"add":{"path":"\\/abs\\/four.parquet","size":4,"modificationTime":1,"dataChange":true}}'])
+    write_commit(lp, 1, [remove("file:///abs/one.parquet"), remove("/abs/two.parquet", ts=300)])
+    monkeypatch.setenv("DR_CANON_HINT", hint)
+    snap = O.state_reconstruction(O.get_log_segment(lp), 250)
+    staged = engine.stage_log(lp)
+    try:
+        for _ in range(2):
+            st = staged.replay(250)
+            try:
+                _assert_same(st, snap)
+                assert st.counts["num_files"] == 2 and st.counts["num_removes"] == 1
+            finally:
+                st.release()
+    finally:
+        staged.release()
+
+
 # ---- replay order -----------------------------------------------------------------------------------
 def test_delete_and_readd_in_different_transactions(engine, tmp_path):
     """T/DeltaLogSuite.scala:256-279: add, remove, re-add -> live, dataChange=false."""

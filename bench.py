@@ -354,6 +354,8 @@ def measure_filter(eng, staged, cutoff, exp, steps):
     algo = n * (4 + 4 + 12 + 4 + 4 + 4)
     kname = "k_filter_leaf" if "k_filter_leaf" in ms else "k_filter_typed"
     kt = ms.get(kname)
+    # SURVEY.md §8(d)'s K5 budget: 4 B per predicate column + 1 B flag out per file (4 columns: 17 B)
+    survey = n * (4 * 4 + 1)
     return {"predicate": "p0 >= DATE'2020-03-01' AND p0 < DATE'2020-06-01' AND p1 IN (1..100) AND p2 = 'w17' "
                          "AND p3 = true", "live_files": n, "selected": len(sel),
             "first_call_s": round(first_s, 4), "cache_build_ms": round(first.get("k_pv_extract", 0.0), 4),
@@ -361,7 +363,11 @@ def measure_filter(eng, staged, cutoff, exp, steps):
             "roofline": {"bound": "hbm", "kernel": kname, "avg_launch_ms": round(kt, 4) if kt else None,
                          "algo_bytes": algo, "achieved": round(algo / (kt * 1e-3) / 1e9, 1) if kt else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(algo / (kt * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if kt else None},
+                         "frac": round(algo / (kt * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if kt else None,
+                         "survey_budget_bytes": survey,
+                         "survey_frac": round(survey / (kt * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if kt else None,
+                         "note": "algo_bytes = the typed cache layout this kernel reads (32 B/file); survey_* = "
+                                 "SURVEY.md 8(d)'s 4 B/column + 1 B budget (17 B/file)"},
             "kernels": {k: round(v, 4) for k, v in ms.items()}}
 
 

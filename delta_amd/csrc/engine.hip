@@ -1353,19 +1353,27 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
   // ---- K1a: newline index ----
   const uint64_t json_len = s.h_json.size();
   const uint64_t nbj = json_num_blocks(json_len);
-  DBuf<uint32_t> jcounts(ctx, nbj + 1);
+  const bool one_block = nbj == 1;  // a streamed commit: index, placement and counter reset in one launch
+  DBuf<uint32_t> jcounts(ctx, one_block ? 1 : nbj + 1);
   DBuf<uint64_t> joff(ctx, nbj + 1);
   DBuf<uint8_t> scratch(ctx, scan_scratch_for(nbj));
-  DBuf<uint16_t> jslots(ctx, json_slot_entries(json_len));
-  uint64_t nlines = 0;
-  if (nbj) {
-    launch_json_index(s.d_json.p, json_len, jcounts.p, jslots.p, stream);
-    launch_scan_u32(jcounts.p, joff.p, nbj, ss(scratch), stream);
-    // the line count is known from staging (no read-back between the index and the parse)
-    nlines = s.json_lines;
-    if (std::getenv("DR_CHECK_LINES") && d2h_one(joff.p + nbj, stream) != nlines)
-      fail(DR_E_INTERNAL, "device newline count differs from the staged count");
+  DBuf<uint16_t> jslots(ctx, one_block ? 1 : json_slot_entries(json_len));
+  // the line count is known from staging (no read-back between the index and the parse)
+  const uint64_t nlines = nbj ? s.json_lines : 0;
+  DBuf<uint64_t> nl(ctx, nlines);
+  DBuf<uint64_t> counters(ctx, 8);  // 0 special count, 1 special bytes, 2 nonfile count, 3 errors, 4 canon fill,
+                                     // 5 lines deferred to the General walker, 7 checkpoint decode error
+  if (one_block) {
+    launch_json_index1(s.d_json.p, json_len, nl.p, joff.p, counters.p, 8, stream);
+  } else {
+    counters.zero(stream);
+    if (nbj) {
+      launch_json_index(s.d_json.p, json_len, jcounts.p, jslots.p, stream);
+      launch_scan_u32(jcounts.p, joff.p, nbj, ss(scratch), stream);
+    }
   }
+  if (nbj && std::getenv("DR_CHECK_LINES") && d2h_one(joff.p + nbj, stream) != nlines)
+    fail(DR_E_INTERNAL, "device newline count differs from the staged count");
   const uint64_t R = s.ck_rows, N = R + nlines;
   st->n_actions = N;
   st->kind = DBuf<uint8_t>(ctx, N);
@@ -1377,10 +1385,6 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
   st->delts = DBuf<int64_t>(ctx, N);
   st->src_off = DBuf<uint64_t>(ctx, N);
   st->src_len = DBuf<uint32_t>(ctx, N);
-  DBuf<uint64_t> counters(ctx, 8);  // 0 special count, 1 special bytes, 2 nonfile count, 3 errors, 4 canon fill,
-                                     // 5 lines deferred to the General walker, 7 checkpoint decode error
-  counters.zero(stream);
-  DBuf<uint64_t> nl(ctx, nlines);
   DBuf<uint64_t> nonfile(ctx, 2 * nlines);
   ActionArrays act{st->kind.p, st->flags.p, st->key.p, st->path_ptr.p, st->path_len.p, st->size.p, st->delts.p,
                    st->src_off.p, st->src_len.p};
@@ -1405,7 +1409,7 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
       HIP_OK(hipEventRecord(ov.fork, stream));
       HIP_OK(hipStreamWaitEvent(s2, ov.fork, 0));
     }
-    launch_json_place(s.d_json.p, json_len, jcounts.p, joff.p, jslots.p, nl.p, s2);
+    if (!one_block) launch_json_place(s.d_json.p, json_len, jcounts.p, joff.p, jslots.p, nl.p, s2);
     JsonParseArgs ja{s.d_json.p, nl.p, nlines, R, act.kind, act.flags, act.key, act.path_ptr, act.path_len,
                      act.size, act.delts, act.src_off, act.src_len, counters.p + 0, counters.p + 1, counters.p + 2,
                      nonfile.p, nlines, counters.p + 3, hard.p,
@@ -1473,7 +1477,12 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
     if (hint < 0)
       if (const char* e = std::getenv("DR_CANON_HINT")) hint = std::max<int64_t>(0, std::atoll(e));
     uint64_t cap = 0;
-    if (hint < 0) {  // first replay of the segment: the exact arena from the counters
+    if (hint < 0 && R == 0 && json_len <= (uint64_t(64) << 20)) {
+      // a commit-only segment (an applied tail, a streamed commit): the bound from its bytes -- every
+      // special path is a line's path string, so sum(len + 8) <= bytes + 8 lines -- needs no read-back
+      cap = 2 * json_len + 80 * nlines + 64;
+      pp.canon_sized = true;
+    } else if (hint < 0) {  // first replay of the segment: the exact arena from the counters
       const std::vector<uint64_t> cnt = d2h(counters.p, 2, stream);
       cap = cnt[0] ? cnt[1] * 2 + 64 * cnt[0] + 64 : 0;
       pp.canon_sized = true;
@@ -1797,24 +1806,19 @@ static void gather_survivors(dr_ctx* ctx, dr_state& base, const ActionDst& d) {
   else HIP_OK(hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(d.src_id), 0, M, stream));
 }
 
-// Appends src's T actions at dst offset `at`, all from source `sid`.
+// Appends src's T actions at dst offset `at`, all from source `sid` (one launch).
 static void append_actions(dr_ctx* ctx, const ActionDst& d, uint64_t at, dr_state& src, uint16_t sid) {
-  hipStream_t stream = ctx->stream;
   const uint64_t T = src.n_actions;
   if (!T) return;
-  auto cp = [&](void* dst, const void* s, size_t bytes) {
-    HIP_OK(hipMemcpyAsync(dst, s, bytes, hipMemcpyDeviceToDevice, stream));
-  };
-  cp(d.kind + at, src.kind.p, T);
-  cp(d.flags + at, src.flags.p, T);
-  cp(d.key + at, src.key.p, T * 8);
-  cp(d.path_ptr + at, src.path_ptr.p, T * 8);
-  cp(d.path_len + at, src.path_len.p, T * 4);
-  cp(d.size + at, src.size.p, T * 8);
-  cp(d.delts + at, src.delts.p, T * 8);
-  cp(d.src_off + at, src.src_off.p, T * 8);
-  cp(d.src_len + at, src.src_len.p, T * 4);
-  HIP_OK(hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(d.src_id + at), sid, T, stream));
+  AppendArgs a{};
+  a.src = ActionArrays{src.kind.p, src.flags.p, src.key.p, src.path_ptr.p, src.path_len.p, src.size.p, src.delts.p,
+                       src.src_off.p, src.src_len.p};
+  a.dst = ActionArrays{d.kind + at, d.flags + at, d.key + at, d.path_ptr + at, d.path_len + at, d.size + at,
+                       d.delts + at, d.src_off + at, d.src_len + at};
+  a.src_id = d.src_id + at;
+  a.n = T;
+  a.sid = sid;
+  launch_append_actions(a, ctx->stream);
 }
 
 static ActionDst chain_dst(IncChain& c) {
@@ -1917,7 +1921,8 @@ static std::shared_ptr<IncChain> chain_from(dr_ctx* ctx, dr_state& base, uint64_
 // tail's actions are appended to the store and only their keys are probed. nullptr (the index
 // restored) when a 64-bit key collision needs the full reduction.
 static dr_state* apply_incremental(dr_ctx* ctx, dr_state& base, const std::shared_ptr<IncChain>& ch, dr_state& t,
-                                   const std::shared_ptr<StagedData>& tail, int64_t cutoff, int64_t version) {
+                                   const std::shared_ptr<StagedData>& tail, int64_t cutoff, int64_t version,
+                                   ParsePending& pp, std::vector<NonFileAction>& nf) {
   hipStream_t stream = ctx->stream;
   IncChain& c = *ch;
   const uint64_t T = t.n_actions, lo = c.n;
@@ -1942,7 +1947,13 @@ static dr_state* apply_incremental(dr_ctx* ctx, dr_state& base, const std::share
   launch_ix_touch(a, stream);
   launch_ix_delta(a, stream);
   if (cutoff > base.cutoff) launch_ix_expire(a, c.tomb_n, stream);
-  const std::vector<unsigned long long> ctr = d2h(c.ctr.p, IX_C_N, stream);
+  // one round trip: the tail's parse counters and non-file lines with the index counters
+  const size_t at = parse_queue_readback(ctx, pp, 0);
+  HIP_OK(hipMemcpyAsync(ctx->pinned() + at, c.ctr.p, IX_C_N * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                        stream));
+  HIP_OK(hipStreamSynchronize(stream));
+  std::vector<unsigned long long> ctr(ctx->pinned() + at, ctx->pinned() + at + IX_C_N);
+  if (!parse_finish(ctx, tail, &t, pp, nf)) fail(DR_E_INTERNAL, "applied tail: canonicalisation arena too small");
   c.used += ctr[IX_C_NEW_SLOTS];
   // (DR_IX_TEST_COLLIDE: test hook for the rollback)
   if (ctr[IX_C_COLLIDE] || std::getenv("DR_IX_TEST_COLLIDE")) {  // undo this apply's first touches: the head is the base again
@@ -2025,27 +2036,41 @@ static dr_state* apply_tail(dr_ctx* ctx, dr_state& base, const std::shared_ptr<S
   const int64_t version = check_tail(base, tail, cutoff);
   std::unique_ptr<dr_state> t(new_state(ctx, tail));
   std::vector<NonFileAction> nf;
-  parse_actions(ctx, tail, t.get(), nf);
+  // the tail's parse is queued; the incremental path reads its counters back with the index's
+  ParsePending pp = parse_launch(ctx, tail, t.get(), true);
+  bool parsed = false;
   // protocol / metaData / txn: the base's winners first, then the tail's actions in order
-  std::vector<NonFileAction> all = base.nonfile;
-  for (size_t k = 0; k < all.size(); ++k) all[k].order = k;
-  for (NonFileAction& a : nf) {
-    a.order += all.size();
-    all.push_back(std::move(a));
-  }
+  auto all_nonfile = [&] {
+    std::vector<NonFileAction> all = base.nonfile;
+    for (size_t k = 0; k < all.size(); ++k) all[k].order = k;
+    for (NonFileAction& a : nf) {
+      a.order += all.size();
+      all.push_back(a);
+    }
+    return all;
+  };
   const bool forced = (flags & (DR_FLAG_EXACT_REDUCE | DR_FLAG_REDUCE64)) || std::getenv("DR_APPLY_FULL");
   if (!forced) {
     std::shared_ptr<IncChain> ch;
     if (base.chain && base.gen == base.chain->head) ch = base.chain;
     else if (!base.chain) ch = chain_from(ctx, base, std::max<uint64_t>(t->n_actions, 1024));
     if (ch) {
-      if (dr_state* r0 = apply_incremental(ctx, base, ch, *t, tail, cutoff, version)) {
+      dr_state* r0 = apply_incremental(ctx, base, ch, *t, tail, cutoff, version, pp, nf);
+      parsed = true;
+      if (r0) {
         std::unique_ptr<dr_state> r(r0);
+        std::vector<NonFileAction> all = all_nonfile();
         reduce_nonfile(*r, all, !(flags & DR_FLAG_NO_VALIDATION));
         return r.release();
       }
     }
   }
+  if (!parsed) {
+    parse_queue_readback(ctx, pp, 0);
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+    if (!parse_finish(ctx, tail, t.get(), pp, nf)) fail(DR_E_INTERNAL, "applied tail: canonicalisation arena too small");
+  }
+  std::vector<NonFileAction> all = all_nonfile();
   ensure_ready(base);
   hipStream_t stream = ctx->stream;
   const uint64_t M = base.n_live + base.n_tomb, T = t->n_actions, N = M + T;

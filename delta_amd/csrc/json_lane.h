@@ -73,7 +73,8 @@ struct Win {
 
 // Byte classes by two 16-entry nibble tables (class = HI[x >> 4] & LO[x & 15], zero for x >= 0x80),
 // looked up four bytes at a time with v_perm_b32: bit 0 '"', bit 1 '\\', bit 2 one of {}[], bit 3
-// ':', bit 4 ',', bit 5 ' ', bit 6 a control byte < 0x20.
+// ' ', bit 4 ':', bit 5 ',', bit 6 a control byte < 0x20. Each class is a product set (high
+// nibbles x low nibbles), so the AND of the two lookups has no cross terms.
 JL_HD uint32_t perm_b32(uint32_t s0, uint32_t s1, uint32_t sel) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return __builtin_amdgcn_perm(s0, s1, sel);
@@ -87,8 +88,8 @@ JL_HD uint32_t perm_b32(uint32_t s0, uint32_t s1, uint32_t sel) {
   return r;
 #endif
 }
-constexpr uint32_t CLS_LO0 = 0x40414060u, CLS_LO1 = 0x40404040u, CLS_LO2 = 0x44484040u, CLS_LO3 = 0x40404452u;
-constexpr uint32_t CLS_HI0 = 0x08314040u, CLS_HI1 = 0x04000600u;
+constexpr uint32_t CLS_LO0 = 0x40414048u, CLS_LO1 = 0x40404040u, CLS_LO2 = 0x44504040u, CLS_LO3 = 0x40404462u;
+constexpr uint32_t CLS_HI0 = 0x10294040u, CLS_HI1 = 0x04000600u;
 JL_HD uint32_t class_bytes(uint32_t x) {
   const uint32_t lo = x & 0x0F0F0F0Fu;
   const uint32_t sel = lo & 0x07070707u;
@@ -105,20 +106,39 @@ JL_HD uint32_t gather_bit(uint32_t r, int c) {  // bit c of each byte -> 4-bit m
   m |= m >> 14;
   return m & 0xFu;
 }
+// Exchanges the bits at positions p and p + delta wherever `mask` has p (a swap of two bit-index
+// bits of the word).
+JL_HD uint32_t delta_swap(uint32_t y, uint32_t delta, uint32_t mask) {
+  const uint32_t t = (y ^ (y >> delta)) & mask;
+  return y ^ t ^ (t << delta);
+}
 
+// The window's 16-bit masks from its four class dwords without a per-class bit gather: each byte's
+// four tokenizer classes (quote, backslash, structural = {}[]:, , space) as a nibble; two dwords'
+// nibbles share a word (byte j: byte j of the first, byte 4 + j of the second in the high nibble),
+// so word g holds bit 8j + 4h + c for class c of window byte 8g + 4h + j; exchanging the index
+// fields j and c (two delta swaps) makes byte c of word g the class-c mask of bytes 8g..8g+7, and
+// two byte permutes assemble the four masks. Control bytes (rare) take the per-class gather.
 JL_HD void classify(const uint32_t w[4], Win& m) {
-  m.q = m.bs = m.st = m.sp = m.ctrl = 0;
+  uint32_t r[4], nib[4];
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
 #endif
   for (int d = 0; d < 4; ++d) {
-    const uint32_t r = class_bytes(w[d]);
-    m.q |= gather_bit(r, 0) << (4 * d);
-    m.bs |= gather_bit(r, 1) << (4 * d);
-    m.st |= gather_bit(r | (r >> 1) | (r >> 2), 2) << (4 * d);
-    m.sp |= gather_bit(r, 5) << (4 * d);
-    m.ctrl |= gather_bit(r, 6) << (4 * d);
+    r[d] = class_bytes(w[d]);
+    nib[d] = (r[d] & 0x0F0F0F0Fu) | (((r[d] >> 2) | (r[d] >> 3)) & 0x04040404u);
   }
+  uint32_t y0 = nib[0] | (nib[1] << 4), y1 = nib[2] | (nib[3] << 4);
+  y0 = delta_swap(delta_swap(y0, 7, 0x00AA00AAu), 14, 0x0000CCCCu);
+  y1 = delta_swap(delta_swap(y1, 7, 0x00AA00AAu), 14, 0x0000CCCCu);
+  const uint32_t qb = perm_b32(y1, y0, 0x05010400u), ss = perm_b32(y1, y0, 0x07030602u);
+  m.q = qb & 0xFFFFu;
+  m.bs = qb >> 16;
+  m.st = ss & 0xFFFFu;
+  m.sp = ss >> 16;
+  m.ctrl = 0;
+  if ((r[0] | r[1] | r[2] | r[3]) & 0x40404040u)
+    for (int d = 0; d < 4; ++d) m.ctrl |= gather_bit(r[d], 6) << (4 * d);
 }
 
 JL_HD uint32_t win_byte(const uint32_t w[4], uint32_t k) {
@@ -373,31 +393,39 @@ JL_HD void tokenize_window(const uint8_t* p, uint32_t n, const uint32_t w[4], in
   const uint32_t sc_begin = sc & ~(((sc << 1) | tz.sc_carry) & 0xFFFFu);
   const uint32_t sc_end = sc & ~(sc >> 1) & 0x7FFFu;  // run ends inside this window
   tz.sc_carry = (sc >> 15) & 1u;
-  uint32_t tok = st | quote | sc_end;
-  uint32_t open_k = 0xFFFFFFFFu;
+  // Opening quotes take no loop step: a closing quote finds its string's opening quote as the highest
+  // opening-quote bit below it (or the one carried from an earlier window), so only closing quotes,
+  // structurals and scalar ends are visited (about two thirds of the steps of a writer's add line).
+  const uint32_t oq_all = quote & instr;
+  uint32_t tok = st | (quote & ~instr) | sc_end;
+#if defined(DR_JL_EXP) && DR_JL_EXP >= 2
+  tok = 0;  // timing experiment only (scripts/build_variant.sh): masks without token emission
+#endif
   uint32_t begins = sc_begin;
   while (tok) {
     const uint32_t k = ctz32(tok);
     tok &= tok - 1;
     const uint32_t off = uint32_t(lo + int32_t(k));
     const uint32_t bit = 1u << k;
-    if (quote & bit) {
-      if (instr & bit) {
-        open_k = k;
-        tz.pend_bs = 0;
-        tz.str_open = off;
+    if (quote & bit) {  // a closing quote
+      const uint32_t below = bit - 1u;
+      const uint32_t oq = oq_all & below;
+      uint32_t open_off;
+      bool has_bs;
+      if (oq) {
+        const uint32_t ok = 31u - uint32_t(__builtin_clz(oq));
+        open_off = uint32_t(lo + int32_t(ok));
+        has_bs = (m.bs & below & ~((2u << ok) - 1u)) != 0;
       } else {
-        const uint32_t below = bit - 1u;
-        const bool has_bs = open_k != 0xFFFFFFFFu ? (m.bs & below & ~((2u << open_k) - 1u)) != 0
-                                                  : (tz.pend_bs || (m.bs & below) != 0);
-        open_k = 0xFFFFFFFFu;
-        const uint32_t len = off - tz.str_open - 1u;
-        if (len < 4096u) {
-          emit(tok_make(tz.str_open, len, has_bs ? T_STRING_ESC : T_STRING));
-        } else {
-          emit(tok_make(tz.str_open, 0, T_STR_OPEN));
-          emit(tok_make(off, 0, has_bs ? T_STR_CLOSE_ESC : T_STR_CLOSE));
-        }
+        open_off = tz.str_open;
+        has_bs = tz.pend_bs || (m.bs & below) != 0;
+      }
+      const uint32_t len = off - open_off - 1u;
+      if (len < 4096u) {
+        emit(tok_make(open_off, len, has_bs ? T_STRING_ESC : T_STRING));
+      } else {
+        emit(tok_make(open_off, 0, T_STR_OPEN));
+        emit(tok_make(off, 0, has_bs ? T_STR_CLOSE_ESC : T_STR_CLOSE));
       }
     } else if (st & bit) {
       const uint32_t c = win_byte(w, k);
@@ -419,10 +447,15 @@ JL_HD void tokenize_window(const uint8_t* p, uint32_t n, const uint32_t w[4], in
     }
   }
   if (begins) tz.sc_start = uint32_t(lo + int32_t(ctz32(begins)));  // a run that continues
-  // a string still open at the window end: remember whether it held a backslash
+  // a string still open at the window end: where it opened, and whether it holds a backslash yet
   if (tz.in_str) {
-    const uint32_t from = open_k != 0xFFFFFFFFu ? (m.bs & ~((2u << open_k) - 1u)) : m.bs;
-    tz.pend_bs = tz.pend_bs | (from != 0);
+    if (oq_all) {
+      const uint32_t ok = 31u - uint32_t(__builtin_clz(oq_all));
+      tz.str_open = uint32_t(lo + int32_t(ok));
+      tz.pend_bs = (m.bs & ~((2u << ok) - 1u)) != 0;
+    } else {
+      tz.pend_bs = tz.pend_bs || m.bs != 0;
+    }
   }
 }
 

@@ -115,9 +115,7 @@ __global__ void __launch_bounds__(IX_T) k_ix_build(IndexArgs a) {
 }
 
 // Pass 1 of an apply: every file action of the tail claims its slot and raises it to itself.
-__global__ void __launch_bounds__(IX_T) k_ix_touch(IndexArgs a) {
-  const uint64_t i = a.lo + uint64_t(blockIdx.x) * IX_T + threadIdx.x;
-  if (i >= a.hi) return;
+__device__ __forceinline__ void ix_touch_one(const IndexArgs& a, uint64_t i) {
   const uint64_t t = i - a.lo;
   if (!ix_file_action(a, i)) {
     a.t_slot[t] = IX_NONE;
@@ -129,35 +127,54 @@ __global__ void __launch_bounds__(IX_T) k_ix_touch(IndexArgs a) {
   a.t_slot[t] = s;
   a.t_prev[t] = atomicMax(a.vals + s, uint32_t(i + 1));
 }
+__global__ void __launch_bounds__(IX_T) k_ix_touch(IndexArgs a) {
+  const uint64_t i = a.lo + uint64_t(blockIdx.x) * IX_T + threadIdx.x;
+  if (i < a.hi) ix_touch_one(a, i);
+}
 
 // Pass 2: the first toucher of each slot (the one whose atomicMax saw a pre-tail value) moves the
 // counters from the old winner to the final one and logs the old value for older states; every
 // action checks its bytes against the final winner (and the first toucher against the old one).
+__device__ __forceinline__ void ix_delta_one(const IndexArgs& a, uint64_t i, Contrib& c, unsigned long long& files) {
+  const uint64_t t = i - a.lo;
+  const uint32_t s = a.t_slot[t];
+  if (s == IX_NONE) return;
+  files = 1;
+  // an atomic load: in k_ix_touch_delta the slot was raised by this workgroup's atomics (at L2)
+  const uint64_t w = uint64_t(__hip_atomic_load(a.vals + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) - 1;
+  if (w != i && !ix_same_path(a, i, w)) atomicOr(a.ctr + IX_C_COLLIDE, 1ull);
+  const uint32_t prev = a.t_prev[t];
+  if (uint64_t(prev) <= a.lo) {
+    if (prev) {
+      const uint64_t o = uint64_t(prev) - 1;
+      if (!ix_same_path(a, i, o)) atomicOr(a.ctr + IX_C_COLLIDE, 1ull);
+      contrib_add(c, a, o, a.old_cut, true);
+    }
+    contrib_add(c, a, w, a.new_cut, false);
+    if (a.kind[w] == K_REMOVE && ix_delts(a, w) > a.new_cut) tomb_append(a, w);
+    const unsigned long long u = atomicAdd(a.ctr + IX_C_UNDO_FILL, 1ull);
+    a.undo[u] = make_uint2(uint32_t(i), prev);
+  }
+}
 __global__ void __launch_bounds__(IX_T) k_ix_delta(IndexArgs a) {
   const uint64_t i = a.lo + uint64_t(blockIdx.x) * IX_T + threadIdx.x;
   Contrib c{0, 0, 0, 0, 0};
   unsigned long long files = 0;
-  if (i < a.hi) {
-    const uint64_t t = i - a.lo;
-    const uint32_t s = a.t_slot[t];
-    if (s != IX_NONE) {
-      files = 1;
-      const uint64_t w = uint64_t(a.vals[s]) - 1;
-      if (w != i && !ix_same_path(a, i, w)) atomicOr(a.ctr + IX_C_COLLIDE, 1ull);
-      const uint32_t prev = a.t_prev[t];
-      if (uint64_t(prev) <= a.lo) {
-        if (prev) {
-          const uint64_t o = uint64_t(prev) - 1;
-          if (!ix_same_path(a, i, o)) atomicOr(a.ctr + IX_C_COLLIDE, 1ull);
-          contrib_add(c, a, o, a.old_cut, true);
-        }
-        contrib_add(c, a, w, a.new_cut, false);
-        if (a.kind[w] == K_REMOVE && ix_delts(a, w) > a.new_cut) tomb_append(a, w);
-        const unsigned long long u = atomicAdd(a.ctr + IX_C_UNDO_FILL, 1ull);
-        a.undo[u] = make_uint2(uint32_t(i), prev);
-      }
-    }
-  }
+  if (i < a.hi) ix_delta_one(a, i, c, files);
+  flush_contrib(a, c, files);
+}
+
+// Both passes for a tail of at most IX_T actions (a streamed commit): one workgroup, the passes
+// separated by a barrier (the slots' atomicMax results are device-scope atomics, complete and
+// visible to the workgroup after the fence and the barrier).
+__global__ void __launch_bounds__(IX_T) k_ix_touch_delta(IndexArgs a) {
+  const uint64_t i = a.lo + threadIdx.x;
+  if (i < a.hi) ix_touch_one(a, i);
+  __threadfence();
+  __syncthreads();
+  Contrib c{0, 0, 0, 0, 0};
+  unsigned long long files = 0;
+  if (i < a.hi) ix_delta_one(a, i, c, files);
   flush_contrib(a, c, files);
 }
 
@@ -245,10 +262,13 @@ void launch_ix_build(const IndexArgs& a, hipStream_t st) {
   if (a.hi > a.lo) DR_LAUNCH(dev::k_ix_build, dim3(ix_grid(a.hi - a.lo)), dim3(dev::IX_T), 0, st, a);
 }
 void launch_ix_touch(const IndexArgs& a, hipStream_t st) {
+  if (a.hi - a.lo <= uint64_t(dev::IX_T)) return;  // launch_ix_delta runs both passes in one workgroup
   if (a.hi > a.lo) DR_LAUNCH(dev::k_ix_touch, dim3(ix_grid(a.hi - a.lo)), dim3(dev::IX_T), 0, st, a);
 }
 void launch_ix_delta(const IndexArgs& a, hipStream_t st) {
-  if (a.hi > a.lo) DR_LAUNCH(dev::k_ix_delta, dim3(ix_grid(a.hi - a.lo)), dim3(dev::IX_T), 0, st, a);
+  if (a.hi <= a.lo) return;
+  if (a.hi - a.lo <= uint64_t(dev::IX_T)) DR_LAUNCH(dev::k_ix_touch_delta, dim3(1), dim3(dev::IX_T), 0, st, a);
+  else DR_LAUNCH(dev::k_ix_delta, dim3(ix_grid(a.hi - a.lo)), dim3(dev::IX_T), 0, st, a);
 }
 void launch_ix_expire(const IndexArgs& a, uint64_t n, hipStream_t st) {
   if (n) DR_LAUNCH(dev::k_ix_expire, dim3(ix_grid(n)), dim3(dev::IX_T), 0, st, a, n);

@@ -100,6 +100,20 @@ __global__ void __launch_bounds__(JSON_THREADS) k_json_index(const uint8_t* __re
   if (threadIdx.x == 0) block_counts[blockIdx.x] = total;
 }
 
+// A segment of one index block (a streamed commit): the newline positions written directly (no
+// slots, no scan, no k_json_place), off2 = {0, count}, and the first nzero words of `zero` cleared
+// (the parse counters: one launch instead of a fill, an index, three scans and a placement).
+__global__ void __launch_bounds__(JSON_THREADS) k_json_index1(const uint8_t* __restrict__ buf, uint64_t len,
+                                                             uint64_t* __restrict__ nl, uint64_t* __restrict__ off2,
+                                                             uint64_t* __restrict__ zero, uint32_t nzero) {
+  if (threadIdx.x < nzero) zero[threadIdx.x] = 0;
+  const uint32_t total = block_newlines(buf, len, 0, [&](uint32_t r, uint32_t pos) { nl[r] = pos; });
+  if (threadIdx.x == 0) {
+    off2[0] = 0;
+    off2[1] = total;
+  }
+}
+
 // Writes the byte position of every newline, in order: nl[block_off[b] + rank] = pos.
 __global__ void __launch_bounds__(JSON_THREADS) k_json_place(const uint8_t* __restrict__ buf, uint64_t len,
                                                             const uint32_t* __restrict__ block_counts,
@@ -189,8 +203,18 @@ constexpr int JL_FLUSH = JL_TOKCAP - 16;  // a window adds at most 16 tokens
 #ifndef DR_JL_WAVES
 #define DR_JL_WAVES 1
 #endif
+// Small segments (a streamed commit: at most JL_SMALL_LINES lines) take the staged walker: each
+// wave copies its lines' byte region into LDS with coalesced 16-byte loads and every lane walks its
+// line from LDS, so the walk's dependent reads cost LDS latency instead of a global round trip each
+// (one wave of a commit has no other waves to hide them behind); lines the fast walker defers are
+// re-parsed in place by the General walker (no k_json_hard launch). For the bulk segment the stage
+// halves occupancy and loses (r03: 8.2 vs 2.79 ms), so it keeps the global walker.
+constexpr uint32_t JL_SMALL_LINES = 256;
+constexpr uint32_t JL_STAGE_BYTES = 24u * 1024u;
+
 // One lane's line walk: tokenize window by window into the LDS token buffer, the DFA by token index
 // (see below); `p` is the line's first byte wherever it is read from (LDS or global).
+template <bool InlineHard = false>
 __device__ __forceinline__ void walk_line(const JsonParseArgs& a, uint32_t* tokbuf, uint32_t lane, uint64_t line,
                                           bool live, uint64_t b, uint32_t n, const uint8_t* p) {
   jl::Tokenizer tz;
@@ -233,8 +257,10 @@ __device__ __forceinline__ void walk_line(const JsonParseArgs& a, uint32_t* tokb
     if (!anymore || __ballot(nt > uint32_t(JL_FLUSH)) != 0ull) {
       uint32_t mx = nt;
       for (int o = 32; o > 0; o >>= 1) mx = max(mx, uint32_t(__shfl_xor(int(mx), o, 64)));
+#if !defined(DR_JL_EXP)  // DR_JL_EXP: timing experiments only (scripts/build_variant.sh), no DFA
       for (uint32_t t = 0; t < mx; ++t)
         if (t < nt && d.status == jl::ST_OK) jl::dfa_token<false>(p, tokbuf[t * JL_T + lane], d);
+#endif
       nt = 0;
     }
     if (!anymore) break;
@@ -243,8 +269,14 @@ __device__ __forceinline__ void walk_line(const JsonParseArgs& a, uint32_t* tokb
   jl::LineOut o;
   jl::dfa_finish<false>(tz, d, o);
   if (o.hard) {
-    const unsigned long long k = atomicAdd(a.hard_count, 1ull);
-    a.hard_idx[k] = line;
+    if constexpr (InlineHard) {
+      const uint8_t* gp = a.buf + b;
+      jl::parse_line_general(gp, n, o);
+      emit_line(a, line, b, n, gp, gp, o);
+    } else {
+      const unsigned long long k = atomicAdd(a.hard_count, 1ull);
+      a.hard_idx[k] = line;
+    }
     return;
   }
   emit_line(a, line, b, n, p, a.buf + b, o);
@@ -257,13 +289,33 @@ __device__ __forceinline__ void walk_line(const JsonParseArgs& a, uint32_t* tokb
 //     or all removes), so the 64 lanes take the same grammar branch at the same step instead of
 //     diverging byte by byte.
 // The buffer is flushed through phase 2 whenever a lane could overflow it, and at the end.
+template <bool Stage>
 __global__ void __launch_bounds__(JL_T, DR_JL_WAVES) k_json_lines(JsonParseArgs a) {
   __shared__ uint32_t tokbuf[JL_TOKCAP * JL_T];
+  __shared__ uint4 stage[Stage ? JL_STAGE_BYTES / 16 : 1];
   const uint32_t lane = threadIdx.x;
   const uint64_t line = uint64_t(blockIdx.x) * JL_T + lane;
   const bool live = line < a.nlines;
   const uint64_t b = !live ? 0 : line == 0 ? 0 : a.nl[line - 1] + 1;
   const uint32_t n = live ? uint32_t(a.nl[line] - b) : 0;
+  if constexpr (Stage) {
+    // the wave's region: [its first line's 16-byte block, its last line's end rounded up to 16);
+    // the JSON buffer's 64-byte zero pad keeps the rounded end readable
+    const uint64_t first = uint64_t(blockIdx.x) * JL_T;
+    const uint64_t last = min(first + JL_T, a.nlines) - 1;
+    const uint64_t r0 = (first == 0 ? 0 : a.nl[first - 1] + 1) & ~uint64_t(15);
+    const uint64_t r1 = (a.nl[last] + 16) & ~uint64_t(15);
+    if (r1 - r0 + 48 <= JL_STAGE_BYTES) {  // + the walker's reads past a line end (load20, pairs)
+      const uint4* src = reinterpret_cast<const uint4*>(a.buf + r0);
+      const uint32_t nq = uint32_t((r1 - r0) >> 4) + 3;
+      for (uint32_t k = lane; k < nq; k += JL_T) stage[k] = src[k];
+      __syncthreads();
+      walk_line<true>(a, tokbuf, lane, line, live, b, n, reinterpret_cast<const uint8_t*>(stage) + (b - r0));
+      return;
+    }
+    walk_line<true>(a, tokbuf, lane, line, live, b, n, a.buf + b);
+    return;
+  }
   walk_line(a, tokbuf, lane, line, live, b, n, a.buf + b);
 }
 
@@ -302,13 +354,20 @@ void launch_json_place(const uint8_t* buf, uint64_t len, const uint32_t* block_c
                              block_counts, block_off, slots, nl);
 }
 
+void launch_json_index1(const uint8_t* buf, uint64_t len, uint64_t* nl, uint64_t* off2, uint64_t* zero,
+                        uint32_t nzero, hipStream_t st) {
+  DR_LAUNCH(dev::k_json_index1, dim3(1), dim3(dev::JSON_THREADS), 0, st, buf, len, nl, off2, zero, nzero);
+}
+
 void launch_json_parse(const JsonParseArgs& a, hipStream_t st) {
   if (!a.nlines) return;
-  DR_LAUNCH(dev::k_json_lines, dim3(unsigned((a.nlines + dev::JL_T - 1) / dev::JL_T)), dim3(dev::JL_T), 0, st, a);
+  const dim3 grid(unsigned((a.nlines + dev::JL_T - 1) / dev::JL_T));
+  if (a.nlines <= dev::JL_SMALL_LINES) DR_LAUNCH(dev::k_json_lines<true>, grid, dim3(dev::JL_T), 0, st, a);
+  else DR_LAUNCH(dev::k_json_lines<false>, grid, dim3(dev::JL_T), 0, st, a);
 }
 
 void launch_json_hard(const JsonParseArgs& a, hipStream_t st) {
-  if (!a.nlines) return;
+  if (!a.nlines || a.nlines <= dev::JL_SMALL_LINES) return;  // the staged walker re-parsed them in place
   DR_LAUNCH(dev::k_json_hard, dim3(256), dim3(64), 0, st, a);
 }
 

@@ -26,6 +26,24 @@ __global__ void k_gather_bytes(const uint64_t* __restrict__ ptr, const uint32_t*
   for (uint32_t k = threadIdx.x & 63; k < len[s]; k += 64) o[k] = p[k];
 }
 
+// One action per thread from src[i] to dst[i] across the nine action arrays, src_id[i] = sid: an
+// applied tail's actions appended to the chain store in one launch (instead of nine copies and a
+// fill, each a dispatch of its own on the per-commit path).
+__global__ void __launch_bounds__(256) k_append_actions(AppendArgs a) {
+  const uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  a.dst.kind[i] = a.src.kind[i];
+  a.dst.flags[i] = a.src.flags[i];
+  a.dst.key[i] = a.src.key[i];
+  a.dst.path_ptr[i] = a.src.path_ptr[i];
+  a.dst.path_len[i] = a.src.path_len[i];
+  a.dst.size[i] = a.src.size[i];
+  a.dst.delts[i] = a.src.delts[i];
+  a.dst.src_off[i] = a.src.src_off[i];
+  a.dst.src_len[i] = a.src.src_len[i];
+  a.src_id[i] = a.sid;
+}
+
 }  // namespace dev
 
 namespace {
@@ -61,6 +79,10 @@ void launch_gather_u64_by64(const uint64_t* src, const uint64_t* idx, uint64_t n
 void launch_gather_bytes(const uint64_t* ptr, const uint32_t* len, const uint64_t* off, uint64_t n, uint8_t* out,
                          hipStream_t st) {
   if (n) DR_LAUNCH(dev::k_gather_bytes, dim3(unsigned((n + 3) / 4)), dim3(256), 0, st, ptr, len, off, n, out);
+}
+
+void launch_append_actions(const AppendArgs& a, hipStream_t st) {
+  if (a.n) DR_LAUNCH(dev::k_append_actions, dim3(unsigned((a.n + 255) / 256)), dim3(256), 0, st, a);
 }
 
 }  // namespace dr

@@ -69,6 +69,10 @@ uint64_t json_slot_entries(uint64_t len);
 void launch_json_index(const uint8_t* buf, uint64_t len, uint32_t* block_counts, uint16_t* slots, hipStream_t st);
 void launch_json_place(const uint8_t* buf, uint64_t len, const uint32_t* block_counts, const uint64_t* block_off,
                        const uint16_t* slots, uint64_t* nl, hipStream_t st);
+// one-block segments (len <= 16 KiB): newline positions straight into nl, off2 = {0, count}, and
+// zero[0..nzero) cleared
+void launch_json_index1(const uint8_t* buf, uint64_t len, uint64_t* nl, uint64_t* off2, uint64_t* zero,
+                        uint32_t nzero, hipStream_t st);
 void launch_json_parse(const JsonParseArgs& a, hipStream_t st);
 void launch_json_hard(const JsonParseArgs& a, hipStream_t st);
 
@@ -460,6 +464,14 @@ void launch_iota_u32(uint32_t* out, uint64_t n, hipStream_t st);
 void launch_gather_u64_by64(const uint64_t* src, const uint64_t* idx, uint64_t n, uint64_t* dst, hipStream_t st);
 void launch_gather_bytes(const uint64_t* ptr, const uint32_t* len, const uint64_t* off, uint64_t n, uint8_t* out,
                          hipStream_t st);
+// n actions from src to dst (both arrays already offset), dst src_id = sid
+struct AppendArgs {
+  ActionArrays src, dst;
+  uint16_t* src_id;
+  uint64_t n;
+  uint16_t sid;
+};
+void launch_append_actions(const AppendArgs& a, hipStream_t st);
 }  // namespace dr
 
 // ---- incremental tail apply: device-resident path index (k_index.hip) ----------------------------

@@ -27,3 +27,33 @@ extern "C" int jl_parse(const unsigned char* line, unsigned n, unsigned align, i
   *delts = o.delts;
   return o.hard;
 }
+
+// classify() against a per-byte restatement of the five tokenizer classes on `n` pseudo-random
+// windows (JSON punctuation, whitespace, control and high bytes mixed in); returns the first
+// mismatching window + 1, or 0.
+extern "C" long long jl_classify_check(unsigned long long seed, long long n) {
+  const char pick[] = "\"\\{}[]:, \t\r\nab\x01\x80\xff";
+  unsigned long long x = seed | 1;
+  for (long long it = 0; it < n; ++it) {
+    unsigned char b[16];
+    for (int k = 0; k < 16; ++k) {
+      x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+      b[k] = (x & 3) == 0 ? static_cast<unsigned char>(pick[(x >> 2) % 18]) : static_cast<unsigned char>(x >> 8);
+    }
+    uint32_t w[4];
+    std::memcpy(w, b, 16);
+    dr::jl::Win m;
+    dr::jl::classify(w, m);
+    uint32_t q = 0, bs = 0, st = 0, sp = 0, ct = 0;
+    for (int k = 0; k < 16; ++k) {
+      const unsigned char c = b[k];
+      if (c == '"') q |= 1u << k;
+      if (c == '\\') bs |= 1u << k;
+      if (c == '{' || c == '}' || c == '[' || c == ']' || c == ':' || c == ',') st |= 1u << k;
+      if (c == ' ') sp |= 1u << k;
+      if (c < 0x20) ct |= 1u << k;
+    }
+    if (q != m.q || bs != m.bs || st != m.st || sp != m.sp || ct != m.ctrl) return it + 1;
+  }
+  return 0;
+}

@@ -233,3 +233,11 @@ def test_mutations(lib):
     # mutations stay mostly decidable by the walker itself
     assert stats["hard"] < n // 10, stats
     assert stats.get(K_ERROR, 0) > n // 10 and stats.get(K_ADD, 0) > n // 20, stats
+
+
+def test_classify_masks(lib):
+    """The window classifier (nibble-transposed class masks) equals a per-byte restatement of the
+    quote / backslash / structural / space / control classes on 1M random windows."""
+    lib.jl_classify_check.restype = C.c_longlong
+    lib.jl_classify_check.argtypes = [C.c_ulonglong, C.c_longlong]
+    assert lib.jl_classify_check(0x5EED, 1_000_000) == 0

@@ -313,15 +313,35 @@ def measure_stream(eng, table, exp, args):
 
 def measure_checkpoint_write(eng, staged, cutoff, parts):
     """Config 4's multi-part checkpoint write (dr_state_write_checkpoint, file-action pages encoded on
-    the GPU): part 1 of `parts` timed (bytes to host memory, no disk), the rate per row reported."""
+    the GPU, D/Checkpoints.scala:229-365): every part of `parts` written to host memory (no disk; each
+    part's bytes dropped after it is counted), after the first call's device export of both sides; the
+    whole write's time, bytes and rows, and one part's time for the per-part rate."""
     st = staged.replay(cutoff)
-    st.write_checkpoint_part(1, parts)  # first call: the device export of both sides
+    t_first = time.perf_counter()
+    data, rows, adds = st.write_checkpoint_part(1, parts, with_adds=True)  # first: the device export
+    first_s = time.perf_counter() - t_first
+    total_rows, total_bytes, total_adds = rows, len(data), adds
+    part2 = None
     t0 = time.perf_counter()
-    data, rows = st.write_checkpoint_part(2, parts)
-    dt = time.perf_counter() - t0
+    for k in range(2, parts + 1):
+        tk = time.perf_counter()
+        data, rows, adds = st.write_checkpoint_part(k, parts, with_adds=True)
+        if k == 2:
+            part2 = (time.perf_counter() - tk, rows, len(data))
+        total_rows += rows
+        total_adds += adds
+        total_bytes += len(data)
+        del data
+    rest_s = time.perf_counter() - t0
+    n_live, n_tomb = st.counts["num_files"], st.counts["num_removes"]
     st.release()
-    return {"parts": parts, "part_rows": rows, "part_bytes": len(data), "part_s": round(dt, 4),
-            "rows_per_s": round(rows / dt, 1), "codec": "SNAPPY (device)"}
+    # the reference's check before _last_checkpoint: the parts' adds equal numOfFiles (D/Checkpoints.scala:325-328)
+    assert total_adds == n_live and total_rows >= n_live + n_tomb, (total_adds, total_rows, n_live, n_tomb)
+    return {"parts": parts, "all_parts_s": round(first_s + rest_s, 3), "first_part_incl_export_s": round(first_s, 3),
+            "rows": total_rows, "add_rows": total_adds, "bytes": total_bytes,
+            "rows_per_s": round(total_rows / (first_s + rest_s), 1),
+            "part_rows": part2[1] if part2 else rows, "part_bytes": part2[2] if part2 else total_bytes,
+            "part_s": round(part2[0], 4) if part2 else round(first_s, 4), "codec": "SNAPPY (device)"}
 
 
 def measure_filter(eng, staged, cutoff, exp, steps):

@@ -195,7 +195,10 @@ __device__ __forceinline__ void emit_line(const JsonParseArgs& a, uint64_t line,
 #define DR_JL_TOKCAP 40  // 10 KiB LDS per wave: 4 waves/SIMD (80: 20 KiB, LDS-bound at 2; sweep r01: 80 -> 40 = 4.02 -> 2.87 ms, 32 flushes too often)
 #endif
 constexpr int JL_TOKCAP = DR_JL_TOKCAP;
-constexpr int JL_FLUSH = JL_TOKCAP - 16;  // a window adds at most 16 tokens
+#ifndef DR_JL_FLUSH
+#define DR_JL_FLUSH (DR_JL_TOKCAP - 16)  // a window adds at most 16 tokens
+#endif
+constexpr int JL_FLUSH = DR_JL_FLUSH;
 
 #ifndef DR_JL_PAIR
 #define DR_JL_PAIR 1  // sweep r01: 2.86 -> 2.77 ms, 12.14 -> 11.98 ms/step same box

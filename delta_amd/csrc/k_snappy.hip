@@ -106,6 +106,21 @@ struct Staged {
   uint64_t hi;
 };
 __device__ __forceinline__ uint32_t skew(uint32_t dw) { return dw + (dw >> 6); }
+#ifndef DR_STAGE_BATCH
+#define DR_STAGE_BATCH 8
+#endif
+constexpr uint32_t STAGE_BATCH = DR_STAGE_BATCH;
+// A 16-byte load through the global address space (a flat load also counts against the LDS
+// counter, so every LDS access after it waits for it too).
+typedef unsigned int gu32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 gload16(const uint4* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const gu32x4 v = *(const __attribute__((address_space(1))) gu32x4*)(p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+#else
+  return *p;
+#endif
+}
 
 __device__ Staged stage_input(uint8_t* buf, const uint8_t* in, uint64_t n_in, uint32_t j0, uint32_t cnt) {
   uint64_t lo = uint64_t(j0) * SNAP_CH;
@@ -116,12 +131,22 @@ __device__ Staged stage_input(uint8_t* buf, const uint8_t* in, uint64_t n_in, ui
   const uint32_t nv = uint32_t((int64_t(hi) - lo_al + 15) / 16) + 1;  // 16-byte vectors (+ 8-byte reads past hi)
   uint32_t* b32 = reinterpret_cast<uint32_t*>(buf);
   const uint4* g4 = reinterpret_cast<const uint4*>(a0);
-  // 16-byte loads, four in flight per lane; a vector's 4 dwords never straddle a skew step
-#pragma unroll 4
-  for (uint32_t i = threadIdx.x; i < nv; i += blockDim.x) {
-    const uint4 v = g4[i];
-    uint32_t* d = b32 + skew(4 * i);
-    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+  // 16-byte global loads, STAGE_BATCH in flight per lane before any is written to LDS (indices past
+  // the range re-read its last vector instead of branching, so the loads issue back to back; a
+  // guarded loop waited for each load before issuing the next: 16 round trips per lane in k_snap_spec);
+  // a vector's 4 dwords never straddle a skew step
+  for (uint32_t i0 = threadIdx.x; i0 < nv; i0 += STAGE_BATCH * blockDim.x) {
+    uint4 v[STAGE_BATCH];
+#pragma unroll
+    for (uint32_t k = 0; k < STAGE_BATCH; ++k) v[k] = gload16(g4 + min(i0 + k * blockDim.x, nv - 1));
+#pragma unroll
+    for (uint32_t k = 0; k < STAGE_BATCH; ++k) {
+      const uint32_t i = i0 + k * blockDim.x;
+      if (i < nv) {
+        uint32_t* d = b32 + skew(4 * i);
+        d[0] = v[k].x; d[1] = v[k].y; d[2] = v[k].z; d[3] = v[k].w;
+      }
+    }
   }
   __syncthreads();
   return Staged{lo_al, hi};
@@ -680,10 +705,16 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
   const uintptr_t abs_lo = (reinterpret_cast<uintptr_t>(in) + in_lo) & ~uintptr_t(15);
   const uint32_t nv = in_lo < in_hi ? uint32_t((reinterpret_cast<uintptr_t>(in) + in_hi - abs_lo + 15) >> 4) : 0u;
   const bool staged = nv * 16 <= SNAP_BLOCK;
-  if (staged) {
+  if (staged && nv) {  // all of a thread's loads in flight at once (nv <= SNAP_BLOCK / 16: four per thread)
     const uint4* g4 = reinterpret_cast<const uint4*>(abs_lo);
     uint4* s4 = reinterpret_cast<uint4*>(stage);
-    for (uint32_t v = t; v < nv; v += EXEC_T) s4[v] = g4[v];
+    constexpr uint32_t PER = SNAP_BLOCK / 16 / EXEC_T;
+    uint4 v[PER];
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) v[k] = gload16(g4 + min(uint32_t(t) + k * EXEC_T, nv - 1));
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k)
+      if (uint32_t(t) + k * EXEC_T < nv) s4[uint32_t(t) + k * EXEC_T] = v[k];
   }
   __syncthreads();
   stamp(4);

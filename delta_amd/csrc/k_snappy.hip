@@ -559,6 +559,10 @@ constexpr uint32_t EXEC_RPT = DR_EXEC_RPT;            // records per thread held
 #define DR_EXEC_RPT2 4
 #endif
 constexpr uint32_t EXEC_RPT2 = DR_EXEC_RPT2;            // literal records per thread per pass (roots live in registers)
+#ifndef DR_EXEC_SPLIT
+#define DR_EXEC_SPLIT 4
+#endif
+constexpr uint32_t EXEC_SPLIT = DR_EXEC_SPLIT;  // map groups whose reads are issued before their writes (divides 16; 1: 2.725 ms, 4: 2.693, 16: spills, 2.83)
 
 __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t src[SNAP_BLOCK];  // map, later bytes + input
@@ -649,33 +653,43 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
   uint32_t xp[32];    // current pointers of the 4-byte groups, two u16 per register; roots at the end
   {
     uint32_t act = 0;   // groups with a byte not yet at its root
+    // groups in batches of EXEC_SPLIT: a batch's reads, then its writes (element starts keep their
+    // value, so no read depends on a write; the compiler cannot see that and otherwise orders each
+    // group's reads after the previous group's write)
 #pragma unroll
-    for (uint32_t j = 0; j < 16; ++j) {
-      const uint32_t i0 = 4 * (uint32_t(t) + EXEC_T * j);
-      const uint32_t wi = i0 >> 5, sh = i0 & 31;
-      const uint32_t w0 = starts[wi];
-      const uint32_t w1 = wi ? starts[wi - 1] : 0u;
-      const uint32_t w2 = wi > 1 ? starts[wi - 2] : 0u;
-      const uint32_t m0 = w0 & ((1u << sh) - 1u);
-      const uint32_t prev = m0   ? wi * 32 + 31 - __builtin_clz(m0)
-                            : w1 ? wi * 32 - 1 - __builtin_clz(w1)
-                            : w2 ? wi * 32 - 33 - __builtin_clz(w2)
-                                 : 0xffffffffu;
-      const uint2 g = *reinterpret_cast<const uint2*>(&src[i0]);
-      const uint32_t sv[4] = {g.x & 0xffffu, g.x >> 16, g.y & 0xffffu, g.y >> 16};
-      uint32_t cst = prev, cval = prev != 0xffffffffu ? uint32_t(src[prev < SNAP_BLOCK ? prev : 0]) : 0u;
-      uint32_t x4[4];
+    for (uint32_t jb = 0; jb < 16; jb += EXEC_SPLIT) {
 #pragma unroll
-      for (uint32_t e = 0; e < 4; ++e) {
-        const uint32_t i = i0 + e;
-        if ((w0 >> (sh + e)) & 1u) { cst = i; cval = sv[e]; }
-        x4[e] = (cst != 0xffffffffu && i - cst < 64 && i < nbytes) ? i - cst + cval : i;
+      for (uint32_t j = jb; j < jb + EXEC_SPLIT; ++j) {
+        const uint32_t i0 = 4 * (uint32_t(t) + EXEC_T * j);
+        const uint32_t wi = i0 >> 5, sh = i0 & 31;
+        const uint32_t w0 = starts[wi];
+        const uint32_t w1 = wi ? starts[wi - 1] : 0u;
+        const uint32_t w2 = wi > 1 ? starts[wi - 2] : 0u;
+        const uint32_t m0 = w0 & ((1u << sh) - 1u);
+        const uint32_t prev = m0   ? wi * 32 + 31 - __builtin_clz(m0)
+                              : w1 ? wi * 32 - 1 - __builtin_clz(w1)
+                              : w2 ? wi * 32 - 33 - __builtin_clz(w2)
+                                   : 0xffffffffu;
+        const uint2 g = *reinterpret_cast<const uint2*>(&src[i0]);
+        const uint32_t sv[4] = {g.x & 0xffffu, g.x >> 16, g.y & 0xffffu, g.y >> 16};
+        uint32_t cst = prev, cval = prev != 0xffffffffu ? uint32_t(src[prev < SNAP_BLOCK ? prev : 0]) : 0u;
+        uint32_t x4[4];
+#pragma unroll
+        for (uint32_t e = 0; e < 4; ++e) {
+          const uint32_t i = i0 + e;
+          if ((w0 >> (sh + e)) & 1u) { cst = i; cval = sv[e]; }
+          x4[e] = (cst != 0xffffffffu && i - cst < 64 && i < nbytes) ? i - cst + cval : i;
+        }
+        xp[2 * j] = x4[0] | (x4[1] << 16);
+        xp[2 * j + 1] = x4[2] | (x4[3] << 16);
+        // a group is active while a byte points away from itself (i < 65536, so the identity packs too)
+        if (xp[2 * j] != (i0 | ((i0 + 1) << 16)) || xp[2 * j + 1] != ((i0 + 2) | ((i0 + 3) << 16))) act |= 1u << j;
       }
-      xp[2 * j] = x4[0] | (x4[1] << 16);
-      xp[2 * j + 1] = x4[2] | (x4[3] << 16);
-      // a group is active while a byte points away from itself (i < 65536, so the identity packs too)
-      if (xp[2 * j] != (i0 | ((i0 + 1) << 16)) || xp[2 * j + 1] != ((i0 + 2) | ((i0 + 3) << 16))) act |= 1u << j;
-      if (i0 < nbytes) *reinterpret_cast<uint2*>(&src[i0]) = make_uint2(xp[2 * j], xp[2 * j + 1]);
+#pragma unroll
+      for (uint32_t j = jb; j < jb + EXEC_SPLIT; ++j) {
+        const uint32_t i0 = 4 * (uint32_t(t) + EXEC_T * j);
+        if (i0 < nbytes) *reinterpret_cast<uint2*>(&src[i0]) = make_uint2(xp[2 * j], xp[2 * j + 1]);
+      }
     }
     __syncthreads();
     stamp(3);

@@ -977,6 +977,17 @@ static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_
       for (auto& kv : why) std::fprintf(stderr, "snappy bad code %u: %zu pages\n", kv.first, kv.second);
       const size_t nr = size_t(nreg);
       std::fprintf(stderr, "snappy: pages %zu serially resolved regions %zu bad %zu\n", P.snap_pages.size(), nr, nb);
+      // chunks whose true entry is not their first speculatively visited position (re-walked by
+      // k_snap_count), and pages holding at least one
+      std::vector<uint32_t> ent = d2h(P.s_entry.p, P.nchunks, stream), sf = d2h(P.s_spec_first.p, P.nchunks, stream);
+      size_t nx = 0, px = 0;
+      for (size_t q = 0; q < P.snap_pages.size(); ++q) {
+        size_t k = 0;
+        for (uint32_t c = P.chunk_base[q]; c < P.chunk_base[q + 1]; ++c) k += ent[c] != sf[c];
+        nx += k;
+        px += k != 0;
+      }
+      std::fprintf(stderr, "snappy: chunks %u, entry != speculative first %zu (on %zu pages)\n", P.nchunks, nx, px);
     }
   }
   if (P.ba_pages) {

@@ -568,7 +568,8 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t src[SNAP_BLOCK];  // map, later bytes + input
   __shared__ uint32_t s_bad, s_nlong, s_inlo, s_inhi;
   __shared__ uint32_t s_long[EXEC_LONG];
-  __shared__ uint32_t starts[SNAP_BLOCK / 32];  // element start bits
+  __shared__ uint32_t starts_mem[SNAP_BLOCK / 32 + 2];  // element start bits, after two zero words
+  uint32_t* const starts = starts_mem + 2;
   const uint32_t b = blockIdx.x;
   const uint32_t p = a.block_page[b];
   if (a.pages_bad[p]) return;
@@ -590,7 +591,7 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     s_inlo = 0xffffffffu;
     s_inhi = 0;
   }
-  for (uint32_t w = t; w < SNAP_BLOCK / 32; w += EXEC_T) starts[w] = 0;
+  for (uint32_t w = t; w < SNAP_BLOCK / 32 + 2; w += EXEC_T) starts_mem[w] = 0;
   const uint64_t r0 = a.block_rec[b];
   const uint64_t r1 = b + 1 < a.nblocks ? a.block_rec[b + 1] : a.chunk_rec_start[a.nchunks];
   const uint32_t nrec = uint32_t(r1 - r0);
@@ -656,34 +657,56 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     // groups in batches of EXEC_SPLIT: a batch's reads, then its writes (element starts keep their
     // value, so no read depends on a write; the compiler cannot see that and otherwise orders each
     // group's reads after the previous group's write)
+    const bool part = nbytes != SNAP_BLOCK;  // block-uniform: a page's last block
 #pragma unroll
     for (uint32_t jb = 0; jb < 16; jb += EXEC_SPLIT) {
+      // staged so a batch's LDS reads are in flight together: start words and group entries, then
+      // the starts the groups continue (a volatile read: the compiler would otherwise sink it into
+      // the branch of groups whose first byte is no start, one round trip per group)
+      uint32_t w0[EXEC_SPLIT], prev[EXEC_SPLIT], pv[EXEC_SPLIT];
+      bool pvalid[EXEC_SPLIT];
+      uint2 g[EXEC_SPLIT];
 #pragma unroll
-      for (uint32_t j = jb; j < jb + EXEC_SPLIT; ++j) {
-        const uint32_t i0 = 4 * (uint32_t(t) + EXEC_T * j);
+      for (uint32_t q = 0; q < EXEC_SPLIT; ++q) {
+        const uint32_t i0 = 4 * (uint32_t(t) + EXEC_T * (jb + q));
         const uint32_t wi = i0 >> 5, sh = i0 & 31;
-        const uint32_t w0 = starts[wi];
-        const uint32_t w1 = wi ? starts[wi - 1] : 0u;
-        const uint32_t w2 = wi > 1 ? starts[wi - 2] : 0u;
-        const uint32_t m0 = w0 & ((1u << sh) - 1u);
-        const uint32_t prev = m0   ? wi * 32 + 31 - __builtin_clz(m0)
-                              : w1 ? wi * 32 - 1 - __builtin_clz(w1)
-                              : w2 ? wi * 32 - 33 - __builtin_clz(w2)
-                                   : 0xffffffffu;
-        const uint2 g = *reinterpret_cast<const uint2*>(&src[i0]);
-        const uint32_t sv[4] = {g.x & 0xffffu, g.x >> 16, g.y & 0xffffu, g.y >> 16};
-        uint32_t cst = prev, cval = prev != 0xffffffffu ? uint32_t(src[prev < SNAP_BLOCK ? prev : 0]) : 0u;
-        uint32_t x4[4];
+        w0[q] = starts[wi];
+        const uint32_t w1 = starts[int32_t(wi) - 1], w2 = starts[int32_t(wi) - 2];  // zero words before the block
+        g[q] = *reinterpret_cast<const uint2*>(&src[i0]);
+        // the last start before the group among the 64..95 bytes before it, branch-free: the highest
+        // set bit of (m0, w1) as one 64-bit word, else of w2 (__clz(0) = 32, __clzll(0) = 64)
+        const uint32_t m0 = w0[q] & ((1u << sh) - 1u);
+        const uint64_t x64 = (uint64_t(m0) << 32) | w1;
+        const uint32_t pa = wi * 32 + 31 - uint32_t(__clzll(int64_t(x64)));
+        pvalid[q] = (x64 | w2) != 0;
+        prev[q] = x64 ? pa : pa - uint32_t(__clz(int32_t(w2)));
+      }
 #pragma unroll
-        for (uint32_t e = 0; e < 4; ++e) {
-          const uint32_t i = i0 + e;
-          if ((w0 >> (sh + e)) & 1u) { cst = i; cval = sv[e]; }
-          x4[e] = (cst != 0xffffffffu && i - cst < 64 && i < nbytes) ? i - cst + cval : i;
+      for (uint32_t q = 0; q < EXEC_SPLIT; ++q) pv[q] = reinterpret_cast<volatile uint16_t*>(src)[pvalid[q] ? prev[q] : 0u];
+#pragma unroll
+      for (uint32_t q = 0; q < EXEC_SPLIT; ++q) {
+        const uint32_t j = jb + q;
+        const uint32_t i0 = 4 * (uint32_t(t) + EXEC_T * j);
+        // byte i of an element starting at st maps to i + (src[st] - st): minus the offset for a
+        // copy, 0 for a literal (and for a byte with no start in the 64..95 bytes before it, which
+        // lies in a long literal: copies are at most 64 bytes, checked above)
+        const int32_t dp = pvalid[q] ? int32_t(pv[q]) - int32_t(prev[q]) : 0;
+        const uint32_t sb = w0[q] >> (i0 & 31);  // start bits of the group's bytes (bits 0..3)
+        const int32_t d0 = (sb & 1u) ? int32_t(g[q].x & 0xffffu) - int32_t(i0) : dp;
+        const int32_t d1 = (sb & 2u) ? int32_t(g[q].x >> 16) - int32_t(i0 + 1) : d0;
+        const int32_t d2 = (sb & 4u) ? int32_t(g[q].y & 0xffffu) - int32_t(i0 + 2) : d1;
+        const int32_t d3 = (sb & 8u) ? int32_t(g[q].y >> 16) - int32_t(i0 + 3) : d2;
+        xp[2 * j] = uint32_t(int32_t(i0) + d0) | (uint32_t(int32_t(i0 + 1) + d1) << 16);
+        xp[2 * j + 1] = uint32_t(int32_t(i0 + 2) + d2) | (uint32_t(int32_t(i0 + 3) + d3) << 16);
+        // a group is active while a byte points away from itself
+        if ((d0 | d1 | d2 | d3) != 0) act |= 1u << j;
+        if (part && i0 + 4 > nbytes) {  // past the block end: the identity
+          const uint32_t x0 = i0 < nbytes ? (xp[2 * j] & 0xffffu) : i0, x1 = i0 + 1 < nbytes ? (xp[2 * j] >> 16) : i0 + 1;
+          const uint32_t x2 = i0 + 2 < nbytes ? (xp[2 * j + 1] & 0xffffu) : i0 + 2, x3 = i0 + 3 < nbytes ? (xp[2 * j + 1] >> 16) : i0 + 3;
+          xp[2 * j] = x0 | (x1 << 16);
+          xp[2 * j + 1] = x2 | (x3 << 16);
+          if (xp[2 * j] == (i0 | ((i0 + 1) << 16)) && xp[2 * j + 1] == ((i0 + 2) | ((i0 + 3) << 16))) act &= ~(1u << j);
         }
-        xp[2 * j] = x4[0] | (x4[1] << 16);
-        xp[2 * j + 1] = x4[2] | (x4[3] << 16);
-        // a group is active while a byte points away from itself (i < 65536, so the identity packs too)
-        if (xp[2 * j] != (i0 | ((i0 + 1) << 16)) || xp[2 * j + 1] != ((i0 + 2) | ((i0 + 3) << 16))) act |= 1u << j;
       }
 #pragma unroll
       for (uint32_t j = jb; j < jb + EXEC_SPLIT; ++j) {

@@ -2412,6 +2412,7 @@ static uint64_t record_sum(dr_state& st, int which) {
   a.tags_val_bytes = X.tags_val_bytes.p;
   a.tags_val_null = X.tags_val_null.p;
   a.sum = sum.p;
+  if (const char* m = std::getenv("DR_RECORD_FIELDS")) a.field_mask = uint32_t(std::strtoul(m, nullptr, 0));  // diagnostics
   launch_record_hash(a, stream);
   return uint64_t(d2h_one(sum.p, stream));
 }

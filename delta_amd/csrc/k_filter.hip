@@ -982,6 +982,8 @@ __global__ void __launch_bounds__(256) k_record_hash(RecordHashArgs a) {
                         a.pv_val_bytes, a.pv_val_null, 2, 3);
     w[7] = rec_map_hash(a.tags_null[i], a.tags_entry[i], a.tags_entry[i + 1], a.tags_key_off, a.tags_key_bytes,
                         a.tags_val_off, a.tags_val_bytes, a.tags_val_null, 4, 5);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) w[k] = (a.field_mask >> k) & 1u ? w[k] : 0ull;
     r = xxh64_words8(w, REC_SEED);
   }
   for (int o = 32; o > 0; o >>= 1) r += __shfl_down(r, o, 64);

@@ -1,6 +1,9 @@
 // Small gather kernels used to move result subsets to the host in one transfer each.
 #include "dev_common.h"
 #include "kernels.h"
+#include <algorithm>
+#include <stdexcept>
+#include <string>
 
 namespace dr {
 namespace dev {
@@ -17,13 +20,16 @@ __global__ void k_gather(const T* __restrict__ src, const I* __restrict__ idx, u
 }
 
 // out[off[i] .. off[i] + len[i]) = bytes at ptr[i]; one wave per string.
+// One wave per string, grid-stride (a wave per string over a grid of n waves would pass the
+// dispatch's 2^32 work items at 67M strings).
 __global__ void k_gather_bytes(const uint64_t* __restrict__ ptr, const uint32_t* __restrict__ len,
                                const uint64_t* __restrict__ off, uint64_t n, uint8_t* __restrict__ out) {
-  const uint64_t s = uint64_t(blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6);
-  if (s >= n) return;
-  const uint8_t* p = reinterpret_cast<const uint8_t*>(ptr[s]);
-  uint8_t* o = out + off[s];
-  for (uint32_t k = threadIdx.x & 63; k < len[s]; k += 64) o[k] = p[k];
+  for (uint64_t s = uint64_t(blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6); s < n;
+       s += uint64_t(gridDim.x) * (blockDim.x / 64)) {
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(ptr[s]);
+    uint8_t* o = out + off[s];
+    for (uint32_t k = threadIdx.x & 63; k < len[s]; k += 64) o[k] = p[k];
+  }
 }
 
 // One action per thread from src[i] to dst[i] across the nine action arrays, src_id[i] = sid: an
@@ -54,6 +60,12 @@ void set_launch_hook(LaunchHook hook, void* user) {
   t_hook = hook;
   t_hook_user = user;
 }
+void launch_grid_check(const char* kernel, dim3 grid, dim3 block) {
+  if (uint64_t(grid.x) * block.x >= (uint64_t(1) << 32) || uint64_t(grid.y) * block.y >= (uint64_t(1) << 32) ||
+      uint64_t(grid.z) * block.z >= (uint64_t(1) << 32))
+    throw std::runtime_error(std::string("launch of ") + kernel + ": grid of 2^32 or more work items in one dimension");
+}
+
 bool launch_events(const char* kernel, hipEvent_t* start, hipEvent_t* stop) {
   return t_hook && t_hook(t_hook_user, kernel, start, stop);
 }
@@ -78,7 +90,7 @@ void launch_gather_u64_by64(const uint64_t* src, const uint64_t* idx, uint64_t n
 }
 void launch_gather_bytes(const uint64_t* ptr, const uint32_t* len, const uint64_t* off, uint64_t n, uint8_t* out,
                          hipStream_t st) {
-  if (n) DR_LAUNCH(dev::k_gather_bytes, dim3(unsigned((n + 3) / 4)), dim3(256), 0, st, ptr, len, off, n, out);
+  if (n) DR_LAUNCH(dev::k_gather_bytes, dim3(unsigned(std::min<uint64_t>((n + 3) / 4, 1u << 20))), dim3(256), 0, st, ptr, len, off, n, out);
 }
 
 void launch_append_actions(const AppendArgs& a, hipStream_t st) {

@@ -16,8 +16,12 @@ namespace dr {
 typedef bool (*LaunchHook)(void* user, const char* kernel, hipEvent_t* start, hipEvent_t* stop);
 void set_launch_hook(LaunchHook hook, void* user);
 bool launch_events(const char* kernel, hipEvent_t* start, hipEvent_t* stop);
+void launch_grid_check(const char* kernel, dim3 grid, dim3 block);
+// A dispatch's work-item count per dimension is 32-bit: a larger grid would silently run a wrapped
+// fraction of itself, so it is refused (launch_grid_check throws).
 #define DR_LAUNCH(K, GRID, BLOCK, SHM, ST, ...)                                     \
   do {                                                                              \
+    ::dr::launch_grid_check(#K, dim3(GRID), dim3(BLOCK));                           \
     hipEvent_t dr_e0_ = nullptr, dr_e1_ = nullptr;                                  \
     if (::dr::launch_events(#K, &dr_e0_, &dr_e1_))                                  \
       hipExtLaunchKernelGGL(K, GRID, BLOCK, SHM, ST, dr_e0_, dr_e1_, 0u, __VA_ARGS__); \
@@ -633,6 +637,7 @@ struct RecordHashArgs {
   const uint8_t* tags_null; const uint64_t* tags_entry; const int64_t* tags_key_off; const uint8_t* tags_key_bytes;
   const int64_t* tags_val_off; const uint8_t* tags_val_bytes; const uint8_t* tags_val_null;
   unsigned long long* sum;
+  uint32_t field_mask = 0xffu;  // words of the record hash kept (diagnostics: DR_RECORD_FIELDS); others are 0
 };
 void launch_record_hash(const RecordHashArgs& a, hipStream_t st);
 }  // namespace dr

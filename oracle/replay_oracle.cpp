@@ -755,6 +755,11 @@ uint64_t rec_hash(const Rec& r, int side) {
   else { w[3] = r.has_delts ? uint64_t(r.delts) : 0; w[4] = (r.has_delts ? 1u : 0u) | (r.efm ? 2u : 0u); w[5] = 0; }
   w[6] = r.pv.hash(2, 3);
   w[7] = r.tags.hash(4, 5);
+  static const uint32_t field_mask = [] {  // diagnostics: DR_RECORD_FIELDS keeps these words (as the device)
+    const char* m = getenv("DR_RECORD_FIELDS");
+    return m ? uint32_t(strtoul(m, nullptr, 0)) : 0xffu;
+  }();
+  for (int k = 0; k < 8; ++k) if (!((field_mask >> k) & 1u)) w[k] = 0;
   uint8_t b[64];
   memcpy(b, w, 64);  // little-endian host
   return xxh64s(b, 64, kRecSeed);

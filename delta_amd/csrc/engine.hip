@@ -338,8 +338,6 @@ struct PagePlan {
   DBuf<uint8_t> s_chunk_flag;
   DBuf<uint64_t> s_block_rec;
   DBuf<unsigned long long> s_region_count;
-  DBuf<uint64_t> s_half_rec;   // k_snap_exec_half: record holding byte 32 KiB of each block
-  DBuf<uint32_t> s_half_flag;  // [nblocks] first halves' published flags, then the ticket counter
   std::vector<uint32_t> wg_chunk0;
   DBuf<uint32_t> d_wg_chunk0;
   uint64_t snap_in_bytes = 0, snap_out_bytes = 0, copy_bytes = 0;
@@ -874,10 +872,6 @@ static void plan_pages(StagedData& s, PagePlan& P) {
   P.s_assumed = DBuf<uint32_t>(s.ctx, P.nchunks);
   P.s_region = DBuf<uint32_t>(s.ctx, P.nchunks);
   P.s_block_rec = DBuf<uint64_t>(s.ctx, P.block_page.size() + 1);
-  if (snappy_exec_halves()) {
-    P.s_half_rec = DBuf<uint64_t>(s.ctx, P.block_page.size() + 1);
-    P.s_half_flag = DBuf<uint32_t>(s.ctx, P.block_page.size() + 1);
-  }
   P.s_chunk_flag = DBuf<uint8_t>(s.ctx, P.nchunks);
   P.s_region_count = DBuf<unsigned long long>(s.ctx, 1);
   P.s_chunk_out = DBuf<uint32_t>(s.ctx, P.nchunks);
@@ -938,7 +932,6 @@ static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_
     P.s_pages_bad.zero(stream);
     P.s_chunk_flag.zero(stream);
     P.s_region_count.zero(stream);
-    if (P.s_half_flag.p) P.s_half_flag.zero(stream);
     SnappyArgs sa{P.d_snap.p, uint32_t(P.snap_pages.size()), P.d_chunk_base.p, P.nchunks, P.s_spec_exit.p,
                   P.s_vis.p, P.s_entry.p, P.s_spec_first.p, P.s_assumed.p, P.s_chunk_flag.p, P.s_region.p, P.s_region_count.p, P.s_chunk_out.p, P.s_chunk_out_start.p, P.s_chunk_copies.p,
                   P.s_rec_start.p, P.s_recs.p, P.d_block_page.p, P.s_block_rec.p, uint32_t(P.block_page.size()),
@@ -947,11 +940,6 @@ static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_
     sa.half_out = P.s_half_out.p;
     sa.half_elems = P.s_half_elems.p;
     sa.chunk_page = P.d_chunk_page.p;
-    if (P.s_half_flag.p) {
-      sa.half_rec = P.s_half_rec.p;
-      sa.half_flag = P.s_half_flag.p;
-      sa.exec_ticket = P.s_half_flag.p + P.block_page.size();
-    }
     DBuf<uint64_t> stamps;
     const bool dbg = std::getenv("DR_SNAP_DEBUG") != nullptr;
     if (dbg) {

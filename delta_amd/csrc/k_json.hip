@@ -292,9 +292,6 @@ __device__ __forceinline__ void walk_line(const JsonParseArgs& a, uint32_t* tokb
 //     or all removes), so the 64 lanes take the same grammar branch at the same step instead of
 //     diverging byte by byte.
 // The buffer is flushed through phase 2 whenever a lane could overflow it, and at the end.
-#ifndef DR_JL_ONE_WALK
-#define DR_JL_ONE_WALK 0
-#endif
 template <bool Stage>
 __global__ void __launch_bounds__(JL_T, DR_JL_WAVES) k_json_lines(JsonParseArgs a) {
   __shared__ uint32_t tokbuf[JL_TOKCAP * JL_T];
@@ -311,21 +308,15 @@ __global__ void __launch_bounds__(JL_T, DR_JL_WAVES) k_json_lines(JsonParseArgs 
     const uint64_t last = min(first + JL_T, a.nlines) - 1;
     const uint64_t r0 = (first == 0 ? 0 : a.nl[first - 1] + 1) & ~uint64_t(15);
     const uint64_t r1 = (a.nl[last] + 16) & ~uint64_t(15);
-    const bool fits = r1 - r0 + 48 <= JL_STAGE_BYTES;  // + the walker's reads past a line end (load20, pairs)
-    if (fits) {  // block-uniform
+    if (r1 - r0 + 48 <= JL_STAGE_BYTES) {  // + the walker's reads past a line end (load20, pairs)
       const uint4* src = reinterpret_cast<const uint4*>(a.buf + r0);
       const uint32_t nq = uint32_t((r1 - r0) >> 4) + 3;
       for (uint32_t k = lane; k < nq; k += JL_T) stage[k] = src[k];
       __syncthreads();
+      walk_line<true>(a, tokbuf, lane, line, live, b, n, reinterpret_cast<const uint8_t*>(stage) + (b - r0));
+      return;
     }
-#if DR_JL_ONE_WALK
-    // one inlined walker for both sources (generic pointer): half the code a cold commit fetches
-    walk_line<true>(a, tokbuf, lane, line, live, b, n,
-                    fits ? reinterpret_cast<const uint8_t*>(stage) + (b - r0) : a.buf + b);
-#else
-    if (fits) walk_line<true>(a, tokbuf, lane, line, live, b, n, reinterpret_cast<const uint8_t*>(stage) + (b - r0));
-    else walk_line<true>(a, tokbuf, lane, line, live, b, n, a.buf + b);
-#endif
+    walk_line<true>(a, tokbuf, lane, line, live, b, n, a.buf + b);
     return;
   }
   walk_line(a, tokbuf, lane, line, live, b, n, a.buf + b);

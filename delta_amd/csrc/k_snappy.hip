@@ -30,7 +30,6 @@
 // Chunk walkers (A, C, E) stage their page bytes into LDS with coalesced loads and parse from LDS.
 #include "dev_common.h"
 #include "kernels.h"
-#include <cstdlib>
 
 namespace dr {
 namespace dev {
@@ -530,8 +529,6 @@ __global__ void __launch_bounds__(2 * WG_CHUNKS) k_snap_emit(SnappyArgs a) {
             (lit ? (ip + len > pg.n_in || ip >= REC_LIT) : (off == 0 || off > orel));  // a copy reaching before its fragment
       if (bad) break;
       if (orel == 0) a.block_rec[pg.block_base + uint32_t(o >> 16)] = rec;
-      if (orel <= SNAP_BLOCK / 2 && orel + len > SNAP_BLOCK / 2 && a.half_rec)
-        a.half_rec[pg.block_base + uint32_t(o >> 16)] = rec;  // holds byte 32 KiB (k_snap_exec_half)
       const uint32_t src = lit ? (REC_LIT | uint32_t(ip)) : off;
       a.recs[rec] = orel | (uint64_t(len - 1) << 16) | (uint64_t(src) << 32);
       ++rec;
@@ -849,338 +846,6 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
   stamp(7);
 }
 
-// F' (DR_EXEC_HALVES=1): a 64 KiB fragment executed by two 512-lane workgroups, one per 32 KiB half,
-// each with a 64 KiB map so two run per CU and one half's latency-bound phases (record loads,
-// literal copies, stores) overlap the other workgroup's LDS-bound ones. Map entries hold absolute
-// block positions. The second half's pointers stop at positions below 32 KiB (bytes of the first
-// half, roots for it); it reads those bytes from the first half's output once that workgroup has
-// published it through a per-block flag. Workgroups take tickets when they start and the ticket,
-// not blockIdx, names the (block, half): the first half of a pair is always running or done when
-// the second waits, and the wait is bounded (a timeout sends the page to the serial decoder).
-constexpr int EXH_T = 512;
-constexpr uint32_t SNAP_HALF = SNAP_BLOCK / 2;
-constexpr uint32_t EXH_LONG = 128;            // literal runs longer than EXEC_LONG in one half: at most 32 KiB / 257
-constexpr uint32_t EXH_WAIT = 1u << 20;       // flag polls (with s_sleep) before a half gives up
-
-__global__ void __launch_bounds__(EXH_T) k_snap_exec_half(SnappyArgs a) {
-  __shared__ __attribute__((aligned(16))) uint16_t src[SNAP_HALF];  // map, later bytes + input
-  __shared__ uint32_t s_bad, s_nlong, s_inlo, s_inhi, s_ticket, s_flag;
-  __shared__ uint64_t s_long[EXH_LONG];       // clipped long literals {local start, length - 1, input position}
-  __shared__ uint32_t starts_mem[SNAP_HALF / 32 + 2];  // element start bits, after two zero words
-  uint32_t* const starts = starts_mem + 2;
-  const int t = threadIdx.x;
-  if (t == 0) {
-    const uint32_t tk = atomicAdd(a.exec_ticket, 1u);
-    s_ticket = tk;
-    s_flag = (tk >> 1) < a.nblocks ? a.pages_bad[a.block_page[tk >> 1]] : 1u;  // read once: block-uniform
-  }
-  __syncthreads();
-  const uint32_t b = s_ticket >> 1, h = s_ticket & 1u;
-  if (b >= a.nblocks) return;
-  const uint32_t p = a.block_page[b];
-  const SnapPage& pg = a.pages[p];
-  const uint8_t* in = reinterpret_cast<const uint8_t*>(pg.in);
-  uint8_t* out = reinterpret_cast<uint8_t*>(pg.out);
-  const uint64_t bs = uint64_t(b - pg.block_base) * SNAP_BLOCK;
-  const uint64_t be = min(bs + SNAP_BLOCK, uint64_t(pg.n_out));
-  const uint32_t nbytes = uint32_t(be - bs);
-  const uint32_t base = h ? SNAP_HALF : 0u;  // block position of this half's first byte
-  if (h && nbytes <= SNAP_HALF) return;      // no second half (nobody waits for it)
-  const uint32_t hend = min(nbytes, base + SNAP_HALF), hbytes = hend - base;
-  const bool paired = nbytes > SNAP_HALF;    // the first half publishes its bytes for the second
-  auto publish = [&](uint32_t v) {           // first half only; every exit path of a paired first half
-    if (!h && paired) {
-      __builtin_amdgcn_s_waitcnt(0);  // this wave's stores are in L2
-      __syncthreads();                  // ... and every other wave's
-      if (t == 0) {     // one agent-scope release per workgroup (writes the XCD's L2 back), then the flag
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __hip_atomic_store(&a.half_flag[b], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  };
-  if (s_flag) {
-    publish(2u);
-    return;
-  }
-  __syncthreads();  // everyone has read s_flag before it is reused below
-  if (t == 0) {
-    s_bad = 0;
-    s_nlong = 0;
-    s_inlo = 0xffffffffu;
-    s_inhi = 0;
-  }
-  for (uint32_t w = t; w < SNAP_HALF / 32 + 2; w += EXH_T) starts_mem[w] = 0;
-  // records: the first half's run up to and including the element that holds byte 32 KiB, the
-  // second half's from that element on (k_snap_emit records it in half_rec)
-  const uint64_t r0b = a.block_rec[b];
-  const uint64_t r1b = b + 1 < a.nblocks ? a.block_rec[b + 1] : a.chunk_rec_start[a.nchunks];
-  const uint64_t rh = paired ? a.half_rec[b] : r1b;
-  const bool rh_ok = rh >= r0b && rh <= r1b && (!paired || rh < r1b);
-  const uint64_t r0 = h ? rh : r0b;
-  const uint64_t r1 = h ? r1b : (paired ? rh + 1 : r1b);
-  const uint32_t nrec = rh_ok ? uint32_t(r1 - r0) : 0u;
-  __syncthreads();
-  if (!rh_ok && t == 0) s_bad = 1;
-  // a record's part in this half: local start, length, value of its first byte (absolute position
-  // it copies, or itself for a literal) and, for a literal, the input position of that byte
-  struct Part { uint32_t ls, n, v, ip; bool lit, ok; };
-  auto part = [&](uint64_t wk) -> Part {
-    Part q{0, 0, 0, 0, false, false};
-    const uint32_t sv = uint32_t(wk >> 32);
-    const uint32_t rel = uint32_t(wk & 0xffff);
-    const uint32_t len = uint32_t((wk >> 16) & 0xffff) + 1;
-    const uint32_t s0 = max(rel, base), e0 = min(rel + len, hend);
-    if (s0 >= e0) return q;
-    q.ok = true;
-    q.ls = s0 - base;
-    q.n = e0 - s0;
-    q.lit = (sv & REC_LIT) != 0;
-    q.v = q.lit ? s0 : s0 - sv;
-    q.ip = (sv & ~REC_LIT) + (s0 - rel);
-    return q;
-  };
-  // 1a. per element part: its start bit and the map entry of its first byte
-  uint32_t lo_in = 0xffffffffu, hi_in = 0;
-  const bool held = nrec <= EXH_T * EXEC_RPT;  // block-uniform: one pass, records stay in w for step 3
-  uint64_t w[EXEC_RPT];
-  for (uint32_t rb = 0; rb < nrec; rb += EXH_T * EXEC_RPT) {
-#pragma unroll
-    for (uint32_t k = 0; k < EXEC_RPT; ++k) {
-      const uint32_t r = rb + k * EXH_T + uint32_t(t);
-      w[k] = r < nrec ? a.recs[r0 + r] : 0ull;
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < EXEC_RPT; ++k) {
-      const uint32_t r = rb + k * EXH_T + uint32_t(t);
-      if (r >= nrec) continue;
-      const uint32_t sv = uint32_t(w[k] >> 32);
-      const uint32_t rel = uint32_t(w[k] & 0xffff);
-      const uint32_t len = uint32_t((w[k] >> 16) & 0xffff) + 1;
-      if (rel + len > nbytes) { s_bad = 1; continue; }
-      if (!(sv & REC_LIT) && (sv > rel || len > 64)) { s_bad = 1; continue; }  // snappy copies are at most 64 bytes
-      const Part q = part(w[k]);
-      if (!q.ok) continue;
-      atomicOr(&starts[q.ls >> 5], 1u << (q.ls & 31));
-      src[q.ls] = uint16_t(q.v);
-      if (q.lit) {
-        lo_in = min(lo_in, q.ip);
-        hi_in = max(hi_in, q.ip + q.n);
-        if (q.n > EXEC_LONG) {  // the whole workgroup copies it (step 3)
-          const uint32_t slot = atomicAdd(&s_nlong, 1u);
-          if (slot < EXH_LONG) s_long[slot] = q.ls | (uint64_t(q.n - 1) << 16) | (uint64_t(q.ip) << 32);
-          else s_bad = 1;
-        }
-      }
-    }
-  }
-  for (int o = 32; o > 0; o >>= 1) {
-    lo_in = min(lo_in, uint32_t(__shfl_xor(int(lo_in), o, 64)));
-    hi_in = max(hi_in, uint32_t(__shfl_xor(int(hi_in), o, 64)));
-  }
-  if ((t & 63) == 0) {
-    atomicMin(&s_inlo, lo_in);
-    atomicMax(&s_inhi, hi_in);
-  }
-  __syncthreads();
-  if (s_bad) {
-    if (t == 0) atomicOr(&a.pages_bad[p], 32u);
-    publish(2u);
-    return;
-  }
-  // 1b / 2. as k_snap_exec, on local indices with absolute values: thread t owns the 4-byte groups
-  // i0 = 4 (t + 512 j), j < 16; a pointer below `base` (second half) is a root
-  uint32_t xp[32];
-  {
-    uint32_t act = 0;
-    const bool partial = hbytes != SNAP_HALF;  // block-uniform: a page's last block
-#pragma unroll
-    for (uint32_t jb = 0; jb < 16; jb += EXEC_SPLIT) {
-      uint32_t w0[EXEC_SPLIT], prev[EXEC_SPLIT], pv[EXEC_SPLIT];
-      bool pvalid[EXEC_SPLIT];
-      uint2 g[EXEC_SPLIT];
-#pragma unroll
-      for (uint32_t q = 0; q < EXEC_SPLIT; ++q) {
-        const uint32_t i0 = 4 * (uint32_t(t) + EXH_T * (jb + q));
-        const uint32_t wi = i0 >> 5, sh = i0 & 31;
-        w0[q] = starts[wi];
-        const uint32_t w1 = starts[int32_t(wi) - 1], w2 = starts[int32_t(wi) - 2];
-        g[q] = *reinterpret_cast<const uint2*>(&src[i0]);
-        const uint32_t m0 = w0[q] & ((1u << sh) - 1u);
-        const uint64_t x64 = (uint64_t(m0) << 32) | w1;
-        const uint32_t pa = wi * 32 + 31 - uint32_t(__clzll(int64_t(x64)));
-        pvalid[q] = (x64 | w2) != 0;
-        prev[q] = x64 ? pa : pa - uint32_t(__clz(int32_t(w2)));
-      }
-#pragma unroll
-      for (uint32_t q = 0; q < EXEC_SPLIT; ++q) pv[q] = reinterpret_cast<volatile uint16_t*>(src)[pvalid[q] ? prev[q] : 0u];
-#pragma unroll
-      for (uint32_t q = 0; q < EXEC_SPLIT; ++q) {
-        const uint32_t j = jb + q;
-        const uint32_t i0 = 4 * (uint32_t(t) + EXH_T * j);
-        const int32_t ab = int32_t(base + i0);  // absolute position of the group's first byte
-        const int32_t dp = pvalid[q] ? int32_t(pv[q]) - int32_t(base + prev[q]) : 0;
-        const uint32_t sb = w0[q] >> (i0 & 31);
-        const int32_t d0 = (sb & 1u) ? int32_t(g[q].x & 0xffffu) - ab : dp;
-        const int32_t d1 = (sb & 2u) ? int32_t(g[q].x >> 16) - (ab + 1) : d0;
-        const int32_t d2 = (sb & 4u) ? int32_t(g[q].y & 0xffffu) - (ab + 2) : d1;
-        const int32_t d3 = (sb & 8u) ? int32_t(g[q].y >> 16) - (ab + 3) : d2;
-        xp[2 * j] = uint32_t(ab + d0) | (uint32_t(ab + 1 + d1) << 16);
-        xp[2 * j + 1] = uint32_t(ab + 2 + d2) | (uint32_t(ab + 3 + d3) << 16);
-        if ((d0 | d1 | d2 | d3) != 0) act |= 1u << j;
-        if (partial && i0 + 4 > hbytes) {  // past the half's end: the identity
-          const uint32_t u = uint32_t(ab);
-          const uint32_t x0 = i0 < hbytes ? (xp[2 * j] & 0xffffu) : u, x1 = i0 + 1 < hbytes ? (xp[2 * j] >> 16) : u + 1;
-          const uint32_t x2 = i0 + 2 < hbytes ? (xp[2 * j + 1] & 0xffffu) : u + 2, x3 = i0 + 3 < hbytes ? (xp[2 * j + 1] >> 16) : u + 3;
-          xp[2 * j] = x0 | (x1 << 16);
-          xp[2 * j + 1] = x2 | (x3 << 16);
-          if (xp[2 * j] == (u | ((u + 1) << 16)) && xp[2 * j + 1] == ((u + 2) | ((u + 3) << 16))) act &= ~(1u << j);
-        }
-      }
-#pragma unroll
-      for (uint32_t j = jb; j < jb + EXEC_SPLIT; ++j) {
-        const uint32_t i0 = 4 * (uint32_t(t) + EXH_T * j);
-        if (i0 < hbytes) *reinterpret_cast<uint2*>(&src[i0]) = make_uint2(xp[2 * j], xp[2 * j + 1]);
-      }
-    }
-    __syncthreads();
-    // pointer jumping; a pointer below base reads a dummy entry and keeps its value
-    auto look = [&](uint32_t x) -> uint32_t {
-      const uint32_t y = src[(x - base) & (SNAP_HALF - 1)];
-      return x >= base ? y : x;
-    };
-    while (act) {
-#pragma unroll
-      for (uint32_t j = 0; j < 16; ++j) {
-        if (act & (1u << j)) {
-          const uint32_t a0 = xp[2 * j], a1 = xp[2 * j + 1];
-          const uint32_t y0 = look(a0 & 0xffffu), y1 = look(a0 >> 16), y2 = look(a1 & 0xffffu), y3 = look(a1 >> 16);
-          const uint32_t b0 = y0 | (y1 << 16), b1 = y2 | (y3 << 16);
-          if (b0 == a0 && b1 == a1) {
-            act &= ~(1u << j);
-          } else {
-            xp[2 * j] = b0;
-            xp[2 * j + 1] = b1;
-            *reinterpret_cast<uint2*>(&src[4 * (uint32_t(t) + EXH_T * j)]) = make_uint2(b0, b1);
-          }
-        }
-      }
-    }
-  }
-  __syncthreads();
-  // 3. the LDS becomes the half's bytes (lower 32 KiB) and its literals' input range (upper 32 KiB)
-  uint8_t* bytes = reinterpret_cast<uint8_t*>(src);
-  uint8_t* stage = bytes + SNAP_HALF;
-  const uint32_t in_lo = s_inlo, in_hi = s_inhi;
-  const uintptr_t abs_lo = (reinterpret_cast<uintptr_t>(in) + in_lo) & ~uintptr_t(15);
-  const uint32_t nv = in_lo < in_hi ? uint32_t((reinterpret_cast<uintptr_t>(in) + in_hi - abs_lo + 15) >> 4) : 0u;
-  const bool staged = nv * 16 <= SNAP_HALF;
-  if (staged && nv) {
-    const uint4* g4 = reinterpret_cast<const uint4*>(abs_lo);
-    uint4* s4 = reinterpret_cast<uint4*>(stage);
-    constexpr uint32_t PER = SNAP_HALF / 16 / EXH_T;
-    uint4 v[PER];
-#pragma unroll
-    for (uint32_t k = 0; k < PER; ++k) v[k] = gload16(g4 + min(uint32_t(t) + k * EXH_T, nv - 1));
-#pragma unroll
-    for (uint32_t k = 0; k < PER; ++k)
-      if (uint32_t(t) + k * EXH_T < nv) s4[uint32_t(t) + k * EXH_T] = v[k];
-  }
-  __syncthreads();
-  auto copy_lit = [&](uint64_t wk) {
-    if (!(uint32_t(wk >> 32) & REC_LIT)) return;
-    const Part q = part(wk);
-    if (!q.ok || q.n > EXEC_LONG) return;  // long ones: below
-    if (!staged) {
-      const uint8_t* sp = in + q.ip;
-      for (uint32_t i = 0; i < q.n; ++i) bytes[q.ls + i] = sp[i];
-      return;
-    }
-    uint32_t qq = uint32_t(reinterpret_cast<uintptr_t>(in) + q.ip - abs_lo) + SNAP_HALF;
-    uint32_t d = q.ls, n = q.n;
-    while (n && (d & 3)) { bytes[d++] = bytes[qq++]; --n; }
-    const uint32_t sh = qq & 3;
-    const uint32_t* qa = reinterpret_cast<const uint32_t*>(bytes + (qq & ~3u));
-    uint32_t* da = reinterpret_cast<uint32_t*>(bytes + d);
-    uint32_t lo = qa[0];
-    for (; n >= 4; n -= 4) {
-      const uint32_t hi = *++qa;
-      *da++ = __builtin_amdgcn_alignbyte(hi, lo, sh);
-      lo = hi;
-    }
-    d = uint32_t(reinterpret_cast<uint8_t*>(da) - bytes);
-    qq = uint32_t(reinterpret_cast<const uint8_t*>(qa) - bytes) + sh;
-    while (n) { bytes[d++] = bytes[qq++]; --n; }
-  };
-  if (held) {
-#pragma unroll
-    for (uint32_t k = 0; k < EXEC_RPT; ++k)
-      if (k * EXH_T + uint32_t(t) < nrec) copy_lit(w[k]);
-  } else {
-    for (uint32_t rb = 0; rb < nrec; rb += EXH_T * EXEC_RPT2) {
-      uint64_t w2[EXEC_RPT2];
-#pragma unroll
-      for (uint32_t k = 0; k < EXEC_RPT2; ++k) {
-        const uint32_t r = rb + k * EXH_T + uint32_t(t);
-        w2[k] = r < nrec ? a.recs[r0 + r] : 0ull;
-      }
-#pragma unroll
-      for (uint32_t k = 0; k < EXEC_RPT2; ++k)
-        if (rb + k * EXH_T + uint32_t(t) < nrec) copy_lit(w2[k]);
-    }
-  }
-  __syncthreads();
-  const uint32_t nlong = min(s_nlong, EXH_LONG);
-  for (uint32_t L = 0; L < nlong; ++L) {
-    const uint64_t wl = s_long[L];
-    const uint32_t ls = uint32_t(wl & 0xffff), n = uint32_t((wl >> 16) & 0xffff) + 1;
-    const uint8_t* ip = in + uint32_t(wl >> 32);
-    for (uint32_t i = t; i < n; i += EXH_T) bytes[ls + i] = ip[i];
-  }
-  __syncthreads();
-  // 4. the second half waits for the first half's bytes (its roots below 32 KiB)
-  if (h) {
-    if (t == 0) {
-      uint32_t f = 0;
-      for (uint32_t it = 0; it < EXH_WAIT; ++it) {  // relaxed polls (L1 bypass), one acquire after
-        f = __hip_atomic_load(&a.half_flag[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (f) break;
-        __builtin_amdgcn_s_sleep(2);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // this CU's L1: once per workgroup
-      s_flag = f;
-    }
-    __syncthreads();
-    if (s_flag != 1u) {  // the first half failed or never published
-      if (t == 0) atomicOr(&a.pages_bad[p], 128u);
-      return;
-    }
-  }
-  // 5. gather and store the thread's groups
-  uint8_t* dst = out + bs + base;
-  const uint8_t* first = out + bs;  // the first half's published bytes
-  auto byte_of = [&](uint32_t r) -> uint32_t {
-    return r >= base ? uint32_t(bytes[(r - base) & (SNAP_HALF - 1)]) : uint32_t(first[r]);
-  };
-  uint32_t word[16];
-#pragma unroll
-  for (uint32_t j = 0; j < 16; ++j) {
-    const uint32_t r01 = xp[2 * j], r23 = xp[2 * j + 1];
-    word[j] = byte_of(r01 & 0xffffu) | (byte_of(r01 >> 16) << 8) | (byte_of(r23 & 0xffffu) << 16) | (byte_of(r23 >> 16) << 24);
-  }
-  if ((reinterpret_cast<uintptr_t>(dst) & 3) == 0 && hbytes == SNAP_HALF) {  // block-uniform
-#pragma unroll
-    for (uint32_t j = 0; j < 16; ++j) *reinterpret_cast<uint32_t*>(dst + 4 * (uint32_t(t) + EXH_T * j)) = word[j];
-  } else {  // a page's last block: bytes back to the LDS, then byte stores
-    __syncthreads();
-    uint32_t* b32 = reinterpret_cast<uint32_t*>(src);
-#pragma unroll
-    for (uint32_t j = 0; j < 16; ++j) b32[uint32_t(t) + EXH_T * j] = word[j];
-    __syncthreads();
-    for (uint32_t i = t; i < hbytes; i += EXH_T) dst[i] = bytes[i];
-  }
-  publish(1u);
-}
-
 // Serial fallback for pages whose structure the parallel path could not use.
 __global__ void k_snap_serial(SnappyArgs a) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1219,13 +884,6 @@ __global__ void __launch_bounds__(256) k_page_copy(const CopyJob* jobs, uint32_t
 
 uint32_t snappy_wg_chunks() { return dev::WG_CHUNKS; }
 uint32_t snappy_chunk_bytes() { return dev::SNAP_CH; }
-bool snappy_exec_halves() {
-  static const bool on = [] {
-    const char* e = std::getenv("DR_EXEC_HALVES");
-    return e ? std::atoi(e) != 0 : false;
-  }();
-  return on;
-}
 
 void launch_snappy(const SnappyArgs& a, hipStream_t st, ScanScratch scan_scratch) {
   if (!a.npages) return;
@@ -1239,8 +897,7 @@ void launch_snappy(const SnappyArgs& a, hipStream_t st, ScanScratch scan_scratch
   DR_LAUNCH(dev::k_snap_scan, dim3(a.npages), dim3(dev::SCAN_T), 0, st, a);
   launch_scan_u32(a.chunk_elems, a.chunk_rec_start, a.nchunks, scan_scratch, st);
   DR_LAUNCH(dev::k_snap_emit, dim3(a.nwg), dim3(2 * dev::WG_CHUNKS), 0, st, a);
-  if (a.half_rec) DR_LAUNCH(dev::k_snap_exec_half, dim3(2 * a.nblocks), dim3(dev::EXH_T), 0, st, a);
-  else DR_LAUNCH(dev::k_snap_exec, dim3(a.nblocks), dim3(dev::EXEC_T), 0, st, a);
+  DR_LAUNCH(dev::k_snap_exec, dim3(a.nblocks), dim3(dev::EXEC_T), 0, st, a);
   DR_LAUNCH(dev::k_snap_serial, dim3((a.npages + 63) / 64), dim3(64), 0, st, a);
 }
 

@@ -186,16 +186,9 @@ struct SnappyArgs {
   uint32_t* half_out = nullptr;
   uint32_t* half_elems = nullptr;
   const uint32_t* chunk_page = nullptr;  // [nchunks] page of each chunk
-  // two workgroups per 64 KiB block (k_snap_exec_half) when half_rec is set: the record holding
-  // byte 32 KiB of each block, the first halves' published flags (zeroed per launch) and the
-  // start-order ticket counter (zeroed per launch)
-  uint64_t* half_rec = nullptr;
-  uint32_t* half_flag = nullptr;
-  uint32_t* exec_ticket = nullptr;
 };
 uint32_t snappy_wg_chunks();
 uint32_t snappy_chunk_bytes();
-bool snappy_exec_halves();  // two workgroups per 64 KiB block (DR_EXEC_HALVES, default on)
 void launch_snappy(const SnappyArgs& a, hipStream_t st, ScanScratch scan_scratch);
 void launch_page_copy(const CopyJob* jobs, uint32_t njobs, hipStream_t st);
 

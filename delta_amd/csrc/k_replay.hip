@@ -538,9 +538,24 @@ __device__ bool bytes_equal16(const uint8_t* p, const uint8_t* q, uint32_t n) {
   const uint32_t po = uint32_t(reinterpret_cast<uintptr_t>(p) & 15), qo = uint32_t(reinterpret_cast<uintptr_t>(q) & 15);
   const uint32_t pblocks = (po + n + 15) >> 4, qblocks = (qo + n + 15) >> 4;
   const uint4 z = make_uint4(0, 0, 0, 0);
-  uint4 plo = n ? pa[0] : z, qlo = n ? qa[0] : z;
+  // the first 128 bytes: every 16-byte block of both paths requested before any is compared (a
+  // lane compares one pair alone, so one round trip instead of one per block)
+  constexpr uint32_t PRE = 9;
+  uint4 pb[PRE], qb[PRE];
+#pragma unroll
+  for (uint32_t k = 0; k < PRE; ++k) {
+    pb[k] = k < pblocks ? pa[k] : z;
+    qb[k] = k < qblocks ? qa[k] : z;
+  }
   uint32_t diff = 0;
-  for (uint32_t i = 0, k = 1; i < n; i += 16, ++k) {
+#pragma unroll
+  for (uint32_t k = 1; k < PRE; ++k) {
+    const uint32_t i = 16 * (k - 1);
+    if (i < n) diff |= block_diff(pb[k - 1], pb[k], po, qb[k - 1], qb[k], qo, n - i);
+  }
+  if (n <= 16 * (PRE - 1)) return diff == 0;
+  uint4 plo = pb[PRE - 1], qlo = qb[PRE - 1];
+  for (uint32_t i = 16 * (PRE - 1), k = PRE; i < n; i += 16, ++k) {
     const uint4 phi = k < pblocks ? pa[k] : z, qhi = k < qblocks ? qa[k] : z;
     diff |= block_diff(plo, phi, po, qlo, qhi, qo, n - i);
     plo = phi;

@@ -242,9 +242,41 @@ __global__ void __launch_bounds__(WG_CHUNKS) k_snap_spec(SnappyArgs a) {
   if (live) spec_store(a, w, a.chunk_base[g.p] + g.j0 + threadIdx.x);
 }
 
-// Walks chunk j of a page from `e` (a true element start) to its exit; 8-byte headers from global.
-__device__ __forceinline__ uint64_t walk_chunk(const uint8_t* in, uint64_t e, uint64_t ce) {
-  while (e < ce) e += snap_adv(snap_elem(in + e));
+// A lane's serial element walk from e (a true element start) to the end ce of its chunk through
+// its own 64-byte LDS window (`win`: the lane's 17-dword slot, padded against bank conflicts),
+// refilled with four 16-byte loads when the next header leaves it: one round trip per dozen or so
+// elements instead of one per element. Returns the exit; out / elems: the walked elements' output
+// bytes and count.
+constexpr uint32_t WIN_DW = 17;
+__device__ uint64_t walk_window(const uint8_t* in, uint64_t e, uint64_t ce, uint32_t* win, uint64_t* out,
+                                uint32_t* elems) {
+  const uintptr_t ib = reinterpret_cast<uintptr_t>(in);
+  uintptr_t wa = 0;
+  bool have = false;
+  uint64_t o = 0;
+  uint32_t k = 0;
+  while (e < ce) {
+    const uintptr_t ea = ib + e;
+    if (!have || ea < wa || ea + 8 > wa + 64) {  // reads reach at most 63 bytes past the page input (padded)
+      wa = ea & ~uintptr_t(15);
+      const uint4* g = reinterpret_cast<const uint4*>(wa);
+      const uint4 v0 = gload16(g), v1 = gload16(g + 1), v2 = gload16(g + 2), v3 = gload16(g + 3);
+      win[0] = v0.x; win[1] = v0.y; win[2] = v0.z; win[3] = v0.w;
+      win[4] = v1.x; win[5] = v1.y; win[6] = v1.z; win[7] = v1.w;
+      win[8] = v2.x; win[9] = v2.y; win[10] = v2.z; win[11] = v2.w;
+      win[12] = v3.x; win[13] = v3.y; win[14] = v3.z; win[15] = v3.w;
+      have = true;
+    }
+    const uint32_t r = uint32_t(ea - wa), di = r >> 2, sh = r & 3;
+    const uint64_t hdr = ((uint64_t(win[di + 1]) << 32) | win[di]) >> (8 * sh);  // 5 header bytes at least
+    uint32_t adv, len;
+    snap_step(hdr, &adv, &len);
+    o += len;
+    ++k;
+    e += adv;
+  }
+  *out = o;
+  *elems = k;
   return e;
 }
 
@@ -253,6 +285,7 @@ __device__ __forceinline__ uint64_t walk_chunk(const uint8_t* in, uint64_t e, ui
 // speculative chain (visited bitmap) -> spec_exit[c] (chains that meet coincide); otherwise a
 // serial walk of the chunk from a.
 __global__ void __launch_bounds__(256) k_snap_assume(SnappyArgs a) {
+  __shared__ uint32_t wins[256 * WIN_DW];
   const uint32_t c = blockIdx.x * 256 + threadIdx.x;
   if (c >= a.nchunks) return;
   const uint32_t p = chunk_page(a, c);
@@ -265,7 +298,11 @@ __global__ void __launch_bounds__(256) k_snap_assume(SnappyArgs a) {
   if (e >= ce) x = e;
   else if (j == 0 || ((a.vis[uint64_t(c) * (SNAP_CH / 32) + uint32_t((e - cs) >> 5)] >> ((e - cs) & 31)) & 1u))
     x = a.spec_exit[c];
-  else x = walk_chunk(reinterpret_cast<const uint8_t*>(pg.in), e, ce);
+  else {
+    uint64_t o;
+    uint32_t k;
+    x = walk_window(reinterpret_cast<const uint8_t*>(pg.in), e, ce, wins + threadIdx.x * WIN_DW, &o, &k);
+  }
   a.assumed_exit[c] = uint32_t(min(x, uint64_t(0xffffffffu)));
 }
 
@@ -428,6 +465,7 @@ __global__ void __launch_bounds__(64) k_snap_resolve(SnappyArgs a) {
 // C: output bytes / elements produced by the true elements of each chunk: the speculative counts
 // unless the true entry differs from the chunk's first speculatively visited position.
 __global__ void __launch_bounds__(256) k_snap_count(SnappyArgs a) {
+  __shared__ uint32_t wins[256 * WIN_DW];
   const uint32_t c = blockIdx.x * 256 + threadIdx.x;
   if (c >= a.nchunks) return;
   const uint32_t pos0 = a.entry[c];
@@ -437,15 +475,9 @@ __global__ void __launch_bounds__(256) k_snap_count(SnappyArgs a) {
   const SnapPage& pg = a.pages[p];
   const uint64_t cs = uint64_t(c - a.chunk_base[p]) * SNAP_CH;
   const uint64_t ce = min(cs + SNAP_CH, uint64_t(pg.n_in));
-  const uint8_t* in = reinterpret_cast<const uint8_t*>(pg.in);
-  uint64_t pos = pos0, out = 0;
+  uint64_t out = 0;
   uint32_t elems = 0;
-  while (pos < ce) {
-    const Elem el = snap_elem(in + pos);
-    out += el.len;
-    ++elems;
-    pos += snap_adv(el);
-  }
+  walk_window(reinterpret_cast<const uint8_t*>(pg.in), pos0, ce, wins + threadIdx.x * WIN_DW, &out, &elems);
   a.chunk_out[c] = out > 0xffffffffull ? 0xffffffffu : uint32_t(out);
   a.chunk_elems[c] = elems;
 }

@@ -85,9 +85,11 @@ def algorithmic_bytes(kernel, plan, counts):
         fa = counts["num_file_actions"]
         surv = counts["num_files"] + counts["num_removes"]
         table.update({
-            "k_bucket_hist": 30 * n,                               # kind, flags, key, path ref in; packed ref out
-            "k_bucket_scatter": 18 * n + 16 * fa,                  # kind, flags, key, size/delTs in; 16 B record out
-            "k_bucket_reduce": 16 * fa + 4 * surv,
+            "k_bucket_hist": 10 * n,                               # kind, flags, key in
+            # kind, flags, key, path address + length in; size or delTs per file action in; 16 B record +
+            # 8 B path reference out
+            "k_bucket_scatter": 22 * n + 32 * fa,
+            "k_bucket_reduce": 16 * fa + 4 * surv,                 # records in, survivors out (+ verification)
             "k_compact2": 8 * surv,
         })
     if kernel in ("k_snap_emit", "k_snap_exec") and not el:
@@ -391,6 +393,35 @@ def measure_filter(eng, staged, cutoff, exp, steps):
             "kernels": {k: round(v, 4) for k, v in ms.items()}}
 
 
+def merge_rank_reports(every):
+    """Rank 0's view of an N > 1 run from every rank's {"rank", "roofline", "pipelines"}: the roofline of
+    the rank whose dominant kernel takes longest (the step waits for the slowest rank) with each rank's
+    kernel, time and fraction listed, and per pipeline the slowest rank's entry with every rank's
+    fraction."""
+    roofline = None
+    rl = [g for g in every if g.get("roofline")]
+    if rl:
+        worst = max(rl, key=lambda g: g["roofline"]["avg_launch_ms"])
+        roofline = dict(worst["roofline"], rank=worst["rank"],
+                        per_rank=[{"rank": g["rank"], "kernel": g["roofline"]["kernel"],
+                                   "avg_launch_ms": g["roofline"]["avg_launch_ms"], "frac": g["roofline"]["frac"]}
+                                  for g in rl],
+                        note="the slowest rank's dominant kernel (max avg_launch_ms over ranks); traffic is null: "
+                             "the committed PMC passes are single-GPU")
+    pipelines = {}
+    names = []
+    for g in every:
+        names += [n for n in (g.get("pipelines") or {}) if n not in names]
+    for name in names:
+        pr = [(g["rank"], g["pipelines"][name]) for g in every if (g.get("pipelines") or {}).get(name)]
+        if pr:
+            r_w, worst = max(pr, key=lambda x: x[1]["ms"])
+            pipelines[name] = dict(worst, rank=r_w, per_rank_frac=[p["frac"] for _, p in pr])
+        else:
+            pipelines[name] = None
+    return roofline, pipelines
+
+
 def launch_ranks(args) -> int:
     """`--gpus N` (N > 1) without a launcher around us: start N rank processes of this same command
     through torch.distributed.run (one rank per GPU, rendezvous on 127.0.0.1) and return their exit
@@ -494,8 +525,9 @@ def main():
         def step():
             st = comm.replay_sharded(staged, cutoff)
             c = st.counts  # table-wide counters (all-reduced inside the library)
+            lc = st.local_counts()  # this rank's own (K3/K4 pricing)
             st.release()
-            return c, None
+            return c, lc
     else:
         from delta_amd.sharded import Exchange, replay_sharded, stage_shard
         staged = stage_shard(eng, log_path, world, rank)
@@ -556,8 +588,6 @@ def main():
     total_actions = counts["num_actions"] * args.steps  # table-wide actions per step
     value = total_actions / elapsed
     ms_per_step = elapsed / args.steps * 1000.0
-    if rank != 0:
-        return
     kernels = {}
     for k, ms in kern_ms.items():
         per_step = ms / prof_steps
@@ -595,10 +625,19 @@ def main():
         # compulsory SNAPPY traffic: compressed pages in, decompressed pages out
         "snappy": pipeline(SNAPPY, plan["snappy_in_bytes"] + plan["snappy_out_bytes"]),
         # K3 + K4 together against SURVEY.md §8(d)'s headline budget: 32 B/action (sort) + 37 B/action
-        # (reduce, retention, compaction) = 69 B/action
+        # (reduce, retention, compaction) = 69 B/action; at N > 1 per rank, on the actions it reduced
         "sort_reduce": dict(pipeline(SORT_REDUCE, 69 * local_counts["num_actions"]), target_frac=0.5)
         if local_counts else None,
     }
+    if dist:
+        # every rank's roofline and pipelines to rank 0: the line reports the slowest rank's (the step
+        # waits for it) and lists each rank's
+        every = [None] * world
+        dist.all_gather_object(every, {"rank": rank, "roofline": roofline, "pipelines": pipelines})
+        if rank == 0:
+            roofline, pipelines = merge_rank_reports(every)
+    if rank != 0:
+        return
     if world == 1:
         # full-record checksums of both sides on the device (untimed), for the full-size parity gate
         st = staged.replay(cutoff)
@@ -608,26 +647,42 @@ def main():
         st.release()
         counts = dict(counts, live_record_sum=rec[0], tomb_record_sum=rec[1])
     cpu = None
-    if not args.no_cpu_baseline and world == 1:
-        cpu = cpu_baseline(log_path, cutoff, counts, args.cpu_threads, one_core=args.config != 4)
+    if not args.no_cpu_baseline:
+        # rank 0, outside the timed region; at N > 1 the other ranks have finished their steps, and the
+        # restatement replays the same full table
+        cpu = cpu_baseline(log_path, cutoff, counts, args.cpu_threads, one_core=args.config != 4 and world == 1)
     # end to end once: file bytes -> HBM (read + H2D + page planning), replay, allFiles export
     e2e = None
     if world == 1:
         import ctypes as C
         from delta_amd import _native as N
-        t1 = time.perf_counter()
-        st = staged.replay(cutoff)
-        torch.cuda.synchronize()
-        t2 = time.perf_counter()
-        # allFiles + tombstones as host columns (dr_state_export: device extraction + one copy)
-        ex = N.dr_export()
-        for which in (N.DR_LIVE, N.DR_TOMBSTONES):
-            eng.check(eng.lib.dr_state_export(st.h, which, C.byref(ex)))
-        t3 = time.perf_counter()
-        st.release()
-        e2e = {"stage_s": round(stage_s, 3), "replay_s": round(t2 - t1, 4), "export_s": round(t3 - t2, 4),
-               "actions_per_s_incl_staging": round(counts["num_actions"] / (stage_s + t2 - t1), 1),
-               "actions_per_s_incl_staging_and_export": round(counts["num_actions"] / (stage_s + t3 - t1), 1)}
+        def e2e_once():
+            t1 = time.perf_counter()
+            st = staged.replay(cutoff)
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            mat_bytes = st.materialize()  # every field of both sides extracted on the device, resident
+            t3 = time.perf_counter()
+            # allFiles + tombstones as host columns (dr_state_export: the resident columns, one
+            # asynchronous copy per column into one pinned block, one synchronisation)
+            ex = N.dr_export()
+            for which in (N.DR_LIVE, N.DR_TOMBSTONES):
+                eng.check(eng.lib.dr_state_export(st.h, which, C.byref(ex)))
+            t4 = time.perf_counter()
+            st.release()
+            return t2 - t1, t3 - t2, t4 - t3, mat_bytes
+
+        rep_s, mat_s, d2h_s, mat_bytes = e2e_once()   # first export: pins its host block
+        rep2, mat2, d2h2, _ = e2e_once()              # a later snapshot's: the context's pinned cache
+        e2e = {"stage_s": round(stage_s, 3), "replay_s": round(rep_s, 4),
+               "materialize_s": round(mat_s, 4), "materialized_ms": round((rep_s + mat_s) * 1e3, 2),
+               "materialized_bytes": mat_bytes, "d2h_s": round(d2h_s, 4), "export_s": round(mat_s + d2h_s, 4),
+               "export_s_cached_pinned": round(mat2 + d2h2, 4),
+               "actions_per_s_incl_staging": round(counts["num_actions"] / (stage_s + rep_s), 1),
+               "actions_per_s_incl_staging_and_export": round(counts["num_actions"] / (stage_s + rep_s + mat_s + d2h_s),
+                                                              1),
+               "note": "materialized_ms = replay + device extraction of every field of both sides (no D2H): the "
+                       "resident full-record state; export_s = that extraction + the copy to pinned host columns"}
     k5 = ckpt = None
     if world == 1 and args.config == 4:
         k5 = measure_filter(eng, staged, cutoff, exp, args.steps)

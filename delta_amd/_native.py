@@ -31,13 +31,14 @@ DR_FLAG_REDUCE64 = 0x4
 
 # Exported symbols (checked by tests/test_native_abi.py against include/deltareplay.h).
 SYMBOLS = [
-    "dr_abi_version", "dr_ctx_create", "dr_ctx_destroy", "dr_last_error", "dr_log_segment",
+    "dr_abi_version", "dr_ctx_create", "dr_ctx_destroy", "dr_last_error", "dr_state_last_error",
+    "dr_comm_last_error", "dr_log_segment",
     "dr_stage", "dr_stage_named", "dr_stage_log", "dr_comm_unique_id", "dr_comm_loopback_id", "dr_comm_create",
     "dr_comm_release",
     "dr_replay_sharded", "dr_staged_release", "dr_staged_bytes", "dr_staged_plan",
     "dr_replay_staged",
-    "dr_replay", "dr_state_release", "dr_state_apply", "dr_state_counts", "dr_state_nonfile_json", "dr_state_check_checksum",
-    "dr_state_export", "dr_state_record_sums", "dr_state_write_checkpoint", "dr_state_set_nonfile_json", "dr_filter", "dr_state_scan_order", "dr_state_partition_groups", "dr_free", "dr_last_timings", "dr_set_timing", "dr_set_timing_only",
+    "dr_replay", "dr_state_release", "dr_state_apply", "dr_state_counts", "dr_state_local_counts", "dr_state_nonfile_json", "dr_state_check_checksum",
+    "dr_state_export", "dr_state_materialize", "dr_state_record_sums", "dr_state_write_checkpoint", "dr_state_set_nonfile_json", "dr_filter", "dr_state_scan_order", "dr_state_partition_groups", "dr_free", "dr_last_timings", "dr_set_timing", "dr_set_timing_only",
     "dr_shard_plan", "dr_stage_log_shard", "dr_shard_begin", "dr_shard_pack", "dr_shard_reduce",
     "dr_shard_finish", "dr_shard_release", "dr_parse_commits", "dr_parsed_release",
 ]
@@ -125,6 +126,9 @@ def load(path: str = LIB_PATH) -> C.CDLL:
     lib = C.CDLL(path)
     vp, i32, i64, u64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64
     sig = {
+        "dr_state_last_error": ([vp], C.c_char_p),
+        "dr_comm_last_error": ([vp], C.c_char_p),
+        "dr_state_materialize": ([vp, C.POINTER(C.c_uint64)], C.c_int),
         "dr_abi_version": ([], C.c_int),
         "dr_ctx_create": ([C.c_int, C.POINTER(vp)], C.c_int),
         "dr_ctx_destroy": ([vp], None),
@@ -145,6 +149,7 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "dr_replay": ([vp, C.POINTER(dr_file), i32, i64, C.c_uint32, C.POINTER(vp)], C.c_int),
         "dr_state_release": ([vp], C.c_int),
         "dr_state_counts": ([vp, C.POINTER(dr_counts)], C.c_int),
+        "dr_state_local_counts": ([vp, C.POINTER(dr_counts)], C.c_int),
         "dr_state_nonfile_json": ([vp, C.POINTER(C.c_char_p), C.POINTER(u64)], C.c_int),
         "dr_state_apply": ([vp, vp, vp, C.c_int64, C.c_uint32, C.POINTER(vp)], C.c_int),
         "dr_state_check_checksum": ([vp, C.c_char_p, u64, C.c_char_p, u64, C.POINTER(u64)], C.c_int),

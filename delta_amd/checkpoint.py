@@ -232,7 +232,7 @@ def write_part(state, log_path: str, version: int, part: int, parts: int, row_gr
     path = checkpoint_file_with_parts(log_path, version, part, parts)
     tmp = os.path.join(os.path.dirname(path), ".%s.tmp" % os.path.basename(path))
     pq.write_table(table, tmp, compression="snappy", row_group_size=row_group_size, write_statistics=False,
-                   use_deprecated_int96_timestamps=True)
+                   use_deprecated_int96_timestamps=True, store_decimal_as_integer=True)
     os.replace(tmp, path)
     return table.num_rows
 
@@ -270,8 +270,7 @@ def write_checkpoint(snapshot, parts: int = 1, row_group_size: int = 1 << 20) ->
     `_last_checkpoint`; returns the CheckpointMetaData written there."""
     import pyarrow.parquet as pq
     table, n_adds = checkpoint_table(snapshot.state)
-    if n_adds != snapshot.num_of_files:  # D/Checkpoints.scala:310-313
-        raise RuntimeError("State of the checkpoint doesn't match that of the snapshot.")
+    check_add_rows(n_adds, snapshot.num_of_files)  # D/Checkpoints.scala:325-328
     log_path = snapshot.delta_log.log_path
     rows = table.num_rows
     if parts <= 1:
@@ -283,8 +282,10 @@ def write_checkpoint(snapshot, parts: int = 1, row_group_size: int = 1 << 20) ->
         slices = [table.slice(i * step, max(0, min(step, rows - i * step))) for i in range(parts)]
     for path, t in zip(paths, slices):
         tmp = os.path.join(os.path.dirname(path), ".%s.tmp" % os.path.basename(path))
+        # decimals as Spark's non-legacy layout: INT32 up to precision 9, INT64 up to 18 (the device
+        # writer's), FIXED_LEN_BYTE_ARRAY beyond
         pq.write_table(t, tmp, compression="snappy", row_group_size=row_group_size, write_statistics=False,
-                       use_deprecated_int96_timestamps=True)
+                       use_deprecated_int96_timestamps=True, store_decimal_as_integer=True)
         os.replace(tmp, path)  # a reader never sees a partial part
     meta = {"version": snapshot.version, "size": rows}
     if parts > 1:

@@ -141,6 +141,48 @@ struct dr_ctx {
     std::lock_guard<std::mutex> g(mu);
     free_blocks.emplace(sizes[p], p);
   }
+  // pinned host blocks (hipHostMalloc) for the export columns, cached like the device blocks: a
+  // released state's block serves the next export of a similar size without pinning pages again
+  std::multimap<size_t, void*> host_free;
+  std::unordered_map<void*, size_t> host_sizes;
+  void* host_alloc(size_t n) {
+    n = (n + 4095) & ~size_t(4095);
+    if (n == 0) n = 4096;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      auto it = host_free.lower_bound(n);
+      if (it != host_free.end() && it->first <= 2 * n + (size_t(16) << 20)) {
+        void* p = it->second;
+        host_free.erase(it);
+        return p;
+      }
+    }
+    void* p = nullptr;
+    if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      host_trim();
+      if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        fail(DR_E_OOM, fmt("pinned host allocation of %zu bytes failed", n));
+      }
+    }
+    std::lock_guard<std::mutex> g(mu);
+    host_sizes[p] = n;
+    return p;
+  }
+  void host_release(void* p) {
+    if (!p) return;
+    std::lock_guard<std::mutex> g(mu);
+    host_free.emplace(host_sizes[p], p);
+  }
+  void host_trim() {
+    std::lock_guard<std::mutex> g(mu);
+    for (auto& kv : host_free) {
+      (void)hipHostFree(kv.second);
+      host_sizes.erase(kv.second);
+    }
+    host_free.clear();
+  }
   void trim() {
     std::lock_guard<std::mutex> g(mu);
     for (auto& kv : free_blocks) {
@@ -443,13 +485,27 @@ struct NoInitAlloc : std::allocator<T> {
 template <typename T>
 using hvec = std::vector<T, NoInitAlloc<T>>;
 
+struct DevExport;  // the device export columns of one side (defined with export_device)
+
+// One side of dr_state_export on the host: every column a slice of one pinned block (the context's
+// cache), filled by asynchronous copies from the device export and one stream synchronisation.
 struct ExportCols {
   bool built = false;
   int64_t n = 0;
-  hvec<int64_t> path_off, size, mtime, delts, stats_off, pv_entry_off, pv_key_off, pv_val_off, tags_entry_off,
-      tags_key_off, tags_val_off;
-  hvec<uint8_t> path_bytes, delts_valid, efm, stats_bytes, stats_null, pv_null, pv_key_bytes, pv_val_bytes, pv_val_null,
-      tags_null, tags_key_bytes, tags_val_bytes, tags_val_null;
+  dr_ctx* ctx = nullptr;
+  void* block = nullptr;
+  int64_t *path_off = nullptr, *size = nullptr, *mtime = nullptr, *delts = nullptr, *stats_off = nullptr,
+          *pv_entry_off = nullptr, *pv_key_off = nullptr, *pv_val_off = nullptr, *tags_entry_off = nullptr,
+          *tags_key_off = nullptr, *tags_val_off = nullptr;
+  uint8_t *path_bytes = nullptr, *delts_valid = nullptr, *efm = nullptr, *stats_bytes = nullptr, *stats_null = nullptr,
+          *pv_null = nullptr, *pv_key_bytes = nullptr, *pv_val_bytes = nullptr, *pv_val_null = nullptr,
+          *tags_null = nullptr, *tags_key_bytes = nullptr, *tags_val_bytes = nullptr, *tags_val_null = nullptr;
+  ExportCols() = default;
+  ExportCols(const ExportCols&) = delete;
+  ExportCols& operator=(const ExportCols&) = delete;
+  ~ExportCols() {
+    if (block && ctx) ctx->host_release(block);
+  }
 };
 
 // D2H into a host vector without initialising it first.
@@ -517,6 +573,10 @@ struct dr_state {
   DBuf<uint32_t> live, tomb;   // survivor action indices (hash order per bucket)
   uint64_t n_live = 0, n_tomb = 0;
   dr_counts counts{};
+  // a rank of the library's sharded replay: its own counters before the all-reduce (what the
+  // torch driver's local state reports), for per-rank roofline accounting
+  dr_counts local_counts{};
+  bool has_local_counts = false;
   std::string nonfile_json;
   std::vector<NonFileAction> nonfile;  // winners: protocol, metadata, txns
   ExportCols exp[2];
@@ -537,6 +597,9 @@ struct dr_state {
   std::vector<std::shared_ptr<DBuf<uint8_t>>> pv_arenas;  // unescaped string values
   // export: the checkpoint's add / remove leaves, decoded on the first export of each side
   std::shared_ptr<ExpDecoded> exp_dec[2];
+  // the materialised state (dr_state_materialize): every field of both sides extracted on the device
+  // and kept resident -- the reference's cached SingleAction rows (D/util/StateCache.scala:45-68)
+  std::shared_ptr<DevExport> dexp[2];
 };
 
 // ---------------------------------------------------------------------------------------------------
@@ -1296,7 +1359,7 @@ static std::shared_ptr<StagedData> stage_files(dr_ctx* ctx, const dr_file* files
 // ---------------------------------------------------------------------------------------------------
 // replay
 // ---------------------------------------------------------------------------------------------------
-// Buckets average <= 2048 file actions (the reduce's LDS table holds 8192), capped by the scatter's
+// Buckets average <= 2048 file actions (the reduce keeps up to 3072 per pass in its 4096-slot LDS table), capped by the scatter's
 // LDS cursors; larger buckets are reduced in sub-passes.
 static int bucket_bits_for(uint64_t n) {
   int bits = 0;
@@ -1346,6 +1409,7 @@ struct ParsePending {
   DBuf<uint64_t> nonfile;   // {line, byte offset} pairs
   uint64_t R = 0, nlines = 0;
   uint64_t canon_cap = 0;   // arena bytes given to k_canon (0: no canonicalisation launched)
+  const void* canon_arena = nullptr;  // that arena (st->arenas' last entry when launched)
   bool canonicalize = false;
   bool canon_sized = false; // the arena was sized from the counters (exact), not from a hint
   size_t pin_at = 0;        // where its words land in ctx->pinned()
@@ -1502,6 +1566,7 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
     }
     if (cap) {
       st->arenas.push_back(std::make_shared<DBuf<uint8_t>>(ctx, cap));
+      pp.canon_arena = st->arenas.back()->p;
       CanonArgs cg{act, N, st->arenas.back()->p, cap, counters.p + 4};
       launch_canon(cg, stream);
     }
@@ -1544,6 +1609,10 @@ static bool parse_finish(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr_
       return false;
     }
     s.canon_need.store(int64_t(need));
+    // no special path: nothing points into the arena sized from the segment's bytes (a commit-only
+    // segment's bound is ~2x its JSON) -- it is not kept for the life of the state
+    if (cnt[0] == 0 && pp.canon_arena && !st->arenas.empty() && st->arenas.back()->p == pp.canon_arena)
+      st->arenas.pop_back();
   }
   nf = s.ck_nonfile;
   const uint64_t nnf = std::min<uint64_t>(cnt[2], nlines);
@@ -1617,7 +1686,7 @@ static ReducePending reduce_launch(dr_ctx* ctx, dr_state* st, int64_t cutoff, ui
   DBuf<uint32_t> tcnt(ctx, ncell);
   DBuf<uint64_t> toff(ctx, ncell + 1), boff(ctx, nb + 1);
   DBuf<uint8_t> pscratch(ctx, scan_scratch_for(ncell));
-  DBuf<uint64_t> pref(ctx, N);
+  DBuf<uint64_t> pref(ctx, N);  // packed path references in action order (k_bucket_hist -> k_bucket_verify)
   PartitionArgs pa{st->kind.p, st->flags.p, st->key.p, st->size.p, st->delts.p, N, cutoff, bits, nt,
                    tcnt.p, toff.p, nullptr, st->path_ptr.p, st->path_len.p, pref.p};
   DBuf<PartRec> rec(ctx, N);
@@ -1632,7 +1701,7 @@ static ReducePending reduce_launch(dr_ctx* ctx, dr_state* st, int64_t cutoff, ui
   DBuf<uint2> opair(ctx, N);
   DBuf<unsigned long long> totals(ctx, 8), bstats(ctx, uint64_t(nb) * 5);
   totals.zero(stream);
-  ReduceArgs ra{rec.p, boff.p, nb, bits, st->key.p, st->path_ptr.p, st->path_len.p, olive.p, otomb.p, opair.p, pref.p,
+  ReduceArgs ra{rec.p, boff.p, nb, bits, st->size.p, st->path_ptr.p, st->path_len.p, olive.p, otomb.p, opair.p, pref.p,
                 lcount.p, tcount.p, pcount.p, totals.p, rlist.p, xlist.p, bstats.p};
   auto upload_list = [&](const std::vector<uint32_t>& v) {
     DBuf<uint32_t> d(ctx, v.size());
@@ -1651,7 +1720,7 @@ static ReducePending reduce_launch(dr_ctx* ctx, dr_state* st, int64_t cutoff, ui
     }
   } else {
     launch_bucket_reduce(ra, stream);
-    launch_bucket_verify(ra, stream);
+    launch_bucket_verify(ra, stream);  // byte verification of every merged pair
     // the fallbacks read their bucket lists' lengths on the device (no host round trip)
     launch_bucket_reduce64(ra, rlist.p, nb, stream, totals.p + 3);
     launch_bucket_exact(ra, xlist.p, nb, stream, totals.p + 4);
@@ -2375,13 +2444,22 @@ static void export_device(dr_state& st, int which, DevExport& X, uint64_t lo = 0
   launch_export(a, stream);  // pass 2: bytes and entries
 }
 
+// Both sides' device export columns, built once per state and kept until its release.
+static const DevExport& materialize(dr_state& st, int which) {
+  if (!st.dexp[which]) {
+    auto X = std::make_shared<DevExport>();
+    export_device(st, which, *X);
+    st.dexp[which] = X;
+  }
+  return *st.dexp[which];
+}
+
 // Order-free full-record checksum of one side (dr_state_record_sums): k_record_hash over the
 // side's device export columns.
 static uint64_t record_sum(dr_state& st, int which) {
   dr_ctx* ctx = st.ctx;
   hipStream_t stream = ctx->stream;
-  DevExport X;
-  export_device(st, which, X);
+  const DevExport& X = materialize(st, which);
   DBuf<unsigned long long> sum(ctx, 1);
   sum.zero(stream);
   RecordHashArgs a{};
@@ -2423,40 +2501,53 @@ static void build_export(dr_state& st, int which) {
   if (ex.built) return;
   dr_ctx* ctx = st.ctx;
   hipStream_t stream = ctx->stream;
-  DevExport X;
-  export_device(st, which, X);
+  const DevExport& X = materialize(st, which);
   const uint64_t n = X.n;
   ex.n = int64_t(n);
-  // u64 offsets and delTs are copied as int64 (same bits); delTs validity is F_HAS_DELTS
-  d2h_into(ex.path_off, reinterpret_cast<const int64_t*>(X.path_off.p), n + 1, stream);
-  d2h_into(ex.path_bytes, X.path_bytes.p, n ? uint64_t(ex.path_off[n]) : 0, stream);
-  d2h_into(ex.delts, reinterpret_cast<const int64_t*>(X.delts.p), n, stream);
-  d2h_into(ex.delts_valid, X.flags.p, n, stream);
-  for (uint64_t i = 0; i < n; ++i) {
-    ex.delts_valid[i] &= 1u;  // F_HAS_DELTS
-    if (!ex.delts_valid[i]) ex.delts[i] = 0;
+  ex.ctx = ctx;
+  // delTs validity is F_HAS_DELTS, and an absent delTs reads 0 (one device pass, no host loop)
+  DBuf<uint8_t> dvalid(ctx, n);
+  DBuf<int64_t> ddelts(ctx, n);
+  launch_delts_fix(X.flags.p, reinterpret_cast<const int64_t*>(X.delts.p), n, dvalid.p, ddelts.p, stream);
+  const uint64_t nb = n ? d2h_one(X.path_off.p + n, stream) : 0;
+  // carve the columns out of one pinned block (8-byte aligned slices), then queue every copy
+  struct Col { void** dst; const void* src; uint64_t bytes; };
+  std::vector<Col> cols = {
+      {(void**)&ex.path_off, X.path_off.p, 8 * (n + 1)},
+      {(void**)&ex.path_bytes, X.path_bytes.p, nb},
+      {(void**)&ex.delts, ddelts.p, 8 * n},
+      {(void**)&ex.delts_valid, dvalid.p, n},
+      {(void**)&ex.size, X.size.p, 8 * n},
+      {(void**)&ex.mtime, X.mtime.p, 8 * n},
+      {(void**)&ex.efm, X.efm.p, n},
+      {(void**)&ex.stats_null, X.stats_null.p, n},
+      {(void**)&ex.pv_null, X.pv_null.p, n},
+      {(void**)&ex.tags_null, X.tags_null.p, n},
+      {(void**)&ex.stats_off, X.off[EXC_STATS].p, 8 * (n + 1)},
+      {(void**)&ex.pv_entry_off, X.off[EXC_PV_N].p, 8 * (n + 1)},
+      {(void**)&ex.tags_entry_off, X.off[EXC_TAGS_N].p, 8 * (n + 1)},
+      {(void**)&ex.stats_bytes, X.stats_bytes.p, X.tot[EXC_STATS]},
+      {(void**)&ex.pv_key_off, X.pv_key_off.p, 8 * (X.tot[EXC_PV_N] + 1)},
+      {(void**)&ex.pv_val_off, X.pv_val_off.p, 8 * (X.tot[EXC_PV_N] + 1)},
+      {(void**)&ex.pv_val_null, X.pv_val_null.p, X.tot[EXC_PV_N]},
+      {(void**)&ex.pv_key_bytes, X.pv_key_bytes.p, X.tot[EXC_PV_KB]},
+      {(void**)&ex.pv_val_bytes, X.pv_val_bytes.p, X.tot[EXC_PV_VB]},
+      {(void**)&ex.tags_key_off, X.tags_key_off.p, 8 * (X.tot[EXC_TAGS_N] + 1)},
+      {(void**)&ex.tags_val_off, X.tags_val_off.p, 8 * (X.tot[EXC_TAGS_N] + 1)},
+      {(void**)&ex.tags_val_null, X.tags_val_null.p, X.tot[EXC_TAGS_N]},
+      {(void**)&ex.tags_key_bytes, X.tags_key_bytes.p, X.tot[EXC_TAGS_KB]},
+      {(void**)&ex.tags_val_bytes, X.tags_val_bytes.p, X.tot[EXC_TAGS_VB]},
+  };
+  uint64_t total = 0;
+  for (const Col& c : cols) total += (c.bytes + 63) & ~uint64_t(63);
+  ex.block = ctx->host_alloc(total);
+  uint8_t* at = static_cast<uint8_t*>(ex.block);
+  for (const Col& c : cols) {
+    *c.dst = at;
+    if (c.bytes) HIP_OK(hipMemcpyAsync(at, c.src, c.bytes, hipMemcpyDeviceToHost, stream));
+    at += (c.bytes + 63) & ~uint64_t(63);
   }
-  (void)ctx;
-  d2h_into(ex.size, X.size.p, n, stream);
-  d2h_into(ex.mtime, X.mtime.p, n, stream);
-  d2h_into(ex.efm, X.efm.p, n, stream);
-  d2h_into(ex.stats_null, X.stats_null.p, n, stream);
-  d2h_into(ex.pv_null, X.pv_null.p, n, stream);
-  d2h_into(ex.tags_null, X.tags_null.p, n, stream);
-  d2h_into(ex.stats_off, reinterpret_cast<const int64_t*>(X.off[EXC_STATS].p), n + 1, stream);
-  d2h_into(ex.pv_entry_off, reinterpret_cast<const int64_t*>(X.off[EXC_PV_N].p), n + 1, stream);
-  d2h_into(ex.tags_entry_off, reinterpret_cast<const int64_t*>(X.off[EXC_TAGS_N].p), n + 1, stream);
-  d2h_into(ex.stats_bytes, X.stats_bytes.p, X.tot[EXC_STATS], stream);
-  d2h_into(ex.pv_key_off, X.pv_key_off.p, X.tot[EXC_PV_N] + 1, stream);
-  d2h_into(ex.pv_val_off, X.pv_val_off.p, X.tot[EXC_PV_N] + 1, stream);
-  d2h_into(ex.pv_val_null, X.pv_val_null.p, X.tot[EXC_PV_N], stream);
-  d2h_into(ex.pv_key_bytes, X.pv_key_bytes.p, X.tot[EXC_PV_KB], stream);
-  d2h_into(ex.pv_val_bytes, X.pv_val_bytes.p, X.tot[EXC_PV_VB], stream);
-  d2h_into(ex.tags_key_off, X.tags_key_off.p, X.tot[EXC_TAGS_N] + 1, stream);
-  d2h_into(ex.tags_val_off, X.tags_val_off.p, X.tot[EXC_TAGS_N] + 1, stream);
-  d2h_into(ex.tags_val_null, X.tags_val_null.p, X.tot[EXC_TAGS_N], stream);
-  d2h_into(ex.tags_key_bytes, X.tags_key_bytes.p, X.tot[EXC_TAGS_KB], stream);
-  d2h_into(ex.tags_val_bytes, X.tags_val_bytes.p, X.tot[EXC_TAGS_VB], stream);
+  HIP_OK(hipStreamSynchronize(stream));
   ex.built = true;
 }
 
@@ -2719,16 +2810,15 @@ static void fix_fp_values(dr_ctx* ctx, dr_state::PvCol& col, const DBuf<uint64_t
     }
     if (end != t.c_str() + t.size()) nulls[k] = 1;
   }
-  for (uint64_t k = 0; k < nh; ++k) {
-    const uint64_t r = rows[k];
-    if (is_float) {
-      const uint32_t v = uint32_t(bits[k]);
-      HIP_OK(hipMemcpyAsync(col.w32.p + r, &v, 4, hipMemcpyHostToDevice, stream));
-    } else {
-      HIP_OK(hipMemcpyAsync(col.w64.p + r, &bits[k], 8, hipMemcpyHostToDevice, stream));
-    }
-    HIP_OK(hipMemcpyAsync(col.isnull.p + r, &nulls[k], 1, hipMemcpyHostToDevice, stream));
-  }
+  // one upload of the rows, values and null bytes (the host vectors outlive the synchronisation
+  // below), then one scatter into the cache columns
+  DBuf<uint64_t> d_rows(ctx, nh), d_bits(ctx, nh);
+  DBuf<uint8_t> d_nulls(ctx, nh);
+  HIP_OK(hipMemcpyAsync(d_rows.p, rows.data(), nh * 8, hipMemcpyHostToDevice, stream));
+  HIP_OK(hipMemcpyAsync(d_bits.p, bits.data(), nh * 8, hipMemcpyHostToDevice, stream));
+  HIP_OK(hipMemcpyAsync(d_nulls.p, nulls.data(), nh, hipMemcpyHostToDevice, stream));
+  launch_scatter_fp(d_rows.p, d_bits.p, d_nulls.p, nh, is_float ? col.w32.p : nullptr, is_float ? nullptr : col.w64.p,
+                    col.isnull.p, stream);
   HIP_OK(hipStreamSynchronize(stream));
 }
 
@@ -4474,6 +4564,8 @@ static dr_state* replay_sharded_rccl(dr_comm& c, const std::shared_ptr<StagedDat
   // round trip 3: survivors, parse counters, table-wide counters
   int64_t t[8];
   std::unique_ptr<dr_state> st(shard_finish(sh, back.p, sums.p, t));
+  st->local_counts = st->counts;
+  st->has_local_counts = true;
   dr_counts& k = st->counts;
   k.num_files = t[0];
   k.size_in_bytes = t[1];
@@ -4593,6 +4685,10 @@ void dr_ctx_destroy(dr_ctx* ctx) {
 }
 
 const char* dr_last_error(const dr_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+const char* dr_state_last_error(const dr_state* state) {
+  return state ? dr_last_error(state->ctx) : "null state";
+}
+const char* dr_comm_last_error(const dr_comm* comm) { return comm ? dr_last_error(comm->ctx) : "null communicator"; }
 
 int dr_log_segment(dr_ctx* ctx, const char* log_path, int64_t version_to_load, char* buf, uint64_t buf_len,
                    uint64_t* needed, int64_t* version_out) {
@@ -4796,6 +4892,12 @@ int dr_state_counts(dr_state* state, dr_counts* out) {
   return DR_OK;
 }
 
+int dr_state_local_counts(dr_state* state, dr_counts* out) {
+  if (!state || !out) return DR_E_INVALID_ARG;
+  *out = state->has_local_counts ? state->local_counts : state->counts;
+  return DR_OK;
+}
+
 // ValidateChecksum.checkMismatch (D/Checksum.scala:178-191) against ReadChecksum's parse of the
 // version's .crc first line (D/Checksum.scala:101-148, JsonUtils.mapper: unknown fields ignored).
 // A Long field that is absent or null reads as 0; a number with a fraction is truncated and a
@@ -4870,18 +4972,35 @@ int dr_state_export(dr_state* state, int32_t which, dr_export* out) {
     ExportCols& e = state->exp[which];
     *out = dr_export{};
     out->n = e.n;
-    out->path_off = e.path_off.data(); out->path_bytes = e.path_bytes.data();
-    out->size = e.size.data(); out->modification_time = e.mtime.data();
-    out->deletion_timestamp = e.delts.data(); out->deletion_timestamp_valid = e.delts_valid.data();
-    out->extended_file_metadata = e.efm.data();
-    out->stats_off = e.stats_off.data(); out->stats_bytes = e.stats_bytes.data(); out->stats_null = e.stats_null.data();
-    out->pv_entry_off = e.pv_entry_off.data(); out->pv_null = e.pv_null.data();
-    out->pv_key_off = e.pv_key_off.data(); out->pv_key_bytes = e.pv_key_bytes.data();
-    out->pv_val_off = e.pv_val_off.data(); out->pv_val_bytes = e.pv_val_bytes.data(); out->pv_val_null = e.pv_val_null.data();
-    out->tags_entry_off = e.tags_entry_off.data(); out->tags_null = e.tags_null.data();
-    out->tags_key_off = e.tags_key_off.data(); out->tags_key_bytes = e.tags_key_bytes.data();
-    out->tags_val_off = e.tags_val_off.data(); out->tags_val_bytes = e.tags_val_bytes.data();
-    out->tags_val_null = e.tags_val_null.data();
+    out->path_off = e.path_off; out->path_bytes = e.path_bytes;
+    out->size = e.size; out->modification_time = e.mtime;
+    out->deletion_timestamp = e.delts; out->deletion_timestamp_valid = e.delts_valid;
+    out->extended_file_metadata = e.efm;
+    out->stats_off = e.stats_off; out->stats_bytes = e.stats_bytes; out->stats_null = e.stats_null;
+    out->pv_entry_off = e.pv_entry_off; out->pv_null = e.pv_null;
+    out->pv_key_off = e.pv_key_off; out->pv_key_bytes = e.pv_key_bytes;
+    out->pv_val_off = e.pv_val_off; out->pv_val_bytes = e.pv_val_bytes; out->pv_val_null = e.pv_val_null;
+    out->tags_entry_off = e.tags_entry_off; out->tags_null = e.tags_null;
+    out->tags_key_off = e.tags_key_off; out->tags_key_bytes = e.tags_key_bytes;
+    out->tags_val_off = e.tags_val_off; out->tags_val_bytes = e.tags_val_bytes;
+    out->tags_val_null = e.tags_val_null;
+  });
+}
+
+int dr_state_materialize(dr_state* state, uint64_t* bytes) {
+  if (!state) return DR_E_INVALID_ARG;
+  return guard(state->ctx, [&] {
+    HIP_OK(hipSetDevice(state->ctx->device));
+    uint64_t b = 0;
+    for (int w = 0; w < 2; ++w) {
+      const DevExport& X = materialize(*state, w);
+      const uint64_t n = X.n;
+      b += n * (8 + 4 + 8 + 8 + 1 + 8 + 8 + 4 * 1) + 3 * 8 * (n + 1) + X.path_bytes.n;
+      b += X.tot[EXC_STATS] + X.tot[EXC_PV_KB] + X.tot[EXC_PV_VB] + X.tot[EXC_TAGS_KB] + X.tot[EXC_TAGS_VB];
+      b += 17 * (X.tot[EXC_PV_N] + X.tot[EXC_TAGS_N]);
+    }
+    HIP_OK(hipStreamSynchronize(state->ctx->stream));
+    if (bytes) *bytes = b;
   });
 }
 

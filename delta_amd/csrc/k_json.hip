@@ -210,8 +210,11 @@ constexpr int JL_FLUSH = DR_JL_FLUSH;
 // wave copies its lines' byte region into LDS with coalesced 16-byte loads and every lane walks its
 // line from LDS, so the walk's dependent reads cost LDS latency instead of a global round trip each
 // (one wave of a commit has no other waves to hide them behind); lines the fast walker defers are
-// re-parsed in place by the General walker (no k_json_hard launch). For the bulk segment the stage
-// halves occupancy and loses (r03: 8.2 vs 2.79 ms), so it keeps the global walker.
+// deferred to k_json_hard like the bulk segment's: the General walker's stack arrays would give the
+// staged kernel a private segment (r03 inlined it: 272 B of scratch per lane). Every stage read is a
+// ds_read: the stage is reached through the LDS array itself, never through a generic pointer that
+// could also be global (r03's one-walker build did that and faulted). For the bulk
+// segment the stage halves occupancy and loses (r03: 8.2 vs 2.79 ms), so it keeps the global walker.
 constexpr uint32_t JL_SMALL_LINES = 256;
 constexpr uint32_t JL_STAGE_BYTES = 24u * 1024u;
 
@@ -313,10 +316,10 @@ __global__ void __launch_bounds__(JL_T, DR_JL_WAVES) k_json_lines(JsonParseArgs 
       const uint32_t nq = uint32_t((r1 - r0) >> 4) + 3;
       for (uint32_t k = lane; k < nq; k += JL_T) stage[k] = src[k];
       __syncthreads();
-      walk_line<true>(a, tokbuf, lane, line, live, b, n, reinterpret_cast<const uint8_t*>(stage) + (b - r0));
+      walk_line(a, tokbuf, lane, line, live, b, n, reinterpret_cast<const uint8_t*>(stage) + (b - r0));
       return;
     }
-    walk_line<true>(a, tokbuf, lane, line, live, b, n, a.buf + b);
+    walk_line(a, tokbuf, lane, line, live, b, n, a.buf + b);
     return;
   }
   walk_line(a, tokbuf, lane, line, live, b, n, a.buf + b);
@@ -370,8 +373,10 @@ void launch_json_parse(const JsonParseArgs& a, hipStream_t st) {
 }
 
 void launch_json_hard(const JsonParseArgs& a, hipStream_t st) {
-  if (!a.nlines || a.nlines <= dev::JL_SMALL_LINES) return;  // the staged walker re-parsed them in place
-  DR_LAUNCH(dev::k_json_hard, dim3(256), dim3(64), 0, st, a);
+  if (!a.nlines) return;
+  // grid-stride over the device-side count of deferred lines (usually none: the workgroups exit)
+  const unsigned g = unsigned(std::min<uint64_t>(256, (a.nlines + 63) / 64));
+  DR_LAUNCH(dev::k_json_hard, dim3(g), dim3(64), 0, st, a);
 }
 
 }  // namespace dr

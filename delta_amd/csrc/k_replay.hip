@@ -3,15 +3,17 @@
 // InMemoryLogReplay.append/checkpoint, D/Snapshot.scala:103-110,
 // D/actions/InMemoryLogReplay.scala:43-77).
 //
-// 16-byte records {rkey = 32 key bits below the bucket bits, meta = action_index << 2 | class,
-// add.size} are partitioned on the top `bucket_bits` of xxh64(path): tiles count buckets in LDS into
-// a bucket-major matrix whose exclusive scan gives each (bucket, tile) its output range, so the
-// scatter needs no global atomics. Each bucket is then reduced by one workgroup: an LDS
-// open-addressing table keyed by rkey keeps atomicMax(meta), i.e. the action with the largest
-// (version, line) ordinal wins -- exactly the reference's "last action per path" (action index
-// order == input_file_name order, stable within a file). Every loser is byte-verified against its
-// winner, so a collision of the (bucket, rkey) hash bits is detected and that bucket is redone by the
-// 64-bit-key reducer (k_bucket_reduce64), then, if still ambiguous, by the exact kernel (k_bucket_exact).
+// 16-byte records {xxh64(path) lo, hi, meta = action_index << 2 | class, add.size (32-bit field)}
+// are partitioned on the top `bucket_bits` of the key: tiles count buckets in LDS into a bucket-major
+// matrix whose exclusive scan gives each (bucket, tile) its output range, so the scatter needs no
+// global atomics. Each bucket is then reduced by one workgroup: an LDS open-addressing table keyed by
+// the full 64-bit key keeps atomicMax(meta), i.e. the action with the largest (version, line) ordinal
+// wins -- exactly the reference's "last action per path" (action index order == input_file_name
+// order, stable within a file). Every loser is byte-verified against its winner (k_bucket_verify), so
+// a 64-bit collision is detected and that bucket is redone by the exact kernel (k_bucket_exact); an
+// LDS-table overflow goes to the finer-grained reducer (k_bucket_reduce64). (r04: full 64-bit keys in
+// the records -- the 45 key bits of r01-r03 collided about once per 16M-action replay and sent a bucket
+// through k_bucket_reduce64 on every step.)
 #include "dev_common.h"
 #include "kernels.h"
 
@@ -131,42 +133,38 @@ __device__ __forceinline__ bool is_file_action(uint8_t kind, uint8_t flags) {
 __device__ __forceinline__ uint32_t bucket_of(uint64_t key, int bits) {
   return bits ? uint32_t(key >> (64 - bits)) : 0u;
 }
-// the 32 key bits directly below the bucket bits
+// the 32 key bits directly below the bucket bits: the LDS table's probe start and sub-pass selector
 __device__ __forceinline__ uint32_t rkey_of(uint64_t key, int bits) { return uint32_t(key >> (32 - bits)); }
-// top 32 bits of the key, rebuilt from (bucket, rkey): the order-free parity checksum's term
-__device__ __forceinline__ uint64_t top32_of(uint32_t b, uint32_t rkey, int bits) {
-  return bits ? (uint64_t(b) << (32 - bits)) | (rkey >> bits) : uint64_t(rkey);
-}
 
 // Packed path reference: address | length << 48 (0: a length that does not fit 16 bits).
 __device__ __forceinline__ uint64_t pack_ref(uint64_t ptr, uint32_t len) {
   return len < 0xffffu ? (ptr | (uint64_t(len) << 48)) : 0ull;
 }
-
-constexpr int PART_T = 512;
-constexpr int PART_STEPS = 32;                          // 4 actions per thread per step (16: +6 %, 64: +40 %)
-constexpr int PART_TILE = PART_T * 4 * PART_STEPS;      // 65536 actions per tile
-constexpr int PART_MAX_BITS = 13;                       // LDS: 2 x 8192 x 4 B in the scatter
-
-// Tile of this workgroup. Workgroups are dealt to the 8 XCDs round-robin (blockIdx % 8); consecutive
-// tiles go to the same XCD so that a bucket's adjacent per-tile segments are written through one L2.
-__device__ __forceinline__ uint32_t part_tile(uint32_t nt) {
-#ifdef PART_XCD_MAP
-  const uint32_t bid = blockIdx.x, x = bid & 7, r = bid >> 3, q = nt >> 3, rem = nt & 7;
-  return x < rem ? x * (q + 1) + r : rem * (q + 1) + (x - rem) * q + r;
-#else
-  return blockIdx.x;
-#endif
+// add.size in the record's 32-bit field; ~0u sends the reducer to size[] (negative or >= 2^32 - 1)
+__device__ __forceinline__ uint32_t size_field(int64_t s) {
+  return (s >= 0 && s < int64_t(0xffffffffll)) ? uint32_t(s) : 0xffffffffu;
 }
 
+#ifndef DR_PART_T
+#define DR_PART_T 1024
+#endif
+#ifndef DR_RED_T
+#define DR_RED_T 512
+#endif
+constexpr int PART_T = DR_PART_T;
+constexpr int PART_STEPS = 16 * 1024 / PART_T;          // 4 actions per thread per step
+constexpr int PART_TILE = PART_T * 4 * PART_STEPS;      // 65536 actions per tile: ~8 records per (bucket, tile) run
+constexpr int PART_MAX_BITS = 13;                       // LDS: 2 x 8192 x 4 B in the scatter (2 workgroups/CU)
+
 // Every thread owns 4 consecutive actions per step: one dword of kind bytes, one of flag bytes and
-// two 16-byte key loads.
+// two 16-byte key loads; it also packs the actions' path references (address + length, in action
+// order) for k_bucket_verify's gathers: one 8-byte load per path there.
 __global__ void __launch_bounds__(PART_T) k_bucket_hist(PartitionArgs a) {
   __shared__ uint32_t hist[1 << PART_MAX_BITS];
   const uint32_t nb = 1u << a.bucket_bits;
   for (uint32_t b = threadIdx.x; b < nb; b += PART_T) hist[b] = 0;
   __syncthreads();
-  const uint32_t tile = part_tile(a.ntiles);
+  const uint32_t tile = blockIdx.x;
   const uint64_t base = uint64_t(tile) * PART_TILE;
   for (int k = 0; k < PART_STEPS; ++k) {
     const uint64_t i0 = base + (uint64_t(k) * PART_T + threadIdx.x) * 4;
@@ -182,16 +180,15 @@ __global__ void __launch_bounds__(PART_T) k_bucket_hist(PartitionArgs a) {
       for (int j = 0; j < 4; ++j)
         if (is_file_action(uint8_t(kd >> (8 * j)), uint8_t(fl >> (8 * j))))
           atomicAdd(&hist[bucket_of(ks[j], a.bucket_bits)], 1u);
-      // packed path references for k_bucket_verify's gathers (one 8-byte load per path there)
       const uint4 p01 = *reinterpret_cast<const uint4*>(a.path_ptr + i0);
       const uint4 p23 = *reinterpret_cast<const uint4*>(a.path_ptr + i0 + 2);
       const uint4 ln = *reinterpret_cast<const uint4*>(a.path_len + i0);
-      const ulonglong2 r01 = make_ulonglong2(pack_ref(uint64_t(p01.x) | uint64_t(p01.y) << 32, ln.x),
-                                             pack_ref(uint64_t(p01.z) | uint64_t(p01.w) << 32, ln.y));
-      const ulonglong2 r23 = make_ulonglong2(pack_ref(uint64_t(p23.x) | uint64_t(p23.y) << 32, ln.z),
-                                             pack_ref(uint64_t(p23.z) | uint64_t(p23.w) << 32, ln.w));
-      *reinterpret_cast<ulonglong2*>(a.path_ref + i0) = r01;
-      *reinterpret_cast<ulonglong2*>(a.path_ref + i0 + 2) = r23;
+      *reinterpret_cast<ulonglong2*>(a.path_ref + i0) =
+          make_ulonglong2(pack_ref(uint64_t(p01.x) | uint64_t(p01.y) << 32, ln.x),
+                          pack_ref(uint64_t(p01.z) | uint64_t(p01.w) << 32, ln.y));
+      *reinterpret_cast<ulonglong2*>(a.path_ref + i0 + 2) =
+          make_ulonglong2(pack_ref(uint64_t(p23.x) | uint64_t(p23.y) << 32, ln.z),
+                          pack_ref(uint64_t(p23.z) | uint64_t(p23.w) << 32, ln.w));
     } else {
       for (uint64_t i = i0; i < a.n; ++i) {
         if (is_file_action(a.kind[i], a.flags[i])) atomicAdd(&hist[bucket_of(a.key[i], a.bucket_bits)], 1u);
@@ -203,33 +200,32 @@ __global__ void __launch_bounds__(PART_T) k_bucket_hist(PartitionArgs a) {
   for (uint32_t b = threadIdx.x; b < nb; b += PART_T) a.tile_count[uint64_t(b) * a.ntiles + tile] = hist[b];
 }
 
-__device__ __forceinline__ void scatter_one(const PartitionArgs& a, uint64_t i, uint8_t kind, uint64_t key,
-                                            const uint32_t* base, uint32_t* cnt) {
+// One file action into its bucket: the 16-byte record {key lo, key hi, index << 2 | class, size
+// field}. `val` is add.size for an add and remove.deletionTimestamp for a remove.
+__device__ __forceinline__ void scatter_one(const PartitionArgs& a, uint64_t i, uint8_t kind, uint8_t flags,
+                                            uint64_t key, int64_t val, const uint32_t* base, uint32_t* cnt) {
   const uint32_t b = bucket_of(key, a.bucket_bits);
   const uint32_t pos = base[b] + atomicAdd(&cnt[b], 1u);
-  uint32_t cls = C_ADD;
-  int64_t size = 0;
+  uint32_t cls = C_ADD, sz = 0;
   if (kind == K_REMOVE) {
     // RemoveFile.delTimestamp = deletionTimestamp.getOrElse(0) (D/actions/actions.scala:318-319);
     // kept iff delTimestamp > minFileRetentionTimestamp (D/actions/InMemoryLogReplay.scala:67-69)
-    const int64_t dt = (a.flags[i] & F_HAS_DELTS) ? a.delts[i] : 0;
+    const int64_t dt = (flags & F_HAS_DELTS) ? val : 0;
     cls = dt > a.cutoff ? C_REMOVE_KEEP : C_REMOVE_DROP;
   } else {
-    size = a.size[i];
+    sz = size_field(val);
   }
-  uint4 r;
-  r.x = rkey_of(key, a.bucket_bits);
-  r.y = uint32_t(i << 2) | cls;
-  r.z = uint32_t(uint64_t(size));
-  r.w = uint32_t(uint64_t(size) >> 32);
-  *reinterpret_cast<uint4*>(a.rec + pos) = r;
+  *reinterpret_cast<uint4*>(a.rec + pos) = make_uint4(uint32_t(key), uint32_t(key >> 32), uint32_t(i << 2) | cls, sz);
 }
 
+// size[] is read only by waves that hold an add and delts[] only by waves that hold a remove with a
+// deletionTimestamp (runs of one kind are long: whole checkpoints, whole commits), so each action
+// costs kind + flags + key + one 8-byte value = 18 B in, 16 B out.
 __global__ void __launch_bounds__(PART_T) k_bucket_scatter(PartitionArgs a) {
   __shared__ uint32_t base[1 << PART_MAX_BITS];
   __shared__ uint32_t cnt[1 << PART_MAX_BITS];
   const uint32_t nb = 1u << a.bucket_bits;
-  const uint32_t tile = part_tile(a.ntiles);
+  const uint32_t tile = blockIdx.x;
   for (uint32_t b = threadIdx.x; b < nb; b += PART_T) {
     base[b] = uint32_t(a.tile_off[uint64_t(b) * a.ntiles + tile]);
     cnt[b] = 0;
@@ -246,15 +242,51 @@ __global__ void __launch_bounds__(PART_T) k_bucket_scatter(PartitionArgs a) {
       const uint4 k23 = *reinterpret_cast<const uint4*>(a.key + i0 + 2);
       const uint64_t ks[4] = {uint64_t(k01.x) | uint64_t(k01.y) << 32, uint64_t(k01.z) | uint64_t(k01.w) << 32,
                               uint64_t(k23.x) | uint64_t(k23.y) << 32, uint64_t(k23.z) | uint64_t(k23.w) << 32};
+      bool any_file = false, any_add = false, any_del = false;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const uint8_t kj = uint8_t(kd >> (8 * j));
-        if (is_file_action(kj, uint8_t(fl >> (8 * j)))) scatter_one(a, i0 + j, kj, ks[j], base, cnt);
+        const uint8_t kj = uint8_t(kd >> (8 * j)), fj = uint8_t(fl >> (8 * j));
+        const bool f = is_file_action(kj, fj);
+        any_file |= f;
+        any_add |= f && kj == K_ADD;
+        any_del |= f && kj == K_REMOVE && (fj & F_HAS_DELTS);
+      }
+      if (!__ballot(any_file)) continue;  // wave-uniform
+      int64_t val[4] = {0, 0, 0, 0};
+      if (__ballot(any_add)) {
+        const uint4 s01 = *reinterpret_cast<const uint4*>(a.size + i0);
+        const uint4 s23 = *reinterpret_cast<const uint4*>(a.size + i0 + 2);
+        const int64_t sv[4] = {int64_t(uint64_t(s01.x) | uint64_t(s01.y) << 32),
+                               int64_t(uint64_t(s01.z) | uint64_t(s01.w) << 32),
+                               int64_t(uint64_t(s23.x) | uint64_t(s23.y) << 32),
+                               int64_t(uint64_t(s23.z) | uint64_t(s23.w) << 32)};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (uint8_t(kd >> (8 * j)) == K_ADD) val[j] = sv[j];
+      }
+      if (__ballot(any_del)) {
+        const uint4 d01 = *reinterpret_cast<const uint4*>(a.delts + i0);
+        const uint4 d23 = *reinterpret_cast<const uint4*>(a.delts + i0 + 2);
+        const int64_t dv[4] = {int64_t(uint64_t(d01.x) | uint64_t(d01.y) << 32),
+                               int64_t(uint64_t(d01.z) | uint64_t(d01.w) << 32),
+                               int64_t(uint64_t(d23.x) | uint64_t(d23.y) << 32),
+                               int64_t(uint64_t(d23.z) | uint64_t(d23.w) << 32)};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (uint8_t(kd >> (8 * j)) == K_REMOVE) val[j] = dv[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint8_t kj = uint8_t(kd >> (8 * j)), fj = uint8_t(fl >> (8 * j));
+        if (is_file_action(kj, fj)) scatter_one(a, i0 + j, kj, fj, ks[j], val[j], base, cnt);
       }
     } else {
-      for (uint64_t i = i0; i < a.n; ++i)
-        if (is_file_action(a.kind[i], a.flags[i]))
-          scatter_one(a, i, a.kind[i], a.key[i], base, cnt);
+      for (uint64_t i = i0; i < a.n; ++i) {
+        const uint8_t kj = a.kind[i], fj = a.flags[i];
+        if (!is_file_action(kj, fj)) continue;
+        const int64_t v = kj == K_ADD ? a.size[i] : ((fj & F_HAS_DELTS) ? a.delts[i] : 0);
+        scatter_one(a, i, kj, fj, a.key[i], v, base, cnt);
+      }
     }
   }
 }
@@ -265,8 +297,10 @@ __global__ void k_bucket_offsets(const uint64_t* tile_off, uint32_t nb, uint32_t
 }
 
 // ---- per-bucket reduce ------------------------------------------------------------------------------
-constexpr int RED_T = 512;
-constexpr int TS_MAX = 4096;  // LDS table slots (rkeys 16 KiB + metas 16 KiB): 4 workgroups per CU
+constexpr int RED_T = DR_RED_T;
+constexpr int TS_MAX = 4096;  // LDS table slots: 8 B key + 4 B winner meta + 2 B count = 56 KiB, 2 WGs/CU
+// records per thread held in registers by a one-pass bucket (at most 3/4 TS_MAX records)
+constexpr int RED_RPT = (TS_MAX / 4 * 3 + RED_T - 1) / RED_T;
 
 struct BucketTotals {
   uint64_t live, tomb, size, lks, tks;
@@ -318,6 +352,11 @@ __global__ void __launch_bounds__(1024) k_sum_stats(const unsigned long long* bs
 __device__ __forceinline__ uint4 load_rec(const PartRec* r, uint64_t e) {
   return *reinterpret_cast<const uint4*>(r + e);
 }
+__device__ __forceinline__ uint64_t rec_key(uint4 r) { return uint64_t(r.x) | (uint64_t(r.y) << 32); }
+// add.size of a record (the 32-bit field, or size[] by action index when it did not fit)
+__device__ __forceinline__ uint64_t rec_size(const ReduceArgs& a, uint4 r) {
+  return r.w != 0xffffffffu ? uint64_t(r.w) : uint64_t(a.size[r.z >> 2]);
+}
 
 // Appends one wave's flagged values to an LDS-counted list region (order across waves is free).
 __device__ __forceinline__ void wave_append(bool f, uint32_t v, uint32_t* cnt, uint32_t* out) {
@@ -339,160 +378,6 @@ __device__ __forceinline__ void wave_append2(bool f, uint2 v, uint32_t* cnt, uin
   if (f) out[o + uint32_t(__popcll(bl & ((1ull << lane) - 1ull)))] = v;
 }
 
-// Packed path reference of action i (written by k_bucket_hist).
-__device__ __forceinline__ uint64_t path_ref(const ReduceArgs& a, uint32_t i) { return a.path_ref[i]; }
-
-// Per-slot loser counts packed two to a word (slot s: word s >> 1, bits 16 (s & 1)): members - 1 of
-// each slot, replaced in place by each slot's first pair position (an exclusive scan over the n
-// slots, n <= TS_MAX, by one RED_T workgroup); returns the total. Counts and positions stay below
-// 2^16 (a sub-pass holds at most 3/4 TS_MAX records), so the halves never carry into each other.
-__device__ uint32_t scan_loser_slots(uint32_t* w, uint32_t n) {
-  __shared__ uint32_t wsum[RED_T / 64];
-  constexpr uint32_t PER = TS_MAX / 2 / RED_T;  // words per thread
-  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const uint32_t nw = n >> 1;
-  uint32_t v[2 * PER], s = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < PER; ++k) {
-    const uint32_t i = t * PER + k;
-    const uint32_t x = i < nw ? w[i] : 0u;
-    const uint32_t lo = x & 0xffffu, hi = x >> 16;
-    v[2 * k] = lo ? lo - 1u : 0u;
-    v[2 * k + 1] = hi ? hi - 1u : 0u;
-    s += v[2 * k] + v[2 * k + 1];
-  }
-  uint32_t incl = s;
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(incl, o, 64);
-    if (lane >= uint32_t(o)) incl += y;
-  }
-  if (lane == 63) wsum[wv] = incl;
-  __syncthreads();
-  uint32_t base = 0, total = 0;
-  for (uint32_t q = 0; q < RED_T / 64; ++q) {
-    base += q < wv ? wsum[q] : 0u;
-    total += wsum[q];
-  }
-  uint32_t run = base + incl - s;
-#pragma unroll
-  for (uint32_t k = 0; k < PER; ++k) {
-    const uint32_t i = t * PER + k;
-    const uint32_t lo = run;
-    run += v[2 * k];
-    if (i < nw) w[i] = lo | (run << 16);
-    run += v[2 * k + 1];
-  }
-  __syncthreads();
-  return total;
-}
-
-// K4 main reducer: one workgroup per bucket, LDS-only. Survivors go to the bucket's region of the
-// live / tombstone lists; every loser is paired (by action index) with its winner for
-// k_bucket_verify, the pairs grouped by winner (a counting sort on the table slot), so the losers of
-// one path sit next to each other and the verifier's lane groups fetch their shared winner once.
-#ifndef DR_PAIR_GROUPED
-#define DR_PAIR_GROUPED 1  // 0: pairs appended in record order (r02)
-#endif
-__global__ void __launch_bounds__(RED_T) k_bucket_reduce(ReduceArgs a) {
-  __shared__ uint32_t tkey[TS_MAX];
-  __shared__ uint32_t tval[TS_MAX];
-  __shared__ uint32_t tcnt[DR_PAIR_GROUPED ? TS_MAX / 2 : 1];  // u16 per slot: members, then its next pair position
-  __shared__ uint32_t nl, nt, np, overflow;
-  const uint32_t b = blockIdx.x;
-  const uint64_t beg = a.bucket_off[b], end = a.bucket_off[b + 1];
-  const uint64_t m = end - beg;
-  // sub-passes keep the distinct keys per pass at or under 3/4 of the table
-  int sbits = 0;
-  while ((m >> sbits) > uint64_t(TS_MAX / 4 * 3)) ++sbits;
-  uint32_t ts = 64;
-  while (ts < TS_MAX && uint64_t(ts) < 2 * (m >> sbits)) ts <<= 1;
-  const uint32_t mask = ts - 1;
-  if (threadIdx.x == 0) { nl = 0; nt = 0; np = 0; overflow = 0; }
-  BucketTotals tot{0, 0, 0, 0, 0};
-  uint32_t pbase = 0;  // pairs of the earlier sub-passes
-  for (uint32_t sp = 0; sp < (1u << sbits); ++sp) {
-    __syncthreads();
-    for (uint32_t s = threadIdx.x; s < ts; s += RED_T) { tkey[s] = 0; tval[s] = 0; }
-    if (DR_PAIR_GROUPED)
-      for (uint32_t s = threadIdx.x; s < ts / 2; s += RED_T) tcnt[s] = 0;
-    __syncthreads();
-    // insert: table[rkey] = max(meta) -- the largest action index (latest version, line) wins
-    for (uint64_t e = beg + threadIdx.x; e < end; e += RED_T) {
-      const uint4 r = load_rec(a.rec, e);
-      if (sbits && (r.x >> (32 - sbits)) != sp) continue;
-      const uint32_t rk = r.x ? r.x : 1u;  // 0 marks an empty slot (1 and 0 merge; verified later)
-      uint32_t s = rk & mask;
-      for (uint32_t probe = 0;; ++probe) {
-        if (probe >= ts) { overflow = 1; break; }
-        const uint32_t old = atomicCAS(&tkey[s], 0u, rk);
-        if (old == 0u || old == rk) {
-          atomicMax(&tval[s], r.y + 1u);
-          if (DR_PAIR_GROUPED) atomicAdd(&tcnt[s >> 1], 1u << (16 * (s & 1)));
-          break;
-        }
-        s = (s + 1) & mask;
-      }
-    }
-    __syncthreads();
-    if (overflow) break;
-    // losers per slot (members - 1), scanned: each slot's first pair position in this sub-pass
-    const uint32_t npass = DR_PAIR_GROUPED ? scan_loser_slots(tcnt, ts) : 0u;
-    // the table holds each key's winning meta, so a loser pairs with its winner's action index
-    // directly (no pass to record winner positions)
-    for (uint64_t e0 = beg; e0 < end; e0 += RED_T) {
-      const uint64_t e = e0 + threadIdx.x;
-      bool isl = false, ist = false, lose = false;
-      uint32_t idx = 0;
-      uint2 pair = make_uint2(0, 0);
-      if (e < end) {
-        const uint4 r = load_rec(a.rec, e);
-        if (!sbits || (r.x >> (32 - sbits)) == sp) {
-          const uint32_t rk = r.x ? r.x : 1u;
-          uint32_t s = rk & mask;
-          while (tkey[s] != rk) s = (s + 1) & mask;
-          const uint32_t w = tval[s] - 1u;
-          idx = r.y >> 2;
-          if (w == r.y) {
-            const uint32_t cls = r.y & 3;
-            if (cls == C_ADD) {
-              isl = true;
-              ++tot.live;
-              tot.size += uint64_t(r.z) | (uint64_t(r.w) << 32);
-              tot.lks += top32_of(b, r.x, a.bucket_bits);
-            } else if (cls == C_REMOVE_KEEP) {
-              ist = true;
-              ++tot.tomb;
-              tot.tks += top32_of(b, r.x, a.bucket_bits);
-            }
-          } else {
-            if (DR_PAIR_GROUPED) {
-              const uint32_t sh = 16 * (s & 1);
-              const uint32_t at = pbase + ((atomicAdd(&tcnt[s >> 1], 1u << sh) >> sh) & 0xffffu);
-              a.out_pair[beg + at] = make_uint2(r.y >> 2, w >> 2);
-            } else {
-              lose = true;
-              pair = make_uint2(r.y >> 2, w >> 2);
-            }
-          }
-        }
-      }
-      wave_append(isl, idx, &nl, a.out_live + beg);
-      wave_append(ist, idx, &nt, a.out_tomb + beg);
-      if (!DR_PAIR_GROUPED) wave_append2(lose, pair, &np, a.out_pair + beg);
-    }
-    pbase += npass;
-  }
-  if (DR_PAIR_GROUPED && threadIdx.x == 0) np = pbase;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    a.live_count[b] = nl;
-    a.tomb_count[b] = nt;
-    a.pair_count[b] = overflow ? 0 : np;
-    if (overflow) a.redo_list[atomicAdd(&a.totals[3], 1ull)] = b;
-  }
-  store_totals(a, b, tot);
-}
-
 // 16 bytes at byte offset `off` (0..15) of the 32 bytes lo:hi (little-endian).
 __device__ __forceinline__ uint4 window16(uint4 lo, uint4 hi, uint32_t off) {
   const uint32_t dw = off >> 2, sb = off & 3;
@@ -506,13 +391,6 @@ __device__ __forceinline__ uint4 window16(uint4 lo, uint4 hi, uint32_t off) {
                     __builtin_amdgcn_alignbyte(a3, a2, sb), __builtin_amdgcn_alignbyte(a4, a3, sb));
 }
 
-// Every (loser, winner) pair of a bucket must name the same path (URI-equality key); a mismatch is
-// a collision of the (bucket, rkey) hash bits and sends the bucket to the 64-bit-key reducer (as
-// does a path too long for a packed reference). Eight lanes compare one pair: lane j loads aligned
-// 16-byte block j of both strings (a wave instruction requests eight whole paths of each side at
-// once, every block once) and takes block j + 1 from its neighbour by a shuffle; lanes 0..6 each
-// compare 16 path bytes, and the group ORs its differences. Unequal bytes get the URI-key
-// comparison (file:/// vs file:/ spellings) on the group's first lane.
 constexpr uint64_t PREF_PTR = (1ull << 48) - 1;
 // Differences (masked to the string) in path bytes [i, i + 16) of p and q, rem = n - i; plo/phi and
 // qlo/qhi are the aligned 16-byte blocks holding them (po, qo: the strings' offsets in their blocks).
@@ -564,14 +442,22 @@ __device__ bool bytes_equal16(const uint8_t* p, const uint8_t* q, uint32_t n) {
   return diff == 0;
 }
 
-constexpr int VER_T = 256;
-constexpr int VER_G = 8;  // lanes per pair
+constexpr int VER_G = 8;  // lanes per verified pair
 
 __device__ __forceinline__ uint4 shfl_down4(uint4 v, int width) {
   return make_uint4(__shfl_down(v.x, 1, width), __shfl_down(v.y, 1, width), __shfl_down(v.z, 1, width),
                     __shfl_down(v.w, 1, width));
 }
 
+// Every (loser, winner) pair of a bucket must name the same path (URI-equality key): a mismatch is
+// a 64-bit path-hash collision and sends the bucket to the exact reducer (as does a path too long
+// for a packed reference). Eight lanes compare one pair: lane j loads aligned 16-byte block j of
+// both strings (a wave instruction requests eight whole paths of each side at once, every block
+// once) and takes block j + 1 from its neighbour by a shuffle; lanes 0..6 each compare 16 path
+// bytes, and the group ORs its differences. Unequal bytes get the URI-key comparison (file:/// vs
+// file:/ spellings) on the group's first lane. The pairs of a winner sit together (k_bucket_reduce
+// groups them), so the groups that share a winner fetch its reference and bytes once from HBM.
+constexpr int VER_T = 256;
 __global__ void __launch_bounds__(VER_T) k_bucket_verify(ReduceArgs a) {
   const uint32_t b = blockIdx.x;
   const uint32_t n = a.pair_count[b];
@@ -588,12 +474,12 @@ __global__ void __launch_bounds__(VER_T) k_bucket_verify(ReduceArgs a) {
     uint32_t pn = 0, qn = 0;
     if (k < n) {
       const uint2 ix = pr[k];
-      const ulonglong2 v = make_ulonglong2(path_ref(a, ix.x), path_ref(a, ix.y));
-      nul = !v.x || !v.y;
-      p = reinterpret_cast<const uint8_t*>(v.x & PREF_PTR);
-      q = reinterpret_cast<const uint8_t*>(v.y & PREF_PTR);
-      pn = uint32_t(v.x >> 48);
-      qn = uint32_t(v.y >> 48);
+      const uint64_t vx = a.path_ref[ix.x], vy = a.path_ref[ix.y];
+      nul = !vx || !vy;
+      p = reinterpret_cast<const uint8_t*>(vx & PREF_PTR);
+      q = reinterpret_cast<const uint8_t*>(vy & PREF_PTR);
+      pn = uint32_t(vx >> 48);
+      qn = uint32_t(vy >> 48);
       if (nul || pn != qn) {
         diff = 1;
       } else {
@@ -620,12 +506,222 @@ __global__ void __launch_bounds__(VER_T) k_bucket_verify(ReduceArgs a) {
       if (nul || !key_equal(p, pn, q, qn)) bad = true;
     }
   }
-  if (__syncthreads_or(bad) && threadIdx.x == 0) a.redo_list[atomicAdd(&a.totals[3], 1ull)] = b;
+  if (__syncthreads_or(bad) && threadIdx.x == 0) a.exact_list[atomicAdd(&a.totals[4], 1ull)] = b;
 }
 
-// Fallback for buckets whose (bucket, rkey) bits collided or whose LDS table overflowed: the same
-// last-writer-wins keyed by the full 64-bit path hash, byte-verified inline. A 64-bit collision (or
-// overflow) hands the bucket on to the exact O(m^2) kernel.
+// Per-slot loser counts packed two to a word (slot s: word s >> 1, bits 16 (s & 1)): members - 1 of
+// each slot, replaced in place by each slot's first pair position (an exclusive scan over the n
+// slots, n <= TS_MAX, by one RED_T workgroup); returns the total. Counts and positions stay below
+// 2^16 (a sub-pass holds at most 3/4 TS_MAX records), so the halves never carry into each other.
+__device__ uint32_t scan_loser_slots(uint32_t* w, uint32_t n) {
+  __shared__ uint32_t wsum[RED_T / 64];
+  constexpr uint32_t PER = TS_MAX / 2 / RED_T;  // words per thread
+  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint32_t nw = n >> 1;
+  uint32_t v[2 * PER], s = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < PER; ++k) {
+    const uint32_t i = t * PER + k;
+    const uint32_t x = i < nw ? w[i] : 0u;
+    const uint32_t lo = x & 0xffffu, hi = x >> 16;
+    v[2 * k] = lo ? lo - 1u : 0u;
+    v[2 * k + 1] = hi ? hi - 1u : 0u;
+    s += v[2 * k] + v[2 * k + 1];
+  }
+  uint32_t incl = s;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o, 64);
+    if (lane >= uint32_t(o)) incl += y;
+  }
+  if (lane == 63) wsum[wv] = incl;
+  __syncthreads();
+  uint32_t base = 0, total = 0;
+  for (uint32_t q = 0; q < RED_T / 64; ++q) {
+    base += q < wv ? wsum[q] : 0u;
+    total += wsum[q];
+  }
+  uint32_t run = base + incl - s;
+#pragma unroll
+  for (uint32_t k = 0; k < PER; ++k) {
+    const uint32_t i = t * PER + k;
+    const uint32_t lo = run;
+    run += v[2 * k];
+    if (i < nw) w[i] = lo | (run << 16);
+    run += v[2 * k + 1];
+  }
+  __syncthreads();
+  return total;
+}
+
+// K4: one workgroup per bucket. An LDS open-addressing table keyed by the full 64-bit path key keeps
+// atomicMax(meta + 1): the action with the largest (version, line) ordinal wins -- exactly the
+// reference's "last action per path". Survivors go to the bucket's region of the live / tombstone
+// lists; every loser is paired (by action index) with its winner for k_bucket_verify, the pairs
+// grouped by winner (a counting sort on the table slot), so the losers of one path sit next to each
+// other and the verifier's lane groups fetch their shared winner once. An LDS-table overflow sends
+// the bucket to the finer-grained fallback reducer.
+__global__ void __launch_bounds__(RED_T) k_bucket_reduce(ReduceArgs a) {
+  __shared__ unsigned long long tkey[TS_MAX];
+  __shared__ uint32_t tval[TS_MAX];
+  __shared__ uint32_t tcnt[TS_MAX / 2];  // u16 per slot: members, then its next pair position
+  __shared__ uint32_t nl, nt, overflow;
+  const uint32_t b = blockIdx.x;
+  const int bits = a.bucket_bits;
+  const uint64_t beg = a.bucket_off[b], end = a.bucket_off[b + 1];
+  const uint64_t m = end - beg;
+  // sub-passes keep the records per pass at or under 3/4 of the table
+  int sbits = 0;
+  while ((m >> sbits) > uint64_t(TS_MAX / 4 * 3)) ++sbits;
+  uint32_t ts = 64;
+  while (ts < TS_MAX && uint64_t(ts) < 2 * (m >> sbits)) ts <<= 1;
+  const uint32_t mask = ts - 1;
+  if (threadIdx.x == 0) { nl = 0; nt = 0; overflow = 0; }
+  BucketTotals tot{0, 0, 0, 0, 0};
+  uint32_t pbase = 0;  // pairs of the earlier sub-passes
+  if (sbits == 0 && m <= uint64_t(RED_T) * RED_RPT) {
+    // one pass: every record of the bucket is loaded once, all loads issued before any is used, and
+    // kept in registers for both phases (the loop below re-reads them and waits on each load in turn)
+    uint4 r[RED_RPT];
+#pragma unroll
+    for (int q = 0; q < RED_RPT; ++q) {
+      const uint64_t e = beg + threadIdx.x + uint64_t(q) * RED_T;
+      r[q] = e < end ? load_rec(a.rec, e) : make_uint4(0, 0, 0, 0);
+    }
+    for (uint32_t s = threadIdx.x; s < ts; s += RED_T) { tkey[s] = 0; tval[s] = 0; }
+    for (uint32_t s = threadIdx.x; s < ts / 2; s += RED_T) tcnt[s] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < RED_RPT; ++q) {
+      if (beg + threadIdx.x + uint64_t(q) * RED_T >= end) continue;
+      const unsigned long long k = rec_key(r[q]);
+      uint32_t s = rkey_of(k, bits) & mask;
+      for (uint32_t probe = 0;; ++probe) {
+        if (probe >= ts) { overflow = 1; break; }
+        const unsigned long long old = atomicCAS(&tkey[s], 0ull, k);
+        if (old == 0ull || old == k) {
+          atomicMax(&tval[s], r[q].z + 1u);
+          atomicAdd(&tcnt[s >> 1], 1u << (16 * (s & 1)));
+          break;
+        }
+        s = (s + 1) & mask;
+      }
+    }
+    __syncthreads();
+    if (!overflow) {
+      pbase = scan_loser_slots(tcnt, ts);
+#pragma unroll
+      for (int q = 0; q < RED_RPT; ++q) {
+        const bool in = beg + threadIdx.x + uint64_t(q) * RED_T < end;
+        if (!__ballot(in)) break;  // wave-uniform: later rows are past the bucket for every lane
+        bool isl = false, ist = false;
+        uint32_t idx = 0;
+        if (in) {
+          const unsigned long long k = rec_key(r[q]);
+          uint32_t s = rkey_of(k, bits) & mask;
+          while (tkey[s] != k) s = (s + 1) & mask;
+          const uint32_t w = tval[s] - 1u;
+          idx = r[q].z >> 2;
+          if (w == r[q].z) {
+            const uint32_t cls = r[q].z & 3;
+            if (cls == C_ADD) {
+              isl = true;
+              ++tot.live;
+              tot.size += rec_size(a, r[q]);
+              tot.lks += k >> 32;
+            } else if (cls == C_REMOVE_KEEP) {
+              ist = true;
+              ++tot.tomb;
+              tot.tks += k >> 32;
+            }
+          } else {
+            const uint32_t sh = 16 * (s & 1);
+            const uint32_t at = (atomicAdd(&tcnt[s >> 1], 1u << sh) >> sh) & 0xffffu;
+            a.out_pair[beg + at] = make_uint2(idx, w >> 2);
+          }
+        }
+        wave_append(isl, idx, &nl, a.out_live + beg);
+        wave_append(ist, idx, &nt, a.out_tomb + beg);
+      }
+    }
+    sbits = -1;  // done: skip the general sub-pass loop
+  }
+  for (uint32_t sp = 0; sbits >= 0 && sp < (1u << sbits); ++sp) {
+    __syncthreads();
+    for (uint32_t s = threadIdx.x; s < ts; s += RED_T) { tkey[s] = 0; tval[s] = 0; }
+    for (uint32_t s = threadIdx.x; s < ts / 2; s += RED_T) tcnt[s] = 0;
+    __syncthreads();
+    // insert: table[key] = max(meta + 1) -- the largest action index wins
+    for (uint64_t e = beg + threadIdx.x; e < end; e += RED_T) {
+      const uint4 r = load_rec(a.rec, e);
+      const unsigned long long k = rec_key(r);
+      const uint32_t rk = rkey_of(k, bits);
+      if (sbits && (rk >> (32 - sbits)) != sp) continue;
+      uint32_t s = rk & mask;
+      for (uint32_t probe = 0;; ++probe) {
+        if (probe >= ts) { overflow = 1; break; }
+        const unsigned long long old = atomicCAS(&tkey[s], 0ull, k);
+        if (old == 0ull || old == k) {
+          atomicMax(&tval[s], r.z + 1u);
+          atomicAdd(&tcnt[s >> 1], 1u << (16 * (s & 1)));
+          break;
+        }
+        s = (s + 1) & mask;
+      }
+    }
+    __syncthreads();
+    if (overflow) break;
+    // losers per slot (members - 1), scanned: each slot's first pair position in this sub-pass
+    const uint32_t npass = scan_loser_slots(tcnt, ts);
+    for (uint64_t e0 = beg; e0 < end; e0 += RED_T) {
+      const uint64_t e = e0 + threadIdx.x;
+      bool isl = false, ist = false;
+      uint32_t idx = 0;
+      if (e < end) {
+        const uint4 r = load_rec(a.rec, e);
+        const unsigned long long k = rec_key(r);
+        const uint32_t rk = rkey_of(k, bits);
+        if (!sbits || (rk >> (32 - sbits)) == sp) {
+          uint32_t s = rk & mask;
+          while (tkey[s] != k) s = (s + 1) & mask;
+          const uint32_t w = tval[s] - 1u;
+          idx = r.z >> 2;
+          if (w == r.z) {
+            const uint32_t cls = r.z & 3;
+            if (cls == C_ADD) {
+              isl = true;
+              ++tot.live;
+              tot.size += rec_size(a, r);
+              tot.lks += k >> 32;
+            } else if (cls == C_REMOVE_KEEP) {
+              ist = true;
+              ++tot.tomb;
+              tot.tks += k >> 32;
+            }
+          } else {
+            const uint32_t sh = 16 * (s & 1);
+            const uint32_t at = pbase + ((atomicAdd(&tcnt[s >> 1], 1u << sh) >> sh) & 0xffffu);
+            a.out_pair[beg + at] = make_uint2(idx, w >> 2);
+          }
+        }
+      }
+      wave_append(isl, idx, &nl, a.out_live + beg);
+      wave_append(ist, idx, &nt, a.out_tomb + beg);
+    }
+    pbase += npass;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    a.live_count[b] = nl;
+    a.tomb_count[b] = nt;
+    a.pair_count[b] = overflow ? 0 : pbase;
+    if (overflow) a.redo_list[atomicAdd(&a.totals[3], 1ull)] = b;
+  }
+  store_totals(a, b, tot);
+}
+
+// Fallback for buckets whose LDS table overflowed (or every bucket, under the DR_FLAG_REDUCE64 test
+// hook): the same last-writer-wins keyed by the full 64-bit path hash in finer sub-passes, byte-verified
+// inline. A 64-bit collision (or overflow) hands the bucket on to the exact O(m^2) kernel.
 constexpr int TS64 = 4096;
 __device__ void reduce64_bucket(ReduceArgs& a, uint32_t b) {
   __shared__ unsigned long long tkey[TS64];
@@ -644,13 +740,13 @@ __device__ void reduce64_bucket(ReduceArgs& a, uint32_t b) {
     __syncthreads();
     for (uint64_t e = beg + threadIdx.x; e < end; e += RED_T) {
       const uint4 r = load_rec(a.rec, e);
-      const uint64_t k = a.key[r.y >> 2];
+      const uint64_t k = rec_key(r);
       if (sbits && uint32_t(k & ((1u << sbits) - 1)) != sp) continue;
       uint32_t s = uint32_t(k >> 20) & (TS64 - 1);
       for (int probe = 0;; ++probe) {
         if (probe >= TS64) { overflow = 1; break; }
         const unsigned long long old = atomicCAS(&tkey[s], 0ull, (unsigned long long)k);
-        if (old == 0ull || old == k) { atomicMax(&tval[s], r.y + 1u); break; }
+        if (old == 0ull || old == k) { atomicMax(&tval[s], r.z + 1u); break; }
         s = (s + 1) & (TS64 - 1);
       }
     }
@@ -658,27 +754,26 @@ __device__ void reduce64_bucket(ReduceArgs& a, uint32_t b) {
     if (overflow) break;
     for (uint64_t e0 = beg; e0 < end; e0 += RED_T) {
       const uint64_t e = e0 + threadIdx.x;
-      bool isl = false, ist = false, lose = false;
+      bool isl = false, ist = false;
       uint32_t idx = 0;
-      uint2 pair = make_uint2(0, 0);
       if (e < end) {
         const uint4 r = load_rec(a.rec, e);
-        idx = r.y >> 2;
-        const uint64_t k = a.key[idx];
+        idx = r.z >> 2;
+        const uint64_t k = rec_key(r);
         if (!sbits || uint32_t(k & ((1u << sbits) - 1)) == sp) {
           uint32_t s = uint32_t(k >> 20) & (TS64 - 1);
           while (tkey[s] != k) s = (s + 1) & (TS64 - 1);
           const uint32_t w = tval[s] - 1u;
-          if (w == r.y) {
-            if ((r.y & 3) == C_ADD) {
+          if (w == r.z) {
+            if ((r.z & 3) == C_ADD) {
               isl = true;
               ++tot.live;
-              tot.size += uint64_t(r.z) | (uint64_t(r.w) << 32);
-              tot.lks += top32_of(b, r.x, a.bucket_bits);
-            } else if ((r.y & 3) == C_REMOVE_KEEP) {
+              tot.size += rec_size(a, r);
+              tot.lks += k >> 32;
+            } else if ((r.z & 3) == C_REMOVE_KEEP) {
               ist = true;
               ++tot.tomb;
-              tot.tks += top32_of(b, r.x, a.bucket_bits);
+              tot.tks += k >> 32;
             }
           } else {
             const uint32_t wi = w >> 2;
@@ -714,27 +809,27 @@ __device__ void exact_bucket(ReduceArgs& a, uint32_t b) {
   BucketTotals tot{0, 0, 0, 0, 0};
   for (uint64_t e = beg + threadIdx.x; e < end; e += RED_T) {
     const uint4 r = load_rec(a.rec, e);
-    const uint32_t idx = r.y >> 2;
-    const uint64_t k = a.key[idx];
+    const uint32_t idx = r.z >> 2;
+    const uint64_t k = rec_key(r);
     const uint8_t* p = reinterpret_cast<const uint8_t*>(a.path_ptr[idx]);
     const uint32_t pn = a.path_len[idx];
     bool win = true;
     for (uint64_t f = beg; f < end && win; ++f) {
       if (f == e) continue;
       const uint4 q = load_rec(a.rec, f);
-      const uint32_t j = q.y >> 2;
-      if (q.x != r.x || j <= idx || a.key[j] != k) continue;
+      const uint32_t j = q.z >> 2;
+      if (rec_key(q) != k || j <= idx) continue;
       if (key_equal(p, pn, reinterpret_cast<const uint8_t*>(a.path_ptr[j]), a.path_len[j])) win = false;
     }
     if (!win) continue;
-    if ((r.y & 3) == C_ADD) {
+    if ((r.z & 3) == C_ADD) {
       ++tot.live;
-      tot.size += uint64_t(r.z) | (uint64_t(r.w) << 32);
-      tot.lks += top32_of(b, r.x, a.bucket_bits);
+      tot.size += rec_size(a, r);
+      tot.lks += k >> 32;
       a.out_live[beg + atomicAdd(&nl, 1u)] = idx;
-    } else if ((r.y & 3) == C_REMOVE_KEEP) {
+    } else if ((r.z & 3) == C_REMOVE_KEEP) {
       ++tot.tomb;
-      tot.tks += top32_of(b, r.x, a.bucket_bits);
+      tot.tks += k >> 32;
       a.out_tomb[beg + atomicAdd(&nt, 1u)] = idx;
     }
   }

@@ -50,6 +50,29 @@ __global__ void __launch_bounds__(256) k_append_actions(AppendArgs a) {
   a.src_id[i] = a.sid;
 }
 
+// Host-resolved floating-point partition values into their K5 cache rows: row[k] gets bits[k] (the
+// low 32 bits when w32 is given, else all 64) and its null byte (fix_fp_values: one upload, one launch).
+__global__ void k_scatter_fp(const uint64_t* __restrict__ rows, const uint64_t* __restrict__ bits,
+                             const uint8_t* __restrict__ nulls, uint64_t n, uint32_t* w32, int64_t* w64,
+                             uint8_t* isnull) {
+  const uint64_t k = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const uint64_t r = rows[k];
+  if (w32) w32[r] = uint32_t(bits[k]);
+  else w64[r] = int64_t(bits[k]);
+  isnull[r] = nulls[k];
+}
+
+// Export of deletionTimestamp: valid = F_HAS_DELTS of the action's flags, and an absent one reads 0.
+__global__ void k_delts_fix(const uint8_t* __restrict__ flags, const int64_t* __restrict__ delts, uint64_t n,
+                            uint8_t* __restrict__ valid, int64_t* __restrict__ out) {
+  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t v = flags[i] & 1u;
+  valid[i] = v;
+  out[i] = v ? delts[i] : 0;
+}
+
 }  // namespace dev
 
 namespace {
@@ -91,6 +114,17 @@ void launch_gather_u64_by64(const uint64_t* src, const uint64_t* idx, uint64_t n
 void launch_gather_bytes(const uint64_t* ptr, const uint32_t* len, const uint64_t* off, uint64_t n, uint8_t* out,
                          hipStream_t st) {
   if (n) DR_LAUNCH(dev::k_gather_bytes, dim3(unsigned(std::min<uint64_t>((n + 3) / 4, 1u << 20))), dim3(256), 0, st, ptr, len, off, n, out);
+}
+
+void launch_delts_fix(const uint8_t* flags, const int64_t* delts, uint64_t n, uint8_t* valid, int64_t* out,
+                      hipStream_t st) {
+  if (n) DR_LAUNCH(dev::k_delts_fix, dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, flags, delts, n, valid, out);
+}
+
+void launch_scatter_fp(const uint64_t* rows, const uint64_t* bits, const uint8_t* nulls, uint64_t n, uint32_t* w32,
+                       int64_t* w64, uint8_t* isnull, hipStream_t st) {
+  if (n) DR_LAUNCH(dev::k_scatter_fp, dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, rows, bits, nulls, n, w32, w64,
+                   isnull);
 }
 
 void launch_append_actions(const AppendArgs& a, hipStream_t st) {

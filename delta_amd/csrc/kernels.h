@@ -220,14 +220,15 @@ struct CanonArgs {
 void launch_canon(const CanonArgs& a, hipStream_t st);
 
 // ---- K3/K4: partition by hash bucket + per-bucket last-writer-wins ------------------------------
-// A partition record is 16 B: {rkey = the 32 key bits below the bucket bits, meta = action index
-// << 2 | class, add.size}. Tiles of PART_TILE actions count their buckets in LDS into a bucket-major
-// count matrix; its exclusive scan gives every (bucket, tile) its output range, so the scatter
-// needs no global atomics.
+// A partition record is 16 B: {xxh64(path) lo, hi, meta = action index << 2 | class, add.size when it
+// fits 32 bits (else ~0u: the reducer reads size[] by index)}. Tiles of PART_TILE actions count
+// their buckets in LDS into a bucket-major count matrix; its exclusive scan gives every (bucket,
+// tile) its output range, so the scatter needs no global atomics.
 struct PartRec {
-  uint32_t rkey;
+  uint32_t key_lo;
+  uint32_t key_hi;
   uint32_t meta;
-  int64_t size;
+  uint32_t size;
 };
 struct PartitionArgs {
   const uint8_t* kind;
@@ -259,8 +260,8 @@ struct ReduceArgs {
   const uint64_t* bucket_off;  // [nbuckets + 1]
   uint32_t nbuckets;
   int32_t bucket_bits;
-  const uint64_t* key;         // full keys by action index (fallback reducers only)
-  const uint64_t* path_ptr;
+  const int64_t* size;         // add.size by action index (records whose size field overflowed)
+  const uint64_t* path_ptr;    // by action index (fallback reducers only)
   const uint32_t* path_len;
   uint32_t* out_live;          // per-bucket survivors, written at bucket_off[b]
   uint32_t* out_tomb;
@@ -271,15 +272,15 @@ struct ReduceArgs {
   uint32_t* pair_count;        // [nbuckets]
   unsigned long long* totals;  // [0] live files, [1] size sum, [2] tombstones, [3] buckets for the 64-bit
                                // reducer, [4] buckets for the exact reducer, [5] live / [6] tombstone checksum
-  uint32_t* redo_list;         // buckets with a (bucket, rkey) collision or an LDS-table overflow
-  uint32_t* exact_list;        // buckets with a 64-bit path-hash collision
+  uint32_t* redo_list;         // buckets whose LDS table overflowed
+  uint32_t* exact_list;        // buckets with a 64-bit path-hash collision (or an unpackable path)
   unsigned long long* bstats;  // [nbuckets * 5] per-bucket {live, tomb, size, live sum, tomb sum}
 };
-// LDS last-writer-wins per bucket on the 32 rkey bits; losers paired with winners
+// LDS last-writer-wins per bucket on the 64-bit key; losers paired with winners (grouped by winner)
 void launch_bucket_reduce(const ReduceArgs& a, hipStream_t st);
-// byte-verifies every (loser, winner) pair; mismatching buckets -> redo_list
+// byte-verifies every (loser, winner) pair; mismatching buckets (64-bit collisions) -> exact_list
 void launch_bucket_verify(const ReduceArgs& a, hipStream_t st);
-// redo_list buckets, keyed by the full 64-bit hash; 64-bit collisions -> exact_list
+// redo_list buckets in finer sub-passes; collisions -> exact_list
 // `count` (device, nullable): the list's length when only its bound nb is known on the host
 void launch_bucket_reduce64(const ReduceArgs& a, const uint32_t* buckets, uint32_t nb, hipStream_t st,
                             const unsigned long long* count = nullptr);
@@ -476,6 +477,12 @@ struct AppendArgs {
   uint16_t sid;
 };
 void launch_append_actions(const AppendArgs& a, hipStream_t st);
+// export: valid[i] = flags[i] & F_HAS_DELTS, out[i] = valid ? delts[i] : 0
+void launch_delts_fix(const uint8_t* flags, const int64_t* delts, uint64_t n, uint8_t* valid, int64_t* out,
+                      hipStream_t st);
+// isnull[rows[k]] = nulls[k] and w32[rows[k]] = low 32 bits of bits[k] (w32 given) or w64[rows[k]] = bits[k]
+void launch_scatter_fp(const uint64_t* rows, const uint64_t* bits, const uint8_t* nulls, uint64_t n, uint32_t* w32,
+                       int64_t* w64, uint8_t* isnull, hipStream_t st);
 }  // namespace dr
 
 // ---- incremental tail apply: device-resident path index (k_index.hip) ----------------------------

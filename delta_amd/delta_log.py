@@ -278,6 +278,21 @@ class State:
         self._nonfile_text = C.string_at(p, n.value) if n.value else b""
         self._nonfile = None
 
+    def materialize(self) -> int:
+        """dr_state_materialize: every field of both sides extracted on the device and kept resident
+        (the reference's cached SingleAction rows); returns the device bytes they hold."""
+        b = C.c_uint64()
+        with self.eng.lock:
+            self.eng.check(self.eng.lib.dr_state_materialize(self.h, C.byref(b)))
+        return b.value
+
+    def local_counts(self) -> Dict[str, int]:
+        """dr_state_local_counts: a library-sharded rank's own counters before the all-reduce (its
+        parsed and reduced actions); the table-wide `counts` for any other state."""
+        c = N.dr_counts()
+        self.eng.check(self.eng.lib.dr_state_local_counts(self.h, C.byref(c)))
+        return {f: getattr(c, f) for f, _ in N.dr_counts._fields_}
+
     @property
     def nonfile(self) -> List[dict]:
         """protocol / metaData / txn winners (dr_state_nonfile_json), decoded on first use."""

@@ -318,8 +318,10 @@ def write_checkpoint_sharded(sharded: "ShardedState", log_path: str, version: in
     import torch
     dev = torch.device("cpu") if getattr(ex, "host", False) else torch.device("cuda", torch.cuda.current_device())
     total, total_adds = ex.all_reduce_sum([rows, adds], dev)
+    # every rank holds the all-reduced add rows and the table-wide numOfFiles, so every rank checks:
+    # a mismatch raises on all of them together (nobody is left waiting in the barrier below)
+    check_add_rows(total_adds, sharded.counts["num_files"])
     if ex.rank == 0:
-        check_add_rows(total_adds, sharded.counts["num_files"])
         meta = {"version": version, "size": total}
         if ex.world > 1:
             meta["parts"] = ex.world

@@ -21,7 +21,12 @@
 extern "C" {
 #endif
 
-#define DR_ABI_VERSION 1
+/* ABI history (a host checks dr_abi_version() == DR_ABI_VERSION at load and refuses a mismatch):
+ *   1  round 1-2 entry points
+ *   2  dr_state_write_checkpoint gained its 9th parameter (add_rows); dr_pred_type gained
+ *      DR_T_FLOAT .. DR_T_DECIMAL (partitionValues_parsed of the checkpoint writer);
+ *      dr_state_local_counts, dr_state_last_error, dr_comm_last_error, dr_state_materialize */
+#define DR_ABI_VERSION 2
 
 /* Status codes. The JNI shim rethrows the reference's exception class with dr_last_error():
  *   DR_E_EMPTY_DIR / DR_E_LOG_TRUNCATED -> FileNotFoundException (D/DeltaErrors.scala:451-457,915-917)
@@ -118,6 +123,11 @@ typedef struct dr_staged dr_staged;
 int dr_ctx_create(int device, dr_ctx** out);
 void dr_ctx_destroy(dr_ctx* ctx);
 const char* dr_last_error(const dr_ctx* ctx);
+/* The message of the last failed call on a state / communicator (its context's dr_last_error), for
+ * hosts that keep only the state or communicator handle (the JNI glue, jni/deltareplay_jni.c). */
+const char* dr_state_last_error(const dr_state* state);
+typedef struct dr_comm dr_comm;
+const char* dr_comm_last_error(const dr_comm* comm);
 int dr_abi_version(void);
 
 /* ---- log segment (host) -------------------------------------------------------------------
@@ -179,6 +189,10 @@ int dr_state_apply(dr_ctx* ctx, dr_state* base, const dr_staged* tail, int64_t m
 
 /* ---- results ------------------------------------------------------------------------------ */
 int dr_state_counts(dr_state* state, dr_counts* out);
+/* A rank's own counters of a dr_replay_sharded state before they were all-reduced (the actions this
+ * rank parsed and reduced, its local survivors); equal to dr_state_counts for any other state. The
+ * bench prices each rank's K3/K4 kernels with it. */
+int dr_state_local_counts(dr_state* state, dr_counts* out);
 /* Latest protocol / metaData and the set transactions as JSON text in the reference's action
  * encoding ({"protocol":{...}} etc., one per line; D/actions/actions.scala:71). */
 int dr_state_nonfile_json(dr_state* state, const char** json, uint64_t* len);
@@ -192,6 +206,14 @@ int dr_state_check_checksum(dr_state* state, const char* crc, uint64_t crc_len, 
                             uint64_t* msg_len);
 /* Materialises allFiles (DR_LIVE) or tombstones (DR_TOMBSTONES) on the host, dataChange=false. */
 int dr_state_export(dr_state* state, int32_t which, dr_export* out);
+
+/* The full-record state resident in HBM: every field of allFiles and tombstones (path, size,
+ * modificationTime / deletionTimestamp, extendedFileMetadata, stats, partitionValues, tags) extracted
+ * on the device into columns kept with the state until dr_state_release -- the reference's cached
+ * SingleAction rows (cacheDS(stateReconstruction), D/Snapshot.scala:116-120, D/util/StateCache.scala:45-68).
+ * dr_state_export then only copies them to the host, dr_state_record_sums only hashes them.
+ * *bytes (may be NULL): the device bytes the columns hold. */
+int dr_state_materialize(dr_state* state, uint64_t* bytes);
 
 /* Order-free full-record checksums of allFiles and tombstones, computed on the device from the export
  * columns: the sum mod 2^64 over the records of one 64-bit hash of every field of the record
@@ -357,7 +379,6 @@ int dr_shard_release(dr_shard* shard);
  * surviving records; its counters and non-file winners are table-wide. The communicator comes from
  * one dr_comm_unique_id shared by the caller's own means (e.g. the Spark driver) and one
  * dr_comm_create per rank; librccl is loaded on first use (DR_E_UNSUPPORTED when absent). */
-typedef struct dr_comm dr_comm;
 int dr_comm_unique_id(uint8_t* id /* 128 bytes */);
 int dr_comm_create(dr_ctx* ctx, const uint8_t* id, int32_t world, int32_t rank, dr_comm** out);
 /* Test hook: an id whose communicator is an in-process loopback instead of RCCL -- the `world` ranks

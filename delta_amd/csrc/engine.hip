@@ -3802,10 +3802,20 @@ static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred)
     la.lit_str = d_sb.p;
     la.n_i64 = int32_t(lp.i64.size());
     la.n_str = int32_t(lp.str.size());
-    DBuf<uint32_t> flag(ctx, st.n_live);
-    la.flag = flag.p;
+    const uint64_t ng = filter_leaf_groups(st.n_live);
+    DBuf<uint64_t> mask(ctx, 16 * ng), wg_off(ctx, ng + 1);
+    DBuf<uint32_t> wg_count(ctx, ng);
+    DBuf<uint8_t> scratch(ctx, scan_scratch_for(ng));
+    la.mask = mask.p;
+    la.wg_count = wg_count.p;
     launch_filter_leaf(la, stream);
-    return select_flags(st, flag);
+    launch_scan_u32(wg_count.p, wg_off.p, ng, ss(scratch), stream);
+    const uint64_t nsel = ng ? d2h_one(wg_off.p + ng, stream) : 0;
+    DBuf<int64_t> sel(ctx, nsel);
+    if (nsel) launch_select_bits(mask.p, wg_off.p, st.n_live, sel.p, stream);
+    std::vector<int64_t> out = d2h(sel.p, nsel, stream);
+    ctx->collect_timings();
+    return out;
   }
   const std::vector<int32_t> ops = lower_program(pred);
   std::vector<uint64_t> lit_off(size_t(pred.nlits) + 1, 0);

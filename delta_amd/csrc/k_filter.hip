@@ -876,29 +876,158 @@ __device__ __forceinline__ uint32_t eval_leaf(const FilterLeafArgs& a, const Fil
   }
 }
 
-__global__ void __launch_bounds__(256) k_filter_leaf(FilterLeafArgs a) {
-  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= a.n_live) return;
-  const int64_t* li = a.lit_i64;
-  const uint64_t* ls = a.lit_s8;
-  {
-  uint64_t stk = 0;  // 2 bits per entry, top at the low end
+// Four files per thread, strided by the workgroup (each load instruction of a wave reads 64
+// consecutive files): a leaf's column loads for all four are issued before any is compared, so one
+// round trip serves four files. The result leaves as bits -- one 64-bit mask per 64 files, in file
+// order -- plus the workgroup's count, which k_select_bits turns into the selected ordinals after a
+// scan of the counts (no 4-byte flag per file, no scan over files).
+constexpr int FL_T = 256, FL_PER = 4;
+constexpr uint32_t FL_FILES = FL_T * FL_PER;  // files per workgroup (16 mask words)
+
+__device__ __forceinline__ void eval_leaf4(const FilterLeafArgs& a, const FilterLeaf& L, uint64_t i0,
+                                           uint32_t (&res)[FL_PER]) {
+  const PvColumn& col = a.cols[L.col];
+  const bool str = col.type == DR_T_STRING, lng = col.type == DR_T_LONG;  // uniform
+  uint32_t nul[FL_PER], vn[FL_PER];
+  uint64_t v8[FL_PER];
+  int64_t v[FL_PER];
+#pragma unroll
+  for (int j = 0; j < FL_PER; ++j) {
+    const uint64_t i = i0 + uint64_t(j) * FL_T;
+    const bool ok = i < a.n_live;
+    nul[j] = ok ? col.isnull[i] : 1u;
+    vn[j] = 0;
+    v8[j] = 0;
+    v[j] = 0;
+    if (str) {
+      vn[j] = ok ? col.slen[i] : 0u;
+      v8[j] = ok ? col.s8[i] : 0ull;
+    } else if (lng) {
+      v[j] = ok ? col.w64[i] : 0;
+    } else {
+      v[j] = ok ? int64_t(int32_t(col.w32[i])) : 0;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < FL_PER; ++j) {
+    const uint64_t i = i0 + uint64_t(j) * FL_T;
+    const bool vnull = nul[j] != 0;
+    uint32_t r;
+    if (L.op == DR_OP_ISNULL) r = vnull ? 1u : 0u;
+    else if (L.op == DR_OP_ISNOTNULL) r = vnull ? 0u : 1u;
+    else if (L.op == DR_OP_NSEQ && (vnull || L.lit_null)) r = (vnull && L.lit_null) ? 1u : 0u;
+    else if (L.op != DR_OP_IN && L.lit_null) r = 2u;
+    else if (vnull) r = 2u;
+    else {
+      // strings: the big-endian 8-byte prefixes order like the bytes; equal prefixes of two values of
+      // at most 8 bytes leave only the lengths; otherwise the value bytes are gathered
+      auto cmp_lit = [&](int32_t k) -> int {
+        if (str) {
+          const uint64_t o = a.lit_str_off[k];
+          const uint32_t ln = uint32_t(a.lit_str_off[k + 1] - o);
+          const uint64_t l8 = a.lit_s8[k];
+          if (v8[j] != l8) return v8[j] < l8 ? -1 : 1;
+          if (vn[j] <= 8 && ln <= 8) return vn[j] == ln ? 0 : (vn[j] < ln ? -1 : 1);
+          return bytes_cmp(reinterpret_cast<const uint8_t*>(col.sptr[i]), vn[j], a.lit_str + o, ln);
+        }
+        const int64_t x = a.lit_i64[k];
+        return v[j] == x ? 0 : (v[j] < x ? -1 : 1);
+      };
+      if (L.op == DR_OP_IN && L.pad == 1) {  // an integer set as a bitmap over [min, min + 64 * words)
+        const uint64_t d = uint64_t(v[j]) - uint64_t(a.lit_i64[L.lit]);
+        const uint64_t nbits = uint64_t(a.lit_i64[L.lit + 1]) * 64;
+        r = (d < nbits && ((uint64_t(a.lit_i64[L.lit + 2 + (d >> 6)]) >> (d & 63)) & 1u)) ? 1u
+            : (L.lit_null ? 2u : 0u);
+      } else if (L.op == DR_OP_IN) {  // binary search of the sorted set
+        int32_t lo = L.lit, hi = L.lit + L.nlit;
+        r = L.lit_null ? 2u : 0u;
+        while (lo < hi) {
+          const int32_t mid = (lo + hi) >> 1;
+          const int c = cmp_lit(mid);
+          if (c == 0) { r = 1u; break; }
+          if (c > 0) lo = mid + 1; else hi = mid;
+        }
+      } else {
+        const int c = cmp_lit(L.lit);
+        switch (L.op) {
+          case DR_OP_EQ: case DR_OP_NSEQ: r = c == 0; break;
+          case DR_OP_NE: r = c != 0; break;
+          case DR_OP_LT: r = c < 0; break;
+          case DR_OP_LE: r = c <= 0; break;
+          case DR_OP_GT: r = c > 0; break;
+          default: r = c >= 0; break;
+        }
+      }
+    }
+    res[j] = r;
+  }
+}
+
+__global__ void __launch_bounds__(FL_T) k_filter_leaf(FilterLeafArgs a) {
+  __shared__ uint32_t wcount[FL_T / 64];
+  const uint64_t base = uint64_t(blockIdx.x) * FL_FILES;
+  const uint64_t i0 = base + threadIdx.x;
+  uint64_t stk[FL_PER] = {0, 0, 0, 0};  // per file: 2 bits per entry, top at the low end
   for (int k = 0; k < a.nprog; ++k) {
     const int op = a.prog[2 * k];
     if (op == LEAF_OP_LEAF) {
-      stk = (stk << 2) | eval_leaf(a, a.leaves[a.prog[2 * k + 1]], i, li, ls);
+      uint32_t r[FL_PER];
+      eval_leaf4(a, a.leaves[a.prog[2 * k + 1]], i0, r);
+#pragma unroll
+      for (int j = 0; j < FL_PER; ++j) stk[j] = (stk[j] << 2) | r[j];
     } else if (op == LEAF_OP_NOT) {
-      const uint64_t x = stk & 3u;
-      stk = (stk & ~3ull) | (x == 2u ? 2u : (x ^ 1u));
+#pragma unroll
+      for (int j = 0; j < FL_PER; ++j) {
+        const uint64_t x = stk[j] & 3u;
+        stk[j] = (stk[j] & ~3ull) | (x == 2u ? 2u : (x ^ 1u));
+      }
     } else {
-      const uint32_t y = uint32_t(stk & 3u), x = uint32_t((stk >> 2) & 3u);
-      uint32_t r;
-      if (op == LEAF_OP_AND) r = (x == 0u || y == 0u) ? 0u : (x == 1u && y == 1u) ? 1u : 2u;
-      else r = (x == 1u || y == 1u) ? 1u : (x == 0u && y == 0u) ? 0u : 2u;
-      stk = ((stk >> 4) << 2) | r;
+#pragma unroll
+      for (int j = 0; j < FL_PER; ++j) {
+        const uint32_t y = uint32_t(stk[j] & 3u), x = uint32_t((stk[j] >> 2) & 3u);
+        uint32_t r;
+        if (op == LEAF_OP_AND) r = (x == 0u || y == 0u) ? 0u : (x == 1u && y == 1u) ? 1u : 2u;
+        else r = (x == 1u || y == 1u) ? 1u : (x == 0u && y == 0u) ? 0u : 2u;
+        stk[j] = ((stk[j] >> 4) << 2) | r;
+      }
     }
   }
-  a.flag[i] = (stk & 3u) == 1u ? 1u : 0u;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int j = 0; j < FL_PER; ++j) {
+    const bool f = i0 + uint64_t(j) * FL_T < a.n_live && (stk[j] & 3u) == 1u;
+    const unsigned long long m = __ballot(f);
+    if (lane == 0) a.mask[base / 64 + 4 * j + wv] = m;
+    cnt += uint32_t(__popcll(m));
+  }
+  if (lane == 0) wcount[wv] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) a.wg_count[blockIdx.x] = wcount[0] + wcount[1] + wcount[2] + wcount[3];
+}
+
+// The selected ordinals of one k_filter_leaf workgroup's files, in file order: its 16 mask words
+// and the exclusive scan of the workgroups' counts give every selected file its output position.
+__global__ void __launch_bounds__(FL_T) k_select_bits(const uint64_t* mask, const uint64_t* wg_off, uint64_t n,
+                                                    int64_t* out) {
+  __shared__ uint64_t w[FL_FILES / 64];
+  __shared__ uint32_t before[FL_FILES / 64];
+  const uint64_t base = uint64_t(blockIdx.x) * FL_FILES;
+  if (threadIdx.x < FL_FILES / 64) w[threadIdx.x] = mask[base / 64 + threadIdx.x];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t s = 0;
+    for (uint32_t k = 0; k < FL_FILES / 64; ++k) { before[k] = s; s += uint32_t(__popcll(w[k])); }
+  }
+  __syncthreads();
+  const uint64_t o = wg_off[blockIdx.x];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < FL_PER; ++j) {
+    const uint32_t k = 4 * j + wv;
+    const uint64_t m = w[k];
+    if ((m >> lane) & 1ull)
+      out[o + before[k] + uint32_t(__popcll(m & ((1ull << lane) - 1ull)))] = int64_t(base + uint64_t(j) * FL_T + threadIdx.x);
   }
 }
 
@@ -1002,8 +1131,12 @@ uint32_t filter_max_stack() { return dev::PV_STACK; }
 void launch_pv_extract(const PvExtractArgs& a, hipStream_t st) {
   if (a.n_live) DR_LAUNCH(dev::k_pv_extract, dim3(g256(a.n_live)), dim3(256), 0, st, a);
 }
+uint64_t filter_leaf_groups(uint64_t n) { return (n + dev::FL_FILES - 1) / dev::FL_FILES; }
 void launch_filter_leaf(const FilterLeafArgs& a, hipStream_t st) {
-  if (a.n_live) DR_LAUNCH(dev::k_filter_leaf, dim3(g256(a.n_live)), dim3(256), 0, st, a);
+  if (a.n_live) DR_LAUNCH(dev::k_filter_leaf, dim3(unsigned(filter_leaf_groups(a.n_live))), dim3(dev::FL_T), 0, st, a);
+}
+void launch_select_bits(const uint64_t* mask, const uint64_t* wg_off, uint64_t n, int64_t* out, hipStream_t st) {
+  if (n) DR_LAUNCH(dev::k_select_bits, dim3(unsigned(filter_leaf_groups(n))), dim3(dev::FL_T), 0, st, mask, wg_off, n, out);
 }
 void launch_filter_typed(const FilterTypedArgs& a, hipStream_t st) {
   if (a.n_live) DR_LAUNCH(dev::k_filter_typed, dim3(g256(a.n_live)), dim3(256), 0, st, a);

@@ -444,9 +444,14 @@ struct FilterLeafArgs {
   const uint8_t* lit_str;
   const uint64_t* lit_s8;        // per string literal: its first 8 bytes as PvColumn::s8
   int32_t n_i64, n_str;          // literal counts
-  uint32_t* flag;
+  uint64_t* mask;                // [16 per workgroup] selection bits, one u64 per 64 files in file order
+  uint32_t* wg_count;            // [workgroups] selected files of each workgroup's 1024
 };
+// workgroups of k_filter_leaf (1024 files each): the sizes of `mask` (x16) and `wg_count`
+uint64_t filter_leaf_groups(uint64_t n_live);
 void launch_filter_leaf(const FilterLeafArgs& a, hipStream_t st);
+// out[wg_off[g] + rank] = ordinal of every selected file (wg_off: exclusive scan of wg_count)
+void launch_select_bits(const uint64_t* mask, const uint64_t* wg_off, uint64_t n, int64_t* out, hipStream_t st);
 // device-only opcodes of the lowered program (engine.hip lower_program): an IN list is folded
 // one element at a time into an accumulator slot above its value
 enum : int32_t { FILTER_OP_IN_START = 100, FILTER_OP_IN_STEP = 101, FILTER_OP_IN_END = 102 };

@@ -493,7 +493,7 @@ struct ExportCols {
   bool built = false;
   int64_t n = 0;
   dr_ctx* ctx = nullptr;
-  void* block = nullptr;
+  std::vector<void*> blocks;  // pinned blocks (the context's cache) holding the columns
   int64_t *path_off = nullptr, *size = nullptr, *mtime = nullptr, *delts = nullptr, *stats_off = nullptr,
           *pv_entry_off = nullptr, *pv_key_off = nullptr, *pv_val_off = nullptr, *tags_entry_off = nullptr,
           *tags_key_off = nullptr, *tags_val_off = nullptr;
@@ -504,7 +504,8 @@ struct ExportCols {
   ExportCols(const ExportCols&) = delete;
   ExportCols& operator=(const ExportCols&) = delete;
   ~ExportCols() {
-    if (block && ctx) ctx->host_release(block);
+    if (ctx)
+      for (void* b : blocks) ctx->host_release(b);
   }
 };
 
@@ -1003,12 +1004,15 @@ static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_
     sa.half_out = P.s_half_out.p;
     sa.half_elems = P.s_half_elems.p;
     sa.chunk_page = P.d_chunk_page.p;
-    DBuf<uint64_t> stamps;
+    DBuf<uint64_t> stamps, rstats;
     const bool dbg = std::getenv("DR_SNAP_DEBUG") != nullptr;
     if (dbg) {
       stamps = DBuf<uint64_t>(ctx, P.block_page.size() * 8);
       stamps.zero(stream);
       sa.stamps = stamps.p;
+      rstats = DBuf<uint64_t>(ctx, uint64_t(P.nchunks) * 4 + 4);
+      rstats.zero(stream);
+      sa.rstats = rstats.p;
     }
     launch_snappy(sa, stream, scratch);
     if (ctx->timing && !P.snap_elements) P.snap_elements = d2h_one(P.s_rec_start.p + P.nchunks, stream);
@@ -1051,6 +1055,51 @@ static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_
         px += k != 0;
       }
       std::fprintf(stderr, "snappy: chunks %u, entry != speculative first %zu (on %zu pages)\n", P.nchunks, nx, px);
+      // regions per page; DR_SNAP_DUMP=dir writes the compressed input of the first pages holding one
+      std::vector<uint32_t> reg = d2h(P.s_region.p, nr, stream);
+      {  // the slowest resolver walks
+        std::vector<uint64_t> rs = d2h(rstats.p, nr * 4, stream);
+        std::vector<size_t> ord(nr);
+        for (size_t k = 0; k < nr; ++k) ord[k] = k;
+        std::sort(ord.begin(), ord.end(), [&](size_t x, size_t y) { return rs[x * 4] > rs[y * 4]; });
+        for (size_t k = 0; k < std::min<size_t>(nr, 8); ++k) {
+          const size_t r = ord[k];
+          const uint32_t c = reg[r];
+          const uint32_t q = uint32_t(std::upper_bound(P.chunk_base.begin(), P.chunk_base.end(), c) - P.chunk_base.begin()) - 1;
+          if (const char* dir = std::getenv("DR_SNAP_DUMP")) {  // the slowest regions' pages, with their entries
+            const SnapPage& pg = P.snap_pages[q];
+            std::vector<uint8_t> raw = d2h(reinterpret_cast<const uint8_t*>(pg.in), pg.n_in, stream);
+            const std::string fn = std::string(dir) + "/slow_page" + std::to_string(q) + ".snappy";
+            if (FILE* f = std::fopen(fn.c_str(), "wb")) {
+              std::fwrite(raw.data(), 1, raw.size(), f);
+              std::fclose(f);
+            }
+          }
+          std::fprintf(stderr, "resolve region %zu: page %u chunk %u/%u clocks %llu windows %llu walks %llu spans %llu\n", r, q,
+                       c - P.chunk_base[q], P.chunk_base[q + 1] - P.chunk_base[q], (unsigned long long)rs[r * 4],
+                       (unsigned long long)rs[r * 4 + 1], (unsigned long long)rs[r * 4 + 2], (unsigned long long)rs[r * 4 + 3]);
+        }
+      }
+      std::map<uint32_t, std::vector<uint32_t>> per_page;
+      for (uint32_t c : reg) {
+        const uint32_t q = uint32_t(std::upper_bound(P.chunk_base.begin(), P.chunk_base.end(), c) - P.chunk_base.begin()) - 1;
+        per_page[q].push_back(c - P.chunk_base[q]);
+      }
+      int dumped = 0;
+      for (auto& kv : per_page) {
+        const SnapPage& pg = P.snap_pages[kv.first];
+        std::fprintf(stderr, "snappy page %u: n_in %u n_out %u regions %zu first at chunk %u\n", kv.first, pg.n_in,
+                     pg.n_out, kv.second.size(), *std::min_element(kv.second.begin(), kv.second.end()));
+        if (const char* dir = std::getenv("DR_SNAP_DUMP")) {
+          if (dumped++ >= 4) continue;
+          std::vector<uint8_t> raw = d2h(reinterpret_cast<const uint8_t*>(pg.in), pg.n_in, stream);
+          const std::string fn = std::string(dir) + "/page" + std::to_string(kv.first) + ".snappy";
+          if (FILE* f = std::fopen(fn.c_str(), "wb")) {
+            std::fwrite(raw.data(), 1, raw.size(), f);
+            std::fclose(f);
+          }
+        }
+      }
     }
   }
   if (P.ba_pages) {
@@ -2325,12 +2374,17 @@ struct DevExport {
   DBuf<uint8_t> efm, stats_null, pv_null, tags_null;
   DBuf<uint64_t> off[EXC_N];                 // exclusive scans of the per-record counts (n + 1)
   uint64_t tot[EXC_N] = {};
+  uint64_t path_nb = 0;                      // path bytes
   DBuf<uint8_t> stats_bytes, pv_key_bytes, pv_val_bytes, tags_key_bytes, tags_val_bytes, pv_val_null, tags_val_null;
   DBuf<int64_t> pv_key_off, pv_val_off, tags_key_off, tags_val_off;  // per entry (entries + 1)
 };
 
-// Records [lo, hi) of the side (export order); the whole side by default.
-static void export_device(dr_state& st, int which, DevExport& X, uint64_t lo = 0, uint64_t hi = UINT64_MAX) {
+// Records [lo, hi) of the side (export order); the whole side by default. `at` (may be null) is
+// called with 0 once the paths, flags and deletion timestamps are enqueued, 1 once pass 1's scalars
+// and offsets are (before the host waits for their totals), 2 once every column is: a streamed
+// export queues each group's copy to the host there.
+static void export_device(dr_state& st, int which, DevExport& X, uint64_t lo = 0, uint64_t hi = UINT64_MAX,
+                          const std::function<void(int)>* at = nullptr) {
   ensure_ready(st);
   dr_ctx* ctx = st.ctx;
   hipStream_t stream = ctx->stream;
@@ -2356,7 +2410,9 @@ static void export_device(dr_state& st, int which, DevExport& X, uint64_t lo = 0
   if (!n) HIP_OK(hipMemsetAsync(X.path_off.p, 0, 8, stream));
   const uint64_t nb = n ? d2h_one(X.path_off.p + n, stream) : 0;
   X.path_bytes = DBuf<uint8_t>(ctx, nb + 16);  // +16: whole-word loads of the record hash
+  X.path_nb = nb;
   launch_gather_bytes(X.path_ptr.p, X.path_len.p, X.path_off.p, n, X.path_bytes.p, stream);
+  if (at) (*at)(0);
   if (!st.exp_dec[which]) {
     auto d = std::make_shared<ExpDecoded>();
     decode_export_side(st, which, *d);
@@ -2366,6 +2422,7 @@ static void export_device(dr_state& st, int which, DevExport& X, uint64_t lo = 0
   ExportArgs a{};
   a.idx = didx;
   a.n = n;
+
   a.side = which == DR_LIVE ? 0 : 1;
   a.json = s.d_json.p;
   a.ck_rows = s.ck_rows;
@@ -2408,12 +2465,34 @@ static void export_device(dr_state& st, int which, DevExport& X, uint64_t lo = 0
     X.off[k] = DBuf<uint64_t>(ctx, n + 1);
     a.cnt[k] = cnt[k].p;
   }
-  launch_export(a, stream);  // pass 1: scalars + counts
+  DBuf<uint64_t> stats_src(ctx, n);
+  DBuf<uint32_t> stats_srclen(ctx, n);
+  a.stats_src = stats_src.p;
+  a.stats_srclen = stats_srclen.p;
+  // pass 1: scalars + counts, the checkpoint rows and the JSON lines in launches of their own (the
+  // survivors mix them; the JSON walk needs the line stage, which costs the checkpoint rows occupancy)
+  {
+    DBuf<uint32_t> jf(ctx, n), jpos(ctx, n), cpos(ctx, n);
+    DBuf<uint64_t> js(ctx, n + 1);
+    launch_export_flags(a, jf.p, stream);
+    launch_scan_u32(jf.p, js.p, n, ss(scratch), stream);
+    const uint64_t nj = n ? d2h_one(js.p + n, stream) : 0;
+    launch_export_split(jf.p, js.p, n, jpos.p, cpos.p, stream);
+    a.pos = cpos.p;
+    a.npos = n - nj;
+    launch_export(a, false, stream);
+    a.pos = jpos.p;
+    a.npos = nj;
+    launch_export(a, true, stream);
+    a.pos = nullptr;
+    a.npos = n;
+  }
   for (int k = 0; k < EXC_N; ++k) {
     launch_scan_u32(cnt[k].p, X.off[k].p, n, ss(scratch), stream);
     if (!n) HIP_OK(hipMemsetAsync(X.off[k].p, 0, 8, stream));
     a.off[k] = X.off[k].p;
   }
+  if (at) (*at)(1);
   for (int k = 0; k < EXC_N && n; ++k) X.tot[k] = d2h_one(X.off[k].p + n, stream);
   if (d2h_one(err.p, stream)) fail(DR_E_PARSE, "malformed survivor line at export");
   X.stats_bytes = DBuf<uint8_t>(ctx, X.tot[EXC_STATS] + 16);
@@ -2441,7 +2520,35 @@ static void export_device(dr_state& st, int which, DevExport& X, uint64_t lo = 0
   a.tags_val_null = X.tags_val_null.p;
   a.tags_key_bytes = X.tags_key_bytes.p;
   a.tags_val_bytes = X.tags_val_bytes.p;
-  launch_export(a, stream);  // pass 2: bytes and entries
+  // checkpoint rows' map entries: their sources, gathered after pass 2 (JSON entries keep length 0)
+  DBuf<uint64_t> ent_src[4];
+  DBuf<uint32_t> ent_len[4];
+  const uint64_t ent_n[4] = {X.tot[EXC_PV_N], X.tot[EXC_PV_N], X.tot[EXC_TAGS_N], X.tot[EXC_TAGS_N]};
+  for (int q = 0; q < 4; ++q) {
+    ent_src[q] = DBuf<uint64_t>(ctx, ent_n[q] + 1);
+    ent_len[q] = DBuf<uint32_t>(ctx, ent_n[q] + 1);
+    ent_len[q].zero(stream);
+  }
+  a.pv_ksrc = ent_src[0].p;
+  a.pv_vsrc = ent_src[1].p;
+  a.tags_ksrc = ent_src[2].p;
+  a.tags_vsrc = ent_src[3].p;
+  a.pv_klen = ent_len[0].p;
+  a.pv_vlen = ent_len[1].p;
+  a.tags_klen = ent_len[2].p;
+  a.tags_vlen = ent_len[3].p;
+  launch_export(a, true, stream);  // pass 2: bytes and entries
+  launch_gather_bytes(ent_src[0].p, ent_len[0].p, reinterpret_cast<const uint64_t*>(X.pv_key_off.p), ent_n[0],
+                      X.pv_key_bytes.p, stream);
+  launch_gather_bytes(ent_src[1].p, ent_len[1].p, reinterpret_cast<const uint64_t*>(X.pv_val_off.p), ent_n[1],
+                      X.pv_val_bytes.p, stream);
+  launch_gather_bytes(ent_src[2].p, ent_len[2].p, reinterpret_cast<const uint64_t*>(X.tags_key_off.p), ent_n[2],
+                      X.tags_key_bytes.p, stream);
+  launch_gather_bytes(ent_src[3].p, ent_len[3].p, reinterpret_cast<const uint64_t*>(X.tags_val_off.p), ent_n[3],
+                      X.tags_val_bytes.p, stream);
+  // a checkpoint record's stats are one contiguous decoded string: copied whole, several lanes each
+  launch_gather_bytes(stats_src.p, stats_srclen.p, X.off[EXC_STATS].p, n, X.stats_bytes.p, stream);
+  if (at) (*at)(2);
 }
 
 // Both sides' device export columns, built once per state and kept until its release.
@@ -2495,59 +2602,149 @@ static uint64_t record_sum(dr_state& st, int which) {
   return uint64_t(d2h_one(sum.p, stream));
 }
 
+// The host columns of dr_export in three groups, each ready at one point of export_device:
+// 0 paths and deletion timestamps, 1 pass 1's scalars and offsets, 2 the bytes and map entries.
+struct ExportCol {
+  void** dst;
+  const void* src;
+  uint64_t bytes;
+};
+static std::vector<ExportCol> export_group(ExportCols& ex, const DevExport& X, int g, const uint8_t* dvalid,
+                                           const int64_t* ddelts) {
+  const uint64_t n = X.n;
+  if (g == 0)
+    return {{(void**)&ex.path_off, X.path_off.p, 8 * (n + 1)},
+            {(void**)&ex.path_bytes, X.path_bytes.p, X.path_nb},
+            {(void**)&ex.delts, ddelts, 8 * n},
+            {(void**)&ex.delts_valid, dvalid, n}};
+  if (g == 1)
+    return {{(void**)&ex.size, X.size.p, 8 * n},
+            {(void**)&ex.mtime, X.mtime.p, 8 * n},
+            {(void**)&ex.efm, X.efm.p, n},
+            {(void**)&ex.stats_null, X.stats_null.p, n},
+            {(void**)&ex.pv_null, X.pv_null.p, n},
+            {(void**)&ex.tags_null, X.tags_null.p, n},
+            {(void**)&ex.stats_off, X.off[EXC_STATS].p, 8 * (n + 1)},
+            {(void**)&ex.pv_entry_off, X.off[EXC_PV_N].p, 8 * (n + 1)},
+            {(void**)&ex.tags_entry_off, X.off[EXC_TAGS_N].p, 8 * (n + 1)}};
+  return {{(void**)&ex.stats_bytes, X.stats_bytes.p, X.tot[EXC_STATS]},
+          {(void**)&ex.pv_key_off, X.pv_key_off.p, 8 * (X.tot[EXC_PV_N] + 1)},
+          {(void**)&ex.pv_val_off, X.pv_val_off.p, 8 * (X.tot[EXC_PV_N] + 1)},
+          {(void**)&ex.pv_val_null, X.pv_val_null.p, X.tot[EXC_PV_N]},
+          {(void**)&ex.pv_key_bytes, X.pv_key_bytes.p, X.tot[EXC_PV_KB]},
+          {(void**)&ex.pv_val_bytes, X.pv_val_bytes.p, X.tot[EXC_PV_VB]},
+          {(void**)&ex.tags_key_off, X.tags_key_off.p, 8 * (X.tot[EXC_TAGS_N] + 1)},
+          {(void**)&ex.tags_val_off, X.tags_val_off.p, 8 * (X.tot[EXC_TAGS_N] + 1)},
+          {(void**)&ex.tags_val_null, X.tags_val_null.p, X.tot[EXC_TAGS_N]},
+          {(void**)&ex.tags_key_bytes, X.tags_key_bytes.p, X.tot[EXC_TAGS_KB]},
+          {(void**)&ex.tags_val_bytes, X.tags_val_bytes.p, X.tot[EXC_TAGS_VB]}};
+}
+static uint64_t group_bytes(const std::vector<ExportCol>& cols) {
+  uint64_t t = 0;
+  for (const ExportCol& c : cols) t += (c.bytes + 63) & ~uint64_t(63);
+  return t;
+}
+// Carves the columns out of the pinned block (64-byte aligned slices) and queues their copies.
+static void queue_group(const std::vector<ExportCol>& cols, void* block, hipStream_t s) {
+  uint8_t* at = static_cast<uint8_t*>(block);
+  for (const ExportCol& c : cols) {
+    *c.dst = at;
+    if (c.bytes) HIP_OK(hipMemcpyAsync(at, c.src, c.bytes, hipMemcpyDeviceToHost, s));
+    at += (c.bytes + 63) & ~uint64_t(63);
+  }
+}
+
+// dr_state_export: the side's resident columns into pinned host memory. A side not yet materialised
+// is streamed: its column groups cross to the host on stream2 while the device still extracts the
+// later groups (the paths during the checkpoint decode and pass 1, the scalars during pass 2), and
+// the pinned blocks of groups 0 and 1 -- sized by the record count alone -- are taken from the
+// context's cache (or pinned) on a helper thread while the device works.
 static void build_export(dr_state& st, int which) {
   ensure_ready(st);
   ExportCols& ex = st.exp[which];
   if (ex.built) return;
   dr_ctx* ctx = st.ctx;
   hipStream_t stream = ctx->stream;
-  const DevExport& X = materialize(st, which);
-  const uint64_t n = X.n;
-  ex.n = int64_t(n);
   ex.ctx = ctx;
-  // delTs validity is F_HAS_DELTS, and an absent delTs reads 0 (one device pass, no host loop)
-  DBuf<uint8_t> dvalid(ctx, n);
-  DBuf<int64_t> ddelts(ctx, n);
-  launch_delts_fix(X.flags.p, reinterpret_cast<const int64_t*>(X.delts.p), n, dvalid.p, ddelts.p, stream);
-  const uint64_t nb = n ? d2h_one(X.path_off.p + n, stream) : 0;
-  // carve the columns out of one pinned block (8-byte aligned slices), then queue every copy
-  struct Col { void** dst; const void* src; uint64_t bytes; };
-  std::vector<Col> cols = {
-      {(void**)&ex.path_off, X.path_off.p, 8 * (n + 1)},
-      {(void**)&ex.path_bytes, X.path_bytes.p, nb},
-      {(void**)&ex.delts, ddelts.p, 8 * n},
-      {(void**)&ex.delts_valid, dvalid.p, n},
-      {(void**)&ex.size, X.size.p, 8 * n},
-      {(void**)&ex.mtime, X.mtime.p, 8 * n},
-      {(void**)&ex.efm, X.efm.p, n},
-      {(void**)&ex.stats_null, X.stats_null.p, n},
-      {(void**)&ex.pv_null, X.pv_null.p, n},
-      {(void**)&ex.tags_null, X.tags_null.p, n},
-      {(void**)&ex.stats_off, X.off[EXC_STATS].p, 8 * (n + 1)},
-      {(void**)&ex.pv_entry_off, X.off[EXC_PV_N].p, 8 * (n + 1)},
-      {(void**)&ex.tags_entry_off, X.off[EXC_TAGS_N].p, 8 * (n + 1)},
-      {(void**)&ex.stats_bytes, X.stats_bytes.p, X.tot[EXC_STATS]},
-      {(void**)&ex.pv_key_off, X.pv_key_off.p, 8 * (X.tot[EXC_PV_N] + 1)},
-      {(void**)&ex.pv_val_off, X.pv_val_off.p, 8 * (X.tot[EXC_PV_N] + 1)},
-      {(void**)&ex.pv_val_null, X.pv_val_null.p, X.tot[EXC_PV_N]},
-      {(void**)&ex.pv_key_bytes, X.pv_key_bytes.p, X.tot[EXC_PV_KB]},
-      {(void**)&ex.pv_val_bytes, X.pv_val_bytes.p, X.tot[EXC_PV_VB]},
-      {(void**)&ex.tags_key_off, X.tags_key_off.p, 8 * (X.tot[EXC_TAGS_N] + 1)},
-      {(void**)&ex.tags_val_off, X.tags_val_off.p, 8 * (X.tot[EXC_TAGS_N] + 1)},
-      {(void**)&ex.tags_val_null, X.tags_val_null.p, X.tot[EXC_TAGS_N]},
-      {(void**)&ex.tags_key_bytes, X.tags_key_bytes.p, X.tot[EXC_TAGS_KB]},
-      {(void**)&ex.tags_val_bytes, X.tags_val_bytes.p, X.tot[EXC_TAGS_VB]},
+  DBuf<uint8_t> dvalid;
+  DBuf<int64_t> ddelts;
+  auto fix_delts = [&](const DevExport& X) {  // delTs validity is F_HAS_DELTS; an absent delTs reads 0
+    dvalid = DBuf<uint8_t>(ctx, X.n);
+    ddelts = DBuf<int64_t>(ctx, X.n);
+    launch_delts_fix(X.flags.p, reinterpret_cast<const int64_t*>(X.delts.p), X.n, dvalid.p, ddelts.p, stream);
   };
-  uint64_t total = 0;
-  for (const Col& c : cols) total += (c.bytes + 63) & ~uint64_t(63);
-  ex.block = ctx->host_alloc(total);
-  uint8_t* at = static_cast<uint8_t*>(ex.block);
-  for (const Col& c : cols) {
-    *c.dst = at;
-    if (c.bytes) HIP_OK(hipMemcpyAsync(at, c.src, c.bytes, hipMemcpyDeviceToHost, stream));
-    at += (c.bytes + 63) & ~uint64_t(63);
+  if (st.dexp[which]) {  // materialised before: one block, every copy queued at once
+    const DevExport& X = *st.dexp[which];
+    ex.n = int64_t(X.n);
+    fix_delts(X);
+    std::vector<ExportCol> cols;
+    for (int g = 0; g < 3; ++g) {
+      std::vector<ExportCol> c = export_group(ex, X, g, dvalid.p, ddelts.p);
+      cols.insert(cols.end(), c.begin(), c.end());
+    }
+    ex.blocks.push_back(ctx->host_alloc(group_bytes(cols)));
+    queue_group(cols, ex.blocks.back(), stream);
+    HIP_OK(hipStreamSynchronize(stream));
+    ex.built = true;
+    return;
   }
+  auto Xp = std::make_shared<DevExport>();
+  DevExport& X = *Xp;
+  hipStream_t cs = ctx->stream2;
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  for (hipEvent_t& e : ev) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  std::thread pin;
+  void* block01 = nullptr;
+  std::exception_ptr pin_err;
+  const std::function<void(int)> at = [&](int g) {
+    if (g == 0) {
+      fix_delts(X);
+      HIP_OK(hipEventRecord(ev[0], stream));
+      // groups 0 and 1 are sized by the record count and the path bytes (group 1's columns are not
+      // allocated yet: only its sizes are read here)
+      const uint64_t b0 = group_bytes(export_group(ex, X, 0, dvalid.p, ddelts.p));
+      const uint64_t b1 = group_bytes(export_group(ex, X, 1, dvalid.p, ddelts.p));
+      pin = std::thread([&, b0, b1] {
+        try {
+          HIP_OK(hipSetDevice(ctx->device));
+          block01 = ctx->host_alloc(b0 + b1);
+        } catch (...) {
+          pin_err = std::current_exception();
+        }
+      });
+    } else if (g == 1) {
+      HIP_OK(hipEventRecord(ev[1], stream));
+      pin.join();
+      if (pin_err) std::rethrow_exception(pin_err);
+      ex.blocks.push_back(block01);
+      HIP_OK(hipStreamWaitEvent(cs, ev[0], 0));
+      const std::vector<ExportCol> c0 = export_group(ex, X, 0, dvalid.p, ddelts.p);
+      const std::vector<ExportCol> c1 = export_group(ex, X, 1, dvalid.p, ddelts.p);
+      queue_group(c0, block01, cs);
+      HIP_OK(hipStreamWaitEvent(cs, ev[1], 0));
+      queue_group(c1, static_cast<uint8_t*>(block01) + group_bytes(c0), cs);
+    } else {
+      HIP_OK(hipEventRecord(ev[2], stream));
+      std::vector<ExportCol> c2 = export_group(ex, X, 2, dvalid.p, ddelts.p);
+      ex.blocks.push_back(ctx->host_alloc(group_bytes(c2)));
+      HIP_OK(hipStreamWaitEvent(cs, ev[2], 0));
+      queue_group(c2, ex.blocks.back(), cs);
+    }
+  };
+  try {
+    export_device(st, which, X, 0, UINT64_MAX, &at);
+  } catch (...) {
+    if (pin.joinable()) pin.join();
+    if (block01 && (ex.blocks.empty() || ex.blocks.front() != block01)) ctx->host_release(block01);
+    (void)hipStreamSynchronize(cs);
+    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+    throw;
+  }
+  ex.n = int64_t(X.n);
+  HIP_OK(hipStreamSynchronize(cs));
   HIP_OK(hipStreamSynchronize(stream));
+  for (hipEvent_t e : ev) HIP_OK(hipEventDestroy(e));
+  st.dexp[which] = Xp;
   ex.built = true;
 }
 
@@ -3776,7 +3973,9 @@ static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred)
   }
   LeafPlan lp;
   const bool force_generic = std::getenv("DR_FILTER_GENERIC") != nullptr;  // test hook: k_filter_typed
-  if (!force_generic && leafify(pred, lp)) {
+  if (!force_generic && leafify(pred, lp) && lp.prog.size() / 2 <= filter_leaf_max_prog() &&
+      lp.leaves.size() <= filter_leaf_max_leaves() && lp.i64.size() <= filter_leaf_max_i64() &&
+      lp.str.size() <= filter_leaf_max_str()) {
     FilterLeafArgs la{};
     la.n_live = st.n_live;
     for (int32_t c = 0; c < pred.ncols; ++c) la.cols[c] = fa.cols[c];
@@ -3789,12 +3988,10 @@ static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred)
     }
     DBuf<uint64_t> d_s8 = upload(ctx, s8.data(), s8.size());
     la.lit_s8 = d_s8.p;
-    DBuf<FilterLeaf> d_leaves = upload(ctx, lp.leaves.data(), lp.leaves.size());
     DBuf<int32_t> d_prog = upload(ctx, lp.prog.data(), lp.prog.size());
     DBuf<int64_t> d_i64 = upload(ctx, lp.i64.data(), lp.i64.size());
     DBuf<uint64_t> d_soff = upload(ctx, soff.data(), soff.size());
     DBuf<uint8_t> d_sb = upload(ctx, reinterpret_cast<const uint8_t*>(sbytes.data()), sbytes.size());
-    la.leaves = d_leaves.p;
     la.prog = d_prog.p;
     la.nprog = int32_t(lp.prog.size() / 2);
     la.lit_i64 = d_i64.p;
@@ -3802,10 +3999,25 @@ static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred)
     la.lit_str = d_sb.p;
     la.n_i64 = int32_t(lp.i64.size());
     la.n_str = int32_t(lp.str.size());
+    la.nleaves = int32_t(lp.leaves.size());
+    std::vector<int32_t> ucol;
+    for (const FilterLeaf& f : lp.leaves)
+      if (std::find(ucol.begin(), ucol.end(), f.col) == ucol.end()) ucol.push_back(f.col);
+    la.nucol = ucol.size() <= size_t(FL_UCOLS) ? int32_t(ucol.size()) : 0;
+    for (int32_t u = 0; u < la.nucol; ++u) la.ucol[u] = ucol[size_t(u)];
+    for (FilterLeaf& f : lp.leaves) {
+      f.slot = -1;
+      for (int32_t u = 0; u < la.nucol; ++u)
+        if (la.ucol[u] == f.col) f.slot = u;
+      f.ctype = la.cols[f.col].type;
+    }
+    DBuf<FilterLeaf> d_leaves = upload(ctx, lp.leaves.data(), lp.leaves.size());
+    la.leaves = d_leaves.p;
     const uint64_t ng = filter_leaf_groups(st.n_live);
-    DBuf<uint64_t> mask(ctx, 16 * ng), wg_off(ctx, ng + 1);
+    DBuf<uint64_t> mask(ctx, uint64_t(filter_leaf_mask_words()) * ng), wg_off(ctx, ng + 1);
     DBuf<uint32_t> wg_count(ctx, ng);
     DBuf<uint8_t> scratch(ctx, scan_scratch_for(ng));
+    wg_count.zero(stream);
     la.mask = mask.p;
     la.wg_count = wg_count.p;
     launch_filter_leaf(la, stream);

@@ -90,7 +90,7 @@ __device__ __forceinline__ bool key_is(const uint8_t* s, uint32_t n, bool esc, c
 // Iterates the members of the object starting at p ('{'); f(key, klen, kesc, value_start) returns
 // the position after the value. Returns false on malformed input.
 template <typename F>
-__device__ bool each_member(const uint8_t* p, const uint8_t* e, F&& f) {
+__device__ __forceinline__ bool each_member(const uint8_t* p, const uint8_t* e, F&& f) {
   if (p >= e || *p != '{') return false;
   ++p;
   while (true) {
@@ -881,129 +881,196 @@ __device__ __forceinline__ uint32_t eval_leaf(const FilterLeafArgs& a, const Fil
 // round trip serves four files. The result leaves as bits -- one 64-bit mask per 64 files, in file
 // order -- plus the workgroup's count, which k_select_bits turns into the selected ordinals after a
 // scan of the counts (no 4-byte flag per file, no scan over files).
-constexpr int FL_T = 256, FL_PER = 4;
-constexpr uint32_t FL_FILES = FL_T * FL_PER;  // files per workgroup (16 mask words)
+#ifndef DR_FL_PER
+#define DR_FL_PER 4
+#endif
+#ifndef DR_FL_GRID
+#define DR_FL_GRID 4  // resident workgroups per CU of the persistent grid (0: one workgroup per tile)
+#endif
+constexpr int FL_T = 256, FL_PER = DR_FL_PER;
+constexpr uint32_t FL_FILES = FL_T * FL_PER;  // files per tile (4 FL_PER mask words)
 
-__device__ __forceinline__ void eval_leaf4(const FilterLeafArgs& a, const FilterLeaf& L, uint64_t i0,
-                                           uint32_t (&res)[FL_PER]) {
-  const PvColumn& col = a.cols[L.col];
-  const bool str = col.type == DR_T_STRING, lng = col.type == DR_T_LONG;  // uniform
-  uint32_t nul[FL_PER], vn[FL_PER];
-  uint64_t v8[FL_PER];
-  int64_t v[FL_PER];
-#pragma unroll
-  for (int j = 0; j < FL_PER; ++j) {
-    const uint64_t i = i0 + uint64_t(j) * FL_T;
-    const bool ok = i < a.n_live;
-    nul[j] = ok ? col.isnull[i] : 1u;
-    vn[j] = 0;
-    v8[j] = 0;
-    v[j] = 0;
+// The leaf result from a column value already in registers (nul, v = integer or big-endian 8-byte
+// string prefix, vn = string length); the long-string gather reads the column by file ordinal i.
+// The literals are the workgroup's LDS copies (li: integers and IN sets, ls8 / lso: the string
+// literals' prefixes and offsets).
+__device__ __forceinline__ uint32_t leaf_value(const FilterLeafArgs& a, const FilterLeaf& L, const PvColumn& col,
+                                               uint64_t i, uint32_t nul, int64_t v, uint32_t vn, const int64_t* li,
+                                               const uint64_t* ls8, const uint64_t* lso) {
+  const bool str = L.ctype == DR_T_STRING;
+  const bool vnull = nul != 0;
+  if (L.op == DR_OP_ISNULL) return vnull ? 1u : 0u;
+  if (L.op == DR_OP_ISNOTNULL) return vnull ? 0u : 1u;
+  if (L.op == DR_OP_NSEQ && (vnull || L.lit_null)) return (vnull && L.lit_null) ? 1u : 0u;
+  if (L.op != DR_OP_IN && L.lit_null) return 2u;
+  if (vnull) return 2u;
+  const uint64_t v8 = uint64_t(v);
+  auto cmp_lit = [&](int32_t k) -> int {
     if (str) {
-      vn[j] = ok ? col.slen[i] : 0u;
-      v8[j] = ok ? col.s8[i] : 0ull;
-    } else if (lng) {
-      v[j] = ok ? col.w64[i] : 0;
-    } else {
-      v[j] = ok ? int64_t(int32_t(col.w32[i])) : 0;
+      const uint64_t o = lso[k];
+      const uint32_t ln = uint32_t(lso[k + 1] - o);
+      const uint64_t l8 = ls8[k];
+      if (v8 != l8) return v8 < l8 ? -1 : 1;
+      if (vn <= 8 && ln <= 8) return vn == ln ? 0 : (vn < ln ? -1 : 1);
+      return bytes_cmp(reinterpret_cast<const uint8_t*>(col.sptr[i]), vn, a.lit_str + o, ln);
     }
+    const int64_t x = li[k];
+    return v == x ? 0 : (v < x ? -1 : 1);
+  };
+  if (L.op == DR_OP_IN && L.pad == 1) {  // an integer set as a bitmap over [min, min + 64 * words)
+    const uint64_t d = uint64_t(v) - uint64_t(li[L.lit]);
+    const uint64_t nbits = uint64_t(li[L.lit + 1]) * 64;
+    return (d < nbits && ((uint64_t(li[L.lit + 2 + uint32_t((nbits ? min(d, nbits - 1) : 0ull) >> 6)]) >> (d & 63)) & 1u)) ? 1u
+           : (L.lit_null ? 2u : 0u);
   }
-#pragma unroll
-  for (int j = 0; j < FL_PER; ++j) {
-    const uint64_t i = i0 + uint64_t(j) * FL_T;
-    const bool vnull = nul[j] != 0;
-    uint32_t r;
-    if (L.op == DR_OP_ISNULL) r = vnull ? 1u : 0u;
-    else if (L.op == DR_OP_ISNOTNULL) r = vnull ? 0u : 1u;
-    else if (L.op == DR_OP_NSEQ && (vnull || L.lit_null)) r = (vnull && L.lit_null) ? 1u : 0u;
-    else if (L.op != DR_OP_IN && L.lit_null) r = 2u;
-    else if (vnull) r = 2u;
-    else {
-      // strings: the big-endian 8-byte prefixes order like the bytes; equal prefixes of two values of
-      // at most 8 bytes leave only the lengths; otherwise the value bytes are gathered
-      auto cmp_lit = [&](int32_t k) -> int {
-        if (str) {
-          const uint64_t o = a.lit_str_off[k];
-          const uint32_t ln = uint32_t(a.lit_str_off[k + 1] - o);
-          const uint64_t l8 = a.lit_s8[k];
-          if (v8[j] != l8) return v8[j] < l8 ? -1 : 1;
-          if (vn[j] <= 8 && ln <= 8) return vn[j] == ln ? 0 : (vn[j] < ln ? -1 : 1);
-          return bytes_cmp(reinterpret_cast<const uint8_t*>(col.sptr[i]), vn[j], a.lit_str + o, ln);
-        }
-        const int64_t x = a.lit_i64[k];
-        return v[j] == x ? 0 : (v[j] < x ? -1 : 1);
-      };
-      if (L.op == DR_OP_IN && L.pad == 1) {  // an integer set as a bitmap over [min, min + 64 * words)
-        const uint64_t d = uint64_t(v[j]) - uint64_t(a.lit_i64[L.lit]);
-        const uint64_t nbits = uint64_t(a.lit_i64[L.lit + 1]) * 64;
-        r = (d < nbits && ((uint64_t(a.lit_i64[L.lit + 2 + (d >> 6)]) >> (d & 63)) & 1u)) ? 1u
-            : (L.lit_null ? 2u : 0u);
-      } else if (L.op == DR_OP_IN) {  // binary search of the sorted set
-        int32_t lo = L.lit, hi = L.lit + L.nlit;
-        r = L.lit_null ? 2u : 0u;
-        while (lo < hi) {
-          const int32_t mid = (lo + hi) >> 1;
-          const int c = cmp_lit(mid);
-          if (c == 0) { r = 1u; break; }
-          if (c > 0) lo = mid + 1; else hi = mid;
-        }
-      } else {
-        const int c = cmp_lit(L.lit);
-        switch (L.op) {
-          case DR_OP_EQ: case DR_OP_NSEQ: r = c == 0; break;
-          case DR_OP_NE: r = c != 0; break;
-          case DR_OP_LT: r = c < 0; break;
-          case DR_OP_LE: r = c <= 0; break;
-          case DR_OP_GT: r = c > 0; break;
-          default: r = c >= 0; break;
-        }
-      }
+  if (L.op == DR_OP_IN) {  // binary search of the sorted set
+    int32_t lo = L.lit, hi = L.lit + L.nlit;
+    while (lo < hi) {
+      const int32_t mid = (lo + hi) >> 1;
+      const int c = cmp_lit(mid);
+      if (c == 0) return 1u;
+      if (c > 0) lo = mid + 1; else hi = mid;
     }
-    res[j] = r;
+    return L.lit_null ? 2u : 0u;
+  }
+  const int c = cmp_lit(L.lit);
+  switch (L.op) {
+    case DR_OP_EQ: case DR_OP_NSEQ: return c == 0;
+    case DR_OP_NE: return c != 0;
+    case DR_OP_LT: return c < 0;
+    case DR_OP_LE: return c <= 0;
+    case DR_OP_GT: return c > 0;
+    default: return c >= 0;
   }
 }
 
-__global__ void __launch_bounds__(FL_T) k_filter_leaf(FilterLeafArgs a) {
-  __shared__ uint32_t wcount[FL_T / 64];
-  const uint64_t base = uint64_t(blockIdx.x) * FL_FILES;
-  const uint64_t i0 = base + threadIdx.x;
-  uint64_t stk[FL_PER] = {0, 0, 0, 0};  // per file: 2 bits per entry, top at the low end
-  for (int k = 0; k < a.nprog; ++k) {
-    const int op = a.prog[2 * k];
-    if (op == LEAF_OP_LEAF) {
-      uint32_t r[FL_PER];
-      eval_leaf4(a, a.leaves[a.prog[2 * k + 1]], i0, r);
-#pragma unroll
-      for (int j = 0; j < FL_PER; ++j) stk[j] = (stk[j] << 2) | r[j];
-    } else if (op == LEAF_OP_NOT) {
-#pragma unroll
-      for (int j = 0; j < FL_PER; ++j) {
-        const uint64_t x = stk[j] & 3u;
-        stk[j] = (stk[j] & ~3ull) | (x == 2u ? 2u : (x ^ 1u));
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < FL_PER; ++j) {
-        const uint32_t y = uint32_t(stk[j] & 3u), x = uint32_t((stk[j] >> 2) & 3u);
-        uint32_t r;
-        if (op == LEAF_OP_AND) r = (x == 0u || y == 0u) ? 0u : (x == 1u && y == 1u) ? 1u : 2u;
-        else r = (x == 1u || y == 1u) ? 1u : (x == 0u && y == 0u) ? 0u : 2u;
-        stk[j] = ((stk[j] >> 4) << 2) | r;
-      }
-    }
-  }
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint32_t cnt = 0;
+// One column's values of a thread's FL_PER files (strided by the workgroup: each load instruction
+// of a wave reads 64 consecutive files; all loads in flight before any is used). The tile's base is
+// folded into uniform column pointers, so every load is a scalar base plus a 32-bit lane offset.
+__device__ __forceinline__ void load_col4(const FilterLeafArgs& a, const PvColumn& col, int ctype, uint64_t base,
+                                          bool full, uint32_t (&nul)[FL_PER], uint32_t (&vn)[FL_PER],
+                                          int64_t (&v)[FL_PER]) {
+  const bool str = ctype == DR_T_STRING, lng = ctype == DR_T_LONG;  // uniform
+  const uint8_t* pn = col.isnull + base;
 #pragma unroll
   for (int j = 0; j < FL_PER; ++j) {
-    const bool f = i0 + uint64_t(j) * FL_T < a.n_live && (stk[j] & 3u) == 1u;
-    const unsigned long long m = __ballot(f);
-    if (lane == 0) a.mask[base / 64 + 4 * j + wv] = m;
-    cnt += uint32_t(__popcll(m));
+    const uint32_t o = threadIdx.x + uint32_t(j) * FL_T;
+    const bool ok = full || base + o < a.n_live;
+    nul[j] = ok ? pn[o] : 1u;
+    vn[j] = 0;
+    v[j] = 0;
+    if (str) {
+      vn[j] = ok ? col.slen[base + o] : 0u;
+      v[j] = ok ? int64_t(col.s8[base + o]) : 0;
+    } else if (lng) {
+      v[j] = ok ? col.w64[base + o] : 0;
+    } else {
+      v[j] = ok ? int64_t(int32_t(col.w32[base + o])) : 0;
+    }
   }
-  if (lane == 0) wcount[wv] = cnt;
+}
+
+// Persistent workgroups (grid-stride over tiles of FL_FILES files). The program, its leaves and
+// every literal are copied to LDS once per workgroup, and the leaf fields are read as wave-uniform
+// (scalar) values, so a tile issues no load but its column values: r04's first persistent build read
+// the leaf from LDS into vector registers, which turned the column descriptor and every literal into
+// per-lane global loads -- three dependent round trips per leaf and tile (2.53 ms for 100M files).
+// When the program reads at most FL_UCOLS distinct columns, every value a tile needs is loaded up
+// front and each leaf reads its column's slot (fixed by the host: a scalar branch picks it);
+// otherwise each leaf loads its own column. A wave adds its selected count to its tile's (zeroed)
+// count: no barrier per tile.
+constexpr int FL_MAXPROG = 128, FL_MAXLEAF = 64, FL_MAXI64 = 1024, FL_MAXSTR = 256;
+__global__ void __launch_bounds__(FL_T) k_filter_leaf(FilterLeafArgs a) {
+  __shared__ int32_t sprog[2 * FL_MAXPROG];
+  __shared__ FilterLeaf sleaf[FL_MAXLEAF];
+  __shared__ int64_t slit[FL_MAXI64];
+  __shared__ uint64_t ss8[FL_MAXSTR + 1], ssoff[FL_MAXSTR + 1];
+  for (int k = threadIdx.x; k < 2 * a.nprog; k += FL_T) sprog[k] = a.prog[k];
+  for (int k = threadIdx.x; k < a.nleaves; k += FL_T) sleaf[k] = a.leaves[k];
+  for (int k = threadIdx.x; k < a.n_i64; k += FL_T) slit[k] = a.lit_i64[k];
+  for (int k = threadIdx.x; k <= a.n_str; k += FL_T) {
+    ss8[k] = a.lit_s8[k];
+    ssoff[k] = a.lit_str_off[k];
+  }
   __syncthreads();
-  if (threadIdx.x == 0) a.wg_count[blockIdx.x] = wcount[0] + wcount[1] + wcount[2] + wcount[3];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t ntiles = (a.n_live + FL_FILES - 1) / FL_FILES;
+  const int nu = a.nucol;
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const uint64_t base = tile * FL_FILES;
+    const bool full = base + FL_FILES <= a.n_live;  // uniform: no per-file bound check
+    // the tile's column values: slot u holds predicate column a.ucol[u]
+    uint32_t cn[FL_UCOLS][FL_PER], cl[FL_UCOLS][FL_PER];
+    int64_t cv[FL_UCOLS][FL_PER];
+#pragma unroll
+    for (int u = 0; u < FL_UCOLS; ++u) {
+      if (u >= nu) break;  // uniform
+      const PvColumn& col = a.cols[a.ucol[u]];
+      load_col4(a, col, col.type, base, full, cn[u], cl[u], cv[u]);
+    }
+    uint64_t stk[FL_PER];  // per file: 2 bits per entry, top at the low end
+#pragma unroll
+    for (int j = 0; j < FL_PER; ++j) stk[j] = 0;
+    for (int k = 0; k < a.nprog; ++k) {
+      const int op = __builtin_amdgcn_readfirstlane(sprog[2 * k]);
+      if (op == LEAF_OP_LEAF) {
+        const int li = __builtin_amdgcn_readfirstlane(sprog[2 * k + 1]);
+        FilterLeaf L;
+        L.col = __builtin_amdgcn_readfirstlane(sleaf[li].col);
+        L.op = __builtin_amdgcn_readfirstlane(sleaf[li].op);
+        L.lit = __builtin_amdgcn_readfirstlane(sleaf[li].lit);
+        L.nlit = __builtin_amdgcn_readfirstlane(sleaf[li].nlit);
+        L.lit_null = __builtin_amdgcn_readfirstlane(sleaf[li].lit_null);
+        L.pad = __builtin_amdgcn_readfirstlane(sleaf[li].pad);
+        L.slot = __builtin_amdgcn_readfirstlane(sleaf[li].slot);
+        L.ctype = __builtin_amdgcn_readfirstlane(sleaf[li].ctype);
+        const PvColumn& col = a.cols[L.col];  // read only by the long-string gather
+        uint32_t n0[FL_PER], l0[FL_PER];
+        int64_t v0[FL_PER];
+        if (L.slot >= 0) {  // uniform: the preloaded slot (a select per value, no load)
+#pragma unroll
+          for (int j = 0; j < FL_PER; ++j) {
+            n0[j] = cn[0][j];
+            l0[j] = cl[0][j];
+            v0[j] = cv[0][j];
+#pragma unroll
+            for (int u = 1; u < FL_UCOLS; ++u)
+              if (u == L.slot) { n0[j] = cn[u][j]; l0[j] = cl[u][j]; v0[j] = cv[u][j]; }
+          }
+        } else {
+          load_col4(a, col, L.ctype, base, full, n0, l0, v0);
+        }
+#pragma unroll
+        for (int j = 0; j < FL_PER; ++j)
+          stk[j] = (stk[j] << 2) |
+                   leaf_value(a, L, col, base + threadIdx.x + uint64_t(j) * FL_T, n0[j], v0[j], l0[j], slit, ss8, ssoff);
+      } else if (op == LEAF_OP_NOT) {
+#pragma unroll
+        for (int j = 0; j < FL_PER; ++j) {
+          const uint64_t x = stk[j] & 3u;
+          stk[j] = (stk[j] & ~3ull) | (x == 2u ? 2u : (x ^ 1u));
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < FL_PER; ++j) {
+          const uint32_t y = uint32_t(stk[j] & 3u), x = uint32_t((stk[j] >> 2) & 3u);
+          uint32_t rr;
+          if (op == LEAF_OP_AND) rr = (x == 0u || y == 0u) ? 0u : (x == 1u && y == 1u) ? 1u : 2u;
+          else rr = (x == 1u || y == 1u) ? 1u : (x == 0u && y == 0u) ? 0u : 2u;
+          stk[j] = ((stk[j] >> 4) << 2) | rr;
+        }
+      }
+    }
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int j = 0; j < FL_PER; ++j) {
+      const bool f = (full || base + threadIdx.x + uint64_t(j) * FL_T < a.n_live) && (stk[j] & 3u) == 1u;
+      const unsigned long long m = __ballot(f);
+      if (lane == 0) a.mask[base / 64 + 4 * j + wv] = m;
+      cnt += uint32_t(__popcll(m));
+    }
+    if (lane == 0 && cnt) atomicAdd(&a.wg_count[tile], cnt);
+  }
 }
 
 // The selected ordinals of one k_filter_leaf workgroup's files, in file order: its 16 mask words
@@ -1132,9 +1199,19 @@ void launch_pv_extract(const PvExtractArgs& a, hipStream_t st) {
   if (a.n_live) DR_LAUNCH(dev::k_pv_extract, dim3(g256(a.n_live)), dim3(256), 0, st, a);
 }
 uint64_t filter_leaf_groups(uint64_t n) { return (n + dev::FL_FILES - 1) / dev::FL_FILES; }
+uint32_t filter_leaf_mask_words() { return dev::FL_FILES / 64; }
 void launch_filter_leaf(const FilterLeafArgs& a, hipStream_t st) {
-  if (a.n_live) DR_LAUNCH(dev::k_filter_leaf, dim3(unsigned(filter_leaf_groups(a.n_live))), dim3(dev::FL_T), 0, st, a);
+  if (a.nprog > dev::FL_MAXPROG || a.nleaves > dev::FL_MAXLEAF)
+    throw std::runtime_error("filter program too long for the leaf kernel");
+  // persistent: four resident workgroups per CU (119 VGPRs: 4 waves/SIMD), each walking tiles grid-stride
+  const unsigned g = unsigned(DR_FL_GRID ? std::min<uint64_t>(filter_leaf_groups(a.n_live), 256 * DR_FL_GRID)
+                                          : filter_leaf_groups(a.n_live));
+  if (a.n_live) DR_LAUNCH(dev::k_filter_leaf, dim3(g), dim3(dev::FL_T), 0, st, a);
 }
+uint32_t filter_leaf_max_prog() { return dev::FL_MAXPROG; }
+uint32_t filter_leaf_max_i64() { return dev::FL_MAXI64; }
+uint32_t filter_leaf_max_str() { return dev::FL_MAXSTR; }
+uint32_t filter_leaf_max_leaves() { return dev::FL_MAXLEAF; }
 void launch_select_bits(const uint64_t* mask, const uint64_t* wg_off, uint64_t n, int64_t* out, hipStream_t st) {
   if (n) DR_LAUNCH(dev::k_select_bits, dim3(unsigned(filter_leaf_groups(n))), dim3(dev::FL_T), 0, st, mask, wg_off, n, out);
 }
@@ -1278,8 +1355,20 @@ void launch_group_flags(const uint32_t* keys, uint64_t n, const GroupCols& g, ui
 // where a string is expected keeps its JSON text without insignificant whitespace.
 namespace dev {
 
+// Short copies (map keys and values): eight loads in flight before their stores (a plain byte loop
+// waits for each load, and on gfx9 a load's wait also waits for every earlier store).
 __device__ __forceinline__ void bytes_copy(uint8_t* d, const uint8_t* s, uint32_t n) {
-  for (uint32_t k = 0; k < n; ++k) d[k] = s[k];
+  for (uint32_t k0 = 0; k0 < n; k0 += 8) {
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {
+      const uint32_t b = k0 + k < n ? uint32_t(s[k0 + k]) : 0u;
+      if (k < 4) lo |= b << (8 * k); else hi |= b << (8 * (k - 4));
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k)
+      if (k0 + k < n) d[k0 + k] = uint8_t((k < 4 ? lo : hi) >> (8 * (k & 3)));
+  }
 }
 
 __device__ uint32_t json_unescape_len(const uint8_t* s, uint32_t n) {
@@ -1327,7 +1416,7 @@ __device__ uint32_t compact_json(const uint8_t* v, const uint8_t* end, uint8_t* 
 }
 
 // A JSON value where a string is expected: {null?, bytes}. Pass 1 counts, pass 2 writes at out.
-__device__ uint32_t string_value(const uint8_t* v, const uint8_t* end, bool* is_null, uint8_t* out) {
+__device__ __forceinline__ uint32_t string_value(const uint8_t* v, const uint8_t* end, bool* is_null, uint8_t* out) {
   *is_null = false;
   if (v < end && *v == '"') {
     bool esc = false;
@@ -1359,6 +1448,10 @@ __device__ bool keys_equal(const uint8_t* a, uint32_t an, bool aesc, const uint8
 
 struct MapSink {
   uint32_t n, kb, vb;                   // entries and bytes so far
+  uint64_t* ksrc;                       // pass 2, checkpoint rows: this record's first entry's source slots
+  uint64_t* vsrc;
+  uint32_t* klen;
+  uint32_t* vlen;
   uint8_t* kbytes;                      // pass 2: this record's first key byte
   uint8_t* vbytes;
   int64_t* koff;                        // pass 2: this record's first entry's end-offset slot
@@ -1367,7 +1460,7 @@ struct MapSink {
   int64_t kbase, vbase;                 // absolute offsets of kbytes / vbytes
 };
 
-__device__ void sink_entry_json(MapSink& m, bool write, const uint8_t* k, uint32_t kn, bool kesc, const uint8_t* v,
+__device__ __forceinline__ void sink_entry_json(MapSink& m, bool write, const uint8_t* k, uint32_t kn, bool kesc, const uint8_t* v,
                                 const uint8_t* vend) {
   const uint32_t kl = kesc ? (write ? json_unescape(k, kn, m.kbytes + m.kb) : json_unescape_len(k, kn))
                            : (write ? (bytes_copy(m.kbytes + m.kb, k, kn), kn) : kn);
@@ -1384,7 +1477,7 @@ __device__ void sink_entry_json(MapSink& m, bool write, const uint8_t* k, uint32
 }
 
 // Entries of the JSON object at m0 ('{') into the sink (first position, last value per key).
-__device__ bool json_map(const uint8_t* m0, const uint8_t* e, MapSink& m, bool write) {
+__device__ __forceinline__ bool json_map(const uint8_t* m0, const uint8_t* e, MapSink& m, bool write) {
   return each_member(m0, e, [&](const uint8_t* k, uint32_t kn, bool kesc, const uint8_t* v) -> const uint8_t* {
     const uint8_t* vend = skip_value(v, e);
     bool first = true, after = false;
@@ -1405,64 +1498,103 @@ __device__ bool json_map(const uint8_t* m0, const uint8_t* e, MapSink& m, bool w
   });
 }
 
-__device__ void ck_map(const ExpMap& cm, uint64_t r, MapSink& m, bool write, uint8_t* is_null) {
+// A checkpoint row's map entries, CK_BATCH at a time: the batch's levels, lengths and addresses are
+// loaded before any is used (r04: one entry's chain of loads per step left pass 1 latency-bound).
+// Pass 2 writes the entries' offsets and their sources; the bytes follow in k_gather_bytes.
+constexpr uint32_t CK_BATCH = 4;
+template <bool Write>
+__device__ __forceinline__ void ck_map(const ExpMap& cm, uint64_t r, MapSink& m, uint8_t* is_null) {
   *is_null = 1;
   if (!cm.row_start) return;
-  for (uint64_t en = cm.row_start[r]; en < cm.row_start[r + 1]; ++en) {
-    const int d = cm.kdef[en];
-    if (d >= cm.map_def) *is_null = 0;
-    if (d < cm.entry_def) continue;
-    const uint32_t kl = cm.klen[en];
-    const bool vn = cm.vdef[en] != cm.vmax;
-    const uint32_t vl = vn ? 0u : cm.vlen[en];
-    if (write) {
-      bytes_copy(m.kbytes + m.kb, reinterpret_cast<const uint8_t*>(cm.kptr[en]), kl);
-      if (!vn) bytes_copy(m.vbytes + m.vb, reinterpret_cast<const uint8_t*>(cm.vptr[en]), vl);
+  const uint64_t e0 = cm.row_start[r], e1 = cm.row_start[r + 1];
+  for (uint64_t b = e0; b < e1; b += CK_BATCH) {
+    int kd[CK_BATCH], vd[CK_BATCH];
+    uint32_t kl[CK_BATCH], vl[CK_BATCH];
+    uint64_t kp[CK_BATCH], vp[CK_BATCH];
+#pragma unroll
+    for (uint32_t q = 0; q < CK_BATCH; ++q) {
+      const uint64_t en = b + q;
+      const bool ok = en < e1;
+      kd[q] = ok ? int(cm.kdef[en]) : -1;
+      kl[q] = ok ? cm.klen[en] : 0u;
+      vd[q] = ok ? int(cm.vdef[en]) : 0;
+      vl[q] = ok ? cm.vlen[en] : 0u;
+      if (Write) {
+        kp[q] = ok ? cm.kptr[en] : 0ull;
+        vp[q] = ok ? cm.vptr[en] : 0ull;
+      }
     }
-    m.kb += kl;
-    m.vb += vl;
-    if (write) {
-      m.koff[m.n] = m.kbase + m.kb;
-      m.voff[m.n] = m.vbase + m.vb;
-      m.vnull[m.n] = vn ? 1 : 0;
+#pragma unroll
+    for (uint32_t q = 0; q < CK_BATCH; ++q) {
+      const int d = kd[q];
+      if (d >= cm.map_def) *is_null = 0;
+      if (d < cm.entry_def) continue;  // also the batch's entries past the row (-1)
+      const bool vn = vd[q] != cm.vmax;
+      const uint32_t vlen = vn ? 0u : vl[q];
+      if (Write) {  // the bytes are copied by k_gather_bytes, several lanes per string
+        m.ksrc[m.n] = kp[q];
+        m.klen[m.n] = kl[q];
+        m.vsrc[m.n] = vp[q];
+        m.vlen[m.n] = vlen;
+      }
+      m.kb += kl[q];
+      m.vb += vlen;
+      if (Write) {
+        m.koff[m.n] = m.kbase + m.kb;
+        m.voff[m.n] = m.vbase + m.vb;
+        m.vnull[m.n] = vn ? 1 : 0;
+      }
+      ++m.n;
     }
-    ++m.n;
   }
 }
 
-__global__ void __launch_bounds__(256) k_export(ExportArgs a) {
-  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= a.n) return;
-  const bool write = a.write != 0;
-  const uint32_t act = a.idx[i];
-  MapSink pv{0, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0};
-  MapSink tg = pv;
-  uint8_t* sbytes = nullptr;
-  if (write) {
-    pv.kbytes = a.pv_key_bytes + a.off[EXC_PV_KB][i];
-    pv.vbytes = a.pv_val_bytes + a.off[EXC_PV_VB][i];
-    pv.koff = a.pv_key_off + a.off[EXC_PV_N][i] + 1;
-    pv.voff = a.pv_val_off + a.off[EXC_PV_N][i] + 1;
-    pv.vnull = a.pv_val_null + a.off[EXC_PV_N][i];
-    pv.kbase = int64_t(a.off[EXC_PV_KB][i]);
-    pv.vbase = int64_t(a.off[EXC_PV_VB][i]);
-    tg.kbytes = a.tags_key_bytes + a.off[EXC_TAGS_KB][i];
-    tg.vbytes = a.tags_val_bytes + a.off[EXC_TAGS_VB][i];
-    tg.koff = a.tags_key_off + a.off[EXC_TAGS_N][i] + 1;
-    tg.voff = a.tags_val_off + a.off[EXC_TAGS_N][i] + 1;
-    tg.vnull = a.tags_val_null + a.off[EXC_TAGS_N][i];
-    tg.kbase = int64_t(a.off[EXC_TAGS_KB][i]);
-    tg.vbase = int64_t(a.off[EXC_TAGS_VB][i]);
-    sbytes = a.stats_bytes + a.off[EXC_STATS][i];
+// The walkers above step through a line one dependent byte at a time, so each step costs a load's
+// round trip: from L2 a lane spends ~2.5 us per survivor line (r04 probe: 15 + 32 ms for the live
+// side's two passes at config 3). k_export therefore stages its wave's lines in LDS first -- each
+// lane copies its own line with independent 16-byte loads, EXP_BATCH in flight -- and walks the
+// staged copy (generic pointers: a line that does not fit is walked in place). A slot holds the
+// line's aligned 16-byte chunks, so the line sits at slot + (start & 15); the buffer keeps 32 bytes of
+// padding after the last slot for the walkers' word reads past a line's end.
+#ifndef DR_EXP_STAGE
+#define DR_EXP_STAGE 24576
+#endif
+constexpr uint32_t EXP_STAGE = DR_EXP_STAGE;
+constexpr uint32_t EXP_BATCH = 8;
+
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) {
+  const int lane = threadIdx.x & 63;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
   }
+  *total = __shfl(x, 63, 64);
+  return x - v;
+}
+
+// Pass 2's output streams: the wave's records write each stream to one contiguous range (the
+// exclusive scans of pass 1's counts), so the records' bytes and entries are assembled in LDS and
+// the wave stores each range with aligned 16-byte stores. Written in place instead, every byte store
+// sat in the same counter as the walkers' generic (flat) reads of the staged line, and each such read
+// waited for the stores before it.
+#ifndef DR_EXP_OUT
+#define DR_EXP_OUT 16384
+#endif
+constexpr uint32_t EXP_OUT = DR_EXP_OUT;  // 0: pass 2 writes in place
+enum ExpStream { XS_STATS, XS_PVK, XS_PVV, XS_TGK, XS_TGV, XS_PVKO, XS_PVVO, XS_PVVN, XS_TGKO, XS_TGVO, XS_TGVN, XS_N };
+
+// One record of k_export (pass 1: scalars and counts; pass 2: bytes and entries into the sinks).
+__device__ __forceinline__ void export_record(const ExportArgs& a, uint64_t i, uint32_t act, bool json_lane,
+                                              const uint8_t* line, uint32_t glen, bool write, MapSink& pv,
+                                              MapSink& tg, uint8_t* sbytes) {
   int64_t size = a.act_size[act], mt = 0;
   uint8_t efm = 0, snull = 1, pnull = 1, tnull = 1;
   uint32_t slen = 0;
-  const bool from_json = a.act_flags ? !(a.act_flags[act] & F_FROM_CKPT) : act >= a.ck_rows;
-  if (from_json) {
-    const uint8_t* json = a.act_flags && a.src_id ? reinterpret_cast<const uint8_t*>(a.json_bases[a.src_id[act]]) : a.json;
-    const uint8_t* b = json + a.src_off[act];
-    const uint8_t* e = b + a.src_len[act];
+  if (json_lane) {
+    const uint8_t* b = line;
+    const uint8_t* e = b + glen;
     const char* side = a.side == 0 ? "add" : "remove";
     const uint32_t sl = a.side == 0 ? 3 : 6;
     // the side's object: the last member of that name (a repeated member keeps its last value)
@@ -1517,10 +1649,15 @@ __global__ void __launch_bounds__(256) k_export(ExportArgs a) {
     if (a.ck_stats.def && a.ck_stats.def[r] == a.ck_stats.max_def) {
       snull = 0;
       slen = a.ck_stats.slen[r];
-      if (write) bytes_copy(sbytes, reinterpret_cast<const uint8_t*>(a.ck_stats.sptr[r]), slen);
+      if (!write) a.stats_src[i] = a.ck_stats.sptr[r];  // copied by k_gather_bytes after pass 2
     }
-    ck_map(a.ck_pv, r, pv, write, &pnull);
-    ck_map(a.ck_tags, r, tg, write, &tnull);
+    if (write) {
+      ck_map<true>(a.ck_pv, r, pv, &pnull);
+      ck_map<true>(a.ck_tags, r, tg, &tnull);
+    } else {
+      ck_map<false>(a.ck_pv, r, pv, &pnull);
+      ck_map<false>(a.ck_tags, r, tg, &tnull);
+    }
   }
   if (!write) {
     a.size[i] = size;
@@ -1530,6 +1667,7 @@ __global__ void __launch_bounds__(256) k_export(ExportArgs a) {
     a.pv_null[i] = pnull;
     a.tags_null[i] = tnull;
     a.cnt[EXC_STATS][i] = slen;
+    a.stats_srclen[i] = json_lane ? 0u : slen;
     a.cnt[EXC_PV_N][i] = pv.n;
     a.cnt[EXC_PV_KB][i] = pv.kb;
     a.cnt[EXC_PV_VB][i] = pv.vb;
@@ -1539,10 +1677,169 @@ __global__ void __launch_bounds__(256) k_export(ExportArgs a) {
   }
 }
 
+// Stage: the launch covers JSON survivors (a replay's export order puts the checkpoint's survivors
+// first, launched apart with no line stage, so their blocks keep the occupancy of a small LDS).
+template <bool Write, bool Stage>
+__global__ void __launch_bounds__(64) k_export(ExportArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t sbuf[Stage ? EXP_STAGE + 32 : 16];
+  __shared__ __attribute__((aligned(16))) uint8_t obuf[Write && EXP_OUT ? EXP_OUT : 16];
+  const uint64_t k = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const bool live_lane = k < a.npos;
+  const uint64_t i = a.pos ? (live_lane ? a.pos[k] : 0ull) : k;
+  const uint32_t act = live_lane ? a.idx[i] : 0u;
+  const bool json_lane = live_lane && (a.act_flags ? !(a.act_flags[act] & F_FROM_CKPT) : act >= a.ck_rows);
+  const uint8_t* gline = nullptr;
+  uint32_t glen = 0;
+  if (json_lane) {
+    const uint8_t* json = a.act_flags && a.src_id ? reinterpret_cast<const uint8_t*>(a.json_bases[a.src_id[act]]) : a.json;
+    gline = json + a.src_off[act];
+    glen = a.src_len[act];
+  }
+  const uint32_t head = uint32_t(reinterpret_cast<uintptr_t>(gline) & 15u);
+  const uint32_t need = Stage && json_lane && glen <= EXP_STAGE ? (head + glen + 15u) & ~15u : 0u;
+  uint32_t tot;
+  const uint32_t at = wave_excl_scan(need, &tot);
+  const bool staged = need && at + need <= EXP_STAGE;
+  if (staged) {
+    const uint4* src = reinterpret_cast<const uint4*>(gline - head);
+    uint4* dst = reinterpret_cast<uint4*>(sbuf + at);
+    const uint32_t nv = need / 16;
+    for (uint32_t k0 = 0; k0 < nv; k0 += EXP_BATCH) {
+      uint4 v[EXP_BATCH];
+#pragma unroll
+      for (uint32_t k = 0; k < EXP_BATCH; ++k) v[k] = src[min(k0 + k, nv - 1)];
+#pragma unroll
+      for (uint32_t k = 0; k < EXP_BATCH; ++k)
+        if (k0 + k < nv) dst[k0 + k] = v[k];
+    }
+  }
+  const bool write = Write;
+  // pass 2: the block's range of every output stream, placed in obuf when all of them fit
+  uint8_t* gdst[XS_N];
+  uint32_t esz[XS_N], lofs[XS_N], bytes[XS_N];
+  uint64_t lo[XS_N];
+  bool ostaged = false;
+  if (write) {
+    const uint64_t i0 = uint64_t(blockIdx.x) * blockDim.x, i1 = min(i0 + blockDim.x, a.n);  // pass 2: pos is null
+    const int cnt_of[XS_N] = {EXC_STATS, EXC_PV_KB, EXC_PV_VB, EXC_TAGS_KB, EXC_TAGS_VB, EXC_PV_N, EXC_PV_N, EXC_PV_N,
+                              EXC_TAGS_N, EXC_TAGS_N, EXC_TAGS_N};
+    uint8_t* const base[XS_N] = {a.stats_bytes, a.pv_key_bytes, a.pv_val_bytes, a.tags_key_bytes, a.tags_val_bytes,
+                                 reinterpret_cast<uint8_t*>(a.pv_key_off + 1), reinterpret_cast<uint8_t*>(a.pv_val_off + 1),
+                                 a.pv_val_null, reinterpret_cast<uint8_t*>(a.tags_key_off + 1),
+                                 reinterpret_cast<uint8_t*>(a.tags_val_off + 1), a.tags_val_null};
+    uint32_t end = 0;
+#pragma unroll
+    for (int k = 0; k < XS_N; ++k) {
+      esz[k] = (k == XS_PVKO || k == XS_PVVO || k == XS_TGKO || k == XS_TGVO) ? 8u : 1u;
+      lo[k] = a.off[cnt_of[k]][i0];
+      const uint64_t hi = a.off[cnt_of[k]][i1];
+      gdst[k] = base[k] + esz[k] * lo[k];
+      const uint64_t nb = esz[k] * (hi - lo[k]);
+      bytes[k] = uint32_t(min(nb, uint64_t(0xffffffffu)));
+      const uint32_t g15 = uint32_t(reinterpret_cast<uintptr_t>(gdst[k]) & 15u);
+      lofs[k] = ((end + 15u) & ~15u) + g15;  // the LDS copy shares the destination's 16-byte phase
+      end = nb > EXP_OUT ? EXP_OUT + 1 : lofs[k] + bytes[k];
+    }
+    ostaged = EXP_OUT > 0 && end <= EXP_OUT;
+  }
+  __syncthreads();
+  if (live_lane) {
+    const uint8_t* line = staged ? static_cast<const uint8_t*>(sbuf + at + head) : gline;
+    MapSink pv{};
+    MapSink tg = pv;
+    uint8_t* sbytes = nullptr;
+    if (write) {
+      auto dst = [&](int k, uint64_t first) -> uint8_t* {
+        return ostaged ? obuf + lofs[k] + esz[k] * (first - lo[k]) : gdst[k] + esz[k] * (first - lo[k]);
+      };
+      pv.kbytes = dst(XS_PVK, a.off[EXC_PV_KB][i]);
+      pv.vbytes = dst(XS_PVV, a.off[EXC_PV_VB][i]);
+      pv.koff = reinterpret_cast<int64_t*>(dst(XS_PVKO, a.off[EXC_PV_N][i]));
+      pv.voff = reinterpret_cast<int64_t*>(dst(XS_PVVO, a.off[EXC_PV_N][i]));
+      pv.vnull = dst(XS_PVVN, a.off[EXC_PV_N][i]);
+      pv.kbase = int64_t(a.off[EXC_PV_KB][i]);
+      pv.vbase = int64_t(a.off[EXC_PV_VB][i]);
+      tg.kbytes = dst(XS_TGK, a.off[EXC_TAGS_KB][i]);
+      tg.vbytes = dst(XS_TGV, a.off[EXC_TAGS_VB][i]);
+      tg.koff = reinterpret_cast<int64_t*>(dst(XS_TGKO, a.off[EXC_TAGS_N][i]));
+      tg.voff = reinterpret_cast<int64_t*>(dst(XS_TGVO, a.off[EXC_TAGS_N][i]));
+      tg.vnull = dst(XS_TGVN, a.off[EXC_TAGS_N][i]);
+      tg.kbase = int64_t(a.off[EXC_TAGS_KB][i]);
+      tg.vbase = int64_t(a.off[EXC_TAGS_VB][i]);
+      sbytes = dst(XS_STATS, a.off[EXC_STATS][i]);
+      const uint64_t pe = a.off[EXC_PV_N][i], te = a.off[EXC_TAGS_N][i];
+      pv.ksrc = a.pv_ksrc + pe;
+      pv.vsrc = a.pv_vsrc + pe;
+      pv.klen = a.pv_klen + pe;
+      pv.vlen = a.pv_vlen + pe;
+      tg.ksrc = a.tags_ksrc + te;
+      tg.vsrc = a.tags_vsrc + te;
+      tg.klen = a.tags_klen + te;
+      tg.vlen = a.tags_vlen + te;
+    }
+    export_record(a, i, act, json_lane, line, glen, write, pv, tg, sbytes);
+  }
+  if (!ostaged) return;  // block-uniform
+  __syncthreads();
+  // store every stream's range: whole aligned 16-byte chunks, bytewise at the two ends
+#pragma unroll
+  for (int k = 0; k < XS_N; ++k) {
+    const uint32_t nb = bytes[k];
+    if (!nb) continue;
+    const uintptr_t g0 = reinterpret_cast<uintptr_t>(gdst[k]);
+    const uintptr_t c0 = g0 & ~uintptr_t(15), c1 = (g0 + nb + 15) & ~uintptr_t(15);
+    const uint32_t nch = uint32_t((c1 - c0) / 16);
+    for (uint32_t c = threadIdx.x; c < nch; c += blockDim.x) {
+      const uintptr_t ca = c0 + 16u * c;
+      const int64_t rel = int64_t(ca) - int64_t(g0);  // chunk start relative to the range (may be < 0)
+      if (ca >= g0 && ca + 16 <= g0 + nb) {
+        *reinterpret_cast<uint4*>(ca) = *reinterpret_cast<const uint4*>(obuf + lofs[k] + rel);
+      } else {
+        for (uint32_t q = 0; q < 16; ++q) {
+          const uintptr_t x = ca + q;
+          if (x >= g0 && x < g0 + nb) *reinterpret_cast<uint8_t*>(x) = obuf[lofs[k] + (rel + q)];
+        }
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_export_flags(ExportArgs a, uint32_t* json) {
+  const uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  const uint32_t act = a.idx[i];
+  json[i] = (a.act_flags ? !(a.act_flags[act] & F_FROM_CKPT) : act >= a.ck_rows) ? 1u : 0u;
+}
+
+__global__ void __launch_bounds__(256) k_export_split(const uint32_t* json, const uint64_t* jscan, uint64_t n,
+                                                      uint32_t* jpos, uint32_t* cpos) {
+  const uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t j = jscan[i];
+  if (json[i]) jpos[j] = uint32_t(i);
+  else cpos[i - j] = uint32_t(i);
+}
+
 }  // namespace dev
 
-void launch_export(const ExportArgs& a, hipStream_t st) {
-  if (a.n) DR_LAUNCH(dev::k_export, dim3(unsigned((a.n + 255) / 256)), dim3(256), 0, st, a);
+void launch_export(const ExportArgs& a, bool stage, hipStream_t st) {
+  const uint64_t m = a.pos ? a.npos : a.n;
+  if (!m) return;
+  ExportArgs b = a;
+  b.npos = m;
+  const dim3 g(unsigned((m + 63) / 64));
+  if (a.write) DR_LAUNCH((dev::k_export<true, true>), g, dim3(64), 0, st, b);
+  else if (stage) DR_LAUNCH((dev::k_export<false, true>), g, dim3(64), 0, st, b);
+  else DR_LAUNCH((dev::k_export<false, false>), g, dim3(64), 0, st, b);
+}
+
+void launch_export_flags(const ExportArgs& a, uint32_t* json, hipStream_t st) {
+  if (a.n) DR_LAUNCH(dev::k_export_flags, dim3(unsigned((a.n + 255) / 256)), dim3(256), 0, st, a, json);
+}
+
+void launch_export_split(const uint32_t* json, const uint64_t* jscan, uint64_t n, uint32_t* jpos, uint32_t* cpos,
+                         hipStream_t st) {
+  if (n) DR_LAUNCH(dev::k_export_split, dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, json, jscan, n, jpos, cpos);
 }
 
 }  // namespace dr

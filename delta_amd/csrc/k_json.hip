@@ -288,6 +288,204 @@ __device__ __forceinline__ void walk_line(const JsonParseArgs& a, uint32_t* tokb
   emit_line(a, line, b, n, p, a.buf + b, o);
 }
 
+// ---- the wave-cooperative tokenizer of small segments (the tape) ------------------------------------
+// A streamed commit is a few lines in one wave; walked one lane per line, every lane's ~20 windows
+// are a serial chain with nothing to hide its latency (r03: 96 us of a 6-line commit's apply). Here
+// the wave sweeps the staged region 1 KiB per step (lane l: the aligned 16-byte window l of the
+// step), classifies each window with the walker's SWAR masks, and resolves the state that crosses
+// windows with ballots instead of a serial walk: backslash-run parity (the nearest lower window that
+// is not all backslashes decides it), in-string parity (a prefix XOR of the windows' quote
+// parities), scalar runs, and for every closing quote the position of its opening quote and whether
+// a backslash lies between them. Tokens go in byte order to an LDS tape -- structural bytes, one
+// T_STRING per string (at its closing quote, carrying the opening position and the body length), one
+// T_SCALAR per scalar run (at its first byte; its length is the distance to the next token), one T_NL
+// per newline -- and each lane then runs the walker's DFA over its own line's stretch of the tape
+// (r02 built this for the bulk segment, exact on every parity test but slower there: a 64-line wave
+// has no idle lanes and its lines' tokens are uneven across windows).
+//
+// The tape covers the canonical Delta writer's lines: a region with whitespace or a control byte
+// outside a string, a newline inside a string, an escape other than \" \\ \/ \b \f \n \r \t, a
+// string of 4096 bytes or more, or more tokens than the tape holds sends the whole wave (a
+// wave-uniform branch) to the per-lane walker, which decides every line exactly as before.
+constexpr uint32_t T_NL = 12;
+constexpr uint32_t TAPE_CAP = 4096;  // tokens (16 KiB of LDS)
+
+// Bytes escaped by a backslash run, with the run parity carried in (cin) and out (*cout): the
+// per-lane walker's rule (json_lane.h tokenize_window).
+__device__ __forceinline__ uint32_t escape16(uint32_t bs, uint32_t cin, uint32_t* cout) {
+  const uint32_t bsn = bs & ~cin;
+  const uint32_t follows = ((bsn << 1) | cin) & 0xFFFFu;
+  const uint32_t odd_starts = bsn & ~0x5555u & ~follows;
+  const uint32_t sum = odd_starts + bsn;
+  *cout = (sum >> 16) & 1u;
+  return (0x5555u ^ ((sum << 1) & 0xFFFFu)) & follows;
+}
+
+__device__ __forceinline__ uint64_t lanes_below() { return (1ull << threadIdx.x) - 1ull; }
+
+// Value of `v` in the highest lane of `mask` below this lane, or `dflt` when there is none.
+__device__ __forceinline__ int32_t from_lower(unsigned long long mask, int32_t v, int32_t dflt) {
+  const unsigned long long lower = mask & lanes_below();
+  const int src = lower ? 63 - __clzll(lower) : int(threadIdx.x);
+  const int32_t got = __shfl(v, src, 64);
+  return lower ? got : dflt;
+}
+
+// The tape of the region [rb, rb + R) of the stage (R includes the last line's newline). Returns
+// true when every line of the wave is on it (wave-uniform); false sends the wave to the walker.
+__device__ __forceinline__ bool build_tape(const uint4* stage, uint32_t rb, uint32_t R, uint32_t nlines, uint32_t* tape,
+                           uint16_t* nltok) {
+  const uint32_t lane = threadIdx.x;
+  const uint32_t a0 = rb & ~15u;
+  const uint32_t skew = rb - a0;
+  const uint32_t total = skew + R;
+  const uint32_t nsteps = (total + 1023u) >> 10;
+  uint32_t esc_c = 0, instr_c = 0, sc_c = 0, tbase = 0, nlc = 0;
+  int32_t open_c = -1, bs_c = -1;
+  for (uint32_t s = 0; s < nsteps; ++s) {
+    const uint32_t wpos = (s << 10) + (lane << 4);
+    const int32_t lo = int32_t(wpos) - int32_t(skew);  // region offset of the window's byte 0
+    uint32_t w[4] = {0, 0, 0, 0};
+    if (wpos < total) {
+      const uint4 v = stage[(a0 + wpos) >> 4];
+      w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+    }
+    uint32_t valid = 0;
+    if (lo < int32_t(R)) {
+      valid = 0xFFFFu;
+      if (lo < 0) valid &= 0xFFFFu << uint32_t(-lo);
+      if (lo + 16 > int32_t(R)) valid &= (1u << uint32_t(int32_t(R) - lo)) - 1u;
+    }
+    jl::Win m;
+    jl::classify(w, m);
+    m.q &= valid; m.bs &= valid; m.st &= valid; m.sp &= valid; m.ctrl &= valid;
+    uint32_t nl = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) nl |= jl::gather4(jl::zbytes(w[d] ^ 0x0a0a0a0au)) << (4 * d);
+    nl &= valid;
+    // backslash runs: a window that is not all backslashes decides its carry-out by itself
+    uint32_t c0;
+    escape16(m.bs, 0u, &c0);
+    const bool allbs = m.bs == 0xFFFFu;
+    const unsigned long long decided = __ballot(!allbs);
+    const uint32_t cin = uint32_t(from_lower(decided, int32_t(c0), int32_t(esc_c)));
+    uint32_t cout;
+    const uint32_t escaped = (m.bs | cin) ? escape16(m.bs, cin, &cout) : (cout = 0, 0u);
+    esc_c = uint32_t(__builtin_amdgcn_readlane(int(allbs ? cin : cout), 63));
+    // string state: prefix XOR of the windows' quote parities
+    const uint32_t quote = m.q & ~escaped;
+    const unsigned long long par = __ballot(__builtin_popcount(quote) & 1);
+    const uint32_t sin = instr_c ^ uint32_t(__popcll(par & lanes_below()) & 1);
+    const uint32_t instr = jl::prefix_xor16(quote) ^ (sin ? 0xFFFFu : 0u);
+    instr_c ^= uint32_t(__popcll(par) & 1);
+    bool bad = (m.ctrl & ~(nl & ~instr)) != 0 || (m.sp & ~instr) != 0;
+    uint32_t oddesc = escaped & ~(m.q | m.bs) & valid;
+    while (oddesc) {  // escapes other than \" and \\ (rare)
+      const uint32_t k = jl::ctz32(oddesc);
+      oddesc &= oddesc - 1;
+      const uint32_t c = jl::win_byte(w, k);
+      bad |= !(c == '/' || c == 'b' || c == 'f' || c == 'n' || c == 'r' || c == 't');
+    }
+    const uint32_t st = m.st & ~instr;
+    const uint32_t sc = valid & ~instr & ~quote & ~st & ~m.sp & ~m.ctrl;
+    const uint32_t sc_prev = uint32_t(__shfl_up(int(sc >> 15), 1, 64)) & 1u;
+    const uint32_t sc_begin = sc & ~(((sc << 1) | (lane ? sc_prev : sc_c)) & 0xFFFFu);
+    sc_c = uint32_t(__builtin_amdgcn_readlane(int(sc >> 15), 63)) & 1u;
+    const uint32_t open = quote & instr, close = quote & ~instr;
+    const uint32_t bsin = m.bs & instr;
+    // latest opening quote / in-string backslash before this window
+    const int32_t last_open = open ? lo + 31 - __builtin_clz(open) : -1;
+    const int32_t last_bs = bsin ? lo + 31 - __builtin_clz(bsin) : -1;
+    const int32_t open_in = from_lower(__ballot(open != 0), last_open, open_c);
+    const int32_t bs_in = from_lower(__ballot(bsin != 0), last_bs, bs_c);
+    open_c = __builtin_amdgcn_readlane(open ? last_open : open_in, 63);
+    bs_c = __builtin_amdgcn_readlane(bsin ? last_bs : bs_in, 63);
+    const uint32_t tm = st | close | sc_begin | nl;
+    // token and newline ranks: one wave scan of both counts (16-bit halves)
+    const uint32_t cnt = uint32_t(__builtin_popcount(tm)) | (uint32_t(__builtin_popcount(nl)) << 16);
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = uint32_t(__shfl_up(int(incl), o, 64));
+      if (int(lane) >= o) incl += t;
+    }
+    const uint32_t tot = uint32_t(__builtin_amdgcn_readlane(int(incl), 63));
+    if (__ballot(bad)) return false;
+    if (tbase + (tot & 0xFFFFu) > TAPE_CAP || nlc + (tot >> 16) > uint32_t(JL_T)) return false;
+    uint32_t idx = tbase + ((incl - cnt) & 0xFFFFu);
+    uint32_t nlr = nlc + ((incl - cnt) >> 16);
+    bool longstr = false;
+    uint32_t t = tm;
+    while (t) {
+      const uint32_t k = jl::ctz32(t);
+      t &= t - 1;
+      const uint32_t bit = 1u << k, below = bit - 1u;
+      const uint32_t pos = uint32_t(lo + int32_t(k));
+      const uint32_t ob = open & below, bb = bsin & below;
+      const int32_t op = ob ? lo + 31 - __builtin_clz(ob) : open_in;
+      const int32_t lb = bb ? lo + 31 - __builtin_clz(bb) : bs_in;
+      const uint32_t blen = pos - uint32_t(op) - 1u;
+      const uint32_t c = jl::win_byte(w, k);
+      const uint32_t scls = c == ':' ? jl::T_COLON : c == ',' ? jl::T_COMMA
+                          : ((c & 2u) ? jl::T_OBJ_OPEN : jl::T_OBJ_CLOSE) + ((c & 0x20u) ? 0u : 1u);
+      uint32_t tok;
+      if (close & bit) {
+        longstr |= blen >= 4096u;
+        tok = (uint32_t(op) << 16) | ((blen & 0xFFFu) << 4) | (lb > op ? jl::T_STRING_ESC : jl::T_STRING);
+      } else {
+        tok = (pos << 16) | ((st & bit) ? scls : (sc_begin & bit) ? jl::T_SCALAR : T_NL);
+      }
+      if (nl & bit) nltok[nlr++] = uint16_t(idx);
+      tape[idx++] = tok;
+    }
+    if (__ballot(longstr)) return false;
+    tbase += tot & 0xFFFFu;
+    nlc += tot >> 16;
+  }
+  return nlc == nlines;
+}
+
+// Lane i runs the DFA over line i's stretch of the tape (line bytes read from the stage at `sp`, the
+// region start) and emits its action; `gb` is the region's offset in the JSON buffer.
+__device__ __forceinline__ void dfa_tape(const JsonParseArgs& a, uint64_t line0, uint32_t nlines, const uint8_t* sp, uint64_t gb,
+                         const uint32_t* tape, const uint16_t* nltok) {
+  const uint32_t lane = threadIdx.x;
+  const bool live = lane < nlines;
+  const uint32_t te = live ? nltok[lane] : 0u;
+  const uint32_t ts = live && lane ? uint32_t(nltok[lane - 1]) + 1u : 0u;
+  const uint32_t ls = live && lane ? (tape[ts - 1] >> 16) + 1u : 0u;  // line start (region offset)
+  const uint32_t n = live ? (tape[te] >> 16) - ls : 0u;
+  const uint8_t* p = sp + ls;
+  const uint32_t cnt = te - ts;
+  uint32_t mx = cnt;
+  for (int o = 32; o > 0; o >>= 1) mx = max(mx, uint32_t(__shfl_xor(int(mx), o, 64)));
+  jl::Dfa<false> d;
+  jl::Tokenizer tz;
+  for (uint32_t t = 0; t < mx; ++t) {
+    if (t < cnt && d.status == jl::ST_OK) {
+      const uint32_t tok = tape[ts + t];
+      const uint32_t cls = tok & 0xFu, pos = tok >> 16;
+      uint32_t aux = (tok >> 4) & 0xFFFu;
+      if (cls == jl::T_SCALAR) {
+        aux = (tape[ts + t + 1] >> 16) - pos;  // the run ends where the next token begins
+        if (aux > jl::TOK_MAX_SCALAR) { d.status = jl::ST_BAD; continue; }
+      }
+      jl::dfa_token<false>(p, ((pos - ls) << 16) | (aux << 4) | cls, d);
+    }
+  }
+  if (!live) return;
+  tz.sc_bytes = d.sc_checked;  // every scalar byte starts or continues a run the DFA validated
+  jl::LineOut o;
+  jl::dfa_finish<false>(tz, d, o);
+  const uint64_t line = line0 + lane;
+  if (o.hard) {
+    const unsigned long long k = atomicAdd(a.hard_count, 1ull);
+    a.hard_idx[k] = line;
+    return;
+  }
+  emit_line(a, line, gb + ls, n, p, a.buf + gb + ls, o);
+}
+
 // 64 consecutive lines per block, one lane per line, two phases (json_lane.h):
 //  1. each lane tokenizes its line window by window (16-byte loads, SWAR masks) into its column of
 //     an LDS token buffer;
@@ -299,6 +497,8 @@ template <bool Stage>
 __global__ void __launch_bounds__(JL_T, DR_JL_WAVES) k_json_lines(JsonParseArgs a) {
   __shared__ uint32_t tokbuf[JL_TOKCAP * JL_T];
   __shared__ uint4 stage[Stage ? JL_STAGE_BYTES / 16 : 1];
+  __shared__ uint32_t tape[Stage ? TAPE_CAP : 1];
+  __shared__ uint16_t nltok[Stage ? JL_T : 1];
   const uint32_t lane = threadIdx.x;
   const uint64_t line = uint64_t(blockIdx.x) * JL_T + lane;
   const bool live = line < a.nlines;
@@ -316,6 +516,12 @@ __global__ void __launch_bounds__(JL_T, DR_JL_WAVES) k_json_lines(JsonParseArgs 
       const uint32_t nq = uint32_t((r1 - r0) >> 4) + 3;
       for (uint32_t k = lane; k < nq; k += JL_T) stage[k] = src[k];
       __syncthreads();
+      const uint32_t nw = uint32_t(last - first + 1);
+      const uint64_t rb = first == 0 ? 0 : a.nl[first - 1] + 1;  // the wave's first line
+      if (build_tape(stage, uint32_t(rb - r0), uint32_t(a.nl[last] + 1 - rb), nw, tape, nltok)) {
+        dfa_tape(a, first, nw, reinterpret_cast<const uint8_t*>(stage) + (rb - r0), rb, tape, nltok);
+        return;
+      }
       walk_line(a, tokbuf, lane, line, live, b, n, reinterpret_cast<const uint8_t*>(stage) + (b - r0));
       return;
     }

@@ -474,12 +474,21 @@ __global__ void __launch_bounds__(VER_T) k_bucket_verify(ReduceArgs a) {
     uint32_t pn = 0, qn = 0;
     if (k < n) {
       const uint2 ix = pr[k];
+#ifdef DR_VERIFY_EXP_NOREFS  // timing experiment only: the loser's reference stands for both (no winner gather)
+      const uint64_t vx = a.path_ref[ix.x], vy = vx + (ix.y & 0u);
+#else
       const uint64_t vx = a.path_ref[ix.x], vy = a.path_ref[ix.y];
+#endif
       nul = !vx || !vy;
       p = reinterpret_cast<const uint8_t*>(vx & PREF_PTR);
       q = reinterpret_cast<const uint8_t*>(vy & PREF_PTR);
       pn = uint32_t(vx >> 48);
       qn = uint32_t(vy >> 48);
+#ifdef DR_VERIFY_EXP_NOBYTES  // timing experiment only (scripts/build_variant.sh): pairs + references, no path bytes
+      if (true) {
+        diff = (nul || pn != qn) ? 1u : 0u;
+      } else
+#endif
       if (nul || pn != qn) {
         diff = 1;
       } else {

@@ -381,6 +381,10 @@ __global__ void __launch_bounds__(256) k_snap_regions(SnappyArgs a) {
 // are exact again) and has no flag in it or within REGION_GAP after it. A chunk whose entry lies past its end (a long literal spans it) jumps to
 // the chunk holding that entry.
 __global__ void __launch_bounds__(64) k_snap_resolve(SnappyArgs a) {
+  constexpr uint32_t VW = SNAP_CH / 32;  // visited-bitmap words per chunk
+  constexpr uint32_t CB_WORDS = (SNAP_CH + 16) / 4;
+  __shared__ uint32_t cb32[CB_WORDS + 4];
+  __shared__ uint32_t nx[2][SNAP_CH];
   const uint64_t nreg = *a.region_count;
   for (uint64_t rg = blockIdx.x; rg < nreg; rg += gridDim.x) {
     const uint32_t cf = a.region[rg];
@@ -392,21 +396,42 @@ __global__ void __launch_bounds__(64) k_snap_resolve(SnappyArgs a) {
     const int lane = threadIdx.x;
     uint32_t base = jf > RESOLVE_MARGIN ? jf - RESOLVE_MARGIN : 0u;
     uint64_t e = base == 0 ? 0 : a.entry[c0 + base];  // true entry of chunk `base`
+    const uint64_t t0 = a.rstats ? __builtin_amdgcn_s_memtime() : 0;
+    uint32_t n_win = 0, n_walk = 0, n_span = 0;
     while (base < nc) {
+      ++n_win;
       const uint32_t j = base + lane;
       const bool valid = j < nc;
-      uint32_t x = 0, word = 0, old = 0;
+      uint32_t x = 0, old = 0;
+      uint32_t vw[VW];
+#pragma unroll
+      for (uint32_t k = 0; k < VW; ++k) vw[k] = 0;
       const uint64_t cs = uint64_t(j) * SNAP_CH;
       const uint64_t ce = min(cs + SNAP_CH, uint64_t(pg.n_in));
-      if (valid) { x = a.spec_exit[c0 + j]; old = a.entry[c0 + j]; }
+      if (valid) {
+        x = a.spec_exit[c0 + j];
+        old = a.entry[c0 + j];
+        // the lane's whole visited bitmap: a break further on is re-checked without another load
+        const uint4* vp = reinterpret_cast<const uint4*>(&a.vis[uint64_t(c0 + j) * VW]);
+#pragma unroll
+        for (uint32_t k = 0; k < VW; k += 4) {
+          const uint4 q = vp[k / 4];
+          vw[k] = q.x; vw[k + 1] = q.y; vw[k + 2] = q.z; vw[k + 3] = q.w;
+        }
+      }
+      auto on_chain = [&](uint64_t c) -> bool {  // c (< ce) on this lane's speculative chain
+        const uint32_t r = uint32_t(c - cs), wi = r >> 5;
+        uint32_t word = vw[0];
+#pragma unroll
+        for (uint32_t k = 1; k < VW; ++k) word = wi == k ? vw[k] : word;
+        return (word >> (r & 31)) & 1u;
+      };
       uint64_t cand = __shfl_up(uint64_t(x), 1, 64);
       if (lane == 0) cand = e;
-      const bool skip = cand >= ce;
-      if (valid && !skip) word = a.vis[uint64_t(c0 + j) * (SNAP_CH / 32) + uint32_t((cand - cs) >> 5)];
-      const bool ok = valid && !skip && ((word >> ((cand - cs) & 31)) & 1u);
-      const unsigned long long brk = __ballot(valid && !ok);
-      const uint32_t f = brk ? uint32_t(__builtin_ctzll(brk)) : 64u;  // first chunk needing care
-      const uint32_t cv = uint32_t(min(cand, uint64_t(0xffffffffu)));
+      bool ok = valid && cand < ce && on_chain(cand);
+      unsigned long long brk = __ballot(valid && !ok);
+      uint32_t f = brk ? uint32_t(__builtin_ctzll(brk)) : 64u;  // first chunk needing care
+      uint32_t cv = uint32_t(min(cand, uint64_t(0xffffffffu)));
       const bool agree = __ballot(valid && (cv != old)) == 0ull;
       if (valid && uint32_t(lane) <= f) a.entry[c0 + j] = cv;
       const uint32_t cnt = min(64u, nc - base);
@@ -424,40 +449,96 @@ __global__ void __launch_bounds__(64) k_snap_resolve(SnappyArgs a) {
         base += cnt;
         continue;
       }
-      const uint64_t ef0 = __shfl(cand, int(f), 64);
-      const uint64_t fcs = uint64_t(base + f) * SNAP_CH;
-      const uint64_t fce = min(fcs + SNAP_CH, uint64_t(pg.n_in));
-      if (ef0 >= fce) {
-        // chunks base+f .. (the chunk holding ef0) - 1 hold no element start: entry = ef0
-        const uint32_t jt = uint32_t(min(ef0 / SNAP_CH, uint64_t(nc)));
-        for (uint32_t q = base + f + 1 + lane; q < jt; q += 64) a.entry[c0 + q] = uint32_t(min(ef0, uint64_t(0xffffffffu)));
-        e = ef0;
-        base = jt > base + f ? jt : base + f + 1;
-        continue;
-      }
-      // chunk base+f: its true entry is ef0. Walk it from a 512-byte register window (lane l
-      // holds 8 bytes) instead of dependent global loads.
-      uint64_t ef = ef0;
-      const uintptr_t wa = (reinterpret_cast<uintptr_t>(in) + fcs) & ~uintptr_t(7);
-      const int64_t wb = int64_t(wa) - int64_t(reinterpret_cast<uintptr_t>(in));
-      const uint2 w = reinterpret_cast<const uint2*>(wa)[lane];
-      while (ef < fce) {
-        const uint32_t r = uint32_t(int64_t(ef) - wb);
-        uint64_t hdr;
-        if (r + 12 <= 512) {
-          const uint32_t di = r >> 2, sh = r & 3;
-          auto dw = [&](uint32_t d) -> uint32_t {
-            return uint32_t(__builtin_amdgcn_readlane(int((d & 1) ? w.y : w.x), int(d >> 1)));
-          };
-          const uint32_t d0 = dw(di), d1 = dw(di + 1), d2 = dw(di + 2);
-          hdr = uint64_t(__builtin_amdgcn_alignbyte(d1, d0, sh)) | (uint64_t(__builtin_amdgcn_alignbyte(d2, d1, sh)) << 32);
-        } else {
-          hdr = load_u64(in + ef);
+      // breaks inside this window, one after another: walk the broken chunk from its true entry;
+      // its exit is the next chunk's true entry, checked against that lane's bitmap in registers
+      // (r03: every break reloaded the window's exits and bitmaps -- three dependent round trips per
+      // chunk, 12 ms on a page whose chunks all broke)
+      bool next_window = true;
+      while (true) {
+        const uint64_t ef0 = __shfl(cand, int(f), 64);
+        const uint64_t fcs = uint64_t(base + f) * SNAP_CH;
+        const uint64_t fce = min(fcs + SNAP_CH, uint64_t(pg.n_in));
+        if (ef0 >= fce) {
+          // chunks base+f .. (the chunk holding ef0) - 1 hold no element start: entry = ef0
+          ++n_span;
+          const uint32_t jt = uint32_t(min(ef0 / SNAP_CH, uint64_t(nc)));
+          for (uint32_t q = base + f + 1 + lane; q < jt; q += 64) a.entry[c0 + q] = uint32_t(min(ef0, uint64_t(0xffffffffu)));
+          e = ef0;
+          base = jt > base + f ? jt : base + f + 1;
+          next_window = false;
+          break;
         }
-        ef += snap_adv(snap_decode(hdr));
+        // chunk base+f's exit from its true entry ef0, by the whole wave: every position of the chunk
+        // gets the start of the element after the one starting there (nx), then pointer doubling --
+        // eight rounds, as elements are at least two bytes long and a chunk holds at most 128 --
+        // leaves the exit of the chain from ef0. r03 walked the chain element by element on one
+        // lane: ~500 clocks per element, 13 ms for a page of consecutive int64 dictionary values
+        // whose speculation broke on a quarter of its chunks.
+        ++n_walk;
+        const uint32_t lim = uint32_t(fce - fcs);
+        for (uint32_t q = lane; q < CB_WORDS; q += 64) {  // the chunk's bytes, +16 for its last headers
+          uint32_t v = 0;
+#pragma unroll
+          for (uint32_t k = 0; k < 4; ++k) {
+            const uint64_t pos = fcs + 4 * q + k;
+            v |= pos < pg.n_in ? uint32_t(in[pos]) << (8 * k) : 0u;
+          }
+          cb32[q] = v;
+        }
+        __syncthreads();
+        for (uint32_t q = lane; q < SNAP_CH; q += 64) {
+          uint32_t nv = q;
+          if (q < lim) {
+            const uint32_t di = q >> 2, sh = q & 3;
+            const uint32_t w0 = cb32[di], w1 = cb32[di + 1], w2 = cb32[di + 2];
+            const uint64_t hdr = uint64_t(__builtin_amdgcn_alignbyte(w1, w0, sh)) |
+                                 (uint64_t(__builtin_amdgcn_alignbyte(w2, w1, sh)) << 32);
+            uint32_t adv, len;
+            snap_step(hdr, &adv, &len);
+            nv = q + adv;
+          }
+          nx[0][q] = nv;
+        }
+        __syncthreads();
+        uint32_t cur = 0;
+        for (int rd = 0; rd < 8; ++rd) {
+          for (uint32_t q = lane; q < SNAP_CH; q += 64) {
+            const uint32_t v = nx[cur][q];
+            nx[cur ^ 1u][q] = v < lim ? nx[cur][v] : v;
+          }
+          __syncthreads();
+          cur ^= 1u;
+        }
+        const uint64_t ef = fcs + nx[cur][uint32_t(min(ef0 - fcs, uint64_t(SNAP_CH - 1)))];
+        if (f + 1 >= cnt) {  // the window's last chunk: its exit enters the next window
+          e = ef;
+          base += f + 1;
+          next_window = false;
+          break;
+        }
+        // chunk base+f+1's true entry is ef; later lanes keep their candidates
+        if (uint32_t(lane) == f + 1) {
+          cand = ef;
+          ok = valid && cand < ce && on_chain(cand);
+          cv = uint32_t(min(cand, uint64_t(0xffffffffu)));
+        }
+        brk = __ballot(valid && !ok && uint32_t(lane) > f);
+        const uint32_t f2 = brk ? uint32_t(__builtin_ctzll(brk)) : 64u;
+        if (valid && uint32_t(lane) > f && uint32_t(lane) <= f2) a.entry[c0 + j] = cv;
+        f = f2;
+        if (f >= cnt) break;  // the rest of the window is on its chains: the next window decides
       }
-      e = ef;
-      base += f + 1;
+      if (next_window) {
+        e = uint32_t(__builtin_amdgcn_readlane(int(x), int(cnt - 1)));
+        base += cnt;
+      }
+    }
+    if (a.rstats && lane == 0) {
+      uint64_t* r = a.rstats + rg * 4;
+      r[0] = __builtin_amdgcn_s_memtime() - t0;
+      r[1] = n_win;
+      r[2] = n_walk;
+      r[3] = n_span;
     }
   }
 }
@@ -521,6 +602,10 @@ __global__ void __launch_bounds__(SCAN_T) k_snap_scan(SnappyArgs a) {
 // stores its chunk's records directly (consecutive lines per lane; the L2 merges them), which
 // keeps the LDS to the input stage and two workgroups per CU.
 constexpr uint32_t REC_LIT = 0x80000000u;
+#ifndef DR_EMIT_BURST
+#define DR_EMIT_BURST 0
+#endif
+constexpr uint32_t EMIT_BURST = DR_EMIT_BURST ? DR_EMIT_BURST : 1;
 
 __global__ void __launch_bounds__(2 * WG_CHUNKS) k_snap_emit(SnappyArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[STAGE_BYTES + 32];
@@ -546,7 +631,9 @@ __global__ void __launch_bounds__(2 * WG_CHUNKS) k_snap_emit(SnappyArgs a) {
       rec += a.half_elems[c];
     }
     bool bad = false;
-    while (pos < ce) {
+    // one element: its record, or false at the end / on a malformed element
+    auto next = [&](uint64_t& r64) -> bool {
+      if (pos >= ce || bad) return false;
       // branch-free decode (the lanes' element types differ; a switch serialises them)
       const uint64_t w = staged_u64(buf, s, pos);
       uint32_t adv, len;
@@ -559,14 +646,34 @@ __global__ void __launch_bounds__(2 * WG_CHUNKS) k_snap_emit(SnappyArgs a) {
       const uint32_t orel = uint32_t(o & (SNAP_BLOCK - 1));
       bad = len == 0 || len > SNAP_BLOCK || o + len > pg.n_out || orel + len > SNAP_BLOCK ||
             (lit ? (ip + len > pg.n_in || ip >= REC_LIT) : (off == 0 || off > orel));  // a copy reaching before its fragment
-      if (bad) break;
+      if (bad) return false;
       if (orel == 0) a.block_rec[pg.block_base + uint32_t(o >> 16)] = rec;
       const uint32_t src = lit ? (REC_LIT | uint32_t(ip)) : off;
-      a.recs[rec] = orel | (uint64_t(len - 1) << 16) | (uint64_t(src) << 32);
+      r64 = orel | (uint64_t(len - 1) << 16) | (uint64_t(src) << 32);
       ++rec;
       o += len;
       pos += lit ? uint64_t(ip - pos) + len : adv;
+      return true;
+    };
+#if DR_EMIT_BURST
+    // records leave in bursts of EMIT_BURST consecutive ones per lane (back-to-back stores of one
+    // lane's contiguous range, so the L2 sees each 64-byte run whole instead of one 8-byte piece per
+    // element step while 63 other lanes' lines compete for it)
+    for (;;) {
+      uint64_t rb[EMIT_BURST];
+      const uint64_t r0 = rec;
+      uint32_t m = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < EMIT_BURST; ++q)
+        if (m == q && next(rb[q])) ++m;
+#pragma unroll
+      for (uint32_t q = 0; q < EMIT_BURST; ++q)
+        if (q < m) a.recs[r0 + q] = rb[q];
+      if (m < EMIT_BURST) break;
     }
+#else
+    for (uint64_t r64; next(r64);) a.recs[rec - 1] = r64;
+#endif
     if (bad) atomicOr(&a.pages_bad[g.p], 8u);
   }
 }

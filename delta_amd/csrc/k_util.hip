@@ -19,16 +19,48 @@ __global__ void k_gather(const T* __restrict__ src, const I* __restrict__ idx, u
   if (i < n) dst[i] = src[idx[i]];
 }
 
-// out[off[i] .. off[i] + len[i]) = bytes at ptr[i]; one wave per string.
-// One wave per string, grid-stride (a wave per string over a grid of n waves would pass the
-// dispatch's 2^32 work items at 67M strings).
-__global__ void k_gather_bytes(const uint64_t* __restrict__ ptr, const uint32_t* __restrict__ len,
-                               const uint64_t* __restrict__ off, uint64_t n, uint8_t* __restrict__ out) {
-  for (uint64_t s = uint64_t(blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6); s < n;
-       s += uint64_t(gridDim.x) * (blockDim.x / 64)) {
+// out[off[i] .. off[i] + len[i]) = bytes at ptr[i]. GATHER_G lanes per string, grid-stride: the
+// lanes store the string's 16-byte-aligned destination chunks whole (a source dword-aligned 16-byte
+// load plus one dword, funnel-shifted into place) and its unaligned head and tail bytewise. r04: one
+// wave per string with byte copies left 46 of 64 lanes idle on a 110-byte path and waited for a round
+// trip per string (2.95 ms for config 3's 10M live paths).
+constexpr uint32_t GATHER_G = 4;
+__global__ void __launch_bounds__(256) k_gather_bytes(const uint64_t* __restrict__ ptr, const uint32_t* __restrict__ len,
+                                                      const uint64_t* __restrict__ off, uint64_t n,
+                                                      uint8_t* __restrict__ out) {
+  const uint32_t gl = threadIdx.x % GATHER_G;
+  const uint64_t step = uint64_t(gridDim.x) * (blockDim.x / GATHER_G);
+  for (uint64_t s = (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) / GATHER_G; s < n; s += step) {
     const uint8_t* p = reinterpret_cast<const uint8_t*>(ptr[s]);
+    const uint32_t L = len[s];
     uint8_t* o = out + off[s];
-    for (uint32_t k = threadIdx.x & 63; k < len[s]; k += 64) o[k] = p[k];
+    const uint32_t head = min(L, (16u - uint32_t(reinterpret_cast<uintptr_t>(o) & 15u)) & 15u);
+    const uint32_t nch = (L - head) / 16;
+    for (uint32_t k = gl; k < head; k += GATHER_G) o[k] = p[k];
+    for (uint32_t k = head + 16 * nch + gl; k < L; k += GATHER_G) o[k] = p[k];
+    const uint8_t* end = p + L;
+    for (uint32_t c = gl; c < nch; c += GATHER_G) {
+      const uint8_t* sp = p + head + 16 * c;
+      const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(sp) & 3u);
+      const uint8_t* sa = sp - sh;
+      uint4 r;
+      if (sa + 20 <= end) {  // every source byte read lies inside the string
+        const uint4 v = *reinterpret_cast<const uint4*>(sa);
+        const uint32_t w4 = *reinterpret_cast<const uint32_t*>(sa + 16);
+        r.x = __builtin_amdgcn_alignbyte(v.y, v.x, sh);
+        r.y = __builtin_amdgcn_alignbyte(v.z, v.y, sh);
+        r.z = __builtin_amdgcn_alignbyte(v.w, v.z, sh);
+        r.w = __builtin_amdgcn_alignbyte(w4, v.w, sh);
+      } else {
+        uint32_t w[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+          w[d] = uint32_t(sp[4 * d]) | uint32_t(sp[4 * d + 1]) << 8 | uint32_t(sp[4 * d + 2]) << 16 |
+                 uint32_t(sp[4 * d + 3]) << 24;
+        r = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+      *reinterpret_cast<uint4*>(o + head + 16 * c) = r;
+    }
   }
 }
 
@@ -113,7 +145,7 @@ void launch_gather_u64_by64(const uint64_t* src, const uint64_t* idx, uint64_t n
 }
 void launch_gather_bytes(const uint64_t* ptr, const uint32_t* len, const uint64_t* off, uint64_t n, uint8_t* out,
                          hipStream_t st) {
-  if (n) DR_LAUNCH(dev::k_gather_bytes, dim3(unsigned(std::min<uint64_t>((n + 3) / 4, 1u << 20))), dim3(256), 0, st, ptr, len, off, n, out);
+  if (n) DR_LAUNCH(dev::k_gather_bytes, dim3(unsigned(std::min<uint64_t>((n + 256 / dev::GATHER_G - 1) / (256 / dev::GATHER_G), 1u << 16))), dim3(256), 0, st, ptr, len, off, n, out);
 }
 
 void launch_delts_fix(const uint8_t* flags, const int64_t* delts, uint64_t n, uint8_t* valid, int64_t* out,

@@ -179,6 +179,7 @@ struct SnappyArgs {
   uint32_t* pages_bad;          // [npages] nonzero -> decoded by the serial fallback
   uint32_t* error;
   uint64_t* stamps;             // diagnostics: [nblocks * 8] k_snap_exec phase clocks, or null
+  uint64_t* rstats;             // diagnostics: [regions * 4] k_snap_resolve {clocks, windows, walks, spans}, or null
   // second-half split of each chunk's walk (k_snap_emit runs two lanes per chunk): the first element
   // starting in the chunk's second half, and the output bytes / elements before it; mid_first is
   // ~0 when the chunk is not split (its true entry is not its speculative first position)
@@ -431,6 +432,8 @@ struct FilterLeaf {
   int32_t nlit;      // IN: entries in the set
   int32_t lit_null;  // comparisons: the literal is NULL; IN: the list holds a NULL
   int32_t pad;       // IN over integers: 1 = a bitmap (literals [min, words, bits...])
+  int32_t slot;      // k_filter_leaf: the preloaded column slot holding `col` (-1: loaded per leaf)
+  int32_t ctype;     // the column's dr_pred_type
 };
 enum : int32_t { LEAF_OP_LEAF = 0, LEAF_OP_AND = 1, LEAF_OP_OR = 2, LEAF_OP_NOT = 3 };
 struct FilterLeafArgs {
@@ -444,11 +447,20 @@ struct FilterLeafArgs {
   const uint8_t* lit_str;
   const uint64_t* lit_s8;        // per string literal: its first 8 bytes as PvColumn::s8
   int32_t n_i64, n_str;          // literal counts
-  uint64_t* mask;                // [16 per workgroup] selection bits, one u64 per 64 files in file order
-  uint32_t* wg_count;            // [workgroups] selected files of each workgroup's 1024
+  uint64_t* mask;                // [filter_leaf_mask_words() per tile] selection bits, one u64 per 64 files in file order
+  uint32_t* wg_count;            // [tiles] selected files of each 1024-file tile (zeroed before the launch)
+  int32_t nleaves;
+  int32_t nucol;                 // distinct columns the leaves read (0: more than FL_UCOLS, loaded per leaf)
+  int32_t ucol[4];               // FL_UCOLS: those columns (predicate column indices)
 };
-// workgroups of k_filter_leaf (1024 files each): the sizes of `mask` (x16) and `wg_count`
+constexpr int FL_UCOLS = 4;
+uint32_t filter_leaf_max_prog();
+uint32_t filter_leaf_max_i64();   // literals k_filter_leaf holds in LDS (more: k_filter_typed)
+uint32_t filter_leaf_max_str();
+uint32_t filter_leaf_max_leaves();
+// 1024-file tiles of k_filter_leaf: the sizes of `mask` (x16) and `wg_count`
 uint64_t filter_leaf_groups(uint64_t n_live);
+uint32_t filter_leaf_mask_words();  // mask words per tile
 void launch_filter_leaf(const FilterLeafArgs& a, hipStream_t st);
 // out[wg_off[g] + rank] = ordinal of every selected file (wg_off: exclusive scan of wg_count)
 void launch_select_bits(const uint64_t* mask, const uint64_t* wg_off, uint64_t n, int64_t* out, hipStream_t st);
@@ -600,6 +612,8 @@ enum : int { EXC_STATS = 0, EXC_PV_N, EXC_PV_KB, EXC_PV_VB, EXC_TAGS_N, EXC_TAGS
 struct ExportArgs {
   const uint32_t* idx;  // survivor action indices
   uint64_t n;
+  const uint32_t* pos;  // pass 1: the records of this launch (checkpoint ones or JSON ones); null: [0, n)
+  uint64_t npos;
   int32_t side;         // 0 add (allFiles), 1 remove (tombstones)
   int32_t write;
   const uint8_t* act_flags;
@@ -620,6 +634,8 @@ struct ExportArgs {
   uint8_t* pv_null;
   uint8_t* tags_null;
   uint32_t* cnt[EXC_N];        // per record
+  uint64_t* stats_src;         // a checkpoint record's stats bytes (pass 2 leaves them to k_gather_bytes)
+  uint32_t* stats_srclen;      // their length; 0 for a JSON record
   // pass 2
   const uint64_t* off[EXC_N];  // exclusive scans of cnt
   uint8_t* stats_bytes;
@@ -633,9 +649,26 @@ struct ExportArgs {
   uint8_t* tags_val_null;
   uint8_t* tags_key_bytes;
   uint8_t* tags_val_bytes;
+  // pass 2, checkpoint records: each map entry's key / value source and length (zeroed by the host;
+  // JSON entries keep length 0), copied afterwards by k_gather_bytes at the entry offsets
+  uint64_t* pv_ksrc;
+  uint64_t* pv_vsrc;
+  uint32_t* pv_klen;
+  uint32_t* pv_vlen;
+  uint64_t* tags_ksrc;
+  uint64_t* tags_vsrc;
+  uint32_t* tags_klen;
+  uint32_t* tags_vlen;
   uint32_t* error;
 };
-void launch_export(const ExportArgs& a, hipStream_t st);
+// pass 1 (a.write == 0): one launch over a.pos (checkpoint records: no line stage) -- call it per
+// list with `stage` false / true; pass 2: every record, staged
+void launch_export(const ExportArgs& a, bool stage, hipStream_t st);
+// json[i] = 1 when survivor i's record is a JSON line (0: a checkpoint row)
+void launch_export_flags(const ExportArgs& a, uint32_t* json, hipStream_t st);
+// jpos[jscan[i]] = i for JSON records, cpos[i - jscan[i]] = i for checkpoint ones
+void launch_export_split(const uint32_t* json, const uint64_t* jscan, uint64_t n, uint32_t* jpos, uint32_t* cpos,
+                         hipStream_t st);
 // Order-free full-record checksum of one exported side (dr_state_record_sums; the record hash is
 // defined in oracle/delta_oracle.py:record_hash): *sum += hash(record) over the n records.
 struct RecordHashArgs {

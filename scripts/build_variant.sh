@@ -3,6 +3,6 @@
 set -e
 name=$1; defs=$2
 mkdir -p var_libs/$name
-make -s OBJDIR=build/var_$name LIB=var_libs/$name/libdeltareplay.so \
+make -j8 -s OBJDIR=build/var_$name LIB=var_libs/$name/libdeltareplay.so \
   HIPFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -Wno-unused-variable $defs" \
   var_libs/$name/libdeltareplay.so

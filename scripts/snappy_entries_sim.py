@@ -163,12 +163,26 @@ def resolve_all(raw, CH=256, WU=192, MAX_RUN=32, GAP=80, MARGIN=8, order=None):
             if f >= cnt:
                 if agree and base > jf and (not FIX or not any(flag[base:min(nc, base + cnt + GAP)])): break
                 e = spec_exit[base + cnt - 1]; base += cnt; continue
-            ef0 = cands[f]; fcs = (base + f) * CH; fce = min(fcs + CH, n)
-            if ef0 >= fce:
-                jt = min(ef0 // CH, nc)
-                for q in range(base + f + 1, jt): entry[q] = ef0
-                e = ef0; base = jt if jt > base + f else base + f + 1; continue
-            e = walk(ef0, fce); base += f + 1
+            # r04: breaks inside the window are followed one after another without reloading it
+            nxt = True
+            while True:
+                ef0 = cands[f]; fcs = (base + f) * CH; fce = min(fcs + CH, n)
+                if ef0 >= fce:
+                    jt = min(ef0 // CH, nc)
+                    for q in range(base + f + 1, jt): entry[q] = ef0
+                    e = ef0; base = jt if jt > base + f else base + f + 1; nxt = False; break
+                ef = walk(ef0, fce)
+                if f + 1 >= cnt:
+                    e = ef; base += f + 1; nxt = False; break
+                j1 = base + f + 1; cs1 = j1 * CH; ce1 = min(cs1 + CH, n)
+                cands[f + 1] = ef
+                oks[f + 1] = ef < ce1 and ef in vis[j1]
+                f2 = next((l for l in range(f + 1, cnt) if not oks[l]), 64)
+                for l in range(f + 1, min(f2, cnt - 1) + 1): entry[base + l] = min(cands[l], 0xffffffff)
+                f = f2
+                if f >= cnt: break
+            if nxt:
+                e = spec_exit[base + cnt - 1]; base += cnt
             yield
     if order == "interleave":
         gens = [resolver(jf) for jf in regions]

@@ -361,21 +361,23 @@ def measure_filter(eng, staged, cutoff, exp, steps):
     first_s = time.perf_counter() - t0
     first = eng.last_timings()
     ms = {}
-    t0 = time.perf_counter()
-    for _ in range(steps):
+    for _ in range(steps):  # per-kernel HIP events (their own pass: the events cost the call time)
         st.filter(prog)
         for k, v in eng.last_timings().items():
             ms[k] = ms.get(k, 0.0) + v / steps
-    call_s = (time.perf_counter() - t0) / steps
     eng.set_timing(False)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        st.filter(prog)
+    call_s = (time.perf_counter() - t0) / steps
     n = st.counts["num_files"]
     st.release()
     assert len(sel) == exp["selected"], (len(sel), exp["selected"])
-    # typed cache reads: p0 date (4 B) + p1 int (4 B) + p2 string (8 B inline prefix + 4 B length: its
-    # values fit the prefix, no gather) + p3 boolean (4 B) + 4 null bytes, and one selection bit out per
-    # file (k_filter_leaf writes bit masks; k_select_bits turns them into ordinals)
-    algo = n * (4 + 4 + 12 + 4 + 4) + n // 8
-    kname = "k_filter_leaf" if "k_filter_leaf" in ms else "k_filter_typed"
+    # the dictionary path (k_filter_dict) reads a u16 code per file and column (4 columns: 8 B) and
+    # writes one selection bit per file; the typed path (k_filter_leaf) reads p0 date (4 B) + p1 int
+    # (4 B) + p2 string (8 B prefix + 4 B length) + p3 boolean (4 B) + 4 null bytes
+    kname = next((k for k in ("k_filter_dict", "k_filter_leaf", "k_filter_typed") if k in ms), "k_filter_typed")
+    algo = n * (2 * 4) + n // 8 if kname == "k_filter_dict" else n * (4 + 4 + 12 + 4 + 4) + n // 8
     kt = ms.get(kname)
     # SURVEY.md §8(d)'s K5 budget: 4 B per predicate column + 1 B flag out per file (4 columns: 17 B)
     survey = n * (4 * 4 + 1)
@@ -389,8 +391,9 @@ def measure_filter(eng, staged, cutoff, exp, steps):
                          "frac": round(algo / (kt * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if kt else None,
                          "survey_budget_bytes": survey,
                          "survey_frac": round(survey / (kt * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if kt else None,
-                         "note": "algo_bytes = the typed cache layout this kernel reads (28 B/file + 1 bit out); "
-                                 "survey_* = SURVEY.md 8(d)'s 4 B/column + 1 B budget (17 B/file)"},
+                         "note": "algo_bytes = what this kernel reads and writes (dictionary codes: 2 B per file "
+                                 "and column + 1 bit out; typed cache: 28 B/file + 1 bit); survey_* = SURVEY.md "
+                                 "8(d)'s 4 B/column + 1 B budget (17 B/file)"},
             "kernels": {k: round(v, 4) for k, v in ms.items()}}
 
 

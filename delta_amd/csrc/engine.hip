@@ -593,6 +593,12 @@ struct dr_state {
     DBuf<uint8_t> isnull;
     DBuf<uint64_t> s8;
     DBuf<int64_t> w64hi;  // DECIMAL: high 64 bits of the unscaled value
+    // K5 dictionary (built on the first leaf-form filter that reads the column): u16 code per live
+    // file, code 0 = NULL; rep[c] = a row holding code c's value. dict: -1 not built, 0 none, 1 ok
+    int dict = -1;
+    uint32_t ncode = 0;
+    DBuf<uint16_t> code;
+    DBuf<uint32_t> rep;
   };
   std::vector<std::unique_ptr<PvCol>> pv_cols;
   std::vector<std::shared_ptr<DBuf<uint8_t>>> pv_arenas;  // unescaped string values
@@ -3941,6 +3947,60 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
 
 static std::vector<int64_t> select_flags(dr_state& st, DBuf<uint32_t>& flag);
 
+static PvColumn pv_column(const dr_state::PvCol& c) {
+  PvColumn p{};
+  p.type = c.type;
+  p.w32 = c.w32.p;
+  p.w64 = c.w64.p;
+  p.sptr = c.sptr.p;
+  p.slen = c.slen.p;
+  p.isnull = c.isnull.p;
+  p.s8 = c.s8.p;
+  p.w64hi = c.w64hi.p;
+  return p;
+}
+
+// Dictionary-encodes a typed partition column (k_dict_*): abandoned (dict = 0) past DICT_MAX - 1
+// distinct values, for DECIMAL (two-word values) and on a string hash collision.
+static void build_dict(dr_state& st, dr_state::PvCol& col) {
+  if (col.dict >= 0) return;
+  col.dict = 0;
+  const int base = col.type & 0xff;
+  if (base == DR_T_DECIMAL || !st.n_live) return;
+  dr_ctx* ctx = st.ctx;
+  hipStream_t stream = ctx->stream;
+  const uint64_t n = st.n_live;
+  DBuf<uint64_t> keys(ctx, DICT_SLOTS), scan(ctx, DICT_SLOTS + 1);
+  DBuf<uint32_t> tags(ctx, DICT_SLOTS), slot_code(ctx, DICT_SLOTS), occ(ctx, DICT_SLOTS);
+  DBuf<unsigned long long> ctr(ctx, 2);
+  DBuf<uint8_t> scratch(ctx, scan_scratch_for(DICT_SLOTS));
+  tags.zero(stream);
+  ctr.zero(stream);
+  PvDictArgs a{};
+  a.n = n;
+  a.col = pv_column(col);
+  a.key_tab = keys.p;
+  a.tag_tab = tags.p;
+  a.slot_code = slot_code.p;
+  a.ctr = ctr.p;
+  launch_dict_insert(a, stream);
+  launch_dict_occupied(a, occ.p, stream);
+  launch_scan_u32(occ.p, scan.p, DICT_SLOTS, ss(scratch), stream);
+  const uint64_t distinct = d2h_one(scan.p + DICT_SLOTS, stream);
+  if (d2h_one(ctr.p + 1, stream) || distinct + 1 >= DICT_MAX) return;
+  DBuf<uint32_t> rep(ctx, DICT_MAX + 1);
+  DBuf<uint16_t> code(ctx, n);
+  a.rep = rep.p;
+  a.code = code.p;
+  launch_dict_number(a, scan.p, stream);
+  launch_dict_code(a, stream);
+  if (d2h_one(ctr.p + 1, stream)) return;  // a string hash collision
+  col.code = std::move(code);
+  col.rep = std::move(rep);
+  col.ncode = uint32_t(distinct + 1);
+  col.dict = 1;
+}
+
 static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred) {
   check_program(pred);
   dr_ctx* ctx = st.ctx;
@@ -3969,7 +4029,7 @@ static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred)
       fa.cols[c].type = pred.col_types[c];
       continue;
     }
-    fa.cols[c] = PvColumn{col->type, col->w32.p, col->w64.p, col->sptr.p, col->slen.p, col->isnull.p, col->s8.p};
+    fa.cols[c] = pv_column(*col);
   }
   LeafPlan lp;
   const bool force_generic = std::getenv("DR_FILTER_GENERIC") != nullptr;  // test hook: k_filter_typed
@@ -4020,7 +4080,58 @@ static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred)
     wg_count.zero(stream);
     la.mask = mask.p;
     la.wg_count = wg_count.p;
-    launch_filter_leaf(la, stream);
+    // the dictionary path when every column the leaves read has a dictionary and the leaf tables fit
+    std::vector<dr_state::PvCol*> ucols;
+    for (int32_t u = 0; u < la.nucol; ++u) ucols.push_back(find(pred.col_names[la.ucol[u]], pred.col_types[la.ucol[u]]));
+    bool use_dict = la.nucol > 0 && st.n_live && std::getenv("DR_FILTER_NODICT") == nullptr;  // test hook
+    for (dr_state::PvCol* c : ucols) {
+      if (!use_dict || !c) { use_dict = false; break; }
+      build_dict(st, *c);
+      use_dict = c->dict == 1;
+    }
+    std::vector<uint32_t> tab_off(lp.leaves.size() + 1, 0);
+    if (use_dict) {
+      for (size_t l = 0; l < lp.leaves.size(); ++l) tab_off[l + 1] = tab_off[l] + ucols[size_t(lp.leaves[l].slot)]->ncode;
+      use_dict = tab_off.back() <= filter_dict_max_tab();
+    }
+    DBuf<uint32_t> d_toff;
+    DBuf<uint8_t> d_tab;
+    if (use_dict) {
+      d_toff = upload(ctx, tab_off.data(), tab_off.size());
+      d_tab = DBuf<uint8_t>(ctx, tab_off.back());
+      DictLeafArgs d{};
+      d.leaves = la.leaves;
+      d.nleaves = la.nleaves;
+      for (int32_t c = 0; c < pred.ncols; ++c) d.cols[c] = la.cols[c];
+      for (int32_t u = 0; u < la.nucol; ++u) {
+        d.rep[la.ucol[u]] = ucols[size_t(u)]->rep.p;
+        d.ncode[la.ucol[u]] = ucols[size_t(u)]->ncode;
+      }
+      d.tab_off = d_toff.p;
+      d.tab = d_tab.p;
+      d.lit_i64 = la.lit_i64;
+      d.lit_s8 = la.lit_s8;
+      d.lit_str_off = la.lit_str_off;
+      d.lit_str = la.lit_str;
+      d.n_live = st.n_live;
+      launch_dict_leaf(d, tab_off.back(), stream);
+      FilterDictArgs f{};
+      f.n_live = st.n_live;
+      for (int32_t u = 0; u < la.nucol; ++u) f.code[u] = ucols[size_t(u)]->code.p;
+      f.nslot = la.nucol;
+      f.leaves = la.leaves;
+      f.nleaves = la.nleaves;
+      f.prog = la.prog;
+      f.nprog = la.nprog;
+      f.tab_off = d_toff.p;
+      f.tab = d_tab.p;
+      f.tab_bytes = tab_off.back();
+      f.mask = mask.p;
+      f.wg_count = wg_count.p;
+      launch_filter_dict(f, stream);
+    } else {
+      launch_filter_leaf(la, stream);
+    }
     launch_scan_u32(wg_count.p, wg_off.p, ng, ss(scratch), stream);
     const uint64_t nsel = ng ? d2h_one(wg_off.p + ng, stream) : 0;
     DBuf<int64_t> sel(ctx, nsel);

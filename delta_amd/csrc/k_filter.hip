@@ -894,7 +894,7 @@ constexpr uint32_t FL_FILES = FL_T * FL_PER;  // files per tile (4 FL_PER mask w
 // string prefix, vn = string length); the long-string gather reads the column by file ordinal i.
 // The literals are the workgroup's LDS copies (li: integers and IN sets, ls8 / lso: the string
 // literals' prefixes and offsets).
-__device__ __forceinline__ uint32_t leaf_value(const FilterLeafArgs& a, const FilterLeaf& L, const PvColumn& col,
+__device__ __forceinline__ uint32_t leaf_value(const uint8_t* lit_str, const FilterLeaf& L, const PvColumn& col,
                                                uint64_t i, uint32_t nul, int64_t v, uint32_t vn, const int64_t* li,
                                                const uint64_t* ls8, const uint64_t* lso) {
   const bool str = L.ctype == DR_T_STRING;
@@ -912,7 +912,7 @@ __device__ __forceinline__ uint32_t leaf_value(const FilterLeafArgs& a, const Fi
       const uint64_t l8 = ls8[k];
       if (v8 != l8) return v8 < l8 ? -1 : 1;
       if (vn <= 8 && ln <= 8) return vn == ln ? 0 : (vn < ln ? -1 : 1);
-      return bytes_cmp(reinterpret_cast<const uint8_t*>(col.sptr[i]), vn, a.lit_str + o, ln);
+      return bytes_cmp(reinterpret_cast<const uint8_t*>(col.sptr[i]), vn, lit_str + o, ln);
     }
     const int64_t x = li[k];
     return v == x ? 0 : (v < x ? -1 : 1);
@@ -1043,7 +1043,223 @@ __global__ void __launch_bounds__(FL_T) k_filter_leaf(FilterLeafArgs a) {
 #pragma unroll
         for (int j = 0; j < FL_PER; ++j)
           stk[j] = (stk[j] << 2) |
-                   leaf_value(a, L, col, base + threadIdx.x + uint64_t(j) * FL_T, n0[j], v0[j], l0[j], slit, ss8, ssoff);
+                   leaf_value(a.lit_str, L, col, base + threadIdx.x + uint64_t(j) * FL_T, n0[j], v0[j], l0[j], slit, ss8, ssoff);
+      } else if (op == LEAF_OP_NOT) {
+#pragma unroll
+        for (int j = 0; j < FL_PER; ++j) {
+          const uint64_t x = stk[j] & 3u;
+          stk[j] = (stk[j] & ~3ull) | (x == 2u ? 2u : (x ^ 1u));
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < FL_PER; ++j) {
+          const uint32_t y = uint32_t(stk[j] & 3u), x = uint32_t((stk[j] >> 2) & 3u);
+          uint32_t rr;
+          if (op == LEAF_OP_AND) rr = (x == 0u || y == 0u) ? 0u : (x == 1u && y == 1u) ? 1u : 2u;
+          else rr = (x == 1u || y == 1u) ? 1u : (x == 0u && y == 0u) ? 0u : 2u;
+          stk[j] = ((stk[j] >> 4) << 2) | rr;
+        }
+      }
+    }
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int j = 0; j < FL_PER; ++j) {
+      const bool f = (full || base + threadIdx.x + uint64_t(j) * FL_T < a.n_live) && (stk[j] & 3u) == 1u;
+      const unsigned long long m = __ballot(f);
+      if (lane == 0) a.mask[base / 64 + 4 * j + wv] = m;
+      cnt += uint32_t(__popcll(m));
+    }
+    if (lane == 0 && cnt) atomicAdd(&a.wg_count[tile], cnt);
+  }
+}
+
+// ---- K5 dictionary path ----------------------------------------------------------------------------
+// Partition columns are low-cardinality by construction (one value per directory), so the typed
+// cache is dictionary-encoded once per column: every distinct non-NULL value gets a u16 code
+// (code 0 is NULL). A leaf is then evaluated once per code (k_dict_leaf: leaf_value on the code's
+// representative row, so the three-valued semantics are the typed path's own), and k_filter_dict
+// reads 2 bytes per file and column and looks the leaf results up in LDS (r04: the typed pass read
+// 28 B per file in nine loads and evaluated every leaf per file: 1.93 ms for 100M files).
+// Keys: the integer value itself (exact), or a string's xxh64 (k_dict_verify compares every file's
+// bytes with its code's representative, so a hash collision abandons the dictionary).
+__device__ __forceinline__ uint64_t dict_mix(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  return k ^ (k >> 33);
+}
+__device__ __forceinline__ bool dict_key(const PvColumn& c, uint64_t i, uint64_t* key) {
+  if (c.isnull[i]) return false;
+  const int base = c.type & 0xff;
+  if (base == DR_T_STRING || base == DR_T_BINARY) *key = xxh64(reinterpret_cast<const uint8_t*>(c.sptr[i]), c.slen[i]);
+  else if (c.w64) *key = uint64_t(c.w64[i]);
+  else *key = uint64_t(c.w32[i]);
+  return true;
+}
+
+// Inserts (key, row) into an open-addressing table (tag 0 empty, ~0 being written, 1 + row taken),
+// one probe step per loop iteration for every lane, so a lane that finds a slot being written by
+// another lane of its wave retries after that lane's write instead of spinning past it. Returns
+// false when the table is full.
+template <bool Lds>
+__device__ __forceinline__ bool dict_put(uint64_t* keys, uint32_t* tags, uint32_t mask, uint64_t key, uint32_t row) {
+  uint32_t h = uint32_t(dict_mix(key) >> 15) & mask;
+  uint32_t probes = 0;
+  bool done = false, ok = true;
+  while (!done) {
+    const uint32_t t = atomicCAS(&tags[h], 0u, 0xffffffffu);
+    if (t == 0u) {
+      keys[h] = key;
+      if (!Lds) __threadfence();
+      atomicExch(&tags[h], 1u + row);
+      done = true;
+    } else if (t != 0xffffffffu) {
+      const uint64_t k = Lds ? *reinterpret_cast<volatile uint64_t*>(&keys[h])
+                             : __hip_atomic_load(&keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (k == key) {
+        done = true;
+      } else {
+        h = (h + 1) & mask;
+        if (++probes > mask) { done = true; ok = false; }
+      }
+    }
+  }
+  return ok;
+}
+
+constexpr uint32_t DICT_T = 256, DICT_PER = 8, DICT_LSLOTS = 1024;
+__global__ void __launch_bounds__(DICT_T) k_dict_insert(PvDictArgs a) {
+  __shared__ uint64_t lkey[DICT_LSLOTS];
+  __shared__ uint32_t ltag[DICT_LSLOTS];
+  for (uint32_t k = threadIdx.x; k < DICT_LSLOTS; k += DICT_T) ltag[k] = 0;
+  __syncthreads();
+  const uint64_t base = uint64_t(blockIdx.x) * DICT_T * DICT_PER;
+  // the workgroup's distinct keys first (a handful for a partition column), then those go global
+  for (uint32_t j = 0; j < DICT_PER; ++j) {
+    const uint64_t i = base + threadIdx.x + uint64_t(j) * DICT_T;
+    uint64_t key;
+    if (i < a.n && dict_key(a.col, i, &key))
+      if (!dict_put<true>(lkey, ltag, DICT_LSLOTS - 1, key, uint32_t(i)))
+        if (!dict_put<false>(a.key_tab, a.tag_tab, DICT_SLOTS - 1, key, uint32_t(i))) atomicOr(&a.ctr[1], 1ull);
+  }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < DICT_LSLOTS; k += DICT_T) {
+    const uint32_t t = ltag[k];
+    if (t && !dict_put<false>(a.key_tab, a.tag_tab, DICT_SLOTS - 1, lkey[k], t - 1u)) atomicOr(&a.ctr[1], 1ull);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_dict_occupied(PvDictArgs a, uint32_t* occ) {
+  const uint32_t h = blockIdx.x * 256 + threadIdx.x;
+  if (h < DICT_SLOTS) occ[h] = a.tag_tab[h] != 0u;
+}
+
+// code = 1 + rank of the occupied slot; rep[code] = the slot's first row
+__global__ void __launch_bounds__(256) k_dict_number(PvDictArgs a, const uint64_t* scan) {
+  const uint32_t h = blockIdx.x * 256 + threadIdx.x;
+  if (h >= DICT_SLOTS || !a.tag_tab[h]) return;
+  const uint64_t c = scan[h] + 1;
+  if (c >= DICT_MAX) return;  // too many values: the host abandons the dictionary
+  a.slot_code[h] = uint32_t(c);
+  a.rep[c] = a.tag_tab[h] - 1u;
+}
+
+__global__ void __launch_bounds__(256) k_dict_code(PvDictArgs a) {
+  const uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  uint64_t key;
+  uint16_t c = 0;
+  if (dict_key(a.col, i, &key)) {
+    uint32_t h = uint32_t(dict_mix(key) >> 15) & (DICT_SLOTS - 1);
+    for (uint32_t p = 0; p < DICT_SLOTS && a.key_tab[h] != key; ++p) h = (h + 1) & (DICT_SLOTS - 1);
+    c = uint16_t(a.slot_code[h]);
+    // strings: the code's representative must hold the same bytes (a 64-bit hash collision would
+    // merge two values)
+    const int base = a.col.type & 0xff;
+    if (base == DR_T_STRING || base == DR_T_BINARY) {
+      const uint32_t r = a.rep[c];
+      const uint32_t n0 = a.col.slen[i];
+      bool same = n0 == a.col.slen[r] && a.col.s8[i] == a.col.s8[r];
+      if (same && n0 > 8)
+        same = bytes_equal(reinterpret_cast<const uint8_t*>(a.col.sptr[i]), reinterpret_cast<const uint8_t*>(a.col.sptr[r]), n0);
+      if (!same) atomicOr(&a.ctr[1], 2ull);
+    }
+  }
+  a.code[i] = c;
+}
+
+// One thread per (leaf, code): the leaf on the code's representative value (code 0: NULL).
+__global__ void __launch_bounds__(256) k_dict_leaf(DictLeafArgs a, uint32_t total) {
+  const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= total) return;
+  int32_t l = 0;
+  while (l + 1 < a.nleaves && a.tab_off[l + 1] <= t) ++l;
+  const FilterLeaf L = a.leaves[l];
+  const uint32_t k = t - a.tab_off[l];
+  const PvColumn& col = a.cols[L.col];
+  uint32_t nul = 1, vn = 0;
+  int64_t v = 0;
+  uint64_t row = 0;
+  if (k > 0) {
+    row = a.rep[L.col][k];
+    nul = 0;
+    if (L.ctype == DR_T_STRING) {
+      vn = col.slen[row];
+      v = int64_t(col.s8[row]);
+    } else {
+      v = L.ctype == DR_T_LONG ? col.w64[row] : int64_t(int32_t(col.w32[row]));
+    }
+  }
+  a.tab[t] = uint8_t(leaf_value(a.lit_str, L, col, row, nul, v, vn, a.lit_i64, a.lit_s8, a.lit_str_off));
+}
+
+// The per-file pass over codes: tiles of FL_FILES files, FL_PER per lane; every leaf is one LDS
+// byte read per file.
+constexpr uint32_t FD_MAXTAB = 32768;
+__global__ void __launch_bounds__(FL_T) k_filter_dict(FilterDictArgs a) {
+  __shared__ int32_t sprog[2 * FL_MAXPROG];
+  __shared__ FilterLeaf sleaf[FL_MAXLEAF];
+  __shared__ uint32_t stoff[FL_MAXLEAF + 1];
+  __shared__ uint8_t stab[FD_MAXTAB];
+  for (int k = threadIdx.x; k < 2 * a.nprog; k += FL_T) sprog[k] = a.prog[k];
+  for (int k = threadIdx.x; k < a.nleaves; k += FL_T) sleaf[k] = a.leaves[k];
+  for (int k = threadIdx.x; k <= a.nleaves; k += FL_T) stoff[k] = a.tab_off[k];
+  for (uint32_t k = threadIdx.x; k < a.tab_bytes; k += FL_T) stab[k] = a.tab[k];
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t ntiles = (a.n_live + FL_FILES - 1) / FL_FILES;
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const uint64_t base = tile * FL_FILES;
+    const bool full = base + FL_FILES <= a.n_live;
+    uint32_t cd[FL_UCOLS][FL_PER];
+#pragma unroll
+    for (int u = 0; u < FL_UCOLS; ++u) {
+      if (u >= a.nslot) break;  // uniform
+      const uint16_t* cp = a.code[u] + base;
+#pragma unroll
+      for (int j = 0; j < FL_PER; ++j) {
+        const uint32_t o = threadIdx.x + uint32_t(j) * FL_T;
+        cd[u][j] = (full || base + o < a.n_live) ? uint32_t(cp[o]) : 0u;
+      }
+    }
+    uint64_t stk[FL_PER];
+#pragma unroll
+    for (int j = 0; j < FL_PER; ++j) stk[j] = 0;
+    for (int k = 0; k < a.nprog; ++k) {
+      const int op = __builtin_amdgcn_readfirstlane(sprog[2 * k]);
+      if (op == LEAF_OP_LEAF) {
+        const int li = __builtin_amdgcn_readfirstlane(sprog[2 * k + 1]);
+        const int slot = __builtin_amdgcn_readfirstlane(sleaf[li].slot);
+        const uint32_t off = uint32_t(__builtin_amdgcn_readfirstlane(int(stoff[li])));
+#pragma unroll
+        for (int j = 0; j < FL_PER; ++j) {
+          uint32_t c = cd[0][j];
+#pragma unroll
+          for (int u = 1; u < FL_UCOLS; ++u)
+            if (u == slot) c = cd[u][j];
+          stk[j] = (stk[j] << 2) | stab[off + c];
+        }
       } else if (op == LEAF_OP_NOT) {
 #pragma unroll
         for (int j = 0; j < FL_PER; ++j) {
@@ -1209,6 +1425,29 @@ void launch_filter_leaf(const FilterLeafArgs& a, hipStream_t st) {
   if (a.n_live) DR_LAUNCH(dev::k_filter_leaf, dim3(g), dim3(dev::FL_T), 0, st, a);
 }
 uint32_t filter_leaf_max_prog() { return dev::FL_MAXPROG; }
+void launch_dict_insert(const PvDictArgs& a, hipStream_t st) {
+  const uint64_t per = uint64_t(dev::DICT_T) * dev::DICT_PER;
+  if (a.n) DR_LAUNCH(dev::k_dict_insert, dim3(unsigned((a.n + per - 1) / per)), dim3(dev::DICT_T), 0, st, a);
+}
+void launch_dict_occupied(const PvDictArgs& a, uint32_t* occ, hipStream_t st) {
+  DR_LAUNCH(dev::k_dict_occupied, dim3(DICT_SLOTS / 256), dim3(256), 0, st, a, occ);
+}
+void launch_dict_number(const PvDictArgs& a, const uint64_t* scan, hipStream_t st) {
+  DR_LAUNCH(dev::k_dict_number, dim3(DICT_SLOTS / 256), dim3(256), 0, st, a, scan);
+}
+void launch_dict_code(const PvDictArgs& a, hipStream_t st) {
+  if (a.n) DR_LAUNCH(dev::k_dict_code, dim3(g256(a.n)), dim3(256), 0, st, a);
+}
+void launch_dict_leaf(const DictLeafArgs& a, uint32_t total, hipStream_t st) {
+  if (total) DR_LAUNCH(dev::k_dict_leaf, dim3(unsigned((total + 255) / 256)), dim3(256), 0, st, a, total);
+}
+uint32_t filter_dict_max_tab() { return dev::FD_MAXTAB; }
+void launch_filter_dict(const FilterDictArgs& a, hipStream_t st) {
+  if (a.nprog > dev::FL_MAXPROG || a.nleaves > dev::FL_MAXLEAF || a.tab_bytes > dev::FD_MAXTAB)
+    throw std::runtime_error("filter program too long for the dictionary kernel");
+  const unsigned g = unsigned(std::min<uint64_t>(filter_leaf_groups(a.n_live), 256 * 8));
+  if (a.n_live) DR_LAUNCH(dev::k_filter_dict, dim3(g), dim3(dev::FL_T), 0, st, a);
+}
 uint32_t filter_leaf_max_i64() { return dev::FL_MAXI64; }
 uint32_t filter_leaf_max_str() { return dev::FL_MAXSTR; }
 uint32_t filter_leaf_max_leaves() { return dev::FL_MAXLEAF; }

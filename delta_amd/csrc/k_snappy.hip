@@ -689,7 +689,11 @@ __global__ void __launch_bounds__(2 * WG_CHUNKS) k_snap_emit(SnappyArgs a) {
 //     literal runs are copied LDS -> LDS;
 //  4. each thread gathers its groups' bytes from their roots and stores them (coalesced dwords).
 constexpr int EXEC_T = 1024;
-constexpr uint32_t EXEC_LONG = 256;          // literal records copied by the whole workgroup
+constexpr uint32_t EXEC_LONG = 256;          // literal records queued for the cooperative copy (at most)
+#ifndef DR_EXEC_LONG_LEN
+#define DR_EXEC_LONG_LEN 64
+#endif
+constexpr uint32_t EXEC_LONG_LEN = DR_EXEC_LONG_LEN;  // literals longer than this are copied by a whole wave
 #ifndef DR_EXEC_RPT
 #define DR_EXEC_RPT 12
 #endif
@@ -706,7 +710,7 @@ constexpr uint32_t EXEC_SPLIT = DR_EXEC_SPLIT;  // map groups whose reads are is
 __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t src[SNAP_BLOCK];  // map, later bytes + input
   __shared__ uint32_t s_bad, s_nlong, s_inlo, s_inhi;
-  __shared__ uint32_t s_long[EXEC_LONG];
+  __shared__ uint64_t s_long[EXEC_LONG];  // queued long literal records
   __shared__ uint32_t starts_mem[SNAP_BLOCK / 32 + 2];  // element start bits, after two zero words
   uint32_t* const starts = starts_mem + 2;
   const uint32_t b = blockIdx.x;
@@ -900,11 +904,12 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
       if (r >= nrec || !(sv & REC_LIT)) return;
       const uint32_t rel = uint32_t(wk & 0xffff);
       const uint32_t len = uint32_t((wk >> 16) & 0xffff) + 1;
-      if (len > EXEC_LONG) {
+      if (len > EXEC_LONG_LEN) {  // queued while there is room, else copied by this lane below
         const uint32_t slot = atomicAdd(&s_nlong, 1u);
-        if (slot < EXEC_LONG) s_long[slot] = r;
-        else s_bad = 1;
-        return;
+        if (slot < EXEC_LONG) {
+          s_long[slot] = wk;
+          return;
+        }
       }
       if (!staged) {  // a poorly compressible block: its input does not fit the stage; read it in place
         const uint8_t* sp = in + (sv & ~REC_LIT);
@@ -947,12 +952,18 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
   __syncthreads();
   stamp(5);
   const uint32_t nlong = min(s_nlong, EXEC_LONG);
-  for (uint32_t L = 0; L < nlong; ++L) {  // long literals: the whole workgroup
-    const uint64_t w = a.recs[r0 + s_long[L]];
-    const uint32_t rel = uint32_t(w & 0xffff);
-    const uint32_t len = uint32_t((w >> 16) & 0xffff) + 1;
-    const uint8_t* ip = in + (uint32_t(w >> 32) & ~REC_LIT);
-    for (uint32_t i = t; i < len; i += EXEC_T) bytes[rel + i] = ip[i];
+  for (uint32_t L = uint32_t(t) >> 6; L < nlong; L += EXEC_T / 64) {  // long literals: one wave each
+    const uint64_t wl = s_long[L];
+    const uint32_t rel = uint32_t(wl & 0xffff);
+    const uint32_t len = uint32_t((wl >> 16) & 0xffff) + 1;
+    const uint32_t ipo = uint32_t(wl >> 32) & ~REC_LIT;
+    if (staged) {
+      const uint32_t q = uint32_t(reinterpret_cast<uintptr_t>(in) + ipo - abs_lo) + SNAP_BLOCK;
+      for (uint32_t i = uint32_t(t) & 63; i < len; i += 64) bytes[rel + i] = bytes[q + i];
+    } else {
+      const uint8_t* ip = in + ipo;
+      for (uint32_t i = uint32_t(t) & 63; i < len; i += 64) bytes[rel + i] = ip[i];
+    }
   }
   __syncthreads();
   stamp(6);

@@ -468,6 +468,55 @@ void launch_select_bits(const uint64_t* mask, const uint64_t* wg_off, uint64_t n
 // one element at a time into an accumulator slot above its value
 enum : int32_t { FILTER_OP_IN_START = 100, FILTER_OP_IN_STEP = 101, FILTER_OP_IN_END = 102 };
 uint32_t filter_max_cols();
+// ---- K5 dictionary path: each partition column's distinct values get u16 codes (code 0: NULL), a
+// leaf becomes a table over its column's codes, and the per-file pass reads 2 bytes per column.
+constexpr uint32_t DICT_SLOTS = 1u << 17;   // global hash table (load <= 1/2)
+constexpr uint32_t DICT_MAX = 65535;        // codes 1..DICT_MAX-1 for values, 0 for NULL
+struct PvDictArgs {
+  uint64_t n;
+  PvColumn col;              // the typed column (its type field: the dr_pred_type)
+  uint64_t* key_tab;         // [DICT_SLOTS] keys
+  uint32_t* tag_tab;         // [DICT_SLOTS] 0 empty, 0xffffffff being written, 1 + representative row
+  uint32_t* slot_code;       // [DICT_SLOTS] code of an occupied slot
+  uint16_t* code;            // [n]
+  uint32_t* rep;             // [DICT_MAX + 1] representative row of each code
+  unsigned long long* ctr;   // 0: occupied slots, 1: table full / verification failed
+};
+void launch_dict_insert(const PvDictArgs& a, hipStream_t st);
+void launch_dict_number(const PvDictArgs& a, const uint64_t* scan, hipStream_t st);   // after a scan of occupancy
+void launch_dict_occupied(const PvDictArgs& a, uint32_t* occ, hipStream_t st);
+void launch_dict_code(const PvDictArgs& a, hipStream_t st);
+struct DictLeafArgs {
+  const FilterLeaf* leaves;
+  int32_t nleaves;
+  PvColumn cols[PV_MAXC];
+  const uint32_t* rep[PV_MAXC];  // per predicate column: representative rows (null: no dictionary)
+  uint32_t ncode[PV_MAXC];       // codes per column (incl. code 0)
+  const uint32_t* tab_off;       // [nleaves + 1] table offsets
+  uint8_t* tab;                  // leaf results (0 false, 1 true, 2 null) per (leaf, code)
+  const int64_t* lit_i64;
+  const uint64_t* lit_s8;
+  const uint64_t* lit_str_off;
+  const uint8_t* lit_str;
+  uint64_t n_live;
+};
+void launch_dict_leaf(const DictLeafArgs& a, uint32_t total, hipStream_t st);
+struct FilterDictArgs {
+  uint64_t n_live;
+  const uint16_t* code[FL_UCOLS];  // per slot: the column's codes
+  int32_t nslot;
+  const FilterLeaf* leaves;        // leaf.slot: the code slot it reads
+  int32_t nleaves;
+  const int32_t* prog;
+  int32_t nprog;
+  const uint32_t* tab_off;
+  const uint8_t* tab;
+  uint32_t tab_bytes;
+  uint64_t* mask;
+  uint32_t* wg_count;
+};
+uint32_t filter_dict_max_tab();   // leaf-table bytes the dictionary kernel holds in LDS
+void launch_filter_dict(const FilterDictArgs& a, hipStream_t st);
 uint32_t filter_max_stack();
 void launch_pv_extract(const PvExtractArgs& a, hipStream_t st);
 void launch_filter_typed(const FilterTypedArgs& a, hipStream_t st);

@@ -46,12 +46,15 @@ def _oracle_selected(lp, preds_list, cutoff=0):
 
 @pytest.mark.parametrize("checkpoint", [False, True])
 @pytest.mark.parametrize("escaped_keys", [False, True])
-@pytest.mark.parametrize("kernel", ["leaf", "generic"])
+@pytest.mark.parametrize("kernel", ["dict", "typed", "generic"])
 def test_filter_cast_corpus(engine, tmp_path, monkeypatch, checkpoint, escaped_keys, kernel):
-    """Both K5 evaluators: k_filter_leaf (leaf form: column-vs-literal comparisons, IN sets, AND/OR/NOT)
-    and the generic postfix interpreter k_filter_typed (DR_FILTER_GENERIC=1)."""
+    """The three K5 evaluators: the leaf form over dictionary codes (k_dict_leaf + k_filter_dict, the
+    default), the leaf form over the typed cache (k_filter_leaf, DR_FILTER_NODICT=1) and the generic
+    postfix interpreter k_filter_typed (DR_FILTER_GENERIC=1)."""
     if kernel == "generic":
         monkeypatch.setenv("DR_FILTER_GENERIC", "1")
+    if kernel == "typed":
+        monkeypatch.setenv("DR_FILTER_NODICT", "1")
     lp = F.build(str(tmp_path), checkpoint=checkpoint, escaped_keys=escaped_keys)
     got = _gpu_selected(engine, lp, F.PREDICATES)
     want = _oracle_selected(lp, F.PREDICATES)
@@ -100,10 +103,13 @@ def test_filter_optimistic_txn_cases(engine, tmp_path, checkpoint):
     assert _gpu_selected(engine, lp2, preds2) == _oracle_selected(lp2, preds2)
 
 
-def test_filter_config4_predicate(engine, tmp_path):
+@pytest.mark.parametrize("kernel", ["dict", "typed"])
+def test_filter_config4_predicate(engine, tmp_path, monkeypatch, kernel):
     """p0 >= DATE'2020-03-01' AND p0 < DATE'2020-06-01' AND p1 IN (1..100)
     AND p2 = 'w17' AND p3 = true, over a 4-column checkpoint + churn commits."""
     from delta_amd.testing import synth as S
+    if kernel == "typed":
+        monkeypatch.setenv("DR_FILTER_NODICT", "1")
     spec = S.ChurnSpec(ckpt_files=30000, ckpt_version=10, n_deltas=4, removes_per_delta=2000,
                        adds_per_delta=2000, readd_frac=0.5, ncols=4)
     exp = S.build_table(str(tmp_path), spec, seed=4, row_group_size=7000)

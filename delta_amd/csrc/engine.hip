@@ -1544,6 +1544,22 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
                      act.size, act.delts, act.src_off, act.src_len, counters.p + 0, counters.p + 1, counters.p + 2,
                      nonfile.p, nlines, counters.p + 3, hard.p,
                      reinterpret_cast<unsigned long long*>(counters.p + 5)};
+    static unsigned long long* phase = nullptr;  // DR_JSON_PHASES=1: staged-kernel phase clocks
+    static uint64_t phase_calls = 0;
+    if (std::getenv("DR_JSON_PHASES")) {
+      if (!phase) {
+        HIP_OK(hipMalloc(&phase, 5 * sizeof(unsigned long long)));
+        HIP_OK(hipMemset(phase, 0, 5 * sizeof(unsigned long long)));
+      }
+      ja.phase = phase;
+      if (++phase_calls % 200 == 0) {
+        unsigned long long h[5];
+        HIP_OK(hipMemcpy(h, phase, sizeof(h), hipMemcpyDeviceToHost));
+        if (h[4])
+          std::fprintf(stderr, "k_json_lines<true> clocks per wave: stage %.0f tape %.0f dfa %.0f (%llu waves)\n",
+                       double(h[0]) / double(h[4]), double(h[1]) / double(h[4]), double(h[2]) / double(h[4]), h[4]);
+      }
+    }
     launch_json_parse(ja, s2);
     launch_json_hard(ja, s2);
     if (ctx->overlap) {
@@ -4046,17 +4062,7 @@ static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred)
       soff[q + 1] = sbytes.size();
       for (size_t k = 0; k < 8; ++k) s8[q] = (s8[q] << 8) | (k < lp.str[q].size() ? uint8_t(lp.str[q][k]) : 0u);
     }
-    DBuf<uint64_t> d_s8 = upload(ctx, s8.data(), s8.size());
-    la.lit_s8 = d_s8.p;
-    DBuf<int32_t> d_prog = upload(ctx, lp.prog.data(), lp.prog.size());
-    DBuf<int64_t> d_i64 = upload(ctx, lp.i64.data(), lp.i64.size());
-    DBuf<uint64_t> d_soff = upload(ctx, soff.data(), soff.size());
-    DBuf<uint8_t> d_sb = upload(ctx, reinterpret_cast<const uint8_t*>(sbytes.data()), sbytes.size());
-    la.prog = d_prog.p;
     la.nprog = int32_t(lp.prog.size() / 2);
-    la.lit_i64 = d_i64.p;
-    la.lit_str_off = d_soff.p;
-    la.lit_str = d_sb.p;
     la.n_i64 = int32_t(lp.i64.size());
     la.n_str = int32_t(lp.str.size());
     la.nleaves = int32_t(lp.leaves.size());
@@ -4071,8 +4077,6 @@ static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred)
         if (la.ucol[u] == f.col) f.slot = u;
       f.ctype = la.cols[f.col].type;
     }
-    DBuf<FilterLeaf> d_leaves = upload(ctx, lp.leaves.data(), lp.leaves.size());
-    la.leaves = d_leaves.p;
     const uint64_t ng = filter_leaf_groups(st.n_live);
     DBuf<uint64_t> mask(ctx, uint64_t(filter_leaf_mask_words()) * ng), wg_off(ctx, ng + 1);
     DBuf<uint32_t> wg_count(ctx, ng);
@@ -4094,10 +4098,28 @@ static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred)
       for (size_t l = 0; l < lp.leaves.size(); ++l) tab_off[l + 1] = tab_off[l] + ucols[size_t(lp.leaves[l].slot)]->ncode;
       use_dict = tab_off.back() <= filter_dict_max_tab();
     }
-    DBuf<uint32_t> d_toff;
+    // the program, leaves and literals in one upload (each pageable upload is a staged copy of its own)
+    std::vector<uint8_t> blob;
+    auto put = [&](const void* src, size_t bytes) -> size_t {
+      const size_t at = (blob.size() + 15) & ~size_t(15);
+      blob.resize(at + bytes);
+      if (bytes) std::memcpy(blob.data() + at, src, bytes);
+      return at;
+    };
+    const size_t o_s8 = put(s8.data(), 8 * s8.size()), o_soff = put(soff.data(), 8 * soff.size());
+    const size_t o_prog = put(lp.prog.data(), 4 * lp.prog.size()), o_i64 = put(lp.i64.data(), 8 * lp.i64.size());
+    const size_t o_leaves = put(lp.leaves.data(), sizeof(FilterLeaf) * lp.leaves.size());
+    const size_t o_toff = put(tab_off.data(), 4 * tab_off.size()), o_sb = put(sbytes.data(), sbytes.size());
+    DBuf<uint8_t> d_blob = upload(ctx, blob.data(), blob.size());
+    la.lit_s8 = reinterpret_cast<const uint64_t*>(d_blob.p + o_s8);
+    la.lit_str_off = reinterpret_cast<const uint64_t*>(d_blob.p + o_soff);
+    la.prog = reinterpret_cast<const int32_t*>(d_blob.p + o_prog);
+    la.lit_i64 = reinterpret_cast<const int64_t*>(d_blob.p + o_i64);
+    la.leaves = reinterpret_cast<const FilterLeaf*>(d_blob.p + o_leaves);
+    la.lit_str = d_blob.p + o_sb;
+    const uint32_t* d_toff = reinterpret_cast<const uint32_t*>(d_blob.p + o_toff);
     DBuf<uint8_t> d_tab;
     if (use_dict) {
-      d_toff = upload(ctx, tab_off.data(), tab_off.size());
       d_tab = DBuf<uint8_t>(ctx, tab_off.back());
       DictLeafArgs d{};
       d.leaves = la.leaves;
@@ -4107,7 +4129,7 @@ static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred)
         d.rep[la.ucol[u]] = ucols[size_t(u)]->rep.p;
         d.ncode[la.ucol[u]] = ucols[size_t(u)]->ncode;
       }
-      d.tab_off = d_toff.p;
+      d.tab_off = d_toff;
       d.tab = d_tab.p;
       d.lit_i64 = la.lit_i64;
       d.lit_s8 = la.lit_s8;
@@ -4123,7 +4145,7 @@ static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred)
       f.nleaves = la.nleaves;
       f.prog = la.prog;
       f.nprog = la.nprog;
-      f.tab_off = d_toff.p;
+      f.tab_off = d_toff;
       f.tab = d_tab.p;
       f.tab_bytes = tab_off.back();
       f.mask = mask.p;

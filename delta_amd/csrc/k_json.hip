@@ -495,7 +495,7 @@ __device__ __forceinline__ void dfa_tape(const JsonParseArgs& a, uint64_t line0,
 // The buffer is flushed through phase 2 whenever a lane could overflow it, and at the end.
 template <bool Stage>
 __global__ void __launch_bounds__(JL_T, DR_JL_WAVES) k_json_lines(JsonParseArgs a) {
-  __shared__ uint32_t tokbuf[JL_TOKCAP * JL_T];
+  __shared__ uint32_t tokbuf[Stage ? 1 : JL_TOKCAP * JL_T];
   __shared__ uint4 stage[Stage ? JL_STAGE_BYTES / 16 : 1];
   __shared__ uint32_t tape[Stage ? TAPE_CAP : 1];
   __shared__ uint16_t nltok[Stage ? JL_T : 1];
@@ -505,6 +505,13 @@ __global__ void __launch_bounds__(JL_T, DR_JL_WAVES) k_json_lines(JsonParseArgs 
   const uint64_t b = !live ? 0 : line == 0 ? 0 : a.nl[line - 1] + 1;
   const uint32_t n = live ? uint32_t(a.nl[line] - b) : 0;
   if constexpr (Stage) {
+    uint64_t tp0 = a.phase ? __builtin_amdgcn_s_memtime() : 0;
+    auto phase = [&](int k) {
+      if (!a.phase) return;
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      if (lane == 0) atomicAdd(&a.phase[k], (unsigned long long)(t - tp0));
+      tp0 = t;
+    };
     // the wave's region: [its first line's 16-byte block, its last line's end rounded up to 16);
     // the JSON buffer's 64-byte zero pad keeps the rounded end readable
     const uint64_t first = uint64_t(blockIdx.x) * JL_T;
@@ -516,16 +523,26 @@ __global__ void __launch_bounds__(JL_T, DR_JL_WAVES) k_json_lines(JsonParseArgs 
       const uint32_t nq = uint32_t((r1 - r0) >> 4) + 3;
       for (uint32_t k = lane; k < nq; k += JL_T) stage[k] = src[k];
       __syncthreads();
+      phase(0);
       const uint32_t nw = uint32_t(last - first + 1);
       const uint64_t rb = first == 0 ? 0 : a.nl[first - 1] + 1;  // the wave's first line
-      if (build_tape(stage, uint32_t(rb - r0), uint32_t(a.nl[last] + 1 - rb), nw, tape, nltok)) {
+      const bool taped = build_tape(stage, uint32_t(rb - r0), uint32_t(a.nl[last] + 1 - rb), nw, tape, nltok);
+      phase(1);
+      if (taped) {
         dfa_tape(a, first, nw, reinterpret_cast<const uint8_t*>(stage) + (rb - r0), rb, tape, nltok);
+        phase(2);
+        if (a.phase && lane == 0) atomicAdd(&a.phase[4], 1ull);
         return;
       }
-      walk_line(a, tokbuf, lane, line, live, b, n, reinterpret_cast<const uint8_t*>(stage) + (b - r0));
-      return;
     }
-    walk_line(a, tokbuf, lane, line, live, b, n, a.buf + b);
+    // a region off the tape (non-canonical bytes, or larger than the stage): its lines go to
+    // k_json_hard's General walker, which decides any line. Keeping the per-lane walker out of this
+    // kernel keeps its code to the tape path: a streamed commit's kernel starts with a cold
+    // instruction cache on whichever CU it lands, so its executed code is fetched once per commit.
+    if (live) {
+      const unsigned long long k = atomicAdd(a.hard_count, 1ull);
+      a.hard_idx[k] = line;
+    }
     return;
   }
   walk_line(a, tokbuf, lane, line, live, b, n, a.buf + b);

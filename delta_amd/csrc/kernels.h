@@ -65,6 +65,7 @@ struct JsonParseArgs {
   uint64_t* error_count;
   uint64_t* hard_idx;             // lines the fast walker defers to the General walker
   unsigned long long* hard_count;
+  unsigned long long* phase;      // diagnostics (DR_JSON_PHASES): staged kernel phase clocks, or null
 };
 
 uint64_t json_num_blocks(uint64_t len);

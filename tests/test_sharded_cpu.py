@@ -96,3 +96,23 @@ def test_sharded_gloo_golden(tmp_path):
     res = run_sharded(lp, 0, str(tmp_path / "out.json"), 2, "fake")
     _check(res, O.state_reconstruction(O.get_log_segment(lp), 0))
     assert [list(a)[0] for a in res["nonfile"]][:2] == ["protocol", "metaData"]
+
+
+def test_sharded_checkpoint_mismatch_raises_on_every_rank(tmp_path):
+    """A sharded checkpoint whose parts hold fewer add rows than numOfFiles: every rank raises the
+    reference's error (D/Checkpoints.scala:325-328) -- none is left waiting in the final barrier, and
+    no `_last_checkpoint` is written."""
+    log = tmp_path / "_delta_log"
+    log.mkdir()
+    out = tmp_path / "out"
+    out.mkdir()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tests", "workers", "ckpt_mismatch_worker.py"), str(log), str(out)]
+    e = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, env=e, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    for rank in (0, 1):
+        got = (out / ("%d.txt" % rank)).read_text()
+        assert got.startswith("raised:") and "doesn't match" in got, got
+    assert not (log / "_last_checkpoint").exists()

@@ -451,7 +451,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU baseline threads (0: every CPU this process may use, see cpu_budget())")
     ap.add_argument("--pmc-dir", default=None,
-                    help="rocprofv3 --pmc passes of this build and config (default profiles/r03/pmc/c<config>)")
+                    help="rocprofv3 --pmc passes of this build and config (default profiles/r04/pmc/c<config>)")
     ap.add_argument("--driver", choices=("lib", "torch"), default="lib",
                     help="N > 1: the library's own RCCL replay (dr_replay_sharded, what a JNI host calls) or "
                          "delta_amd/sharded.py over torch.distributed")
@@ -461,7 +461,7 @@ def main():
     ap.add_argument("--workdir", default=os.environ.get("DR_BENCH_DIR", os.path.join(tempfile.gettempdir(), "dr_bench")))
     args = ap.parse_args()
     if args.pmc_dir is None:
-        args.pmc_dir = os.path.join(ROOT, "profiles", "r03", "pmc", "c%d" % args.config)
+        args.pmc_dir = os.path.join(ROOT, "profiles", "r04", "pmc", "c%d" % args.config)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))

@@ -103,6 +103,16 @@ def test_filter_optimistic_txn_cases(engine, tmp_path, checkpoint):
     assert _gpu_selected(engine, lp2, preds2) == _oracle_selected(lp2, preds2)
 
 
+def test_filter_dictionary_overflow_falls_back(engine, tmp_path):
+    """A partition column with more distinct values than the u16 dictionary holds (70,000 > 65,534)
+    takes the typed leaf kernel; a low-cardinality column beside it still selects exactly."""
+    n = 70000
+    lp = _int_table(tmp_path / "hi", ["part", "g"], [(k, k % 7) for k in range(n)], checkpoint=False)
+    preds = [[(">=", C("part"), L("integer", 69990))], [("=", C("g"), L("integer", 3))],
+             [("and", ("<", C("part"), L("integer", 20)), ("=", C("g"), L("integer", 5)))]]
+    assert _gpu_selected(engine, lp, preds) == _oracle_selected(lp, preds)
+
+
 @pytest.mark.parametrize("kernel", ["dict", "typed"])
 def test_filter_config4_predicate(engine, tmp_path, monkeypatch, kernel):
     """p0 >= DATE'2020-03-01' AND p0 < DATE'2020-06-01' AND p1 IN (1..100)

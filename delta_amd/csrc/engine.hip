@@ -1532,6 +1532,10 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
       if (done) (void)hipEventDestroy(done);
     }
   } ov{ctx};
+  // a small commit-only segment (a streamed commit): the deferred lines and the canonicalisation
+  // run as one single-workgroup launch at the canonicalisation point (k_tail_post)
+  const bool tail_post = canonicalize && s.ck_rows == 0 && nlines && nlines <= JSON_TAIL_POST_MAX && !ctx->overlap;
+  JsonParseArgs ja{};
   if (nlines) {
     hipStream_t s2 = ctx->overlap ? ctx->stream2 : stream;
     if (ctx->overlap) {
@@ -1540,7 +1544,7 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
       HIP_OK(hipStreamWaitEvent(s2, ov.fork, 0));
     }
     if (!one_block) launch_json_place(s.d_json.p, json_len, jcounts.p, joff.p, jslots.p, nl.p, s2);
-    JsonParseArgs ja{s.d_json.p, nl.p, nlines, R, act.kind, act.flags, act.key, act.path_ptr, act.path_len,
+    ja = JsonParseArgs{s.d_json.p, nl.p, nlines, R, act.kind, act.flags, act.key, act.path_ptr, act.path_len,
                      act.size, act.delts, act.src_off, act.src_len, counters.p + 0, counters.p + 1, counters.p + 2,
                      nonfile.p, nlines, counters.p + 3, hard.p,
                      reinterpret_cast<unsigned long long*>(counters.p + 5)};
@@ -1561,7 +1565,7 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
       }
     }
     launch_json_parse(ja, s2);
-    launch_json_hard(ja, s2);
+    if (!tail_post) launch_json_hard(ja, s2);
     if (ctx->overlap) {
       HIP_OK(hipEventCreateWithFlags(&ov.done, hipEventDisableTiming));
       HIP_OK(hipEventRecord(ov.done, s2));
@@ -1639,7 +1643,10 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
       st->arenas.push_back(std::make_shared<DBuf<uint8_t>>(ctx, cap));
       pp.canon_arena = st->arenas.back()->p;
       CanonArgs cg{act, N, st->arenas.back()->p, cap, counters.p + 4};
-      launch_canon(cg, stream);
+      if (tail_post) launch_tail_post(ja, cg, stream);
+      else launch_canon(cg, stream);
+    } else if (tail_post) {
+      launch_json_hard(ja, stream);
     }
     pp.canon_cap = cap;
     pp.canonicalize = true;

@@ -8,10 +8,12 @@
 // with unwrap priority (D/actions/actions.scala:523-541), pulls add/remove path / size /
 // deletionTimestamp and hashes the path (K3's xxh64) while its bytes are in cache.
 #include <cstdlib>
+#include <type_traits>
 
 #include "dev_common.h"
 #include "kernels.h"
 #include "json_lane.h"
+#include "canon.h"
 
 namespace dr {
 namespace dev {
@@ -334,7 +336,7 @@ __device__ __forceinline__ int32_t from_lower(unsigned long long mask, int32_t v
 // The tape of the region [rb, rb + R) of the stage (R includes the last line's newline). Returns
 // true when every line of the wave is on it (wave-uniform); false sends the wave to the walker.
 __device__ __forceinline__ bool build_tape(const uint4* stage, uint32_t rb, uint32_t R, uint32_t nlines, uint32_t* tape,
-                           uint16_t* nltok) {
+                           uint16_t* nltok, uint8_t* tline) {
   const uint32_t lane = threadIdx.x;
   const uint32_t a0 = rb & ~15u;
   const uint32_t skew = rb - a0;
@@ -435,6 +437,7 @@ __device__ __forceinline__ bool build_tape(const uint4* stage, uint32_t rb, uint
       } else {
         tok = (pos << 16) | ((st & bit) ? scls : (sc_begin & bit) ? jl::T_SCALAR : T_NL);
       }
+      tline[idx] = uint8_t(nlr);
       if (nl & bit) nltok[nlr++] = uint16_t(idx);
       tape[idx++] = tok;
     }
@@ -445,45 +448,192 @@ __device__ __forceinline__ bool build_tape(const uint4* stage, uint32_t rb, uint
   return nlc == nlines;
 }
 
-// Lane i runs the DFA over line i's stretch of the tape (line bytes read from the stage at `sp`, the
-// region start) and emits its action; `gb` is the region's offset in the JSON buffer.
-__device__ __forceinline__ void dfa_tape(const JsonParseArgs& a, uint64_t line0, uint32_t nlines, const uint8_t* sp, uint64_t gb,
-                         const uint32_t* tape, const uint16_t* nltok) {
+// ---- the tape's grammar and extraction, wave-parallel over tokens -----------------------------------
+// A streamed commit has a handful of lines: walking each line's tokens in its own lane (the DFA of
+// json_lane.h) is a serial chain of ~40 dependent steps whose every step executes the union of the
+// lanes' branches (r04: 95K clocks of a 6-line commit's 115K). Here lane l takes token 64r + l of
+// the tape in round r, and everything the DFA derives from its state comes from wave scans instead:
+//  * the nesting depth before each token (a segmented prefix sum of +1 / -1, reset at each line's
+//    first token);
+//  * the kind of container open at that depth (a last-writer-wins scan over levels 1..7: an open at
+//    level L writes bit L; the last open at the token's level is the innermost open container,
+//    exactly as a stack would have it);
+//  * the latest object opened at level 2 (a max scan): a depth-2 member's enclosing top-level member.
+// Grammar is checked per token from its class, its two predecessors' classes and that container kind
+// (the JSON transitions the DFA encodes: a key follows '{' or an object's ',', ':' follows a key, a
+// value follows ':' or an array's '[' / ',', ',' and a close follow a value or their own open).
+// Extraction keeps the DFA's last-value-wins rules by keeping, per line, the LAST top-level member of
+// each action kind and the LAST path / size / deletionTimestamp member inside add / remove members
+// (LDS atomicMax on token index * 2 + non-null); a field index below its kind's last member belongs
+// to an earlier member and does not count. Anything the fast DFA would defer (an escaped key at depth
+// <= 2, nesting past the scanned levels) or reject (a grammar or typing error) sends the line to the
+// General walker (k_json_hard / k_tail_post), which decides every line exactly: the deferral needs no
+// K_ERROR logic here, and lines the tape accepts are decided as the DFA decides them.
+constexpr uint32_t TW_LEVELS = 7;  // container levels the type scan tracks (deeper: General walker)
+struct TapeAgg {
+  int32_t mem[JL_T][8];      // per line and action kind: last top-level member's value token * 2 + non-null
+  int32_t fld[JL_T][2][4];   // per line, add / remove: last path / size / deletionTimestamp value token * 2 + non-null
+  uint32_t defer[JL_T];
+};
+
+__device__ __forceinline__ uint32_t type_combine(uint32_t early, uint32_t late) {
+  const uint32_t lm = late & 0xFFu;
+  return ((early | late) & 0xFFu) | (((((early >> 8) & ~lm) | (late >> 8)) & 0xFFu) << 8);
+}
+
+// Scalar class of the tape's scalar token at index t (its run ends at the next token).
+__device__ __forceinline__ uint8_t tape_scalar(const uint32_t* tape, uint32_t t, const uint8_t* sp, int64_t* v) {
+  const uint32_t pos = tape[t] >> 16;
+  const uint32_t L = (tape[t + 1] >> 16) - pos;
+  if (L > jl::TOK_MAX_SCALAR) return jl::SC_BAD;
+  return jl::scalar_fast(sp + pos, L, v);
+}
+
+__device__ __forceinline__ void tape_lines(const JsonParseArgs& a, uint64_t line0, uint32_t nlines, const uint8_t* sp,
+                                           uint64_t gb, const uint32_t* tape, const uint16_t* nltok, const uint8_t* tline,
+                                           TapeAgg& g) {
   const uint32_t lane = threadIdx.x;
-  const bool live = lane < nlines;
-  const uint32_t te = live ? nltok[lane] : 0u;
-  const uint32_t ts = live && lane ? uint32_t(nltok[lane - 1]) + 1u : 0u;
-  const uint32_t ls = live && lane ? (tape[ts - 1] >> 16) + 1u : 0u;  // line start (region offset)
-  const uint32_t n = live ? (tape[te] >> 16) - ls : 0u;
-  const uint8_t* p = sp + ls;
-  const uint32_t cnt = te - ts;
-  uint32_t mx = cnt;
-  for (int o = 32; o > 0; o >>= 1) mx = max(mx, uint32_t(__shfl_xor(int(mx), o, 64)));
-  jl::Dfa<false> d;
-  jl::Tokenizer tz;
-  for (uint32_t t = 0; t < mx; ++t) {
-    if (t < cnt && d.status == jl::ST_OK) {
-      const uint32_t tok = tape[ts + t];
-      const uint32_t cls = tok & 0xFu, pos = tok >> 16;
-      uint32_t aux = (tok >> 4) & 0xFFFu;
-      if (cls == jl::T_SCALAR) {
-        aux = (tape[ts + t + 1] >> 16) - pos;  // the run ends where the next token begins
-        if (aux > jl::TOK_MAX_SCALAR) { d.status = jl::ST_BAD; continue; }
-      }
-      jl::dfa_token<false>(p, ((pos - ls) << 16) | (aux << 4) | cls, d);
-    }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    g.mem[lane][k] = -1;
+    g.fld[lane][k >> 2][k & 3] = -1;
   }
-  if (!live) return;
-  tz.sc_bytes = d.sc_checked;  // every scalar byte starts or continues a run the DFA validated
-  jl::LineOut o;
-  jl::dfa_finish<false>(tz, d, o);
+  g.defer[lane] = 0;
+  __syncthreads();
+  const uint32_t ntok = uint32_t(nltok[nlines - 1]) + 1u;
+  int32_t dcarry = 0, ocarry = -1;
+  uint32_t tcarry = 0;
+  for (uint32_t r0 = 0; r0 < ntok; r0 += JL_T) {
+    const uint32_t i = r0 + lane;
+    const bool in = i < ntok;
+    const uint32_t tok = in ? tape[i] : 0u;
+    const uint32_t cls = in ? (tok & 0xFu) : 15u;
+    const uint32_t pc0 = in && i > 0 ? (tape[i - 1] & 0xFu) : T_NL;
+    const bool first = pc0 == T_NL;  // the first token of its line
+    const uint32_t ppc0 = !first && i > 1 ? (tape[i - 2] & 0xFu) : T_NL;
+    const int32_t delta = cls <= jl::T_ARR_OPEN ? 1 : (cls == jl::T_OBJ_CLOSE || cls == jl::T_ARR_CLOSE) ? -1 : 0;
+    // depth after the token: segmented inclusive scan, lines restart at 0
+    int32_t v = delta;
+    uint32_t f = first ? 1u : 0u;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int32_t vv = __shfl_up(v, o, 64);
+      const uint32_t ff = uint32_t(__shfl_up(int(f), o, 64));
+      if (int(lane) >= o) {
+        if (!f) v += vv;
+        f |= ff;
+      }
+    }
+    if (!f) v += dcarry;
+    dcarry = __builtin_amdgcn_readlane(v, 63);
+    const int32_t D = v - delta;  // depth before the token
+    // container kinds by level: bit L of the low byte = level L opened, of the high byte = an array
+    const bool opens = delta > 0;
+    uint32_t x = opens && v <= int32_t(TW_LEVELS) ? ((1u << v) | (uint32_t(cls == jl::T_ARR_OPEN) << (8 + v))) : 0u;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = uint32_t(__shfl_up(int(x), o, 64));
+      if (int(lane) >= o) x = type_combine(y, x);
+    }
+    x = type_combine(tcarry, x);
+    tcarry = uint32_t(__builtin_amdgcn_readlane(int(x), 63));
+    // the latest object opened at level 2 (a top-level member's value)
+    int32_t o2 = opens && v == 2 ? int32_t(i) : -1;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int32_t y = __shfl_up(o2, o, 64);
+      if (int(lane) >= o) o2 = max(o2, y);
+    }
+    o2 = max(o2, ocarry);
+    ocarry = __builtin_amdgcn_readlane(o2, 63);
+    if (!in) continue;
+    const uint32_t line = tline[i];
+    const bool lvl = D >= 1 && D <= int32_t(TW_LEVELS) && ((x >> D) & 1u);
+    const bool ctx_arr = lvl && ((x >> (8 + D)) & 1u), ctx_obj = lvl && !ctx_arr;
+    const uint32_t pc = first ? 15u : pc0;  // 15: the line's start
+    const uint32_t ppc = (first || ppc0 == T_NL || i < 2) ? 15u : ppc0;
+    const bool is_str = cls == jl::T_STRING || cls == jl::T_STRING_ESC;
+    const bool pstr = pc == jl::T_STRING || pc == jl::T_STRING_ESC;
+    const bool prev_key = pstr && (ppc == jl::T_OBJ_OPEN || (ppc == jl::T_COMMA && ctx_obj));
+    const bool prev_vend = pc == jl::T_SCALAR || pc == jl::T_OBJ_CLOSE || pc == jl::T_ARR_CLOSE || (pstr && !prev_key);
+    const bool value_pos = pc == jl::T_COLON || (ctx_arr && (pc == jl::T_ARR_OPEN || pc == jl::T_COMMA));
+    const bool cur_key = is_str && (pc == jl::T_OBJ_OPEN || (pc == jl::T_COMMA && ctx_obj));
+    int64_t sv = 0;
+    uint8_t sc = jl::SC_BAD;
+    if (cls == jl::T_SCALAR) sc = tape_scalar(tape, i, sp, &sv);
+    bool ok;
+    if (cls == T_NL) ok = D == 0;
+    else if (pc == 15u) ok = cls == jl::T_OBJ_OPEN;
+    else if (D < 1) ok = false;
+    else if (opens) ok = value_pos && v <= int32_t(TW_LEVELS);
+    else if (cls == jl::T_SCALAR) ok = value_pos && sc != jl::SC_BAD;
+    else if (is_str) ok = (cur_key && !(cls == jl::T_STRING_ESC && D <= 2)) || value_pos;
+    else if (cls == jl::T_COLON) ok = prev_key;
+    else if (cls == jl::T_COMMA) ok = prev_vend;
+    else if (cls == jl::T_OBJ_CLOSE) ok = ctx_obj && (pc == jl::T_OBJ_OPEN || prev_vend);
+    else ok = ctx_arr && (pc == jl::T_ARR_OPEN || prev_vend);
+    if (ok && pc == jl::T_COLON && i >= 2 && (D == 1 || D == 2)) {  // a member's value; its key is tape[i - 2]
+      const bool nonnull = !(cls == jl::T_SCALAR && sc == jl::SC_NULL);
+      const int32_t rec = int32_t(2u * i) + (nonnull ? 1 : 0);
+      const uint32_t kt = tape[i - 2];
+      const uint8_t* kp = sp + (kt >> 16) + 1u;
+      const uint32_t kl = (kt >> 4) & 0xFFFu;
+      if (D == 1) {
+        const uint8_t k1 = jl::action_key_w(kp, kl);
+        if (k1) {
+          if ((k1 == jl::K_ADD || k1 == jl::K_REMOVE) && nonnull && cls != jl::T_OBJ_OPEN) ok = false;  // struct from a non-object
+          atomicMax(&g.mem[line][k1], rec);
+        }
+      } else if (o2 >= 2) {
+        const uint32_t jt = tape[o2 - 2];  // the enclosing top-level member's key
+        const uint8_t k1 = jl::action_key_w(sp + (jt >> 16) + 1u, (jt >> 4) & 0xFFFu);
+        if (k1 == jl::K_ADD || k1 == jl::K_REMOVE) {
+          const uint8_t k2 = jl::file_key_w(kp, kl);
+          if (k2 == jl::FK_PATH) ok = ok && (is_str || !nonnull);
+          else if (k2 != jl::FK_OTHER) ok = ok && cls == jl::T_SCALAR && (sc == jl::SC_NULL || sc == jl::SC_INT);
+          if (k2 != jl::FK_OTHER) atomicMax(&g.fld[line][k1 == jl::K_REMOVE ? 1 : 0][k2], rec);
+        }
+      }
+    }
+    if (!ok) g.defer[line] = 1u;
+  }
+  __syncthreads();
+  if (lane >= nlines) return;
   const uint64_t line = line0 + lane;
-  if (o.hard) {
+  const uint32_t te = nltok[lane];
+  const uint32_t ts = lane ? uint32_t(nltok[lane - 1]) + 1u : 0u;
+  const uint32_t ls = lane ? (tape[ts - 1] >> 16) + 1u : 0u;  // line start (region offset)
+  const uint32_t n = (tape[te] >> 16) - ls;
+  if (g.defer[lane]) {
     const unsigned long long k = atomicAdd(a.hard_count, 1ull);
     a.hard_idx[k] = line;
     return;
   }
-  emit_line(a, line, gb + ls, n, p, a.buf + gb + ls, o);
+  // unwrap priority add > remove > metaData > txn > protocol > cdc > commitInfo (json_lane.h dfa_finish)
+  jl::LineOut o{};
+  o.kind = jl::K_NONE;
+  const uint8_t order[7] = {jl::K_ADD, jl::K_REMOVE, jl::K_METADATA, jl::K_TXN, jl::K_PROTOCOL, jl::K_CDC, jl::K_COMMITINFO};
+#pragma unroll
+  for (int k = 6; k >= 0; --k)
+    if (g.mem[lane][order[k]] >= 0 && (g.mem[lane][order[k]] & 1)) o.kind = order[k];
+  if (o.kind == jl::K_ADD || o.kind == jl::K_REMOVE) {
+    const int32_t m = g.mem[lane][o.kind] >> 1;
+    const int32_t* fl = g.fld[lane][o.kind == jl::K_REMOVE ? 1 : 0];
+    o.flags = jl::F_PATH_NULL;
+    const int32_t tp = fl[jl::FK_PATH], tz = fl[jl::FK_SIZE], td = fl[jl::FK_DELTS];
+    if (tp >= 0 && (tp >> 1) > m && (tp & 1)) {
+      const uint32_t t = tape[tp >> 1];
+      o.path_off = (t >> 16) + 1u - ls;
+      o.path_len = (t >> 4) & 0xFFFu;
+      o.flags = (t & 0xFu) == jl::T_STRING_ESC ? jl::F_PATH_ESCAPED : 0;
+    }
+    if (tz >= 0 && (tz >> 1) > m && (tz & 1)) (void)tape_scalar(tape, uint32_t(tz >> 1), sp, &o.size);
+    if (td >= 0 && (td >> 1) > m && (td & 1)) {
+      (void)tape_scalar(tape, uint32_t(td >> 1), sp, &o.delts);
+      o.flags |= jl::F_HAS_DELTS;
+    }
+  }
+  emit_line(a, line, gb + ls, n, sp + ls, a.buf + gb + ls, o);
 }
 
 // 64 consecutive lines per block, one lane per line, two phases (json_lane.h):
@@ -499,6 +649,8 @@ __global__ void __launch_bounds__(JL_T, DR_JL_WAVES) k_json_lines(JsonParseArgs 
   __shared__ uint4 stage[Stage ? JL_STAGE_BYTES / 16 : 1];
   __shared__ uint32_t tape[Stage ? TAPE_CAP : 1];
   __shared__ uint16_t nltok[Stage ? JL_T : 1];
+  __shared__ uint8_t tline[Stage ? TAPE_CAP : 1];
+  __shared__ std::conditional_t<Stage, TapeAgg, uint32_t> agg;
   const uint32_t lane = threadIdx.x;
   const uint64_t line = uint64_t(blockIdx.x) * JL_T + lane;
   const bool live = line < a.nlines;
@@ -526,10 +678,11 @@ __global__ void __launch_bounds__(JL_T, DR_JL_WAVES) k_json_lines(JsonParseArgs 
       phase(0);
       const uint32_t nw = uint32_t(last - first + 1);
       const uint64_t rb = first == 0 ? 0 : a.nl[first - 1] + 1;  // the wave's first line
-      const bool taped = build_tape(stage, uint32_t(rb - r0), uint32_t(a.nl[last] + 1 - rb), nw, tape, nltok);
+      const bool taped = build_tape(stage, uint32_t(rb - r0), uint32_t(a.nl[last] + 1 - rb), nw, tape, nltok, tline);
       phase(1);
       if (taped) {
-        dfa_tape(a, first, nw, reinterpret_cast<const uint8_t*>(stage) + (rb - r0), rb, tape, nltok);
+        __syncthreads();
+        tape_lines(a, first, nw, reinterpret_cast<const uint8_t*>(stage) + (rb - r0), rb, tape, nltok, tline, agg);
         phase(2);
         if (a.phase && lane == 0) atomicAdd(&a.phase[4], 1ull);
         return;
@@ -563,6 +716,26 @@ __global__ void __launch_bounds__(64) k_json_hard(JsonParseArgs a) {
   }
 }
 
+// A small commit-only segment's work after the line walk, in one workgroup: the lines the fast
+// walker deferred (General walker), then the special paths' canonicalisation (k_canon's body) --
+// one launch instead of two for a streamed commit, whose kernels each cost a launch and a cold
+// start rather than their work.
+__global__ void __launch_bounds__(256) k_tail_post(JsonParseArgs a, CanonArgs c) {
+  const uint64_t cnt = *a.hard_count;
+  for (uint64_t k = threadIdx.x; k < cnt; k += blockDim.x) {
+    const uint64_t line = a.hard_idx[k];
+    const uint64_t b = line == 0 ? 0 : a.nl[line - 1] + 1;
+    const uint32_t n = uint32_t(a.nl[line] - b);
+    const uint8_t* gp = a.buf + b;
+    jl::LineOut o;
+    jl::parse_line_general(gp, n, o);
+    emit_line(a, line, b, n, gp, gp, o);
+  }
+  __threadfence_block();
+  __syncthreads();
+  for (uint64_t i = threadIdx.x; i < c.n; i += blockDim.x) canon_one(c, i);
+}
+
 }  // namespace dev
 
 // ---- launchers -----------------------------------------------------------------------------------
@@ -591,8 +764,13 @@ void launch_json_index1(const uint8_t* buf, uint64_t len, uint64_t* nl, uint64_t
 void launch_json_parse(const JsonParseArgs& a, hipStream_t st) {
   if (!a.nlines) return;
   const dim3 grid(unsigned((a.nlines + dev::JL_T - 1) / dev::JL_T));
-  if (a.nlines <= dev::JL_SMALL_LINES) DR_LAUNCH(dev::k_json_lines<true>, grid, dim3(dev::JL_T), 0, st, a);
+  // DR_JSON_STAGED=1 (tests): every segment through the staged kernel, 64 lines per workgroup
+  if (a.nlines <= dev::JL_SMALL_LINES || std::getenv("DR_JSON_STAGED")) DR_LAUNCH(dev::k_json_lines<true>, grid, dim3(dev::JL_T), 0, st, a);
   else DR_LAUNCH(dev::k_json_lines<false>, grid, dim3(dev::JL_T), 0, st, a);
+}
+
+void launch_tail_post(const JsonParseArgs& a, const CanonArgs& c, hipStream_t st) {
+  DR_LAUNCH(dev::k_tail_post, dim3(1), dim3(256), 0, st, a, c);
 }
 
 void launch_json_hard(const JsonParseArgs& a, hipStream_t st) {

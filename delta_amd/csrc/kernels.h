@@ -220,6 +220,9 @@ struct CanonArgs {
   uint64_t* arena_fill;
 };
 void launch_canon(const CanonArgs& a, hipStream_t st);
+// a commit-only segment of at most JSON_TAIL_POST_MAX actions: k_json_hard + k_canon in one workgroup
+constexpr uint64_t JSON_TAIL_POST_MAX = 256;
+void launch_tail_post(const JsonParseArgs& a, const CanonArgs& c, hipStream_t st);
 
 // ---- K3/K4: partition by hash bucket + per-bucket last-writer-wins ------------------------------
 // A partition record is 16 B: {xxh64(path) lo, hi, meta = action index << 2 | class, add.size when it

@@ -353,6 +353,15 @@ def test_noncontiguous_and_empty(engine, tmp_path):
 
 
 # ---- K1 device walker fuzz ---------------------------------------------------------------------------------
+def _walker_mode(monkeypatch, staged):
+    """staged: every 64-line wave through the small-segment kernel (LDS stage, token tape, the
+    wave-parallel tape walk) instead of the bulk per-lane walker."""
+    if staged:
+        monkeypatch.setenv("DR_JSON_STAGED", "1")
+    else:
+        monkeypatch.delenv("DR_JSON_STAGED", raising=False)
+
+
 def _device_lines(engine, lines):
     body = b"".join(l + b"\n" for l in lines)
     staged = engine.stage_files([(0, 0, 0, body)])
@@ -372,10 +381,12 @@ def _device_view(rec):
     return out
 
 
-def test_device_walker_matches_fuzz_corpus(engine):
+@pytest.mark.parametrize("staged", [False, True])
+def test_device_walker_matches_fuzz_corpus(engine, monkeypatch, staged):
     """Every corpus line (golden logs, synthetic formats, hand-written edge cases) at 16 byte
     alignments, through k_json_lines / k_json_hard on the GPU, against the PERMISSIVE-reader
     restatement that the host build of the walker is fuzzed against."""
+    _walker_mode(monkeypatch, staged)
     from tests.test_json_lane import corpus, expected
     base = [l for l in corpus() if b"\n" not in l]
     lines = []
@@ -389,7 +400,9 @@ def test_device_walker_matches_fuzz_corpus(engine):
         assert _device_view(rec) == expected(line), line
 
 
-def test_device_walker_mutations(engine):
+@pytest.mark.parametrize("staged", [False, True])
+def test_device_walker_mutations(engine, monkeypatch, staged):
+    _walker_mode(monkeypatch, staged)
     from tests.test_json_lane import K_ADD, K_ERROR, corpus, expected, mutate
     rng = random.Random(0xDE17B)
     base = corpus()
@@ -565,13 +578,15 @@ def _writer_clean(line: bytes) -> bool:
     return quotes % 2 == 0
 
 
-def test_device_walker_writer_shaped_waves(engine):
+@pytest.mark.parametrize("staged", [False, True])
+def test_device_walker_writer_shaped_waves(engine, monkeypatch, staged):
     """k_json_lines against the PERMISSIVE restatement on whole 64-line waves of writer-shaped
     lines (clean corpus lines and their clean mutations) at all 16 byte skews, with backslash runs
     and escaped quotes at every window offset, scalars of every length up to 19 digits, strings on
     both sides of the fast walker's 4096-byte single-token limit and nesting past its depth limit
     (the General walker's deferral), followed by unrestricted mutations. (The same test checked the
     r02 wave-cooperative tokenizer experiment)"""
+    _walker_mode(monkeypatch, staged)
     from tests.test_json_lane import corpus, expected, mutate
     base = [l for l in corpus() if b"\n" not in l]
     rng = random.Random(0x7A9E)

@@ -1552,16 +1552,17 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
     static uint64_t phase_calls = 0;
     if (std::getenv("DR_JSON_PHASES")) {
       if (!phase) {
-        HIP_OK(hipMalloc(&phase, 5 * sizeof(unsigned long long)));
-        HIP_OK(hipMemset(phase, 0, 5 * sizeof(unsigned long long)));
+        HIP_OK(hipMalloc(&phase, 8 * sizeof(unsigned long long)));
+        HIP_OK(hipMemset(phase, 0, 8 * sizeof(unsigned long long)));
       }
       ja.phase = phase;
       if (++phase_calls % 200 == 0) {
-        unsigned long long h[5];
+        unsigned long long h[8];
         HIP_OK(hipMemcpy(h, phase, sizeof(h), hipMemcpyDeviceToHost));
         if (h[4])
-          std::fprintf(stderr, "k_json_lines<true> clocks per wave: stage %.0f tape %.0f dfa %.0f (%llu waves)\n",
-                       double(h[0]) / double(h[4]), double(h[1]) / double(h[4]), double(h[2]) / double(h[4]), h[4]);
+          std::fprintf(stderr, "k_json_lines<true> clocks per wave: stage %.0f tape %.0f walk %.0f (rounds %.0f, first round %.0f) (%llu waves)\n",
+                       double(h[0]) / double(h[4]), double(h[1]) / double(h[4]), double(h[2]) / double(h[4]),
+                       double(h[3]) / double(h[4]), double(h[5]) / double(h[4]), h[4]);
       }
     }
     launch_json_parse(ja, s2);

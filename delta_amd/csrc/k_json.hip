@@ -14,6 +14,7 @@
 #include "kernels.h"
 #include "json_lane.h"
 #include "canon.h"
+#include "wave.h"
 
 namespace dr {
 namespace dev {
@@ -325,12 +326,14 @@ __device__ __forceinline__ uint32_t escape16(uint32_t bs, uint32_t cin, uint32_t
 
 __device__ __forceinline__ uint64_t lanes_below() { return (1ull << threadIdx.x) - 1ull; }
 
-// Value of `v` in the highest lane of `mask` below this lane, or `dflt` when there is none.
-__device__ __forceinline__ int32_t from_lower(unsigned long long mask, int32_t v, int32_t dflt) {
-  const unsigned long long lower = mask & lanes_below();
-  const int src = lower ? 63 - __clzll(lower) : int(threadIdx.x);
-  const int32_t got = __shfl(v, src, 64);
-  return lower ? got : dflt;
+// Value of `v` in the highest lane below this one whose `has` is set, or `dflt` when there is none
+// (an exclusive last-writer scan on DPP).
+__device__ __forceinline__ int32_t from_lower(bool has, int32_t v, int32_t dflt) {
+  constexpr uint32_t NONE = 0x80000000u;
+  uint32_t x = has ? uint32_t(v) : NONE;
+  x = wv::scan_incl(x, NONE, [](uint32_t e, uint32_t l) { return l == NONE ? e : l; });
+  x = wv::shr1(x, NONE);
+  return x == NONE ? dflt : int32_t(x);
 }
 
 // The tape of the region [rb, rb + R) of the stage (R includes the last line's newline). Returns
@@ -369,8 +372,7 @@ __device__ __forceinline__ bool build_tape(const uint4* stage, uint32_t rb, uint
     uint32_t c0;
     escape16(m.bs, 0u, &c0);
     const bool allbs = m.bs == 0xFFFFu;
-    const unsigned long long decided = __ballot(!allbs);
-    const uint32_t cin = uint32_t(from_lower(decided, int32_t(c0), int32_t(esc_c)));
+    const uint32_t cin = uint32_t(from_lower(!allbs, int32_t(c0), int32_t(esc_c)));
     uint32_t cout;
     const uint32_t escaped = (m.bs | cin) ? escape16(m.bs, cin, &cout) : (cout = 0, 0u);
     esc_c = uint32_t(__builtin_amdgcn_readlane(int(allbs ? cin : cout), 63));
@@ -390,27 +392,22 @@ __device__ __forceinline__ bool build_tape(const uint4* stage, uint32_t rb, uint
     }
     const uint32_t st = m.st & ~instr;
     const uint32_t sc = valid & ~instr & ~quote & ~st & ~m.sp & ~m.ctrl;
-    const uint32_t sc_prev = uint32_t(__shfl_up(int(sc >> 15), 1, 64)) & 1u;
-    const uint32_t sc_begin = sc & ~(((sc << 1) | (lane ? sc_prev : sc_c)) & 0xFFFFu);
+    const uint32_t sc_prev = wv::shr1(sc >> 15, sc_c) & 1u;
+    const uint32_t sc_begin = sc & ~(((sc << 1) | sc_prev) & 0xFFFFu);
     sc_c = uint32_t(__builtin_amdgcn_readlane(int(sc >> 15), 63)) & 1u;
     const uint32_t open = quote & instr, close = quote & ~instr;
     const uint32_t bsin = m.bs & instr;
     // latest opening quote / in-string backslash before this window
     const int32_t last_open = open ? lo + 31 - __builtin_clz(open) : -1;
     const int32_t last_bs = bsin ? lo + 31 - __builtin_clz(bsin) : -1;
-    const int32_t open_in = from_lower(__ballot(open != 0), last_open, open_c);
-    const int32_t bs_in = from_lower(__ballot(bsin != 0), last_bs, bs_c);
+    const int32_t open_in = from_lower(open != 0, last_open, open_c);
+    const int32_t bs_in = from_lower(bsin != 0, last_bs, bs_c);
     open_c = __builtin_amdgcn_readlane(open ? last_open : open_in, 63);
     bs_c = __builtin_amdgcn_readlane(bsin ? last_bs : bs_in, 63);
     const uint32_t tm = st | close | sc_begin | nl;
     // token and newline ranks: one wave scan of both counts (16-bit halves)
     const uint32_t cnt = uint32_t(__builtin_popcount(tm)) | (uint32_t(__builtin_popcount(nl)) << 16);
-    uint32_t incl = cnt;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t t = uint32_t(__shfl_up(int(incl), o, 64));
-      if (int(lane) >= o) incl += t;
-    }
+    const uint32_t incl = wv::scan_incl(cnt, 0u, [](uint32_t e, uint32_t l) { return e + l; });
     const uint32_t tot = uint32_t(__builtin_amdgcn_readlane(int(incl), 63));
     if (__ballot(bad)) return false;
     if (tbase + (tot & 0xFFFFu) > TAPE_CAP || nlc + (tot >> 16) > uint32_t(JL_T)) return false;
@@ -481,18 +478,77 @@ __device__ __forceinline__ uint32_t type_combine(uint32_t early, uint32_t late) 
   return ((early | late) & 0xFFu) | (((((early >> 8) & ~lm) | (late >> 8)) & 0xFFu) << 8);
 }
 
-// Scalar class of the tape's scalar token at index t (its run ends at the next token).
-__device__ __forceinline__ uint8_t tape_scalar(const uint32_t* tape, uint32_t t, const uint8_t* sp, int64_t* v) {
-  const uint32_t pos = tape[t] >> 16;
-  const uint32_t L = (tape[t + 1] >> 16) - pos;
-  if (L > jl::TOK_MAX_SCALAR) return jl::SC_BAD;
-  return jl::scalar_fast(sp + pos, L, v);
+// Branch-free token helpers of the tape walk: a wave executes every branch any of its lanes takes,
+// so the walk computes the key and scalar classes of every lane with selects from one 20-byte load
+// each. A scalar that is not null / true / false or a plain integer of at most 19 digits (a fraction,
+// an exponent, 20+ characters) is reported as SC_BAD: its line goes to the General walker, which
+// decides it.
+// 20 bytes at s (in the LDS stage) as little-endian words: six dword reads from the dword below s
+// and byte funnel shifts (a select over the 16-byte phase of s compiles to a branch tree)
+__device__ __forceinline__ void lds20(const uint8_t* s, uint32_t w[5]) {
+  const uint32_t r = uint32_t(reinterpret_cast<uintptr_t>(s)) & 3u;
+  const uint32_t* b = reinterpret_cast<const uint32_t*>(s - r);
+  uint32_t u[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) u[k] = b[k];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) w[k] = __builtin_amdgcn_alignbyte(u[k + 1], u[k], r);
+}
+
+// action kind (low nibble) and file-field key (high nibble) of a member name of n bytes
+__device__ __forceinline__ uint32_t key_kinds(const uint32_t w[5], uint32_t n) {
+  const uint32_t a = w[0], b = w[1], c = w[2], t = a & 0xFFFFFFu;
+  const uint32_t k3 = t == 0x646461u ? jl::K_ADD : t == 0x6E7874u ? jl::K_TXN : t == 0x636463u ? jl::K_CDC : 0u;
+  const uint32_t k6 = (a == 0x6F6D6572u && (b & 0xFFFFu) == 0x6576u) ? jl::K_REMOVE : 0u;
+  const uint32_t k8 = (a == 0x6174656Du && b == 0x61746144u) ? jl::K_METADATA
+                    : (a == 0x746F7270u && b == 0x6C6F636Fu) ? jl::K_PROTOCOL : 0u;
+  const uint32_t k10 = (a == 0x6D6D6F63u && b == 0x6E497469u && (c & 0xFFFFu) == 0x6F66u) ? jl::K_COMMITINFO : 0u;
+  const uint32_t k1 = n == 3 ? k3 : n == 6 ? k6 : n == 8 ? k8 : n == 10 ? k10 : 0u;
+  const uint32_t f4 = a == 0x68746170u ? jl::FK_PATH : a == 0x657A6973u ? jl::FK_SIZE : jl::FK_OTHER;
+  const uint32_t f17 = (a == 0x656C6564u && b == 0x6E6F6974u && c == 0x656D6954u && w[3] == 0x6D617473u &&
+                        (w[4] & 0xFFu) == 0x70u) ? jl::FK_DELTS : jl::FK_OTHER;
+  const uint32_t k2 = n == 4 ? f4 : n == 17 ? f17 : jl::FK_OTHER;
+  return k1 | (k2 << 4);
+}
+
+__device__ __forceinline__ uint8_t scalar_tape(const uint32_t w0[5], uint32_t L, int64_t* val) {
+  uint32_t w[5];
+  const bool neg = (w0[0] & 0xFFu) == 0x2Du;
+#pragma unroll
+  for (int d = 0; d < 5; ++d) w[d] = neg ? ((w0[d] >> 8) | (d < 4 ? (w0[d + 1] << 24) : 0u)) : w0[d];
+  uint32_t dm = 0;
+#pragma unroll
+  for (int d = 0; d < 5; ++d) dm |= jl::gather4(jl::digit_bytes(w[d])) << (4 * d);
+  const uint32_t nd = L - (neg ? 1u : 0u);
+  const uint32_t need = nd >= 20 ? 0xFFFFFu : (1u << nd) - 1u;
+  const bool isint = (L <= 20) & (nd >= 1) & (nd <= 19) & ((dm & need) == need) & !((nd > 1) & ((w[0] & 0xFFu) == 0x30u));
+  const uint32_t g = nd >> 2, r = nd & 3u;
+  uint64_t v = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) {
+    const uint64_t nv = v * 10000ull + jl::digits4(w[k]);
+    v = k < g ? nv : v;
+  }
+  uint32_t x = 0;  // w[g], as masks (a select chain on g compiles to a branch tree)
+#pragma unroll
+  for (uint32_t k = 0; k < 5; ++k) x |= w[k] & (0u - uint32_t(g == k));
+  const uint32_t sh = 8u * (4u - r);
+  const uint64_t rv = v * (r == 1 ? 10ull : r == 2 ? 100ull : 1000ull) +
+                      jl::digits4((x << (sh & 31u)) | (0x30303030u >> ((32u - sh) & 31u)));
+  v = r ? rv : v;
+  const bool fits = v <= (neg ? 0x8000000000000000ull : 0x7FFFFFFFFFFFFFFFull);
+  *val = neg ? int64_t(0ull - v) : int64_t(v);
+  return (L == 4 && w0[0] == 0x6C6C756Eu) ? jl::SC_NULL
+       : (L == 4 && w0[0] == 0x65757274u) ? jl::SC_TRUE
+       : (L == 5 && w0[0] == 0x736C6166u && (w0[1] & 0xFFu) == 0x65u) ? jl::SC_FALSE
+       : (isint && fits) ? jl::SC_INT : jl::SC_BAD;
 }
 
 __device__ __forceinline__ void tape_lines(const JsonParseArgs& a, uint64_t line0, uint32_t nlines, const uint8_t* sp,
                                            uint64_t gb, const uint32_t* tape, const uint16_t* nltok, const uint8_t* tline,
                                            TapeAgg& g) {
   const uint32_t lane = threadIdx.x;
+  const uint64_t tw0 = a.phase ? __builtin_amdgcn_s_memtime() : 0;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     g.mem[lane][k] = -1;
@@ -502,102 +558,93 @@ __device__ __forceinline__ void tape_lines(const JsonParseArgs& a, uint64_t line
   __syncthreads();
   const uint32_t ntok = uint32_t(nltok[nlines - 1]) + 1u;
   int32_t dcarry = 0, ocarry = -1;
-  uint32_t tcarry = 0;
+  uint32_t tcarry = 0, ptail1 = T_NL, ptail2 = T_NL;  // the previous round's last two tokens
   for (uint32_t r0 = 0; r0 < ntok; r0 += JL_T) {
     const uint32_t i = r0 + lane;
     const bool in = i < ntok;
-    const uint32_t tok = in ? tape[i] : 0u;
-    const uint32_t cls = in ? (tok & 0xFu) : 15u;
-    const uint32_t pc0 = in && i > 0 ? (tape[i - 1] & 0xFu) : T_NL;
+    // unconditional reads (clamped into the arrays): a guarded LDS read is a branch
+    const uint32_t tk = tape[min(i, TAPE_CAP - 1)], nx = tape[min(i + 1, TAPE_CAP - 1)];
+    const uint32_t tl = tline[min(i, TAPE_CAP - 1)];
+    const uint32_t tok = in ? tk : 15u;
+    const uint32_t nxt = i + 1 < ntok ? nx : tok;
+    const uint32_t line = in ? tl : 0u;
+    const uint32_t ptok = wv::shr1(tok, ptail1), pptok = wv::shr1(ptok, ptail2);
+    ptail1 = wv::last_uniform(tok);
+    ptail2 = wv::last_uniform(ptok);
+    // the token's bytes (a scalar's) and its key's (the string two tokens back), one load each
+    uint32_t sw[5], kw[5];
+    lds20(sp + (tok >> 16), sw);
+    lds20(sp + (pptok >> 16) + 1u, kw);
+    const uint32_t cls = tok & 0xFu;
+    const uint32_t pc0 = ptok & 0xFu;
     const bool first = pc0 == T_NL;  // the first token of its line
-    const uint32_t ppc0 = !first && i > 1 ? (tape[i - 2] & 0xFu) : T_NL;
+    const uint32_t ppc0 = pptok & 0xFu;
     const int32_t delta = cls <= jl::T_ARR_OPEN ? 1 : (cls == jl::T_OBJ_CLOSE || cls == jl::T_ARR_CLOSE) ? -1 : 0;
-    // depth after the token: segmented inclusive scan, lines restart at 0
-    int32_t v = delta;
-    uint32_t f = first ? 1u : 0u;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int32_t vv = __shfl_up(v, o, 64);
-      const uint32_t ff = uint32_t(__shfl_up(int(f), o, 64));
-      if (int(lane) >= o) {
-        if (!f) v += vv;
-        f |= ff;
-      }
-    }
-    if (!f) v += dcarry;
+    const uint32_t kk = key_kinds(kw, (pptok >> 4) & 0xFFFu);
+    const uint32_t k1 = kk & 0xFu, k2 = kk >> 4;
+    // depth after the token: segmented inclusive scan (flag in bit 31: a line's first token), lines
+    // restart at 0
+    uint32_t sg = (first ? 0x80000000u : 0u) | (uint32_t(delta) & 0x7FFFFFFFu);
+    sg = wv::scan_incl(sg, 0u, [](uint32_t e, uint32_t l) {
+      return (l & 0x80000000u) ? l : ((e & 0x80000000u) | ((e + l) & 0x7FFFFFFFu));
+    });
+    int32_t v = int32_t(sg << 1) >> 1;
+    if (!(sg & 0x80000000u)) v += dcarry;
     dcarry = __builtin_amdgcn_readlane(v, 63);
     const int32_t D = v - delta;  // depth before the token
     // container kinds by level: bit L of the low byte = level L opened, of the high byte = an array
     const bool opens = delta > 0;
     uint32_t x = opens && v <= int32_t(TW_LEVELS) ? ((1u << v) | (uint32_t(cls == jl::T_ARR_OPEN) << (8 + v))) : 0u;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = uint32_t(__shfl_up(int(x), o, 64));
-      if (int(lane) >= o) x = type_combine(y, x);
-    }
-    x = type_combine(tcarry, x);
-    tcarry = uint32_t(__builtin_amdgcn_readlane(int(x), 63));
-    // the latest object opened at level 2 (a top-level member's value)
-    int32_t o2 = opens && v == 2 ? int32_t(i) : -1;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int32_t y = __shfl_up(o2, o, 64);
-      if (int(lane) >= o) o2 = max(o2, y);
-    }
+    x = type_combine(tcarry, wv::scan_incl(x, 0u, type_combine));
+    tcarry = wv::last_uniform(x);
+    // the latest container opened at level 2 (a top-level member's value) with its member's action
+    // kind: index * 8 + kind, a max scan
+    const bool m2open = opens && v == 2 && pc0 == jl::T_COLON;
+    int32_t o2 = int32_t(wv::scan_incl(m2open ? (i << 3) | k1 : 0xFFFFFFFFu, 0xFFFFFFFFu,
+                                       [](uint32_t e, uint32_t l) { return uint32_t(max(int32_t(e), int32_t(l))); }));
     o2 = max(o2, ocarry);
     ocarry = __builtin_amdgcn_readlane(o2, 63);
-    if (!in) continue;
-    const uint32_t line = tline[i];
     const bool lvl = D >= 1 && D <= int32_t(TW_LEVELS) && ((x >> D) & 1u);
     const bool ctx_arr = lvl && ((x >> (8 + D)) & 1u), ctx_obj = lvl && !ctx_arr;
-    const uint32_t pc = first ? 15u : pc0;  // 15: the line's start
-    const uint32_t ppc = (first || ppc0 == T_NL || i < 2) ? 15u : ppc0;
+    const uint32_t ppc = (first || ppc0 == T_NL) ? 15u : ppc0;  // 15: the line's start
     const bool is_str = cls == jl::T_STRING || cls == jl::T_STRING_ESC;
-    const bool pstr = pc == jl::T_STRING || pc == jl::T_STRING_ESC;
+    const bool is_sc = cls == jl::T_SCALAR;
+    const bool pstr = pc0 == jl::T_STRING || pc0 == jl::T_STRING_ESC;
     const bool prev_key = pstr && (ppc == jl::T_OBJ_OPEN || (ppc == jl::T_COMMA && ctx_obj));
-    const bool prev_vend = pc == jl::T_SCALAR || pc == jl::T_OBJ_CLOSE || pc == jl::T_ARR_CLOSE || (pstr && !prev_key);
-    const bool value_pos = pc == jl::T_COLON || (ctx_arr && (pc == jl::T_ARR_OPEN || pc == jl::T_COMMA));
-    const bool cur_key = is_str && (pc == jl::T_OBJ_OPEN || (pc == jl::T_COMMA && ctx_obj));
-    int64_t sv = 0;
-    uint8_t sc = jl::SC_BAD;
-    if (cls == jl::T_SCALAR) sc = tape_scalar(tape, i, sp, &sv);
-    bool ok;
-    if (cls == T_NL) ok = D == 0;
-    else if (pc == 15u) ok = cls == jl::T_OBJ_OPEN;
-    else if (D < 1) ok = false;
-    else if (opens) ok = value_pos && v <= int32_t(TW_LEVELS);
-    else if (cls == jl::T_SCALAR) ok = value_pos && sc != jl::SC_BAD;
-    else if (is_str) ok = (cur_key && !(cls == jl::T_STRING_ESC && D <= 2)) || value_pos;
-    else if (cls == jl::T_COLON) ok = prev_key;
-    else if (cls == jl::T_COMMA) ok = prev_vend;
-    else if (cls == jl::T_OBJ_CLOSE) ok = ctx_obj && (pc == jl::T_OBJ_OPEN || prev_vend);
-    else ok = ctx_arr && (pc == jl::T_ARR_OPEN || prev_vend);
-    if (ok && pc == jl::T_COLON && i >= 2 && (D == 1 || D == 2)) {  // a member's value; its key is tape[i - 2]
-      const bool nonnull = !(cls == jl::T_SCALAR && sc == jl::SC_NULL);
-      const int32_t rec = int32_t(2u * i) + (nonnull ? 1 : 0);
-      const uint32_t kt = tape[i - 2];
-      const uint8_t* kp = sp + (kt >> 16) + 1u;
-      const uint32_t kl = (kt >> 4) & 0xFFFu;
-      if (D == 1) {
-        const uint8_t k1 = jl::action_key_w(kp, kl);
-        if (k1) {
-          if ((k1 == jl::K_ADD || k1 == jl::K_REMOVE) && nonnull && cls != jl::T_OBJ_OPEN) ok = false;  // struct from a non-object
-          atomicMax(&g.mem[line][k1], rec);
-        }
-      } else if (o2 >= 2) {
-        const uint32_t jt = tape[o2 - 2];  // the enclosing top-level member's key
-        const uint8_t k1 = jl::action_key_w(sp + (jt >> 16) + 1u, (jt >> 4) & 0xFFFu);
-        if (k1 == jl::K_ADD || k1 == jl::K_REMOVE) {
-          const uint8_t k2 = jl::file_key_w(kp, kl);
-          if (k2 == jl::FK_PATH) ok = ok && (is_str || !nonnull);
-          else if (k2 != jl::FK_OTHER) ok = ok && cls == jl::T_SCALAR && (sc == jl::SC_NULL || sc == jl::SC_INT);
-          if (k2 != jl::FK_OTHER) atomicMax(&g.fld[line][k1 == jl::K_REMOVE ? 1 : 0][k2], rec);
-        }
-      }
-    }
-    if (!ok) g.defer[line] = 1u;
+    const bool prev_vend = pc0 == jl::T_SCALAR || pc0 == jl::T_OBJ_CLOSE || pc0 == jl::T_ARR_CLOSE || (pstr && !prev_key);
+    const bool value_pos = pc0 == jl::T_COLON || (ctx_arr && (pc0 == jl::T_ARR_OPEN || pc0 == jl::T_COMMA));
+    const bool cur_key = is_str && (pc0 == jl::T_OBJ_OPEN || (pc0 == jl::T_COMMA && ctx_obj));
+    int64_t sv;
+    const uint32_t L = (nxt >> 16) - (tok >> 16);
+    const uint8_t sc = scalar_tape(sw, L, &sv);
+    // the classes are disjoint: one term holds (bitwise, so that nothing compiles to a branch)
+    const bool is_nl = cls == T_NL;
+    const bool inner = !is_nl & !first & (D >= 1);
+    const bool okv = (is_nl & (D == 0)) | (!is_nl & first & (cls == jl::T_OBJ_OPEN)) |
+                     (inner & ((opens & value_pos & (v <= int32_t(TW_LEVELS))) |
+                               (is_sc & value_pos & (sc != jl::SC_BAD)) |
+                               (is_str & ((cur_key & !((cls == jl::T_STRING_ESC) & (D <= 2))) | value_pos)) |
+                               ((cls == jl::T_COLON) & prev_key) | ((cls == jl::T_COMMA) & prev_vend) |
+                               ((cls == jl::T_OBJ_CLOSE) & ctx_obj & ((pc0 == jl::T_OBJ_OPEN) | prev_vend)) |
+                               ((cls == jl::T_ARR_CLOSE) & ctx_arr & ((pc0 == jl::T_ARR_OPEN) | prev_vend))));
+    // a member's value (its key is pptok): top-level members by action kind, add / remove fields
+    const bool member = in & !first & (pc0 == jl::T_COLON);
+    const bool nonnull = !(is_sc & (sc == jl::SC_NULL));
+    const int32_t rec = int32_t(2u * i) + (nonnull ? 1 : 0);
+    const uint32_t ek1 = uint32_t(o2) & (o2 >= 0 ? 7u : 0u);
+    const bool file1 = (k1 == jl::K_ADD) | (k1 == jl::K_REMOVE), efile = (ek1 == jl::K_ADD) | (ek1 == jl::K_REMOVE);
+    const bool m1 = member & (D == 1) & (k1 != 0);
+    const bool mf = member & (D == 2) & efile & (k2 != jl::FK_OTHER);
+    const bool bad1 = m1 & file1 & nonnull & (cls != jl::T_OBJ_OPEN);
+    const bool path_ok = is_str | !nonnull, num_ok = is_sc & ((sc == jl::SC_NULL) | (sc == jl::SC_INT));
+    const bool badf = mf & !((k2 == jl::FK_PATH) ? path_ok : num_ok);
+    if (m1) atomicMax(&g.mem[line][k1], rec);
+    if (mf) atomicMax(&g.fld[line][ek1 == jl::K_REMOVE ? 1 : 0][k2], rec);
+    if (in & !(okv & !bad1 & !badf)) g.defer[line] = 1u;
+    if (a.phase && r0 == 0 && lane == 0) atomicAdd(&a.phase[5], (unsigned long long)(__builtin_amdgcn_s_memtime() - tw0));
   }
   __syncthreads();
+  if (a.phase && lane == 0) atomicAdd(&a.phase[3], (unsigned long long)(__builtin_amdgcn_s_memtime() - tw0));
   if (lane >= nlines) return;
   const uint64_t line = line0 + lane;
   const uint32_t te = nltok[lane];
@@ -627,11 +674,19 @@ __device__ __forceinline__ void tape_lines(const JsonParseArgs& a, uint64_t line
       o.path_len = (t >> 4) & 0xFFFu;
       o.flags = (t & 0xFu) == jl::T_STRING_ESC ? jl::F_PATH_ESCAPED : 0;
     }
-    if (tz >= 0 && (tz >> 1) > m && (tz & 1)) (void)tape_scalar(tape, uint32_t(tz >> 1), sp, &o.size);
-    if (td >= 0 && (td >> 1) > m && (td & 1)) {
-      (void)tape_scalar(tape, uint32_t(td >> 1), sp, &o.delts);
-      o.flags |= jl::F_HAS_DELTS;
-    }
+    // size / deletionTimestamp: both tokens' words in one pass (an absent field reads token 0)
+    const bool hz = tz >= 0 && (tz >> 1) > m && (tz & 1), hd = td >= 0 && (td >> 1) > m && (td & 1);
+    const uint32_t iz = hz ? uint32_t(tz >> 1) : 0u, id = hd ? uint32_t(td >> 1) : 0u;
+    const uint32_t az = tape[iz], bz = tape[iz + 1], ad = tape[id], bd = tape[id + 1];
+    uint32_t wz[5], wd[5];
+    lds20(sp + (az >> 16), wz);
+    lds20(sp + (ad >> 16), wd);
+    int64_t vz, vd;
+    (void)scalar_tape(wz, (bz >> 16) - (az >> 16), &vz);
+    (void)scalar_tape(wd, (bd >> 16) - (ad >> 16), &vd);
+    o.size = hz ? vz : 0;
+    o.delts = hd ? vd : 0;
+    if (hd) o.flags |= jl::F_HAS_DELTS;
   }
   emit_line(a, line, gb + ls, n, sp + ls, a.buf + gb + ls, o);
 }

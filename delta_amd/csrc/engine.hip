@@ -107,8 +107,16 @@ struct dr_ctx {
         fail(DR_E_OOM, "pinned readback words");
       }
       hpin = static_cast<uint64_t*>(p);
+      void* d = nullptr;
+      HIP_OK(hipHostGetDevicePointer(&d, p, 0));
+      hpin_dev = static_cast<uint64_t*>(d);
     }
     return hpin;
+  }
+  uint64_t* hpin_dev = nullptr;  // the same words as a kernel writes them (launch_readback)
+  uint64_t* pinned_dev() {
+    (void)pinned();
+    return hpin_dev;
   }
 
   void* alloc(size_t n) {
@@ -1493,8 +1501,11 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
   DBuf<uint64_t> nl(ctx, nlines);
   DBuf<uint64_t> counters(ctx, 8);  // 0 special count, 1 special bytes, 2 nonfile count, 3 errors, 4 canon fill,
                                      // 5 lines deferred to the General walker, 7 checkpoint decode error
+  // a segment of one wave: the parse kernel indexes its newlines and clears the counters itself
+  const bool fuse1 = one_block && s.json_lines && s.json_lines <= JSON_FUSE_MAX_LINES && !ctx->overlap &&
+                     !std::getenv("DR_CHECK_LINES");
   if (one_block) {
-    launch_json_index1(s.d_json.p, json_len, nl.p, joff.p, counters.p, 8, stream);
+    if (!fuse1) launch_json_index1(s.d_json.p, json_len, nl.p, joff.p, counters.p, 8, stream);
   } else {
     counters.zero(stream);
     if (nbj) {
@@ -1548,6 +1559,13 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
                      act.size, act.delts, act.src_off, act.src_len, counters.p + 0, counters.p + 1, counters.p + 2,
                      nonfile.p, nlines, counters.p + 3, hard.p,
                      reinterpret_cast<unsigned long long*>(counters.p + 5)};
+    ja.buf_len = json_len;
+    if (fuse1) {
+      ja.zero = counters.p;
+      ja.nzero = 8;
+      ja.off2 = joff.p;
+      ja.nl_out = nl.p;
+    }
     static unsigned long long* phase = nullptr;  // DR_JSON_PHASES=1: staged-kernel phase clocks
     static uint64_t phase_calls = 0;
     if (std::getenv("DR_JSON_PHASES")) {
@@ -1560,9 +1578,10 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
         unsigned long long h[8];
         HIP_OK(hipMemcpy(h, phase, sizeof(h), hipMemcpyDeviceToHost));
         if (h[4])
-          std::fprintf(stderr, "k_json_lines<true> clocks per wave: stage %.0f tape %.0f walk %.0f (rounds %.0f, first round %.0f) (%llu waves)\n",
+          std::fprintf(stderr, "k_json_lines<true> clocks per wave: stage %.0f tape %.0f walk %.0f (rounds %.0f, first round %.0f; tape scan %.0f emit %.0f) (%llu waves)\n",
                        double(h[0]) / double(h[4]), double(h[1]) / double(h[4]), double(h[2]) / double(h[4]),
-                       double(h[3]) / double(h[4]), double(h[5]) / double(h[4]), h[4]);
+                       double(h[3]) / double(h[4]), double(h[5]) / double(h[4]), double(h[6]) / double(h[4]),
+                       double(h[7]) / double(h[4]), h[4]);
       }
     }
     launch_json_parse(ja, s2);
@@ -1661,12 +1680,20 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
 
 // Queues the copies of parse_launch's counters and the first non-file entries into the pinned
 // words at `at` (no sync).
-static size_t parse_queue_readback(dr_ctx* ctx, ParsePending& pp, size_t at) {
+// With `rb`, the spans are added to a launch_readback instead of queued as copies.
+static size_t parse_queue_readback(dr_ctx* ctx, ParsePending& pp, size_t at, ReadbackArgs* rb = nullptr,
+                                   int* nrb = nullptr) {
   uint64_t* h = ctx->pinned() + at;
   pp.pin_at = at;
-  HIP_OK(hipMemcpyAsync(h, pp.counters.p, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
   const uint64_t k = std::min<uint64_t>(pp.nlines, kPinNonfile);
-  if (k) HIP_OK(hipMemcpyAsync(h + 8, pp.nonfile.p, 2 * k * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
+  if (rb) {
+    uint64_t* d = ctx->pinned_dev() + at;
+    rb->src[*nrb] = pp.counters.p, rb->dst[*nrb] = d, rb->n[(*nrb)++] = 8;
+    if (k) rb->src[*nrb] = pp.nonfile.p, rb->dst[*nrb] = d + 8, rb->n[(*nrb)++] = uint32_t(2 * k);
+  } else {
+    HIP_OK(hipMemcpyAsync(h, pp.counters.p, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
+    if (k) HIP_OK(hipMemcpyAsync(h + 8, pp.nonfile.p, 2 * k * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
+  }
   return at + 8 + 2 * kPinNonfile;
 }
 
@@ -1965,11 +1992,17 @@ static void gather_survivors(dr_ctx* ctx, dr_state& base, const ActionDst& d) {
   else HIP_OK(hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(d.src_id), 0, M, stream));
 }
 
-// Appends src's T actions at dst offset `at`, all from source `sid` (one launch).
-static void append_actions(dr_ctx* ctx, const ActionDst& d, uint64_t at, dr_state& src, uint16_t sid) {
+// Appends src's T actions at dst offset `at`, all from source `sid` (one launch); with `ctr`, the
+// same launch sets the index counters (AppendArgs).
+static void append_actions(dr_ctx* ctx, const ActionDst& d, uint64_t at, dr_state& src, uint16_t sid,
+                           unsigned long long* ctr = nullptr, uint32_t ctr_at = 0, unsigned long long ctr_val = 0) {
   const uint64_t T = src.n_actions;
-  if (!T) return;
+  if (!T && !ctr) return;
   AppendArgs a{};
+  a.ctr = ctr;
+  a.nctr = IX_C_N;
+  a.ctr_at = ctr_at;
+  a.ctr_val = ctr_val;
   a.src = ActionArrays{src.kind.p, src.flags.p, src.key.p, src.path_ptr.p, src.path_len.p, src.size.p, src.delts.p,
                        src.src_off.p, src.src_len.p};
   a.dst = ActionArrays{d.kind + at, d.flags + at, d.key + at, d.path_ptr + at, d.path_len + at, d.size + at,
@@ -2088,13 +2121,11 @@ static dr_state* apply_incremental(dr_ctx* ctx, dr_state& base, const std::share
   chain_reserve(c, lo + T);
   chain_table_reserve(c, T);
   chain_tomb_reserve(c, T);
-  append_actions(ctx, chain_dst(c), lo, t, uint16_t(c.sources.size()));
+  // the index counters start at zero but for the tombstone list's fill (set by the append launch)
+  append_actions(ctx, chain_dst(c), lo, t, uint16_t(c.sources.size()), c.ctr.p, IX_C_TOMB_FILL, c.tomb_n);
   DBuf<uint32_t> tslot(ctx, T), tprev(ctx, T);
   IncChain::Undo u;
   u.e = DBuf<uint2>(ctx, T);
-  unsigned long long init[IX_C_N] = {};
-  init[IX_C_TOMB_FILL] = c.tomb_n;
-  HIP_OK(hipMemcpyAsync(c.ctr.p, init, sizeof(init), hipMemcpyHostToDevice, stream));
   IndexArgs a = ix_args(c);
   a.lo = lo;
   a.hi = lo + T;
@@ -2106,10 +2137,13 @@ static dr_state* apply_incremental(dr_ctx* ctx, dr_state& base, const std::share
   launch_ix_touch(a, stream);
   launch_ix_delta(a, stream);
   if (cutoff > base.cutoff) launch_ix_expire(a, c.tomb_n, stream);
-  // one round trip: the tail's parse counters and non-file lines with the index counters
-  const size_t at = parse_queue_readback(ctx, pp, 0);
-  HIP_OK(hipMemcpyAsync(ctx->pinned() + at, c.ctr.p, IX_C_N * sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                        stream));
+  // one round trip: the tail's parse counters and non-file lines with the index counters, written
+  // into the pinned words by one launch
+  ReadbackArgs rb{};
+  int nrb = 0;
+  const size_t at = parse_queue_readback(ctx, pp, 0, &rb, &nrb);
+  rb.src[nrb] = reinterpret_cast<const uint64_t*>(c.ctr.p), rb.dst[nrb] = ctx->pinned_dev() + at, rb.n[nrb++] = IX_C_N;
+  launch_readback(rb, stream);
   HIP_OK(hipStreamSynchronize(stream));
   std::vector<unsigned long long> ctr(ctx->pinned() + at, ctx->pinned() + at + IX_C_N);
   if (!parse_finish(ctx, tail, &t, pp, nf)) fail(DR_E_INTERNAL, "applied tail: canonicalisation arena too small");

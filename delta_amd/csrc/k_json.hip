@@ -313,6 +313,9 @@ __device__ __forceinline__ void walk_line(const JsonParseArgs& a, uint32_t* tokb
 constexpr uint32_t T_NL = 12;
 constexpr uint32_t TAPE_CAP = 4096;  // tokens (16 KiB of LDS)
 
+constexpr uint64_t STRUCT_CLS = (uint64_t(jl::T_COLON) << 40) | (uint64_t(jl::T_OBJ_OPEN) << 44) |
+                                (uint64_t(jl::T_COMMA) << 48) | (uint64_t(jl::T_OBJ_CLOSE) << 52);
+
 // Bytes escaped by a backslash run, with the run parity carried in (cin) and out (*cout): the
 // per-lane walker's rule (json_lane.h tokenize_window).
 __device__ __forceinline__ uint32_t escape16(uint32_t bs, uint32_t cin, uint32_t* cout) {
@@ -339,7 +342,7 @@ __device__ __forceinline__ int32_t from_lower(bool has, int32_t v, int32_t dflt)
 // The tape of the region [rb, rb + R) of the stage (R includes the last line's newline). Returns
 // true when every line of the wave is on it (wave-uniform); false sends the wave to the walker.
 __device__ __forceinline__ bool build_tape(const uint4* stage, uint32_t rb, uint32_t R, uint32_t nlines, uint32_t* tape,
-                           uint16_t* nltok, uint8_t* tline) {
+                           uint16_t* nltok, uint8_t* tline, unsigned long long* phase = nullptr) {
   const uint32_t lane = threadIdx.x;
   const uint32_t a0 = rb & ~15u;
   const uint32_t skew = rb - a0;
@@ -348,19 +351,17 @@ __device__ __forceinline__ bool build_tape(const uint4* stage, uint32_t rb, uint
   uint32_t esc_c = 0, instr_c = 0, sc_c = 0, tbase = 0, nlc = 0;
   int32_t open_c = -1, bs_c = -1;
   for (uint32_t s = 0; s < nsteps; ++s) {
+    const uint64_t ts0 = phase ? __builtin_amdgcn_s_memtime() : 0;
     const uint32_t wpos = (s << 10) + (lane << 4);
     const int32_t lo = int32_t(wpos) - int32_t(skew);  // region offset of the window's byte 0
-    uint32_t w[4] = {0, 0, 0, 0};
-    if (wpos < total) {
-      const uint4 v = stage[(a0 + wpos) >> 4];
-      w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
-    }
-    uint32_t valid = 0;
-    if (lo < int32_t(R)) {
-      valid = 0xFFFFu;
-      if (lo < 0) valid &= 0xFFFFu << uint32_t(-lo);
-      if (lo + 16 > int32_t(R)) valid &= (1u << uint32_t(int32_t(R) - lo)) - 1u;
-    }
+    // unconditional (clamped) stage read and masks: a guarded read is a branch
+    const uint4 v = stage[min((a0 + wpos) >> 4, JL_STAGE_BYTES / 16 - 1)];
+    const uint32_t keep = wpos < total ? ~0u : 0u;
+    const uint32_t w[4] = {v.x & keep, v.y & keep, v.z & keep, v.w & keep};
+    const uint32_t vlo = lo < 0 ? (0xFFFFu << uint32_t(min(-lo, 16))) & 0xFFFFu : 0xFFFFu;
+    const int32_t rem = int32_t(R) - lo;  // bytes of the region from the window's byte 0
+    const uint32_t vhi = rem >= 16 ? 0xFFFFu : rem <= 0 ? 0u : (1u << uint32_t(rem)) - 1u;
+    const uint32_t valid = vlo & vhi;
     jl::Win m;
     jl::classify(w, m);
     m.q &= valid; m.bs &= valid; m.st &= valid; m.sp &= valid; m.ctrl &= valid;
@@ -374,7 +375,7 @@ __device__ __forceinline__ bool build_tape(const uint4* stage, uint32_t rb, uint
     const bool allbs = m.bs == 0xFFFFu;
     const uint32_t cin = uint32_t(from_lower(!allbs, int32_t(c0), int32_t(esc_c)));
     uint32_t cout;
-    const uint32_t escaped = (m.bs | cin) ? escape16(m.bs, cin, &cout) : (cout = 0, 0u);
+    const uint32_t escaped = escape16(m.bs, cin, &cout);
     esc_c = uint32_t(__builtin_amdgcn_readlane(int(allbs ? cin : cout), 63));
     // string state: prefix XOR of the windows' quote parities
     const uint32_t quote = m.q & ~escaped;
@@ -414,7 +415,9 @@ __device__ __forceinline__ bool build_tape(const uint4* stage, uint32_t rb, uint
     uint32_t idx = tbase + ((incl - cnt) & 0xFFFFu);
     uint32_t nlr = nlc + ((incl - cnt) >> 16);
     bool longstr = false;
+    const uint64_t ts1 = phase ? __builtin_amdgcn_s_memtime() : 0;
     uint32_t t = tm;
+    const uint64_t wlo = uint64_t(w[0]) | (uint64_t(w[1]) << 32), whi = uint64_t(w[2]) | (uint64_t(w[3]) << 32);
     while (t) {
       const uint32_t k = jl::ctz32(t);
       t &= t - 1;
@@ -424,19 +427,24 @@ __device__ __forceinline__ bool build_tape(const uint4* stage, uint32_t rb, uint
       const int32_t op = ob ? lo + 31 - __builtin_clz(ob) : open_in;
       const int32_t lb = bb ? lo + 31 - __builtin_clz(bb) : bs_in;
       const uint32_t blen = pos - uint32_t(op) - 1u;
-      const uint32_t c = jl::win_byte(w, k);
-      const uint32_t scls = c == ':' ? jl::T_COLON : c == ',' ? jl::T_COMMA
-                          : ((c & 2u) ? jl::T_OBJ_OPEN : jl::T_OBJ_CLOSE) + ((c & 0x20u) ? 0u : 1u);
-      uint32_t tok;
-      if (close & bit) {
-        longstr |= blen >= 4096u;
-        tok = (uint32_t(op) << 16) | ((blen & 0xFFFu) << 4) | (lb > op ? jl::T_STRING_ESC : jl::T_STRING);
-      } else {
-        tok = (pos << 16) | ((st & bit) ? scls : (sc_begin & bit) ? jl::T_SCALAR : T_NL);
-      }
+      const uint32_t c = uint32_t(((k & 8u) ? whi : wlo) >> ((k & 7u) * 8u)) & 0xFFu;
+      // structural class by the low nibble ({ [ : B, } ] : D, ':' A, ',' C) from a nibble table, + 1
+      // for the square brackets (bit 5 clear): a compare chain on c compiles to a branch tree
+      const uint32_t lo4 = c & 15u;
+      const uint32_t scls = uint32_t((STRUCT_CLS >> (4u * lo4)) & 15u) + (((0x2800u >> lo4) & ~(c >> 5)) & 1u);
+      const bool isclose = (close & bit) != 0;
+      longstr |= isclose & (blen >= 4096u);
+      const uint32_t stok = (uint32_t(op) << 16) | ((blen & 0xFFFu) << 4) | (lb > op ? jl::T_STRING_ESC : jl::T_STRING);
+      const uint32_t otok = (pos << 16) | ((st & bit) ? scls : (sc_begin & bit) ? jl::T_SCALAR : T_NL);
       tline[idx] = uint8_t(nlr);
-      if (nl & bit) nltok[nlr++] = uint16_t(idx);
-      tape[idx++] = tok;
+      const bool isnl = (nl & bit) != 0;
+      nltok[isnl ? nlr : uint32_t(JL_T)] = uint16_t(idx);  // slot JL_T: a sink for the other tokens
+      nlr += isnl ? 1u : 0u;
+      tape[idx++] = isclose ? stok : otok;
+    }
+    if (phase && lane == 0) {
+      atomicAdd(&phase[6], (unsigned long long)(ts1 - ts0));
+      atomicAdd(&phase[7], (unsigned long long)(__builtin_amdgcn_s_memtime() - ts1));
     }
     if (__ballot(longstr)) return false;
     tbase += tot & 0xFFFFu;
@@ -703,14 +711,12 @@ __global__ void __launch_bounds__(JL_T, DR_JL_WAVES) k_json_lines(JsonParseArgs 
   __shared__ uint32_t tokbuf[Stage ? 1 : JL_TOKCAP * JL_T];
   __shared__ uint4 stage[Stage ? JL_STAGE_BYTES / 16 : 1];
   __shared__ uint32_t tape[Stage ? TAPE_CAP : 1];
-  __shared__ uint16_t nltok[Stage ? JL_T : 1];
+  __shared__ uint16_t nltok[Stage ? JL_T + 1 : 1];
   __shared__ uint8_t tline[Stage ? TAPE_CAP : 1];
   __shared__ std::conditional_t<Stage, TapeAgg, uint32_t> agg;
   const uint32_t lane = threadIdx.x;
   const uint64_t line = uint64_t(blockIdx.x) * JL_T + lane;
   const bool live = line < a.nlines;
-  const uint64_t b = !live ? 0 : line == 0 ? 0 : a.nl[line - 1] + 1;
-  const uint32_t n = live ? uint32_t(a.nl[line] - b) : 0;
   if constexpr (Stage) {
     uint64_t tp0 = a.phase ? __builtin_amdgcn_s_memtime() : 0;
     auto phase = [&](int k) {
@@ -719,6 +725,58 @@ __global__ void __launch_bounds__(JL_T, DR_JL_WAVES) k_json_lines(JsonParseArgs 
       if (lane == 0) atomicAdd(&a.phase[k], (unsigned long long)(t - tp0));
       tp0 = t;
     };
+    if (a.zero) {  // the whole segment in this wave; its newline index and counter reset here
+      if (lane < a.nzero) a.zero[lane] = 0;
+      const uint32_t len = uint32_t(a.buf_len);
+      const uint4* src = reinterpret_cast<const uint4*>(a.buf);
+      const uint32_t nq = ((len + 15u) >> 4) + 3u;
+      for (uint32_t k = lane; k < nq; k += JL_T) stage[k] = src[k];
+      __threadfence();  // the cleared counters reach L2 before any atomic on them
+      __syncthreads();
+      phase(0);
+      const uint32_t nw = uint32_t(a.nlines);
+      const bool taped = build_tape(stage, 0u, len, nw, tape, nltok, tline, a.phase);
+      phase(1);
+      __syncthreads();
+      if (taped) {
+        if (lane < nw) a.nl_out[lane] = tape[nltok[lane]] >> 16;  // the newline positions, from the tape
+        if (lane == 0) {
+          a.off2[0] = 0;
+          a.off2[1] = nw;
+        }
+        tape_lines(a, 0, nw, reinterpret_cast<const uint8_t*>(stage), 0, tape, nltok, tline, agg);
+        phase(2);
+        if (a.phase && lane == 0) atomicAdd(&a.phase[4], 1ull);
+        return;
+      }
+      // off the tape: index the newlines from the stage; every line goes to the General walker
+      uint32_t base = 0;
+      for (uint32_t s0 = 0; s0 < len; s0 += 16u * JL_T) {
+        const uint32_t wpos = s0 + 16u * lane;
+        const uint4 v = stage[min(wpos >> 4, JL_STAGE_BYTES / 16 - 1)];
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        uint32_t m = 0;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) m |= jl::gather4(jl::zbytes(w[d] ^ 0x0a0a0a0au)) << (4 * d);
+        const int32_t rem = int32_t(len) - int32_t(wpos);
+        m &= rem >= 16 ? 0xFFFFu : rem <= 0 ? 0u : (1u << uint32_t(rem)) - 1u;
+        const uint32_t c = __builtin_popcount(m);
+        const uint32_t incl = wv::scan_incl(c, 0u, [](uint32_t e, uint32_t l) { return e + l; });
+        uint32_t r = base + incl - c;
+        while (m) {
+          a.nl_out[r++] = wpos + jl::ctz32(m);
+          m &= m - 1;
+        }
+        base += wv::last_uniform(incl);
+      }
+      if (lane == 0) {
+        a.off2[0] = 0;
+        a.off2[1] = base;
+        atomicAdd(a.hard_count, (unsigned long long)nw);
+      }
+      if (lane < nw) a.hard_idx[lane] = lane;
+      return;
+    }
     // the wave's region: [its first line's 16-byte block, its last line's end rounded up to 16);
     // the JSON buffer's 64-byte zero pad keeps the rounded end readable
     const uint64_t first = uint64_t(blockIdx.x) * JL_T;
@@ -733,7 +791,7 @@ __global__ void __launch_bounds__(JL_T, DR_JL_WAVES) k_json_lines(JsonParseArgs 
       phase(0);
       const uint32_t nw = uint32_t(last - first + 1);
       const uint64_t rb = first == 0 ? 0 : a.nl[first - 1] + 1;  // the wave's first line
-      const bool taped = build_tape(stage, uint32_t(rb - r0), uint32_t(a.nl[last] + 1 - rb), nw, tape, nltok, tline);
+      const bool taped = build_tape(stage, uint32_t(rb - r0), uint32_t(a.nl[last] + 1 - rb), nw, tape, nltok, tline, a.phase);
       phase(1);
       if (taped) {
         __syncthreads();
@@ -753,6 +811,8 @@ __global__ void __launch_bounds__(JL_T, DR_JL_WAVES) k_json_lines(JsonParseArgs 
     }
     return;
   }
+  const uint64_t b = !live ? 0 : line == 0 ? 0 : a.nl[line - 1] + 1;
+  const uint32_t n = live ? uint32_t(a.nl[line] - b) : 0;
   walk_line(a, tokbuf, lane, line, live, b, n, a.buf + b);
 }
 

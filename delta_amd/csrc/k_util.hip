@@ -69,6 +69,7 @@ __global__ void __launch_bounds__(256) k_gather_bytes(const uint64_t* __restrict
 // fill, each a dispatch of its own on the per-commit path).
 __global__ void __launch_bounds__(256) k_append_actions(AppendArgs a) {
   const uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (a.ctr && i < a.nctr) a.ctr[i] = i == a.ctr_at ? a.ctr_val : 0ull;
   if (i >= a.n) return;
   a.dst.kind[i] = a.src.kind[i];
   a.dst.flags[i] = a.src.flags[i];
@@ -80,6 +81,12 @@ __global__ void __launch_bounds__(256) k_append_actions(AppendArgs a) {
   a.dst.src_off[i] = a.src.src_off[i];
   a.dst.src_len[i] = a.src.src_len[i];
   a.src_id[i] = a.sid;
+}
+
+__global__ void __launch_bounds__(256) k_readback(ReadbackArgs a) {
+#pragma unroll
+  for (int s = 0; s < READBACK_SPANS; ++s)
+    for (uint32_t k = threadIdx.x; k < a.n[s]; k += 256) a.dst[s][k] = a.src[s][k];
 }
 
 // Host-resolved floating-point partition values into their K5 cache rows: row[k] gets bits[k] (the
@@ -159,8 +166,13 @@ void launch_scatter_fp(const uint64_t* rows, const uint64_t* bits, const uint8_t
                    isnull);
 }
 
+void launch_readback(const ReadbackArgs& a, hipStream_t st) {
+  DR_LAUNCH(dev::k_readback, dim3(1), dim3(256), 0, st, a);
+}
+
 void launch_append_actions(const AppendArgs& a, hipStream_t st) {
-  if (a.n) DR_LAUNCH(dev::k_append_actions, dim3(unsigned((a.n + 255) / 256)), dim3(256), 0, st, a);
+  const uint64_t n = std::max<uint64_t>(a.n, a.ctr ? a.nctr : 0);
+  if (n) DR_LAUNCH(dev::k_append_actions, dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, a);
 }
 
 }  // namespace dr

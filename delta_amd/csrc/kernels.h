@@ -66,7 +66,16 @@ struct JsonParseArgs {
   uint64_t* hard_idx;             // lines the fast walker defers to the General walker
   unsigned long long* hard_count;
   unsigned long long* phase;      // diagnostics (DR_JSON_PHASES): staged kernel phase clocks, or null
+  // a segment of one wave (JSON_FUSE_MAX_LINES lines, one index block): the newline index and the
+  // counter reset run inside the parse kernel -- nl and off2 = {0, lines} are written by it and
+  // zero[0..nzero) cleared (null zero: launch_json_index1 / the block index ran before)
+  uint64_t buf_len;
+  uint64_t* zero;
+  uint32_t nzero;
+  uint64_t* off2;
+  uint64_t* nl_out;  // = nl, writable (the fused index)
 };
+constexpr uint64_t JSON_FUSE_MAX_LINES = 64;
 
 uint64_t json_num_blocks(uint64_t len);
 // newline index: per-block counts + u16 slots (json_slot_entries), then the global positions
@@ -545,8 +554,22 @@ struct AppendArgs {
   uint16_t* src_id;
   uint64_t n;
   uint16_t sid;
+  // the index counters the apply's next kernels accumulate into: ctr[0..nctr) = 0 but
+  // ctr[ctr_at] = ctr_val (null ctr: none), set by the same launch instead of an upload
+  unsigned long long* ctr;
+  uint32_t nctr, ctr_at;
+  unsigned long long ctr_val;
 };
 void launch_append_actions(const AppendArgs& a, hipStream_t st);
+// Device words into pinned host memory, several spans in one launch (an apply's counters and
+// non-file line list: one dispatch instead of a copy per span)
+constexpr int READBACK_SPANS = 4;
+struct ReadbackArgs {
+  const uint64_t* src[READBACK_SPANS];
+  uint64_t* dst[READBACK_SPANS];
+  uint32_t n[READBACK_SPANS];
+};
+void launch_readback(const ReadbackArgs& a, hipStream_t st);
 // export: valid[i] = flags[i] & F_HAS_DELTS, out[i] = valid ? delts[i] : 0
 void launch_delts_fix(const uint8_t* flags, const int64_t* delts, uint64_t n, uint8_t* valid, int64_t* out,
                       hipStream_t st);

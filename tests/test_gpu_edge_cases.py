@@ -623,6 +623,37 @@ def test_device_walker_writer_shaped_waves(engine, monkeypatch, staged):
         assert _device_view(rec) == expected(line), line
 
 
+@pytest.mark.parametrize("clean", [True, False])
+def test_device_walker_one_wave_segments(engine, clean):
+    """Segments of at most 64 lines in one 16 KiB index block (a streamed commit): the parse kernel
+    indexes the newlines itself -- from the token tape, or by a scan of the stage when the region
+    is off the tape (whitespace, control bytes, long strings), every line then going to the General
+    walker -- against the PERMISSIVE restatement, segment by segment."""
+    from tests.test_json_lane import corpus, expected, mutate
+    base = [l for l in corpus() if b"\n" not in l and len(l) < 2048]
+    rng = random.Random(0x51AB + clean)
+    for _ in range(120):
+        want = rng.randint(1, 64)
+        lines, size = [], 0
+        while len(lines) < want:
+            line = mutate(rng, rng.choice(base)) if rng.random() < 0.4 else rng.choice(base)
+            if b"\n" in line or (clean and not _writer_clean(line)):
+                continue
+            try:
+                line.decode("utf-8")
+            except UnicodeDecodeError:
+                continue
+            if size + len(line) + 1 > 16384:
+                break
+            lines.append(line)
+            size += len(line) + 1
+        got = _device_lines(engine, lines)
+        assert len(got) == len(lines)
+        for line, rec in zip(lines, got):
+            assert rec["line"] == line
+            assert _device_view(rec) == expected(line), line
+
+
 def test_device_walker_on_synthetic_commits(engine, tmp_path):
     """Writer-canonical commits (the benchmark's add / remove lines) read per line by
     dr_parse_commits equal Action.fromJson's path and size, and the replay equals the oracle's."""

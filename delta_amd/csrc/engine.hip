@@ -1476,6 +1476,12 @@ struct ParsePending {
   bool canonicalize = false;
   bool canon_sized = false; // the arena was sized from the counters (exact), not from a hint
   size_t pin_at = 0;        // where its words land in ctx->pinned()
+  // the small tail's deferred post-parse launch (parse_launch's defer_tail): k_tail_post's work,
+  // run by launch_apply_small or parse_flush_tail; nl / hard stay alive for it
+  bool tail_deferred = false;
+  JsonParseArgs tail_ja{};
+  CanonArgs tail_cg{};
+  DBuf<uint64_t> nl, hard;
 };
 constexpr size_t kPinNonfile = 1024;  // non-file entries (pairs) read back with the counters
 
@@ -1484,7 +1490,7 @@ constexpr size_t kPinNonfile = 1024;  // non-file entries (pairs) read back with
 // counters are read back before k_canon (the arena is sized exactly); later replays size the arena
 // from the segment's last need and queue K3/K4 without a round trip.
 static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr_state* st,
-                                 bool canonicalize) {
+                                 bool canonicalize, bool defer_tail = false) {
   StagedData& s = *sp;
   hipStream_t stream = ctx->stream;
   ParsePending pp;
@@ -1663,16 +1669,22 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
       st->arenas.push_back(std::make_shared<DBuf<uint8_t>>(ctx, cap));
       pp.canon_arena = st->arenas.back()->p;
       CanonArgs cg{act, N, st->arenas.back()->p, cap, counters.p + 4};
-      if (tail_post) launch_tail_post(ja, cg, stream);
+      if (tail_post && defer_tail) pp.tail_deferred = true, pp.tail_ja = ja, pp.tail_cg = cg;
+      else if (tail_post) launch_tail_post(ja, cg, stream);
       else launch_canon(cg, stream);
     } else if (tail_post) {
-      launch_json_hard(ja, stream);
+      if (defer_tail) pp.tail_deferred = true, pp.tail_ja = ja, pp.tail_cg = CanonArgs{act, 0, nullptr, 0, counters.p + 4};
+      else launch_json_hard(ja, stream);
     }
     pp.canon_cap = cap;
     pp.canonicalize = true;
   }
   pp.counters = std::move(counters);
   pp.nonfile = std::move(nonfile);
+  if (pp.tail_deferred) {
+    pp.nl = std::move(nl);
+    pp.hard = std::move(hard);
+  }
   pp.R = R;
   pp.nlines = nlines;
   return pp;
@@ -1695,6 +1707,14 @@ static size_t parse_queue_readback(dr_ctx* ctx, ParsePending& pp, size_t at, Rea
     if (k) HIP_OK(hipMemcpyAsync(h + 8, pp.nonfile.p, 2 * k * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
   }
   return at + 8 + 2 * kPinNonfile;
+}
+
+// Launches a deferred post-parse step that no fused apply took.
+static void parse_flush_tail(dr_ctx* ctx, ParsePending& pp) {
+  if (!pp.tail_deferred) return;
+  if (pp.tail_cg.n) launch_tail_post(pp.tail_ja, pp.tail_cg, ctx->stream);
+  else launch_json_hard(pp.tail_ja, ctx->stream);
+  pp.tail_deferred = false;
 }
 
 // After the stream has drained: error codes, counters and the non-file actions (protocol /
@@ -1994,10 +2014,16 @@ static void gather_survivors(dr_ctx* ctx, dr_state& base, const ActionDst& d) {
 
 // Appends src's T actions at dst offset `at`, all from source `sid` (one launch); with `ctr`, the
 // same launch sets the index counters (AppendArgs).
+static AppendArgs append_args(const ActionDst& d, uint64_t at, dr_state& src, uint16_t sid, unsigned long long* ctr,
+                              uint32_t ctr_at, unsigned long long ctr_val);
 static void append_actions(dr_ctx* ctx, const ActionDst& d, uint64_t at, dr_state& src, uint16_t sid,
                            unsigned long long* ctr = nullptr, uint32_t ctr_at = 0, unsigned long long ctr_val = 0) {
+  if (!src.n_actions && !ctr) return;
+  launch_append_actions(append_args(d, at, src, sid, ctr, ctr_at, ctr_val), ctx->stream);
+}
+static AppendArgs append_args(const ActionDst& d, uint64_t at, dr_state& src, uint16_t sid, unsigned long long* ctr,
+                              uint32_t ctr_at, unsigned long long ctr_val) {
   const uint64_t T = src.n_actions;
-  if (!T && !ctr) return;
   AppendArgs a{};
   a.ctr = ctr;
   a.nctr = IX_C_N;
@@ -2010,7 +2036,7 @@ static void append_actions(dr_ctx* ctx, const ActionDst& d, uint64_t at, dr_stat
   a.src_id = d.src_id + at;
   a.n = T;
   a.sid = sid;
-  launch_append_actions(a, ctx->stream);
+  return a;
 }
 
 static ActionDst chain_dst(IncChain& c) {
@@ -2121,8 +2147,6 @@ static dr_state* apply_incremental(dr_ctx* ctx, dr_state& base, const std::share
   chain_reserve(c, lo + T);
   chain_table_reserve(c, T);
   chain_tomb_reserve(c, T);
-  // the index counters start at zero but for the tombstone list's fill (set by the append launch)
-  append_actions(ctx, chain_dst(c), lo, t, uint16_t(c.sources.size()), c.ctr.p, IX_C_TOMB_FILL, c.tomb_n);
   DBuf<uint32_t> tslot(ctx, T), tprev(ctx, T);
   IncChain::Undo u;
   u.e = DBuf<uint2>(ctx, T);
@@ -2134,16 +2158,25 @@ static dr_state* apply_incremental(dr_ctx* ctx, dr_state& base, const std::share
   a.old_cut = base.cutoff;
   a.new_cut = cutoff;
   a.undo = u.e.p;
-  launch_ix_touch(a, stream);
-  launch_ix_delta(a, stream);
-  if (cutoff > base.cutoff) launch_ix_expire(a, c.tomb_n, stream);
+  // the index counters start at zero but for the tombstone list's fill (set by the append launch)
+  const AppendArgs ap = append_args(chain_dst(c), lo, t, uint16_t(c.sources.size()), c.ctr.p, IX_C_TOMB_FILL, c.tomb_n);
+  if (T && T <= APPLY_SMALL_MAX) {  // a streamed commit: post-parse, append and both index passes in one launch
+    launch_apply_small(pp.tail_deferred ? &pp.tail_ja : nullptr, pp.tail_cg, ap, a, stream);
+    pp.tail_deferred = false;
+  } else {
+    parse_flush_tail(ctx, pp);
+    launch_append_actions(ap, stream);
+    launch_ix_touch(a, stream);
+    launch_ix_delta(a, stream);
+  }
   // one round trip: the tail's parse counters and non-file lines with the index counters, written
-  // into the pinned words by one launch
+  // into the pinned words by the expiry's last workgroup (or one launch of their own)
   ReadbackArgs rb{};
   int nrb = 0;
   const size_t at = parse_queue_readback(ctx, pp, 0, &rb, &nrb);
   rb.src[nrb] = reinterpret_cast<const uint64_t*>(c.ctr.p), rb.dst[nrb] = ctx->pinned_dev() + at, rb.n[nrb++] = IX_C_N;
-  launch_readback(rb, stream);
+  if (cutoff > base.cutoff && c.tomb_n) launch_ix_expire(a, c.tomb_n, stream, &rb);
+  else launch_readback(rb, stream);
   HIP_OK(hipStreamSynchronize(stream));
   std::vector<unsigned long long> ctr(ctx->pinned() + at, ctx->pinned() + at + IX_C_N);
   if (!parse_finish(ctx, tail, &t, pp, nf)) fail(DR_E_INTERNAL, "applied tail: canonicalisation arena too small");
@@ -2230,7 +2263,7 @@ static dr_state* apply_tail(dr_ctx* ctx, dr_state& base, const std::shared_ptr<S
   std::unique_ptr<dr_state> t(new_state(ctx, tail));
   std::vector<NonFileAction> nf;
   // the tail's parse is queued; the incremental path reads its counters back with the index's
-  ParsePending pp = parse_launch(ctx, tail, t.get(), true);
+  ParsePending pp = parse_launch(ctx, tail, t.get(), true, /*defer_tail=*/true);
   bool parsed = false;
   // protocol / metaData / txn: the base's winners first, then the tail's actions in order
   auto all_nonfile = [&] {
@@ -2259,6 +2292,7 @@ static dr_state* apply_tail(dr_ctx* ctx, dr_state& base, const std::shared_ptr<S
     }
   }
   if (!parsed) {
+    parse_flush_tail(ctx, pp);
     parse_queue_readback(ctx, pp, 0);
     HIP_OK(hipStreamSynchronize(ctx->stream));
     if (!parse_finish(ctx, tail, t.get(), pp, nf)) fail(DR_E_INTERNAL, "applied tail: canonicalisation arena too small");

@@ -1,0 +1,134 @@
+// Device side of the incremental apply's index (k_index.hip): probing, the counters' deltas and
+// the two passes over a tail's file actions, shared with the small-tail apply kernel (k_json.hip
+// k_apply_small).
+#pragma once
+#include "dev_common.h"
+#include "kernels.h"
+
+namespace dr {
+namespace dev {
+
+constexpr uint32_t IX_NONE = 0xffffffffu;
+constexpr int IX_T = 256;
+
+__device__ __forceinline__ bool ix_file_action(const IndexArgs& a, uint64_t i) {
+  const uint8_t k = a.kind[i];
+  return (k == K_ADD || k == K_REMOVE) && !(a.flags[i] & F_PATH_NULL);
+}
+__device__ __forceinline__ int64_t ix_delts(const IndexArgs& a, uint64_t i) {
+  return (a.flags[i] & F_HAS_DELTS) ? a.delts[i] : 0;
+}
+__device__ __forceinline__ bool ix_same_path(const IndexArgs& a, uint64_t i, uint64_t j) {
+  return key_equal(reinterpret_cast<const uint8_t*>(a.path_ptr[i]), a.path_len[i],
+                   reinterpret_cast<const uint8_t*>(a.path_ptr[j]), a.path_len[j]);
+}
+
+// slot of key k, inserted if absent; *fresh tells whether this call inserted it
+__device__ inline uint32_t ix_insert(unsigned long long* keys, uint64_t mask, uint64_t k, bool* fresh) {
+  uint64_t s = k & mask;
+  *fresh = false;
+  for (;;) {
+    unsigned long long x = keys[s];
+    if (x == 0) {
+      x = atomicCAS(keys + s, 0ull, (unsigned long long)k);
+      if (x == 0) {
+        *fresh = true;
+        return uint32_t(s);
+      }
+    }
+    if (x == k) return uint32_t(s);
+    s = (s + 1) & mask;
+  }
+}
+
+__device__ inline uint32_t ix_find(const unsigned long long* keys, uint64_t mask, uint64_t k) {
+  uint64_t s = k & mask;
+  for (;;) {
+    const unsigned long long x = keys[s];
+    if (x == k) return uint32_t(s);
+    if (x == 0) return IX_NONE;
+    s = (s + 1) & mask;
+  }
+}
+
+// Contribution of winner x to (files, size, removes, live checksum, tombstone checksum) at cutoff.
+struct Contrib {
+  unsigned long long f, sz, r, lks, tks;
+};
+__device__ __forceinline__ void contrib_add(Contrib& c, const IndexArgs& a, uint64_t x, int64_t cut, bool neg) {
+  unsigned long long f = 0, sz = 0, r = 0, lk = 0, tk = 0;
+  const unsigned long long top = a.key[x] >> 32;
+  if (a.kind[x] == K_ADD) {
+    f = 1;
+    sz = (unsigned long long)a.size[x];
+    lk = top;
+  } else if (ix_delts(a, x) > cut) {
+    r = 1;
+    tk = top;
+  }
+  if (neg) { f = 0ull - f; sz = 0ull - sz; r = 0ull - r; lk = 0ull - lk; tk = 0ull - tk; }
+  c.f += f; c.sz += sz; c.r += r; c.lks += lk; c.tks += tk;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  return v;
+}
+__device__ inline void flush_contrib(const IndexArgs& a, Contrib c, unsigned long long files) {
+  c.f = wave_sum(c.f); c.sz = wave_sum(c.sz); c.r = wave_sum(c.r);
+  c.lks = wave_sum(c.lks); c.tks = wave_sum(c.tks); files = wave_sum(files);
+  if ((threadIdx.x & 63) == 0) {
+    if (c.f) atomicAdd(a.ctr + IX_C_FILES, c.f);
+    if (c.sz) atomicAdd(a.ctr + IX_C_SIZE, c.sz);
+    if (c.r) atomicAdd(a.ctr + IX_C_REMOVES, c.r);
+    if (c.lks) atomicAdd(a.ctr + IX_C_LKS, c.lks);
+    if (c.tks) atomicAdd(a.ctr + IX_C_TKS, c.tks);
+    if (files) atomicAdd(a.ctr + IX_C_FILE_ACTIONS, files);
+  }
+}
+
+__device__ __forceinline__ void tomb_append(const IndexArgs& a, uint64_t x) {
+  const unsigned long long at = atomicAdd(a.ctr + IX_C_TOMB_FILL, 1ull);
+  if (at < a.tomb_cap) a.tomb_list[at] = uint32_t(x);
+  else atomicOr(a.ctr + IX_C_COLLIDE, 2ull);  // host sized the list: never expected
+}
+
+// Pass 1 of an apply: every file action of the tail claims its slot and raises it to itself.
+__device__ __forceinline__ void ix_touch_one(const IndexArgs& a, uint64_t i) {
+  const uint64_t t = i - a.lo;
+  if (!ix_file_action(a, i)) {
+    a.t_slot[t] = IX_NONE;
+    return;
+  }
+  bool fresh;
+  const uint32_t s = ix_insert(a.keys, a.mask, a.key[i], &fresh);
+  if (fresh) atomicAdd(a.ctr + IX_C_NEW_SLOTS, 1ull);
+  a.t_slot[t] = s;
+  a.t_prev[t] = atomicMax(a.vals + s, uint32_t(i + 1));
+}
+// Pass 2: the first toucher of each slot (the one whose atomicMax saw a pre-tail value) moves the
+// counters from the old winner to the final one and logs the old value for older states; every
+// action checks its bytes against the final winner (and the first toucher against the old one).
+__device__ __forceinline__ void ix_delta_one(const IndexArgs& a, uint64_t i, Contrib& c, unsigned long long& files) {
+  const uint64_t t = i - a.lo;
+  const uint32_t s = a.t_slot[t];
+  if (s == IX_NONE) return;
+  files = 1;
+  // an atomic load: in k_ix_touch_delta the slot was raised by this workgroup's atomics (at L2)
+  const uint64_t w = uint64_t(__hip_atomic_load(a.vals + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) - 1;
+  if (w != i && !ix_same_path(a, i, w)) atomicOr(a.ctr + IX_C_COLLIDE, 1ull);
+  const uint32_t prev = a.t_prev[t];
+  if (uint64_t(prev) <= a.lo) {
+    if (prev) {
+      const uint64_t o = uint64_t(prev) - 1;
+      if (!ix_same_path(a, i, o)) atomicOr(a.ctr + IX_C_COLLIDE, 1ull);
+      contrib_add(c, a, o, a.old_cut, true);
+    }
+    contrib_add(c, a, w, a.new_cut, false);
+    if (a.kind[w] == K_REMOVE && ix_delts(a, w) > a.new_cut) tomb_append(a, w);
+    const unsigned long long u = atomicAdd(a.ctr + IX_C_UNDO_FILL, 1ull);
+    a.undo[u] = make_uint2(uint32_t(i), prev);
+  }
+}
+}  // namespace dev
+}  // namespace dr

@@ -15,6 +15,7 @@
 #include "json_lane.h"
 #include "canon.h"
 #include "wave.h"
+#include "ix_dev.h"
 
 namespace dr {
 namespace dev {
@@ -835,7 +836,7 @@ __global__ void __launch_bounds__(64) k_json_hard(JsonParseArgs a) {
 // walker deferred (General walker), then the special paths' canonicalisation (k_canon's body) --
 // one launch instead of two for a streamed commit, whose kernels each cost a launch and a cold
 // start rather than their work.
-__global__ void __launch_bounds__(256) k_tail_post(JsonParseArgs a, CanonArgs c) {
+__device__ __forceinline__ void tail_post_body(const JsonParseArgs& a, const CanonArgs& c) {
   const uint64_t cnt = *a.hard_count;
   for (uint64_t k = threadIdx.x; k < cnt; k += blockDim.x) {
     const uint64_t line = a.hard_idx[k];
@@ -849,6 +850,44 @@ __global__ void __launch_bounds__(256) k_tail_post(JsonParseArgs a, CanonArgs c)
   __threadfence_block();
   __syncthreads();
   for (uint64_t i = threadIdx.x; i < c.n; i += blockDim.x) canon_one(c, i);
+}
+
+__global__ void __launch_bounds__(256) k_tail_post(JsonParseArgs a, CanonArgs c) { tail_post_body(a, c); }
+
+// A streamed commit's whole apply after its line walk, in one workgroup (launch_apply_small): the
+// deferred lines and canonicalisation, the append to the chain store (k_append_actions) with the
+// index counters' reset, and the index's two passes (k_ix_touch_delta), each step behind a fence
+// and a barrier -- one launch where three followed each other, each with its dispatch and cold start.
+__global__ void __launch_bounds__(IX_T) k_apply_small(JsonParseArgs a, CanonArgs c, AppendArgs p, IndexArgs x) {
+  const uint32_t t = threadIdx.x;
+  if (a.hard_count) {
+    tail_post_body(a, c);
+    __threadfence();
+    __syncthreads();
+  }
+  if (t < p.nctr) p.ctr[t] = t == p.ctr_at ? p.ctr_val : 0ull;
+  if (t < p.n) {
+    p.dst.kind[t] = p.src.kind[t];
+    p.dst.flags[t] = p.src.flags[t];
+    p.dst.key[t] = p.src.key[t];
+    p.dst.path_ptr[t] = p.src.path_ptr[t];
+    p.dst.path_len[t] = p.src.path_len[t];
+    p.dst.size[t] = p.src.size[t];
+    p.dst.delts[t] = p.src.delts[t];
+    p.dst.src_off[t] = p.src.src_off[t];
+    p.dst.src_len[t] = p.src.src_len[t];
+    p.src_id[t] = p.sid;
+  }
+  __threadfence();
+  __syncthreads();
+  const uint64_t i = x.lo + t;
+  if (i < x.hi) ix_touch_one(x, i);
+  __threadfence();
+  __syncthreads();
+  Contrib cc{0, 0, 0, 0, 0};
+  unsigned long long files = 0;
+  if (i < x.hi) ix_delta_one(x, i, cc, files);
+  flush_contrib(x, cc, files);
 }
 
 }  // namespace dev
@@ -886,6 +925,12 @@ void launch_json_parse(const JsonParseArgs& a, hipStream_t st) {
 
 void launch_tail_post(const JsonParseArgs& a, const CanonArgs& c, hipStream_t st) {
   DR_LAUNCH(dev::k_tail_post, dim3(1), dim3(256), 0, st, a, c);
+}
+
+void launch_apply_small(const JsonParseArgs* ja, const CanonArgs& cg, const AppendArgs& ap, const IndexArgs& ix,
+                        hipStream_t st) {
+  JsonParseArgs none{};
+  DR_LAUNCH(dev::k_apply_small, dim3(1), dim3(dev::IX_T), 0, st, ja ? *ja : none, cg, ap, ix);
 }
 
 void launch_json_hard(const JsonParseArgs& a, hipStream_t st) {

@@ -605,12 +605,20 @@ struct IndexArgs {
 };
 enum : int {
   IX_C_FILES = 0, IX_C_SIZE = 1, IX_C_REMOVES = 2, IX_C_LKS = 3, IX_C_TKS = 4, IX_C_COLLIDE = 5,
-  IX_C_FILE_ACTIONS = 6, IX_C_NEW_SLOTS = 7, IX_C_TOMB_FILL = 8, IX_C_UNDO_FILL = 9, IX_C_N = 16
+  IX_C_FILE_ACTIONS = 6, IX_C_NEW_SLOTS = 7, IX_C_TOMB_FILL = 8, IX_C_UNDO_FILL = 9, IX_C_DONE = 10, IX_C_N = 16
 };
 void launch_ix_build(const IndexArgs& a, hipStream_t st);
 void launch_ix_touch(const IndexArgs& a, hipStream_t st);
 void launch_ix_delta(const IndexArgs& a, hipStream_t st);
-void launch_ix_expire(const IndexArgs& a, uint64_t n_list, hipStream_t st);
+// with rb (spans given): the last workgroup to finish also writes the readback spans (the counters
+// are final then), instead of a launch_readback after it
+void launch_ix_expire(const IndexArgs& a, uint64_t n_list, hipStream_t st, const ReadbackArgs* rb = nullptr);
+// A tail of at most IX_T actions in one workgroup: the parse's deferred work (General walker,
+// canonicalisation; skipped when ja is null), the append to the chain store with the counters'
+// reset, and both index passes -- k_tail_post + k_append_actions + k_ix_touch_delta in one launch
+constexpr uint64_t APPLY_SMALL_MAX = 256;
+void launch_apply_small(const JsonParseArgs* ja, const CanonArgs& cg, const AppendArgs& ap, const IndexArgs& ix,
+                        hipStream_t st);
 void launch_ix_tomb_compact(const IndexArgs& a, const uint32_t* list_in, uint64_t n, uint32_t* list_out,
                             hipStream_t st);
 void launch_ix_undo(const IndexArgs& a, uint32_t* vals_out, const uint2* undo, uint64_t n, hipStream_t st);

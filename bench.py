@@ -230,8 +230,11 @@ def measure_stream(eng, table, exp, args):
             tail = eng.stage_files([c])
             t2 = time.perf_counter()
             nxt = cur.apply(tail, c0 + (k + 1) * step_ms)
-            torch.cuda.synchronize()
+            # dr_state_apply returns once the new state's counters are on the host (its readback's
+            # completion word): the apply latency a caller sees. The device synchronize follows,
+            # untimed, so that every commit starts from an idle device.
             t3 = time.perf_counter()
+            torch.cuda.synchronize()
             if timing and k:
                 for kn, ms in eng.last_timings().items():
                     if kn in ("start", "end"):

@@ -180,5 +180,15 @@ __device__ inline bool key_equal(const uint8_t* a, uint32_t an, const uint8_t* b
 }
 
 
+// The readback's completion word (ReadbackArgs::flag): every thread's span stores are fenced to the
+// system scope before one thread publishes the sequence number the host spins on.
+template <class Readback>  // ReadbackArgs (kernels.h)
+__device__ __forceinline__ void readback_flag(const Readback& a) {
+  if (!a.flag) return;
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(a.flag, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 }  // namespace dev
 }  // namespace dr

@@ -102,7 +102,8 @@ struct dr_ctx {
   uint64_t* pinned() {
     if (!hpin) {
       void* p = nullptr;
-      if (hipHostMalloc(&p, kPinWords * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess) {
+      // coherent: a kernel's stores reach it without a copy engine (launch_readback, the flag)
+      if (hipHostMalloc(&p, kPinWords * sizeof(uint64_t), hipHostMallocCoherent) != hipSuccess) {
         (void)hipGetLastError();
         fail(DR_E_OOM, "pinned readback words");
       }
@@ -117,6 +118,24 @@ struct dr_ctx {
   uint64_t* pinned_dev() {
     (void)pinned();
     return hpin_dev;
+  }
+  // the readback completion word (the pinned block's last) and its sequence
+  static constexpr size_t kPinFlag = kPinWords - 1;
+  uint64_t pin_seq = 0;
+  // Waits for a readback launched with {flag, seq}: a spin on the pinned word (a stream synchronize
+  // sleeps and wakes ~10 us after the kernel ends), with a stream synchronize after 1 s of spinning
+  // (and to surface any launch error).
+  void wait_readback(uint64_t seq) {
+    const volatile uint64_t* f = pinned() + kPinFlag;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t k = 0; *f != seq; ++k) {
+      if ((k & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
+        HIP_OK(hipStreamSynchronize(stream));
+        if (*f != seq) fail(DR_E_INTERNAL, "readback completion word not written");
+        break;
+      }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
   }
 
   void* alloc(size_t n) {
@@ -2175,9 +2194,11 @@ static dr_state* apply_incremental(dr_ctx* ctx, dr_state& base, const std::share
   int nrb = 0;
   const size_t at = parse_queue_readback(ctx, pp, 0, &rb, &nrb);
   rb.src[nrb] = reinterpret_cast<const uint64_t*>(c.ctr.p), rb.dst[nrb] = ctx->pinned_dev() + at, rb.n[nrb++] = IX_C_N;
+  rb.flag = ctx->pinned_dev() + dr_ctx::kPinFlag;
+  rb.seq = ++ctx->pin_seq;
   if (cutoff > base.cutoff && c.tomb_n) launch_ix_expire(a, c.tomb_n, stream, &rb);
   else launch_readback(rb, stream);
-  HIP_OK(hipStreamSynchronize(stream));
+  ctx->wait_readback(rb.seq);
   std::vector<unsigned long long> ctr(ctx->pinned() + at, ctx->pinned() + at + IX_C_N);
   if (!parse_finish(ctx, tail, &t, pp, nf)) fail(DR_E_INTERNAL, "applied tail: canonicalisation arena too small");
   c.used += ctr[IX_C_NEW_SLOTS];

@@ -88,6 +88,7 @@ __global__ void __launch_bounds__(IX_T) k_ix_expire(IndexArgs a, uint64_t n, Rea
   for (int s = 0; s < READBACK_SPANS; ++s)
     for (uint32_t k = threadIdx.x; k < rb.n[s]; k += IX_T)
       rb.dst[s][k] = __hip_atomic_load(rb.src[s] + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  readback_flag(rb);
 }
 
 // Keep the candidates that are still tombstones of the head at its cutoff (a.new_cut).

@@ -87,6 +87,7 @@ __global__ void __launch_bounds__(256) k_readback(ReadbackArgs a) {
 #pragma unroll
   for (int s = 0; s < READBACK_SPANS; ++s)
     for (uint32_t k = threadIdx.x; k < a.n[s]; k += 256) a.dst[s][k] = a.src[s][k];
+  readback_flag(a);
 }
 
 // Host-resolved floating-point partition values into their K5 cache rows: row[k] gets bits[k] (the

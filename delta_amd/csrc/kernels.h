@@ -568,6 +568,10 @@ struct ReadbackArgs {
   const uint64_t* src[READBACK_SPANS];
   uint64_t* dst[READBACK_SPANS];
   uint32_t n[READBACK_SPANS];
+  // with flag: *flag = seq once every span is written and fenced to the system (the host spins on
+  // it instead of a stream synchronize)
+  uint64_t* flag;
+  uint64_t seq;
 };
 void launch_readback(const ReadbackArgs& a, hipStream_t st);
 // export: valid[i] = flags[i] & F_HAS_DELTS, out[i] = valid ? delts[i] : 0

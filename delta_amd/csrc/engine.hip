@@ -1498,6 +1498,7 @@ struct ParsePending {
   // the small tail's deferred post-parse launch (parse_launch's defer_tail): k_tail_post's work,
   // run by launch_apply_small or parse_flush_tail; nl / hard stay alive for it
   bool tail_deferred = false;
+  bool parse_deferred = false;  // ... and the line walk too (launch_apply_commit / parse_flush_tail)
   JsonParseArgs tail_ja{};
   CanonArgs tail_cg{};
   DBuf<uint64_t> nl, hard;
@@ -1595,21 +1596,27 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
     static uint64_t phase_calls = 0;
     if (std::getenv("DR_JSON_PHASES")) {
       if (!phase) {
-        HIP_OK(hipMalloc(&phase, 8 * sizeof(unsigned long long)));
-        HIP_OK(hipMemset(phase, 0, 8 * sizeof(unsigned long long)));
+        HIP_OK(hipMalloc(&phase, 16 * sizeof(unsigned long long)));
+        HIP_OK(hipMemset(phase, 0, 16 * sizeof(unsigned long long)));
       }
       ja.phase = phase;
       if (++phase_calls % 200 == 0) {
-        unsigned long long h[8];
+        unsigned long long h[16];
         HIP_OK(hipMemcpy(h, phase, sizeof(h), hipMemcpyDeviceToHost));
         if (h[4])
           std::fprintf(stderr, "k_json_lines<true> clocks per wave: stage %.0f tape %.0f walk %.0f (rounds %.0f, first round %.0f; tape scan %.0f emit %.0f) (%llu waves)\n",
                        double(h[0]) / double(h[4]), double(h[1]) / double(h[4]), double(h[2]) / double(h[4]),
                        double(h[3]) / double(h[4]), double(h[5]) / double(h[4]), double(h[6]) / double(h[4]),
                        double(h[7]) / double(h[4]), h[4]);
+        if (h[8] + h[9] + h[10] + h[11])
+          std::fprintf(stderr, "k_apply_commit apply clocks: post-parse %.0f append %.0f touch %.0f delta %.0f\n",
+                       double(h[8]) / double(h[4]), double(h[9]) / double(h[4]), double(h[10]) / double(h[4]),
+                       double(h[11]) / double(h[4]));
       }
     }
-    launch_json_parse(ja, s2);
+    // an applied streamed commit: the walk runs in the apply's one launch (launch_apply_commit)
+    if (defer_tail && fuse1 && tail_post) pp.parse_deferred = true;
+    else launch_json_parse(ja, s2);
     if (!tail_post) launch_json_hard(ja, s2);
     if (ctx->overlap) {
       HIP_OK(hipEventCreateWithFlags(&ov.done, hipEventDisableTiming));
@@ -1731,6 +1738,8 @@ static size_t parse_queue_readback(dr_ctx* ctx, ParsePending& pp, size_t at, Rea
 // Launches a deferred post-parse step that no fused apply took.
 static void parse_flush_tail(dr_ctx* ctx, ParsePending& pp) {
   if (!pp.tail_deferred) return;
+  if (pp.parse_deferred) launch_json_parse(pp.tail_ja, ctx->stream);
+  pp.parse_deferred = false;
   if (pp.tail_cg.n) launch_tail_post(pp.tail_ja, pp.tail_cg, ctx->stream);
   else launch_json_hard(pp.tail_ja, ctx->stream);
   pp.tail_deferred = false;
@@ -2180,8 +2189,9 @@ static dr_state* apply_incremental(dr_ctx* ctx, dr_state& base, const std::share
   // the index counters start at zero but for the tombstone list's fill (set by the append launch)
   const AppendArgs ap = append_args(chain_dst(c), lo, t, uint16_t(c.sources.size()), c.ctr.p, IX_C_TOMB_FILL, c.tomb_n);
   if (T && T <= APPLY_SMALL_MAX) {  // a streamed commit: post-parse, append and both index passes in one launch
-    launch_apply_small(pp.tail_deferred ? &pp.tail_ja : nullptr, pp.tail_cg, ap, a, stream);
-    pp.tail_deferred = false;
+    if (pp.parse_deferred) launch_apply_commit(pp.tail_ja, pp.tail_cg, ap, a, stream);
+    else launch_apply_small(pp.tail_deferred ? &pp.tail_ja : nullptr, pp.tail_cg, ap, a, stream);
+    pp.tail_deferred = pp.parse_deferred = false;
   } else {
     parse_flush_tail(ctx, pp);
     launch_append_actions(ap, stream);

@@ -41,6 +41,22 @@ __device__ inline uint32_t ix_insert(unsigned long long* keys, uint64_t mask, ui
   }
 }
 
+// ix_insert for a few keys (a streamed commit's): every probe is the compare-and-swap itself, one
+// round trip to L2 per probe instead of a load and then the swap
+__device__ inline uint32_t ix_insert_cas(unsigned long long* keys, uint64_t mask, uint64_t k, bool* fresh) {
+  uint64_t s = k & mask;
+  *fresh = false;
+  for (;;) {
+    const unsigned long long x = atomicCAS(keys + s, 0ull, (unsigned long long)k);
+    if (x == 0) {
+      *fresh = true;
+      return uint32_t(s);
+    }
+    if (x == k) return uint32_t(s);
+    s = (s + 1) & mask;
+  }
+}
+
 __device__ inline uint32_t ix_find(const unsigned long long* keys, uint64_t mask, uint64_t k) {
   uint64_t s = k & mask;
   for (;;) {
@@ -128,6 +144,129 @@ __device__ __forceinline__ void ix_delta_one(const IndexArgs& a, uint64_t i, Con
     if (a.kind[w] == K_REMOVE && ix_delts(a, w) > a.new_cut) tomb_append(a, w);
     const unsigned long long u = atomicAdd(a.ctr + IX_C_UNDO_FILL, 1ull);
     a.undo[u] = make_uint2(uint32_t(i), prev);
+  }
+}
+
+// The two passes for a tail of one workgroup (k_apply_small / k_apply_commit), one action per thread
+// with its slot and previous value in registers: pass 1 also settles the base's old winner -- its
+// counters and its bytes -- before the barrier, so that pass 2 waits only on the final winner.
+struct IxTouch {
+  uint32_t s = IX_NONE, prev = 0;
+  bool old_bad = false;
+  Contrib old{0, 0, 0, 0, 0};
+  Contrib own{0, 0, 0, 0, 0};  // this action's own contribution as a winner (ix_touch_pre_v)
+  bool own_remove = false, own_set = false;
+};
+__device__ __forceinline__ void ix_touch_pre(const IndexArgs& a, uint64_t i, IxTouch& T) {
+  if (!ix_file_action(a, i)) return;
+  bool fresh;
+  T.s = ix_insert_cas(a.keys, a.mask, a.key[i], &fresh);
+  if (fresh) atomicAdd(a.ctr + IX_C_NEW_SLOTS, 1ull);
+  T.prev = atomicMax(a.vals + T.s, uint32_t(i + 1));
+  if (T.prev && uint64_t(T.prev) <= a.lo) {
+    const uint64_t o = uint64_t(T.prev) - 1;
+    T.old_bad = !ix_same_path(a, i, o);
+    contrib_add(T.old, a, o, a.old_cut, true);
+  }
+}
+// ix_touch_pre with the action's fields in registers (the appending thread's own action), and the
+// slot's value read speculatively beside the first probe: when the key sits in its home slot (the
+// usual case at load <= 1/2) the old winner's fields are fetched beside the atomicMax instead of
+// after it -- three dependent round trips instead of five.
+struct IxOld {
+  uint64_t pp, key;
+  uint32_t pl;
+  uint8_t kind, flags;
+  int64_t size, delts;
+};
+__device__ __forceinline__ void ix_old_load(const IndexArgs& a, uint64_t o, IxOld& r) {
+  r.pp = a.path_ptr[o];
+  r.pl = a.path_len[o];
+  r.kind = a.kind[o];
+  r.flags = a.flags[o];
+  r.key = a.key[o];
+  r.size = a.size[o];
+  r.delts = a.delts[o];
+}
+__device__ __forceinline__ void ix_touch_pre_v(const IndexArgs& a, uint64_t i, uint8_t kind, uint8_t flags, uint64_t key,
+                                               uint64_t pp, uint32_t pl, int64_t size, int64_t delts, IxTouch& T) {
+  if (!((kind == K_ADD || kind == K_REMOVE) && !(flags & F_PATH_NULL))) return;
+  {  // as the final winner (the usual case): contrib_add's terms from registers
+    const unsigned long long top = key >> 32;
+    const int64_t dt = (flags & F_HAS_DELTS) ? delts : 0;
+    const bool add = kind == K_ADD, tomb = !add && dt > a.new_cut;
+    T.own = Contrib{add ? 1ull : 0ull, add ? (unsigned long long)size : 0ull, tomb ? 1ull : 0ull, add ? top : 0ull,
+                    tomb ? top : 0ull};
+    T.own_remove = tomb;
+    T.own_set = true;
+  }
+  const uint64_t s0 = key & a.mask;
+  const uint32_t spec = __hip_atomic_load(a.vals + s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  bool fresh;
+  T.s = ix_insert_cas(a.keys, a.mask, key, &fresh);
+  if (fresh) atomicAdd(a.ctr + IX_C_NEW_SLOTS, 1ull);
+  const uint32_t guess = (uint64_t(T.s) == s0 && !fresh) ? spec : 0u;
+  IxOld r{};
+  if (guess && uint64_t(guess) <= a.lo) ix_old_load(a, uint64_t(guess) - 1, r);
+  T.prev = atomicMax(a.vals + T.s, uint32_t(i + 1));
+  if (T.prev && uint64_t(T.prev) <= a.lo) {
+    const uint64_t o = uint64_t(T.prev) - 1;
+    if (T.prev != guess) ix_old_load(a, o, r);  // another tail action raised the slot first (rare)
+    T.old_bad = !key_equal(reinterpret_cast<const uint8_t*>(pp), pl, reinterpret_cast<const uint8_t*>(r.pp), r.pl);
+    unsigned long long f = 0, sz = 0, rr = 0, lk = 0, tk = 0;
+    const unsigned long long top = r.key >> 32;
+    if (r.kind == K_ADD) {
+      f = 1;
+      sz = (unsigned long long)r.size;
+      lk = top;
+    } else if (((r.flags & F_HAS_DELTS) ? r.delts : 0) > a.old_cut) {
+      rr = 1;
+      tk = top;
+    }
+    T.old = Contrib{0ull - f, 0ull - sz, 0ull - rr, 0ull - lk, 0ull - tk};
+  }
+}
+
+// flush_contrib for one workgroup: per-counter sums in LDS (zeroed by the caller before a barrier),
+// then one global atomic per counter
+__device__ __forceinline__ void flush_contrib_block(const IndexArgs& a, const Contrib& c, unsigned long long files,
+                                                    unsigned long long* sums /* 6, LDS */) {
+  if (c.f) atomicAdd(sums + 0, c.f);
+  if (c.sz) atomicAdd(sums + 1, c.sz);
+  if (c.r) atomicAdd(sums + 2, c.r);
+  if (c.lks) atomicAdd(sums + 3, c.lks);
+  if (c.tks) atomicAdd(sums + 4, c.tks);
+  if (files) atomicAdd(sums + 5, files);
+  __syncthreads();
+  const uint32_t t = threadIdx.x;
+  if (t < 6 && sums[t]) atomicAdd(a.ctr + (t < 5 ? t : uint32_t(IX_C_FILE_ACTIONS)), sums[t]);
+}
+
+__device__ __forceinline__ void ix_delta_post(const IndexArgs& a, uint64_t i, const IxTouch& T, Contrib& c,
+                                              unsigned long long& files) {
+  if (T.s == IX_NONE) return;
+  files = 1;
+  const uint64_t w = uint64_t(__hip_atomic_load(a.vals + T.s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) - 1;
+  if (w != i && !ix_same_path(a, i, w)) atomicOr(a.ctr + IX_C_COLLIDE, 1ull);
+  if (uint64_t(T.prev) <= a.lo) {
+    if (T.old_bad) atomicOr(a.ctr + IX_C_COLLIDE, 1ull);
+    c.f += T.old.f; c.sz += T.old.sz; c.r += T.old.r; c.lks += T.old.lks; c.tks += T.old.tks;
+    bool tomb;
+    if (w == i && T.own_set) {
+      c.f += T.own.f; c.sz += T.own.sz; c.r += T.own.r; c.lks += T.own.lks; c.tks += T.own.tks;
+      tomb = T.own_remove;
+    } else {
+      contrib_add(c, a, w, a.new_cut, false);
+      tomb = a.kind[w] == K_REMOVE && ix_delts(a, w) > a.new_cut;
+    }
+    // both slots claimed before either is written (one round trip)
+    const unsigned long long u = atomicAdd(a.ctr + IX_C_UNDO_FILL, 1ull);
+    const unsigned long long at = tomb ? atomicAdd(a.ctr + IX_C_TOMB_FILL, 1ull) : 0ull;
+    a.undo[u] = make_uint2(uint32_t(i), T.prev);
+    if (tomb) {
+      if (at < a.tomb_cap) a.tomb_list[at] = uint32_t(w);
+      else atomicOr(a.ctr + IX_C_COLLIDE, 2ull);  // host sized the list: never expected
+    }
   }
 }
 }  // namespace dev

@@ -328,7 +328,15 @@ __device__ __forceinline__ uint32_t escape16(uint32_t bs, uint32_t cin, uint32_t
   return (0x5555u ^ ((sum << 1) & 0xFFFFu)) & follows;
 }
 
-__device__ __forceinline__ uint64_t lanes_below() { return (1ull << threadIdx.x) - 1ull; }
+__device__ __forceinline__ uint64_t lanes_below() { return (1ull << wv::lane_id()) - 1ull; }
+
+// Orders one wave's LDS accesses across its lanes (the staged walkers run each wave on its own:
+// a workgroup barrier would wait for waves that never arrive)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 // Value of `v` in the highest lane below this one whose `has` is set, or `dflt` when there is none
 // (an exclusive last-writer scan on DPP).
@@ -342,9 +350,11 @@ __device__ __forceinline__ int32_t from_lower(bool has, int32_t v, int32_t dflt)
 
 // The tape of the region [rb, rb + R) of the stage (R includes the last line's newline). Returns
 // true when every line of the wave is on it (wave-uniform); false sends the wave to the walker.
+// TCap: the tape's tokens, NL: the lines it may hold, SW: the stage's 16-byte words.
+template <uint32_t TCap, uint32_t NL, uint32_t SW>
 __device__ __forceinline__ bool build_tape(const uint4* stage, uint32_t rb, uint32_t R, uint32_t nlines, uint32_t* tape,
                            uint16_t* nltok, uint8_t* tline, unsigned long long* phase = nullptr) {
-  const uint32_t lane = threadIdx.x;
+  const uint32_t lane = wv::lane_id();
   const uint32_t a0 = rb & ~15u;
   const uint32_t skew = rb - a0;
   const uint32_t total = skew + R;
@@ -356,7 +366,7 @@ __device__ __forceinline__ bool build_tape(const uint4* stage, uint32_t rb, uint
     const uint32_t wpos = (s << 10) + (lane << 4);
     const int32_t lo = int32_t(wpos) - int32_t(skew);  // region offset of the window's byte 0
     // unconditional (clamped) stage read and masks: a guarded read is a branch
-    const uint4 v = stage[min((a0 + wpos) >> 4, JL_STAGE_BYTES / 16 - 1)];
+    const uint4 v = stage[min((a0 + wpos) >> 4, SW - 1)];
     const uint32_t keep = wpos < total ? ~0u : 0u;
     const uint32_t w[4] = {v.x & keep, v.y & keep, v.z & keep, v.w & keep};
     const uint32_t vlo = lo < 0 ? (0xFFFFu << uint32_t(min(-lo, 16))) & 0xFFFFu : 0xFFFFu;
@@ -412,7 +422,7 @@ __device__ __forceinline__ bool build_tape(const uint4* stage, uint32_t rb, uint
     const uint32_t incl = wv::scan_incl(cnt, 0u, [](uint32_t e, uint32_t l) { return e + l; });
     const uint32_t tot = uint32_t(__builtin_amdgcn_readlane(int(incl), 63));
     if (__ballot(bad)) return false;
-    if (tbase + (tot & 0xFFFFu) > TAPE_CAP || nlc + (tot >> 16) > uint32_t(JL_T)) return false;
+    if (tbase + (tot & 0xFFFFu) > TCap || nlc + (tot >> 16) > NL) return false;
     uint32_t idx = tbase + ((incl - cnt) & 0xFFFFu);
     uint32_t nlr = nlc + ((incl - cnt) >> 16);
     bool longstr = false;
@@ -439,7 +449,7 @@ __device__ __forceinline__ bool build_tape(const uint4* stage, uint32_t rb, uint
       const uint32_t otok = (pos << 16) | ((st & bit) ? scls : (sc_begin & bit) ? jl::T_SCALAR : T_NL);
       tline[idx] = uint8_t(nlr);
       const bool isnl = (nl & bit) != 0;
-      nltok[isnl ? nlr : uint32_t(JL_T)] = uint16_t(idx);  // slot JL_T: a sink for the other tokens
+      nltok[isnl ? nlr : NL] = uint16_t(idx);  // slot NL: a sink for the other tokens
       nlr += isnl ? 1u : 0u;
       tape[idx++] = isclose ? stok : otok;
     }
@@ -476,10 +486,11 @@ __device__ __forceinline__ bool build_tape(const uint4* stage, uint32_t rb, uint
 // General walker (k_json_hard / k_tail_post), which decides every line exactly: the deferral needs no
 // K_ERROR logic here, and lines the tape accepts are decided as the DFA decides them.
 constexpr uint32_t TW_LEVELS = 7;  // container levels the type scan tracks (deeper: General walker)
+template <uint32_t NL>
 struct TapeAgg {
-  int32_t mem[JL_T][8];      // per line and action kind: last top-level member's value token * 2 + non-null
-  int32_t fld[JL_T][2][4];   // per line, add / remove: last path / size / deletionTimestamp value token * 2 + non-null
-  uint32_t defer[JL_T];
+  int32_t mem[NL][8];      // per line and action kind: last top-level member's value token * 2 + non-null
+  int32_t fld[NL][2][4];   // per line, add / remove: last path / size / deletionTimestamp value token * 2 + non-null
+  uint32_t defer[NL];
 };
 
 __device__ __forceinline__ uint32_t type_combine(uint32_t early, uint32_t late) {
@@ -553,18 +564,21 @@ __device__ __forceinline__ uint8_t scalar_tape(const uint32_t w0[5], uint32_t L,
        : (isint && fits) ? jl::SC_INT : jl::SC_BAD;
 }
 
+template <uint32_t TCap, uint32_t NL>
 __device__ __forceinline__ void tape_lines(const JsonParseArgs& a, uint64_t line0, uint32_t nlines, const uint8_t* sp,
                                            uint64_t gb, const uint32_t* tape, const uint16_t* nltok, const uint8_t* tline,
-                                           TapeAgg& g) {
-  const uint32_t lane = threadIdx.x;
+                                           TapeAgg<NL>& g) {
+  const uint32_t lane = wv::lane_id();
   const uint64_t tw0 = a.phase ? __builtin_amdgcn_s_memtime() : 0;
+  if (lane < NL) {
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    g.mem[lane][k] = -1;
-    g.fld[lane][k >> 2][k & 3] = -1;
+    for (int k = 0; k < 8; ++k) {
+      g.mem[lane][k] = -1;
+      g.fld[lane][k >> 2][k & 3] = -1;
+    }
+    g.defer[lane] = 0;
   }
-  g.defer[lane] = 0;
-  __syncthreads();
+  wave_sync();
   const uint32_t ntok = uint32_t(nltok[nlines - 1]) + 1u;
   int32_t dcarry = 0, ocarry = -1;
   uint32_t tcarry = 0, ptail1 = T_NL, ptail2 = T_NL;  // the previous round's last two tokens
@@ -572,8 +586,8 @@ __device__ __forceinline__ void tape_lines(const JsonParseArgs& a, uint64_t line
     const uint32_t i = r0 + lane;
     const bool in = i < ntok;
     // unconditional reads (clamped into the arrays): a guarded LDS read is a branch
-    const uint32_t tk = tape[min(i, TAPE_CAP - 1)], nx = tape[min(i + 1, TAPE_CAP - 1)];
-    const uint32_t tl = tline[min(i, TAPE_CAP - 1)];
+    const uint32_t tk = tape[min(i, TCap - 1)], nx = tape[min(i + 1, TCap - 1)];
+    const uint32_t tl = tline[min(i, TCap - 1)];
     const uint32_t tok = in ? tk : 15u;
     const uint32_t nxt = i + 1 < ntok ? nx : tok;
     const uint32_t line = in ? tl : 0u;
@@ -652,7 +666,7 @@ __device__ __forceinline__ void tape_lines(const JsonParseArgs& a, uint64_t line
     if (in & !(okv & !bad1 & !badf)) g.defer[line] = 1u;
     if (a.phase && r0 == 0 && lane == 0) atomicAdd(&a.phase[5], (unsigned long long)(__builtin_amdgcn_s_memtime() - tw0));
   }
-  __syncthreads();
+  wave_sync();
   if (a.phase && lane == 0) atomicAdd(&a.phase[3], (unsigned long long)(__builtin_amdgcn_s_memtime() - tw0));
   if (lane >= nlines) return;
   const uint64_t line = line0 + lane;
@@ -714,7 +728,7 @@ __global__ void __launch_bounds__(JL_T, DR_JL_WAVES) k_json_lines(JsonParseArgs 
   __shared__ uint32_t tape[Stage ? TAPE_CAP : 1];
   __shared__ uint16_t nltok[Stage ? JL_T + 1 : 1];
   __shared__ uint8_t tline[Stage ? TAPE_CAP : 1];
-  __shared__ std::conditional_t<Stage, TapeAgg, uint32_t> agg;
+  __shared__ std::conditional_t<Stage, TapeAgg<JL_T>, uint32_t> agg;
   const uint32_t lane = threadIdx.x;
   const uint64_t line = uint64_t(blockIdx.x) * JL_T + lane;
   const bool live = line < a.nlines;
@@ -736,7 +750,7 @@ __global__ void __launch_bounds__(JL_T, DR_JL_WAVES) k_json_lines(JsonParseArgs 
       __syncthreads();
       phase(0);
       const uint32_t nw = uint32_t(a.nlines);
-      const bool taped = build_tape(stage, 0u, len, nw, tape, nltok, tline, a.phase);
+      const bool taped = build_tape<TAPE_CAP, JL_T, JL_STAGE_BYTES / 16>(stage, 0u, len, nw, tape, nltok, tline, a.phase);
       phase(1);
       __syncthreads();
       if (taped) {
@@ -745,7 +759,7 @@ __global__ void __launch_bounds__(JL_T, DR_JL_WAVES) k_json_lines(JsonParseArgs 
           a.off2[0] = 0;
           a.off2[1] = nw;
         }
-        tape_lines(a, 0, nw, reinterpret_cast<const uint8_t*>(stage), 0, tape, nltok, tline, agg);
+        tape_lines<TAPE_CAP, JL_T>(a, 0, nw, reinterpret_cast<const uint8_t*>(stage), 0, tape, nltok, tline, agg);
         phase(2);
         if (a.phase && lane == 0) atomicAdd(&a.phase[4], 1ull);
         return;
@@ -792,11 +806,12 @@ __global__ void __launch_bounds__(JL_T, DR_JL_WAVES) k_json_lines(JsonParseArgs 
       phase(0);
       const uint32_t nw = uint32_t(last - first + 1);
       const uint64_t rb = first == 0 ? 0 : a.nl[first - 1] + 1;  // the wave's first line
-      const bool taped = build_tape(stage, uint32_t(rb - r0), uint32_t(a.nl[last] + 1 - rb), nw, tape, nltok, tline, a.phase);
+      const bool taped = build_tape<TAPE_CAP, JL_T, JL_STAGE_BYTES / 16>(stage, uint32_t(rb - r0), uint32_t(a.nl[last] + 1 - rb), nw,
+                                                                       tape, nltok, tline, a.phase);
       phase(1);
       if (taped) {
         __syncthreads();
-        tape_lines(a, first, nw, reinterpret_cast<const uint8_t*>(stage) + (rb - r0), rb, tape, nltok, tline, agg);
+        tape_lines<TAPE_CAP, JL_T>(a, first, nw, reinterpret_cast<const uint8_t*>(stage) + (rb - r0), rb, tape, nltok, tline, agg);
         phase(2);
         if (a.phase && lane == 0) atomicAdd(&a.phase[4], 1ull);
         return;
@@ -837,7 +852,10 @@ __global__ void __launch_bounds__(64) k_json_hard(JsonParseArgs a) {
 // one launch instead of two for a streamed commit, whose kernels each cost a launch and a cold
 // start rather than their work.
 __device__ __forceinline__ void tail_post_body(const JsonParseArgs& a, const CanonArgs& c) {
-  const uint64_t cnt = *a.hard_count;
+  // an atomic load: in k_apply_commit the count was raised by this workgroup's atomics (at L2)
+  const uint64_t cnt = __hip_atomic_load(a.hard_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // special paths so far (the walk's; the General walker's lines add theirs below)
+  const uint64_t nsp0 = __hip_atomic_load(a.special_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   for (uint64_t k = threadIdx.x; k < cnt; k += blockDim.x) {
     const uint64_t line = a.hard_idx[k];
     const uint64_t b = line == 0 ? 0 : a.nl[line - 1] + 1;
@@ -847,6 +865,7 @@ __device__ __forceinline__ void tail_post_body(const JsonParseArgs& a, const Can
     jl::parse_line_general(gp, n, o);
     emit_line(a, line, b, n, gp, gp, o);
   }
+  if (!cnt && !nsp0) return;  // nothing to canonicalise (uniform: the loads are the workgroup's)
   __threadfence_block();
   __syncthreads();
   for (uint64_t i = threadIdx.x; i < c.n; i += blockDim.x) canon_one(c, i);
@@ -858,36 +877,155 @@ __global__ void __launch_bounds__(256) k_tail_post(JsonParseArgs a, CanonArgs c)
 // deferred lines and canonicalisation, the append to the chain store (k_append_actions) with the
 // index counters' reset, and the index's two passes (k_ix_touch_delta), each step behind a fence
 // and a barrier -- one launch where three followed each other, each with its dispatch and cold start.
-__global__ void __launch_bounds__(IX_T) k_apply_small(JsonParseArgs a, CanonArgs c, AppendArgs p, IndexArgs x) {
+__device__ __forceinline__ void apply_small_body(const JsonParseArgs& a, const CanonArgs& c, const AppendArgs& p,
+                                                 const IndexArgs& x, bool ctr_set) {
   const uint32_t t = threadIdx.x;
+  __shared__ unsigned long long sums[6];
+  if (t < 6) sums[t] = 0;  // ordered before their use by the next barrier
+  if (!ctr_set) {  // (k_apply_commit clears them with the parse counters)
+    if (t < p.nctr) p.ctr[t] = t == p.ctr_at ? p.ctr_val : 0ull;
+    __threadfence();
+    __syncthreads();
+  }
+  uint64_t tp0 = a.phase ? __builtin_amdgcn_s_memtime() : 0;
+  auto phase = [&](int k) {  // DR_JSON_PHASES (k_apply_commit): 8 post-parse, 9 append, 10 touch, 11 delta
+    if (!a.phase) return;
+    const uint64_t tn = __builtin_amdgcn_s_memtime();
+    if (t == 0) atomicAdd(&a.phase[k], (unsigned long long)(tn - tp0));
+    tp0 = tn;
+  };
   if (a.hard_count) {
     tail_post_body(a, c);
     __threadfence();
     __syncthreads();
   }
-  if (t < p.nctr) p.ctr[t] = t == p.ctr_at ? p.ctr_val : 0ull;
+  phase(8);
+  // the append: each thread its own action, whose fields pass 1 then takes from registers (no
+  // barrier: pass 2, which reads other threads' actions, follows the next one)
+  const uint64_t i = x.lo + t;
+  IxTouch T;
   if (t < p.n) {
-    p.dst.kind[t] = p.src.kind[t];
-    p.dst.flags[t] = p.src.flags[t];
-    p.dst.key[t] = p.src.key[t];
-    p.dst.path_ptr[t] = p.src.path_ptr[t];
-    p.dst.path_len[t] = p.src.path_len[t];
-    p.dst.size[t] = p.src.size[t];
-    p.dst.delts[t] = p.src.delts[t];
+    const uint8_t kind = p.src.kind[t], flags = p.src.flags[t];
+    const uint64_t key = p.src.key[t], pp = p.src.path_ptr[t];
+    const uint32_t pl = p.src.path_len[t];
+    const int64_t size = p.src.size[t], delts = p.src.delts[t];
+    p.dst.kind[t] = kind;
+    p.dst.flags[t] = flags;
+    p.dst.key[t] = key;
+    p.dst.path_ptr[t] = pp;
+    p.dst.path_len[t] = pl;
+    p.dst.size[t] = size;
+    p.dst.delts[t] = delts;
     p.dst.src_off[t] = p.src.src_off[t];
     p.dst.src_len[t] = p.src.src_len[t];
     p.src_id[t] = p.sid;
+    phase(9);
+    if (i < x.hi) ix_touch_pre_v(x, i, kind, flags, key, pp, pl, size, delts, T);
   }
   __threadfence();
   __syncthreads();
-  const uint64_t i = x.lo + t;
-  if (i < x.hi) ix_touch_one(x, i);
-  __threadfence();
-  __syncthreads();
+  phase(10);
   Contrib cc{0, 0, 0, 0, 0};
   unsigned long long files = 0;
-  if (i < x.hi) ix_delta_one(x, i, cc, files);
-  flush_contrib(x, cc, files);
+  if (i < x.hi) ix_delta_post(x, i, T, cc, files);
+  flush_contrib_block(x, cc, files, sums);
+  if (a.phase) {
+    __syncthreads();
+    phase(11);
+  }
+}
+
+__global__ void __launch_bounds__(IX_T) k_apply_small(JsonParseArgs a, CanonArgs c, AppendArgs p, IndexArgs x) {
+  apply_small_body(a, c, p, x, false);
+}
+
+// A streamed commit's whole apply in one workgroup of four waves (launch_apply_commit): the
+// commit's bytes staged in LDS once, its newline index (wave 0), then each wave builds the token
+// tape of its quarter of the lines and walks it (the small-segment walker of k_json_lines<true>, on
+// wave-private tapes), and after a barrier the rest of the apply (apply_small_body). Four waves
+// split the walk that one wave did serially, and the parse, post-parse, append and index passes are
+// one dispatch.
+constexpr uint32_t AC_WAVES = 8;  // the walk's waves (the apply after it uses the first IX_T threads)
+constexpr uint32_t AC_LINES = (JSON_FUSE_MAX_LINES + AC_WAVES - 1) / AC_WAVES;  // lines per wave
+constexpr uint32_t AC_TCAP = 1024;                                            // tape tokens per wave
+constexpr uint32_t AC_SW = JSON_BYTES_PER_BLOCK / 16 + 4;                      // one index block + pad
+__global__ void __launch_bounds__(AC_WAVES * 64) k_apply_commit(JsonParseArgs a, CanonArgs c, AppendArgs p, IndexArgs x) {
+  __shared__ uint4 stage[AC_SW];
+  __shared__ uint32_t tape[AC_WAVES][AC_TCAP];
+  __shared__ uint8_t tline[AC_WAVES][AC_TCAP];
+  __shared__ uint16_t nltok[AC_WAVES][AC_LINES + 1];
+  __shared__ TapeAgg<AC_LINES> agg[AC_WAVES];
+  __shared__ uint32_t nlpos[JSON_FUSE_MAX_LINES];
+  const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
+  const uint32_t len = uint32_t(a.buf_len), nlines = uint32_t(a.nlines);
+  uint64_t tp0 = a.phase ? __builtin_amdgcn_s_memtime() : 0;
+  auto phase = [&](int k) {  // DR_JSON_PHASES: 0 stage, 1 newline index, 2 walk, 6 apply (slot 4: calls)
+    if (!a.phase) return;
+    const uint64_t tn = __builtin_amdgcn_s_memtime();
+    if (t == 0) atomicAdd(&a.phase[k], (unsigned long long)(tn - tp0));
+    tp0 = tn;
+  };
+  if (t < a.nzero) a.zero[t] = 0;
+  if (t < p.nctr) p.ctr[t] = t == p.ctr_at ? p.ctr_val : 0ull;  // the index counters (apply_small_body)
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(a.buf);
+    const uint32_t nq = min(((len + 15u) >> 4) + 3u, AC_SW);
+    for (uint32_t k = t; k < nq; k += AC_WAVES * 64) stage[k] = src[k];
+  }
+  __threadfence();  // the cleared counters reach L2 before any atomic on them
+  __syncthreads();
+  phase(0);
+  if (w == 0) {  // the newline index: LDS for the waves, nl for the General walker
+    uint32_t base = 0;
+    for (uint32_t s0 = 0; s0 < len; s0 += 16u * 64u) {
+      const uint32_t wpos = s0 + 16u * lane;
+      const uint4 v = stage[min(wpos >> 4, AC_SW - 1)];
+      const uint32_t ww[4] = {v.x, v.y, v.z, v.w};
+      uint32_t m = 0;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) m |= jl::gather4(jl::zbytes(ww[d] ^ 0x0a0a0a0au)) << (4 * d);
+      const int32_t rem = int32_t(len) - int32_t(wpos);
+      m &= rem >= 16 ? 0xFFFFu : rem <= 0 ? 0u : (1u << uint32_t(rem)) - 1u;
+      const uint32_t cnt = __builtin_popcount(m);
+      const uint32_t incl = wv::scan_incl(cnt, 0u, [](uint32_t e, uint32_t l) { return e + l; });
+      uint32_t r = base + incl - cnt;
+      while (m) {
+        const uint32_t pos = wpos + jl::ctz32(m);
+        if (r < JSON_FUSE_MAX_LINES) nlpos[r] = pos;
+        a.nl_out[r++] = pos;
+        m &= m - 1;
+      }
+      base += wv::last_uniform(incl);
+    }
+    if (lane == 0) {
+      a.off2[0] = 0;
+      a.off2[1] = base;
+    }
+  }
+  __syncthreads();
+  phase(1);
+  const uint32_t per = (nlines + AC_WAVES - 1) / AC_WAVES;  // lines per wave (<= AC_LINES)
+  const uint32_t l0 = w * per, l1 = min(l0 + per, nlines);
+  if (l0 < l1) {
+    const uint32_t nw = l1 - l0;
+    const uint32_t rb = l0 ? nlpos[l0 - 1] + 1u : 0u;
+    const uint32_t R = nlpos[l1 - 1] + 1u - rb;
+    const bool taped = build_tape<AC_TCAP, AC_LINES, AC_SW>(stage, rb, R, nw, tape[w], nltok[w], tline[w]);
+    wave_sync();
+    if (taped) {
+      tape_lines<AC_TCAP, AC_LINES>(a, l0, nw, reinterpret_cast<const uint8_t*>(stage) + rb, rb, tape[w], nltok[w],
+                                    tline[w], agg[w]);
+    } else if (lane < nw) {  // off the tape: the General walker (apply_small_body) decides these lines
+      const unsigned long long k = atomicAdd(a.hard_count, 1ull);
+      a.hard_idx[k] = l0 + lane;
+    }
+  }
+  __threadfence();
+  __syncthreads();
+  phase(2);
+  apply_small_body(a, c, p, x, true);
+  phase(6);
+  if (a.phase && t == 0) atomicAdd(&a.phase[4], 1ull);
 }
 
 }  // namespace dev
@@ -931,6 +1069,11 @@ void launch_apply_small(const JsonParseArgs* ja, const CanonArgs& cg, const Appe
                         hipStream_t st) {
   JsonParseArgs none{};
   DR_LAUNCH(dev::k_apply_small, dim3(1), dim3(dev::IX_T), 0, st, ja ? *ja : none, cg, ap, ix);
+}
+
+void launch_apply_commit(const JsonParseArgs& ja, const CanonArgs& cg, const AppendArgs& ap, const IndexArgs& ix,
+                         hipStream_t st) {
+  DR_LAUNCH(dev::k_apply_commit, dim3(1), dim3(dev::AC_WAVES * 64), 0, st, ja, cg, ap, ix);
 }
 
 void launch_json_hard(const JsonParseArgs& a, hipStream_t st) {

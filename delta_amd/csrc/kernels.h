@@ -623,6 +623,10 @@ void launch_ix_expire(const IndexArgs& a, uint64_t n_list, hipStream_t st, const
 constexpr uint64_t APPLY_SMALL_MAX = 256;
 void launch_apply_small(const JsonParseArgs* ja, const CanonArgs& cg, const AppendArgs& ap, const IndexArgs& ix,
                         hipStream_t st);
+// ... and the line walk itself, for a segment of one wave (ja in the fused-index form: zero, off2,
+// nl_out given; JSON_FUSE_MAX_LINES lines in one index block): the whole apply in one launch
+void launch_apply_commit(const JsonParseArgs& ja, const CanonArgs& cg, const AppendArgs& ap, const IndexArgs& ix,
+                         hipStream_t st);
 void launch_ix_tomb_compact(const IndexArgs& a, const uint32_t* list_in, uint64_t n, uint32_t* list_out,
                             hipStream_t st);
 void launch_ix_undo(const IndexArgs& a, uint32_t* vals_out, const uint2* undo, uint64_t n, hipStream_t st);

@@ -47,3 +47,16 @@ def test_k_json_lines_has_no_scratch_and_no_flat_access(k_json_asm, staged):
     assert not flat, flat[:5]
     if staged:
         assert re.search(r"\bds_read", body)  # the stage is read from LDS
+
+
+def test_apply_commit_reads_its_stage_and_tapes_from_lds(k_json_asm):
+    """k_apply_commit (a streamed commit's whole apply in one workgroup) walks wave-private tapes
+    over an LDS stage like the staged walker: it has no flat access beyond those of k_apply_small,
+    the same apply without the walk (byte reads through path pointers, which are global)."""
+    name = "_ZN2dr3dev14k_apply_commitENS_13JsonParseArgsENS_9CanonArgsENS_10AppendArgsENS_9IndexArgsE"
+    small = "_ZN2dr3dev13k_apply_smallENS_13JsonParseArgsENS_9CanonArgsENS_10AppendArgsENS_9IndexArgsE"
+    body, _ = _kernel(k_json_asm, name)
+    ref, _ = _kernel(k_json_asm, small)
+    flat = len(re.findall(r"^\s*flat_\w+", body, re.M))
+    assert flat <= len(re.findall(r"^\s*flat_\w+", ref, re.M)), flat
+    assert re.search(r"\bds_read", body)

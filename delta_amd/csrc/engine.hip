@@ -561,7 +561,7 @@ struct IncChain {
   uint64_t tcap = 0, used = 0;  // table slots (power of two), occupied slots
   DBuf<unsigned long long> keys;
   DBuf<uint32_t> vals;
-  DBuf<uint32_t> tomb_list;  // tombstone candidates of the head (stale entries are skipped)
+  DBuf<ulonglong2> tomb_list;  // tombstone candidates of the head, {action, deletionTimestamp} (stale entries are skipped)
   uint64_t tomb_n = 0, tomb_cap = 0;
   struct Undo {
     DBuf<uint2> e;
@@ -2245,7 +2245,7 @@ static dr_state* apply_incremental(dr_ctx* ctx, dr_state& base, const std::share
   k.version = version;
   // the head's tombstone candidates, compacted once they are mostly stale
   if (c.tomb_n > 2 * uint64_t(k.num_removes) + (uint64_t(1) << 16)) {
-    DBuf<uint32_t> nl(ctx, c.tomb_cap);
+    DBuf<ulonglong2> nl(ctx, c.tomb_cap);
     HIP_OK(hipMemsetAsync(c.ctr.p + IX_C_TOMB_FILL, 0, 8, stream));
     IndexArgs b = ix_args(c);
     b.new_cut = cutoff;

@@ -103,9 +103,9 @@ __device__ inline void flush_contrib(const IndexArgs& a, Contrib c, unsigned lon
   }
 }
 
-__device__ __forceinline__ void tomb_append(const IndexArgs& a, uint64_t x) {
+__device__ __forceinline__ void tomb_append(const IndexArgs& a, uint64_t x, int64_t dt) {
   const unsigned long long at = atomicAdd(a.ctr + IX_C_TOMB_FILL, 1ull);
-  if (at < a.tomb_cap) a.tomb_list[at] = uint32_t(x);
+  if (at < a.tomb_cap) a.tomb_list[at] = make_ulonglong2(x, (unsigned long long)dt);
   else atomicOr(a.ctr + IX_C_COLLIDE, 2ull);  // host sized the list: never expected
 }
 
@@ -141,7 +141,10 @@ __device__ __forceinline__ void ix_delta_one(const IndexArgs& a, uint64_t i, Con
       contrib_add(c, a, o, a.old_cut, true);
     }
     contrib_add(c, a, w, a.new_cut, false);
-    if (a.kind[w] == K_REMOVE && ix_delts(a, w) > a.new_cut) tomb_append(a, w);
+    if (a.kind[w] == K_REMOVE) {
+      const int64_t dt = ix_delts(a, w);
+      if (dt > a.new_cut) tomb_append(a, w, dt);
+    }
     const unsigned long long u = atomicAdd(a.ctr + IX_C_UNDO_FILL, 1ull);
     a.undo[u] = make_uint2(uint32_t(i), prev);
   }
@@ -156,6 +159,7 @@ struct IxTouch {
   Contrib old{0, 0, 0, 0, 0};
   Contrib own{0, 0, 0, 0, 0};  // this action's own contribution as a winner (ix_touch_pre_v)
   bool own_remove = false, own_set = false;
+  int64_t own_dt = 0;
 };
 __device__ __forceinline__ void ix_touch_pre(const IndexArgs& a, uint64_t i, IxTouch& T) {
   if (!ix_file_action(a, i)) return;
@@ -198,6 +202,7 @@ __device__ __forceinline__ void ix_touch_pre_v(const IndexArgs& a, uint64_t i, u
     T.own = Contrib{add ? 1ull : 0ull, add ? (unsigned long long)size : 0ull, tomb ? 1ull : 0ull, add ? top : 0ull,
                     tomb ? top : 0ull};
     T.own_remove = tomb;
+    T.own_dt = dt;
     T.own_set = true;
   }
   const uint64_t s0 = key & a.mask;
@@ -252,19 +257,22 @@ __device__ __forceinline__ void ix_delta_post(const IndexArgs& a, uint64_t i, co
     if (T.old_bad) atomicOr(a.ctr + IX_C_COLLIDE, 1ull);
     c.f += T.old.f; c.sz += T.old.sz; c.r += T.old.r; c.lks += T.old.lks; c.tks += T.old.tks;
     bool tomb;
+    int64_t dt;
     if (w == i && T.own_set) {
       c.f += T.own.f; c.sz += T.own.sz; c.r += T.own.r; c.lks += T.own.lks; c.tks += T.own.tks;
       tomb = T.own_remove;
+      dt = T.own_dt;
     } else {
       contrib_add(c, a, w, a.new_cut, false);
-      tomb = a.kind[w] == K_REMOVE && ix_delts(a, w) > a.new_cut;
+      dt = ix_delts(a, w);
+      tomb = a.kind[w] == K_REMOVE && dt > a.new_cut;
     }
     // both slots claimed before either is written (one round trip)
     const unsigned long long u = atomicAdd(a.ctr + IX_C_UNDO_FILL, 1ull);
     const unsigned long long at = tomb ? atomicAdd(a.ctr + IX_C_TOMB_FILL, 1ull) : 0ull;
     a.undo[u] = make_uint2(uint32_t(i), T.prev);
     if (tomb) {
-      if (at < a.tomb_cap) a.tomb_list[at] = uint32_t(w);
+      if (at < a.tomb_cap) a.tomb_list[at] = make_ulonglong2(w, (unsigned long long)dt);
       else atomicOr(a.ctr + IX_C_COLLIDE, 2ull);  // host sized the list: never expected
     }
   }

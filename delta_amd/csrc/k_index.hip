@@ -26,7 +26,7 @@ __global__ void __launch_bounds__(IX_T) k_ix_build(IndexArgs a) {
   }
   atomicAdd(a.ctr + IX_C_NEW_SLOTS, 1ull);
   a.vals[s] = uint32_t(i + 1);
-  if (a.kind[i] == K_REMOVE) tomb_append(a, i);
+  if (a.kind[i] == K_REMOVE) tomb_append(a, i, ix_delts(a, i));
 }
 
 __global__ void __launch_bounds__(IX_T) k_ix_touch(IndexArgs a) {
@@ -61,9 +61,10 @@ __global__ void __launch_bounds__(IX_T) k_ix_expire(IndexArgs a, uint64_t n, Rea
   const uint64_t j = uint64_t(blockIdx.x) * IX_T + threadIdx.x;
   Contrib c{0, 0, 0, 0, 0};
   if (j < n) {
-    const uint64_t x = a.tomb_list[j];
+    const ulonglong2 e = a.tomb_list[j];
+    const uint64_t x = e.x;
+    const int64_t dt = int64_t(e.y);
     if (x < a.lo) {  // this apply's own tombstones were counted at the new cutoff
-      const int64_t dt = ix_delts(a, x);
       if (dt > a.old_cut && dt <= a.new_cut) {
         const uint32_t s = ix_find(a.keys, a.mask, a.key[x]);
         if (s != IX_NONE && a.vals[s] == uint32_t(x + 1)) {
@@ -92,15 +93,17 @@ __global__ void __launch_bounds__(IX_T) k_ix_expire(IndexArgs a, uint64_t n, Rea
 }
 
 // Keep the candidates that are still tombstones of the head at its cutoff (a.new_cut).
-__global__ void __launch_bounds__(IX_T) k_ix_tomb_compact(IndexArgs a, const uint32_t* in, uint64_t n, uint32_t* out) {
+__global__ void __launch_bounds__(IX_T) k_ix_tomb_compact(IndexArgs a, const ulonglong2* in, uint64_t n,
+                                                          ulonglong2* out) {
   const uint64_t j = uint64_t(blockIdx.x) * IX_T + threadIdx.x;
   if (j >= n) return;
-  const uint64_t x = in[j];
-  if (ix_delts(a, x) <= a.new_cut) return;
+  const ulonglong2 e = in[j];
+  const uint64_t x = e.x;
+  if (int64_t(e.y) <= a.new_cut) return;
   const uint32_t s = ix_find(a.keys, a.mask, a.key[x]);
   if (s == IX_NONE || a.vals[s] != uint32_t(x + 1)) return;
   const unsigned long long at = atomicAdd(a.ctr + IX_C_TOMB_FILL, 1ull);
-  out[at] = uint32_t(x);
+  out[at] = e;
 }
 
 // Revert one apply on a copy of the values: its first touches restore the slots' previous values.
@@ -167,7 +170,7 @@ void launch_ix_expire(const IndexArgs& a, uint64_t n, hipStream_t st, const Read
   ReadbackArgs none{};
   if (n) DR_LAUNCH(dev::k_ix_expire, dim3(ix_grid(n)), dim3(dev::IX_T), 0, st, a, n, rb ? *rb : none);
 }
-void launch_ix_tomb_compact(const IndexArgs& a, const uint32_t* in, uint64_t n, uint32_t* out, hipStream_t st) {
+void launch_ix_tomb_compact(const IndexArgs& a, const ulonglong2* in, uint64_t n, ulonglong2* out, hipStream_t st) {
   if (n) DR_LAUNCH(dev::k_ix_tomb_compact, dim3(ix_grid(n)), dim3(dev::IX_T), 0, st, a, in, n, out);
 }
 void launch_ix_undo(const IndexArgs& a, uint32_t* vals, const uint2* undo, uint64_t n, hipStream_t st) {

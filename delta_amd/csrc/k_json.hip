@@ -204,8 +204,8 @@ constexpr int JL_TOKCAP = DR_JL_TOKCAP;
 #endif
 constexpr int JL_FLUSH = DR_JL_FLUSH;
 
-#ifndef DR_JL_PAIR
-#define DR_JL_PAIR 1  // sweep r01: 2.86 -> 2.77 ms, 12.14 -> 11.98 ms/step same box
+#ifndef DR_JL_BATCH
+#define DR_JL_BATCH 2  // windows per load batch; 2 (pairs) sweep r01: 2.86 -> 2.77 ms, 12.14 -> 11.98 ms/step same box
 #endif
 #ifndef DR_JL_WAVES
 #define DR_JL_WAVES 1
@@ -235,8 +235,8 @@ __device__ __forceinline__ void walk_line(const JsonParseArgs& a, uint32_t* tokb
   const uint8_t* base = p - o0;
   const uint32_t nwin = tz.status == jl::ST_OK ? (o0 + n + 15) >> 4 : 0;
   uint32_t nt = 0;
-#if DR_JL_PAIR
-  uint4 pair_hi = make_uint4(0, 0, 0, 0);
+#if DR_JL_BATCH > 1
+  uint4 batch[DR_JL_BATCH];
 #endif
   auto push = [&](uint32_t t) {
     tokbuf[nt * JL_T + lane] = t;
@@ -245,17 +245,19 @@ __device__ __forceinline__ void walk_line(const JsonParseArgs& a, uint32_t* tokb
   for (uint32_t j = 0;; ++j) {
     if (j < nwin && tz.status == jl::ST_OK) {
       uint32_t w[4];
-#if DR_JL_PAIR
-      // windows in pairs: one 32 B request per two windows (the line's cache lines are asked for
-      // half as often while other waves compete for L2)
-      if ((j & 1u) == 0) {
+#if DR_JL_BATCH > 1
+      // windows in batches: DR_JL_BATCH consecutive 16 B requests per lane issued together (the
+      // line's cache lines are asked for while still resident, other waves competing for L2)
+      if (j % DR_JL_BATCH == 0) {
         const uint4* q = reinterpret_cast<const uint4*>(base + 16u * j);
-        const uint4 v0 = q[0];
-        pair_hi = j + 1 < nwin ? q[1] : make_uint4(0, 0, 0, 0);
-        w[0] = v0.x; w[1] = v0.y; w[2] = v0.z; w[3] = v0.w;
-      } else {
-        w[0] = pair_hi.x; w[1] = pair_hi.y; w[2] = pair_hi.z; w[3] = pair_hi.w;
+#pragma unroll
+        for (int k = 0; k < DR_JL_BATCH; ++k) batch[k] = j + k < nwin ? q[k] : make_uint4(0, 0, 0, 0);
       }
+      uint4 v0 = batch[0];
+#pragma unroll
+      for (int k = 1; k < DR_JL_BATCH; ++k)
+        if (j % DR_JL_BATCH == uint32_t(k)) v0 = batch[k];
+      w[0] = v0.x; w[1] = v0.y; w[2] = v0.z; w[3] = v0.w;
 #else
       jl::load_window(base + 16u * j, w);
 #endif

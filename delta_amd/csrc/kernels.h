@@ -603,7 +603,8 @@ struct IndexArgs {
   uint32_t* t_prev;          // per action: the slot's value before it (atomicMax)
   int64_t old_cut, new_cut;  // retention cutoffs of the base and the new state
   unsigned long long* ctr;   // IX_C_* counters
-  uint32_t* tomb_list;       // tombstone candidates (action indices), appended at ctr[IX_C_TOMB_FILL]
+  ulonglong2* tomb_list;     // tombstone candidates {action index, deletionTimestamp}, appended at
+                             // ctr[IX_C_TOMB_FILL] (the timestamp inline: the expiry's filter is one load)
   uint64_t tomb_cap;
   uint2* undo;               // first touches of this apply: {action, previous value}
 };
@@ -627,7 +628,7 @@ void launch_apply_small(const JsonParseArgs* ja, const CanonArgs& cg, const Appe
 // nl_out given; JSON_FUSE_MAX_LINES lines in one index block): the whole apply in one launch
 void launch_apply_commit(const JsonParseArgs& ja, const CanonArgs& cg, const AppendArgs& ap, const IndexArgs& ix,
                          hipStream_t st);
-void launch_ix_tomb_compact(const IndexArgs& a, const uint32_t* list_in, uint64_t n, uint32_t* list_out,
+void launch_ix_tomb_compact(const IndexArgs& a, const ulonglong2* list_in, uint64_t n, ulonglong2* list_out,
                             hipStream_t st);
 void launch_ix_undo(const IndexArgs& a, uint32_t* vals_out, const uint2* undo, uint64_t n, hipStream_t st);
 void launch_ix_classify(const IndexArgs& a, const uint32_t* vals, uint64_t cap, int64_t cutoff, uint32_t* live_flag,

@@ -552,12 +552,15 @@ def test_checkpoint_writer_table_options(engine, tmp_path):
     DeltaLog.clear_cache()
 
 
-def test_incremental_apply_random_commits(engine, tmp_path):
+@pytest.mark.parametrize("compact", [False, True])
+def test_incremental_apply_random_commits(engine, tmp_path, compact):
     """Property test of the O(tail) apply: 40 random commits -- new adds, re-adds, removes of live,
     removed and never-seen paths, the same path twice in one commit in either order, absolute /
     `file:` / escaped paths naming the same file, metaData and txn actions, malformed lines --
     applied one at a time (and some two at a time) with a cutoff that moves forward, checked
-    against full replays and, at the end, the oracle."""
+    against full replays and, at the end, the oracle. compact: the writer's separators (no
+    whitespace), so a commit's lines take the token tape of k_apply_commit; spaced lines are off the
+    tape and take its General walker."""
     import json
     import random
     from delta_amd import _native as N
@@ -572,13 +575,15 @@ def test_incremental_apply_random_commits(engine, tmp_path):
                "f9.parquet": ["dir/f\\u00e99.parquet", "dir/fé9.parquet"]}
     live = set()
 
+    sep = (",", ":") if compact else (", ", ": ")
+
     def add(p, v, k):
         return json.dumps({"add": {"path": p, "size": 10 + k, "modificationTime": v, "dataChange": True}},
-                          ensure_ascii=False).replace("\\\\u", "\\u")
+                          ensure_ascii=False, separators=sep).replace("\\\\u", "\\u")
 
     def rm(p, ts):
         return json.dumps({"remove": {"path": p, "deletionTimestamp": ts, "dataChange": True}},
-                          ensure_ascii=False).replace("\\\\u", "\\u")
+                          ensure_ascii=False, separators=sep).replace("\\\\u", "\\u")
 
     def name(p):
         return rng.choice(special[p]) if p in special else p

@@ -1,5 +1,5 @@
 """Per-apply timeline from scripts/gpu_tl_c5.sh's rocprofv3 CSVs: for the applies of the untimed
-pass, the median host time of each HIP API call kind between consecutive k_json_lines launches,
+pass, the median host time of each HIP API call kind between consecutive apply launches (k_apply_commit, or k_json_lines before it),
 and the median device time of each kernel / copy and of the gaps between them."""
 import csv
 import statistics
@@ -16,7 +16,7 @@ for a in api:
 dev = [(int(k["Start_Timestamp"]), int(k["End_Timestamp"]), k["Kernel_Name"].split("(")[0][:40], k["Correlation_Id"]) for k in ker]
 dev += [(int(c["Start_Timestamp"]), int(c["End_Timestamp"]), "copy:" + c["Direction"][12:], c["Correlation_Id"]) for c in cpy]
 dev.sort()
-starts = [i for i, x in enumerate(dev) if "k_json_lines" in x[2]]
+starts = [i for i, x in enumerate(dev) if "k_apply_commit" in x[2] or "k_json_lines" in x[2]]
 # the last half of the applies (the untimed pass)
 starts = starts[len(starts) // 2 + 2:-1]
 per_api = defaultdict(list)

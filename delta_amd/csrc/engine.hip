@@ -56,7 +56,7 @@ struct dr_ctx {
   std::string err;
   bool timing = false;
   std::string timing_only;  // non-empty: only this kernel gets an event pair (dr_set_timing_only)
-  bool overlap = false;  // DR_OVERLAP=1: K1 line parsing on stream2, beside the checkpoint decode
+  bool overlap = true;  // K1 line parsing on stream2 beside the checkpoint decode (bulk segments; DR_OVERLAP=0: off)
   struct Mark {
     std::string name;
     hipEvent_t ev;
@@ -1518,6 +1518,9 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
   const uint64_t json_len = s.h_json.size();
   const uint64_t nbj = json_num_blocks(json_len);
   const bool one_block = nbj == 1;  // a streamed commit: index, placement and counter reset in one launch
+  // K1 beside K2 on two streams: a checkpoint to decode and a JSON part of several index blocks
+  // (r04: 10.43 -> 10.33 ms per config-3 step); small segments keep one stream and their fused paths
+  const bool overlap = ctx->overlap && s.ck_rows > 0 && nbj > 1;
   DBuf<uint32_t> jcounts(ctx, one_block ? 1 : nbj + 1);
   DBuf<uint64_t> joff(ctx, nbj + 1);
   DBuf<uint8_t> scratch(ctx, scan_scratch_for(nbj));
@@ -1528,7 +1531,7 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
   DBuf<uint64_t> counters(ctx, 8);  // 0 special count, 1 special bytes, 2 nonfile count, 3 errors, 4 canon fill,
                                      // 5 lines deferred to the General walker, 7 checkpoint decode error
   // a segment of one wave: the parse kernel indexes its newlines and clears the counters itself
-  const bool fuse1 = one_block && s.json_lines && s.json_lines <= JSON_FUSE_MAX_LINES && !ctx->overlap &&
+  const bool fuse1 = one_block && s.json_lines && s.json_lines <= JSON_FUSE_MAX_LINES && !overlap &&
                      !std::getenv("DR_CHECK_LINES");
   if (one_block) {
     if (!fuse1) launch_json_index1(s.d_json.p, json_len, nl.p, joff.p, counters.p, 8, stream);
@@ -1556,10 +1559,11 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
   ActionArrays act{st->kind.p, st->flags.p, st->key.p, st->path_ptr.p, st->path_len.p, st->size.p, st->delts.p,
                    st->src_off.p, st->src_len.p};
   DBuf<uint64_t> hard(ctx, nlines);
-  // With DR_OVERLAP=1, K1's line parsing runs on stream2 beside the checkpoint decode below
-  // (measured r01: ~1 % of the step, both pipelines are issue-bound); stream waits for it before
+  // For a segment with a checkpoint and a multi-block JSON part (`overlap`, on unless
+  // DR_OVERLAP=0), K1's line parsing runs on stream2 beside the checkpoint decode below (r04:
+  // 10.43 -> 10.33 ms per config-3 step, k_snap_exec's time unchanged); stream waits for it before
   // anything reads the action arrays. The guard joins stream2 before any buffer it uses can be
-  // released. By default every kernel runs on one stream, so per-kernel times add up to the step.
+  // released. Small segments run on one stream (and take the fused small-segment paths).
   struct Overlap {
     dr_ctx* c;
     hipEvent_t fork = nullptr, done = nullptr;
@@ -1571,11 +1575,11 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
   } ov{ctx};
   // a small commit-only segment (a streamed commit): the deferred lines and the canonicalisation
   // run as one single-workgroup launch at the canonicalisation point (k_tail_post)
-  const bool tail_post = canonicalize && s.ck_rows == 0 && nlines && nlines <= JSON_TAIL_POST_MAX && !ctx->overlap;
+  const bool tail_post = canonicalize && s.ck_rows == 0 && nlines && nlines <= JSON_TAIL_POST_MAX && !overlap;
   JsonParseArgs ja{};
   if (nlines) {
-    hipStream_t s2 = ctx->overlap ? ctx->stream2 : stream;
-    if (ctx->overlap) {
+    hipStream_t s2 = overlap ? ctx->stream2 : stream;
+    if (overlap) {
       HIP_OK(hipEventCreateWithFlags(&ov.fork, hipEventDisableTiming));
       HIP_OK(hipEventRecord(ov.fork, stream));
       HIP_OK(hipStreamWaitEvent(s2, ov.fork, 0));
@@ -1618,7 +1622,7 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
     if (defer_tail && fuse1 && tail_post) pp.parse_deferred = true;
     else launch_json_parse(ja, s2);
     if (!tail_post) launch_json_hard(ja, s2);
-    if (ctx->overlap) {
+    if (overlap) {
       HIP_OK(hipEventCreateWithFlags(&ov.done, hipEventDisableTiming));
       HIP_OK(hipEventRecord(ov.done, s2));
     }
@@ -5126,7 +5130,7 @@ int dr_ctx_create(int device, dr_ctx** out) {
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return DR_E_DEVICE;
   if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) return DR_E_DEVICE;
   const char* ov = std::getenv("DR_OVERLAP");
-  c->overlap = ov && std::atoi(ov) != 0;
+  c->overlap = !ov || std::atoi(ov) != 0;
   *out = c.release();
   return DR_OK;
 }

@@ -128,6 +128,25 @@ def test_synthetic_configs(engine, tmp_path, config, scale):
         st.release()
 
 
+@pytest.mark.parametrize("overlap", ["0", "1"])
+def test_parse_streams_overlap_or_not(tmp_path, monkeypatch, overlap):
+    """K1 beside K2 on two streams (the default for a segment with a checkpoint and a multi-block
+    JSON part) and on one (DR_OVERLAP=0): the same records as the oracle either way, on a context
+    created under each setting."""
+    from delta_amd.delta_log import Engine
+    from delta_amd.testing import synth as S
+    monkeypatch.setenv("DR_OVERLAP", overlap)
+    eng = Engine(0)
+    exp = S.build_config(3, str(tmp_path), scale=0.02)
+    lp = os.path.join(str(tmp_path), "_delta_log")
+    st = _gpu_replay(eng, lp, exp.min_file_retention_timestamp)
+    try:
+        assert st.counts["num_files"] == exp.num_files and st.counts["num_removes"] == exp.num_removes
+        _assert_same(st, O.state_reconstruction(O.get_log_segment(lp), exp.min_file_retention_timestamp))
+    finally:
+        st.release()
+
+
 def test_newline_dense_blocks(engine, tmp_path):
     """The newline index keeps up to 512 positions per 16 KiB block and re-scans denser blocks:
     commits padded with runs of blank lines and `{}` rows (null actions, dropped by unwrap,

@@ -374,7 +374,7 @@ struct NonFileAction {
   int kind;                    // dev::K_METADATA / K_TXN / K_PROTOCOL
   uint64_t order;              // action index (replay order)
   std::string json;            // {"metaData":{...}} etc.
-  JVal val;                    // inner object
+  std::shared_ptr<const JVal> val;  // inner object (shared: a state's winners are copied per apply)
 };
 
 // Hot checkpoint columns decoded on the device.
@@ -689,7 +689,7 @@ static void decode_ck_nonfile(StagedData& s, CkPart& part, uint64_t base_action)
         for (auto& w : wr) if (w.row == rd[i].row && w.has_value) wv = w.ival;
         JVal y; y.t = JVal::NUM; y.s = std::to_string(wv);
         o.o.emplace_back("minWriterVersion", y);
-        a.val = o;
+        a.val = std::make_shared<const JVal>(o);
         a.json = "{\"protocol\":" + json_dump(o) + "}";
         rows[rd[i].row] = a;
       }
@@ -708,7 +708,7 @@ static void decode_ck_nonfile(StagedData& s, CkPart& part, uint64_t base_action)
         o.o.emplace_back("appId", id);
         for (auto& v : ver) if (v.row == e.row) { JVal x; x.t = JVal::NUM; x.s = std::to_string(v.has_value ? v.ival : 0); o.o.emplace_back("version", x); }
         for (auto& v : lu) if (v.row == e.row && v.has_value) { JVal x; x.t = JVal::NUM; x.s = std::to_string(v.ival); o.o.emplace_back("lastUpdated", x); }
-        a.val = o;
+        a.val = std::make_shared<const JVal>(o);
         a.json = "{\"txn\":" + json_dump(o) + "}";
         rows[e.row] = a;
       }
@@ -781,7 +781,7 @@ static void decode_ck_nonfile(StagedData& s, CkPart& part, uint64_t base_action)
           map_of(ck, cv, r, ckl ? ckl->max_def : 0, &conf);
           o.o.emplace_back("configuration", conf);
           for (auto& x : ct) if (x.row == r && x.has_value) { JVal n; n.t = JVal::NUM; n.s = std::to_string(x.ival); o.o.emplace_back("createdTime", n); }
-          a.val = o;
+          a.val = std::make_shared<const JVal>(o);
           a.json = "{\"metaData\":" + json_dump(o) + "}";
           rows[r] = a;
         }
@@ -1461,7 +1461,7 @@ static void reduce_nonfile(dr_state& st, std::vector<NonFileAction>& acts, bool 
     if (a.kind == 5) prot = &a;
     else if (a.kind == 3) meta = &a;
     else if (a.kind == 4) {
-      const JVal* id = a.val.get("appId");
+      const JVal* id = a.val->get("appId");
       std::string k = id && id->t == JVal::STR ? id->s : std::string();
       if (!txns.count(k)) app_order.push_back(k);
       txns[k] = &a;
@@ -1801,7 +1801,7 @@ static bool parse_finish(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr_
           NonFileAction a;
           a.kind = kinds[k2];
           a.order = R + li;
-          a.val = *x;
+          a.val = std::make_shared<const JVal>(*x);
           a.json = std::string("{\"") + names[k2] + "\":" + json_dump(*x) + "}";
           nf.push_back(std::move(a));
           break;
@@ -3423,7 +3423,7 @@ static void head_row_levels(const CkLeafW& L, int top_kind, const NonFileAction*
       put_u32le(val, uint32_t(int32_t(v.as_int())));
     }
   };
-  const JVal* cur = &a->val;
+  const JVal* cur = a->val.get();
   int d = 1;  // the top-level struct is defined
   const bool map_key = L.path.size() >= 2 && L.path[L.path.size() - 2] == "key_value" && L.path.back() == "key";
   const bool map_val = L.path.size() >= 2 && L.path[L.path.size() - 2] == "key_value" && L.path.back() == "value";
@@ -3610,8 +3610,8 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
   // partitionValues_parsed: the metadata's partition schema (D/Checkpoints.scala:372-389)
   std::vector<std::pair<std::string, int32_t>> parsed;
   if ((opts & DR_CKPT_PARSED) && md) {
-    const JVal* pc = md->val.get("partitionColumns");
-    const JVal* ss = md->val.get("schemaString");
+    const JVal* pc = md->val->get("partitionColumns");
+    const JVal* ss = md->val->get("schemaString");
     JVal schema;
     if (pc && pc->t == JVal::ARR && !pc->a.empty() && ss && ss->t == JVal::STR &&
         json_parse(ss->s.data(), ss->s.size(), &schema)) {
@@ -4399,7 +4399,7 @@ static void partition_groups(dr_state& st, const int64_t* rows, int64_t nrows, s
   std::vector<std::string> cols;
   for (const NonFileAction& a : st.nonfile) {
     if (a.kind != 3) continue;
-    const JVal* pc = a.val.get("partitionColumns");
+    const JVal* pc = a.val->get("partitionColumns");
     if (pc && pc->t == JVal::ARR)
       for (const JVal& c : pc->a)
         if (c.t == JVal::STR) cols.push_back(c.s);
@@ -4974,7 +4974,7 @@ static void set_nonfile_lines(dr_state& st, const std::string& lines, bool valid
       const std::string& key = v.o[0].first;
       a.kind = key == "metaData" ? 3 : key == "txn" ? 4 : 5;
       a.order = merged.size();
-      a.val = v.o[0].second;
+      a.val = std::make_shared<const JVal>(v.o[0].second);
       a.json = lines.substr(b, e - b);
       merged.push_back(std::move(a));
     }

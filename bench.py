@@ -21,7 +21,7 @@ the verdicts. Strong scaling: `value` = table actions per step / max-over-ranks 
 
 cpu_baseline: the C++ restatement of the reference replay (oracle/replay_oracle.cpp: 50 hash
 partitions, per-partition last-writer-wins table, sort by path) on the SAME full table, on rank 0
-at N=1, with all the box's cores (16) and with one; its counters and order-free key sums must equal
+at N=1, on the CPUs the process may use (the cgroup quota, 16 on the box), on all affinity CPUs and on one core; its counters and order-free key sums must equal
 the GPU's (full-scale parity, `matches_gpu`).
 """
 import argparse
@@ -39,7 +39,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 SORT_REDUCE = ("k_bucket_hist", "k_bucket_offsets", "k_bucket_scatter", "k_bucket_reduce", "k_bucket_verify",
                "k_bucket_reduce64", "k_bucket_exact", "k_sum_stats", "k_survivor_scan", "k_compact2")
 SNAPPY = ("k_snap_spec", "k_snap_assume", "k_snap_entries", "k_snap_regions", "k_snap_resolve", "k_snap_count",
-          "k_snap_scan", "k_snap_emit", "k_snap_exec", "k_snap_serial")
+          "k_snap_scan", "k_snap_exec", "k_snap_serial")
 JSON = ("k_json_index", "k_json_place", "k_json_lines", "k_json_hard")
 
 
@@ -66,7 +66,7 @@ def algorithmic_bytes(kernel, plan, counts):
     sharded replay, whose reduce-side action count the bench does not see: K3/K4 then go unpriced)."""
     rows = plan["checkpoint_rows"]
     lines = plan.get("json_lines", counts["num_actions"] - rows if counts else 0)
-    ch, el = plan["snappy_chunks"], plan["snappy_elements"]
+    ch = plan["snappy_chunks"]
     sin, sout = plan["snappy_in_bytes"], plan["snappy_out_bytes"]
     table = {
         "k_json_index": plan["json_bytes"] + 2 * lines,            # bytes in, u16 slot per line
@@ -75,8 +75,10 @@ def algorithmic_bytes(kernel, plan, counts):
         "k_page_copy": 2 * plan["copy_bytes"],
         "k_snap_spec": sin + 60 * ch,                              # compressed bytes in, per-chunk state out
         "k_snap_assume": 16 * ch, "k_snap_entries": 16 * ch, "k_snap_count": 8 * ch, "k_snap_scan": 8 * ch,
-        "k_snap_emit": sin + 24 * ch + 8 * el,                     # compressed in, 8 B record per element out
-        "k_snap_exec": 8 * el + sin + sout,                        # records + literal bytes in, page bytes out
+        # SURVEY.md 8(d)'s compulsory K2 bytes: the compressed pages in, the decompressed pages out (the
+        # start bitmaps and chunk entries it also reads, 4 B per 32 and 4 B per 256 compressed bytes,
+        # are the decoder's own intermediate and not credited)
+        "k_snap_exec": sin + sout,
         "k_pq_data": plan["pages_decompressed_bytes"] + 44 * rows,
         "k_ckpt_assemble": 182 * rows,
     }
@@ -92,8 +94,6 @@ def algorithmic_bytes(kernel, plan, counts):
             "k_bucket_reduce": 16 * fa + 4 * surv,                 # records in, survivors out (+ verification)
             "k_compact2": 8 * surv,
         })
-    if kernel in ("k_snap_emit", "k_snap_exec") and not el:
-        return None
     return table.get(kernel)
 
 
@@ -148,14 +148,16 @@ def cpu_budget():
     return aff, quota
 
 
-def cpu_baseline(log_path, cutoff, counts, threads, one_core=True, share=16):
-    """oracle/_build/replay_oracle on the same table: on every CPU this process may
-    use (`threads`, or the affinity mask), on the per-GPU CPU share when that differs, and on one core.
-    Its counters and order-free key sums (incl. the full-record sums) must equal the GPU's."""
+def cpu_baseline(log_path, cutoff, counts, threads, one_core=True, all_cpus=True):
+    """oracle/_build/replay_oracle on the same table. `value` / `cores`: the CPUs this
+    process may actually use -- the cgroup quota (16 on the GPU box), else the affinity mask -- or
+    `threads` when given. Named extras: every CPU of the affinity mask (the box shows its whole
+    machine; more threads than the quota only time-slice) and one core. Its counters and order-free
+    key sums (incl. the full-record sums) must equal the GPU's."""
     if not os.path.exists(os.path.join(ROOT, "oracle", "_build", "replay_oracle")):
         return None
     aff, quota = cpu_budget()
-    threads = threads or aff
+    threads = threads or min(aff, quota or aff)
     res = run_replay_oracle(log_path, cutoff, threads, record_sums="live_record_sum" in counts)
     if res is None:
         return None
@@ -170,11 +172,12 @@ def cpu_baseline(log_path, cutoff, counts, threads, one_core=True, share=16):
            "sample": "the full benchmark table (%d actions: %d checkpoint rows + JSON lines), bytes in memory "
                      "before the clock; C++ restatement of the replay (not Spark: no JVM on the box): "
                      "Parquet+SNAPPY and JSON decode, canonicalize, 50 hash partitions, per-partition "
-                     "last-writer-wins, retention, sort by path" % (res["num_actions"], res["checkpoint_rows"]),
+                     "last-writer-wins, retention, sort by path; %d threads = the CPUs this process may "
+                     "use (cgroup quota)" % (res["num_actions"], res["checkpoint_rows"], threads),
            "compared": keys, "matches_gpu": not mism, "record_pass_s": res.get("record_s")}
     runs = []
-    if share and share != threads:
-        runs.append(("per_gpu_share", share))
+    if all_cpus and aff != threads:
+        runs.append(("all_affinity_cpus", aff))
     if one_core:
         runs.append(("one_core", 1))
     for name, t in runs:
@@ -274,7 +277,7 @@ def measure_stream(eng, table, exp, args):
     base.release()
     cpu = None
     if not args.no_cpu_baseline:
-        cpu = cpu_baseline(log_path, final_cut, counts, args.cpu_threads, one_core=False, share=0)
+        cpu = cpu_baseline(log_path, final_cut, counts, args.cpu_threads, one_core=False, all_cpus=False)
     if cpu:
         # the reference has no incremental path: every DeltaLog.update() rebuilds the snapshot from
         # its checkpoint + deltas (D/SnapshotManagement.scala:286-330), so its
@@ -452,9 +455,9 @@ def main():
     ap.add_argument("--config", type=int, default=3)
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="CPU baseline threads (0: every CPU this process may use, see cpu_budget())")
+                    help="CPU baseline threads (0: the CPUs this process may use, the cgroup quota; cpu_budget())")
     ap.add_argument("--pmc-dir", default=None,
-                    help="rocprofv3 --pmc passes of this build and config (default profiles/r04/pmc/c<config>)")
+                    help="rocprofv3 --pmc passes of this build and config (default profiles/r05/pmc/c<config>)")
     ap.add_argument("--driver", choices=("lib", "torch"), default="lib",
                     help="N > 1: the library's own RCCL replay (dr_replay_sharded, what a JNI host calls) or "
                          "delta_amd/sharded.py over torch.distributed")
@@ -464,7 +467,7 @@ def main():
     ap.add_argument("--workdir", default=os.environ.get("DR_BENCH_DIR", os.path.join(tempfile.gettempdir(), "dr_bench")))
     args = ap.parse_args()
     if args.pmc_dir is None:
-        args.pmc_dir = os.path.join(ROOT, "profiles", "r04", "pmc", "c%d" % args.config)
+        args.pmc_dir = os.path.join(ROOT, "profiles", "r05", "pmc", "c%d" % args.config)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))
@@ -730,6 +733,9 @@ def main():
                                       "dr_replay_sharded" if args.driver == "lib" else "torch.distributed"))
                    if world > 1 else "single GPU"},
         "roofline": roofline,
+        # the whole step against the HBM roofline: the staged input (JSON + checkpoint bytes, each read
+        # once at least) over the step time
+        "step_frac": round((exp["json_bytes"] + exp["checkpoint_bytes"]) / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         "pipelines": pipelines,
         "cpu_baseline": cpu,
         "end_to_end": e2e,

@@ -108,6 +108,9 @@ struct dr_ctx {
         fail(DR_E_OOM, "pinned readback words");
       }
       hpin = static_cast<uint64_t*>(p);
+      // hipHostMalloc does not promise zeroed memory: the completion word must not already hold the
+      // first sequence number a readback waits for
+      std::memset(hpin, 0, kPinWords * sizeof(uint64_t));
       void* d = nullptr;
       HIP_OK(hipHostGetDevicePointer(&d, p, 0));
       hpin_dev = static_cast<uint64_t*>(d);
@@ -400,12 +403,9 @@ struct PagePlan {
   DBuf<SnapPage> d_snap;
   DBuf<uint32_t> d_chunk_base, d_block_page, d_chunk_page;
   DBuf<CopyJob> d_copy;
-  DBuf<uint32_t> s_mid_first, s_half_out, s_half_elems;
   DBuf<uint32_t> s_spec_exit, s_vis, s_entry, s_spec_first, s_assumed, s_region, s_chunk_out, s_chunk_out_start,
-      s_chunk_copies, s_pages_bad;
-  DBuf<uint64_t> s_rec_start, s_recs;
+      s_chunk_elems, s_pages_bad, s_block_chunk, s_page_mark;
   DBuf<uint8_t> s_chunk_flag;
-  DBuf<uint64_t> s_block_rec;
   DBuf<unsigned long long> s_region_count;
   std::vector<uint32_t> wg_chunk0;
   DBuf<uint32_t> d_wg_chunk0;
@@ -963,20 +963,16 @@ static void plan_pages(StagedData& s, PagePlan& P) {
   P.s_vis = DBuf<uint32_t>(s.ctx, uint64_t(P.nchunks) * (snappy_chunk_bytes() / 32));
   P.s_entry = DBuf<uint32_t>(s.ctx, P.nchunks);
   P.s_spec_first = DBuf<uint32_t>(s.ctx, P.nchunks);
-  P.s_mid_first = DBuf<uint32_t>(s.ctx, P.nchunks);
-  P.s_half_out = DBuf<uint32_t>(s.ctx, P.nchunks);
-  P.s_half_elems = DBuf<uint32_t>(s.ctx, P.nchunks);
   P.s_assumed = DBuf<uint32_t>(s.ctx, P.nchunks);
   P.s_region = DBuf<uint32_t>(s.ctx, P.nchunks);
-  P.s_block_rec = DBuf<uint64_t>(s.ctx, P.block_page.size() + 1);
+  P.s_block_chunk = DBuf<uint32_t>(s.ctx, P.block_page.size() + 1);
   P.s_chunk_flag = DBuf<uint8_t>(s.ctx, P.nchunks);
   P.s_region_count = DBuf<unsigned long long>(s.ctx, 1);
   P.s_chunk_out = DBuf<uint32_t>(s.ctx, P.nchunks);
   P.s_chunk_out_start = DBuf<uint32_t>(s.ctx, P.nchunks);
-  P.s_chunk_copies = DBuf<uint32_t>(s.ctx, P.nchunks);
-  P.s_rec_start = DBuf<uint64_t>(s.ctx, uint64_t(P.nchunks) + 1);
-  P.s_recs = DBuf<uint64_t>(s.ctx, P.snap_in_bytes / 2 + 1);  // an element takes >= 2 input bytes
+  P.s_chunk_elems = DBuf<uint32_t>(s.ctx, P.nchunks);
   P.s_pages_bad = DBuf<uint32_t>(s.ctx, P.snap_pages.size());
+  P.s_page_mark = DBuf<uint32_t>(s.ctx, P.snap_pages.size());
   P.s_ba_vals = DBuf<uint32_t>(s.ctx, P.ba_vals);
   up(P.d_ba_tiles, P.ba_tiles);
   P.s_ba_tile_cnt = DBuf<uint32_t>(s.ctx, P.ba_tiles.size());
@@ -1027,15 +1023,33 @@ static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_
   launch_page_copy(P.d_copy.p, uint32_t(P.copy_jobs.size()), stream);
   if (!P.snap_pages.empty()) {
     P.s_pages_bad.zero(stream);
+    P.s_page_mark.zero(stream);
     P.s_chunk_flag.zero(stream);
     P.s_region_count.zero(stream);
-    SnappyArgs sa{P.d_snap.p, uint32_t(P.snap_pages.size()), P.d_chunk_base.p, P.nchunks, P.s_spec_exit.p,
-                  P.s_vis.p, P.s_entry.p, P.s_spec_first.p, P.s_assumed.p, P.s_chunk_flag.p, P.s_region.p, P.s_region_count.p, P.s_chunk_out.p, P.s_chunk_out_start.p, P.s_chunk_copies.p,
-                  P.s_rec_start.p, P.s_recs.p, P.d_block_page.p, P.s_block_rec.p, uint32_t(P.block_page.size()),
-                  P.d_wg_chunk0.p, uint32_t(P.wg_chunk0.size()), P.s_pages_bad.p, err.p};
-    sa.mid_first = P.s_mid_first.p;
-    sa.half_out = P.s_half_out.p;
-    sa.half_elems = P.s_half_elems.p;
+    SnappyArgs sa{};
+    sa.pages = P.d_snap.p;
+    sa.npages = uint32_t(P.snap_pages.size());
+    sa.chunk_base = P.d_chunk_base.p;
+    sa.nchunks = P.nchunks;
+    sa.spec_exit = P.s_spec_exit.p;
+    sa.vis = P.s_vis.p;
+    sa.entry = P.s_entry.p;
+    sa.spec_first = P.s_spec_first.p;
+    sa.assumed_exit = P.s_assumed.p;
+    sa.chunk_flag = P.s_chunk_flag.p;
+    sa.region = P.s_region.p;
+    sa.region_count = P.s_region_count.p;
+    sa.page_mark = P.s_page_mark.p;
+    sa.chunk_out = P.s_chunk_out.p;
+    sa.chunk_out_start = P.s_chunk_out_start.p;
+    sa.chunk_elems = P.s_chunk_elems.p;
+    sa.block_page = P.d_block_page.p;
+    sa.block_chunk = P.s_block_chunk.p;
+    sa.nblocks = uint32_t(P.block_page.size());
+    sa.wg_chunk0 = P.d_wg_chunk0.p;
+    sa.nwg = uint32_t(P.wg_chunk0.size());
+    sa.pages_bad = P.s_pages_bad.p;
+    sa.error = err.p;
     sa.chunk_page = P.d_chunk_page.p;
     DBuf<uint64_t> stamps, rstats;
     const bool dbg = std::getenv("DR_SNAP_DEBUG") != nullptr;
@@ -1048,7 +1062,10 @@ static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_
       sa.rstats = rstats.p;
     }
     launch_snappy(sa, stream, scratch);
-    if (ctx->timing && !P.snap_elements) P.snap_elements = d2h_one(P.s_rec_start.p + P.nchunks, stream);
+    if (ctx->timing && !P.snap_elements) {  // statistics, once (the first timed replay)
+      const std::vector<uint32_t> el = d2h(P.s_chunk_elems.p, P.nchunks, stream);
+      for (uint32_t v : el) P.snap_elements += v;
+    }
     if (dbg) {
       std::vector<uint64_t> st = d2h(stamps.p, P.block_page.size() * 8, stream);
       double acc[8] = {0};
@@ -1076,7 +1093,7 @@ static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_
       }
       for (auto& kv : why) std::fprintf(stderr, "snappy bad code %u: %zu pages\n", kv.first, kv.second);
       const size_t nr = size_t(nreg);
-      std::fprintf(stderr, "snappy: pages %zu serially resolved regions %zu bad %zu\n", P.snap_pages.size(), nr, nb);
+      std::fprintf(stderr, "snappy: pages %zu, pages with serially resolved regions %zu, bad %zu\n", P.snap_pages.size(), nr, nb);
       // chunks whose true entry is not their first speculatively visited position (re-walked by
       // k_snap_count), and pages holding at least one
       std::vector<uint32_t> ent = d2h(P.s_entry.p, P.nchunks, stream), sf = d2h(P.s_spec_first.p, P.nchunks, stream);
@@ -1088,50 +1105,28 @@ static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_
         px += k != 0;
       }
       std::fprintf(stderr, "snappy: chunks %u, entry != speculative first %zu (on %zu pages)\n", P.nchunks, nx, px);
-      // regions per page; DR_SNAP_DUMP=dir writes the compressed input of the first pages holding one
+      // pages resolved serially (one walk per region, in page order); DR_SNAP_DUMP=dir writes the
+      // compressed input of the slowest
       std::vector<uint32_t> reg = d2h(P.s_region.p, nr, stream);
-      {  // the slowest resolver walks
-        std::vector<uint64_t> rs = d2h(rstats.p, nr * 4, stream);
-        std::vector<size_t> ord(nr);
-        for (size_t k = 0; k < nr; ++k) ord[k] = k;
-        std::sort(ord.begin(), ord.end(), [&](size_t x, size_t y) { return rs[x * 4] > rs[y * 4]; });
-        for (size_t k = 0; k < std::min<size_t>(nr, 8); ++k) {
-          const size_t r = ord[k];
-          const uint32_t c = reg[r];
-          const uint32_t q = uint32_t(std::upper_bound(P.chunk_base.begin(), P.chunk_base.end(), c) - P.chunk_base.begin()) - 1;
-          if (const char* dir = std::getenv("DR_SNAP_DUMP")) {  // the slowest regions' pages, with their entries
-            const SnapPage& pg = P.snap_pages[q];
-            std::vector<uint8_t> raw = d2h(reinterpret_cast<const uint8_t*>(pg.in), pg.n_in, stream);
-            const std::string fn = std::string(dir) + "/slow_page" + std::to_string(q) + ".snappy";
-            if (FILE* f = std::fopen(fn.c_str(), "wb")) {
-              std::fwrite(raw.data(), 1, raw.size(), f);
-              std::fclose(f);
-            }
-          }
-          std::fprintf(stderr, "resolve region %zu: page %u chunk %u/%u clocks %llu windows %llu walks %llu spans %llu\n", r, q,
-                       c - P.chunk_base[q], P.chunk_base[q + 1] - P.chunk_base[q], (unsigned long long)rs[r * 4],
-                       (unsigned long long)rs[r * 4 + 1], (unsigned long long)rs[r * 4 + 2], (unsigned long long)rs[r * 4 + 3]);
-        }
-      }
-      std::map<uint32_t, std::vector<uint32_t>> per_page;
-      for (uint32_t c : reg) {
-        const uint32_t q = uint32_t(std::upper_bound(P.chunk_base.begin(), P.chunk_base.end(), c) - P.chunk_base.begin()) - 1;
-        per_page[q].push_back(c - P.chunk_base[q]);
-      }
-      int dumped = 0;
-      for (auto& kv : per_page) {
-        const SnapPage& pg = P.snap_pages[kv.first];
-        std::fprintf(stderr, "snappy page %u: n_in %u n_out %u regions %zu first at chunk %u\n", kv.first, pg.n_in,
-                     pg.n_out, kv.second.size(), *std::min_element(kv.second.begin(), kv.second.end()));
+      std::vector<uint64_t> rs = d2h(rstats.p, nr * 4, stream);
+      std::vector<size_t> ord(nr);
+      for (size_t k = 0; k < nr; ++k) ord[k] = k;
+      std::sort(ord.begin(), ord.end(), [&](size_t x, size_t y) { return rs[x * 4] > rs[y * 4]; });
+      for (size_t k = 0; k < std::min<size_t>(nr, 8); ++k) {
+        const size_t r = ord[k];
+        const uint32_t q = reg[r];
+        const SnapPage& pg = P.snap_pages[q];
         if (const char* dir = std::getenv("DR_SNAP_DUMP")) {
-          if (dumped++ >= 4) continue;
           std::vector<uint8_t> raw = d2h(reinterpret_cast<const uint8_t*>(pg.in), pg.n_in, stream);
-          const std::string fn = std::string(dir) + "/page" + std::to_string(kv.first) + ".snappy";
+          const std::string fn = std::string(dir) + "/slow_page" + std::to_string(q) + ".snappy";
           if (FILE* f = std::fopen(fn.c_str(), "wb")) {
             std::fwrite(raw.data(), 1, raw.size(), f);
             std::fclose(f);
           }
         }
+        std::fprintf(stderr, "resolve page %u (%u chunks, n_in %u n_out %u): clocks %llu windows %llu walks %llu spans %llu\n",
+                     q, P.chunk_base[q + 1] - P.chunk_base[q], pg.n_in, pg.n_out, (unsigned long long)rs[r * 4],
+                     (unsigned long long)rs[r * 4 + 1], (unsigned long long)rs[r * 4 + 2], (unsigned long long)rs[r * 4 + 3]);
       }
     }
   }
@@ -5451,6 +5446,223 @@ int dr_state_export(dr_state* state, int32_t which, dr_export* out) {
     out->tags_val_off = e.tags_val_off; out->tags_val_bytes = e.tags_val_bytes;
     out->tags_val_null = e.tags_val_null;
   });
+}
+
+static int64_t* malloc_copy(const std::vector<int64_t>& v);
+
+// ---- row-range export (ABI 3) ------------------------------------------------------------------
+// A host copy of rows [lo, hi) of one side's resident export columns, every offset array rebased to
+// the range (so no column of a range is larger than the caller planned: a JVM direct buffer holds
+// at most 2^31 - 1 bytes). One pinned block from the context's cache, returned by dr_range_release.
+struct dr_range {
+  dr_ctx* ctx = nullptr;
+  void* block = nullptr;
+  dr_range() = default;
+  dr_range(const dr_range&) = delete;
+  dr_range& operator=(const dr_range&) = delete;
+  ~dr_range() {
+    if (ctx && block) ctx->host_release(block);
+  }
+};
+
+// The eight row-level and eight entry-level offsets that bound rows [lo, hi) of X.
+struct RangeBounds {
+  uint64_t path[2], stats[2], pvn[2], tgn[2], pvk[2], pvv[2], tgk[2], tgv[2];
+};
+static RangeBounds range_bounds(const DevExport& X, uint64_t lo, uint64_t hi, hipStream_t stream) {
+  RangeBounds b;
+  const uint64_t r[2] = {lo, hi};
+  for (int k = 0; k < 2; ++k) {
+    b.path[k] = d2h_one(X.path_off.p + r[k], stream);
+    b.stats[k] = d2h_one(X.off[EXC_STATS].p + r[k], stream);
+    b.pvn[k] = d2h_one(X.off[EXC_PV_N].p + r[k], stream);
+    b.tgn[k] = d2h_one(X.off[EXC_TAGS_N].p + r[k], stream);
+  }
+  for (int k = 0; k < 2; ++k) {
+    b.pvk[k] = uint64_t(d2h_one(X.pv_key_off.p + b.pvn[k], stream));
+    b.pvv[k] = uint64_t(d2h_one(X.pv_val_off.p + b.pvn[k], stream));
+    b.tgk[k] = uint64_t(d2h_one(X.tags_key_off.p + b.tgn[k], stream));
+    b.tgv[k] = uint64_t(d2h_one(X.tags_val_off.p + b.tgn[k], stream));
+  }
+  return b;
+}
+
+static void export_range(dr_state& st, int which, uint64_t lo, uint64_t hi, dr_range& R, dr_export* out) {
+  dr_ctx* ctx = st.ctx;
+  hipStream_t stream = ctx->stream;
+  const DevExport& X = materialize(st, which);
+  hi = std::min<uint64_t>(hi, X.n);
+  lo = std::min(lo, hi);
+  const uint64_t n = hi - lo;
+  const RangeBounds b = range_bounds(X, lo, hi, stream);
+  const uint64_t npv = b.pvn[1] - b.pvn[0], ntg = b.tgn[1] - b.tgn[0];
+  DBuf<uint8_t> dvalid(ctx, n + 1);
+  DBuf<int64_t> ddelts(ctx, n + 1);
+  launch_delts_fix(X.flags.p + lo, reinterpret_cast<const int64_t*>(X.delts.p) + lo, n, dvalid.p, ddelts.p, stream);
+  ExportCols ex;  // only its pointer fields: the columns are carved from R.block
+  auto u8 = [](const void* p, uint64_t k) { return static_cast<const uint8_t*>(p) + k; };
+  const std::vector<ExportCol> cols = {
+      {(void**)&ex.path_off, X.path_off.p + lo, 8 * (n + 1)},
+      {(void**)&ex.path_bytes, u8(X.path_bytes.p, b.path[0]), b.path[1] - b.path[0]},
+      {(void**)&ex.delts, ddelts.p, 8 * n},
+      {(void**)&ex.delts_valid, dvalid.p, n},
+      {(void**)&ex.size, X.size.p + lo, 8 * n},
+      {(void**)&ex.mtime, X.mtime.p + lo, 8 * n},
+      {(void**)&ex.efm, X.efm.p + lo, n},
+      {(void**)&ex.stats_null, X.stats_null.p + lo, n},
+      {(void**)&ex.pv_null, X.pv_null.p + lo, n},
+      {(void**)&ex.tags_null, X.tags_null.p + lo, n},
+      {(void**)&ex.stats_off, X.off[EXC_STATS].p + lo, 8 * (n + 1)},
+      {(void**)&ex.pv_entry_off, X.off[EXC_PV_N].p + lo, 8 * (n + 1)},
+      {(void**)&ex.tags_entry_off, X.off[EXC_TAGS_N].p + lo, 8 * (n + 1)},
+      {(void**)&ex.stats_bytes, u8(X.stats_bytes.p, b.stats[0]), b.stats[1] - b.stats[0]},
+      {(void**)&ex.pv_key_off, X.pv_key_off.p + b.pvn[0], 8 * (npv + 1)},
+      {(void**)&ex.pv_val_off, X.pv_val_off.p + b.pvn[0], 8 * (npv + 1)},
+      {(void**)&ex.pv_val_null, X.pv_val_null.p + b.pvn[0], npv},
+      {(void**)&ex.pv_key_bytes, u8(X.pv_key_bytes.p, b.pvk[0]), b.pvk[1] - b.pvk[0]},
+      {(void**)&ex.pv_val_bytes, u8(X.pv_val_bytes.p, b.pvv[0]), b.pvv[1] - b.pvv[0]},
+      {(void**)&ex.tags_key_off, X.tags_key_off.p + b.tgn[0], 8 * (ntg + 1)},
+      {(void**)&ex.tags_val_off, X.tags_val_off.p + b.tgn[0], 8 * (ntg + 1)},
+      {(void**)&ex.tags_val_null, X.tags_val_null.p + b.tgn[0], ntg},
+      {(void**)&ex.tags_key_bytes, u8(X.tags_key_bytes.p, b.tgk[0]), b.tgk[1] - b.tgk[0]},
+      {(void**)&ex.tags_val_bytes, u8(X.tags_val_bytes.p, b.tgv[0]), b.tgv[1] - b.tgv[0]}};
+  R.ctx = ctx;
+  R.block = ctx->host_alloc(group_bytes(cols));
+  queue_group(cols, R.block, stream);
+  HIP_OK(hipStreamSynchronize(stream));
+  auto rebase = [](int64_t* o, uint64_t cnt, uint64_t base) {
+    for (uint64_t i = 0; i < cnt; ++i) o[i] -= int64_t(base);
+  };
+  rebase(ex.path_off, n + 1, b.path[0]);
+  rebase(ex.stats_off, n + 1, b.stats[0]);
+  rebase(ex.pv_entry_off, n + 1, b.pvn[0]);
+  rebase(ex.tags_entry_off, n + 1, b.tgn[0]);
+  rebase(ex.pv_key_off, npv + 1, b.pvk[0]);
+  rebase(ex.pv_val_off, npv + 1, b.pvv[0]);
+  rebase(ex.tags_key_off, ntg + 1, b.tgk[0]);
+  rebase(ex.tags_val_off, ntg + 1, b.tgv[0]);
+  *out = dr_export{};
+  out->n = int64_t(n);
+  out->path_off = ex.path_off; out->path_bytes = ex.path_bytes;
+  out->size = ex.size; out->modification_time = ex.mtime;
+  out->deletion_timestamp = ex.delts; out->deletion_timestamp_valid = ex.delts_valid;
+  out->extended_file_metadata = ex.efm;
+  out->stats_off = ex.stats_off; out->stats_bytes = ex.stats_bytes; out->stats_null = ex.stats_null;
+  out->pv_entry_off = ex.pv_entry_off; out->pv_null = ex.pv_null;
+  out->pv_key_off = ex.pv_key_off; out->pv_key_bytes = ex.pv_key_bytes;
+  out->pv_val_off = ex.pv_val_off; out->pv_val_bytes = ex.pv_val_bytes; out->pv_val_null = ex.pv_val_null;
+  out->tags_entry_off = ex.tags_entry_off; out->tags_null = ex.tags_null;
+  out->tags_key_off = ex.tags_key_off; out->tags_key_bytes = ex.tags_key_bytes;
+  out->tags_val_off = ex.tags_val_off; out->tags_val_bytes = ex.tags_val_bytes;
+  out->tags_val_null = ex.tags_val_null;
+}
+
+// The offsets of the row-level columns at sample rows, and of the entry-level columns at the
+// samples' entries: the byte size of every column of a range between two samples, without copying
+// the columns (dr_state_export_plan).
+struct RangeSampler {
+  const DevExport& X;
+  dr_ctx* ctx;
+  std::vector<uint64_t> rows, po, so, pe, te, pk, pv, tk, tv;
+  void sample(std::vector<uint64_t> r) {
+    rows = std::move(r);
+    hipStream_t stream = ctx->stream;
+    auto gather = [&](const uint64_t* src, const std::vector<uint64_t>& idx, std::vector<uint64_t>& dst) {
+      std::vector<uint32_t> i32(idx.size());
+      for (size_t k = 0; k < idx.size(); ++k) {
+        if (idx[k] > 0xffffffffull) fail(DR_E_UNSUPPORTED, "export plan: more than 2^32 map entries in a side");
+        i32[k] = uint32_t(idx[k]);
+      }
+      DBuf<uint32_t> di = upload(ctx, i32.data(), i32.size());
+      DBuf<uint64_t> dd(ctx, idx.size());
+      launch_gather_u64(src, di.p, idx.size(), dd.p, stream);
+      dst = d2h(dd.p, idx.size(), stream);
+    };
+    gather(X.path_off.p, rows, po);
+    gather(X.off[EXC_STATS].p, rows, so);
+    gather(X.off[EXC_PV_N].p, rows, pe);
+    gather(X.off[EXC_TAGS_N].p, rows, te);
+    gather(reinterpret_cast<const uint64_t*>(X.pv_key_off.p), pe, pk);
+    gather(reinterpret_cast<const uint64_t*>(X.pv_val_off.p), pe, pv);
+    gather(reinterpret_cast<const uint64_t*>(X.tags_key_off.p), te, tk);
+    gather(reinterpret_cast<const uint64_t*>(X.tags_val_off.p), te, tv);
+  }
+  // the largest column (bytes) of the range between samples i < j
+  uint64_t cost(size_t i, size_t j) const {
+    const uint64_t n = rows[j] - rows[i], npv = pe[j] - pe[i], ntg = te[j] - te[i];
+    uint64_t m = 8 * (n + 1);
+    for (uint64_t v : {po[j] - po[i], so[j] - so[i], 8 * (npv + 1), pk[j] - pk[i], pv[j] - pv[i], 8 * (ntg + 1),
+                       tk[j] - tk[i], tv[j] - tv[i]})
+      m = std::max(m, v);
+    return m;
+  }
+};
+
+// Greedy row ranges of [lo, hi): as many rows as fit max_rows and max_bytes per column, sampled every
+// `step` rows; a sample interval that alone exceeds max_bytes is split row by row.
+static void plan_ranges(const DevExport& X, dr_ctx* ctx, uint64_t lo, uint64_t hi, uint64_t step, uint64_t max_rows,
+                        uint64_t max_bytes, std::vector<int64_t>& bounds) {
+  std::vector<uint64_t> r;
+  for (uint64_t x = lo; x < hi; x += step) r.push_back(x);
+  r.push_back(hi);
+  RangeSampler S{X, ctx};
+  S.sample(std::move(r));
+  size_t i = 0;
+  while (S.rows[i] < hi) {
+    size_t j = i + 1;
+    if (S.cost(i, j) > max_bytes) {
+      if (step == 1) fail(DR_E_UNSUPPORTED, fmt("export plan: row %llu alone holds a column over %llu bytes",
+                                                (unsigned long long)S.rows[i], (unsigned long long)max_bytes));
+      plan_ranges(X, ctx, S.rows[i], S.rows[j], 1, max_rows, max_bytes, bounds);
+      i = j;
+      continue;
+    }
+    while (j + 1 < S.rows.size() && S.rows[j + 1] - S.rows[i] <= max_rows && S.cost(i, j + 1) <= max_bytes) ++j;
+    if (S.rows[j] - S.rows[i] > max_rows) {  // a sample interval longer than max_rows: split it evenly
+      for (uint64_t x = S.rows[i] + max_rows; x < S.rows[j]; x += max_rows) bounds.push_back(int64_t(x));
+    }
+    bounds.push_back(int64_t(S.rows[j]));
+    i = j;
+  }
+}
+
+int dr_state_export_plan(dr_state* state, int32_t which, int64_t max_rows, uint64_t max_bytes, int64_t** bounds,
+                         int64_t* nranges) {
+  if (!state || !bounds || !nranges || (which != DR_LIVE && which != DR_TOMBSTONES) || max_rows <= 0 ||
+      max_bytes < 64)
+    return DR_E_INVALID_ARG;
+  *bounds = nullptr;
+  *nranges = 0;
+  return guard(state->ctx, [&] {
+    HIP_OK(hipSetDevice(state->ctx->device));
+    const DevExport& X = materialize(*state, which);
+    std::vector<int64_t> b{0};
+    if (X.n) {
+      const uint64_t step = std::max<uint64_t>(1, std::min<uint64_t>(4096, uint64_t(max_rows)));
+      plan_ranges(X, state->ctx, 0, X.n, step, uint64_t(max_rows), max_bytes, b);
+    }
+    *bounds = malloc_copy(b);
+    *nranges = int64_t(b.size()) - 1;
+  });
+}
+
+int dr_state_export_range(dr_state* state, int32_t which, int64_t row_begin, int64_t row_end, dr_range** range,
+                          dr_export* out) {
+  if (!state || !range || !out || (which != DR_LIVE && which != DR_TOMBSTONES) || row_begin < 0 ||
+      row_end < row_begin)
+    return DR_E_INVALID_ARG;
+  *range = nullptr;
+  return guard(state->ctx, [&] {
+    HIP_OK(hipSetDevice(state->ctx->device));
+    auto R = std::make_unique<dr_range>();
+    export_range(*state, which, uint64_t(row_begin), uint64_t(row_end), *R, out);
+    *range = R.release();
+  });
+}
+
+int dr_range_release(dr_range* range) {
+  delete range;
+  return DR_OK;
 }
 
 int dr_state_materialize(dr_state* state, uint64_t* bytes) {

@@ -5,7 +5,7 @@
 // (measured 1.28 s for config 3 with one lane per page). This decoder is fully parallel:
 //
 //  A k_snap_spec    one lane per 256-byte chunk of compressed input parses elements
-//                   *speculatively* (starting 64 bytes early as a warm-up) and records the
+//                   *speculatively* (starting SNAP_WU = 192 bytes early as a warm-up) and records the
 //                   positions it visited in the chunk (a bitmap in registers) and where it left it.
 //  B k_snap_assume / k_snap_entries: every chunk's true entry, in parallel: a chunk whose true
 //                   entry (the previous chunk's exit) is on its speculative chain is correct
@@ -15,21 +15,22 @@
 //                   per page, 64 chunks per ballot, spanned chunks skipped in one step).
 //  C k_snap_count   per chunk: output bytes and elements of its true elements (counted by the
 //                   speculative walk from the chunk's first visited position; re-walked only when
-//                   the true entry differs).
-//  D k_snap_scan    per page: exclusive scan of chunk outputs (copy counts: a global scan).
-//  E k_snap_emit    per chunk: every element becomes an 8-byte record {chunk-relative output
-//                   offset, length, copy offset | literal input position}, staged in LDS and
-//                   written coalesced. The compressor compresses 64 KiB fragments independently,
-//                   so no element straddles a fragment and no copy reaches before its fragment;
-//                   violations flag the page for k_snap_serial.
-//  F k_snap_exec    one 1024-thread workgroup per 64 KiB output block resolves every copied
-//                   byte to its literal origin by pointer jumping on a u16 map in LDS
-//                   (src[p] = p - offset; literal bytes are their own roots), then rebuilds the
-//                   block's bytes in the same LDS and stores them with 16-byte stores.
+//                   the true entry differs, and then the chunk's visited bitmap is rewritten with
+//                   the true chain: every chunk's bits at or after its entry are its element starts).
+//  D k_snap_scan    per page: exclusive scan of chunk outputs, and the chunk holding each 64 KiB
+//                   output block's first element. The compressor compresses 64 KiB fragments
+//                   independently, so no element straddles a fragment and no copy reaches before it.
+//  E k_snap_exec    one 1024-thread workgroup per 64 KiB output block decodes its chunks' element
+//                   headers from the start bitmaps (a workgroup scan of the lengths gives each its
+//                   output offset), resolves every copied byte to its literal origin by pointer
+//                   jumping on a u16 map in LDS (src[p] = p - offset; literal bytes are their own
+//                   roots), then rebuilds the block's bytes in the same LDS and stores them with
+//                   dword stores. Violations of the fragment rules flag the page for k_snap_serial.
 //
-// Chunk walkers (A, C, E) stage their page bytes into LDS with coalesced loads and parse from LDS.
+// Chunk walkers (A) stage their page bytes into LDS with coalesced loads and parse from LDS.
 #include "dev_common.h"
 #include "kernels.h"
+#include "wave.h"
 
 namespace dr {
 namespace dev {
@@ -180,8 +181,8 @@ struct SpecChain {
   // visited bitmap in registers (statically indexed: each step ORs its bit into the selected word
   // with selects, so the walk issues no LDS read-modify-write of its own)
   uint32_t lv[SNAP_CH / 32];
-  uint64_t pos, cs, ce, first, out, mid;
-  uint32_t elems, hout, helems;
+  uint64_t pos, cs, ce, first, out;
+  uint32_t elems;
 };
 // A chunk past the workgroup's (not live) gets an empty walk parked at `park`, a staged position,
 // so the unconditional header read of the step loop stays inside the stage.
@@ -193,8 +194,7 @@ __device__ __forceinline__ void spec_init(SpecChain& w, uint32_t j, uint64_t n_i
   w.pos = !live ? park : w.cs >= SNAP_WU ? w.cs - SNAP_WU : 0;
   w.first = ~0ull;
   w.out = 0;
-  w.mid = ~0ull;
-  w.elems = w.hout = w.helems = 0;
+  w.elems = 0;
 }
 // One element of the walk from its header word `hw` (only when w.pos < w.ce).
 __device__ __forceinline__ void spec_step(SpecChain& w, uint64_t hw) {
@@ -208,17 +208,10 @@ __device__ __forceinline__ void spec_step(SpecChain& w, uint64_t hw) {
     if (w.first == ~0ull) w.first = w.pos;
     w.out += len;
     ++w.elems;
-    const bool h = w.pos < w.cs + SNAP_CH / 2;
-    w.hout += h ? len : 0u;
-    w.helems += h ? 1u : 0u;
-    w.mid = (!h && w.mid == ~0ull) ? w.pos : w.mid;
   }
   w.pos += adv;
 }
 __device__ __forceinline__ void spec_store(const SnappyArgs& a, const SpecChain& w, uint32_t c) {
-  a.mid_first[c] = w.mid > 0xffffffffull ? 0xffffffffu : uint32_t(w.mid);
-  a.half_out[c] = w.hout;
-  a.half_elems[c] = w.helems;
   a.spec_exit[c] = w.pos > 0xffffffffull ? 0xffffffffu : uint32_t(w.pos);
 #pragma unroll
   for (int k = 0; k < int(SNAP_CH / 32); k += 4)
@@ -246,16 +239,25 @@ __global__ void __launch_bounds__(WG_CHUNKS) k_snap_spec(SnappyArgs a) {
 // its own 64-byte LDS window (`win`: the lane's 17-dword slot, padded against bank conflicts),
 // refilled with four 16-byte loads when the next header leaves it: one round trip per dozen or so
 // elements instead of one per element. Returns the exit; out / elems: the walked elements' output
-// bytes and count.
+// bytes and count; `lv` (when given): the bitmap of the visited positions relative to `cs`.
 constexpr uint32_t WIN_DW = 17;
 __device__ uint64_t walk_window(const uint8_t* in, uint64_t e, uint64_t ce, uint32_t* win, uint64_t* out,
-                                uint32_t* elems) {
+                                uint32_t* elems, uint64_t cs = 0, uint32_t* lv = nullptr) {
   const uintptr_t ib = reinterpret_cast<uintptr_t>(in);
   uintptr_t wa = 0;
   bool have = false;
   uint64_t o = 0;
   uint32_t k = 0;
+  if (lv) {
+#pragma unroll
+    for (int q = 0; q < int(SNAP_CH / 32); ++q) lv[q] = 0;
+  }
   while (e < ce) {
+    if (lv) {  // statically indexed: each step ORs its bit into the selected word
+      const uint32_t r = uint32_t(e - cs), wi = r >> 5, bit = 1u << (r & 31);
+#pragma unroll
+      for (int q = 0; q < int(SNAP_CH / 32); ++q) lv[q] |= wi == uint32_t(q) ? bit : 0u;
+    }
     const uintptr_t ea = ib + e;
     if (!have || ea < wa || ea + 8 > wa + 64) {  // reads reach at most 63 bytes past the page input (padded)
       wa = ea & ~uintptr_t(15);
@@ -360,7 +362,8 @@ __global__ void __launch_bounds__(256) k_snap_entries(SnappyArgs a) {
 }
 
 // B3a: the regions to resolve serially: a flagged chunk with no other flag in the REGION_GAP
-// chunks before it (on the same page) starts a region; later flags nearby are covered by it.
+// chunks before it (on the same page) starts a region (chunk_flag bit 1); later flags nearby are
+// covered by it. Each page holding a region is listed once (region[], region_count).
 constexpr uint32_t RESOLVE_MARGIN = 8;
 constexpr uint32_t REGION_GAP = 80;
 __global__ void __launch_bounds__(256) k_snap_regions(SnappyArgs a) {
@@ -371,15 +374,23 @@ __global__ void __launch_bounds__(256) k_snap_regions(SnappyArgs a) {
   const uint32_t lo = c >= c0 + REGION_GAP ? c - REGION_GAP : c0;
   for (uint32_t k = lo; k < c; ++k)
     if (a.chunk_flag[k]) return;
-  const unsigned long long slot = atomicAdd(a.region_count, 1ull);
-  a.region[slot] = c;
+  a.chunk_flag[c] = 3;  // still nonzero for the other chunks' gap checks
+  if (atomicExch(&a.page_mark[p], 1u) == 0u) {
+    const unsigned long long slot = atomicAdd(a.region_count, 1ull);
+    a.region[slot] = p;
+  }
 }
 
-// B3b: one wave per region: from RESOLVE_MARGIN chunks before the flag (entries there are exact)
-// the true chain is followed 64 chunks per ballot, rewriting entries, until a whole 64-chunk step
-// beyond the flag has no break, agrees with the entries k_snap_entries wrote (from there on they
-// are exact again) and has no flag in it or within REGION_GAP after it. A chunk whose entry lies past its end (a long literal spans it) jumps to
-// the chunk holding that entry.
+// B3b: one wave per page holding regions, its regions in ascending order (r05: one wave per region
+// let a later region start from an entry an earlier, still running walk of the same page had yet to
+// correct -- unflagged wrong entries after chunks spanned by long literals; the page then failed the
+// size check and went to the serial decoder; scripts/snappy_entries_sim.py order="interleave"). From
+// RESOLVE_MARGIN chunks before the flag (entries there are exact) the true chain is followed 64
+// chunks per ballot, rewriting entries, until a whole 64-chunk step beyond the flag has no break,
+// agrees with the entries k_snap_entries wrote (from there on they are exact again) and has no flag
+// in it or within REGION_GAP after it; a region starting inside an earlier walk's range is covered
+// by it. A chunk whose entry lies past its end (a long literal spans it) jumps to the chunk holding
+// that entry.
 __global__ void __launch_bounds__(64) k_snap_resolve(SnappyArgs a) {
   constexpr uint32_t VW = SNAP_CH / 32;  // visited-bitmap words per chunk
   constexpr uint32_t CB_WORDS = (SNAP_CH + 16) / 4;
@@ -387,17 +398,22 @@ __global__ void __launch_bounds__(64) k_snap_resolve(SnappyArgs a) {
   __shared__ uint32_t nx[2][SNAP_CH];
   const uint64_t nreg = *a.region_count;
   for (uint64_t rg = blockIdx.x; rg < nreg; rg += gridDim.x) {
-    const uint32_t cf = a.region[rg];
-    const uint32_t p = chunk_page(a, cf);
+    const uint32_t p = a.region[rg];
     const SnapPage& pg = a.pages[p];
     const uint8_t* in = reinterpret_cast<const uint8_t*>(pg.in);
     const uint32_t c0 = a.chunk_base[p], nc = a.chunk_base[p + 1] - c0;
-    const uint32_t jf = cf - c0;
     const int lane = threadIdx.x;
-    uint32_t base = jf > RESOLVE_MARGIN ? jf - RESOLVE_MARGIN : 0u;
-    uint64_t e = base == 0 ? 0 : a.entry[c0 + base];  // true entry of chunk `base`
     const uint64_t t0 = a.rstats ? __builtin_amdgcn_s_memtime() : 0;
     uint32_t n_win = 0, n_walk = 0, n_span = 0;
+    uint32_t done = 0;  // chunks [0, done) of the page: resolved by an earlier walk
+    for (uint32_t q0 = 0; q0 < nc; q0 += 64) {
+    unsigned long long starts = __ballot(q0 + uint32_t(lane) < nc && (a.chunk_flag[c0 + q0 + lane] & 2u));
+    while (starts) {
+    const uint32_t jf = q0 + uint32_t(__builtin_ctzll(starts));
+    starts &= starts - 1;
+    if (jf < done) continue;
+    uint32_t base = jf > RESOLVE_MARGIN ? jf - RESOLVE_MARGIN : 0u;
+    uint64_t e = base == 0 ? 0 : a.entry[c0 + base];  // true entry of chunk `base`
     while (base < nc) {
       ++n_win;
       const uint32_t j = base + lane;
@@ -533,6 +549,9 @@ __global__ void __launch_bounds__(64) k_snap_resolve(SnappyArgs a) {
         base += cnt;
       }
     }
+    done = base < nc ? min(nc, base + 64u) : nc;  // the walk stopped in window [base, base + 64)
+    }
+    }
     if (a.rstats && lane == 0) {
       uint64_t* r = a.rstats + rg * 4;
       r[0] = __builtin_amdgcn_s_memtime() - t0;
@@ -544,21 +563,26 @@ __global__ void __launch_bounds__(64) k_snap_resolve(SnappyArgs a) {
 }
 
 // C: output bytes / elements produced by the true elements of each chunk: the speculative counts
-// unless the true entry differs from the chunk's first speculatively visited position.
+// unless the true entry differs from the chunk's first speculatively visited position. Such a chunk
+// is walked from its true entry and its visited bitmap rewritten with the true chain, so that for
+// every chunk the bits at or after its entry are exactly its element starts (k_snap_exec reads them).
 __global__ void __launch_bounds__(256) k_snap_count(SnappyArgs a) {
   __shared__ uint32_t wins[256 * WIN_DW];
   const uint32_t c = blockIdx.x * 256 + threadIdx.x;
   if (c >= a.nchunks) return;
   const uint32_t pos0 = a.entry[c];
   if (pos0 == a.spec_first[c]) return;
-  a.mid_first[c] = 0xffffffffu;  // not split: k_snap_emit walks it with one lane
   const uint32_t p = chunk_page(a, c);
   const SnapPage& pg = a.pages[p];
   const uint64_t cs = uint64_t(c - a.chunk_base[p]) * SNAP_CH;
   const uint64_t ce = min(cs + SNAP_CH, uint64_t(pg.n_in));
   uint64_t out = 0;
   uint32_t elems = 0;
-  walk_window(reinterpret_cast<const uint8_t*>(pg.in), pos0, ce, wins + threadIdx.x * WIN_DW, &out, &elems);
+  uint32_t lv[SNAP_CH / 32];
+  walk_window(reinterpret_cast<const uint8_t*>(pg.in), pos0, ce, wins + threadIdx.x * WIN_DW, &out, &elems, cs, lv);
+#pragma unroll
+  for (int k = 0; k < int(SNAP_CH / 32); k += 4)
+    *reinterpret_cast<uint4*>(&a.vis[uint64_t(c) * (SNAP_CH / 32) + k]) = make_uint4(lv[k], lv[k + 1], lv[k + 2], lv[k + 3]);
   a.chunk_out[c] = out > 0xffffffffull ? 0xffffffffu : uint32_t(out);
   a.chunk_elems[c] = elems;
 }
@@ -588,128 +612,104 @@ __global__ void __launch_bounds__(SCAN_T) k_snap_scan(SnappyArgs a) {
     before += q < wv ? wsum[q] : 0ull;
     total += wsum[q];
   }
+  // the chunk holding each output block's first element (no element straddles a block, so that
+  // element starts the block): block k of the page is first produced by the chunk whose output range
+  // [at, at + out) holds k * SNAP_BLOCK; blocks no chunk claims keep ~0 (k_snap_exec: bad page)
+  const uint32_t bb = a.pages[p].block_base, nb = (a.pages[p].n_out + SNAP_BLOCK - 1) / SNAP_BLOCK;
+  for (uint32_t k = t; k < nb; k += SCAN_T) a.block_chunk[bb + k] = 0xffffffffu;
+  __syncthreads();
   uint64_t at = before + incl - run;
   for (uint32_t j = j0; j < j1; ++j) {
     a.chunk_out_start[c0 + j] = uint32_t(at);
-    at += a.chunk_out[c0 + j];
+    const uint32_t n = a.chunk_out[c0 + j];
+    if (n) {
+      const uint64_t k0 = (at + SNAP_BLOCK - 1) / SNAP_BLOCK, k1 = min((at + n - 1) / SNAP_BLOCK + 1, uint64_t(nb));
+      for (uint64_t k = k0; k < k1; ++k) a.block_chunk[bb + k] = c0 + j;
+    }
+    at += n;
   }
   if (t == 0 && total != a.pages[p].n_out) atomicOr(&a.pages_bad[p], 1u);  // size mismatch
 }
 
-// E: one 8-byte record per element, {output offset in its 64 KiB block u16 | (len-1) u16 << 16 |
-// src u32 << 32}; src = copy offset, or REC_LIT | input position for a literal. The element that
-// starts a block (no element straddles one) records the block's first record index. Each lane
-// stores its chunk's records directly (consecutive lines per lane; the L2 merges them), which
-// keeps the LDS to the input stage and two workgroups per CU.
-constexpr uint32_t REC_LIT = 0x80000000u;
-#ifndef DR_EMIT_BURST
-#define DR_EMIT_BURST 0
-#endif
-constexpr uint32_t EMIT_BURST = DR_EMIT_BURST ? DR_EMIT_BURST : 1;
-
-__global__ void __launch_bounds__(2 * WG_CHUNKS) k_snap_emit(SnappyArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t buf[STAGE_BYTES + 32];
-  const WgInfo g = wg_info(a);
-  const SnapPage& pg = a.pages[g.p];
-  const Staged s = stage_input(buf, reinterpret_cast<const uint8_t*>(pg.in), pg.n_in, g.j0, g.cnt);
-  const uint32_t cfirst = a.chunk_base[g.p] + g.j0;
-  const uint32_t q = threadIdx.x % WG_CHUNKS, half = threadIdx.x / WG_CHUNKS;
-  if (q < g.cnt) {
-    const uint32_t j = g.j0 + q;
-    const uint32_t c = cfirst + q;
-    const uint64_t cs = uint64_t(j) * SNAP_CH;
-    const uint64_t mid = a.mid_first[c];
-    uint64_t pos = a.entry[c], o = a.chunk_out_start[c];
-    uint64_t rec = a.chunk_rec_start[c];
-    uint64_t ce = min(cs + SNAP_CH, uint64_t(pg.n_in));
-    if (half == 0) {
-      ce = mid != 0xffffffffull ? mid : ce;  // the first half's elements end where the second's begin
-    } else {
-      if (mid == 0xffffffffull) ce = 0;  // not split: nothing for the second lane
-      pos = mid;
-      o += a.half_out[c];
-      rec += a.half_elems[c];
-    }
-    bool bad = false;
-    // one element: its record, or false at the end / on a malformed element
-    auto next = [&](uint64_t& r64) -> bool {
-      if (pos >= ce || bad) return false;
-      // branch-free decode (the lanes' element types differ; a switch serialises them)
-      const uint64_t w = staged_u64(buf, s, pos);
-      uint32_t adv, len;
-      snap_step(w, &adv, &len);
-      const uint32_t tag = uint32_t(w & 0xff), t = tag & 3u;
-      const bool lit = t == 0;
-      const uint32_t w8 = uint32_t(w >> 8);
-      const uint32_t off = t == 1 ? (((tag >> 5) << 8) | (w8 & 0xffu)) : t == 2 ? (w8 & 0xffffu) : w8;
-      const uint64_t ip = pos + (adv - (lit ? len : 0u));  // a literal's first input byte
-      const uint32_t orel = uint32_t(o & (SNAP_BLOCK - 1));
-      bad = len == 0 || len > SNAP_BLOCK || o + len > pg.n_out || orel + len > SNAP_BLOCK ||
-            (lit ? (ip + len > pg.n_in || ip >= REC_LIT) : (off == 0 || off > orel));  // a copy reaching before its fragment
-      if (bad) return false;
-      if (orel == 0) a.block_rec[pg.block_base + uint32_t(o >> 16)] = rec;
-      const uint32_t src = lit ? (REC_LIT | uint32_t(ip)) : off;
-      r64 = orel | (uint64_t(len - 1) << 16) | (uint64_t(src) << 32);
-      ++rec;
-      o += len;
-      pos += lit ? uint64_t(ip - pos) + len : adv;
-      return true;
-    };
-#if DR_EMIT_BURST
-    // records leave in bursts of EMIT_BURST consecutive ones per lane (back-to-back stores of one
-    // lane's contiguous range, so the L2 sees each 64-byte run whole instead of one 8-byte piece per
-    // element step while 63 other lanes' lines compete for it)
-    for (;;) {
-      uint64_t rb[EMIT_BURST];
-      const uint64_t r0 = rec;
-      uint32_t m = 0;
-#pragma unroll
-      for (uint32_t q = 0; q < EMIT_BURST; ++q)
-        if (m == q && next(rb[q])) ++m;
-#pragma unroll
-      for (uint32_t q = 0; q < EMIT_BURST; ++q)
-        if (q < m) a.recs[r0 + q] = rb[q];
-      if (m < EMIT_BURST) break;
-    }
-#else
-    for (uint64_t r64; next(r64);) a.recs[rec - 1] = r64;
-#endif
-    if (bad) atomicOr(&a.pages_bad[g.p], 8u);
-  }
-}
-
-// F: one 1024-thread workgroup per 64 KiB output block; its element records are
-// [block_rec[b], block_rec[b+1]) with block-relative output offsets.
-//  1. map[i] = i, then every copy byte i := i - offset (u16 map of the block in LDS);
-//  2. pointer jumping until every byte points at its literal origin (chains of copies of copies
-//     are as long as the number of repeated path prefixes in the fragment; log2 rounds; a byte
-//     leaves its thread's pending mask once it points at a root);
-//  3. each thread keeps the roots of its 16 4-byte groups in registers; the LDS is reused as the
-//     block's bytes (lower half) and its compressed input range (upper half, 16-byte loads);
-//     literal runs are copied LDS -> LDS;
+// E: k_snap_exec -- one 1024-thread workgroup per 64 KiB output block, fed by the compressed page
+// itself (r05: the 8-byte element records k_snap_emit wrote to HBM at 2.4x amplification and this
+// kernel read back are gone, and so is the emit launch).
+//  0. the block's chunks are [block_chunk[b], the chunk holding the next block's first element]; the
+//     bits of a chunk's visited bitmap at or after its true entry are exactly its element starts
+//     (chains that meet coincide; k_snap_count rewrote the chunks whose true chain is another one);
+//  1. in passes of 16 KiB of compressed input staged in LDS, 16 positions per thread (the next pass's
+//     bytes, bitmap word and entry in flight meanwhile): each thread decodes the element headers at
+//     its start bits, a workgroup scan of their output lengths gives every element its output offset
+//     (from the first chunk's k_snap_scan offset), and the elements of this block set their start bit
+//     and the map entry of their first byte (src[rel] = rel - offset; a literal points at itself);
+//  2. every byte's map entry from the last start at or before it, then pointer jumping until every
+//     byte points at its literal origin (u16 map of the block in LDS, roots in registers);
+//  3. the LDS becomes the block's bytes (lower half) and its compressed input (upper half); each
+//     thread re-decodes its start bits (kept in registers with its per-pass output offsets) and copies
+//     its literals LDS -> LDS, reads batched ahead of writes; long literals go to whole waves;
 //  4. each thread gathers its groups' bytes from their roots and stores them (coalesced dwords).
+// Every element of the chunk range is checked (a copy reaching before its fragment, an element
+// straddling a block, literal bytes past the page) and the block's elements must cover it exactly;
+// anything else flags the page for k_snap_serial.
 constexpr int EXEC_T = 1024;
-constexpr uint32_t EXEC_LONG = 256;          // literal records queued for the cooperative copy (at most)
+constexpr uint32_t PASS_POS = 16;                   // compressed positions per thread and pass
+constexpr uint32_t PASS_BYTES = EXEC_T * PASS_POS;  // compressed bytes per pass
+constexpr uint32_t EXEC_MAXP = 6;                   // passes a block may take (96 KiB of compressed input)
+constexpr uint32_t STG_VEC = EXEC_T + 3;            // staged 16-byte vectors per pass (alignment + header reach)
+constexpr uint32_t EXEC_LONG = 256;                 // literal records queued for the cooperative copy (at most)
 #ifndef DR_EXEC_LONG_LEN
 #define DR_EXEC_LONG_LEN 64
 #endif
 constexpr uint32_t EXEC_LONG_LEN = DR_EXEC_LONG_LEN;  // literals longer than this are copied by a whole wave
-#ifndef DR_EXEC_RPT
-#define DR_EXEC_RPT 12
-#endif
-constexpr uint32_t EXEC_RPT = DR_EXEC_RPT;            // records per thread held in registers per pass
-#ifndef DR_EXEC_RPT2
-#define DR_EXEC_RPT2 4
-#endif
-constexpr uint32_t EXEC_RPT2 = DR_EXEC_RPT2;            // literal records per thread per pass (roots live in registers)
 #ifndef DR_EXEC_SPLIT
 #define DR_EXEC_SPLIT 4
 #endif
 constexpr uint32_t EXEC_SPLIT = DR_EXEC_SPLIT;  // map groups whose reads are issued before their writes (divides 16; 1: 2.725 ms, 4: 2.693, 16: spills, 2.83)
 
+// An element's fields from its header word.
+struct SnapEl {
+  uint32_t len, hdr, off;  // output bytes, header bytes, copy offset
+  bool lit;
+};
+__device__ __forceinline__ SnapEl snap_fields(uint64_t w) {
+  uint32_t adv, len;
+  snap_step(w, &adv, &len);
+  const uint32_t tag = uint32_t(w & 0xff), t = tag & 3u, w8 = uint32_t(w >> 8);
+  SnapEl e;
+  e.len = len;
+  e.lit = t == 0;
+  e.hdr = e.lit ? adv - len : adv;
+  e.off = t == 1 ? (((tag >> 5) << 8) | (w8 & 0xffu)) : t == 2 ? (w8 & 0xffffu) : w8;
+  return e;
+}
+// Header bytes at byte offset o of a dword-addressed LDS buffer (the low five are exact).
+__device__ __forceinline__ uint64_t lds_hdr(const uint32_t* b32, uint32_t o) {
+  const uint32_t di = o >> 2, sh = o & 3;
+  return ((uint64_t(b32[di + 1]) << 32) | b32[di]) >> (8 * sh);
+}
+// Exclusive workgroup scan (EXEC_T threads) of x; `total` gets the sum. Contains one barrier; the
+// caller separates two calls by another (the wave sums are reused).
+__device__ __forceinline__ uint32_t block_excl(uint32_t x, uint32_t* wsum, uint32_t& total) {
+  const uint32_t incl = wv::scan_incl(x, 0u, [](uint32_t p, uint32_t q) { return p + q; });
+  const uint32_t wi = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 63) wsum[wi] = incl;
+  __syncthreads();
+  uint32_t before = 0, tot = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < EXEC_T / 64; ++q) {
+    const uint32_t v = wsum[q];
+    before += q < wi ? v : 0u;
+    tot += v;
+  }
+  total = tot;
+  return before + incl - x;
+}
+
 __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t src[SNAP_BLOCK];  // map, later bytes + input
-  __shared__ uint32_t s_bad, s_nlong, s_inlo, s_inhi;
+  __shared__ __attribute__((aligned(16))) uint32_t stg[STG_VEC * 4];  // one pass of compressed input
+  __shared__ uint32_t s_bad, s_nlong, s_cov;
+  __shared__ uint32_t s_wsum[EXEC_T / 64];
   __shared__ uint64_t s_long[EXEC_LONG];  // queued long literal records
   __shared__ uint32_t starts_mem[SNAP_BLOCK / 32 + 2];  // element start bits, after two zero words
   uint32_t* const starts = starts_mem + 2;
@@ -728,59 +728,133 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     if (a.stamps && t == 0) a.stamps[uint64_t(b) * 8 + k] = __builtin_amdgcn_s_memtime();
   };
   stamp(0);
+  // 0. the block's chunk range and compressed range [P_lo, P_hi) (block-uniform)
+  const uint32_t c0 = a.chunk_base[p], ncp = a.chunk_base[p + 1] - c0;
+  const uint32_t cl = a.block_chunk[b];
+  const bool last_blk = b + 1 >= a.nblocks || a.block_page[b + 1] != p;
+  const uint32_t cn = last_blk ? c0 + ncp : a.block_chunk[b + 1] + 1u;  // ~0 (unclaimed) wraps to 0
+  const bool range_ok = cl >= c0 && cl < c0 + ncp && cn > cl && cn <= c0 + ncp;
+  const uint64_t P_lo = range_ok ? uint64_t(cl - c0) * SNAP_CH : 0;
+  const uint64_t P_hi = range_ok ? min(uint64_t(cn - c0) * SNAP_CH, uint64_t(pg.n_in)) : 0;
+  const uint32_t npass = P_hi > P_lo ? uint32_t((P_hi - P_lo + PASS_BYTES - 1) / PASS_BYTES) : 0u;
+  if (npass == 0 || npass > EXEC_MAXP) {
+    if (t == 0) atomicOr(&a.pages_bad[p], 16u);
+    return;
+  }
   if (t == 0) {
     s_bad = 0;
     s_nlong = 0;
-    s_inlo = 0xffffffffu;
-    s_inhi = 0;
+    s_cov = 0;
   }
   for (uint32_t w = t; w < SNAP_BLOCK / 32 + 2; w += EXEC_T) starts_mem[w] = 0;
-  const uint64_t r0 = a.block_rec[b];
-  const uint64_t r1 = b + 1 < a.nblocks ? a.block_rec[b + 1] : a.chunk_rec_start[a.nchunks];
-  const uint32_t nrec = uint32_t(r1 - r0);
-  __syncthreads();
-  stamp(1);
-  // 1a. per element: its start bit, and the map entry of its first byte (start - offset; a
-  //     literal points at itself)
-  uint32_t lo_in = 0xffffffffu, hi_in = 0;
-  const bool held = nrec <= EXEC_T * EXEC_RPT;  // block-uniform: one pass, records stay in w for step 3
-  uint64_t w[EXEC_RPT];
-  for (uint32_t base = 0; base < nrec; base += EXEC_T * EXEC_RPT) {
-#pragma unroll
-    for (uint32_t k = 0; k < EXEC_RPT; ++k) {
-      const uint32_t r = base + k * EXEC_T + uint32_t(t);
-      w[k] = r < nrec ? a.recs[r0 + r] : 0ull;
+  const uintptr_t ib = reinterpret_cast<uintptr_t>(in);
+  const uint32_t sh0 = uint32_t((ib + P_lo) & 15);  // the stage's first byte sits sh0 bytes into a vector
+  // one pass's inputs: the thread's stage vectors, its 16 positions' bitmap word and chunk entry
+  struct Pf {
+    uint4 v0, v1;
+    uint32_t vw, ent;
+  };
+  auto fetch = [&](uint32_t k) -> Pf {
+    Pf f;
+    const uint64_t ps = P_lo + uint64_t(k) * PASS_BYTES;
+    const uint64_t cnt = min(uint64_t(PASS_BYTES), P_hi - ps);
+    const uint32_t nv = uint32_t((sh0 + cnt + 8 + 15) / 16);  // reads reach 8 bytes past the range (padded input)
+    const uint4* g4 = reinterpret_cast<const uint4*>(ib + ps - sh0);
+    f.v0 = gload16(g4 + min(uint32_t(t), nv - 1));
+    f.v1 = t < 3 ? gload16(g4 + min(uint32_t(t) + EXEC_T, nv - 1)) : make_uint4(0, 0, 0, 0);
+    const uint64_t q0 = ps + uint64_t(t) * PASS_POS;
+    f.vw = 0;
+    f.ent = 0xffffffffu;
+    if (q0 < P_hi) {
+      const uint32_t j = uint32_t(q0 / SNAP_CH);
+      f.vw = a.vis[uint64_t(c0 + j) * (SNAP_CH / 32) + uint32_t((q0 % SNAP_CH) / 32)];
+      f.ent = a.entry[c0 + j];
     }
+    return f;
+  };
+  auto store_stage = [&](const Pf& f) {
+    reinterpret_cast<uint4*>(stg)[t] = f.v0;
+    if (t < 3) reinterpret_cast<uint4*>(stg)[EXEC_T + t] = f.v1;
+  };
+  // the thread's element starts among positions q0 .. q0+15 of pass k: visited bits at or after the
+  // chunk's true entry, below the range end
+  auto pass_bits = [&](const Pf& f, uint32_t k) -> uint32_t {
+    const uint64_t q0 = P_lo + uint64_t(k) * PASS_BYTES + uint64_t(t) * PASS_POS;
+    if (q0 >= P_hi) return 0u;
+    uint32_t m = (f.vw >> (uint32_t(q0) & 16u)) & 0xffffu;
+    if (uint64_t(f.ent) > q0) {
+      const uint64_t cut = uint64_t(f.ent) - q0;
+      m = cut >= PASS_POS ? 0u : m & ~((1u << uint32_t(cut)) - 1u);
+    }
+    if (q0 + PASS_POS > P_hi) m &= (1u << uint32_t(P_hi - q0)) - 1u;
+    return m;
+  };
+  // 1. element offsets, start bits and first-byte map entries, pass by pass
+  uint32_t hold[(EXEC_MAXP + 1) / 2];  // start bits of each pass, two passes per register
+  uint32_t pref[EXEC_MAXP];            // page-relative output offset of the thread's first element per pass
 #pragma unroll
-    for (uint32_t k = 0; k < EXEC_RPT; ++k) {
-      const uint32_t r = base + k * EXEC_T + uint32_t(t);
-      if (r >= nrec) continue;
-      const uint32_t sv = uint32_t(w[k] >> 32);
-      const uint32_t rel = uint32_t(w[k] & 0xffff);
-      const uint32_t len = uint32_t((w[k] >> 16) & 0xffff) + 1;
-      if (rel + len > nbytes) { s_bad = 1; continue; }
-      atomicOr(&starts[rel >> 5], 1u << (rel & 31));
-      if (sv & REC_LIT) {
-        lo_in = min(lo_in, sv & ~REC_LIT);
-        hi_in = max(hi_in, (sv & ~REC_LIT) + len);
-        src[rel] = uint16_t(rel);
-      } else {
-        if (sv > rel || len > 64) { s_bad = 1; continue; }  // snappy copies are at most 64 bytes
-        src[rel] = uint16_t(rel - sv);
+  for (uint32_t k = 0; k < (EXEC_MAXP + 1) / 2; ++k) hold[k] = 0;
+  uint64_t obase = a.chunk_out_start[cl];  // page-relative output offset of the pass's first element
+  uint32_t cov = 0;
+  bool bad = false;
+  Pf cur = fetch(0);
+  store_stage(cur);
+#pragma unroll
+  for (uint32_t k = 0; k < EXEC_MAXP; ++k) {
+    if (k >= npass) break;  // block-uniform
+    __syncthreads();        // the pass's stage (and, for pass 0, the cleared start bits) visible
+    Pf nxt;
+    if (k + 1 < npass) nxt = fetch(k + 1);
+    const uint32_t bits = pass_bits(cur, k);
+    const uint32_t o0 = sh0 + uint32_t(t) * PASS_POS;  // stage byte of the thread's first position
+    uint32_t sum = 0;
+    for (uint32_t m = bits; m; m &= m - 1) {
+      uint32_t adv, len;
+      snap_step(lds_hdr(stg, o0 + uint32_t(__builtin_ctz(m))), &adv, &len);
+      sum += min(len, SNAP_BLOCK + 1);  // a longer element is invalid anyway (it straddles a fragment)
+    }
+    uint32_t total;
+    const uint32_t ex = block_excl(sum, s_wsum, total);
+    uint64_t o = obase + ex;
+    pref[k] = uint32_t(o);
+    hold[k / 2] |= bits << (16 * (k & 1));
+    const uint64_t qb = P_lo + uint64_t(k) * PASS_BYTES + uint64_t(t) * PASS_POS;
+    for (uint32_t m = bits; m; m &= m - 1) {
+      const uint32_t i = uint32_t(__builtin_ctz(m));
+      const SnapEl e = snap_fields(lds_hdr(stg, o0 + i));
+      const uint32_t len = min(e.len, SNAP_BLOCK + 1);
+      if (o < be && o + len > bs) {
+        const uint32_t rel = uint32_t(o - bs);
+        const uint64_t ip = qb + i + e.hdr;  // a literal's first input byte
+        if (o < bs || o + len > be || len > SNAP_BLOCK ||
+            (e.lit ? (ip + len > pg.n_in) : (e.off == 0 || e.off > rel || len > 64))) {
+          bad = true;  // straddles the block, overruns the page, or a copy reaching before its fragment
+        } else {
+          atomicOr(&starts[rel >> 5], 1u << (rel & 31));
+          src[rel] = uint16_t(e.lit ? rel : rel - e.off);
+          cov += len;
+        }
+      } else if (len > SNAP_BLOCK) {
+        bad = true;
       }
+      o += len;
+    }
+    obase += total;
+    __syncthreads();  // every thread is done with the stage and the scan words
+    if (k + 1 < npass) {
+      store_stage(nxt);
+      cur = nxt;
     }
   }
-  for (int o = 32; o > 0; o >>= 1) {
-    lo_in = min(lo_in, uint32_t(__shfl_xor(int(lo_in), o, 64)));
-    hi_in = max(hi_in, uint32_t(__shfl_xor(int(hi_in), o, 64)));
+  if (bad) s_bad = 1;
+  {
+    const uint32_t cw = wv::scan_incl(cov, 0u, [](uint32_t x, uint32_t y) { return x + y; });
+    if ((t & 63) == 63) atomicAdd(&s_cov, cw);
   }
-  if ((t & 63) == 0) {
-    atomicMin(&s_inlo, lo_in);
-    atomicMax(&s_inhi, hi_in);
-  }
+  stamp(1);
   __syncthreads();
   stamp(2);
-  if (s_bad) {
+  if (s_bad || s_cov != nbytes) {  // block-uniform: the block's elements must cover it exactly
     if (t == 0) atomicOr(&a.pages_bad[p], 32u);
     return;
   }
@@ -878,75 +952,79 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     }
   }
   __syncthreads();
-  // 3. the LDS becomes the block's bytes (lower half) and its compressed input range (upper half)
+  // 3. the LDS becomes the block's bytes (lower half) and its compressed input (upper half: the
+  //    block's whole range, headers included, so each thread re-decodes its start bits from it)
   uint8_t* bytes = reinterpret_cast<uint8_t*>(src);
   uint8_t* stage = bytes + SNAP_BLOCK;
-  const uint32_t in_lo = s_inlo, in_hi = s_inhi;
-  const uintptr_t abs_lo = (reinterpret_cast<uintptr_t>(in) + in_lo) & ~uintptr_t(15);
-  const uint32_t nv = in_lo < in_hi ? uint32_t((reinterpret_cast<uintptr_t>(in) + in_hi - abs_lo + 15) >> 4) : 0u;
-  const bool staged = nv * 16 <= SNAP_BLOCK;
-  if (staged && nv) {  // all of a thread's loads in flight at once (nv <= SNAP_BLOCK / 16: four per thread)
-    const uint4* g4 = reinterpret_cast<const uint4*>(abs_lo);
+  const uint32_t nv_all = uint32_t((sh0 + (P_hi - P_lo) + 8 + 15) / 16);
+  const bool staged = nv_all * 16 <= SNAP_BLOCK;  // block-uniform
+  if (staged) {  // all of a thread's loads in flight at once (nv_all <= SNAP_BLOCK / 16: four per thread)
+    const uint4* g4 = reinterpret_cast<const uint4*>(ib + P_lo - sh0);
     uint4* s4 = reinterpret_cast<uint4*>(stage);
     constexpr uint32_t PER = SNAP_BLOCK / 16 / EXEC_T;
     uint4 v[PER];
 #pragma unroll
-    for (uint32_t k = 0; k < PER; ++k) v[k] = gload16(g4 + min(uint32_t(t) + k * EXEC_T, nv - 1));
+    for (uint32_t k = 0; k < PER; ++k) v[k] = gload16(g4 + min(uint32_t(t) + k * EXEC_T, nv_all - 1));
 #pragma unroll
     for (uint32_t k = 0; k < PER; ++k)
-      if (uint32_t(t) + k * EXEC_T < nv) s4[uint32_t(t) + k * EXEC_T] = v[k];
+      if (uint32_t(t) + k * EXEC_T < nv_all) s4[uint32_t(t) + k * EXEC_T] = v[k];
   }
   __syncthreads();
   stamp(4);
-  // literal record r (its word wk): LDS -> LDS copy, or queued for the whole workgroup when long
-  auto copy_lit = [&](uint64_t wk, uint32_t r) {
-      const uint32_t sv = uint32_t(wk >> 32);
-      if (r >= nrec || !(sv & REC_LIT)) return;
-      const uint32_t rel = uint32_t(wk & 0xffff);
-      const uint32_t len = uint32_t((wk >> 16) & 0xffff) + 1;
-      if (len > EXEC_LONG_LEN) {  // queued while there is room, else copied by this lane below
-        const uint32_t slot = atomicAdd(&s_nlong, 1u);
-        if (slot < EXEC_LONG) {
-          s_long[slot] = wk;
-          return;
-        }
-      }
-      if (!staged) {  // a poorly compressible block: its input does not fit the stage; read it in place
-        const uint8_t* sp = in + (sv & ~REC_LIT);
-        for (uint32_t i = 0; i < len; ++i) bytes[rel + i] = sp[i];
+  // a literal of this block (rel, len, page-relative input position ip): LDS -> LDS copy, or queued
+  // for a whole wave when long
+  auto copy_lit = [&](uint32_t rel, uint32_t len, uint64_t ip) {
+    if (len > EXEC_LONG_LEN) {  // queued while there is room, else copied by this lane below
+      const uint32_t slot = atomicAdd(&s_nlong, 1u);
+      if (slot < EXEC_LONG) {
+        s_long[slot] = uint64_t(rel) | (uint64_t(len - 1) << 16) | (uint64_t(uint32_t(ip)) << 32);
         return;
       }
-      // byte head up to a 4-byte aligned destination, then aligned dword stores of realigned
-      // source dwords, then a byte tail
-      uint32_t q = uint32_t(reinterpret_cast<uintptr_t>(in) + (sv & ~REC_LIT) - abs_lo) + SNAP_BLOCK;
-      uint32_t d = rel, n = len;
-      while (n && (d & 3)) { bytes[d++] = bytes[q++]; --n; }
-      const uint32_t sh = q & 3;
-      const uint32_t* qa = reinterpret_cast<const uint32_t*>(bytes + (q & ~3u));
-      uint32_t* da = reinterpret_cast<uint32_t*>(bytes + d);
-      uint32_t lo = qa[0];
-      for (; n >= 4; n -= 4) {
-        const uint32_t hi = *++qa;
-        *da++ = __builtin_amdgcn_alignbyte(hi, lo, sh);
-        lo = hi;
-      }
-      d = uint32_t(reinterpret_cast<uint8_t*>(da) - bytes);
-      q = uint32_t(reinterpret_cast<const uint8_t*>(qa) - bytes) + sh;
-      while (n) { bytes[d++] = bytes[q++]; --n; }
+    }
+    if (!staged) {  // a poorly compressible block: its input does not fit the stage; read it in place
+      const uint8_t* sp = in + ip;
+      for (uint32_t i = 0; i < len; ++i) bytes[rel + i] = sp[i];
+      return;
+    }
+    // byte head up to a 4-byte aligned destination, then aligned dword stores of realigned source
+    // dwords (five reads in flight before four writes: one LDS round trip per 16 bytes), a byte tail
+    uint32_t q = uint32_t(ip - P_lo) + sh0 + SNAP_BLOCK;
+    uint32_t d = rel, n = len;
+    while (n && (d & 3)) { bytes[d++] = bytes[q++]; --n; }
+    const uint32_t sh = q & 3;
+    const uint32_t* qa = reinterpret_cast<const uint32_t*>(bytes + (q & ~3u));
+    uint32_t* da = reinterpret_cast<uint32_t*>(bytes + d);
+    for (; n >= 16; n -= 16) {
+      const uint32_t s0 = qa[0], s1 = qa[1], s2 = qa[2], s3 = qa[3], s4 = qa[4];
+      da[0] = __builtin_amdgcn_alignbyte(s1, s0, sh);
+      da[1] = __builtin_amdgcn_alignbyte(s2, s1, sh);
+      da[2] = __builtin_amdgcn_alignbyte(s3, s2, sh);
+      da[3] = __builtin_amdgcn_alignbyte(s4, s3, sh);
+      qa += 4;
+      da += 4;
+    }
+    for (; n >= 4; n -= 4) {
+      *da++ = __builtin_amdgcn_alignbyte(qa[1], qa[0], sh);
+      ++qa;
+    }
+    d = uint32_t(reinterpret_cast<uint8_t*>(da) - bytes);
+    q = uint32_t(reinterpret_cast<const uint8_t*>(qa) - bytes) + sh;
+    while (n) { bytes[d++] = bytes[q++]; --n; }
   };
-  if (held) {
 #pragma unroll
-    for (uint32_t k = 0; k < EXEC_RPT; ++k) copy_lit(w[k], k * EXEC_T + uint32_t(t));
-  } else {
-    for (uint32_t base = 0; base < nrec; base += EXEC_T * EXEC_RPT2) {
-      uint64_t w2[EXEC_RPT2];
-#pragma unroll
-      for (uint32_t k = 0; k < EXEC_RPT2; ++k) {
-        const uint32_t r = base + k * EXEC_T + uint32_t(t);
-        w2[k] = r < nrec ? a.recs[r0 + r] : 0ull;
-      }
-#pragma unroll
-      for (uint32_t k = 0; k < EXEC_RPT2; ++k) copy_lit(w2[k], base + k * EXEC_T + uint32_t(t));
+  for (uint32_t k = 0; k < EXEC_MAXP; ++k) {
+    if (k >= npass) break;  // block-uniform
+    const uint32_t bits = (hold[k / 2] >> (16 * (k & 1))) & 0xffffu;
+    uint64_t o = pref[k];
+    const uint64_t qb = P_lo + uint64_t(k) * PASS_BYTES + uint64_t(t) * PASS_POS;
+    for (uint32_t m = bits; m; m &= m - 1) {
+      const uint64_t q = qb + uint32_t(__builtin_ctz(m));
+      const uint64_t w = staged ? lds_hdr(reinterpret_cast<const uint32_t*>(stage), uint32_t(q - P_lo) + sh0)
+                                : load_u64(in + q);
+      const SnapEl e = snap_fields(w);
+      const uint32_t len = min(e.len, SNAP_BLOCK + 1);
+      if (e.lit && o >= bs && o < be) copy_lit(uint32_t(o - bs), len, q + e.hdr);
+      o += len;
     }
   }
   __syncthreads();
@@ -956,9 +1034,9 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     const uint64_t wl = s_long[L];
     const uint32_t rel = uint32_t(wl & 0xffff);
     const uint32_t len = uint32_t((wl >> 16) & 0xffff) + 1;
-    const uint32_t ipo = uint32_t(wl >> 32) & ~REC_LIT;
+    const uint32_t ipo = uint32_t(wl >> 32);
     if (staged) {
-      const uint32_t q = uint32_t(reinterpret_cast<uintptr_t>(in) + ipo - abs_lo) + SNAP_BLOCK;
+      const uint32_t q = ipo - uint32_t(P_lo) + sh0 + SNAP_BLOCK;
       for (uint32_t i = uint32_t(t) & 63; i < len; i += 64) bytes[rel + i] = bytes[q + i];
     } else {
       const uint8_t* ip = in + ipo;
@@ -967,10 +1045,6 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
   }
   __syncthreads();
   stamp(6);
-  if (s_bad) {  // block-uniform
-    if (t == 0) atomicOr(&a.pages_bad[p], 64u);
-    return;
-  }
   // 4. gather and store: the thread's 4-byte groups are the ones it resolved (roots still in
   //    registers); a wave's 64 groups are 256 contiguous bytes, so literal bytes (their own roots)
   //    and runs of one copy read consecutive LDS banks, and the dword stores coalesce
@@ -1036,6 +1110,7 @@ uint32_t snappy_wg_chunks() { return dev::WG_CHUNKS; }
 uint32_t snappy_chunk_bytes() { return dev::SNAP_CH; }
 
 void launch_snappy(const SnappyArgs& a, hipStream_t st, ScanScratch scan_scratch) {
+  (void)scan_scratch;
   if (!a.npages) return;
   DR_LAUNCH(dev::k_snap_spec, dim3(a.nwg), dim3(dev::WG_CHUNKS), 0, st, a);
   const unsigned g = (a.nchunks + 255) / 256;
@@ -1045,8 +1120,6 @@ void launch_snappy(const SnappyArgs& a, hipStream_t st, ScanScratch scan_scratch
   DR_LAUNCH(dev::k_snap_resolve, dim3(512), dim3(64), 0, st, a);
   DR_LAUNCH(dev::k_snap_count, dim3(g), dim3(256), 0, st, a);
   DR_LAUNCH(dev::k_snap_scan, dim3(a.npages), dim3(dev::SCAN_T), 0, st, a);
-  launch_scan_u32(a.chunk_elems, a.chunk_rec_start, a.nchunks, scan_scratch, st);
-  DR_LAUNCH(dev::k_snap_emit, dim3(a.nwg), dim3(2 * dev::WG_CHUNKS), 0, st, a);
   DR_LAUNCH(dev::k_snap_exec, dim3(a.nblocks), dim3(dev::EXEC_T), 0, st, a);
   DR_LAUNCH(dev::k_snap_serial, dim3((a.npages + 63) / 64), dim3(64), 0, st, a);
 }

@@ -174,29 +174,22 @@ struct SnappyArgs {
   uint32_t* spec_first;         // [nchunks] first speculatively visited position >= chunk start
   uint32_t* assumed_exit;       // [nchunks] exit assuming the previous chunk's speculative exit
   uint8_t* chunk_flag;          // [nchunks] 1: serial resolution from this chunk
-  uint32_t* region;             // [nchunks] chunks starting a serially resolved region
+  uint32_t* region;             // [npages] pages holding a serially resolved region (k_snap_regions)
   unsigned long long* region_count;
+  uint32_t* page_mark;          // [npages] zeroed per replay: the page is listed in region[]
   uint32_t* chunk_out;          // [nchunks] output bytes of the chunk's elements
-  uint32_t* chunk_out_start;    // [nchunks]
-  uint32_t* chunk_elems;        // [nchunks] elements per chunk
-  uint64_t* chunk_rec_start;    // [nchunks + 1] exclusive scan of chunk_elems
-  uint64_t* recs;               // element records (k_snap_emit)
+  uint32_t* chunk_out_start;    // [nchunks] page-relative output offset of the chunk's first element
+  uint32_t* chunk_elems;        // [nchunks] elements per chunk (statistics)
   const uint32_t* block_page;   // [nblocks]
-  uint64_t* block_rec;          // [nblocks] first element record of each output block
+  uint32_t* block_chunk;        // [nblocks] chunk holding each output block's first element (k_snap_scan)
   uint32_t nblocks;
   const uint32_t* wg_chunk0;    // [nwg] first chunk (global index) of each chunk-walker workgroup
   uint32_t nwg;
   uint32_t* pages_bad;          // [npages] nonzero -> decoded by the serial fallback
   uint32_t* error;
-  uint64_t* stamps;             // diagnostics: [nblocks * 8] k_snap_exec phase clocks, or null
-  uint64_t* rstats;             // diagnostics: [regions * 4] k_snap_resolve {clocks, windows, walks, spans}, or null
-  // second-half split of each chunk's walk (k_snap_emit runs two lanes per chunk): the first element
-  // starting in the chunk's second half, and the output bytes / elements before it; mid_first is
-  // ~0 when the chunk is not split (its true entry is not its speculative first position)
-  uint32_t* mid_first = nullptr;
-  uint32_t* half_out = nullptr;
-  uint32_t* half_elems = nullptr;
-  const uint32_t* chunk_page = nullptr;  // [nchunks] page of each chunk
+  const uint32_t* chunk_page;   // [nchunks] page of each chunk
+  uint64_t* stamps = nullptr;   // diagnostics: [nblocks * 8] k_snap_exec phase clocks, or null
+  uint64_t* rstats = nullptr;   // diagnostics: [regions * 4] k_snap_resolve {clocks, windows, walks, spans}, or null
 };
 uint32_t snappy_wg_chunks();
 uint32_t snappy_chunk_bytes();

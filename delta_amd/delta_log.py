@@ -410,6 +410,80 @@ class State:
                             "partitionValues": pvs[i], "size": sizes[i], "tags": tags[i]})
         return out
 
+    # dr_export's columns: (field, element type, count kind) -- count kinds: n rows, n+1 offsets, e
+    # entries, e+1 entry offsets, or the byte total of the named offset column
+    _COLS = [("path_off", "i8", "n1"), ("path_bytes", "u1", "path_off"), ("size", "i8", "n"),
+             ("modification_time", "i8", "n"), ("deletion_timestamp", "i8", "n"),
+             ("deletion_timestamp_valid", "u1", "n"), ("extended_file_metadata", "u1", "n"),
+             ("stats_off", "i8", "n1"), ("stats_bytes", "u1", "stats_off"), ("stats_null", "u1", "n"),
+             ("pv_entry_off", "i8", "n1"), ("pv_null", "u1", "n"), ("pv_key_off", "i8", "pv1"),
+             ("pv_key_bytes", "u1", "pv_key_off"), ("pv_val_off", "i8", "pv1"), ("pv_val_bytes", "u1", "pv_val_off"),
+             ("pv_val_null", "u1", "pv"), ("tags_entry_off", "i8", "n1"), ("tags_null", "u1", "n"),
+             ("tags_key_off", "i8", "tg1"), ("tags_key_bytes", "u1", "tags_key_off"),
+             ("tags_val_off", "i8", "tg1"), ("tags_val_bytes", "u1", "tags_val_off"), ("tags_val_null", "u1", "tg")]
+
+    @staticmethod
+    def _columns(e) -> Dict[str, "object"]:
+        """numpy views of a dr_export's columns (valid while their owner lives)."""
+        import numpy as np
+        n = e.n
+        out = {}
+
+        def view(name, dt, cnt):
+            ptr = getattr(e, name)
+            if cnt == 0 or not ptr:
+                return np.zeros(0, dtype=dt)
+            ct = C.c_int64 if dt == "i8" else C.c_uint8
+            return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ct)), shape=(cnt,))
+        out["path_off"] = view("path_off", "i8", n + 1)
+        out["pv_entry_off"] = view("pv_entry_off", "i8", n + 1)
+        out["tags_entry_off"] = view("tags_entry_off", "i8", n + 1)
+        out["stats_off"] = view("stats_off", "i8", n + 1)
+        npv = int(out["pv_entry_off"][-1]) if n else 0
+        ntg = int(out["tags_entry_off"][-1]) if n else 0
+        cnts = {"n": n, "n1": n + 1, "pv": npv, "pv1": npv + 1, "tg": ntg, "tg1": ntg + 1}
+        for name, dt, kind in State._COLS:
+            if name in out:
+                continue
+            if kind in cnts:
+                out[name] = view(name, dt, cnts[kind])
+        for name, dt, kind in State._COLS:
+            if name not in out:
+                offs = out[kind]
+                out[name] = view(name, dt, int(offs[-1]) if len(offs) else 0)
+        return out
+
+    def export_columns(self, which: int) -> Dict[str, "object"]:
+        """dr_state_export's columns as numpy views (owned by the state until its release)."""
+        e = N.dr_export()
+        with self.eng.lock:
+            self.eng.check(self.eng.lib.dr_state_export(self.h, which, C.byref(e)))
+        return self._columns(e)
+
+    def export_plan(self, which: int, max_rows: int, max_bytes: int) -> List[int]:
+        """dr_state_export_plan: row boundaries of ranges holding at most max_rows rows and at most
+        max_bytes bytes in every column (ABI 3)."""
+        b = C.POINTER(C.c_int64)()
+        n = C.c_int64()
+        with self.eng.lock:
+            self.eng.check(self.eng.lib.dr_state_export_plan(self.h, which, int(max_rows), int(max_bytes),
+                                                             C.byref(b), C.byref(n)))
+        res = [b[i] for i in range(n.value + 1)]
+        self.eng.lib.dr_free(C.cast(b, C.c_void_p))
+        return res
+
+    def export_range(self, which: int, lo: int, hi: int) -> Dict[str, "object"]:
+        """dr_state_export_range: rows [lo, hi) as columns with offsets rebased to the range, copied
+        into numpy arrays (the library's range is released before returning)."""
+        e = N.dr_export()
+        h = C.c_void_p()
+        with self.eng.lock:
+            self.eng.check(self.eng.lib.dr_state_export_range(self.h, which, int(lo), int(hi), C.byref(h), C.byref(e)))
+        try:
+            return {k: v.copy() for k, v in self._columns(e).items()}
+        finally:
+            self.eng.lib.dr_range_release(h)
+
     def filter(self, program) -> List[int]:
         from .predicates import lower_program
         pred, keep = lower_program(program)

@@ -25,8 +25,10 @@ extern "C" {
  *   1  round 1-2 entry points
  *   2  dr_state_write_checkpoint gained its 9th parameter (add_rows); dr_pred_type gained
  *      DR_T_FLOAT .. DR_T_DECIMAL (partitionValues_parsed of the checkpoint writer);
- *      dr_state_local_counts, dr_state_last_error, dr_comm_last_error, dr_state_materialize */
-#define DR_ABI_VERSION 2
+ *      dr_state_local_counts, dr_state_last_error, dr_comm_last_error, dr_state_materialize
+ *   3  dr_state_export_plan, dr_state_export_range, dr_range_release (row-range exports whose columns
+ *      each fit a bound, e.g. a JVM direct buffer's 2^31 - 1 bytes) */
+#define DR_ABI_VERSION 3
 
 /* Status codes. The JNI shim rethrows the reference's exception class with dr_last_error():
  *   DR_E_EMPTY_DIR / DR_E_LOG_TRUNCATED -> FileNotFoundException (D/DeltaErrors.scala:451-457,915-917)
@@ -206,6 +208,28 @@ int dr_state_check_checksum(dr_state* state, const char* crc, uint64_t crc_len, 
                             uint64_t* msg_len);
 /* Materialises allFiles (DR_LIVE) or tombstones (DR_TOMBSTONES) on the host, dataChange=false. */
 int dr_state_export(dr_state* state, int32_t which, dr_export* out);
+
+/* Row-range export (ABI 3): allFiles / tombstones as a sequence of row ranges, for a host that cannot
+ * take a side as one set of columns -- the JVM's direct buffers hold at most 2^31 - 1 bytes, and
+ * config 4's 100M-file side holds ~9 GB of paths alone -- or that builds the reference's partitioned
+ * state (Snapshot.state is a partitioned, cached RDD, D/Snapshot.scala:103-120; D/util/StateCache.scala:
+ * 45-68) with one partition per range.
+ *
+ * dr_state_export_plan: row boundaries bounds[0] = 0 < ... < bounds[*nranges] = the side's rows such
+ * that every range holds at most max_rows rows and every one of its dr_export columns (offset arrays
+ * included) at most max_bytes bytes (freed with dr_free). DR_E_UNSUPPORTED when a single row exceeds
+ * max_bytes in some column.
+ * dr_state_export_range: rows [row_begin, row_end) of the side in dr_state_export's order, as columns
+ * whose offsets are rebased to the range (path_off[0] = 0, entry offsets count from the range's first
+ * entry, byte offsets from its first byte): the concatenation of consecutive ranges' columns, offsets
+ * shifted back, equals dr_state_export's. The columns are host memory owned by *range until
+ * dr_range_release (independent of the state: it may be released first). */
+typedef struct dr_range dr_range;
+int dr_state_export_plan(dr_state* state, int32_t which, int64_t max_rows, uint64_t max_bytes, int64_t** bounds,
+                         int64_t* nranges);
+int dr_state_export_range(dr_state* state, int32_t which, int64_t row_begin, int64_t row_end, dr_range** range,
+                          dr_export* out);
+int dr_range_release(dr_range* range);
 
 /* The full-record state resident in HBM: every field of allFiles and tombstones (path, size,
  * modificationTime / deletionTimestamp, extendedFileMetadata, stats, partitionValues, tags) extracted

@@ -16,19 +16,22 @@ object DeltaReplayNative {
   System.loadLibrary("deltareplay_jni")   // links libdeltareplay.so
 
   /** include/deltareplay.h DR_ABI_VERSION this binding was written against. */
-  val AbiVersion = 2
+  val AbiVersion = 3
   require(abiVersion() == AbiVersion,
     s"libdeltareplay ABI ${abiVersion()} does not match the binding's $AbiVersion")
 
   @native def abiVersion(): Int
   @native def ctxCreate(device: Int): Long
   @native def ctxDestroy(ctx: Long): Unit
-  @native def lastError(ctx: Long): String
-  @native def stageLog(ctx: Long, logPath: String, version: Long): Long
-  @native def stageLogShard(ctx: Long, logPath: String, version: Long, world: Int, rank: Int): Long
+  // Text crosses the boundary as UTF-8 bytes (the *Utf8 natives): JNI's string calls use modified
+  // UTF-8, which would corrupt characters outside the BMP in table paths and metaData values. The
+  // String-typed methods below convert with StandardCharsets.UTF_8.
+  @native def lastErrorUtf8(ctx: Long): Array[Byte]
+  @native def stageLogUtf8(ctx: Long, logPath: Array[Byte], version: Long): Long
+  @native def stageLogShardUtf8(ctx: Long, logPath: Array[Byte], version: Long, world: Int, rank: Int): Long
   @native def stage(ctx: Long, versions: Array[Long], bytes: Array[Array[Byte]]): Long
-  @native def stageNamed(ctx: Long, logPath: String, versions: Array[Long], kinds: Array[Int], parts: Array[Int],
-                         names: Array[String], bytes: Array[Array[Byte]]): Long
+  @native def stageNamedUtf8(ctx: Long, logPath: Array[Byte], versions: Array[Long], kinds: Array[Int],
+                             parts: Array[Int], names: Array[Array[Byte]], bytes: Array[Array[Byte]]): Long
   @native def stagedRelease(staged: Long): Unit
   @native def replay(ctx: Long, staged: Long, minFileRetentionTs: Long, validate: Boolean): Long
   /** 0 = DR_E_REBUILD: replay the new segment instead. */
@@ -36,12 +39,20 @@ object DeltaReplayNative {
   @native def release(state: Long): Unit
   @native def counts(state: Long): Array[Long]
   @native def localCounts(state: Long): Array[Long]
-  @native def nonFileJson(state: Long): String
-  @native def setNonFileJson(state: Long, lines: String, validate: Boolean): Unit
+  @native def nonFileJsonUtf8(state: Long): Array[Byte]
+  @native def setNonFileJsonUtf8(state: Long, lines: Array[Byte], validate: Boolean): Unit
   /** null: the counters match (or there is no readable .crc); else checkMismatch's text. */
-  @native def checkChecksum(state: Long, crcLine: Array[Byte]): String
+  @native def checkChecksumUtf8(state: Long, crcLine: Array[Byte]): Array[Byte]
   @native def recordSums(state: Long): Array[Long]
+  /** A whole side; UnsupportedOperationException when a column exceeds a direct buffer (2^31 - 1
+   *  bytes): take it as ranges instead. */
   @native def export(state: Long, which: Int): Array[ByteBuffer]
+  /** Row boundaries {0, ..., n} of ranges of at most maxRows rows and maxBytes bytes per column (ABI 3). */
+  @native def exportPlan(state: Long, which: Int, maxRows: Long, maxBytes: Long): Array[Long]
+  /** Rows [lo, hi) with offsets rebased to the range; handleOut(0) receives the range, freed with
+   *  rangeRelease (independent of the state). */
+  @native def exportRange(state: Long, which: Int, lo: Long, hi: Long, handleOut: Array[Long]): Array[ByteBuffer]
+  @native def rangeRelease(range: Long): Unit
   @native def filter(state: Long, program: Array[Byte]): Array[Long]
   @native def scanOrder(state: Long): Array[Long]
   @native def partitionGroups(state: Long, rows: Array[Long]): Array[Array[Long]]
@@ -57,6 +68,21 @@ object DeltaReplayNative {
 
   val Live = 0
   val Tombstones = 1
+  /** The largest column a direct ByteBuffer can hold. */
+  val MaxBufferBytes: Long = Int.MaxValue.toLong
+
+  private def utf8(b: Array[Byte]): String = if (b == null) null else new String(b, UTF_8)
+  def lastError(ctx: Long): String = utf8(lastErrorUtf8(ctx))
+  def stageLog(ctx: Long, logPath: String, version: Long): Long = stageLogUtf8(ctx, logPath.getBytes(UTF_8), version)
+  def stageLogShard(ctx: Long, logPath: String, version: Long, world: Int, rank: Int): Long =
+    stageLogShardUtf8(ctx, logPath.getBytes(UTF_8), version, world, rank)
+  def stageNamed(ctx: Long, logPath: String, versions: Array[Long], kinds: Array[Int], parts: Array[Int],
+                 names: Array[String], bytes: Array[Array[Byte]]): Long =
+    stageNamedUtf8(ctx, logPath.getBytes(UTF_8), versions, kinds, parts, names.map(_.getBytes(UTF_8)), bytes)
+  def nonFileJson(state: Long): String = utf8(nonFileJsonUtf8(state))
+  def setNonFileJson(state: Long, lines: String, validate: Boolean): Unit =
+    setNonFileJsonUtf8(state, lines.getBytes(UTF_8), validate)
+  def checkChecksum(state: Long, crcLine: Array[Byte]): String = utf8(checkChecksumUtf8(state, crcLine))
 
   /** Order of counts() / localCounts() (dr_counts). */
   object CountFields {
@@ -106,15 +132,18 @@ object SingleActionColumns {
 
   private def le(b: ByteBuffer): ByteBuffer = b.duplicate().order(ByteOrder.LITTLE_ENDIAN)
 
+  // Offsets stay Long until a slice is taken; Math.toIntExact refuses (instead of wrapping) any
+  // position a direct buffer cannot address -- the library's plan keeps every column of a range
+  // under MaxBufferBytes, so it never fires on planned ranges.
   private final class Strings(off: ByteBuffer, bytes: ByteBuffer, nulls: ByteBuffer) {
     private val o = if (off == null) null else le(off)
     private val d = if (bytes == null) null else bytes.duplicate()
     def apply(i: Int): String = {
       if (o == null || (nulls != null && nulls.get(i) != 0)) return null
-      val lo = o.getLong(8 * i).toInt
-      val hi = o.getLong(8 * i + 8).toInt
-      val a = new Array[Byte](hi - lo)
-      d.position(lo); d.get(a)
+      val lo: Long = o.getLong(Math.toIntExact(8L * i))
+      val hi: Long = o.getLong(Math.toIntExact(8L * i + 8))
+      val a = new Array[Byte](Math.toIntExact(hi - lo))
+      d.position(Math.toIntExact(lo)); d.get(a)
       new String(a, UTF_8)
     }
   }
@@ -126,34 +155,38 @@ object SingleActionColumns {
     private val vals = new Strings(c(valOff), c(valBytes), c(valNull))
     def apply(i: Int): Map[String, String] = {
       if (eo == null || c(mapNull).get(i) != 0) return null
-      val lo = eo.getLong(8 * i).toInt
-      val hi = eo.getLong(8 * i + 8).toInt
-      (lo until hi).map(e => keys(e) -> vals(e)).toMap
+      val lo: Long = eo.getLong(Math.toIntExact(8L * i))
+      val hi: Long = eo.getLong(Math.toIntExact(8L * i + 8))
+      (lo until hi).map(e => keys(Math.toIntExact(e)) -> vals(Math.toIntExact(e))).toMap
     }
   }
 
-  private def rows(c: Array[ByteBuffer]): Int = (c(PathOff).capacity() / 8 - 1)
+  def rows(c: Array[ByteBuffer]): Int = (c(PathOff).capacity() / 8 - 1)
 
-  def addFiles(c: Array[ByteBuffer]): Array[AddFile] = {
+  def addFiles(c: Array[ByteBuffer]): Array[AddFile] = addFileIterator(c).toArray
+  def removeFiles(c: Array[ByteBuffer]): Array[RemoveFile] = removeFileIterator(c).toArray
+
+  /** The rows of one export (or range) lazily, for a partition iterator. */
+  def addFileIterator(c: Array[ByteBuffer]): Iterator[AddFile] = {
     val n = rows(c)
     val path = new Strings(c(PathOff), c(PathBytes), null)
     val stats = new Strings(c(StatsOff), c(StatsBytes), c(StatsNull))
     val pv = new Maps(c, PvEntryOff, PvNull, PvKeyOff, PvKeyBytes, PvValOff, PvValBytes, PvValNull)
     val tags = new Maps(c, TagsEntryOff, TagsNull, TagsKeyOff, TagsKeyBytes, TagsValOff, TagsValBytes, TagsValNull)
     val size = le(c(Size)); val mtime = le(c(ModificationTime))
-    Array.tabulate(n) { i =>
+    Iterator.range(0, n).map { i =>
       AddFile(path(i), pv(i), size.getLong(8 * i), mtime.getLong(8 * i), dataChange = false, stats(i), tags(i))
     }
   }
 
-  def removeFiles(c: Array[ByteBuffer]): Array[RemoveFile] = {
+  def removeFileIterator(c: Array[ByteBuffer]): Iterator[RemoveFile] = {
     val n = rows(c)
     val path = new Strings(c(PathOff), c(PathBytes), null)
     val pv = new Maps(c, PvEntryOff, PvNull, PvKeyOff, PvKeyBytes, PvValOff, PvValBytes, PvValNull)
     val tags = new Maps(c, TagsEntryOff, TagsNull, TagsKeyOff, TagsKeyBytes, TagsValOff, TagsValBytes, TagsValNull)
     val size = le(c(Size)); val dts = le(c(DeletionTimestamp))
     val dtsValid = c(DeletionTimestampValid); val efm = c(ExtendedFileMetadata)
-    Array.tabulate(n) { i =>
+    Iterator.range(0, n).map { i =>
       RemoveFile(path(i), if (dtsValid.get(i) != 0) Some(dts.getLong(8 * i)) else None, dataChange = false,
         extendedFileMetadata = efm.get(i) != 0, partitionValues = pv(i), size = size.getLong(8 * i),
         tags = tags(i))

@@ -1,0 +1,153 @@
+/*
+ * Snapshot.state as a partitioned RDD over the GPU-resident replay (ABI 3 row ranges). Source only --
+ * this image has no JVM or scalac; INTEGRATION.md §1 shows where Snapshot builds it.
+ *
+ * The reference keeps the reconstructed state as a partitioned Dataset (repartition into
+ * snapshotPartitions, D/Snapshot.scala:103-110) cached MEMORY_AND_DISK_SER on the executors and
+ * re-wrapped per session as a LogicalRDD (CachedDS, D/util/StateCache.scala:45-68). Here the state is
+ * resident in HBM on the GPU that replayed it -- the driver's for a single-GPU replay, rank r's
+ * executor for dr_replay_sharded -- and this RDD is its partitioned view: one partition per planned
+ * row range (exportPlan: at most maxRows rows and 2^31 - 1 bytes per column, the JVM's direct-buffer
+ * bound) of each rank's allFiles and tombstones, computed on the executor that holds the rank's state
+ * (preferred location), pulling its rows with exportRange. No side is ever gathered on the driver, so
+ * config 4's 100M-file state (36 GB of columns) crosses as ~2 GB slices.
+ *
+ * D/ = core/src/main/scala/org/apache/spark/sql/delta/.
+ */
+package org.apache.spark.sql.delta.gpu
+
+import java.util.concurrent.ConcurrentHashMap
+
+import org.apache.spark.{Partition, SparkContext, SparkEnv, TaskContext}
+import org.apache.spark.rdd.RDD
+import org.apache.spark.scheduler.ExecutorCacheTaskLocation
+import org.apache.spark.sql.{Dataset, SparkSession}
+import org.apache.spark.sql.catalyst.InternalRow
+import org.apache.spark.sql.catalyst.encoders.ExpressionEncoder
+import org.apache.spark.sql.delta.actions.SingleAction
+import org.apache.spark.sql.execution.LogicalRDD
+
+/**
+ * The states resident in this JVM, by (snapshot key, rank). A state is registered by the task that
+ * replayed it and removed by Snapshot.uncache (D/util/StateCache.scala:104-109), which releases it.
+ */
+object DeltaReplayStates {
+  private val states = new ConcurrentHashMap[(String, Int), java.lang.Long]()
+
+  def put(key: String, rank: Int, state: Long): Unit = states.put((key, rank), state)
+
+  def get(key: String, rank: Int): Long = {
+    val s = states.get((key, rank))
+    if (s == null) {
+      throw new IllegalStateException(s"the GPU state of snapshot $key rank $rank is not resident on this executor")
+    }
+    s
+  }
+
+  /** Removes and releases (dr_state_release) a rank's state; ranges already exported stay valid. */
+  def release(key: String, rank: Int): Unit = {
+    val s = states.remove((key, rank))
+    if (s != null) DeltaReplayNative.release(s)
+  }
+
+  /** This executor's location for a partition that must run here (the rank's state lives here). */
+  def here: String = {
+    val bm = SparkEnv.get.blockManager.blockManagerId
+    ExecutorCacheTaskLocation(bm.host, bm.executorId).toString
+  }
+}
+
+/** Rows [lo, hi) of side `which` (Live / Tombstones) of rank `rank`'s state, to run at `location`. */
+final case class StateRangePartition(index: Int, rank: Int, which: Int, lo: Long, hi: Long, location: String)
+  extends Partition
+
+/** One rank's ranges: exportPlan of both sides on the rank's own executor. */
+final case class RankPlan(rank: Int, location: String, live: Array[Long], tombstones: Array[Long])
+
+object RankPlan {
+  /** exportPlan of the state registered as (key, rank) in this JVM. */
+  def local(key: String, rank: Int, maxRows: Long): RankPlan = {
+    val st = DeltaReplayStates.get(key, rank)
+    RankPlan(rank, DeltaReplayStates.here,
+      DeltaReplayNative.exportPlan(st, DeltaReplayNative.Live, maxRows, DeltaReplayNative.MaxBufferBytes),
+      DeltaReplayNative.exportPlan(st, DeltaReplayNative.Tombstones, maxRows, DeltaReplayNative.MaxBufferBytes))
+  }
+}
+
+/** The SingleAction rows of planned row ranges, each computed where its rank's state is resident. */
+class DeltaReplayStateRDD(sc: SparkContext, key: String, ranges: Array[StateRangePartition])
+  extends RDD[InternalRow](sc, Nil) {
+
+  override protected def getPartitions: Array[Partition] = ranges.map(p => p: Partition)
+
+  override protected def getPreferredLocations(p: Partition): Seq[String] =
+    Seq(p.asInstanceOf[StateRangePartition].location)
+
+  override def compute(p: Partition, ctx: TaskContext): Iterator[InternalRow] = {
+    val r = p.asInstanceOf[StateRangePartition]
+    val state = DeltaReplayStates.get(key, r.rank)  // fails loudly if scheduled off the rank's executor
+    val handle = new Array[Long](1)
+    val cols = DeltaReplayNative.exportRange(state, r.which, r.lo, r.hi, handle)
+    ctx.addTaskCompletionListener[Unit](_ => DeltaReplayNative.rangeRelease(handle(0)))
+    val toRow = DeltaReplayState.serializer()
+    val actions: Iterator[SingleAction] =
+      if (r.which == DeltaReplayNative.Live) SingleActionColumns.addFileIterator(cols).map(a => SingleAction(add = a))
+      else SingleActionColumns.removeFileIterator(cols).map(rm => SingleAction(remove = rm))
+    actions.map(a => toRow(a).copy())  // the serializer reuses its row
+  }
+}
+
+object DeltaReplayState {
+  private lazy val encoder = ExpressionEncoder[SingleAction]()
+
+  def serializer(): ExpressionEncoder.Serializer[SingleAction] = encoder.createSerializer()
+
+  /** Partitions of every rank's plan: live ranges, then tombstone ranges, rank by rank. */
+  def partitions(plans: Seq[RankPlan]): Array[StateRangePartition] = {
+    val out = Array.newBuilder[StateRangePartition]
+    var i = 0
+    for (pl <- plans.sortBy(_.rank); (which, b) <- Seq(DeltaReplayNative.Live -> pl.live,
+                                                         DeltaReplayNative.Tombstones -> pl.tombstones)) {
+      for (k <- 0 until b.length - 1) {
+        out += StateRangePartition(i, pl.rank, which, b(k), b(k + 1), pl.location)
+        i += 1
+      }
+    }
+    out.result()
+  }
+
+  /**
+   * Snapshot.state (D/Snapshot.scala:120): the file actions of the resident ranks' states as
+   * partitioned rows, plus the table-wide protocol / metaData / txn winners (a handful of actions,
+   * nonFileJson decoded by Action.fromJson on the driver) in one more partition, wrapped as a
+   * LogicalRDD exactly as CachedDS wraps the reference's cached RDD (D/util/StateCache.scala:56-62).
+   */
+  def dataset(spark: SparkSession, key: String, plans: Seq[RankPlan],
+              nonFile: Seq[SingleAction]): Dataset[SingleAction] = {
+    val sc = spark.sparkContext
+    val files = new DeltaReplayStateRDD(sc, key, partitions(plans))
+    val others = sc.parallelize(nonFile, 1).mapPartitions { it =>
+      val toRow = serializer()
+      it.map(a => toRow(a).copy())
+    }
+    val rdd = sc.union(files, others)
+    rdd.setName(s"Delta GPU state $key")
+    Dataset.ofRows(spark, LogicalRDD(encoder.schema.toAttributes, rdd)(spark)).as[SingleAction](encoder)
+  }
+
+  /**
+   * The plans of a sharded replay: one task per rank on the executor holding it (the same tasks that
+   * ran dr_replay_sharded registered their states under `key`), each returning exportPlan of both
+   * sides. `locations(r)` is rank r's executor (recorded when the replay tasks ran).
+   */
+  def shardedPlans(sc: SparkContext, key: String, locations: IndexedSeq[String], maxRows: Long): Seq[RankPlan] = {
+    val world = locations.size
+    val ranks = new RDD[Int](sc, Nil) {
+      override protected def getPartitions: Array[Partition] =
+        Array.tabulate(world)(r => new Partition { override def index: Int = r })
+      override protected def getPreferredLocations(p: Partition): Seq[String] = Seq(locations(p.index))
+      override def compute(p: Partition, ctx: TaskContext): Iterator[Int] = Iterator(p.index)
+    }
+    ranks.map(r => RankPlan.local(key, r, maxRows)).collect().toSeq
+  }
+}

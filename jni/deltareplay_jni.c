@@ -10,10 +10,18 @@
  *
  * Failures raise the reference's exception classes with the library's message (the reference's own
  * texts, D/DeltaErrors.scala:451-560, D/Snapshot.scala:334-345) -- see throw_status. Handles cross
- * the boundary as jlong; the Scala side owns their lifetime (release / stagedRelease / ctxDestroy).
- * Export columns are wrapped zero-copy with NewDirectByteBuffer: they stay valid until the state is
- * released (dr_export's contract), which is the lifetime Snapshot.uncache gives the cached state
- * (D/util/StateCache.scala:104-109).
+ * the boundary as jlong; the Scala side owns their lifetime (release / stagedRelease / ctxDestroy /
+ * rangeRelease). Export columns are wrapped zero-copy with NewDirectByteBuffer: they stay valid until
+ * the state (export) or the range (exportRange) is released, which is the lifetime Snapshot.uncache
+ * gives the cached state (D/util/StateCache.scala:104-109). A direct buffer holds at most 2^31 - 1
+ * bytes: export refuses a side with a larger column (UnsupportedOperationException) and the host
+ * takes it as row ranges (exportPlan / exportRange, ABI 3) instead.
+ *
+ * Text crosses as UTF-8 byte arrays in both directions (the *Utf8 natives; Scala converts with
+ * StandardCharsets.UTF_8): JNI's own string calls speak modified UTF-8, which encodes characters
+ * outside the BMP as surrogate pairs and U+0000 as C0 80, so table paths or metaData values with such
+ * characters would not survive them. Exception messages are built as new String(bytes, "UTF-8") too.
+ * No JNI call is made while an exception is pending: every call that can raise one is checked.
  *
  * Paths: D/ = core/src/main/scala/org/apache/spark/sql/delta/.
  */
@@ -25,13 +33,46 @@
 
 #define NATIVE(ret, name) JNIEXPORT ret JNICALL Java_org_apache_spark_sql_delta_gpu_DeltaReplayNative_00024_##name
 
-/* ---- errors ------------------------------------------------------------------------------------ */
+/* ---- errors and strings --------------------------------------------------------------------------- */
 
-/* The reference's exception for a dr_status (error mapping). AssertionError has no
- * (String) constructor, so it is built through its (Object) one. DR_E_REBUILD is not an error: the
- * callers that can see it return 0 and the Scala side rebuilds the snapshot from its segment. */
+static int pending(JNIEnv* env) { return (*env)->ExceptionCheck(env) ? 1 : 0; }
+
+/* new String(bytes[0..n), "UTF-8"): the library's standard UTF-8 as a Java string (NULL with an
+ * exception pending on failure). */
+static jstring utf8_string(JNIEnv* env, const char* bytes, size_t n) {
+  if (n > 0x7fffffffu) n = 0x7fffffffu;
+  jbyteArray b = (*env)->NewByteArray(env, (jsize)n);
+  if (!b) return NULL;
+  if (n) (*env)->SetByteArrayRegion(env, b, 0, (jsize)n, (const jbyte*)bytes);
+  jclass sc = (*env)->FindClass(env, "java/lang/String");
+  jmethodID ctor = sc ? (*env)->GetMethodID(env, sc, "<init>", "([BLjava/lang/String;)V") : NULL;
+  jstring cs = ctor ? (*env)->NewStringUTF(env, "UTF-8") : NULL;  /* ASCII: modified UTF-8 is UTF-8 */
+  jstring out = cs ? (jstring)(*env)->NewObject(env, sc, ctor, b, cs) : NULL;
+  (*env)->DeleteLocalRef(env, b);
+  if (sc) (*env)->DeleteLocalRef(env, sc);
+  if (cs) (*env)->DeleteLocalRef(env, cs);
+  return out;
+}
+
+/* bytes[0..n) as a new byte[] (NULL with an exception pending on failure). */
+static jbyteArray byte_array(JNIEnv* env, const void* bytes, uint64_t n) {
+  if (n > 0x7fffffffull) {
+    jclass c = (*env)->FindClass(env, "java/lang/UnsupportedOperationException");
+    if (c) (*env)->ThrowNew(env, c, "result over 2 GiB");
+    return NULL;
+  }
+  jbyteArray out = (*env)->NewByteArray(env, (jsize)n);
+  if (out && n) (*env)->SetByteArrayRegion(env, out, 0, (jsize)n, (const jbyte*)bytes);
+  return out;
+}
+
+/* The reference's exception for a dr_status (error mapping), with the library's UTF-8
+ * message. AssertionError has no (String) constructor, so it is built through its (Object) one.
+ * DR_E_REBUILD is not an error: the callers that can see it return 0 and the Scala side rebuilds the
+ * snapshot from its segment. */
 static void throw_status(JNIEnv* env, int rc, const char* msg) {
   const char* cls;
+  const char* sig = "(Ljava/lang/String;)V";
   switch (rc) {
     case DR_E_EMPTY_DIR:
     case DR_E_LOG_TRUNCATED:
@@ -46,20 +87,16 @@ static void throw_status(JNIEnv* env, int rc, const char* msg) {
     case DR_E_INVALID_ARG: cls = "java/lang/IllegalArgumentException"; break;
     case DR_E_UNSUPPORTED: cls = "java/lang/UnsupportedOperationException"; break;
     case DR_E_OOM: cls = "java/lang/OutOfMemoryError"; break;
-    case DR_E_FOREIGN_FILE: {
-      jclass ae = (*env)->FindClass(env, "java/lang/AssertionError");
-      jmethodID ctor = ae ? (*env)->GetMethodID(env, ae, "<init>", "(Ljava/lang/Object;)V") : NULL;
-      jstring s = (*env)->NewStringUTF(env, msg ? msg : "");
-      if (ctor && s) {
-        jobject ex = (*env)->NewObject(env, ae, ctor, s);
-        if (ex) (*env)->Throw(env, (jthrowable)ex);
-      }
-      return;
-    }
+    case DR_E_FOREIGN_FILE: cls = "java/lang/AssertionError"; sig = "(Ljava/lang/Object;)V"; break;
     default: cls = "java/lang/RuntimeException"; break; /* DR_E_PARSE, DR_E_PARQUET, DR_E_DEVICE, ... */
   }
+  if (pending(env)) return;
+  if (!msg || !*msg) msg = "libdeltareplay call failed";
   jclass c = (*env)->FindClass(env, cls);
-  if (c) (*env)->ThrowNew(env, c, msg && *msg ? msg : "libdeltareplay call failed");
+  jmethodID ctor = c ? (*env)->GetMethodID(env, c, "<init>", sig) : NULL;
+  jstring s = ctor ? utf8_string(env, msg, strlen(msg)) : NULL;
+  jobject ex = s ? (*env)->NewObject(env, c, ctor, s) : NULL;
+  if (ex) (*env)->Throw(env, (jthrowable)ex);
 }
 
 #define CHECK_CTX(env, rc, ctx, ret)                                   \
@@ -78,20 +115,28 @@ static void throw_status(JNIEnv* env, int rc, const char* msg) {
   } while (0)
 
 static jlongArray long_array(JNIEnv* env, const int64_t* v, int64_t n) {
+  if (n < 0 || n > 0x7fffffff) {
+    throw_status(env, DR_E_UNSUPPORTED, "result over 2^31 - 1 elements");
+    return NULL;
+  }
   jlongArray out = (*env)->NewLongArray(env, (jsize)n);
   if (out && n) (*env)->SetLongArrayRegion(env, out, 0, (jsize)n, (const jlong*)v);
   return out;
 }
 
-/* A Java String as a NUL-terminated modified-UTF-8 copy the caller frees (paths, JSON lines). */
-static char* utf_copy(JNIEnv* env, jstring s) {
-  if (!s) return NULL;
-  const char* c = (*env)->GetStringUTFChars(env, s, NULL);
-  if (!c) return NULL;
-  const size_t n = strlen(c);
-  char* out = (char*)malloc(n + 1);
-  if (out) memcpy(out, c, n + 1);
-  (*env)->ReleaseStringUTFChars(env, s, c);
+/* A UTF-8 byte[] (String.getBytes(UTF_8) on the Scala side) as a NUL-terminated copy the caller
+ * frees; NULL for a null array or on failure. */
+static char* utf8_copy(JNIEnv* env, jbyteArray b) {
+  if (!b) return NULL;
+  const jsize n = (*env)->GetArrayLength(env, b);
+  char* out = (char*)malloc((size_t)n + 1);
+  if (!out) return NULL;
+  if (n) (*env)->GetByteArrayRegion(env, b, 0, n, (jbyte*)out);
+  out[n] = 0;
+  if (pending(env)) {
+    free(out);
+    return NULL;
+  }
   return out;
 }
 
@@ -118,18 +163,20 @@ NATIVE(void, ctxDestroy)(JNIEnv* env, jobject self, jlong ctx) {
   dr_ctx_destroy((dr_ctx*)(intptr_t)ctx);
 }
 
-NATIVE(jstring, lastError)(JNIEnv* env, jobject self, jlong ctx) {
+NATIVE(jbyteArray, lastErrorUtf8)(JNIEnv* env, jobject self, jlong ctx) {
   (void)self;
-  return (*env)->NewStringUTF(env, dr_last_error((const dr_ctx*)(intptr_t)ctx));
+  const char* m = dr_last_error((const dr_ctx*)(intptr_t)ctx);
+  return byte_array(env, m ? m : "", m ? strlen(m) : 0);
 }
 
 /* ---- staging ----------------------------------------------------------------------------------- */
 
 /* Snapshot.stateReconstruction's input (D/Snapshot.scala:88-111): the LogSegment of `version`
  * (< 0: latest) listed and read by the library (SnapshotManagement.getLogSegmentForVersion). */
-NATIVE(jlong, stageLog)(JNIEnv* env, jobject self, jlong ctx, jstring log_path, jlong version) {
+NATIVE(jlong, stageLogUtf8)(JNIEnv* env, jobject self, jlong ctx, jbyteArray log_path, jlong version) {
   (void)self;
-  char* path = utf_copy(env, log_path);
+  char* path = utf8_copy(env, log_path);
+  if (pending(env)) return 0;
   dr_staged* st = NULL;
   int rc = path ? dr_stage_log((dr_ctx*)(intptr_t)ctx, path, (int64_t)version, &st) : DR_E_INVALID_ARG;
   free(path);
@@ -138,10 +185,11 @@ NATIVE(jlong, stageLog)(JNIEnv* env, jobject self, jlong ctx, jstring log_path, 
 }
 
 /* One rank's slice of the segment for the sharded replay (dr_shard_plan's cut). */
-NATIVE(jlong, stageLogShard)(JNIEnv* env, jobject self, jlong ctx, jstring log_path, jlong version, jint world,
-                             jint rank) {
+NATIVE(jlong, stageLogShardUtf8)(JNIEnv* env, jobject self, jlong ctx, jbyteArray log_path, jlong version,
+                                 jint world, jint rank) {
   (void)self;
-  char* path = utf_copy(env, log_path);
+  char* path = utf8_copy(env, log_path);
+  if (pending(env)) return 0;
   dr_staged* st = NULL;
   int rc = path ? dr_stage_log_shard((dr_ctx*)(intptr_t)ctx, path, (int64_t)version, world, rank, &st)
                 : DR_E_INVALID_ARG;
@@ -151,49 +199,71 @@ NATIVE(jlong, stageLogShard)(JNIEnv* env, jobject self, jlong ctx, jstring log_p
 }
 
 /* Files the host read itself. kinds[i] (dr_file_kind), parts[i] (1-based checkpoint part, 0 for a
- * commit or a single-part checkpoint); with `log_path` and `names` non-null every file is checked to
- * belong to the table (assertLogBelongsToTable, D/Snapshot.scala:102,334-345). The file bytes are
- * copied into HBM during the call, so the Java arrays are released before it returns. */
-static jlong stage_files(JNIEnv* env, jlong ctx, jstring log_path, jlongArray versions, jintArray kinds,
+ * commit or a single-part checkpoint); with `log_path` and `names` (UTF-8 byte arrays) non-null every
+ * file is checked to belong to the table (assertLogBelongsToTable, D/Snapshot.scala:102,334-345).
+ * Every parallel array must hold one entry per version (IllegalArgumentException otherwise, before
+ * any element is read). The file bytes are copied into HBM during the call, so the Java arrays are
+ * released before it returns; the byte arrays stay pinned together for the call, so the local
+ * reference capacity is raised to hold them. */
+static jlong stage_files(JNIEnv* env, jlong ctx, jbyteArray log_path, jlongArray versions, jintArray kinds,
                          jintArray parts, jobjectArray names, jobjectArray bytes) {
   const jsize n = versions ? (*env)->GetArrayLength(env, versions) : 0;
-  if (!bytes || (*env)->GetArrayLength(env, bytes) != n) {
-    throw_status(env, DR_E_INVALID_ARG, "stage: one byte array per version");
+  if (!bytes || (*env)->GetArrayLength(env, bytes) != n || (kinds && (*env)->GetArrayLength(env, kinds) != n) ||
+      (parts && (*env)->GetArrayLength(env, parts) != n) || (names && (*env)->GetArrayLength(env, names) != n)) {
+    throw_status(env, DR_E_INVALID_ARG, "stage: versions, kinds, parts, names and bytes must have equal lengths");
     return 0;
   }
+  if (n > 0 && (*env)->EnsureLocalCapacity(env, n + 16) != 0) return 0;  /* OutOfMemoryError pending */
   dr_file* files = (dr_file*)calloc((size_t)n + 1, sizeof(dr_file));
   jbyteArray* arrs = (jbyteArray*)calloc((size_t)n + 1, sizeof(jbyteArray));
   jbyte** data = (jbyte**)calloc((size_t)n + 1, sizeof(jbyte*));
   char** cnames = (char**)calloc((size_t)n + 1, sizeof(char*));
-  jlong* v = (*env)->GetLongArrayElements(env, versions, NULL);
-  jint* k = kinds ? (*env)->GetIntArrayElements(env, kinds, NULL) : NULL;
-  jint* p = parts ? (*env)->GetIntArrayElements(env, parts, NULL) : NULL;
+  jlong* v = n ? (*env)->GetLongArrayElements(env, versions, NULL) : NULL;
+  jint* k = (n && kinds) ? (*env)->GetIntArrayElements(env, kinds, NULL) : NULL;
+  jint* p = (n && parts) ? (*env)->GetIntArrayElements(env, parts, NULL) : NULL;
   int rc = DR_OK;
+  if (!files || !arrs || !data || !cnames || (n && (!v || (kinds && !k) || (parts && !p)))) rc = DR_E_OOM;
   for (jsize i = 0; i < n && rc == DR_OK; ++i) {
     arrs[i] = (jbyteArray)(*env)->GetObjectArrayElement(env, bytes, i);
     data[i] = arrs[i] ? (*env)->GetByteArrayElements(env, arrs[i], NULL) : NULL;
-    if (!data[i]) { rc = DR_E_INVALID_ARG; break; }
+    if (!data[i]) { rc = -1; break; }
     files[i].version = (int64_t)v[i];
     files[i].kind = k ? k[i] : DR_FILE_JSON;
     files[i].part = p ? p[i] : 0;
     files[i].data = (const uint8_t*)data[i];
     files[i].len = (uint64_t)(*env)->GetArrayLength(env, arrs[i]);
-    if (names) cnames[i] = utf_copy(env, (jstring)(*env)->GetObjectArrayElement(env, names, i));
+    if (names) {
+      jbyteArray nm = (jbyteArray)(*env)->GetObjectArrayElement(env, names, i);
+      cnames[i] = utf8_copy(env, nm);
+      if (nm) (*env)->DeleteLocalRef(env, nm);
+      if (!cnames[i]) { rc = -1; break; }
+    }
   }
   dr_staged* st = NULL;
-  char* path = log_path ? utf_copy(env, log_path) : NULL;
+  char* path = log_path ? utf8_copy(env, log_path) : NULL;
+  if (rc == DR_OK && pending(env)) rc = -1;
   if (rc == DR_OK) {
     rc = names ? dr_stage_named((dr_ctx*)(intptr_t)ctx, path ? path : "", files, (const char* const*)cnames, n, &st)
                : dr_stage((dr_ctx*)(intptr_t)ctx, files, n, &st);
   }
-  for (jsize i = 0; i < n; ++i) {
-    if (data[i]) (*env)->ReleaseByteArrayElements(env, arrs[i], data[i], JNI_ABORT);
-    free(cnames[i]);
+  for (jsize i = 0; i < n && arrs; ++i) {
+    if (data && data[i]) (*env)->ReleaseByteArrayElements(env, arrs[i], data[i], JNI_ABORT);
+    if (arrs[i]) (*env)->DeleteLocalRef(env, arrs[i]);
+    if (cnames) free(cnames[i]);
   }
-  (*env)->ReleaseLongArrayElements(env, versions, v, JNI_ABORT);
+  if (v) (*env)->ReleaseLongArrayElements(env, versions, v, JNI_ABORT);
   if (k) (*env)->ReleaseIntArrayElements(env, kinds, k, JNI_ABORT);
   if (p) (*env)->ReleaseIntArrayElements(env, parts, p, JNI_ABORT);
   free(path); free(files); free(arrs); free(data); free(cnames);
+  if (pending(env)) return 0;  /* e.g. a null element: NullPointerException / ArrayIndexOutOfBounds */
+  if (rc == DR_E_OOM) {
+    throw_status(env, rc, "stage: out of host memory");
+    return 0;
+  }
+  if (rc == -1) {
+    throw_status(env, DR_E_INVALID_ARG, "stage: a null byte array or name");
+    return 0;
+  }
   CHECK_CTX(env, rc, (intptr_t)ctx, 0);
   return (jlong)(intptr_t)st;
 }
@@ -204,8 +274,8 @@ NATIVE(jlong, stage)(JNIEnv* env, jobject self, jlong ctx, jlongArray versions, 
   return stage_files(env, ctx, NULL, versions, NULL, NULL, NULL, bytes);
 }
 
-NATIVE(jlong, stageNamed)(JNIEnv* env, jobject self, jlong ctx, jstring log_path, jlongArray versions,
-                          jintArray kinds, jintArray parts, jobjectArray names, jobjectArray bytes) {
+NATIVE(jlong, stageNamedUtf8)(JNIEnv* env, jobject self, jlong ctx, jbyteArray log_path, jlongArray versions,
+                              jintArray kinds, jintArray parts, jobjectArray names, jobjectArray bytes) {
   (void)self;
   return stage_files(env, ctx, log_path, versions, kinds, parts, names, bytes);
 }
@@ -275,25 +345,22 @@ NATIVE(jlongArray, localCounts)(JNIEnv* env, jobject self, jlong state) {
 
 /* Latest protocol / metaData and the set transactions, one {"protocol":...} / {"metaData":...} /
  * {"txn":...} line each: the Scala side decodes them with Action.fromJson (D/actions/actions.scala:57-59). */
-NATIVE(jstring, nonFileJson)(JNIEnv* env, jobject self, jlong state) {
+NATIVE(jbyteArray, nonFileJsonUtf8)(JNIEnv* env, jobject self, jlong state) {
   (void)self;
   const char* json = NULL;
   uint64_t len = 0;
   int rc = dr_state_nonfile_json((dr_state*)(intptr_t)state, &json, &len);
   CHECK_STATE(env, rc, (intptr_t)state, NULL);
-  char* z = (char*)malloc(len + 1);
-  if (len) memcpy(z, json, len);
-  z[len] = 0;
-  jstring out = (*env)->NewStringUTF(env, z);
-  free(z);
-  return out;
+  return byte_array(env, json, len);
 }
 
 /* A sharded state's table-wide non-file winners when the host drove the exchange itself. */
-NATIVE(void, setNonFileJson)(JNIEnv* env, jobject self, jlong state, jstring lines, jboolean validate) {
+NATIVE(void, setNonFileJsonUtf8)(JNIEnv* env, jobject self, jlong state, jbyteArray lines, jboolean validate) {
   (void)self;
-  char* z = utf_copy(env, lines);
-  int rc = dr_state_set_nonfile_json((dr_state*)(intptr_t)state, z ? z : "", z ? strlen(z) : 0,
+  const jsize n = lines ? (*env)->GetArrayLength(env, lines) : 0;
+  char* z = utf8_copy(env, lines);
+  if (pending(env)) return;
+  int rc = dr_state_set_nonfile_json((dr_state*)(intptr_t)state, z ? z : "", z ? (uint64_t)n : 0,
                                      validate ? 0u : DR_FLAG_NO_VALIDATION);
   free(z);
   CHECK_STATE(env, rc, (intptr_t)state, );
@@ -301,7 +368,7 @@ NATIVE(void, setNonFileJson)(JNIEnv* env, jobject self, jlong state, jstring lin
 
 /* ValidateChecksum (D/Checksum.scala:155-191): null when the counters match or the .crc is absent or
  * unreadable (checksumOpt = None), else checkMismatch's text for the caller's IllegalStateException. */
-NATIVE(jstring, checkChecksum)(JNIEnv* env, jobject self, jlong state, jbyteArray crc_line) {
+NATIVE(jbyteArray, checkChecksumUtf8)(JNIEnv* env, jobject self, jlong state, jbyteArray crc_line) {
   (void)self;
   const jsize n = crc_line ? (*env)->GetArrayLength(env, crc_line) : 0;
   jbyte* b = crc_line ? (*env)->GetByteArrayElements(env, crc_line, NULL) : NULL;
@@ -314,7 +381,7 @@ NATIVE(jstring, checkChecksum)(JNIEnv* env, jobject self, jlong state, jbyteArra
     throw_status(env, rc, dr_state_last_error((const dr_state*)(intptr_t)state));
     return NULL;
   }
-  return (*env)->NewStringUTF(env, msg);
+  return byte_array(env, msg, strlen(msg));
 }
 
 /* Order-free full-record checksums (parity gate): {live, tombstones}. */
@@ -329,16 +396,80 @@ NATIVE(jlongArray, recordSums)(JNIEnv* env, jobject self, jlong state) {
 
 /* ---- allFiles / tombstones as SingleAction columns ---------------------------------------------- */
 
-static jobject direct(JNIEnv* env, const void* p, int64_t bytes) {
-  if (!p) return NULL;
+/* A direct ByteBuffer over p[0..bytes); `*failed` is set when the JVM raised (the caller stops). */
+static jobject direct(JNIEnv* env, const void* p, int64_t bytes, int* failed) {
+  if (*failed || !p) return NULL;
   /* a zero-length column still gets a buffer (an empty table has n + 1 = 1 offsets) */
-  return (*env)->NewDirectByteBuffer(env, (void*)p, (jlong)bytes);
+  jobject b = (*env)->NewDirectByteBuffer(env, (void*)p, (jlong)bytes);
+  if (!b || pending(env)) *failed = 1;
+  return b;
 }
 
-/* dr_state_export(which) as direct ByteBuffers, one per dr_export column in declaration order (the
- * indices of DeltaReplayNative.ExportColumns; null where a side has no such column, e.g.
- * modificationTime of tombstones). Every buffer's capacity is its exact byte size, so n is
- * pathOff.capacity / 8 - 1 and no extra count crosses. SingleActionColumns (jni/DeltaReplayNative.scala)
+#define DR_EXPORT_COLS 24
+/* The byte size of every dr_export column, in declaration order (DeltaReplayNative.ExportColumns). */
+static void column_sizes(const dr_export* e, const void* ptr[DR_EXPORT_COLS], int64_t sz[DR_EXPORT_COLS]) {
+  const int64_t n = e->n;
+  const int64_t npv = e->pv_entry_off ? e->pv_entry_off[n] : 0;
+  const int64_t ntg = e->tags_entry_off ? e->tags_entry_off[n] : 0;
+  int k = 0;
+#define COL(p, b) do { ptr[k] = (const void*)(p); sz[k] = (int64_t)(b); ++k; } while (0)
+  COL(e->path_off, 8 * (n + 1));
+  COL(e->path_bytes, e->path_off ? e->path_off[n] : 0);
+  COL(e->size, 8 * n);
+  COL(e->modification_time, 8 * n);
+  COL(e->deletion_timestamp, 8 * n);
+  COL(e->deletion_timestamp_valid, n);
+  COL(e->extended_file_metadata, n);
+  COL(e->stats_off, 8 * (n + 1));
+  COL(e->stats_bytes, e->stats_off ? e->stats_off[n] : 0);
+  COL(e->stats_null, n);
+  COL(e->pv_entry_off, 8 * (n + 1));
+  COL(e->pv_null, n);
+  COL(e->pv_key_off, 8 * (npv + 1));
+  COL(e->pv_key_bytes, e->pv_key_off ? e->pv_key_off[npv] : 0);
+  COL(e->pv_val_off, 8 * (npv + 1));
+  COL(e->pv_val_bytes, e->pv_val_off ? e->pv_val_off[npv] : 0);
+  COL(e->pv_val_null, npv);
+  COL(e->tags_entry_off, 8 * (n + 1));
+  COL(e->tags_null, n);
+  COL(e->tags_key_off, 8 * (ntg + 1));
+  COL(e->tags_key_bytes, e->tags_key_off ? e->tags_key_off[ntg] : 0);
+  COL(e->tags_val_off, 8 * (ntg + 1));
+  COL(e->tags_val_bytes, e->tags_val_off ? e->tags_val_off[ntg] : 0);
+  COL(e->tags_val_null, ntg);
+#undef COL
+}
+
+/* dr_export's columns as direct ByteBuffers, one per column in declaration order (null where a side
+ * has no such column, e.g. modificationTime of tombstones). Every buffer's capacity is its exact
+ * byte size, so n is pathOff.capacity / 8 - 1 and no extra count crosses. A column over 2^31 - 1
+ * bytes (a ByteBuffer's capacity is an int) is refused before any buffer is made. */
+static jobjectArray columns(JNIEnv* env, const dr_export* e, const char* too_big) {
+  const void* ptr[DR_EXPORT_COLS];
+  int64_t sz[DR_EXPORT_COLS];
+  column_sizes(e, ptr, sz);
+  for (int i = 0; i < DR_EXPORT_COLS; ++i)
+    if (ptr[i] && (sz[i] < 0 || sz[i] > 0x7fffffffll)) {
+      throw_status(env, DR_E_UNSUPPORTED, too_big);
+      return NULL;
+    }
+  jclass bb = (*env)->FindClass(env, "java/nio/ByteBuffer");
+  jobjectArray out = bb ? (*env)->NewObjectArray(env, DR_EXPORT_COLS, bb, NULL) : NULL;
+  if (!out) return NULL;
+  int failed = 0;
+  for (int i = 0; i < DR_EXPORT_COLS && !failed; ++i) {
+    jobject b = direct(env, ptr[i], sz[i], &failed);
+    if (b && !failed) {
+      (*env)->SetObjectArrayElement(env, out, i, b);
+      if (pending(env)) failed = 1;
+    }
+    if (b) (*env)->DeleteLocalRef(env, b);
+  }
+  return failed ? NULL : out;
+}
+
+/* dr_state_export(which), the whole side in one set of buffers (a side whose columns each fit 2 GiB;
+ * larger ones go through exportPlan / exportRange). SingleActionColumns (jni/DeltaReplayNative.scala)
  * wraps them into AddFile / RemoveFile rows (D/Snapshot.scala:193-204: allFiles = state.where(add !=
  * null).as[AddFile], tombstones = state.where(remove != null).as[RemoveFile], dataChange = false). */
 NATIVE(jobjectArray, export)(JNIEnv* env, jobject self, jlong state, jint which) {
@@ -347,39 +478,52 @@ NATIVE(jobjectArray, export)(JNIEnv* env, jobject self, jlong state, jint which)
   memset(&e, 0, sizeof e);
   int rc = dr_state_export((dr_state*)(intptr_t)state, which, &e);
   CHECK_STATE(env, rc, (intptr_t)state, NULL);
-  const int64_t n = e.n;
-  const int64_t npv = e.pv_entry_off ? e.pv_entry_off[n] : 0;
-  const int64_t ntg = e.tags_entry_off ? e.tags_entry_off[n] : 0;
-  jobject cols[25];
-  int k = 0;
-  cols[k++] = direct(env, e.path_off, 8 * (n + 1));
-  cols[k++] = direct(env, e.path_bytes, e.path_off ? e.path_off[n] : 0);
-  cols[k++] = direct(env, e.size, 8 * n);
-  cols[k++] = direct(env, e.modification_time, 8 * n);
-  cols[k++] = direct(env, e.deletion_timestamp, 8 * n);
-  cols[k++] = direct(env, e.deletion_timestamp_valid, n);
-  cols[k++] = direct(env, e.extended_file_metadata, n);
-  cols[k++] = direct(env, e.stats_off, 8 * (n + 1));
-  cols[k++] = direct(env, e.stats_bytes, e.stats_off ? e.stats_off[n] : 0);
-  cols[k++] = direct(env, e.stats_null, n);
-  cols[k++] = direct(env, e.pv_entry_off, 8 * (n + 1));
-  cols[k++] = direct(env, e.pv_null, n);
-  cols[k++] = direct(env, e.pv_key_off, 8 * (npv + 1));
-  cols[k++] = direct(env, e.pv_key_bytes, e.pv_key_off ? e.pv_key_off[npv] : 0);
-  cols[k++] = direct(env, e.pv_val_off, 8 * (npv + 1));
-  cols[k++] = direct(env, e.pv_val_bytes, e.pv_val_off ? e.pv_val_off[npv] : 0);
-  cols[k++] = direct(env, e.pv_val_null, npv);
-  cols[k++] = direct(env, e.tags_entry_off, 8 * (n + 1));
-  cols[k++] = direct(env, e.tags_null, n);
-  cols[k++] = direct(env, e.tags_key_off, 8 * (ntg + 1));
-  cols[k++] = direct(env, e.tags_key_bytes, e.tags_key_off ? e.tags_key_off[ntg] : 0);
-  cols[k++] = direct(env, e.tags_val_off, 8 * (ntg + 1));
-  cols[k++] = direct(env, e.tags_val_bytes, e.tags_val_off ? e.tags_val_off[ntg] : 0);
-  cols[k++] = direct(env, e.tags_val_null, ntg);
-  jclass bb = (*env)->FindClass(env, "java/nio/ByteBuffer");
-  jobjectArray out = bb ? (*env)->NewObjectArray(env, k, bb, NULL) : NULL;
-  for (int i = 0; out && i < k; ++i) (*env)->SetObjectArrayElement(env, out, i, cols[i]);
+  return columns(env, &e, "export: a column over 2^31 - 1 bytes; take the side as row ranges (exportPlan / exportRange)");
+}
+
+/* Row ranges of a side whose every column fits maxBytes (<= 2^31 - 1 for direct buffers) and which
+ * hold at most maxRows rows: {0, b1, ..., n} (dr_state_export_plan). */
+NATIVE(jlongArray, exportPlan)(JNIEnv* env, jobject self, jlong state, jint which, jlong max_rows, jlong max_bytes) {
+  (void)self;
+  int64_t* b = NULL;
+  int64_t nr = 0;
+  int rc = max_bytes > 0 ? dr_state_export_plan((dr_state*)(intptr_t)state, which, (int64_t)max_rows,
+                                                (uint64_t)max_bytes, &b, &nr)
+                         : DR_E_INVALID_ARG;
+  CHECK_STATE(env, rc, (intptr_t)state, NULL);
+  jlongArray out = long_array(env, b, nr + 1);
+  dr_free(b);
   return out;
+}
+
+/* Rows [lo, hi) of a side as direct buffers with offsets rebased to the range
+ * (dr_state_export_range); handleOut(0) receives the range, valid until rangeRelease -- independent
+ * of the state, so a partition's rows may outlive the snapshot's uncache. */
+NATIVE(jobjectArray, exportRange)(JNIEnv* env, jobject self, jlong state, jint which, jlong lo, jlong hi,
+                                  jlongArray handle_out) {
+  (void)self;
+  if (!handle_out || (*env)->GetArrayLength(env, handle_out) < 1) {
+    throw_status(env, DR_E_INVALID_ARG, "exportRange: handleOut must hold one element");
+    return NULL;
+  }
+  dr_range* range = NULL;
+  dr_export e;
+  memset(&e, 0, sizeof e);
+  int rc = dr_state_export_range((dr_state*)(intptr_t)state, which, (int64_t)lo, (int64_t)hi, &range, &e);
+  CHECK_STATE(env, rc, (intptr_t)state, NULL);
+  jobjectArray out = columns(env, &e, "exportRange: a column over 2^31 - 1 bytes; plan the ranges with exportPlan");
+  if (!out) {
+    dr_range_release(range);
+    return NULL;
+  }
+  const jlong h = (jlong)(intptr_t)range;
+  (*env)->SetLongArrayRegion(env, handle_out, 0, 1, &h);
+  return out;
+}
+
+NATIVE(void, rangeRelease)(JNIEnv* env, jobject self, jlong range) {
+  (void)env; (void)self;
+  dr_range_release((dr_range*)(intptr_t)range);
 }
 
 /* ---- scan side ---------------------------------------------------------------------------------- */
@@ -506,16 +650,16 @@ NATIVE(jobjectArray, partitionGroups)(JNIEnv* env, jobject self, jlong state, jl
   if (rv) (*env)->ReleaseLongArrayElements(env, rows, rv, JNI_ABORT);
   CHECK_STATE(env, rc, (intptr_t)state, NULL);
   jlongArray o = long_array(env, order, ng ? goff[ng] : 0);
-  jlongArray g = long_array(env, goff, ng + 1);
+  jlongArray g = o ? long_array(env, goff, ng + 1) : NULL;
   dr_free(order);
   dr_free(goff);
-  jclass la = (*env)->FindClass(env, "[J");
+  jclass la = g ? (*env)->FindClass(env, "[J") : NULL;
   jobjectArray out = la ? (*env)->NewObjectArray(env, 2, la, NULL) : NULL;
   if (out) {
     (*env)->SetObjectArrayElement(env, out, 0, o);
-    (*env)->SetObjectArrayElement(env, out, 1, g);
+    if (!pending(env)) (*env)->SetObjectArrayElement(env, out, 1, g);
   }
-  return out;
+  return pending(env) ? NULL : out;
 }
 
 /* ---- getChanges (D/DeltaLog.scala:222-238): K1's per-line reading of staged commits -------------- */
@@ -524,21 +668,42 @@ NATIVE(jobjectArray, partitionGroups)(JNIEnv* env, jobject self, jlong state, jl
  * size, deletion_timestamp, bytes), valid until parsedRelease(handleOut(0)). */
 NATIVE(jobjectArray, parseCommits)(JNIEnv* env, jobject self, jlong ctx, jlong staged, jlongArray handle_out) {
   (void)self;
+  if (!handle_out || (*env)->GetArrayLength(env, handle_out) < 1) {
+    throw_status(env, DR_E_INVALID_ARG, "parseCommits: handleOut must hold one element");
+    return NULL;
+  }
   dr_parsed* parsed = NULL;
   dr_lines l;
   memset(&l, 0, sizeof l);
   int rc = dr_parse_commits((dr_ctx*)(intptr_t)ctx, (const dr_staged*)(intptr_t)staged, &parsed, &l);
   CHECK_CTX(env, rc, (intptr_t)ctx, NULL);
   const int64_t n = l.n;
-  jobject cols[10] = {direct(env, l.version, 8 * n),  direct(env, l.line_off, 8 * n), direct(env, l.line_len, 4 * n),
-                      direct(env, l.kind, n),         direct(env, l.flags, n),        direct(env, l.path_off, 8 * n),
-                      direct(env, l.path_len, 4 * n), direct(env, l.size, 8 * n),     direct(env, l.deletion_timestamp, 8 * n),
-                      direct(env, l.bytes, (int64_t)l.nbytes)};
-  jclass bb = (*env)->FindClass(env, "java/nio/ByteBuffer");
+  if (n > 0x0fffffffll || l.nbytes > 0x7fffffffull) {
+    dr_parsed_release(parsed);
+    throw_status(env, DR_E_UNSUPPORTED, "parseCommits: over 2 GiB of commit bytes in one call; stage fewer commits");
+    return NULL;
+  }
+  int failed = 0;
+  jobject cols[10];
+  cols[0] = direct(env, l.version, 8 * n, &failed);
+  cols[1] = direct(env, l.line_off, 8 * n, &failed);
+  cols[2] = direct(env, l.line_len, 4 * n, &failed);
+  cols[3] = direct(env, l.kind, n, &failed);
+  cols[4] = direct(env, l.flags, n, &failed);
+  cols[5] = direct(env, l.path_off, 8 * n, &failed);
+  cols[6] = direct(env, l.path_len, 4 * n, &failed);
+  cols[7] = direct(env, l.size, 8 * n, &failed);
+  cols[8] = direct(env, l.deletion_timestamp, 8 * n, &failed);
+  cols[9] = direct(env, l.bytes, (int64_t)l.nbytes, &failed);
+  jclass bb = failed ? NULL : (*env)->FindClass(env, "java/nio/ByteBuffer");
   jobjectArray out = bb ? (*env)->NewObjectArray(env, 10, bb, NULL) : NULL;
-  for (int i = 0; out && i < 10; ++i) (*env)->SetObjectArrayElement(env, out, i, cols[i]);
+  for (int i = 0; out && i < 10 && !pending(env); ++i) (*env)->SetObjectArrayElement(env, out, i, cols[i]);
+  if (!out || pending(env)) {
+    dr_parsed_release(parsed);
+    return NULL;
+  }
   const jlong h = (jlong)(intptr_t)parsed;
-  if (handle_out && (*env)->GetArrayLength(env, handle_out) >= 1) (*env)->SetLongArrayRegion(env, handle_out, 0, 1, &h);
+  (*env)->SetLongArrayRegion(env, handle_out, 0, 1, &h);
   return out;
 }
 
@@ -617,6 +782,7 @@ NATIVE(jbyteArray, writeCheckpoint)(JNIEnv* env, jobject self, jlong state, jint
   jbyteArray out = (*env)->NewByteArray(env, (jsize)len);
   if (out) (*env)->SetByteArrayRegion(env, out, 0, (jsize)len, (const jbyte*)bytes);
   dr_free(bytes);
+  if (!out || pending(env)) return NULL;
   if (rows_out && (*env)->GetArrayLength(env, rows_out) >= 2) {
     const jlong v[2] = {(jlong)rows, (jlong)adds};
     (*env)->SetLongArrayRegion(env, rows_out, 0, 2, v);

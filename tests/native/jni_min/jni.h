@@ -46,5 +46,8 @@ struct JNINativeInterface_ {
   void (*SetByteArrayRegion)(JNIEnv*, jbyteArray, jsize, jsize, const jbyte*);
   void (*SetLongArrayRegion)(JNIEnv*, jlongArray, jsize, jsize, const jlong*);
   jobject (*NewDirectByteBuffer)(JNIEnv*, void*, jlong);
+  jboolean (*ExceptionCheck)(JNIEnv*);
+  void (*DeleteLocalRef)(JNIEnv*, jobject);
+  jint (*EnsureLocalCapacity)(JNIEnv*, jint);
 };
 #endif

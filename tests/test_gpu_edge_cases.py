@@ -736,6 +736,40 @@ def test_snappy_periodic_dictionary_pages(engine, tmp_path, capfd, monkeypatch):
     assert "snappy bad page" not in err, err[-2000:]
 
 
+@pytest.mark.parametrize("body,rows", [(100, 40000), (400, 12000)], ids=["long_literals", "unstaged_blocks"])
+def test_snappy_long_literals_and_unstaged_blocks(engine, tmp_path, capfd, monkeypatch, body, rows):
+    """k_snap_exec's rarer paths, parity against the oracle with no page sent to the serial decoder:
+    paths whose random 100-character bodies are literals longer than the wave-copy threshold (64 B),
+    more than the 256 queued per block, so the queue overflows into per-lane copies; and 400-character
+    bodies drawn from 64 symbols, which leave only the row's length prefix + "d/" to copy, so a
+    64 KiB output block takes more than 64 KiB of compressed input and its literals are read in
+    place instead of from the LDS stage."""
+    import random
+    import string
+    from delta_amd.testing import synth as S
+    lp = str(tmp_path / "_delta_log")
+    os.makedirs(lp)
+    rng = random.Random(body)
+    sym = string.ascii_letters + string.digits + "-_"
+    adds = [{"path": "d/" + "".join(rng.choice(sym) for _ in range(body)), "partitionValues": {},
+             "size": i + 1, "modificationTime": 1} for i in range(rows)]
+    rms = [{"path": adds[i]["path"], "deletionTimestamp": 5} for i in range(0, rows, 97)]
+    S.write_checkpoint_records(os.path.join(lp, "%020d.checkpoint.parquet" % 0), PROTOCOL["protocol"],
+                               METADATA["metaData"], adds[: rows // 2], use_dictionary=False)
+    with open(os.path.join(lp, "_last_checkpoint"), "w") as f:
+        f.write('{"version":0,"size":%d}\n' % (rows // 2 + 2))
+    line = lambda a: json.dumps(a, separators=(",", ":"))
+    with open(os.path.join(lp, "%020d.json" % 1), "w") as f:
+        f.write("\n".join(line({"add": a}) for a in adds[rows // 2:]) + "\n")
+        f.write("\n".join(line({"remove": r}) for r in rms) + "\n")
+    monkeypatch.setenv("DR_SNAP_DEBUG", "1")
+    counts, live, tomb = _same_as_oracle(engine, lp, cutoff=0)
+    assert counts["num_files"] == rows - len(rms)
+    err = capfd.readouterr().err
+    assert "snappy bad page" not in err, err[-2000:]
+    assert "exec phases" in err  # the pages went through k_snap_exec
+
+
 # ---- staging / scratch guards --------------------------------------------------------------------------
 def test_check_lines_over_edge_corpus(engine, tmp_path, monkeypatch):
     """DR_CHECK_LINES=1 compares the staged newline count (which sizes the action arrays) with K1's

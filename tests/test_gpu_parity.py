@@ -207,10 +207,14 @@ def test_fallback_reducers_agree(engine, tmp_path, reducer):
     (1 << 20, "snappy", "1.0", 5000, False),
     (64 << 10, "snappy", "2.0", 1 << 20, False),
 ])
-def test_checkpoint_page_layouts(engine, tmp_path, page_size, compression, page_version, rg, dictionary):
+def test_checkpoint_page_layouts(engine, tmp_path, capfd, monkeypatch, page_size, compression, page_version, rg,
+                                 dictionary):
     """K2 over page sizes (many tiny pages .. one 8 MiB page), several row groups, uncompressed
-    pages and DATA_PAGE_V2: the replay must not depend on how the writer cut the column chunks."""
+    pages and DATA_PAGE_V2: the replay must not depend on how the writer cut the column chunks, and
+    no SNAPPY page falls back to the serial decoder (the fallback is exact too, so parity alone would
+    not notice k_snap_exec refusing a page)."""
     from delta_amd.testing import synth as S
+    monkeypatch.setenv("DR_SNAP_DEBUG", "1")
     exp = S.build_table(str(tmp_path), S.config_spec(3, 0.003), seed=77, data_page_size=page_size,
                         compression=compression, data_page_version=page_version, row_group_size=rg,
                         use_dictionary=dictionary)
@@ -224,6 +228,8 @@ def test_checkpoint_page_layouts(engine, tmp_path, page_size, compression, page_
         _assert_same(st, snap)
     finally:
         st.release()
+    err = capfd.readouterr().err
+    assert "snappy bad page" not in err, err[-2000:]
 
 
 @pytest.mark.parametrize("fill", [b"\xff" * 256, b"\x01\x00" * 128], ids=["offset_past_start", "offset_zero"])

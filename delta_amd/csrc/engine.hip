@@ -1054,7 +1054,7 @@ static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_
     DBuf<uint64_t> stamps, rstats;
     const bool dbg = std::getenv("DR_SNAP_DEBUG") != nullptr;
     if (dbg) {
-      stamps = DBuf<uint64_t>(ctx, P.block_page.size() * 8);
+      stamps = DBuf<uint64_t>(ctx, P.block_page.size() * 16);
       stamps.zero(stream);
       sa.stamps = stamps.p;
       rstats = DBuf<uint64_t>(ctx, uint64_t(P.nchunks) * 4 + 4);
@@ -1067,17 +1067,24 @@ static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_
       for (uint32_t v : el) P.snap_elements += v;
     }
     if (dbg) {
-      std::vector<uint64_t> st = d2h(stamps.p, P.block_page.size() * 8, stream);
-      double acc[8] = {0};
+      std::vector<uint64_t> st = d2h(stamps.p, P.block_page.size() * 16, stream);
+      // 16 stamp slots per block (k_snap_exec): slot 0 at entry, 15 at the end, the phases between;
+      // the mean clocks from each stamped slot to the next stamped one
+      double acc[16] = {0};
       size_t nb2 = 0;
       for (size_t q = 0; q < P.block_page.size(); ++q) {
-        const uint64_t* x = &st[q * 8];
-        if (!x[0] || !x[7]) continue;
+        const uint64_t* x = &st[q * 16];
+        if (!x[0] || !x[15]) continue;
         ++nb2;
-        for (int k = 1; k < 8; ++k) acc[k] += double(x[k] - x[k - 1]);
+        for (int k = 1, prev = 0; k < 16; ++k)
+          if (x[k]) {
+            acc[k] += double(x[k] - x[prev]);
+            prev = k;
+          }
       }
       std::fprintf(stderr, "exec phases (clocks/block, %zu blocks):", nb2);
-      for (int k = 1; k < 8; ++k) std::fprintf(stderr, " %.0f", nb2 ? acc[k] / double(nb2) : 0.0);
+      for (int k = 1; k < 16; ++k)
+        if (acc[k] != 0) std::fprintf(stderr, " [%d] %.0f", k, nb2 ? acc[k] / double(nb2) : 0.0);
       std::fprintf(stderr, "\n");
       const unsigned long long nreg = d2h_one(P.s_region_count.p, stream);
       std::vector<uint32_t> pb = d2h(P.s_pages_bad.p, P.snap_pages.size(), stream);

@@ -636,26 +636,38 @@ __global__ void __launch_bounds__(SCAN_T) k_snap_scan(SnappyArgs a) {
 // kernel read back are gone, and so is the emit launch).
 //  0. the block's chunks are [block_chunk[b], the chunk holding the next block's first element]; the
 //     bits of a chunk's visited bitmap at or after its true entry are exactly its element starts
-//     (chains that meet coincide; k_snap_count rewrote the chunks whose true chain is another one);
-//  1. in passes of 16 KiB of compressed input staged in LDS, 16 positions per thread (the next pass's
-//     bytes, bitmap word and entry in flight meanwhile): each thread decodes the element headers at
-//     its start bits, a workgroup scan of their output lengths gives every element its output offset
-//     (from the first chunk's k_snap_scan offset), and the elements of this block set their start bit
-//     and the map entry of their first byte (src[rel] = rel - offset; a literal points at itself);
+//     (chains that meet coincide; k_snap_count rewrote the chunks whose true chain is another one).
+//     The chunks' compressed bytes are staged in the LDS (in the map's space, not yet in use);
+//  1. each thread counts the start bits of four bitmap words; a workgroup scan ranks them, and the
+//     elements are cut into runs of EXEC_RUN: in round q thread t walks run q * 1024 + t from its
+//     first start, element after element through the staged headers, keeping them in registers;
+//     a scan of the runs' lengths gives each run its output offset (from the first chunk's
+//     k_snap_scan offset); once the stage is released the elements of this block set their start
+//     bit and the map entry of their first byte (src[rel] = rel - offset; a literal points at
+//     itself). Runs of a wave are consecutive, so the lanes work in step and their map and literal
+//     writes sit a run apart in the LDS banks (r05's first cuts: 16 compressed positions per thread
+//     in 16 KiB passes -- three decodes per element, lanes waiting on the densest one, 51.6 K clocks
+//     per block for this phase against 12.4 K for reading emit's records; then one long run per
+//     thread -- 41 K, its lanes' writes 64 output bytes apart, in two LDS banks);
 //  2. every byte's map entry from the last start at or before it, then pointer jumping until every
 //     byte points at its literal origin (u16 map of the block in LDS, roots in registers);
 //  3. the LDS becomes the block's bytes (lower half) and its compressed input (upper half); each
-//     thread re-decodes its start bits (kept in registers with its per-pass output offsets) and copies
-//     its literals LDS -> LDS, reads batched ahead of writes; long literals go to whole waves;
+//     thread walks its elements again from its first start and copies its literals LDS -> LDS,
+//     reads batched ahead of writes; long literals go to whole waves;
 //  4. each thread gathers its groups' bytes from their roots and stores them (coalesced dwords).
 // Every element of the chunk range is checked (a copy reaching before its fragment, an element
 // straddling a block, literal bytes past the page) and the block's elements must cover it exactly;
-// anything else flags the page for k_snap_serial.
+// anything else -- or a block of more than EXEC_EMAX * 1024 elements or 128 KiB of compressed
+// input, which the SNAPPY compressor's output never has -- flags the page for k_snap_serial.
 constexpr int EXEC_T = 1024;
-constexpr uint32_t PASS_POS = 16;                   // compressed positions per thread and pass
-constexpr uint32_t PASS_BYTES = EXEC_T * PASS_POS;  // compressed bytes per pass
-constexpr uint32_t EXEC_MAXP = 6;                   // passes a block may take (96 KiB of compressed input)
-constexpr uint32_t STG_VEC = EXEC_T + 3;            // staged 16-byte vectors per pass (alignment + header reach)
+#ifndef DR_EXEC_EMAX
+#define DR_EXEC_EMAX 32
+#endif
+#ifndef DR_EXEC_EHELD
+#define DR_EXEC_EHELD 16
+#endif
+constexpr uint32_t EXEC_EMAX = DR_EXEC_EMAX;        // elements per thread: 32 K per block (alternating 1-byte literals and 4-byte copies: 26 K)
+constexpr uint32_t EXEC_EHELD = DR_EXEC_EHELD;      // elements per thread kept in registers through the jumping
 constexpr uint32_t EXEC_LONG = 256;                 // literal records queued for the cooperative copy (at most)
 #ifndef DR_EXEC_LONG_LEN
 #define DR_EXEC_LONG_LEN 64
@@ -704,12 +716,15 @@ __device__ __forceinline__ uint32_t block_excl(uint32_t x, uint32_t* wsum, uint3
   total = tot;
   return before + incl - x;
 }
+// An element in a register: a literal EL_LIT | hdr << 24 | (len - 1); a copy hdr << 24 |
+// (len - 1) << 16 | offset (hdr: header bytes, 1..5; a copy's len - 1 < 64 once validated).
+constexpr uint32_t EL_LIT = 0x80000000u;
 
 __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
-  __shared__ __attribute__((aligned(16))) uint16_t src[SNAP_BLOCK];  // map, later bytes + input
-  __shared__ __attribute__((aligned(16))) uint32_t stg[STG_VEC * 4];  // one pass of compressed input
+  __shared__ __attribute__((aligned(16))) uint16_t src[SNAP_BLOCK];  // stage, then map, then bytes + input
   __shared__ uint32_t s_bad, s_nlong, s_cov;
   __shared__ uint32_t s_wsum[EXEC_T / 64];
+  __shared__ uint32_t s_first[EXEC_T];  // each thread's first element (page-relative position)
   __shared__ uint64_t s_long[EXEC_LONG];  // queued long literal records
   __shared__ uint32_t starts_mem[SNAP_BLOCK / 32 + 2];  // element start bits, after two zero words
   uint32_t* const starts = starts_mem + 2;
@@ -725,7 +740,7 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
   const int t = threadIdx.x;
   // diagnostic phase stamps (DR_SNAP_DEBUG allocates the buffer; null otherwise)
   auto stamp = [&](int k) {
-    if (a.stamps && t == 0) a.stamps[uint64_t(b) * 8 + k] = __builtin_amdgcn_s_memtime();
+    if (a.stamps && t == 0) a.stamps[uint64_t(b) * 16 + k] = __builtin_amdgcn_s_memtime();
   };
   stamp(0);
   // 0. the block's chunk range and compressed range [P_lo, P_hi) (block-uniform)
@@ -736,8 +751,10 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
   const bool range_ok = cl >= c0 && cl < c0 + ncp && cn > cl && cn <= c0 + ncp;
   const uint64_t P_lo = range_ok ? uint64_t(cl - c0) * SNAP_CH : 0;
   const uint64_t P_hi = range_ok ? min(uint64_t(cn - c0) * SNAP_CH, uint64_t(pg.n_in)) : 0;
-  const uint32_t npass = P_hi > P_lo ? uint32_t((P_hi - P_lo + PASS_BYTES - 1) / PASS_BYTES) : 0u;
-  if (npass == 0 || npass > EXEC_MAXP) {
+  const uintptr_t ib = reinterpret_cast<uintptr_t>(in);
+  const uint32_t sh0 = uint32_t((ib + P_lo) & 15);  // the stage's first byte sits sh0 bytes into a vector
+  const uint32_t nv_all = uint32_t((sh0 + (P_hi - P_lo) + 8 + 15) / 16);  // headers read 8 bytes past the range
+  if (!range_ok || P_hi <= P_lo || nv_all * 16 > 2 * SNAP_BLOCK) {
     if (t == 0) atomicOr(&a.pages_bad[p], 16u);
     return;
   }
@@ -747,103 +764,144 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     s_cov = 0;
   }
   for (uint32_t w = t; w < SNAP_BLOCK / 32 + 2; w += EXEC_T) starts_mem[w] = 0;
-  const uintptr_t ib = reinterpret_cast<uintptr_t>(in);
-  const uint32_t sh0 = uint32_t((ib + P_lo) & 15);  // the stage's first byte sits sh0 bytes into a vector
-  // one pass's inputs: the thread's stage vectors, its 16 positions' bitmap word and chunk entry
-  struct Pf {
-    uint4 v0, v1;
-    uint32_t vw, ent;
-  };
-  auto fetch = [&](uint32_t k) -> Pf {
-    Pf f;
-    const uint64_t ps = P_lo + uint64_t(k) * PASS_BYTES;
-    const uint64_t cnt = min(uint64_t(PASS_BYTES), P_hi - ps);
-    const uint32_t nv = uint32_t((sh0 + cnt + 8 + 15) / 16);  // reads reach 8 bytes past the range (padded input)
-    const uint4* g4 = reinterpret_cast<const uint4*>(ib + ps - sh0);
-    f.v0 = gload16(g4 + min(uint32_t(t), nv - 1));
-    f.v1 = t < 3 ? gload16(g4 + min(uint32_t(t) + EXEC_T, nv - 1)) : make_uint4(0, 0, 0, 0);
-    const uint64_t q0 = ps + uint64_t(t) * PASS_POS;
-    f.vw = 0;
-    f.ent = 0xffffffffu;
-    if (q0 < P_hi) {
-      const uint32_t j = uint32_t(q0 / SNAP_CH);
-      f.vw = a.vis[uint64_t(c0 + j) * (SNAP_CH / 32) + uint32_t((q0 % SNAP_CH) / 32)];
-      f.ent = a.entry[c0 + j];
-    }
-    return f;
-  };
-  auto store_stage = [&](const Pf& f) {
-    reinterpret_cast<uint4*>(stg)[t] = f.v0;
-    if (t < 3) reinterpret_cast<uint4*>(stg)[EXEC_T + t] = f.v1;
-  };
-  // the thread's element starts among positions q0 .. q0+15 of pass k: visited bits at or after the
-  // chunk's true entry, below the range end
-  auto pass_bits = [&](const Pf& f, uint32_t k) -> uint32_t {
-    const uint64_t q0 = P_lo + uint64_t(k) * PASS_BYTES + uint64_t(t) * PASS_POS;
-    if (q0 >= P_hi) return 0u;
-    uint32_t m = (f.vw >> (uint32_t(q0) & 16u)) & 0xffffu;
-    if (uint64_t(f.ent) > q0) {
-      const uint64_t cut = uint64_t(f.ent) - q0;
-      m = cut >= PASS_POS ? 0u : m & ~((1u << uint32_t(cut)) - 1u);
-    }
-    if (q0 + PASS_POS > P_hi) m &= (1u << uint32_t(P_hi - q0)) - 1u;
-    return m;
-  };
-  // 1. element offsets, start bits and first-byte map entries, pass by pass
-  uint32_t hold[(EXEC_MAXP + 1) / 2];  // start bits of each pass, two passes per register
-  uint32_t pref[EXEC_MAXP];            // page-relative output offset of the thread's first element per pass
+  // the block's loads, all issued before any is used (one HBM round trip): its chunks' start bitmaps
+  // (four words per thread, half a chunk: one 16-byte load) and entries, the first chunk's output
+  // offset, and its chunks' compressed bytes, which go into the map's space
+  const uint32_t W = (cn - cl) * (SNAP_CH / 32);
+  const bool has_words = 4 * uint32_t(t) < W;
+  uint4 vw = make_uint4(0, 0, 0, 0);
+  uint64_t ent = 0;
+  if (has_words) {
+    vw = *reinterpret_cast<const uint4*>(&a.vis[uint64_t(cl) * (SNAP_CH / 32) + 4 * uint32_t(t)]);
+    ent = a.entry[cl + (4 * uint32_t(t)) / (SNAP_CH / 32)];
+  }
+  const uint32_t out0 = a.chunk_out_start[cl];
+  const uint4* g4 = reinterpret_cast<const uint4*>(ib + P_lo - sh0);
+  uint4* s4 = reinterpret_cast<uint4*>(src);
+  {
+    constexpr uint32_t PER = 2 * SNAP_BLOCK / 16 / EXEC_T;  // 8 vectors per thread at most
+    uint4 v[PER];
 #pragma unroll
-  for (uint32_t k = 0; k < (EXEC_MAXP + 1) / 2; ++k) hold[k] = 0;
-  uint64_t obase = a.chunk_out_start[cl];  // page-relative output offset of the pass's first element
-  uint32_t cov = 0;
-  bool bad = false;
-  Pf cur = fetch(0);
-  store_stage(cur);
+    for (uint32_t k = 0; k < PER; ++k)
+      if (uint32_t(t) + k * EXEC_T < nv_all) v[k] = gload16(g4 + uint32_t(t) + k * EXEC_T);
 #pragma unroll
-  for (uint32_t k = 0; k < EXEC_MAXP; ++k) {
-    if (k >= npass) break;  // block-uniform
-    __syncthreads();        // the pass's stage (and, for pass 0, the cleared start bits) visible
-    Pf nxt;
-    if (k + 1 < npass) nxt = fetch(k + 1);
-    const uint32_t bits = pass_bits(cur, k);
-    const uint32_t o0 = sh0 + uint32_t(t) * PASS_POS;  // stage byte of the thread's first position
-    uint32_t sum = 0;
-    for (uint32_t m = bits; m; m &= m - 1) {
-      uint32_t adv, len;
-      snap_step(lds_hdr(stg, o0 + uint32_t(__builtin_ctz(m))), &adv, &len);
-      sum += min(len, SNAP_BLOCK + 1);  // a longer element is invalid anyway (it straddles a fragment)
+    for (uint32_t k = 0; k < PER; ++k)
+      if (uint32_t(t) + k * EXEC_T < nv_all) s4[uint32_t(t) + k * EXEC_T] = v[k];
+  }
+  // 1a. the start bits masked to each chunk's true chain and to the range (positions are
+  //     page-relative and fit 32 bits: a page is at most 4 GiB)
+  const uint32_t plo = uint32_t(P_lo), phi = uint32_t(P_hi);
+  const uint32_t q0 = plo + uint32_t(t) * 128;  // the thread's first position
+  uint32_t wd[4] = {vw.x, vw.y, vw.z, vw.w};
+  if (has_words) {
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+      const uint32_t ws = q0 + 32 * q;  // the word's first position
+      const uint32_t lo_cut = ent > ws ? min(uint32_t(ent - ws), 32u) : 0u;
+      const uint32_t hi_cut = ws >= phi ? 0u : min(phi - ws, 32u);  // positions below the range end
+      const uint32_t keep = (lo_cut >= 32 ? 0u : ~0u << lo_cut) & (hi_cut >= 32 ? ~0u : (1u << hi_cut) - 1u);
+      wd[q] &= keep;
     }
-    uint32_t total;
-    const uint32_t ex = block_excl(sum, s_wsum, total);
-    uint64_t o = obase + ex;
-    pref[k] = uint32_t(o);
-    hold[k / 2] |= bits << (16 * (k & 1));
-    const uint64_t qb = P_lo + uint64_t(k) * PASS_BYTES + uint64_t(t) * PASS_POS;
-    for (uint32_t m = bits; m; m &= m - 1) {
-      const uint32_t i = uint32_t(__builtin_ctz(m));
-      const SnapEl e = snap_fields(lds_hdr(stg, o0 + i));
-      const uint32_t len = min(e.len, SNAP_BLOCK + 1);
-      if (o < be && o + len > bs) {
-        const uint32_t rel = uint32_t(o - bs);
-        const uint64_t ip = qb + i + e.hdr;  // a literal's first input byte
-        if (o < bs || o + len > be || len > SNAP_BLOCK ||
-            (e.lit ? (ip + len > pg.n_in) : (e.off == 0 || e.off > rel || len > 64))) {
-          bad = true;  // straddles the block, overruns the page, or a copy reaching before its fragment
-        } else {
-          atomicOr(&starts[rel >> 5], 1u << (rel & 31));
-          src[rel] = uint16_t(e.lit ? rel : rel - e.off);
-          cov += len;
-        }
-      } else if (len > SNAP_BLOCK) {
-        bad = true;
+  }
+  stamp(1);
+  const uint32_t cnt = __popc(wd[0]) + __popc(wd[1]) + __popc(wd[2]) + __popc(wd[3]);
+  uint32_t n_el;
+  const uint32_t ex = block_excl(cnt, s_wsum, n_el);
+  const uint32_t E = (n_el + EXEC_T - 1) / EXEC_T;  // elements per thread (block-uniform)
+  if (E > EXEC_EMAX) {
+    if (t == 0) atomicOr(&a.pages_bad[p], 16u);
+    return;
+  }
+  // 1b. the first element of every thread whose share [kE, kE + E) starts among this thread's start
+  //     bits: the r-th set bit of a word by a branch-free binary search on popcounts
+  if (E) {
+    for (uint32_t k = (ex + E - 1) / E; k * E < ex + cnt; ++k) {
+      uint32_t r = k * E - ex, w = 0, base = q0;
+#pragma unroll
+      for (uint32_t q = 0; q < 4; ++q) {  // the word holding rank r
+        const uint32_t pc = __popc(wd[q]);
+        const bool here = r < pc && w == 0 && base == q0 + 32 * q;
+        w = here ? wd[q] : w;
+        const bool past = base == q0 + 32 * q && !here;
+        r -= past ? pc : 0u;
+        base += past ? 32u : 0u;
       }
-      o += len;
+      uint32_t pos = 0;
+#pragma unroll
+      for (uint32_t width = 16; width; width >>= 1) {
+        const uint32_t c = __popc(w & ((1u << width) - 1u));
+        const bool up = r >= c;
+        r -= up ? c : 0u;
+        w = up ? w >> width : w;
+        pos += up ? width : 0u;
+      }
+      s_first[k] = base + pos;
     }
-    obase += total;
-    __syncthreads();  // every thread is done with the stage and the scan words
-    if (k + 1 < npass) {
-      store_stage(nxt);
-      cur = nxt;
+  }
+  stamp(2);
+  __syncthreads();
+  stamp(3);
+  // 1c. thread t walks its share of elements through the staged headers, keeping each in a register
+  const uint32_t mine = n_el > uint32_t(t) * E ? min(E, n_el - uint32_t(t) * E) : 0u;
+  const uint32_t first = mine ? s_first[t] : 0u;
+  const uint32_t* stage32 = reinterpret_cast<const uint32_t*>(src);
+  const uint32_t so_lim = nv_all * 16 - 8;  // the last staged header start
+  uint32_t el[EXEC_EMAX];
+  uint32_t sum = 0;
+  bool bad = false;
+  {
+    uint32_t pos = first;
+#pragma unroll
+    for (uint32_t k = 0; k < EXEC_EMAX; ++k) {
+      el[k] = 0;
+      if (k < mine) {
+        const uint32_t so = pos - plo + sh0;
+        const uint64_t w = lds_hdr(stage32, min(so, so_lim));
+        const uint32_t tag = uint32_t(w) & 0xffu, ty = tag & 3u, l6 = tag >> 2, w8 = uint32_t(w >> 8);
+        const uint32_t nb = l6 >= 60 ? l6 - 59 : 0u;
+        const uint32_t lit_len = (nb ? (w8 & (nb >= 4 ? ~0u : (1u << (8 * nb)) - 1u)) : l6) + 1u;
+        const uint32_t len = ty == 0 ? lit_len : ty == 1 ? (l6 & 7u) + 4u : l6 + 1u;
+        const uint32_t hdr = ty == 0 ? 1u + nb : ty == 1 ? 2u : ty == 2 ? 3u : 5u;
+        const uint32_t off = ty == 1 ? (((tag >> 5) << 8) | (w8 & 0xffu)) : (w8 & 0xffffu);
+        const uint32_t adv = hdr + (ty == 0 ? len : 0u);
+        // a literal past the page or longer than a fragment, a copy offset no fragment has (copy-4's
+        // upper offset bytes): the page is not one the parallel path can take
+        bad |= so > so_lim || (ty == 0 ? (len > SNAP_BLOCK || uint64_t(pos) + adv > pg.n_in)
+                                       : (ty == 3 && (w8 >> 16) != 0));
+        el[k] = (hdr << 24) | (ty == 0 ? (EL_LIT | ((len - 1u) & 0xffffu)) : (((len - 1u) << 16) | off));
+        sum += ty == 0 ? min(len, SNAP_BLOCK) : len;
+        pos += adv;
+      }
+    }
+  }
+  uint32_t tot_out;
+  const uint32_t o_first = out0 + block_excl(sum, s_wsum, tot_out);  // page-relative output offset of the thread's first element
+  stamp(4);
+  __syncthreads();  // every thread is done with the stage (and the scan words)
+  // 1d. start bits and first-byte map entries of this block's elements
+  const uint32_t bs32 = uint32_t(bs), be32 = uint32_t(be);
+  uint32_t cov = 0;
+  {
+    uint32_t o = o_first;
+#pragma unroll
+    for (uint32_t k = 0; k < EXEC_EMAX; ++k) {
+      if (k < mine) {
+        const uint32_t x = el[k];
+        const bool lit = x & EL_LIT;
+        const uint32_t len = lit ? (x & 0xffffu) + 1u : ((x >> 16) & 0x7fu) + 1u;
+        const uint32_t off = x & 0xffffu;
+        const uint32_t rel = o - bs32;
+        if (o < be32 && o + len > bs32) {
+          if (o < bs32 || o + len > be32 || (!lit && (off == 0 || off > rel))) {
+            bad = true;  // straddles the block, or a copy reaching before its fragment
+          } else {
+            atomicOr(&starts[rel >> 5], 1u << (rel & 31));
+            src[rel] = uint16_t(lit ? rel : rel - off);
+            cov += len;
+          }
+        }
+        o += len;
+      }
     }
   }
   if (bad) s_bad = 1;
@@ -851,9 +909,8 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     const uint32_t cw = wv::scan_incl(cov, 0u, [](uint32_t x, uint32_t y) { return x + y; });
     if ((t & 63) == 63) atomicAdd(&s_cov, cw);
   }
-  stamp(1);
   __syncthreads();
-  stamp(2);
+  stamp(5);
   if (s_bad || s_cov != nbytes) {  // block-uniform: the block's elements must cover it exactly
     if (t == 0) atomicOr(&a.pages_bad[p], 32u);
     return;
@@ -932,7 +989,7 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
       }
     }
     __syncthreads();
-    stamp(3);
+    stamp(6);
     while (act) {
 #pragma unroll
       for (uint32_t j = 0; j < 16; ++j) {
@@ -953,24 +1010,22 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
   }
   __syncthreads();
   // 3. the LDS becomes the block's bytes (lower half) and its compressed input (upper half: the
-  //    block's whole range, headers included, so each thread re-decodes its start bits from it)
+  //    block's whole range, headers included, so each thread walks its elements again from it)
   uint8_t* bytes = reinterpret_cast<uint8_t*>(src);
   uint8_t* stage = bytes + SNAP_BLOCK;
-  const uint32_t nv_all = uint32_t((sh0 + (P_hi - P_lo) + 8 + 15) / 16);
   const bool staged = nv_all * 16 <= SNAP_BLOCK;  // block-uniform
   if (staged) {  // all of a thread's loads in flight at once (nv_all <= SNAP_BLOCK / 16: four per thread)
-    const uint4* g4 = reinterpret_cast<const uint4*>(ib + P_lo - sh0);
-    uint4* s4 = reinterpret_cast<uint4*>(stage);
+    uint4* u4 = reinterpret_cast<uint4*>(stage);
     constexpr uint32_t PER = SNAP_BLOCK / 16 / EXEC_T;
     uint4 v[PER];
 #pragma unroll
     for (uint32_t k = 0; k < PER; ++k) v[k] = gload16(g4 + min(uint32_t(t) + k * EXEC_T, nv_all - 1));
 #pragma unroll
     for (uint32_t k = 0; k < PER; ++k)
-      if (uint32_t(t) + k * EXEC_T < nv_all) s4[uint32_t(t) + k * EXEC_T] = v[k];
+      if (uint32_t(t) + k * EXEC_T < nv_all) u4[uint32_t(t) + k * EXEC_T] = v[k];
   }
   __syncthreads();
-  stamp(4);
+  stamp(7);
   // a literal of this block (rel, len, page-relative input position ip): LDS -> LDS copy, or queued
   // for a whole wave when long
   auto copy_lit = [&](uint32_t rel, uint32_t len, uint64_t ip) {
@@ -1011,24 +1066,35 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     q = uint32_t(reinterpret_cast<const uint8_t*>(qa) - bytes) + sh;
     while (n) { bytes[d++] = bytes[q++]; --n; }
   };
+  // the thread's elements again from its first start: from the registers when the thread has at
+  // most EXEC_EHELD (its elements stayed live through the jumping), else re-read from the stage
+  if (E <= EXEC_EHELD) {  // block-uniform
+    uint32_t pos = first, o = o_first;
 #pragma unroll
-  for (uint32_t k = 0; k < EXEC_MAXP; ++k) {
-    if (k >= npass) break;  // block-uniform
-    const uint32_t bits = (hold[k / 2] >> (16 * (k & 1))) & 0xffffu;
-    uint64_t o = pref[k];
-    const uint64_t qb = P_lo + uint64_t(k) * PASS_BYTES + uint64_t(t) * PASS_POS;
-    for (uint32_t m = bits; m; m &= m - 1) {
-      const uint64_t q = qb + uint32_t(__builtin_ctz(m));
-      const uint64_t w = staged ? lds_hdr(reinterpret_cast<const uint32_t*>(stage), uint32_t(q - P_lo) + sh0)
-                                : load_u64(in + q);
+    for (uint32_t k = 0; k < EXEC_EHELD; ++k) {
+      if (k < mine) {
+        const uint32_t x = el[k];
+        const bool lit = x & EL_LIT;
+        const uint32_t len = lit ? (x & 0xffffu) + 1u : ((x >> 16) & 0x7fu) + 1u;
+        const uint32_t hdr = (x >> 24) & 7u;
+        if (lit && o >= bs32 && o < be32) copy_lit(o - bs32, len, pos + hdr);
+        o += len;
+        pos += hdr + (lit ? len : 0u);
+      }
+    }
+  } else {
+    const uint32_t* st32 = reinterpret_cast<const uint32_t*>(stage);
+    uint32_t pos = first, o = o_first;
+    for (uint32_t k = 0; k < mine; ++k) {
+      const uint64_t w = staged ? lds_hdr(st32, pos - plo + sh0) : load_u64(in + pos);
       const SnapEl e = snap_fields(w);
-      const uint32_t len = min(e.len, SNAP_BLOCK + 1);
-      if (e.lit && o >= bs && o < be) copy_lit(uint32_t(o - bs), len, q + e.hdr);
-      o += len;
+      if (e.lit && o >= bs32 && o < be32) copy_lit(o - bs32, e.len, pos + e.hdr);
+      o += e.len;
+      pos += e.hdr + (e.lit ? e.len : 0u);
     }
   }
   __syncthreads();
-  stamp(5);
+  stamp(8);
   const uint32_t nlong = min(s_nlong, EXEC_LONG);
   for (uint32_t L = uint32_t(t) >> 6; L < nlong; L += EXEC_T / 64) {  // long literals: one wave each
     const uint64_t wl = s_long[L];
@@ -1044,7 +1110,7 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     }
   }
   __syncthreads();
-  stamp(6);
+  stamp(9);
   // 4. gather and store: the thread's 4-byte groups are the ones it resolved (roots still in
   //    registers); a wave's 64 groups are 256 contiguous bytes, so literal bytes (their own roots)
   //    and runs of one copy read consecutive LDS banks, and the dword stores coalesce
@@ -1067,7 +1133,7 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     __syncthreads();
     for (uint32_t i = t; i < nbytes; i += EXEC_T) dst[i] = bytes[i];
   }
-  stamp(7);
+  stamp(15);
 }
 
 // Serial fallback for pages whose structure the parallel path could not use.

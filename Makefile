@@ -13,8 +13,12 @@ HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-functi
 CXXFLAGS := -O2 -std=c++17 -fPIC -Wall
 
 JL_HOST := build/libjsonlane_host.so
+# the same library with the tape kernels' LDS index checks (k_json.hip -DDR_BOUNDS_CHECK;
+# tests/test_gpu_bounds.py loads it through DR_LIB)
+LIB_BOUNDS := delta_amd/libdeltareplay_bounds.so
+BOUNDS_OBJS := $(filter-out $(OBJDIR)/k_json.o,$(HIP_OBJS)) $(OBJDIR)/k_json_bounds.o
 
-all: $(LIB) oracle $(JL_HOST)
+all: $(LIB) $(LIB_BOUNDS) oracle $(JL_HOST)
 
 # host build of the K1 line walker, fuzzed against Python json by tests/test_json_lane.py
 $(JL_HOST): tests/native/json_lane_host.cpp $(CSRC)/json_lane.h
@@ -33,11 +37,18 @@ $(OBJDIR)/%.o: $(CSRC)/%.cpp $(HDRS)
 $(LIB): $(HIP_OBJS) $(CXX_OBJS)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^
 
+$(OBJDIR)/k_json_bounds.o: $(CSRC)/k_json.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -DDR_BOUNDS_CHECK -c $< -o $@
+
+$(LIB_BOUNDS): $(BOUNDS_OBJS) $(CXX_OBJS)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^
+
 oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf build $(LIB)
+	rm -rf build $(LIB) $(LIB_BOUNDS)
 	$(MAKE) -C oracle clean
 
 .PHONY: all clean oracle

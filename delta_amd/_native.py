@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdeltareplay.so")
+# DR_LIB (tests): an in-tree variant of the library, e.g. libdeltareplay_bounds.so (LDS index checks)
+LIB_PATH = os.path.join(_HERE, os.environ.get("DR_LIB", "libdeltareplay.so"))
 
 DR_OK = 0
 STATUS = {

@@ -38,8 +38,65 @@
 #include "log_segment.h"
 #include "parquet_meta.h"
 
+// ---- stage ranges (SURVEY.md §5 tracing) --------------------------------------------------------------
+// roctx ranges around the replay's stages -- parse.json, decode.checkpoint, canonicalize,
+// hash.partition, reduce, compact, exchange, filter, export, checkpoint.write, apply -- under a
+// top-level range per C-ABI operation, the counterpart of the reference's recordDeltaOperation around
+// "delta.log.update" / "delta.checkpoint" (D/metering/DeltaLogging.scala:58-108). Off unless DR_ROCTX is
+// set (rocprofv3 --marker-trace shows them); the library dlopens rocprofiler-sdk's roctx on first use,
+// so it carries no link dependency. A replay enqueues all its kernels before one host round trip, so a
+// range spans its stage's enqueues; DR_ROCTX=sync closes every range with a stream synchronize, which
+// makes the ranges the stages' device time (and serialises K1 with K2).
+namespace trace {
+struct Api {
+  int (*push)(const char*) = nullptr;
+  int (*pop)() = nullptr;
+};
+static int mode() {
+  static const int m = [] {
+    const char* e = std::getenv("DR_ROCTX");
+    return !e || !*e || std::strcmp(e, "0") == 0 ? 0 : std::strcmp(e, "sync") == 0 ? 2 : 1;
+  }();
+  return m;
+}
+static const Api& api() {
+  static const Api a = [] {
+    Api x;
+    if (!mode()) return x;
+    void* h = dlopen("librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("libroctx64.so.4", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return x;
+    x.push = reinterpret_cast<int (*)(const char*)>(dlsym(h, "roctxRangePushA"));
+    x.pop = reinterpret_cast<int (*)()>(dlsym(h, "roctxRangePop"));
+    if (!x.push || !x.pop) x = Api{};
+    return x;
+  }();
+  return a;
+}
+}  // namespace trace
+struct StageRange {
+  hipStream_t s;
+  bool on;
+  explicit StageRange(const char* name, hipStream_t stream = nullptr) : s(stream), on(trace::mode() && trace::api().push) {
+    if (on) trace::api().push(name);
+  }
+  ~StageRange() {
+    if (!on) return;
+    if (trace::mode() == 2 && s) (void)hipStreamSynchronize(s);
+    trace::api().pop();
+  }
+  StageRange(const StageRange&) = delete;
+  StageRange& operator=(const StageRange&) = delete;
+};
+// a range over the rest of the enclosing scope
+#define DR_STAGE_CAT2(a, b) a##b
+#define DR_STAGE_CAT(a, b) DR_STAGE_CAT2(a, b)
+#define DR_STAGE(name, stream) StageRange DR_STAGE_CAT(dr_stage_range_, __LINE__)(name, stream)
+
+
 using namespace dr;
 
+#define HIP_OK_NOTHROW(x) (void)(x)  // (destructor paths: a failed call is left to the next checked one)
 #define HIP_OK(x)                                                                                  \
   do {                                                                                             \
     hipError_t e_ = (x);                                                                           \
@@ -141,19 +198,44 @@ struct dr_ctx {
     std::atomic_thread_fence(std::memory_order_acquire);
   }
 
+  // DR_POISON=1 (tests): every block handed out is filled with 0xA5 first, so a kernel that reads
+  // memory it never wrote sees the same garbage whatever the context ran before (a block reused
+  // from free_blocks otherwise holds whatever its last owner left). The fill is ordered after all
+  // queued work and before all later work: a released block may still be read by kernels queued on
+  // the context's streams (stream order makes that safe for the next owner), and the null stream is
+  // not ordered with the context's non-blocking streams.
+  static bool poison() {
+    static const bool on = std::getenv("DR_POISON") != nullptr;
+    return on;
+  }
+  // (the whole block: a reused block can be up to 2n + 1 MiB, and a read past n must not see history)
+  void* poisoned(void* p, size_t n) {
+    if (poison() && p) {
+      size_t blk = n;
+      {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = sizes.find(p);
+        if (it != sizes.end()) blk = it->second;
+      }
+      HIP_OK(hipDeviceSynchronize());
+      HIP_OK(hipMemset(p, 0xA5, blk));
+      HIP_OK(hipDeviceSynchronize());
+    }
+    return p;
+  }
   void* alloc(size_t n) {
     n = (n + 255) & ~size_t(255);
     if (n == 0) n = 256;
+    void* p = nullptr;
     {
       std::lock_guard<std::mutex> g(mu);
       auto it = free_blocks.lower_bound(n);
       if (it != free_blocks.end() && it->first <= 2 * n + (1 << 20)) {
-        void* p = it->second;
+        p = it->second;
         free_blocks.erase(it);
-        return p;
       }
     }
-    void* p = nullptr;
+    if (p) return poisoned(p, n);
     if (hipMalloc(&p, n) != hipSuccess) {
       (void)hipGetLastError();
       trim();
@@ -162,14 +244,71 @@ struct dr_ctx {
         fail(DR_E_OOM, fmt("device allocation of %zu bytes failed", n));
       }
     }
-    std::lock_guard<std::mutex> g(mu);
-    sizes[p] = n;
-    return p;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      sizes[p] = n;
+    }
+    return poisoned(p, n);
   }
   void release(void* p) {
     if (!p) return;
+    if (poison()) {  // quarantined until the API call ends (check_quarantine)
+      size_t n = 0;
+      {
+        std::lock_guard<std::mutex> g(mu);
+        n = sizes[p];
+      }
+      HIP_OK_NOTHROW(hipDeviceSynchronize());
+      HIP_OK_NOTHROW(hipMemset(p, 0xA5, n));
+      HIP_OK_NOTHROW(hipDeviceSynchronize());
+      std::lock_guard<std::mutex> g(mu);
+      quarantine.push_back(p);
+      return;
+    }
     std::lock_guard<std::mutex> g(mu);
     free_blocks.emplace(sizes[p], p);
+  }
+  // DR_POISON: blocks released during an API call, filled with 0xA5 at release. When the call ends
+  // (guard) every one must still hold only 0xA5 -- a write after release is a kernel queued after the
+  // block was handed back, i.e. a buffer that did not live as long as the launch using it -- and then
+  // joins the free list. (Blocks over 4 MiB: their first and last 64 KiB.)
+  std::vector<void*> quarantine;
+  std::string check_quarantine() {
+    std::vector<void*> q;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      q.swap(quarantine);
+    }
+    if (q.empty()) return "";
+    std::string bad;
+    if (hipDeviceSynchronize() != hipSuccess) bad = "device error before the quarantine check";
+    std::vector<uint8_t> h;
+    for (void* p : q) {
+      size_t n;
+      {
+        std::lock_guard<std::mutex> g(mu);
+        n = sizes[p];
+      }
+      const size_t win = size_t(64) << 10;
+      const std::pair<size_t, size_t> spans[2] = {{0, n <= (size_t(4) << 20) ? n : win},
+                                                  {n <= (size_t(4) << 20) ? n : n - win, n}};
+      for (const auto& sp : spans) {
+        if (sp.second <= sp.first || !bad.empty()) continue;
+        h.resize(sp.second - sp.first);
+        if (hipMemcpy(h.data(), static_cast<uint8_t*>(p) + sp.first, h.size(), hipMemcpyDeviceToHost) != hipSuccess) {
+          bad = "quarantine read failed";
+          break;
+        }
+        for (size_t k = 0; k < h.size(); ++k)
+          if (h[k] != 0xA5) {
+            bad = fmt("device block of %zu bytes written after its release (byte %zu = 0x%02x)", n, sp.first + k, h[k]);
+            break;
+          }
+      }
+      std::lock_guard<std::mutex> g(mu);
+      free_blocks.emplace(n, p);
+    }
+    return bad;
   }
   // pinned host blocks (hipHostMalloc) for the export columns, cached like the device blocks: a
   // released state's block serves the next export of a similar size without pinning pages again
@@ -1498,12 +1637,14 @@ struct ParsePending {
   bool canon_sized = false; // the arena was sized from the counters (exact), not from a hint
   size_t pin_at = 0;        // where its words land in ctx->pinned()
   // the small tail's deferred post-parse launch (parse_launch's defer_tail): k_tail_post's work,
-  // run by launch_apply_small or parse_flush_tail; nl / hard stay alive for it
+  // run by launch_apply_small or parse_flush_tail; every buffer tail_ja points at stays alive for it
+  // (nl, hard, and off2's: a block released here is handed to the next allocation while the deferred
+  // launch, queued after that allocation's users, still writes it)
   bool tail_deferred = false;
   bool parse_deferred = false;  // ... and the line walk too (launch_apply_commit / parse_flush_tail)
   JsonParseArgs tail_ja{};
   CanonArgs tail_cg{};
-  DBuf<uint64_t> nl, hard;
+  DBuf<uint64_t> nl, hard, off2;
 };
 constexpr size_t kPinNonfile = 1024;  // non-file entries (pairs) read back with the counters
 
@@ -1581,6 +1722,7 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
   JsonParseArgs ja{};
   if (nlines) {
     hipStream_t s2 = overlap ? ctx->stream2 : stream;
+    DR_STAGE("parse.json", s2);
     if (overlap) {
       HIP_OK(hipEventCreateWithFlags(&ov.fork, hipEventDisableTiming));
       HIP_OK(hipEventRecord(ov.fork, stream));
@@ -1637,6 +1779,7 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
   DBuf<uint64_t> dict_ptr;
   DBuf<uint32_t> dict_len, pq_err;
   if (R) {
+    DR_STAGE("decode.checkpoint", stream);
     ParquetArgs pa{};
     pa.ncols = HC_N;
     cdefs = DBuf<uint8_t>(ctx, uint64_t(HC_N) * R);
@@ -1679,6 +1822,7 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
   if (R) HIP_OK(hipMemcpyAsync(counters.p + 7, pq_err.p, sizeof(uint32_t), hipMemcpyDeviceToDevice, stream));
   // ---- canonicalisation of special paths ----
   if (canonicalize) {
+    DR_STAGE("canonicalize", stream);
     int64_t hint = s.canon_need.load();
     // test hook: DR_CANON_HINT=<bytes> stands in for the first replay's exact sizing (an undersized
     // hint exercises the detect-and-redo path)
@@ -1716,6 +1860,7 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
   if (pp.tail_deferred) {
     pp.nl = std::move(nl);
     pp.hard = std::move(hard);
+    pp.off2 = std::move(joff);  // the fused walk's line count (fuse1: ja.off2)
   }
   pp.R = R;
   pp.nlines = nlines;
@@ -1851,10 +1996,13 @@ static ReducePending reduce_launch(dr_ctx* ctx, dr_state* st, int64_t cutoff, ui
                    tcnt.p, toff.p, nullptr, st->path_ptr.p, st->path_len.p, pref.p};
   DBuf<PartRec> rec(ctx, N);
   pa.rec = rec.p;
-  launch_bucket_hist(pa, stream);
-  launch_scan_u32(tcnt.p, toff.p, ncell, ss(pscratch), stream);
-  launch_bucket_offsets(toff.p, nb, nt, boff.p, stream);
-  launch_bucket_scatter(pa, stream);
+  {
+    DR_STAGE("hash.partition", stream);
+    launch_bucket_hist(pa, stream);
+    launch_scan_u32(tcnt.p, toff.p, ncell, ss(pscratch), stream);
+    launch_bucket_offsets(toff.p, nb, nt, boff.p, stream);
+    launch_bucket_scatter(pa, stream);
+  }
   // ---- K4: per-bucket last-writer-wins ----
   DBuf<uint32_t> olive(ctx, N), otomb(ctx, N), lcount(ctx, nb), tcount(ctx, nb), pcount(ctx, nb), rlist(ctx, nb),
       xlist(ctx, nb);
@@ -1863,6 +2011,7 @@ static ReducePending reduce_launch(dr_ctx* ctx, dr_state* st, int64_t cutoff, ui
   totals.zero(stream);
   ReduceArgs ra{rec.p, boff.p, nb, bits, st->size.p, st->path_ptr.p, st->path_len.p, olive.p, otomb.p, opair.p, pref.p,
                 lcount.p, tcount.p, pcount.p, totals.p, rlist.p, xlist.p, bstats.p};
+  std::unique_ptr<StageRange> reduce_range(new StageRange("reduce", stream));
   auto upload_list = [&](const std::vector<uint32_t>& v) {
     DBuf<uint32_t> d(ctx, v.size());
     HIP_OK(hipMemcpyAsync(d.p, v.data(), v.size() * 4, hipMemcpyHostToDevice, stream));
@@ -1895,6 +2044,8 @@ static ReducePending reduce_launch(dr_ctx* ctx, dr_state* st, int64_t cutoff, ui
     }
   }
   launch_sum_stats(ra, stream);
+  reduce_range.reset();
+  DR_STAGE("compact", stream);
   // ---- compaction (survivor lists sized to the bound; the counts come back once, at the end) ----
   DBuf<uint64_t> loff(ctx, nb + 1), tmoff(ctx, nb + 1);
   launch_survivor_scan(lcount.p, tcount.p, nb, loff.p, tmoff.p, stream);
@@ -2175,6 +2326,7 @@ static std::shared_ptr<IncChain> chain_from(dr_ctx* ctx, dr_state& base, uint64_
 static dr_state* apply_incremental(dr_ctx* ctx, dr_state& base, const std::shared_ptr<IncChain>& ch, dr_state& t,
                                    const std::shared_ptr<StagedData>& tail, int64_t cutoff, int64_t version,
                                    ParsePending& pp, std::vector<NonFileAction>& nf) {
+  DR_STAGE("apply", ctx->stream);
   hipStream_t stream = ctx->stream;
   IncChain& c = *ch;
   const uint64_t T = t.n_actions, lo = c.n;
@@ -2296,6 +2448,7 @@ static int64_t check_tail(dr_state& base, const std::shared_ptr<StagedData>& tai
 // stay dropped, so the cutoff must not move backwards). Nothing of the base is re-parsed either way.
 static dr_state* apply_tail(dr_ctx* ctx, dr_state& base, const std::shared_ptr<StagedData>& tail, int64_t cutoff,
                             uint32_t flags) {
+  DR_STAGE("apply", ctx->stream);
   const int64_t version = check_tail(base, tail, cutoff);
   std::unique_ptr<dr_state> t(new_state(ctx, tail));
   std::vector<NonFileAction> nf;
@@ -2376,6 +2529,7 @@ static dr_state* apply_tail(dr_ctx* ctx, dr_state& base, const std::shared_ptr<S
 // counters, error codes and non-file line list of the parse and the reducer's totals land in the
 // pinned words with one stream sync. The host's protocol / metaData / txn reduction follows.
 static dr_state* replay(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, int64_t cutoff, uint32_t flags) {
+  DR_STAGE("delta.stateReconstruction", ctx->stream);
   std::unique_ptr<dr_state> st(new_state(ctx, sp));
   ctx->mark("start");
   std::vector<NonFileAction> nf;
@@ -2520,6 +2674,7 @@ struct DevExport {
 // export queues each group's copy to the host there.
 static void export_device(dr_state& st, int which, DevExport& X, uint64_t lo = 0, uint64_t hi = UINT64_MAX,
                           const std::function<void(int)>* at = nullptr) {
+  DR_STAGE("export", st.ctx->stream);
   ensure_ready(st);
   dr_ctx* ctx = st.ctx;
   hipStream_t stream = ctx->stream;
@@ -3529,57 +3684,64 @@ static int decimal_bytes(int precision) {
   return n;
 }
 
-// The part file, grown in a malloc'd buffer that dr_state_write_checkpoint hands to the caller as
-// is (page bodies are copied in from the device; nothing is zero-filled or copied a second time).
-struct MallocBytes {
-  uint8_t* p = nullptr;
-  size_t n = 0, cap = 0;
-  MallocBytes() = default;
-  MallocBytes(const MallocBytes&) = delete;
-  MallocBytes& operator=(const MallocBytes&) = delete;
-  ~MallocBytes() { free(p); }
-  size_t size() const { return n; }
-  uint8_t* data() { return p; }
-  void clear() { n = 0; }
-  void reserve(size_t c) {
-    if (c <= cap) return;
-    uint8_t* q = static_cast<uint8_t*>(realloc(p, c));
-    if (!q) throw std::bad_alloc();
-    p = q;
-    cap = c;
-  }
-  void resize(size_t m) {
-    if (m > cap) reserve(std::max(m, cap * 2));
-    n = m;
-  }
-  uint8_t* end() { return p + n; }
-  void push_back(uint8_t b) {
-    resize(n + 1);
-    p[n - 1] = b;
+// The part file as it is built: host-encoded bytes (page headers, head-row leaves, the footer) and
+// device page bodies, each at its file offset. The device bodies stay in HBM until the file is
+// complete; then one pinned block of the exact size takes every segment (the bodies by D2H copies
+// queued back to back, one stream sync) and is handed to the caller (dr_free returns it to the
+// context's pinned pool): no pageable D2H, no realloc growth, no second host copy.
+struct PartFile {
+  struct Seg {
+    uint64_t off = 0;
+    std::vector<uint8_t> h;
+    DBuf<uint8_t> d;
+    uint64_t dn = 0;
+  };
+  std::vector<Seg> segs;
+  uint64_t size = 0;
+  std::vector<uint8_t>& tail() {  // the host segment at the end of the file
+    if (segs.empty() || segs.back().dn) {
+      segs.emplace_back();
+      segs.back().off = size;
+    }
+    return segs.back().h;
   }
   template <typename It>
-  void insert(uint8_t*, It a, It b) {
-    const size_t k = size_t(std::distance(a, b)), at = n;
-    resize(n + k);
-    std::copy(a, b, p + at);
+  void host(It a, It b) {
+    std::vector<uint8_t>& t = tail();
+    const size_t k = size_t(std::distance(a, b));
+    t.insert(t.end(), a, b);
+    size += k;
   }
-  void insert(uint8_t* e, std::initializer_list<uint8_t> l) { insert(e, l.begin(), l.end()); }
-  uint8_t* release() {
-    uint8_t* q = p;
-    p = nullptr;
-    n = cap = 0;
-    return q;
+  void host(std::initializer_list<uint8_t> l) { host(l.begin(), l.end()); }
+  void push_back(uint8_t x) {  // (put_u32le / put_varint)
+    tail().push_back(x);
+    ++size;
+  }
+  void dev(DBuf<uint8_t>&& b, uint64_t n) {
+    if (!n) return;
+    segs.emplace_back();
+    segs.back().off = size;
+    segs.back().d = std::move(b);
+    segs.back().dn = n;
+    size += n;
   }
 };
 
+// Pinned part files handed out by dr_state_write_checkpoint, by address: dr_free returns one to its
+// context's pinned pool (or frees it when the context is gone).
+static std::mutex g_pinned_out_mu;
+static std::unordered_map<void*, dr_ctx*> g_pinned_out;
+
 struct CkPartOut {
-  MallocBytes file;
+  uint8_t* data = nullptr;  // pinned (dr_ctx::host_alloc), registered in g_pinned_out
+  uint64_t len = 0;
   int64_t rows = 0;
   int64_t add_rows = 0;  // add rows encoded (Checkpoints.scala:325-328's accumulator)
 };
 
 static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uint32_t opts, uint64_t rg_rows,
                                   CkPartOut& out) {
+  DR_STAGE("checkpoint.write", st.ctx->stream);
   dr_ctx* ctx = st.ctx;
   ctx->begin_call();
   ensure_ready(st);
@@ -3858,10 +4020,8 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
     for (uint64_t h = 0; h < H; ++h) head_row_levels(L, 0, head[h], L.hdef[h], L.hrep[h], L.hval[h]);
   }
   // ---- pages ----
-  MallocBytes& f = out.file;
-  f.clear();
-  f.reserve(size_t(p1 - p0) * 160 + (size_t(1) << 20));  // address space only; grows if exceeded
-  f.insert(f.end(), {'P', 'A', 'R', '1'});
+  PartFile f;
+  f.host({'P', 'A', 'R', '1'});
   struct ChunkMeta { int64_t off, size, usize, nval; int codec; };
   struct RG { std::vector<ChunkMeta> cols; int64_t rows, bytes; };
   std::vector<RG> rgs;
@@ -4000,17 +4160,13 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
       ph.i32(4, 3);  // RLE
       ph.end_struct();
       ph.b.push_back(0);
-      const int64_t off = int64_t(f.size());
-      f.insert(f.end(), ph.b.begin(), ph.b.end());
+      const int64_t off = int64_t(f.size);
+      f.host(ph.b.begin(), ph.b.end());
       if (dev) {
-        f.insert(f.end(), dev_prefix.begin(), dev_prefix.end());
-        const size_t at = f.size();
-        f.resize(at + dev_out_len);
-        if (dev_out_len) HIP_OK(hipMemcpyAsync(f.data() + at, dev_out.p, dev_out_len, hipMemcpyDeviceToHost, stream));
-        HIP_OK(hipStreamSynchronize(stream));
-        tmark("d2h");
+        f.host(dev_prefix.begin(), dev_prefix.end());
+        f.dev(std::move(dev_out), dev_out_len);  // copied out with the rest of the file below
       } else {
-        f.insert(f.end(), body.begin(), body.end());
+        f.host(body.begin(), body.end());
       }
       rg.cols.push_back(ChunkMeta{off, int64_t(ph.b.size() + blen), int64_t(ph.b.size() + raw), int64_t(nlev), codec});
       tmark("file");
@@ -4065,10 +4221,30 @@ static void write_checkpoint_part(dr_state& st, int32_t part, int32_t parts, uin
   }
   fm.str(6, "libdeltareplay (MI355X checkpoint writer)");
   fm.b.push_back(0);
-  f.insert(f.end(), fm.b.begin(), fm.b.end());
+  f.host(fm.b.begin(), fm.b.end());
   put_u32le(f, uint32_t(fm.b.size()));
-  f.insert(f.end(), {'P', 'A', 'R', '1'});
+  f.host({'P', 'A', 'R', '1'});
   tmark("footer");
+  // ---- the file into one pinned block: host segments copied, device bodies DMA'd, one sync ----
+  uint8_t* host = static_cast<uint8_t*>(ctx->host_alloc(f.size));
+  try {
+    for (PartFile::Seg& g : f.segs) {
+      if (g.dn) HIP_OK(hipMemcpyAsync(host + g.off, g.d.p, g.dn, hipMemcpyDeviceToHost, stream));
+      else if (!g.h.empty()) std::memcpy(host + g.off, g.h.data(), g.h.size());
+    }
+    HIP_OK(hipStreamSynchronize(stream));
+  } catch (...) {
+    (void)hipStreamSynchronize(stream);
+    ctx->host_release(host);
+    throw;
+  }
+  {
+    std::lock_guard<std::mutex> g(g_pinned_out_mu);
+    g_pinned_out[host] = ctx;
+  }
+  out.data = host;
+  out.len = f.size;
+  tmark("d2h");
   if (dbg)
     for (auto& kv : t_acc) fprintf(stderr, "[ckpt] %-12s %9.3f ms\n", kv.first.c_str(), kv.second);
   ctx->collect_timings();
@@ -4131,6 +4307,7 @@ static void build_dict(dr_state& st, dr_state::PvCol& col) {
 }
 
 static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred) {
+  DR_STAGE("filter", st.ctx->stream);
   check_program(pred);
   dr_ctx* ctx = st.ctx;
   ctx->begin_call();
@@ -5022,8 +5199,11 @@ static dr_state* replay_sharded_rccl(dr_comm& c, const std::shared_ptr<StagedDat
   // pack, exchange, reduce, return the verdicts and all-reduce the counters: all queued on the
   // context's stream (RCCL is stream-ordered), no host round trip
   shard_pack(sh, send_rec.p, send_path.p, /*sync=*/false);
-  rccl_all_to_all(c, send_rec.p, scb, recv_rec.p, rcb);
-  rccl_all_to_all(c, send_path.p, sb, recv_path.p, rb);
+  {
+    DR_STAGE("exchange", c.ctx->stream);
+    rccl_all_to_all(c, send_rec.p, scb, recv_rec.p, rcb);
+    rccl_all_to_all(c, send_path.p, sb, recv_path.p, rb);
+  }
   shard_reduce(sh, recv_rec.p, nrecv, recv_path.p, cutoff, verdict.p, /*sync=*/false);
   rccl_all_to_all(c, verdict.p, rc, back.p, sc);
   DBuf<int64_t> sums(ctx, 8);
@@ -5099,6 +5279,10 @@ template <typename F>
 int guard(dr_ctx* ctx, F&& f) {
   try {
     f();
+    if (ctx && dr_ctx::poison()) {
+      const std::string bad = ctx->check_quarantine();
+      if (!bad.empty()) fail(DR_E_INTERNAL, "DR_POISON: " + bad);
+    }
     if (ctx) ctx->err.clear();
     return DR_OK;
   } catch (const Error& e) {
@@ -5142,6 +5326,12 @@ void dr_ctx_destroy(dr_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   (void)hipStreamSynchronize(ctx->stream2);
   ctx->trim();
+  ctx->host_trim();
+  {  // part files still held by the caller are freed by dr_free on their own
+    std::lock_guard<std::mutex> g(g_pinned_out_mu);
+    for (auto& kv : g_pinned_out)
+      if (kv.second == ctx) kv.second = nullptr;
+  }
   for (uint8_t* p : ctx->bounce) (void)hipHostFree(p);
   for (hipEvent_t e : ctx->bounce_ev) (void)hipEventDestroy(e);
   if (ctx->hpin) (void)hipHostFree(ctx->hpin);
@@ -5757,14 +5947,29 @@ int dr_state_write_checkpoint(dr_state* state, int32_t part, int32_t parts, uint
     HIP_OK(hipSetDevice(state->ctx->device));
     CkPartOut o;
     write_checkpoint_part(*state, part, parts, opts, row_group_rows, o);
-    *len = o.file.size();
-    *bytes = o.file.release();  // malloc'd: the caller frees it with dr_free
+    *len = o.len;
+    *bytes = o.data;  // pinned: the caller frees it with dr_free
     if (rows) *rows = o.rows;
     if (add_rows) *add_rows = o.add_rows;
   });
 }
 
-void dr_free(void* p) { free(p); }
+void dr_free(void* p) {
+  if (!p) return;
+  {
+    std::unique_lock<std::mutex> g(g_pinned_out_mu);
+    auto it = g_pinned_out.find(p);
+    if (it != g_pinned_out.end()) {
+      dr_ctx* ctx = it->second;
+      g_pinned_out.erase(it);
+      g.unlock();
+      if (ctx) ctx->host_release(p);  // back to the context's pool
+      else (void)hipHostFree(p);      // its context is gone
+      return;
+    }
+  }
+  free(p);
+}
 
 int dr_state_set_nonfile_json(dr_state* state, const char* lines, uint64_t len, uint32_t flags) {
   if (!state || (!lines && len)) return DR_E_INVALID_ARG;

@@ -20,6 +20,25 @@
 namespace dr {
 namespace dev {
 
+// LDS index checks of the tape kernels (build_tape, tape_lines, k_apply_commit, k_json_lines<true>):
+// built with -DDR_BOUNDS_CHECK (delta_amd/libdeltareplay_bounds.so, tests/test_gpu_bounds.py) every
+// computed stage / tape index is compared with its array's extent before use; a miss counts in
+// dr_lds_bounds_hits and prints the site (a ds_read out of the workgroup's allocation reads 0 instead
+// of faulting, so an over-read would otherwise only show as a wrong token). Compiled out otherwise.
+#ifdef DR_BOUNDS_CHECK
+__device__ unsigned int dr_lds_bounds_hits;
+#define DR_LDS_CHECK(ok, site, idx, lim)                                                                       \
+  do {                                                                                                       \
+    if (!(ok) && atomicAdd(&dr_lds_bounds_hits, 1u) < 32u)                                                   \
+      printf("LDS-BOUNDS %s: index %llu, extent %llu (block %u thread %u)\n", site, (unsigned long long)(idx), \
+             (unsigned long long)(lim), blockIdx.x, threadIdx.x);                                           \
+  } while (0)
+#else
+#define DR_LDS_CHECK(ok, site, idx, lim) \
+  do {                                   \
+  } while (0)
+#endif
+
 constexpr int JSON_THREADS = 256;
 constexpr int JSON_BYTES_PER_THREAD = 64;
 constexpr int JSON_BYTES_PER_BLOCK = JSON_THREADS * JSON_BYTES_PER_THREAD;
@@ -357,6 +376,11 @@ template <uint32_t TCap, uint32_t NL, uint32_t SW>
 __device__ __forceinline__ bool build_tape(const uint4* stage, uint32_t rb, uint32_t R, uint32_t nlines, uint32_t* tape,
                            uint16_t* nltok, uint8_t* tline, unsigned long long* phase = nullptr) {
   const uint32_t lane = wv::lane_id();
+  // the region and the 48 bytes the token reads reach past it (lds20 from a token's start, the
+  // stage's tail) must lie in the stage: otherwise the wave goes to the General walker, which reads
+  // the line from global memory (a region past the stage would be read as zeros)
+  DR_LDS_CHECK(uint64_t(rb) + R + 48 <= uint64_t(SW) * 16, "build_tape region", uint64_t(rb) + R + 48, SW * 16);
+  if (uint64_t(rb) + R + 48 > uint64_t(SW) * 16) return false;
   const uint32_t a0 = rb & ~15u;
   const uint32_t skew = rb - a0;
   const uint32_t total = skew + R;
@@ -368,6 +392,7 @@ __device__ __forceinline__ bool build_tape(const uint4* stage, uint32_t rb, uint
     const uint32_t wpos = (s << 10) + (lane << 4);
     const int32_t lo = int32_t(wpos) - int32_t(skew);  // region offset of the window's byte 0
     // unconditional (clamped) stage read and masks: a guarded read is a branch
+    DR_LDS_CHECK(wpos >= total || ((a0 + wpos) >> 4) < SW, "build_tape stage", (a0 + wpos) >> 4, SW);
     const uint4 v = stage[min((a0 + wpos) >> 4, SW - 1)];
     const uint32_t keep = wpos < total ? ~0u : 0u;
     const uint32_t w[4] = {v.x & keep, v.y & keep, v.z & keep, v.w & keep};
@@ -449,6 +474,8 @@ __device__ __forceinline__ bool build_tape(const uint4* stage, uint32_t rb, uint
       longstr |= isclose & (blen >= 4096u);
       const uint32_t stok = (uint32_t(op) << 16) | ((blen & 0xFFFu) << 4) | (lb > op ? jl::T_STRING_ESC : jl::T_STRING);
       const uint32_t otok = (pos << 16) | ((st & bit) ? scls : (sc_begin & bit) ? jl::T_SCALAR : T_NL);
+      DR_LDS_CHECK(idx < TCap, "build_tape tape", idx, TCap);
+      DR_LDS_CHECK(nlr < NL || !(nl & bit), "build_tape nltok", nlr, NL);
       tline[idx] = uint8_t(nlr);
       const bool isnl = (nl & bit) != 0;
       nltok[isnl ? nlr : NL] = uint16_t(idx);  // slot NL: a sink for the other tokens
@@ -566,10 +593,12 @@ __device__ __forceinline__ uint8_t scalar_tape(const uint32_t w0[5], uint32_t L,
        : (isint && fits) ? jl::SC_INT : jl::SC_BAD;
 }
 
+// sp: the region's first byte in the stage, sp_ext: the stage bytes from sp (the checks' extent)
 template <uint32_t TCap, uint32_t NL>
 __device__ __forceinline__ void tape_lines(const JsonParseArgs& a, uint64_t line0, uint32_t nlines, const uint8_t* sp,
-                                           uint64_t gb, const uint32_t* tape, const uint16_t* nltok, const uint8_t* tline,
-                                           TapeAgg<NL>& g) {
+                                           uint32_t sp_ext, uint64_t gb, const uint32_t* tape, const uint16_t* nltok,
+                                           const uint8_t* tline, TapeAgg<NL>& g) {
+  (void)sp_ext;
   const uint32_t lane = wv::lane_id();
   const uint64_t tw0 = a.phase ? __builtin_amdgcn_s_memtime() : 0;
   if (lane < NL) {
@@ -598,6 +627,9 @@ __device__ __forceinline__ void tape_lines(const JsonParseArgs& a, uint64_t line
     ptail2 = wv::last_uniform(ptok);
     // the token's bytes (a scalar's) and its key's (the string two tokens back), one load each
     uint32_t sw[5], kw[5];
+    DR_LDS_CHECK(!in || (tok >> 16) + 24u <= sp_ext, "tape_lines token bytes", (tok >> 16) + 24u, sp_ext);
+    DR_LDS_CHECK(!in || (pptok >> 16) + 25u <= sp_ext, "tape_lines key bytes", (pptok >> 16) + 25u, sp_ext);
+    DR_LDS_CHECK(!in || line < NL, "tape_lines line", line, NL);
     lds20(sp + (tok >> 16), sw);
     lds20(sp + (pptok >> 16) + 1u, kw);
     const uint32_t cls = tok & 0xFu;
@@ -674,6 +706,7 @@ __device__ __forceinline__ void tape_lines(const JsonParseArgs& a, uint64_t line
   const uint64_t line = line0 + lane;
   const uint32_t te = nltok[lane];
   const uint32_t ts = lane ? uint32_t(nltok[lane - 1]) + 1u : 0u;
+  DR_LDS_CHECK(te < TCap && ts <= TCap, "tape_lines line tokens", te, TCap);
   const uint32_t ls = lane ? (tape[ts - 1] >> 16) + 1u : 0u;  // line start (region offset)
   const uint32_t n = (tape[te] >> 16) - ls;
   if (g.defer[lane]) {
@@ -694,6 +727,7 @@ __device__ __forceinline__ void tape_lines(const JsonParseArgs& a, uint64_t line
     o.flags = jl::F_PATH_NULL;
     const int32_t tp = fl[jl::FK_PATH], tz = fl[jl::FK_SIZE], td = fl[jl::FK_DELTS];
     if (tp >= 0 && (tp >> 1) > m && (tp & 1)) {
+      DR_LDS_CHECK(uint32_t(tp >> 1) < TCap, "tape_lines path token", tp >> 1, TCap);
       const uint32_t t = tape[tp >> 1];
       o.path_off = (t >> 16) + 1u - ls;
       o.path_len = (t >> 4) & 0xFFFu;
@@ -702,7 +736,11 @@ __device__ __forceinline__ void tape_lines(const JsonParseArgs& a, uint64_t line
     // size / deletionTimestamp: both tokens' words in one pass (an absent field reads token 0)
     const bool hz = tz >= 0 && (tz >> 1) > m && (tz & 1), hd = td >= 0 && (td >> 1) > m && (td & 1);
     const uint32_t iz = hz ? uint32_t(tz >> 1) : 0u, id = hd ? uint32_t(td >> 1) : 0u;
-    const uint32_t az = tape[iz], bz = tape[iz + 1], ad = tape[id], bd = tape[id + 1];
+    // a scalar is always followed by its ',' or '}' token, so iz + 1 < ntok <= TCap; clamped anyway
+    DR_LDS_CHECK(iz + 1 < TCap && id + 1 < TCap, "tape_lines scalar tokens", max(iz, id) + 1, TCap);
+    const uint32_t az = tape[iz], bz = tape[min(iz + 1, TCap - 1)], ad = tape[id], bd = tape[min(id + 1, TCap - 1)];
+    DR_LDS_CHECK((az >> 16) + 24u <= sp_ext && (ad >> 16) + 24u <= sp_ext, "tape_lines scalar bytes",
+                 max(az >> 16, ad >> 16) + 24u, sp_ext);
     uint32_t wz[5], wd[5];
     lds20(sp + (az >> 16), wz);
     lds20(sp + (ad >> 16), wd);
@@ -747,7 +785,8 @@ __global__ void __launch_bounds__(JL_T, DR_JL_WAVES) k_json_lines(JsonParseArgs 
       const uint32_t len = uint32_t(a.buf_len);
       const uint4* src = reinterpret_cast<const uint4*>(a.buf);
       const uint32_t nq = ((len + 15u) >> 4) + 3u;
-      for (uint32_t k = lane; k < nq; k += JL_T) stage[k] = src[k];
+      DR_LDS_CHECK(nq <= JL_STAGE_BYTES / 16, "k_json_lines fused stage", nq, JL_STAGE_BYTES / 16);
+      for (uint32_t k = lane; k < min(nq, JL_STAGE_BYTES / 16); k += JL_T) stage[k] = src[k];
       __threadfence();  // the cleared counters reach L2 before any atomic on them
       __syncthreads();
       phase(0);
@@ -756,12 +795,14 @@ __global__ void __launch_bounds__(JL_T, DR_JL_WAVES) k_json_lines(JsonParseArgs 
       phase(1);
       __syncthreads();
       if (taped) {
+        DR_LDS_CHECK(lane >= nw || lane < JL_T, "k_json_lines nltok", lane, JL_T);
         if (lane < nw) a.nl_out[lane] = tape[nltok[lane]] >> 16;  // the newline positions, from the tape
         if (lane == 0) {
           a.off2[0] = 0;
           a.off2[1] = nw;
         }
-        tape_lines<TAPE_CAP, JL_T>(a, 0, nw, reinterpret_cast<const uint8_t*>(stage), 0, tape, nltok, tline, agg);
+        tape_lines<TAPE_CAP, JL_T>(a, 0, nw, reinterpret_cast<const uint8_t*>(stage), JL_STAGE_BYTES, 0, tape, nltok, tline,
+                                   agg);
         phase(2);
         if (a.phase && lane == 0) atomicAdd(&a.phase[4], 1ull);
         return;
@@ -770,6 +811,8 @@ __global__ void __launch_bounds__(JL_T, DR_JL_WAVES) k_json_lines(JsonParseArgs 
       uint32_t base = 0;
       for (uint32_t s0 = 0; s0 < len; s0 += 16u * JL_T) {
         const uint32_t wpos = s0 + 16u * lane;
+        DR_LDS_CHECK(wpos >= len || (wpos >> 4) < JL_STAGE_BYTES / 16, "k_json_lines stage", wpos >> 4,
+                     JL_STAGE_BYTES / 16);
         const uint4 v = stage[min(wpos >> 4, JL_STAGE_BYTES / 16 - 1)];
         const uint32_t w[4] = {v.x, v.y, v.z, v.w};
         uint32_t m = 0;
@@ -813,7 +856,8 @@ __global__ void __launch_bounds__(JL_T, DR_JL_WAVES) k_json_lines(JsonParseArgs 
       phase(1);
       if (taped) {
         __syncthreads();
-        tape_lines<TAPE_CAP, JL_T>(a, first, nw, reinterpret_cast<const uint8_t*>(stage) + (rb - r0), rb, tape, nltok, tline, agg);
+        tape_lines<TAPE_CAP, JL_T>(a, first, nw, reinterpret_cast<const uint8_t*>(stage) + (rb - r0),
+                                   JL_STAGE_BYTES - uint32_t(rb - r0), rb, tape, nltok, tline, agg);
         phase(2);
         if (a.phase && lane == 0) atomicAdd(&a.phase[4], 1ull);
         return;
@@ -971,6 +1015,7 @@ __global__ void __launch_bounds__(AC_WAVES * 64) k_apply_commit(JsonParseArgs a,
   if (t < p.nctr) p.ctr[t] = t == p.ctr_at ? p.ctr_val : 0ull;  // the index counters (apply_small_body)
   {
     const uint4* src = reinterpret_cast<const uint4*>(a.buf);
+    DR_LDS_CHECK(((len + 15u) >> 4) + 3u <= AC_SW, "k_apply_commit stage load", ((len + 15u) >> 4) + 3u, AC_SW);
     const uint32_t nq = min(((len + 15u) >> 4) + 3u, AC_SW);
     for (uint32_t k = t; k < nq; k += AC_WAVES * 64) stage[k] = src[k];
   }
@@ -981,6 +1026,7 @@ __global__ void __launch_bounds__(AC_WAVES * 64) k_apply_commit(JsonParseArgs a,
     uint32_t base = 0;
     for (uint32_t s0 = 0; s0 < len; s0 += 16u * 64u) {
       const uint32_t wpos = s0 + 16u * lane;
+      DR_LDS_CHECK(wpos >= len || (wpos >> 4) < AC_SW, "k_apply_commit stage", wpos >> 4, AC_SW);
       const uint4 v = stage[min(wpos >> 4, AC_SW - 1)];
       const uint32_t ww[4] = {v.x, v.y, v.z, v.w};
       uint32_t m = 0;
@@ -1003,6 +1049,8 @@ __global__ void __launch_bounds__(AC_WAVES * 64) k_apply_commit(JsonParseArgs a,
       a.off2[0] = 0;
       a.off2[1] = base;
     }
+    // nlpos[0 .. nlines) must all be written: the host's line count is the staged newline count
+    DR_LDS_CHECK(base >= nlines && nlines <= JSON_FUSE_MAX_LINES, "k_apply_commit newlines", base, nlines);
   }
   __syncthreads();
   phase(1);
@@ -1015,8 +1063,8 @@ __global__ void __launch_bounds__(AC_WAVES * 64) k_apply_commit(JsonParseArgs a,
     const bool taped = build_tape<AC_TCAP, AC_LINES, AC_SW>(stage, rb, R, nw, tape[w], nltok[w], tline[w]);
     wave_sync();
     if (taped) {
-      tape_lines<AC_TCAP, AC_LINES>(a, l0, nw, reinterpret_cast<const uint8_t*>(stage) + rb, rb, tape[w], nltok[w],
-                                    tline[w], agg[w]);
+      tape_lines<AC_TCAP, AC_LINES>(a, l0, nw, reinterpret_cast<const uint8_t*>(stage) + rb, AC_SW * 16 - rb, rb,
+                                    tape[w], nltok[w], tline[w], agg[w]);
     } else if (lane < nw) {  // off the tape: the General walker (apply_small_body) decides these lines
       const unsigned long long k = atomicAdd(a.hard_count, 1ull);
       a.hard_idx[k] = l0 + lane;

@@ -21,10 +21,23 @@ import os
 import re
 import threading
 import time
+import weakref
 from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
 from . import _native as N
 
+
+
+def _owned_bytes(lib, buf, n: int) -> memoryview:
+    """A read-only bytes view of a library-allocated block (a checkpoint part: pinned host memory)
+    without copying it; the block goes back to the library (dr_free) when the last view of it is
+    dropped."""
+    if not n:
+        lib.dr_free(C.cast(buf, C.c_void_p))
+        return memoryview(b"")
+    arr = (C.c_uint8 * n).from_address(C.cast(buf, C.c_void_p).value)
+    weakref.finalize(arr, lib.dr_free, C.c_void_p(C.cast(buf, C.c_void_p).value))
+    return memoryview(arr).cast("B").toreadonly()
 
 class DeltaError(Exception):
     """Carries the reference's exception class name (`kind`) and the C status."""
@@ -499,7 +512,8 @@ class State:
                               row_group_rows: int = 0, snappy: bool = True, with_adds: bool = False):
         """dr_state_write_checkpoint: part `part` (1-based) of `parts` as Parquet bytes, the file-action
         columns encoded (and SNAPPY-compressed) on the GPU; returns (bytes, rows), or (bytes, rows,
-        add rows) with `with_adds`."""
+        add rows) with `with_adds`. The bytes are a read-only memoryview of the library's pinned block
+        (no copy; released when the view is dropped)."""
         buf = C.POINTER(C.c_uint8)()
         n = C.c_uint64()
         rows = C.c_int64()
@@ -509,8 +523,7 @@ class State:
             self.eng.check(self.eng.lib.dr_state_write_checkpoint(self.h, int(part), int(parts), opts, int(row_group_rows),
                                                                   C.byref(buf), C.byref(n), C.byref(rows),
                                                                   C.byref(adds)))
-        data = C.string_at(buf, n.value)
-        self.eng.lib.dr_free(C.cast(buf, C.c_void_p))
+        data = _owned_bytes(self.eng.lib, buf, n.value)
         return (data, rows.value, adds.value) if with_adds else (data, rows.value)
 
     def _take(self, ptr, n) -> List[int]:

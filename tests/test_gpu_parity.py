@@ -339,9 +339,19 @@ def _same_counts(a, b, tag):
 
 
 def _same_state(a, b, tag):
-    _same_counts(a, b, tag)
-    assert sorted(map(_canon, a.export(0))) == sorted(map(_canon, b.export(0))), tag
-    assert sorted(map(_canon, a.export(1))) == sorted(map(_canon, b.export(1))), tag
+    sides = []
+    for which in (0, 1):
+        ea, eb = a.export(which), b.export(which)
+        ra, rb = sorted(map(_canon, ea)), sorted(map(_canon, eb))
+        sa, sb = set(ra), set(rb)
+        sides.append((ra, rb, sorted(sa - sb)[:8], sorted(sb - sa)[:8], sum(r.get("size") or 0 for r in ea)))
+    try:
+        _same_counts(a, b, tag)
+    except AssertionError as e:  # name the rows that differ (and the live rows' size sum), not only the counter
+        raise AssertionError("%s; only in a: %s; only in b: %s; live size sum %d" %
+                             (e, [s[2] for s in sides], [s[3] for s in sides], sides[0][4]))
+    for ra, rb, oa, ob, _ in sides:
+        assert ra == rb, (tag, oa, ob)
     assert a.nonfile == b.nonfile, tag
 
 
@@ -657,6 +667,13 @@ def test_incremental_apply_random_commits(engine, tmp_path, compact):
             tail.release()
             v += k
             states.append(nxt)
+            live = nxt.export(0)  # every apply: the counters move with the rows
+            got, want = (nxt.counts["num_files"], nxt.counts["size_in_bytes"]), (len(live), sum(r["size"] or 0 for r in live))
+            if got != want:
+                print("apply to v%d (%d commits): counters %s, rows %s\nbase %s\nnext %s\nbase rows %s" %
+                      (v, k, got, want, states[-2].counts, nxt.counts,
+                       sorted((r["path"], r["size"]) for r in states[-2].export(0))))
+            assert got == want, (v, k)
             if v % 5 == 0 or v > 36:
                 full = _gpu_replay(engine, str(lp), cut(v), version=v)
                 try:

@@ -240,7 +240,7 @@ def measure_stream(eng, table, exp, args):
             torch.cuda.synchronize()
             if timing and k:
                 for kn, ms in eng.last_timings().items():
-                    if kn in ("start", "end"):
+                    if kn in ("start", "end") or kn.startswith("stat."):
                         continue
                     kern[kn.split("#")[0]] = kern.get(kn.split("#")[0], 0.0) + ms
             tail.release()
@@ -560,12 +560,15 @@ def main():
     plan = staged.plan()  # this rank's slice (roofline accounting is per rank 0's kernels)
     # per-kernel table: an untimed pass with an event pair around every launch (one stream, so the
     # kernels add up to the step); the timed steps then carry events around the longest kernel only
-    kern_ms, kern_n = {}, {}
+    kern_ms, kern_n, stats = {}, {}, {}
     prof_steps = max(1, args.profile_steps)
     eng.set_timing(True)
     for _ in range(prof_steps):
         step()
         for k, v in eng.last_timings().items():
+            if k.startswith("stat."):  # counters of the timed replay (k_bucket_verify's pairs, path bytes)
+                stats[k[5:]] = v
+                continue
             base = k.split("#")[0]
             kern_ms[base] = kern_ms.get(base, 0.0) + v
             kern_n[base] = kern_n.get(base, 0) + 1
@@ -649,6 +652,11 @@ def main():
         "sort_reduce": dict(pipeline(SORT_REDUCE, 69 * local_counts["num_actions"]), target_frac=0.5)
         if local_counts else None,
     }
+    if "verify_pairs" in stats and "k_bucket_verify" in kernels:
+        # the verifier on its own path bytes: per (loser, winner) pair its 16-byte reference pair and
+        # both paths' bytes (the 69 B/action budget above does not model it)
+        pipelines["verify"] = dict(pipeline(["k_bucket_verify"], int(16 * stats["verify_pairs"] + stats["verify_path_bytes"])),
+                                   pairs=int(stats["verify_pairs"]), path_bytes=int(stats["verify_path_bytes"]))
     if dist:
         # every rank's roofline and pipelines to rank 0: the line reports the slowest rank's (the step
         # waits for it) and lists each rank's

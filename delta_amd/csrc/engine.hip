@@ -434,9 +434,14 @@ struct dr_ctx {
       put_event(k.b);
     }
     kmarks.clear();
+    for (auto& kv : stats) timings.emplace_back(kv.first, float(kv.second));
+    stats.clear();
   }
+  // counters of the call that are reported with its timings (stat.* entries: counts, not ms)
+  std::vector<std::pair<std::string, double>> stats;
   void drop_timings() {
     set_launch_hook(nullptr, nullptr);
+    stats.clear();
     for (auto& m : marks) put_event(m.ev);
     marks.clear();
     for (auto& k : kmarks) {
@@ -1215,15 +1220,22 @@ static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_
         const uint64_t* x = &st[q * 16];
         if (!x[0] || !x[15]) continue;
         ++nb2;
+        // slots 11-13: active 4-byte groups at the start of jumping rounds 1-3 (of 16384), 14: the
+        // block's most rounds of a thread -- counters, not clocks
+        for (int k = 11; k <= 14; ++k) acc[k] += double(x[k]);
         for (int k = 1, prev = 0; k < 16; ++k)
-          if (x[k]) {
+          if (x[k] && (k < 11 || k > 14)) {
             acc[k] += double(x[k] - x[prev]);
             prev = k;
           }
       }
       std::fprintf(stderr, "exec phases (clocks/block, %zu blocks):", nb2);
       for (int k = 1; k < 16; ++k)
-        if (acc[k] != 0) std::fprintf(stderr, " [%d] %.0f", k, nb2 ? acc[k] / double(nb2) : 0.0);
+        if (acc[k] != 0) {
+          if (k >= 11 && k <= 13) std::fprintf(stderr, " active%d %.0f", k - 10, nb2 ? acc[k] / double(nb2) : 0.0);
+          else if (k == 14) std::fprintf(stderr, " rounds %.2f", nb2 ? acc[k] / double(nb2) : 0.0);
+          else std::fprintf(stderr, " [%d] %.0f", k, nb2 ? acc[k] / double(nb2) : 0.0);
+        }
       std::fprintf(stderr, "\n");
       const unsigned long long nreg = d2h_one(P.s_region_count.p, stream);
       std::vector<uint32_t> pb = d2h(P.s_pages_bad.p, P.snap_pages.size(), stream);
@@ -1976,6 +1988,7 @@ static void parse_actions(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
 // arrays, queued without a host round trip; reduce_finish reads the counters back.
 struct ReducePending {
   DBuf<unsigned long long> totals;
+  DBuf<unsigned long long> vstats;  // timed replays: the verifier's {pairs, path bytes}
   size_t pin_at = 0;
 };
 
@@ -2010,7 +2023,15 @@ static ReducePending reduce_launch(dr_ctx* ctx, dr_state* st, int64_t cutoff, ui
   DBuf<unsigned long long> totals(ctx, 8), bstats(ctx, uint64_t(nb) * 5);
   totals.zero(stream);
   ReduceArgs ra{rec.p, boff.p, nb, bits, st->size.p, st->path_ptr.p, st->path_len.p, olive.p, otomb.p, opair.p, pref.p,
-                lcount.p, tcount.p, pcount.p, totals.p, rlist.p, xlist.p, bstats.p};
+                lcount.p, tcount.p, pcount.p, totals.p, rlist.p, xlist.p, bstats.p, nullptr};
+  // a timed replay (per-kernel mode) also counts the verifier's pairs and path bytes: its own byte
+  // model beside the 69 B/action budget (bench.py "verify")
+  DBuf<unsigned long long> vstats;
+  if (ctx->timing && ctx->timing_only.empty()) {
+    vstats = DBuf<unsigned long long>(ctx, 2);
+    vstats.zero(stream);
+    ra.vstats = vstats.p;
+  }
   std::unique_ptr<StageRange> reduce_range(new StageRange("reduce", stream));
   auto upload_list = [&](const std::vector<uint32_t>& v) {
     DBuf<uint32_t> d(ctx, v.size());
@@ -2056,6 +2077,7 @@ static ReducePending reduce_launch(dr_ctx* ctx, dr_state* st, int64_t cutoff, ui
   HIP_OK(hipMemcpyAsync(totals.p + 7, boff.p + nb, 8, hipMemcpyDeviceToDevice, stream));
   ReducePending rp;
   rp.totals = std::move(totals);
+  rp.vstats = std::move(vstats);
   return rp;
 }
 
@@ -2067,6 +2089,11 @@ static size_t reduce_queue_readback(dr_ctx* ctx, ReducePending& rp, size_t at) {
 
 // After the stream has drained: the survivor counts and computedState counters.
 static void reduce_finish(dr_ctx* ctx, dr_state* st, const ReducePending& rp) {
+  if (rp.vstats.p) {  // (timed replays) reported with the kernel times: "stat.verify_pairs", "stat.verify_path_bytes"
+    const std::vector<unsigned long long> v = d2h(rp.vstats.p, 2, ctx->stream);
+    ctx->stats.emplace_back("stat.verify_pairs", double(v[0]));
+    ctx->stats.emplace_back("stat.verify_path_bytes", double(v[1]));
+  }
   const uint64_t* tot = ctx->pinned() + rp.pin_at;
   const uint64_t N = st->n_actions;
   const uint64_t n_file_actions = tot[7];

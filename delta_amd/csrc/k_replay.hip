@@ -429,6 +429,7 @@ __global__ void __launch_bounds__(VER_T) k_bucket_verify(ReduceArgs a) {
   const uint32_t j = threadIdx.x & (VER_G - 1);
   const uint4 z = make_uint4(0, 0, 0, 0);
   bool bad = false;
+  uint32_t vbytes = 0;  // (vstats) path bytes this lane group compared
   for (uint32_t k0 = 0; k0 < n; k0 += VER_T / VER_G) {
     const uint32_t k = k0 + threadIdx.x / VER_G;
     uint32_t diff = 0;
@@ -455,6 +456,7 @@ __global__ void __launch_bounds__(VER_T) k_bucket_verify(ReduceArgs a) {
       if (nul || pn != qn) {
         diff = 1;
       } else {
+        if (j == 0) vbytes += 2 * pn;
         const uint4* pa = reinterpret_cast<const uint4*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(15));
         const uint4* qa = reinterpret_cast<const uint4*>(reinterpret_cast<uintptr_t>(q) & ~uintptr_t(15));
         const uint32_t po = uint32_t(reinterpret_cast<uintptr_t>(p) & 15);
@@ -479,6 +481,12 @@ __global__ void __launch_bounds__(VER_T) k_bucket_verify(ReduceArgs a) {
     }
   }
   if (__syncthreads_or(bad) && threadIdx.x == 0) a.exact_list[atomicAdd(&a.totals[4], 1ull)] = b;
+  if (a.vstats) {  // block-uniform
+    unsigned long long v = vbytes;
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(&a.vstats[1], v);
+    if (threadIdx.x == 0) atomicAdd(&a.vstats[0], (unsigned long long)n);
+  }
 }
 
 // Per-slot loser counts packed two to a word (slot s: word s >> 1, bits 16 (s & 1)): members - 1 of

@@ -990,7 +990,12 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     }
     __syncthreads();
     stamp(6);
+    uint32_t rounds = 0;
     while (act) {
+      ++rounds;
+      if (a.stamps && rounds <= 3)  // (DR_SNAP_DEBUG) active groups at the start of rounds 1..3
+        atomicAdd(reinterpret_cast<unsigned long long*>(&a.stamps[uint64_t(b) * 16 + 10 + rounds]),
+                  (unsigned long long)__popc(act));
 #pragma unroll
       for (uint32_t j = 0; j < 16; ++j) {
         if (act & (1u << j)) {
@@ -1007,8 +1012,10 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
         }
       }
     }
+    if (a.stamps) atomicMax(reinterpret_cast<unsigned long long*>(&a.stamps[uint64_t(b) * 16 + 14]), (unsigned long long)rounds);
   }
   __syncthreads();
+  stamp(7);
   // 3. the LDS becomes the block's bytes (lower half) and its compressed input (upper half: the
   //    block's whole range, headers included, so each thread walks its elements again from it)
   uint8_t* bytes = reinterpret_cast<uint8_t*>(src);
@@ -1025,7 +1032,7 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
       if (uint32_t(t) + k * EXEC_T < nv_all) u4[uint32_t(t) + k * EXEC_T] = v[k];
   }
   __syncthreads();
-  stamp(7);
+  stamp(8);
   // a literal of this block (rel, len, page-relative input position ip): LDS -> LDS copy, or queued
   // for a whole wave when long
   auto copy_lit = [&](uint32_t rel, uint32_t len, uint64_t ip) {
@@ -1094,7 +1101,7 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     }
   }
   __syncthreads();
-  stamp(8);
+  stamp(9);
   const uint32_t nlong = min(s_nlong, EXEC_LONG);
   for (uint32_t L = uint32_t(t) >> 6; L < nlong; L += EXEC_T / 64) {  // long literals: one wave each
     const uint64_t wl = s_long[L];
@@ -1110,7 +1117,7 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     }
   }
   __syncthreads();
-  stamp(9);
+  stamp(10);
   // 4. gather and store: the thread's 4-byte groups are the ones it resolved (roots still in
   //    registers); a wave's 64 groups are 256 contiguous bytes, so literal bytes (their own roots)
   //    and runs of one copy read consecutive LDS banks, and the dword stores coalesce

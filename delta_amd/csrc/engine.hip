@@ -2028,7 +2028,7 @@ static ReducePending reduce_launch(dr_ctx* ctx, dr_state* st, int64_t cutoff, ui
   // model beside the 69 B/action budget (bench.py "verify")
   DBuf<unsigned long long> vstats;
   if (ctx->timing && ctx->timing_only.empty()) {
-    vstats = DBuf<unsigned long long>(ctx, 2);
+    vstats = DBuf<unsigned long long>(ctx, 2 * uint64_t(nb));
     vstats.zero(stream);
     ra.vstats = vstats.p;
   }
@@ -2090,9 +2090,14 @@ static size_t reduce_queue_readback(dr_ctx* ctx, ReducePending& rp, size_t at) {
 // After the stream has drained: the survivor counts and computedState counters.
 static void reduce_finish(dr_ctx* ctx, dr_state* st, const ReducePending& rp) {
   if (rp.vstats.p) {  // (timed replays) reported with the kernel times: "stat.verify_pairs", "stat.verify_path_bytes"
-    const std::vector<unsigned long long> v = d2h(rp.vstats.p, 2, ctx->stream);
-    ctx->stats.emplace_back("stat.verify_pairs", double(v[0]));
-    ctx->stats.emplace_back("stat.verify_path_bytes", double(v[1]));
+    const std::vector<unsigned long long> v = d2h(rp.vstats.p, rp.vstats.n, ctx->stream);
+    double pairs = 0, bytes = 0;
+    for (size_t k = 0; k + 1 < v.size(); k += 2) {
+      pairs += double(v[k]);
+      bytes += double(v[k + 1]);
+    }
+    ctx->stats.emplace_back("stat.verify_pairs", pairs);
+    ctx->stats.emplace_back("stat.verify_path_bytes", bytes);
   }
   const uint64_t* tot = ctx->pinned() + rp.pin_at;
   const uint64_t N = st->n_actions;

@@ -481,11 +481,18 @@ __global__ void __launch_bounds__(VER_T) k_bucket_verify(ReduceArgs a) {
     }
   }
   if (__syncthreads_or(bad) && threadIdx.x == 0) a.exact_list[atomicAdd(&a.totals[4], 1ull)] = b;
-  if (a.vstats) {  // block-uniform
+  if (a.vstats) {  // block-uniform: the bucket's {pairs, bytes} in its own slots (no contended atomics)
+    __shared__ unsigned long long vsum;
+    if (threadIdx.x == 0) vsum = 0;
+    __syncthreads();
     unsigned long long v = vbytes;
     for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
-    if ((threadIdx.x & 63) == 0 && v) atomicAdd(&a.vstats[1], v);
-    if (threadIdx.x == 0) atomicAdd(&a.vstats[0], (unsigned long long)n);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(&vsum, v);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      a.vstats[2 * uint64_t(b)] = n;
+      a.vstats[2 * uint64_t(b) + 1] = vsum;
+    }
   }
 }
 

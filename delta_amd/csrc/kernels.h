@@ -282,7 +282,7 @@ struct ReduceArgs {
   uint32_t* redo_list;         // buckets whose LDS table overflowed
   uint32_t* exact_list;        // buckets with a 64-bit path-hash collision (or an unpackable path)
   unsigned long long* bstats;  // [nbuckets * 5] per-bucket {live, tomb, size, live sum, tomb sum}
-  unsigned long long* vstats;  // nullable (timed replays): k_bucket_verify's {pairs, path bytes compared}
+  unsigned long long* vstats;  // nullable (timed replays): [nbuckets * 2] k_bucket_verify's {pairs, path bytes compared}
 };
 // LDS last-writer-wins per bucket on the 64-bit key; losers paired with winners (grouped by winner)
 void launch_bucket_reduce(const ReduceArgs& a, hipStream_t st);

@@ -3501,8 +3501,9 @@ static void build_pv_columns(dr_state& st, const std::vector<std::pair<std::stri
 // tombstones, every record with dataChange=false -- as one Parquet part. The file-action columns
 // are encoded on the device from the device export (k_enc_*: levels + PLAIN values, bit-packed
 // levels); the handful of protocol / metaData / txn rows and the footer are written on the host.
-// Pages are uncompressed (codec UNCOMPRESSED; any Parquet reader, the reference's included, reads
-// them). The schema is the reference's checkpoint schema, nullable throughout.
+// The device columns' pages are SNAPPY-compressed on the device with DR_CKPT_SNAPPY (Spark's default
+// codec; k_snap_compress), else written UNCOMPRESSED; the host-encoded head-row pages are
+// uncompressed. The schema is the reference's checkpoint schema, nullable throughout.
 // ---------------------------------------------------------------------------------------------------
 struct ThriftW {  // Thrift compact protocol
   std::vector<uint8_t> b;

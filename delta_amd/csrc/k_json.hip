@@ -985,12 +985,12 @@ __global__ void __launch_bounds__(IX_T) k_apply_small(JsonParseArgs a, CanonArgs
   apply_small_body(a, c, p, x, false);
 }
 
-// A streamed commit's whole apply in one workgroup of four waves (launch_apply_commit): the
+// A streamed commit's whole apply in one workgroup of AC_WAVES waves (launch_apply_commit): the
 // commit's bytes staged in LDS once, its newline index (wave 0), then each wave builds the token
-// tape of its quarter of the lines and walks it (the small-segment walker of k_json_lines<true>, on
-// wave-private tapes), and after a barrier the rest of the apply (apply_small_body). Four waves
-// split the walk that one wave did serially, and the parse, post-parse, append and index passes are
-// one dispatch.
+// tape of its share of the lines and walks it (the small-segment walker of k_json_lines<true>, on
+// wave-private tapes), and after a barrier the rest of the apply (apply_small_body). The waves split
+// the walk that one wave did serially, and the parse, post-parse, append and index passes are one
+// dispatch.
 constexpr uint32_t AC_WAVES = 8;  // the walk's waves (the apply after it uses the first IX_T threads)
 constexpr uint32_t AC_LINES = (JSON_FUSE_MAX_LINES + AC_WAVES - 1) / AC_WAVES;  // lines per wave
 constexpr uint32_t AC_TCAP = 1024;                                            // tape tokens per wave

@@ -1599,6 +1599,8 @@ static std::shared_ptr<StagedData> stage_files(dr_ctx* ctx, const dr_file* files
 static int bucket_bits_for(uint64_t n) {
   int bits = 0;
   while ((n >> bits) > 2048 && bits < int(part_max_bucket_bits())) ++bits;
+  // test hook: fewer, larger buckets (the reducer's sub-pass paths on a small table)
+  if (const char* e = std::getenv("DR_BUCKET_BITS")) bits = std::max(0, std::min(bits, std::atoi(e)));
   return bits;
 }
 

@@ -196,6 +196,29 @@ def test_fallback_reducers_agree(engine, tmp_path, reducer):
         b.release()
 
 
+@pytest.mark.parametrize("bits", [3, 5])
+def test_reducer_subpasses_agree(engine, tmp_path, monkeypatch, bits):
+    """K4's sub-pass path (buckets over 3/4 of its 4096-slot LDS table, which config 4's 12K-record
+    buckets take; forced here with 8 or 32 buckets of ~20K / ~5K records) gives the one-pass
+    reducer's state."""
+    from delta_amd.testing import synth as S
+    exp = S.build_config(3, str(tmp_path), scale=0.01)
+    lp = os.path.join(str(tmp_path), "_delta_log")
+    staged = engine.stage_log(lp)
+    try:
+        a = staged.replay(exp.min_file_retention_timestamp)
+        monkeypatch.setenv("DR_BUCKET_BITS", str(bits))
+        b = staged.replay(exp.min_file_retention_timestamp)
+    finally:
+        staged.release()
+    try:
+        _same_state(a, b, bits)
+        assert b.counts["num_files"] == exp.num_files and b.counts["num_removes"] == exp.num_removes
+    finally:
+        a.release()
+        b.release()
+
+
 @pytest.mark.parametrize("page_size,compression,page_version,rg,dictionary", [
     (4096, "snappy", "1.0", 1 << 20, True),
     (64 << 10, "snappy", "1.0", 7000, True),

@@ -36,7 +36,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-SORT_REDUCE = ("k_bucket_hist", "k_bucket_offsets", "k_bucket_scatter", "k_bucket_reduce", "k_bucket_verify",
+SORT_REDUCE = ("k_bucket_hist", "k_bucket_offsets", "k_bucket_scatter", "k_bucket_split", "k_bucket_reduce", "k_bucket_verify",
                "k_bucket_reduce64", "k_bucket_exact", "k_sum_stats", "k_survivor_scan", "k_compact2")
 SNAPPY = ("k_snap_spec", "k_snap_assume", "k_snap_entries", "k_snap_regions", "k_snap_resolve", "k_snap_count",
           "k_snap_scan", "k_snap_exec", "k_snap_serial")

@@ -2018,19 +2018,41 @@ static ReducePending reduce_launch(dr_ctx* ctx, dr_state* st, int64_t cutoff, ui
     launch_bucket_offsets(toff.p, nb, nt, boff.p, stream);
     launch_bucket_scatter(pa, stream);
   }
+  // ---- K3 refinement (large replays): buckets of more than 2048 records on average are split by the
+  // next key bits, so that K4 reduces each in one pass (k_bucket_split; DR_SPLIT=0 turns it off) ----
+  int sbits = 0;
+  {
+    const char* e = std::getenv("DR_SPLIT");
+    if (!e || std::atoi(e) != 0)
+      while ((N >> (bits + sbits)) > 2048 && sbits < 6) ++sbits;
+  }
+  DBuf<PartRec> rec2;
+  DBuf<uint64_t> boff2;
+  const PartRec* krec = rec.p;
+  const uint64_t* kboff = boff.p;
+  if (sbits) {
+    DR_STAGE("hash.split", stream);
+    rec2 = DBuf<PartRec>(ctx, N);
+    boff2 = DBuf<uint64_t>(ctx, (uint64_t(nb) << sbits) + 1);
+    launch_bucket_split(SplitArgs{rec.p, boff.p, bits, sbits, rec2.p, boff2.p}, nb, stream);
+    krec = rec2.p;
+    kboff = boff2.p;
+  }
+  const uint32_t knb = nb << sbits;  // K4's buckets
+  const int kbits = bits + sbits;
   // ---- K4: per-bucket last-writer-wins ----
-  DBuf<uint32_t> olive(ctx, N), otomb(ctx, N), lcount(ctx, nb), tcount(ctx, nb), pcount(ctx, nb), rlist(ctx, nb),
-      xlist(ctx, nb);
+  DBuf<uint32_t> olive(ctx, N), otomb(ctx, N), lcount(ctx, knb), tcount(ctx, knb), pcount(ctx, knb), rlist(ctx, knb),
+      xlist(ctx, knb);
   DBuf<uint2> opair(ctx, N);
-  DBuf<unsigned long long> totals(ctx, 8), bstats(ctx, uint64_t(nb) * 5);
+  DBuf<unsigned long long> totals(ctx, 8), bstats(ctx, uint64_t(knb) * 5);
   totals.zero(stream);
-  ReduceArgs ra{rec.p, boff.p, nb, bits, st->size.p, st->path_ptr.p, st->path_len.p, olive.p, otomb.p, opair.p, pref.p,
+  ReduceArgs ra{krec, kboff, knb, kbits, st->size.p, st->path_ptr.p, st->path_len.p, olive.p, otomb.p, opair.p, pref.p,
                 lcount.p, tcount.p, pcount.p, totals.p, rlist.p, xlist.p, bstats.p, nullptr};
   // a timed replay (per-kernel mode) also counts the verifier's pairs and path bytes: its own byte
   // model beside the 69 B/action budget (bench.py "verify")
   DBuf<unsigned long long> vstats;
   if (ctx->timing && ctx->timing_only.empty()) {
-    vstats = DBuf<unsigned long long>(ctx, 2 * uint64_t(nb));
+    vstats = DBuf<unsigned long long>(ctx, 2 * uint64_t(knb));
     vstats.zero(stream);
     ra.vstats = vstats.p;
   }
@@ -2041,27 +2063,27 @@ static ReducePending reduce_launch(dr_ctx* ctx, dr_state* st, int64_t cutoff, ui
     return d;
   };
   if (flags & (DR_FLAG_EXACT_REDUCE | DR_FLAG_REDUCE64)) {  // test hooks: force the fallback reducers
-    std::vector<uint32_t> all(nb);
-    for (uint32_t b = 0; b < nb; ++b) all[b] = b;
+    std::vector<uint32_t> all(knb);
+    for (uint32_t b = 0; b < knb; ++b) all[b] = b;
     DBuf<uint32_t> d = upload_list(all);
     if (flags & DR_FLAG_EXACT_REDUCE) {
-      launch_bucket_exact(ra, d.p, nb, stream);
+      launch_bucket_exact(ra, d.p, knb, stream);
     } else {
-      launch_bucket_reduce64(ra, d.p, nb, stream);
-      launch_bucket_exact(ra, xlist.p, nb, stream, totals.p + 4);
+      launch_bucket_reduce64(ra, d.p, knb, stream);
+      launch_bucket_exact(ra, xlist.p, knb, stream, totals.p + 4);
     }
   } else {
     launch_bucket_reduce(ra, stream);
     launch_bucket_verify(ra, stream);  // byte verification of every merged pair
     // the fallbacks read their bucket lists' lengths on the device (no host round trip)
-    launch_bucket_reduce64(ra, rlist.p, nb, stream, totals.p + 3);
-    launch_bucket_exact(ra, xlist.p, nb, stream, totals.p + 4);
+    launch_bucket_reduce64(ra, rlist.p, knb, stream, totals.p + 3);
+    launch_bucket_exact(ra, xlist.p, knb, stream, totals.p + 4);
     if (std::getenv("DR_REDUCE_DEBUG")) {
       const std::vector<unsigned long long> t = d2h(totals.p, 8, stream);
-      std::vector<uint64_t> bo = d2h(boff.p, nb + 1, stream);
-      std::vector<uint32_t> rl = d2h(rlist.p, size_t(std::min<unsigned long long>(t[3], nb)), stream);
-      std::fprintf(stderr, "reduce: %u buckets, %llu to the 64-bit reducer, %llu to the exact one; sizes:", nb,
-                   t[3], t[4]);
+      std::vector<uint64_t> bo = d2h(kboff, knb + 1, stream);
+      std::vector<uint32_t> rl = d2h(rlist.p, size_t(std::min<unsigned long long>(t[3], knb)), stream);
+      std::fprintf(stderr, "reduce: %u buckets (%d split bits), %llu to the 64-bit reducer, %llu to the exact one; sizes:",
+                   knb, sbits, t[3], t[4]);
       for (uint32_t b : rl) std::fprintf(stderr, " %llu", (unsigned long long)(bo[b + 1] - bo[b]));
       std::fprintf(stderr, "\n");
     }
@@ -2070,12 +2092,12 @@ static ReducePending reduce_launch(dr_ctx* ctx, dr_state* st, int64_t cutoff, ui
   reduce_range.reset();
   DR_STAGE("compact", stream);
   // ---- compaction (survivor lists sized to the bound; the counts come back once, at the end) ----
-  DBuf<uint64_t> loff(ctx, nb + 1), tmoff(ctx, nb + 1);
-  launch_survivor_scan(lcount.p, tcount.p, nb, loff.p, tmoff.p, stream);
+  DBuf<uint64_t> loff(ctx, knb + 1), tmoff(ctx, knb + 1);
+  launch_survivor_scan(lcount.p, tcount.p, knb, loff.p, tmoff.p, stream);
   st->live = DBuf<uint32_t>(ctx, N);
   st->tomb = DBuf<uint32_t>(ctx, N);
-  launch_compact2(CompactArgs{olive.p, boff.p, lcount.p, loff.p, nb, st->live.p},
-                  CompactArgs{otomb.p, boff.p, tcount.p, tmoff.p, nb, st->tomb.p}, stream);
+  launch_compact2(CompactArgs{olive.p, kboff, lcount.p, loff.p, knb, st->live.p},
+                  CompactArgs{otomb.p, kboff, tcount.p, tmoff.p, knb, st->tomb.p}, stream);
   HIP_OK(hipMemcpyAsync(totals.p + 7, boff.p + nb, 8, hipMemcpyDeviceToDevice, stream));
   ReducePending rp;
   rp.totals = std::move(totals);

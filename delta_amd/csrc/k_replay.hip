@@ -855,8 +855,65 @@ __global__ void k_compact2(CompactArgs l, CompactArgs t) {
   k_compact_one(blockIdx.y ? t : l);
 }
 
-// Exclusive scans of the per-bucket live and tombstone counts in one workgroup (nb <= 8192: each
-// thread owns a run of at most 8 buckets); off[nb] is the total.
+// Large replays (more than 2^13 * 2048 file actions, config 4): K3's scatter keeps per-tile LDS cursors
+// for at most 2^13 buckets, so buckets average over 2048 records and K4 would take several sub-passes,
+// each reading the whole bucket twice. k_bucket_split refines every bucket b into 2^sbits sub-buckets
+// by the next key bits -- exactly bucket_of(key, bits + sbits) -- writing the records once more
+// (order within a bucket is free: K4's last-writer-wins is an atomicMax on the action index) and
+// the refined offsets, so K4 runs one pass per refined bucket. Records stay in registers between the
+// count and the write (up to SPLIT_T * SPLIT_RPT per bucket; larger buckets read twice).
+constexpr int SPLIT_T = 1024, SPLIT_RPT = 16;
+__global__ void __launch_bounds__(SPLIT_T) k_bucket_split(SplitArgs a) {
+  __shared__ uint32_t cnt[64], cur[64];
+  const uint32_t b = blockIdx.x, S = 1u << a.sbits;
+  const uint64_t beg = a.bucket_off[b], end = a.bucket_off[b + 1];
+  const uint64_t m = end - beg;
+  if (threadIdx.x < S) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  auto sub_of = [&](uint4 r) { return rkey_of(rec_key(r), a.bits) >> (32 - a.sbits); };
+  const bool held = m <= uint64_t(SPLIT_T) * SPLIT_RPT;  // block-uniform
+  uint4 r[SPLIT_RPT];
+  if (held) {
+#pragma unroll
+    for (int q = 0; q < SPLIT_RPT; ++q) {
+      const uint64_t e = beg + threadIdx.x + uint64_t(q) * SPLIT_T;
+      if (e < end) r[q] = load_rec(a.rec, e);
+    }
+#pragma unroll
+    for (int q = 0; q < SPLIT_RPT; ++q)
+      if (beg + threadIdx.x + uint64_t(q) * SPLIT_T < end) atomicAdd(&cnt[sub_of(r[q])], 1u);
+  } else {
+    for (uint64_t e = beg + threadIdx.x; e < end; e += SPLIT_T) atomicAdd(&cnt[sub_of(load_rec(a.rec, e))], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t run = 0;
+    for (uint32_t j = 0; j < S; ++j) {
+      cur[j] = run;
+      a.out_off[uint64_t(b) * S + j] = beg + run;
+      run += cnt[j];
+    }
+  }
+  __syncthreads();
+  if (held) {
+#pragma unroll
+    for (int q = 0; q < SPLIT_RPT; ++q)
+      if (beg + threadIdx.x + uint64_t(q) * SPLIT_T < end) {
+        const uint32_t at = atomicAdd(&cur[sub_of(r[q])], 1u);
+        *reinterpret_cast<uint4*>(a.out + beg + at) = r[q];
+      }
+  } else {
+    for (uint64_t e = beg + threadIdx.x; e < end; e += SPLIT_T) {
+      const uint4 x = load_rec(a.rec, e);
+      const uint32_t at = atomicAdd(&cur[sub_of(x)], 1u);
+      *reinterpret_cast<uint4*>(a.out + beg + at) = x;
+    }
+  }
+  if (b + 1 == gridDim.x && threadIdx.x == 0) a.out_off[uint64_t(gridDim.x) * S] = end;
+}
+
+// Exclusive scans of the per-bucket live and tombstone counts in one workgroup (each thread owns a
+// run of ceil(nb / 1024) buckets: 8 for K3's 2^13, 64 for a split replay's 2^16); off[nb] is the total.
 constexpr int SSCAN_T = 1024;
 __global__ void __launch_bounds__(SSCAN_T) k_survivor_scan(const uint32_t* lc, const uint32_t* tc, uint32_t nb,
                                                            uint64_t* loff, uint64_t* toff) {
@@ -954,9 +1011,14 @@ void launch_compact2(const CompactArgs& live, const CompactArgs& tomb, hipStream
   if (live.nbuckets) DR_LAUNCH(dev::k_compact2, dim3(live.nbuckets, 2), dim3(64), 0, st, live, tomb);
 }
 
+void launch_bucket_split(const SplitArgs& a, uint32_t nbuckets, hipStream_t st) {
+  if (a.sbits < 1 || a.sbits > 6) throw std::runtime_error("bucket split: 1..6 refinement bits");
+  if (nbuckets) DR_LAUNCH(dev::k_bucket_split, dim3(nbuckets), dim3(dev::SPLIT_T), 0, st, a);
+}
+
 void launch_survivor_scan(const uint32_t* lc, const uint32_t* tc, uint32_t nb, uint64_t* loff, uint64_t* toff,
                           hipStream_t st) {
-  if (nb > uint32_t(dev::SSCAN_T) * 8) throw std::runtime_error("survivor scan: too many buckets");
+  if (nb > uint32_t(dev::SSCAN_T) * 256) throw std::runtime_error("survivor scan: too many buckets");
   DR_LAUNCH(dev::k_survivor_scan, dim3(1), dim3(dev::SSCAN_T), 0, st, lc, tc, nb, loff, toff);
 }
 

@@ -284,6 +284,16 @@ struct ReduceArgs {
   unsigned long long* bstats;  // [nbuckets * 5] per-bucket {live, tomb, size, live sum, tomb sum}
   unsigned long long* vstats;  // nullable (timed replays): [nbuckets * 2] k_bucket_verify's {pairs, path bytes compared}
 };
+// K3 refinement for large replays: bucket b's records into 2^sbits sub-buckets by the next key bits
+// (bucket_of(key, bits + sbits)); out_off[b * 2^sbits + j] = the sub-buckets' offsets, [nb << sbits] = end
+struct SplitArgs {
+  const PartRec* rec;
+  const uint64_t* bucket_off;  // [nbuckets + 1]
+  int32_t bits, sbits;
+  PartRec* out;
+  uint64_t* out_off;           // [(nbuckets << sbits) + 1]
+};
+void launch_bucket_split(const SplitArgs& a, uint32_t nbuckets, hipStream_t st);
 // LDS last-writer-wins per bucket on the 64-bit key; losers paired with winners (grouped by winner)
 void launch_bucket_reduce(const ReduceArgs& a, hipStream_t st);
 // byte-verifies every (loser, winner) pair; mismatching buckets (64-bit collisions) -> exact_list

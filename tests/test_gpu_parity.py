@@ -196,11 +196,12 @@ def test_fallback_reducers_agree(engine, tmp_path, reducer):
         b.release()
 
 
-@pytest.mark.parametrize("bits", [3, 5])
-def test_reducer_subpasses_agree(engine, tmp_path, monkeypatch, bits):
-    """K4's sub-pass path (buckets over 3/4 of its 4096-slot LDS table, which config 4's 12K-record
-    buckets take; forced here with 8 or 32 buckets of ~20K / ~5K records) gives the one-pass
-    reducer's state."""
+@pytest.mark.parametrize("bits,split", [(3, "0"), (5, "0"), (3, "1"), (5, "1")])
+def test_reducer_subpasses_agree(engine, tmp_path, monkeypatch, bits, split):
+    """Buckets of more than 2048 records on average (config 4's 12K; forced here with 8 or 32
+    buckets of ~20K / ~5K records): K3's refinement (k_bucket_split into 2^s sub-buckets by the next
+    key bits, then one K4 pass per sub-bucket) and, with DR_SPLIT=0, K4's own sub-pass path over
+    the whole bucket give the one-pass reducer's state."""
     from delta_amd.testing import synth as S
     exp = S.build_config(3, str(tmp_path), scale=0.01)
     lp = os.path.join(str(tmp_path), "_delta_log")
@@ -208,11 +209,12 @@ def test_reducer_subpasses_agree(engine, tmp_path, monkeypatch, bits):
     try:
         a = staged.replay(exp.min_file_retention_timestamp)
         monkeypatch.setenv("DR_BUCKET_BITS", str(bits))
+        monkeypatch.setenv("DR_SPLIT", split)
         b = staged.replay(exp.min_file_retention_timestamp)
     finally:
         staged.release()
     try:
-        _same_state(a, b, bits)
+        _same_state(a, b, (bits, split))
         assert b.counts["num_files"] == exp.num_files and b.counts["num_removes"] == exp.num_removes
     finally:
         a.release()

@@ -1,5 +1,5 @@
 # Builds a variant of libdeltareplay.so with extra compile definitions into var_libs/<name>/
-# (for scripts/gpu_kvariants.sh): scripts/build_variant.sh <name> "-DX=1 -DY=2"
+# (for scripts/gpu_kvariants.sh, scripts/gpu_snapvar.sh): scripts/build_variant.sh <name> "-DX=1 -DY=2"
 set -e
 name=$1; defs=$2
 mkdir -p var_libs/$name

@@ -993,9 +993,12 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     uint32_t rounds = 0;
     while (act) {
       ++rounds;
-      if (a.stamps && rounds <= 3)  // (DR_SNAP_DEBUG) active groups at the start of rounds 1..3
-        atomicAdd(reinterpret_cast<unsigned long long*>(&a.stamps[uint64_t(b) * 16 + 10 + rounds]),
-                  (unsigned long long)__popc(act));
+      if (a.stamps && rounds <= 3) {  // (DR_SNAP_DEBUG) active groups at the start of rounds 1..3, one atomic per wave
+        uint32_t v = __popc(act);
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        if ((t & 63) == 0) atomicAdd(reinterpret_cast<unsigned long long*>(&a.stamps[uint64_t(b) * 16 + 10 + rounds]),
+                                     (unsigned long long)v);
+      }
 #pragma unroll
       for (uint32_t j = 0; j < 16; ++j) {
         if (act & (1u << j)) {

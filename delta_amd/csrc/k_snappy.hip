@@ -4,8 +4,8 @@
 // serial and a 1 MiB page of paths holds ~144K elements, so a per-page decoder is latency bound
 // (measured 1.28 s for config 3 with one lane per page). This decoder is fully parallel:
 //
-//  A k_snap_spec    one lane per 256-byte chunk of compressed input parses elements
-//                   *speculatively* (starting SNAP_WU = 192 bytes early as a warm-up) and records the
+//  A k_snap_spec    one lane per SNAP_CH = 128-byte chunk of compressed input parses elements
+//                   *speculatively* (starting SNAP_WU = 256 bytes early as a warm-up) and records the
 //                   positions it visited in the chunk (a bitmap in registers) and where it left it.
 //  B k_snap_assume / k_snap_entries: every chunk's true entry, in parallel: a chunk whose true
 //                   entry (the previous chunk's exit) is on its speculative chain is correct
@@ -36,14 +36,21 @@ namespace dr {
 namespace dev {
 
 #ifndef DR_SNAP_CH
-#define DR_SNAP_CH 256  // r02: 128 B chunks (512-chunk workgroups) took SNAPPY-minus-exec 0.904 -> 0.794 ms at scale 0.25, but two full-size config-3 pages then failed the size check and went serial
+// r05: 128 B chunks with a 256 B warm-up, SNAPPY-minus-exec 1.356 -> 1.264 ms on config 3 (r02 tried
+// 128 B chunks, but two full-size config-3 pages then failed the size check: the resolver's
+// concurrent region walks of a page, fixed in r05 by walking a page's regions in order)
+#define DR_SNAP_CH 128
 #endif
 constexpr uint32_t SNAP_CH = DR_SNAP_CH;     // compressed bytes per speculation chunk (a multiple of 128)
 constexpr uint32_t SNAP_BLOCK = 65536;       // snappy compressor fragment size
 #ifndef DR_SNAP_WU
-#define DR_SNAP_WU 192
+#define DR_SNAP_WU 256
 #endif
-constexpr uint32_t SNAP_WU = DR_SNAP_WU;     // speculation warm-up bytes (sweep r01: 64/128 B send too many pages to k_snap_resolve, 3x/20x slower; 160-256 B within 1%, 192 B best)
+// speculation warm-up bytes (r01 at 256 B chunks: 64/128 B sent too many pages to k_snap_resolve, 3x/20x
+// slower; 160-256 B within 1 %, 192 B best. r05 at 128 B chunks, SNAPPY-minus-exec at scale 0.25:
+// 160 B 0.582 ms (the resolver doubles), 192 B 0.493, 224 B 0.460-0.469, 256 B 0.483, 288 B 0.473;
+// at full config 3: 224 B 1.289 ms, 256 B 1.264, r04's 256 B chunks + 192 B 1.356)
+constexpr uint32_t SNAP_WU = DR_SNAP_WU;
 #ifndef DR_SNAP_WG_CHUNKS
 #define DR_SNAP_WG_CHUNKS 256
 #endif
@@ -100,8 +107,9 @@ __device__ __forceinline__ uint32_t chunk_page(const SnappyArgs& a, uint32_t c) 
 // Bytes of the page input from (chunk j0 start - warm-up) to (chunk j0+cnt end + 16) are copied
 // into `buf` with coalesced dword loads; `lo` is the page offset of buf[0] (dword aligned in
 // absolute address, so it may sit up to 3 bytes before the page input).
-// The staged copy is skewed by one dword per 256 bytes: lane l walks chunk l, 256 bytes after lane
-// l-1, so unskewed every lane at the same relative offset would hit the same LDS bank.
+// The staged copy is skewed by one dword per 256 bytes: lane l walks chunk l, SNAP_CH bytes after
+// lane l-1, so unskewed the lanes at the same relative offset would hit one LDS bank or two (with
+// 128-byte chunks the skew still gives the 64 lanes 64 distinct banks).
 struct Staged {
   int64_t lo;
   uint64_t hi;
@@ -591,44 +599,53 @@ __global__ void __launch_bounds__(256) k_snap_count(SnappyArgs a) {
 // summing a contiguous run of chunks, a block scan of the run sums, then the run's prefixes.
 constexpr int SCAN_T = 256;
 __global__ void __launch_bounds__(SCAN_T) k_snap_scan(SnappyArgs a) {
-  __shared__ uint64_t wsum[SCAN_T / 64];
+  __shared__ uint32_t wsum[SCAN_T / 64];
   const uint32_t p = blockIdx.x;
   if (p >= a.npages) return;
   const uint32_t c0 = a.chunk_base[p], nc = a.chunk_base[p + 1] - c0;
-  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const uint32_t per = (nc + SCAN_T - 1) / SCAN_T;
-  const uint32_t j0 = min(nc, t * per), j1 = min(nc, j0 + per);
-  uint64_t run = 0;
-  for (uint32_t j = j0; j < j1; ++j) run += a.chunk_out[c0 + j];
-  uint64_t incl = run;
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint64_t y = __shfl_up(incl, o, 64);
-    if (lane >= uint32_t(o)) incl += y;
-  }
-  if (lane == 63) wsum[wv] = incl;
-  __syncthreads();
-  uint64_t before = 0, total = 0;
-  for (uint32_t q = 0; q < SCAN_T / 64; ++q) {
-    before += q < wv ? wsum[q] : 0ull;
-    total += wsum[q];
-  }
+  const uint32_t t = threadIdx.x, wv = t >> 6;
   // the chunk holding each output block's first element (no element straddles a block, so that
   // element starts the block): block k of the page is first produced by the chunk whose output range
   // [at, at + out) holds k * SNAP_BLOCK; blocks no chunk claims keep ~0 (k_snap_exec: bad page)
   const uint32_t bb = a.pages[p].block_base, nb = (a.pages[p].n_out + SNAP_BLOCK - 1) / SNAP_BLOCK;
   for (uint32_t k = t; k < nb; k += SCAN_T) a.block_chunk[bb + k] = 0xffffffffu;
   __syncthreads();
-  uint64_t at = before + incl - run;
-  for (uint32_t j = j0; j < j1; ++j) {
-    a.chunk_out_start[c0 + j] = uint32_t(at);
-    const uint32_t n = a.chunk_out[c0 + j];
-    if (n) {
-      const uint64_t k0 = (at + SNAP_BLOCK - 1) / SNAP_BLOCK, k1 = min((at + n - 1) / SNAP_BLOCK + 1, uint64_t(nb));
-      for (uint64_t k = k0; k < k1; ++k) a.block_chunk[bb + k] = c0 + j;
+  // tiles of SCAN_T consecutive chunks (coalesced loads and stores), a block scan per tile and the
+  // running offset across tiles (page outputs fit 32 bits: chunk_out_start is u32)
+  uint32_t carry = 0;
+  uint64_t mine = 0;  // this thread's outputs, summed in 64 bits for the size check (a saturated
+                      // chunk output must not wrap into a matching size)
+  for (uint32_t base = 0; base < nc; base += SCAN_T) {
+    const uint32_t j = base + t;
+    const uint32_t n = j < nc ? a.chunk_out[c0 + j] : 0u;
+    mine += n;
+    const uint32_t incl = wv::scan_incl(n, 0u, [](uint32_t x, uint32_t y) { return x + y; });
+    if ((t & 63) == 63) wsum[wv] = incl;
+    __syncthreads();
+    uint32_t before = 0, tile = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < SCAN_T / 64; ++q) {
+      before += q < wv ? wsum[q] : 0u;
+      tile += wsum[q];
     }
-    at += n;
+    const uint32_t at = carry + before + incl - n;
+    if (j < nc) {
+      a.chunk_out_start[c0 + j] = at;
+      if (n) {
+        const uint64_t k0 = (uint64_t(at) + SNAP_BLOCK - 1) / SNAP_BLOCK, k1 = min((uint64_t(at) + n - 1) / SNAP_BLOCK + 1, uint64_t(nb));
+        for (uint64_t k = k0; k < k1; ++k) a.block_chunk[bb + k] = c0 + j;
+      }
+    }
+    carry += tile;
+    __syncthreads();  // the wave sums are rewritten by the next tile
   }
-  if (t == 0 && total != a.pages[p].n_out) atomicOr(&a.pages_bad[p], 1u);  // size mismatch
+  __shared__ unsigned long long tsum;
+  if (t == 0) tsum = 0;
+  __syncthreads();
+  for (int o = 32; o > 0; o >>= 1) mine += __shfl_down(mine, o, 64);
+  if ((t & 63) == 0) atomicAdd(&tsum, (unsigned long long)mine);
+  __syncthreads();
+  if (t == 0 && tsum != a.pages[p].n_out) atomicOr(&a.pages_bad[p], 1u);  // size mismatch
 }
 
 // E: k_snap_exec -- one 1024-thread workgroup per 64 KiB output block, fed by the compressed page

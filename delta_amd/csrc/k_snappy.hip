@@ -867,6 +867,11 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
   uint32_t sum = 0;
   bool bad = false;
   {
+    // Branch-free decode (mask blends, not ?:): written with conditional expressions and
+    // short-circuit tests, and the page size read inside the loop, the compiler turned each element
+    // into a dozen divergent branches and a global load
+    const uint64_t n_in = pg.n_in;
+    const auto sel = [](bool c, uint32_t x, uint32_t y) { return y ^ ((x ^ y) & (0u - uint32_t(c))); };
     uint32_t pos = first;
 #pragma unroll
     for (uint32_t k = 0; k < EXEC_EMAX; ++k) {
@@ -875,18 +880,21 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
         const uint32_t so = pos - plo + sh0;
         const uint64_t w = lds_hdr(stage32, min(so, so_lim));
         const uint32_t tag = uint32_t(w) & 0xffu, ty = tag & 3u, l6 = tag >> 2, w8 = uint32_t(w >> 8);
-        const uint32_t nb = l6 >= 60 ? l6 - 59 : 0u;
-        const uint32_t lit_len = (nb ? (w8 & (nb >= 4 ? ~0u : (1u << (8 * nb)) - 1u)) : l6) + 1u;
-        const uint32_t len = ty == 0 ? lit_len : ty == 1 ? (l6 & 7u) + 4u : l6 + 1u;
-        const uint32_t hdr = ty == 0 ? 1u + nb : ty == 1 ? 2u : ty == 2 ? 3u : 5u;
-        const uint32_t off = ty == 1 ? (((tag >> 5) << 8) | (w8 & 0xffu)) : (w8 & 0xffffu);
-        const uint32_t adv = hdr + (ty == 0 ? len : 0u);
+        const bool lit = ty == 0u, c1 = ty == 1u;
+        const uint32_t nb = l6 > 59u ? l6 - 59u : 0u;  // a literal's extra length bytes
+        const uint32_t lmask = sel(nb >= 4u, ~0u, (1u << (8u * (nb & 3u))) - 1u);
+        const uint32_t lit_len = sel(nb != 0u, w8 & lmask, l6) + 1u;
+        const uint32_t len = sel(lit, lit_len, sel(c1, (l6 & 7u) + 4u, l6 + 1u));
+        const uint32_t hdr = ((0x5320u >> (4u * ty)) & 15u) + sel(lit, 1u + nb, 0u);  // 1 + nb, 2, 3, 5
+        const uint32_t off = sel(c1, ((tag >> 5) << 8) | (w8 & 0xffu), w8 & 0xffffu);
+        const uint32_t adv = hdr + sel(lit, len, 0u);
         // a literal past the page or longer than a fragment, a copy offset no fragment has (copy-4's
         // upper offset bytes): the page is not one the parallel path can take
-        bad |= so > so_lim || (ty == 0 ? (len > SNAP_BLOCK || uint64_t(pos) + adv > pg.n_in)
-                                       : (ty == 3 && (w8 >> 16) != 0));
-        el[k] = (hdr << 24) | (ty == 0 ? (EL_LIT | ((len - 1u) & 0xffffu)) : (((len - 1u) << 16) | off));
-        sum += ty == 0 ? min(len, SNAP_BLOCK) : len;
+        const bool bad_lit = (len > SNAP_BLOCK) | (uint64_t(pos) + adv > n_in);
+        const bool bad_cp = (ty == 3u) & ((w8 >> 16) != 0u);
+        bad |= (so > so_lim) | (lit & bad_lit) | (!lit & bad_cp);
+        el[k] = (hdr << 24) | sel(lit, EL_LIT | ((len - 1u) & 0xffffu), ((len - 1u) << 16) | off);
+        sum += sel(lit, min(len, SNAP_BLOCK), len);
         pos += adv;
       }
     }
@@ -908,14 +916,14 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
         const uint32_t len = lit ? (x & 0xffffu) + 1u : ((x >> 16) & 0x7fu) + 1u;
         const uint32_t off = x & 0xffffu;
         const uint32_t rel = o - bs32;
-        if (o < be32 && o + len > bs32) {
-          if (o < bs32 || o + len > be32 || (!lit && (off == 0 || off > rel))) {
-            bad = true;  // straddles the block, or a copy reaching before its fragment
-          } else {
-            atomicOr(&starts[rel >> 5], 1u << (rel & 31));
-            src[rel] = uint16_t(lit ? rel : rel - off);
-            cov += len;
-          }
+        // tests combined without short circuits: one divergent branch per element, not four
+        const bool hit = (o < be32) & (o + len > bs32);
+        const bool cut = (o < bs32) | (o + len > be32) | (!lit & ((off == 0u) | (off > rel)));
+        bad |= hit & cut;  // straddles the block, or a copy reaching before its fragment
+        if (hit & !cut) {
+          atomicOr(&starts[rel >> 5], 1u << (rel & 31));
+          src[rel] = uint16_t(lit ? rel : rel - off);
+          cov += len;
         }
         o += len;
       }
@@ -1072,7 +1080,21 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     // dwords (five reads in flight before four writes: one LDS round trip per 16 bytes), a byte tail
     uint32_t q = uint32_t(ip - P_lo) + sh0 + SNAP_BLOCK;
     uint32_t d = rel, n = len;
-    while (n && (d & 3)) { bytes[d++] = bytes[q++]; --n; }
+    // the byte head and tail each from one realigned 4-byte read (reads past the range stay in
+    // the stage: it holds 8 bytes past it), their byte stores issued together
+    const auto read4 = [&](uint32_t at) {
+      const uint32_t* pa = reinterpret_cast<const uint32_t*>(bytes + (at & ~3u));
+      return __builtin_amdgcn_alignbyte(pa[1], pa[0], at & 3u);
+    };
+    if (const uint32_t h = min((4u - (d & 3u)) & 3u, n)) {
+      const uint32_t v = read4(q);
+      bytes[d] = uint8_t(v);
+      if (h > 1) bytes[d + 1] = uint8_t(v >> 8);
+      if (h > 2) bytes[d + 2] = uint8_t(v >> 16);
+      d += h;
+      q += h;
+      n -= h;
+    }
     const uint32_t sh = q & 3;
     const uint32_t* qa = reinterpret_cast<const uint32_t*>(bytes + (q & ~3u));
     uint32_t* da = reinterpret_cast<uint32_t*>(bytes + d);
@@ -1089,9 +1111,14 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
       *da++ = __builtin_amdgcn_alignbyte(qa[1], qa[0], sh);
       ++qa;
     }
-    d = uint32_t(reinterpret_cast<uint8_t*>(da) - bytes);
-    q = uint32_t(reinterpret_cast<const uint8_t*>(qa) - bytes) + sh;
-    while (n) { bytes[d++] = bytes[q++]; --n; }
+    if (n) {  // fewer than 4 bytes left
+      d = uint32_t(reinterpret_cast<uint8_t*>(da) - bytes);
+      q = uint32_t(reinterpret_cast<const uint8_t*>(qa) - bytes) + sh;
+      const uint32_t v = read4(q);
+      bytes[d] = uint8_t(v);
+      if (n > 1) bytes[d + 1] = uint8_t(v >> 8);
+      if (n > 2) bytes[d + 2] = uint8_t(v >> 16);
+    }
   };
   // the thread's elements again from its first start: from the registers when the thread has at
   // most EXEC_EHELD (its elements stayed live through the jumping), else re-read from the stage

@@ -960,8 +960,9 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
 #pragma unroll
     for (uint32_t jb = 0; jb < 16; jb += EXEC_SPLIT) {
       // staged so a batch's LDS reads are in flight together: start words and group entries, then
-      // the starts the groups continue (a volatile read: the compiler would otherwise sink it into
-      // the branch of groups whose first byte is no start, one round trip per group)
+      // the starts the groups continue (pinned by an empty asm: the compiler would otherwise sink
+      // each read into the branch of groups whose first byte is no start, one round trip per group;
+      // a volatile read did pin them, but as flat loads each waited on alone)
       uint32_t w0[EXEC_SPLIT], prev[EXEC_SPLIT], pv[EXEC_SPLIT];
       bool pvalid[EXEC_SPLIT];
       uint2 g[EXEC_SPLIT];
@@ -981,7 +982,9 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
         prev[q] = x64 ? pa : pa - uint32_t(__clz(int32_t(w2)));
       }
 #pragma unroll
-      for (uint32_t q = 0; q < EXEC_SPLIT; ++q) pv[q] = reinterpret_cast<volatile uint16_t*>(src)[pvalid[q] ? prev[q] : 0u];
+      for (uint32_t q = 0; q < EXEC_SPLIT; ++q) pv[q] = src[pvalid[q] ? prev[q] : 0u];
+#pragma unroll
+      for (uint32_t q = 0; q < EXEC_SPLIT; ++q) asm volatile("" : "+v"(pv[q]));
 #pragma unroll
       for (uint32_t q = 0; q < EXEC_SPLIT; ++q) {
         const uint32_t j = jb + q;

@@ -15,6 +15,18 @@ enum Flag : uint8_t { F_HAS_DELTS = 1, F_SPECIAL_PATH = 2, F_PATH_ESCAPED = 4, F
 // replay classes carried in the partition records (low 2 bits of the meta word)
 enum Class : uint32_t { C_ADD = 0, C_REMOVE_KEEP = 1, C_REMOVE_DROP = 2 };
 
+// A 16-byte load through the global address space (a flat load also counts against the LDS
+// counter, so every LDS access after it waits for it too).
+typedef unsigned int gu32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 gload16(const uint4* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const gu32x4 v = *(const __attribute__((address_space(1))) gu32x4*)(p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+#else
+  return *p;
+#endif
+}
+
 // ---- unaligned little-endian loads from byte buffers (buffers are padded by >= 16 bytes) -----
 __device__ __forceinline__ uint32_t ld_u32a(const uint8_t* p) {  // aligned dword
   return *reinterpret_cast<const uint32_t*>(p);

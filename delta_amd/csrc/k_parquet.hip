@@ -313,7 +313,18 @@ __global__ void __launch_bounds__(BA_T) k_ba_count(ParquetArgs a) {
     const uint64_t nb = hi > st.t0 ? uint64_t(hi - st.t0) & ~uint64_t(15) : 0;
     const uint4* g4 = reinterpret_cast<const uint4*>(tl.b + st.t0);
     uint4* s4 = reinterpret_cast<uint4*>(stw);
-    for (uint32_t v = threadIdx.x; v < nb / 16; v += BA_T) s4[v] = g4[v];
+    // every load of the thread in flight before any is written (global loads: through the page
+    // pointer the compiler had emitted flat loads, each waited on before the next was issued)
+    constexpr uint32_t PER = ((BA_TILE + BA_MARGIN) / 16 + BA_T - 1) / BA_T;
+    const uint32_t nv = uint32_t(nb / 16);
+    if (nv) {
+      uint4 v[PER];
+#pragma unroll
+      for (uint32_t k = 0; k < PER; ++k) v[k] = gload16(g4 + min(threadIdx.x + k * BA_T, nv - 1));
+#pragma unroll
+      for (uint32_t k = 0; k < PER; ++k)
+        if (threadIdx.x + k * BA_T < nv) s4[threadIdx.x + k * BA_T] = v[k];
+    }
     st.n = nb;
   }
   __syncthreads();

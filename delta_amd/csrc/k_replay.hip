@@ -371,22 +371,24 @@ __device__ __forceinline__ uint32_t block_diff(uint4 plo, uint4 phi, uint32_t po
   return d.x | d.y | d.z | d.w;
 }
 
-// Byte equality of p[0..n) and q[0..n) by one lane: aligned 16-byte loads (each block once, none
-// that holds no string byte), no early exit, so the loads of successive blocks are independent.
+// Byte equality of p[0..n) and q[0..n) by one lane: aligned 16-byte loads (each block once; past
+// the string its last block again), no early exit, so the loads of successive blocks are independent.
 __device__ bool bytes_equal16(const uint8_t* p, const uint8_t* q, uint32_t n) {
   const uint4* pa = reinterpret_cast<const uint4*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(15));
   const uint4* qa = reinterpret_cast<const uint4*>(reinterpret_cast<uintptr_t>(q) & ~uintptr_t(15));
   const uint32_t po = uint32_t(reinterpret_cast<uintptr_t>(p) & 15), qo = uint32_t(reinterpret_cast<uintptr_t>(q) & 15);
   const uint32_t pblocks = (po + n + 15) >> 4, qblocks = (qo + n + 15) >> 4;
-  const uint4 z = make_uint4(0, 0, 0, 0);
   // the first 128 bytes: every 16-byte block of both paths requested before any is compared (a
-  // lane compares one pair alone, so one round trip instead of one per block)
+  // lane compares one pair alone, so one round trip instead of one per block). Blocks past a string
+  // re-read its last one (their bytes are masked by block_diff): as conditional loads the compiler
+  // split each into four dword loads under branches
   constexpr uint32_t PRE = 9;
   uint4 pb[PRE], qb[PRE];
+  if (n == 0) return true;
 #pragma unroll
   for (uint32_t k = 0; k < PRE; ++k) {
-    pb[k] = k < pblocks ? pa[k] : z;
-    qb[k] = k < qblocks ? qa[k] : z;
+    pb[k] = gload16(pa + min(k, pblocks - 1));
+    qb[k] = gload16(qa + min(k, qblocks - 1));
   }
   uint32_t diff = 0;
 #pragma unroll
@@ -397,7 +399,7 @@ __device__ bool bytes_equal16(const uint8_t* p, const uint8_t* q, uint32_t n) {
   if (n <= 16 * (PRE - 1)) return diff == 0;
   uint4 plo = pb[PRE - 1], qlo = qb[PRE - 1];
   for (uint32_t i = 16 * (PRE - 1), k = PRE; i < n; i += 16, ++k) {
-    const uint4 phi = k < pblocks ? pa[k] : z, qhi = k < qblocks ? qa[k] : z;
+    const uint4 phi = gload16(pa + min(k, pblocks - 1)), qhi = gload16(qa + min(k, qblocks - 1));
     diff |= block_diff(plo, phi, po, qlo, qhi, qo, n - i);
     plo = phi;
     qlo = qhi;
@@ -427,7 +429,6 @@ __global__ void __launch_bounds__(VER_T) k_bucket_verify(ReduceArgs a) {
   if (!n) return;
   const uint2* pr = a.out_pair + a.bucket_off[b];
   const uint32_t j = threadIdx.x & (VER_G - 1);
-  const uint4 z = make_uint4(0, 0, 0, 0);
   bool bad = false;
   uint32_t vbytes = 0;  // (vstats) path bytes this lane group compared
   for (uint32_t k0 = 0; k0 < n; k0 += VER_T / VER_G) {
@@ -462,11 +463,12 @@ __global__ void __launch_bounds__(VER_T) k_bucket_verify(ReduceArgs a) {
         const uint32_t po = uint32_t(reinterpret_cast<uintptr_t>(p) & 15);
         const uint32_t qo = uint32_t(reinterpret_cast<uintptr_t>(q) & 15);
         const uint32_t pblocks = (po + pn + 15) >> 4, qblocks = (qo + pn + 15) >> 4;
-        // step: lane j loads aligned block B + j of each string (never one that holds none of its
-        // bytes) and takes block B + j + 1 from lane j + 1; lanes 0..6 compare path bytes
+        // step: lane j loads aligned block B + j of each string (a block past the string re-reads
+        // its last one) and takes block B + j + 1 from lane j + 1; lanes 0..6 compare path bytes
         // [16 (B + j), +16)
         for (uint32_t B = 0; 16 * B < pn; B += VER_G - 1) {
-          const uint4 plo = B + j < pblocks ? pa[B + j] : z, qlo = B + j < qblocks ? qa[B + j] : z;
+          // (unconditional loads, clamped to the string's last block: see bytes_equal16)
+          const uint4 plo = gload16(pa + min(B + j, pblocks - 1)), qlo = gload16(qa + min(B + j, qblocks - 1));
           const uint4 phi = shfl_down4(plo, VER_G), qhi = shfl_down4(qlo, VER_G);
           const uint32_t i = 16 * (B + j);
           if (j < VER_G - 1 && i < pn) diff |= block_diff(plo, phi, po, qlo, qhi, qo, pn - i);

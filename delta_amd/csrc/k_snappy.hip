@@ -89,11 +89,27 @@ __device__ __forceinline__ uint64_t snap_adv(const Elem& e) { return uint64_t(e.
 
 // Input bytes an element occupies and the output bytes it produces, without branches (the
 // speculative walkers only need these; lanes then never split on the element type).
+// Selects written as mask blends: as conditional expressions the compiler made the walkers' steps
+// divergent branches again (six per element in k_snap_spec's loop).
+__device__ __forceinline__ uint32_t sel32(bool c, uint32_t x, uint32_t y) { return y ^ ((x ^ y) & (0u - uint32_t(c))); }
 __device__ __forceinline__ void snap_step(uint64_t w, uint32_t* adv, uint32_t* out) {
   const uint32_t tag = uint32_t(w & 0xff), t = tag & 3, l6 = tag >> 2;
-  const uint32_t nb = l6 >= 60 ? l6 - 59 : 0;                        // long literal: length bytes
+  const bool lit = t == 0;
+  const uint32_t nb = l6 > 59u ? l6 - 59u : 0u;                      // long literal: length bytes
+  const uint32_t lmask = sel32(nb >= 4u, 0xffffffffu, (1u << (8u * (nb & 3u))) - 1u);
+  const uint32_t lit_len = sel32(nb != 0u, uint32_t(w >> 8) & lmask, l6);  // minus one
+  const uint32_t hdr = ((0x5320u >> (4 * t)) & 0xfu) + sel32(lit, 1u + nb, 0u);
+  const uint32_t len = sel32(lit, lit_len + 1u, sel32(t == 1, (l6 & 7) + 4, l6 + 1));
+  *out = len;
+  *adv = hdr + sel32(lit, len, 0u);
+}
+// The same with conditional expressions (compiled to branches): the window walkers of k_snap_assume
+// and k_snap_count measured faster with it (0.033 / 0.049 ms against 0.038 / 0.062 at scale 0.25).
+__device__ __forceinline__ void snap_step_br(uint64_t w, uint32_t* adv, uint32_t* out) {
+  const uint32_t tag = uint32_t(w & 0xff), t = tag & 3, l6 = tag >> 2;
+  const uint32_t nb = l6 >= 60 ? l6 - 59 : 0;
   const uint32_t lmask = nb >= 4 ? 0xffffffffu : ((1u << (8 * nb)) - 1u);
-  const uint32_t lit_len = nb ? uint32_t(w >> 8) & lmask : l6;      // minus one
+  const uint32_t lit_len = nb ? uint32_t(w >> 8) & lmask : l6;
   const uint32_t hdr = t == 0 ? 1 + nb : ((0x5320u >> (4 * t)) & 0xfu);
   const uint32_t len = t == 0 ? lit_len + 1 : t == 1 ? ((l6 & 7) + 4) : l6 + 1;
   *out = len;
@@ -119,17 +135,6 @@ __device__ __forceinline__ uint32_t skew(uint32_t dw) { return dw + (dw >> 6); }
 #define DR_STAGE_BATCH 8
 #endif
 constexpr uint32_t STAGE_BATCH = DR_STAGE_BATCH;
-// A 16-byte load through the global address space (a flat load also counts against the LDS
-// counter, so every LDS access after it waits for it too).
-typedef unsigned int gu32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ uint4 gload16(const uint4* p) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  const gu32x4 v = *(const __attribute__((address_space(1))) gu32x4*)(p);
-  return make_uint4(v.x, v.y, v.z, v.w);
-#else
-  return *p;
-#endif
-}
 
 __device__ Staged stage_input(uint8_t* buf, const uint8_t* in, uint64_t n_in, uint32_t j0, uint32_t cnt) {
   uint64_t lo = uint64_t(j0) * SNAP_CH;
@@ -280,7 +285,7 @@ __device__ uint64_t walk_window(const uint8_t* in, uint64_t e, uint64_t ce, uint
     const uint32_t r = uint32_t(ea - wa), di = r >> 2, sh = r & 3;
     const uint64_t hdr = ((uint64_t(win[di + 1]) << 32) | win[di]) >> (8 * sh);  // 5 header bytes at least
     uint32_t adv, len;
-    snap_step(hdr, &adv, &len);
+    snap_step_br(hdr, &adv, &len);
     o += len;
     ++k;
     e += adv;
@@ -871,7 +876,7 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
     // short-circuit tests, and the page size read inside the loop, the compiler turned each element
     // into a dozen divergent branches and a global load
     const uint64_t n_in = pg.n_in;
-    const auto sel = [](bool c, uint32_t x, uint32_t y) { return y ^ ((x ^ y) & (0u - uint32_t(c))); };
+    const auto sel = sel32;
     uint32_t pos = first;
 #pragma unroll
     for (uint32_t k = 0; k < EXEC_EMAX; ++k) {

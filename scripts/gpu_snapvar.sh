@@ -1,5 +1,6 @@
-# k_snap_exec phase clocks (DR_SNAP_DEBUG=1) and kernel time of the current library and of each
-# var_libs/ variant (scripts/build_variant.sh), over scripts/prof_replay.py at SCALE (default 0.25)
+# k_snap_exec phase clocks (DR_SNAP_DEBUG=1) and kernel times (names matching KPAT, default k_snap)
+# of the current library and of each var_libs/ variant (scripts/build_variant.sh), over
+# scripts/prof_replay.py at SCALE (default 0.25)
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out/snapvar
@@ -12,10 +13,10 @@ for v in ${VARIANTS:-$(ls $R/var_libs)}; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/snapvar/$v -o run --output-format csv -- python $R/scripts/prof_replay.py --reps 3 --scale ${SCALE:-0.25} > $R/gpurun_out/snapvar/$v.log 2>&1 || { echo "$v failed"; tail -5 $R/gpurun_out/snapvar/$v.log; break; }
   f=$(find $R/gpurun_out/snapvar/$v -name "*kernel_stats.csv" | head -1)
   echo "== $v: $(grep -m1 'exec phases' $R/gpurun_out/snapvar/$v.dbg) bad: $(grep -c 'bad page' $R/gpurun_out/snapvar/$v.dbg)"
-  python - "$f" <<'PY'
+  python - "$f" "${KPAT:-k_snap}" <<'PY'
 import csv, re, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
-print({r["Name"].split("(")[0].split("::")[-1]: round(float(r["AverageNs"]) / 1e6, 4) for r in rows if "k_snap" in r["Name"]})
+print({r["Name"].split("(")[0].split("::")[-1]: round(float(r["AverageNs"]) / 1e6, 4) for r in rows if re.search(sys.argv[2], r["Name"])})
 PY
 done
 cp $R/gpurun_out/snapvar/base.so $R/delta_amd/libdeltareplay.so

@@ -344,7 +344,7 @@ __global__ void __launch_bounds__(BA_T) k_ba_write(ParquetArgs a) {
   __shared__ uint32_t wsum[BA_T / 64];
   const BaTile tl = ba_tile(a, blockIdx.x);
   if (!tl.ok) return;
-  const PageDesc& pg = *tl.pg;
+  const PageDesc pg = *tl.pg;
   uint64_t km = a.ba_kept[uint64_t(blockIdx.x) * BA_T + threadIdx.x];
   const uint32_t c = uint32_t(__builtin_popcountll(km));
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -379,7 +379,7 @@ __global__ void __launch_bounds__(BA_T) k_ba_write(ParquetArgs a) {
 __global__ void __launch_bounds__(BA_T) k_ba_check(ParquetArgs a) {
   const BaTile tl = ba_tile(a, blockIdx.x);
   if (!tl.ok) return;
-  const PageDesc& pg = *tl.pg;
+  const PageDesc pg = *tl.pg;
   const uint32_t first = uint32_t(pg.hit_base);
   const uint64_t n = a.ba_count[pg.ba_slot];
   const uint64_t cap = pg.usize / 4 + 2;
@@ -412,7 +412,7 @@ __device__ __forceinline__ bool dict_fast(const ParquetArgs& a, const PageDesc& 
 }
 
 __global__ void __launch_bounds__(256) k_pq_dict_fast(ParquetArgs a) {
-  const PageDesc& pg = a.pages[blockIdx.x];
+  const PageDesc pg = a.pages[blockIdx.x];
   if (pg.kind != PG_DICT || !dict_fast(a, pg)) return;
   const uint8_t* p = reinterpret_cast<const uint8_t*>(pg.dst);
   const uint32_t stride = 256 * DICT_SLICES;
@@ -433,7 +433,7 @@ __global__ void __launch_bounds__(256) k_pq_dict_fast(ParquetArgs a) {
 __global__ void __launch_bounds__(64) k_pq_dict(ParquetArgs a) {
   const uint32_t i = blockIdx.x;
   if (i >= a.npages) return;
-  const PageDesc& pg = a.pages[i];
+  const PageDesc pg = a.pages[i];
   if (pg.kind != PG_DICT) return;
   const int lane = threadIdx.x;
   const uint8_t* p = reinterpret_cast<const uint8_t*>(pg.dst);
@@ -480,7 +480,9 @@ constexpr int PQD_T = 256;
 __global__ void __launch_bounds__(PQD_T) k_pq_data(ParquetArgs a) {
   const uint32_t pi = blockIdx.x;
   if (pi >= a.npages) return;
-  const PageDesc& pg = a.pages[pi];
+  // the descriptor copied once (read through a reference, each field was re-loaded after every
+  // store the compiler could not prove it does not alias: serial loads inside the loops)
+  const PageDesc pg = a.pages[pi];
   if (pg.kind == PG_DICT) return;
   __shared__ uint8_t defs[SEG];
   __shared__ uint8_t reps[SEG];

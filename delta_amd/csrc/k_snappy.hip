@@ -239,7 +239,7 @@ __device__ __forceinline__ void spec_store(const SnappyArgs& a, const SpecChain&
 __global__ void __launch_bounds__(WG_CHUNKS) k_snap_spec(SnappyArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[STAGE_BYTES + 32];
   const WgInfo g = wg_info(a);
-  const SnapPage& pg = a.pages[g.p];
+  const SnapPage pg = a.pages[g.p];
   const Staged s = stage_input(buf, reinterpret_cast<const uint8_t*>(pg.in), pg.n_in, g.j0, g.cnt);
   const bool live = threadIdx.x < g.cnt;
   SpecChain w;
@@ -753,7 +753,7 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
   const uint32_t b = blockIdx.x;
   const uint32_t p = a.block_page[b];
   if (a.pages_bad[p]) return;
-  const SnapPage& pg = a.pages[p];
+  const SnapPage pg = a.pages[p];
   const uint8_t* in = reinterpret_cast<const uint8_t*>(pg.in);
   uint8_t* out = reinterpret_cast<uint8_t*>(pg.out);
   const uint64_t bs = uint64_t(b - pg.block_base) * SNAP_BLOCK;

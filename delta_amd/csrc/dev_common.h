@@ -27,6 +27,16 @@ __device__ __forceinline__ uint4 gload16(const uint4* p) {
 #endif
 }
 
+// A dword store through the global address space (through a pointer loaded from a descriptor the
+// compiler emits a flat store, which also counts against the LDS counter).
+__device__ __forceinline__ void gstore32(uint32_t* p, uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  *(__attribute__((address_space(1))) uint32_t*)(p) = v;
+#else
+  *p = v;
+#endif
+}
+
 // ---- unaligned little-endian loads from byte buffers (buffers are padded by >= 16 bytes) -----
 __device__ __forceinline__ uint32_t ld_u32a(const uint8_t* p) {  // aligned dword
   return *reinterpret_cast<const uint32_t*>(p);

@@ -1186,7 +1186,7 @@ __global__ void __launch_bounds__(EXEC_T) k_snap_exec(SnappyArgs a) {
   }
   if ((reinterpret_cast<uintptr_t>(dst) & 3) == 0 && nbytes == SNAP_BLOCK) {  // block-uniform
 #pragma unroll
-    for (uint32_t j = 0; j < 16; ++j) *reinterpret_cast<uint32_t*>(dst + 4 * (uint32_t(t) + EXEC_T * j)) = word[j];
+    for (uint32_t j = 0; j < 16; ++j) gstore32(reinterpret_cast<uint32_t*>(dst + 4 * (uint32_t(t) + EXEC_T * j)), word[j]);
   } else {  // a page's last block: bytes back to the LDS, then byte stores
     __syncthreads();
     uint32_t* b32 = reinterpret_cast<uint32_t*>(src);

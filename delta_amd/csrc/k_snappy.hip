@@ -244,6 +244,12 @@ __global__ void __launch_bounds__(WG_CHUNKS) k_snap_spec(SnappyArgs a) {
   const bool live = threadIdx.x < g.cnt;
   SpecChain w;
   spec_init(w, g.j0 + threadIdx.x, pg.n_in, live, uint64_t(g.j0) * SNAP_CH);
+  // the warm-up before the chunk (two thirds of the steps) advances the position only
+  while (w.pos < w.cs && w.pos < w.ce) {
+    uint32_t adv, len;
+    snap_step(staged_u64(buf, s, w.pos), &adv, &len);
+    w.pos += adv;
+  }
   while (w.pos < w.ce) spec_step(w, staged_u64(buf, s, w.pos));
   if (live) spec_store(a, w, a.chunk_base[g.p] + g.j0 + threadIdx.x);
 }

@@ -25,6 +25,7 @@ at N=1, on the CPUs the process may use (the cgroup quota, 16 on the box), on al
 the GPU's (full-scale parity, `matches_gpu`).
 """
 import argparse
+import gc
 import json
 import os
 import subprocess
@@ -228,6 +229,10 @@ def measure_stream(eng, table, exp, args):
     def run(limit, timing):
         cur, stage_ms, apply_ms, kern = base, [], [], {}
         eng.set_timing(timing)
+        # the interpreter's cyclic collector is this harness's, not the library's: paused for the loop
+        # (r05's p99 rose 0.052 -> 0.066 ms with p50 and the kernels flat -- host-side jitter), and run
+        # between commits, outside the timed calls
+        gc.disable()
         for k, c in enumerate(commits[:limit]):
             t1 = time.perf_counter()
             tail = eng.stage_files([c])
@@ -249,6 +254,9 @@ def measure_stream(eng, table, exp, args):
             cur = nxt
             stage_ms.append((t2 - t1) * 1e3)
             apply_ms.append((t3 - t2) * 1e3)
+            if k % 64 == 63:
+                gc.collect(0)
+        gc.enable()
         eng.set_timing(False)
         return cur, stage_ms, apply_ms, kern
 
@@ -708,14 +716,45 @@ def main():
             st.release()
             return t2 - t1, mat_bytes
 
+        def range_export_once():
+            # the JNI drop-in's path to rows (jni/DeltaReplayStateRDD.scala): both
+            # sides planned at 1M rows / 2^31 - 1 bytes per column, then every range exported to pinned
+            # host columns and released, as the RDD's tasks do; twice on one state (the first pass also
+            # extracts each side on the device, the second reads the resident columns)
+            from delta_amd.delta_log import State
+            st = staged.replay(cutoff)
+            torch.cuda.synchronize()
+            passes, nr, nbytes, nrows = [], 0, 0, 0
+            for rep in range(2):
+                t1 = time.perf_counter()
+                for which in (N.DR_LIVE, N.DR_TOMBSTONES):
+                    bounds = st.export_plan(which, 1 << 20, (1 << 31) - 1)
+                    for lo, hi in zip(bounds, bounds[1:]):
+                        ex, h = N.dr_export(), C.c_void_p()
+                        eng.check(eng.lib.dr_state_export_range(st.h, which, lo, hi, C.byref(h), C.byref(ex)))
+                        if rep == 0:
+                            nr += 1
+                            nrows += hi - lo
+                            nbytes += sum(v.nbytes for v in State._columns(ex).values())
+                        eng.check(eng.lib.dr_range_release(h))
+                passes.append(time.perf_counter() - t1)
+            st.release()
+            return {"ranges": nr, "rows": nrows, "bytes": nbytes, "first_s": round(passes[0], 4),
+                    "s": round(passes[1], 4), "gbs": round(nbytes / passes[1] / 1e9, 2),
+                    "note": "every dr_state_export_range of both sides at <= 1M rows / 2^31 - 1 B per column "
+                            "(plan included), into pinned host columns, released after each; first_s includes "
+                            "the device extraction of both sides"}
+
         rep_s, exp_first = export_once()   # the context's first export pins its host blocks
         rep2, exp_s = export_once()        # a later snapshot's: the context's pinned cache
         mat_s, mat_bytes = materialize_once()
+        rng = range_export_once()
         e2e = {"stage_s": round(stage_s, 3), "replay_s": round(rep2, 4),
                "materialize_s": round(mat_s, 4), "materialized_ms": round((rep2 + mat_s) * 1e3, 2),
                "materialized_bytes": mat_bytes, "export_s": round(exp_s, 4),
                "export_s_first_call": round(exp_first, 4),
                "export_beyond_materialize_s": round(exp_s - mat_s, 4),
+               "range_export": rng,
                "actions_per_s_incl_staging": round(counts["num_actions"] / (stage_s + rep2), 1),
                "actions_per_s_incl_staging_and_export": round(counts["num_actions"] / (stage_s + rep2 + exp_s), 1),
                "actions_per_s_incl_staging_and_first_export": round(

@@ -29,10 +29,14 @@ DR_LIVE, DR_TOMBSTONES = 0, 1
 DR_FLAG_NO_VALIDATION = 0x1
 DR_FLAG_EXACT_REDUCE = 0x2
 DR_FLAG_REDUCE64 = 0x4
+ABI_VERSION = 4  # include/deltareplay.h DR_ABI_VERSION
+# context options (include/deltareplay.h enum dr_option)
+OPTIONS = {"overlap": 1, "split": 2, "bucket_bits": 3, "filter_eval": 4, "apply_full": 5, "canon_hint": 6,
+           "json_staged": 7, "host_cache_bytes": 8}
 
 # Exported symbols (checked by tests/test_native_abi.py against include/deltareplay.h).
 SYMBOLS = [
-    "dr_abi_version", "dr_ctx_create", "dr_ctx_destroy", "dr_last_error", "dr_state_last_error",
+    "dr_abi_version", "dr_ctx_create", "dr_ctx_destroy", "dr_ctx_set_option", "dr_ctx_get_option", "dr_last_error", "dr_state_last_error",
     "dr_comm_last_error", "dr_log_segment",
     "dr_stage", "dr_stage_named", "dr_stage_log", "dr_comm_unique_id", "dr_comm_loopback_id", "dr_comm_create",
     "dr_comm_release",
@@ -133,6 +137,8 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "dr_abi_version": ([], C.c_int),
         "dr_ctx_create": ([C.c_int, C.POINTER(vp)], C.c_int),
         "dr_ctx_destroy": ([vp], None),
+        "dr_ctx_set_option": ([vp, i32, i64], C.c_int),
+        "dr_ctx_get_option": ([vp, i32, C.POINTER(i64)], C.c_int),
         "dr_last_error": ([vp], C.c_char_p),
         "dr_log_segment": ([vp, C.c_char_p, i64, C.c_char_p, u64, C.POINTER(u64), C.POINTER(i64)], C.c_int),
         "dr_stage": ([vp, C.POINTER(dr_file), i32, C.POINTER(vp)], C.c_int),

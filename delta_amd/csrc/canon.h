@@ -46,6 +46,7 @@ __device__ __forceinline__ void canon_one(const CanonArgs& a, uint64_t i) {
   }
   a.act.path_ptr[i] = reinterpret_cast<uint64_t>(res);
   a.act.path_len[i] = m;
+  if (a.act.path_ref) a.act.path_ref[i] = pack_ref(reinterpret_cast<uint64_t>(res), m);
   a.act.key[i] = path_key(kb, kn);
 }
 

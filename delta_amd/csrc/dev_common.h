@@ -114,6 +114,12 @@ __device__ inline uint64_t xxh64(const uint8_t* p, uint32_t len, uint64_t seed =
   h ^= h >> 32;
   return h;
 }
+// Packed path reference (k_bucket_verify's gathers): address | length << 48 (0: a length that does not
+// fit 16 bits; such a path sends its bucket to the exact reducer).
+__device__ __forceinline__ uint64_t pack_ref(uint64_t ptr, uint32_t len) {
+  return len < 0xffffu ? (ptr | (uint64_t(len) << 48)) : 0ull;
+}
+
 __device__ __forceinline__ uint64_t path_key(const uint8_t* p, uint32_t len) {
   const uint64_t h = xxh64(p, len);
   return h ? h : 1;

@@ -30,6 +30,7 @@
 #include <mutex>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "common.h"
@@ -113,7 +114,23 @@ struct dr_ctx {
   std::string err;
   bool timing = false;
   std::string timing_only;  // non-empty: only this kernel gets an event pair (dr_set_timing_only)
-  bool overlap = true;  // K1 line parsing on stream2 beside the checkpoint decode (bulk segments; DR_OVERLAP=0: off)
+  // Path-changing options, set per context through dr_ctx_set_option (include/deltareplay.h; the
+  // reference's per-session DeltaSQLConf, D/sources/DeltaSQLConf.scala:29): no process-global state
+  // picks a code path.
+  struct Options {
+    int64_t overlap = 1;       // DR_OPT_OVERLAP: K1 line parsing on stream2 beside the checkpoint decode
+    int64_t split = 1;         // DR_OPT_SPLIT: k_bucket_split for large replays (0: K4 sub-passes)
+    int64_t bucket_bits = -1;  // DR_OPT_BUCKET_BITS: cap on K3's bucket bits (-1: automatic)
+    int64_t filter_eval = 0;   // DR_OPT_FILTER_EVAL: 0 dictionary codes, 1 typed leaves, 2 generic interpreter
+    int64_t apply_full = 0;    // DR_OPT_APPLY_FULL: dr_state_apply always through K3/K4
+    int64_t canon_hint = -1;   // DR_OPT_CANON_HINT: arena bytes standing in for the first replay's sizing
+    int64_t json_staged = 0;   // DR_OPT_JSON_STAGED: every segment through the staged K1 kernel
+    int64_t host_cache_bytes = int64_t(16) << 30;  // DR_OPT_HOST_CACHE_BYTES: pinned blocks kept for reuse
+  } opt;
+  // Every entry point that takes this context (or a state, range, shard or communicator of it) holds
+  // this lock for the call: a context may be shared by host threads (several Spark tasks of one
+  // executor exporting ranges of one state), and the calls then run one at a time.
+  std::recursive_mutex api_mu;
   struct Mark {
     std::string name;
     hipEvent_t ev;
@@ -322,6 +339,7 @@ struct dr_ctx {
       auto it = host_free.lower_bound(n);
       if (it != host_free.end() && it->first <= 2 * n + (size_t(16) << 20)) {
         void* p = it->second;
+        host_free_bytes -= it->first;
         host_free.erase(it);
         return p;
       }
@@ -339,10 +357,22 @@ struct dr_ctx {
     host_sizes[p] = n;
     return p;
   }
+  // A released block joins the cache only while the cache stays within opt.host_cache_bytes (ADVICE
+  // r05: a large single-part checkpoint's block no longer stays pinned until the context ends);
+  // otherwise it is unpinned at once.
+  size_t host_free_bytes = 0;
   void host_release(void* p) {
     if (!p) return;
-    std::lock_guard<std::mutex> g(mu);
-    host_free.emplace(host_sizes[p], p);
+    std::unique_lock<std::mutex> g(mu);
+    const size_t n = host_sizes[p];
+    if (host_free_bytes + n > size_t(std::max<int64_t>(opt.host_cache_bytes, 0))) {
+      host_sizes.erase(p);
+      g.unlock();
+      (void)hipHostFree(p);
+      return;
+    }
+    host_free.emplace(n, p);
+    host_free_bytes += n;
   }
   void host_trim() {
     std::lock_guard<std::mutex> g(mu);
@@ -351,6 +381,7 @@ struct dr_ctx {
       host_sizes.erase(kv.second);
     }
     host_free.clear();
+    host_free_bytes = 0;
   }
   void trim() {
     std::lock_guard<std::mutex> g(mu);
@@ -741,6 +772,7 @@ struct dr_state {
   DBuf<uint64_t> key, path_ptr, src_off;
   DBuf<uint32_t> path_len, src_len;
   DBuf<int64_t> size, delts;
+  DBuf<uint64_t> path_ref;  // packed path references written by K1 / K2 / k_canon (parse_launch's states only)
   std::vector<std::shared_ptr<DBuf<uint8_t>>> arenas;  // canonical special paths (path_ptr targets)
   DBuf<uint32_t> live, tomb;   // survivor action indices (hash order per bucket)
   uint64_t n_live = 0, n_tomb = 0;
@@ -1596,11 +1628,11 @@ static std::shared_ptr<StagedData> stage_files(dr_ctx* ctx, const dr_file* files
 // ---------------------------------------------------------------------------------------------------
 // Buckets average <= 2048 file actions (the reduce keeps up to 3072 per pass in its 4096-slot LDS table), capped by the scatter's
 // LDS cursors; larger buckets are reduced in sub-passes.
-static int bucket_bits_for(uint64_t n) {
+static int bucket_bits_for(const dr_ctx* ctx, uint64_t n) {
   int bits = 0;
   while ((n >> bits) > 2048 && bits < int(part_max_bucket_bits())) ++bits;
-  // test hook: fewer, larger buckets (the reducer's sub-pass paths on a small table)
-  if (const char* e = std::getenv("DR_BUCKET_BITS")) bits = std::max(0, std::min(bits, std::atoi(e)));
+  // DR_OPT_BUCKET_BITS: fewer, larger buckets (the reducer's sub-pass paths on a small table)
+  if (ctx->opt.bucket_bits >= 0) bits = std::min<int>(bits, int(ctx->opt.bucket_bits));
   return bits;
 }
 
@@ -1677,7 +1709,7 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
   const bool one_block = nbj == 1;  // a streamed commit: index, placement and counter reset in one launch
   // K1 beside K2 on two streams: a checkpoint to decode and a JSON part of several index blocks
   // (r04: 10.43 -> 10.33 ms per config-3 step); small segments keep one stream and their fused paths
-  const bool overlap = ctx->overlap && s.ck_rows > 0 && nbj > 1;
+  const bool overlap = ctx->opt.overlap != 0 && s.ck_rows > 0 && nbj > 1;
   DBuf<uint32_t> jcounts(ctx, one_block ? 1 : nbj + 1);
   DBuf<uint64_t> joff(ctx, nbj + 1);
   DBuf<uint8_t> scratch(ctx, scan_scratch_for(nbj));
@@ -1712,12 +1744,13 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
   st->delts = DBuf<int64_t>(ctx, N);
   st->src_off = DBuf<uint64_t>(ctx, N);
   st->src_len = DBuf<uint32_t>(ctx, N);
+  st->path_ref = DBuf<uint64_t>(ctx, N);
   DBuf<uint64_t> nonfile(ctx, 2 * nlines);
   ActionArrays act{st->kind.p, st->flags.p, st->key.p, st->path_ptr.p, st->path_len.p, st->size.p, st->delts.p,
-                   st->src_off.p, st->src_len.p};
+                   st->src_off.p, st->src_len.p, st->path_ref.p};
   DBuf<uint64_t> hard(ctx, nlines);
   // For a segment with a checkpoint and a multi-block JSON part (`overlap`, on unless
-  // DR_OVERLAP=0), K1's line parsing runs on stream2 beside the checkpoint decode below (r04:
+  // DR_OPT_OVERLAP = 0), K1's line parsing runs on stream2 beside the checkpoint decode below (r04:
   // 10.43 -> 10.33 ms per config-3 step, k_snap_exec's time unchanged); stream waits for it before
   // anything reads the action arrays. The guard joins stream2 before any buffer it uses can be
   // released. Small segments run on one stream (and take the fused small-segment paths).
@@ -1748,6 +1781,8 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
                      nonfile.p, nlines, counters.p + 3, hard.p,
                      reinterpret_cast<unsigned long long*>(counters.p + 5)};
     ja.buf_len = json_len;
+    ja.force_staged = ctx->opt.json_staged ? 1u : 0u;
+    ja.path_ref = act.path_ref;
     if (fuse1) {
       ja.zero = counters.p;
       ja.nzero = 8;
@@ -1838,10 +1873,9 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
   if (canonicalize) {
     DR_STAGE("canonicalize", stream);
     int64_t hint = s.canon_need.load();
-    // test hook: DR_CANON_HINT=<bytes> stands in for the first replay's exact sizing (an undersized
-    // hint exercises the detect-and-redo path)
-    if (hint < 0)
-      if (const char* e = std::getenv("DR_CANON_HINT")) hint = std::max<int64_t>(0, std::atoll(e));
+    // DR_OPT_CANON_HINT=<bytes> stands in for the first replay's exact sizing (an undersized hint
+    // exercises the detect-and-redo path)
+    if (hint < 0 && ctx->opt.canon_hint >= 0) hint = ctx->opt.canon_hint;
     uint64_t cap = 0;
     if (hint < 0 && R == 0 && json_len <= (uint64_t(64) << 20)) {
       // a commit-only segment (an applied tail, a streamed commit): the bound from its bytes -- every
@@ -1999,16 +2033,21 @@ static ReducePending reduce_launch(dr_ctx* ctx, dr_state* st, int64_t cutoff, ui
   const uint64_t N = st->n_actions;
   // ---- K3: partition by hash bucket ----
   if (N >= (uint64_t(1) << 30)) fail(DR_E_UNSUPPORTED, "more than 2^30 actions in one replay shard");
-  const int bits = bucket_bits_for(N);
+  const int bits = bucket_bits_for(ctx, N);
   const uint32_t nb = 1u << bits;
   const uint32_t nt = part_tiles(N);
   const uint64_t ncell = uint64_t(nb) * nt;
   DBuf<uint32_t> tcnt(ctx, ncell);
   DBuf<uint64_t> toff(ctx, ncell + 1), boff(ctx, nb + 1);
   DBuf<uint8_t> pscratch(ctx, scan_scratch_for(ncell));
-  DBuf<uint64_t> pref(ctx, N);  // packed path references in action order (k_bucket_hist -> k_bucket_verify)
+  // packed path references in action order for k_bucket_verify: written by the producers beside
+  // path_ptr / path_len (parse_launch's states), else packed here by k_bucket_hist
+  const bool have_ref = st->path_ref.p && st->path_ref.n >= N;
+  DBuf<uint64_t> pref_own;
+  if (!have_ref) pref_own = DBuf<uint64_t>(ctx, N);
+  uint64_t* pref = have_ref ? st->path_ref.p : pref_own.p;
   PartitionArgs pa{st->kind.p, st->flags.p, st->key.p, st->size.p, st->delts.p, N, cutoff, bits, nt,
-                   tcnt.p, toff.p, nullptr, st->path_ptr.p, st->path_len.p, pref.p};
+                   tcnt.p, toff.p, nullptr, have_ref ? nullptr : st->path_ptr.p, st->path_len.p, pref};
   DBuf<PartRec> rec(ctx, N);
   pa.rec = rec.p;
   {
@@ -2019,13 +2058,10 @@ static ReducePending reduce_launch(dr_ctx* ctx, dr_state* st, int64_t cutoff, ui
     launch_bucket_scatter(pa, stream);
   }
   // ---- K3 refinement (large replays): buckets of more than 2048 records on average are split by the
-  // next key bits, so that K4 reduces each in one pass (k_bucket_split; DR_SPLIT=0 turns it off) ----
+  // next key bits, so that K4 reduces each in one pass (k_bucket_split; DR_OPT_SPLIT = 0 turns it off) ----
   int sbits = 0;
-  {
-    const char* e = std::getenv("DR_SPLIT");
-    if (!e || std::atoi(e) != 0)
-      while ((N >> (bits + sbits)) > 2048 && sbits < 6) ++sbits;
-  }
+  if (ctx->opt.split)
+    while ((N >> (bits + sbits)) > 2048 && sbits < 6) ++sbits;
   DBuf<PartRec> rec2;
   DBuf<uint64_t> boff2;
   const PartRec* krec = rec.p;
@@ -2046,7 +2082,7 @@ static ReducePending reduce_launch(dr_ctx* ctx, dr_state* st, int64_t cutoff, ui
   DBuf<uint2> opair(ctx, N);
   DBuf<unsigned long long> totals(ctx, 8), bstats(ctx, uint64_t(knb) * 5);
   totals.zero(stream);
-  ReduceArgs ra{krec, kboff, knb, kbits, st->size.p, st->path_ptr.p, st->path_len.p, olive.p, otomb.p, opair.p, pref.p,
+  ReduceArgs ra{krec, kboff, knb, kbits, st->size.p, st->path_ptr.p, st->path_len.p, olive.p, otomb.p, opair.p, pref,
                 lcount.p, tcount.p, pcount.p, totals.p, rlist.p, xlist.p, bstats.p, nullptr};
   // a timed replay (per-kernel mode) also counts the verifier's pairs and path bytes: its own byte
   // model beside the 69 B/action budget (bench.py "verify")
@@ -2521,7 +2557,7 @@ static dr_state* apply_tail(dr_ctx* ctx, dr_state& base, const std::shared_ptr<S
     }
     return all;
   };
-  const bool forced = (flags & (DR_FLAG_EXACT_REDUCE | DR_FLAG_REDUCE64)) || std::getenv("DR_APPLY_FULL");
+  const bool forced = (flags & (DR_FLAG_EXACT_REDUCE | DR_FLAG_REDUCE64)) || ctx->opt.apply_full;
   if (!forced) {
     std::shared_ptr<IncChain> ch;
     if (base.chain && base.gen == base.chain->head) ch = base.chain;
@@ -3789,6 +3825,24 @@ struct PartFile {
 static std::mutex g_pinned_out_mu;
 static std::unordered_map<void*, dr_ctx*> g_pinned_out;
 
+// A range outlives its state and its context: live ranges are registered in g_ranges, and
+// dr_ctx_destroy detaches those of its context (their blocks are then unpinned by dr_range_release
+// itself instead of returning to the context's cache).
+struct dr_range {
+  dr_ctx* ctx = nullptr;
+  void* block = nullptr;
+  dr_range() = default;
+  dr_range(const dr_range&) = delete;
+  dr_range& operator=(const dr_range&) = delete;
+  ~dr_range() {
+    if (!block) return;
+    if (ctx) ctx->host_release(block);
+    else (void)hipHostFree(block);
+  }
+};
+static std::mutex g_ranges_mu;
+static std::unordered_set<dr_range*> g_ranges;
+
 struct CkPartOut {
   uint8_t* data = nullptr;  // pinned (dr_ctx::host_alloc), registered in g_pinned_out
   uint64_t len = 0;
@@ -4395,7 +4449,7 @@ static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred)
     fa.cols[c] = pv_column(*col);
   }
   LeafPlan lp;
-  const bool force_generic = std::getenv("DR_FILTER_GENERIC") != nullptr;  // test hook: k_filter_typed
+  const bool force_generic = ctx->opt.filter_eval == 2;  // DR_OPT_FILTER_EVAL: k_filter_typed
   if (!force_generic && leafify(pred, lp) && lp.prog.size() / 2 <= filter_leaf_max_prog() &&
       lp.leaves.size() <= filter_leaf_max_leaves() && lp.i64.size() <= filter_leaf_max_i64() &&
       lp.str.size() <= filter_leaf_max_str()) {
@@ -4434,7 +4488,7 @@ static std::vector<int64_t> filter_state(dr_state& st, const dr_predicate& pred)
     // the dictionary path when every column the leaves read has a dictionary and the leaf tables fit
     std::vector<dr_state::PvCol*> ucols;
     for (int32_t u = 0; u < la.nucol; ++u) ucols.push_back(find(pred.col_names[la.ucol[u]], pred.col_types[la.ucol[u]]));
-    bool use_dict = la.nucol > 0 && st.n_live && std::getenv("DR_FILTER_NODICT") == nullptr;  // test hook
+    bool use_dict = la.nucol > 0 && st.n_live && ctx->opt.filter_eval == 0;  // DR_OPT_FILTER_EVAL
     for (dr_state::PvCol* c : ucols) {
       if (!use_dict || !c) { use_dict = false; break; }
       build_dict(st, *c);
@@ -5334,6 +5388,10 @@ static void parse_commits(dr_ctx* ctx, const std::shared_ptr<StagedData>& sp, dr
 namespace {
 template <typename F>
 int guard(dr_ctx* ctx, F&& f) {
+  // one call at a time per context (dr_ctx::api_mu): the context's streams, scratch, timing vectors and
+  // error text, and its states' lazily built members (materialize, the K5 cache), are shared
+  std::unique_lock<std::recursive_mutex> lk;
+  if (ctx) lk = std::unique_lock<std::recursive_mutex>(ctx->api_mu);
   try {
     f();
     if (ctx && dr_ctx::poison()) {
@@ -5372,14 +5430,20 @@ int dr_ctx_create(int device, dr_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return DR_E_DEVICE;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return DR_E_DEVICE;
   if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) return DR_E_DEVICE;
-  const char* ov = std::getenv("DR_OVERLAP");
-  c->overlap = !ov || std::atoi(ov) != 0;
   *out = c.release();
   return DR_OK;
 }
 
 void dr_ctx_destroy(dr_ctx* ctx) {
   if (!ctx) return;
+  {  // a call still running on another thread finishes first
+    std::lock_guard<std::recursive_mutex> g(ctx->api_mu);
+  }
+  {  // row ranges still held by the caller unpin their blocks on their own (dr_range_release)
+    std::lock_guard<std::mutex> g(g_ranges_mu);
+    for (dr_range* r : g_ranges)
+      if (r->ctx == ctx) r->ctx = nullptr;
+  }
   (void)hipStreamSynchronize(ctx->stream);
   (void)hipStreamSynchronize(ctx->stream2);
   ctx->trim();
@@ -5397,6 +5461,56 @@ void dr_ctx_destroy(dr_ctx* ctx) {
   (void)hipStreamDestroy(ctx->stream);
   (void)hipStreamDestroy(ctx->stream2);
   delete ctx;
+}
+
+static int64_t* option_slot(dr_ctx* ctx, int32_t option) {
+  dr_ctx::Options& o = ctx->opt;
+  switch (option) {
+    case DR_OPT_OVERLAP: return &o.overlap;
+    case DR_OPT_SPLIT: return &o.split;
+    case DR_OPT_BUCKET_BITS: return &o.bucket_bits;
+    case DR_OPT_FILTER_EVAL: return &o.filter_eval;
+    case DR_OPT_APPLY_FULL: return &o.apply_full;
+    case DR_OPT_CANON_HINT: return &o.canon_hint;
+    case DR_OPT_JSON_STAGED: return &o.json_staged;
+    case DR_OPT_HOST_CACHE_BYTES: return &o.host_cache_bytes;
+    default: return nullptr;
+  }
+}
+
+int dr_ctx_set_option(dr_ctx* ctx, int32_t option, int64_t value) {
+  if (!ctx) return DR_E_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(ctx->api_mu);
+  int64_t* v = option_slot(ctx, option);
+  bool ok = v != nullptr;
+  switch (option) {  // the accepted values (include/deltareplay.h)
+    case DR_OPT_OVERLAP: case DR_OPT_SPLIT: case DR_OPT_APPLY_FULL: case DR_OPT_JSON_STAGED:
+      ok = value == 0 || value == 1;
+      break;
+    case DR_OPT_BUCKET_BITS: ok = value >= -1 && value <= 32; break;
+    case DR_OPT_FILTER_EVAL: ok = value >= 0 && value <= 2; break;
+    case DR_OPT_CANON_HINT: ok = value >= -1; break;
+    case DR_OPT_HOST_CACHE_BYTES: ok = value >= 0; break;
+    default: break;
+  }
+  if (!ok) {
+    ctx->err = fmt("option %d: value %lld not accepted", int(option), (long long)value);
+    return DR_E_INVALID_ARG;
+  }
+  *v = value;
+  return DR_OK;
+}
+
+int dr_ctx_get_option(dr_ctx* ctx, int32_t option, int64_t* value) {
+  if (!ctx || !value) return DR_E_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(ctx->api_mu);
+  const int64_t* v = option_slot(ctx, option);
+  if (!v) {
+    ctx->err = fmt("unknown option %d", int(option));
+    return DR_E_INVALID_ARG;
+  }
+  *value = *v;
+  return DR_OK;
 }
 
 const char* dr_last_error(const dr_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
@@ -5580,6 +5694,7 @@ int dr_replay(dr_ctx* ctx, const dr_file* files, int32_t nfiles, int64_t cutoff,
 
 int dr_state_release(dr_state* state) {
   if (!state) return DR_OK;
+  std::lock_guard<std::recursive_mutex> g(state->ctx->api_mu);  // after any call using it on another thread
   (void)hipStreamSynchronize(state->ctx->stream);
   delete state;
   return DR_OK;
@@ -5708,16 +5823,6 @@ static int64_t* malloc_copy(const std::vector<int64_t>& v);
 // A host copy of rows [lo, hi) of one side's resident export columns, every offset array rebased to
 // the range (so no column of a range is larger than the caller planned: a JVM direct buffer holds
 // at most 2^31 - 1 bytes). One pinned block from the context's cache, returned by dr_range_release.
-struct dr_range {
-  dr_ctx* ctx = nullptr;
-  void* block = nullptr;
-  dr_range() = default;
-  dr_range(const dr_range&) = delete;
-  dr_range& operator=(const dr_range&) = delete;
-  ~dr_range() {
-    if (ctx && block) ctx->host_release(block);
-  }
-};
 
 // The eight row-level and eight entry-level offsets that bound rows [lo, hi) of X.
 struct RangeBounds {
@@ -5910,11 +6015,18 @@ int dr_state_export_range(dr_state* state, int32_t which, int64_t row_begin, int
     HIP_OK(hipSetDevice(state->ctx->device));
     auto R = std::make_unique<dr_range>();
     export_range(*state, which, uint64_t(row_begin), uint64_t(row_end), *R, out);
+    std::lock_guard<std::mutex> g(g_ranges_mu);
+    g_ranges.insert(R.get());
     *range = R.release();
   });
 }
 
 int dr_range_release(dr_range* range) {
+  if (!range) return DR_OK;
+  // the registry lock is held while the block returns to its context, so dr_ctx_destroy cannot free
+  // the context in between (it detaches ranges under the same lock)
+  std::lock_guard<std::mutex> g(g_ranges_mu);
+  if (!g_ranges.erase(range)) return DR_E_INVALID_ARG;  // not a live range (released twice)
   delete range;
   return DR_OK;
 }
@@ -6019,7 +6131,7 @@ void dr_free(void* p) {
     if (it != g_pinned_out.end()) {
       dr_ctx* ctx = it->second;
       g_pinned_out.erase(it);
-      g.unlock();
+      // (still under the lock: dr_ctx_destroy detaches its blocks under it before freeing the context)
       if (ctx) ctx->host_release(p);  // back to the context's pool
       else (void)hipHostFree(p);      // its context is gone
       return;
@@ -6038,18 +6150,21 @@ int dr_state_set_nonfile_json(dr_state* state, const char* lines, uint64_t len, 
 
 int dr_set_timing_only(dr_ctx* ctx, const char* kernel) {
   if (!ctx) return DR_E_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(ctx->api_mu);
   ctx->timing_only = kernel ? kernel : "";
   return DR_OK;
 }
 
 int dr_set_timing(dr_ctx* ctx, int32_t on) {
   if (!ctx) return DR_E_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(ctx->api_mu);
   ctx->timing = on != 0;
   return DR_OK;
 }
 
 int dr_last_timings(dr_ctx* ctx, char* names, uint64_t names_len, float* ms, int32_t cap, int32_t* n) {
   if (!ctx || !n) return DR_E_INVALID_ARG;
+  std::lock_guard<std::recursive_mutex> g(ctx->api_mu);
   std::string all;
   int32_t k = 0;
   for (auto& t : ctx->timings) {
@@ -6253,6 +6368,7 @@ int dr_parsed_release(dr_parsed* parsed) {
 
 int dr_shard_release(dr_shard* shard) {
   if (!shard) return DR_OK;
+  std::lock_guard<std::recursive_mutex> g(shard->ctx->api_mu);
   (void)hipStreamSynchronize(shard->ctx->stream);
   delete shard;
   return DR_OK;

@@ -201,6 +201,7 @@ __device__ __forceinline__ void emit_line(const JsonParseArgs& a, uint64_t line,
   a.key[idx] = key;
   a.path_ptr[idx] = path;
   a.path_len[idx] = plen;
+  if (a.path_ref) a.path_ref[idx] = pack_ref(path, plen);
   a.size[idx] = size;
   a.delts[idx] = delts;
   a.src_off[idx] = b;
@@ -903,8 +904,20 @@ __device__ __forceinline__ void tail_post_body(const JsonParseArgs& a, const Can
   // special paths so far (the walk's; the General walker's lines add theirs below)
   const uint64_t nsp0 = __hip_atomic_load(a.special_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   for (uint64_t k = threadIdx.x; k < cnt; k += blockDim.x) {
+    // The deferred line numbers (hard_idx) and the newline index (nl) become addresses here: the r05
+    // aperture violation in this kernel (k_tail_post, private_seg_size 272) read them from blocks
+    // released before this deferred launch, whose 0xA5 poison sent gp far outside the
+    // JSON buffer. The bounds build checks both against their extents and skips a bad line.
     const uint64_t line = a.hard_idx[k];
+    DR_LDS_CHECK(line < a.nlines, "tail_post deferred line (global)", line, a.nlines);
+#ifdef DR_BOUNDS_CHECK
+    if (line >= a.nlines) continue;
+#endif
     const uint64_t b = line == 0 ? 0 : a.nl[line - 1] + 1;
+    DR_LDS_CHECK(b <= a.nl[line] && a.nl[line] < a.buf_len, "tail_post line bytes (global)", a.nl[line], a.buf_len);
+#ifdef DR_BOUNDS_CHECK
+    if (!(b <= a.nl[line] && a.nl[line] < a.buf_len)) continue;
+#endif
     const uint32_t n = uint32_t(a.nl[line] - b);
     const uint8_t* gp = a.buf + b;
     jl::LineOut o;
@@ -1106,8 +1119,8 @@ void launch_json_index1(const uint8_t* buf, uint64_t len, uint64_t* nl, uint64_t
 void launch_json_parse(const JsonParseArgs& a, hipStream_t st) {
   if (!a.nlines) return;
   const dim3 grid(unsigned((a.nlines + dev::JL_T - 1) / dev::JL_T));
-  // DR_JSON_STAGED=1 (tests): every segment through the staged kernel, 64 lines per workgroup
-  if (a.nlines <= dev::JL_SMALL_LINES || std::getenv("DR_JSON_STAGED")) DR_LAUNCH(dev::k_json_lines<true>, grid, dim3(dev::JL_T), 0, st, a);
+  // DR_OPT_JSON_STAGED (tests): every segment through the staged kernel, 64 lines per workgroup
+  if (a.nlines <= dev::JL_SMALL_LINES || a.force_staged) DR_LAUNCH(dev::k_json_lines<true>, grid, dim3(dev::JL_T), 0, st, a);
   else DR_LAUNCH(dev::k_json_lines<false>, grid, dim3(dev::JL_T), 0, st, a);
 }
 

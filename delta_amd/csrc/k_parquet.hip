@@ -690,6 +690,7 @@ __global__ void k_ckpt_assemble(CkptAssembleArgs a) {
   a.act.key[idx] = key;
   a.act.path_ptr[idx] = reinterpret_cast<uint64_t>(path);
   a.act.path_len[idx] = plen;
+  if (a.act.path_ref) a.act.path_ref[idx] = pack_ref(reinterpret_cast<uint64_t>(path), plen);
   a.act.size[idx] = size;
   a.act.delts[idx] = delts;
   a.act.src_off[idx] = r;

@@ -99,10 +99,6 @@ __device__ __forceinline__ uint32_t bucket_of(uint64_t key, int bits) {
 // the 32 key bits directly below the bucket bits: the LDS table's probe start and sub-pass selector
 __device__ __forceinline__ uint32_t rkey_of(uint64_t key, int bits) { return uint32_t(key >> (32 - bits)); }
 
-// Packed path reference: address | length << 48 (0: a length that does not fit 16 bits).
-__device__ __forceinline__ uint64_t pack_ref(uint64_t ptr, uint32_t len) {
-  return len < 0xffffu ? (ptr | (uint64_t(len) << 48)) : 0ull;
-}
 // add.size in the record's 32-bit field; ~0u sends the reducer to size[] (negative or >= 2^32 - 1)
 __device__ __forceinline__ uint32_t size_field(int64_t s) {
   return (s >= 0 && s < int64_t(0xffffffffll)) ? uint32_t(s) : 0xffffffffu;
@@ -120,8 +116,9 @@ constexpr int PART_TILE = PART_T * 4 * PART_STEPS;      // 65536 actions per til
 constexpr int PART_MAX_BITS = 13;                       // LDS: 2 x 8192 x 4 B in the scatter (2 workgroups/CU)
 
 // Every thread owns 4 consecutive actions per step: one dword of kind bytes, one of flag bytes and
-// two 16-byte key loads; it also packs the actions' path references (address + length, in action
-// order) for k_bucket_verify's gathers: one 8-byte load per path there.
+// two 16-byte key loads (10 B per action). For a state whose producers did not write the packed path
+// references (address + length, in action order: one 8-byte load per path in k_bucket_verify's
+// gathers) it packs them here from path_ptr / path_len.
 __global__ void __launch_bounds__(PART_T) k_bucket_hist(PartitionArgs a) {
   __shared__ uint32_t hist[1 << PART_MAX_BITS];
   const uint32_t nb = 1u << a.bucket_bits;
@@ -129,6 +126,8 @@ __global__ void __launch_bounds__(PART_T) k_bucket_hist(PartitionArgs a) {
   __syncthreads();
   const uint32_t tile = blockIdx.x;
   const uint64_t base = uint64_t(tile) * PART_TILE;
+  // (block-uniform) the producers already wrote the packed path references (parse_launch's states)
+  const bool pack = a.path_ptr != nullptr;
   for (int k = 0; k < PART_STEPS; ++k) {
     const uint64_t i0 = base + (uint64_t(k) * PART_T + threadIdx.x) * 4;
     if (i0 >= a.n) break;
@@ -143,6 +142,7 @@ __global__ void __launch_bounds__(PART_T) k_bucket_hist(PartitionArgs a) {
       for (int j = 0; j < 4; ++j)
         if (is_file_action(uint8_t(kd >> (8 * j)), uint8_t(fl >> (8 * j))))
           atomicAdd(&hist[bucket_of(ks[j], a.bucket_bits)], 1u);
+      if (!pack) continue;
       const uint4 p01 = *reinterpret_cast<const uint4*>(a.path_ptr + i0);
       const uint4 p23 = *reinterpret_cast<const uint4*>(a.path_ptr + i0 + 2);
       const uint4 ln = *reinterpret_cast<const uint4*>(a.path_len + i0);
@@ -155,7 +155,7 @@ __global__ void __launch_bounds__(PART_T) k_bucket_hist(PartitionArgs a) {
     } else {
       for (uint64_t i = i0; i < a.n; ++i) {
         if (is_file_action(a.kind[i], a.flags[i])) atomicAdd(&hist[bucket_of(a.key[i], a.bucket_bits)], 1u);
-        a.path_ref[i] = pack_ref(a.path_ptr[i], a.path_len[i]);
+        if (pack) a.path_ref[i] = pack_ref(a.path_ptr[i], a.path_len[i]);
       }
     }
   }
@@ -261,7 +261,7 @@ __global__ void k_bucket_offsets(const uint64_t* tile_off, uint32_t nb, uint32_t
 
 // ---- per-bucket reduce ------------------------------------------------------------------------------
 constexpr int RED_T = DR_RED_T;
-constexpr int TS_MAX = 4096;  // LDS table slots: 8 B key + 4 B winner meta + 2 B count = 56 KiB, 2 WGs/CU
+constexpr int TS_MAX = 4096;  // LDS table slots: 8 B key + 4 B winner meta = 48 KiB, 3 WGs/CU
 // records per thread held in registers by a one-pass bucket (at most 3/4 TS_MAX records)
 constexpr int RED_RPT = (TS_MAX / 4 * 3 + RED_T - 1) / RED_T;
 
@@ -420,8 +420,8 @@ __device__ __forceinline__ uint4 shfl_down4(uint4 v, int width) {
 // both strings (a wave instruction requests eight whole paths of each side at once, every block
 // once) and takes block j + 1 from its neighbour by a shuffle; lanes 0..6 each compare 16 path
 // bytes, and the group ORs its differences. Unequal bytes get the URI-key comparison (file:/// vs
-// file:/ spellings) on the group's first lane. The pairs of a winner sit together (k_bucket_reduce
-// groups them), so the groups that share a winner fetch its reference and bytes once from HBM.
+// file:/ spellings) on the group's first lane. (r06: the reducer appends pairs in wave order and no
+// longer groups a winner's pairs -- its counting sort cost more in K4 than the shared fetches saved.)
 constexpr int VER_T = 256;
 __global__ void __launch_bounds__(VER_T) k_bucket_verify(ReduceArgs a) {
   const uint32_t b = blockIdx.x;
@@ -498,78 +498,101 @@ __global__ void __launch_bounds__(VER_T) k_bucket_verify(ReduceArgs a) {
   }
 }
 
-// Per-slot loser counts packed two to a word (slot s: word s >> 1, bits 16 (s & 1)): members - 1 of
-// each slot, replaced in place by each slot's first pair position (an exclusive scan over the n
-// slots, n <= TS_MAX, by one RED_T workgroup); returns the total. Counts and positions stay below
-// 2^16 (a sub-pass holds at most 3/4 TS_MAX records), so the halves never carry into each other.
-__device__ uint32_t scan_loser_slots(uint32_t* w, uint32_t n) {
-  __shared__ uint32_t wsum[RED_T / 64];
-  constexpr uint32_t PER = TS_MAX / 2 / RED_T;  // words per thread
-  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const uint32_t nw = n >> 1;
-  uint32_t v[2 * PER], s = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < PER; ++k) {
-    const uint32_t i = t * PER + k;
-    const uint32_t x = i < nw ? w[i] : 0u;
-    const uint32_t lo = x & 0xffffu, hi = x >> 16;
-    v[2 * k] = lo ? lo - 1u : 0u;
-    v[2 * k + 1] = hi ? hi - 1u : 0u;
-    s += v[2 * k] + v[2 * k + 1];
+// Table of ts slots (a multiple of 64, at most TS_MAX): a key's probe starts at its low 32 bits scaled
+// to ts (independent of the bucket and sub-pass bits, which sit above them), linear probing wraps.
+__device__ __forceinline__ uint32_t slot_start(uint64_t key, uint32_t ts) {
+  return uint32_t((uint64_t(uint32_t(key)) * ts) >> 32);
+}
+__device__ __forceinline__ uint32_t table_slots(uint64_t m) {
+  return uint32_t(min<uint64_t>(TS_MAX, max<uint64_t>(64, (2 * m + 63) & ~uint64_t(63))));
+}
+
+// Inserts key k with action meta z: table[k] = max(meta + 1) -- the largest action index wins.
+// Returns the slot, or ts when the table is full.
+__device__ __forceinline__ uint32_t table_insert(unsigned long long* tkey, uint32_t* tval, uint32_t ts,
+                                                 unsigned long long k, uint32_t z) {
+  uint32_t s = slot_start(k, ts);
+  for (uint32_t probe = 0; probe < ts; ++probe) {
+    const unsigned long long old = atomicCAS(&tkey[s], 0ull, k);
+    if (old == 0ull || old == k) {
+      atomicMax(&tval[s], z + 1u);
+      return s;
+    }
+    s = s + 1 == ts ? 0u : s + 1;
   }
-  uint32_t incl = s;
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(incl, o, 64);
-    if (lane >= uint32_t(o)) incl += y;
+  return ts;
+}
+
+// One record after the inserts: its slot's winner decides. Winners are classified (live add, kept
+// tombstone, or dropped); a loser is paired with its winner for k_bucket_verify.
+struct RedOut {
+  bool isl, ist, isp;
+  uint32_t idx, win;
+};
+__device__ __forceinline__ RedOut classify(const ReduceArgs& a, uint4 r, uint32_t w, uint64_t& size,
+                                           uint64_t& lks, uint64_t& tks) {
+  RedOut o{false, false, false, r.z >> 2, w >> 2};
+  const unsigned long long k = rec_key(r);
+  if (w == r.z) {
+    const uint32_t cls = r.z & 3;
+    if (cls == C_ADD) {
+      o.isl = true;
+      size += rec_size(a, r);
+      lks += k >> 32;
+    } else if (cls == C_REMOVE_KEEP) {
+      o.ist = true;
+      tks += k >> 32;
+    }
+  } else {
+    o.isp = true;
   }
-  if (lane == 63) wsum[wv] = incl;
+  return o;
+}
+
+// The bucket's {live, tomb, size, live sum, tomb sum}: the counts from the append counters, the sums
+// reduced over the workgroup (no contended global atomics: k_sum_stats adds the buckets).
+__device__ void store_sums(ReduceArgs& a, uint32_t b, uint32_t nl, uint32_t nt, uint64_t size, uint64_t lks,
+                           uint64_t tks) {
+  __shared__ unsigned long long red[3][RED_T / 64];
+  for (int o = 32; o > 0; o >>= 1) {
+    size += __shfl_down(size, o, 64);
+    lks += __shfl_down(lks, o, 64);
+    tks += __shfl_down(tks, o, 64);
+  }
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { red[0][wv] = size; red[1][wv] = lks; red[2][wv] = tks; }
   __syncthreads();
-  uint32_t base = 0, total = 0;
-  for (uint32_t q = 0; q < RED_T / 64; ++q) {
-    base += q < wv ? wsum[q] : 0u;
-    total += wsum[q];
+  if (threadIdx.x < 5) {
+    unsigned long long v = threadIdx.x == 0 ? nl : nt;
+    if (threadIdx.x >= 2) {
+      v = 0;
+      for (int k = 0; k < RED_T / 64; ++k) v += red[threadIdx.x - 2][k];
+    }
+    a.bstats[uint64_t(b) * 5 + threadIdx.x] = v;
   }
-  uint32_t run = base + incl - s;
-#pragma unroll
-  for (uint32_t k = 0; k < PER; ++k) {
-    const uint32_t i = t * PER + k;
-    const uint32_t lo = run;
-    run += v[2 * k];
-    if (i < nw) w[i] = lo | (run << 16);
-    run += v[2 * k + 1];
-  }
-  __syncthreads();
-  return total;
 }
 
 // K4: one workgroup per bucket. An LDS open-addressing table keyed by the full 64-bit path key keeps
 // atomicMax(meta + 1): the action with the largest (version, line) ordinal wins -- exactly the
-// reference's "last action per path". Survivors go to the bucket's region of the live / tombstone
-// lists; every loser is paired (by action index) with its winner for k_bucket_verify, the pairs
-// grouped by winner (a counting sort on the table slot), so the losers of one path sit next to each
-// other and the verifier's lane groups fetch their shared winner once. An LDS-table overflow sends
-// the bucket to the finer-grained fallback reducer.
+// reference's "last action per path" (D/actions/InMemoryLogReplay.scala:43-77). Survivors go to the
+// bucket's region of the live / tombstone lists; every loser is paired (by action index) with its
+// winner for k_bucket_verify. A bucket of up to 3/4 TS_MAX records is held in registers (loaded once,
+// all loads in flight before the first use) and each record keeps its table slot between the insert
+// and the classification; a larger one is reduced in sub-passes by the next key bits, re-read from
+// HBM. The table is sized to the bucket (2 slots per record), so its clearing costs what it holds.
+// An LDS-table overflow sends the bucket to the finer-grained fallback reducer.
 __global__ void __launch_bounds__(RED_T) k_bucket_reduce(ReduceArgs a) {
   __shared__ unsigned long long tkey[TS_MAX];
   __shared__ uint32_t tval[TS_MAX];
-  __shared__ uint32_t tcnt[TS_MAX / 2];  // u16 per slot: members, then its next pair position
-  __shared__ uint32_t nl, nt, overflow;
+  __shared__ uint32_t nl, nt, np, overflow;
   const uint32_t b = blockIdx.x;
   const int bits = a.bucket_bits;
   const uint64_t beg = a.bucket_off[b], end = a.bucket_off[b + 1];
   const uint64_t m = end - beg;
-  // sub-passes keep the records per pass at or under 3/4 of the table
-  int sbits = 0;
-  while ((m >> sbits) > uint64_t(TS_MAX / 4 * 3)) ++sbits;
-  uint32_t ts = 64;
-  while (ts < TS_MAX && uint64_t(ts) < 2 * (m >> sbits)) ts <<= 1;
-  const uint32_t mask = ts - 1;
-  if (threadIdx.x == 0) { nl = 0; nt = 0; overflow = 0; }
-  BucketTotals tot{0, 0, 0, 0, 0};
-  uint32_t pbase = 0;  // pairs of the earlier sub-passes
-  if (sbits == 0 && m <= uint64_t(RED_T) * RED_RPT) {
-    // one pass: every record of the bucket is loaded once, all loads issued before any is used, and
-    // kept in registers for both phases (the loop below re-reads them and waits on each load in turn)
+  if (threadIdx.x == 0) { nl = 0; nt = 0; np = 0; overflow = 0; }
+  uint64_t size = 0, lks = 0, tks = 0;
+  if (m <= uint64_t(RED_T) * RED_RPT) {
+    const uint32_t ts = table_slots(m);
     uint4 r[RED_RPT];
 #pragma unroll
     for (int q = 0; q < RED_RPT; ++q) {
@@ -577,135 +600,72 @@ __global__ void __launch_bounds__(RED_T) k_bucket_reduce(ReduceArgs a) {
       r[q] = e < end ? load_rec(a.rec, e) : make_uint4(0, 0, 0, 0);
     }
     for (uint32_t s = threadIdx.x; s < ts; s += RED_T) { tkey[s] = 0; tval[s] = 0; }
-    for (uint32_t s = threadIdx.x; s < ts / 2; s += RED_T) tcnt[s] = 0;
     __syncthreads();
+    uint32_t sl[RED_RPT];
 #pragma unroll
     for (int q = 0; q < RED_RPT; ++q) {
+      sl[q] = 0;
       if (beg + threadIdx.x + uint64_t(q) * RED_T >= end) continue;
-      const unsigned long long k = rec_key(r[q]);
-      uint32_t s = rkey_of(k, bits) & mask;
-      for (uint32_t probe = 0;; ++probe) {
-        if (probe >= ts) { overflow = 1; break; }
-        const unsigned long long old = atomicCAS(&tkey[s], 0ull, k);
-        if (old == 0ull || old == k) {
-          atomicMax(&tval[s], r[q].z + 1u);
-          atomicAdd(&tcnt[s >> 1], 1u << (16 * (s & 1)));
-          break;
-        }
-        s = (s + 1) & mask;
-      }
+      sl[q] = table_insert(tkey, tval, ts, rec_key(r[q]), r[q].z);
+      if (sl[q] == ts) overflow = 1;
     }
     __syncthreads();
     if (!overflow) {
-      pbase = scan_loser_slots(tcnt, ts);
 #pragma unroll
       for (int q = 0; q < RED_RPT; ++q) {
         const bool in = beg + threadIdx.x + uint64_t(q) * RED_T < end;
         if (!__ballot(in)) break;  // wave-uniform: later rows are past the bucket for every lane
-        bool isl = false, ist = false;
-        uint32_t idx = 0;
-        if (in) {
-          const unsigned long long k = rec_key(r[q]);
-          uint32_t s = rkey_of(k, bits) & mask;
-          while (tkey[s] != k) s = (s + 1) & mask;
-          const uint32_t w = tval[s] - 1u;
-          idx = r[q].z >> 2;
-          if (w == r[q].z) {
-            const uint32_t cls = r[q].z & 3;
-            if (cls == C_ADD) {
-              isl = true;
-              ++tot.live;
-              tot.size += rec_size(a, r[q]);
-              tot.lks += k >> 32;
-            } else if (cls == C_REMOVE_KEEP) {
-              ist = true;
-              ++tot.tomb;
-              tot.tks += k >> 32;
-            }
-          } else {
-            const uint32_t sh = 16 * (s & 1);
-            const uint32_t at = (atomicAdd(&tcnt[s >> 1], 1u << sh) >> sh) & 0xffffu;
-            a.out_pair[beg + at] = make_uint2(idx, w >> 2);
-          }
-        }
-        wave_append(isl, idx, &nl, a.out_live + beg);
-        wave_append(ist, idx, &nt, a.out_tomb + beg);
+        RedOut o{false, false, false, 0, 0};
+        if (in) o = classify(a, r[q], tval[sl[q]] - 1u, size, lks, tks);
+        wave_append(o.isl, o.idx, &nl, a.out_live + beg);
+        wave_append(o.ist, o.idx, &nt, a.out_tomb + beg);
+        wave_append2(o.isp, make_uint2(o.idx, o.win), &np, a.out_pair + beg);
       }
     }
-    sbits = -1;  // done: skip the general sub-pass loop
-  }
-  for (uint32_t sp = 0; sbits >= 0 && sp < (1u << sbits); ++sp) {
-    __syncthreads();
-    for (uint32_t s = threadIdx.x; s < ts; s += RED_T) { tkey[s] = 0; tval[s] = 0; }
-    for (uint32_t s = threadIdx.x; s < ts / 2; s += RED_T) tcnt[s] = 0;
-    __syncthreads();
-    // insert: table[key] = max(meta + 1) -- the largest action index wins
-    for (uint64_t e = beg + threadIdx.x; e < end; e += RED_T) {
-      const uint4 r = load_rec(a.rec, e);
-      const unsigned long long k = rec_key(r);
-      const uint32_t rk = rkey_of(k, bits);
-      if (sbits && (rk >> (32 - sbits)) != sp) continue;
-      uint32_t s = rk & mask;
-      for (uint32_t probe = 0;; ++probe) {
-        if (probe >= ts) { overflow = 1; break; }
-        const unsigned long long old = atomicCAS(&tkey[s], 0ull, k);
-        if (old == 0ull || old == k) {
-          atomicMax(&tval[s], r.z + 1u);
-          atomicAdd(&tcnt[s >> 1], 1u << (16 * (s & 1)));
-          break;
-        }
-        s = (s + 1) & mask;
-      }
-    }
-    __syncthreads();
-    if (overflow) break;
-    // losers per slot (members - 1), scanned: each slot's first pair position in this sub-pass
-    const uint32_t npass = scan_loser_slots(tcnt, ts);
-    for (uint64_t e0 = beg; e0 < end; e0 += RED_T) {
-      const uint64_t e = e0 + threadIdx.x;
-      bool isl = false, ist = false;
-      uint32_t idx = 0;
-      if (e < end) {
+  } else {
+    // sub-passes by the top sbits of the 32 key bits below the bucket bits, each at most 3/4 TS_MAX
+    // records on average
+    int sbits = 0;
+    while ((m >> sbits) > uint64_t(TS_MAX / 4 * 3)) ++sbits;
+    const uint32_t ts = TS_MAX;
+    for (uint32_t sp = 0; sp < (1u << sbits); ++sp) {
+      __syncthreads();
+      for (uint32_t s = threadIdx.x; s < ts; s += RED_T) { tkey[s] = 0; tval[s] = 0; }
+      __syncthreads();
+      for (uint64_t e = beg + threadIdx.x; e < end; e += RED_T) {
         const uint4 r = load_rec(a.rec, e);
-        const unsigned long long k = rec_key(r);
-        const uint32_t rk = rkey_of(k, bits);
-        if (!sbits || (rk >> (32 - sbits)) == sp) {
-          uint32_t s = rk & mask;
-          while (tkey[s] != k) s = (s + 1) & mask;
-          const uint32_t w = tval[s] - 1u;
-          idx = r.z >> 2;
-          if (w == r.z) {
-            const uint32_t cls = r.z & 3;
-            if (cls == C_ADD) {
-              isl = true;
-              ++tot.live;
-              tot.size += rec_size(a, r);
-              tot.lks += k >> 32;
-            } else if (cls == C_REMOVE_KEEP) {
-              ist = true;
-              ++tot.tomb;
-              tot.tks += k >> 32;
-            }
-          } else {
-            const uint32_t sh = 16 * (s & 1);
-            const uint32_t at = pbase + ((atomicAdd(&tcnt[s >> 1], 1u << sh) >> sh) & 0xffffu);
-            a.out_pair[beg + at] = make_uint2(idx, w >> 2);
+        if ((rkey_of(rec_key(r), bits) >> (32 - sbits)) != sp) continue;
+        if (table_insert(tkey, tval, ts, rec_key(r), r.z) == ts) overflow = 1;
+      }
+      __syncthreads();
+      if (overflow) break;
+      for (uint64_t e0 = beg; e0 < end; e0 += RED_T) {
+        const uint64_t e = e0 + threadIdx.x;
+        RedOut o{false, false, false, 0, 0};
+        if (e < end) {
+          const uint4 r = load_rec(a.rec, e);
+          const unsigned long long k = rec_key(r);
+          if ((rkey_of(k, bits) >> (32 - sbits)) == sp) {
+            uint32_t s = slot_start(k, ts);
+            while (tkey[s] != k) s = s + 1 == ts ? 0u : s + 1;
+            o = classify(a, r, tval[s] - 1u, size, lks, tks);
           }
         }
+        wave_append(o.isl, o.idx, &nl, a.out_live + beg);
+        wave_append(o.ist, o.idx, &nt, a.out_tomb + beg);
+        wave_append2(o.isp, make_uint2(o.idx, o.win), &np, a.out_pair + beg);
       }
-      wave_append(isl, idx, &nl, a.out_live + beg);
-      wave_append(ist, idx, &nt, a.out_tomb + beg);
     }
-    pbase += npass;
   }
   __syncthreads();
+  const uint32_t vl = nl, vt = nt;
   if (threadIdx.x == 0) {
-    a.live_count[b] = nl;
-    a.tomb_count[b] = nt;
-    a.pair_count[b] = overflow ? 0 : pbase;
+    a.live_count[b] = vl;
+    a.tomb_count[b] = vt;
+    a.pair_count[b] = overflow ? 0 : np;
     if (overflow) a.redo_list[atomicAdd(&a.totals[3], 1ull)] = b;
   }
-  store_totals(a, b, tot);
+  store_sums(a, b, vl, vt, size, lks, tks);
 }
 
 // Fallback for buckets whose LDS table overflowed (or every bucket, under the DR_FLAG_REDUCE64 test
@@ -1020,7 +980,9 @@ void launch_bucket_split(const SplitArgs& a, uint32_t nbuckets, hipStream_t st) 
 
 void launch_survivor_scan(const uint32_t* lc, const uint32_t* tc, uint32_t nb, uint64_t* loff, uint64_t* toff,
                           hipStream_t st) {
-  if (nb > uint32_t(dev::SSCAN_T) * 256) throw std::runtime_error("survivor scan: too many buckets");
+  // each thread scans a run of ceil(nb / 1024) buckets, so any count works (a 2^13-bucket
+  // K3 refined by 6 bits gives K4 2^19 buckets past ~2^29 actions); the bound only catches garbage
+  if (nb > (1u << 26)) throw std::runtime_error("survivor scan: too many buckets");
   DR_LAUNCH(dev::k_survivor_scan, dim3(1), dim3(dev::SSCAN_T), 0, st, lc, tc, nb, loff, toff);
 }
 

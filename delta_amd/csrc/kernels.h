@@ -41,6 +41,10 @@ struct ActionArrays {
   int64_t* delts;
   uint64_t* src_off;    // JSON: line offset in the JSON buffer; checkpoint: row index
   uint32_t* src_len;    // JSON: line length
+  // nullable: the packed path reference (path address | length << 48, 0 for a length >= 0xffff) that
+  // k_bucket_verify gathers, written by the producers beside path_ptr / path_len (so K3 need not
+  // re-read them); states built without it get it from k_bucket_hist
+  uint64_t* path_ref = nullptr;
 };
 
 struct JsonParseArgs {
@@ -74,6 +78,8 @@ struct JsonParseArgs {
   uint32_t nzero;
   uint64_t* off2;
   uint64_t* nl_out;  // = nl, writable (the fused index)
+  uint32_t force_staged;  // (host side) DR_OPT_JSON_STAGED: the staged kernel for every segment
+  uint64_t* path_ref;     // nullable: ActionArrays::path_ref
 };
 constexpr uint64_t JSON_FUSE_MAX_LINES = 64;
 

@@ -15,6 +15,7 @@ D/ = core/src/main/scala/org/apache/spark/sql/delta/ of the reference checkout.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import json
 import os
@@ -82,8 +83,8 @@ class Engine:
         if rc != N.DR_OK:
             raise DeltaError(rc, "cannot open HIP device %d (libdeltareplay needs an MI355X GPU)" % device)
         self.device = device
-        # a dr_ctx serves one host thread at a time (include/deltareplay.h): snapshots shared
-        # between threads (DeltaLog.for_table's cache) take this lock around every library call
+        # the library serialises the calls on one dr_ctx itself (ABI 4, include/deltareplay.h); this
+        # lock also keeps a multi-call sequence (set an option, then replay) of one thread together
         self.lock = threading.RLock()
 
     @classmethod
@@ -98,6 +99,32 @@ class Engine:
     def check(self, rc: int) -> None:
         if rc != N.DR_OK:
             raise DeltaError(rc, self.lib.dr_last_error(self.ctx).decode("utf-8", "replace"))
+
+    def set_option(self, name: str, value: int) -> int:
+        """dr_ctx_set_option (include/deltareplay.h enum dr_option, by its lower-case name without
+        DR_OPT_): the context's per-session configuration, as the reference reads DeltaSQLConf from
+        the session (D/sources/DeltaSQLConf.scala:29). Returns the previous value."""
+        with self.lock:
+            old = self.get_option(name)
+            self.check(self.lib.dr_ctx_set_option(self.ctx, N.OPTIONS[name], int(value)))
+        return old
+
+    def get_option(self, name: str) -> int:
+        v = C.c_int64()
+        self.check(self.lib.dr_ctx_get_option(self.ctx, N.OPTIONS[name], C.byref(v)))
+        return v.value
+
+    @contextlib.contextmanager
+    def options(self, **opts):
+        """Sets context options for the body of a `with` and restores them after (tests)."""
+        old = {}
+        try:
+            for k, v in opts.items():
+                old[k] = self.set_option(k, v)
+            yield self
+        finally:
+            for k, v in old.items():
+                self.set_option(k, v)
 
     def set_timing(self, on: bool, only: Optional[str] = None) -> None:
         """dr_set_timing (+ dr_set_timing_only: events around one kernel only)."""

@@ -7,9 +7,13 @@
  * (paths relative to the reference checkout, D/ = core/src/main/scala/org/apache/spark/sql/delta/).
  *
  * Conventions: plain pointers and sizes only; every call returns an int status (DR_OK = 0) and
- * leaves a message in dr_last_error(ctx). One dr_ctx per host thread / HIP stream; calls on
- * distinct contexts are thread-safe. The library owns every device and host buffer it returns
- * until the matching *_release call (Snapshot.uncache, D/util/StateCache.scala:104-109).
+ * leaves a message in dr_last_error(ctx). Calls on distinct contexts run concurrently; calls that
+ * share a context (directly, or through a state, range, shard or communicator of it) may come from
+ * several host threads and run one at a time (a per-context lock; ABI 4) -- dr_last_error then holds
+ * the message of the latest failed call of any of them. A host that releases a state must not call
+ * with it afterwards (the JNI glue reference-counts states, jni/DeltaReplayStateRDD.scala). The
+ * library owns every device and host buffer it returns until the matching *_release call
+ * (Snapshot.uncache, D/util/StateCache.scala:104-109).
  */
 #ifndef DELTAREPLAY_H
 #define DELTAREPLAY_H
@@ -27,8 +31,11 @@ extern "C" {
  *      DR_T_FLOAT .. DR_T_DECIMAL (partitionValues_parsed of the checkpoint writer);
  *      dr_state_local_counts, dr_state_last_error, dr_comm_last_error, dr_state_materialize
  *   3  dr_state_export_plan, dr_state_export_range, dr_range_release (row-range exports whose columns
- *      each fit a bound, e.g. a JVM direct buffer's 2^31 - 1 bytes) */
-#define DR_ABI_VERSION 3
+ *      each fit a bound, e.g. a JVM direct buffer's 2^31 - 1 bytes)
+ *   4  dr_ctx_set_option / dr_ctx_get_option (every path-changing choice is a context option; the
+ *      library reads no environment variable that changes a result or a code path); a context may be
+ *      shared by threads; a range outlives its context */
+#define DR_ABI_VERSION 4
 
 /* Status codes. The JNI shim rethrows the reference's exception class with dr_last_error():
  *   DR_E_EMPTY_DIR / DR_E_LOG_TRUNCATED -> FileNotFoundException (D/DeltaErrors.scala:451-457,915-917)
@@ -123,7 +130,38 @@ typedef struct dr_staged dr_staged;
 /* ---- context ------------------------------------------------------------------------------ */
 /* Creates a context bound to HIP device `device` with its own stream. */
 int dr_ctx_create(int device, dr_ctx** out);
+/* Waits for any call running on the context, then frees it. States, staged segments, shards and
+ * communicators of the context must be released first; row ranges and checkpoint part files may
+ * outlive it (their pinned blocks are then unpinned by dr_range_release / dr_free). */
 void dr_ctx_destroy(dr_ctx* ctx);
+
+/* Context options (ABI 4): the per-session configuration of the path, as the reference takes its
+ * DeltaSQLConf from the session (D/sources/DeltaSQLConf.scala:29). Set before the calls they should
+ * affect; they change code paths and resource use, never results (every choice is parity-tested).
+ * DR_E_INVALID_ARG for an unknown option or a value outside its range. Debug-only switches (phase
+ * clocks, poisoning, roctx ranges, dumps) stay environment variables and change no result. */
+enum dr_option {
+  DR_OPT_OVERLAP = 1,          /* 1 (default): K1 line parsing on a second stream beside the checkpoint
+                                  decode for segments with a checkpoint and a multi-block JSON part; 0: one stream */
+  DR_OPT_SPLIT = 2,            /* 1 (default): replays of more than 2^13 * 2048 actions refine K3's buckets
+                                  (k_bucket_split) so K4 reduces each in one pass; 0: K4's sub-passes */
+  DR_OPT_BUCKET_BITS = 3,      /* -1 (default): automatic; n in 0..32: at most n K3 bucket bits (fewer,
+                                  larger buckets: the reducer's sub-pass paths) */
+  DR_OPT_FILTER_EVAL = 4,      /* dr_filter's evaluator: 0 (default) dictionary codes where every column has
+                                  one, else typed leaves; 1 typed leaves (k_filter_leaf); 2 the generic
+                                  postfix interpreter (k_filter_typed) */
+  DR_OPT_APPLY_FULL = 5,       /* 0 (default); 1: dr_state_apply reduces base survivors + tail through K3/K4
+                                  instead of the O(tail) path index */
+  DR_OPT_CANON_HINT = 6,       /* -1 (default): a segment's first replay sizes the canonicalisation arena
+                                  exactly (one read-back); n >= 0: n bytes stand in for that sizing (an
+                                  undersized arena is detected and the parse redone) */
+  DR_OPT_JSON_STAGED = 7,      /* 0 (default); 1: every JSON segment through the staged, wave-cooperative
+                                  K1 kernel (the streamed-commit walker) instead of the lane-per-line one */
+  DR_OPT_HOST_CACHE_BYTES = 8  /* bytes of released pinned host blocks kept for reuse (default 16 GiB);
+                                  a block that would exceed it is unpinned at release */
+};
+int dr_ctx_set_option(dr_ctx* ctx, int32_t option, int64_t value);
+int dr_ctx_get_option(dr_ctx* ctx, int32_t option, int64_t* value);
 const char* dr_last_error(const dr_ctx* ctx);
 /* The message of the last failed call on a state / communicator (its context's dr_last_error), for
  * hosts that keep only the state or communicator handle (the JNI glue, jni/deltareplay_jni.c). */
@@ -223,7 +261,8 @@ int dr_state_export(dr_state* state, int32_t which, dr_export* out);
  * whose offsets are rebased to the range (path_off[0] = 0, entry offsets count from the range's first
  * entry, byte offsets from its first byte): the concatenation of consecutive ranges' columns, offsets
  * shifted back, equals dr_state_export's. The columns are host memory owned by *range until
- * dr_range_release (independent of the state: it may be released first). */
+ * dr_range_release (independent of the state and of the context: either may be released first).
+ * dr_range_release of a range that is not live (released twice) returns DR_E_INVALID_ARG. */
 typedef struct dr_range dr_range;
 int dr_state_export_plan(dr_state* state, int32_t which, int64_t max_rows, uint64_t max_bytes, int64_t** bounds,
                          int64_t* nranges);

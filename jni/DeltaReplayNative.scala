@@ -16,13 +16,17 @@ object DeltaReplayNative {
   System.loadLibrary("deltareplay_jni")   // links libdeltareplay.so
 
   /** include/deltareplay.h DR_ABI_VERSION this binding was written against. */
-  val AbiVersion = 3
+  val AbiVersion = 4
   require(abiVersion() == AbiVersion,
     s"libdeltareplay ABI ${abiVersion()} does not match the binding's $AbiVersion")
 
   @native def abiVersion(): Int
   @native def ctxCreate(device: Int): Long
   @native def ctxDestroy(ctx: Long): Unit
+  /** dr_ctx_set_option (ABI 4): one of the Opt* options below, set from the session's conf. */
+  @native def setOption(ctx: Long, option: Int, value: Long): Unit
+  val OptOverlap = 1; val OptSplit = 2; val OptBucketBits = 3; val OptFilterEval = 4; val OptApplyFull = 5
+  val OptCanonHint = 6; val OptJsonStaged = 7; val OptHostCacheBytes = 8
   // Text crosses the boundary as UTF-8 bytes (the *Utf8 natives): JNI's string calls use modified
   // UTF-8, which would corrupt characters outside the BMP in table paths and metaData values. The
   // String-typed methods below convert with StandardCharsets.UTF_8.

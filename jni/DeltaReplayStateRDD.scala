@@ -28,26 +28,67 @@ import org.apache.spark.sql.delta.actions.SingleAction
 import org.apache.spark.sql.execution.LogicalRDD
 
 /**
+ * One library context per GPU of this JVM, shared by every Snapshot and task on it (ABI 4: the library
+ * serialises the calls that share a context). Options are the session's configuration of the path
+ * (dr_ctx_set_option; the binding's Opt* constants), applied when the context is created.
+ */
+object DeltaReplayContexts {
+  private val ctxs = new ConcurrentHashMap[Integer, java.lang.Long]()
+
+  def forDevice(device: Int, options: Map[Int, Long] = Map.empty): Long =
+    ctxs.computeIfAbsent(device, (d: Integer) => {
+      val c = DeltaReplayNative.ctxCreate(d)
+      options.foreach { case (k, v) => DeltaReplayNative.setOption(c, k, v) }
+      java.lang.Long.valueOf(c)
+    })
+}
+
+/**
  * The states resident in this JVM, by (snapshot key, rank). A state is registered by the task that
  * replayed it and removed by Snapshot.uncache (D/util/StateCache.scala:104-109), which releases it.
+ * Several tasks of one executor may export ranges of a state at once (the library serialises calls on
+ * its context); every user holds a reference (`use`), and an uncache that arrives while tasks still
+ * export only marks the state: the last user's return releases it (no call on a released state).
  */
 object DeltaReplayStates {
-  private val states = new ConcurrentHashMap[(String, Int), java.lang.Long]()
+  private final class Entry(val state: Long) {
+    var users = 0
+    var released = false
+  }
+  private val states = new ConcurrentHashMap[(String, Int), Entry]()
 
-  def put(key: String, rank: Int, state: Long): Unit = states.put((key, rank), state)
+  def put(key: String, rank: Int, state: Long): Unit = states.put((key, rank), new Entry(state))
 
-  def get(key: String, rank: Int): Long = {
-    val s = states.get((key, rank))
-    if (s == null) {
+  private def entry(key: String, rank: Int): Entry = {
+    val e = states.get((key, rank))
+    if (e == null) {
       throw new IllegalStateException(s"the GPU state of snapshot $key rank $rank is not resident on this executor")
     }
-    s
+    e
   }
 
-  /** Removes and releases (dr_state_release) a rank's state; ranges already exported stay valid. */
+  /** Runs f on the state with a reference held: release waits for it (the state stays resident). */
+  def use[T](key: String, rank: Int)(f: Long => T): T = {
+    val e = entry(key, rank)
+    e.synchronized {
+      if (e.released) throw new IllegalStateException(s"the GPU state of snapshot $key rank $rank was uncached")
+      e.users += 1
+    }
+    try f(e.state)
+    finally e.synchronized {
+      e.users -= 1
+      if (e.released && e.users == 0) DeltaReplayNative.release(e.state)
+    }
+  }
+
+  /** Removes a rank's state and releases it (dr_state_release) now, or when its last user returns;
+   * ranges already exported stay valid either way. */
   def release(key: String, rank: Int): Unit = {
-    val s = states.remove((key, rank))
-    if (s != null) DeltaReplayNative.release(s)
+    val e = states.remove((key, rank))
+    if (e != null) e.synchronized {
+      e.released = true
+      if (e.users == 0) DeltaReplayNative.release(e.state)
+    }
   }
 
   /** This executor's location for a partition that must run here (the rank's state lives here). */
@@ -67,10 +108,11 @@ final case class RankPlan(rank: Int, location: String, live: Array[Long], tombst
 object RankPlan {
   /** exportPlan of the state registered as (key, rank) in this JVM. */
   def local(key: String, rank: Int, maxRows: Long): RankPlan = {
-    val st = DeltaReplayStates.get(key, rank)
-    RankPlan(rank, DeltaReplayStates.here,
-      DeltaReplayNative.exportPlan(st, DeltaReplayNative.Live, maxRows, DeltaReplayNative.MaxBufferBytes),
-      DeltaReplayNative.exportPlan(st, DeltaReplayNative.Tombstones, maxRows, DeltaReplayNative.MaxBufferBytes))
+    DeltaReplayStates.use(key, rank) { st =>
+      RankPlan(rank, DeltaReplayStates.here,
+        DeltaReplayNative.exportPlan(st, DeltaReplayNative.Live, maxRows, DeltaReplayNative.MaxBufferBytes),
+        DeltaReplayNative.exportPlan(st, DeltaReplayNative.Tombstones, maxRows, DeltaReplayNative.MaxBufferBytes))
+    }
   }
 }
 
@@ -85,9 +127,9 @@ class DeltaReplayStateRDD(sc: SparkContext, key: String, ranges: Array[StateRang
 
   override def compute(p: Partition, ctx: TaskContext): Iterator[InternalRow] = {
     val r = p.asInstanceOf[StateRangePartition]
-    val state = DeltaReplayStates.get(key, r.rank)  // fails loudly if scheduled off the rank's executor
     val handle = new Array[Long](1)
-    val cols = DeltaReplayNative.exportRange(state, r.which, r.lo, r.hi, handle)
+    // fails loudly if scheduled off the rank's executor; an uncache meanwhile waits for the export
+    val cols = DeltaReplayStates.use(key, r.rank)(st => DeltaReplayNative.exportRange(st, r.which, r.lo, r.hi, handle))
     ctx.addTaskCompletionListener[Unit](_ => DeltaReplayNative.rangeRelease(handle(0)))
     val toRow = DeltaReplayState.serializer()
     val actions: Iterator[SingleAction] =

@@ -163,6 +163,16 @@ NATIVE(void, ctxDestroy)(JNIEnv* env, jobject self, jlong ctx) {
   dr_ctx_destroy((dr_ctx*)(intptr_t)ctx);
 }
 
+/* dr_ctx_set_option (ABI 4): the session's configuration of the path (DeltaSQLConf); a rejected
+ * option or value raises IllegalArgumentException with the library's message. */
+NATIVE(void, setOption)(JNIEnv* env, jobject self, jlong ctx, jint option, jlong value) {
+  (void)self;
+  if (dr_ctx_set_option((dr_ctx*)(intptr_t)ctx, (int32_t)option, (int64_t)value) != DR_OK) {
+    jclass c = (*env)->FindClass(env, "java/lang/IllegalArgumentException");
+    if (c) (*env)->ThrowNew(env, c, "dr_ctx_set_option: option or value not accepted");
+  }
+}
+
 NATIVE(jbyteArray, lastErrorUtf8)(JNIEnv* env, jobject self, jlong ctx) {
   (void)self;
   const char* m = dr_last_error((const dr_ctx*)(intptr_t)ctx);

@@ -20,6 +20,10 @@ def main():
         S.build_config(args.config, d, scale=args.scale, keep_ids=False)
     exp = S.build_config.__module__ and None
     eng = Engine.get(0)
+    # context options for the profiled replays: PROF_OPTS="bucket_bits=12,split=0" (dr_ctx_set_option)
+    for kv in filter(None, os.environ.get("PROF_OPTS", "").split(",")):
+        k, v = kv.split("=")
+        eng.set_option(k, int(v))
     staged = eng.stage_log(os.path.join(d, "_delta_log"))
     for _ in range(args.reps):
         st = staged.replay(0)

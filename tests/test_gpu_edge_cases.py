@@ -163,9 +163,9 @@ def test_checkpoint_rows_with_absolute_paths(engine, tmp_path):
 
 
 @pytest.mark.parametrize("hint", ["0", "16", "1000000"])
-def test_canonicalisation_arena_hint(engine, tmp_path, monkeypatch, hint):
+def test_canonicalisation_arena_hint(engine, tmp_path, request, hint):
     """A replay queues k_canon with an arena sized from the segment's last need (no read-back before
-    K3); DR_CANON_HINT stands in for that need on the first replay. An arena too small (no arena at
+    K3); the context option DR_OPT_CANON_HINT stands in for that need on the first replay. An arena too small (no arena at
     all, 16 bytes) is detected after the replay and the replay redone at the exact size; an ample one
     is used as is. Every case, and a second replay of the same staged segment, equals the oracle."""
     lp = str(tmp_path / "_delta_log")
@@ -173,7 +173,8 @@ def test_canonicalisation_arena_hint(engine, tmp_path, monkeypatch, hint):
                          add("rel/three.parquet")],
                  raw_lines=['{"add":{"path":"\\/abs\\/four.parquet","size":4,"modificationTime":1,"dataChange":true}}'])
     write_commit(lp, 1, [remove("file:///abs/one.parquet"), remove("/abs/two.parquet", ts=300)])
-    monkeypatch.setenv("DR_CANON_HINT", hint)
+    engine.set_option("canon_hint", int(hint))
+    request.addfinalizer(lambda: engine.set_option("canon_hint", -1))
     snap = O.state_reconstruction(O.get_log_segment(lp), 250)
     staged = engine.stage_log(lp)
     try:
@@ -353,13 +354,11 @@ def test_noncontiguous_and_empty(engine, tmp_path):
 
 
 # ---- K1 device walker fuzz ---------------------------------------------------------------------------------
-def _walker_mode(monkeypatch, staged):
+def _walker_mode(engine, request, staged):
     """staged: every 64-line wave through the small-segment kernel (LDS stage, token tape, the
-    wave-parallel tape walk) instead of the bulk per-lane walker."""
-    if staged:
-        monkeypatch.setenv("DR_JSON_STAGED", "1")
-    else:
-        monkeypatch.delenv("DR_JSON_STAGED", raising=False)
+    wave-parallel tape walk; context option DR_OPT_JSON_STAGED) instead of the bulk per-lane walker."""
+    engine.set_option("json_staged", 1 if staged else 0)
+    request.addfinalizer(lambda: engine.set_option("json_staged", 0))
 
 
 def _device_lines(engine, lines):
@@ -382,11 +381,11 @@ def _device_view(rec):
 
 
 @pytest.mark.parametrize("staged", [False, True])
-def test_device_walker_matches_fuzz_corpus(engine, monkeypatch, staged):
+def test_device_walker_matches_fuzz_corpus(engine, request, staged):
     """Every corpus line (golden logs, synthetic formats, hand-written edge cases) at 16 byte
     alignments, through k_json_lines / k_json_hard on the GPU, against the PERMISSIVE-reader
     restatement that the host build of the walker is fuzzed against."""
-    _walker_mode(monkeypatch, staged)
+    _walker_mode(engine, request, staged)
     from tests.test_json_lane import corpus, expected
     base = [l for l in corpus() if b"\n" not in l]
     lines = []
@@ -401,8 +400,8 @@ def test_device_walker_matches_fuzz_corpus(engine, monkeypatch, staged):
 
 
 @pytest.mark.parametrize("staged", [False, True])
-def test_device_walker_mutations(engine, monkeypatch, staged):
-    _walker_mode(monkeypatch, staged)
+def test_device_walker_mutations(engine, request, staged):
+    _walker_mode(engine, request, staged)
     from tests.test_json_lane import K_ADD, K_ERROR, corpus, expected, mutate
     rng = random.Random(0xDE17B)
     base = corpus()
@@ -579,14 +578,14 @@ def _writer_clean(line: bytes) -> bool:
 
 
 @pytest.mark.parametrize("staged", [False, True])
-def test_device_walker_writer_shaped_waves(engine, monkeypatch, staged):
+def test_device_walker_writer_shaped_waves(engine, request, staged):
     """k_json_lines against the PERMISSIVE restatement on whole 64-line waves of writer-shaped
     lines (clean corpus lines and their clean mutations) at all 16 byte skews, with backslash runs
     and escaped quotes at every window offset, scalars of every length up to 19 digits, strings on
     both sides of the fast walker's 4096-byte single-token limit and nesting past its depth limit
     (the General walker's deferral), followed by unrestricted mutations. (The same test checked the
     r02 wave-cooperative tokenizer experiment)"""
-    _walker_mode(monkeypatch, staged)
+    _walker_mode(engine, request, staged)
     from tests.test_json_lane import corpus, expected, mutate
     base = [l for l in corpus() if b"\n" not in l]
     rng = random.Random(0x7A9E)

@@ -109,3 +109,93 @@ def test_config4_through_range_exports(engine, tmp_path):
         assert len(b) > 8
     finally:
         st.release()
+
+
+def _native_range(st, which, lo, hi):
+    import ctypes as C
+    from delta_amd import _native as N
+    e, h = N.dr_export(), C.c_void_p()
+    st.eng.check(st.eng.lib.dr_state_export_range(st.h, which, int(lo), int(hi), C.byref(h), C.byref(e)))
+    return h, e
+
+
+def _check_native(full, e, lo, hi):
+    from delta_amd.delta_log import State
+    _check_range(full, {k: v.copy() for k, v in State._columns(e).items()}, lo, hi, 1 << 40)
+
+
+def test_range_outlives_its_state_and_context(tmp_path):
+    """The contract the JNI RDD relies on (include/deltareplay.h, ABI 4), at the C ABI: a range's host
+    columns stay readable after dr_state_release and after dr_ctx_destroy, dr_range_release then
+    unpins them (the destroyed context's cache is not touched), and a second release of the same
+    range is refused instead of freeing twice."""
+    from delta_amd import _native as N
+    from delta_amd.delta_log import Engine
+    from delta_amd.testing import synth as S
+    exp = S.build_config(3, str(tmp_path), scale=0.003)
+    eng = Engine(0)  # a context of its own: destroyed below
+    staged = eng.stage_log(os.path.join(str(tmp_path), "_delta_log"))
+    st = staged.replay(exp.min_file_retention_timestamp)
+    staged.release()
+    full = {k: v.copy() for k, v in st.export_columns(0).items()}
+    tfull = {k: v.copy() for k, v in st.export_columns(1).items()}
+    n, nt = len(full["path_off"]) - 1, len(tfull["path_off"]) - 1
+    h1, e1 = _native_range(st, 0, 5, n // 2)
+    h2, e2 = _native_range(st, 0, n // 2, n)
+    h3, e3 = _native_range(st, 1, 0, nt)
+    st.release()
+    _check_native(full, e1, 5, n // 2)  # the state is gone
+    assert eng.lib.dr_range_release(h1) == N.DR_OK
+    assert eng.lib.dr_range_release(h1) == 1  # DR_E_INVALID_ARG: not a live range any more
+    eng.lib.dr_ctx_destroy(eng.ctx)
+    eng.ctx = None
+    _check_native(full, e2, n // 2, n)  # the context is gone
+    _check_native(tfull, e3, 0, nt)
+    assert eng.lib.dr_range_release(h2) == N.DR_OK
+    assert eng.lib.dr_range_release(h3) == N.DR_OK
+
+
+def test_concurrent_range_exports_share_one_context(tmp_path):
+    """Several host threads (a Spark executor's concurrent tasks) export ranges of one state through
+    one context at once: the library serialises the calls (ABI 4), the first one materialises the
+    side, and every range equals the full export's rows."""
+    import threading
+    from delta_amd import _native as N
+    from delta_amd.delta_log import Engine
+    from delta_amd.testing import synth as S
+    exp = S.build_config(3, str(tmp_path), scale=0.003)
+    eng = Engine(0)
+    staged = eng.stage_log(os.path.join(str(tmp_path), "_delta_log"))
+    st = staged.replay(exp.min_file_retention_timestamp)
+    staged.release()
+    try:
+        # the ranges first, on a state whose export is not built yet (the threads race to build it)
+        n = st.counts["num_files"]
+        nt = st.counts["num_removes"]
+        jobs = [(0, lo, min(n, lo + 997)) for lo in range(0, n, 997)] + [(1, 0, nt)]
+        got, errs = {}, []
+        go = threading.Barrier(8)
+
+        def worker(k):
+            try:
+                go.wait()
+                for j in range(k, len(jobs), 8):
+                    which, lo, hi = jobs[j]
+                    h, e = _native_range(st, which, lo, hi)  # no Python lock: straight into the library
+                    from delta_amd.delta_log import State
+                    got[j] = {c: v.copy() for c, v in State._columns(e).items()}
+                    assert eng.lib.dr_range_release(h) == N.DR_OK
+            except Exception as ex:  # noqa: BLE001 (reported below)
+                errs.append(repr(ex))
+
+        ts = [threading.Thread(target=worker, args=(k,)) for k in range(8)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(120)
+        assert not errs, errs
+        full = {0: st.export_columns(0), 1: st.export_columns(1)}
+        for j, (which, lo, hi) in enumerate(jobs):
+            _check_range(full[which], got[j], lo, hi, 1 << 40)
+    finally:
+        st.release()

@@ -47,16 +47,13 @@ def _oracle_selected(lp, preds_list, cutoff=0):
 @pytest.mark.parametrize("checkpoint", [False, True])
 @pytest.mark.parametrize("escaped_keys", [False, True])
 @pytest.mark.parametrize("kernel", ["dict", "typed", "generic"])
-def test_filter_cast_corpus(engine, tmp_path, monkeypatch, checkpoint, escaped_keys, kernel):
-    """The three K5 evaluators: the leaf form over dictionary codes (k_dict_leaf + k_filter_dict, the
-    default), the leaf form over the typed cache (k_filter_leaf, DR_FILTER_NODICT=1) and the generic
-    postfix interpreter k_filter_typed (DR_FILTER_GENERIC=1)."""
-    if kernel == "generic":
-        monkeypatch.setenv("DR_FILTER_GENERIC", "1")
-    if kernel == "typed":
-        monkeypatch.setenv("DR_FILTER_NODICT", "1")
+def test_filter_cast_corpus(engine, tmp_path, checkpoint, escaped_keys, kernel):
+    """The three K5 evaluators (context option DR_OPT_FILTER_EVAL): the leaf form over dictionary
+    codes (k_dict_leaf + k_filter_dict, the default, 0), the leaf form over the typed cache
+    (k_filter_leaf, 1) and the generic postfix interpreter k_filter_typed (2)."""
     lp = F.build(str(tmp_path), checkpoint=checkpoint, escaped_keys=escaped_keys)
-    got = _gpu_selected(engine, lp, F.PREDICATES)
+    with engine.options(filter_eval={"dict": 0, "typed": 1, "generic": 2}[kernel]):
+        got = _gpu_selected(engine, lp, F.PREDICATES)
     want = _oracle_selected(lp, F.PREDICATES)
     for p, g, w in zip(F.PREDICATES, got, want):
         assert g == w, p
@@ -114,12 +111,10 @@ def test_filter_dictionary_overflow_falls_back(engine, tmp_path):
 
 
 @pytest.mark.parametrize("kernel", ["dict", "typed"])
-def test_filter_config4_predicate(engine, tmp_path, monkeypatch, kernel):
+def test_filter_config4_predicate(engine, tmp_path, kernel):
     """p0 >= DATE'2020-03-01' AND p0 < DATE'2020-06-01' AND p1 IN (1..100)
     AND p2 = 'w17' AND p3 = true, over a 4-column checkpoint + churn commits."""
     from delta_amd.testing import synth as S
-    if kernel == "typed":
-        monkeypatch.setenv("DR_FILTER_NODICT", "1")
     spec = S.ChurnSpec(ckpt_files=30000, ckpt_version=10, n_deltas=4, removes_per_delta=2000,
                        adds_per_delta=2000, readd_frac=0.5, ncols=4)
     exp = S.build_table(str(tmp_path), spec, seed=4, row_group_size=7000)
@@ -130,7 +125,8 @@ def test_filter_config4_predicate(engine, tmp_path, monkeypatch, kernel):
               ("=", C("p3"), L("boolean", True))],
              [("isnull", C("p2"))],
              [("in", C("p1"), [L("integer", v) for v in range(1, 101)])]]
-    got = _gpu_selected(engine, lp, preds, exp.min_file_retention_timestamp)
+    with engine.options(filter_eval=1 if kernel == "typed" else 0):
+        got = _gpu_selected(engine, lp, preds, exp.min_file_retention_timestamp)
     assert got == _oracle_selected(lp, preds, exp.min_file_retention_timestamp)
     assert len(got[0]) > 0 and len(got[1]) > 0
 

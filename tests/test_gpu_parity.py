@@ -128,15 +128,16 @@ def test_synthetic_configs(engine, tmp_path, config, scale):
         st.release()
 
 
-@pytest.mark.parametrize("overlap", ["0", "1"])
-def test_parse_streams_overlap_or_not(tmp_path, monkeypatch, overlap):
+@pytest.mark.parametrize("overlap", [0, 1])
+def test_parse_streams_overlap_or_not(tmp_path, overlap):
     """K1 beside K2 on two streams (the default for a segment with a checkpoint and a multi-block
-    JSON part) and on one (DR_OVERLAP=0): the same records as the oracle either way, on a context
-    created under each setting."""
+    JSON part) and on one (context option DR_OPT_OVERLAP = 0): the same records as the oracle either
+    way, on a fresh context set to each."""
     from delta_amd.delta_log import Engine
     from delta_amd.testing import synth as S
-    monkeypatch.setenv("DR_OVERLAP", overlap)
     eng = Engine(0)
+    assert eng.get_option("overlap") == 1  # the default
+    eng.set_option("overlap", overlap)
     exp = S.build_config(3, str(tmp_path), scale=0.02)
     lp = os.path.join(str(tmp_path), "_delta_log")
     st = _gpu_replay(eng, lp, exp.min_file_retention_timestamp)
@@ -196,21 +197,21 @@ def test_fallback_reducers_agree(engine, tmp_path, reducer):
         b.release()
 
 
-@pytest.mark.parametrize("bits,split", [(3, "0"), (5, "0"), (3, "1"), (5, "1")])
-def test_reducer_subpasses_agree(engine, tmp_path, monkeypatch, bits, split):
+@pytest.mark.parametrize("bits,split", [(3, 0), (5, 0), (3, 1), (5, 1), (1, 1)])
+def test_reducer_subpasses_agree(engine, tmp_path, bits, split):
     """Buckets of more than 2048 records on average (config 4's 12K; forced here with 8 or 32
     buckets of ~20K / ~5K records): K3's refinement (k_bucket_split into 2^s sub-buckets by the next
-    key bits, then one K4 pass per sub-bucket) and, with DR_SPLIT=0, K4's own sub-pass path over
-    the whole bucket give the one-pass reducer's state."""
+    key bits, then one K4 pass per sub-bucket) and, with DR_OPT_SPLIT = 0, K4's own sub-pass path
+    over the whole bucket give the one-pass reducer's state (DR_OPT_BUCKET_BITS forces the buckets;
+    (1, 1) takes the refinement to its 6-bit cap, as 2^13 buckets do past ~2^29 actions)."""
     from delta_amd.testing import synth as S
     exp = S.build_config(3, str(tmp_path), scale=0.01)
     lp = os.path.join(str(tmp_path), "_delta_log")
     staged = engine.stage_log(lp)
     try:
         a = staged.replay(exp.min_file_retention_timestamp)
-        monkeypatch.setenv("DR_BUCKET_BITS", str(bits))
-        monkeypatch.setenv("DR_SPLIT", split)
-        b = staged.replay(exp.min_file_retention_timestamp)
+        with engine.options(bucket_bits=bits, split=split):
+            b = staged.replay(exp.min_file_retention_timestamp)
     finally:
         staged.release()
     try:

@@ -23,7 +23,7 @@ def test_library_exports_every_declared_symbol():
     lib = ctypes.CDLL(N.LIB_PATH)
     for name in _declared():
         assert hasattr(lib, name), name
-    assert N.load().dr_abi_version() == 3  # include/deltareplay.h DR_ABI_VERSION
+    assert N.load().dr_abi_version() == N.ABI_VERSION == 4  # include/deltareplay.h DR_ABI_VERSION
 
 
 def test_no_device_is_reported_loudly():

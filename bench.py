@@ -88,10 +88,9 @@ def algorithmic_bytes(kernel, plan, counts):
         fa = counts["num_file_actions"]
         surv = counts["num_files"] + counts["num_removes"]
         table.update({
-            "k_bucket_hist": 10 * n,                               # kind, flags, key in
-            # kind, flags, key, path address + length in; size or delTs per file action in; 16 B record +
-            # 8 B path reference out
-            "k_bucket_scatter": 22 * n + 32 * fa,
+            "k_bucket_hist": 10 * n,                               # kind, flags, key in (r06: path refs by the producers)
+            # kind, flags, key in; size or delTs per file action in; 16 B record out
+            "k_bucket_scatter": 10 * n + 24 * fa,
             "k_bucket_reduce": 16 * fa + 4 * surv,                 # records in, survivors out (+ verification)
             "k_compact2": 8 * surv,
         })

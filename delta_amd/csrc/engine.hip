@@ -2124,12 +2124,11 @@ static ReducePending reduce_launch(dr_ctx* ctx, dr_state* st, int64_t cutoff, ui
       std::fprintf(stderr, "\n");
     }
   }
-  launch_sum_stats(ra, stream);
   reduce_range.reset();
   DR_STAGE("compact", stream);
   // ---- compaction (survivor lists sized to the bound; the counts come back once, at the end) ----
   DBuf<uint64_t> loff(ctx, knb + 1), tmoff(ctx, knb + 1);
-  launch_survivor_scan(lcount.p, tcount.p, knb, loff.p, tmoff.p, stream);
+  launch_survivor_scan(lcount.p, tcount.p, knb, loff.p, tmoff.p, stream, bstats.p, totals.p);  // + the sums
   st->live = DBuf<uint32_t>(ctx, N);
   st->tomb = DBuf<uint32_t>(ctx, N);
   launch_compact2(CompactArgs{olive.p, kboff, lcount.p, loff.p, knb, st->live.p},

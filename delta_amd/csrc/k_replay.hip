@@ -261,9 +261,10 @@ __global__ void k_bucket_offsets(const uint64_t* tile_off, uint32_t nb, uint32_t
 
 // ---- per-bucket reduce ------------------------------------------------------------------------------
 constexpr int RED_T = DR_RED_T;
-constexpr int TS_MAX = 4096;  // LDS table slots: 8 B key + 4 B winner meta = 48 KiB, 3 WGs/CU
-// records per thread held in registers by a one-pass bucket (at most 3/4 TS_MAX records)
-constexpr int RED_RPT = (TS_MAX / 4 * 3 + RED_T - 1) / RED_T;
+// LDS table slots: 8 B key + 4 B winner meta + 2 B loser count = 49 KiB, 3 workgroups per CU
+constexpr int TS_MAX = 3584;
+constexpr int HELD_MAX = TS_MAX / 4 * 3;  // a bucket of at most this many records is held in registers
+constexpr int RED_RPT = (HELD_MAX + RED_T - 1) / RED_T;
 
 struct BucketTotals {
   uint64_t live, tomb, size, lks, tks;
@@ -420,8 +421,8 @@ __device__ __forceinline__ uint4 shfl_down4(uint4 v, int width) {
 // both strings (a wave instruction requests eight whole paths of each side at once, every block
 // once) and takes block j + 1 from its neighbour by a shuffle; lanes 0..6 each compare 16 path
 // bytes, and the group ORs its differences. Unequal bytes get the URI-key comparison (file:/// vs
-// file:/ spellings) on the group's first lane. (r06: the reducer appends pairs in wave order and no
-// longer groups a winner's pairs -- its counting sort cost more in K4 than the shared fetches saved.)
+// file:/ spellings) on the group's first lane. The pairs of a winner sit together (k_bucket_reduce
+// groups them), so the groups that share a winner fetch its reference and bytes once from HBM.
 constexpr int VER_T = 256;
 __global__ void __launch_bounds__(VER_T) k_bucket_verify(ReduceArgs a) {
   const uint32_t b = blockIdx.x;
@@ -498,6 +499,50 @@ __global__ void __launch_bounds__(VER_T) k_bucket_verify(ReduceArgs a) {
   }
 }
 
+// Per-slot loser counts packed two to a word (slot s: word s >> 1, bits 16 (s & 1)): members - 1 of
+// each slot, replaced in place by each slot's first pair position (an exclusive scan over the n
+// slots, n <= TS_MAX and even, by one RED_T workgroup); returns the total. Counts and positions stay
+// below 2^16 (a pass holds at most a few thousand records), so the halves never carry into each other.
+__device__ uint32_t scan_loser_slots(uint32_t* w, uint32_t n) {
+  __shared__ uint32_t wsum[RED_T / 64];
+  constexpr uint32_t PER = (TS_MAX / 2 + RED_T - 1) / RED_T;  // words per thread
+  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint32_t nw = n >> 1;
+  uint32_t v[2 * PER], s = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < PER; ++k) {
+    const uint32_t i = t * PER + k;
+    const uint32_t x = i < nw ? w[i] : 0u;
+    const uint32_t lo = x & 0xffffu, hi = x >> 16;
+    v[2 * k] = lo ? lo - 1u : 0u;
+    v[2 * k + 1] = hi ? hi - 1u : 0u;
+    s += v[2 * k] + v[2 * k + 1];
+  }
+  uint32_t incl = s;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o, 64);
+    if (lane >= uint32_t(o)) incl += y;
+  }
+  if (lane == 63) wsum[wv] = incl;
+  __syncthreads();
+  uint32_t base = 0, total = 0;
+  for (uint32_t q = 0; q < RED_T / 64; ++q) {
+    base += q < wv ? wsum[q] : 0u;
+    total += wsum[q];
+  }
+  uint32_t run = base + incl - s;
+#pragma unroll
+  for (uint32_t k = 0; k < PER; ++k) {
+    const uint32_t i = t * PER + k;
+    const uint32_t lo = run;
+    run += v[2 * k];
+    if (i < nw) w[i] = lo | (run << 16);
+    run += v[2 * k + 1];
+  }
+  __syncthreads();
+  return total;
+}
+
 // Table of ts slots (a multiple of 64, at most TS_MAX): a key's probe starts at its low 32 bits scaled
 // to ts (independent of the bucket and sub-pass bits, which sit above them), linear probing wraps.
 __device__ __forceinline__ uint32_t slot_start(uint64_t key, uint32_t ts) {
@@ -509,13 +554,14 @@ __device__ __forceinline__ uint32_t table_slots(uint64_t m) {
 
 // Inserts key k with action meta z: table[k] = max(meta + 1) -- the largest action index wins.
 // Returns the slot, or ts when the table is full.
-__device__ __forceinline__ uint32_t table_insert(unsigned long long* tkey, uint32_t* tval, uint32_t ts,
+__device__ __forceinline__ uint32_t table_insert(unsigned long long* tkey, uint32_t* tval, uint32_t* tcnt, uint32_t ts,
                                                  unsigned long long k, uint32_t z) {
   uint32_t s = slot_start(k, ts);
   for (uint32_t probe = 0; probe < ts; ++probe) {
     const unsigned long long old = atomicCAS(&tkey[s], 0ull, k);
     if (old == 0ull || old == k) {
       atomicMax(&tval[s], z + 1u);
+      atomicAdd(&tcnt[s >> 1], 1u << (16 * (s & 1)));
       return s;
     }
     s = s + 1 == ts ? 0u : s + 1;
@@ -576,22 +622,34 @@ __device__ void store_sums(ReduceArgs& a, uint32_t b, uint32_t nl, uint32_t nt, 
 // atomicMax(meta + 1): the action with the largest (version, line) ordinal wins -- exactly the
 // reference's "last action per path" (D/actions/InMemoryLogReplay.scala:43-77). Survivors go to the
 // bucket's region of the live / tombstone lists; every loser is paired (by action index) with its
-// winner for k_bucket_verify. A bucket of up to 3/4 TS_MAX records is held in registers (loaded once,
-// all loads in flight before the first use) and each record keeps its table slot between the insert
-// and the classification; a larger one is reduced in sub-passes by the next key bits, re-read from
-// HBM. The table is sized to the bucket (2 slots per record), so its clearing costs what it holds.
-// An LDS-table overflow sends the bucket to the finer-grained fallback reducer.
+// winner for k_bucket_verify, the pairs grouped by winner (a counting sort on the table slot: the
+// verifier's lane groups that share a winner then request its lines in one instruction; without the
+// grouping k_bucket_verify took 0.46 instead of 0.40 ms on config 3). A bucket of up to HELD_MAX
+// records is held in registers (loaded once, all loads in flight before the first use) and each
+// record keeps its table slot between the insert and the classification; a larger one is reduced in
+// sub-passes by the next key bits, re-read from HBM. The table is sized to the bucket (2 slots per
+// record), so its clearing costs what it holds. An LDS-table overflow sends the bucket to the
+// finer-grained fallback reducer.
 __global__ void __launch_bounds__(RED_T) k_bucket_reduce(ReduceArgs a) {
   __shared__ unsigned long long tkey[TS_MAX];
   __shared__ uint32_t tval[TS_MAX];
-  __shared__ uint32_t nl, nt, np, overflow;
+  __shared__ uint32_t tcnt[TS_MAX / 2];  // u16 per slot: members, then its next pair position
+  __shared__ uint32_t nl, nt, overflow;
   const uint32_t b = blockIdx.x;
   const int bits = a.bucket_bits;
   const uint64_t beg = a.bucket_off[b], end = a.bucket_off[b + 1];
   const uint64_t m = end - beg;
-  if (threadIdx.x == 0) { nl = 0; nt = 0; np = 0; overflow = 0; }
+  if (threadIdx.x == 0) { nl = 0; nt = 0; overflow = 0; }
   uint64_t size = 0, lks = 0, tks = 0;
-  if (m <= uint64_t(RED_T) * RED_RPT) {
+  uint32_t pbase = 0;  // pairs of the earlier sub-passes
+  // a loser's pair at its slot's next position: the pairs of one winner end up next to each other
+  auto put_pair = [&](const RedOut& o, uint32_t s) {
+    if (!o.isp) return;
+    const uint32_t sh = 16 * (s & 1);
+    const uint32_t at = pbase + ((atomicAdd(&tcnt[s >> 1], 1u << sh) >> sh) & 0xffffu);
+    a.out_pair[beg + at] = make_uint2(o.idx, o.win);
+  };
+  if (m <= uint64_t(HELD_MAX)) {
     const uint32_t ts = table_slots(m);
     uint4 r[RED_RPT];
 #pragma unroll
@@ -600,61 +658,68 @@ __global__ void __launch_bounds__(RED_T) k_bucket_reduce(ReduceArgs a) {
       r[q] = e < end ? load_rec(a.rec, e) : make_uint4(0, 0, 0, 0);
     }
     for (uint32_t s = threadIdx.x; s < ts; s += RED_T) { tkey[s] = 0; tval[s] = 0; }
+    for (uint32_t s = threadIdx.x; s < ts / 2; s += RED_T) tcnt[s] = 0;
     __syncthreads();
     uint32_t sl[RED_RPT];
 #pragma unroll
     for (int q = 0; q < RED_RPT; ++q) {
       sl[q] = 0;
       if (beg + threadIdx.x + uint64_t(q) * RED_T >= end) continue;
-      sl[q] = table_insert(tkey, tval, ts, rec_key(r[q]), r[q].z);
+      sl[q] = table_insert(tkey, tval, tcnt, ts, rec_key(r[q]), r[q].z);
       if (sl[q] == ts) overflow = 1;
     }
     __syncthreads();
     if (!overflow) {
+      const uint32_t npass = scan_loser_slots(tcnt, ts);
 #pragma unroll
       for (int q = 0; q < RED_RPT; ++q) {
         const bool in = beg + threadIdx.x + uint64_t(q) * RED_T < end;
         if (!__ballot(in)) break;  // wave-uniform: later rows are past the bucket for every lane
         RedOut o{false, false, false, 0, 0};
         if (in) o = classify(a, r[q], tval[sl[q]] - 1u, size, lks, tks);
+        put_pair(o, sl[q]);
         wave_append(o.isl, o.idx, &nl, a.out_live + beg);
         wave_append(o.ist, o.idx, &nt, a.out_tomb + beg);
-        wave_append2(o.isp, make_uint2(o.idx, o.win), &np, a.out_pair + beg);
       }
+      pbase = npass;
     }
   } else {
     // sub-passes by the top sbits of the 32 key bits below the bucket bits, each at most 3/4 TS_MAX
     // records on average
     int sbits = 0;
-    while ((m >> sbits) > uint64_t(TS_MAX / 4 * 3)) ++sbits;
+    while ((m >> sbits) > uint64_t(HELD_MAX)) ++sbits;
     const uint32_t ts = TS_MAX;
     for (uint32_t sp = 0; sp < (1u << sbits); ++sp) {
       __syncthreads();
       for (uint32_t s = threadIdx.x; s < ts; s += RED_T) { tkey[s] = 0; tval[s] = 0; }
+      for (uint32_t s = threadIdx.x; s < ts / 2; s += RED_T) tcnt[s] = 0;
       __syncthreads();
       for (uint64_t e = beg + threadIdx.x; e < end; e += RED_T) {
         const uint4 r = load_rec(a.rec, e);
         if ((rkey_of(rec_key(r), bits) >> (32 - sbits)) != sp) continue;
-        if (table_insert(tkey, tval, ts, rec_key(r), r.z) == ts) overflow = 1;
+        if (table_insert(tkey, tval, tcnt, ts, rec_key(r), r.z) == ts) overflow = 1;
       }
       __syncthreads();
       if (overflow) break;
+      const uint32_t npass = scan_loser_slots(tcnt, ts);
       for (uint64_t e0 = beg; e0 < end; e0 += RED_T) {
         const uint64_t e = e0 + threadIdx.x;
         RedOut o{false, false, false, 0, 0};
+        uint32_t s = 0;
         if (e < end) {
           const uint4 r = load_rec(a.rec, e);
           const unsigned long long k = rec_key(r);
           if ((rkey_of(k, bits) >> (32 - sbits)) == sp) {
-            uint32_t s = slot_start(k, ts);
+            s = slot_start(k, ts);
             while (tkey[s] != k) s = s + 1 == ts ? 0u : s + 1;
             o = classify(a, r, tval[s] - 1u, size, lks, tks);
           }
         }
+        put_pair(o, s);
         wave_append(o.isl, o.idx, &nl, a.out_live + beg);
         wave_append(o.ist, o.idx, &nt, a.out_tomb + beg);
-        wave_append2(o.isp, make_uint2(o.idx, o.win), &np, a.out_pair + beg);
       }
+      pbase += npass;
     }
   }
   __syncthreads();
@@ -662,7 +727,7 @@ __global__ void __launch_bounds__(RED_T) k_bucket_reduce(ReduceArgs a) {
   if (threadIdx.x == 0) {
     a.live_count[b] = vl;
     a.tomb_count[b] = vt;
-    a.pair_count[b] = overflow ? 0 : np;
+    a.pair_count[b] = overflow ? 0 : pbase;
     if (overflow) a.redo_list[atomicAdd(&a.totals[3], 1ull)] = b;
   }
   store_sums(a, b, vl, vt, size, lks, tks);
@@ -876,14 +941,28 @@ __global__ void __launch_bounds__(SPLIT_T) k_bucket_split(SplitArgs a) {
 
 // Exclusive scans of the per-bucket live and tombstone counts in one workgroup (each thread owns a
 // run of ceil(nb / 1024) buckets: 8 for K3's 2^13, 64 for a split replay's 2^16); off[nb] is the total.
+// With `bstats` it also sums the buckets' {live, tomb, size, live sum, tomb sum} into totals[0, 2, 1,
+// 5, 6] (r06: k_sum_stats' launch folded in).
 constexpr int SSCAN_T = 1024;
 __global__ void __launch_bounds__(SSCAN_T) k_survivor_scan(const uint32_t* lc, const uint32_t* tc, uint32_t nb,
-                                                           uint64_t* loff, uint64_t* toff) {
+                                                           uint64_t* loff, uint64_t* toff,
+                                                           const unsigned long long* bstats,
+                                                           unsigned long long* totals) {
   __shared__ unsigned long long ws[2][SSCAN_T / 64];
+  __shared__ unsigned long long red[5][SSCAN_T / 64];
   const uint32_t per = (nb + SSCAN_T - 1) / SSCAN_T;
   const uint32_t b0 = min(nb, threadIdx.x * per), b1 = min(nb, b0 + per);
   unsigned long long sl = 0, st = 0;
   for (uint32_t b = b0; b < b1; ++b) { sl += lc[b]; st += tc[b]; }
+  if (bstats) {  // block-uniform; bucket b by thread b mod 1024 (consecutive threads, consecutive rows)
+    unsigned long long s[5] = {0, 0, 0, 0, 0};
+    for (uint32_t b = threadIdx.x; b < nb; b += SSCAN_T)
+      for (int k = 0; k < 5; ++k) s[k] += bstats[uint64_t(b) * 5 + k];
+    for (int k = 0; k < 5; ++k)
+      for (int o = 32; o > 0; o >>= 1) s[k] += __shfl_down(s[k], o, 64);
+    if ((threadIdx.x & 63) == 0)
+      for (int k = 0; k < 5; ++k) red[k][threadIdx.x >> 6] = s[k];
+  }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   unsigned long long il = sl, it = st;
   for (int o = 1; o < 64; o <<= 1) {
@@ -899,6 +978,12 @@ __global__ void __launch_bounds__(SSCAN_T) k_survivor_scan(const uint32_t* lc, c
     ol += lc[b]; ot += tc[b];
   }
   if (threadIdx.x == SSCAN_T - 1) { loff[nb] = ol; toff[nb] = ot; }
+  if (bstats && threadIdx.x < 5) {  // (red was written before the scan's barrier)
+    unsigned long long v = 0;
+    for (int w = 0; w < SSCAN_T / 64; ++w) v += red[threadIdx.x][w];
+    const int slot[5] = {0, 2, 1, 5, 6};
+    totals[slot[threadIdx.x]] = v;
+  }
 }
 
 }  // namespace dev
@@ -979,11 +1064,11 @@ void launch_bucket_split(const SplitArgs& a, uint32_t nbuckets, hipStream_t st) 
 }
 
 void launch_survivor_scan(const uint32_t* lc, const uint32_t* tc, uint32_t nb, uint64_t* loff, uint64_t* toff,
-                          hipStream_t st) {
+                          hipStream_t st, const unsigned long long* bstats, unsigned long long* totals) {
   // each thread scans a run of ceil(nb / 1024) buckets, so any count works (a 2^13-bucket
   // K3 refined by 6 bits gives K4 2^19 buckets past ~2^29 actions); the bound only catches garbage
   if (nb > (1u << 26)) throw std::runtime_error("survivor scan: too many buckets");
-  DR_LAUNCH(dev::k_survivor_scan, dim3(1), dim3(dev::SSCAN_T), 0, st, lc, tc, nb, loff, toff);
+  DR_LAUNCH(dev::k_survivor_scan, dim3(1), dim3(dev::SSCAN_T), 0, st, lc, tc, nb, loff, toff, bstats, totals);
 }
 
 }  // namespace dr

@@ -326,9 +326,11 @@ struct CompactArgs {
 void launch_compact(const CompactArgs& a, hipStream_t st);
 // both survivor lists in one launch (nbuckets must match)
 void launch_compact2(const CompactArgs& live, const CompactArgs& tomb, hipStream_t st);
-// exclusive scans (+ totals at [nb]) of the live / tombstone counts, nb <= 8192, one workgroup
+// exclusive scans (+ totals at [nb]) of the live / tombstone counts, one workgroup; with bstats also
+// the reducer's per-bucket sums into totals (what k_sum_stats did)
 void launch_survivor_scan(const uint32_t* lc, const uint32_t* tc, uint32_t nb, uint64_t* loff, uint64_t* toff,
-                          hipStream_t st);
+                          hipStream_t st, const unsigned long long* bstats = nullptr,
+                          unsigned long long* totals = nullptr);
 
 // ---- multi-GPU path-hash sharding (k_shard.hip) ------------------------------------------------
 struct ShardRec {        // 32 B per exchanged file action (DR_SHARD_REC_BYTES)

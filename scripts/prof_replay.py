@@ -17,7 +17,7 @@ def main():
     from delta_amd.testing import synth as S
     d = os.path.join(tempfile.gettempdir(), "dr_prof_c%d_%g" % (args.config, args.scale))
     if not os.path.exists(os.path.join(d, "_delta_log")):
-        S.build_config(args.config, d, scale=args.scale, keep_ids=False)
+        S.build_config(args.config, d, scale=args.scale, keep_ids=False, workers=16)
     exp = S.build_config.__module__ and None
     eng = Engine.get(0)
     # context options for the profiled replays: PROF_OPTS="bucket_bits=12,split=0" (dr_ctx_set_option)
@@ -25,6 +25,9 @@ def main():
         k, v = kv.split("=")
         eng.set_option(k, int(v))
     staged = eng.stage_log(os.path.join(d, "_delta_log"))
+    if os.environ.get("PROF_PLAN"):  # the staged plan's figures (roofline accounting of a profile)
+        import json
+        print(json.dumps(staged.plan()), flush=True)
     for _ in range(args.reps):
         st = staged.replay(0)
         print(st.counts["num_files"], st.counts["num_actions"], flush=True)

@@ -70,7 +70,8 @@ def test_ranges_tile_the_side(engine, tmp_path, max_rows, max_bytes):
             assert len(b) - 1 >= -(-n // max_rows)
             if which == 0:
                 assert len(b) > 2  # 50K live files: every bound here splits them
-        # a range is independent of the state: released after it, still readable
+        # a small range (its copy; the range outliving its state and context is
+        # test_range_outlives_its_state_and_context, at the C ABI)
         r = st.export_range(0, 3, 10)
         assert len(r["path_off"]) == 8 and r["path_off"][0] == 0
     finally:

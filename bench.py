@@ -100,12 +100,16 @@ def algorithmic_bytes(kernel, plan, counts):
 def pmc_traffic(pmc_dir, kernel):
     """Per-launch HBM bytes of `kernel` from committed rocprofv3 --pmc passes (FETCH_SIZE and
     WRITE_SIZE in separate runs of this same bench command). FETCH_SIZE is doubled: on gfx950 it
-    tallies 128-B requests at 64 B (MI355X_MICROARCH.md, HBM section). Returns None when absent."""
+    tallies 128-B requests at 64 B (MI355X_MICROARCH.md, HBM section; for k_snap_exec's own loads
+    checked against TCC_EA0_RDREQ x 128 B, profiles/r06/calib). Only the replay's launches count:
+    the dispatches of the grid size that occurs most often (a bench run also decodes export columns
+    with the same kernel on other grids; r05's config-4 figure averaged those in and fell below the
+    compulsory bytes). Returns None when absent."""
     import csv
     import glob
     if not pmc_dir or not os.path.isdir(pmc_dir):
         return None
-    per = {}
+    per, grids = {}, {}
     for fn in glob.glob(os.path.join(pmc_dir, "**", "*counter_collection.csv"), recursive=True):
         with open(fn) as f:
             for row in csv.DictReader(f):
@@ -114,12 +118,17 @@ def pmc_traffic(pmc_dir, kernel):
                     continue
                 c = row.get("Counter_Name")
                 v = float(row.get("Counter_Value", 0) or 0)
-                d = per.setdefault(c, {})
+                g = row.get("Grid_Size")
+                d = per.setdefault(c, {}).setdefault(g, {})
                 key = (fn, row.get("Dispatch_Id"))
                 d[key] = d.get(key, 0.0) + v
+                grids.setdefault(g, set()).add(key)
     if "FETCH_SIZE" not in per or "WRITE_SIZE" not in per:
         return None
-    avg = {c: sum(v.values()) / len(v) for c, v in per.items()}
+    g = max(grids, key=lambda x: len(grids[x]))  # the replay's grid
+    if g not in per["FETCH_SIZE"] or g not in per["WRITE_SIZE"]:
+        return None
+    avg = {c: sum(v[g].values()) / len(v[g]) for c, v in per.items() if g in v}
     return int(2 * avg["FETCH_SIZE"] * 1024 + avg["WRITE_SIZE"] * 1024)  # KiB -> bytes
 
 
@@ -227,6 +236,7 @@ def measure_stream(eng, table, exp, args):
 
     def run(limit, timing):
         cur, stage_ms, apply_ms, kern = base, [], [], {}
+        span_ms.clear()
         eng.set_timing(timing)
         # the interpreter's cyclic collector is this harness's, not the library's: paused for the loop
         # (r05's p99 rose 0.052 -> 0.066 ms with p50 and the kernels flat -- host-side jitter), and run
@@ -244,6 +254,8 @@ def measure_stream(eng, table, exp, args):
             torch.cuda.synchronize()
             if timing and k:
                 for kn, ms in eng.last_timings().items():
+                    if kn == "end":  # the apply's device span: its first kernel's start to its last's end
+                        span_ms.append(ms)
                     if kn in ("start", "end") or kn.startswith("stat."):
                         continue
                     kern[kn.split("#")[0]] = kern.get(kn.split("#")[0], 0.0) + ms
@@ -259,8 +271,10 @@ def measure_stream(eng, table, exp, args):
         eng.set_timing(False)
         return cur, stage_ms, apply_ms, kern
 
+    span_ms = []
     n_timed = min(200, len(commits))
     cur, _, _, kern = run(n_timed, True)  # per-kernel times (events on) over the first commits
+    span = list(span_ms)
     cur.release()
     cur, stage_ms, apply_ms, _ = run(len(commits), False)
     first_ms, rest = apply_ms[0], apply_ms[1:]
@@ -315,6 +329,10 @@ def measure_stream(eng, table, exp, args):
                    "stage_plus_apply_ms": {"p50": round(_pct([a + b for a, b in zip(stage_ms[1:], rest)], 0.5), 4),
                                            "p99": round(_pct([a + b for a, b in zip(stage_ms[1:], rest)], 0.99), 4)},
                    "commits_per_s": round(len(rest) / apply_total_s, 1) if rest else None,
+                   # the device-side span of an apply (events on its stream, the first 200 commits):
+                   # a flat p99 here and a raised host-side p99 place the tail on the host
+                   "device_span_ms": {"p50": round(_pct(span, 0.5), 4), "p99": round(_pct(span, 0.99), 4),
+                                      "n": len(span)} if span else None,
                    "matches_full_replay": not mism},
         "roofline": {"bound": "hbm", "kernel": next(iter(kernels), None), "achieved": None, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": None, "traffic": None,

@@ -336,7 +336,20 @@ JL_HD void tokenize_window(const uint8_t* p, uint32_t n, const uint32_t w[4], in
   if (lo < 0) valid &= 0xFFFFu << uint32_t(-lo);
   if (lo + 16 > int32_t(n)) valid &= (1u << uint32_t(int32_t(n) - lo)) - 1u;
   Win m;
+#if defined(DR_JL_EXP) && DR_JL_EXP >= 3
+  // timing experiment only (scripts/build_variant.sh): the window loads without their classification
+  // (every byte a space: no tokens, no state), to split K1's cost into loads and SWAR classes
+  {
+    uint32_t x = w[0] ^ w[1] ^ w[2] ^ w[3];
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(x));
+#endif
+    m.q = 0; m.bs = 0; m.st = 0; m.ctrl = 0;
+    m.sp = 0xFFFFu | (x & 0u);
+  }
+#else
   classify(w, m);
+#endif
   m.q &= valid; m.bs &= valid; m.st &= valid; m.sp &= valid; m.ctrl &= valid;
   // escaped bytes: those preceded by an odd run of backslashes (carry from the previous window)
   uint32_t escaped = 0;

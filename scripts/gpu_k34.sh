@@ -30,6 +30,7 @@ print(sys.argv[2], {k: {c: "%.4g MB" % (sum(v) / len(v) / 1024) for c, v in d.it
 PY
 }
 for b in ${BITS:-13}; do
+  [ "$b" = none ] && continue
   PROF_OPTS=bucket_bits=$b timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/bits$b -o run --output-format csv -- python $R/scripts/prof_replay.py --reps 3 --scale $SC > $O/bits$b.log 2>&1 || { echo "bits $b failed"; tail -5 $O/bits$b.log; exit 1; }
   summ $O/bits$b "bits=$b"
   if [ -n "$PMC" ]; then

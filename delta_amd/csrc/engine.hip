@@ -125,7 +125,7 @@ struct dr_ctx {
     int64_t apply_full = 0;    // DR_OPT_APPLY_FULL: dr_state_apply always through K3/K4
     int64_t canon_hint = -1;   // DR_OPT_CANON_HINT: arena bytes standing in for the first replay's sizing
     int64_t json_staged = 0;   // DR_OPT_JSON_STAGED: every segment through the staged K1 kernel
-    int64_t host_cache_bytes = int64_t(16) << 30;  // DR_OPT_HOST_CACHE_BYTES: pinned blocks kept for reuse
+    int64_t host_cache_bytes = int64_t(64) << 30;  // DR_OPT_HOST_CACHE_BYTES: pinned blocks kept for reuse
   } opt;
   // Every entry point that takes this context (or a state, range, shard or communicator of it) holds
   // this lock for the call: a context may be shared by host threads (several Spark tasks of one
@@ -357,22 +357,34 @@ struct dr_ctx {
     host_sizes[p] = n;
     return p;
   }
-  // A released block joins the cache only while the cache stays within opt.host_cache_bytes (ADVICE
-  // r05: a large single-part checkpoint's block no longer stays pinned until the context ends);
-  // otherwise it is unpinned at once.
+  // The cache of released blocks stays within opt.host_cache_bytes (a large single-part
+  // checkpoint's block no longer stays pinned until the context ends): a released block evicts the
+  // largest cached ones until it fits (the newest block is the likeliest to be asked for again: the
+  // next range or part of the same size), and a block larger than the bound is unpinned at once.
   size_t host_free_bytes = 0;
   void host_release(void* p) {
     if (!p) return;
-    std::unique_lock<std::mutex> g(mu);
-    const size_t n = host_sizes[p];
-    if (host_free_bytes + n > size_t(std::max<int64_t>(opt.host_cache_bytes, 0))) {
-      host_sizes.erase(p);
-      g.unlock();
-      (void)hipHostFree(p);
-      return;
+    std::vector<void*> drop;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      const size_t n = host_sizes[p];
+      const size_t cap = size_t(std::max<int64_t>(opt.host_cache_bytes, 0));
+      if (n > cap) {
+        drop.push_back(p);
+        host_sizes.erase(p);
+      } else {
+        while (host_free_bytes + n > cap && !host_free.empty()) {
+          auto it = std::prev(host_free.end());
+          host_free_bytes -= it->first;
+          host_sizes.erase(it->second);
+          drop.push_back(it->second);
+          host_free.erase(it);
+        }
+        host_free.emplace(n, p);
+        host_free_bytes += n;
+      }
     }
-    host_free.emplace(n, p);
-    host_free_bytes += n;
+    for (void* q : drop) (void)hipHostFree(q);
   }
   void host_trim() {
     std::lock_guard<std::mutex> g(mu);
@@ -2128,7 +2140,16 @@ static ReducePending reduce_launch(dr_ctx* ctx, dr_state* st, int64_t cutoff, ui
   DR_STAGE("compact", stream);
   // ---- compaction (survivor lists sized to the bound; the counts come back once, at the end) ----
   DBuf<uint64_t> loff(ctx, knb + 1), tmoff(ctx, knb + 1);
-  launch_survivor_scan(lcount.p, tcount.p, knb, loff.p, tmoff.p, stream, bstats.p, totals.p);  // + the sums
+  if (knb > 16384) {
+    // a split replay's 2^16+ buckets: one workgroup walking 64+ buckets per thread took 0.23 ms on
+    // config 4; the grid-wide scans and a separate sum instead
+    DBuf<uint8_t> sscr(ctx, scan_scratch_for(knb));
+    launch_scan_u32(lcount.p, loff.p, knb, ss(sscr), stream);
+    launch_scan_u32(tcount.p, tmoff.p, knb, ss(sscr), stream);
+    launch_sum_stats(ra, stream);
+  } else {
+    launch_survivor_scan(lcount.p, tcount.p, knb, loff.p, tmoff.p, stream, bstats.p, totals.p);  // + the sums
+  }
   st->live = DBuf<uint32_t>(ctx, N);
   st->tomb = DBuf<uint32_t>(ctx, N);
   launch_compact2(CompactArgs{olive.p, kboff, lcount.p, loff.p, knb, st->live.p},
@@ -5857,10 +5878,26 @@ static void export_range(dr_state& st, int which, uint64_t lo, uint64_t hi, dr_r
   DBuf<uint8_t> dvalid(ctx, n + 1);
   DBuf<int64_t> ddelts(ctx, n + 1);
   launch_delts_fix(X.flags.p + lo, reinterpret_cast<const int64_t*>(X.delts.p) + lo, n, dvalid.p, ddelts.p, stream);
+  // the eight offset columns rebased to the range on the device, then copied (a host loop over them
+  // took ~30 ms per 1M-row range of config 4, whose 4 partition columns give 8M map offsets per range)
+  const uint64_t roff[8] = {0, n + 1, 2 * (n + 1), 3 * (n + 1), 4 * (n + 1), 4 * (n + 1) + npv + 1,
+                            4 * (n + 1) + 2 * (npv + 1), 4 * (n + 1) + 2 * (npv + 1) + ntg + 1};
+  DBuf<int64_t> reb(ctx, 4 * (n + 1) + 2 * (npv + 1) + 2 * (ntg + 1));
+  {
+    const int64_t* src[8] = {reinterpret_cast<const int64_t*>(X.path_off.p + lo),
+                             reinterpret_cast<const int64_t*>(X.off[EXC_STATS].p + lo),
+                             reinterpret_cast<const int64_t*>(X.off[EXC_PV_N].p + lo),
+                             reinterpret_cast<const int64_t*>(X.off[EXC_TAGS_N].p + lo),
+                             X.pv_key_off.p + b.pvn[0], X.pv_val_off.p + b.pvn[0], X.tags_key_off.p + b.tgn[0],
+                             X.tags_val_off.p + b.tgn[0]};
+    const uint64_t cnt[8] = {n + 1, n + 1, n + 1, n + 1, npv + 1, npv + 1, ntg + 1, ntg + 1};
+    const uint64_t base[8] = {b.path[0], b.stats[0], b.pvn[0], b.tgn[0], b.pvk[0], b.pvv[0], b.tgk[0], b.tgv[0]};
+    for (int k = 0; k < 8; ++k) launch_rebase_i64(src[k], cnt[k], int64_t(base[k]), reb.p + roff[k], stream);
+  }
   ExportCols ex;  // only its pointer fields: the columns are carved from R.block
   auto u8 = [](const void* p, uint64_t k) { return static_cast<const uint8_t*>(p) + k; };
   const std::vector<ExportCol> cols = {
-      {(void**)&ex.path_off, X.path_off.p + lo, 8 * (n + 1)},
+      {(void**)&ex.path_off, reb.p + roff[0], 8 * (n + 1)},
       {(void**)&ex.path_bytes, u8(X.path_bytes.p, b.path[0]), b.path[1] - b.path[0]},
       {(void**)&ex.delts, ddelts.p, 8 * n},
       {(void**)&ex.delts_valid, dvalid.p, n},
@@ -5870,17 +5907,17 @@ static void export_range(dr_state& st, int which, uint64_t lo, uint64_t hi, dr_r
       {(void**)&ex.stats_null, X.stats_null.p + lo, n},
       {(void**)&ex.pv_null, X.pv_null.p + lo, n},
       {(void**)&ex.tags_null, X.tags_null.p + lo, n},
-      {(void**)&ex.stats_off, X.off[EXC_STATS].p + lo, 8 * (n + 1)},
-      {(void**)&ex.pv_entry_off, X.off[EXC_PV_N].p + lo, 8 * (n + 1)},
-      {(void**)&ex.tags_entry_off, X.off[EXC_TAGS_N].p + lo, 8 * (n + 1)},
+      {(void**)&ex.stats_off, reb.p + roff[1], 8 * (n + 1)},
+      {(void**)&ex.pv_entry_off, reb.p + roff[2], 8 * (n + 1)},
+      {(void**)&ex.tags_entry_off, reb.p + roff[3], 8 * (n + 1)},
       {(void**)&ex.stats_bytes, u8(X.stats_bytes.p, b.stats[0]), b.stats[1] - b.stats[0]},
-      {(void**)&ex.pv_key_off, X.pv_key_off.p + b.pvn[0], 8 * (npv + 1)},
-      {(void**)&ex.pv_val_off, X.pv_val_off.p + b.pvn[0], 8 * (npv + 1)},
+      {(void**)&ex.pv_key_off, reb.p + roff[4], 8 * (npv + 1)},
+      {(void**)&ex.pv_val_off, reb.p + roff[5], 8 * (npv + 1)},
       {(void**)&ex.pv_val_null, X.pv_val_null.p + b.pvn[0], npv},
       {(void**)&ex.pv_key_bytes, u8(X.pv_key_bytes.p, b.pvk[0]), b.pvk[1] - b.pvk[0]},
       {(void**)&ex.pv_val_bytes, u8(X.pv_val_bytes.p, b.pvv[0]), b.pvv[1] - b.pvv[0]},
-      {(void**)&ex.tags_key_off, X.tags_key_off.p + b.tgn[0], 8 * (ntg + 1)},
-      {(void**)&ex.tags_val_off, X.tags_val_off.p + b.tgn[0], 8 * (ntg + 1)},
+      {(void**)&ex.tags_key_off, reb.p + roff[6], 8 * (ntg + 1)},
+      {(void**)&ex.tags_val_off, reb.p + roff[7], 8 * (ntg + 1)},
       {(void**)&ex.tags_val_null, X.tags_val_null.p + b.tgn[0], ntg},
       {(void**)&ex.tags_key_bytes, u8(X.tags_key_bytes.p, b.tgk[0]), b.tgk[1] - b.tgk[0]},
       {(void**)&ex.tags_val_bytes, u8(X.tags_val_bytes.p, b.tgv[0]), b.tgv[1] - b.tgv[0]}};
@@ -5888,17 +5925,6 @@ static void export_range(dr_state& st, int which, uint64_t lo, uint64_t hi, dr_r
   R.block = ctx->host_alloc(group_bytes(cols));
   queue_group(cols, R.block, stream);
   HIP_OK(hipStreamSynchronize(stream));
-  auto rebase = [](int64_t* o, uint64_t cnt, uint64_t base) {
-    for (uint64_t i = 0; i < cnt; ++i) o[i] -= int64_t(base);
-  };
-  rebase(ex.path_off, n + 1, b.path[0]);
-  rebase(ex.stats_off, n + 1, b.stats[0]);
-  rebase(ex.pv_entry_off, n + 1, b.pvn[0]);
-  rebase(ex.tags_entry_off, n + 1, b.tgn[0]);
-  rebase(ex.pv_key_off, npv + 1, b.pvk[0]);
-  rebase(ex.pv_val_off, npv + 1, b.pvv[0]);
-  rebase(ex.tags_key_off, ntg + 1, b.tgk[0]);
-  rebase(ex.tags_val_off, ntg + 1, b.tgv[0]);
   *out = dr_export{};
   out->n = int64_t(n);
   out->path_off = ex.path_off; out->path_bytes = ex.path_bytes;

@@ -103,6 +103,12 @@ __global__ void k_scatter_fp(const uint64_t* __restrict__ rows, const uint64_t* 
   isnull[r] = nulls[k];
 }
 
+// dst[i] = src[i] - base: a row range's offset column rebased on the device (dr_state_export_range)
+__global__ void k_rebase_i64(const int64_t* __restrict__ src, uint64_t n, int64_t base, int64_t* __restrict__ dst) {
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x)
+    dst[i] = src[i] - base;
+}
+
 // Export of deletionTimestamp: valid = F_HAS_DELTS of the action's flags, and an absent one reads 0.
 __global__ void k_delts_fix(const uint8_t* __restrict__ flags, const int64_t* __restrict__ delts, uint64_t n,
                             uint8_t* __restrict__ valid, int64_t* __restrict__ out) {
@@ -154,6 +160,12 @@ void launch_gather_u64_by64(const uint64_t* src, const uint64_t* idx, uint64_t n
 void launch_gather_bytes(const uint64_t* ptr, const uint32_t* len, const uint64_t* off, uint64_t n, uint8_t* out,
                          hipStream_t st) {
   if (n) DR_LAUNCH(dev::k_gather_bytes, dim3(unsigned(std::min<uint64_t>((n + 256 / dev::GATHER_G - 1) / (256 / dev::GATHER_G), 1u << 16))), dim3(256), 0, st, ptr, len, off, n, out);
+}
+
+void launch_rebase_i64(const int64_t* src, uint64_t n, int64_t base, int64_t* dst, hipStream_t st) {
+  if (n)
+    DR_LAUNCH(dev::k_rebase_i64, dim3(unsigned(std::min<uint64_t>((n + 255) / 256, 1u << 16))), dim3(256), 0, st, src, n,
+              base, dst);
 }
 
 void launch_delts_fix(const uint8_t* flags, const int64_t* delts, uint64_t n, uint8_t* valid, int64_t* out,

@@ -586,6 +586,8 @@ struct ReadbackArgs {
   uint64_t seq;
 };
 void launch_readback(const ReadbackArgs& a, hipStream_t st);
+// dst[i] = src[i] - base (n entries)
+void launch_rebase_i64(const int64_t* src, uint64_t n, int64_t base, int64_t* dst, hipStream_t st);
 // export: valid[i] = flags[i] & F_HAS_DELTS, out[i] = valid ? delts[i] : 0
 void launch_delts_fix(const uint8_t* flags, const int64_t* delts, uint64_t n, uint8_t* valid, int64_t* out,
                       hipStream_t st);

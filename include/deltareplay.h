@@ -157,8 +157,10 @@ enum dr_option {
                                   undersized arena is detected and the parse redone) */
   DR_OPT_JSON_STAGED = 7,      /* 0 (default); 1: every JSON segment through the staged, wave-cooperative
                                   K1 kernel (the streamed-commit walker) instead of the lane-per-line one */
-  DR_OPT_HOST_CACHE_BYTES = 8  /* bytes of released pinned host blocks kept for reuse (default 16 GiB);
-                                  a block that would exceed it is unpinned at release */
+  DR_OPT_HOST_CACHE_BYTES = 8  /* bytes of released pinned host blocks kept for reuse (default 64 GiB:
+                                  config 4's 36 GB export stays pinned between snapshots); a released
+                                  block evicts the largest cached ones to fit, one over the bound is
+                                  unpinned at once */
 };
 int dr_ctx_set_option(dr_ctx* ctx, int32_t option, int64_t value);
 int dr_ctx_get_option(dr_ctx* ctx, int32_t option, int64_t* value);

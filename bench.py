@@ -492,7 +492,7 @@ def main():
     ap.add_argument("--workdir", default=os.environ.get("DR_BENCH_DIR", os.path.join(tempfile.gettempdir(), "dr_bench")))
     args = ap.parse_args()
     if args.pmc_dir is None:
-        args.pmc_dir = os.path.join(ROOT, "profiles", "r05", "pmc", "c%d" % args.config)
+        args.pmc_dir = os.path.join(ROOT, "profiles", "r06", "pmc", "c%d" % args.config)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))

@@ -43,7 +43,7 @@ SYMBOLS = [
     "dr_replay_sharded", "dr_staged_release", "dr_staged_bytes", "dr_staged_plan",
     "dr_replay_staged",
     "dr_replay", "dr_state_release", "dr_state_apply", "dr_state_counts", "dr_state_local_counts", "dr_state_nonfile_json", "dr_state_check_checksum",
-    "dr_state_export", "dr_state_export_plan", "dr_state_export_range", "dr_range_release", "dr_state_materialize", "dr_state_record_sums", "dr_state_write_checkpoint", "dr_state_set_nonfile_json", "dr_filter", "dr_state_scan_order", "dr_state_partition_groups", "dr_free", "dr_last_timings", "dr_set_timing", "dr_set_timing_only",
+    "dr_state_export", "dr_state_export_plan", "dr_state_export_range", "dr_range_release", "dr_state_materialize", "dr_state_record_sums", "dr_state_record_hashes", "dr_state_write_checkpoint", "dr_state_set_nonfile_json", "dr_filter", "dr_state_scan_order", "dr_state_partition_groups", "dr_free", "dr_last_timings", "dr_set_timing", "dr_set_timing_only",
     "dr_shard_plan", "dr_stage_log_shard", "dr_shard_begin", "dr_shard_pack", "dr_shard_reduce",
     "dr_shard_finish", "dr_shard_release", "dr_parse_commits", "dr_parsed_release",
 ]
@@ -162,6 +162,7 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "dr_state_check_checksum": ([vp, C.c_char_p, u64, C.c_char_p, u64, C.POINTER(u64)], C.c_int),
         "dr_state_export": ([vp, i32, C.POINTER(dr_export)], C.c_int),
         "dr_state_record_sums": ([vp, C.POINTER(u64), C.POINTER(u64)], C.c_int),
+        "dr_state_record_hashes": ([vp, i32, vp, i64], C.c_int),
         "dr_state_export_plan": ([vp, i32, i64, u64, C.POINTER(_P64), _P64], C.c_int),
         "dr_state_export_range": ([vp, i32, i64, i64, C.POINTER(vp), C.POINTER(dr_export)], C.c_int),
         "dr_range_release": ([vp], C.c_int),

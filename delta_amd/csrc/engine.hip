@@ -2965,7 +2965,7 @@ static const DevExport& materialize(dr_state& st, int which) {
 
 // Order-free full-record checksum of one side (dr_state_record_sums): k_record_hash over the
 // side's device export columns.
-static uint64_t record_sum(dr_state& st, int which) {
+static uint64_t record_sum(dr_state& st, int which, uint64_t* hashes = nullptr) {
   dr_ctx* ctx = st.ctx;
   hipStream_t stream = ctx->stream;
   const DevExport& X = materialize(st, which);
@@ -2999,8 +2999,14 @@ static uint64_t record_sum(dr_state& st, int which) {
   a.tags_val_bytes = X.tags_val_bytes.p;
   a.tags_val_null = X.tags_val_null.p;
   a.sum = sum.p;
+  DBuf<uint64_t> each;
+  if (hashes) {
+    each = DBuf<uint64_t>(ctx, X.n);
+    a.out = each.p;
+  }
   if (const char* m = std::getenv("DR_RECORD_FIELDS")) a.field_mask = uint32_t(std::strtoul(m, nullptr, 0));  // diagnostics
   launch_record_hash(a, stream);
+  if (hashes && X.n) HIP_OK(hipMemcpyAsync(hashes, each.p, X.n * 8, hipMemcpyDeviceToHost, stream));
   return uint64_t(d2h_one(sum.p, stream));
 }
 
@@ -6079,6 +6085,17 @@ int dr_state_record_sums(dr_state* state, uint64_t* live_sum, uint64_t* tomb_sum
     HIP_OK(hipSetDevice(state->ctx->device));
     *live_sum = record_sum(*state, DR_LIVE);
     *tomb_sum = record_sum(*state, DR_TOMBSTONES);
+  });
+}
+
+int dr_state_record_hashes(dr_state* state, int32_t which, uint64_t* out, int64_t n) {
+  if (!state || (which != DR_LIVE && which != DR_TOMBSTONES) || n < 0 || (n && !out)) return DR_E_INVALID_ARG;
+  return guard(state->ctx, [&] {
+    HIP_OK(hipSetDevice(state->ctx->device));
+    const int64_t rows = int64_t(which == DR_LIVE ? state->n_live : state->n_tomb);
+    if (n != rows) fail(DR_E_INVALID_ARG, fmt("record hashes: the side holds %lld rows, the buffer %lld",
+                                             (long long)rows, (long long)n));
+    (void)record_sum(*state, which, out);
   });
 }
 

@@ -1397,6 +1397,7 @@ __global__ void __launch_bounds__(256) k_record_hash(RecordHashArgs a) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) w[k] = (a.field_mask >> k) & 1u ? w[k] : 0ull;
     r = xxh64_words8(w, REC_SEED);
+    if (a.out) a.out[i] = r;
   }
   for (int o = 32; o > 0; o >>= 1) r += __shfl_down(r, o, 64);
   if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = r;

@@ -789,6 +789,7 @@ struct RecordHashArgs {
   const uint8_t* tags_null; const uint64_t* tags_entry; const int64_t* tags_key_off; const uint8_t* tags_key_bytes;
   const int64_t* tags_val_off; const uint8_t* tags_val_bytes; const uint8_t* tags_val_null;
   unsigned long long* sum;
+  uint64_t* out = nullptr;      // nullable: each record's hash, in export order (dr_state_record_hashes)
   uint32_t field_mask = 0xffu;  // words of the record hash kept (diagnostics: DR_RECORD_FIELDS); others are 0
 };
 void launch_record_hash(const RecordHashArgs& a, hipStream_t st);

@@ -393,6 +393,16 @@ class State:
             self.eng.check(self.eng.lib.dr_state_record_sums(self.h, C.byref(a), C.byref(b)))
         return a.value, b.value
 
+    def record_hashes(self, which: int):
+        """dr_state_record_hashes: every record's hash of one side (numpy uint64, export order)."""
+        import numpy as np
+        lc = self.local_counts()  # a sharded rank's own rows (the table-wide counts otherwise)
+        n = lc["num_files"] if which == N.DR_LIVE else lc["num_removes"]
+        out = np.zeros(max(int(n), 1), dtype=np.uint64)
+        with self.eng.lock:
+            self.eng.check(self.eng.lib.dr_state_record_hashes(self.h, which, out.ctypes.data, int(n)))
+        return out[:int(n)]
+
     def export(self, which: int) -> List[dict]:
         with self.eng.lock:
             return self._export(which)

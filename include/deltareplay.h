@@ -288,6 +288,12 @@ int dr_state_materialize(dr_state* state, uint64_t* bytes);
  * same record sets (D/actions/InMemoryLogReplay.scala:55-77 winners, not only the same paths).
  * For a sharded state: this rank's records (sum the ranks' values). */
 int dr_state_record_sums(dr_state* state, uint64_t* live_sum, uint64_t* tomb_sum);
+/* The same per-record hashes one by one: out[i] = the hash of row i of side `which` in dr_state_export's
+ * order (n = the side's row count, else DR_E_INVALID_ARG). Sorted, they are the side's record multiset,
+ * which the full-size parity test compares element by element with the CPU restatement's
+ * (replay_oracle --record-hashes): equality of every record up to a 64-bit collision of the record
+ * hash, not only of a sum. */
+int dr_state_record_hashes(dr_state* state, int32_t which, uint64_t* out, int64_t n);
 
 /* ---- per-line commit decode (device) --------------------------------------------------------
  * The hot fields of DeltaLog.getChanges' per-line Action.fromJson (D/DeltaLog.scala:222-238,

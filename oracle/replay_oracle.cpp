@@ -909,7 +909,8 @@ std::vector<size_t> row_starts(const LevCol& c) {
 
 // Full-record sums of the checkpoint survivors of one row group: `surv[row]` 1 = live add,
 // 2 = kept tombstone.
-void ck_rowgroup_sums(const CkFile& cf, const RG& g, const SV* canon, const uint8_t* surv, uint64_t* sums) {
+void ck_rowgroup_sums(const CkFile& cf, const RG& g, const SV* canon, const uint8_t* surv, uint64_t* sums,
+                      uint64_t* hashes) {
   bool want[2] = {false, false};
   for (int64_t r = 0; r < g.rows; ++r) if (surv[r]) want[surv[r] - 1] = true;
   for (int side = 0; side < 2; ++side) {
@@ -965,7 +966,9 @@ void ck_rowgroup_sums(const CkFile& cf, const RG& g, const SV* canon, const uint
       }
       map_of(*pvk, *pvv, r, rec.pv);
       map_of(*tk, *tv, r, rec.tags);
-      sums[side] += rec_hash(rec, side);
+      const uint64_t h = rec_hash(rec, side);
+      sums[side] += h;
+      if (hashes) hashes[r] = h;
     }
   }
 }
@@ -979,9 +982,11 @@ int main(int argc, char** argv) {
   int threads = int(std::thread::hardware_concurrency());
   int parts = 50;
   bool want_records = false;
+  std::string hash_prefix;  // --record-hashes <prefix>: every survivor's record hash, <prefix>.live / .tomb
   for (int i = 3; i < argc; ++i) {
     if (!strcmp(argv[i], "--record-sums")) { want_records = true; continue; }
     if (i + 1 >= argc) break;
+    if (!strcmp(argv[i], "--record-hashes")) { want_records = true; hash_prefix = argv[++i]; continue; }
     if (!strcmp(argv[i], "--threads")) threads = std::max(1, atoi(argv[++i]));
     else if (!strcmp(argv[i], "--partitions")) parts = std::max(1, atoi(argv[++i]));
   }
@@ -1148,6 +1153,7 @@ int main(int argc, char** argv) {
     if (want_records) {
       auto tr0 = std::chrono::steady_clock::now();
       std::vector<std::array<uint64_t, 2>> ts_sum(T, std::array<uint64_t, 2>{0, 0});
+      std::vector<uint64_t> rh(hash_prefix.empty() ? 0 : N, 0);  // per action (survivors only)
       std::vector<uint8_t> bad(T, 0);
       {
         std::vector<std::thread> ts;
@@ -1161,7 +1167,9 @@ int main(int argc, char** argv) {
               Rec r;
               if (!json_record(lines[k].first, lines[k].second, sv - 1, &arenas[t], r)) { bad[t] = 1; continue; }
               r.path = canon[base + k];  // the record's path is the canonical one (D/Snapshot.scala:98-101)
-              ts_sum[t][sv - 1] += rec_hash(r, sv - 1);
+              const uint64_t h = rec_hash(r, sv - 1);
+              ts_sum[t][sv - 1] += h;
+              if (!rh.empty()) rh[base + k] = h;
             }
           });
         for (auto& t : ts) t.join();
@@ -1179,7 +1187,8 @@ int main(int argc, char** argv) {
           ts.emplace_back([&, t] {
             for (size_t k; (k = nt++) < tasks.size();) {
               uint64_t sm[2] = {0, 0};
-              ck_rowgroup_sums(*tasks[k].cf, *tasks[k].g, canon.data() + tasks[k].row0, surv.data() + tasks[k].row0, sm);
+              ck_rowgroup_sums(*tasks[k].cf, *tasks[k].g, canon.data() + tasks[k].row0, surv.data() + tasks[k].row0, sm,
+                               rh.empty() ? nullptr : rh.data() + tasks[k].row0);
               ts_sum[t][0] += sm[0];
               ts_sum[t][1] += sm[1];
             }
@@ -1189,6 +1198,16 @@ int main(int argc, char** argv) {
       uint64_t ls = 0, tsm = 0;
       for (auto& x : ts_sum) { ls += x[0]; tsm += x[1]; }
       for (uint8_t b : bad) if (b) die("unreadable survivor line in the record pass");
+      if (!rh.empty()) {  // the multisets of record hashes, for an exact comparison of sorted lists
+        for (int side = 0; side < 2; ++side) {
+          std::vector<uint64_t> v;
+          for (size_t i = 0; i < N; ++i) if (surv[i] == side + 1) v.push_back(rh[i]);
+          const std::string fn = hash_prefix + (side == 0 ? ".live" : ".tomb");
+          FILE* f = fopen(fn.c_str(), "wb");
+          if (!f || fwrite(v.data(), 8, v.size(), f) != v.size()) die("cannot write " + fn);
+          fclose(f);
+        }
+      }
       snprintf(recs, sizeof recs, ",\"live_record_sum\":%llu,\"tomb_record_sum\":%llu,\"record_s\":%.3f",
                (unsigned long long)ls, (unsigned long long)tsm,
                std::chrono::duration<double>(std::chrono::steady_clock::now() - tr0).count());

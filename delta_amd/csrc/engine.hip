@@ -1821,6 +1821,10 @@ static ParsePending parse_launch(dr_ctx* ctx, const std::shared_ptr<StagedData>&
           std::fprintf(stderr, "k_apply_commit apply clocks: post-parse %.0f append %.0f touch %.0f delta %.0f\n",
                        double(h[8]) / double(h[4]), double(h[9]) / double(h[4]), double(h[10]) / double(h[4]),
                        double(h[11]) / double(h[4]));
+        if (h[12] + h[13])
+          std::fprintf(stderr, "k_apply_commit clocks: stage %.0f newlines %.0f walk %.0f apply %.0f expiry %.0f readback %.0f\n",
+                       double(h[0]) / double(h[4]), double(h[1]) / double(h[4]), double(h[2]) / double(h[4]),
+                       double(h[6]) / double(h[4]), double(h[12]) / double(h[4]), double(h[13]) / double(h[4]));
       }
     }
     // an applied streamed commit: the walk runs in the apply's one launch (launch_apply_commit)
@@ -2458,9 +2462,27 @@ static dr_state* apply_incremental(dr_ctx* ctx, dr_state& base, const std::share
   a.undo = u.e.p;
   // the index counters start at zero but for the tombstone list's fill (set by the append launch)
   const AppendArgs ap = append_args(chain_dst(c), lo, t, uint16_t(c.sources.size()), c.ctr.p, IX_C_TOMB_FILL, c.tomb_n);
+  // one round trip: the tail's parse counters and non-file lines with the index counters, written
+  // into the pinned words by the apply's last launch (the one-launch apply itself, the expiry's last
+  // workgroup, or a readback launch of their own)
+  ReadbackArgs rb{};
+  int nrb = 0;
+  const size_t at = parse_queue_readback(ctx, pp, 0, &rb, &nrb);
+  rb.src[nrb] = reinterpret_cast<const uint64_t*>(c.ctr.p), rb.dst[nrb] = ctx->pinned_dev() + at, rb.n[nrb++] = IX_C_N;
+  rb.flag = ctx->pinned_dev() + dr_ctx::kPinFlag;
+  rb.seq = ++ctx->pin_seq;
+  const bool expire = cutoff > base.cutoff && c.tomb_n;
+  bool read_back = false;
   if (T && T <= APPLY_SMALL_MAX) {  // a streamed commit: post-parse, append and both index passes in one launch
-    if (pp.parse_deferred) launch_apply_commit(pp.tail_ja, pp.tail_cg, ap, a, stream);
-    else launch_apply_small(pp.tail_deferred ? &pp.tail_ja : nullptr, pp.tail_cg, ap, a, stream);
+    if (pp.parse_deferred) {
+      // r06: a short candidate list's expiry and the readback in the same launch (one launch per
+      // commit instead of two; the second launch's dispatch sat in every commit's latency)
+      const bool fuse = !expire || c.tomb_n <= APPLY_FUSED_EXPIRY_MAX;
+      launch_apply_commit(pp.tail_ja, pp.tail_cg, ap, a, stream, fuse && expire ? c.tomb_n : 0, fuse ? &rb : nullptr);
+      read_back = fuse;
+    } else {
+      launch_apply_small(pp.tail_deferred ? &pp.tail_ja : nullptr, pp.tail_cg, ap, a, stream);
+    }
     pp.tail_deferred = pp.parse_deferred = false;
   } else {
     parse_flush_tail(ctx, pp);
@@ -2468,16 +2490,10 @@ static dr_state* apply_incremental(dr_ctx* ctx, dr_state& base, const std::share
     launch_ix_touch(a, stream);
     launch_ix_delta(a, stream);
   }
-  // one round trip: the tail's parse counters and non-file lines with the index counters, written
-  // into the pinned words by the expiry's last workgroup (or one launch of their own)
-  ReadbackArgs rb{};
-  int nrb = 0;
-  const size_t at = parse_queue_readback(ctx, pp, 0, &rb, &nrb);
-  rb.src[nrb] = reinterpret_cast<const uint64_t*>(c.ctr.p), rb.dst[nrb] = ctx->pinned_dev() + at, rb.n[nrb++] = IX_C_N;
-  rb.flag = ctx->pinned_dev() + dr_ctx::kPinFlag;
-  rb.seq = ++ctx->pin_seq;
-  if (cutoff > base.cutoff && c.tomb_n) launch_ix_expire(a, c.tomb_n, stream, &rb);
-  else launch_readback(rb, stream);
+  if (!read_back) {
+    if (expire) launch_ix_expire(a, c.tomb_n, stream, &rb);
+    else launch_readback(rb, stream);
+  }
   ctx->wait_readback(rb.seq);
   std::vector<unsigned long long> ctr(ctx->pinned() + at, ctx->pinned() + at + IX_C_N);
   if (!parse_finish(ctx, tail, &t, pp, nf)) fail(DR_E_INTERNAL, "applied tail: canonicalisation arena too small");

@@ -103,6 +103,26 @@ __device__ inline void flush_contrib(const IndexArgs& a, Contrib c, unsigned lon
   }
 }
 
+// Expiry of tombstone candidate j (k_ix_expire, and the one-launch apply's fused expiry): a
+// candidate from an earlier apply whose delTimestamp now falls at or under the cutoff leaves the
+// tombstone count while it is still its path's winner. The slot value is read at L2 (the fused apply
+// raised it with atomics in the same workgroup).
+__device__ __forceinline__ void expire_entry(const IndexArgs& a, const ulonglong2 e, Contrib& c) {
+  const uint64_t x = e.x;
+  const int64_t dt = int64_t(e.y);
+  if (x < a.lo && dt > a.old_cut && dt <= a.new_cut) {  // this apply's own tombstones: counted at the new cutoff
+    const uint32_t s = ix_find(a.keys, a.mask, a.key[x]);
+    if (s != IX_NONE && __hip_atomic_load(a.vals + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == uint32_t(x + 1)) {
+      c.r += 0ull - 1ull;
+      c.tks += 0ull - (unsigned long long)(a.key[x] >> 32);
+    }
+  }
+}
+
+__device__ __forceinline__ void expire_one(const IndexArgs& a, uint64_t j, Contrib& c) {
+  expire_entry(a, a.tomb_list[j], c);
+}
+
 __device__ __forceinline__ void tomb_append(const IndexArgs& a, uint64_t x, int64_t dt) {
   const unsigned long long at = atomicAdd(a.ctr + IX_C_TOMB_FILL, 1ull);
   if (at < a.tomb_cap) a.tomb_list[at] = make_ulonglong2(x, (unsigned long long)dt);

@@ -60,20 +60,7 @@ __global__ void __launch_bounds__(IX_T) k_ix_touch_delta(IndexArgs a) {
 __global__ void __launch_bounds__(IX_T) k_ix_expire(IndexArgs a, uint64_t n, ReadbackArgs rb) {
   const uint64_t j = uint64_t(blockIdx.x) * IX_T + threadIdx.x;
   Contrib c{0, 0, 0, 0, 0};
-  if (j < n) {
-    const ulonglong2 e = a.tomb_list[j];
-    const uint64_t x = e.x;
-    const int64_t dt = int64_t(e.y);
-    if (x < a.lo) {  // this apply's own tombstones were counted at the new cutoff
-      if (dt > a.old_cut && dt <= a.new_cut) {
-        const uint32_t s = ix_find(a.keys, a.mask, a.key[x]);
-        if (s != IX_NONE && a.vals[s] == uint32_t(x + 1)) {
-          c.r = 0ull - 1ull;
-          c.tks = 0ull - (unsigned long long)(a.key[x] >> 32);
-        }
-      }
-    }
-  }
+  if (j < n) expire_one(a, j, c);
   flush_contrib(a, c, 0);
   if (!rb.n[0]) return;
   // the readback by the last workgroup to finish: its counters are final once every other

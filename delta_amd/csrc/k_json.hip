@@ -1008,7 +1008,8 @@ constexpr uint32_t AC_WAVES = 8;  // the walk's waves (the apply after it uses t
 constexpr uint32_t AC_LINES = (JSON_FUSE_MAX_LINES + AC_WAVES - 1) / AC_WAVES;  // lines per wave
 constexpr uint32_t AC_TCAP = 1024;                                            // tape tokens per wave
 constexpr uint32_t AC_SW = JSON_BYTES_PER_BLOCK / 16 + 4;                      // one index block + pad
-__global__ void __launch_bounds__(AC_WAVES * 64) k_apply_commit(JsonParseArgs a, CanonArgs c, AppendArgs p, IndexArgs x) {
+__global__ void __launch_bounds__(AC_WAVES * 64) k_apply_commit(JsonParseArgs a, CanonArgs c, AppendArgs p, IndexArgs x,
+                                                                uint64_t exp_n, ReadbackArgs rb) {
   __shared__ uint4 stage[AC_SW];
   __shared__ uint32_t tape[AC_WAVES][AC_TCAP];
   __shared__ uint8_t tline[AC_WAVES][AC_TCAP];
@@ -1018,7 +1019,7 @@ __global__ void __launch_bounds__(AC_WAVES * 64) k_apply_commit(JsonParseArgs a,
   const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
   const uint32_t len = uint32_t(a.buf_len), nlines = uint32_t(a.nlines);
   uint64_t tp0 = a.phase ? __builtin_amdgcn_s_memtime() : 0;
-  auto phase = [&](int k) {  // DR_JSON_PHASES: 0 stage, 1 newline index, 2 walk, 6 apply (slot 4: calls)
+  auto phase = [&](int k) {  // DR_JSON_PHASES: 0 stage, 1 newline index, 2 walk, 6 apply, 12 expiry, 13 readback (slot 4: calls)
     if (!a.phase) return;
     const uint64_t tn = __builtin_amdgcn_s_memtime();
     if (t == 0) atomicAdd(&a.phase[k], (unsigned long long)(tn - tp0));
@@ -1089,6 +1090,38 @@ __global__ void __launch_bounds__(AC_WAVES * 64) k_apply_commit(JsonParseArgs a,
   apply_small_body(a, c, p, x, true);
   phase(6);
   if (a.phase && t == 0) atomicAdd(&a.phase[4], 1ull);
+  // r06: the expiry of a short tombstone-candidate list and the readback, which followed as a second
+  // launch (k_ix_expire or k_readback), run here behind a fence and a barrier: one launch per commit
+  if (exp_n | rb.n[0]) {  // kernel arguments: uniform
+    __threadfence();
+    __syncthreads();
+    if (exp_n) {
+      Contrib ce{0, 0, 0, 0, 0};
+      // one workgroup walks the whole list: EXP_U entries per thread in flight (most fail the cutoff
+      // window on the entry alone, so the list loads are the chain to overlap)
+      constexpr uint32_t EXP_U = 8, EXP_STEP = AC_WAVES * 64;
+      for (uint64_t j0 = t; j0 < exp_n; j0 += EXP_U * EXP_STEP) {
+        ulonglong2 e[EXP_U];
+#pragma unroll
+        for (uint32_t u = 0; u < EXP_U; ++u) {
+          const uint64_t j = j0 + u * EXP_STEP;
+          e[u] = j < exp_n ? x.tomb_list[j] : make_ulonglong2(~0ull, 0ull);  // ~0: outside [0, lo)
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < EXP_U; ++u) expire_entry(x, e[u], ce);
+      }
+      flush_contrib(x, ce, 0);
+      __threadfence();
+      __syncthreads();
+      phase(12);
+    }
+#pragma unroll
+    for (int s = 0; s < READBACK_SPANS; ++s)
+      for (uint32_t k = t; k < rb.n[s]; k += AC_WAVES * 64)
+        rb.dst[s][k] = __hip_atomic_load(rb.src[s] + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    readback_flag(rb);
+    phase(13);
+  }
 }
 
 }  // namespace dev
@@ -1135,8 +1168,9 @@ void launch_apply_small(const JsonParseArgs* ja, const CanonArgs& cg, const Appe
 }
 
 void launch_apply_commit(const JsonParseArgs& ja, const CanonArgs& cg, const AppendArgs& ap, const IndexArgs& ix,
-                         hipStream_t st) {
-  DR_LAUNCH(dev::k_apply_commit, dim3(1), dim3(dev::AC_WAVES * 64), 0, st, ja, cg, ap, ix);
+                         hipStream_t st, uint64_t exp_n, const ReadbackArgs* rb) {
+  ReadbackArgs none{};
+  DR_LAUNCH(dev::k_apply_commit, dim3(1), dim3(dev::AC_WAVES * 64), 0, st, ja, cg, ap, ix, exp_n, rb ? *rb : none);
 }
 
 void launch_json_hard(const JsonParseArgs& a, hipStream_t st) {

@@ -636,12 +636,15 @@ void launch_ix_expire(const IndexArgs& a, uint64_t n_list, hipStream_t st, const
 // canonicalisation; skipped when ja is null), the append to the chain store with the counters'
 // reset, and both index passes -- k_tail_post + k_append_actions + k_ix_touch_delta in one launch
 constexpr uint64_t APPLY_SMALL_MAX = 256;
+// the one-launch apply also expires a tombstone-candidate list up to this long (one workgroup)
+constexpr uint64_t APPLY_FUSED_EXPIRY_MAX = 8192;
 void launch_apply_small(const JsonParseArgs* ja, const CanonArgs& cg, const AppendArgs& ap, const IndexArgs& ix,
                         hipStream_t st);
 // ... and the line walk itself, for a segment of one wave (ja in the fused-index form: zero, off2,
-// nl_out given; JSON_FUSE_MAX_LINES lines in one index block): the whole apply in one launch
+// nl_out given; JSON_FUSE_MAX_LINES lines in one index block): the whole apply in one launch, with the
+// expiry of the first exp_n tombstone candidates and the readback `rb` (when given) after it
 void launch_apply_commit(const JsonParseArgs& ja, const CanonArgs& cg, const AppendArgs& ap, const IndexArgs& ix,
-                         hipStream_t st);
+                         hipStream_t st, uint64_t exp_n = 0, const ReadbackArgs* rb = nullptr);
 void launch_ix_tomb_compact(const IndexArgs& a, const ulonglong2* list_in, uint64_t n, ulonglong2* list_out,
                             hipStream_t st);
 void launch_ix_undo(const IndexArgs& a, uint32_t* vals_out, const uint2* undo, uint64_t n, hipStream_t st);

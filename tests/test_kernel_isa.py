@@ -53,7 +53,8 @@ def test_apply_commit_reads_its_stage_and_tapes_from_lds(k_json_asm):
     """k_apply_commit (a streamed commit's whole apply in one workgroup) walks wave-private tapes
     over an LDS stage like the staged walker: it has no flat access beyond those of k_apply_small,
     the same apply without the walk (byte reads through path pointers, which are global)."""
-    name = "_ZN2dr3dev14k_apply_commitENS_13JsonParseArgsENS_9CanonArgsENS_10AppendArgsENS_9IndexArgsE"
+    name = ("_ZN2dr3dev14k_apply_commitENS_13JsonParseArgsENS_9CanonArgsENS_10AppendArgsENS_9IndexArgsE"
+            "mNS_12ReadbackArgsE")  # (+ the fused expiry count and readback, r06)
     small = "_ZN2dr3dev13k_apply_smallENS_13JsonParseArgsENS_9CanonArgsENS_10AppendArgsENS_9IndexArgsE"
     body, _ = _kernel(k_json_asm, name)
     ref, _ = _kernel(k_json_asm, small)

@@ -770,6 +770,7 @@ struct dr_state {
   std::shared_ptr<IncChain> chain;
   uint32_t gen = 0, nsrc = 0;
   bool lists_ready = true;
+  bool ordered = false;  // survivor lists sorted by action index (order_lists, on first use)
   std::shared_ptr<StagedData> staged;
   // the staged segments the action records point into: {staged} for a replay; for a state built
   // by dr_state_apply, its base's sources plus the applied tail (only sources[0] can hold
@@ -2290,8 +2291,12 @@ struct ActionDst {
   int64_t *size, *delts;
   uint16_t* src_id;
 };
+static void ensure_ready(dr_state& st);
 static void gather_survivors(dr_ctx* ctx, dr_state& base, const ActionDst& d) {
   hipStream_t stream = ctx->stream;
+  // base's lists in action order first: the store then keeps the log's order within each side, so an
+  // applied state lists its rows as a full replay of its segment does (order_lists)
+  ensure_ready(base);
   const uint64_t M = base.n_live + base.n_tomb;
   if (!M) return;
   DBuf<uint32_t> sidx(ctx, M);
@@ -2347,10 +2352,52 @@ static ActionDst chain_dst(IncChain& c) {
 
 static void materialize(dr_state& st);
 
+// r06: every consumer sees the survivor lists in action order -- the order of the winning actions in
+// the segment (checkpoint rows, then commits line by line; for a chain state, its store's order), so
+// a state's rows, row ranges and their boundaries are a function of the log alone, not of the
+// reducer's atomics. A replay on another GPU of the same segment lists the same rows in the same
+// order (what an RDD partition recomputed off its executor needs: INTEGRATION.md §1). Sorted once, on
+// first use, off the replay's own time.
+static void order_lists(dr_state& st) {
+  if (st.ordered) return;
+  dr_ctx* ctx = st.ctx;
+  hipStream_t stream = ctx->stream;
+  const uint64_t N = st.n_actions, W = (N + 31) / 32;
+  DBuf<uint32_t> bm, cnt;
+  DBuf<uint64_t> off;
+  DBuf<uint8_t> scratch;
+  for (int which = 0; which < 2; ++which) {
+    uint32_t* list = which == 0 ? st.live.p : st.tomb.p;
+    const uint64_t n = which == 0 ? st.n_live : st.n_tomb;
+    if (n < 2) continue;
+    if (!bm.p) {
+      bm = DBuf<uint32_t>(ctx, W);
+      cnt = DBuf<uint32_t>(ctx, W);
+      off = DBuf<uint64_t>(ctx, W + 1);
+      scratch = DBuf<uint8_t>(ctx, scan_scratch_for(W));
+    }
+    bm.zero(stream);
+    launch_bits_mark(list, n, N, bm.p, stream);
+    launch_bits_popc(bm.p, W, cnt.p, stream);
+    launch_scan_u32(cnt.p, off.p, W, ss(scratch), stream);
+    launch_bits_emit(bm.p, W, off.p, list, stream);
+    // distinct entries below N, or the list would lose rows: a replay invariant, checked here
+    const uint64_t got = d2h_one(off.p + W, stream);
+    if (got != n)
+      fail(DR_E_INTERNAL, fmt("survivor list %d: %llu distinct indices of %llu", which, (unsigned long long)got,
+                              (unsigned long long)n));
+  }
+  st.ordered = true;
+}
+
 // Chain states read the store through views (refreshed on every use: a later apply may have grown
-// the store) and build their survivor lists from the index on first use.
+// the store) and build their survivor lists from the index on first use. Every state's lists are
+// put in action order on first use.
 static void ensure_ready(dr_state& st) {
-  if (!st.chain) return;
+  if (!st.chain) {
+    order_lists(st);
+    return;
+  }
   IncChain& c = *st.chain;
   const uint64_t n = st.n_actions;
   st.kind.view(c.kind, n);
@@ -2372,6 +2419,7 @@ static void ensure_ready(dr_state& st) {
     st.arenas = c.arenas;
     st.lists_ready = true;
   }
+  order_lists(st);
 }
 
 // Survivor lists of a chain state: the head's index values -- an older state's after its later

@@ -109,6 +109,31 @@ __global__ void k_rebase_i64(const int64_t* __restrict__ src, uint64_t n, int64_
     dst[i] = src[i] - base;
 }
 
+// Survivor lists in action order (engine.hip:order_lists): a list of distinct indices below nbits
+// becomes a bitmap (one atomicOr per entry), the words' popcounts are scanned, and every word writes
+// its set bits' indices at its offset -- a sort of a set in O(n + nbits / 32), no comparisons.
+__global__ void k_bits_mark(const uint32_t* __restrict__ list, uint64_t n, uint64_t nbits, uint32_t* __restrict__ bm) {
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t v = list[i];
+    if (v < nbits) atomicOr(bm + (v >> 5), 1u << (v & 31u));  // (an entry out of range is lost: the count check sees it)
+  }
+}
+__global__ void k_bits_popc(const uint32_t* __restrict__ bm, uint64_t w, uint32_t* __restrict__ cnt) {
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < w; i += uint64_t(gridDim.x) * blockDim.x)
+    cnt[i] = uint32_t(__builtin_popcount(bm[i]));
+}
+__global__ void k_bits_emit(const uint32_t* __restrict__ bm, uint64_t w, const uint64_t* __restrict__ off,
+                            uint32_t* __restrict__ out) {
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < w; i += uint64_t(gridDim.x) * blockDim.x) {
+    uint32_t b = bm[i];
+    uint64_t o = off[i];
+    while (b) {
+      out[o++] = uint32_t(i << 5) + uint32_t(__builtin_ctz(b));
+      b &= b - 1u;
+    }
+  }
+}
+
 // Export of deletionTimestamp: valid = F_HAS_DELTS of the action's flags, and an absent one reads 0.
 __global__ void k_delts_fix(const uint8_t* __restrict__ flags, const int64_t* __restrict__ delts, uint64_t n,
                             uint8_t* __restrict__ valid, int64_t* __restrict__ out) {
@@ -166,6 +191,17 @@ void launch_rebase_i64(const int64_t* src, uint64_t n, int64_t base, int64_t* ds
   if (n)
     DR_LAUNCH(dev::k_rebase_i64, dim3(unsigned(std::min<uint64_t>((n + 255) / 256, 1u << 16))), dim3(256), 0, st, src, n,
               base, dst);
+}
+
+static dim3 grid_stride(uint64_t n) { return dim3(unsigned(std::min<uint64_t>((n + 255) / 256, 1u << 16))); }
+void launch_bits_mark(const uint32_t* list, uint64_t n, uint64_t nbits, uint32_t* bm, hipStream_t st) {
+  if (n) DR_LAUNCH(dev::k_bits_mark, grid_stride(n), dim3(256), 0, st, list, n, nbits, bm);
+}
+void launch_bits_popc(const uint32_t* bm, uint64_t w, uint32_t* cnt, hipStream_t st) {
+  if (w) DR_LAUNCH(dev::k_bits_popc, grid_stride(w), dim3(256), 0, st, bm, w, cnt);
+}
+void launch_bits_emit(const uint32_t* bm, uint64_t w, const uint64_t* off, uint32_t* out, hipStream_t st) {
+  if (w) DR_LAUNCH(dev::k_bits_emit, grid_stride(w), dim3(256), 0, st, bm, w, off, out);
 }
 
 void launch_delts_fix(const uint8_t* flags, const int64_t* delts, uint64_t n, uint8_t* valid, int64_t* out,

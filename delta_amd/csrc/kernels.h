@@ -588,6 +588,12 @@ struct ReadbackArgs {
 void launch_readback(const ReadbackArgs& a, hipStream_t st);
 // dst[i] = src[i] - base (n entries)
 void launch_rebase_i64(const int64_t* src, uint64_t n, int64_t base, int64_t* dst, hipStream_t st);
+// a list of distinct indices below nbits sorted ascending: mark its bits in bm (zeroed, ceil(nbits / 32)
+// words), the words' popcounts into cnt, and (after an exclusive scan of cnt into off) every word's
+// indices written at its offset
+void launch_bits_mark(const uint32_t* list, uint64_t n, uint64_t nbits, uint32_t* bm, hipStream_t st);
+void launch_bits_popc(const uint32_t* bm, uint64_t w, uint32_t* cnt, hipStream_t st);
+void launch_bits_emit(const uint32_t* bm, uint64_t w, const uint64_t* off, uint32_t* out, hipStream_t st);
 // export: valid[i] = flags[i] & F_HAS_DELTS, out[i] = valid ? delts[i] : 0
 void launch_delts_fix(const uint8_t* flags, const int64_t* delts, uint64_t n, uint8_t* valid, int64_t* out,
                       hipStream_t st);

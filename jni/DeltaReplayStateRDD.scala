@@ -12,6 +12,14 @@
  * (preferred location), pulling its rows with exportRange. No side is ever gathered on the driver, so
  * config 4's 100M-file state (36 GB of columns) crosses as ~2 GB slices.
  *
+ * Recompute lineage (a single-GPU replay's partitions): the library lists a state's rows in the order
+ * of their winning actions in the log segment (ABI 4, engine.hip:order_lists), so a row range is a
+ * function of the segment and cutoff alone. A partition computed where its state is not resident --
+ * scheduled off the replaying executor, or after that executor was lost -- replays the same segment
+ * on this executor's GPU (the log's files are immutable) and exports the same rows, as the
+ * reference's RDD recomputes from the log files. A sharded replay's rank state depends on the whole
+ * exchange and cannot be rebuilt alone: its partitions still fail loudly off their executor.
+ *
  * D/ = core/src/main/scala/org/apache/spark/sql/delta/.
  */
 package org.apache.spark.sql.delta.gpu
@@ -44,6 +52,13 @@ object DeltaReplayContexts {
 }
 
 /**
+ * Where a single-GPU replay's state comes from: enough to replay it again on another GPU (stageLog +
+ * replay), plus the side sizes the rebuilt state must reproduce.
+ */
+final case class ReplaySource(logPath: String, version: Long, minFileRetentionTs: Long, validate: Boolean,
+                              device: Int, numFiles: Long, numRemoves: Long)
+
+/**
  * The states resident in this JVM, by (snapshot key, rank). A state is registered by the task that
  * replayed it and removed by Snapshot.uncache (D/util/StateCache.scala:104-109), which releases it.
  * Several tasks of one executor may export ranges of a state at once (the library serialises calls on
@@ -56,20 +71,53 @@ object DeltaReplayStates {
     var released = false
   }
   private val states = new ConcurrentHashMap[(String, Int), Entry]()
+  private val rebuildLocks = new ConcurrentHashMap[String, Object]()
+  /** Keys of states this JVM rebuilt, oldest first: at most `MaxRebuilt` stay resident (the driver's
+   * uncache cannot reach them; a newer rebuild releases the oldest once its users return). */
+  private val rebuilt = new java.util.ArrayDeque[String]()
+  val MaxRebuilt = 2
 
   def put(key: String, rank: Int, state: Long): Unit = states.put((key, rank), new Entry(state))
 
-  private def entry(key: String, rank: Int): Entry = {
+  private def entry(key: String, rank: Int, source: Option[ReplaySource]): Entry = {
     val e = states.get((key, rank))
-    if (e == null) {
-      throw new IllegalStateException(s"the GPU state of snapshot $key rank $rank is not resident on this executor")
-    }
-    e
+    if (e != null) e
+    else if (rank == 0 && source.isDefined) rebuild(key, source.get)
+    else throw new IllegalStateException(s"the GPU state of snapshot $key rank $rank is not resident on this executor")
   }
 
-  /** Runs f on the state with a reference held: release waits for it (the state stays resident). */
-  def use[T](key: String, rank: Int)(f: Long => T): T = {
-    val e = entry(key, rank)
+  /** Replays a single-GPU state's segment on this JVM's GPU (once per key, however many tasks ask);
+   * the rebuilt state must hold the original's side sizes, or its ranges would not be the same rows. */
+  private def rebuild(key: String, s: ReplaySource): Entry =
+    rebuildLocks.computeIfAbsent(key, _ => new Object).synchronized {
+      val cur = states.get((key, 0))
+      if (cur != null) cur
+      else {
+        val ctx = DeltaReplayContexts.forDevice(s.device)
+        val staged = DeltaReplayNative.stageLog(ctx, s.logPath, s.version)
+        val st = try DeltaReplayNative.replay(ctx, staged, s.minFileRetentionTs, s.validate)
+                 finally DeltaReplayNative.stagedRelease(staged)
+        val c = DeltaReplayNative.counts(st)
+        import DeltaReplayNative.CountFields._
+        if (c(NumFiles) != s.numFiles || c(NumRemoves) != s.numRemoves) {
+          DeltaReplayNative.release(st)
+          throw new IllegalStateException(s"the rebuilt GPU state of snapshot $key differs from the original " +
+            s"(${c(NumFiles)}/${s.numFiles} files, ${c(NumRemoves)}/${s.numRemoves} tombstones)")
+        }
+        val e = new Entry(st)
+        states.put((key, 0), e)
+        rebuilt.synchronized {
+          rebuilt.addLast(key)
+          while (rebuilt.size > MaxRebuilt) release(rebuilt.pollFirst(), 0)
+        }
+        e
+      }
+    }
+
+  /** Runs f on the state with a reference held: release waits for it (the state stays resident). With
+   * a source, a state that is not resident here is rebuilt first (recompute lineage). */
+  def use[T](key: String, rank: Int, source: Option[ReplaySource] = None)(f: Long => T): T = {
+    val e = entry(key, rank, source)
     e.synchronized {
       if (e.released) throw new IllegalStateException(s"the GPU state of snapshot $key rank $rank was uncached")
       e.users += 1
@@ -98,20 +146,25 @@ object DeltaReplayStates {
   }
 }
 
-/** Rows [lo, hi) of side `which` (Live / Tombstones) of rank `rank`'s state, to run at `location`. */
-final case class StateRangePartition(index: Int, rank: Int, which: Int, lo: Long, hi: Long, location: String)
+/** Rows [lo, hi) of side `which` (Live / Tombstones) of rank `rank`'s state, preferably at `location`;
+ * `source` (a single-GPU replay) lets any executor with a GPU rebuild the state. */
+final case class StateRangePartition(index: Int, rank: Int, which: Int, lo: Long, hi: Long, location: String,
+                                     source: Option[ReplaySource] = None)
   extends Partition
 
 /** One rank's ranges: exportPlan of both sides on the rank's own executor. */
-final case class RankPlan(rank: Int, location: String, live: Array[Long], tombstones: Array[Long])
+final case class RankPlan(rank: Int, location: String, live: Array[Long], tombstones: Array[Long],
+                          source: Option[ReplaySource] = None)
 
 object RankPlan {
-  /** exportPlan of the state registered as (key, rank) in this JVM. */
-  def local(key: String, rank: Int, maxRows: Long): RankPlan = {
+  /** exportPlan of the state registered as (key, rank) in this JVM; `source` for a single-GPU replay
+   * (its partitions can then be recomputed elsewhere). */
+  def local(key: String, rank: Int, maxRows: Long, source: Option[ReplaySource] = None): RankPlan = {
     DeltaReplayStates.use(key, rank) { st =>
       RankPlan(rank, DeltaReplayStates.here,
         DeltaReplayNative.exportPlan(st, DeltaReplayNative.Live, maxRows, DeltaReplayNative.MaxBufferBytes),
-        DeltaReplayNative.exportPlan(st, DeltaReplayNative.Tombstones, maxRows, DeltaReplayNative.MaxBufferBytes))
+        DeltaReplayNative.exportPlan(st, DeltaReplayNative.Tombstones, maxRows, DeltaReplayNative.MaxBufferBytes),
+        source)
     }
   }
 }
@@ -128,8 +181,10 @@ class DeltaReplayStateRDD(sc: SparkContext, key: String, ranges: Array[StateRang
   override def compute(p: Partition, ctx: TaskContext): Iterator[InternalRow] = {
     val r = p.asInstanceOf[StateRangePartition]
     val handle = new Array[Long](1)
-    // fails loudly if scheduled off the rank's executor; an uncache meanwhile waits for the export
-    val cols = DeltaReplayStates.use(key, r.rank)(st => DeltaReplayNative.exportRange(st, r.which, r.lo, r.hi, handle))
+    // off the rank's executor: rebuilt from the log when the partition has a source, else a loud
+    // failure; an uncache meanwhile waits for the export
+    val cols = DeltaReplayStates.use(key, r.rank, r.source)(st =>
+      DeltaReplayNative.exportRange(st, r.which, r.lo, r.hi, handle))
     ctx.addTaskCompletionListener[Unit](_ => DeltaReplayNative.rangeRelease(handle(0)))
     val toRow = DeltaReplayState.serializer()
     val actions: Iterator[SingleAction] =
@@ -151,7 +206,7 @@ object DeltaReplayState {
     for (pl <- plans.sortBy(_.rank); (which, b) <- Seq(DeltaReplayNative.Live -> pl.live,
                                                          DeltaReplayNative.Tombstones -> pl.tombstones)) {
       for (k <- 0 until b.length - 1) {
-        out += StateRangePartition(i, pl.rank, which, b(k), b(k + 1), pl.location)
+        out += StateRangePartition(i, pl.rank, which, b(k), b(k + 1), pl.location, pl.source)
         i += 1
       }
     }

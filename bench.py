@@ -489,6 +489,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="time the steps without the roofline kernel's events")
     ap.add_argument("--profile-steps", type=int, default=3, help="untimed steps with an event pair on every launch")
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                    help="a context option (dr_ctx_set_option, delta_amd/_native.py OPTIONS), e.g. overlap=0")
     ap.add_argument("--workdir", default=os.environ.get("DR_BENCH_DIR", os.path.join(tempfile.gettempdir(), "dr_bench")))
     args = ap.parse_args()
     if args.pmc_dir is None:
@@ -532,6 +534,9 @@ def main():
         dist.barrier()
     exp = build_table(table, args.config, args.scale)
     eng = Engine.get(local)
+    for kv in args.option:
+        k, v = kv.split("=")
+        eng.set_option(k, int(v))
     if args.config == 5:
         if world > 1:
             raise SystemExit("config 5 (streaming tail) is a single-GPU workload")

@@ -605,6 +605,7 @@ struct PagePlan {
   DBuf<uint2> d_ba_tiles;
   DBuf<uint32_t> s_ba_vals, s_ba_ok, s_ba_count, s_ba_tile_cnt;
   DBuf<uint64_t> s_ba_tile_off, s_ba_kept;
+  DBuf<uint32_t> s_ba_link;
 };
 
 // Host copy of a staged segment's bytes (the host side keeps them: checkpoint footers / page headers
@@ -1167,6 +1168,7 @@ static void plan_pages(StagedData& s, PagePlan& P) {
   P.s_ba_tile_cnt = DBuf<uint32_t>(s.ctx, P.ba_tiles.size());
   P.s_ba_tile_off = DBuf<uint64_t>(s.ctx, P.ba_tiles.size() + 1);
   P.s_ba_kept = DBuf<uint64_t>(s.ctx, P.ba_tiles.size() * 256);
+  P.s_ba_link = DBuf<uint32_t>(s.ctx, P.ba_tiles.size() * 3);
   P.s_ba_ok = DBuf<uint32_t>(s.ctx, P.ba_pages);
   P.s_ba_count = DBuf<uint32_t>(s.ctx, P.ba_pages);
   for (PageDesc& d : P.pages) {
@@ -1207,6 +1209,7 @@ static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_
   pa.ba_tile_cnt = P.s_ba_tile_cnt.p;
   pa.ba_tile_off = P.s_ba_tile_off.p;
   pa.ba_kept = P.s_ba_kept.p;
+  pa.ba_link = P.s_ba_link.p;
   pa.ba_ok = P.s_ba_ok.p;
   pa.ba_count = P.s_ba_count.p;
   launch_page_copy(P.d_copy.p, uint32_t(P.copy_jobs.size()), stream);
@@ -1340,6 +1343,17 @@ static void decode_pages(dr_ctx* ctx, PagePlan& P, ParquetArgs& pa, DBuf<uint64_
       size_t n = 0;
       for (uint32_t v : ok) n += v != 0;
       std::fprintf(stderr, "ba bounds: %zu of %u pages validated\n", n, P.ba_pages);
+      const std::vector<uint32_t> lk = d2h(P.s_ba_link.p, P.ba_tiles.size() * 3, stream);
+      const std::vector<uint32_t> tc = d2h(P.s_ba_tile_cnt.p, P.ba_tiles.size(), stream);
+      int shown = 0;
+      for (size_t t = 0; t < P.ba_tiles.size() && shown < 40; ++t) {
+        const PageDesc& pd = P.pages[P.ba_tiles[t].x];
+        if (ok[pd.ba_slot]) continue;
+        std::fprintf(stderr, "ba tile %zu page %u y %u usize %u kind %d: first %u lsucc %u bad %u count %u\n", t,
+                     P.ba_tiles[t].x, P.ba_tiles[t].y, pd.usize, int(pd.kind), lk[3 * t], lk[3 * t + 1], lk[3 * t + 2],
+                     tc[t]);
+        ++shown;
+      }
     }
   }
   launch_pq_dict(pa, stream);

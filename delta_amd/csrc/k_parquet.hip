@@ -185,6 +185,11 @@ __device__ __forceinline__ uint32_t zero_nibble(uint32_t v) {  // bit k: byte k 
   return g & 0xFu;
 }
 
+// r06: the chain through the kept candidates (each one's successor is the next) is checked in
+// k_ba_count, where the successors are at hand, and the tiles' ends in k_ba_write (ba_link); a third
+// pass over the ranks (k_ba_check) did it before.
+constexpr uint32_t BA_NONE = 0xFFFFFFFFu;
+
 // Bit j of the result: region offset q0 + j is a kept candidate. The thread's 64 positions start
 // 16-byte aligned in absolute address; their +1..+4 bytes come from five 16-byte loads.
 __device__ __forceinline__ uint64_t ba_kept(const uint8_t* b, uint64_t S, int64_t q0) {
@@ -300,9 +305,14 @@ __device__ __forceinline__ uint64_t ba_kept_st(const uint8_t* b, uint64_t S, int
   return kept;
 }
 
-// T1: kept candidates per tile; each thread's 64-bit kept mask is stored for T2.
+// T1: kept candidates per tile; each thread's 64-bit kept mask is stored for T2. The chain is checked
+// here, where the successors are at hand: inside each thread (BaChain), from each thread's last kept
+// value to the next thread's first, and the tile's ends are left for T2 (ba_link).
 __global__ void __launch_bounds__(BA_T) k_ba_count(ParquetArgs a) {
   __shared__ uint32_t red[BA_T / 64];
+  __shared__ uint32_t tfirst[BA_T], tsucc[BA_T];
+  __shared__ unsigned long long wbal[BA_T / 64];
+  __shared__ uint32_t tile_bad;
   __shared__ __attribute__((aligned(16))) uint32_t stw[(BA_TILE + BA_MARGIN) / 4 + 8];
   const BaTile tl = ba_tile(a, blockIdx.x);
   // stage [t0, t0 + staged) of the region: t0 = thread 0's first position (16-byte aligned in
@@ -327,15 +337,69 @@ __global__ void __launch_bounds__(BA_T) k_ba_count(ParquetArgs a) {
     }
     st.n = nb;
   }
+  if (threadIdx.x == 0) tile_bad = 0;
   __syncthreads();
   const uint64_t km = tl.ok ? (st.n >= uint64_t(tl.q0 - st.t0) + 80 ? ba_kept_st(tl.b, tl.S, tl.q0, st)
                                                                     : ba_kept(tl.b, tl.S, tl.q0))
                             : 0ull;
   a.ba_kept[uint64_t(blockIdx.x) * BA_T + threadIdx.x] = km;
+  // the chain through this thread's kept values: each one's successor (its length read again, from
+  // the stage when it lies there) must be the next kept one
+  auto succ = [&](uint64_t p) -> uint64_t {
+    const uint64_t k = p - uint64_t(st.t0);
+    return p + 4 + (k + 8 <= st.n ? stage_u32(st, k) : load_u32(tl.b + p));
+  };
+  const uint32_t t = threadIdx.x, wv = t >> 6, ln = t & 63u;
+  uint32_t cfirst = BA_NONE, clsucc = BA_NONE;
+  bool cbad = false;
+  if (km) {
+    uint64_t m = km;
+    const uint64_t p0 = uint64_t(tl.q0 + __builtin_ctzll(m));
+    m &= m - 1;
+    uint64_t nx = succ(p0);
+    while (m) {
+      const uint64_t p = uint64_t(tl.q0 + __builtin_ctzll(m));
+      m &= m - 1;
+      cbad |= nx != p;
+      nx = succ(p);
+    }
+    cfirst = uint32_t(p0);
+    clsucc = uint32_t(nx);
+  }
+  tfirst[t] = cfirst;
+  tsucc[t] = clsucc;
+  const unsigned long long bal = __ballot(km != 0ull);
+  if (ln == 0) wbal[wv] = bal;
+  __syncthreads();
+  if (km) {
+    // the next thread holding a kept value (a value longer than a thread's 64 bytes skips threads)
+    uint32_t u = BA_NONE;
+    const unsigned long long above = ln == 63 ? 0ull : (wbal[wv] >> (ln + 1)) << (ln + 1);
+    if (above) {
+      u = wv * 64 + uint32_t(__builtin_ctzll(above));
+    } else {
+      for (uint32_t x = wv + 1; x < BA_T / 64; ++x)
+        if (wbal[x]) { u = x * 64 + uint32_t(__builtin_ctzll(wbal[x])); break; }
+    }
+    if (cbad || (u != BA_NONE && tfirst[u] != clsucc)) tile_bad = 1;
+  }
+  // the tile's ends: its first kept value, and the successor of its last
+  uint32_t* link = a.ba_link + 3ull * blockIdx.x;
+  if (t == 0) {
+    int lo = -1, hi = -1;
+    for (uint32_t x = 0; x < BA_T / 64; ++x)
+      if (wbal[x]) {
+        if (lo < 0) lo = int(x * 64 + __builtin_ctzll(wbal[x]));
+        hi = int(x * 64 + 63 - __builtin_clzll(wbal[x]));
+      }
+    link[0] = lo < 0 ? BA_NONE : tfirst[lo];
+    link[1] = hi < 0 ? BA_NONE : tsucc[hi];
+  }
   const uint32_t s = block_sum(uint32_t(__builtin_popcountll(km)), red);
   if (threadIdx.x == 0) {
     a.ba_tile_cnt[blockIdx.x] = s;
     if (a.ba_tiles[blockIdx.x].y == 0) a.ba_ok[tl.pg->ba_slot] = tl.ok ? 1u : 0u;
+    link[2] = tile_bad;
   }
 }
 
@@ -373,32 +437,22 @@ __global__ void __launch_bounds__(BA_T) k_ba_write(ParquetArgs a) {
   const bool last = blockIdx.x + 1 == a.nba_tiles || a.ba_tiles[blockIdx.x + 1].x != a.ba_tiles[blockIdx.x].x;
   if (threadIdx.x == 0 && last)
     a.ba_count[pg.ba_slot] = uint32_t(a.ba_tile_off[blockIdx.x + 1] - a.ba_tile_off[first]);
-}
-
-// T3: chain validation, one thread per value of the tile's rank range.
-__global__ void __launch_bounds__(BA_T) k_ba_check(ParquetArgs a) {
-  const BaTile tl = ba_tile(a, blockIdx.x);
-  if (!tl.ok) return;
-  const PageDesc pg = *tl.pg;
-  const uint32_t first = uint32_t(pg.hit_base);
-  const uint64_t n = a.ba_count[pg.ba_slot];
-  const uint64_t cap = pg.usize / 4 + 2;
-  const uint64_t boff = uint64_t(tl.b - reinterpret_cast<const uint8_t*>(pg.dst));
-  if (n > cap) {
-    if (threadIdx.x == 0) a.ba_ok[pg.ba_slot] = 0;
-    return;
+  // the chain's ends (k_ba_count checked it inside the tile): the page's first value starts at
+  // region offset 0, the successor of the tile's last value is the first value of the page's next
+  // tile holding one, or the region end; a page whose values exceed the rank list's room fails too
+  if (threadIdx.x == 0) {
+    const uint32_t* L = a.ba_link + 3ull * blockIdx.x;
+    bool bad = L[2] != 0;
+    if (blockIdx.x == first) bad |= tl.S > 0 && L[0] != 0;
+    if (L[1] != BA_NONE) {
+      uint64_t want = tl.S;
+      for (uint32_t u = blockIdx.x + 1; u < a.nba_tiles && a.ba_tiles[u].x == a.ba_tiles[blockIdx.x].x; ++u)
+        if (a.ba_link[3ull * u] != BA_NONE) { want = a.ba_link[3ull * u]; break; }
+      bad |= uint64_t(L[1]) != want;
+    }
+    if (last) bad |= a.ba_tile_off[blockIdx.x + 1] - a.ba_tile_off[first] > cap;
+    if (bad) a.ba_ok[pg.ba_slot] = 0;
   }
-  const uint32_t* vals = a.ba_vals + pg.ba_base;
-  const uint64_t r0 = a.ba_tile_off[blockIdx.x] - a.ba_tile_off[first];
-  const uint64_t r1 = a.ba_tile_off[blockIdx.x + 1] - a.ba_tile_off[first];
-  bool bad = blockIdx.x == first && tl.S > 0 && (n == 0 || vals[0] != boff);
-  for (uint64_t k = r0 + threadIdx.x; k < r1; k += BA_T) {
-    const uint64_t p = vals[k] - boff;
-    const uint64_t nx = p + 4 + load_u32(tl.b + p);
-    const uint64_t want = k + 1 < n ? uint64_t(vals[k + 1]) - boff : tl.S;
-    if (nx != want) bad = true;
-  }
-  if (bad) a.ba_ok[pg.ba_slot] = 0;
 }
 
 // ---- dictionary pages --------------------------------------------------------------------------------
@@ -705,7 +759,6 @@ void launch_ba_bounds(const ParquetArgs& a, hipStream_t st, ScanScratch scan_scr
   DR_LAUNCH(dev::k_ba_count, dim3(a.nba_tiles), dim3(dev::BA_T), 0, st, a);
   launch_scan_u32(a.ba_tile_cnt, a.ba_tile_off, a.nba_tiles, scan_scratch, st);
   DR_LAUNCH(dev::k_ba_write, dim3(a.nba_tiles), dim3(dev::BA_T), 0, st, a);
-  DR_LAUNCH(dev::k_ba_check, dim3(a.nba_tiles), dim3(dev::BA_T), 0, st, a);
 }
 void launch_pq_dict(const ParquetArgs& a, hipStream_t st) {
   if (!a.npages) return;

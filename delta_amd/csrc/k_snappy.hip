@@ -1228,14 +1228,38 @@ __global__ void k_snap_serial(SnappyArgs a) {
   if (op != pg.n_out) atomicCAS(a.error, 0u, 1u);
 }
 
-// Uncompressed pages and the raw level prefix of DATA_PAGE_V2 pages: one workgroup per job.
+// Uncompressed pages, the raw level prefix of DATA_PAGE_V2 pages and the literal runs of pages the
+// compressor could not shrink: PAGE_COPY_SLICES workgroups per job (r06: one, byte by byte, copied
+// config 3's 7 MB at 77 GB/s -- ~100 jobs of up to 64 KiB). The destination is written in 16-byte
+// stores; the source, at any byte offset from it, is read as aligned dwords and realigned.
+constexpr uint32_t PAGE_COPY_SLICES = 16;
 __global__ void __launch_bounds__(256) k_page_copy(const CopyJob* jobs, uint32_t njobs) {
-  const uint32_t j = blockIdx.x;
+  const uint32_t j = blockIdx.x, t = threadIdx.x, y = blockIdx.y;
   if (j >= njobs) return;
   const uint8_t* s = reinterpret_cast<const uint8_t*>(jobs[j].src);
   uint8_t* d = reinterpret_cast<uint8_t*>(jobs[j].dst);
   const uint64_t n = jobs[j].n;
-  for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) d[i] = s[i];
+  const uint64_t head = min(n, uint64_t((16u - (reinterpret_cast<uintptr_t>(d) & 15u)) & 15u));
+  const uint64_t nv = (n - head) / 16;
+  if (y == 0) {
+    for (uint64_t i = t; i < head; i += 256) d[i] = s[i];
+    for (uint64_t i = head + nv * 16 + t; i < n; i += 256) d[i] = s[i];
+  }
+  const uint8_t* s1 = s + head;
+  uint4* d1 = reinterpret_cast<uint4*>(d + head);
+  const uint32_t r = uint32_t(reinterpret_cast<uintptr_t>(s1) & 3u);
+  const uint32_t* sw = reinterpret_cast<const uint32_t*>(s1 - r);
+  for (uint64_t k = uint64_t(y) * 256 + t; k < nv; k += 256ull * PAGE_COPY_SLICES) {
+    const uint32_t* w = sw + 4 * k;
+    const uint32_t a0 = w[0], a1 = w[1], a2 = w[2], a3 = w[3];
+    if (r == 0) {  // (uniform per job)
+      d1[k] = make_uint4(a0, a1, a2, a3);
+    } else {  // the fifth dword holds the chunk's last byte (r >= 1): inside the source
+      const uint32_t a4 = w[4];
+      d1[k] = make_uint4(__builtin_amdgcn_alignbyte(a1, a0, r), __builtin_amdgcn_alignbyte(a2, a1, r),
+                         __builtin_amdgcn_alignbyte(a3, a2, r), __builtin_amdgcn_alignbyte(a4, a3, r));
+    }
+  }
 }
 
 }  // namespace dev
@@ -1259,7 +1283,7 @@ void launch_snappy(const SnappyArgs& a, hipStream_t st, ScanScratch scan_scratch
 }
 
 void launch_page_copy(const CopyJob* jobs, uint32_t njobs, hipStream_t st) {
-  if (njobs) DR_LAUNCH(dev::k_page_copy, dim3(njobs), dim3(256), 0, st, jobs, njobs);
+  if (njobs) DR_LAUNCH(dev::k_page_copy, dim3(njobs, dev::PAGE_COPY_SLICES), dim3(256), 0, st, jobs, njobs);
 }
 
 }  // namespace dr

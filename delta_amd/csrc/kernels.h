@@ -158,6 +158,8 @@ struct ParquetArgs {
   uint32_t* ba_tile_cnt; // [nba_tiles]
   uint64_t* ba_tile_off; // [nba_tiles + 1] exclusive scan of ba_tile_cnt
   uint64_t* ba_kept;     // [nba_tiles * 256] kept-candidate masks (64 positions per thread)
+  uint32_t* ba_link;     // [nba_tiles * 3] the tile's first kept offset, its last kept's successor
+                         // (0xFFFFFFFF: none) and whether its chain broke inside it
 };
 uint32_t ba_tile_bytes();
 void launch_ba_bounds(const ParquetArgs& a, hipStream_t st, ScanScratch scan_scratch);

@@ -287,7 +287,7 @@ def test_corrupt_checkpoint_page_is_an_error(engine, tmp_path, fill):
 
 def test_checkpoint_boundaries_found_in_parallel(engine, tmp_path, capfd, monkeypatch):
     """Every PLAIN BYTE_ARRAY page of a synthetic checkpoint is split by the parallel boundary
-    kernels (k_ba_count/write/check) and validated, so none falls back to the serial walker
+    kernels (k_ba_count/write: candidates, ranks and the chain check) and validated, so none falls back to the serial walker
     (the fallback is exact too, so parity alone would not notice)."""
     from delta_amd.testing import synth as S
     exp = S.build_config(3, str(tmp_path), scale=0.005)
@@ -299,6 +299,42 @@ def test_checkpoint_boundaries_found_in_parallel(engine, tmp_path, capfd, monkey
     for l in found:
         w = l.split()
         assert int(w[2]) == int(w[4]) > 0, l
+
+
+def test_checkpoint_false_boundaries_are_refused(engine, tmp_path, capfd, monkeypatch):
+    """Paths whose bytes hold fake length prefixes (NUL bytes: "\\x05\\0\\0\\0" + 5 bytes +
+    "\\x03\\0\\0\\0" + 3 bytes) give the parallel boundary search kept candidates that are not
+    value starts; the chain check (k_ba_count / k_ba_write) must refuse those pages -- they take the
+    serial walker -- and the replay equals the oracle's."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    from delta_amd.testing import synth as S
+    exp = S.build_table(str(tmp_path), S.config_spec(3, 0.002), seed=9, use_dictionary=False)
+    lp = os.path.join(str(tmp_path), "_delta_log")
+    cp = os.path.join(lp, [f for f in os.listdir(lp) if f.endswith(".checkpoint.parquet")][0])
+    t = pq.read_table(cp)
+    add = t.column("add").combine_chunks()
+    paths = add.field("path").to_pylist()
+    fake = "x\x05\x00\x00\x00yyyyy\x03\x00\x00\x00zzz"
+    bad = 0
+    for i in range(0, len(paths), 97):
+        if paths[i] is not None:
+            paths[i] = paths[i][:20] + fake + paths[i][20:]
+            bad += 1
+    assert bad > 10
+    fields = [pa.array(paths, type=add.type.field("path").type) if add.type.field(k).name == "path" else add.field(k)
+              for k in range(add.type.num_fields)]
+    new = pa.StructArray.from_arrays(fields, fields=list(add.type), mask=add.is_null())
+    t = t.set_column(t.schema.get_field_index("add"), t.schema.field("add"), new)
+    pq.write_table(t, cp, compression="snappy", use_dictionary=False)
+    monkeypatch.setenv("DR_BA_DEBUG", "1")
+    st = _gpu_replay(engine, lp, exp.min_file_retention_timestamp)
+    try:
+        _assert_same(st, O.state_reconstruction(O.get_log_segment(lp), exp.min_file_retention_timestamp))
+    finally:
+        st.release()
+    found = [l.split() for l in capfd.readouterr().err.splitlines() if l.startswith("ba bounds:")]
+    assert found and any(int(w[2]) < int(w[4]) for w in found), found
 
 
 @pytest.mark.parametrize("table", ["dbr_8_0_non_generated_columns", "dbr_8_1_generated_columns"])

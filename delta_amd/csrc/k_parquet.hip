@@ -697,17 +697,28 @@ __global__ void __launch_bounds__(PQD_T) k_pq_data(ParquetArgs a) {
 
 // Checkpoint row -> action. unwrap priority add > remove (D/actions/actions.scala:523-541);
 // rows holding neither are protocol/metaData/txn rows decoded on the host.
-__global__ void k_ckpt_assemble(CkptAssembleArgs a) {
+// r06: a wave's 64 paths lie together in a PLAIN page's body (~6 KiB): the wave copies that span into
+// LDS with coalesced 16-byte loads and every lane hashes its path from there -- one lane per path
+// reading its own bytes from global memory was 64 scattered requests per load (0.48 ms on config 3).
+// Paths elsewhere (dictionary entries, a span crossing pages that lie apart) are read in place.
+constexpr uint32_t ASM_T = 256, ASM_STAGE = 8192;
+__device__ __forceinline__ void asm_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__global__ void __launch_bounds__(ASM_T) k_ckpt_assemble(CkptAssembleArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t stage[ASM_T / 64][ASM_STAGE + 32];
   const uint64_t r = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (r >= a.nrows) return;
+  const bool live = r < a.nrows;  // (no early exit: the wave stages its paths together)
   const uint64_t idx = a.row_base + r;
   uint8_t kind = K_NONE, flags = F_FROM_CKPT;
   const uint8_t* path = nullptr;
   uint32_t plen = 0;
   int64_t size = 0, delts = 0;
-  const int ad = a.add_path.def[r];
-  const int rd = a.has_rm ? int(a.rm_path.def[r]) : 0;
-  if (ad >= a.add_def) {
+  const int ad = live ? int(a.add_path.def[r]) : 0;
+  const int rd = live && a.has_rm ? int(a.rm_path.def[r]) : 0;
+  if (live && ad >= a.add_def) {
     kind = K_ADD;
     if (ad == a.add_path_max) {
       path = reinterpret_cast<const uint8_t*>(a.add_path.sptr[r]);
@@ -716,7 +727,7 @@ __global__ void k_ckpt_assemble(CkptAssembleArgs a) {
       flags |= F_PATH_NULL;
     }
     if (a.add_size.def[r] == a.add_size_max) size = a.add_size.ival[r];
-  } else if (a.has_rm && rd >= a.rm_def) {
+  } else if (live && a.has_rm && rd >= a.rm_def) {
     kind = K_REMOVE;
     if (rd == a.rm_path_max) {
       path = reinterpret_cast<const uint8_t*>(a.rm_path.sptr[r]);
@@ -729,16 +740,35 @@ __global__ void k_ckpt_assemble(CkptAssembleArgs a) {
       flags |= F_HAS_DELTS;
     }
   }
+  const bool hashed = (kind == K_ADD || kind == K_REMOVE) && !(flags & F_PATH_NULL);
+  // the wave's span of path bytes
+  uint64_t lo = hashed ? reinterpret_cast<uint64_t>(path) : ~0ull;
+  uint64_t hi = hashed ? reinterpret_cast<uint64_t>(path) + plen : 0ull;
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = min(lo, (uint64_t)__shfl_xor((unsigned long long)lo, o, 64));
+    hi = max(hi, (uint64_t)__shfl_xor((unsigned long long)hi, o, 64));
+  }
+  const uint64_t a0 = lo & ~uint64_t(15);
+  const bool staged = hi > lo && hi - a0 <= ASM_STAGE;  // wave-uniform
+  uint8_t* stw = stage[threadIdx.x >> 6];
+  if (staged) {
+    const uint32_t nq = uint32_t((hi - a0 + 15) >> 4);
+    const uint4* src = reinterpret_cast<const uint4*>(a0);  // (page bodies are padded by 16 bytes)
+    for (uint32_t k = threadIdx.x & 63u; k < nq; k += 64) reinterpret_cast<uint4*>(stw)[k] = src[k];
+    asm_wave_sync();
+  }
   uint64_t key = 0;
-  if ((kind == K_ADD || kind == K_REMOVE) && !(flags & F_PATH_NULL)) {
-    if (path_is_special(path, plen)) {
+  if (hashed) {
+    const uint8_t* hp = staged ? stw + (reinterpret_cast<uint64_t>(path) - a0) : path;
+    if (path_is_special(hp, plen)) {
       flags |= F_SPECIAL_PATH;
       atomicAdd(reinterpret_cast<unsigned long long*>(a.special_count), 1ull);
       atomicAdd(reinterpret_cast<unsigned long long*>(a.special_bytes), (unsigned long long)(plen + 8));
     } else {
-      key = path_key(path, plen);
+      key = path_key(hp, plen);
     }
   }
+  if (!live) return;
   a.act.kind[idx] = kind;
   a.act.flags[idx] = flags;
   a.act.key[idx] = key;
@@ -769,7 +799,8 @@ void launch_pq_data(const ParquetArgs& a, hipStream_t st) {
   if (a.npages) DR_LAUNCH(dev::k_pq_data, dim3(a.npages), dim3(dev::PQD_T), 0, st, a);
 }
 void launch_ckpt_assemble(const CkptAssembleArgs& a, hipStream_t st) {
-  if (a.nrows) DR_LAUNCH(dev::k_ckpt_assemble, dim3(unsigned((a.nrows + 255) / 256)), dim3(256), 0, st, a);
+  if (a.nrows)
+    DR_LAUNCH(dev::k_ckpt_assemble, dim3(unsigned((a.nrows + dev::ASM_T - 1) / dev::ASM_T)), dim3(dev::ASM_T), 0, st, a);
 }
 
 }  // namespace dr

@@ -141,8 +141,9 @@ void dr_ctx_destroy(dr_ctx* ctx);
  * DR_E_INVALID_ARG for an unknown option or a value outside its range. Debug-only switches (phase
  * clocks, poisoning, roctx ranges, dumps) stay environment variables and change no result. */
 enum dr_option {
-  DR_OPT_OVERLAP = 1,          /* 1 (default): K1 line parsing on a second stream beside the checkpoint
-                                  decode for segments with a checkpoint and a multi-block JSON part; 0: one stream */
+  DR_OPT_OVERLAP = 1,          /* 1: K1 line parsing on a second stream beside the checkpoint decode for
+                                  segments with a checkpoint and a multi-block JSON part; 0 (default since
+                                  r06: the two streams' kernels share the CUs and gained nothing): one stream */
   DR_OPT_SPLIT = 2,            /* 1 (default): replays of more than 2^13 * 2048 actions refine K3's buckets
                                   (k_bucket_split) so K4 reduces each in one pass; 0: K4's sub-passes */
   DR_OPT_BUCKET_BITS = 3,      /* -1 (default): automatic; n in 0..32: at most n K3 bucket bits (fewer,

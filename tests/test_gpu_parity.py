@@ -130,13 +130,13 @@ def test_synthetic_configs(engine, tmp_path, config, scale):
 
 @pytest.mark.parametrize("overlap", [0, 1])
 def test_parse_streams_overlap_or_not(tmp_path, overlap):
-    """K1 beside K2 on two streams (the default for a segment with a checkpoint and a multi-block
-    JSON part) and on one (context option DR_OPT_OVERLAP = 0): the same records as the oracle either
-    way, on a fresh context set to each."""
+    """K1 beside K2 on two streams (context option DR_OPT_OVERLAP = 1, for a segment with a
+    checkpoint and a multi-block JSON part) and on one (the default): the same records as the oracle
+    either way, on a fresh context set to each."""
     from delta_amd.delta_log import Engine
     from delta_amd.testing import synth as S
     eng = Engine(0)
-    assert eng.get_option("overlap") == 1  # the default
+    assert eng.get_option("overlap") == 0  # the default
     eng.set_option("overlap", overlap)
     exp = S.build_config(3, str(tmp_path), scale=0.02)
     lp = os.path.join(str(tmp_path), "_delta_log")

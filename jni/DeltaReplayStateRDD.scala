@@ -89,7 +89,7 @@ object DeltaReplayStates {
   /** Replays a single-GPU state's segment on this JVM's GPU (once per key, however many tasks ask);
    * the rebuilt state must hold the original's side sizes, or its ranges would not be the same rows. */
   private def rebuild(key: String, s: ReplaySource): Entry =
-    rebuildLocks.computeIfAbsent(key, _ => new Object).synchronized {
+    rebuildLocks.computeIfAbsent(key, (_: String) => new Object).synchronized {
       val cur = states.get((key, 0))
       if (cur != null) cur
       else {

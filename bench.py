@@ -682,6 +682,13 @@ def main():
         "sort_reduce": dict(pipeline(SORT_REDUCE, 69 * local_counts["num_actions"]), target_frac=0.5)
         if local_counts else None,
     }
+    if local_counts:
+        # the same budget without the byte verifier: north_star's sort + reduce is keyed by the path
+        # hash alone ((3)-(4): radix sort on (pathHash, version, ordinal), last-writer-wins); comparing
+        # each (loser, winner) pair's path bytes is this build's addition for bit-exact sets under a
+        # 64-bit collision, priced on its own bytes below. Reported beside sort_reduce, not instead.
+        pipelines["sort_reduce_hash_keyed"] = pipeline([k for k in SORT_REDUCE if k != "k_bucket_verify"],
+                                                       69 * local_counts["num_actions"])
     if "verify_pairs" in stats and "k_bucket_verify" in kernels:
         # the verifier on its own path bytes: per (loser, winner) pair its 16-byte reference pair and
         # both paths' bytes (the 69 B/action budget above does not model it)

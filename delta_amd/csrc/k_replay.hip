@@ -188,7 +188,12 @@ __global__ void __launch_bounds__(PART_T) k_bucket_scatter(PartitionArgs a) {
   __shared__ uint32_t base[1 << PART_MAX_BITS];
   __shared__ uint32_t cnt[1 << PART_MAX_BITS];
   const uint32_t nb = 1u << a.bucket_bits;
-  const uint32_t tile = blockIdx.x;
+  // XCD-aware tiles (r06): workgroup i runs on XCD i % 8, so it takes the (i / 8)-th tile of XCD
+  // (i % 8)'s contiguous share -- adjacent tiles' runs of a bucket share their boundary lines, which
+  // then fill in one L2 (0.285 -> 0.276 ms on config 3)
+  const uint32_t per = (a.ntiles + 7) / 8, xcd = blockIdx.x % 8, slot = blockIdx.x / 8;
+  const uint32_t tile = xcd * per + slot;
+  if (tile >= a.ntiles) return;  // (the grid is rounded up to a multiple of 8)
   for (uint32_t b = threadIdx.x; b < nb; b += PART_T) {
     base[b] = uint32_t(a.tile_off[uint64_t(b) * a.ntiles + tile]);
     cnt[b] = 0;
@@ -1019,7 +1024,7 @@ void launch_bucket_hist(const PartitionArgs& a, hipStream_t st) {
 }
 
 void launch_bucket_scatter(const PartitionArgs& a, hipStream_t st) {
-  if (a.ntiles) DR_LAUNCH(dev::k_bucket_scatter, dim3(a.ntiles), dim3(dev::PART_T), 0, st, a);
+  if (a.ntiles) DR_LAUNCH(dev::k_bucket_scatter, dim3(8 * ((a.ntiles + 7) / 8)), dim3(dev::PART_T), 0, st, a);
 }
 
 void launch_bucket_offsets(const uint64_t* tile_off, uint32_t nb, uint32_t nt, uint64_t* bucket_off, hipStream_t st) {
